@@ -1,0 +1,518 @@
+/* asv_oracle.c -- CPU restatement of the rfarl env step (TEST INFRASTRUCTURE ONLY).
+ *
+ * Checker for the HIP kernels in distributional_rl_decision_and_control_amd/csrc and the
+ * bench's CPU baseline. It is never linked into or called by the product path.
+ * Pinned against tests/golden/ (captured from the reference by tools/capture_oracle.py).
+ *
+ * Arithmetic follows the reference's operation order (np.matrix products written out as
+ * the row sums they compute) so that f64 results agree to ~1e-13; the reference's BLAS
+ * may fuse some of those sums, hence tolerances rather than bit equality on f64 state.
+ */
+#include "asv_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+static const double PI = 3.141592653589793;
+
+void or_default_params(OrParams* p) {
+  memset(p, 0, sizeof(*p));
+  p->dt = 0.05; /* wamv.py:46 */
+  p->N = 10;    /* wamv.py:47 */
+  p->length = 5.0;
+  p->width = 2.5;
+  p->r = 0.5 * sqrt(p->length * p->length + p->width * p->width); /* wamv.py:53-54 */
+  p->goal_dis = 2.0;
+  p->min_thrust = -500.0;
+  p->max_thrust = 1000.0;
+  p->m = 400;
+  p->Izz = 450;
+  p->xDotU = 20; p->yDotV = 0; p->yDotR = 0; p->nDotR = -980; p->nDotV = 0;
+  p->xU = -100; p->xUU = -150; p->yV = -100; p->yVV = -150; p->yR = 0; p->yRV = 0;
+  p->yVR = 0; p->yRR = 0; p->nR = -980; p->nRR = -950; p->nV = 0; p->nVV = 0; p->nRV = 0;
+  p->nVR = 0;
+  /* A = M_RB + M_A = diag(380, 400, 1430); P = inv(A^T A) A^T, computed by numpy in the
+   * reference (wamv.py:271). The exact f64 values are supplied by the host; the defaults
+   * below are the values numpy produces for the default A (checked by the tests). */
+  p->P[0] = 1.0 / 380.0; p->P[4] = 1.0 / 400.0; p->P[8] = 1.0 / 1430.0;
+  double tc[5] = {0.0, -500.0, -1000.0, 500.0, 1000.0};
+  memcpy(p->thrust_change, tc, sizeof(tc));
+  p->range = 20.0;
+  p->angle = 2 * PI;
+  p->r_mean_ratio = 0.8;
+  p->max_obj_num = 5;
+  p->timestep_penalty = -0.1;
+  p->COLREGs_penalty = -0.1;
+  p->collision_penalty = -5.0;
+  p->goal_reward = 10.0;
+  p->core_r = 0.5;
+  p->episode_limit = 1000;
+}
+
+/* ---------------------------------------------------------------- current (env.py:458-501) */
+static double compute_speed(double Gamma, double d, double r) { /* env.py:497-501 */
+  if (d <= r) return Gamma / (2 * PI * r * r) * d;
+  return Gamma / (2 * PI * d);
+}
+
+void or_current(const double* cores, int n, double core_r, double x, double y, double out[3]) {
+  out[0] = out[1] = out[2] = 0.0;
+  if (n <= 0) return; /* env.py:459-460 */
+  /* KDTree query returns every core in ascending distance (env.py:463); the "outer core"
+   * skip at :473-478 only continues its inner loop, so every core contributes. */
+  int order[16];
+  double dist[16];
+  for (int k = 0; k < n; ++k) {
+    double dx = cores[4 * k] - x, dy = cores[4 * k + 1] - y;
+    dist[k] = sqrt(dx * dx + dy * dy);
+    order[k] = k;
+  }
+  for (int a = 1; a < n; ++a) { /* stable insertion sort by distance */
+    int oi = order[a];
+    double di = dist[oi];
+    int b = a - 1;
+    while (b >= 0 && dist[order[b]] > di) { order[b + 1] = order[b]; --b; }
+    order[b + 1] = oi;
+  }
+  double vx = 0.0, vy = 0.0;
+  for (int t = 0; t < n; ++t) {
+    const double* c = cores + 4 * order[t];
+    double rx = c[0] - x, ry = c[1] - y;
+    double dis = sqrt(rx * rx + ry * ry);
+    rx /= dis; ry /= dis;
+    double tx, ty;
+    if (c[2] != 0.0) { tx = -ry; ty = rx; }  /* [[0,-1],[1,0]] */
+    else { tx = ry; ty = -rx; }              /* [[0,1],[-1,0]] */
+    double sp = compute_speed(c[3], dis, core_r);
+    vx += tx * sp;
+    vy += ty * sp;
+  }
+  out[0] = vx; out[1] = vy; out[2] = 0.0;
+}
+
+/* ---------------------------------------------------------------- dynamics (wamv.py:204-279) */
+static void compute_motion(const OrParams* p, OrRobot* rb) {
+  double c = cos(rb->theta), s = sin(rb->theta);
+  /* project_to_robot_frame(is_vector=True): R_rw = R_wr^T = [[c, s], [-s, c]] (wamv.py:305-322) */
+  double u_r = c * rb->vr[0] + s * rb->vr[1];
+  double v_r = -s * rb->vr[0] + c * rb->vr[1];
+  double u = c * rb->v[0] + s * rb->v[1];
+  double v = -s * rb->v[0] + c * rb->v[1];
+  double r = rb->v[2];
+  /* -C_RB V (wamv.py:242,270) */
+  double mr = p->m * r;
+  double cv0 = -(-mr * v), cv1 = -(mr * u), cv2 = 0.0;
+  /* N = C_A + D + D_n (wamv.py:243-248) */
+  double ca02 = p->yDotV * v_r + p->yDotR * r;
+  double ca12 = -p->xDotU * u_r;
+  double ca20 = -p->yDotV * v_r - p->yDotR * r;
+  double ca21 = p->xDotU * u_r;
+  double au = fabs(u_r), av = fabs(v_r), ar = fabs(r);
+  /* element-wise (C_A + D) + D_n with D = -1.0*[...], D_n = -1.0*[...] */
+  double n00 = (0.0 + -p->xU) + -(p->xUU * au);
+  double n02 = (ca02 + -0.0) + -0.0;
+  double n11 = (0.0 + -p->yV) + -(p->yVV * av + p->yRV * ar);
+  double n12 = (ca12 + -p->yR) + -(p->yVR * av + p->yRR * ar);
+  double n20 = (ca20 + -0.0) + -0.0;
+  double n21 = (ca21 + -p->nV) + -(p->nVV * av + p->nRV * ar);
+  double n22 = (0.0 + -p->nR) + -(p->nVR * av + p->nRR * ar);
+  double nv0 = n00 * u_r + 0.0 * v_r + n02 * r;
+  double nv1 = 0.0 * u_r + n11 * v_r + n12 * r;
+  double nv2 = n20 * u_r + n21 * v_r + n22 * r;
+  /* tau_p (wamv.py:251-264) */
+  double fxl = rb->tl * cos(rb->lp), fyl = rb->tl * sin(rb->lp);
+  double mxl = fxl * p->width / 2, myl = -fyl * p->length / 2;
+  double fxr = rb->tr * cos(rb->rp), fyr = rb->tr * sin(rb->rp);
+  double mxr = -fxr * p->width / 2, myr = -fyr * p->length / 2;
+  double fx = fxl + fxr, fy = fyl + fyr, mn = mxl + myl + mxr + myr;
+  double b0 = cv0 - nv0 + fx, b1 = cv1 - nv1 + fy, b2 = cv2 - nv2 + mn;
+  /* acc = inv(A^T A) A^T b (wamv.py:271) */
+  double a0 = p->P[0] * b0 + p->P[1] * b1 + p->P[2] * b2;
+  double a1 = p->P[3] * b0 + p->P[4] * b1 + p->P[5] * b2;
+  double a2 = p->P[6] * b0 + p->P[7] * b1 + p->P[8] * b2;
+  double w0 = u_r + a0 * p->dt, w1 = v_r + a1 * p->dt, w2 = r + a2 * p->dt;
+  /* back to world frame with R_wr = [[c, -s], [s, c]] (wamv.py:277-279) */
+  rb->vr[0] = c * w0 + -s * w1;
+  rb->vr[1] = s * w0 + c * w1;
+  rb->vr[2] = w2;
+}
+
+static void update_state(const OrParams* p, OrRobot* rb, const double action[2],
+                         const double cur[3], int is_new, int continuous) {
+  /* update_velocity (wamv.py:201-202) */
+  rb->v[0] = rb->vr[0] + cur[0];
+  rb->v[1] = rb->vr[1] + cur[1];
+  rb->v[2] = rb->vr[2] + cur[2];
+  rb->x += rb->v[0] * p->dt;
+  rb->y += rb->v[1] * p->dt;
+  rb->theta += rb->v[2] * p->dt;
+  while (rb->theta < 0.0) rb->theta += 2 * PI;       /* wamv.py:213-216 */
+  while (rb->theta >= 2 * PI) rb->theta -= 2 * PI;
+  if (is_new) {
+    double l, r;
+    if (continuous) { l = action[0] * 1000.0; r = action[1] * 1000.0; }
+    else {
+      int a = (int)action[0];
+      l = p->thrust_change[a / 5];
+      r = p->thrust_change[a % 5];
+    }
+    rb->tl += l * p->dt * p->N;
+    rb->tl = rb->tl < p->min_thrust ? p->min_thrust : (rb->tl > p->max_thrust ? p->max_thrust : rb->tl);
+    rb->tr += r * p->dt * p->N;
+    rb->tr = rb->tr < p->min_thrust ? p->min_thrust : (rb->tr > p->max_thrust ? p->max_thrust : rb->tr);
+  }
+  compute_motion(p, rb);
+}
+
+static double dist_to_goal(const OrRobot* rb) { /* wamv.py:167-168 */
+  double dx = rb->goal[0] - rb->x, dy = rb->goal[1] - rb->y;
+  return sqrt(dx * dx + dy * dy);
+}
+
+double or_robot_act(const OrParams* p, OrRobot* rb, const double action[2], int continuous,
+                    const double* cores, int n_cores) {
+  double before = dist_to_goal(rb); /* env.py:254 */
+  for (int idx = 0; idx < p->N; ++idx) { /* env.py:257-260 */
+    double cur[3];
+    or_current(cores, n_cores, p->core_r, rb->x, rb->y, cur);
+    update_state(p, rb, action, cur, idx == 0, continuous);
+  }
+  double after = dist_to_goal(rb);
+  double rew = 0;
+  rew += p->timestep_penalty; /* env.py:274 */
+  rew += before - after;      /* env.py:277 */
+  return rew;
+}
+
+/* ---------------------------------------------------------------- perception (wamv.py:436-529) */
+static double wrap_to_pi(double a) { /* wamv.py:425-434 */
+  while (a < -PI) a += 2 * PI;
+  while (a >= PI) a -= 2 * PI;
+  return a;
+}
+
+static int check_apply_colregs(const OrParams* p, OrRobot* rb, const double* obj) {
+  /* wamv.py:398-423 */
+  double ovx = obj[2], ovy = obj[3];
+  if (sqrt(ovx * ovx + ovy * ovy) < 0.5) return 0;
+  double c = cos(rb->theta), s = sin(rb->theta);
+  double ev0 = c * rb->v[0] + s * rb->v[1];
+  double ev1 = -s * rb->v[0] + c * rb->v[1];
+  if (sqrt(ev0 * ev0 + ev1 * ev1) < 0.5) return 0;
+  /* project_ego_to_vehicle_frame (wamv.py:324-342) */
+  double al = atan2(ovy, ovx);
+  double ca = cos(al), sa = sin(al);
+  double px = -ca * obj[0] + -sa * obj[1];
+  double py = sa * obj[0] + -ca * obj[1];
+  double qx = ca * ev0 + sa * ev1;
+  double qy = -sa * ev0 + ca * ev1;
+  /* left crossing zone (wamv.py:344-362) */
+  int x_in = (px >= -9.0) && (px <= 12.0);
+  int y_in = (py >= -17.0) && (py <= 0.0);
+  double x_diff = px - 12.0, y_diff = py - (-7.0);
+  double grad = -7.0 / 12.0;
+  int in_tri = y_diff > grad * x_diff;
+  double ang = atan2(qy, qx);
+  int left = x_in && y_in && !in_tri && (ang >= PI / 4) && (ang <= 3 * PI / 4);
+  /* head-on zone (wamv.py:364-377) */
+  int hx = (px >= 0.0) && (px <= 17.0);
+  int hy = (py >= -0.5 * 9.0) && (py <= 0.5 * 9.0);
+  int head = hx && hy && (fabs(ang) > 3 * PI / 4);
+  if (left || head) {
+    /* compute_COLREGs_turn_angle (wamv.py:379-396) */
+    double ego_ang = atan2(ev1, ev0);
+    double obj_ang = atan2(obj[1], obj[0]);
+    double base1 = obj[4] + 1.0;
+    double dist = sqrt(obj[0] * obj[0] + obj[1] * obj[1]);
+    double add1 = asin(base1 / dist);
+    double tang = sqrt(dist * dist - base1 * base1);
+    double add2 = atan2(p->r, tang);
+    double desired = wrap_to_pi(obj_ang + add1 + add2);
+    rb->phi = wrap_to_pi(desired - ego_ang);
+    return rb->phi > 0 ? 1 : 0;
+  }
+  return 0;
+}
+
+int or_perceive(const OrParams* p, OrRobot* robots, int n_robots, int i, const double* obstacles,
+                int n_obs, int O, const double* noise, double* self_obs, double* objs) {
+  OrRobot* rb = &robots[i];
+  if (rb->deactivated) return -1; /* wamv.py:437-438 */
+  double c = cos(rb->theta), s = sin(rb->theta);
+  /* self observation (wamv.py:443-453) */
+  double gx = rb->goal[0], gy = rb->goal[1];
+  double tx = -(c * rb->x + s * rb->y), ty = -(-s * rb->x + c * rb->y);
+  self_obs[0] = (c * gx + s * gy) + tx;
+  self_obs[1] = (-s * gx + c * gy) + ty;
+  self_obs[2] = c * rb->v[0] + s * rb->v[1];
+  self_obs[3] = -s * rb->v[0] + c * rb->v[1];
+  self_obs[4] = rb->v[2];
+  self_obs[5] = rb->tl;
+  self_obs[6] = rb->tr;
+  if (dist_to_goal(rb) <= p->goal_dis) rb->reach_goal = 1; /* wamv.py:462,170-172 */
+
+  /* candidate list in the reference's append order: obstacles, then other robots */
+  double cand[64][5];
+  double key[64];
+  int nc = 0;
+  const int R_slots = O; /* slot base for robots */
+  for (int pass = 0; pass < 2; ++pass) {
+    int n = pass == 0 ? n_obs : n_robots;
+    for (int k = 0; k < n; ++k) {
+      double ox, oy, orad, vx0, vy0;
+      const double* nz;
+      if (pass == 0) {
+        ox = obstacles[3 * k]; oy = obstacles[3 * k + 1]; orad = obstacles[3 * k + 2];
+        vx0 = 0.0; vy0 = 0.0;
+        nz = noise + 5 * k;
+      } else {
+        if (k == i) continue;
+        if (robots[k].deactivated) continue; /* wamv.py:489-491 */
+        ox = robots[k].x; oy = robots[k].y; orad = p->r;
+        vx0 = robots[k].v[0]; vy0 = robots[k].v[1];
+        nz = noise + 5 * (R_slots + k);
+      }
+      double pxn = ox + nz[0], pyn = oy + nz[1];              /* pos_observation */
+      double vxn = vx0 + nz[2], vyn = vy0 + nz[3];            /* vel_observation */
+      double rn = p->r_mean_ratio * orad +
+                  (1 - p->r_mean_ratio) * nz[4] / PI * orad;  /* r_observation */
+      /* check_detection (wamv.py:293-303) */
+      double qx = (c * pxn + s * pyn) + tx, qy = (-s * pxn + c * pyn) + ty;
+      if (sqrt(qx * qx + qy * qy) > p->range + rn) continue;
+      double ang = atan2(qy, qx);
+      if (ang < -0.5 * p->angle || ang > 0.5 * p->angle) continue;
+      if (!rb->collision) { /* check_collision (wamv.py:281-291) */
+        double d = sqrt((rb->x - ox) * (rb->x - ox) + (rb->y - oy) * (rb->y - oy)) - orad - p->r;
+        if (d <= 0.0) rb->collision = 1;
+      }
+      cand[nc][0] = qx; cand[nc][1] = qy;
+      cand[nc][2] = c * vxn + s * vyn; cand[nc][3] = -s * vxn + c * vyn;
+      cand[nc][4] = rn;
+      key[nc] = sqrt(qx * qx + qy * qy) - rn - p->r; /* compute_distance(in_robot_frame) */
+      ++nc;
+    }
+  }
+  /* heapq.nsmallest(max_obj_num, key) == stable sort by key, first max_obj_num */
+  int idx[64];
+  for (int a = 0; a < nc; ++a) idx[a] = a;
+  for (int a = 1; a < nc; ++a) {
+    int v = idx[a];
+    int b = a - 1;
+    while (b >= 0 && key[idx[b]] > key[v]) { idx[b + 1] = idx[b]; --b; }
+    idx[b + 1] = v;
+  }
+  int cnt = nc < p->max_obj_num ? nc : p->max_obj_num;
+  for (int a = 0; a < cnt; ++a) memcpy(objs + 5 * a, cand[idx[a]], 5 * sizeof(double));
+  rb->apply_colregs = 0; /* wamv.py:517-521 */
+  for (int a = 0; a < cnt; ++a) {
+    if (check_apply_colregs(p, rb, objs + 5 * a)) { rb->apply_colregs = 1; break; }
+  }
+  return cnt;
+}
+
+int or_env_step(const OrParams* p, OrRobot* robots, int n_robots, int R, const double* obstacles,
+                int n_obs, int O, const double* cores, int n_cores, const double* actions,
+                int continuous, const double* noise, int32_t* ep_ts, double* rewards,
+                uint8_t* dones, uint8_t* infos, double* self_obs, double* objs, int32_t* cnt) {
+  for (int i = 0; i < n_robots; ++i) { /* env.py:247-277 */
+    rewards[i] = 0.0;
+    if (robots[i].deactivated) continue;
+    rewards[i] = or_robot_act(p, &robots[i], actions + 2 * i, continuous, cores, n_cores);
+  }
+  for (int i = 0; i < n_robots; ++i) /* get_observations (env.py:341-356) */
+    cnt[i] = or_perceive(p, robots, n_robots, i, obstacles, n_obs, O, noise + (size_t)i * (O + R) * 5,
+                         self_obs + 7 * i, objs + 25 * i);
+  for (int i = 0; i < n_robots; ++i) { /* env.py:294-328 */
+    OrRobot* rb = &robots[i];
+    if (rb->deactivated) {
+      dones[i] = 1;
+      if (rb->collision) infos[i] = 4;
+      else if (rb->reach_goal) infos[i] = 5;
+      else return -1;
+      continue;
+    }
+    double pen = 0.0;
+    if (rb->apply_colregs) pen += p->COLREGs_penalty * rb->phi;
+    rewards[i] += pen;
+    if (*ep_ts >= p->episode_limit) { dones[i] = 1; infos[i] = 1; }
+    else if (rb->collision) { rewards[i] += p->collision_penalty; dones[i] = 1; infos[i] = 2; }
+    else if (rb->reach_goal) { rewards[i] += p->goal_reward; dones[i] = 1; infos[i] = 3; }
+    else { dones[i] = 0; infos[i] = 0; }
+  }
+  *ep_ts += 1;
+  return 0;
+}
+
+/* ---------------------------------------------------------------- C51 (agent.py:616-631) */
+void or_c51_project(const float* pns_a, const float* returns, const float* nonterminal,
+                    const float* support, int B, int atoms, float vmin, float vmax,
+                    float gamma_n, float* m) {
+  float dz = (vmax - vmin) / (float)(atoms - 1);
+  (void)dz;
+  long* l = (long*)malloc(sizeof(long) * atoms);
+  long* u = (long*)malloc(sizeof(long) * atoms);
+  float* bb = (float*)malloc(sizeof(float) * atoms);
+  float delta = (float)(((double)vmax - (double)vmin) / (double)(atoms - 1));
+  for (int b = 0; b < B; ++b) {
+    float ntg = nonterminal[b] * gamma_n;
+    for (int j = 0; j < atoms; ++j) {
+      float tz = returns[b] + ntg * support[j];
+      tz = tz < vmin ? vmin : (tz > vmax ? vmax : tz);
+      float bj = (tz - vmin) / delta;
+      bb[j] = bj;
+      l[j] = (long)floorf(bj);
+      u[j] = (long)ceilf(bj);
+    }
+    for (int j = 0; j < atoms; ++j) if (u[j] > 0 && l[j] == u[j]) l[j] -= 1;
+    for (int j = 0; j < atoms; ++j) if (l[j] < atoms - 1 && l[j] == u[j]) u[j] += 1;
+    float* mb = m + (size_t)b * atoms;
+    for (int j = 0; j < atoms; ++j) mb[j] = 0.0f;
+    const float* pb = pns_a + (size_t)b * atoms;
+    for (int j = 0; j < atoms; ++j) mb[l[j]] += pb[j] * ((float)u[j] - bb[j]);
+    for (int j = 0; j < atoms; ++j) mb[u[j]] += pb[j] * (bb[j] - (float)l[j]);
+  }
+  free(l); free(u); free(bb);
+}
+
+/* ---------------------------------------------------------------- batched CPU baseline */
+typedef struct { uint32_t v[4]; } u32x4;
+
+static u32x4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+  for (int r = 0; r < 10; ++r) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0, h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
+    uint32_t n0 = h1 ^ c1 ^ k0, n2 = h0 ^ c3 ^ k1;
+    c0 = n0; c1 = l1; c2 = n2; c3 = l0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  u32x4 o = {{c0, c1, c2, c3}};
+  return o;
+}
+
+typedef struct { uint32_t c0, c1, c2, c3, k0, k1; u32x4 buf; int left; } Rng;
+
+static double rng_u01(Rng* g) { /* (0, 1] double from 2x u32 */
+  if (g->left == 0) {
+    g->buf = philox(g->c0, g->c1, g->c2, g->c3, g->k0, g->k1);
+    g->c3++;
+    g->left = 2;
+  }
+  int k = 2 - g->left;
+  g->left--;
+  uint64_t hi = g->buf.v[2 * k], lo = g->buf.v[2 * k + 1];
+  uint64_t x = ((hi << 32) | lo) >> 11;
+  return ((double)x + 1.0) * (1.0 / 9007199254740992.0);
+}
+
+static double rng_normal(Rng* g) {
+  double u1 = rng_u01(g), u2 = rng_u01(g);
+  return sqrt(-2.0 * log(u1)) * cos(2 * PI * u2);
+}
+
+static double rng_vonmises(Rng* g, double kappa) { /* Best & Fisher, numpy legacy form */
+  double rr = 1 + sqrt(1 + 4 * kappa * kappa);
+  double rho = (rr - sqrt(2 * rr)) / (2 * kappa);
+  double s = (1 + rho * rho) / (2 * rho);
+  double W;
+  for (int it = 0; it < 64; ++it) {
+    double U = rng_u01(g);
+    double Z = cos(PI * U);
+    W = (1 + s * Z) / (s + Z);
+    double Y = kappa * (s - W);
+    double V = rng_u01(g);
+    if ((Y * (2 - Y) - V >= 0) || (log(Y / V) + 1 - Y >= 0)) break;
+  }
+  double U = rng_u01(g);
+  double res = acos(W);
+  if (U < 0.5) res = -res;
+  return res;
+}
+
+static void reset_env(const OrParams* p, OrRobot* rob, int R, double* obs, int O, int* n_rob,
+                      int* n_obs, Rng* g, double W, double msgd) {
+  int nr = 0;
+  for (int it = 0; it < 500 && nr < R; ++it) { /* env.py:106-120 */
+    double sx = 2 + (W - 4) * rng_u01(g), sy = 2 + (W - 4) * rng_u01(g);
+    double gx = 2 + (W - 4) * rng_u01(g), gy = 2 + (W - 4) * rng_u01(g);
+    int ok = sqrt((gx - sx) * (gx - sx) + (gy - sy) * (gy - sy)) >= msgd;
+    for (int k = 0; k < nr && ok; ++k) {
+      double ds = hypot(rob[k].x - sx, rob[k].y - sy), dg = hypot(rob[k].goal[0] - gx, rob[k].goal[1] - gy);
+      if (ds <= 10.0 || dg <= 10.0) ok = 0;
+    }
+    if (!ok) continue;
+    OrRobot* rb = &rob[nr++];
+    memset(rb, 0, sizeof(*rb));
+    rb->x = sx; rb->y = sy; rb->goal[0] = gx; rb->goal[1] = gy;
+    rb->theta = 2 * PI * (1.0 - rng_u01(g));
+  }
+  int no = 0;
+  for (int it = 0; it < 500 && no < O; ++it) { /* env.py:151-162 */
+    double ox = 5 + (W - 10) * rng_u01(g), oy = 5 + (W - 10) * rng_u01(g), orad = 1.0;
+    int ok = 1;
+    for (int k = 0; k < nr && ok; ++k)
+      if (hypot(ox - rob[k].x, oy - rob[k].y) < orad + 10.0 || hypot(ox - rob[k].goal[0], oy - rob[k].goal[1]) < orad + 10.0) ok = 0;
+    for (int k = 0; k < no && ok; ++k)
+      if (hypot(obs[3 * k] - ox, obs[3 * k + 1] - oy) <= obs[3 * k + 2] + orad) ok = 0;
+    if (!ok) continue;
+    obs[3 * no] = ox; obs[3 * no + 1] = oy; obs[3 * no + 2] = orad;
+    ++no;
+  }
+  *n_rob = nr;
+  *n_obs = no;
+}
+
+int64_t or_batch_rollout(const OrParams* p, int E, int R, int O, int steps, uint64_t seed,
+                         int threads, double* checksum) {
+  int64_t total = 0;
+  double chk = 0.0;
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(static) reduction(+ : total, chk)
+#endif
+  for (int e = 0; e < E; ++e) {
+    OrRobot rob[64];
+    double obs[3 * 64];
+    int nr, no;
+    Rng g = {(uint32_t)e, 0, 0, 0, (uint32_t)seed, (uint32_t)(seed >> 32), {{0, 0, 0, 0}}, 0};
+    reset_env(p, rob, R, obs, O, &nr, &no, &g, 55.0, 40.0);
+    int32_t ep_ts = 0;
+    double* noise = (double*)malloc(sizeof(double) * R * (O + R) * 5);
+    double act[2 * 64], rew[64], so[7 * 64], ob[25 * 64];
+    uint8_t dn[64], inf[64];
+    int32_t cnt[64];
+    for (int t = 0; t < steps; ++t) {
+      for (int i = 0; i < nr; ++i) {
+        act[2 * i] = 2 * rng_u01(&g) - 1;
+        act[2 * i + 1] = 2 * rng_u01(&g) - 1;
+        if (rob[i].deactivated) continue;
+        for (int k = 0; k < O + nr; ++k) {
+          double* nz = noise + ((size_t)i * (O + R) + k) * 5;
+          nz[0] = 0.05 * rng_normal(&g); nz[1] = 0.05 * rng_normal(&g);
+          nz[2] = 0.05 * rng_normal(&g); nz[3] = 0.05 * rng_normal(&g);
+          nz[4] = rng_vonmises(&g, 1.0);
+        }
+      }
+      or_env_step(p, rob, nr, R, obs, no, O, NULL, 0, act, 1, noise, &ep_ts, rew, dn, inf, so, ob, cnt);
+      total += 1;
+      int all_off = 1;
+      for (int i = 0; i < nr; ++i) {
+        if (!rob[i].deactivated) {
+          chk += rew[i];
+          if (rob[i].collision || rob[i].reach_goal) rob[i].deactivated = 1; /* trainer.py:168-170 */
+        }
+        if (!rob[i].deactivated) all_off = 0;
+      }
+      if (all_off || ep_ts >= p->episode_limit) {
+        reset_env(p, rob, R, obs, O, &nr, &no, &g, 55.0, 40.0);
+        ep_ts = 0;
+      }
+    }
+    free(noise);
+  }
+  if (checksum) *checksum = chk;
+  return total;
+}
