@@ -1,0 +1,201 @@
+"""ctypes binding of libasvrl.so (include/asvrl.h).
+
+The product path has exactly one compute backend: the gfx950 kernels in this library.
+`lib()` raises if the library is missing or was built for another ABI; nothing falls back
+to a CPU implementation.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libasvrl.so")
+ABI_VERSION = 1
+
+SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
+OBS_DIM = 40   # self 7 | objects 25 | mask 5 | pad 3
+TR_DIM = 88    # obs 40 | next obs 40 | action 2 | reward | done | pad 4
+
+# robot state fields (enum AsvRobotField)
+F_X, F_Y, F_THETA, F_VR0, F_VR1, F_VR2, F_V0, F_V1, F_V2, F_TL, F_TR, F_LP, F_RP, F_GX, F_GY, F_PHI, F_RET = range(17)
+NUM_FIELDS = 17
+
+FLAG_DEACTIVATED, FLAG_COLLISION, FLAG_REACH_GOAL, FLAG_COLREGS = 1, 2, 4, 8
+
+INFO_NORMAL, INFO_TOO_LONG, INFO_COLLISION, INFO_REACH_GOAL, INFO_DEACT_COLLISION, INFO_DEACT_GOAL = range(6)
+INFO_ABSENT = 255
+INFO_STRINGS = {
+    INFO_NORMAL: "normal",
+    INFO_TOO_LONG: "too long episode",
+    INFO_COLLISION: "collision",
+    INFO_REACH_GOAL: "reach goal",
+    INFO_DEACT_COLLISION: "deactivated after collision",
+    INFO_DEACT_GOAL: "deactivated after reaching goal",
+}
+
+_HYDRO = ["xDotU", "yDotV", "yDotR", "nDotR", "nDotV", "xU", "xUU", "yV", "yVV", "yR", "yRV", "yVR", "yRR",
+          "nR", "nRR", "nV", "nVV", "nRV", "nVR"]
+
+
+class AsvParams(C.Structure):
+    _fields_ = ([("dt", C.c_double), ("N", C.c_int32), ("episode_limit", C.c_int32),
+                 ("length", C.c_double), ("width", C.c_double), ("r", C.c_double), ("goal_dis", C.c_double),
+                 ("min_thrust", C.c_double), ("max_thrust", C.c_double), ("m", C.c_double), ("Izz", C.c_double)]
+                + [(n, C.c_double) for n in _HYDRO]
+                + [("P", C.c_double * 9), ("left_thrust_change", C.c_double * 5),
+                   ("right_thrust_change", C.c_double * 5), ("range", C.c_double), ("angle", C.c_double),
+                   ("pos_std", C.c_double), ("vel_std", C.c_double), ("r_kappa", C.c_double),
+                   ("r_mean_ratio", C.c_double), ("max_obj_num", C.c_int32), ("_pad0", C.c_int32),
+                   ("timestep_penalty", C.c_double), ("COLREGs_penalty", C.c_double),
+                   ("collision_penalty", C.c_double), ("goal_reward", C.c_double), ("core_r", C.c_double)])
+
+
+class AsvEnvState(C.Structure):
+    _fields_ = [("n_envs", C.c_int32), ("max_robots", C.c_int32), ("max_obs", C.c_int32), ("max_cores", C.c_int32),
+                ("rs", C.c_void_p), ("rflags", C.c_void_p), ("n_robots", C.c_void_p), ("n_obs", C.c_void_p),
+                ("n_cores", C.c_void_p), ("ep_ts", C.c_void_p), ("obstacles", C.c_void_p), ("cores", C.c_void_p)]
+
+
+class AsvStepCtl(C.Structure):
+    _fields_ = [("is_continuous", C.c_int32), ("do_dynamics", C.c_int32), ("trainer_deactivate", C.c_int32),
+                ("noise_mode", C.c_int32), ("seed", C.c_uint64), ("counter", C.c_uint64),
+                ("counter_dev", C.c_void_p), ("gamma", C.c_double), ("env_mask", C.c_void_p)]
+
+
+class AsvStepOut(C.Structure):
+    _fields_ = [("obs", C.c_void_p), ("obs64", C.c_void_p), ("obj_cnt", C.c_void_p), ("reward", C.c_void_p),
+                ("done", C.c_void_p), ("info", C.c_void_p), ("env_done", C.c_void_p), ("stats", C.c_void_p)]
+
+
+class AsvResetCfg(C.Structure):
+    _fields_ = [("num_robots", C.c_int32), ("num_obs", C.c_int32), ("num_cores", C.c_int32), ("_pad0", C.c_int32),
+                ("min_start_goal_dis", C.c_double), ("width", C.c_double), ("height", C.c_double),
+                ("clear_r", C.c_double), ("obs_r_lo", C.c_double), ("obs_r_hi", C.c_double), ("v_lo", C.c_double),
+                ("v_hi", C.c_double), ("v_rel_max", C.c_double), ("p_rel", C.c_double)]
+
+
+# (name, restype, argtypes) of every exported entry point, mirroring include/asvrl.h
+_VP, _I32, _I64, _U64, _F, _D = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_float, C.c_double
+EXPORTS = [
+    ("asvrl_env_step", C.c_int, [C.POINTER(AsvParams), C.POINTER(AsvEnvState), _VP, _VP, C.POINTER(AsvStepCtl),
+                                 C.POINTER(AsvStepOut), _VP]),
+    ("asvrl_env_reset", C.c_int, [C.POINTER(AsvParams), C.POINTER(AsvEnvState), C.POINTER(AsvResetCfg), _VP, _U64,
+                                  _U64, _VP, _VP]),
+    ("asvrl_current_field", C.c_int, [_VP, _I32, _D, _VP, _I32, _VP, _VP]),
+    ("asvrl_quantile_huber", C.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, _F, _F, _VP, _VP, _VP, _VP]),
+    ("asvrl_c51_project", C.c_int, [_VP, _VP, _VP, _VP, _I32, _I32, _F, _F, _F, _F, _VP, _VP]),
+    ("asvrl_replay_push", C.c_int, [_VP, _VP, _VP, _VP, _I32, _VP, _VP, _I32, _VP, _I64, _VP, _VP, _VP]),
+    ("asvrl_replay_sample", C.c_int, [_VP, _I64, _VP, _VP, _I32, _U64, _U64, _VP, _VP, _VP, _VP]),
+    ("asvrl_replay_write_rows", C.c_int, [_VP, _VP, _I32, _VP, _VP]),
+    ("asvrl_last_error", C.c_char_p, []),
+    ("asvrl_abi_version", C.c_int, []),
+]
+
+_lib = None
+
+
+class AsvrlError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libasvrl.so (built by __graft_entry__.build / `python -m ...build`). Raises if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise AsvrlError(f"libasvrl.so not found at {LIB_PATH}: build it with "
+                         "`python -m distributional_rl_decision_and_control_amd.build` (hipcc, gfx950). "
+                         "There is no CPU fallback.")
+    L = C.CDLL(LIB_PATH)
+    for name, res, args in EXPORTS:
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    v = L.asvrl_abi_version()
+    if v != ABI_VERSION:
+        raise AsvrlError(f"libasvrl.so ABI {v} != expected {ABI_VERSION}; rebuild")
+    _lib = L
+    return L
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib().asvrl_last_error().decode(errors="replace")
+        raise AsvrlError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(t):
+    """Raw device pointer of a torch tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return C.c_void_p(t.data_ptr())
+
+
+def stream_ptr(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)
+
+
+def params_from(robot=None, env=None, max_obj_num=5, episode_limit=1000):
+    """AsvParams from a Robot-like object (wamv.py:45-125 attribute names) and env rewards.
+
+    P = inv(A^T A) A^T is evaluated with the reference's own numpy matrix expression
+    (wamv.py:267-271) so the kernel multiplies by the exact same f64 constants."""
+    p = AsvParams()
+    src = robot if robot is not None else _DefaultRobot()
+    p.dt = float(src.dt)
+    p.N = int(src.N)
+    p.episode_limit = int(episode_limit)
+    p.length, p.width = float(src.length), float(src.width)
+    p.r = float(src.r)
+    p.goal_dis = float(src.goal_dis)
+    p.min_thrust, p.max_thrust = float(src.min_thrust), float(src.max_thrust)
+    p.m, p.Izz = float(src.m), float(src.Izz)
+    for n in _HYDRO:
+        setattr(p, n, float(getattr(src, n)))
+    import warnings
+    warnings.filterwarnings("ignore", category=PendingDeprecationWarning, message=".*matrix subclass.*")
+    M_RB = np.matrix([[src.m, 0.0, 0.0], [0.0, src.m, 0.0], [0.0, 0.0, src.Izz]])
+    M_A = -1.0 * np.matrix([[src.xDotU, 0.0, 0.0], [0.0, src.yDotV, src.yDotR], [0.0, src.nDotV, src.nDotR]])
+    A = M_RB + M_A
+    P = np.asarray(np.linalg.inv(A.transpose() * A) * A.transpose(), dtype=np.float64).reshape(-1)
+    for k in range(9):
+        p.P[k] = float(P[k])
+    for k in range(5):
+        p.left_thrust_change[k] = float(src.left_thrust_change[k])
+        p.right_thrust_change[k] = float(src.right_thrust_change[k])
+    per = src.perception if hasattr(src, "perception") else src
+    p.range, p.angle = float(per.range), float(per.angle)
+    p.pos_std, p.vel_std = float(per.pos_std), float(per.vel_std)
+    p.r_kappa, p.r_mean_ratio = float(per.r_kappa), float(per.r_mean_ratio)
+    p.max_obj_num = int(getattr(per, "max_obj_num", max_obj_num))
+    e = env if env is not None else _DefaultEnv()
+    p.timestep_penalty = float(e.timestep_penalty)
+    p.COLREGs_penalty = float(e.COLREGs_penalty)
+    p.collision_penalty = float(e.collision_penalty)
+    p.goal_reward = float(e.goal_reward)
+    p.core_r = float(e.r)
+    return p
+
+
+class _DefaultRobot:
+    """Reference defaults (wamv.py:22-25,45-125)."""
+    dt, N, length, width = 0.05, 10, 5.0, 2.5
+    r = 0.5 * np.sqrt(5.0 ** 2 + 2.5 ** 2)
+    goal_dis, min_thrust, max_thrust = 2.0, -500.0, 1000.0
+    m, Izz = 400, 450
+    xDotU, yDotV, yDotR, nDotR, nDotV = 20, 0, 0, -980, 0
+    xU, xUU, yV, yVV, yR, yRV, yVR, yRR = -100, -150, -100, -150, 0, 0, 0, 0
+    nR, nRR, nV, nVV, nRV, nVR = -980, -950, 0, 0, 0, 0
+    left_thrust_change = right_thrust_change = [0.0, -500.0, -1000.0, 500.0, 1000.0]
+    range, angle, max_obj_num = 20.0, 2 * np.pi, 5
+    pos_std, vel_std, r_kappa, r_mean_ratio = 0.05, 0.05, 1.0, 0.8
+
+
+class _DefaultEnv:
+    """Reference defaults (env.py:35,47-50)."""
+    r = 0.5
+    timestep_penalty, COLREGs_penalty, collision_penalty, goal_reward = -0.1, -0.1, -5.0, 10.0

@@ -1,0 +1,44 @@
+"""Build libasvrl.so for gfx950 in-tree (hipcc cross-compiles; no GPU needed).
+
+    python -m distributional_rl_decision_and_control_amd.build [--force]
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SOURCES = [os.path.join(HERE, "csrc", f) for f in ("asvrl_env.hip", "asvrl_learn.hip")]
+HEADERS = [os.path.join(HERE, "csrc", "asvrl_common.h"), os.path.join(ROOT, "include", "asvrl.h")]
+OUT = os.path.join(HERE, "lib", "libasvrl.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("ASVRL_OFFLOAD_ARCH", "gfx950")
+
+# -ffp-contract=off: the env kernel reproduces the reference's f64 operation order; FMA
+# contraction would change rounding (the masks are compared bit-exactly).
+FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=off",
+         "-munsafe-fp-atomics", "-I", os.path.join(ROOT, "include")]
+
+
+def stale():
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    return any(os.path.getmtime(f) > t for f in SOURCES + HEADERS)
+
+
+def build_lib(force=False, verbose=False):
+    if not force and not stale():
+        return OUT
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    tmp = OUT + ".tmp"
+    cmd = [HIPCC] + FLAGS + ["-o", tmp] + SOURCES
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build_lib(force="--force" in sys.argv, verbose=True))

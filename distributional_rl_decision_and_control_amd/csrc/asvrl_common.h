@@ -1,0 +1,103 @@
+// asvrl_common.h -- shared device helpers for libasvrl.so (gfx950): error plumbing for the
+// C ABI, Philox-4x32-10 counter RNG and the distributions the env draws from.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "asvrl.h"
+
+namespace asvrl {
+
+constexpr double kPi = 3.141592653589793;   // np.pi
+constexpr double kTwoPi = 2 * kPi;           // 2 * np.pi (exact doubling)
+constexpr int kWave = 64;                    // CDNA wavefront
+
+void set_error(const std::string& msg);
+int check_launch(const char* what);
+
+#define ASVRL_REQUIRE(cond, msg)            \
+  do {                                      \
+    if (!(cond)) {                          \
+      ::asvrl::set_error(std::string(msg)); \
+      return 1;                             \
+    }                                       \
+  } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ------------------------------------------------------------------ Philox-4x32-10
+struct U4 {
+  uint32_t x, y, z, w;
+};
+
+__host__ __device__ inline U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = static_cast<uint64_t>(0xD2511F53u) * c.x;
+    const uint64_t p1 = static_cast<uint64_t>(0xCD9E8D57u) * c.z;
+    const uint32_t h0 = static_cast<uint32_t>(p0 >> 32), l0 = static_cast<uint32_t>(p0);
+    const uint32_t h1 = static_cast<uint32_t>(p1 >> 32), l1 = static_cast<uint32_t>(p1);
+    c = U4{h1 ^ c.y ^ k0, l1, h0 ^ c.w ^ k1, l0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// Stream of doubles in (0, 1] from one (key, counter-prefix); each Philox call yields two.
+struct Stream {
+  uint32_t k0, k1, c1, c2, c3;
+  uint32_t n;   // calls made
+  U4 buf;
+  int left;
+  __device__ Stream(uint64_t seed, uint32_t a, uint32_t b, uint32_t c)
+      : k0(static_cast<uint32_t>(seed)), k1(static_cast<uint32_t>(seed >> 32)), c1(a), c2(b), c3(c),
+        n(0), buf{0, 0, 0, 0}, left(0) {}
+  __device__ double u01() {
+    if (left == 0) {
+      buf = philox4x32_10(U4{n++, c1, c2, c3}, k0, k1);
+      left = 2;
+    }
+    uint64_t hi, lo;
+    if (left == 2) { hi = buf.x; lo = buf.y; } else { hi = buf.z; lo = buf.w; }
+    --left;
+    const uint64_t bits = ((hi << 32) | lo) >> 11;
+    return (static_cast<double>(bits) + 1.0) * (1.0 / 9007199254740992.0);
+  }
+  // Box-Muller pair
+  __device__ void normal2(double& a, double& b) {
+    const double u1 = u01(), u2 = u01();
+    const double rad = sqrt(-2.0 * log(u1));
+    double s, c;
+    sincos(kTwoPi * u2, &s, &c);
+    a = rad * c;
+    b = rad * s;
+  }
+  // von Mises(mu=0, kappa) by Best & Fisher, the algorithm numpy's legacy vonmises uses
+  __device__ double vonmises(double kappa) {
+    if (kappa < 1e-8) return kPi * (2 * u01() - 1);
+    const double r = 1 + sqrt(1 + 4 * kappa * kappa);
+    const double rho = (r - sqrt(2 * r)) / (2 * kappa);
+    const double s = (1 + rho * rho) / (2 * rho);
+    double W = 1.0;
+    for (int it = 0; it < 256; ++it) {  // acceptance rate > 0.65 at kappa = 1; bounded loop
+      const double U = u01();
+      const double Z = cos(kPi * U);
+      W = (1 + s * Z) / (s + Z);
+      const double Y = kappa * (s - W);
+      const double V = u01();
+      if ((Y * (2 - Y) - V >= 0) || (log(Y / V) + 1 - Y >= 0)) break;
+    }
+    const double U = u01();
+    double res = acos(W);
+    if (U < 0.5) res = -res;
+    return res;
+  }
+};
+
+}  // namespace asvrl

@@ -1,0 +1,686 @@
+// asvrl_env.hip -- the vectorised ASV marine-env step and reset on gfx950.
+//
+// Replaces MarineNavEnv3.step / reset (rfarl/rfarl/envs/marinenav/env.py:72-164,240-333)
+// and the per-robot Robot methods they call (rfarl/rfarl/envs/marinenav/vehicles/wamv.py).
+//
+// Layout: robot state is field-major SoA in HBM (rs[field][e * R + i]); a workgroup of 256
+// lanes owns floor(256 / R) whole envs, lane = (env_in_block, robot). Phase 1 runs the N
+// Fossen substeps of each robot entirely in registers (f64, one sincos per substep). The
+// post-move positions/velocities of the block's robots and the env's buoys are then staged
+// in LDS, and phase 2 does each robot's perception sweep over obstacles + other vehicles
+// from LDS, keeping the 5 nearest candidates in registers (stable insertion network), then
+// COLREGs, reward, done/info and -- in the fused training loop -- trainer.py's deactivation
+// and the episode-end test, reduced per env through LDS.
+//
+// Arithmetic follows the reference's operation order (np.matrix products as explicit row
+// sums, no FMA contraction: built with -ffp-contract=off) so f64 state agrees with the
+// reference to ~1e-14 and collision/goal/done masks bit-exactly.
+#include "asvrl_common.h"
+
+namespace asvrl {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kMaxCores = 16;
+
+struct Regs {
+  double x, y, th, vr0, vr1, vr2, v0, v1, v2, tl, tr, lp, rp;
+};
+
+__device__ inline double clampd(double v, double lo, double hi) {  // np.clip
+  return v < lo ? lo : (v > hi ? hi : v);
+}
+
+// env.py:458-501. Cores contribute in ascending-distance order (KDTree query with k = all).
+__device__ inline void current_at(const double* __restrict__ cores, int nc, double core_r, double x,
+                                  double y, double& cx, double& cy) {
+  cx = 0.0;
+  cy = 0.0;
+  if (nc <= 0) return;
+  double prev_d = -1.0;
+  int prev_k = -1;
+  for (int t = 0; t < nc; ++t) {
+    double best_d = 0.0;
+    int best_k = -1;
+    for (int k = 0; k < nc; ++k) {
+      const double dx = cores[4 * k] - x, dy = cores[4 * k + 1] - y;
+      const double d = sqrt(dx * dx + dy * dy);
+      const bool after = (d > prev_d) || (d == prev_d && k > prev_k);
+      if (after && (best_k < 0 || d < best_d)) {
+        best_d = d;
+        best_k = k;
+      }
+    }
+    prev_d = best_d;
+    prev_k = best_k;
+    const double* c = cores + 4 * best_k;
+    double rx = c[0] - x, ry = c[1] - y;
+    const double dis = sqrt(rx * rx + ry * ry);
+    rx /= dis;
+    ry /= dis;
+    double tx, ty;
+    if (c[2] != 0.0) { tx = -ry; ty = rx; } else { tx = ry; ty = -rx; }
+    const double sp = dis <= core_r ? c[3] / (2 * kPi * core_r * core_r) * dis : c[3] / (2 * kPi * dis);
+    cx += tx * sp;
+    cy += ty * sp;
+  }
+}
+
+// One robot's action: N substeps of Robot.update_state (wamv.py:204-231) + compute_motion
+// (wamv.py:233-279) with the current sampled at the pre-move position (env.py:257-260).
+__device__ inline void robot_act(const AsvParams& p, Regs& r, double a0, double a1, int continuous,
+                                 const double* cores, int nc) {
+  // propulsion (wamv.py:251-264) depends only on the thrusts, which change on substep 0
+  double fx = 0, fy = 0, mn = 0;
+  const double clp = cos(r.lp), slp = sin(r.lp), crp = cos(r.rp), srp = sin(r.rp);
+  for (int idx = 0; idx < p.N; ++idx) {
+    double cx = 0.0, cy = 0.0;
+    if (nc > 0) current_at(cores, nc, p.core_r, r.x, r.y, cx, cy);
+    r.v0 = r.vr0 + cx;  // update_velocity (wamv.py:201-202)
+    r.v1 = r.vr1 + cy;
+    r.v2 = r.vr2 + 0.0;
+    r.x += r.v0 * p.dt;
+    r.y += r.v1 * p.dt;
+    r.th += r.v2 * p.dt;
+    while (r.th < 0.0) r.th += kTwoPi;
+    while (r.th >= kTwoPi) r.th -= kTwoPi;
+    if (idx == 0) {
+      double l, rr;
+      if (continuous) {
+        l = a0 * 1000.0;
+        rr = a1 * 1000.0;
+      } else {
+        const int a = static_cast<int>(a0);
+        l = p.left_thrust_change[a / 5];
+        rr = p.right_thrust_change[a % 5];
+      }
+      r.tl = clampd(r.tl + l * p.dt * p.N, p.min_thrust, p.max_thrust);
+      r.tr = clampd(r.tr + rr * p.dt * p.N, p.min_thrust, p.max_thrust);
+      const double fxl = r.tl * clp, fyl = r.tl * slp;
+      const double fxr = r.tr * crp, fyr = r.tr * srp;
+      const double mxl = fxl * p.width / 2, myl = -fyl * p.length / 2;
+      const double mxr = -fxr * p.width / 2, myr = -fyr * p.length / 2;
+      fx = fxl + fxr;
+      fy = fyl + fyr;
+      mn = mxl + myl + mxr + myr;
+    }
+    // compute_motion
+    double s, c;
+    sincos(r.th, &s, &c);
+    const double u_r = c * r.vr0 + s * r.vr1;
+    const double v_r = -s * r.vr0 + c * r.vr1;
+    const double u = c * r.v0 + s * r.v1;
+    const double v = -s * r.v0 + c * r.v1;
+    const double w = r.v2;
+    const double mr = p.m * w;
+    const double cv0 = -(-mr * v), cv1 = -(mr * u), cv2 = 0.0;
+    const double ca02 = p.yDotV * v_r + p.yDotR * w;
+    const double ca12 = -p.xDotU * u_r;
+    const double ca20 = -p.yDotV * v_r - p.yDotR * w;
+    const double ca21 = p.xDotU * u_r;
+    const double au = fabs(u_r), av = fabs(v_r), ar = fabs(w);
+    const double n00 = (0.0 + -p.xU) + -(p.xUU * au);
+    const double n02 = (ca02 + -0.0) + -0.0;
+    const double n11 = (0.0 + -p.yV) + -(p.yVV * av + p.yRV * ar);
+    const double n12 = (ca12 + -p.yR) + -(p.yVR * av + p.yRR * ar);
+    const double n20 = (ca20 + -0.0) + -0.0;
+    const double n21 = (ca21 + -p.nV) + -(p.nVV * av + p.nRV * ar);
+    const double n22 = (0.0 + -p.nR) + -(p.nVR * av + p.nRR * ar);
+    const double nv0 = n00 * u_r + 0.0 * v_r + n02 * w;
+    const double nv1 = 0.0 * u_r + n11 * v_r + n12 * w;
+    const double nv2 = n20 * u_r + n21 * v_r + n22 * w;
+    const double b0 = cv0 - nv0 + fx, b1 = cv1 - nv1 + fy, b2 = cv2 - nv2 + mn;
+    const double acc0 = p.P[0] * b0 + p.P[1] * b1 + p.P[2] * b2;
+    const double acc1 = p.P[3] * b0 + p.P[4] * b1 + p.P[5] * b2;
+    const double acc2 = p.P[6] * b0 + p.P[7] * b1 + p.P[8] * b2;
+    const double w0 = u_r + acc0 * p.dt, w1 = v_r + acc1 * p.dt, w2 = w + acc2 * p.dt;
+    r.vr0 = c * w0 + -s * w1;
+    r.vr1 = s * w0 + c * w1;
+    r.vr2 = w2;
+  }
+}
+
+__device__ inline double wrap_to_pi(double a) {  // wamv.py:425-434
+  while (a < -kPi) a += kTwoPi;
+  while (a >= kPi) a -= kTwoPi;
+  return a;
+}
+
+// check_apply_COLREGs (wamv.py:398-423) for one kept object; phi written when evaluated.
+__device__ __attribute__((noinline)) bool colregs(double rself, double c, double s, double v0, double v1,
+                               double ox, double oy, double ovx, double ovy, double orad,
+                               double& phi) {
+  if (sqrt(ovx * ovx + ovy * ovy) < 0.5) return false;
+  const double ev0 = c * v0 + s * v1;
+  const double ev1 = -s * v0 + c * v1;
+  if (sqrt(ev0 * ev0 + ev1 * ev1) < 0.5) return false;
+  const double al = atan2(ovy, ovx);  // project_ego_to_vehicle_frame (wamv.py:324-342)
+  double sa, ca;
+  sincos(al, &sa, &ca);
+  const double px = -ca * ox + -sa * oy;
+  const double py = sa * ox + -ca * oy;
+  const double qx = ca * ev0 + sa * ev1;
+  const double qy = -sa * ev0 + ca * ev1;
+  const double ang = atan2(qy, qx);
+  const bool x_in = (px >= -9.0) && (px <= 12.0);  // wamv.py:344-362
+  const bool y_in = (py >= -17.0) && (py <= 0.0);
+  const bool in_tri = (py - (-7.0)) > (-7.0 / 12.0) * (px - 12.0);
+  const bool left = x_in && y_in && !in_tri && (ang >= kPi / 4) && (ang <= 3 * kPi / 4);
+  const bool head = (px >= 0.0) && (px <= 17.0) && (py >= -0.5 * 9.0) && (py <= 0.5 * 9.0) &&
+                    (fabs(ang) > 3 * kPi / 4);  // wamv.py:364-377
+  if (!(left || head)) return false;
+  const double ego_ang = atan2(ev1, ev0);  // compute_COLREGs_turn_angle (wamv.py:379-396)
+  const double obj_ang = atan2(oy, ox);
+  const double base1 = orad + 1.0;
+  const double dist = sqrt(ox * ox + oy * oy);
+  const double add1 = asin(base1 / dist);
+  const double tang = sqrt(dist * dist - base1 * base1);
+  const double add2 = atan2(rself, tang);
+  const double desired = wrap_to_pi(obj_ang + add1 + add2);
+  phi = wrap_to_pi(desired - ego_ang);
+  return phi > 0;
+}
+
+struct Cand {
+  double key, a, b, c, d, e;
+};
+
+__device__ inline void cswap(bool cond, Cand& x, Cand& y) {
+  if (cond) {
+    const Cand t = x;
+    x = y;
+    y = t;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void env_step_kernel(AsvParams p, AsvEnvState s,
+                                                          const double* __restrict__ actions,
+                                                          const double* __restrict__ noise,
+                                                          AsvStepCtl ctl, AsvStepOut out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int R = s.max_robots;
+  const int O = s.max_obs;
+  const int epb = kBlock / R;
+  const int tid = threadIdx.x;
+  const int le = tid / R;
+  const int i = tid - le * R;
+  const int e = blockIdx.x * epb + le;
+  const bool lane_env = (le < epb) && (e < s.n_envs);
+  const bool env_on = lane_env && (ctl.env_mask == nullptr || ctl.env_mask[e] != 0);
+  const int nrob = lane_env ? s.n_robots[e] : 0;
+  const bool exists = env_on && i < nrob;
+  const size_t NT = static_cast<size_t>(s.n_envs) * R;
+  const size_t idx = static_cast<size_t>(e) * R + i;
+
+  // LDS carve (16-B aligned pieces): positions/velocities of the block's robots after the
+  // move, their pre-step deactivated flags, the envs' obstacles and per-env reductions.
+  double* sx = reinterpret_cast<double*>(smem);
+  double* sy = sx + kBlock;
+  double* sv0 = sy + kBlock;
+  double* sv1 = sv0 + kBlock;
+  double* sob = sv1 + kBlock;  // [epb][O][3]
+  int* salive = reinterpret_cast<int*>(sob + static_cast<size_t>(epb) * O * 3);  // [epb]
+  unsigned char* soff = reinterpret_cast<unsigned char*>(salive + epb);          // [kBlock]
+
+  Regs r{};
+  uint8_t fl = 0;
+  if (exists) {
+    const double* rs = s.rs;
+    r.x = rs[ASVRL_F_X * NT + idx];
+    r.y = rs[ASVRL_F_Y * NT + idx];
+    r.th = rs[ASVRL_F_THETA * NT + idx];
+    r.vr0 = rs[ASVRL_F_VR0 * NT + idx];
+    r.vr1 = rs[ASVRL_F_VR1 * NT + idx];
+    r.vr2 = rs[ASVRL_F_VR2 * NT + idx];
+    r.v0 = rs[ASVRL_F_V0 * NT + idx];
+    r.v1 = rs[ASVRL_F_V1 * NT + idx];
+    r.v2 = rs[ASVRL_F_V2 * NT + idx];
+    r.tl = rs[ASVRL_F_TL * NT + idx];
+    r.tr = rs[ASVRL_F_TR * NT + idx];
+    r.lp = rs[ASVRL_F_LP * NT + idx];
+    r.rp = rs[ASVRL_F_RP * NT + idx];
+    fl = s.rflags[idx];
+  }
+  const bool deact = (fl & ASVRL_FLAG_DEACTIVATED) != 0;
+  const bool active = exists && !deact;
+  const int ep_ts = env_on ? s.ep_ts[e] : 0;
+  double gx = 0, gy = 0;
+  if (exists) {
+    gx = s.rs[ASVRL_F_GX * NT + idx];
+    gy = s.rs[ASVRL_F_GY * NT + idx];
+  }
+
+  // ---------------- phase 1: dynamics (env.py:247-277)
+  double reward = 0.0;
+  if (active && ctl.do_dynamics) {
+    const double d_before = sqrt((gx - r.x) * (gx - r.x) + (gy - r.y) * (gy - r.y));
+    const int nc = s.n_cores[e];
+    const double* cores = s.cores + static_cast<size_t>(e) * s.max_cores * 4;
+    robot_act(p, r, actions[2 * idx], actions[2 * idx + 1], ctl.is_continuous, cores,
+              nc < s.max_cores ? nc : s.max_cores);
+    const double d_after = sqrt((gx - r.x) * (gx - r.x) + (gy - r.y) * (gy - r.y));
+    reward = 0.0;
+    reward += p.timestep_penalty;
+    reward += d_before - d_after;
+  }
+
+  // ---------------- stage for perception
+  sx[tid] = r.x;
+  sy[tid] = r.y;
+  sv0[tid] = r.v0;
+  sv1[tid] = r.v1;
+  soff[tid] = exists ? (deact ? 1 : 0) : 1;
+  if (env_on) {
+    const int no = s.n_obs[e];
+    for (int k = i; k < O; k += R) {
+      const double* ob = s.obstacles + (static_cast<size_t>(e) * O + k) * 3;
+      double* dst = sob + (static_cast<size_t>(le) * O + k) * 3;
+      if (k < no) {
+        dst[0] = ob[0];
+        dst[1] = ob[1];
+        dst[2] = ob[2];
+      }
+    }
+    if (i == 0) salive[le] = 0;
+  }
+  __syncthreads();
+
+  // ---------------- phase 2: perception_output (wamv.py:436-529)
+  bool coll = (fl & ASVRL_FLAG_COLLISION) != 0;
+  bool reach = (fl & ASVRL_FLAG_REACH_GOAL) != 0;
+  bool apply = false;
+  double phi = exists ? s.rs[ASVRL_F_PHI * NT + idx] : 0.0;
+  int cnt = -1;
+  Cand t0{INFINITY, 0, 0, 0, 0, 0}, t1 = t0, t2 = t0, t3 = t0, t4 = t0;
+  double so0 = 0, so1 = 0, so2 = 0, so3 = 0, so4 = 0;
+  if (active) {
+    double sn, cs;
+    sincos(r.th, &sn, &cs);
+    const double tx = -(cs * r.x + sn * r.y), ty = -(-sn * r.x + cs * r.y);
+    so0 = (cs * gx + sn * gy) + tx;
+    so1 = (-sn * gx + cs * gy) + ty;
+    so2 = cs * r.v0 + sn * r.v1;
+    so3 = -sn * r.v0 + cs * r.v1;
+    so4 = r.v2;
+    if (sqrt((gx - r.x) * (gx - r.x) + (gy - r.y) * (gy - r.y)) <= p.goal_dis) reach = true;
+
+    const int no = s.n_obs[e];
+    const int base = le * R;
+    const double* nz_base =
+        noise != nullptr ? noise + idx * static_cast<size_t>(O + R) * 5 : nullptr;
+    const uint64_t ctr = ctl.counter + (ctl.counter_dev != nullptr ? *ctl.counter_dev : 0ull);
+    Stream rng(ctl.seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull, static_cast<uint32_t>(idx),
+               static_cast<uint32_t>(idx >> 32) ^ 0x5EEDu, static_cast<uint32_t>(ctr));
+    int nkept = 0;
+    const int ncand = no + nrob;
+    for (int k = 0; k < ncand; ++k) {
+      double ox, oy, orad, vx0, vy0;
+      int slot;
+      if (k < no) {
+        const double* ob = sob + (static_cast<size_t>(le) * O + k) * 3;
+        ox = ob[0];
+        oy = ob[1];
+        orad = ob[2];
+        vx0 = 0.0;
+        vy0 = 0.0;
+        slot = k;
+      } else {
+        const int j = k - no;
+        if (j == i || soff[base + j]) continue;  // self / deactivated (wamv.py:487-491)
+        ox = sx[base + j];
+        oy = sy[base + j];
+        orad = p.r;
+        vx0 = sv0[base + j];
+        vy0 = sv1[base + j];
+        slot = O + j;
+      }
+      double n0, n1, n2, n3, n4;
+      if (ctl.noise_mode == 0) {
+        const double* nz = nz_base + slot * 5;
+        n0 = nz[0]; n1 = nz[1]; n2 = nz[2]; n3 = nz[3]; n4 = nz[4];
+      } else {
+        rng.normal2(n0, n1);
+        rng.normal2(n2, n3);
+        n0 *= p.pos_std; n1 *= p.pos_std; n2 *= p.vel_std; n3 *= p.vel_std;
+        n4 = rng.vonmises(p.r_kappa);
+      }
+      const double pxn = ox + n0, pyn = oy + n1;  // Perception (wamv.py:27-40)
+      const double vxn = vx0 + n2, vyn = vy0 + n3;
+      const double rn = p.r_mean_ratio * orad + (1 - p.r_mean_ratio) * n4 / kPi * orad;
+      const double qx = (cs * pxn + sn * pyn) + tx, qy = (-sn * pxn + cs * pyn) + ty;
+      const double qn = sqrt(qx * qx + qy * qy);
+      if (qn > p.range + rn) continue;  // check_detection (wamv.py:293-303)
+      const double ang = atan2(qy, qx);
+      if (ang < -0.5 * p.angle || ang > 0.5 * p.angle) continue;
+      if (!coll) {  // check_collision (wamv.py:281-291), true positions
+        const double d = sqrt((r.x - ox) * (r.x - ox) + (r.y - oy) * (r.y - oy)) - orad - p.r;
+        if (d <= 0.0) coll = true;
+      }
+      Cand cd{qn - rn - p.r, qx, qy, cs * vxn + sn * vyn, -sn * vxn + cs * vyn, rn};
+      // heapq.nsmallest == stable ascending order: a new candidate passes equal keys
+      cswap(cd.key < t0.key, cd, t0);
+      cswap(cd.key < t1.key, cd, t1);
+      cswap(cd.key < t2.key, cd, t2);
+      cswap(cd.key < t3.key, cd, t3);
+      cswap(cd.key < t4.key, cd, t4);
+      ++nkept;
+    }
+    cnt = nkept < p.max_obj_num ? nkept : p.max_obj_num;
+    // COLREGs over the kept objects in order, stop at the first hit (wamv.py:517-521)
+    if (cnt > 0) apply = colregs(p.r, cs, sn, r.v0, r.v1, t0.a, t0.b, t0.c, t0.d, t0.e, phi);
+    if (!apply && cnt > 1) apply = colregs(p.r, cs, sn, r.v0, r.v1, t1.a, t1.b, t1.c, t1.d, t1.e, phi);
+    if (!apply && cnt > 2) apply = colregs(p.r, cs, sn, r.v0, r.v1, t2.a, t2.b, t2.c, t2.d, t2.e, phi);
+    if (!apply && cnt > 3) apply = colregs(p.r, cs, sn, r.v0, r.v1, t3.a, t3.b, t3.c, t3.d, t3.e, phi);
+    if (!apply && cnt > 4) apply = colregs(p.r, cs, sn, r.v0, r.v1, t4.a, t4.b, t4.c, t4.d, t4.e, phi);
+  }
+
+  // ---------------- reward / done / info (env.py:290-331)
+  uint8_t done = 1, info = ASVRL_INFO_ABSENT;
+  if (exists) {
+    if (deact) {
+      reward = 0.0;
+      done = 1;
+      info = coll ? ASVRL_INFO_DEACT_COLLISION : (reach ? ASVRL_INFO_DEACT_GOAL : ASVRL_INFO_ABSENT);
+    } else if (ctl.do_dynamics) {
+      double pen = 0.0;
+      if (apply) pen += p.COLREGs_penalty * phi;
+      reward += pen;
+      if (ep_ts >= p.episode_limit) {
+        done = 1;
+        info = ASVRL_INFO_TOO_LONG;
+      } else if (coll) {
+        reward += p.collision_penalty;
+        done = 1;
+        info = ASVRL_INFO_COLLISION;
+      } else if (reach) {
+        reward += p.goal_reward;
+        done = 1;
+        info = ASVRL_INFO_REACH_GOAL;
+      } else {
+        done = 0;
+        info = ASVRL_INFO_NORMAL;
+      }
+    } else {
+      done = 0;
+      info = ASVRL_INFO_NORMAL;
+    }
+  }
+
+  // ---------------- trainer-side bookkeeping (trainer.py:157-172), fused
+  uint8_t nfl = static_cast<uint8_t>((fl & ASVRL_FLAG_DEACTIVATED) | (coll ? ASVRL_FLAG_COLLISION : 0) |
+                                     (reach ? ASVRL_FLAG_REACH_GOAL : 0) | (apply ? ASVRL_FLAG_COLREGS : 0));
+  double ret = 0.0;
+  if (exists) ret = s.rs[ASVRL_F_RET * NT + idx];
+  if (active && ctl.do_dynamics && ctl.trainer_deactivate) {
+    if (ctl.gamma > 0) ret += pow(ctl.gamma, static_cast<double>(ep_ts)) * reward;
+    if (coll || reach) nfl |= ASVRL_FLAG_DEACTIVATED;
+  }
+  if (ctl.trainer_deactivate && ctl.do_dynamics && exists && !(nfl & ASVRL_FLAG_DEACTIVATED))
+    atomicAdd(&salive[le], 1);
+
+  // ---------------- write back
+  if (exists) {
+    double* rs = s.rs;
+    if (ctl.do_dynamics) {
+      rs[ASVRL_F_X * NT + idx] = r.x;
+      rs[ASVRL_F_Y * NT + idx] = r.y;
+      rs[ASVRL_F_THETA * NT + idx] = r.th;
+      rs[ASVRL_F_VR0 * NT + idx] = r.vr0;
+      rs[ASVRL_F_VR1 * NT + idx] = r.vr1;
+      rs[ASVRL_F_VR2 * NT + idx] = r.vr2;
+      rs[ASVRL_F_V0 * NT + idx] = r.v0;
+      rs[ASVRL_F_V1 * NT + idx] = r.v1;
+      rs[ASVRL_F_V2 * NT + idx] = r.v2;
+      rs[ASVRL_F_TL * NT + idx] = r.tl;
+      rs[ASVRL_F_TR * NT + idx] = r.tr;
+      rs[ASVRL_F_RET * NT + idx] = ret;
+    }
+    rs[ASVRL_F_PHI * NT + idx] = phi;
+    s.rflags[idx] = nfl;
+  }
+  if (env_on && i < R) {
+    // packed f32 obs row (replay_buffer.py:51-69 + the .float() of agent.py:363-366)
+    float4* o4 = reinterpret_cast<float4*>(out.obs + idx * ASVRL_OBS_DIM);
+    const bool a = active;
+    const float m0 = (a && cnt > 0) ? 1.f : 0.f, m1 = (a && cnt > 1) ? 1.f : 0.f,
+                m2 = (a && cnt > 2) ? 1.f : 0.f, m3 = (a && cnt > 3) ? 1.f : 0.f,
+                m4 = (a && cnt > 4) ? 1.f : 0.f;
+    auto f = [](double v, float m) { return m != 0.f ? static_cast<float>(v) : 0.f; };
+    const float sf = a ? 1.f : 0.f;
+    o4[0] = make_float4(f(so0, sf), f(so1, sf), f(so2, sf), f(so3, sf));
+    o4[1] = make_float4(f(so4, sf), f(r.tl, sf), f(r.tr, sf), f(t0.a, m0));
+    o4[2] = make_float4(f(t0.b, m0), f(t0.c, m0), f(t0.d, m0), f(t0.e, m0));
+    o4[3] = make_float4(f(t1.a, m1), f(t1.b, m1), f(t1.c, m1), f(t1.d, m1));
+    o4[4] = make_float4(f(t1.e, m1), f(t2.a, m2), f(t2.b, m2), f(t2.c, m2));
+    o4[5] = make_float4(f(t2.d, m2), f(t2.e, m2), f(t3.a, m3), f(t3.b, m3));
+    o4[6] = make_float4(f(t3.c, m3), f(t3.d, m3), f(t3.e, m3), f(t4.a, m4));
+    o4[7] = make_float4(f(t4.b, m4), f(t4.c, m4), f(t4.d, m4), f(t4.e, m4));
+    o4[8] = make_float4(m0, m1, m2, m3);
+    o4[9] = make_float4(m4, 0.f, 0.f, 0.f);
+    if (out.obs64 != nullptr) {
+      double* o = out.obs64 + idx * 32;
+      const double v[32] = {so0, so1, so2, so3, so4, r.tl, r.tr,
+                            t0.a, t0.b, t0.c, t0.d, t0.e, t1.a, t1.b, t1.c, t1.d, t1.e,
+                            t2.a, t2.b, t2.c, t2.d, t2.e, t3.a, t3.b, t3.c, t3.d, t3.e,
+                            t4.a, t4.b, t4.c, t4.d, t4.e};
+#pragma unroll
+      for (int k = 0; k < 32; ++k) {
+        const bool keep = a && (k < 7 || (k - 7) / 5 < cnt);
+        o[k] = keep ? v[k] : 0.0;
+      }
+    }
+    out.obj_cnt[idx] = static_cast<int8_t>(exists ? cnt : -1);
+    out.reward[idx] = reward;
+    out.done[idx] = done;
+    out.info[idx] = info;
+  }
+  __syncthreads();
+  if (env_on && i == 0 && ctl.do_dynamics) {
+    s.ep_ts[e] = ep_ts + 1;  // env.py:330
+    if (ctl.trainer_deactivate && out.env_done != nullptr) {
+      const bool end = (ep_ts >= p.episode_limit) || salive[le] == 0;  // trainer.py:172
+      out.env_done[e] = end ? 1 : 0;
+      if (end && out.stats != nullptr) {
+        double sr = 0, sc = 0, sg = 0, sk = 0, st = 0;
+        for (int j = 0; j < nrob; ++j) {
+          const size_t jd = static_cast<size_t>(e) * R + j;
+          const uint8_t fj = s.rflags[jd];
+          sr += s.rs[ASVRL_F_RET * NT + jd];
+          sc += 1;
+          sg += (fj & ASVRL_FLAG_REACH_GOAL) ? 1 : 0;
+          sk += (fj & ASVRL_FLAG_COLLISION) ? 1 : 0;
+          st += (fj & ASVRL_FLAG_DEACTIVATED) ? 0 : 1;
+        }
+        atomicAdd(out.stats + 0, sr);
+        atomicAdd(out.stats + 1, sc);
+        atomicAdd(out.stats + 2, sg);
+        atomicAdd(out.stats + 3, sk);
+        atomicAdd(out.stats + 4, st);
+        atomicAdd(out.stats + 5, 1.0);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ reset (env.py:72-164)
+__device__ inline bool far_enough(double ax, double ay, double bx, double by, double lim, bool strict) {
+  const double dx = ax - bx, dy = ay - by;
+  const double d = sqrt(dx * dx + dy * dy);
+  return strict ? !(d <= lim) : !(d < lim);
+}
+
+__global__ __launch_bounds__(kBlock) void env_reset_kernel(AsvParams p, AsvEnvState s, AsvResetCfg cfg,
+                                                           const uint8_t* __restrict__ mask,
+                                                           uint64_t seed, uint64_t counter,
+                                                           const uint64_t* __restrict__ counter_dev) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= s.n_envs) return;
+  if (mask != nullptr && mask[e] == 0) return;
+  const int R = s.max_robots, O = s.max_obs, Cmax = s.max_cores;
+  const size_t NT = static_cast<size_t>(s.n_envs) * R;
+  double* rs = s.rs;
+  const uint64_t ctr = counter + (counter_dev != nullptr ? *counter_dev : 0ull);
+  Stream g(seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull, static_cast<uint32_t>(e), 0xA5E7u,
+           static_cast<uint32_t>(ctr));
+  const int want_r = cfg.num_robots < R ? cfg.num_robots : R;
+  // robots: rejection sampling of start/goal pairs, <= 500 draws (env.py:106-120)
+  int nr = 0;
+  for (int it = 0; it < 500 && nr < want_r; ++it) {
+    const double sxv = 2.0 + (cfg.width - 4.0) * (1.0 - g.u01());
+    const double syv = 2.0 + (cfg.height - 4.0) * (1.0 - g.u01());
+    const double gxv = 2.0 + (cfg.width - 4.0) * (1.0 - g.u01());
+    const double gyv = 2.0 + (cfg.height - 4.0) * (1.0 - g.u01());
+    bool ok = far_enough(gxv, gyv, sxv, syv, cfg.min_start_goal_dis, false);  // env.py:361
+    for (int k = 0; k < nr && ok; ++k) {
+      const size_t kd = static_cast<size_t>(e) * R + k;
+      ok = far_enough(rs[ASVRL_F_X * NT + kd], rs[ASVRL_F_Y * NT + kd], sxv, syv, cfg.clear_r, true) &&
+           far_enough(rs[ASVRL_F_GX * NT + kd], rs[ASVRL_F_GY * NT + kd], gxv, gyv, cfg.clear_r, true);
+    }
+    if (!ok) continue;
+    const size_t id = static_cast<size_t>(e) * R + nr;
+    rs[ASVRL_F_X * NT + id] = sxv;  // reset_robot / reset_state (env.py:166-176, wamv.py:177-193)
+    rs[ASVRL_F_Y * NT + id] = syv;
+    rs[ASVRL_F_GX * NT + id] = gxv;
+    rs[ASVRL_F_GY * NT + id] = gyv;
+    rs[ASVRL_F_THETA * NT + id] = kTwoPi * (1.0 - g.u01());
+    for (int f = ASVRL_F_VR0; f <= ASVRL_F_RP; ++f) rs[f * NT + id] = 0.0;
+    rs[ASVRL_F_PHI * NT + id] = 0.0;
+    rs[ASVRL_F_RET * NT + id] = 0.0;
+    s.rflags[id] = 0;
+    ++nr;
+  }
+  for (int k = nr; k < R; ++k) s.rflags[static_cast<size_t>(e) * R + k] = ASVRL_FLAG_DEACTIVATED;
+  // vortex cores (env.py:123-136, check_core :378-418)
+  double* cores = s.cores + static_cast<size_t>(e) * Cmax * 4;
+  const int want_c = cfg.num_cores < Cmax ? cfg.num_cores : Cmax;
+  int nc = 0;
+  for (int it = 0; it < 500 && nc < want_c; ++it) {
+    const double cx = cfg.width * (1.0 - g.u01());
+    const double cy = cfg.height * (1.0 - g.u01());
+    const double cw = g.u01() <= 0.5 ? 1.0 : 0.0;
+    const double ve = cfg.v_lo + (cfg.v_hi - cfg.v_lo) * (1.0 - g.u01());
+    const double Gamma = 2 * kPi * p.core_r * ve;
+    bool ok = !(cx - p.core_r < 0.0 || cx + p.core_r > cfg.width) &&
+              !(cy - p.core_r < 0.0 || cy + p.core_r > cfg.width);  // (sic) env.py:383
+    for (int k = 0; k < nr && ok; ++k) {
+      const size_t kd = static_cast<size_t>(e) * R + k;
+      ok = far_enough(cx, cy, rs[ASVRL_F_X * NT + kd], rs[ASVRL_F_Y * NT + kd], p.core_r + cfg.clear_r, false) &&
+           far_enough(cx, cy, rs[ASVRL_F_GX * NT + kd], rs[ASVRL_F_GY * NT + kd], p.core_r + cfg.clear_r, false);
+    }
+    for (int k = 0; k < nc && ok; ++k) {
+      const double dx = cores[4 * k] - cx, dy = cores[4 * k + 1] - cy;
+      const double dis = sqrt(dx * dx + dy * dy);
+      if (cores[4 * k + 2] == cw) {
+        const double bi = cores[4 * k + 3] / (2 * kPi * cfg.v_rel_max);
+        const double bj = Gamma / (2 * kPi * cfg.v_rel_max);
+        if (dis < bi + bj) ok = false;
+      } else {
+        const double gl = fmax(cores[4 * k + 3], Gamma), gs = fmin(cores[4 * k + 3], Gamma);
+        const double v1 = gl / (2 * kPi * (dis - 2 * p.core_r));
+        const double v2 = gs / (2 * kPi * p.core_r);
+        if (v1 > cfg.p_rel * v2) ok = false;
+      }
+    }
+    if (!ok) continue;
+    cores[4 * nc] = cx;
+    cores[4 * nc + 1] = cy;
+    cores[4 * nc + 2] = cw;
+    cores[4 * nc + 3] = Gamma;
+    ++nc;
+  }
+  // static obstacles (env.py:151-162, check_obstacle :420-456)
+  double* obs = s.obstacles + static_cast<size_t>(e) * O * 3;
+  const int want_o = cfg.num_obs < O ? cfg.num_obs : O;
+  int no = 0;
+  for (int it = 0; it < 500 && no < want_o; ++it) {
+    const double ox = 5.0 + (cfg.width - 10.0) * (1.0 - g.u01());
+    const double oy = 5.0 + (cfg.height - 10.0) * (1.0 - g.u01());
+    const double orad = cfg.obs_r_lo + (cfg.obs_r_hi - cfg.obs_r_lo) * (1.0 - g.u01());
+    bool ok = !(ox - orad < 0.0 || ox + orad > cfg.width) && !(oy - orad < 0.0 || oy + orad > cfg.height);
+    for (int k = 0; k < nr && ok; ++k) {
+      const size_t kd = static_cast<size_t>(e) * R + k;
+      ok = far_enough(ox, oy, rs[ASVRL_F_X * NT + kd], rs[ASVRL_F_Y * NT + kd], orad + cfg.clear_r, false) &&
+           far_enough(ox, oy, rs[ASVRL_F_GX * NT + kd], rs[ASVRL_F_GY * NT + kd], orad + cfg.clear_r, false);
+    }
+    for (int k = 0; k < nc && ok; ++k) ok = far_enough(cores[4 * k], cores[4 * k + 1], ox, oy, p.core_r + orad, true);
+    for (int k = 0; k < no && ok; ++k) ok = far_enough(obs[3 * k], obs[3 * k + 1], ox, oy, obs[3 * k + 2] + orad, true);
+    if (!ok) continue;
+    obs[3 * no] = ox;
+    obs[3 * no + 1] = oy;
+    obs[3 * no + 2] = orad;
+    ++no;
+  }
+  s.n_robots[e] = nr;
+  s.n_cores[e] = nc;
+  s.n_obs[e] = no;
+  s.ep_ts[e] = 0;
+}
+
+__global__ __launch_bounds__(kBlock) void current_kernel(const double* __restrict__ cores, int nc, double core_r,
+                                                        const double* __restrict__ xy, int n, double* __restrict__ out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  double cx, cy;
+  current_at(cores, nc, core_r, xy[2 * k], xy[2 * k + 1], cx, cy);
+  out[3 * k] = cx;
+  out[3 * k + 1] = cy;
+  out[3 * k + 2] = 0.0;
+}
+
+}  // namespace
+
+size_t env_step_smem(int R, int O) {
+  const int epb = kBlock / R;
+  return sizeof(double) * (4 * kBlock + static_cast<size_t>(epb) * O * 3) + sizeof(int) * epb + kBlock;
+}
+
+}  // namespace asvrl
+
+using namespace asvrl;
+
+extern "C" int asvrl_env_step(const AsvParams* params, const AsvEnvState* state, const double* actions,
+                              const double* noise, const AsvStepCtl* ctl, const AsvStepOut* out,
+                              void* stream) {
+  ASVRL_REQUIRE(params && state && ctl && out, "asvrl_env_step: null argument");
+  ASVRL_REQUIRE(state->max_robots >= 1 && state->max_robots <= kBlock, "asvrl_env_step: max_robots must be in [1, 256]");
+  ASVRL_REQUIRE(state->max_obs >= 0 && state->max_cores >= 0 && state->max_cores <= kMaxCores,
+                "asvrl_env_step: bad max_obs/max_cores");
+  ASVRL_REQUIRE(params->max_obj_num >= 0 && params->max_obj_num <= ASVRL_MAX_OBJ, "asvrl_env_step: max_obj_num > 5");
+  ASVRL_REQUIRE(params->N >= 1, "asvrl_env_step: N < 1");
+  ASVRL_REQUIRE(out->obs && out->obj_cnt && out->reward && out->done && out->info, "asvrl_env_step: null output");
+  ASVRL_REQUIRE(ctl->noise_mode != 0 || noise != nullptr, "asvrl_env_step: noise_mode 0 needs injected noise");
+  ASVRL_REQUIRE(!ctl->do_dynamics || actions != nullptr, "asvrl_env_step: actions required");
+  ASVRL_REQUIRE(state->rs && state->rflags && state->n_robots && state->n_obs && state->n_cores && state->ep_ts,
+                "asvrl_env_step: null state array");
+  if (state->n_envs == 0) return 0;
+  const int epb = kBlock / state->max_robots;
+  const int grid = (state->n_envs + epb - 1) / epb;
+  const size_t smem = env_step_smem(state->max_robots, state->max_obs);
+  ASVRL_REQUIRE(smem <= 160 * 1024, "asvrl_env_step: max_obs too large for LDS");
+  hipLaunchKernelGGL(env_step_kernel, dim3(grid), dim3(kBlock), smem, as_stream(stream), *params, *state,
+                     actions, noise, *ctl, *out);
+  return check_launch("asvrl_env_step");
+}
+
+extern "C" int asvrl_env_reset(const AsvParams* params, const AsvEnvState* state, const AsvResetCfg* cfg,
+                               const uint8_t* env_mask, uint64_t seed, uint64_t counter,
+                               const uint64_t* counter_dev, void* stream) {
+  ASVRL_REQUIRE(params && state && cfg, "asvrl_env_reset: null argument");
+  ASVRL_REQUIRE(state->max_cores <= kMaxCores, "asvrl_env_reset: max_cores > 16");
+  ASVRL_REQUIRE(cfg->width > 4.0 && cfg->height > 4.0, "asvrl_env_reset: map too small");
+  if (state->n_envs == 0) return 0;
+  const int grid = (state->n_envs + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(env_reset_kernel, dim3(grid), dim3(kBlock), 0, as_stream(stream), *params, *state, *cfg,
+                     env_mask, seed, counter, counter_dev);
+  return check_launch("asvrl_env_reset");
+}
+
+extern "C" int asvrl_current_field(const double* cores, int32_t n_cores, double core_r, const double* xy,
+                                   int32_t n, double* out, void* stream) {
+  ASVRL_REQUIRE(xy && out && (n_cores == 0 || cores), "asvrl_current_field: null argument");
+  ASVRL_REQUIRE(n_cores >= 0 && n_cores <= kMaxCores, "asvrl_current_field: n_cores > 16");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(current_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, as_stream(stream), cores,
+                     n_cores, core_r, xy, n, out);
+  return check_launch("asvrl_current_field");
+}

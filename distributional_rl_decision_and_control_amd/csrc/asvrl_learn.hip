@@ -1,0 +1,313 @@
+// asvrl_learn.hip -- learner-side kernels of the rfarl hot path on gfx950:
+//   * the fused quantile-Huber loss + gradient (agent.py:406-412, 701-707),
+//   * the C51 categorical projection (agent.py:616-631), bit-exact to the CPU reference,
+//   * the replay ring (ReplayBuffer.add/sample, replay_buffer.py:22-69) resident in HBM,
+// plus the ABI's error plumbing.
+#include "asvrl_common.h"
+
+namespace asvrl {
+
+thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int check_launch(const char* what) {
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    set_error(std::string(what) + ": " + hipGetErrorString(err));
+    return 2;
+  }
+  return 0;
+}
+
+namespace {
+
+__device__ inline float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+// ------------------------------------------------------------------ quantile Huber
+// One wave per batch row: lane i owns expected quantile qe[b,i] (i = lane, lane+64, ...)
+// and sweeps the Np target quantiles, which are wave-uniform loads.
+constexpr int kQhWaves = 4;
+
+__global__ __launch_bounds__(kQhWaves * kWave) void quantile_huber_kernel(
+    const float* __restrict__ qt, const float* __restrict__ qe, const float* __restrict__ tau, int B,
+    int N, int Np, float kappa, float gscale, float* __restrict__ row_loss, float* __restrict__ dqe) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int b = blockIdx.x * kQhWaves + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const float* qtb = qt + static_cast<size_t>(b) * Np;
+  float part = 0.f;
+  for (int i0 = 0; i0 < N; i0 += kWave) {
+    const int i = i0 + lane;
+    if (i < N) {
+      const float e = qe[static_cast<size_t>(b) * N + i];
+      const float t = tau[static_cast<size_t>(b) * N + i];
+      float acc_l = 0.f, acc_g = 0.f;
+      for (int j = 0; j < Np; ++j) {
+        const float d = qtb[j] - e;  // td_error = Q_targets - Q_expected (agent.py:406)
+        const float ad = fabsf(d);
+        const bool quad = ad <= kappa;
+        const float h = quad ? 0.5f * (d * d) : kappa * (ad - 0.5f * kappa);
+        const float w = fabsf(t - (d < 0.f ? 1.f : 0.f));  // |tau - 1{td < 0}| (agent.py:409)
+        acc_l += w * h / kappa;
+        acc_g += w * (quad ? d : (d > 0.f ? kappa : -kappa)) / kappa;
+      }
+      part += acc_l;
+      dqe[static_cast<size_t>(b) * N + i] = -acc_g * gscale;
+    }
+  }
+  part = wave_sum(part);
+  if (lane == 0) row_loss[b] = part / static_cast<float>(Np);
+}
+
+__global__ __launch_bounds__(1024) void mean_kernel(const float* __restrict__ x, int n, float* __restrict__ out) {
+  __shared__ float sh[1024 / kWave];
+  float v = 0.f;
+  for (int k = threadIdx.x; k < n; k += blockDim.x) v += x[k];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x < kWave) {
+    float w = threadIdx.x < (blockDim.x >> 6) ? sh[threadIdx.x] : 0.f;
+    w = wave_sum(w);
+    if (threadIdx.x == 0) out[0] = w / static_cast<float>(n);
+  }
+}
+
+// ------------------------------------------------------------------ C51 projection
+// One wave per row, lane j = atom j. The reference accumulates with two sequential CPU
+// index_add_ passes (lower masses, then upper masses, each in atom order); lane k rebuilds
+// m[k] in exactly that order from shuffles, so the f32 result is bit-identical.
+__global__ __launch_bounds__(4 * kWave) void c51_kernel(const float* __restrict__ pns_a,
+                                                        const float* __restrict__ ret,
+                                                        const float* __restrict__ nonterm,
+                                                        const float* __restrict__ support, int B, int atoms,
+                                                        float vmin, float vmax, float dz, float gamma_n,
+                                                        float* __restrict__ m) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const bool on = lane < atoms;
+  float lower = 0.f, upper = 0.f;
+  int l = -1, u = -1;
+  if (on) {
+    const float ntg = nonterm[b] * gamma_n;
+    float tz = ret[b] + ntg * support[lane];      // Tz = R + nonterminal * gamma^n * z
+    tz = fminf(fmaxf(tz, vmin), vmax);            // clamp(Vmin, Vmax)
+    const float bb = (tz - vmin) / dz;            // b = (Tz - Vmin) / delta_z
+    l = static_cast<int>(floorf(bb));
+    u = static_cast<int>(ceilf(bb));
+    if (u > 0 && l == u) l -= 1;                  // agent.py:623
+    if (l < atoms - 1 && l == u) u += 1;          // agent.py:624
+    const float p = pns_a[static_cast<size_t>(b) * atoms + lane];
+    lower = p * (static_cast<float>(u) - bb);
+    upper = p * (bb - static_cast<float>(l));
+  }
+  float acc = 0.f;
+  for (int j = 0; j < atoms; ++j) {
+    const int lj = __shfl(l, j, kWave);
+    const float vj = __shfl(lower, j, kWave);
+    if (lj == lane) acc += vj;
+  }
+  for (int j = 0; j < atoms; ++j) {
+    const int uj = __shfl(u, j, kWave);
+    const float vj = __shfl(upper, j, kWave);
+    if (uj == lane) acc += vj;
+  }
+  if (on) m[static_cast<size_t>(b) * atoms + lane] = acc;
+}
+
+// ------------------------------------------------------------------ replay ring
+constexpr int kPushBlock = 256;
+
+__global__ __launch_bounds__(kPushBlock) void replay_count_kernel(const int8_t* __restrict__ cnt, int n,
+                                                                  int* __restrict__ work) {
+  __shared__ int sh[kPushBlock / kWave];
+  const int k = blockIdx.x * kPushBlock + threadIdx.x;
+  const bool v = k < n && cnt[k] >= 0;
+  const unsigned long long bal = __ballot(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = __popcll(bal);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int w = 0; w < kPushBlock / kWave; ++w) t += sh[w];
+    work[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(kPushBlock) void replay_write_kernel(
+    const float* __restrict__ obs_prev, const float* __restrict__ obs_next, const int8_t* __restrict__ cnt,
+    const double* __restrict__ actions, int adim, const double* __restrict__ reward,
+    const uint8_t* __restrict__ done, int n, float* __restrict__ ring, int64_t cap,
+    const int64_t* __restrict__ ring_state, int* __restrict__ work, int nblocks) {
+  __shared__ int sh[kPushBlock / kWave];
+  __shared__ int s_off, s_tot;
+  // block offset = sum of earlier blocks' counts (deterministic slot order)
+  int before = 0, total = 0;
+  for (int k = threadIdx.x; k < nblocks; k += kPushBlock) {
+    const int c = work[k];
+    total += c;
+    if (k < static_cast<int>(blockIdx.x)) before += c;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    before += __shfl_xor(before, off, kWave);
+    total += __shfl_xor(total, off, kWave);
+  }
+  if (threadIdx.x == 0) { s_off = 0; s_tot = 0; }
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&s_off, before);
+    atomicAdd(&s_tot, total);
+  }
+  const int k = blockIdx.x * kPushBlock + threadIdx.x;
+  const bool v = k < n && cnt[k] >= 0;
+  const unsigned long long bal = __ballot(v);
+  const int lane = threadIdx.x & 63;
+  const int rank_in_wave = __popcll(bal & ((1ull << lane) - 1ull));
+  if (lane == 0) sh[threadIdx.x >> 6] = __popcll(bal);
+  __syncthreads();
+  const int64_t head_in = ring_state[0];
+  if (blockIdx.x == 0 && threadIdx.x == 0) work[nblocks] = s_tot;  // for the finalize kernel
+  if (!v) return;
+  int wave_off = 0;
+  for (int w = 0; w < (threadIdx.x >> 6); ++w) wave_off += sh[w];
+  const int64_t slot = (head_in + s_off + wave_off + rank_in_wave) % cap;
+  float4* dst = reinterpret_cast<float4*>(ring + slot * ASVRL_TR_DIM);
+  const float4* a4 = reinterpret_cast<const float4*>(obs_prev + static_cast<size_t>(k) * ASVRL_OBS_DIM);
+  const float4* b4 = reinterpret_cast<const float4*>(obs_next + static_cast<size_t>(k) * ASVRL_OBS_DIM);
+#pragma unroll
+  for (int q = 0; q < ASVRL_OBS_DIM / 4; ++q) dst[q] = a4[q];
+#pragma unroll
+  for (int q = 0; q < ASVRL_OBS_DIM / 4; ++q) dst[ASVRL_OBS_DIM / 4 + q] = b4[q];
+  const float a0 = static_cast<float>(actions[static_cast<size_t>(k) * adim]);
+  const float a1 = adim > 1 ? static_cast<float>(actions[static_cast<size_t>(k) * adim + 1]) : 0.f;
+  dst[2 * ASVRL_OBS_DIM / 4] = make_float4(a0, a1, static_cast<float>(reward[k]), done[k] ? 1.f : 0.f);
+  dst[2 * ASVRL_OBS_DIM / 4 + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+__global__ void replay_finalize_kernel(int64_t* ring_state, const int* __restrict__ work, int nblocks, int64_t cap) {
+  const int64_t tot = work[nblocks];
+  ring_state[0] = (ring_state[0] + tot) % cap;
+  const int64_t ns = ring_state[1] + tot;
+  ring_state[1] = ns < cap ? ns : cap;
+}
+
+// one wave per sampled row, 22 lanes x float4
+__global__ __launch_bounds__(4 * kWave) void replay_sample_kernel(const float* __restrict__ ring, int64_t cap,
+                                                                  const int64_t* __restrict__ ring_state,
+                                                                  const int64_t* __restrict__ indices, int B,
+                                                                  uint64_t seed, uint64_t counter,
+                                                                  const uint64_t* __restrict__ counter_dev,
+                                                                  float* __restrict__ out, int64_t* out_slots) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int64_t head = ring_state[0];
+  const int64_t size = ring_state[1];
+  int64_t k;
+  if (indices != nullptr) {
+    k = indices[b];
+  } else {
+    const uint64_t ctr = counter + (counter_dev != nullptr ? *counter_dev : 0ull);
+    const U4 r = philox4x32_10(U4{static_cast<uint32_t>(b), 0x5A3Bu, static_cast<uint32_t>(ctr >> 32),
+                                  static_cast<uint32_t>(ctr)},
+                               static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
+    const uint64_t bits = (static_cast<uint64_t>(r.x) << 32) | r.y;
+    k = size > 0 ? static_cast<int64_t>(bits % static_cast<uint64_t>(size)) : 0;
+  }
+  const int64_t slot = ((head - size + k) % cap + cap) % cap;  // deque index 0 = oldest
+  if (lane == 0 && out_slots != nullptr) out_slots[b] = slot;
+  if (lane < ASVRL_TR_DIM / 4) {
+    const float4* src = reinterpret_cast<const float4*>(ring + slot * ASVRL_TR_DIM);
+    reinterpret_cast<float4*>(out + static_cast<size_t>(b) * ASVRL_TR_DIM)[lane] = src[lane];
+  }
+}
+
+__global__ __launch_bounds__(4 * kWave) void replay_write_rows_kernel(const float* __restrict__ rows,
+                                                                      const int64_t* __restrict__ slots, int n,
+                                                                      float* __restrict__ ring) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= n || lane >= ASVRL_TR_DIM / 4) return;
+  reinterpret_cast<float4*>(ring + slots[b] * ASVRL_TR_DIM)[lane] =
+      reinterpret_cast<const float4*>(rows + static_cast<size_t>(b) * ASVRL_TR_DIM)[lane];
+}
+
+}  // namespace
+}  // namespace asvrl
+
+using namespace asvrl;
+
+extern "C" const char* asvrl_last_error(void) { return g_last_error.c_str(); }
+extern "C" int asvrl_abi_version(void) { return ASVRL_ABI_VERSION; }
+
+extern "C" int asvrl_quantile_huber(const float* qt, const float* qe, const float* tau, int32_t B, int32_t N,
+                                    int32_t Np, float kappa, float grad_scale, float* row_loss, float* loss,
+                                    float* dqe, void* stream) {
+  ASVRL_REQUIRE(qt && qe && tau && row_loss && dqe, "asvrl_quantile_huber: null argument");
+  ASVRL_REQUIRE(B >= 0 && N >= 1 && Np >= 1 && kappa > 0.f, "asvrl_quantile_huber: bad shape/kappa");
+  if (B == 0) return 0;
+  const float gscale = grad_scale / (static_cast<float>(B) * static_cast<float>(Np));
+  hipLaunchKernelGGL(quantile_huber_kernel, dim3((B + kQhWaves - 1) / kQhWaves), dim3(kQhWaves * kWave), 0,
+                     as_stream(stream), qt, qe, tau, B, N, Np, kappa, gscale, row_loss, dqe);
+  if (int rc = check_launch("asvrl_quantile_huber")) return rc;
+  if (loss != nullptr) {
+    hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(1024), 0, as_stream(stream), row_loss, B, loss);
+    return check_launch("asvrl_quantile_huber(mean)");
+  }
+  return 0;
+}
+
+extern "C" int asvrl_c51_project(const float* pns_a, const float* returns, const float* nonterminal,
+                                 const float* support, int32_t B, int32_t atoms, float vmin, float vmax,
+                                 float delta_z, float gamma_n, float* m, void* stream) {
+  ASVRL_REQUIRE(pns_a && returns && nonterminal && support && m, "asvrl_c51_project: null argument");
+  ASVRL_REQUIRE(atoms >= 2 && atoms <= kWave, "asvrl_c51_project: atoms must be in [2, 64]");
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(c51_kernel, dim3((B + 3) / 4), dim3(4 * kWave), 0, as_stream(stream), pns_a, returns,
+                     nonterminal, support, B, atoms, vmin, vmax, delta_z, gamma_n, m);
+  return check_launch("asvrl_c51_project");
+}
+
+extern "C" int asvrl_replay_push(const float* obs_prev, const float* obs_next, const int8_t* obj_cnt_next,
+                                 const double* actions, int32_t action_dim, const double* reward,
+                                 const uint8_t* done, int32_t n, float* ring, int64_t capacity,
+                                 int64_t* ring_state, int32_t* work, void* stream) {
+  ASVRL_REQUIRE(obs_prev && obs_next && obj_cnt_next && actions && reward && done && ring && ring_state && work,
+                "asvrl_replay_push: null argument");
+  ASVRL_REQUIRE(capacity >= n && capacity > 0, "asvrl_replay_push: capacity smaller than one push");
+  ASVRL_REQUIRE(action_dim == 1 || action_dim == 2, "asvrl_replay_push: action_dim must be 1 or 2");
+  if (n <= 0) return 0;
+  const int nb = (n + kPushBlock - 1) / kPushBlock;
+  hipLaunchKernelGGL(replay_count_kernel, dim3(nb), dim3(kPushBlock), 0, as_stream(stream), obj_cnt_next, n, work);
+  if (int rc = check_launch("asvrl_replay_push(count)")) return rc;
+  hipLaunchKernelGGL(replay_write_kernel, dim3(nb), dim3(kPushBlock), 0, as_stream(stream), obs_prev, obs_next,
+                     obj_cnt_next, actions, action_dim, reward, done, n, ring, capacity, ring_state, work, nb);
+  if (int rc = check_launch("asvrl_replay_push(write)")) return rc;
+  hipLaunchKernelGGL(replay_finalize_kernel, dim3(1), dim3(1), 0, as_stream(stream), ring_state, work, nb, capacity);
+  return check_launch("asvrl_replay_push(finalize)");
+}
+
+extern "C" int asvrl_replay_sample(const float* ring, int64_t capacity, const int64_t* ring_state,
+                                   const int64_t* indices, int32_t B, uint64_t seed, uint64_t counter,
+                                   const uint64_t* counter_dev, float* out, int64_t* out_slots, void* stream) {
+  ASVRL_REQUIRE(ring && ring_state && out, "asvrl_replay_sample: null argument");
+  ASVRL_REQUIRE(capacity > 0, "asvrl_replay_sample: bad capacity");
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(replay_sample_kernel, dim3((B + 3) / 4), dim3(4 * kWave), 0, as_stream(stream), ring,
+                     capacity, ring_state, indices, B, seed, counter, counter_dev, out, out_slots);
+  return check_launch("asvrl_replay_sample");
+}
+
+extern "C" int asvrl_replay_write_rows(const float* rows, const int64_t* slots, int32_t n, float* ring,
+                                       void* stream) {
+  ASVRL_REQUIRE(rows && slots && ring, "asvrl_replay_write_rows: null argument");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(replay_write_rows_kernel, dim3((n + 3) / 4), dim3(4 * kWave), 0, as_stream(stream), rows,
+                     slots, n, ring);
+  return check_launch("asvrl_replay_write_rows");
+}

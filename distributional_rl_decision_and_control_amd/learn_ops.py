@@ -1,0 +1,131 @@
+"""Learner operators on the gfx950 kernels: quantile-Huber loss, C51 projection, replay ring.
+
+All three run only through libasvrl.so (no torch fallback for the ops themselves).
+"""
+import ctypes as C
+
+import torch
+
+from . import _abi
+from ._abi import OBS_DIM, TR_DIM
+
+
+# ---------------------------------------------------------------------- quantile Huber
+class _QuantileHuber(torch.autograd.Function):
+    """Forward = agent.py:406-412 quantile-Huber loss (mean over batch, mean over target
+    quantiles, sum over expected quantiles); backward = d/d qe from the same kernel."""
+
+    @staticmethod
+    def forward(ctx, qt, qe, tau, kappa):
+        qt = qt.detach().float().contiguous()
+        qe_c = qe.detach().float().contiguous()
+        tau = tau.detach().float().contiguous()
+        B, N = qe_c.shape
+        Np = qt.shape[1]
+        assert qt.shape[0] == B and tau.shape == (B, N)
+        row = torch.empty(B, dtype=torch.float32, device=qe.device)
+        loss = torch.empty((), dtype=torch.float32, device=qe.device)
+        dqe = torch.empty_like(qe_c)
+        rc = _abi.lib().asvrl_quantile_huber(_abi.ptr(qt), _abi.ptr(qe_c), _abi.ptr(tau), B, N, Np, float(kappa), 1.0,
+                                             _abi.ptr(row), _abi.ptr(loss), _abi.ptr(dqe), _abi.stream_ptr())
+        _abi.check(rc, "asvrl_quantile_huber")
+        ctx.save_for_backward(dqe)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (dqe,) = ctx.saved_tensors
+        return None, dqe * g, None, None
+
+
+def quantile_huber_loss(q_targets, q_expected, taus, kappa=1.0):
+    """q_targets (B, N') detached targets, q_expected (B, N), taus (B, N) or (B, N, 1)."""
+    if taus.dim() == 3:
+        taus = taus.squeeze(-1)
+    return _QuantileHuber.apply(q_targets, q_expected, taus, kappa)
+
+
+# ---------------------------------------------------------------------- C51
+def c51_project(pns_a, returns, nonterminal, support, vmin=-1.0, vmax=1.0, gamma_n=0.99 ** 3, out=None):
+    """Target distribution m of agent.py:616-631 (bit-identical to the reference's CPU f32).
+
+    gamma_n and delta_z are rounded to f32 as torch does for python scalars against f32
+    tensors; nonterminal may be (B,) or (B, 1)."""
+    pns_a = pns_a.float().contiguous()
+    B, atoms = pns_a.shape
+    R = returns.float().reshape(B).contiguous()
+    nt = nonterminal.float().reshape(B).contiguous()
+    sup = support.float().contiguous()
+    m = out if out is not None else torch.empty_like(pns_a)
+    dz = float(torch.tensor((vmax - vmin) / (atoms - 1), dtype=torch.float32))
+    g32 = float(torch.tensor(gamma_n, dtype=torch.float32))
+    rc = _abi.lib().asvrl_c51_project(_abi.ptr(pns_a), _abi.ptr(R), _abi.ptr(nt), _abi.ptr(sup), B, atoms,
+                                      float(vmin), float(vmax), dz, g32, _abi.ptr(m), _abi.stream_ptr())
+    _abi.check(rc, "asvrl_c51_project")
+    return m
+
+
+# ---------------------------------------------------------------------- replay ring
+class DeviceReplay:
+    """HBM-resident ring of transitions (ReplayBuffer, replay_buffer.py:6-69).
+
+    Row layout (f32, ASVRL_TR_DIM = 88): obs 40 | next obs 40 | action 2 | reward | done | pad.
+    obs rows are the packed state_batch layout: self 7 | objects 5x5 | mask 5 | pad 3.
+    head/size live in device memory so push/sample can be captured in a HIP graph."""
+
+    def __init__(self, capacity, device="cuda"):
+        _abi.lib()
+        self.capacity = int(capacity)
+        self.device = torch.device(device)
+        self.ring = torch.zeros((self.capacity, TR_DIM), dtype=torch.float32, device=self.device)
+        self.state = torch.zeros(2, dtype=torch.int64, device=self.device)  # head, size
+        self._work = None
+        self._n_host = 0  # host mirror for the compat path (exact when fed by add())
+
+    def push(self, obs_prev, obs_next, obj_cnt_next, actions, reward, done, stream=None):
+        n = obs_prev.shape[0]
+        if self._work is None or self._work.numel() < (n + 255) // 256 + 1:
+            self._work = torch.zeros((n + 255) // 256 + 1, dtype=torch.int32, device=self.device)
+        adim = actions.shape[1] if actions.dim() == 2 else 1
+        rc = _abi.lib().asvrl_replay_push(_abi.ptr(obs_prev), _abi.ptr(obs_next), _abi.ptr(obj_cnt_next),
+                                          _abi.ptr(actions), adim, _abi.ptr(reward), _abi.ptr(done), n,
+                                          _abi.ptr(self.ring), self.capacity, _abi.ptr(self.state),
+                                          _abi.ptr(self._work), _abi.stream_ptr(stream))
+        _abi.check(rc, "asvrl_replay_push")
+
+    def write_rows(self, rows, slots, stream=None):
+        rc = _abi.lib().asvrl_replay_write_rows(_abi.ptr(rows), _abi.ptr(slots), rows.shape[0], _abi.ptr(self.ring),
+                                                _abi.stream_ptr(stream))
+        _abi.check(rc, "asvrl_replay_write_rows")
+
+    def size(self):
+        return int(self.state[1].item())
+
+    def gather(self, indices, out=None, stream=None):
+        """Rows at deque positions `indices` (0 = oldest), device int64."""
+        B = indices.shape[0]
+        out = out if out is not None else torch.empty((B, TR_DIM), dtype=torch.float32, device=self.device)
+        rc = _abi.lib().asvrl_replay_sample(_abi.ptr(self.ring), self.capacity, _abi.ptr(self.state),
+                                            _abi.ptr(indices), B, 0, 0, None, _abi.ptr(out), None,
+                                            _abi.stream_ptr(stream))
+        _abi.check(rc, "asvrl_replay_sample")
+        return out
+
+    def sample(self, B, seed=0, counter=0, counter_dev=None, out=None, stream=None):
+        """B rows drawn uniformly with replacement on the device (Philox)."""
+        out = out if out is not None else torch.empty((B, TR_DIM), dtype=torch.float32, device=self.device)
+        rc = _abi.lib().asvrl_replay_sample(_abi.ptr(self.ring), self.capacity, _abi.ptr(self.state), None, B,
+                                            int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter) & 0xFFFFFFFFFFFFFFFF,
+                                            _abi.ptr(counter_dev), _abi.ptr(out), None, _abi.stream_ptr(stream))
+        _abi.check(rc, "asvrl_replay_sample")
+        return out
+
+
+def split_rows(rows):
+    """(B, 88) replay rows -> (states, actions, rewards, next_states, dones) in the shapes
+    Agent.train_* builds (agent.py:387-392): states = (self (B,7), objs (B,5,5), mask (B,5))."""
+    B = rows.shape[0]
+    s = (rows[:, 0:7], rows[:, 7:32].reshape(B, 5, 5), rows[:, 32:37])
+    ns = (rows[:, OBS_DIM:OBS_DIM + 7], rows[:, OBS_DIM + 7:OBS_DIM + 32].reshape(B, 5, 5),
+          rows[:, OBS_DIM + 32:OBS_DIM + 37])
+    return s, rows[:, 80:82], rows[:, 82:83], ns, rows[:, 83:84]

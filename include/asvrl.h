@@ -1,0 +1,217 @@
+/* asvrl.h -- C ABI of libasvrl.so, the MI355X (gfx950) kernels behind the rfarl training
+ * hot path: the vectorised ASV marine-env step and the distributional Bellman update.
+ *
+ * The reference (pszenher/Distributional_RL_Decision_and_Control, rfarl/) is pure Python
+ * and has no FFI; each entry point below replaces the Python function cited next to it
+ * (paths relative to /root/reference/rfarl/rfarl/). The Python surfaces that call these
+ * (MarineNavEnv3, Agent, Trainer) live in distributional_rl_decision_and_control_amd/ and
+ * bind this header through ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *  - Every pointer argument is a DEVICE pointer unless its comment says "host".
+ *    The caller owns all memory (allocated as torch tensors); the library keeps no state.
+ *  - `stream` is a hipStream_t passed as void* (NULL = the default stream). All work is
+ *    stream-ordered; no entry point synchronises the device.
+ *  - Return value: 0 on success, nonzero on a bad argument or launch failure, with a
+ *    thread-local message from asvrl_last_error(). No C++ exception crosses the ABI.
+ */
+#ifndef ASVRL_H
+#define ASVRL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ASVRL_ABI_VERSION 1
+
+#define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
+#define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
+#define ASVRL_MAX_OBJ 5    /* wamv.py:14 max_obj_num */
+#define ASVRL_OBS_DIM 40   /* packed f32 obs row: self 7 | objects 5x5 | mask 5 | pad 3
+                              (= replay_buffer.py:51-69 state_batch, padded to 16 B) */
+#define ASVRL_TR_DIM 88    /* replay row: obs 40 | next obs 40 | action 2 | reward | done | pad 4 */
+
+/* Robot state fields, field-major SoA: rs[f * (n_envs * max_robots) + e * max_robots + i] */
+enum AsvRobotField {
+  ASVRL_F_X = 0, ASVRL_F_Y, ASVRL_F_THETA,           /* wamv.py:92-94 */
+  ASVRL_F_VR0, ASVRL_F_VR1, ASVRL_F_VR2,               /* velocity_r (wamv.py:95) */
+  ASVRL_F_V0, ASVRL_F_V1, ASVRL_F_V2,                  /* velocity, one substep stale (:96) */
+  ASVRL_F_TL, ASVRL_F_TR, ASVRL_F_LP, ASVRL_F_RP,      /* thrusts, thruster angles (:98-101) */
+  ASVRL_F_GX, ASVRL_F_GY,                              /* goal (:129) */
+  ASVRL_F_PHI,                                         /* COLREGs turn angle (:396) */
+  ASVRL_F_RET,                                         /* discounted episode return (trainer.py:161) */
+  ASVRL_NUM_FIELDS
+};
+
+/* Robot flag bits (u8 per robot) */
+#define ASVRL_FLAG_DEACTIVATED 1u  /* wamv.py:132, written by trainer.py:168-170 */
+#define ASVRL_FLAG_COLLISION 2u    /* wamv.py:130 */
+#define ASVRL_FLAG_REACH_GOAL 4u   /* wamv.py:131 */
+#define ASVRL_FLAG_COLREGS 8u      /* wamv.py:517-521 apply_COLREGs */
+
+/* info codes of env.step (env.py:291-328) */
+#define ASVRL_INFO_NORMAL 0
+#define ASVRL_INFO_TOO_LONG 1
+#define ASVRL_INFO_COLLISION 2
+#define ASVRL_INFO_REACH_GOAL 3
+#define ASVRL_INFO_DEACT_COLLISION 4
+#define ASVRL_INFO_DEACT_GOAL 5
+#define ASVRL_INFO_ABSENT 255      /* slot beyond the env's robot count */
+
+/* Vehicle, perception and reward parameters (wamv.py:45-125, env.py:33-54). Passed by
+ * value to the kernels; one set per env batch. */
+typedef struct AsvParams {
+  double dt;                 /* wamv.py:46 */
+  int32_t N;                 /* wamv.py:47 substeps per action */
+  int32_t episode_limit;     /* env.py:312 */
+  double length, width;      /* wamv.py:51-52 */
+  double r;                  /* collision radius = detect_r (wamv.py:53-54) */
+  double goal_dis;           /* wamv.py:79 */
+  double min_thrust, max_thrust; /* wamv.py:84-85 */
+  double m, Izz;             /* wamv.py:103-104 */
+  double xDotU, yDotV, yDotR, nDotR, nDotV, xU, xUU, yV, yVV, yR, yRV, yVR, yRR, nR, nRR, nV,
+      nVV, nRV, nVR;         /* wamv.py:107-125 */
+  double P[9];               /* inv(A^T A) A^T, A = M_RB + M_A (wamv.py:267-271), row-major,
+                                computed on the host with the reference's numpy expression */
+  double left_thrust_change[5], right_thrust_change[5]; /* wamv.py:86-88 discrete grid */
+  double range, angle;       /* wamv.py:12-13 */
+  double pos_std, vel_std, r_kappa, r_mean_ratio; /* wamv.py:22-25 */
+  int32_t max_obj_num;       /* wamv.py:14 (<= ASVRL_MAX_OBJ) */
+  int32_t _pad0;
+  double timestep_penalty, COLREGs_penalty, collision_penalty, goal_reward; /* env.py:47-50 */
+  double core_r;             /* env.py:35 vortex core radius */
+} AsvParams;
+
+/* A batch of E envs, resident in HBM. All arrays are caller-owned device memory. */
+typedef struct AsvEnvState {
+  int32_t n_envs, max_robots, max_obs, max_cores;
+  double* rs;        /* [ASVRL_NUM_FIELDS][n_envs * max_robots] robot state (field-major SoA) */
+  uint8_t* rflags;   /* [n_envs * max_robots] ASVRL_FLAG_* */
+  int32_t* n_robots; /* [n_envs] robots placed by reset (<= max_robots; env.py:106-120 may place fewer) */
+  int32_t* n_obs;    /* [n_envs] */
+  int32_t* n_cores;  /* [n_envs] */
+  int32_t* ep_ts;    /* [n_envs] episode_timesteps (env.py:64) */
+  double* obstacles; /* [n_envs][max_obs][3] x, y, r (env.py:16-22) */
+  double* cores;     /* [n_envs][max_cores][4] x, y, clockwise, Gamma (env.py:7-14) */
+} AsvEnvState;
+
+/* Per-call control of asvrl_env_step. */
+typedef struct AsvStepCtl {
+  int32_t is_continuous;      /* env.step is_continuous_action (env.py:240) */
+  int32_t do_dynamics;        /* 0: observation only (reset's get_observations, env.py:164) */
+  int32_t trainer_deactivate; /* 1: apply trainer.py:157-172 in-kernel (deactivate on flags,
+                                 episode-end test, discounted return) */
+  int32_t noise_mode;         /* 0: injected draws (noise != NULL, parity with the reference's
+                                 per-robot RandomState); 1: Philox-4x32-10 in registers */
+  uint64_t seed, counter;     /* Philox key / per-step counter (noise_mode 1) */
+  const uint64_t* counter_dev; /* optional device counter added to `counter` (keeps a captured
+                                  HIP graph drawing fresh noise on every replay) */
+  double gamma;               /* discount for ASVRL_F_RET (trainer.py:161); 0 disables */
+  const uint8_t* env_mask;    /* optional [n_envs]: only envs with mask != 0 are processed */
+} AsvStepCtl;
+
+/* Outputs of asvrl_env_step (device). Optional members may be NULL. */
+typedef struct AsvStepOut {
+  float* obs;        /* [n_envs*max_robots][ASVRL_OBS_DIM] packed f32 observation */
+  double* obs64;     /* optional [n_envs*max_robots][32] f64 self(7)+objects(25) (compat path) */
+  int8_t* obj_cnt;   /* [n_envs*max_robots] objects kept (0..5); -1 = (None, None) */
+  double* reward;    /* [n_envs*max_robots] (env.py:242-328) */
+  uint8_t* done;     /* [n_envs*max_robots] */
+  uint8_t* info;     /* [n_envs*max_robots] ASVRL_INFO_* */
+  uint8_t* env_done; /* optional [n_envs] trainer episode end (trainer.py:172) */
+  double* stats;     /* optional [8] running sums over finished robot-episodes:
+                        return, count, reach-goal, collision, timeout, env-episodes */
+} AsvStepOut;
+
+/* Reset parameters (env.py:33-54,72-164, curriculum values from the schedule). */
+typedef struct AsvResetCfg {
+  int32_t num_robots, num_obs, num_cores, _pad0;
+  double min_start_goal_dis, width, height, clear_r;
+  double obs_r_lo, obs_r_hi;       /* env.py:39 */
+  double v_lo, v_hi;               /* env.py:38 core edge speed */
+  double v_rel_max, p_rel;         /* env.py:36-37 */
+} AsvResetCfg;
+
+/* ---------------------------------------------------------------- env */
+
+/* MarineNavEnv3.step (env.py:240-333) for every env of the batch in one launch: the N
+ * Fossen substeps per robot (wamv.py:204-279, current field env.py:458-501), the sector
+ * "LiDAR" object list with top-5 selection and collision test (wamv.py:436-529), COLREGs
+ * (wamv.py:324-434) and reward/done/info (env.py:271-331).
+ * actions: [n_envs*max_robots][2] f64; discrete actions pass the action index in [0].
+ * noise (noise_mode 0): [n_envs*max_robots][max_obs + max_robots][5] f64 draws
+ *   [n_px, n_py, n_vx, n_vy, vonmises] per candidate slot (slot k < max_obs: obstacle k,
+ *   slot max_obs + j: robot j), in the order Perception makes them (wamv.py:27-40). */
+int asvrl_env_step(const AsvParams* params, const AsvEnvState* state, const double* actions,
+                   const double* noise, const AsvStepCtl* ctl, const AsvStepOut* out,
+                   void* stream);
+
+/* MarineNavEnv3.reset (env.py:72-164) for envs with env_mask != 0, sampled on the device
+ * with Philox (same rejection rules and iteration caps; not the reference's RandomState
+ * stream -- the parity path resets on the host). Follow with asvrl_env_step(do_dynamics=0,
+ * env_mask) to produce the reset observation. */
+int asvrl_env_reset(const AsvParams* params, const AsvEnvState* state, const AsvResetCfg* cfg,
+                    const uint8_t* env_mask, uint64_t seed, uint64_t counter,
+                    const uint64_t* counter_dev, void* stream);
+
+/* Ocean current of env.py:458-501 at n query points xy [n][2] for one env's cores
+ * [n_cores][4] -> out [n][3]. Used for the initial velocity of reset_with_eval_config
+ * (env.py:609-610); the step kernel evaluates the same field per substep. */
+int asvrl_current_field(const double* cores, int32_t n_cores, double core_r, const double* xy,
+                        int32_t n, double* out, void* stream);
+
+/* ---------------------------------------------------------------- learner */
+
+/* Quantile-Huber loss of agent.py:406-412 (+ calculate_huber_loss agent.py:701-707) and its
+ * gradient w.r.t. the expected quantiles:
+ *   delta[b,i,j] = qt[b,j] - qe[b,i]
+ *   row_loss[b]  = (1/Np) sum_j sum_i |tau[b,i] - 1{delta<0}| * H_kappa(delta) / kappa
+ *   loss[0]      = mean_b row_loss[b]
+ *   dqe[b,i]     = grad_scale * d loss / d qe[b,i]
+ * qt [B][Np], qe [B][N], tau [B][N] f32. loss may be NULL. */
+int asvrl_quantile_huber(const float* qt, const float* qe, const float* tau, int32_t B, int32_t N,
+                         int32_t Np, float kappa, float grad_scale, float* row_loss, float* loss,
+                         float* dqe, void* stream);
+
+/* C51 categorical projection of agent.py:616-631 (Tz, clamp, b, l/u with the l == u fix,
+ * index_add_ of p(u - b) then p(b - l)), bit-identical to the reference's CPU f32 result.
+ * pns_a [B][atoms], returns [B], nonterminal [B], support [atoms] -> m [B][atoms]. */
+int asvrl_c51_project(const float* pns_a, const float* returns, const float* nonterminal,
+                      const float* support, int32_t B, int32_t atoms, float vmin, float vmax,
+                      float delta_z, float gamma_n, float* m, void* stream);
+
+/* ---------------------------------------------------------------- replay (replay_buffer.py) */
+
+/* ReplayBuffer.add (replay_buffer.py:22-24) for every robot that acted in the last step
+ * (obj_cnt_next >= 0), in slot order, into a ring of `capacity` rows of ASVRL_TR_DIM f32.
+ * ring_state: int64[2] = {head, size} in device memory (updated by the call, so the call
+ * is capturable in a HIP graph). work: int32[ceil(n / 256) + 1] scratch. */
+int asvrl_replay_push(const float* obs_prev, const float* obs_next, const int8_t* obj_cnt_next,
+                      const double* actions, int32_t action_dim, const double* reward,
+                      const uint8_t* done, int32_t n, float* ring, int64_t capacity,
+                      int64_t* ring_state, int32_t* work, void* stream);
+
+/* ReplayBuffer.sample (replay_buffer.py:26-45): gather B rows. With `indices` (host-chosen,
+ * deque order: 0 = oldest) the rows are exactly those; with indices == NULL, B positions are
+ * drawn uniformly (with replacement) by Philox(seed, counter + *counter_dev).
+ * out [B][ASVRL_TR_DIM]; out_slots optional [B]. */
+int asvrl_replay_sample(const float* ring, int64_t capacity, const int64_t* ring_state,
+                        const int64_t* indices, int32_t B, uint64_t seed, uint64_t counter,
+                        const uint64_t* counter_dev, float* out, int64_t* out_slots, void* stream);
+
+/* Host-side index copy helper for a ring with known (host) head/size: write rows given by
+ * slot into the ring (used by the compat ReplayBuffer.add, one transition per call). */
+int asvrl_replay_write_rows(const float* rows, const int64_t* slots, int32_t n, float* ring,
+                            void* stream);
+
+/* ---------------------------------------------------------------- misc */
+const char* asvrl_last_error(void);
+int asvrl_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ASVRL_H */

@@ -1,0 +1,231 @@
+"""GPU parity of the env-step kernel against the reference's own outputs (tests/golden).
+
+Every step of every captured MarineNavEnv3 trace becomes one env of a single batched launch
+(teacher-forced: the captured pre-step state, flags, actions and the exact perception noise
+the reference drew), so one kernel launch is checked against ~800 reference steps:
+  * f64 state, rewards and observations within 1e-12 (abs, scaled by magnitude),
+  * collision / reach-goal / done / info / object-count / COLREGs masks bit-exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import env_oracle as eo
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-12
+
+
+def _close(a, b, tol=TOL):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    scale = np.maximum(1.0, np.abs(b))
+    return np.all(np.abs(a - b) <= tol * scale), float(np.max(np.abs(a - b) / scale)) if a.size else 0.0
+
+
+def _batch_from_traces(traces, continuous):
+    """Flatten (trace, step) pairs into env rows of one DeviceEnvBatch."""
+    rows = []
+    for name, tr in traces.items():
+        if name.startswith("disc") == continuous:
+            continue
+        for t in range(len(tr["reward"])):
+            rows.append((name, t, eo.trace_step_inputs(tr, t), tr))
+    return rows
+
+
+def _run_rows(rows, continuous):
+    from distributional_rl_decision_and_control_amd.device_env import DeviceEnvBatch
+    from distributional_rl_decision_and_control_amd import _abi
+
+    E = len(rows)
+    R = max(r[2]["state_before"].shape[0] for r in rows)
+    O = max(r[2]["O"] for r in rows)
+    Cm = 8
+    z = np.load(eo.GOLDEN + "/env_dynamics.npz")
+    params = _abi.params_from()
+    assert np.array_equal(np.array(params.P[:]), z["P"].reshape(-1)), "host P differs from the reference's numpy P"
+    b = DeviceEnvBatch(E, R, O, Cm, obs64=True, params=params)
+    rs = np.zeros((_abi.NUM_FIELDS, E * R))
+    fl = np.zeros(E * R, np.uint8)
+    nrob = np.zeros(E, np.int32)
+    nobs = np.zeros(E, np.int32)
+    ncor = np.zeros(E, np.int32)
+    ep = np.zeros(E, np.int32)
+    obst = np.zeros((E, O, 3))
+    cores = np.zeros((E, Cm, 4))
+    acts = np.zeros((E * R, 2))
+    noise = np.zeros((E * R, O + R, 5))
+    for e, (_, _, inp, tr) in enumerate(rows):
+        n = inp["state_before"].shape[0]
+        base = e * R
+        sb = inp["state_before"]
+        rs[:13, base:base + n] = sb.T
+        rs[_abi.F_GX, base:base + n] = inp["goals"][:, 0]
+        rs[_abi.F_GY, base:base + n] = inp["goals"][:, 1]
+        fl[base:base + n] = (inp["deact"] * _abi.FLAG_DEACTIVATED) | (inp["coll"] * _abi.FLAG_COLLISION) | (
+            inp["reach"] * _abi.FLAG_REACH_GOAL)
+        nrob[e] = n
+        nobs[e] = inp["n_obs"]
+        ncor[e] = inp["n_cores"]
+        ep[e] = inp["ep_ts"]
+        Oe = inp["O"]
+        obst[e, :Oe] = inp["obstacles"]
+        cores[e, :inp["n_cores"]] = inp["cores"][:inp["n_cores"]]
+        acts[base:base + n] = inp["actions"]
+        nz = inp["noise"]  # [n, Oe + n, 5]
+        noise[base:base + n, :Oe] = nz[:, :Oe]
+        noise[base:base + n, O:O + n] = nz[:, Oe:Oe + n]
+    dev = b.device
+    b.rs.copy_(torch.from_numpy(rs))
+    b.rflags.copy_(torch.from_numpy(fl))
+    b.n_robots.copy_(torch.from_numpy(nrob))
+    b.n_obs.copy_(torch.from_numpy(nobs))
+    b.n_cores.copy_(torch.from_numpy(ncor))
+    b.ep_ts.copy_(torch.from_numpy(ep))
+    b.obstacles.copy_(torch.from_numpy(obst))
+    b.cores.copy_(torch.from_numpy(cores))
+    a_d = torch.from_numpy(acts).to(dev)
+    n_d = torch.from_numpy(noise).to(dev)
+    b.step(a_d, is_continuous=continuous, noise=n_d)
+    torch.cuda.synchronize()
+    return b, R
+
+
+def _check_rows(rows, b, R):
+    from distributional_rl_decision_and_control_amd import _abi
+    rs = b.rs.cpu().numpy()
+    fl = b.rflags.cpu().numpy()
+    o64 = b.obs64.cpu().numpy()
+    cnt = b.obj_cnt.cpu().numpy()
+    rew = b.reward.cpu().numpy()
+    done = b.done.cpu().numpy()
+    info = b.info.cpu().numpy()
+    obs32 = b.obs.cpu().numpy()
+    worst = {}
+    for e, (name, t, inp, tr) in enumerate(rows):
+        n = inp["state_before"].shape[0]
+        sl = slice(e * R, e * R + n)
+        checks = {
+            "state": (rs[:13, sl].T, tr["state_after"][t][:n]),
+            "reward": (rew[sl], tr["reward"][t][:n]),
+            "self_obs": (o64[sl, :7], tr["self_obs"][t][:n]),
+            "obj_obs": (o64[sl, 7:32].reshape(n, 5, 5), tr["obj_obs"][t][:n]),
+        }
+        for k, (got, ref) in checks.items():
+            ok, err = _close(got, ref)
+            worst[k] = max(worst.get(k, 0.0), err)
+            assert ok, f"{name} step {t}: {k} off by {err}"
+        valid = tr["obs_valid"][t][:n]
+        ref_cnt = np.where(valid == 1, tr["obj_cnt"][t][:n], -1)
+        assert np.array_equal(cnt[sl].astype(int), ref_cnt.astype(int)), f"{name} step {t}: object count"
+        assert np.array_equal(done[sl], tr["done"][t][:n]), f"{name} step {t}: done mask"
+        assert np.array_equal(info[sl], tr["info"][t][:n]), f"{name} step {t}: info"
+        assert np.array_equal((fl[sl] & _abi.FLAG_COLLISION) > 0, tr["collision"][t][:n] > 0), f"{name} {t}: collision"
+        assert np.array_equal((fl[sl] & _abi.FLAG_REACH_GOAL) > 0, tr["reach"][t][:n] > 0), f"{name} {t}: reach"
+        act = inp["deact"] == 0
+        assert np.array_equal(((fl[sl] & _abi.FLAG_COLREGS) > 0)[act], tr["apply_colregs"][t][:n][act] > 0)
+        phi_ref = tr["phi"][t][:n]
+        m = ~np.isnan(phi_ref)
+        if m.any():
+            ok, err = _close(rs[_abi.F_PHI, sl][m], phi_ref[m])
+            assert ok, f"{name} step {t}: phi off by {err}"
+        # packed f32 row == the reference's state_batch(...).float() layout
+        so = tr["self_obs"][t][:n].astype(np.float32)
+        oo = tr["obj_obs"][t][:n].astype(np.float32).reshape(n, 25)
+        mask = (np.arange(5)[None, :] < ref_cnt[:, None]).astype(np.float32)
+        for i in range(n):
+            if ref_cnt[i] < 0:
+                assert not obs32[e * R + i].any()
+                continue
+            np.testing.assert_array_equal(obs32[e * R + i, :7], so[i])
+            np.testing.assert_array_equal(obs32[e * R + i, 7:32], oo[i])
+            np.testing.assert_array_equal(obs32[e * R + i, 32:37], mask[i])
+    return worst
+
+
+@pytest.mark.parametrize("continuous", [True, False])
+def test_env_step_matches_reference_traces(continuous):
+    traces = eo.load_traces()
+    rows = _batch_from_traces(traces, continuous)
+    assert len(rows) > 0
+    b, R = _run_rows(rows, continuous)
+    worst = _check_rows(rows, b, R)
+    print("worst relative errors:", worst)
+
+
+@pytest.mark.parametrize("case", ["cont", "disc", "cont_cores"])
+def test_dynamics_matches_reference(case):
+    """F1: N Fossen substeps from random states (wamv.py:204-279), incl. theta wrap, thrust
+    saturation, discrete action grid and the 4-core current field."""
+    from distributional_rl_decision_and_control_amd.device_env import DeviceEnvBatch
+    from distributional_rl_decision_and_control_amd import _abi
+    z = np.load(eo.GOLDEN + "/env_dynamics.npz")
+    sb, sa, acts = z[case + "/state_before"], z[case + "/state_after"], z[case + "/actions"]
+    E = sb.shape[0]
+    b = DeviceEnvBatch(E, 1, 0, 8)
+    rs = np.zeros((_abi.NUM_FIELDS, E))
+    rs[:13] = sb.T
+    b.rs.copy_(torch.from_numpy(rs))
+    b.n_robots.fill_(1)
+    if case == "cont_cores":
+        b.n_cores.fill_(4)
+        c = np.zeros((E, 8, 4))
+        c[:, :4] = z["cores"][None]
+        b.cores.copy_(torch.from_numpy(c))
+    b.step(torch.from_numpy(acts).cuda(), is_continuous=case != "disc",
+           noise=torch.zeros((E, 1, 5), dtype=torch.float64, device="cuda"))
+    got = b.rs[:13].T.cpu().numpy()
+    ok, err = _close(got, sa)
+    assert ok, f"dynamics {case}: max rel err {err}"
+
+
+def test_current_field_matches_reference():
+    from distributional_rl_decision_and_control_amd.device_env import current_field
+    z = np.load(eo.GOLDEN + "/env_dynamics.npz")
+    out = current_field(torch.from_numpy(z["cores"]).cuda(), float(z["core_r"]),
+                        torch.from_numpy(z["current_query"]).cuda()).cpu().numpy()
+    ok, err = _close(out, z["current_value"])
+    assert ok, err
+
+
+def test_env_step_philox_invariants_full_size():
+    """Config-2 size (4096 envs x 5 robots, 4 buoys): device reset + 50 Philox-noise steps.
+    Size-independent properties: theta in [0, 2pi), thrust within bounds, masks consistent
+    with info codes, deactivated robots frozen, identical results on a replay."""
+    from distributional_rl_decision_and_control_amd.device_env import DeviceEnvBatch, reset_cfg
+    from distributional_rl_decision_and_control_amd import _abi
+    E, R, O = 4096, 5, 4
+
+    def run():
+        b = DeviceEnvBatch(E, R, O, 0)
+        b.reset(reset_cfg(5, 4, 0, 40.0), seed=7)
+        b.step(None, do_dynamics=False, seed=7, counter=0)
+        g = torch.Generator(device="cuda").manual_seed(3)
+        snaps = []
+        for t in range(50):
+            a = (torch.rand((E * R, 2), generator=g, device="cuda", dtype=torch.float64) * 2 - 1).contiguous()
+            prev_fl = b.rflags.clone()
+            prev_rs = b.rs.clone()
+            b.step(a, seed=7, counter=t + 1, trainer_deactivate=True, gamma=0.99)
+            th = b.rs[_abi.F_THETA]
+            assert bool(((th >= 0) & (th < 2 * np.pi)).all())
+            for f in (_abi.F_TL, _abi.F_TR):
+                assert bool(((b.rs[f] >= -500) & (b.rs[f] <= 1000)).all())
+            was_off = (prev_fl & _abi.FLAG_DEACTIVATED) > 0
+            assert torch.equal(b.rs[:13][:, was_off], prev_rs[:13][:, was_off])
+            info = b.info
+            fl = b.rflags
+            coll = (fl & _abi.FLAG_COLLISION) > 0
+            assert bool((coll[info == _abi.INFO_COLLISION]).all())
+            assert bool((b.done[info == _abi.INFO_NORMAL] == 0).all())
+            snaps.append(b.reward.clone())
+        return torch.stack(snaps), b
+
+    r1, b1 = run()
+    r2, _ = run()
+    assert torch.equal(r1, r2), "Philox path must be deterministic for a fixed seed"
+    n = b1.n_robots.cpu().numpy()
+    assert n.min() >= 1 and n.max() <= R
+    assert b1.n_obs.cpu().numpy().max() <= O
