@@ -1,0 +1,151 @@
+"""Distributional Bellman updates of rfarl's Agent (agent.py:386-476, 597-641) on the GPU.
+
+The quantile-Huber loss and its gradient come from the fused gfx950 kernel
+(learn_ops.quantile_huber_loss), the C51 target from the bit-exact projection kernel
+(learn_ops.c51_project); the MLP layers run on torch (hipBLASLt/MFMA), optionally under bf16
+autocast. Data-parallel training passes a GradSync, which all-reduces each network's flat
+gradient over RCCL between backward and clip -- twice per AC-IQN step (critic, then actor
+through the *updated* critic, agent.py:395-427), once for IQN / Rainbow.
+"""
+import torch
+import torch.distributed as dist
+
+from .learn_ops import c51_project, quantile_huber_loss
+
+
+class FlatGrads:
+    """Gives every parameter of `params` a .grad that is a view into one flat buffer, so a
+    gradient all-reduce is one collective on contiguous memory."""
+
+    def __init__(self, params):
+        self.params = [p for p in params if p.requires_grad]
+        n = sum(p.numel() for p in self.params)
+        dev = self.params[0].device
+        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        off = 0
+        for p in self.params:
+            p.grad = self.flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+
+    def zero_(self):
+        self.flat.zero_()
+
+    def assign(self, grads):
+        torch._foreach_copy_([p.grad for p in self.params], list(grads))
+
+
+class GradSync:
+    """All-reduce(average) of a FlatGrads buffer over the default process group (RCCL on
+    MI355X: backend "nccl"; gloo on CPU tests)."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.avg_supported = dist.is_initialized() and dist.get_backend(group) == "nccl"
+
+    def __call__(self, fg: FlatGrads):
+        if self.world == 1:
+            return
+        if self.avg_supported:
+            dist.all_reduce(fg.flat, op=dist.ReduceOp.AVG, group=self.group)
+        else:
+            dist.all_reduce(fg.flat, op=dist.ReduceOp.SUM, group=self.group)
+            fg.flat.div_(self.world)
+
+
+def _clip(params, max_norm):
+    return torch.nn.utils.clip_grad_norm_(params, max_norm)
+
+
+def ac_iqn_update(policy_local, policy_target, actor_opt, critic_opt, critic_grads, actor_grads, states, actions,
+                  rewards, next_states, dones, gamma=0.99, num_tau=8, taus=(None, None, None), sync=None,
+                  amp_dtype=None, max_norm=0.5):
+    """train_AC_IQN (agent.py:386-432). rewards/dones (B, 1). Returns (critic_loss, actor_loss,
+    critic_grad_norm, actor_grad_norm) as 0-d device tensors (no host sync)."""
+    actor, critic = policy_local.actor, policy_local.critic
+    amp = torch.autocast("cuda", dtype=amp_dtype) if amp_dtype is not None else _null()
+    # ---- critic (agent.py:395-416)
+    critic_grads.zero_()
+    with torch.no_grad(), amp:
+        next_actions = policy_target.actor(next_states)
+        q_next, _ = policy_target.critic(next_states, next_actions, num_tau, taus=taus[0])
+    q_next = q_next.float()
+    q_targets = rewards + gamma * q_next * (1.0 - dones)  # (B, N')
+    with amp:
+        q_exp, tau_e = critic(states, actions, num_tau, taus=taus[1])
+    critic_loss = quantile_huber_loss(q_targets, q_exp.float(), tau_e)
+    critic_loss.backward()
+    if sync is not None:
+        sync(critic_grads)
+    cgn = _clip(critic_grads.params, max_norm)
+    critic_opt.step()
+    # ---- actor through the updated critic (agent.py:419-427); only actor grads are needed
+    with amp:
+        a_out = actor(states)
+        q_pi, _ = critic(states, a_out, num_tau, taus=taus[2])
+    actor_loss = -q_pi.float().mean()
+    g = torch.autograd.grad(actor_loss, actor_grads.params)
+    actor_grads.assign(g)
+    if sync is not None:
+        sync(actor_grads)
+    agn = _clip(actor_grads.params, max_norm)
+    actor_opt.step()
+    return critic_loss.detach(), actor_loss.detach(), cgn, agn
+
+
+def iqn_update(policy_local, policy_target, opt, grads, states, actions, rewards, next_states, dones, gamma=0.99,
+               num_tau=8, taus=(None, None), sync=None, amp_dtype=None, max_norm=0.5):
+    """train_IQN (agent.py:434-476); actions (B,) int64. Target = max over actions per tau
+    sample (agent.py:452), not argmax of the mean."""
+    amp = torch.autocast("cuda", dtype=amp_dtype) if amp_dtype is not None else _null()
+    grads.zero_()
+    with torch.no_grad(), amp:
+        qn, _ = policy_target(next_states, num_tau, taus=taus[0])
+    qn = qn.float().max(2)[0]  # (B, N)
+    q_targets = rewards + gamma * qn * (1.0 - dones)
+    with amp:
+        qe, tau_e = policy_local(states, num_tau, taus=taus[1])
+    B = qe.shape[0]
+    qe = qe.float().gather(2, actions.view(B, 1, 1).expand(B, num_tau, 1)).squeeze(-1)
+    loss = quantile_huber_loss(q_targets, qe, tau_e)
+    loss.backward()
+    if sync is not None:
+        sync(grads)
+    gn = _clip(grads.params, max_norm)
+    opt.step()
+    return loss.detach(), gn
+
+
+def rainbow_update(policy_local, policy_target, opt, grads, support, states, actions, returns, next_states,
+                   nonterminals, weights, gamma=0.99, n=3, vmin=-1.0, vmax=1.0, sync=None, max_norm=0.5,
+                   reset_target_noise=True):
+    """train_Rainbow (agent.py:597-641) with the projection on the C51 kernel. Returns the
+    per-sample loss (for update_priorities) and the pre-clip grad norm."""
+    B = actions.shape[0]
+    log_ps = policy_local(states, log=True)
+    log_ps_a = log_ps[torch.arange(B, device=actions.device), actions]
+    with torch.no_grad():
+        pns = policy_local(next_states)
+        dns = support.expand_as(pns) * pns
+        argmax_ns = dns.sum(2).argmax(1)
+        if reset_target_noise:
+            policy_target.reset_noise()
+        pns = policy_target(next_states)
+        pns_a = pns[torch.arange(B, device=actions.device), argmax_ns]
+        m = c51_project(pns_a, returns, nonterminals, support, vmin, vmax, gamma ** n)
+    loss = -torch.sum(m * log_ps_a, 1)
+    grads.zero_()
+    (weights * loss).mean().backward()
+    if sync is not None:
+        sync(grads)
+    gn = _clip(grads.params, max_norm)
+    opt.step()
+    return loss.detach(), gn
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

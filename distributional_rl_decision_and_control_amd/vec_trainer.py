@@ -1,0 +1,215 @@
+"""VecTrainer -- the fused rollout + learn loop of rfarl's Trainer.learn (trainer.py:85-255),
+batched over E envs on one GPU, data-parallel over ranks.
+
+One iteration (= one `step` of bench.py):
+  1. act: the local actor on every robot of every env (E*R rows), epsilon-greedy on device
+     (trainer.py:106-135, agent.py:207-225; linear epsilon schedule trainer.py:257-264)
+  2. env step kernel with the trainer bookkeeping fused (asvrl_env_step)
+  3. replay push of the transitions of robots that acted (asvrl_replay_push, trainer.py:157-166)
+  4. device reset of finished envs + their first observation (asvrl_env_reset, trainer.py:212-245)
+  5. learn: sample B transitions (asvrl_replay_sample) and one distributional update
+     (AC-IQN: two dependent optimizer steps, critic then actor; IQN: one)
+  6. hard target update every `target_update_interval` learn steps (agent.py:643-679, TAU=1)
+
+Cadence in the batched setting: one learn step of batch B per iteration (after
+`learning_starts` transitions) replaces the reference's one B=64 step per 4 single-env
+timesteps; target updates count learn steps (2500 = 10000 timesteps / UPDATE_EVERY 4).
+With `graphs=True` steps 1-5 are captured once into a HIP graph and replayed.
+"""
+import time
+
+import torch
+
+from .learn_ops import DeviceReplay, split_rows
+from .learner import FlatGrads, GradSync, ac_iqn_update, iqn_update
+from .policy.AC_IQN_model import AC_IQN_Policy
+from .policy.IQN_model import IQN_Policy
+from .vec_env import VecMarineNavEnv, split_obs
+
+DEFAULT_NET = dict(self_dimension=7, object_dimension=5, max_object_num=5, self_feature_dimension=56,
+                   object_feature_dimension=40, concat_feature_dimension=256, hidden_dimension=128)
+
+
+class VecTrainer:
+    def __init__(self, n_envs=4096, agent_type="AC-IQN", num_robots=5, num_obs=4, num_cores=0, min_start_goal_dis=40.0,
+                 width=55.0, batch_size=4096, num_tau=32, buffer_size=4_000_000, lr=1e-4, gamma=0.99,
+                 learning_starts=None, target_update_interval=2500, total_timesteps=6_000_000,
+                 exploration_fraction=0.25, initial_eps=0.6, final_eps=0.05, amp_dtype=torch.bfloat16, seed=0,
+                 device="cuda", sync=None, graphs=False, schedule=None, net_seed=100):
+        self.device = torch.device(device)
+        self.agent_type = agent_type
+        self.continuous = agent_type == "AC-IQN"
+        self.env = VecMarineNavEnv(n_envs, num_robots, num_obs, num_cores, min_start_goal_dis, width, seed=seed,
+                                   device=self.device, is_continuous=self.continuous, gamma=gamma, schedule=schedule)
+        self.E, self.R = n_envs, self.env.max_robots
+        self.B, self.num_tau, self.gamma = batch_size, num_tau, gamma
+        self.amp_dtype = amp_dtype
+        self.sync = sync
+        self.seed = seed
+        self.target_update_interval = target_update_interval
+        self.total_timesteps = total_timesteps
+        self.exploration_fraction, self.initial_eps, self.final_eps = exploration_fraction, initial_eps, final_eps
+        self.learning_starts = learning_starts if learning_starts is not None else batch_size
+        capturable = bool(graphs)
+        if agent_type == "AC-IQN":
+            self.local = AC_IQN_Policy(**DEFAULT_NET, value_ranges_of_action=[[-1.0, 1.0], [-1.0, 1.0]],
+                                       device=self.device, seed=net_seed)
+            self.target = AC_IQN_Policy(**DEFAULT_NET, value_ranges_of_action=[[-1.0, 1.0], [-1.0, 1.0]],
+                                        device=self.device, seed=net_seed)
+            for p in list(self.target.actor.parameters()) + list(self.target.critic.parameters()):
+                p.requires_grad_(False)
+            self.critic_grads = FlatGrads(self.local.critic.parameters())
+            self.actor_grads = FlatGrads(self.local.actor.parameters())
+            self.actor_opt = torch.optim.Adam(self.local.actor.parameters(), lr=lr, capturable=capturable)
+            self.critic_opt = torch.optim.Adam(self.local.critic.parameters(), lr=lr, capturable=capturable)
+            self.action_dim = 2
+        elif agent_type == "IQN":
+            self.local = IQN_Policy(**DEFAULT_NET, action_size=25, device=self.device, seed=net_seed).to(self.device)
+            self.target = IQN_Policy(**DEFAULT_NET, action_size=25, device=self.device, seed=net_seed).to(self.device)
+            for p in self.target.parameters():
+                p.requires_grad_(False)
+            self.grads = FlatGrads(self.local.parameters())
+            self.opt = torch.optim.Adam(self.local.parameters(), lr=lr, capturable=capturable)
+            self.action_dim = 1
+        else:
+            raise NotImplementedError(f"VecTrainer agent_type {agent_type!r} (AC-IQN and IQN are batched)")
+        NT = self.E * self.R
+        self.replay = DeviceReplay(max(buffer_size, 2 * NT), device=self.device)
+        self.actions = torch.zeros((NT, 2), dtype=torch.float64, device=self.device)
+        self.learn_counter = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.batch_rows = torch.zeros((self.B, 88), dtype=torch.float32, device=self.device)
+        self.learn_steps = 0
+        self.iterations = 0
+        self.last_losses = None
+        self.graphs = graphs
+        self._graph = None
+        self._graph_learn = None
+        self._gen = torch.Generator(device=self.device)
+        self._gen.manual_seed(seed + 12345)
+        self.env.reset()
+
+    # ------------------------------------------------------------------ pieces
+    def epsilon(self):
+        """trainer.py:257-264 as a device scalar of the device step counter (graph-safe)."""
+        steps = self.env.counter.to(torch.float32) * float(self.E)
+        progress = steps / float(self.total_timesteps)
+        r = progress / self.exploration_fraction
+        eps = self.initial_eps + r * (self.final_eps - self.initial_eps)
+        return torch.where(progress < self.exploration_fraction, eps, torch.full_like(eps, self.final_eps))
+
+    @torch.no_grad()
+    def act(self):
+        obs = split_obs(self.env.obs_cur)
+        NT = obs[0].shape[0]
+        eps = self.epsilon()
+        explore = torch.rand((NT, 1), device=self.device) < eps
+        if self.agent_type == "AC-IQN":
+            amp = torch.autocast("cuda", dtype=self.amp_dtype) if self.amp_dtype is not None else _null()
+            with amp:
+                a = self.local.actor(obs).float()
+            rnd = torch.rand((NT, 2), device=self.device) * 2.0 - 1.0
+            self.actions.copy_(torch.where(explore, rnd, a))
+        else:
+            amp = torch.autocast("cuda", dtype=self.amp_dtype) if self.amp_dtype is not None else _null()
+            with amp:
+                q, _ = self.local(obs, self.local.K)
+            greedy = q.float().mean(dim=1).argmax(dim=1)
+            rnd = torch.randint(0, 25, (NT,), device=self.device)
+            self.actions[:, 0].copy_(torch.where(explore.squeeze(1), rnd, greedy))
+
+    def rollout(self):
+        self.act()
+        env = self.env
+        env.step(self.actions)
+        self.replay.push(env.obs_cur, env.obs_next, env.cnt_next, self.actions[:, :self.action_dim].contiguous()
+                         if self.action_dim == 1 else self.actions, env.batch.reward, env.batch.done)
+        env.auto_reset()
+
+    def learn(self):
+        rows = self.replay.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter, out=self.batch_rows)
+        s, a, r, ns, d = split_rows(rows)
+        if self.agent_type == "AC-IQN":
+            out = ac_iqn_update(self.local, self.target, self.actor_opt, self.critic_opt, self.critic_grads,
+                                self.actor_grads, s, a, r, ns, d, gamma=self.gamma, num_tau=self.num_tau,
+                                sync=self.sync, amp_dtype=self.amp_dtype)
+        else:
+            act = a[:, 0].to(torch.int64)
+            out = iqn_update(self.local, self.target, self.opt, self.grads, s, act, r, ns, d, gamma=self.gamma,
+                             num_tau=self.num_tau, sync=self.sync, amp_dtype=self.amp_dtype)
+        self.learn_counter += 1
+        return out
+
+    def hard_update(self):
+        """soft_update with TAU = 1.0 (agent.py:643-679): target <- local."""
+        with torch.no_grad():
+            if self.agent_type == "AC-IQN":
+                pairs = list(zip(self.target.actor.parameters(), self.local.actor.parameters())) + \
+                    list(zip(self.target.critic.parameters(), self.local.critic.parameters()))
+            else:
+                pairs = list(zip(self.target.parameters(), self.local.parameters()))
+            torch._foreach_copy_([t for t, _ in pairs], [l for _, l in pairs])
+
+    # ------------------------------------------------------------------ iteration
+    def _iteration_body(self, do_learn):
+        self.rollout()
+        out = self.learn() if do_learn else None
+        self.env.advance_device()
+        return out
+
+    def iteration(self, timing=None):
+        """One fused rollout+learn iteration. Returns losses (device tensors) or None."""
+        do_learn = self.replay_size_host() >= self.learning_starts
+        if self.graphs and do_learn:
+            if self._graph is None:
+                self._capture()
+            self._graph.replay()
+            out = self._graph_out
+        else:
+            out = self._iteration_body(do_learn)
+        self.env.advance_host()
+        self.iterations += 1
+        if do_learn:
+            self.learn_steps += 1
+            if self.learn_steps % self.target_update_interval == 0:
+                self.hard_update()
+        self.last_losses = out
+        return out
+
+    def replay_size_host(self):
+        # host-side estimate avoids a device sync every iteration: exact once the buffer
+        # has been observed >= learning_starts (it only grows until full)
+        if getattr(self, "_replay_ready", False):
+            return self.learning_starts
+        n = self.replay.size()
+        if n >= self.learning_starts:
+            self._replay_ready = True
+        return n
+
+    def _capture(self):
+        # warm up the captured region on a side stream (allocator + autograd state)
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                self._iteration_body(True)
+                self.env.advance_host()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._graph_out = self._iteration_body(True)
+        self._graph = g
+
+    def run(self, iterations):
+        t0 = time.time()
+        for _ in range(iterations):
+            self.iteration()
+        torch.cuda.synchronize(self.device)
+        return time.time() - t0
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

@@ -1,0 +1,205 @@
+"""CPU restatement of rfarl's distributional learners (TEST INFRASTRUCTURE ONLY).
+
+Functional torch-fp32 versions of the networks and update steps, written against weight
+dicts keyed like the reference's state_dicts -- independent of the product's nn.Modules:
+  ac_iqn_train   agent.py:386-432 (+ AC_IQN_model.py:284-323, 410-480)
+  iqn_train      agent.py:434-476 (+ IQN_model.py:56-110)
+  rainbow_train  agent.py:597-641 (+ Rainbow_model.py:17-139), C51 target m restated in
+                 explicit per-atom loops (the reference's index_add_ order)
+  adam_step      torch.optim.Adam defaults (single-tensor form), clip_grad_norm_
+Pinned against tests/golden/learn_*.npz (captured from the reference). Only tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline import this.
+"""
+import math
+
+import numpy as np
+import torch
+
+F = torch.nn.functional
+
+
+def _lin(w, p, x):
+    return F.linear(x, w[p + ".weight"], w[p + ".bias"])
+
+
+def _features(w, s_self, s_obj, s_mask, obj_feat=40, max_obj=5, obj_dim=5):
+    B = s_self.shape[0]
+    f1 = torch.relu(_lin(w, "self_encoder.0", s_self))
+    f2 = torch.relu(_lin(w, "object_encoder.0", s_obj.reshape(B * max_obj, obj_dim))).view(B, max_obj, obj_feat)
+    f2 = f2.masked_fill(s_mask.unsqueeze(-1) < 0.5, 0.0).reshape(B, max_obj * obj_feat)
+    return torch.cat((f1, f2), 1)
+
+
+def actor_forward(w, s):
+    f = _features(w, *s)
+    f = torch.relu(_lin(w, "hidden_layer", f))
+    f = torch.relu(_lin(w, "hidden_layer_2", f))
+    return torch.tensor(2.0 / torch.pi) * torch.atan(_lin(w, "output_layer", f))
+
+
+def _cos(taus, n=64):
+    pis = torch.FloatTensor([np.pi * i for i in range(n)]).view(1, 1, n)
+    return torch.cos(taus * pis)
+
+
+def critic_forward(w, s, a, taus):
+    """taus (B, N, 1) -> quantiles (B, N)."""
+    B, N = taus.shape[0], taus.shape[1]
+    f = _features(w, *s)
+    c = torch.relu(_lin(w, "cos_embedding", _cos(taus).view(B * N, 64))).view(B, N, -1)
+    f = (f.unsqueeze(1) * c).view(B * N, -1)
+    f = torch.relu(_lin(w, "hidden_layer", f))
+    af = torch.relu(_lin(w, "action_encoder.0", a))
+    f = (af.unsqueeze(1) * f.view(B, N, -1)).view(B * N, -1)
+    f = torch.relu(_lin(w, "hidden_layer_2", f))
+    return _lin(w, "output_layer", f).view(B, N)
+
+
+def iqn_forward(w, s, taus, action_size=25):
+    B, N = taus.shape[0], taus.shape[1]
+    f = _features(w, *s)
+    c = torch.relu(_lin(w, "cos_embedding", _cos(taus).view(B * N, 64))).view(B, N, -1)
+    f = (f.unsqueeze(1) * c).view(B * N, -1)
+    f = torch.relu(_lin(w, "hidden_layer", f))
+    f = torch.relu(_lin(w, "hidden_layer_2", f))
+    return _lin(w, "output_layer", f).view(B, N, action_size)
+
+
+def quantile_huber(q_targets, q_expected, taus, k=1.0):
+    """agent.py:406-412: q_targets (B, N'), q_expected (B, N), taus (B, N, 1)."""
+    td = q_targets.unsqueeze(1) - q_expected.unsqueeze(-1)
+    h = torch.where(td.abs() <= k, 0.5 * td.pow(2), k * (td.abs() - 0.5 * k))
+    ql = (taus - (td.detach() < 0).float()).abs() * h / k
+    return ql.sum(dim=1).mean(dim=1).mean()
+
+
+def clip_(grads, max_norm):
+    total = torch.norm(torch.stack([torch.norm(g, 2.0) for g in grads]), 2.0)
+    coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
+    for g in grads:
+        g.mul_(coef)
+    return float(total)
+
+
+class Adam:
+    """torch.optim.Adam(lr) defaults: betas (0.9, 0.999), eps 1e-8, no weight decay."""
+
+    def __init__(self, names, lr=1e-4):
+        self.names, self.lr, self.t = names, lr, 0
+        self.m, self.v = {}, {}
+
+    def step(self, w, grads):
+        self.t += 1
+        b1, b2, eps = 0.9, 0.999, 1e-8
+        bc1 = 1 - b1 ** self.t
+        bc2 = 1 - b2 ** self.t
+        for n, g in zip(self.names, grads):
+            m = self.m.setdefault(n, torch.zeros_like(g))
+            v = self.v.setdefault(n, torch.zeros_like(g))
+            m.lerp_(g, 1 - b1)
+            v.mul_(b2).addcmul_(g, g, value=1 - b2)
+            denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+            w[n].data.addcdiv_(m, denom, value=-self.lr / bc1)
+
+
+def _leaf(sd):
+    return {k: torch.tensor(np.asarray(v), dtype=torch.float32).requires_grad_(True) for k, v in sd.items()}
+
+
+class ACIQNRef:
+    """State of an AC-IQN agent on the CPU: local/target actor+critic weights and two Adams."""
+
+    def __init__(self, actor_sd, critic_sd, lr=1e-4, gamma=0.99):
+        self.actor, self.critic = _leaf(actor_sd), _leaf(critic_sd)
+        self.t_actor = {k: v.detach().clone() for k, v in self.actor.items()}
+        self.t_critic = {k: v.detach().clone() for k, v in self.critic.items()}
+        self.aopt = Adam(list(self.actor), lr)
+        self.copt = Adam(list(self.critic), lr)
+        self.gamma = gamma
+
+    def train(self, s, a, r, ns, d, taus):
+        """agent.py:386-432 with the three tau draws supplied. r, d: (B, 1)."""
+        with torch.no_grad():
+            na = actor_forward(self.t_actor, ns)
+            qn = critic_forward(self.t_critic, ns, na, taus[0])
+        qt = r + self.gamma * qn * (1.0 - d)
+        qe = critic_forward(self.critic, s, a, taus[1])
+        closs = quantile_huber(qt, qe, taus[1])
+        names = list(self.critic)
+        g = torch.autograd.grad(closs, [self.critic[n] for n in names])
+        g = [x.clone() for x in g]
+        cgn = clip_(g, 0.5)
+        self.copt.step(self.critic, g)
+        ao = actor_forward(self.actor, s)
+        aloss = -critic_forward(self.critic, s, ao, taus[2]).mean()
+        an = list(self.actor)
+        g = [x.clone() for x in torch.autograd.grad(aloss, [self.actor[n] for n in an])]
+        agn = clip_(g, 0.5)
+        self.aopt.step(self.actor, g)
+        return float(closs.detach()), float(aloss.detach()), cgn, agn
+
+
+class IQNRef:
+    def __init__(self, sd, lr=1e-4, gamma=0.99):
+        self.w = _leaf(sd)
+        self.t = {k: v.detach().clone() for k, v in self.w.items()}
+        self.opt = Adam(list(self.w), lr)
+        self.gamma = gamma
+
+    def train(self, s, a, r, ns, d, taus):
+        """agent.py:434-476; a (B,) int64, taus (target, local)."""
+        with torch.no_grad():
+            qn = iqn_forward(self.t, ns, taus[0]).max(2)[0]
+        qt = r + self.gamma * qn * (1.0 - d)
+        B, N = taus[1].shape[0], taus[1].shape[1]
+        qe = iqn_forward(self.w, s, taus[1]).gather(2, a.view(B, 1, 1).expand(B, N, 1)).squeeze(-1)
+        loss = quantile_huber(qt, qe, taus[1])
+        names = list(self.w)
+        g = [x.clone() for x in torch.autograd.grad(loss, [self.w[n] for n in names])]
+        gn = clip_(g, 0.5)
+        self.opt.step(self.w, g)
+        return float(loss.detach()), gn
+
+
+# ---------------------------------------------------------------------------- Rainbow / C51
+def _noisy(w, p, x, training=True):
+    if training:
+        W = w[p + ".weight_mu"] + w[p + ".weight_sigma"] * w[p + ".weight_epsilon"]
+        b = w[p + ".bias_mu"] + w[p + ".bias_sigma"] * w[p + ".bias_epsilon"]
+    else:
+        W, b = w[p + ".weight_mu"], w[p + ".bias_mu"]
+    return F.linear(x, W, b)
+
+
+def rainbow_forward(w, s, atoms=51, action_size=25, obj_feat=8, log=False):
+    f = _features(w, *s, obj_feat=obj_feat)
+    v = _noisy(w, "output_layer_v", torch.relu(_noisy(w, "hidden_layer_v_2", torch.relu(_noisy(w, "hidden_layer_v", f)))))
+    a = _noisy(w, "output_layer_a", torch.relu(_noisy(w, "hidden_layer_a_2", torch.relu(_noisy(w, "hidden_layer_a", f)))))
+    v, a = v.view(-1, 1, atoms), a.view(-1, action_size, atoms)
+    q = v + a - a.mean(1, keepdim=True)
+    return F.log_softmax(q, dim=2) if log else F.softmax(q, dim=2)
+
+
+def c51_target(pns_a, returns, nonterminal, support, gamma_n, vmin=-1.0, vmax=1.0):
+    """agent.py:616-631 in numpy f32, accumulating lower masses then upper masses atom by atom."""
+    p = np.asarray(pns_a, np.float32)
+    B, A = p.shape
+    R = np.asarray(returns, np.float32).reshape(B)
+    nt = np.asarray(nonterminal, np.float32).reshape(B)
+    z = np.asarray(support, np.float32)
+    g = np.float32(gamma_n)
+    dz = np.float32((vmax - vmin) / (A - 1))
+    tz = np.clip(R[:, None] + (nt * g)[:, None] * z[None, :], np.float32(vmin), np.float32(vmax)).astype(np.float32)
+    b = ((tz - np.float32(vmin)) / dz).astype(np.float32)
+    l, u = np.floor(b).astype(np.int64), np.ceil(b).astype(np.int64)
+    l[(u > 0) & (l == u)] -= 1
+    u[(l < A - 1) & (l == u)] += 1
+    m = np.zeros((B, A), np.float32)
+    rows = np.arange(B)
+    lo = (p * (u.astype(np.float32) - b)).astype(np.float32)
+    hi = (p * (b - l.astype(np.float32))).astype(np.float32)
+    for j in range(A):
+        m[rows, l[:, j]] += lo[:, j]
+    for j in range(A):
+        m[rows, u[:, j]] += hi[:, j]
+    return m

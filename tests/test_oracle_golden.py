@@ -1,0 +1,133 @@
+"""CPU: pin the oracle against the reference's own outputs (tests/golden, captured by
+tools/capture_oracle.py from /root/reference). If these pass, the oracle is a faithful
+checker for the GPU tests at sizes the fixtures do not cover."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import env_oracle as eo
+from oracle import learn_ref as lr
+
+GOLD = eo.GOLDEN
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b) / np.maximum(1.0, np.abs(b)))) if a.size else 0.0
+
+
+@pytest.fixture(scope="module")
+def dyn():
+    return np.load(GOLD + "/env_dynamics.npz")
+
+
+def test_P_matrix_is_diag_inverse(dyn):
+    P = dyn["P"]
+    assert np.count_nonzero(P - np.diag(np.diag(P))) == 0
+    np.testing.assert_allclose(np.diag(P), [1 / 380, 1 / 400, 1 / 1430], rtol=1e-15)
+
+
+@pytest.mark.parametrize("case", ["cont", "disc", "cont_cores"])
+def test_oracle_dynamics(dyn, case):
+    p = eo.default_params(dyn["P"])
+    sb, sa, a = dyn[case + "/state_before"], dyn[case + "/state_after"], dyn[case + "/actions"]
+    worst = 0.0
+    for k in range(sb.shape[0]):
+        st, _ = eo.robot_act(p, sb[k], np.zeros(2), a[k], case != "disc", dyn["cores"] if "cores" in case else None)
+        worst = max(worst, _rel(st, sa[k]))
+    assert worst < 1e-12
+
+
+def test_oracle_current_field(dyn):
+    for (x, y), ref in zip(dyn["current_query"], dyn["current_value"]):
+        assert _rel(eo.current(dyn["cores"], float(dyn["core_r"]), x, y), ref) < 1e-13
+
+
+@pytest.mark.parametrize("name", list(eo.load_traces().keys()))
+def test_oracle_env_step_traces(name):
+    tr = eo.load_traces()[name]
+    n = int(tr["n_robots"])
+    p = eo.default_params()
+    for t in range(len(tr["reward"])):
+        i = eo.trace_step_inputs(tr, t)
+        out = eo.env_step(p, i["state_before"], i["goals"], i["deact"], i["coll"], i["reach"], i["obstacles"],
+                          i["n_obs"], i["O"], i["cores"], i["n_cores"], i["actions"], not name.startswith("disc"),
+                          i["noise"], i["ep_ts"])
+        for k in ("state_after", "reward", "self_obs", "obj_obs"):
+            assert _rel(out[k], tr[k][t][:n]) < 1e-12, (name, t, k)
+        ref_cnt = np.where(tr["obs_valid"][t][:n] == 1, tr["obj_cnt"][t][:n], -1)
+        assert np.array_equal(out["obj_cnt"], ref_cnt), (name, t)
+        for k in ("done", "info", "collision", "reach"):
+            assert np.array_equal(out[k], tr[k][t][:n]), (name, t, k)
+        act = i["deact"] == 0
+        assert np.array_equal(out["apply_colregs"][act], tr["apply_colregs"][t][:n][act]), (name, t)
+        assert out["ep_ts"] == tr["ep_ts"][t] + 1
+
+
+def test_traces_cover_every_branch():
+    """The fixture set exercises collisions, goals, timeouts, COLREGs, cores, discrete."""
+    tr = eo.load_traces()
+    allinfo = np.concatenate([t["info"].reshape(-1) for t in tr.values()])
+    for code in (0, 1, 2, 3, 4, 5):
+        assert (allinfo == code).any(), code
+    assert sum(int(t["apply_colregs"].sum()) for t in tr.values()) > 20
+    assert any(int(t["n_cores"]) > 0 for t in tr.values())
+
+
+@pytest.mark.parametrize("tag", ["b64", "b1024"])
+def test_c51_oracles_bit_exact(tag):
+    z = np.load(GOLD + "/learn_rainbow.npz")
+    args = (z[tag + "/pns_a"], z[tag + "/returns"], z[tag + "/nonterminal"], z[tag + "/support"])
+    np.testing.assert_array_equal(eo.c51_project(*args), z[tag + "/m"])
+    np.testing.assert_array_equal(lr.c51_target(*args, gamma_n=0.99 ** 3), z[tag + "/m"])
+
+
+def _batch(z, p):
+    t = lambda k: torch.tensor(z[p + k], dtype=torch.float32)  # noqa: E731
+    s = (t("s_self"), t("s_obj"), t("s_mask"))
+    ns = (t("ns_self"), t("ns_obj"), t("ns_mask"))
+    return s, t("a"), t("r").unsqueeze(-1), ns, t("d").unsqueeze(-1)
+
+
+def _sd(z, prefix):
+    return {k[len(prefix):]: z[k] for k in z.files if k.startswith(prefix)}
+
+
+def test_learn_ref_ac_iqn_vs_reference():
+    z = np.load(GOLD + "/learn_ac_iqn.npz")
+    ref = lr.ACIQNRef(_sd(z, "init/actor/"), _sd(z, "init/critic/"))
+    for step in range(3):
+        s, a, r, ns, d = _batch(z, f"step{step}/")
+        taus = [torch.tensor(x) for x in z[f"step{step}/taus"]]
+        cl, al, cgn, agn = ref.train(s, a, r, ns, d, taus)
+        np.testing.assert_allclose(cl, z[f"step{step}/critic_loss"], rtol=1e-5)
+        np.testing.assert_allclose(al, z[f"step{step}/actor_loss"], rtol=1e-5)
+        np.testing.assert_allclose([cgn, agn], z[f"step{step}/grad_norms"], rtol=1e-4)
+        if step in (0, 2):
+            for k, v in ref.actor.items():
+                np.testing.assert_allclose(v.detach().numpy(), z[f"after{step}/actor/{k}"], rtol=1e-4, atol=1e-6)
+            for k, v in ref.critic.items():
+                np.testing.assert_allclose(v.detach().numpy(), z[f"after{step}/critic/{k}"], rtol=1e-4, atol=1e-6)
+
+
+def test_learn_ref_ac_iqn_32_quantiles():
+    z = np.load(GOLD + "/learn_ac_iqn.npz")
+    ref = lr.ACIQNRef(_sd(z, "init/actor/"), _sd(z, "init/critic/"))
+    s, a, r, ns, d = _batch(z, "n32/")
+    cl, al, _, _ = ref.train(s, a, r, ns, d, [torch.tensor(x) for x in z["n32/taus"]])
+    np.testing.assert_allclose(cl, z["n32/critic_loss"], rtol=1e-5)
+    np.testing.assert_allclose(al, z["n32/actor_loss"], rtol=1e-5)
+
+
+def test_learn_ref_iqn_vs_reference():
+    z = np.load(GOLD + "/learn_iqn.npz")
+    ref = lr.IQNRef(_sd(z, "init/"))
+    for step in range(3):
+        s, a, r, ns, d = _batch(z, f"step{step}/")
+        taus = [torch.tensor(x) for x in z[f"step{step}/taus"]]
+        loss, gn = ref.train(s, a.long(), r, ns, d, taus)
+        np.testing.assert_allclose(loss, z[f"step{step}/loss"], rtol=1e-5)
+        np.testing.assert_allclose(gn, z[f"step{step}/grad_norms"][0], rtol=1e-4)
+        if step in (0, 2):
+            for k, v in ref.w.items():
+                np.testing.assert_allclose(v.detach().numpy(), z[f"after{step}/{k}"], rtol=1e-4, atol=1e-6)
