@@ -90,6 +90,7 @@ EXPORTS = [
     ("asvrl_replay_write_rows", C.c_int, [_VP, _VP, _I32, _VP, _VP]),
     ("asvrl_last_error", C.c_char_p, []),
     ("asvrl_abi_version", C.c_int, []),
+    ("asvrl_struct_sizes", None, [C.c_void_p]),
 ]
 
 _lib = None

@@ -1,0 +1,210 @@
+"""Agent -- drop-in for rfarl.agent.Agent (agent.py:18-707) for the distributional agents.
+
+Same constructor (keyword names and defaults), fields (agent_type, GAMMA, BATCH_SIZE,
+training, memory, policy_local/policy_target), act_* / train / soft_update /
+save_latest_model / load_model surfaces and return types. Differences:
+  * tensors live on the GPU: `device="cpu"` (the reference default) selects the current
+    HIP device -- the kernels have no CPU implementation and no CPU fallback;
+  * train_* run the fused gfx950 quantile-Huber / C51 kernels (learner.py);
+  * load_model rebuilds the optimizers for the loaded networks (the reference keeps
+    optimizing the replaced ones, agent.py:684-698 vs :75-76,98);
+  * DQN / DDPG / SAC (non-distributional baselines) are out of scope and raise.
+"""
+import copy
+import random
+
+import numpy as np
+import torch
+
+from . import _abi
+from .learner import FlatGrads, ac_iqn_update, iqn_update, rainbow_update
+from .policy.AC_IQN_model import AC_IQN_Policy
+from .policy.IQN_model import IQN_Policy
+from .policy.Rainbow_model import Rainbow_Policy
+from .policy.replay_memory_rainbow import ReplayMemory
+from .utils.replay_buffer import ReplayBuffer
+
+DISTRIBUTIONAL = ("AC-IQN", "IQN", "Rainbow")
+
+
+def resolve_device(device):
+    """The reference passes device strings like "cpu" (train_RL_agents.py -D); the hot path
+    needs the GPU, so "cpu"/None map to the current HIP device. No device -> error."""
+    _abi.lib()
+    if not torch.cuda.is_available():
+        raise _abi.AsvrlError("the rfarl hot path runs on an MI355X (HIP) device; none is visible")
+    if device is None or str(device) == "cpu":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device(device)
+
+
+class Agent:
+    def __init__(self, self_dimension=7, object_dimension=5, max_object_num=5, self_feature_dimension=56,
+                 object_feature_dimension=40, concat_feature_dimension=256, hidden_dimension=128,
+                 value_ranges_of_action=[[-1.0, 1.0], [-1.0, 1.0]], action_size=25, multi_steps=3, BATCH_SIZE=64,
+                 BUFFER_SIZE=1_000_000, LR=1e-4, TAU=1.0, GAMMA=0.99, device="cpu", seed=0, training=True,
+                 agent_type=None):
+        self.device = resolve_device(device)
+        self.LR = LR
+        self.TAU = TAU
+        self.GAMMA = GAMMA
+        self.BUFFER_SIZE = BUFFER_SIZE
+        self.BATCH_SIZE = BATCH_SIZE
+        self.training = training
+        self.value_ranges_of_action = copy.deepcopy(value_ranges_of_action)
+        self.action_size = action_size
+        self.agent_type = agent_type
+        self.num_tau = 8  # training quantiles N = N' (AC_IQN_model.py:462, IQN_model.py:74)
+        self.tau_override = None  # optional list of pre-drawn taus for the next train() (tests)
+        self._net_args = (self_dimension, object_dimension, max_object_num, self_feature_dimension,
+                          object_feature_dimension, concat_feature_dimension, hidden_dimension)
+        if agent_type not in DISTRIBUTIONAL:
+            if agent_type in ("DQN", "DDPG", "SAC"):
+                raise NotImplementedError(f"{agent_type} is a non-distributional baseline, outside this "
+                                          "framework's hot path (SURVEY.md section 2, row 14)")
+            raise RuntimeError("Agent type not implemented!")
+        if training:
+            self.policy_local = self._make_policy(seed, value_ranges_of_action, action_size)
+            self.policy_target = self._make_policy(seed, value_ranges_of_action, action_size)
+            self._make_optimizers()
+            if agent_type == "Rainbow":
+                self.atoms = 51
+                self.Vmin = -1.0
+                self.Vmax = 1.0
+                self.support = torch.linspace(self.Vmin, self.Vmax, self.atoms).to(self.device)
+                self.delta_z = (self.Vmax - self.Vmin) / (self.atoms - 1)
+                self.n = multi_steps
+                self.memory = ReplayMemory(self.device, BUFFER_SIZE)
+            else:
+                self.memory = ReplayBuffer(BUFFER_SIZE, BATCH_SIZE, object_dimension, max_object_num,
+                                           device=self.device)
+
+    # ------------------------------------------------------------------ construction
+    def _make_policy(self, seed, value_ranges_of_action, action_size):
+        a = self._net_args
+        if self.agent_type == "AC-IQN":
+            return AC_IQN_Policy(*a, value_ranges_of_action, self.device, seed)
+        if self.agent_type == "IQN":
+            return IQN_Policy(*a, action_size, self.device, seed).to(self.device)
+        return Rainbow_Policy(*a, action_size, 51, self.device, seed).to(self.device)
+
+    def _make_optimizers(self):
+        if self.agent_type == "AC-IQN":
+            self.critic_grads = FlatGrads(self.policy_local.critic.parameters())
+            self.actor_grads = FlatGrads(self.policy_local.actor.parameters())
+            self.actor_optimizer = torch.optim.Adam(self.policy_local.actor.parameters(), lr=self.LR)
+            self.critic_optimizer = torch.optim.Adam(self.policy_local.critic.parameters(), lr=self.LR)
+        else:
+            self.grads = FlatGrads(self.policy_local.parameters())
+            self.optimizer = torch.optim.Adam(self.policy_local.parameters(), lr=self.LR)
+
+    # ------------------------------------------------------------------ acting (agent.py:207-324)
+    def state_to_tensor(self, states):
+        self_state_batch, object_batch, object_batch_mask = states
+        self_t = torch.tensor(self_state_batch).float().to(self.device)
+        if len(object_batch) == 0:
+            return self_t, None, None
+        return (self_t, torch.tensor(object_batch).float().to(self.device),
+                torch.tensor(object_batch_mask).float().to(self.device))
+
+    def _batch1(self, state):
+        return self.state_to_tensor(self.memory.state_batch([state]))
+
+    def act_ac_iqn(self, state, eps=0.0, cvar=1.0, use_eval=True):
+        if random.random() > eps:
+            s = self._batch1(state)
+            self.policy_local.actor.eval() if use_eval else self.policy_local.actor.train()
+            with torch.no_grad():
+                action = self.policy_local.actor(s).cpu().data.numpy()[0].tolist()
+            self.policy_local.actor.train()
+        else:
+            action = [np.random.uniform(low=lo, high=hi) for lo, hi in self.value_ranges_of_action]
+        return action
+
+    def act_iqn(self, state, eps=0.0, cvar=1.0, use_eval=True, taus=None):
+        s = self._batch1(state)
+        self.policy_local.eval() if use_eval else self.policy_local.train()
+        with torch.no_grad():
+            quantiles, taus = self.policy_local(s, self.policy_local.K, cvar, taus=taus)
+            action_values = quantiles.mean(dim=1)
+        self.policy_local.train()
+        if random.random() > eps:
+            action = np.argmax(action_values.cpu().data.numpy())
+        else:
+            action = random.choice(np.arange(self.action_size))
+        return action, quantiles.cpu().data.numpy(), taus.cpu().data.numpy()
+
+    def act_rainbow(self, state, eps=0.0, use_eval=True):
+        s = self._batch1(state)
+        self.policy_local.eval() if use_eval else self.policy_local.train()
+        with torch.no_grad():
+            p = self.policy_local(s)
+        self.policy_local.train()
+        if random.random() > eps:
+            return (p * self.support).sum(2).argmax(1).item()
+        return random.choice(np.arange(self.action_size))
+
+    def act_dqn(self, *a, **k):
+        raise NotImplementedError("DQN is outside this framework's hot path")
+
+    act_ddpg = act_sac = act_dqn
+
+    # ------------------------------------------------------------------ learning (agent.py:370-641)
+    def train(self):
+        if self.agent_type == "AC-IQN":
+            return self.train_AC_IQN()
+        if self.agent_type == "IQN":
+            return self.train_IQN()
+        if self.agent_type == "Rainbow":
+            return self.train_Rainbow()
+        raise RuntimeError("Agent type not implemented!")
+
+    def _taus(self, k):
+        t, self.tau_override = self.tau_override, None
+        if t is None:
+            return (None,) * k
+        return tuple(torch.as_tensor(x, device=self.device, dtype=torch.float32) for x in t)
+
+    def train_AC_IQN(self):
+        s, a, r, ns, d = self.memory.sample()
+        cl, al, _, _ = ac_iqn_update(self.policy_local, self.policy_target, self.actor_optimizer,
+                                     self.critic_optimizer, self.critic_grads, self.actor_grads, s, a, r, ns, d,
+                                     gamma=self.GAMMA, num_tau=self.num_tau, taus=self._taus(3))
+        return cl.cpu().numpy(), al.cpu().numpy()
+
+    def train_IQN(self):
+        s, a, r, ns, d = self.memory.sample()
+        loss, _ = iqn_update(self.policy_local, self.policy_target, self.optimizer, self.grads, s,
+                             a[:, 0].to(torch.int64), r, ns, d, gamma=self.GAMMA, num_tau=self.num_tau,
+                             taus=self._taus(2))
+        return loss.cpu().numpy()
+
+    def train_Rainbow(self, reset_target_noise=True):
+        idxs, s, a, R, ns, nt, w = self.memory.sample(self.BATCH_SIZE)
+        loss, _ = rainbow_update(self.policy_local, self.policy_target, self.optimizer, self.grads, self.support, s, a,
+                                 R, ns, nt, w, gamma=self.GAMMA, n=self.n, vmin=self.Vmin, vmax=self.Vmax,
+                                 reset_target_noise=reset_target_noise)
+        loss = loss.cpu().numpy()
+        self.memory.update_priorities(idxs, loss)
+        return loss
+
+    def soft_update(self):
+        """theta_t <- TAU theta + (1 - TAU) theta_t (agent.py:643-679)."""
+        if self.agent_type == "AC-IQN":
+            pairs = list(zip(self.policy_target.actor.parameters(), self.policy_local.actor.parameters())) + \
+                list(zip(self.policy_target.critic.parameters(), self.policy_local.critic.parameters()))
+        else:
+            pairs = list(zip(self.policy_target.parameters(), self.policy_local.parameters()))
+        with torch.no_grad():
+            for t, l in pairs:
+                t.data.copy_(self.TAU * l.data + (1.0 - self.TAU) * t.data)
+
+    def save_latest_model(self, directory):
+        self.policy_local.save(directory)
+
+    def load_model(self, path, device="cpu"):
+        dev = resolve_device(device)
+        cls = {"AC-IQN": AC_IQN_Policy, "IQN": IQN_Policy, "Rainbow": Rainbow_Policy}[self.agent_type]
+        self.policy_local = cls.load(path, dev)
+        if self.training:
+            self._make_optimizers()

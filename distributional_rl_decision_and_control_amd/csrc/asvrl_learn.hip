@@ -244,6 +244,13 @@ using namespace asvrl;
 
 extern "C" const char* asvrl_last_error(void) { return g_last_error.c_str(); }
 extern "C" int asvrl_abi_version(void) { return ASVRL_ABI_VERSION; }
+extern "C" void asvrl_struct_sizes(int64_t* out5) {
+  out5[0] = sizeof(AsvParams);
+  out5[1] = sizeof(AsvEnvState);
+  out5[2] = sizeof(AsvStepCtl);
+  out5[3] = sizeof(AsvStepOut);
+  out5[4] = sizeof(AsvResetCfg);
+}
 
 extern "C" int asvrl_quantile_huber(const float* qt, const float* qe, const float* tau, int32_t B, int32_t N,
                                     int32_t Np, float kappa, float grad_scale, float* row_loss, float* loss,

@@ -210,6 +210,9 @@ int asvrl_replay_write_rows(const float* rows, const int64_t* slots, int32_t n, 
 /* ---------------------------------------------------------------- misc */
 const char* asvrl_last_error(void);
 int asvrl_abi_version(void);
+/* sizeof(AsvParams, AsvEnvState, AsvStepCtl, AsvStepOut, AsvResetCfg) as compiled, for
+ * binding checks (host pointer to 5 int64). */
+void asvrl_struct_sizes(int64_t* out5);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,138 @@
+"""End-to-end parity of the drop-in MarineNavEnv3 against the reference's own traces.
+
+Unlike test_env_kernel_gpu (teacher-forced, one launch), these run the env exactly like a
+reference user: construct with the same seed, reset (host RandomState sampler), then feed
+the recorded actions step after step. Every perception-noise draw comes from the robots'
+own RandomStates, so observations, rewards, dones, infos and states must track the
+reference over the whole trace (f64 tolerance 1e-9 after up to 150 chained steps; masks
+and info strings exact).
+"""
+import numpy as np
+import pytest
+
+from oracle import env_oracle as eo
+
+pytestmark = pytest.mark.gpu
+
+# trace name -> (seed, num_robots, num_obs, min_start_goal_dis, width, num_cores, continuous)
+PLAIN = {
+    "cont_r5o4_s0": (0, 5, 4, 40.0, 55, 0, True),
+    "cont_r5o4_s1": (1, 5, 4, 40.0, 55, 0, True),
+    "disc_r5o4_s2": (2, 5, 4, 40.0, 55, 0, False),
+    "cont_r12o8_s6": (6, 12, 8, 40.0, 110, 0, True),
+    "cores_r5o4_s8": (8, 5, 4, 30.0, 55, 4, True),
+}
+EDITED = {  # traces whose capture edited the scene after reset (crowd / goal / timeout)
+    "crowd_r8o4_s3": (3, 8, 4, 30.0, 80, 0, True),
+    "crowd_r8o4_s5": (5, 8, 4, 30.0, 80, 0, True),
+    "goal_r5o4_s9": (9, 5, 4, 40.0, 55, 0, True),
+    "timeout_r5o4_s7": (7, 5, 4, 40.0, 55, 0, True),
+}
+INFO = {0: "normal", 1: "too long episode", 2: "collision", 3: "reach goal", 4: "deactivated after collision",
+        5: "deactivated after reaching goal"}
+
+
+def _env(cfg):
+    from distributional_rl_decision_and_control_amd.envs.marinenav.env import MarineNavEnv3
+    seed, R, O, msgd, width, cores, _ = cfg
+    env = MarineNavEnv3(seed=seed)
+    env.num_robots, env.num_cores, env.num_obs, env.min_start_goal_dis = R, cores, O, msgd
+    env.width = env.height = width
+    return env
+
+
+def _state(r):
+    return np.array([r.x, r.y, r.theta, *r.velocity_r, *r.velocity, r.left_thrust, r.right_thrust, r.left_pos,
+                     r.right_pos], dtype=np.float64)
+
+
+def _replay(env, tr, continuous, tol):
+    n = len(env.robots)
+    assert n == int(tr["n_robots"])
+    for t in range(len(tr["reward"])):
+        sb = tr["state_before"][t][:n]
+        for i, r in enumerate(env.robots):
+            np.testing.assert_allclose(_state(r), sb[i], rtol=tol, atol=tol, err_msg=f"t={t} robot {i} pre-state")
+        acts = []
+        for i, r in enumerate(env.robots):
+            if r.deactivated:
+                acts.append(None)
+            elif continuous:
+                acts.append([float(v) for v in tr["actions"][t][i]])
+            else:
+                acts.append(int(tr["actions"][t][i][0]))
+        env.episode_timesteps = int(tr["ep_ts"][t])
+        obs, rew, done, info = env.step(acts, continuous)
+        for i, r in enumerate(env.robots):
+            assert bool(done[i]) == bool(tr["done"][t][i]), (t, i)
+            assert info[i]["state"] == INFO[int(tr["info"][t][i])], (t, i)
+            assert r.collision == bool(tr["collision"][t][i]) and r.reach_goal == bool(tr["reach"][t][i]), (t, i)
+            np.testing.assert_allclose(rew[i], tr["reward"][t][i], rtol=tol, atol=tol)
+            s, o = obs[i]
+            if not tr["obs_valid"][t][i]:
+                assert s is None and o is None
+                continue
+            np.testing.assert_allclose(s, tr["self_obs"][t][i], rtol=tol, atol=tol)
+            assert len(o) == tr["obj_cnt"][t][i]
+            if len(o):
+                np.testing.assert_allclose(np.array(o), tr["obj_obs"][t][i][:len(o)], rtol=tol, atol=tol)
+        for i, r in enumerate(env.robots):  # trainer.py:168-170
+            if not r.deactivated and (r.collision or r.reach_goal):
+                r.deactivated = True
+
+
+@pytest.mark.parametrize("name", list(PLAIN))
+def test_dropin_env_matches_reference_trace(name):
+    tr = eo.load_traces()[name]
+    env = _env(PLAIN[name])
+    env.reset()
+    _replay(env, tr, PLAIN[name][6], 1e-9)
+
+
+@pytest.mark.parametrize("name", list(EDITED))
+def test_dropin_env_matches_edited_trace(name):
+    from distributional_rl_decision_and_control_amd.envs.marinenav.env import Obstacle
+    tr = eo.load_traces()[name]
+    env = _env(EDITED[name])
+    env.reset()
+    n = int(tr["n_robots"])
+    sb = tr["state_before"][0][:n]
+    for i, r in enumerate(env.robots):  # the scene edit of tools/capture_oracle.py, from the fixture
+        r.x, r.y, r.theta = sb[i, 0], sb[i, 1], sb[i, 2]
+        r.velocity_r, r.velocity = sb[i, 3:6].copy(), sb[i, 6:9].copy()
+        r.left_thrust, r.right_thrust = sb[i, 9], sb[i, 10]
+    env.obstacles = [Obstacle(*o) for o in tr["obstacles"][:int(tr["n_obs"])]]
+    _replay(env, tr, True, 1e-9)
+
+
+def test_reset_observation_matches_reference():
+    """reset() = host sampler + device observation, vs env_reset.npz (env.py:72-164)."""
+    from distributional_rl_decision_and_control_amd.envs.marinenav.env import MarineNavEnv3
+    import contextlib
+    import io
+    z = np.load(eo.GOLDEN + "/env_reset.npz")
+    schedule = {"timesteps": [0, 1000000, 2000000, 3000000, 4000000, 5000000], "num_robots": [3, 4, 5, 5, 5, 5],
+                "num_cores": [0, 0, 0, 0, 0, 0], "num_obstacles": [0, 0, 0, 2, 3, 4],
+                "min_start_goal_dis": [30.0, 35.0, 40.0, 40.0, 40.0, 40.0]}
+    for c in range(int(z["n_cases"])):
+        p = f"c{c}/"
+        kind, seed = str(z[p + "kind"]), int(z[p + "seed"])
+        if kind == "sched":
+            env = MarineNavEnv3(seed=seed, schedule=schedule)
+            env.total_timesteps = int(z[p + "total_timesteps"])
+        elif kind == "cores":
+            env = MarineNavEnv3(seed=seed)
+            env.num_robots, env.num_cores, env.num_obs, env.min_start_goal_dis = 4, 4, 3, 30.0
+        else:
+            env = MarineNavEnv3(seed=seed)
+            env.num_robots, env.num_cores, env.num_obs, env.min_start_goal_dis = 17, 0, 4, 40.0
+            env.width = env.height = 110
+        with contextlib.redirect_stdout(io.StringIO()):
+            obs, _, _ = env.reset()
+        n = int(z[p + "n_robots"])
+        for i in range(n):
+            np.testing.assert_allclose(obs[i][0], z[p + "self_obs"][i], rtol=1e-12, atol=1e-12)
+            k = int(z[p + "obj_cnt"][i])
+            assert len(obs[i][1]) == k
+            if k:
+                np.testing.assert_allclose(np.array(obs[i][1]), z[p + "obj_obs"][i][:k], rtol=1e-12, atol=1e-12)
