@@ -75,6 +75,15 @@ class AsvResetCfg(C.Structure):
                 ("v_hi", C.c_double), ("v_rel_max", C.c_double), ("p_rel", C.c_double)]
 
 
+class AsvCriticWeights(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("wc_frag", "w1_frag", "w2_frag", "w2t_frag", "w1t_frag", "bc", "b1", "b2",
+                                          "wo", "bo")]
+
+
+class AsvCriticActs(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("cos", "h0", "dzc", "h1g", "dz1", "h2", "dz2", "dq")]
+
+
 # (name, restype, argtypes) of every exported entry point, mirroring include/asvrl.h
 _VP, _I32, _I64, _U64, _F, _D = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_float, C.c_double
 EXPORTS = [
@@ -85,6 +94,10 @@ EXPORTS = [
     ("asvrl_current_field", C.c_int, [_VP, _I32, _D, _VP, _I32, _VP, _VP]),
     ("asvrl_quantile_huber", C.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, _F, _F, _VP, _VP, _VP, _VP]),
     ("asvrl_c51_project", C.c_int, [_VP, _VP, _VP, _VP, _I32, _I32, _F, _F, _F, _F, _VP, _VP]),
+    ("asvrl_critic_forward", C.c_int, [C.POINTER(AsvCriticWeights), _VP, _VP, _VP, _I32, _I32, _VP, _VP]),
+    ("asvrl_critic_train", C.c_int, [C.POINTER(AsvCriticWeights), _VP, _VP, _VP, _VP, _I32, _I32, _I32, _F, _VP, _VP,
+                                     _VP, _VP, C.POINTER(AsvCriticActs), _VP]),
+    ("asvrl_critic_actor_grad", C.c_int, [C.POINTER(AsvCriticWeights), _VP, _VP, _VP, _I32, _I32, _F, _VP, _VP, _VP]),
     ("asvrl_replay_push", C.c_int, [_VP, _VP, _VP, _VP, _I32, _VP, _VP, _I32, _VP, _I64, _VP, _VP, _VP]),
     ("asvrl_replay_sample", C.c_int, [_VP, _I64, _VP, _VP, _I32, _U64, _U64, _VP, _VP, _VP, _VP]),
     ("asvrl_replay_write_rows", C.c_int, [_VP, _VP, _I32, _VP, _VP]),

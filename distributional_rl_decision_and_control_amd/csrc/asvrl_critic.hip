@@ -1,0 +1,368 @@
+// asvrl_critic.hip -- the IQN critic trunk of AC-IQN (AC_IQN_model.py:410-480) fused on MFMA.
+//
+// Rows are (sample b, quantile tau) pairs, R = B*N. Per row:
+//   c   = relu(Wc cos(tau*pi*k) + bc)            k = 0..63          (cos_embedding, 64 -> 256)
+//   h0  = F[b] * c                                F = state features  (observation_processor)
+//   h1  = relu(W1 h0 + b1)                                            (hidden_layer, 256 -> 128)
+//   h1g = h1 * G[b]                               G = action features (action_encoder)
+//   h2  = relu(W2 h1g + b2)                                           (hidden_layer_2, 128 -> 128)
+//   q   = wo . h2 + bo                                                (output_layer, 128 -> 1)
+//
+// Mapping (one wave = 32 rows, v_mfma_f32_32x32x16_bf16): features are the MFMA M dimension and
+// rows the N dimension, so a layer's f32 accumulator (lane = row, registers = features) is fed
+// to the next layer as its B operand straight from registers -- registers 8s..8s+7 of a 32-row
+// block hold features 16s + 8(j>>2) + 4h + (j&3) (h = lane>>5). The weights (A operand) are
+// pre-packed on the host into per-lane fragments in exactly that k order (critic_pack.py), one
+// 16-B load per lane per MFMA. Nothing between layers touches LDS or HBM.
+//
+// Modes:
+//   FWD    q only (target critic, agent.py:399)
+//   TRAIN  forward + quantile-Huber loss vs the target quantiles (agent.py:406-412) + backward:
+//          dF (B,256), dG (B,128) reduced over each sample's taus in registers (xor shuffles),
+//          and bf16 row-major activations for the weight gradients (dW = dZ^T X, a split-K
+//          GEMM on the host side)
+//   ACTOR  forward + backward of -mean(q) to the action features only (agent.py:420-425)
+#include "asvrl_common.h"
+
+namespace asvrl {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kC = 256, kH = 128, kNcos = 64;
+constexpr int kWaves = 4;
+enum { MODE_FWD = 0, MODE_TRAIN = 1, MODE_ACTOR = 2 };
+
+struct CriticArgs {
+  AsvCriticWeights w;
+  const float* F;
+  const float* G;
+  const float* taus;
+  const float* qt;  // (B, Np) target quantiles (TRAIN)
+  int B, N, Np;
+  float kappa, gscale, dq_const;
+  float* q;         // (R) optional
+  float* row_loss;  // (R) TRAIN
+  float* dF;        // (B, 256)
+  float* dG;        // (B, 128)
+  AsvCriticActs acts;
+};
+
+__device__ __forceinline__ __bf16* bp(void* p) { return reinterpret_cast<__bf16*>(p); }
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// feature index held by accumulator register g of 32-feature block mb in lane half h
+__device__ __forceinline__ int feat(int mb, int g, int h) { return mb * 32 + (g & 3) + 8 * (g >> 2) + 4 * h; }
+
+__device__ __forceinline__ float seg_sum(float v, int n) {  // sum over aligned groups of n lanes
+  for (int off = 1; off < n; off <<= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// bf16x4 store of the 4 consecutive features (j&3 = 0..3) of register group (s, q)
+__device__ __forceinline__ void store4(__bf16* base, const float* v) {
+  bf16x4 x;
+  x[0] = (__bf16)v[0];
+  x[1] = (__bf16)v[1];
+  x[2] = (__bf16)v[2];
+  x[3] = (__bf16)v[3];
+  *reinterpret_cast<bf16x4*>(base) = x;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kWaves * 64) void critic_kernel(CriticArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int tile = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const int R = a.B * a.N;
+  if (tile * 32 >= R) return;
+  const int r = lane & 31, h = lane >> 5;
+  const int grow = tile * 32 + r;
+  const int b = grow / a.N;
+  const float tau = a.taus[grow];
+  const float* Fb = a.F + static_cast<size_t>(b) * kC;
+  const float* Gb = a.G + static_cast<size_t>(b) * kH;
+  const bf16x8* WC = reinterpret_cast<const bf16x8*>(a.w.wc_frag);
+  const bf16x8* W1 = reinterpret_cast<const bf16x8*>(a.w.w1_frag);
+  const bf16x8* W2 = reinterpret_cast<const bf16x8*>(a.w.w2_frag);
+
+  // ---------------- layer 0: c = relu(Wc cos + bc), h0 = F[b] * c
+  f32x16 acc0[8];
+#pragma unroll
+  for (int mb = 0; mb < 8; ++mb) acc0[mb] = f32x16{};
+#pragma unroll
+  for (int ks = 0; ks < kNcos / 16; ++ks) {
+    bf16x8 bx;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = ks * 16 + 8 * h + j;
+      const float pis = static_cast<float>(3.141592653589793 * k);  // torch.FloatTensor([pi*i])
+      bx[j] = (__bf16)cosf(tau * pis);
+    }
+    if (MODE == MODE_TRAIN) *reinterpret_cast<bf16x8*>(bp(a.acts.cos) + static_cast<size_t>(grow) * kNcos + ks * 16 + 8 * h) = bx;
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb) acc0[mb] = mfma(WC[(mb * 4 + ks) * 64 + lane], bx, acc0[mb]);
+  }
+  bf16x8 cpk[16], hpk[16];
+#pragma unroll
+  for (int mb = 0; mb < 8; ++mb) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float hv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = feat(mb, 8 * s + j, h);
+        float x = acc0[mb][8 * s + j] + a.w.bc[m];
+        x = x > 0.f ? x : 0.f;
+        cpk[mb * 2 + s][j] = (__bf16)x;
+        hv[j] = Fb[m] * x;
+        hpk[mb * 2 + s][j] = (__bf16)hv[j];
+      }
+      if (MODE == MODE_TRAIN) {
+        __bf16* row = bp(a.acts.h0) + static_cast<size_t>(grow) * kC + mb * 32 + 16 * s + 4 * h;
+        store4(row, hv);
+        store4(row + 8, hv + 4);
+      }
+    }
+  }
+
+  // ---------------- layer 1: h1 = relu(W1 h0 + b1), h1g = h1 * G[b]
+  f32x16 acc1[4];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) acc1[mb] = f32x16{};
+#pragma unroll
+  for (int ks = 0; ks < kC / 16; ++ks) {
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) acc1[mb] = mfma(W1[(mb * 16 + ks) * 64 + lane], hpk[ks], acc1[mb]);
+  }
+  bf16x8 h1pk[8], gpk[8];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float gv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = feat(mb, 8 * s + j, h);
+        float x = acc1[mb][8 * s + j] + a.w.b1[m];
+        x = x > 0.f ? x : 0.f;
+        h1pk[mb * 2 + s][j] = (__bf16)x;
+        gv[j] = x * Gb[m];
+        gpk[mb * 2 + s][j] = (__bf16)gv[j];
+      }
+      if (MODE == MODE_TRAIN) {
+        __bf16* row = bp(a.acts.h1g) + static_cast<size_t>(grow) * kH + mb * 32 + 16 * s + 4 * h;
+        store4(row, gv);
+        store4(row + 8, gv + 4);
+      }
+    }
+  }
+
+  // ---------------- layer 2: h2 = relu(W2 h1g + b2), q = wo . h2 + bo
+  f32x16 acc2[4];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) acc2[mb] = f32x16{};
+#pragma unroll
+  for (int ks = 0; ks < kH / 16; ++ks) {
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) acc2[mb] = mfma(W2[(mb * 8 + ks) * 64 + lane], gpk[ks], acc2[mb]);
+  }
+  float part = 0.f;
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int m = feat(mb, g, h);
+      float x = acc2[mb][g] + a.w.b2[m];
+      acc2[mb][g] = x;  // keep z2 for the relu mask
+      part += a.w.wo[m] * (x > 0.f ? x : 0.f);
+    }
+  }
+  const float q = part + __shfl_xor(part, 32, 64) + a.w.bo[0];
+  if (a.q != nullptr && h == 0) a.q[grow] = q;
+  if (MODE == MODE_FWD) return;
+
+  // ---------------- dL/dq
+  float dq;
+  if (MODE == MODE_TRAIN) {
+    const float* qt = a.qt + static_cast<size_t>(b) * a.Np;
+    float wl = 0.f, wg = 0.f;
+    for (int j = 0; j < a.Np; ++j) {
+      const float d = qt[j] - q;  // td_error (agent.py:406)
+      const float ad = fabsf(d);
+      const bool quad = ad <= a.kappa;
+      const float hub = quad ? 0.5f * (d * d) : a.kappa * (ad - 0.5f * a.kappa);
+      const float w = fabsf(tau - (d < 0.f ? 1.f : 0.f));
+      wl += w * hub / a.kappa;
+      wg += w * (quad ? d : (d > 0.f ? a.kappa : -a.kappa)) / a.kappa;
+    }
+    dq = -wg * a.gscale;
+    if (h == 0) {
+      a.row_loss[grow] = wl;
+      a.acts.dq[grow] = dq;
+    }
+  } else {
+    dq = a.dq_const;
+  }
+
+  // ---------------- dz2 = dq * wo * 1[z2 > 0]
+  bf16x8 dz2pk[8];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float hv[8], dv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = feat(mb, 8 * s + j, h);
+        const float z = acc2[mb][8 * s + j];
+        hv[j] = z > 0.f ? z : 0.f;
+        dv[j] = z > 0.f ? dq * a.w.wo[m] : 0.f;
+        dz2pk[mb * 2 + s][j] = (__bf16)dv[j];
+      }
+      if (MODE == MODE_TRAIN) {
+        const size_t o = static_cast<size_t>(grow) * kH + mb * 32 + 16 * s + 4 * h;
+        store4(bp(a.acts.h2) + o, hv);
+        store4(bp(a.acts.h2) + o + 8, hv + 4);
+        store4(bp(a.acts.dz2) + o, dv);
+        store4(bp(a.acts.dz2) + o + 8, dv + 4);
+      }
+    }
+  }
+
+  // ---------------- layer 3: dh1g = W2^T dz2; dG[b] = sum_taus dh1g * h1; dz1 = dh1g * G * 1[h1 > 0]
+  const bf16x8* W2T = reinterpret_cast<const bf16x8*>(a.w.w2t_frag);
+  f32x16 acc3[4];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) acc3[mb] = f32x16{};
+#pragma unroll
+  for (int ks = 0; ks < kH / 16; ++ks) {
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) acc3[mb] = mfma(W2T[(mb * 8 + ks) * 64 + lane], dz2pk[ks], acc3[mb]);
+  }
+  const bool writer = (r % a.N) == 0;
+  bf16x8 dz1pk[8];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float dv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = feat(mb, 8 * s + j, h);
+        const float d = acc3[mb][8 * s + j];
+        const float h1 = static_cast<float>(h1pk[mb * 2 + s][j]);
+        const float gsum = seg_sum(d * h1, a.N);
+        if (writer) a.dG[static_cast<size_t>(b) * kH + m] = gsum;
+        dv[j] = h1 > 0.f ? d * Gb[m] : 0.f;
+        dz1pk[mb * 2 + s][j] = (__bf16)dv[j];
+      }
+      if (MODE == MODE_TRAIN) {
+        __bf16* row = bp(a.acts.dz1) + static_cast<size_t>(grow) * kH + mb * 32 + 16 * s + 4 * h;
+        store4(row, dv);
+        store4(row + 8, dv + 4);
+      }
+    }
+  }
+  if (MODE == MODE_ACTOR) return;
+
+  // ---------------- layer 4: dh0 = W1^T dz1; dF[b] = sum_taus dh0 * c; dzc = dh0 * F * 1[c > 0]
+  const bf16x8* W1T = reinterpret_cast<const bf16x8*>(a.w.w1t_frag);
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {  // 2 x 4 output blocks keeps 64 accumulator registers live
+    f32x16 acc4[4];
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) acc4[q4] = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < kH / 16; ++ks) {
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4)
+        acc4[q4] = mfma(W1T[((half * 4 + q4) * 8 + ks) * 64 + lane], dz1pk[ks], acc4[q4]);
+    }
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      const int mb = half * 4 + q4;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float dv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int m = feat(mb, 8 * s + j, h);
+          const float d = acc4[q4][8 * s + j];
+          const float c = static_cast<float>(cpk[mb * 2 + s][j]);
+          const float fsum = seg_sum(d * c, a.N);
+          if (writer) a.dF[static_cast<size_t>(b) * kC + m] = fsum;
+          dv[j] = c > 0.f ? d * Fb[m] : 0.f;
+        }
+        __bf16* row = bp(a.acts.dzc) + static_cast<size_t>(grow) * kC + mb * 32 + 16 * s + 4 * h;
+        store4(row, dv);
+        store4(row + 8, dv + 4);
+      }
+    }
+  }
+}
+
+int launch(int mode, const CriticArgs& a, void* stream) {
+  const int R = a.B * a.N;
+  const int tiles = (R + 31) / 32;
+  const dim3 grid((tiles + kWaves - 1) / kWaves), block(kWaves * 64);
+  hipStream_t st = as_stream(stream);
+  if (mode == MODE_FWD) hipLaunchKernelGGL(critic_kernel<MODE_FWD>, grid, block, 0, st, a);
+  else if (mode == MODE_TRAIN) hipLaunchKernelGGL(critic_kernel<MODE_TRAIN>, grid, block, 0, st, a);
+  else hipLaunchKernelGGL(critic_kernel<MODE_ACTOR>, grid, block, 0, st, a);
+  return check_launch("asvrl_critic");
+}
+
+int validate(const AsvCriticWeights* w, const float* F, const float* G, const float* taus, int B, int N) {
+  ASVRL_REQUIRE(w && F && G && taus, "asvrl_critic: null argument");
+  ASVRL_REQUIRE(w->wc_frag && w->w1_frag && w->w2_frag && w->bc && w->b1 && w->b2 && w->wo && w->bo,
+                "asvrl_critic: null weight");
+  ASVRL_REQUIRE(N >= 1 && N <= 32 && (32 % N) == 0, "asvrl_critic: N must divide 32");
+  ASVRL_REQUIRE(B >= 0 && (static_cast<int64_t>(B) * N) % 32 == 0, "asvrl_critic: B*N must be a multiple of 32");
+  return 0;
+}
+
+}  // namespace
+}  // namespace asvrl
+
+using namespace asvrl;
+
+extern "C" int asvrl_critic_forward(const AsvCriticWeights* w, const float* F, const float* G, const float* taus,
+                                    int32_t B, int32_t N, float* q, void* stream) {
+  if (int rc = validate(w, F, G, taus, B, N)) return rc;
+  ASVRL_REQUIRE(q != nullptr, "asvrl_critic_forward: null q");
+  if (B == 0) return 0;
+  CriticArgs a{};
+  a.w = *w; a.F = F; a.G = G; a.taus = taus; a.B = B; a.N = N; a.q = q;
+  return launch(MODE_FWD, a, stream);
+}
+
+extern "C" int asvrl_critic_train(const AsvCriticWeights* w, const float* F, const float* G, const float* taus,
+                                  const float* q_targets, int32_t B, int32_t N, int32_t Np, float kappa, float* q,
+                                  float* row_loss, float* dF, float* dG, const AsvCriticActs* acts, void* stream) {
+  if (int rc = validate(w, F, G, taus, B, N)) return rc;
+  ASVRL_REQUIRE(q_targets && row_loss && dF && dG && acts && w->w2t_frag && w->w1t_frag, "asvrl_critic_train: null argument");
+  ASVRL_REQUIRE(acts->cos && acts->h0 && acts->dzc && acts->h1g && acts->dz1 && acts->h2 && acts->dz2 && acts->dq,
+                "asvrl_critic_train: null activation buffer");
+  ASVRL_REQUIRE(Np >= 1 && kappa > 0.f, "asvrl_critic_train: bad Np/kappa");
+  if (B == 0) return 0;
+  CriticArgs a{};
+  a.w = *w; a.F = F; a.G = G; a.taus = taus; a.qt = q_targets; a.B = B; a.N = N; a.Np = Np; a.kappa = kappa;
+  a.gscale = 1.f / (static_cast<float>(B) * static_cast<float>(Np));
+  a.q = q; a.row_loss = row_loss; a.dF = dF; a.dG = dG; a.acts = *acts;
+  return launch(MODE_TRAIN, a, stream);
+}
+
+extern "C" int asvrl_critic_actor_grad(const AsvCriticWeights* w, const float* F, const float* G, const float* taus,
+                                       int32_t B, int32_t N, float dq, float* q, float* dG, void* stream) {
+  if (int rc = validate(w, F, G, taus, B, N)) return rc;
+  ASVRL_REQUIRE(dG && w->w2t_frag, "asvrl_critic_actor_grad: null argument");
+  if (B == 0) return 0;
+  CriticArgs a{};
+  a.w = *w; a.F = F; a.G = G; a.taus = taus; a.B = B; a.N = N; a.dq_const = dq; a.q = q; a.dG = dG;
+  return launch(MODE_ACTOR, a, stream);
+}

@@ -1,0 +1,234 @@
+"""Fused MFMA critic (csrc/asvrl_critic.hip) behind the AC-IQN update.
+
+CriticPack turns a Critic's f32 weights into the bf16 A-operand fragments the kernel loads
+(one 16-byte load per lane per v_mfma_f32_32x32x16_bf16), in the k order of the kernel's
+register chaining: a layer fed from the previous accumulator sees its inputs in the order
+16s + 8(j>>2) + 4h + (j&3) within each 32-feature block. Refreshing is one gather + cast per
+matrix into preallocated buffers, so it can live inside a captured HIP graph.
+
+ac_iqn_update_fused is learner.ac_iqn_update (agent.py:386-432) with the critic trunk --
+cos embedding, both hidden layers, the output layer, the quantile-Huber loss and the whole
+backward -- in two kernel launches per critic pass, the state/action encoders and the actor
+on torch, and the trunk's weight gradients as split-K bf16 GEMMs over the saved activations.
+"""
+import ctypes as C
+
+import torch
+
+from . import _abi
+from .learner import _clip, _null
+from .policy.AC_IQN_model import encode_observation
+
+_IDX = {}
+
+
+def frag_index(M, K, chained, device):
+    """Flat indices into a row-major (M, K) matrix, ordered [mb][ks][lane][j]."""
+    key = (M, K, chained, str(device))
+    if key not in _IDX:
+        mb = torch.arange(M // 32).view(-1, 1, 1, 1)
+        ks = torch.arange(K // 16).view(1, -1, 1, 1)
+        lane = torch.arange(64).view(1, 1, -1, 1)
+        j = torch.arange(8).view(1, 1, 1, -1)
+        r, h = lane & 31, lane >> 5
+        row = mb * 32 + r
+        col = ks * 16 + ((8 * (j >> 2) + 4 * h + (j & 3)) if chained else (8 * h + j))
+        _IDX[key] = (row * K + col).reshape(-1).to(device)
+    return _IDX[key]
+
+
+class CriticPack:
+    """bf16 fragment images of one Critic's trunk weights + pointers (AsvCriticWeights)."""
+
+    def __init__(self, critic):
+        dev = critic.cos_embedding.weight.device
+        self.critic = critic
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        self.wc = torch.empty(256 * 64, **bf)
+        self.w1 = torch.empty(128 * 256, **bf)
+        self.w2 = torch.empty(128 * 128, **bf)
+        self.w2t = torch.empty(128 * 128, **bf)
+        self.w1t = torch.empty(256 * 128, **bf)
+        self._w2t_f = torch.empty(128, 128, device=dev)
+        self._w1t_f = torch.empty(256, 128, device=dev)
+        self.idx = dict(wc=frag_index(256, 64, False, dev), w1=frag_index(128, 256, True, dev),
+                        w2=frag_index(128, 128, True, dev), w2t=frag_index(128, 128, True, dev),
+                        w1t=frag_index(256, 128, True, dev))
+        self.refresh()
+        s = _abi.AsvCriticWeights()
+        s.wc_frag, s.w1_frag, s.w2_frag = self.wc.data_ptr(), self.w1.data_ptr(), self.w2.data_ptr()
+        s.w2t_frag, s.w1t_frag = self.w2t.data_ptr(), self.w1t.data_ptr()
+        s.bc, s.b1 = critic.cos_embedding.bias.data_ptr(), critic.hidden_layer.bias.data_ptr()
+        s.b2, s.wo = critic.hidden_layer_2.bias.data_ptr(), critic.output_layer.weight.data_ptr()
+        s.bo = critic.output_layer.bias.data_ptr()
+        self.struct = s
+
+    @torch.no_grad()
+    def refresh(self):
+        c = self.critic
+        W1 = c.hidden_layer.weight
+        W2 = c.hidden_layer_2.weight
+        torch.index_select(c.cos_embedding.weight.reshape(-1), 0, self.idx["wc"], out=self._tmp(self.wc))
+        self.wc.copy_(self._t)
+        torch.index_select(W1.reshape(-1), 0, self.idx["w1"], out=self._tmp(self.w1))
+        self.w1.copy_(self._t)
+        torch.index_select(W2.reshape(-1), 0, self.idx["w2"], out=self._tmp(self.w2))
+        self.w2.copy_(self._t)
+        self._w2t_f.copy_(W2.t())
+        torch.index_select(self._w2t_f.reshape(-1), 0, self.idx["w2t"], out=self._tmp(self.w2t))
+        self.w2t.copy_(self._t)
+        self._w1t_f.copy_(W1.t())
+        torch.index_select(self._w1t_f.reshape(-1), 0, self.idx["w1t"], out=self._tmp(self.w1t))
+        self.w1t.copy_(self._t)
+
+    def _tmp(self, like):
+        t = getattr(self, "_tbuf", None)
+        if t is None or t.numel() < like.numel():
+            self._tbuf = torch.empty(256 * 128, dtype=torch.float32, device=like.device)
+        self._t = self._tbuf[:like.numel()]
+        return self._t
+
+
+def critic_forward(pack, F, G, taus, N, q=None, stream=None):
+    B = F.shape[0]
+    q = q if q is not None else torch.empty(B * N, dtype=torch.float32, device=F.device)
+    rc = _abi.lib().asvrl_critic_forward(C.byref(pack.struct), _abi.ptr(F), _abi.ptr(G), _abi.ptr(taus), B, N,
+                                         _abi.ptr(q), _abi.stream_ptr(stream))
+    _abi.check(rc, "asvrl_critic_forward")
+    return q.view(B, N)
+
+
+class TrainBuffers:
+    def __init__(self, B, N, device):
+        R = B * N
+        bf = dict(dtype=torch.bfloat16, device=device)
+        self.B, self.N = B, N
+        self.cos = torch.empty(R, 64, **bf)
+        self.h0 = torch.empty(R, 256, **bf)
+        self.dzc = torch.empty(R, 256, **bf)
+        self.h1g = torch.empty(R, 128, **bf)
+        self.dz1 = torch.empty(R, 128, **bf)
+        self.h2 = torch.empty(R, 128, **bf)
+        self.dz2 = torch.empty(R, 128, **bf)
+        f = dict(dtype=torch.float32, device=device)
+        self.dq = torch.empty(R, **f)
+        self.row_loss = torch.empty(R, **f)
+        self.q = torch.empty(R, **f)
+        self.dF = torch.empty(B, 256, **f)
+        self.dG = torch.empty(B, 128, **f)
+        a = _abi.AsvCriticActs()
+        a.cos, a.h0, a.dzc, a.h1g = self.cos.data_ptr(), self.h0.data_ptr(), self.dzc.data_ptr(), self.h1g.data_ptr()
+        a.dz1, a.h2, a.dz2, a.dq = self.dz1.data_ptr(), self.h2.data_ptr(), self.dz2.data_ptr(), self.dq.data_ptr()
+        self.struct = a
+
+
+def critic_train(pack, F, G, taus, q_targets, bufs, kappa=1.0, stream=None):
+    B, N, Np = F.shape[0], bufs.N, q_targets.shape[1]
+    rc = _abi.lib().asvrl_critic_train(C.byref(pack.struct), _abi.ptr(F), _abi.ptr(G), _abi.ptr(taus),
+                                       _abi.ptr(q_targets), B, N, Np, float(kappa), _abi.ptr(bufs.q),
+                                       _abi.ptr(bufs.row_loss), _abi.ptr(bufs.dF), _abi.ptr(bufs.dG),
+                                       C.byref(bufs.struct), _abi.stream_ptr(stream))
+    _abi.check(rc, "asvrl_critic_train")
+    return bufs.row_loss.sum() / float(B * Np)
+
+
+def critic_actor_grad(pack, F, G, taus, N, q, dG, stream=None):
+    B = F.shape[0]
+    rc = _abi.lib().asvrl_critic_actor_grad(C.byref(pack.struct), _abi.ptr(F), _abi.ptr(G), _abi.ptr(taus), B, N,
+                                            -1.0 / float(B * N), _abi.ptr(q), _abi.ptr(dG), _abi.stream_ptr(stream))
+    _abi.check(rc, "asvrl_critic_actor_grad")
+
+
+def _splitk_dw(dz, x, out):
+    """out (f32, (O, I)) <- dz^T x with dz (R, O), x (R, I) bf16, as a split-K batched GEMM."""
+    R = dz.shape[0]
+    g = max(1, R // 512)
+    while R % g:
+        g -= 1
+    part = torch.bmm(dz.view(g, R // g, dz.shape[1]).transpose(1, 2), x.view(g, R // g, x.shape[1]))
+    torch.sum(part, 0, dtype=torch.float32, out=out)
+
+
+def trunk_weight_grads(critic, bufs):
+    """Weight/bias gradients of the fused trunk layers from the TRAIN activations."""
+    _splitk_dw(bufs.dzc, bufs.cos, critic.cos_embedding.weight.grad)
+    torch.sum(bufs.dzc, 0, dtype=torch.float32, out=critic.cos_embedding.bias.grad)
+    _splitk_dw(bufs.dz1, bufs.h0, critic.hidden_layer.weight.grad)
+    torch.sum(bufs.dz1, 0, dtype=torch.float32, out=critic.hidden_layer.bias.grad)
+    _splitk_dw(bufs.dz2, bufs.h1g, critic.hidden_layer_2.weight.grad)
+    torch.sum(bufs.dz2, 0, dtype=torch.float32, out=critic.hidden_layer_2.bias.grad)
+    _splitk_dw(bufs.dq.view(-1, 1).to(torch.bfloat16), bufs.h2, critic.output_layer.weight.grad)
+    critic.output_layer.bias.grad.copy_(bufs.dq.sum().view(1))
+
+
+def fused_supported(critic, B, N):
+    return (critic.concat_feature_dimension == 256 and critic.hidden_dimension == 128 and critic.n == 64
+            and N <= 32 and 32 % N == 0 and (B * N) % 32 == 0)
+
+
+class FusedACIQN:
+    """State for ac_iqn_update_fused: weight packs and activation buffers (allocated once)."""
+
+    def __init__(self, policy_local, policy_target, B, N):
+        self.local_pack = CriticPack(policy_local.critic)
+        self.target_pack = CriticPack(policy_target.critic)
+        self.bufs = TrainBuffers(B, N, policy_local.critic.cos_embedding.weight.device)
+        dev = self.bufs.q.device
+        self.q_next = torch.empty(B * N, dtype=torch.float32, device=dev)
+        self.q_pi = torch.empty(B * N, dtype=torch.float32, device=dev)
+        self.dG_pi = torch.empty(B, 128, dtype=torch.float32, device=dev)
+        self.B, self.N = B, N
+
+
+def ac_iqn_update_fused(fz, policy_local, policy_target, actor_opt, critic_opt, critic_grads, actor_grads, states,
+                        actions, rewards, next_states, dones, gamma=0.99, taus=(None, None, None), sync=None,
+                        amp_dtype=torch.bfloat16, max_norm=0.5):
+    actor, critic = policy_local.actor, policy_local.critic
+    tcritic = policy_target.critic
+    B, N = fz.B, fz.N
+    dev = fz.bufs.q.device
+    amp = torch.autocast("cuda", dtype=amp_dtype) if amp_dtype is not None else _null()
+
+    def draw(t):
+        return torch.rand(B, N, device=dev) if t is None else t.reshape(B, N).float().contiguous()
+
+    # ---- critic (agent.py:395-416)
+    critic_grads.zero_()
+    with torch.no_grad():
+        with amp:
+            na = policy_target.actor(next_states)
+        Ft = encode_observation(tcritic.self_encoder, tcritic.object_encoder, next_states, tcritic.max_object_num,
+                                tcritic.object_dimension, tcritic.object_feature_dimension).float().contiguous()
+        Gt = tcritic.action_encoder(na.float()).contiguous()
+        fz.target_pack.refresh()
+        q_next = critic_forward(fz.target_pack, Ft, Gt, draw(taus[0]), N, q=fz.q_next)
+        q_targets = (rewards + gamma * q_next * (1.0 - dones)).contiguous()
+    F = encode_observation(critic.self_encoder, critic.object_encoder, states, critic.max_object_num,
+                           critic.object_dimension, critic.object_feature_dimension)
+    G = critic.action_encoder(actions)
+    fz.local_pack.refresh()
+    critic_loss = critic_train(fz.local_pack, F.detach().float().contiguous(), G.detach().float().contiguous(),
+                               draw(taus[1]), q_targets, fz.bufs)
+    trunk_weight_grads(critic, fz.bufs)
+    torch.autograd.backward([F, G], [fz.bufs.dF, fz.bufs.dG])
+    if sync is not None:
+        sync(critic_grads)
+    cgn = _clip(critic_grads.params, max_norm)
+    critic_opt.step()
+    # ---- actor through the updated critic (agent.py:419-427)
+    fz.local_pack.refresh()
+    with amp:
+        a_out = actor(states)
+    with torch.no_grad():
+        F2 = encode_observation(critic.self_encoder, critic.object_encoder, states, critic.max_object_num,
+                                critic.object_dimension, critic.object_feature_dimension).float().contiguous()
+    G2 = critic.action_encoder(a_out.float())
+    critic_actor_grad(fz.local_pack, F2, G2.detach().float().contiguous(), draw(taus[2]), N, fz.q_pi, fz.dG_pi)
+    actor_loss = -fz.q_pi.mean()
+    g = torch.autograd.grad(G2, actor_grads.params, grad_outputs=fz.dG_pi)
+    actor_grads.assign(g)
+    if sync is not None:
+        sync(actor_grads)
+    agn = _clip(actor_grads.params, max_norm)
+    actor_opt.step()
+    return critic_loss.detach(), actor_loss.detach(), cgn, agn

@@ -20,6 +20,7 @@ import time
 
 import torch
 
+from .fused_critic import FusedACIQN, ac_iqn_update_fused, fused_supported
 from .learn_ops import DeviceReplay, split_rows
 from .learner import FlatGrads, GradSync, ac_iqn_update, iqn_update
 from .policy.AC_IQN_model import AC_IQN_Policy
@@ -35,7 +36,7 @@ class VecTrainer:
                  width=55.0, batch_size=4096, num_tau=32, buffer_size=4_000_000, lr=1e-4, gamma=0.99,
                  learning_starts=None, target_update_interval=2500, total_timesteps=6_000_000,
                  exploration_fraction=0.25, initial_eps=0.6, final_eps=0.05, amp_dtype=torch.bfloat16, seed=0,
-                 device="cuda", sync=None, graphs=False, schedule=None, net_seed=100):
+                 device="cuda", sync=None, graphs=False, schedule=None, net_seed=100, fused=True):
         self.device = torch.device(device)
         self.agent_type = agent_type
         self.continuous = agent_type == "AC-IQN"
@@ -63,6 +64,9 @@ class VecTrainer:
             self.actor_opt = torch.optim.Adam(self.local.actor.parameters(), lr=lr, capturable=capturable)
             self.critic_opt = torch.optim.Adam(self.local.critic.parameters(), lr=lr, capturable=capturable)
             self.action_dim = 2
+            self.fused = None
+            if fused and amp_dtype is not None and fused_supported(self.local.critic, batch_size, num_tau):
+                self.fused = FusedACIQN(self.local, self.target, batch_size, num_tau)
         elif agent_type == "IQN":
             self.local = IQN_Policy(**DEFAULT_NET, action_size=25, device=self.device, seed=net_seed).to(self.device)
             self.target = IQN_Policy(**DEFAULT_NET, action_size=25, device=self.device, seed=net_seed).to(self.device)
@@ -128,7 +132,11 @@ class VecTrainer:
     def learn(self):
         rows = self.replay.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter, out=self.batch_rows)
         s, a, r, ns, d = split_rows(rows)
-        if self.agent_type == "AC-IQN":
+        if self.agent_type == "AC-IQN" and self.fused is not None:
+            out = ac_iqn_update_fused(self.fused, self.local, self.target, self.actor_opt, self.critic_opt,
+                                      self.critic_grads, self.actor_grads, s, a, r, ns, d, gamma=self.gamma,
+                                      sync=self.sync, amp_dtype=self.amp_dtype)
+        elif self.agent_type == "AC-IQN":
             out = ac_iqn_update(self.local, self.target, self.actor_opt, self.critic_opt, self.critic_grads,
                                 self.actor_grads, s, a, r, ns, d, gamma=self.gamma, num_tau=self.num_tau,
                                 sync=self.sync, amp_dtype=self.amp_dtype)

@@ -183,6 +183,56 @@ int asvrl_c51_project(const float* pns_a, const float* returns, const float* non
                       const float* support, int32_t B, int32_t atoms, float vmin, float vmax,
                       float delta_z, float gamma_n, float* m, void* stream);
 
+/* ---------------------------------------------------------------- fused IQN critic (MFMA) */
+
+/* Critic trunk weights of AC_IQN_model.py:392-408 (concat 256, hidden 128, 64 cosines), the
+ * matrices pre-packed into bf16 MFMA A-operand fragments (64 lanes x 8 bf16 per
+ * 32x32x16 fragment, in the k order the kernel's register chaining needs -- built by
+ * critic_pack.py from the f32 nn.Linear weights). Biases / output row stay f32. */
+typedef struct AsvCriticWeights {
+  const void* wc_frag;   /* cos_embedding.weight  (256 x 64)  : 32 fragments */
+  const void* w1_frag;   /* hidden_layer.weight   (128 x 256) : 64 fragments */
+  const void* w2_frag;   /* hidden_layer_2.weight (128 x 128) : 32 fragments */
+  const void* w2t_frag;  /* its transpose, for the backward   : 32 fragments */
+  const void* w1t_frag;  /* hidden_layer.weight^T (256 x 128) : 64 fragments */
+  const float* bc;       /* cos_embedding.bias [256] */
+  const float* b1;       /* hidden_layer.bias [128] */
+  const float* b2;       /* hidden_layer_2.bias [128] */
+  const float* wo;       /* output_layer.weight [128] */
+  const float* bo;       /* output_layer.bias [1] */
+} AsvCriticWeights;
+
+/* bf16 row-major activations the TRAIN mode writes for the weight gradients
+ * (dW = dZ^T X per layer), R = B*N rows. */
+typedef struct AsvCriticActs {
+  void* cos;   /* [R][64]   cos(tau pi k)            -> d cos_embedding.weight with dzc */
+  void* h0;    /* [R][256]  F * c                    -> d hidden_layer.weight with dz1 */
+  void* dzc;   /* [R][256]  dL/d(cos_embedding pre-activation) */
+  void* h1g;   /* [R][128]  h1 * G                   -> d hidden_layer_2.weight with dz2 */
+  void* dz1;   /* [R][128]  dL/d(hidden_layer pre-activation) */
+  void* h2;    /* [R][128]  relu(hidden_layer_2)     -> d output_layer.weight with dq */
+  void* dz2;   /* [R][128]  dL/d(hidden_layer_2 pre-activation) */
+  float* dq;   /* [R]       dL/dq */
+} AsvCriticActs;
+
+/* Critic.forward (AC_IQN_model.py:462-480) from precomputed state features F (B x 256,
+ * observation_processor) and action features G (B x 128, action_encoder): q [B*N].
+ * Requires N | 32 and 32 | B*N. */
+int asvrl_critic_forward(const AsvCriticWeights* w, const float* F, const float* G, const float* taus,
+                         int32_t B, int32_t N, float* q, void* stream);
+
+/* Critic update of train_AC_IQN (agent.py:395-414): forward, the quantile-Huber loss against
+ * q_targets (B x Np) and its backward in one launch. row_loss[R] sums to B*Np*loss; dF, dG
+ * are the gradients w.r.t. F and G; acts receive the activations for the weight gradients. */
+int asvrl_critic_train(const AsvCriticWeights* w, const float* F, const float* G, const float* taus,
+                       const float* q_targets, int32_t B, int32_t N, int32_t Np, float kappa, float* q,
+                       float* row_loss, float* dF, float* dG, const AsvCriticActs* acts, void* stream);
+
+/* Actor update's critic pass (agent.py:419-425): forward, then d(loss)/dG for dL/dq = dq on
+ * every row (= -1/(B*N) for loss = -mean q). q [R] optional. */
+int asvrl_critic_actor_grad(const AsvCriticWeights* w, const float* F, const float* G, const float* taus,
+                            int32_t B, int32_t N, float dq, float* q, float* dG, void* stream);
+
 /* ---------------------------------------------------------------- replay (replay_buffer.py) */
 
 /* ReplayBuffer.add (replay_buffer.py:22-24) for every robot that acted in the last step
