@@ -59,8 +59,20 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
 // feature index held by accumulator register g of 32-feature block mb in lane half h
 __device__ __forceinline__ int feat(int mb, int g, int h) { return mb * 32 + (g & 3) + 8 * (g >> 2) + 4 * h; }
 
-__device__ __forceinline__ float seg_sum(float v, int n) {  // sum over aligned groups of n lanes
-  for (int off = 1; off < n; off <<= 1) v += __shfl_xor(v, off, 64);
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// Sum over aligned groups of NT lanes (NT | 32), every lane of a group gets the sum: xor-1 and
+// xor-2 quad butterflies, row_half_mirror (8), row_mirror (16) on DPP, one bpermute for 32.
+template <int NT>
+__device__ __forceinline__ float seg_sum(float v) {
+  if (NT >= 2) v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  if (NT >= 4) v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  if (NT >= 8) v += dpp<0x141>(v);  // row_half_mirror
+  if (NT >= 16) v += dpp<0x140>(v); // row_mirror
+  if (NT >= 32) v += __shfl_xor(v, 16, 64);
   return v;
 }
 
@@ -74,15 +86,15 @@ __device__ __forceinline__ void store4(__bf16* base, const float* v) {
   *reinterpret_cast<bf16x4*>(base) = x;
 }
 
-template <int MODE>
+template <int MODE, int NT>
 __global__ __launch_bounds__(kWaves * 64) void critic_kernel(CriticArgs a) {
   const int lane = threadIdx.x & 63;
   const int tile = blockIdx.x * kWaves + (threadIdx.x >> 6);
-  const int R = a.B * a.N;
+  const int R = a.B * NT;
   if (tile * 32 >= R) return;
   const int r = lane & 31, h = lane >> 5;
   const int grow = tile * 32 + r;
-  const int b = grow / a.N;
+  const int b = grow / NT;
   const float tau = a.taus[grow];
   const float* Fb = a.F + static_cast<size_t>(b) * kC;
   const float* Gb = a.G + static_cast<size_t>(b) * kH;
@@ -90,42 +102,50 @@ __global__ __launch_bounds__(kWaves * 64) void critic_kernel(CriticArgs a) {
   const bf16x8* W1 = reinterpret_cast<const bf16x8*>(a.w.w1_frag);
   const bf16x8* W2 = reinterpret_cast<const bf16x8*>(a.w.w2_frag);
 
-  // ---------------- layer 0: c = relu(Wc cos + bc), h0 = F[b] * c
-  f32x16 acc0[8];
-#pragma unroll
-  for (int mb = 0; mb < 8; ++mb) acc0[mb] = f32x16{};
+  // ---------------- layer 0: c = relu(Wc cos + bc), h0 = F[b] * c   (two halves of 4 blocks)
+  bf16x8 cx[kNcos / 16];
 #pragma unroll
   for (int ks = 0; ks < kNcos / 16; ++ks) {
-    bf16x8 bx;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int k = ks * 16 + 8 * h + j;
       const float pis = static_cast<float>(3.141592653589793 * k);  // torch.FloatTensor([pi*i])
-      bx[j] = (__bf16)cosf(tau * pis);
+      cx[ks][j] = (__bf16)cosf(tau * pis);
     }
-    if (MODE == MODE_TRAIN) *reinterpret_cast<bf16x8*>(bp(a.acts.cos) + static_cast<size_t>(grow) * kNcos + ks * 16 + 8 * h) = bx;
-#pragma unroll
-    for (int mb = 0; mb < 8; ++mb) acc0[mb] = mfma(WC[(mb * 4 + ks) * 64 + lane], bx, acc0[mb]);
+    if (MODE == MODE_TRAIN)
+      *reinterpret_cast<bf16x8*>(bp(a.acts.cos) + static_cast<size_t>(grow) * kNcos + ks * 16 + 8 * h) = cx[ks];
   }
   bf16x8 cpk[16], hpk[16];
 #pragma unroll
-  for (int mb = 0; mb < 8; ++mb) {
+  for (int half = 0; half < 2; ++half) {
+    f32x16 acc0[4];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      float hv[8];
+    for (int q4 = 0; q4 < 4; ++q4) acc0[q4] = f32x16{};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int m = feat(mb, 8 * s + j, h);
-        float x = acc0[mb][8 * s + j] + a.w.bc[m];
-        x = x > 0.f ? x : 0.f;
-        cpk[mb * 2 + s][j] = (__bf16)x;
-        hv[j] = Fb[m] * x;
-        hpk[mb * 2 + s][j] = (__bf16)hv[j];
-      }
-      if (MODE == MODE_TRAIN) {
-        __bf16* row = bp(a.acts.h0) + static_cast<size_t>(grow) * kC + mb * 32 + 16 * s + 4 * h;
-        store4(row, hv);
-        store4(row + 8, hv + 4);
+    for (int ks = 0; ks < kNcos / 16; ++ks) {
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) acc0[q4] = mfma(WC[((half * 4 + q4) * 4 + ks) * 64 + lane], cx[ks], acc0[q4]);
+    }
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      const int mb = half * 4 + q4;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float hv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int m = feat(mb, 8 * s + j, h);
+          float x = acc0[q4][8 * s + j] + a.w.bc[m];
+          x = x > 0.f ? x : 0.f;
+          cpk[mb * 2 + s][j] = (__bf16)x;
+          hv[j] = Fb[m] * x;
+          hpk[mb * 2 + s][j] = (__bf16)hv[j];
+        }
+        if (MODE == MODE_TRAIN) {
+          __bf16* row = bp(a.acts.h0) + static_cast<size_t>(grow) * kC + mb * 32 + 16 * s + 4 * h;
+          store4(row, hv);
+          store4(row + 8, hv + 4);
+        }
       }
     }
   }
@@ -244,21 +264,27 @@ __global__ __launch_bounds__(kWaves * 64) void critic_kernel(CriticArgs a) {
 #pragma unroll
     for (int mb = 0; mb < 4; ++mb) acc3[mb] = mfma(W2T[(mb * 8 + ks) * 64 + lane], dz2pk[ks], acc3[mb]);
   }
-  const bool writer = (r % a.N) == 0;
+  const bool writer = (r % NT) == 0;
   bf16x8 dz1pk[8];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      float dv[8];
+      float dv[8], gs[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gs[j] = acc3[mb][8 * s + j] * static_cast<float>(h1pk[mb * 2 + s][j]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gs[j] = seg_sum<NT>(gs[j]);
+      if (writer) {
+        float* o = a.dG + static_cast<size_t>(b) * kH + mb * 32 + 16 * s + 4 * h;
+        *reinterpret_cast<float4*>(o) = make_float4(gs[0], gs[1], gs[2], gs[3]);
+        *reinterpret_cast<float4*>(o + 8) = make_float4(gs[4], gs[5], gs[6], gs[7]);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int m = feat(mb, 8 * s + j, h);
-        const float d = acc3[mb][8 * s + j];
         const float h1 = static_cast<float>(h1pk[mb * 2 + s][j]);
-        const float gsum = seg_sum(d * h1, a.N);
-        if (writer) a.dG[static_cast<size_t>(b) * kH + m] = gsum;
-        dv[j] = h1 > 0.f ? d * Gb[m] : 0.f;
+        dv[j] = h1 > 0.f ? acc3[mb][8 * s + j] * Gb[m] : 0.f;
         dz1pk[mb * 2 + s][j] = (__bf16)dv[j];
       }
       if (MODE == MODE_TRAIN) {
@@ -288,15 +314,21 @@ __global__ __launch_bounds__(kWaves * 64) void critic_kernel(CriticArgs a) {
       const int mb = half * 4 + q4;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        float dv[8];
+        float dv[8], fs[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) fs[j] = acc4[q4][8 * s + j] * static_cast<float>(cpk[mb * 2 + s][j]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) fs[j] = seg_sum<NT>(fs[j]);
+        if (writer) {
+          float* o = a.dF + static_cast<size_t>(b) * kC + mb * 32 + 16 * s + 4 * h;
+          *reinterpret_cast<float4*>(o) = make_float4(fs[0], fs[1], fs[2], fs[3]);
+          *reinterpret_cast<float4*>(o + 8) = make_float4(fs[4], fs[5], fs[6], fs[7]);
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int m = feat(mb, 8 * s + j, h);
-          const float d = acc4[q4][8 * s + j];
           const float c = static_cast<float>(cpk[mb * 2 + s][j]);
-          const float fsum = seg_sum(d * c, a.N);
-          if (writer) a.dF[static_cast<size_t>(b) * kC + m] = fsum;
-          dv[j] = c > 0.f ? d * Fb[m] : 0.f;
+          dv[j] = c > 0.f ? acc4[q4][8 * s + j] * Fb[m] : 0.f;
         }
         __bf16* row = bp(a.acts.dzc) + static_cast<size_t>(grow) * kC + mb * 32 + 16 * s + 4 * h;
         store4(row, dv);
@@ -306,14 +338,21 @@ __global__ __launch_bounds__(kWaves * 64) void critic_kernel(CriticArgs a) {
   }
 }
 
+template <int NT>
+void launch_n(int mode, const CriticArgs& a, dim3 grid, dim3 block, hipStream_t st) {
+  if (mode == MODE_FWD) hipLaunchKernelGGL((critic_kernel<MODE_FWD, NT>), grid, block, 0, st, a);
+  else if (mode == MODE_TRAIN) hipLaunchKernelGGL((critic_kernel<MODE_TRAIN, NT>), grid, block, 0, st, a);
+  else hipLaunchKernelGGL((critic_kernel<MODE_ACTOR, NT>), grid, block, 0, st, a);
+}
+
 int launch(int mode, const CriticArgs& a, void* stream) {
   const int R = a.B * a.N;
   const int tiles = (R + 31) / 32;
   const dim3 grid((tiles + kWaves - 1) / kWaves), block(kWaves * 64);
   hipStream_t st = as_stream(stream);
-  if (mode == MODE_FWD) hipLaunchKernelGGL(critic_kernel<MODE_FWD>, grid, block, 0, st, a);
-  else if (mode == MODE_TRAIN) hipLaunchKernelGGL(critic_kernel<MODE_TRAIN>, grid, block, 0, st, a);
-  else hipLaunchKernelGGL(critic_kernel<MODE_ACTOR>, grid, block, 0, st, a);
+  if (a.N == 8) launch_n<8>(mode, a, grid, block, st);
+  else if (a.N == 16) launch_n<16>(mode, a, grid, block, st);
+  else launch_n<32>(mode, a, grid, block, st);
   return check_launch("asvrl_critic");
 }
 
@@ -321,7 +360,7 @@ int validate(const AsvCriticWeights* w, const float* F, const float* G, const fl
   ASVRL_REQUIRE(w && F && G && taus, "asvrl_critic: null argument");
   ASVRL_REQUIRE(w->wc_frag && w->w1_frag && w->w2_frag && w->bc && w->b1 && w->b2 && w->wo && w->bo,
                 "asvrl_critic: null weight");
-  ASVRL_REQUIRE(N >= 1 && N <= 32 && (32 % N) == 0, "asvrl_critic: N must divide 32");
+  ASVRL_REQUIRE(N == 8 || N == 16 || N == 32, "asvrl_critic: N must be 8, 16 or 32");
   ASVRL_REQUIRE(B >= 0 && (static_cast<int64_t>(B) * N) % 32 == 0, "asvrl_critic: B*N must be a multiple of 32");
   return 0;
 }

@@ -163,7 +163,7 @@ def trunk_weight_grads(critic, bufs):
 
 def fused_supported(critic, B, N):
     return (critic.concat_feature_dimension == 256 and critic.hidden_dimension == 128 and critic.n == 64
-            and N <= 32 and 32 % N == 0 and (B * N) % 32 == 0)
+            and N in (8, 16, 32) and (B * N) % 32 == 0)
 
 
 class FusedACIQN:

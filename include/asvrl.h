@@ -217,7 +217,7 @@ typedef struct AsvCriticActs {
 
 /* Critic.forward (AC_IQN_model.py:462-480) from precomputed state features F (B x 256,
  * observation_processor) and action features G (B x 128, action_encoder): q [B*N].
- * Requires N | 32 and 32 | B*N. */
+ * Requires N in {8, 16, 32} (taus of a sample stay inside one 32-row wave tile). */
 int asvrl_critic_forward(const AsvCriticWeights* w, const float* F, const float* G, const float* taus,
                          int32_t B, int32_t N, float* q, void* stream);
 
