@@ -94,6 +94,7 @@ EXPORTS = [
     ("asvrl_current_field", C.c_int, [_VP, _I32, _D, _VP, _I32, _VP, _VP]),
     ("asvrl_quantile_huber", C.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, _F, _F, _VP, _VP, _VP, _VP]),
     ("asvrl_c51_project", C.c_int, [_VP, _VP, _VP, _VP, _I32, _I32, _F, _F, _F, _F, _VP, _VP]),
+    ("asvrl_critic_pack", C.c_int, [_VP, _VP, _VP, C.POINTER(AsvCriticWeights), _VP]),
     ("asvrl_critic_forward", C.c_int, [C.POINTER(AsvCriticWeights), _VP, _VP, _VP, _I32, _I32, _VP, _VP]),
     ("asvrl_critic_train", C.c_int, [C.POINTER(AsvCriticWeights), _VP, _VP, _VP, _VP, _I32, _I32, _I32, _F, _VP, _VP,
                                      _VP, _VP, C.POINTER(AsvCriticActs), _VP]),
@@ -101,6 +102,10 @@ EXPORTS = [
     ("asvrl_replay_push", C.c_int, [_VP, _VP, _VP, _VP, _I32, _VP, _VP, _I32, _VP, _I64, _VP, _VP, _VP]),
     ("asvrl_replay_sample", C.c_int, [_VP, _I64, _VP, _VP, _I32, _U64, _U64, _VP, _VP, _VP, _VP]),
     ("asvrl_replay_write_rows", C.c_int, [_VP, _VP, _I32, _VP, _VP]),
+    ("asvrl_adam_clip", C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, _F, _F, _VP, _VP, _VP]),
+    ("asvrl_linear_wgrad_workspace", _I64, [_I32, _I32]),
+    ("asvrl_linear_wgrad", C.c_int, [_VP, _I64, _VP, _I64, _I32, _I32, _I32, _VP, _VP, _I32, _VP, _I64, _VP]),
+    ("asvrl_linear_wgrad_vec", C.c_int, [_VP, _VP, _I64, _I32, _I32, _VP, _VP, _I32, _VP, _I64, _VP]),
     ("asvrl_last_error", C.c_char_p, []),
     ("asvrl_abi_version", C.c_int, []),
     ("asvrl_struct_sizes", None, [C.c_void_p]),

@@ -356,6 +356,55 @@ int launch(int mode, const CriticArgs& a, void* stream) {
   return check_launch("asvrl_critic");
 }
 
+// ------------------------------------------------------------------ weight packing
+// The A-operand fragment images of AsvCriticWeights from the row-major f32 weights: element
+// o = ((mb*KS + ks)*64 + lane)*8 + j of an (M x K) image holds W[mb*32 + (lane&31)][col] with
+// col = ks*16 + 8h + j for the input-fed layer and ks*16 + 8(j>>2) + 4h + (j&3) for the
+// accumulator-fed (chained) layers; h = lane >> 5. One thread per element, all five images.
+constexpr int kPackWc = 256 * 64, kPackW1 = 128 * 256, kPackW2 = 128 * 128;
+constexpr int kPackTotal = kPackWc + 2 * kPackW1 + 2 * kPackW2;
+
+__device__ __forceinline__ void frag_rc(int o, int K, bool chained, int& row, int& col) {
+  const int j = o & 7, lane = (o >> 3) & 63, blk = o >> 9;
+  const int KS = K / 16;
+  const int ks = blk % KS, mb = blk / KS, h = lane >> 5;
+  row = mb * 32 + (lane & 31);
+  col = ks * 16 + (chained ? (8 * (j >> 2) + 4 * h + (j & 3)) : (8 * h + j));
+}
+
+__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ wc, const float* __restrict__ w1,
+                                                   const float* __restrict__ w2, AsvCriticWeights w) {
+  int o = blockIdx.x * 256 + threadIdx.x;
+  if (o >= kPackTotal) return;
+  int row, col;
+  if (o < kPackWc) {                                    // cos_embedding.weight (256 x 64)
+    frag_rc(o, 64, false, row, col);
+    const_cast<__bf16*>(static_cast<const __bf16*>(w.wc_frag))[o] = (__bf16)wc[row * 64 + col];
+    return;
+  }
+  o -= kPackWc;
+  if (o < kPackW1) {                                    // hidden_layer.weight (128 x 256)
+    frag_rc(o, 256, true, row, col);
+    const_cast<__bf16*>(static_cast<const __bf16*>(w.w1_frag))[o] = (__bf16)w1[row * 256 + col];
+    return;
+  }
+  o -= kPackW1;
+  if (o < kPackW2) {                                    // hidden_layer_2.weight (128 x 128)
+    frag_rc(o, 128, true, row, col);
+    const_cast<__bf16*>(static_cast<const __bf16*>(w.w2_frag))[o] = (__bf16)w2[row * 128 + col];
+    return;
+  }
+  o -= kPackW2;
+  if (o < kPackW2) {                                    // its transpose
+    frag_rc(o, 128, true, row, col);
+    const_cast<__bf16*>(static_cast<const __bf16*>(w.w2t_frag))[o] = (__bf16)w2[col * 128 + row];
+    return;
+  }
+  o -= kPackW2;                                         // hidden_layer.weight^T (256 x 128)
+  frag_rc(o, 128, true, row, col);
+  const_cast<__bf16*>(static_cast<const __bf16*>(w.w1t_frag))[o] = (__bf16)w1[col * 256 + row];
+}
+
 int validate(const AsvCriticWeights* w, const float* F, const float* G, const float* taus, int B, int N) {
   ASVRL_REQUIRE(w && F && G && taus, "asvrl_critic: null argument");
   ASVRL_REQUIRE(w->wc_frag && w->w1_frag && w->w2_frag && w->bc && w->b1 && w->b2 && w->wo && w->bo,
@@ -404,4 +453,13 @@ extern "C" int asvrl_critic_actor_grad(const AsvCriticWeights* w, const float* F
   CriticArgs a{};
   a.w = *w; a.F = F; a.G = G; a.taus = taus; a.B = B; a.N = N; a.dq_const = dq; a.q = q; a.dG = dG;
   return launch(MODE_ACTOR, a, stream);
+}
+
+extern "C" int asvrl_critic_pack(const float* wc, const float* w1, const float* w2, const AsvCriticWeights* w,
+                                 void* stream) {
+  ASVRL_REQUIRE(wc && w1 && w2 && w, "asvrl_critic_pack: null argument");
+  ASVRL_REQUIRE(w->wc_frag && w->w1_frag && w->w2_frag && w->w2t_frag && w->w1t_frag,
+                "asvrl_critic_pack: null fragment buffer");
+  hipLaunchKernelGGL(pack_kernel, dim3((kPackTotal + 255) / 256), dim3(256), 0, as_stream(stream), wc, w1, w2, *w);
+  return check_launch("asvrl_critic_pack");
 }

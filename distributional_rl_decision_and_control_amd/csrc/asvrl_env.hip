@@ -509,111 +509,175 @@ __device__ inline bool far_enough(double ax, double ay, double bx, double by, do
   return strict ? !(d <= lim) : !(d < lim);
 }
 
-__global__ __launch_bounds__(kBlock) void env_reset_kernel(AsvParams p, AsvEnvState s, AsvResetCfg cfg,
-                                                           const uint8_t* __restrict__ mask,
-                                                           uint64_t seed, uint64_t counter,
-                                                           const uint64_t* __restrict__ counter_dev) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= s.n_envs) return;
+// One wave per env being reset. Every phase is rejection sampling with at most 500 draws in
+// the reference's order (robots env.py:106-120, cores :123-136 with check_core :378-418,
+// obstacles :151-162 with check_obstacle :420-456); here the wave evaluates 64 consecutive
+// candidates at once, accepts the lowest-numbered valid one and restarts right after it --
+// the same accepted sequence as drawing candidates one by one, because candidate c's values
+// come from its own Philox counter (c, env, phase, step) and not from a shared stream.
+// The accepted set of the phase lives in LDS.
+constexpr int kResetWaves = 4;
+constexpr int kResetMaxR = 32;
+constexpr int kResetMaxO = 32;
+
+struct CandDraw {
+  uint32_t k0, k1, e, ctr;
+  __device__ double u(int phase, int cand, int j) const {   // j-th double of candidate cand
+    const U4 r = philox4x32_10(U4{static_cast<uint32_t>(cand) * 4u + static_cast<uint32_t>(j >> 1), e,
+                                  static_cast<uint32_t>(phase), ctr}, k0, k1);
+    const uint64_t hi = (j & 1) ? r.z : r.x, lo = (j & 1) ? r.w : r.y;
+    const uint64_t bits = ((hi << 32) | lo) >> 11;
+    return (static_cast<double>(bits) + 1.0) * (1.0 / 9007199254740992.0);   // (0, 1]
+  }
+};
+
+__global__ __launch_bounds__(kResetWaves * kWave) void env_reset_kernel(AsvParams p, AsvEnvState s, AsvResetCfg cfg,
+                                                                        const uint8_t* __restrict__ mask,
+                                                                        uint64_t seed, uint64_t counter,
+                                                                        const uint64_t* __restrict__ counter_dev) {
+  __shared__ double srob[kResetWaves][4][kResetMaxR];      // x, y, gx, gy of accepted robots
+  __shared__ double score[kResetWaves][kMaxCores][4];      // x, y, clockwise, Gamma
+  __shared__ double sobs[kResetWaves][kResetMaxO][3];      // x, y, r
+  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  const int e = blockIdx.x * kResetWaves + wv;
+  if (e >= s.n_envs) return;                     // wave-uniform exits
   if (mask != nullptr && mask[e] == 0) return;
   const int R = s.max_robots, O = s.max_obs, Cmax = s.max_cores;
   const size_t NT = static_cast<size_t>(s.n_envs) * R;
   double* rs = s.rs;
   const uint64_t ctr = counter + (counter_dev != nullptr ? *counter_dev : 0ull);
-  Stream g(seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull, static_cast<uint32_t>(e), 0xA5E7u,
-           static_cast<uint32_t>(ctr));
+  const uint64_t key = seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull;
+  const CandDraw g{static_cast<uint32_t>(key), static_cast<uint32_t>(key >> 32), static_cast<uint32_t>(e),
+                   static_cast<uint32_t>(ctr)};
+  constexpr int kDraws = 500;
+
+  // ---- robots
   const int want_r = cfg.num_robots < R ? cfg.num_robots : R;
-  // robots: rejection sampling of start/goal pairs, <= 500 draws (env.py:106-120)
   int nr = 0;
-  for (int it = 0; it < 500 && nr < want_r; ++it) {
-    const double sxv = 2.0 + (cfg.width - 4.0) * (1.0 - g.u01());
-    const double syv = 2.0 + (cfg.height - 4.0) * (1.0 - g.u01());
-    const double gxv = 2.0 + (cfg.width - 4.0) * (1.0 - g.u01());
-    const double gyv = 2.0 + (cfg.height - 4.0) * (1.0 - g.u01());
-    bool ok = far_enough(gxv, gyv, sxv, syv, cfg.min_start_goal_dis, false);  // env.py:361
-    for (int k = 0; k < nr && ok; ++k) {
-      const size_t kd = static_cast<size_t>(e) * R + k;
-      ok = far_enough(rs[ASVRL_F_X * NT + kd], rs[ASVRL_F_Y * NT + kd], sxv, syv, cfg.clear_r, true) &&
-           far_enough(rs[ASVRL_F_GX * NT + kd], rs[ASVRL_F_GY * NT + kd], gxv, gyv, cfg.clear_r, true);
+  for (int base = 0; nr < want_r && base < kDraws;) {
+    const int c = base + lane;
+    const double sxv = 2.0 + (cfg.width - 4.0) * (1.0 - g.u(0, c, 0));
+    const double syv = 2.0 + (cfg.height - 4.0) * (1.0 - g.u(0, c, 1));
+    const double gxv = 2.0 + (cfg.width - 4.0) * (1.0 - g.u(0, c, 2));
+    const double gyv = 2.0 + (cfg.height - 4.0) * (1.0 - g.u(0, c, 3));
+    bool ok = c < kDraws && far_enough(gxv, gyv, sxv, syv, cfg.min_start_goal_dis, false);  // env.py:361
+    for (int k = 0; k < nr && ok; ++k)
+      ok = far_enough(srob[wv][0][k], srob[wv][1][k], sxv, syv, cfg.clear_r, true) &&
+           far_enough(srob[wv][2][k], srob[wv][3][k], gxv, gyv, cfg.clear_r, true);
+    const uint64_t bal = __ballot(ok);
+    if (bal == 0) {
+      base += kWave;
+      continue;
     }
-    if (!ok) continue;
-    const size_t id = static_cast<size_t>(e) * R + nr;
-    rs[ASVRL_F_X * NT + id] = sxv;  // reset_robot / reset_state (env.py:166-176, wamv.py:177-193)
-    rs[ASVRL_F_Y * NT + id] = syv;
-    rs[ASVRL_F_GX * NT + id] = gxv;
-    rs[ASVRL_F_GY * NT + id] = gyv;
-    rs[ASVRL_F_THETA * NT + id] = kTwoPi * (1.0 - g.u01());
-    for (int f = ASVRL_F_VR0; f <= ASVRL_F_RP; ++f) rs[f * NT + id] = 0.0;
-    rs[ASVRL_F_PHI * NT + id] = 0.0;
-    rs[ASVRL_F_RET * NT + id] = 0.0;
-    s.rflags[id] = 0;
+    const int f = __ffsll(static_cast<unsigned long long>(bal)) - 1;
+    if (lane == f) {
+      srob[wv][0][nr] = sxv;
+      srob[wv][1][nr] = syv;
+      srob[wv][2][nr] = gxv;
+      srob[wv][3][nr] = gyv;
+      const size_t id = static_cast<size_t>(e) * R + nr;
+      rs[ASVRL_F_X * NT + id] = sxv;  // reset_robot / reset_state (env.py:166-176, wamv.py:177-193)
+      rs[ASVRL_F_Y * NT + id] = syv;
+      rs[ASVRL_F_GX * NT + id] = gxv;
+      rs[ASVRL_F_GY * NT + id] = gyv;
+      rs[ASVRL_F_THETA * NT + id] = kTwoPi * (1.0 - g.u(0, c, 4));
+      for (int fld = ASVRL_F_VR0; fld <= ASVRL_F_RP; ++fld) rs[fld * NT + id] = 0.0;
+      rs[ASVRL_F_PHI * NT + id] = 0.0;
+      rs[ASVRL_F_RET * NT + id] = 0.0;
+      s.rflags[id] = 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
     ++nr;
+    base += f + 1;
   }
-  for (int k = nr; k < R; ++k) s.rflags[static_cast<size_t>(e) * R + k] = ASVRL_FLAG_DEACTIVATED;
-  // vortex cores (env.py:123-136, check_core :378-418)
+  for (int k = nr + lane; k < R; k += kWave) s.rflags[static_cast<size_t>(e) * R + k] = ASVRL_FLAG_DEACTIVATED;
+
+  // ---- vortex cores (env.py:123-136, check_core :378-418)
   double* cores = s.cores + static_cast<size_t>(e) * Cmax * 4;
   const int want_c = cfg.num_cores < Cmax ? cfg.num_cores : Cmax;
   int nc = 0;
-  for (int it = 0; it < 500 && nc < want_c; ++it) {
-    const double cx = cfg.width * (1.0 - g.u01());
-    const double cy = cfg.height * (1.0 - g.u01());
-    const double cw = g.u01() <= 0.5 ? 1.0 : 0.0;
-    const double ve = cfg.v_lo + (cfg.v_hi - cfg.v_lo) * (1.0 - g.u01());
+  for (int base = 0; nc < want_c && base < kDraws;) {
+    const int c = base + lane;
+    const double cx = cfg.width * (1.0 - g.u(1, c, 0));
+    const double cy = cfg.height * (1.0 - g.u(1, c, 1));
+    const double cw = g.u(1, c, 2) <= 0.5 ? 1.0 : 0.0;
+    const double ve = cfg.v_lo + (cfg.v_hi - cfg.v_lo) * (1.0 - g.u(1, c, 3));
     const double Gamma = 2 * kPi * p.core_r * ve;
-    bool ok = !(cx - p.core_r < 0.0 || cx + p.core_r > cfg.width) &&
+    bool ok = c < kDraws && !(cx - p.core_r < 0.0 || cx + p.core_r > cfg.width) &&
               !(cy - p.core_r < 0.0 || cy + p.core_r > cfg.width);  // (sic) env.py:383
-    for (int k = 0; k < nr && ok; ++k) {
-      const size_t kd = static_cast<size_t>(e) * R + k;
-      ok = far_enough(cx, cy, rs[ASVRL_F_X * NT + kd], rs[ASVRL_F_Y * NT + kd], p.core_r + cfg.clear_r, false) &&
-           far_enough(cx, cy, rs[ASVRL_F_GX * NT + kd], rs[ASVRL_F_GY * NT + kd], p.core_r + cfg.clear_r, false);
-    }
+    for (int k = 0; k < nr && ok; ++k)
+      ok = far_enough(cx, cy, srob[wv][0][k], srob[wv][1][k], p.core_r + cfg.clear_r, false) &&
+           far_enough(cx, cy, srob[wv][2][k], srob[wv][3][k], p.core_r + cfg.clear_r, false);
     for (int k = 0; k < nc && ok; ++k) {
-      const double dx = cores[4 * k] - cx, dy = cores[4 * k + 1] - cy;
+      const double dx = score[wv][k][0] - cx, dy = score[wv][k][1] - cy;
       const double dis = sqrt(dx * dx + dy * dy);
-      if (cores[4 * k + 2] == cw) {
-        const double bi = cores[4 * k + 3] / (2 * kPi * cfg.v_rel_max);
+      if (score[wv][k][2] == cw) {
+        const double bi = score[wv][k][3] / (2 * kPi * cfg.v_rel_max);
         const double bj = Gamma / (2 * kPi * cfg.v_rel_max);
         if (dis < bi + bj) ok = false;
       } else {
-        const double gl = fmax(cores[4 * k + 3], Gamma), gs = fmin(cores[4 * k + 3], Gamma);
+        const double gl = fmax(score[wv][k][3], Gamma), gs = fmin(score[wv][k][3], Gamma);
         const double v1 = gl / (2 * kPi * (dis - 2 * p.core_r));
         const double v2 = gs / (2 * kPi * p.core_r);
         if (v1 > cfg.p_rel * v2) ok = false;
       }
     }
-    if (!ok) continue;
-    cores[4 * nc] = cx;
-    cores[4 * nc + 1] = cy;
-    cores[4 * nc + 2] = cw;
-    cores[4 * nc + 3] = Gamma;
+    const uint64_t bal = __ballot(ok);
+    if (bal == 0) {
+      base += kWave;
+      continue;
+    }
+    const int f = __ffsll(static_cast<unsigned long long>(bal)) - 1;
+    if (lane == f) {
+      score[wv][nc][0] = cores[4 * nc] = cx;
+      score[wv][nc][1] = cores[4 * nc + 1] = cy;
+      score[wv][nc][2] = cores[4 * nc + 2] = cw;
+      score[wv][nc][3] = cores[4 * nc + 3] = Gamma;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
     ++nc;
+    base += f + 1;
   }
-  // static obstacles (env.py:151-162, check_obstacle :420-456)
+
+  // ---- static obstacles (env.py:151-162, check_obstacle :420-456)
   double* obs = s.obstacles + static_cast<size_t>(e) * O * 3;
   const int want_o = cfg.num_obs < O ? cfg.num_obs : O;
   int no = 0;
-  for (int it = 0; it < 500 && no < want_o; ++it) {
-    const double ox = 5.0 + (cfg.width - 10.0) * (1.0 - g.u01());
-    const double oy = 5.0 + (cfg.height - 10.0) * (1.0 - g.u01());
-    const double orad = cfg.obs_r_lo + (cfg.obs_r_hi - cfg.obs_r_lo) * (1.0 - g.u01());
-    bool ok = !(ox - orad < 0.0 || ox + orad > cfg.width) && !(oy - orad < 0.0 || oy + orad > cfg.height);
-    for (int k = 0; k < nr && ok; ++k) {
-      const size_t kd = static_cast<size_t>(e) * R + k;
-      ok = far_enough(ox, oy, rs[ASVRL_F_X * NT + kd], rs[ASVRL_F_Y * NT + kd], orad + cfg.clear_r, false) &&
-           far_enough(ox, oy, rs[ASVRL_F_GX * NT + kd], rs[ASVRL_F_GY * NT + kd], orad + cfg.clear_r, false);
+  for (int base = 0; no < want_o && base < kDraws;) {
+    const int c = base + lane;
+    const double ox = 5.0 + (cfg.width - 10.0) * (1.0 - g.u(2, c, 0));
+    const double oy = 5.0 + (cfg.height - 10.0) * (1.0 - g.u(2, c, 1));
+    const double orad = cfg.obs_r_lo + (cfg.obs_r_hi - cfg.obs_r_lo) * (1.0 - g.u(2, c, 2));
+    bool ok = c < kDraws && !(ox - orad < 0.0 || ox + orad > cfg.width) && !(oy - orad < 0.0 || oy + orad > cfg.height);
+    for (int k = 0; k < nr && ok; ++k)
+      ok = far_enough(ox, oy, srob[wv][0][k], srob[wv][1][k], orad + cfg.clear_r, false) &&
+           far_enough(ox, oy, srob[wv][2][k], srob[wv][3][k], orad + cfg.clear_r, false);
+    for (int k = 0; k < nc && ok; ++k) ok = far_enough(score[wv][k][0], score[wv][k][1], ox, oy, p.core_r + orad, true);
+    for (int k = 0; k < no && ok; ++k) ok = far_enough(sobs[wv][k][0], sobs[wv][k][1], ox, oy, sobs[wv][k][2] + orad, true);
+    const uint64_t bal = __ballot(ok);
+    if (bal == 0) {
+      base += kWave;
+      continue;
     }
-    for (int k = 0; k < nc && ok; ++k) ok = far_enough(cores[4 * k], cores[4 * k + 1], ox, oy, p.core_r + orad, true);
-    for (int k = 0; k < no && ok; ++k) ok = far_enough(obs[3 * k], obs[3 * k + 1], ox, oy, obs[3 * k + 2] + orad, true);
-    if (!ok) continue;
-    obs[3 * no] = ox;
-    obs[3 * no + 1] = oy;
-    obs[3 * no + 2] = orad;
+    const int f = __ffsll(static_cast<unsigned long long>(bal)) - 1;
+    if (lane == f) {
+      sobs[wv][no][0] = obs[3 * no] = ox;
+      sobs[wv][no][1] = obs[3 * no + 1] = oy;
+      sobs[wv][no][2] = obs[3 * no + 2] = orad;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
     ++no;
+    base += f + 1;
   }
-  s.n_robots[e] = nr;
-  s.n_cores[e] = nc;
-  s.n_obs[e] = no;
-  s.ep_ts[e] = 0;
+  if (lane == 0) {
+    s.n_robots[e] = nr;
+    s.n_cores[e] = nc;
+    s.n_obs[e] = no;
+    s.ep_ts[e] = 0;
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void current_kernel(const double* __restrict__ cores, int nc, double core_r,
@@ -667,11 +731,13 @@ extern "C" int asvrl_env_reset(const AsvParams* params, const AsvEnvState* state
                                const uint64_t* counter_dev, void* stream) {
   ASVRL_REQUIRE(params && state && cfg, "asvrl_env_reset: null argument");
   ASVRL_REQUIRE(state->max_cores <= kMaxCores, "asvrl_env_reset: max_cores > 16");
+  ASVRL_REQUIRE(state->max_robots <= kResetMaxR && state->max_obs <= kResetMaxO,
+                "asvrl_env_reset: max_robots and max_obs must be <= 32");
   ASVRL_REQUIRE(cfg->width > 4.0 && cfg->height > 4.0, "asvrl_env_reset: map too small");
   if (state->n_envs == 0) return 0;
-  const int grid = (state->n_envs + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(env_reset_kernel, dim3(grid), dim3(kBlock), 0, as_stream(stream), *params, *state, *cfg,
-                     env_mask, seed, counter, counter_dev);
+  const int grid = (state->n_envs + kResetWaves - 1) / kResetWaves;
+  hipLaunchKernelGGL(env_reset_kernel, dim3(grid), dim3(kResetWaves * kWave), 0, as_stream(stream), *params, *state,
+                     *cfg, env_mask, seed, counter, counter_dev);
   return check_launch("asvrl_env_reset");
 }
 

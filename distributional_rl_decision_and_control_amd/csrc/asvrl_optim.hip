@@ -1,0 +1,100 @@
+// asvrl_optim.hip -- the optimiser step of the batched learner on gfx950: global-norm
+// gradient clipping (torch.nn.utils.clip_grad_norm_(params, 0.5), agent.py:415,426,471,636)
+// fused with Adam (optim.Adam(lr=1e-4), agent.py:75-76,98) over ONE flat f32 parameter
+// buffer. Two launches per optimizer step regardless of the parameter count:
+//   1. sumsq_kernel: kNormBlocks partial sums of g^2 in f64 (one per block), step += 1
+//   2. adam_kernel : every block folds the partials in the same fixed order (so all blocks
+//      see the identical norm), scales g by min(1, max_norm / (norm + 1e-6)) in place, as
+//      clip_grad_norm_ does, then applies Adam with the bias corrections of the new step.
+#include "asvrl_common.h"
+
+namespace asvrl {
+namespace {
+
+constexpr int kNormBlocks = 64;
+constexpr int kOptThreads = 256;
+
+__global__ __launch_bounds__(kOptThreads) void sumsq_kernel(const float* __restrict__ g, int64_t n,
+                                                             double* __restrict__ partial, float* step) {
+  double acc = 0.0;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kOptThreads + threadIdx.x; i < n;
+       i += static_cast<int64_t>(kNormBlocks) * kOptThreads) {
+    const double x = g[i];
+    acc += x * x;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, kWave);
+  __shared__ double s[kOptThreads / kWave];
+  if ((threadIdx.x & (kWave - 1)) == 0) s[threadIdx.x / kWave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < kOptThreads / kWave; ++w) t += s[w];
+    partial[blockIdx.x] = t;
+    if (blockIdx.x == 0) step[0] += 1.f;
+  }
+}
+
+__global__ __launch_bounds__(kOptThreads) void adam_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                            float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                            const double* __restrict__ partial,
+                                                            const float* __restrict__ step, float lr, float beta1,
+                                                            float beta2, float eps, float max_norm,
+                                                            float* __restrict__ norm_out) {
+  __shared__ float s_coef;
+  if (threadIdx.x < kWave) {
+    double x = threadIdx.x < kNormBlocks ? partial[threadIdx.x] : 0.0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, kWave);  // same value in every lane/block
+    const float norm = static_cast<float>(sqrt(x));
+    if (threadIdx.x == 0) {
+      float coef = 1.f;
+      if (max_norm > 0.f) {
+        coef = max_norm / (norm + 1e-6f);   // clip_grad_norm_: clip_coef, clamped to 1
+        coef = coef < 1.f ? coef : 1.f;
+      }
+      s_coef = coef;
+      if (blockIdx.x == 0 && norm_out != nullptr) norm_out[0] = norm;
+    }
+  }
+  __syncthreads();
+  const float coef = s_coef;
+  const double t = static_cast<double>(step[0]);
+  const float step_size = static_cast<float>(static_cast<double>(lr) / (1.0 - pow(static_cast<double>(beta1), t)));
+  const float bc2_sqrt = static_cast<float>(sqrt(1.0 - pow(static_cast<double>(beta2), t)));
+  const float w1 = static_cast<float>(1.0 - static_cast<double>(beta1));
+  const float w2 = static_cast<float>(1.0 - static_cast<double>(beta2));
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kOptThreads + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * kOptThreads) {
+    const float gi = g[i] * coef;
+    g[i] = gi;
+    const float mi = m[i] + w1 * (gi - m[i]);          // exp_avg.lerp_(grad, 1 - beta1)
+    const float vi = v[i] * beta2 + w2 * gi * gi;      // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] = p[i] - step_size * (mi / denom);            // param.addcdiv_(exp_avg, denom, -step_size)
+  }
+}
+
+}  // namespace
+}  // namespace asvrl
+
+using namespace asvrl;
+
+extern "C" int asvrl_adam_clip(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+                               float* step, float lr, float beta1, float beta2, float eps, float max_norm,
+                               float* norm_out, double* work, void* stream) {
+  ASVRL_REQUIRE(params && grads && exp_avg && exp_avg_sq && step && work, "asvrl_adam_clip: null argument");
+  ASVRL_REQUIRE(n >= 0, "asvrl_adam_clip: negative size");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(sumsq_kernel, dim3(kNormBlocks), dim3(kOptThreads), 0, as_stream(stream), grads, n, work,
+                     step);
+  if (int rc = check_launch("asvrl_adam_clip(norm)")) return rc;
+  int64_t nb = (n + 4LL * kOptThreads - 1) / (4LL * kOptThreads);
+  nb = nb < 1 ? 1 : (nb > 1024 ? 1024 : nb);
+  hipLaunchKernelGGL(adam_kernel, dim3(static_cast<unsigned>(nb)), dim3(kOptThreads), 0, as_stream(stream), params,
+                     grads, exp_avg, exp_avg_sq, n, work, step, lr, beta1, beta2, eps, max_norm, norm_out);
+  return check_launch("asvrl_adam_clip(step)");
+}

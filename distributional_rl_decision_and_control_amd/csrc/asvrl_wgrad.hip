@@ -1,0 +1,291 @@
+// asvrl_wgrad.hip -- weight gradients of the learner's Linear layers on gfx950:
+//   dW[m][k] = sum_r dZ[r][m] * X[r][k],   db[m] = sum_r dZ[r][m]
+// over R rows of bf16 activations (the torch backward's grad_weight = dZ^T X and
+// grad_bias = dZ.sum(0) of every nn.Linear on the path, AC_IQN_model.py:398-404, 476-479).
+//
+// The reduction runs over the ROW index, which is the memory-major index of both operands,
+// so an MFMA operand fragment ("8 consecutive rows of one column") is a transposed read:
+// each workgroup stages 32-row chunks of dZ and X into LDS with coalesced 16-byte loads
+// (next chunk prefetched into registers while the current one is consumed) and feeds
+// v_mfma_f32_32x32x16_bf16 from ds_read_b64_tr_b16. LDS rows are padded to a stride of
+// 64 mod 256 bytes, which makes the 32-lane halves of every transposed read conflict-free.
+// Each wave owns a fixed set of 32x32 output blocks for the whole R range of its workgroup;
+// workgroups write f32 partials that a second launch sums in a fixed order (deterministic).
+#include "asvrl_common.h"
+
+namespace asvrl {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWgThreads = 256;
+constexpr int kRC = 32;           // rows per staged chunk (2 MFMA k-steps)
+constexpr int kMaxGroups = 256;
+
+__host__ __device__ constexpr int lds_stride(int cols) {  // bytes, == 64 (mod 256)
+  return ((2 * cols - 64 + 255) / 256) * 256 + 64;
+}
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// Operand fragment of rows [r0, r0 + 16) x columns [c0, c0 + 32) of a row-major LDS image:
+// lane l gets column c0 + (l & 31), rows r0 + 8(l >> 5) + j, j = 0..7.
+__device__ __forceinline__ bf16x8 frag_tr(const char* img, int stride, int r0, int c0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int col = c0 + 16 * (g & 1) + 4 * p;
+  const int row = r0 + 8 * (g >> 1) + q;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const char* a0 = img + row * stride + col * 2;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * stride));
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int N, int STEP>
+__device__ __forceinline__ void load_rows(u32x4 (&r)[N], const __bf16* __restrict__ base, int64_t ld, int64_t row,
+                                          int c8) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) r[i] = *reinterpret_cast<const u32x4*>(base + (row + i * STEP) * ld + c8 * 8);
+}
+
+template <int M, int K>
+struct Shape {
+  static constexpr int NMB = M / 32, NKB = K / 32, NB = NMB * NKB, NBW = NB / 4;
+  static constexpr bool kWide = NBW >= NKB;                // wave covers whole m-blocks
+  static constexpr int NMW = kWide ? NBW / NKB : 1;        // m-blocks per wave
+  static constexpr int NKW = kWide ? NKB : NBW;            // k-blocks per wave
+  static constexpr int SZ = lds_stride(M), SX = lds_stride(K);
+  static constexpr int CZ = kRC * M / 8 / kWgThreads;      // 16-B chunks per thread (dZ)
+  static constexpr int CX = kRC * K / 8 / kWgThreads;      // (X)
+  static_assert(M % 32 == 0 && K % 32 == 0 && NB % 4 == 0, "block grid must split over 4 waves");
+  static_assert(kWide ? (NBW % NKB == 0) : (NKB % NBW == 0), "wave blocks must tile rows or columns");
+  static_assert(CZ >= 1 && CX >= 1, "at least one chunk per thread");
+};
+
+template <int M, int K>
+__global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const __bf16* __restrict__ dz, int64_t ldz,
+                                                            const __bf16* __restrict__ x, int64_t ldx, int chunks,
+                                                            int chunks_per_group, float* __restrict__ partial) {
+  using S = Shape<M, K>;
+  __shared__ __attribute__((aligned(16))) char lz[kRC * S::SZ];
+  __shared__ __attribute__((aligned(16))) char lx[kRC * S::SX];
+  __shared__ float lbias[kWgThreads][8];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int c_beg = blockIdx.x * chunks_per_group;
+  const int c_end = min(chunks, c_beg + chunks_per_group);
+
+  // thread t always stages column chunk t % (M/8) (resp. K/8), rows t / (M/8) + i * (256*8/M)
+  const int zc8 = t % (M / 8), zr = t / (M / 8);
+  const int xc8 = t % (K / 8), xr = t / (K / 8);
+  constexpr int ZRS = kWgThreads * 8 / M, XRS = kWgThreads * 8 / K;   // row step between a thread's chunks
+  u32x4 rz[S::CZ], rx[S::CX];
+  float bacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  f32x16 acc[S::NMW * S::NKW];
+#pragma unroll
+  for (int i = 0; i < S::NMW * S::NKW; ++i) acc[i] = f32x16{};
+  const int mb0 = S::kWide ? w * S::NMW : (w * S::NBW) / S::NKB;
+  const int kb0 = S::kWide ? 0 : (w * S::NBW) % S::NKB;
+
+  if (c_beg < c_end) {
+    load_rows<S::CZ, ZRS>(rz, dz, ldz, static_cast<int64_t>(c_beg) * kRC + zr, zc8);
+    load_rows<S::CX, XRS>(rx, x, ldx, static_cast<int64_t>(c_beg) * kRC + xr, xc8);
+  }
+  for (int c = c_beg; c < c_end; ++c) {
+#pragma unroll
+    for (int i = 0; i < S::CZ; ++i) {
+      *reinterpret_cast<u32x4*>(lz + (zr + i * ZRS) * S::SZ + zc8 * 16) = rz[i];
+      const bf16x8 v = __builtin_bit_cast(bf16x8, rz[i]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bacc[j] += static_cast<float>(v[j]);
+    }
+#pragma unroll
+    for (int i = 0; i < S::CX; ++i) *reinterpret_cast<u32x4*>(lx + (xr + i * XRS) * S::SX + xc8 * 16) = rx[i];
+    __syncthreads();
+    if (c + 1 < c_end) {   // prefetch under the MFMAs
+      load_rows<S::CZ, ZRS>(rz, dz, ldz, static_cast<int64_t>(c + 1) * kRC + zr, zc8);
+      load_rows<S::CX, XRS>(rx, x, ldx, static_cast<int64_t>(c + 1) * kRC + xr, xc8);
+    }
+#pragma unroll
+    for (int ks = 0; ks < kRC / 16; ++ks) {
+      bf16x8 fa[S::NMW], fb[S::NKW];
+#pragma unroll
+      for (int i = 0; i < S::NMW; ++i) fa[i] = frag_tr(lz, S::SZ, ks * 16, (mb0 + i) * 32, lane);
+#pragma unroll
+      for (int j = 0; j < S::NKW; ++j) fb[j] = frag_tr(lx, S::SX, ks * 16, (kb0 + j) * 32, lane);
+#pragma unroll
+      for (int i = 0; i < S::NMW; ++i)
+#pragma unroll
+        for (int j = 0; j < S::NKW; ++j) acc[i * S::NKW + j] = mfma(fa[i], fb[j], acc[i * S::NKW + j]);
+    }
+    __syncthreads();
+  }
+
+  // partial dW block (mb, kb): lane l holds column l&31, rows (reg&3) + 8(reg>>2) + 4h
+  float* pw = partial + static_cast<int64_t>(blockIdx.x) * (M * K + M);
+  const int h = lane >> 5, col = lane & 31;
+#pragma unroll
+  for (int i = 0; i < S::NMW; ++i)
+#pragma unroll
+    for (int j = 0; j < S::NKW; ++j)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int m = (mb0 + i) * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        pw[m * K + (kb0 + j) * 32 + col] = acc[i * S::NKW + j][reg];
+      }
+  // partial db: threads sharing a column chunk fold their sums
+#pragma unroll
+  for (int j = 0; j < 8; ++j) lbias[t][j] = bacc[j];
+  __syncthreads();
+  if (t < M / 8) {
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int u = t; u < kWgThreads; u += M / 8)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += lbias[u][j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pw[M * K + t * 8 + j] = s[j];
+  }
+}
+
+// dw[k] = sum_r dq[r] * X[r][k], db = sum_r dq[r] for an output layer with one unit.
+// Thread t reads 16 bytes (8 columns) of row t / (K/8) + i * RP: RP rows in flight per block.
+template <int K>
+__global__ __launch_bounds__(kWgThreads) void wgrad_vec_kernel(const float* __restrict__ dq,
+                                                                const __bf16* __restrict__ x, int64_t ldx, int R,
+                                                                int rows_per_group, float* __restrict__ partial) {
+  constexpr int C8 = K / 8, RP = kWgThreads / C8;
+  const int t = threadIdx.x, c8 = t % C8, rr = t / C8;
+  const int r_beg = blockIdx.x * rows_per_group, r_end = min(R, r_beg + rows_per_group);
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float b = 0.f;
+  for (int r = r_beg + rr; r < r_end; r += RP) {
+    const float d = dq[r];
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + static_cast<int64_t>(r) * ldx + c8 * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] += d * static_cast<float>(v[j]);
+    b += d;
+  }
+  __shared__ float sa[kWgThreads][9];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sa[t][j] = a[j];
+  sa[t][8] = b;
+  __syncthreads();
+  float* pw = partial + static_cast<int64_t>(blockIdx.x) * (K + 1);
+  if (t < K) {   // column t = 8 * (t / 8) + t % 8 lives in threads with c8 == t / 8
+    float s = 0.f;
+    for (int u = t / 8; u < kWgThreads; u += C8) s += sa[u][t % 8];
+    pw[t] = s;
+  }
+  if (t == 0) {
+    float s = 0.f;
+    for (int u = 0; u < kWgThreads; u += C8) s += sa[u][8];   // c8 == 0 threads saw every row once
+    pw[K] = s;
+  }
+}
+
+// out[i] (+)= sum_g partial[g][i], i < nw + nb (the trailing nb go to db). A block covers 64
+// outputs; its 4 waves take groups g = 4u + wave with two independent accumulators each, and
+// the 4 wave sums are folded in a fixed order (deterministic).
+__global__ __launch_bounds__(kWgThreads) void partial_sum_kernel(const float* __restrict__ partial, int groups,
+                                                                  int nw, int nb, float* __restrict__ dw,
+                                                                  float* __restrict__ db, int accumulate) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;
+  const int n = nw + nb;
+  float s0 = 0.f, s1 = 0.f;
+  if (i < n) {
+    int g = wv;
+    for (; g + 4 < groups; g += 8) {
+      s0 += partial[static_cast<int64_t>(g) * n + i];
+      s1 += partial[static_cast<int64_t>(g + 4) * n + i];
+    }
+    if (g < groups) s0 += partial[static_cast<int64_t>(g) * n + i];
+  }
+  __shared__ float red[4][64];
+  red[wv][lane] = s0 + s1;
+  __syncthreads();
+  if (wv != 0 || i >= n) return;
+  if (i >= nw && db == nullptr) return;
+  const float s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  float* o = i < nw ? dw + i : db + (i - nw);
+  *o = accumulate ? *o + s : s;
+}
+
+template <int M, int K>
+int launch_wgrad(const __bf16* dz, int64_t ldz, const __bf16* x, int64_t ldx, int R, float* work, hipStream_t st,
+                 int& groups) {
+  const int chunks = R / kRC;
+  // partial traffic is groups * M * K floats: cap it near 16 MB for the large layers
+  int cap = (1 << 22) / (M * K);
+  cap = cap < 64 ? 64 : (cap > kMaxGroups ? kMaxGroups : cap);
+  groups = chunks < cap ? chunks : cap;
+  const int per = (chunks + groups - 1) / groups;
+  groups = (chunks + per - 1) / per;
+  hipLaunchKernelGGL((wgrad_kernel<M, K>), dim3(groups), dim3(kWgThreads), 0, st, dz, ldz, x, ldx, chunks, per,
+                     work);
+  return check_launch("asvrl_linear_wgrad");
+}
+
+}  // namespace
+}  // namespace asvrl
+
+using namespace asvrl;
+
+extern "C" int64_t asvrl_linear_wgrad_workspace(int32_t M, int32_t K) {
+  return static_cast<int64_t>(kMaxGroups) * (static_cast<int64_t>(M) * K + M);
+}
+
+extern "C" int asvrl_linear_wgrad(const void* dz, int64_t ldz, const void* x, int64_t ldx, int32_t R, int32_t M,
+                                  int32_t K, float* dw, float* db, int32_t accumulate, float* work,
+                                  int64_t work_floats, void* stream) {
+  ASVRL_REQUIRE(dz && x && dw && work, "asvrl_linear_wgrad: null argument");
+  ASVRL_REQUIRE(R >= 0 && R % kRC == 0, "asvrl_linear_wgrad: R must be a multiple of 32");
+  ASVRL_REQUIRE(ldz >= M && ldx >= K && ldz % 8 == 0 && ldx % 8 == 0,
+                "asvrl_linear_wgrad: leading dimensions must cover the rows and be multiples of 8");
+  ASVRL_REQUIRE((reinterpret_cast<uintptr_t>(dz) | reinterpret_cast<uintptr_t>(x)) % 16 == 0,
+                "asvrl_linear_wgrad: operands must be 16-byte aligned");
+  ASVRL_REQUIRE(work_floats >= asvrl_linear_wgrad_workspace(M, K), "asvrl_linear_wgrad: workspace too small");
+  if (R == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  const __bf16* z = static_cast<const __bf16*>(dz);
+  const __bf16* xx = static_cast<const __bf16*>(x);
+  int groups = 0, rc = 0;
+  if (M == 256 && K == 64) rc = launch_wgrad<256, 64>(z, ldz, xx, ldx, R, work, st, groups);
+  else if (M == 128 && K == 256) rc = launch_wgrad<128, 256>(z, ldz, xx, ldx, R, work, st, groups);
+  else if (M == 128 && K == 128) rc = launch_wgrad<128, 128>(z, ldz, xx, ldx, R, work, st, groups);
+  else if (M == 64 && K == 64) rc = launch_wgrad<64, 64>(z, ldz, xx, ldx, R, work, st, groups);
+  else ASVRL_REQUIRE(false, "asvrl_linear_wgrad: unsupported (M, K)");
+  if (rc) return rc;
+  const int n = M * K + M;
+  hipLaunchKernelGGL(partial_sum_kernel, dim3((n + 63) / 64), dim3(kWgThreads), 0, st, work, groups, M * K, M, dw,
+                     db, accumulate);
+  return check_launch("asvrl_linear_wgrad(sum)");
+}
+
+extern "C" int asvrl_linear_wgrad_vec(const float* dq, const void* x, int64_t ldx, int32_t R, int32_t K, float* dw,
+                                      float* db, int32_t accumulate, float* work, int64_t work_floats, void* stream) {
+  ASVRL_REQUIRE(dq && x && dw && work, "asvrl_linear_wgrad_vec: null argument");
+  ASVRL_REQUIRE(K == 128 || K == 256 || K == 64, "asvrl_linear_wgrad_vec: K must be 64, 128 or 256");
+  ASVRL_REQUIRE(ldx >= K && ldx % 8 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0,
+                "asvrl_linear_wgrad_vec: x must be 16-byte aligned with ldx >= K, a multiple of 8");
+  ASVRL_REQUIRE(work_floats >= static_cast<int64_t>(kMaxGroups) * (K + 1), "asvrl_linear_wgrad_vec: workspace too small");
+  if (R <= 0) return 0;
+  hipStream_t st = as_stream(stream);
+  int groups = R < kMaxGroups ? R : kMaxGroups;
+  const int per = (R + groups - 1) / groups;
+  groups = (R + per - 1) / per;
+  const __bf16* xx = static_cast<const __bf16*>(x);
+  if (K == 128) hipLaunchKernelGGL(wgrad_vec_kernel<128>, dim3(groups), dim3(kWgThreads), 0, st, dq, xx, ldx, R, per, work);
+  else if (K == 256) hipLaunchKernelGGL(wgrad_vec_kernel<256>, dim3(groups), dim3(kWgThreads), 0, st, dq, xx, ldx, R, per, work);
+  else hipLaunchKernelGGL(wgrad_vec_kernel<64>, dim3(groups), dim3(kWgThreads), 0, st, dq, xx, ldx, R, per, work);
+  if (int rc = check_launch("asvrl_linear_wgrad_vec")) return rc;
+  hipLaunchKernelGGL(partial_sum_kernel, dim3((K + 1 + 63) / 64), dim3(kWgThreads), 0, st, work, groups, K, 1, dw,
+                     db, accumulate);
+  return check_launch("asvrl_linear_wgrad_vec(sum)");
+}

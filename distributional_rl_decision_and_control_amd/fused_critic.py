@@ -16,7 +16,7 @@ import ctypes as C
 import torch
 
 from . import _abi
-from .learner import _clip, _null
+from .learner import clip_and_step
 from .policy.AC_IQN_model import encode_observation
 
 _IDX = {}
@@ -49,12 +49,9 @@ class CriticPack:
         self.w2 = torch.empty(128 * 128, **bf)
         self.w2t = torch.empty(128 * 128, **bf)
         self.w1t = torch.empty(256 * 128, **bf)
-        self._w2t_f = torch.empty(128, 128, device=dev)
-        self._w1t_f = torch.empty(256, 128, device=dev)
         self.idx = dict(wc=frag_index(256, 64, False, dev), w1=frag_index(128, 256, True, dev),
                         w2=frag_index(128, 128, True, dev), w2t=frag_index(128, 128, True, dev),
                         w1t=frag_index(256, 128, True, dev))
-        self.refresh()
         s = _abi.AsvCriticWeights()
         s.wc_frag, s.w1_frag, s.w2_frag = self.wc.data_ptr(), self.w1.data_ptr(), self.w2.data_ptr()
         s.w2t_frag, s.w1t_frag = self.w2t.data_ptr(), self.w1t.data_ptr()
@@ -62,31 +59,26 @@ class CriticPack:
         s.b2, s.wo = critic.hidden_layer_2.bias.data_ptr(), critic.output_layer.weight.data_ptr()
         s.bo = critic.output_layer.bias.data_ptr()
         self.struct = s
+        self.refresh()
+
+    def refresh(self, stream=None):
+        """Re-pack from the critic's current f32 weights: one asvrl_critic_pack launch."""
+        c = self.critic
+        rc = _abi.lib().asvrl_critic_pack(_abi.ptr(c.cos_embedding.weight), _abi.ptr(c.hidden_layer.weight),
+                                          _abi.ptr(c.hidden_layer_2.weight), C.byref(self.struct),
+                                          _abi.stream_ptr(stream))
+        _abi.check(rc, "asvrl_critic_pack")
 
     @torch.no_grad()
-    def refresh(self):
+    def reference_images(self):
+        """The same five images by torch gathers (frag_index), for the packing test."""
         c = self.critic
-        W1 = c.hidden_layer.weight
-        W2 = c.hidden_layer_2.weight
-        torch.index_select(c.cos_embedding.weight.reshape(-1), 0, self.idx["wc"], out=self._tmp(self.wc))
-        self.wc.copy_(self._t)
-        torch.index_select(W1.reshape(-1), 0, self.idx["w1"], out=self._tmp(self.w1))
-        self.w1.copy_(self._t)
-        torch.index_select(W2.reshape(-1), 0, self.idx["w2"], out=self._tmp(self.w2))
-        self.w2.copy_(self._t)
-        self._w2t_f.copy_(W2.t())
-        torch.index_select(self._w2t_f.reshape(-1), 0, self.idx["w2t"], out=self._tmp(self.w2t))
-        self.w2t.copy_(self._t)
-        self._w1t_f.copy_(W1.t())
-        torch.index_select(self._w1t_f.reshape(-1), 0, self.idx["w1t"], out=self._tmp(self.w1t))
-        self.w1t.copy_(self._t)
-
-    def _tmp(self, like):
-        t = getattr(self, "_tbuf", None)
-        if t is None or t.numel() < like.numel():
-            self._tbuf = torch.empty(256 * 128, dtype=torch.float32, device=like.device)
-        self._t = self._tbuf[:like.numel()]
-        return self._t
+        W1, W2 = c.hidden_layer.weight, c.hidden_layer_2.weight
+        out = {}
+        for name, W in (("wc", c.cos_embedding.weight), ("w1", W1), ("w2", W2), ("w2t", W2.t().contiguous()),
+                        ("w1t", W1.t().contiguous())):
+            out[name] = torch.index_select(W.reshape(-1), 0, self.idx[name]).to(torch.bfloat16)
+        return out
 
 
 def critic_forward(pack, F, G, taus, N, q=None, stream=None):
@@ -116,6 +108,9 @@ class TrainBuffers:
         self.q = torch.empty(R, **f)
         self.dF = torch.empty(B, 256, **f)
         self.dG = torch.empty(B, 128, **f)
+        self.work_floats = max(int(_abi.lib().asvrl_linear_wgrad_workspace(M, K))
+                               for M, K in ((256, 64), (128, 256), (128, 128)))
+        self.work = torch.empty(self.work_floats, **f)
         a = _abi.AsvCriticActs()
         a.cos, a.h0, a.dzc, a.h1g = self.cos.data_ptr(), self.h0.data_ptr(), self.dzc.data_ptr(), self.h1g.data_ptr()
         a.dz1, a.h2, a.dz2, a.dq = self.dz1.data_ptr(), self.h2.data_ptr(), self.dz2.data_ptr(), self.dq.data_ptr()
@@ -139,26 +134,31 @@ def critic_actor_grad(pack, F, G, taus, N, q, dG, stream=None):
     _abi.check(rc, "asvrl_critic_actor_grad")
 
 
-def _splitk_dw(dz, x, out):
-    """out (f32, (O, I)) <- dz^T x with dz (R, O), x (R, I) bf16, as a split-K batched GEMM."""
-    R = dz.shape[0]
-    g = max(1, R // 512)
-    while R % g:
-        g -= 1
-    part = torch.bmm(dz.view(g, R // g, dz.shape[1]).transpose(1, 2), x.view(g, R // g, x.shape[1]))
-    torch.sum(part, 0, dtype=torch.float32, out=out)
+def linear_wgrad(dz, x, dw, db, work, accumulate=False, stream=None):
+    """dw (M, K) f32 <- dz^T x, db (M,) <- dz.sum(0) with dz (R, M), x (R, K) bf16 (asvrl_linear_wgrad)."""
+    R, M = dz.shape
+    K = x.shape[1]
+    rc = _abi.lib().asvrl_linear_wgrad(_abi.ptr(dz), dz.stride(0), _abi.ptr(x), x.stride(0), R, M, K, _abi.ptr(dw),
+                                       _abi.ptr(db), int(accumulate), _abi.ptr(work), work.numel(),
+                                       _abi.stream_ptr(stream))
+    _abi.check(rc, "asvrl_linear_wgrad")
+
+
+def linear_wgrad_vec(dq, x, dw, db, work, accumulate=False, stream=None):
+    """dw (K,) <- dq^T x, db (1,) <- dq.sum() with dq (R,) f32, x (R, K) bf16."""
+    R, K = x.shape
+    rc = _abi.lib().asvrl_linear_wgrad_vec(_abi.ptr(dq), _abi.ptr(x), x.stride(0), R, K, _abi.ptr(dw), _abi.ptr(db),
+                                           int(accumulate), _abi.ptr(work), work.numel(), _abi.stream_ptr(stream))
+    _abi.check(rc, "asvrl_linear_wgrad_vec")
 
 
 def trunk_weight_grads(critic, bufs):
-    """Weight/bias gradients of the fused trunk layers from the TRAIN activations."""
-    _splitk_dw(bufs.dzc, bufs.cos, critic.cos_embedding.weight.grad)
-    torch.sum(bufs.dzc, 0, dtype=torch.float32, out=critic.cos_embedding.bias.grad)
-    _splitk_dw(bufs.dz1, bufs.h0, critic.hidden_layer.weight.grad)
-    torch.sum(bufs.dz1, 0, dtype=torch.float32, out=critic.hidden_layer.bias.grad)
-    _splitk_dw(bufs.dz2, bufs.h1g, critic.hidden_layer_2.weight.grad)
-    torch.sum(bufs.dz2, 0, dtype=torch.float32, out=critic.hidden_layer_2.bias.grad)
-    _splitk_dw(bufs.dq.view(-1, 1).to(torch.bfloat16), bufs.h2, critic.output_layer.weight.grad)
-    critic.output_layer.bias.grad.copy_(bufs.dq.sum().view(1))
+    """Weight/bias gradients of the fused trunk layers from the TRAIN activations: four
+    asvrl_linear_wgrad launches pairs (MFMA reduction over the B*N rows + partial sum)."""
+    linear_wgrad(bufs.dzc, bufs.cos, critic.cos_embedding.weight.grad, critic.cos_embedding.bias.grad, bufs.work)
+    linear_wgrad(bufs.dz1, bufs.h0, critic.hidden_layer.weight.grad, critic.hidden_layer.bias.grad, bufs.work)
+    linear_wgrad(bufs.dz2, bufs.h1g, critic.hidden_layer_2.weight.grad, critic.hidden_layer_2.bias.grad, bufs.work)
+    linear_wgrad_vec(bufs.dq, bufs.h2, critic.output_layer.weight.grad, critic.output_layer.bias.grad, bufs.work)
 
 
 def fused_supported(critic, B, N):
@@ -178,6 +178,11 @@ class FusedACIQN:
         self.q_pi = torch.empty(B * N, dtype=torch.float32, device=dev)
         self.dG_pi = torch.empty(B, 128, dtype=torch.float32, device=dev)
         self.B, self.N = B, N
+        self.target_dirty = False  # the pack was just built
+
+    def target_changed(self):
+        """Call after the target critic's weights change (hard/soft update): re-packed lazily."""
+        self.target_dirty = True
 
 
 def ac_iqn_update_fused(fz, policy_local, policy_target, actor_opt, critic_opt, critic_grads, actor_grads, states,
@@ -187,7 +192,9 @@ def ac_iqn_update_fused(fz, policy_local, policy_target, actor_opt, critic_opt, 
     tcritic = policy_target.critic
     B, N = fz.B, fz.N
     dev = fz.bufs.q.device
-    amp = torch.autocast("cuda", dtype=amp_dtype) if amp_dtype is not None else _null()
+    # the actor and the encoders stay fp32 here: their GEMMs are small and autocast would
+    # re-cast every weight to bf16 on every call (54 cast kernels per step); only the critic
+    # trunk, which holds the FLOPs, runs bf16 (in the fused kernels)
 
     def draw(t):
         return torch.rand(B, N, device=dev) if t is None else t.reshape(B, N).float().contiguous()
@@ -195,12 +202,13 @@ def ac_iqn_update_fused(fz, policy_local, policy_target, actor_opt, critic_opt, 
     # ---- critic (agent.py:395-416)
     critic_grads.zero_()
     with torch.no_grad():
-        with amp:
-            na = policy_target.actor(next_states)
+        na = policy_target.actor(next_states)
         Ft = encode_observation(tcritic.self_encoder, tcritic.object_encoder, next_states, tcritic.max_object_num,
                                 tcritic.object_dimension, tcritic.object_feature_dimension).float().contiguous()
         Gt = tcritic.action_encoder(na.float()).contiguous()
-        fz.target_pack.refresh()
+        if fz.target_dirty:
+            fz.target_pack.refresh()
+            fz.target_dirty = False
         q_next = critic_forward(fz.target_pack, Ft, Gt, draw(taus[0]), N, q=fz.q_next)
         q_targets = (rewards + gamma * q_next * (1.0 - dones)).contiguous()
     F = encode_observation(critic.self_encoder, critic.object_encoder, states, critic.max_object_num,
@@ -213,12 +221,10 @@ def ac_iqn_update_fused(fz, policy_local, policy_target, actor_opt, critic_opt, 
     torch.autograd.backward([F, G], [fz.bufs.dF, fz.bufs.dG])
     if sync is not None:
         sync(critic_grads)
-    cgn = _clip(critic_grads.params, max_norm)
-    critic_opt.step()
+    cgn = clip_and_step(critic_opt, critic_grads, max_norm)
     # ---- actor through the updated critic (agent.py:419-427)
     fz.local_pack.refresh()
-    with amp:
-        a_out = actor(states)
+    a_out = actor(states)
     with torch.no_grad():
         F2 = encode_observation(critic.self_encoder, critic.object_encoder, states, critic.max_object_num,
                                 critic.object_dimension, critic.object_feature_dimension).float().contiguous()
@@ -229,6 +235,5 @@ def ac_iqn_update_fused(fz, policy_local, policy_target, actor_opt, critic_opt, 
     actor_grads.assign(g)
     if sync is not None:
         sync(actor_grads)
-    agn = _clip(actor_grads.params, max_norm)
-    actor_opt.step()
+    agn = clip_and_step(actor_opt, actor_grads, max_norm)
     return critic_loss.detach(), actor_loss.detach(), cgn, agn

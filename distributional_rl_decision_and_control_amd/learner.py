@@ -7,9 +7,12 @@ autocast. Data-parallel training passes a GradSync, which all-reduces each netwo
 gradient over RCCL between backward and clip -- twice per AC-IQN step (critic, then actor
 through the *updated* critic, agent.py:395-427), once for IQN / Rainbow.
 """
+import ctypes as C
+
 import torch
 import torch.distributed as dist
 
+from . import _abi
 from .learn_ops import c51_project, quantile_huber_loss
 
 
@@ -57,6 +60,59 @@ def _clip(params, max_norm):
     return torch.nn.utils.clip_grad_norm_(params, max_norm)
 
 
+class FusedAdam:
+    """clip_grad_norm_(params, max_norm) + optim.Adam(params, lr).step() (agent.py:75-76,98,
+    415-416) as the two launches of asvrl_adam_clip over flat buffers.
+
+    The parameters are re-pointed at one flat f32 buffer (p.data becomes a view, so modules,
+    state_dict and load_state_dict keep working) and their .grad at a FlatGrads buffer in the
+    same order; `grads` is that FlatGrads, to be all-reduced by GradSync before step().
+    Construct it before anything caches parameter pointers (CriticPack)."""
+
+    def __init__(self, params, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, max_norm=0.5):
+        self.params = [p for p in params if p.requires_grad]
+        dev = self.params[0].device
+        n = sum(p.numel() for p in self.params)
+        self.flat = torch.empty(n, dtype=torch.float32, device=dev)
+        off = 0
+        with torch.no_grad():
+            for p in self.params:
+                k = p.numel()
+                self.flat[off:off + k].copy_(p.reshape(-1))
+                p.data = self.flat[off:off + k].view_as(p)
+                off += k
+        self.grads = FlatGrads(self.params)
+        self.exp_avg = torch.zeros_like(self.flat)
+        self.exp_avg_sq = torch.zeros_like(self.flat)
+        self.step_t = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.norm = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.work = torch.zeros(64, dtype=torch.float64, device=dev)
+        self.lr, self.betas, self.eps, self.max_norm = float(lr), tuple(betas), float(eps), float(max_norm)
+        self.n = n
+
+    def zero_grad(self):
+        self.grads.zero_()
+
+    def step(self):
+        """Clip + Adam; returns the pre-clip global norm as a 0-d device tensor."""
+        rc = _abi.lib().asvrl_adam_clip(
+            _abi.ptr(self.flat), _abi.ptr(self.grads.flat), _abi.ptr(self.exp_avg), _abi.ptr(self.exp_avg_sq),
+            self.n, _abi.ptr(self.step_t), self.lr, self.betas[0], self.betas[1], self.eps, self.max_norm,
+            _abi.ptr(self.norm), _abi.ptr(self.work), _abi.stream_ptr(None))
+        _abi.check(rc, "asvrl_adam_clip")
+        return self.norm[0]
+
+
+def clip_and_step(opt, grads, max_norm):
+    """Global-norm clip then optimizer step; returns the pre-clip norm (device scalar)."""
+    if isinstance(opt, FusedAdam):
+        assert opt.max_norm == max_norm and opt.grads.flat.data_ptr() == grads.flat.data_ptr()
+        return opt.step()
+    n = _clip(grads.params, max_norm)
+    opt.step()
+    return n
+
+
 def ac_iqn_update(policy_local, policy_target, actor_opt, critic_opt, critic_grads, actor_grads, states, actions,
                   rewards, next_states, dones, gamma=0.99, num_tau=8, taus=(None, None, None), sync=None,
                   amp_dtype=None, max_norm=0.5):
@@ -77,8 +133,7 @@ def ac_iqn_update(policy_local, policy_target, actor_opt, critic_opt, critic_gra
     critic_loss.backward()
     if sync is not None:
         sync(critic_grads)
-    cgn = _clip(critic_grads.params, max_norm)
-    critic_opt.step()
+    cgn = clip_and_step(critic_opt, critic_grads, max_norm)
     # ---- actor through the updated critic (agent.py:419-427); only actor grads are needed
     with amp:
         a_out = actor(states)
@@ -88,8 +143,7 @@ def ac_iqn_update(policy_local, policy_target, actor_opt, critic_opt, critic_gra
     actor_grads.assign(g)
     if sync is not None:
         sync(actor_grads)
-    agn = _clip(actor_grads.params, max_norm)
-    actor_opt.step()
+    agn = clip_and_step(actor_opt, actor_grads, max_norm)
     return critic_loss.detach(), actor_loss.detach(), cgn, agn
 
 
@@ -111,8 +165,7 @@ def iqn_update(policy_local, policy_target, opt, grads, states, actions, rewards
     loss.backward()
     if sync is not None:
         sync(grads)
-    gn = _clip(grads.params, max_norm)
-    opt.step()
+    gn = clip_and_step(opt, grads, max_norm)
     return loss.detach(), gn
 
 
@@ -138,8 +191,7 @@ def rainbow_update(policy_local, policy_target, opt, grads, support, states, act
     (weights * loss).mean().backward()
     if sync is not None:
         sync(grads)
-    gn = _clip(grads.params, max_norm)
-    opt.step()
+    gn = clip_and_step(opt, grads, max_norm)
     return loss.detach(), gn
 
 

@@ -22,7 +22,7 @@ import torch
 
 from .fused_critic import FusedACIQN, ac_iqn_update_fused, fused_supported
 from .learn_ops import DeviceReplay, split_rows
-from .learner import FlatGrads, GradSync, ac_iqn_update, iqn_update
+from .learner import FlatGrads, FusedAdam, GradSync, ac_iqn_update, iqn_update
 from .policy.AC_IQN_model import AC_IQN_Policy
 from .policy.IQN_model import IQN_Policy
 from .vec_env import VecMarineNavEnv, split_obs
@@ -36,7 +36,8 @@ class VecTrainer:
                  width=55.0, batch_size=4096, num_tau=32, buffer_size=4_000_000, lr=1e-4, gamma=0.99,
                  learning_starts=None, target_update_interval=2500, total_timesteps=6_000_000,
                  exploration_fraction=0.25, initial_eps=0.6, final_eps=0.05, amp_dtype=torch.bfloat16, seed=0,
-                 device="cuda", sync=None, graphs=False, schedule=None, net_seed=100, fused=True):
+                 device="cuda", sync=None, graphs=False, schedule=None, net_seed=100, fused=True,
+                 fused_adam=True):
         self.device = torch.device(device)
         self.agent_type = agent_type
         self.continuous = agent_type == "AC-IQN"
@@ -59,10 +60,16 @@ class VecTrainer:
                                         device=self.device, seed=net_seed)
             for p in list(self.target.actor.parameters()) + list(self.target.critic.parameters()):
                 p.requires_grad_(False)
-            self.critic_grads = FlatGrads(self.local.critic.parameters())
-            self.actor_grads = FlatGrads(self.local.actor.parameters())
-            self.actor_opt = torch.optim.Adam(self.local.actor.parameters(), lr=lr, capturable=capturable)
-            self.critic_opt = torch.optim.Adam(self.local.critic.parameters(), lr=lr, capturable=capturable)
+            if fused_adam:
+                # clip + Adam as two kernels over flat buffers (must precede FusedACIQN's packs)
+                self.actor_opt = FusedAdam(self.local.actor.parameters(), lr=lr)
+                self.critic_opt = FusedAdam(self.local.critic.parameters(), lr=lr)
+                self.actor_grads, self.critic_grads = self.actor_opt.grads, self.critic_opt.grads
+            else:
+                self.critic_grads = FlatGrads(self.local.critic.parameters())
+                self.actor_grads = FlatGrads(self.local.actor.parameters())
+                self.actor_opt = torch.optim.Adam(self.local.actor.parameters(), lr=lr, capturable=capturable)
+                self.critic_opt = torch.optim.Adam(self.local.critic.parameters(), lr=lr, capturable=capturable)
             self.action_dim = 2
             self.fused = None
             if fused and amp_dtype is not None and fused_supported(self.local.critic, batch_size, num_tau):
@@ -72,8 +79,12 @@ class VecTrainer:
             self.target = IQN_Policy(**DEFAULT_NET, action_size=25, device=self.device, seed=net_seed).to(self.device)
             for p in self.target.parameters():
                 p.requires_grad_(False)
-            self.grads = FlatGrads(self.local.parameters())
-            self.opt = torch.optim.Adam(self.local.parameters(), lr=lr, capturable=capturable)
+            if fused_adam:
+                self.opt = FusedAdam(self.local.parameters(), lr=lr)
+                self.grads = self.opt.grads
+            else:
+                self.grads = FlatGrads(self.local.parameters())
+                self.opt = torch.optim.Adam(self.local.parameters(), lr=lr, capturable=capturable)
             self.action_dim = 1
         else:
             raise NotImplementedError(f"VecTrainer agent_type {agent_type!r} (AC-IQN and IQN are batched)")
@@ -108,7 +119,9 @@ class VecTrainer:
         eps = self.epsilon()
         explore = torch.rand((NT, 1), device=self.device) < eps
         if self.agent_type == "AC-IQN":
-            amp = torch.autocast("cuda", dtype=self.amp_dtype) if self.amp_dtype is not None else _null()
+            # fp32 actor when the critic is fused (see ac_iqn_update_fused)
+            use_amp = self.amp_dtype is not None and self.fused is None
+            amp = torch.autocast("cuda", dtype=self.amp_dtype) if use_amp else _null()
             with amp:
                 a = self.local.actor(obs).float()
             rnd = torch.rand((NT, 2), device=self.device) * 2.0 - 1.0
@@ -156,6 +169,8 @@ class VecTrainer:
             else:
                 pairs = list(zip(self.target.parameters(), self.local.parameters()))
             torch._foreach_copy_([t for t, _ in pairs], [l for _, l in pairs])
+            if self.agent_type == "AC-IQN" and self.fused is not None:
+                self.fused.target_pack.refresh()  # eager, outside any captured graph
 
     # ------------------------------------------------------------------ iteration
     def _iteration_body(self, do_learn):

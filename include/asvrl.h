@@ -215,6 +215,11 @@ typedef struct AsvCriticActs {
   float* dq;   /* [R]       dL/dq */
 } AsvCriticActs;
 
+/* Fill the five bf16 fragment images of w (wc_frag .. w1t_frag) from the row-major f32
+ * weights cos_embedding.weight (256 x 64), hidden_layer.weight (128 x 256) and
+ * hidden_layer_2.weight (128 x 128) (AC_IQN_model.py:398-402). One launch. */
+int asvrl_critic_pack(const float* wc, const float* w1, const float* w2, const AsvCriticWeights* w, void* stream);
+
 /* Critic.forward (AC_IQN_model.py:462-480) from precomputed state features F (B x 256,
  * observation_processor) and action features G (B x 128, action_encoder): q [B*N].
  * Requires N in {8, 16, 32} (taus of a sample stay inside one 32-row wave tile). */
@@ -256,6 +261,37 @@ int asvrl_replay_sample(const float* ring, int64_t capacity, const int64_t* ring
  * slot into the ring (used by the compat ReplayBuffer.add, one transition per call). */
 int asvrl_replay_write_rows(const float* rows, const int64_t* slots, int32_t n, float* ring,
                             void* stream);
+
+/* ---------------------------------------------------------------- optimiser (agent.py) */
+
+/* clip_grad_norm_(params, max_norm) followed by optim.Adam(lr, betas, eps).step() over one
+ * flat f32 parameter buffer of n elements (agent.py:75-76,98 with the clips at
+ * agent.py:415,426,471,636). grads are scaled in place by min(1, max_norm / (norm + 1e-6))
+ * (max_norm <= 0: no clipping); *step (f32, device) is incremented before the bias
+ * corrections are taken; norm_out (f32 device scalar, optional) receives the pre-clip global
+ * norm that clip_grad_norm_ returns. work: >= 64 doubles of device scratch. Two launches,
+ * no host synchronisation (capturable). */
+int asvrl_adam_clip(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+                    float* step, float lr, float beta1, float beta2, float eps, float max_norm,
+                    float* norm_out, double* work, void* stream);
+
+/* ---------------------------------------------------------------- Linear weight gradients */
+
+/* grad_weight / grad_bias of an nn.Linear from bf16 activations over R rows (the backward's
+ * dW = dZ^T X, db = dZ.sum(0), AC_IQN_model.py:398-404 layers): dw[m][k] = sum_r dz[r][m] x[r][k],
+ * db[m] = sum_r dz[r][m] (db optional). dz (R x M, leading dim ldz) and x (R x K, ldx) are bf16
+ * row-major, 16-byte aligned, ld multiples of 8; R a multiple of 32. (M, K) in {(256, 64),
+ * (128, 256), (128, 128), (64, 64)}. accumulate = 0 overwrites dw/db, 1 adds. Deterministic
+ * (fixed-order partial sums). work: asvrl_linear_wgrad_workspace(M, K) floats. */
+int64_t asvrl_linear_wgrad_workspace(int32_t M, int32_t K);
+int asvrl_linear_wgrad(const void* dz, int64_t ldz, const void* x, int64_t ldx, int32_t R, int32_t M,
+                       int32_t K, float* dw, float* db, int32_t accumulate, float* work,
+                       int64_t work_floats, void* stream);
+
+/* The one-unit output layer's version: dw[k] = sum_r dq[r] x[r][k], db = sum_r dq[r] with dq f32
+ * (R) and x bf16 (R x K, ldx); K in {64, 128, 256}; work >= 256 * (K + 1) floats. */
+int asvrl_linear_wgrad_vec(const float* dq, const void* x, int64_t ldx, int32_t R, int32_t K, float* dw,
+                           float* db, int32_t accumulate, float* work, int64_t work_floats, void* stream);
 
 /* ---------------------------------------------------------------- misc */
 const char* asvrl_last_error(void);

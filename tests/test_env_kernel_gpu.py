@@ -229,3 +229,69 @@ def test_env_step_philox_invariants_full_size():
     n = b1.n_robots.cpu().numpy()
     assert n.min() >= 1 and n.max() <= R
     assert b1.n_obs.cpu().numpy().max() <= O
+
+
+@pytest.mark.parametrize("R,O,Cn,W", [(5, 4, 0, 55.0), (5, 4, 4, 55.0), (17, 4, 0, 110.0)])
+def test_device_reset_invariants(R, O, Cn, W):
+    """asvrl_env_reset (wave-per-env rejection sampler) satisfies every acceptance rule of
+    MarineNavEnv3.reset (env.py:106-162, check_core :378-418, check_obstacle :420-456) on all
+    envs, clears the robot state, deactivates unused slots, and is deterministic in
+    (seed, counter). Rules checked: start-goal distance >= min_start_goal_dis; pairwise
+    starts and goals > clear_r; starts/goals in [2, W-2]; obstacles in [5, W-5], clear of
+    starts/goals by r + clear_r and of each other by r_i + r_j; cores inside the map and
+    clear of starts/goals by core_r + clear_r."""
+    from distributional_rl_decision_and_control_amd import _abi
+    from distributional_rl_decision_and_control_amd.device_env import DeviceEnvBatch, reset_cfg
+    E = 2048
+    cfg = reset_cfg(R, O, Cn, 40.0, width=W, height=W)
+
+    def make(counter):
+        b = DeviceEnvBatch(E, R, O, max(Cn, 1))
+        b.rs.fill_(123.0)
+        b.reset(cfg, seed=11, counter=counter)
+        torch.cuda.synchronize()
+        return b
+
+    b = make(0)
+    b2 = make(0)
+    assert torch.equal(b.rs, b2.rs) and torch.equal(b.obstacles, b2.obstacles) and torch.equal(b.cores, b2.cores)
+    b3 = make(1)
+    assert not torch.equal(b.rs, b3.rs)
+    rs = b.rs.cpu().numpy().reshape(-1, E, R)
+    fl = b.rflags.cpu().numpy().reshape(E, R)
+    nr = b.n_robots.cpu().numpy()
+    no = b.n_obs.cpu().numpy()
+    nc = b.n_cores.cpu().numpy()
+    assert (b.ep_ts.cpu().numpy() == 0).all()
+    assert nr.min() >= 1 and nr.max() <= R and (nr == R).mean() > 0.9
+    assert no.max() <= O and (no == O).mean() > 0.9
+    assert nc.max() <= Cn and (nc == Cn).mean() > 0.9
+    x, y, gx, gy = rs[_abi.F_X], rs[_abi.F_Y], rs[_abi.F_GX], rs[_abi.F_GY]
+    core_r = float(b.params.core_r)
+    for e in range(0, E, 7):
+        n = nr[e]
+        assert (fl[e, :n] == 0).all() and (fl[e, n:] == _abi.FLAG_DEACTIVATED).all()
+        sx, sy, tx, ty = x[e, :n], y[e, :n], gx[e, :n], gy[e, :n]
+        assert (np.hypot(tx - sx, ty - sy) >= 40.0).all()
+        for arr in (sx, sy, tx, ty):
+            assert ((arr >= 2.0) & (arr <= W - 2.0)).all()
+        for vx, vy in ((sx, sy), (tx, ty)):
+            d = np.hypot(vx[:, None] - vx[None], vy[:, None] - vy[None])
+            assert (d[~np.eye(n, dtype=bool)] > 10.0).all()
+        for f in range(_abi.F_VR0, _abi.F_RP + 1):
+            assert (rs[f][e, :n] == 0.0).all()
+        assert ((rs[_abi.F_THETA][e, :n] >= 0) & (rs[_abi.F_THETA][e, :n] < 2 * np.pi)).all()
+        ob = b.obstacles[e, :no[e]].cpu().numpy()
+        for (ox, oy, r) in ob:
+            assert 5.0 <= ox <= W - 5.0 and 5.0 <= oy <= W - 5.0
+            assert (np.hypot(sx - ox, sy - oy) >= r + 10.0).all() and (np.hypot(tx - ox, ty - oy) >= r + 10.0).all()
+        if len(ob) > 1:
+            d = np.hypot(ob[:, None, 0] - ob[None, :, 0], ob[:, None, 1] - ob[None, :, 1])
+            rr = ob[:, None, 2] + ob[None, :, 2]
+            assert (d[~np.eye(len(ob), dtype=bool)] > rr[~np.eye(len(ob), dtype=bool)]).all()
+        co = b.cores[e, :nc[e]].cpu().numpy()
+        for (cx, cy, cw, G) in co:
+            assert core_r <= cx <= W - core_r and core_r <= cy <= W - core_r
+            assert (np.hypot(sx - cx, sy - cy) >= core_r + 10.0).all()
+            assert (np.hypot(tx - cx, ty - cy) >= core_r + 10.0).all()
+            assert cw in (0.0, 1.0) and G > 0

@@ -36,6 +36,22 @@ def _cos(x, y):
     return float((x @ y) / (x.norm() * y.norm() + 1e-30))
 
 
+def test_pack_kernel_matches_fragment_index():
+    """asvrl_critic_pack writes exactly the frag_index gathers (bit-exact bf16 images)."""
+    from distributional_rl_decision_and_control_amd.fused_critic import CriticPack
+    critic, _, _, _ = _setup(64, 8)
+    pack = CriticPack(critic)
+    torch.cuda.synchronize()
+    ref = pack.reference_images()
+    for name in ("wc", "w1", "w2", "w2t", "w1t"):
+        assert torch.equal(getattr(pack, name), ref[name]), name
+    with torch.no_grad():
+        critic.hidden_layer.weight.mul_(-0.5)
+    pack.refresh()
+    ref = pack.reference_images()
+    assert torch.equal(pack.w1, ref["w1"]) and torch.equal(pack.w1t, ref["w1t"])
+
+
 @pytest.mark.parametrize("B,N", [(64, 8), (256, 32), (4096, 32)])
 def test_fused_forward(B, N):
     from distributional_rl_decision_and_control_amd.fused_critic import CriticPack, critic_forward
