@@ -32,8 +32,10 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kC = 256, kH = 128, kNcos = 64;
-constexpr int kWaves = 4;
 enum { MODE_FWD = 0, MODE_TRAIN = 1, MODE_ACTOR = 2 };
+#ifndef ASVRL_CRITIC_PERSISTENT
+#define ASVRL_CRITIC_PERSISTENT 0
+#endif
 
 struct CriticArgs {
   AsvCriticWeights w;
@@ -86,21 +88,26 @@ __device__ __forceinline__ void store4(__bf16* base, const float* v) {
   *reinterpret_cast<bf16x4*>(base) = x;
 }
 
+// LDS-resident forward weights: fragment images of Wc, W1, W2 (128 KB) + bc, b1, b2, wo.
+constexpr int kFragWC = kC * kNcos / 8, kFragW1 = kH * kC / 8, kFragW2 = kH * kH / 8;
+struct CriticLds {
+  bf16x8 wc[kFragWC];
+  bf16x8 w1[kFragW1];
+  bf16x8 w2[kFragW2];
+  float bc[kC], b1[kH], b2[kH], wo[kH];
+};
+
 template <int MODE, int NT>
-__global__ __launch_bounds__(kWaves * 64) void critic_kernel(CriticArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int tile = blockIdx.x * kWaves + (threadIdx.x >> 6);
-  const int R = a.B * NT;
-  if (tile * 32 >= R) return;
+__device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds& L, int tile, int lane) {
   const int r = lane & 31, h = lane >> 5;
   const int grow = tile * 32 + r;
   const int b = grow / NT;
   const float tau = a.taus[grow];
   const float* Fb = a.F + static_cast<size_t>(b) * kC;
   const float* Gb = a.G + static_cast<size_t>(b) * kH;
-  const bf16x8* WC = reinterpret_cast<const bf16x8*>(a.w.wc_frag);
-  const bf16x8* W1 = reinterpret_cast<const bf16x8*>(a.w.w1_frag);
-  const bf16x8* W2 = reinterpret_cast<const bf16x8*>(a.w.w2_frag);
+  const bf16x8* WC = L.wc;
+  const bf16x8* W1 = L.w1;
+  const bf16x8* W2 = L.w2;
 
   // ---------------- layer 0: c = relu(Wc cos + bc), h0 = F[b] * c   (two halves of 4 blocks)
   bf16x8 cx[kNcos / 16];
@@ -135,7 +142,7 @@ __global__ __launch_bounds__(kWaves * 64) void critic_kernel(CriticArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int m = feat(mb, 8 * s + j, h);
-          float x = acc0[q4][8 * s + j] + a.w.bc[m];
+          float x = acc0[q4][8 * s + j] + L.bc[m];
           x = x > 0.f ? x : 0.f;
           cpk[mb * 2 + s][j] = (__bf16)x;
           hv[j] = Fb[m] * x;
@@ -168,7 +175,7 @@ __global__ __launch_bounds__(kWaves * 64) void critic_kernel(CriticArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int m = feat(mb, 8 * s + j, h);
-        float x = acc1[mb][8 * s + j] + a.w.b1[m];
+        float x = acc1[mb][8 * s + j] + L.b1[m];
         x = x > 0.f ? x : 0.f;
         h1pk[mb * 2 + s][j] = (__bf16)x;
         gv[j] = x * Gb[m];
@@ -197,9 +204,9 @@ __global__ __launch_bounds__(kWaves * 64) void critic_kernel(CriticArgs a) {
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
       const int m = feat(mb, g, h);
-      float x = acc2[mb][g] + a.w.b2[m];
+      float x = acc2[mb][g] + L.b2[m];
       acc2[mb][g] = x;  // keep z2 for the relu mask
-      part += a.w.wo[m] * (x > 0.f ? x : 0.f);
+      part += L.wo[m] * (x > 0.f ? x : 0.f);
     }
   }
   const float q = part + __shfl_xor(part, 32, 64) + a.w.bo[0];
@@ -241,7 +248,7 @@ __global__ __launch_bounds__(kWaves * 64) void critic_kernel(CriticArgs a) {
         const int m = feat(mb, 8 * s + j, h);
         const float z = acc2[mb][8 * s + j];
         hv[j] = z > 0.f ? z : 0.f;
-        dv[j] = z > 0.f ? dq * a.w.wo[m] : 0.f;
+        dv[j] = z > 0.f ? dq * L.wo[m] : 0.f;
         dz2pk[mb * 2 + s][j] = (__bf16)dv[j];
       }
       if (MODE == MODE_TRAIN) {
@@ -256,6 +263,7 @@ __global__ __launch_bounds__(kWaves * 64) void critic_kernel(CriticArgs a) {
 
   // ---------------- layer 3: dh1g = W2^T dz2; dG[b] = sum_taus dh1g * h1; dz1 = dh1g * G * 1[h1 > 0]
   const bf16x8* W2T = reinterpret_cast<const bf16x8*>(a.w.w2t_frag);
+  asm volatile("" : "+v"(W2T));  // not loop-invariant for the compiler (see critic_kernel)
   f32x16 acc3[4];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) acc3[mb] = f32x16{};
@@ -298,6 +306,7 @@ __global__ __launch_bounds__(kWaves * 64) void critic_kernel(CriticArgs a) {
 
   // ---------------- layer 4: dh0 = W1^T dz1; dF[b] = sum_taus dh0 * c; dzc = dh0 * F * 1[c > 0]
   const bf16x8* W1T = reinterpret_cast<const bf16x8*>(a.w.w1t_frag);
+  asm volatile("" : "+v"(W1T));
 #pragma unroll
   for (int half = 0; half < 2; ++half) {  // 2 x 4 output blocks keeps 64 accumulator registers live
     f32x16 acc4[4];
@@ -338,21 +347,80 @@ __global__ __launch_bounds__(kWaves * 64) void critic_kernel(CriticArgs a) {
   }
 }
 
+// Persistent: one workgroup per CU stages the forward weights into LDS once, then its waves
+// walk the 32-row tiles. 8 waves (2 per SIMD) where the registers allow, 4 for TRAIN.
+template <int MODE> struct CriticWaves { static constexpr int n = 8; };
+template <> struct CriticWaves<MODE_TRAIN> { static constexpr int n = 4; };
+
+template <int MODE, int NT>
+__global__ __launch_bounds__(CriticWaves<MODE>::n * 64) void critic_kernel(CriticArgs a) {
+  constexpr int W = CriticWaves<MODE>::n;
+  __shared__ CriticLds L;
+  {
+    const bf16x8* gwc = reinterpret_cast<const bf16x8*>(a.w.wc_frag);
+    const bf16x8* gw1 = reinterpret_cast<const bf16x8*>(a.w.w1_frag);
+    const bf16x8* gw2 = reinterpret_cast<const bf16x8*>(a.w.w2_frag);
+    for (int i = threadIdx.x; i < kFragWC; i += W * 64) L.wc[i] = gwc[i];
+    for (int i = threadIdx.x; i < kFragW1; i += W * 64) L.w1[i] = gw1[i];
+    for (int i = threadIdx.x; i < kFragW2; i += W * 64) L.w2[i] = gw2[i];
+    for (int i = threadIdx.x; i < kC; i += W * 64) L.bc[i] = a.w.bc[i];
+    for (int i = threadIdx.x; i < kH; i += W * 64) {
+      L.b1[i] = a.w.b1[i];
+      L.b2[i] = a.w.b2[i];
+      L.wo[i] = a.w.wo[i];
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int tiles = a.B * NT / 32;
+#if ASVRL_CRITIC_PERSISTENT
+  for (int tile = blockIdx.x * W + (threadIdx.x >> 6); tile < tiles; tile += gridDim.x * W) {
+    // opaque per-iteration copy of the LDS base: keeps the (loop-invariant) weight-fragment
+    // reads inside the loop instead of hoisting thousands of them into registers
+    const CriticLds* Lp = &L;
+    asm volatile("" : "+v"(Lp));
+    critic_tile<MODE, NT>(a, *Lp, tile, lane);
+  }
+#else
+  const int tile = blockIdx.x * W + (threadIdx.x >> 6);
+  if (tile < tiles) critic_tile<MODE, NT>(a, L, tile, lane);
+#endif
+}
+
+int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+template <int MODE, int NT>
+void launch_mode(const CriticArgs& a, hipStream_t st) {
+  constexpr int W = CriticWaves<MODE>::n;
+  const int tiles = a.B * NT / 32;
+  int grid = (tiles + W - 1) / W;
+#if ASVRL_CRITIC_PERSISTENT
+  if (grid > num_cus()) grid = num_cus();
+#endif
+  hipLaunchKernelGGL((critic_kernel<MODE, NT>), dim3(grid), dim3(W * 64), 0, st, a);
+}
+
 template <int NT>
-void launch_n(int mode, const CriticArgs& a, dim3 grid, dim3 block, hipStream_t st) {
-  if (mode == MODE_FWD) hipLaunchKernelGGL((critic_kernel<MODE_FWD, NT>), grid, block, 0, st, a);
-  else if (mode == MODE_TRAIN) hipLaunchKernelGGL((critic_kernel<MODE_TRAIN, NT>), grid, block, 0, st, a);
-  else hipLaunchKernelGGL((critic_kernel<MODE_ACTOR, NT>), grid, block, 0, st, a);
+void launch_n(int mode, const CriticArgs& a, hipStream_t st) {
+  if (mode == MODE_FWD) launch_mode<MODE_FWD, NT>(a, st);
+  else if (mode == MODE_TRAIN) launch_mode<MODE_TRAIN, NT>(a, st);
+  else launch_mode<MODE_ACTOR, NT>(a, st);
 }
 
 int launch(int mode, const CriticArgs& a, void* stream) {
-  const int R = a.B * a.N;
-  const int tiles = (R + 31) / 32;
-  const dim3 grid((tiles + kWaves - 1) / kWaves), block(kWaves * 64);
   hipStream_t st = as_stream(stream);
-  if (a.N == 8) launch_n<8>(mode, a, grid, block, st);
-  else if (a.N == 16) launch_n<16>(mode, a, grid, block, st);
-  else launch_n<32>(mode, a, grid, block, st);
+  if (a.N == 8) launch_n<8>(mode, a, st);
+  else if (a.N == 16) launch_n<16>(mode, a, st);
+  else launch_n<32>(mode, a, st);
   return check_launch("asvrl_critic");
 }
 
