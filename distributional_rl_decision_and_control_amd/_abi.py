@@ -11,7 +11,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libasvrl.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
 OBS_DIM = 40   # self 7 | objects 25 | mask 5 | pad 3
@@ -86,6 +86,30 @@ class AsvCriticActs(C.Structure):
 
 # (name, restype, argtypes) of every exported entry point, mirroring include/asvrl.h
 _VP, _I32, _I64, _U64, _F, _D = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_float, C.c_double
+class AsvCriticIO(C.Structure):
+    _fields_ = [("F", _VP), ("G", _VP), ("taus", _VP), ("B", _I32), ("N", _I32), ("Np", _I32), ("kappa", C.c_float),
+                ("q_targets", _VP), ("q_next", _VP), ("rewards", _VP), ("dones", _VP), ("ld_rd", _I64),
+                ("gamma", C.c_float), ("dq", C.c_float), ("q", _VP), ("row_loss", _VP), ("dF", _VP), ("dG", _VP),
+                ("dzF", _VP), ("dzG", _VP), ("w_ae", _VP), ("dA", _VP)]
+
+
+class AsvMlpSrc(C.Structure):
+    _fields_ = [(n, _VP) for n in ("self_w", "self_b", "obj_w", "obj_b", "w1", "w2", "ae_w")]
+
+
+class AsvMlpWeights(C.Structure):
+    _fields_ = [(n, _VP) for n in ("enc_frag", "b_enc", "w1_frag", "w2_frag", "w2t_frag", "w1t_frag", "b1", "b2",
+                                   "wout", "bout", "ae_frag", "b_ae")] + [("out_scale", C.c_float)]
+
+
+class AsvMlpIO(C.Structure):
+    _fields_ = [("x", _VP), ("ldx", _I64), ("act", _VP), ("lda", _I64), ("n", _I32), ("F", _VP), ("G", _VP),
+                ("xb", _VP), ("a_out", _VP), ("ld_aout", _I64), ("a_out64", _VP), ("pre", _VP), ("h0", _VP),
+                ("h1", _VP), ("h2", _VP), ("dA", _VP), ("dout", _VP), ("dz2", _VP), ("dz1", _VP), ("dz0", _VP),
+                ("step_dev", _VP), ("eps_steps_per_count", _D), ("eps_total", _D), ("eps_fraction", _D),
+                ("eps_initial", _D), ("eps_final", _D), ("seed", _U64)]
+
+
 EXPORTS = [
     ("asvrl_env_step", C.c_int, [C.POINTER(AsvParams), C.POINTER(AsvEnvState), _VP, _VP, C.POINTER(AsvStepCtl),
                                  C.POINTER(AsvStepOut), _VP]),
@@ -95,17 +119,23 @@ EXPORTS = [
     ("asvrl_quantile_huber", C.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, _F, _F, _VP, _VP, _VP, _VP]),
     ("asvrl_c51_project", C.c_int, [_VP, _VP, _VP, _VP, _I32, _I32, _F, _F, _F, _F, _VP, _VP]),
     ("asvrl_critic_pack", C.c_int, [_VP, _VP, _VP, C.POINTER(AsvCriticWeights), _VP]),
-    ("asvrl_critic_forward", C.c_int, [C.POINTER(AsvCriticWeights), _VP, _VP, _VP, _I32, _I32, _VP, _VP]),
-    ("asvrl_critic_train", C.c_int, [C.POINTER(AsvCriticWeights), _VP, _VP, _VP, _VP, _I32, _I32, _I32, _F, _VP, _VP,
-                                     _VP, _VP, C.POINTER(AsvCriticActs), _VP]),
-    ("asvrl_critic_actor_grad", C.c_int, [C.POINTER(AsvCriticWeights), _VP, _VP, _VP, _I32, _I32, _F, _VP, _VP, _VP]),
+    ("asvrl_critic_forward", C.c_int, [C.POINTER(AsvCriticWeights), C.POINTER(AsvCriticIO), _VP]),
+    ("asvrl_critic_train", C.c_int, [C.POINTER(AsvCriticWeights), C.POINTER(AsvCriticIO), C.POINTER(AsvCriticActs),
+                                     _VP]),
+    ("asvrl_critic_actor_grad", C.c_int, [C.POINTER(AsvCriticWeights), C.POINTER(AsvCriticIO), _VP]),
     ("asvrl_replay_push", C.c_int, [_VP, _VP, _VP, _VP, _I32, _VP, _VP, _I32, _VP, _I64, _VP, _VP, _VP]),
     ("asvrl_replay_sample", C.c_int, [_VP, _I64, _VP, _VP, _I32, _U64, _U64, _VP, _VP, _VP, _VP]),
     ("asvrl_replay_write_rows", C.c_int, [_VP, _VP, _I32, _VP, _VP]),
     ("asvrl_adam_clip", C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, _F, _F, _VP, _VP, _VP]),
     ("asvrl_linear_wgrad_workspace", _I64, [_I32, _I32]),
     ("asvrl_linear_wgrad", C.c_int, [_VP, _I64, _VP, _I64, _I32, _I32, _I32, _VP, _VP, _I32, _VP, _I64, _VP]),
-    ("asvrl_linear_wgrad_vec", C.c_int, [_VP, _VP, _I64, _I32, _I32, _VP, _VP, _I32, _VP, _I64, _VP]),
+    ("asvrl_linear_wgrad_vec", C.c_int, [_VP, _I64, _VP, _I64, _I32, _I32, _VP, _VP, _I32, _VP, _I64, _VP]),
+    ("asvrl_mlp_pack", C.c_int, [C.POINTER(AsvMlpSrc), C.POINTER(AsvMlpWeights), _VP]),
+    ("asvrl_mlp_encode", C.c_int, [C.POINTER(AsvMlpWeights), C.POINTER(AsvMlpIO), _VP]),
+    ("asvrl_actor_forward", C.c_int, [C.POINTER(AsvMlpWeights), C.POINTER(AsvMlpIO), _I32, _VP]),
+    ("asvrl_actor_backward", C.c_int, [C.POINTER(AsvMlpWeights), C.POINTER(AsvMlpIO), _VP]),
+    ("asvrl_encoder_fold", C.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, _I32, _VP]),
+    ("asvrl_small_wgrad", C.c_int, [_VP, _I64, _VP, _I64, _I32, _I32, _I32, _VP, _VP, _I32, _VP, _I64, _VP]),
     ("asvrl_last_error", C.c_char_p, []),
     ("asvrl_abi_version", C.c_int, []),
     ("asvrl_struct_sizes", None, [C.c_void_p]),

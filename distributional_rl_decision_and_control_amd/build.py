@@ -9,8 +9,9 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SOURCES = [os.path.join(HERE, "csrc", f) for f in ("asvrl_env.hip", "asvrl_learn.hip", "asvrl_critic.hip",
-                                                             "asvrl_optim.hip", "asvrl_wgrad.hip")]
-HEADERS = [os.path.join(HERE, "csrc", "asvrl_common.h"), os.path.join(ROOT, "include", "asvrl.h")]
+                                                             "asvrl_optim.hip", "asvrl_wgrad.hip", "asvrl_mlp.hip")]
+HEADERS = [os.path.join(HERE, "csrc", "asvrl_common.h"), os.path.join(HERE, "csrc", "asvrl_mfma.h"),
+           os.path.join(ROOT, "include", "asvrl.h")]
 OUT = os.path.join(HERE, "lib", "libasvrl.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("ASVRL_OFFLOAD_ARCH", "gfx950")

@@ -19,6 +19,9 @@ constexpr int kWave = 64;                    // CDNA wavefront
 
 void set_error(const std::string& msg);
 int check_launch(const char* what);
+// out[i] (+)= sum_g partial[g][i] over i < nw (-> dw) and the trailing nb (-> db, optional)
+int launch_partial_sum(const float* partial, int groups, int nw, int nb, float* dw, float* db, int accumulate,
+                       hipStream_t st);
 
 #define ASVRL_REQUIRE(cond, msg)            \
   do {                                      \

@@ -23,13 +23,10 @@
 //          GEMM on the host side)
 //   ACTOR  forward + backward of -mean(q) to the action features only (agent.py:420-425)
 #include "asvrl_common.h"
+#include "asvrl_mfma.h"
 
 namespace asvrl {
 namespace {
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kC = 256, kH = 128, kNcos = 64;
 enum { MODE_FWD = 0, MODE_TRAIN = 1, MODE_ACTOR = 2 };
@@ -47,46 +44,20 @@ struct CriticArgs {
   float kappa, gscale, dq_const;
   float* q;         // (R) optional
   float* row_loss;  // (R) TRAIN
-  float* dF;        // (B, 256)
-  float* dG;        // (B, 128)
+  float* dF;        // (B, 256) optional
+  float* dG;        // (B, 128) optional
   AsvCriticActs acts;
+  // q_targets = r + gamma * q_next * (1 - d) formed in the loss loop (agent.py:399-400)
+  const float* qn;
+  const float* rew;
+  const float* don;
+  int64_t ld_rd;
+  float gamma;
+  void* dzF;        // (B, 256) bf16: dF * 1[F > 0]
+  float* dzG;       // (B, 128): dG * 1[G > 0]
+  const float* wae; // (128, 2) action_encoder.weight (ACTOR dA)
+  float* dA;        // (B, 2)
 };
-
-__device__ __forceinline__ __bf16* bp(void* p) { return reinterpret_cast<__bf16*>(p); }
-
-__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-// feature index held by accumulator register g of 32-feature block mb in lane half h
-__device__ __forceinline__ int feat(int mb, int g, int h) { return mb * 32 + (g & 3) + 8 * (g >> 2) + 4 * h; }
-
-template <int CTRL>
-__device__ __forceinline__ float dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-
-// Sum over aligned groups of NT lanes (NT | 32), every lane of a group gets the sum: xor-1 and
-// xor-2 quad butterflies, row_half_mirror (8), row_mirror (16) on DPP, one bpermute for 32.
-template <int NT>
-__device__ __forceinline__ float seg_sum(float v) {
-  if (NT >= 2) v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
-  if (NT >= 4) v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
-  if (NT >= 8) v += dpp<0x141>(v);  // row_half_mirror
-  if (NT >= 16) v += dpp<0x140>(v); // row_mirror
-  if (NT >= 32) v += __shfl_xor(v, 16, 64);
-  return v;
-}
-
-// bf16x4 store of the 4 consecutive features (j&3 = 0..3) of register group (s, q)
-__device__ __forceinline__ void store4(__bf16* base, const float* v) {
-  bf16x4 x;
-  x[0] = (__bf16)v[0];
-  x[1] = (__bf16)v[1];
-  x[2] = (__bf16)v[2];
-  x[3] = (__bf16)v[3];
-  *reinterpret_cast<bf16x4*>(base) = x;
-}
 
 // LDS-resident forward weights: fragment images of Wc, W1, W2 (128 KB) + bc, b1, b2, wo.
 constexpr int kFragWC = kC * kNcos / 8, kFragW1 = kH * kC / 8, kFragW2 = kH * kH / 8;
@@ -216,10 +187,17 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
   // ---------------- dL/dq
   float dq;
   if (MODE == MODE_TRAIN) {
-    const float* qt = a.qt + static_cast<size_t>(b) * a.Np;
+    const float* qt = a.qn != nullptr ? a.qn + static_cast<size_t>(b) * a.Np : a.qt + static_cast<size_t>(b) * a.Np;
+    float rb = 0.f, nd = 0.f;
+    if (a.qn != nullptr) {
+      rb = a.rew[b * a.ld_rd];
+      nd = 1.0f - a.don[b * a.ld_rd];
+    }
     float wl = 0.f, wg = 0.f;
     for (int j = 0; j < a.Np; ++j) {
-      const float d = qt[j] - q;  // td_error (agent.py:406)
+      // rewards + gamma * q_next * (1 - dones), in torch's evaluation order
+      const float target = a.qn != nullptr ? rb + (a.gamma * qt[j]) * nd : qt[j];
+      const float d = target - q;  // td_error (agent.py:406)
       const float ad = fabsf(d);
       const bool quad = ad <= a.kappa;
       const float hub = quad ? 0.5f * (d * d) : a.kappa * (ad - 0.5f * a.kappa);
@@ -273,6 +251,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
     for (int mb = 0; mb < 4; ++mb) acc3[mb] = mfma(W2T[(mb * 8 + ks) * 64 + lane], dz2pk[ks], acc3[mb]);
   }
   const bool writer = (r % NT) == 0;
+  float pa0 = 0.f, pa1 = 0.f;   // ACTOR: partial dA over this lane's features
   bf16x8 dz1pk[8];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) {
@@ -283,17 +262,30 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
       for (int j = 0; j < 8; ++j) gs[j] = acc3[mb][8 * s + j] * static_cast<float>(h1pk[mb * 2 + s][j]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) gs[j] = seg_sum<NT>(gs[j]);
-      if (writer) {
-        float* o = a.dG + static_cast<size_t>(b) * kH + mb * 32 + 16 * s + 4 * h;
-        *reinterpret_cast<float4*>(o) = make_float4(gs[0], gs[1], gs[2], gs[3]);
-        *reinterpret_cast<float4*>(o + 8) = make_float4(gs[4], gs[5], gs[6], gs[7]);
-      }
+      float gz[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int m = feat(mb, 8 * s + j, h);
+        const float gm = Gb[m];
         const float h1 = static_cast<float>(h1pk[mb * 2 + s][j]);
-        dv[j] = h1 > 0.f ? acc3[mb][8 * s + j] * Gb[m] : 0.f;
+        dv[j] = h1 > 0.f ? acc3[mb][8 * s + j] * gm : 0.f;
         dz1pk[mb * 2 + s][j] = (__bf16)dv[j];
+        gz[j] = gm > 0.f ? gs[j] : 0.f;   // through the action encoder's relu
+        if (MODE == MODE_ACTOR && a.dA != nullptr) {
+          pa0 += gz[j] * a.wae[2 * m];
+          pa1 += gz[j] * a.wae[2 * m + 1];
+        }
+      }
+      if (writer) {
+        const size_t ob = static_cast<size_t>(b) * kH + mb * 32 + 16 * s + 4 * h;
+        if (a.dG != nullptr) {
+          *reinterpret_cast<float4*>(a.dG + ob) = make_float4(gs[0], gs[1], gs[2], gs[3]);
+          *reinterpret_cast<float4*>(a.dG + ob + 8) = make_float4(gs[4], gs[5], gs[6], gs[7]);
+        }
+        if (a.dzG != nullptr) {
+          *reinterpret_cast<float4*>(a.dzG + ob) = make_float4(gz[0], gz[1], gz[2], gz[3]);
+          *reinterpret_cast<float4*>(a.dzG + ob + 8) = make_float4(gz[4], gz[5], gz[6], gz[7]);
+        }
       }
       if (MODE == MODE_TRAIN) {
         __bf16* row = bp(a.acts.dz1) + static_cast<size_t>(grow) * kH + mb * 32 + 16 * s + 4 * h;
@@ -302,7 +294,17 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
       }
     }
   }
-  if (MODE == MODE_ACTOR) return;
+  if (MODE == MODE_ACTOR) {
+    if (a.dA != nullptr) {
+      pa0 += __shfl_xor(pa0, 32, 64);
+      pa1 += __shfl_xor(pa1, 32, 64);
+      if (writer && h == 0) {
+        a.dA[2 * b] = pa0;
+        a.dA[2 * b + 1] = pa1;
+      }
+    }
+    return;
+  }
 
   // ---------------- layer 4: dh0 = W1^T dz1; dF[b] = sum_taus dh0 * c; dzc = dh0 * F * 1[c > 0]
   const bf16x8* W1T = reinterpret_cast<const bf16x8*>(a.w.w1t_frag);
@@ -328,16 +330,25 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
         for (int j = 0; j < 8; ++j) fs[j] = acc4[q4][8 * s + j] * static_cast<float>(cpk[mb * 2 + s][j]);
 #pragma unroll
         for (int j = 0; j < 8; ++j) fs[j] = seg_sum<NT>(fs[j]);
-        if (writer) {
-          float* o = a.dF + static_cast<size_t>(b) * kC + mb * 32 + 16 * s + 4 * h;
-          *reinterpret_cast<float4*>(o) = make_float4(fs[0], fs[1], fs[2], fs[3]);
-          *reinterpret_cast<float4*>(o + 8) = make_float4(fs[4], fs[5], fs[6], fs[7]);
-        }
+        float fz[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int m = feat(mb, 8 * s + j, h);
+          const float fm = Fb[m];
           const float c = static_cast<float>(cpk[mb * 2 + s][j]);
-          dv[j] = c > 0.f ? acc4[q4][8 * s + j] * Fb[m] : 0.f;
+          dv[j] = c > 0.f ? acc4[q4][8 * s + j] * fm : 0.f;
+          fz[j] = fm > 0.f ? fs[j] : 0.f;   // through the encoders' relu / mask
+        }
+        if (writer) {
+          const size_t ob = static_cast<size_t>(b) * kC + mb * 32 + 16 * s + 4 * h;
+          if (a.dF != nullptr) {
+            *reinterpret_cast<float4*>(a.dF + ob) = make_float4(fs[0], fs[1], fs[2], fs[3]);
+            *reinterpret_cast<float4*>(a.dF + ob + 8) = make_float4(fs[4], fs[5], fs[6], fs[7]);
+          }
+          if (a.dzF != nullptr) {
+            store4(bp(a.dzF) + ob, fz);
+            store4(bp(a.dzF) + ob + 8, fz + 4);
+          }
         }
         __bf16* row = bp(a.acts.dzc) + static_cast<size_t>(grow) * kC + mb * 32 + 16 * s + 4 * h;
         store4(row, dv);
@@ -432,13 +443,6 @@ int launch(int mode, const CriticArgs& a, void* stream) {
 constexpr int kPackWc = 256 * 64, kPackW1 = 128 * 256, kPackW2 = 128 * 128;
 constexpr int kPackTotal = kPackWc + 2 * kPackW1 + 2 * kPackW2;
 
-__device__ __forceinline__ void frag_rc(int o, int K, bool chained, int& row, int& col) {
-  const int j = o & 7, lane = (o >> 3) & 63, blk = o >> 9;
-  const int KS = K / 16;
-  const int ks = blk % KS, mb = blk / KS, h = lane >> 5;
-  row = mb * 32 + (lane & 31);
-  col = ks * 16 + (chained ? (8 * (j >> 2) + 4 * h + (j & 3)) : (8 * h + j));
-}
 
 __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ wc, const float* __restrict__ w1,
                                                    const float* __restrict__ w2, AsvCriticWeights w) {
@@ -473,13 +477,24 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ wc,
   const_cast<__bf16*>(static_cast<const __bf16*>(w.w1t_frag))[o] = (__bf16)w1[col * 256 + row];
 }
 
-int validate(const AsvCriticWeights* w, const float* F, const float* G, const float* taus, int B, int N) {
-  ASVRL_REQUIRE(w && F && G && taus, "asvrl_critic: null argument");
+int validate(const AsvCriticWeights* w, const AsvCriticIO* io) {
+  ASVRL_REQUIRE(w && io && io->F && io->G && io->taus, "asvrl_critic: null argument");
   ASVRL_REQUIRE(w->wc_frag && w->w1_frag && w->w2_frag && w->bc && w->b1 && w->b2 && w->wo && w->bo,
                 "asvrl_critic: null weight");
-  ASVRL_REQUIRE(N == 8 || N == 16 || N == 32, "asvrl_critic: N must be 8, 16 or 32");
-  ASVRL_REQUIRE(B >= 0 && (static_cast<int64_t>(B) * N) % 32 == 0, "asvrl_critic: B*N must be a multiple of 32");
+  ASVRL_REQUIRE(io->N == 8 || io->N == 16 || io->N == 32, "asvrl_critic: N must be 8, 16 or 32");
+  ASVRL_REQUIRE(io->B >= 0 && (static_cast<int64_t>(io->B) * io->N) % 32 == 0,
+                "asvrl_critic: B*N must be a multiple of 32");
   return 0;
+}
+
+CriticArgs make_args(const AsvCriticWeights* w, const AsvCriticIO* io) {
+  CriticArgs a{};
+  a.w = *w;
+  a.F = io->F; a.G = io->G; a.taus = io->taus; a.B = io->B; a.N = io->N; a.Np = io->Np; a.kappa = io->kappa;
+  a.qt = io->q_targets; a.qn = io->q_next; a.rew = io->rewards; a.don = io->dones; a.ld_rd = io->ld_rd;
+  a.gamma = io->gamma; a.dq_const = io->dq; a.q = io->q; a.row_loss = io->row_loss; a.dF = io->dF; a.dG = io->dG;
+  a.dzF = io->dzF; a.dzG = io->dzG; a.wae = io->w_ae; a.dA = io->dA;
+  return a;
 }
 
 }  // namespace
@@ -487,40 +502,35 @@ int validate(const AsvCriticWeights* w, const float* F, const float* G, const fl
 
 using namespace asvrl;
 
-extern "C" int asvrl_critic_forward(const AsvCriticWeights* w, const float* F, const float* G, const float* taus,
-                                    int32_t B, int32_t N, float* q, void* stream) {
-  if (int rc = validate(w, F, G, taus, B, N)) return rc;
-  ASVRL_REQUIRE(q != nullptr, "asvrl_critic_forward: null q");
-  if (B == 0) return 0;
-  CriticArgs a{};
-  a.w = *w; a.F = F; a.G = G; a.taus = taus; a.B = B; a.N = N; a.q = q;
-  return launch(MODE_FWD, a, stream);
+extern "C" int asvrl_critic_forward(const AsvCriticWeights* w, const AsvCriticIO* io, void* stream) {
+  if (int rc = validate(w, io)) return rc;
+  ASVRL_REQUIRE(io->q != nullptr, "asvrl_critic_forward: null q");
+  if (io->B == 0) return 0;
+  return launch(MODE_FWD, make_args(w, io), stream);
 }
 
-extern "C" int asvrl_critic_train(const AsvCriticWeights* w, const float* F, const float* G, const float* taus,
-                                  const float* q_targets, int32_t B, int32_t N, int32_t Np, float kappa, float* q,
-                                  float* row_loss, float* dF, float* dG, const AsvCriticActs* acts, void* stream) {
-  if (int rc = validate(w, F, G, taus, B, N)) return rc;
-  ASVRL_REQUIRE(q_targets && row_loss && dF && dG && acts && w->w2t_frag && w->w1t_frag, "asvrl_critic_train: null argument");
+extern "C" int asvrl_critic_train(const AsvCriticWeights* w, const AsvCriticIO* io, const AsvCriticActs* acts,
+                                  void* stream) {
+  if (int rc = validate(w, io)) return rc;
+  ASVRL_REQUIRE(io->row_loss && acts && w->w2t_frag && w->w1t_frag, "asvrl_critic_train: null argument");
+  ASVRL_REQUIRE(io->q_targets || (io->q_next && io->rewards && io->dones),
+                "asvrl_critic_train: needs q_targets or q_next + rewards + dones");
   ASVRL_REQUIRE(acts->cos && acts->h0 && acts->dzc && acts->h1g && acts->dz1 && acts->h2 && acts->dz2 && acts->dq,
                 "asvrl_critic_train: null activation buffer");
-  ASVRL_REQUIRE(Np >= 1 && kappa > 0.f, "asvrl_critic_train: bad Np/kappa");
-  if (B == 0) return 0;
-  CriticArgs a{};
-  a.w = *w; a.F = F; a.G = G; a.taus = taus; a.qt = q_targets; a.B = B; a.N = N; a.Np = Np; a.kappa = kappa;
-  a.gscale = 1.f / (static_cast<float>(B) * static_cast<float>(Np));
-  a.q = q; a.row_loss = row_loss; a.dF = dF; a.dG = dG; a.acts = *acts;
+  ASVRL_REQUIRE(io->Np >= 1 && io->kappa > 0.f, "asvrl_critic_train: bad Np/kappa");
+  if (io->B == 0) return 0;
+  CriticArgs a = make_args(w, io);
+  a.gscale = 1.f / (static_cast<float>(io->B) * static_cast<float>(io->Np));
+  a.acts = *acts;
   return launch(MODE_TRAIN, a, stream);
 }
 
-extern "C" int asvrl_critic_actor_grad(const AsvCriticWeights* w, const float* F, const float* G, const float* taus,
-                                       int32_t B, int32_t N, float dq, float* q, float* dG, void* stream) {
-  if (int rc = validate(w, F, G, taus, B, N)) return rc;
-  ASVRL_REQUIRE(dG && w->w2t_frag, "asvrl_critic_actor_grad: null argument");
-  if (B == 0) return 0;
-  CriticArgs a{};
-  a.w = *w; a.F = F; a.G = G; a.taus = taus; a.B = B; a.N = N; a.dq_const = dq; a.q = q; a.dG = dG;
-  return launch(MODE_ACTOR, a, stream);
+extern "C" int asvrl_critic_actor_grad(const AsvCriticWeights* w, const AsvCriticIO* io, void* stream) {
+  if (int rc = validate(w, io)) return rc;
+  ASVRL_REQUIRE(w->w2t_frag && (io->dG || io->dA), "asvrl_critic_actor_grad: needs dG or dA");
+  ASVRL_REQUIRE(!io->dA || io->w_ae, "asvrl_critic_actor_grad: dA needs w_ae");
+  if (io->B == 0) return 0;
+  return launch(MODE_ACTOR, make_args(w, io), stream);
 }
 
 extern "C" int asvrl_critic_pack(const float* wc, const float* w1, const float* w2, const AsvCriticWeights* w,

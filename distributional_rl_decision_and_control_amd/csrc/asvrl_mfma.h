@@ -1,0 +1,75 @@
+// asvrl_mfma.h -- shared MFMA helpers of the learner kernels (gfx950, wave64).
+//
+// Convention (v_mfma_f32_32x32x16_bf16): features are the MFMA M dimension, rows (samples) the
+// N dimension. A 32x32 accumulator block has its row-of-batch on the lane (lane & 31) and its
+// features in the 16 registers: register g of lane half h (= lane >> 5) holds feature
+// (g & 3) + 8 (g >> 2) + 4 h of the block. Registers 8s..8s+7, converted to bf16, are directly
+// the B operand of a following layer's k-step s ("chained" k order 16s + 8(j>>2) + 4h + (j&3));
+// the A operand (weights) is pre-packed into per-lane fragments in that same k order.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace asvrl {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ __bf16* bp(void* p) { return reinterpret_cast<__bf16*>(p); }
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// feature index held by accumulator register g of 32-feature block mb in lane half h
+__device__ __forceinline__ int feat(int mb, int g, int h) { return mb * 32 + (g & 3) + 8 * (g >> 2) + 4 * h; }
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// Sum over aligned groups of NT lanes (NT | 32), every lane of a group gets the sum: xor-1 and
+// xor-2 quad butterflies, row_half_mirror (8), row_mirror (16) on DPP, one bpermute for 32.
+template <int NT>
+__device__ __forceinline__ float seg_sum(float v) {
+  if (NT >= 2) v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  if (NT >= 4) v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  if (NT >= 8) v += dpp<0x141>(v);  // row_half_mirror
+  if (NT >= 16) v += dpp<0x140>(v); // row_mirror
+  if (NT >= 32) v += __shfl_xor(v, 16, 64);
+  return v;
+}
+
+// bf16x4 store of 4 consecutive features
+__device__ __forceinline__ void store4(__bf16* base, const float* v) {
+  bf16x4 x;
+  x[0] = (__bf16)v[0];
+  x[1] = (__bf16)v[1];
+  x[2] = (__bf16)v[2];
+  x[3] = (__bf16)v[3];
+  *reinterpret_cast<bf16x4*>(base) = x;
+}
+
+// 4 consecutive bf16 -> f32
+__device__ __forceinline__ void load4(const __bf16* base, float* v) {
+  const bf16x4 x = *reinterpret_cast<const bf16x4*>(base);
+  v[0] = static_cast<float>(x[0]);
+  v[1] = static_cast<float>(x[1]);
+  v[2] = static_cast<float>(x[2]);
+  v[3] = static_cast<float>(x[3]);
+}
+
+// Fragment image element o of an (M x K) weight: ((mb*KS + ks)*64 + lane)*8 + j holds
+// W[mb*32 + (lane&31)][col] with col = ks*16 + 8h + j (input-fed layer) or
+// ks*16 + 8(j>>2) + 4h + (j&3) (chained layer).
+__device__ __forceinline__ void frag_rc(int o, int K, bool chained, int& row, int& col) {
+  const int j = o & 7, lane = (o >> 3) & 63, blk = o >> 9;
+  const int KS = K / 16;
+  const int ks = blk % KS, mb = blk / KS, h = lane >> 5;
+  row = mb * 32 + (lane & 31);
+  col = ks * 16 + (chained ? (8 * (j >> 2) + 4 * h + (j & 3)) : (8 * h + j));
+}
+
+}  // namespace asvrl

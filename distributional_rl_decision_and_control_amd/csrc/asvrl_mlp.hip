@@ -1,0 +1,606 @@
+// asvrl_mlp.hip -- the per-row MLPs of AC-IQN on MFMA (gfx950): the observation encoders
+// (AC_IQN_model.py:284-308: self_encoder 7 -> 56, object_encoder 5 -> 40 per object, masked,
+// concatenated to 256), the Actor head (:310-321: 256 -> 128 -> 128 -> 2, (2/pi) atan) and the
+// critic's action_encoder (2 -> 128).
+//
+// The two encoders are ONE block-structured 256 x 32 matrix acting on columns 0..31 of the packed
+// observation row [self 7 | objects 5x5 | mask 5 | pad 3]: rows 0..55 see columns 0..6 (self),
+// rows 56+40o .. 95+40o see columns 7+5o .. 11+5o (object o). masked_fill(mask < 0.5, 0) is a
+// per-feature multiplier in the epilogue. Same tile convention as the critic (asvrl_mfma.h):
+// one wave = 32 rows, features on the MFMA M dimension, accumulators chained as B operands.
+//
+// Modes of mlp_kernel:
+//   ENCODE  F = encoders(obs) [B][256] f32 and G = relu(W_ae a + b_ae) [B][128] f32 (inputs of the
+//           fused critic), plus a bf16 copy of obs columns 0..31 (operand of the encoder wgrad)
+//   ACT     Actor on every robot row with epsilon-greedy exploration (agent.py:207-225,
+//           trainer.py:257-264): f64 actions for the env kernel
+//   FWD     Actor forward, f32 actions (target actor, agent.py:398)
+//   TRAIN   Actor forward saving bf16 activations for actor_bwd_kernel (agent.py:419-426)
+#include "asvrl_common.h"
+#include "asvrl_mfma.h"
+
+namespace asvrl {
+namespace {
+
+constexpr int kEnc = 256, kObsK = 32, kHid = 128, kNa = 2;
+constexpr int kSelfF = 56, kObjF = 40, kSelfIn = 7, kObjIn = 5, kObjN = 5;
+constexpr int kFragEnc = kEnc * kObsK / 8;   // 1024 fragments
+constexpr int kFragAe = kHid * 16 / 8;       // 256 (action encoder, K padded 2 -> 16)
+constexpr int kFragH1 = kHid * kEnc / 8;     // 4096
+constexpr int kFragH2 = kHid * kHid / 8;     // 2048
+constexpr int kMlpWaves = 4;
+enum { MLP_ENCODE = 0, MLP_ACT = 1, MLP_FWD = 2, MLP_TRAIN = 3 };
+
+struct MlpArgs {
+  AsvMlpWeights w;
+  AsvMlpIO io;
+};
+
+struct ActorLds {
+  bf16x8 enc[kFragEnc];
+  bf16x8 w1[kFragH1];
+  bf16x8 w2[kFragH2];
+  float benc[kEnc], b1[kHid], b2[kHid], wout[kNa * kHid], bout[kNa];
+};
+
+// object index of encoder feature m (>= 56)
+__host__ __device__ constexpr int obj_of(int m) { return (m - kSelfF) / kObjF; }
+
+// Encoder output of one 32-row tile: B operand from obs columns 0..31, 8 blocks in 2 halves;
+// epilogue bias + relu + mask. Hands each finished (block, s) group of 8 features to `emit`.
+template <typename Emit>
+__device__ __forceinline__ void encode_tile(const bf16x8* ENC, const float* benc, const bf16x8 (&bx)[2],
+                                            const float (&mk)[kObjN], int lane, Emit emit) {
+  const int h = lane >> 5;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    f32x16 acc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = mfma(ENC[((half * 4 + q) * 2 + ks) * 64 + lane], bx[ks], acc[q]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int mb = half * 4 + q;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int g = 8 * s + j;
+          const int m0 = mb * 32 + (g & 3) + 8 * (g >> 2);   // feature for h = 0; h = 1 adds 4
+          const float mk0 = m0 < kSelfF ? 1.f : (mk[obj_of(m0)] < 0.5f ? 0.f : 1.f);
+          const float mk1 = m0 + 4 < kSelfF ? 1.f : (mk[obj_of(m0 + 4)] < 0.5f ? 0.f : 1.f);
+          float x = acc[q][g] + benc[m0 + 4 * h];
+          x = x > 0.f ? x : 0.f;
+          v[j] = x * (h ? mk1 : mk0);
+        }
+        emit(mb, s, v);
+      }
+    }
+  }
+}
+
+// bf16 B operand of the encoder (obs columns 0..31) + the object mask, for row `row`
+__device__ __forceinline__ void load_obs(const float* __restrict__ x, int64_t ldx, int row, int h, bf16x8 (&bx)[2],
+                                         float (&mk)[kObjN]) {
+  const float* xr = x + static_cast<int64_t>(row) * ldx;
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const float4 u = *reinterpret_cast<const float4*>(xr + ks * 16 + 8 * h);
+    const float4 v = *reinterpret_cast<const float4*>(xr + ks * 16 + 8 * h + 4);
+    bx[ks][0] = (__bf16)u.x; bx[ks][1] = (__bf16)u.y; bx[ks][2] = (__bf16)u.z; bx[ks][3] = (__bf16)u.w;
+    bx[ks][4] = (__bf16)v.x; bx[ks][5] = (__bf16)v.y; bx[ks][6] = (__bf16)v.z; bx[ks][7] = (__bf16)v.w;
+  }
+#pragma unroll
+  for (int o = 0; o < kObjN; ++o) mk[o] = xr[32 + o];
+}
+
+// ------------------------------------------------------------------ ENCODE (critic F, G)
+__global__ __launch_bounds__(kMlpWaves * 64) void encode_kernel(MlpArgs a) {
+  const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
+  const int tile = blockIdx.x * kMlpWaves + (threadIdx.x >> 6);
+  const AsvMlpIO& io = a.io;
+  if (tile * 32 >= io.n) return;
+  const int row = tile * 32 + r;
+  const bool valid = row < io.n;
+  const int rr = valid ? row : io.n - 1;
+  bf16x8 bx[2];
+  float mk[kObjN];
+  load_obs(io.x, io.ldx, rr, h, bx, mk);
+  if (io.xb != nullptr && valid) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      *reinterpret_cast<bf16x8*>(bp(io.xb) + static_cast<int64_t>(row) * kObsK + ks * 16 + 8 * h) = bx[ks];
+  }
+  const bf16x8* ENC = reinterpret_cast<const bf16x8*>(a.w.enc_frag);
+  float* Fr = io.F + static_cast<int64_t>(rr) * kEnc;
+  encode_tile(ENC, a.w.b_enc, bx, mk, lane, [&](int mb, int s, const float* v) {
+    if (!valid) return;
+    float* o = Fr + mb * 32 + 16 * s + 4 * h;
+    *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(o + 8) = make_float4(v[4], v[5], v[6], v[7]);
+  });
+  if (io.G == nullptr) return;
+  // action encoder: B operand = (a0, a1, 0, ...) in lane half 0
+  bf16x8 ba{};
+  if (h == 0) {
+    const float* ar = io.act + static_cast<int64_t>(rr) * io.lda;
+    ba[0] = (__bf16)ar[0];
+    ba[1] = (__bf16)ar[1];
+  }
+  const bf16x8* AE = reinterpret_cast<const bf16x8*>(a.w.ae_frag);
+  float* Gr = io.G + static_cast<int64_t>(rr) * kHid;
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) {
+    const f32x16 acc = mfma(AE[mb * 64 + lane], ba, f32x16{});
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = acc[8 * s + j] + a.w.b_ae[feat(mb, 8 * s + j, h)];
+        v[j] = x > 0.f ? x : 0.f;
+      }
+      if (valid) {
+        float* o = Gr + mb * 32 + 16 * s + 4 * h;
+        *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(o + 8) = make_float4(v[4], v[5], v[6], v[7]);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ Actor forward (ACT/FWD/TRAIN)
+template <int MODE>
+__device__ __forceinline__ void actor_tile(const MlpArgs& a, const ActorLds& L, int tile, int lane) {
+  const AsvMlpIO& io = a.io;
+  const int h = lane >> 5, r = lane & 31;
+  const int row = tile * 32 + r;
+  const bool valid = row < io.n;
+  const int rr = valid ? row : io.n - 1;
+  bf16x8 bx[2];
+  float mk[kObjN];
+  load_obs(io.x, io.ldx, rr, h, bx, mk);
+  if (MODE == MLP_TRAIN && valid) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      *reinterpret_cast<bf16x8*>(bp(io.xb) + static_cast<int64_t>(row) * kObsK + ks * 16 + 8 * h) = bx[ks];
+  }
+  // encoders -> h0 (chained B operand of hidden_layer)
+  bf16x8 fpk[16];
+  encode_tile(L.enc, L.benc, bx, mk, lane, [&](int mb, int s, const float* v) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fpk[mb * 2 + s][j] = (__bf16)v[j];
+    if (MODE == MLP_TRAIN && valid) {
+      __bf16* o = bp(io.h0) + static_cast<int64_t>(row) * kEnc + mb * 32 + 16 * s + 4 * h;
+      store4(o, v);
+      store4(o + 8, v + 4);
+    }
+  });
+  // hidden_layer 256 -> 128, relu
+  f32x16 acc1[4];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) acc1[mb] = f32x16{};
+#pragma unroll
+  for (int ks = 0; ks < kEnc / 16; ++ks)
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) acc1[mb] = mfma(L.w1[(mb * 16 + ks) * 64 + lane], fpk[ks], acc1[mb]);
+  bf16x8 h1pk[8];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = acc1[mb][8 * s + j] + L.b1[feat(mb, 8 * s + j, h)];
+        v[j] = x > 0.f ? x : 0.f;
+        h1pk[mb * 2 + s][j] = (__bf16)v[j];
+      }
+      if (MODE == MLP_TRAIN && valid) {
+        __bf16* o = bp(io.h1) + static_cast<int64_t>(row) * kHid + mb * 32 + 16 * s + 4 * h;
+        store4(o, v);
+        store4(o + 8, v + 4);
+      }
+    }
+  // hidden_layer_2 128 -> 128, relu; output_layer 128 -> 2
+  f32x16 acc2[4];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) acc2[mb] = f32x16{};
+#pragma unroll
+  for (int ks = 0; ks < kHid / 16; ++ks)
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) acc2[mb] = mfma(L.w2[(mb * 8 + ks) * 64 + lane], h1pk[ks], acc2[mb]);
+  float p0 = 0.f, p1 = 0.f;
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = feat(mb, 8 * s + j, h);
+        const float x = acc2[mb][8 * s + j] + L.b2[m];
+        v[j] = x > 0.f ? x : 0.f;
+        p0 += L.wout[m] * v[j];
+        p1 += L.wout[kHid + m] * v[j];
+      }
+      if (MODE == MLP_TRAIN && valid) {
+        __bf16* o = bp(io.h2) + static_cast<int64_t>(row) * kHid + mb * 32 + 16 * s + 4 * h;
+        store4(o, v);
+        store4(o + 8, v + 4);
+      }
+    }
+  const float z0 = p0 + __shfl_xor(p0, 32, 64) + L.bout[0];
+  const float z1 = p1 + __shfl_xor(p1, 32, 64) + L.bout[1];
+  const float a0 = a.w.out_scale * atanf(z0);   // atan_scale * torch.atan(actions)
+  const float a1 = a.w.out_scale * atanf(z1);
+  if (!valid || h != 0) return;
+  if (MODE == MLP_ACT) {
+    // epsilon-greedy (agent.py:207-225): greedy iff random() > eps, else uniform(-1, 1) per dim;
+    // eps: linear schedule of the device step counter (trainer.py:257-264)
+    const uint64_t step = io.step_dev != nullptr ? static_cast<uint64_t>(*io.step_dev) : 0ull;
+    const double progress = static_cast<double>(step) * io.eps_steps_per_count / io.eps_total;
+    const double eps = progress < io.eps_fraction
+                           ? io.eps_initial + (progress / io.eps_fraction) * (io.eps_final - io.eps_initial)
+                           : io.eps_final;
+    const U4 u = philox4x32_10(U4{static_cast<uint32_t>(row), static_cast<uint32_t>(step),
+                                  static_cast<uint32_t>(step >> 32), 0xAC7u},
+                               static_cast<uint32_t>(io.seed), static_cast<uint32_t>(io.seed >> 32));
+    const double c = (static_cast<double>(u.x >> 8) + 1.0) * (1.0 / 16777216.0);   // (0, 1]
+    double* o = io.a_out64 + static_cast<int64_t>(row) * 2;
+    if (c > eps) {
+      o[0] = a0;
+      o[1] = a1;
+    } else {
+      o[0] = 2.0 * (static_cast<double>(u.y >> 8) * (1.0 / 16777216.0)) - 1.0;
+      o[1] = 2.0 * (static_cast<double>(u.z >> 8) * (1.0 / 16777216.0)) - 1.0;
+    }
+  } else {
+    float* o = io.a_out + static_cast<int64_t>(row) * io.ld_aout;
+    o[0] = a0;
+    o[1] = a1;
+    if (MODE == MLP_TRAIN) {
+      io.pre[static_cast<int64_t>(row) * 2] = z0;
+      io.pre[static_cast<int64_t>(row) * 2 + 1] = z1;
+    }
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kMlpWaves * 64) void actor_kernel(MlpArgs a) {
+  __shared__ ActorLds L;
+  {
+    const bf16x8* ge = reinterpret_cast<const bf16x8*>(a.w.enc_frag);
+    const bf16x8* g1 = reinterpret_cast<const bf16x8*>(a.w.w1_frag);
+    const bf16x8* g2 = reinterpret_cast<const bf16x8*>(a.w.w2_frag);
+    for (int i = threadIdx.x; i < kFragEnc; i += kMlpWaves * 64) L.enc[i] = ge[i];
+    for (int i = threadIdx.x; i < kFragH1; i += kMlpWaves * 64) L.w1[i] = g1[i];
+    for (int i = threadIdx.x; i < kFragH2; i += kMlpWaves * 64) L.w2[i] = g2[i];
+    for (int i = threadIdx.x; i < kEnc; i += kMlpWaves * 64) L.benc[i] = a.w.b_enc[i];
+    for (int i = threadIdx.x; i < kHid; i += kMlpWaves * 64) {
+      L.b1[i] = a.w.b1[i];
+      L.b2[i] = a.w.b2[i];
+      L.wout[i] = a.w.wout[i];
+      L.wout[kHid + i] = a.w.wout[kHid + i];
+    }
+    if (threadIdx.x < kNa) L.bout[threadIdx.x] = a.w.bout[threadIdx.x];
+  }
+  __syncthreads();
+  const int tile = blockIdx.x * kMlpWaves + (threadIdx.x >> 6);
+  if (tile * 32 < a.io.n) actor_tile<MODE>(a, L, tile, threadIdx.x & 63);
+}
+
+// ------------------------------------------------------------------ Actor backward
+// From dL/d(action) [n][2]: dOut = dA * scale / (1 + z^2) (atan), dz2 = (Wout^T dOut) 1[h2 > 0],
+// dz1 = (W2^T dz2) 1[h1 > 0], dz0 = (W1^T dz1) 1[h0 > 0] (relu and masked_fill both zero where
+// h0 == 0). Writes dOut f32 and dz2, dz1, dz0 bf16 for the weight gradients.
+struct ActorBwdLds {
+  bf16x8 w2t[kFragH2];
+  bf16x8 w1t[kFragH1];
+  float wout[kNa * kHid];
+};
+
+__global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_kernel(MlpArgs a) {
+  __shared__ ActorBwdLds L;
+  {
+    const bf16x8* g2 = reinterpret_cast<const bf16x8*>(a.w.w2t_frag);
+    const bf16x8* g1 = reinterpret_cast<const bf16x8*>(a.w.w1t_frag);
+    for (int i = threadIdx.x; i < kFragH2; i += kMlpWaves * 64) L.w2t[i] = g2[i];
+    for (int i = threadIdx.x; i < kFragH1; i += kMlpWaves * 64) L.w1t[i] = g1[i];
+    for (int i = threadIdx.x; i < kNa * kHid; i += kMlpWaves * 64) L.wout[i] = a.w.wout[i];
+  }
+  __syncthreads();
+  const AsvMlpIO& io = a.io;
+  const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
+  const int tile = blockIdx.x * kMlpWaves + (threadIdx.x >> 6);
+  if (tile * 32 >= io.n) return;
+  const int row = tile * 32 + r;
+  const bool valid = row < io.n;
+  const int64_t rr = valid ? row : io.n - 1;
+  const float z0 = io.pre[rr * 2], z1 = io.pre[rr * 2 + 1];
+  const float d0 = io.dA[rr * 2] * a.w.out_scale / (1.f + z0 * z0);
+  const float d1 = io.dA[rr * 2 + 1] * a.w.out_scale / (1.f + z1 * z1);
+  if (valid && h == 0) {
+    io.dout[row * 2] = d0;
+    io.dout[row * 2 + 1] = d1;
+  }
+  // dz2 (chained B operand of W2^T)
+  bf16x8 dz2pk[8];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int64_t off = rr * kHid + mb * 32 + 16 * s + 4 * h;
+      float hv[8], dv[8];
+      load4(bp(io.h2) + off, hv);
+      load4(bp(io.h2) + off + 8, hv + 4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = feat(mb, 8 * s + j, h);
+        dv[j] = hv[j] > 0.f ? L.wout[m] * d0 + L.wout[kHid + m] * d1 : 0.f;
+        dz2pk[mb * 2 + s][j] = (__bf16)dv[j];
+      }
+      if (valid) {
+        store4(bp(io.dz2) + row * kHid + mb * 32 + 16 * s + 4 * h, dv);
+        store4(bp(io.dz2) + row * kHid + mb * 32 + 16 * s + 4 * h + 8, dv + 4);
+      }
+    }
+  // dh1 = W2^T dz2 -> dz1
+  f32x16 acc3[4];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) acc3[mb] = f32x16{};
+#pragma unroll
+  for (int ks = 0; ks < kHid / 16; ++ks)
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) acc3[mb] = mfma(L.w2t[(mb * 8 + ks) * 64 + lane], dz2pk[ks], acc3[mb]);
+  bf16x8 dz1pk[8];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int64_t off = rr * kHid + mb * 32 + 16 * s + 4 * h;
+      float hv[8], dv[8];
+      load4(bp(io.h1) + off, hv);
+      load4(bp(io.h1) + off + 8, hv + 4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        dv[j] = hv[j] > 0.f ? acc3[mb][8 * s + j] : 0.f;
+        dz1pk[mb * 2 + s][j] = (__bf16)dv[j];
+      }
+      if (valid) {
+        store4(bp(io.dz1) + row * kHid + mb * 32 + 16 * s + 4 * h, dv);
+        store4(bp(io.dz1) + row * kHid + mb * 32 + 16 * s + 4 * h + 8, dv + 4);
+      }
+    }
+  // dh0 = W1^T dz1 -> dz0 (two halves of 4 blocks)
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    f32x16 acc4[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc4[q] = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < kHid / 16; ++ks)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc4[q] = mfma(L.w1t[((half * 4 + q) * 8 + ks) * 64 + lane], dz1pk[ks], acc4[q]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int mb = half * 4 + q;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int64_t off = rr * kEnc + mb * 32 + 16 * s + 4 * h;
+        float hv[8], dv[8];
+        load4(bp(io.h0) + off, hv);
+        load4(bp(io.h0) + off + 8, hv + 4);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dv[j] = hv[j] > 0.f ? acc4[q][8 * s + j] : 0.f;
+        if (valid) {
+          store4(bp(io.dz0) + row * kEnc + mb * 32 + 16 * s + 4 * h, dv);
+          store4(bp(io.dz0) + row * kEnc + mb * 32 + 16 * s + 4 * h + 8, dv + 4);
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ packing
+// enc image (256 x 32, input-fed) from self_encoder / object_encoder, b_enc, the action-encoder
+// image (128 x 16, input-fed, columns 2..15 zero) and the chained W1, W2, W2^T, W1^T images.
+constexpr int kPackEnc = kEnc * kObsK, kPackAe = kHid * 16, kPackW1 = kHid * kEnc, kPackW2 = kHid * kHid;
+
+__device__ __forceinline__ float enc_weight(const AsvMlpSrc& s, int m, int k) {
+  if (m < kSelfF) return k < kSelfIn ? s.self_w[m * kSelfIn + k] : 0.f;
+  const int o = obj_of(m), j = (m - kSelfF) % kObjF, c = k - kSelfIn - kObjIn * o;
+  return (c >= 0 && c < kObjIn) ? s.obj_w[j * kObjIn + c] : 0.f;
+}
+
+__global__ __launch_bounds__(256) void mlp_pack_kernel(AsvMlpSrc src, AsvMlpWeights w) {
+  int o = blockIdx.x * 256 + threadIdx.x;
+  int row, col;
+  if (o < kPackEnc) {
+    frag_rc(o, kObsK, false, row, col);
+    const_cast<__bf16*>(static_cast<const __bf16*>(w.enc_frag))[o] = (__bf16)enc_weight(src, row, col);
+    if (o < kEnc)
+      const_cast<float*>(w.b_enc)[o] = o < kSelfF ? src.self_b[o] : src.obj_b[(o - kSelfF) % kObjF];
+    return;
+  }
+  o -= kPackEnc;
+  if (o < kPackAe) {
+    if (w.ae_frag == nullptr) return;
+    frag_rc(o, 16, false, row, col);
+    const_cast<__bf16*>(static_cast<const __bf16*>(w.ae_frag))[o] =
+        (__bf16)(col < kNa ? src.ae_w[row * kNa + col] : 0.f);
+    return;
+  }
+  o -= kPackAe;
+  if (src.w1 == nullptr) return;
+  if (o < kPackW1) {
+    frag_rc(o, kEnc, true, row, col);
+    const_cast<__bf16*>(static_cast<const __bf16*>(w.w1_frag))[o] = (__bf16)src.w1[row * kEnc + col];
+    return;
+  }
+  o -= kPackW1;
+  if (o < kPackW2) {
+    frag_rc(o, kHid, true, row, col);
+    const_cast<__bf16*>(static_cast<const __bf16*>(w.w2_frag))[o] = (__bf16)src.w2[row * kHid + col];
+    return;
+  }
+  o -= kPackW2;
+  if (o < kPackW2) {
+    frag_rc(o, kHid, true, row, col);
+    const_cast<__bf16*>(static_cast<const __bf16*>(w.w2t_frag))[o] = (__bf16)src.w2[col * kHid + row];
+    return;
+  }
+  o -= kPackW2;
+  if (o < kPackW1) {  // W1^T (256 x 128)
+    frag_rc(o, kHid, true, row, col);
+    const_cast<__bf16*>(static_cast<const __bf16*>(w.w1t_frag))[o] = (__bf16)src.w1[col * kEnc + row];
+  }
+}
+
+// Encoder weight gradient (256 x 32 image) folded back onto the two Linear layers:
+// self_w[m][k] = dW[m][k]; obj_w[j][c] = sum_o dW[56 + 40o + j][7 + 5o + c]; likewise biases.
+__global__ __launch_bounds__(256) void enc_fold_kernel(const float* __restrict__ dw, const float* __restrict__ db,
+                                                        float* self_w, float* self_b, float* obj_w, float* obj_b,
+                                                        int accumulate) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  auto put = [&](float* p, float v) { *p = accumulate ? *p + v : v; };
+  if (t < kSelfF * kSelfIn) {
+    const int m = t / kSelfIn, k = t % kSelfIn;
+    put(self_w + t, dw[m * kObsK + k]);
+  } else if (t < kSelfF * kSelfIn + kObjF * kObjIn) {
+    const int u = t - kSelfF * kSelfIn, j = u / kObjIn, c = u % kObjIn;
+    float s = 0.f;
+    for (int o = 0; o < kObjN; ++o) s += dw[(kSelfF + kObjF * o + j) * kObsK + kSelfIn + kObjIn * o + c];
+    put(obj_w + u, s);
+  } else if (t < kSelfF * kSelfIn + kObjF * kObjIn + kSelfF) {
+    const int m = t - kSelfF * kSelfIn - kObjF * kObjIn;
+    put(self_b + m, db[m]);
+  } else if (t < kSelfF * kSelfIn + kObjF * kObjIn + kSelfF + kObjF) {
+    const int j = t - kSelfF * kSelfIn - kObjF * kObjIn - kSelfF;
+    float s = 0.f;
+    for (int o = 0; o < kObjN; ++o) s += db[kSelfF + kObjF * o + j];
+    put(obj_b + j, s);
+  }
+}
+
+// dW[m][k] = sum_r dz[r][m] x[r][k], db[m] = sum_r dz[r][m] for a small f32 input (K <= 4): the
+// critic action_encoder (2 -> 128). Block b handles rows [256b, 256b + 256); partials [blk][M*K+M].
+__global__ __launch_bounds__(256) void small_wgrad_kernel(const float* __restrict__ dz, int64_t ldz,
+                                                           const float* __restrict__ x, int64_t ldx, int R, int M,
+                                                           int K, float* __restrict__ partial) {
+  const int t = threadIdx.x;
+  const int per = 256 / M;   // rows in flight (M divides 256)
+  const int m = t % M, rq = t / M;
+  float sw[4] = {0.f, 0.f, 0.f, 0.f}, sb = 0.f;
+  const int r0 = blockIdx.x * 256, r1 = min(R, r0 + 256);
+  for (int r = r0 + rq; r < r1; r += per) {
+    const float d = dz[static_cast<int64_t>(r) * ldz + m];
+    sb += d;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (k < K) sw[k] += d * x[static_cast<int64_t>(r) * ldx + k];
+  }
+  __shared__ float red[256][5];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) red[t][k] = sw[k];
+  red[t][4] = sb;
+  __syncthreads();
+  if (t < M) {
+    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int u = t; u < 256; u += M)
+#pragma unroll
+      for (int k = 0; k < 5; ++k) acc[k] += red[u][k];
+    float* p = partial + static_cast<int64_t>(blockIdx.x) * (M * K + M);
+    for (int k = 0; k < K; ++k) p[t * K + k] = acc[k];
+    p[M * K + t] = acc[4];
+  }
+}
+
+}  // namespace
+}  // namespace asvrl
+
+using namespace asvrl;
+
+extern "C" int asvrl_mlp_pack(const AsvMlpSrc* src, const AsvMlpWeights* w, void* stream) {
+  ASVRL_REQUIRE(src && w && src->self_w && src->self_b && src->obj_w && src->obj_b && w->enc_frag && w->b_enc,
+                "asvrl_mlp_pack: null argument");
+  ASVRL_REQUIRE(!src->w1 || (src->w2 && w->w1_frag && w->w2_frag && w->w2t_frag && w->w1t_frag),
+                "asvrl_mlp_pack: actor weights need all four hidden-layer images");
+  ASVRL_REQUIRE(!w->ae_frag || src->ae_w, "asvrl_mlp_pack: action-encoder image without weights");
+  const int total = kPackEnc + kPackAe + (src->w1 ? 2 * kPackW1 + 2 * kPackW2 : 0);
+  hipLaunchKernelGGL(mlp_pack_kernel, dim3((total + 255) / 256), dim3(256), 0, as_stream(stream), *src, *w);
+  return check_launch("asvrl_mlp_pack");
+}
+
+extern "C" int asvrl_mlp_encode(const AsvMlpWeights* w, const AsvMlpIO* io, void* stream) {
+  ASVRL_REQUIRE(w && io && io->x && io->F && w->enc_frag && w->b_enc, "asvrl_mlp_encode: null argument");
+  ASVRL_REQUIRE(!io->G || (io->act && w->ae_frag && w->b_ae), "asvrl_mlp_encode: G needs actions and ae weights");
+  ASVRL_REQUIRE(io->ldx % 4 == 0 && reinterpret_cast<uintptr_t>(io->x) % 16 == 0,
+                "asvrl_mlp_encode: obs rows must be 16-byte aligned");
+  if (io->n <= 0) return 0;
+  MlpArgs a{*w, *io};
+  const int tiles = (io->n + 31) / 32;
+  hipLaunchKernelGGL(encode_kernel, dim3((tiles + kMlpWaves - 1) / kMlpWaves), dim3(kMlpWaves * 64), 0,
+                     as_stream(stream), a);
+  return check_launch("asvrl_mlp_encode");
+}
+
+extern "C" int asvrl_actor_forward(const AsvMlpWeights* w, const AsvMlpIO* io, int32_t mode, void* stream) {
+  ASVRL_REQUIRE(w && io && io->x && w->enc_frag && w->w1_frag && w->w2_frag && w->b1 && w->b2 && w->wout && w->bout,
+                "asvrl_actor_forward: null argument");
+  ASVRL_REQUIRE(mode == MLP_ACT || mode == MLP_FWD || mode == MLP_TRAIN, "asvrl_actor_forward: bad mode");
+  ASVRL_REQUIRE(mode != MLP_ACT || io->a_out64, "asvrl_actor_forward: ACT needs a_out64");
+  ASVRL_REQUIRE(mode == MLP_ACT || io->a_out, "asvrl_actor_forward: needs a_out");
+  ASVRL_REQUIRE(mode != MLP_TRAIN || (io->xb && io->h0 && io->h1 && io->h2 && io->pre),
+                "asvrl_actor_forward: TRAIN needs xb, h0, h1, h2, pre");
+  ASVRL_REQUIRE(io->ldx % 4 == 0 && reinterpret_cast<uintptr_t>(io->x) % 16 == 0,
+                "asvrl_actor_forward: obs rows must be 16-byte aligned");
+  if (io->n <= 0) return 0;
+  MlpArgs a{*w, *io};
+  const int tiles = (io->n + 31) / 32;
+  const dim3 grid((tiles + kMlpWaves - 1) / kMlpWaves), block(kMlpWaves * 64);
+  hipStream_t st = as_stream(stream);
+  if (mode == MLP_ACT) hipLaunchKernelGGL(actor_kernel<MLP_ACT>, grid, block, 0, st, a);
+  else if (mode == MLP_FWD) hipLaunchKernelGGL(actor_kernel<MLP_FWD>, grid, block, 0, st, a);
+  else hipLaunchKernelGGL(actor_kernel<MLP_TRAIN>, grid, block, 0, st, a);
+  return check_launch("asvrl_actor_forward");
+}
+
+extern "C" int asvrl_actor_backward(const AsvMlpWeights* w, const AsvMlpIO* io, void* stream) {
+  ASVRL_REQUIRE(w && io && w->w2t_frag && w->w1t_frag && w->wout && io->dA && io->pre && io->h0 && io->h1 &&
+                    io->h2 && io->dout && io->dz2 && io->dz1 && io->dz0,
+                "asvrl_actor_backward: null argument");
+  if (io->n <= 0) return 0;
+  MlpArgs a{*w, *io};
+  const int tiles = (io->n + 31) / 32;
+  hipLaunchKernelGGL(actor_bwd_kernel, dim3((tiles + kMlpWaves - 1) / kMlpWaves), dim3(kMlpWaves * 64), 0,
+                     as_stream(stream), a);
+  return check_launch("asvrl_actor_backward");
+}
+
+extern "C" int asvrl_encoder_fold(const float* dw, const float* db, float* self_w, float* self_b, float* obj_w,
+                                  float* obj_b, int32_t accumulate, void* stream) {
+  ASVRL_REQUIRE(dw && db && self_w && self_b && obj_w && obj_b, "asvrl_encoder_fold: null argument");
+  const int n = kSelfF * kSelfIn + kObjF * kObjIn + kSelfF + kObjF;
+  hipLaunchKernelGGL(enc_fold_kernel, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream), dw, db, self_w,
+                     self_b, obj_w, obj_b, accumulate);
+  return check_launch("asvrl_encoder_fold");
+}
+
+extern "C" int asvrl_small_wgrad(const float* dz, int64_t ldz, const float* x, int64_t ldx, int32_t R, int32_t M,
+                                 int32_t K, float* dw, float* db, int32_t accumulate, float* work, int64_t work_floats,
+                                 void* stream) {
+  ASVRL_REQUIRE(dz && x && dw && work, "asvrl_small_wgrad: null argument");
+  ASVRL_REQUIRE(M >= 1 && M <= 256 && 256 % M == 0 && K >= 1 && K <= 4, "asvrl_small_wgrad: M | 256, K <= 4");
+  if (R <= 0) return 0;
+  const int groups = (R + 255) / 256;
+  ASVRL_REQUIRE(work_floats >= static_cast<int64_t>(groups) * (M * K + M), "asvrl_small_wgrad: workspace too small");
+  hipLaunchKernelGGL(small_wgrad_kernel, dim3(groups), dim3(256), 0, as_stream(stream), dz, ldz, x, ldx, R, M, K,
+                     work);
+  if (int rc = check_launch("asvrl_small_wgrad")) return rc;
+  return launch_partial_sum(work, groups, M * K, M, dw, db, accumulate, as_stream(stream));
+}

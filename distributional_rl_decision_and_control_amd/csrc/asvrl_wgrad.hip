@@ -62,11 +62,13 @@ struct Shape {
   static constexpr int NMW = kWide ? NBW / NKB : 1;        // m-blocks per wave
   static constexpr int NKW = kWide ? NKB : NBW;            // k-blocks per wave
   static constexpr int SZ = lds_stride(M), SX = lds_stride(K);
-  static constexpr int CZ = kRC * M / 8 / kWgThreads;      // 16-B chunks per thread (dZ)
-  static constexpr int CX = kRC * K / 8 / kWgThreads;      // (X)
+  static constexpr int NCZ = kRC * M / 8, NCX = kRC * K / 8;           // 16-B chunks per staged chunk
+  static constexpr int CZ = NCZ >= kWgThreads ? NCZ / kWgThreads : 1;    // per thread (dZ)
+  static constexpr int CX = NCX >= kWgThreads ? NCX / kWgThreads : 1;    // (X); < 256 chunks: some threads idle
   static_assert(M % 32 == 0 && K % 32 == 0 && NB % 4 == 0, "block grid must split over 4 waves");
   static_assert(kWide ? (NBW % NKB == 0) : (NKB % NBW == 0), "wave blocks must tile rows or columns");
-  static_assert(CZ >= 1 && CX >= 1, "at least one chunk per thread");
+  static_assert(NCZ % kWgThreads == 0 || kWgThreads % NCZ == 0, "dZ chunks must tile the block");
+  static_assert(NCX % kWgThreads == 0 || kWgThreads % NCX == 0, "X chunks must tile the block");
 };
 
 template <int M, int K>
@@ -85,6 +87,7 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const __bf16* __restr
   const int zc8 = t % (M / 8), zr = t / (M / 8);
   const int xc8 = t % (K / 8), xr = t / (K / 8);
   constexpr int ZRS = kWgThreads * 8 / M, XRS = kWgThreads * 8 / K;   // row step between a thread's chunks
+  const bool zact = t < S::NCZ, xact = t < S::NCX;                     // staging threads
   u32x4 rz[S::CZ], rx[S::CX];
   float bacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   f32x16 acc[S::NMW * S::NKW];
@@ -94,23 +97,27 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const __bf16* __restr
   const int kb0 = S::kWide ? 0 : (w * S::NBW) % S::NKB;
 
   if (c_beg < c_end) {
-    load_rows<S::CZ, ZRS>(rz, dz, ldz, static_cast<int64_t>(c_beg) * kRC + zr, zc8);
-    load_rows<S::CX, XRS>(rx, x, ldx, static_cast<int64_t>(c_beg) * kRC + xr, xc8);
+    if (zact) load_rows<S::CZ, ZRS>(rz, dz, ldz, static_cast<int64_t>(c_beg) * kRC + zr, zc8);
+    if (xact) load_rows<S::CX, XRS>(rx, x, ldx, static_cast<int64_t>(c_beg) * kRC + xr, xc8);
   }
   for (int c = c_beg; c < c_end; ++c) {
+    if (zact) {
 #pragma unroll
-    for (int i = 0; i < S::CZ; ++i) {
-      *reinterpret_cast<u32x4*>(lz + (zr + i * ZRS) * S::SZ + zc8 * 16) = rz[i];
-      const bf16x8 v = __builtin_bit_cast(bf16x8, rz[i]);
+      for (int i = 0; i < S::CZ; ++i) {
+        *reinterpret_cast<u32x4*>(lz + (zr + i * ZRS) * S::SZ + zc8 * 16) = rz[i];
+        const bf16x8 v = __builtin_bit_cast(bf16x8, rz[i]);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) bacc[j] += static_cast<float>(v[j]);
+        for (int j = 0; j < 8; ++j) bacc[j] += static_cast<float>(v[j]);
+      }
     }
+    if (xact) {
 #pragma unroll
-    for (int i = 0; i < S::CX; ++i) *reinterpret_cast<u32x4*>(lx + (xr + i * XRS) * S::SX + xc8 * 16) = rx[i];
+      for (int i = 0; i < S::CX; ++i) *reinterpret_cast<u32x4*>(lx + (xr + i * XRS) * S::SX + xc8 * 16) = rx[i];
+    }
     __syncthreads();
     if (c + 1 < c_end) {   // prefetch under the MFMAs
-      load_rows<S::CZ, ZRS>(rz, dz, ldz, static_cast<int64_t>(c + 1) * kRC + zr, zc8);
-      load_rows<S::CX, XRS>(rx, x, ldx, static_cast<int64_t>(c + 1) * kRC + xr, xc8);
+      if (zact) load_rows<S::CZ, ZRS>(rz, dz, ldz, static_cast<int64_t>(c + 1) * kRC + zr, zc8);
+      if (xact) load_rows<S::CX, XRS>(rx, x, ldx, static_cast<int64_t>(c + 1) * kRC + xr, xc8);
     }
 #pragma unroll
     for (int ks = 0; ks < kRC / 16; ++ks) {
@@ -156,7 +163,7 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const __bf16* __restr
 // dw[k] = sum_r dq[r] * X[r][k], db = sum_r dq[r] for an output layer with one unit.
 // Thread t reads 16 bytes (8 columns) of row t / (K/8) + i * RP: RP rows in flight per block.
 template <int K>
-__global__ __launch_bounds__(kWgThreads) void wgrad_vec_kernel(const float* __restrict__ dq,
+__global__ __launch_bounds__(kWgThreads) void wgrad_vec_kernel(const float* __restrict__ dq, int64_t ldq,
                                                                 const __bf16* __restrict__ x, int64_t ldx, int R,
                                                                 int rows_per_group, float* __restrict__ partial) {
   constexpr int C8 = K / 8, RP = kWgThreads / C8;
@@ -165,7 +172,7 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_vec_kernel(const float* __re
   float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float b = 0.f;
   for (int r = r_beg + rr; r < r_end; r += RP) {
-    const float d = dq[r];
+    const float d = dq[static_cast<int64_t>(r) * ldq];
     const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + static_cast<int64_t>(r) * ldx + c8 * 8);
 #pragma unroll
     for (int j = 0; j < 8; ++j) a[j] += d * static_cast<float>(v[j]);
@@ -233,6 +240,15 @@ int launch_wgrad(const __bf16* dz, int64_t ldz, const __bf16* x, int64_t ldx, in
 }
 
 }  // namespace
+
+int launch_partial_sum(const float* partial, int groups, int nw, int nb, float* dw, float* db, int accumulate,
+                       hipStream_t st) {
+  const int n = nw + nb;
+  hipLaunchKernelGGL(partial_sum_kernel, dim3((n + 63) / 64), dim3(kWgThreads), 0, st, partial, groups, nw, nb, dw,
+                     db, accumulate);
+  return check_launch("partial_sum");
+}
+
 }  // namespace asvrl
 
 using namespace asvrl;
@@ -260,6 +276,7 @@ extern "C" int asvrl_linear_wgrad(const void* dz, int64_t ldz, const void* x, in
   else if (M == 128 && K == 256) rc = launch_wgrad<128, 256>(z, ldz, xx, ldx, R, work, st, groups);
   else if (M == 128 && K == 128) rc = launch_wgrad<128, 128>(z, ldz, xx, ldx, R, work, st, groups);
   else if (M == 64 && K == 64) rc = launch_wgrad<64, 64>(z, ldz, xx, ldx, R, work, st, groups);
+  else if (M == 256 && K == 32) rc = launch_wgrad<256, 32>(z, ldz, xx, ldx, R, work, st, groups);
   else ASVRL_REQUIRE(false, "asvrl_linear_wgrad: unsupported (M, K)");
   if (rc) return rc;
   const int n = M * K + M;
@@ -268,7 +285,7 @@ extern "C" int asvrl_linear_wgrad(const void* dz, int64_t ldz, const void* x, in
   return check_launch("asvrl_linear_wgrad(sum)");
 }
 
-extern "C" int asvrl_linear_wgrad_vec(const float* dq, const void* x, int64_t ldx, int32_t R, int32_t K, float* dw,
+extern "C" int asvrl_linear_wgrad_vec(const float* dq, int64_t ldq, const void* x, int64_t ldx, int32_t R, int32_t K, float* dw,
                                       float* db, int32_t accumulate, float* work, int64_t work_floats, void* stream) {
   ASVRL_REQUIRE(dq && x && dw && work, "asvrl_linear_wgrad_vec: null argument");
   ASVRL_REQUIRE(K == 128 || K == 256 || K == 64, "asvrl_linear_wgrad_vec: K must be 64, 128 or 256");
@@ -281,9 +298,9 @@ extern "C" int asvrl_linear_wgrad_vec(const float* dq, const void* x, int64_t ld
   const int per = (R + groups - 1) / groups;
   groups = (R + per - 1) / per;
   const __bf16* xx = static_cast<const __bf16*>(x);
-  if (K == 128) hipLaunchKernelGGL(wgrad_vec_kernel<128>, dim3(groups), dim3(kWgThreads), 0, st, dq, xx, ldx, R, per, work);
-  else if (K == 256) hipLaunchKernelGGL(wgrad_vec_kernel<256>, dim3(groups), dim3(kWgThreads), 0, st, dq, xx, ldx, R, per, work);
-  else hipLaunchKernelGGL(wgrad_vec_kernel<64>, dim3(groups), dim3(kWgThreads), 0, st, dq, xx, ldx, R, per, work);
+  if (K == 128) hipLaunchKernelGGL(wgrad_vec_kernel<128>, dim3(groups), dim3(kWgThreads), 0, st, dq, ldq, xx, ldx, R, per, work);
+  else if (K == 256) hipLaunchKernelGGL(wgrad_vec_kernel<256>, dim3(groups), dim3(kWgThreads), 0, st, dq, ldq, xx, ldx, R, per, work);
+  else hipLaunchKernelGGL(wgrad_vec_kernel<64>, dim3(groups), dim3(kWgThreads), 0, st, dq, ldq, xx, ldx, R, per, work);
   if (int rc = check_launch("asvrl_linear_wgrad_vec")) return rc;
   hipLaunchKernelGGL(partial_sum_kernel, dim3((K + 1 + 63) / 64), dim3(kWgThreads), 0, st, work, groups, K, 1, dw,
                      db, accumulate);

@@ -81,12 +81,24 @@ class CriticPack:
         return out
 
 
+def _io(F, G, taus, N, **kw):
+    """AsvCriticIO for one launch; tensors become device pointers, None -> NULL."""
+    io = _abi.AsvCriticIO()
+    io.F, io.G, io.taus = F.data_ptr(), G.data_ptr(), taus.data_ptr()
+    io.B, io.N = F.shape[0], N
+    io.Np, io.kappa, io.gamma, io.dq, io.ld_rd = kw.pop("Np", 0), kw.pop("kappa", 1.0), kw.pop("gamma", 0.0), \
+        kw.pop("dq", 0.0), kw.pop("ld_rd", 1)
+    for k, v in kw.items():
+        setattr(io, k, v.data_ptr() if v is not None else None)
+    return io
+
+
 def critic_forward(pack, F, G, taus, N, q=None, stream=None):
     B = F.shape[0]
     q = q if q is not None else torch.empty(B * N, dtype=torch.float32, device=F.device)
-    rc = _abi.lib().asvrl_critic_forward(C.byref(pack.struct), _abi.ptr(F), _abi.ptr(G), _abi.ptr(taus), B, N,
-                                         _abi.ptr(q), _abi.stream_ptr(stream))
-    _abi.check(rc, "asvrl_critic_forward")
+    io = _io(F, G, taus, N, q=q)
+    _abi.check(_abi.lib().asvrl_critic_forward(C.byref(pack.struct), C.byref(io), _abi.stream_ptr(stream)),
+               "asvrl_critic_forward")
     return q.view(B, N)
 
 
@@ -117,21 +129,31 @@ class TrainBuffers:
         self.struct = a
 
 
-def critic_train(pack, F, G, taus, q_targets, bufs, kappa=1.0, stream=None):
-    B, N, Np = F.shape[0], bufs.N, q_targets.shape[1]
-    rc = _abi.lib().asvrl_critic_train(C.byref(pack.struct), _abi.ptr(F), _abi.ptr(G), _abi.ptr(taus),
-                                       _abi.ptr(q_targets), B, N, Np, float(kappa), _abi.ptr(bufs.q),
-                                       _abi.ptr(bufs.row_loss), _abi.ptr(bufs.dF), _abi.ptr(bufs.dG),
-                                       C.byref(bufs.struct), _abi.stream_ptr(stream))
-    _abi.check(rc, "asvrl_critic_train")
+def critic_train(pack, F, G, taus, q_targets, bufs, kappa=1.0, stream=None, q_next=None, rewards=None, dones=None,
+                 gamma=0.99, dzF=None, dzG=None, with_dFdG=True):
+    """TRAIN launch. Targets: q_targets (B, Np), or q_next (B, Np) with rewards/dones column
+    views (stride ld) combined in the kernel. Returns the loss as a 0-d device tensor."""
+    B, N = F.shape[0], bufs.N
+    Np = (q_targets if q_targets is not None else q_next).shape[1]
+    kw = dict(q=bufs.q, row_loss=bufs.row_loss, dzF=dzF, dzG=dzG)
+    if with_dFdG:
+        kw.update(dF=bufs.dF, dG=bufs.dG)
+    if q_targets is not None:
+        kw["q_targets"] = q_targets
+    else:
+        kw.update(q_next=q_next, rewards=rewards, dones=dones, ld_rd=rewards.stride(0), gamma=float(gamma))
+    io = _io(F, G, taus, N, Np=Np, kappa=float(kappa), **kw)
+    _abi.check(_abi.lib().asvrl_critic_train(C.byref(pack.struct), C.byref(io), C.byref(bufs.struct),
+                                             _abi.stream_ptr(stream)), "asvrl_critic_train")
     return bufs.row_loss.sum() / float(B * Np)
 
 
-def critic_actor_grad(pack, F, G, taus, N, q, dG, stream=None):
+def critic_actor_grad(pack, F, G, taus, N, q, dG=None, stream=None, w_ae=None, dA=None):
+    """ACTOR launch: dq = -1/(B*N) on every row; writes dG and/or dA (with w_ae)."""
     B = F.shape[0]
-    rc = _abi.lib().asvrl_critic_actor_grad(C.byref(pack.struct), _abi.ptr(F), _abi.ptr(G), _abi.ptr(taus), B, N,
-                                            -1.0 / float(B * N), _abi.ptr(q), _abi.ptr(dG), _abi.stream_ptr(stream))
-    _abi.check(rc, "asvrl_critic_actor_grad")
+    io = _io(F, G, taus, N, dq=-1.0 / float(B * N), q=q, dG=dG, w_ae=w_ae, dA=dA)
+    _abi.check(_abi.lib().asvrl_critic_actor_grad(C.byref(pack.struct), C.byref(io), _abi.stream_ptr(stream)),
+               "asvrl_critic_actor_grad")
 
 
 def linear_wgrad(dz, x, dw, db, work, accumulate=False, stream=None):
@@ -145,9 +167,10 @@ def linear_wgrad(dz, x, dw, db, work, accumulate=False, stream=None):
 
 
 def linear_wgrad_vec(dq, x, dw, db, work, accumulate=False, stream=None):
-    """dw (K,) <- dq^T x, db (1,) <- dq.sum() with dq (R,) f32, x (R, K) bf16."""
+    """dw (K,) <- dq^T x, db (1,) <- dq.sum() with dq (R,) f32 (any stride), x (R, K) bf16."""
     R, K = x.shape
-    rc = _abi.lib().asvrl_linear_wgrad_vec(_abi.ptr(dq), _abi.ptr(x), x.stride(0), R, K, _abi.ptr(dw), _abi.ptr(db),
+    rc = _abi.lib().asvrl_linear_wgrad_vec(_abi.ptr(dq), dq.stride(0), _abi.ptr(x), x.stride(0), R, K, _abi.ptr(dw),
+                                           _abi.ptr(db),
                                            int(accumulate), _abi.ptr(work), work.numel(), _abi.stream_ptr(stream))
     _abi.check(rc, "asvrl_linear_wgrad_vec")
 

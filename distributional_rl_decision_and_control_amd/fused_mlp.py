@@ -1,0 +1,175 @@
+"""Per-row MLPs of AC-IQN on the gfx950 kernels of csrc/asvrl_mlp.hip.
+
+MlpPack holds the bf16 images one network's per-row layers are read from (both observation
+encoders as a single block-structured 256 x 32 matrix, the Actor's hidden layers in the chained
+fragment order plus their transposes, the critic's action encoder) and refreshes them in one
+launch (asvrl_mlp_pack) after every optimizer step. The wrappers below are thin: tensors in,
+device pointers out, no host synchronisation, so everything is capturable in a HIP graph.
+
+Reference layers: AC_IQN_model.py:254-262 (Actor), 389-404 (Critic encoders), forward passes
+:284-321 and :462-480.
+"""
+import ctypes as C
+
+import torch
+
+from . import _abi
+
+ENC, OBSK, HID = 256, 32, 128
+MODE_ACT, MODE_FWD, MODE_TRAIN = 1, 2, 3
+
+
+def _p(t):
+    return t.data_ptr() if t is not None else None
+
+
+class MlpPack:
+    """Packed images of an Actor (kind='actor') or of a Critic's encoders (kind='critic')."""
+
+    def __init__(self, net, kind):
+        assert kind in ("actor", "critic")
+        self.net, self.kind = net, kind
+        dev = net.self_encoder[0].weight.device
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        self.enc = torch.zeros(ENC * OBSK, **bf)
+        self.b_enc = torch.zeros(ENC, dtype=torch.float32, device=dev)
+        w = _abi.AsvMlpWeights()
+        w.enc_frag, w.b_enc = self.enc.data_ptr(), self.b_enc.data_ptr()
+        if kind == "actor":
+            self.w1 = torch.zeros(HID * ENC, **bf)
+            self.w2 = torch.zeros(HID * HID, **bf)
+            self.w2t = torch.zeros(HID * HID, **bf)
+            self.w1t = torch.zeros(ENC * HID, **bf)
+            w.w1_frag, w.w2_frag, w.w2t_frag, w.w1t_frag = (self.w1.data_ptr(), self.w2.data_ptr(),
+                                                           self.w2t.data_ptr(), self.w1t.data_ptr())
+            w.b1, w.b2 = net.hidden_layer.bias.data_ptr(), net.hidden_layer_2.bias.data_ptr()
+            w.wout, w.bout = net.output_layer.weight.data_ptr(), net.output_layer.bias.data_ptr()
+            w.out_scale = float(net.atan_scale.float().item())
+        else:
+            self.ae = torch.zeros(HID * 16, **bf)
+            w.ae_frag = self.ae.data_ptr()
+            w.b_ae = net.action_encoder[0].bias.data_ptr()
+        self.w = w
+        self.refresh()
+
+    def src(self):
+        n = self.net
+        s = _abi.AsvMlpSrc()
+        s.self_w, s.self_b = n.self_encoder[0].weight.data_ptr(), n.self_encoder[0].bias.data_ptr()
+        s.obj_w, s.obj_b = n.object_encoder[0].weight.data_ptr(), n.object_encoder[0].bias.data_ptr()
+        if self.kind == "actor":
+            s.w1, s.w2 = n.hidden_layer.weight.data_ptr(), n.hidden_layer_2.weight.data_ptr()
+        else:
+            s.ae_w = n.action_encoder[0].weight.data_ptr()
+        return s
+
+    def refresh(self, stream=None):
+        src = self.src()
+        _abi.check(_abi.lib().asvrl_mlp_pack(C.byref(src), C.byref(self.w), _abi.stream_ptr(stream)),
+                   "asvrl_mlp_pack")
+
+
+def _rows(x):
+    """(pointer base tensor, row stride in floats) of a row-major f32 view."""
+    assert x.dtype == torch.float32 and x.stride(-1) == 1
+    return x, x.stride(0)
+
+
+def mlp_encode(pack, x, F, G=None, act=None, xb=None, stream=None):
+    """F = observation_processor(x) [n][256]; G = action_encoder(act) [n][128]; xb = bf16 x[:, :32]."""
+    x, ldx = _rows(x)
+    io = _abi.AsvMlpIO()
+    io.x, io.ldx, io.n = x.data_ptr(), ldx, x.shape[0]
+    io.F, io.G, io.xb = _p(F), _p(G), _p(xb)
+    if act is not None:
+        io.act, io.lda = act.data_ptr(), act.stride(0)
+    _abi.check(_abi.lib().asvrl_mlp_encode(C.byref(pack.w), C.byref(io), _abi.stream_ptr(stream)),
+               "asvrl_mlp_encode")
+
+
+def actor_forward(pack, x, a_out, stream=None):
+    """Actor.forward(x) -> a_out [n][2] f32 (no saved activations)."""
+    x, ldx = _rows(x)
+    io = _abi.AsvMlpIO()
+    io.x, io.ldx, io.n = x.data_ptr(), ldx, x.shape[0]
+    io.a_out, io.ld_aout = a_out.data_ptr(), a_out.stride(0)
+    _abi.check(_abi.lib().asvrl_actor_forward(C.byref(pack.w), C.byref(io), MODE_FWD, _abi.stream_ptr(stream)),
+               "asvrl_actor_forward")
+
+
+def actor_act(pack, x, actions64, step_dev, steps_per_count, total, fraction, initial, final, seed, stream=None):
+    """Epsilon-greedy batched act (agent.py:207-225) into f64 actions [n][2]."""
+    x, ldx = _rows(x)
+    io = _abi.AsvMlpIO()
+    io.x, io.ldx, io.n = x.data_ptr(), ldx, x.shape[0]
+    io.a_out64 = actions64.data_ptr()
+    io.step_dev = step_dev.data_ptr()
+    io.eps_steps_per_count, io.eps_total, io.eps_fraction = float(steps_per_count), float(total), float(fraction)
+    io.eps_initial, io.eps_final, io.seed = float(initial), float(final), int(seed) & 0xFFFFFFFFFFFFFFFF
+    _abi.check(_abi.lib().asvrl_actor_forward(C.byref(pack.w), C.byref(io), MODE_ACT, _abi.stream_ptr(stream)),
+               "asvrl_actor_forward(act)")
+
+
+class ActorBuffers:
+    """Saved activations and backward outputs of one Actor training pass over B rows."""
+
+    def __init__(self, B, device):
+        bf = dict(dtype=torch.bfloat16, device=device)
+        f = dict(dtype=torch.float32, device=device)
+        self.B = B
+        self.xb = torch.empty(B, OBSK, **bf)
+        self.h0 = torch.empty(B, ENC, **bf)
+        self.h1 = torch.empty(B, HID, **bf)
+        self.h2 = torch.empty(B, HID, **bf)
+        self.pre = torch.empty(B, 2, **f)
+        self.a_out = torch.empty(B, 2, **f)
+        self.dA = torch.empty(B, 2, **f)
+        self.dout = torch.empty(B, 2, **f)
+        self.dz2 = torch.empty(B, HID, **bf)
+        self.dz1 = torch.empty(B, HID, **bf)
+        self.dz0 = torch.empty(B, ENC, **bf)
+
+    def io(self, x=None):
+        io = _abi.AsvMlpIO()
+        if x is not None:
+            x, ldx = _rows(x)
+            io.x, io.ldx = x.data_ptr(), ldx
+        io.n = self.B
+        io.xb, io.h0, io.h1, io.h2, io.pre = (self.xb.data_ptr(), self.h0.data_ptr(), self.h1.data_ptr(),
+                                              self.h2.data_ptr(), self.pre.data_ptr())
+        io.a_out, io.ld_aout = self.a_out.data_ptr(), 2
+        io.dA, io.dout = self.dA.data_ptr(), self.dout.data_ptr()
+        io.dz2, io.dz1, io.dz0 = self.dz2.data_ptr(), self.dz1.data_ptr(), self.dz0.data_ptr()
+        return io
+
+
+def actor_train_forward(pack, x, bufs, stream=None):
+    io = bufs.io(x)
+    _abi.check(_abi.lib().asvrl_actor_forward(C.byref(pack.w), C.byref(io), MODE_TRAIN, _abi.stream_ptr(stream)),
+               "asvrl_actor_forward(train)")
+    return bufs.a_out
+
+
+def actor_backward(pack, bufs, stream=None):
+    """bufs.dA -> dout, dz2, dz1, dz0 (pre-activation gradients of every Actor layer)."""
+    io = bufs.io()
+    _abi.check(_abi.lib().asvrl_actor_backward(C.byref(pack.w), C.byref(io), _abi.stream_ptr(stream)),
+               "asvrl_actor_backward")
+
+
+def encoder_fold(dw, db, net, accumulate=False, stream=None):
+    """256 x 32 encoder-image gradient -> self_encoder / object_encoder .grad."""
+    se, oe = net.self_encoder[0], net.object_encoder[0]
+    _abi.check(_abi.lib().asvrl_encoder_fold(dw.data_ptr(), db.data_ptr(), se.weight.grad.data_ptr(),
+                                             se.bias.grad.data_ptr(), oe.weight.grad.data_ptr(),
+                                             oe.bias.grad.data_ptr(), int(accumulate), _abi.stream_ptr(stream)),
+               "asvrl_encoder_fold")
+
+
+def small_wgrad(dz, x, dw, db, work, accumulate=False, stream=None):
+    """dw (M, K) <- dz^T x, db <- dz.sum(0) for f32 dz (R, M) and a small f32 x (R, K <= 4)."""
+    R, M = dz.shape
+    K = x.shape[1]
+    _abi.check(_abi.lib().asvrl_small_wgrad(dz.data_ptr(), dz.stride(0), x.data_ptr(), x.stride(0), R, M, K,
+                                            dw.data_ptr(), _p(db), int(accumulate), work.data_ptr(), work.numel(),
+                                            _abi.stream_ptr(stream)), "asvrl_small_wgrad")

@@ -1,0 +1,134 @@
+"""The whole AC-IQN update (Agent.train_AC_IQN, agent.py:386-432) on hand-written gfx950
+kernels: about 40 launches per step, no torch autograd, no host synchronisation.
+
+Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | done):
+  critic (agent.py:395-416)
+    target actor(ns) -> na                               asvrl_actor_forward(FWD)
+    target encoders(ns, na) -> Ft, Gt                    asvrl_mlp_encode
+    target trunk -> q_next                               asvrl_critic_forward
+    local encoders(s, a) -> F, G (+ bf16 obs copy)       asvrl_mlp_encode
+    trunk forward + quantile-Huber vs r + g q_next (1-d) + backward
+                                                          asvrl_critic_train (targets formed in-kernel)
+    trunk weight grads                                   asvrl_linear_wgrad x3 + _vec
+    encoder grads (256x32 image, folded) and action-encoder grads
+                                                          asvrl_linear_wgrad + asvrl_encoder_fold
+                                                          + asvrl_small_wgrad
+    [RCCL all-reduce] clip + Adam                        asvrl_adam_clip
+    re-pack trunk and encoders                           asvrl_critic_pack + asvrl_mlp_pack
+  actor (agent.py:419-427), through the UPDATED critic
+    actor(s) saving activations -> a                     asvrl_actor_forward(TRAIN)
+    encoders(s, a) -> F2, G2                             asvrl_mlp_encode
+    trunk forward + backward of -mean(q) to the action   asvrl_critic_actor_grad (dA in-kernel)
+    actor backward                                       asvrl_actor_backward
+    actor weight grads                                   asvrl_linear_wgrad x3 + _vec x2 + fold
+    [RCCL all-reduce] clip + Adam, re-pack actor         asvrl_adam_clip + asvrl_mlp_pack
+
+Arithmetic: bf16 MFMA operands with f32 accumulation everywhere, f32 master weights / Adam.
+"""
+import torch
+
+from .fused_critic import (CriticPack, TrainBuffers, critic_actor_grad, critic_forward, critic_train,
+                           linear_wgrad, linear_wgrad_vec, trunk_weight_grads)
+from .fused_mlp import (ActorBuffers, MlpPack, actor_act, actor_backward, actor_forward, actor_train_forward,
+                        encoder_fold, mlp_encode, small_wgrad)
+from .learner import clip_and_step
+
+OBS = 40
+
+
+def supported(policy, B, N):
+    c, a = policy.critic, policy.actor
+    return (c.concat_feature_dimension == 256 and c.hidden_dimension == 128 and c.n == 64 and N in (8, 16, 32)
+            and (B * N) % 32 == 0 and B % 32 == 0 and c.self_dimension == 7 and c.object_dimension == 5
+            and c.max_object_num == 5 and c.self_feature_dimension == 56 and c.object_feature_dimension == 40
+            and a.hidden_dimension == 128 and a.concat_feature_dimension == 256 and a.action_dimension == 2
+            and c.action_dimension == 2)
+
+
+class FusedACIQNState:
+    """Packs and buffers of the fused update (allocated once, pointer-stable for graph replay)."""
+
+    def __init__(self, policy_local, policy_target, B, N):
+        dev = policy_local.critic.cos_embedding.weight.device
+        self.B, self.N, self.device = B, N, dev
+        self.local_trunk = CriticPack(policy_local.critic)
+        self.target_trunk = CriticPack(policy_target.critic)
+        self.local_cenc = MlpPack(policy_local.critic, "critic")
+        self.target_cenc = MlpPack(policy_target.critic, "critic")
+        self.actor = MlpPack(policy_local.actor, "actor")
+        self.target_actor = MlpPack(policy_target.actor, "actor")
+        self.bufs = TrainBuffers(B, N, dev)
+        self.abufs = ActorBuffers(B, dev)
+        f = dict(dtype=torch.float32, device=dev)
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        self.na = torch.empty(B, 2, **f)
+        self.Ft, self.Gt = torch.empty(B, 256, **f), torch.empty(B, 128, **f)
+        self.F, self.G = torch.empty(B, 256, **f), torch.empty(B, 128, **f)
+        self.F2, self.G2 = torch.empty(B, 256, **f), torch.empty(B, 128, **f)
+        self.xb = torch.empty(B, 32, **bf)
+        self.q_next = torch.empty(B * N, **f)
+        self.q_pi = torch.empty(B * N, **f)
+        self.dzF = torch.empty(B, 256, **bf)
+        self.dzG = torch.empty(B, 128, **f)
+        self.enc_dw = torch.empty(256, 32, **f)
+        self.enc_db = torch.empty(256, **f)
+        self.swork = torch.empty(((B + 255) // 256) * (128 * 2 + 128), **f)
+
+    def target_changed(self):
+        """Re-pack the target networks after a hard/soft update (eager, outside graphs)."""
+        self.target_trunk.refresh()
+        self.target_cenc.refresh()
+        self.target_actor.refresh()
+
+    def act(self, obs_rows, actions64, step_dev, steps_per_count, total, fraction, initial, final, seed):
+        actor_act(self.actor, obs_rows, actions64, step_dev, steps_per_count, total, fraction, initial, final, seed)
+
+
+def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, actor_grads, rows, gamma=0.99,
+                         taus=None, sync=None, max_norm=0.5):
+    """One AC-IQN update from replay rows [B][88]. taus: (3, B, N) or None (drawn here).
+    Returns (critic_loss, actor_loss, critic_grad_norm, actor_grad_norm) as device scalars."""
+    B, N = st.B, st.N
+    critic, actor = policy_local.critic, policy_local.actor
+    if taus is None:
+        taus = torch.rand(3, B, N, device=st.device)
+    s_rows, ns_rows = rows[:, 0:OBS], rows[:, OBS:2 * OBS]
+    a_rows, r_col, d_col = rows[:, 80:82], rows[:, 82], rows[:, 83]
+    bufs, ab, work = st.bufs, st.abufs, st.bufs.work
+
+    # ---- critic (agent.py:395-416); every critic .grad is overwritten below (no zeroing)
+    actor_forward(st.target_actor, ns_rows, st.na)
+    mlp_encode(st.target_cenc, ns_rows, st.Ft, st.Gt, act=st.na)
+    critic_forward(st.target_trunk, st.Ft, st.Gt, taus[0], N, q=st.q_next)
+    mlp_encode(st.local_cenc, s_rows, st.F, st.G, act=a_rows, xb=st.xb)
+    critic_loss = critic_train(st.local_trunk, st.F, st.G, taus[1], None, bufs, q_next=st.q_next.view(B, N),
+                               rewards=r_col, dones=d_col, gamma=gamma, dzF=st.dzF, dzG=st.dzG, with_dFdG=False)
+    trunk_weight_grads(critic, bufs)
+    linear_wgrad(st.dzF, st.xb, st.enc_dw, st.enc_db, work)
+    encoder_fold(st.enc_dw, st.enc_db, critic)
+    ae = critic.action_encoder[0]
+    small_wgrad(st.dzG, a_rows, ae.weight.grad, ae.bias.grad, st.swork)
+    if sync is not None:
+        sync(critic_grads)
+    cgn = clip_and_step(critic_opt, critic_grads, max_norm)
+    st.local_trunk.refresh()
+    st.local_cenc.refresh()
+
+    # ---- actor through the updated critic (agent.py:419-427)
+    actor_train_forward(st.actor, s_rows, ab)
+    mlp_encode(st.local_cenc, s_rows, st.F2, st.G2, act=ab.a_out)
+    critic_actor_grad(st.local_trunk, st.F2, st.G2, taus[2], N, st.q_pi, w_ae=ae.weight, dA=ab.dA)
+    actor_loss = -st.q_pi.mean()
+    actor_backward(st.actor, ab)
+    linear_wgrad(ab.dz1, ab.h0, actor.hidden_layer.weight.grad, actor.hidden_layer.bias.grad, work)
+    linear_wgrad(ab.dz2, ab.h1, actor.hidden_layer_2.weight.grad, actor.hidden_layer_2.bias.grad, work)
+    ow, obias = actor.output_layer.weight.grad, actor.output_layer.bias.grad
+    linear_wgrad_vec(ab.dout[:, 0], ab.h2, ow[0], obias[0:1], work)
+    linear_wgrad_vec(ab.dout[:, 1], ab.h2, ow[1], obias[1:2], work)
+    linear_wgrad(ab.dz0, ab.xb, st.enc_dw, st.enc_db, work)
+    encoder_fold(st.enc_dw, st.enc_db, actor)
+    if sync is not None:
+        sync(actor_grads)
+    agn = clip_and_step(actor_opt, actor_grads, max_norm)
+    st.actor.refresh()
+    return critic_loss.detach(), actor_loss.detach(), cgn, agn

@@ -21,6 +21,8 @@ import time
 import torch
 
 from .fused_critic import FusedACIQN, ac_iqn_update_fused, fused_supported
+from .fused_update import FusedACIQNState, ac_iqn_update_fused2
+from .fused_update import supported as fused2_supported
 from .learn_ops import DeviceReplay, split_rows
 from .learner import FlatGrads, FusedAdam, GradSync, ac_iqn_update, iqn_update
 from .policy.AC_IQN_model import AC_IQN_Policy
@@ -71,8 +73,13 @@ class VecTrainer:
                 self.actor_opt = torch.optim.Adam(self.local.actor.parameters(), lr=lr, capturable=capturable)
                 self.critic_opt = torch.optim.Adam(self.local.critic.parameters(), lr=lr, capturable=capturable)
             self.action_dim = 2
-            self.fused = None
-            if fused and amp_dtype is not None and fused_supported(self.local.critic, batch_size, num_tau):
+            self.fused = self.fused2 = None
+            # fused=True: the whole update on hand-written kernels (fused_update.py, needs the fused
+            # optimiser); "v1": only the critic trunk fused; False: torch
+            if fused is True and fused_adam and amp_dtype is not None and fused2_supported(self.local, batch_size,
+                                                                                          num_tau):
+                self.fused2 = FusedACIQNState(self.local, self.target, batch_size, num_tau)
+            elif fused and amp_dtype is not None and fused_supported(self.local.critic, batch_size, num_tau):
                 self.fused = FusedACIQN(self.local, self.target, batch_size, num_tau)
         elif agent_type == "IQN":
             self.local = IQN_Policy(**DEFAULT_NET, action_size=25, device=self.device, seed=net_seed).to(self.device)
@@ -114,6 +121,11 @@ class VecTrainer:
 
     @torch.no_grad()
     def act(self):
+        if getattr(self, "fused2", None) is not None:
+            # one kernel: actor on every robot row + epsilon-greedy on the device step counter
+            self.fused2.act(self.env.obs_cur, self.actions, self.env.counter, self.E, self.total_timesteps,
+                            self.exploration_fraction, self.initial_eps, self.final_eps, self.seed + 4242)
+            return
         obs = split_obs(self.env.obs_cur)
         NT = obs[0].shape[0]
         eps = self.epsilon()
@@ -144,6 +156,11 @@ class VecTrainer:
 
     def learn(self):
         rows = self.replay.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter, out=self.batch_rows)
+        if self.agent_type == "AC-IQN" and self.fused2 is not None:
+            out = ac_iqn_update_fused2(self.fused2, self.local, self.actor_opt, self.critic_opt, self.critic_grads,
+                                       self.actor_grads, rows, gamma=self.gamma, sync=self.sync)
+            self.learn_counter += 1
+            return out
         s, a, r, ns, d = split_rows(rows)
         if self.agent_type == "AC-IQN" and self.fused is not None:
             out = ac_iqn_update_fused(self.fused, self.local, self.target, self.actor_opt, self.critic_opt,
@@ -171,6 +188,8 @@ class VecTrainer:
             torch._foreach_copy_([t for t, _ in pairs], [l for _, l in pairs])
             if self.agent_type == "AC-IQN" and self.fused is not None:
                 self.fused.target_pack.refresh()  # eager, outside any captured graph
+            if self.agent_type == "AC-IQN" and self.fused2 is not None:
+                self.fused2.target_changed()
 
     # ------------------------------------------------------------------ iteration
     def _iteration_body(self, do_learn):

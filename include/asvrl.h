@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 1
+#define ASVRL_ABI_VERSION 2
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -220,23 +220,43 @@ typedef struct AsvCriticActs {
  * hidden_layer_2.weight (128 x 128) (AC_IQN_model.py:398-402). One launch. */
 int asvrl_critic_pack(const float* wc, const float* w1, const float* w2, const AsvCriticWeights* w, void* stream);
 
-/* Critic.forward (AC_IQN_model.py:462-480) from precomputed state features F (B x 256,
- * observation_processor) and action features G (B x 128, action_encoder): q [B*N].
- * Requires N in {8, 16, 32} (taus of a sample stay inside one 32-row wave tile). */
-int asvrl_critic_forward(const AsvCriticWeights* w, const float* F, const float* G, const float* taus,
-                         int32_t B, int32_t N, float* q, void* stream);
+/* Inputs / outputs of one critic launch. F (B x 256) = observation_processor features,
+ * G (B x 128) = action_encoder features, taus (B x N); N in {8, 16, 32}. */
+typedef struct AsvCriticIO {
+  const float* F;
+  const float* G;
+  const float* taus;
+  int32_t B, N, Np;
+  float kappa;
+  const float* q_targets;  /* TRAIN: [B][Np], or NULL with q_next set: */
+  const float* q_next;     /*   q_targets = rewards + gamma * q_next * (1 - dones) (agent.py:399-400) */
+  const float* rewards;    /*   B values at stride ld_rd floats */
+  const float* dones;
+  int64_t ld_rd;
+  float gamma;
+  float dq;                /* ACTOR: dL/dq of every row (-1/(B*N) for actor_loss = -mean q) */
+  float* q;                /* [B*N] (FWD: required) */
+  float* row_loss;         /* TRAIN: [B*N], sums to B*Np*loss */
+  float* dF;               /* TRAIN optional: dL/dF [B][256] */
+  float* dG;               /* TRAIN / ACTOR optional: dL/dG [B][128] */
+  void* dzF;               /* TRAIN optional: bf16 [B][256] dF * 1[F > 0] (encoder pre-activation grad) */
+  float* dzG;              /* TRAIN optional: [B][128] dG * 1[G > 0] (action-encoder pre-activation grad) */
+  const float* w_ae;       /* ACTOR with dA: action_encoder.weight [128][2] */
+  float* dA;               /* ACTOR optional: dL/d(action) [B][2] = W_ae^T (dG * 1[G > 0]) */
+} AsvCriticIO;
+
+/* Critic.forward (AC_IQN_model.py:462-480): q [B*N]. */
+int asvrl_critic_forward(const AsvCriticWeights* w, const AsvCriticIO* io, void* stream);
 
 /* Critic update of train_AC_IQN (agent.py:395-414): forward, the quantile-Huber loss against
- * q_targets (B x Np) and its backward in one launch. row_loss[R] sums to B*Np*loss; dF, dG
- * are the gradients w.r.t. F and G; acts receive the activations for the weight gradients. */
-int asvrl_critic_train(const AsvCriticWeights* w, const float* F, const float* G, const float* taus,
-                       const float* q_targets, int32_t B, int32_t N, int32_t Np, float kappa, float* q,
-                       float* row_loss, float* dF, float* dG, const AsvCriticActs* acts, void* stream);
+ * the targets and its backward in one launch; acts receive the activations for the weight
+ * gradients. */
+int asvrl_critic_train(const AsvCriticWeights* w, const AsvCriticIO* io, const AsvCriticActs* acts,
+                       void* stream);
 
-/* Actor update's critic pass (agent.py:419-425): forward, then d(loss)/dG for dL/dq = dq on
- * every row (= -1/(B*N) for loss = -mean q). q [R] optional. */
-int asvrl_critic_actor_grad(const AsvCriticWeights* w, const float* F, const float* G, const float* taus,
-                            int32_t B, int32_t N, float dq, float* q, float* dG, void* stream);
+/* Actor update's critic pass (agent.py:419-425): forward, then the backward of
+ * sum_rows dq * q to G (dG) and through the action encoder to the action (dA). */
+int asvrl_critic_actor_grad(const AsvCriticWeights* w, const AsvCriticIO* io, void* stream);
 
 /* ---------------------------------------------------------------- replay (replay_buffer.py) */
 
@@ -281,17 +301,98 @@ int asvrl_adam_clip(float* params, float* grads, float* exp_avg, float* exp_avg_
  * dW = dZ^T X, db = dZ.sum(0), AC_IQN_model.py:398-404 layers): dw[m][k] = sum_r dz[r][m] x[r][k],
  * db[m] = sum_r dz[r][m] (db optional). dz (R x M, leading dim ldz) and x (R x K, ldx) are bf16
  * row-major, 16-byte aligned, ld multiples of 8; R a multiple of 32. (M, K) in {(256, 64),
- * (128, 256), (128, 128), (64, 64)}. accumulate = 0 overwrites dw/db, 1 adds. Deterministic
+ * (128, 256), (128, 128), (64, 64), (256, 32)}. accumulate = 0 overwrites dw/db, 1 adds. Deterministic
  * (fixed-order partial sums). work: asvrl_linear_wgrad_workspace(M, K) floats. */
 int64_t asvrl_linear_wgrad_workspace(int32_t M, int32_t K);
 int asvrl_linear_wgrad(const void* dz, int64_t ldz, const void* x, int64_t ldx, int32_t R, int32_t M,
                        int32_t K, float* dw, float* db, int32_t accumulate, float* work,
                        int64_t work_floats, void* stream);
 
-/* The one-unit output layer's version: dw[k] = sum_r dq[r] x[r][k], db = sum_r dq[r] with dq f32
- * (R) and x bf16 (R x K, ldx); K in {64, 128, 256}; work >= 256 * (K + 1) floats. */
-int asvrl_linear_wgrad_vec(const float* dq, const void* x, int64_t ldx, int32_t R, int32_t K, float* dw,
+/* One output unit's version: dw[k] = sum_r dq[r*ldq] x[r][k], db = sum_r dq[r*ldq] with dq f32 and
+ * x bf16 (R x K, ldx); K in {64, 128, 256}; work >= 256 * (K + 1) floats. */
+int asvrl_linear_wgrad_vec(const float* dq, int64_t ldq, const void* x, int64_t ldx, int32_t R, int32_t K, float* dw,
                            float* db, int32_t accumulate, float* work, int64_t work_floats, void* stream);
+
+/* ---------------------------------------------------------------- per-row MLPs (actor, encoders) */
+
+/* f32 parameters of one AC-IQN network's per-row layers (AC_IQN_model.py:254-262, 389-404):
+ * self_encoder (56 x 7), object_encoder (40 x 5); for an Actor also hidden_layer (128 x 256) and
+ * hidden_layer_2 (128 x 128); for a Critic also action_encoder (128 x 2). Unused entries NULL. */
+typedef struct AsvMlpSrc {
+  const float* self_w;
+  const float* self_b;
+  const float* obj_w;
+  const float* obj_b;
+  const float* w1;
+  const float* w2;
+  const float* ae_w;
+} AsvMlpSrc;
+
+/* Packed images the kernels read (filled by asvrl_mlp_pack, which writes through these
+ * pointers) plus direct pointers to the remaining f32 parameters. */
+typedef struct AsvMlpWeights {
+  const void* enc_frag;   /* both encoders as one block-structured 256 x 32 bf16 image (16 KB) */
+  const float* b_enc;     /* [256] their biases (written by the pack) */
+  const void* w1_frag;    /* hidden_layer, chained order (64 KB)          (Actor) */
+  const void* w2_frag;    /* hidden_layer_2 (32 KB)                        (Actor) */
+  const void* w2t_frag;   /* hidden_layer_2^T (32 KB, backward)            (Actor) */
+  const void* w1t_frag;   /* hidden_layer^T (64 KB, backward)              (Actor) */
+  const float* b1;        /* hidden_layer.bias [128]                       (Actor) */
+  const float* b2;        /* hidden_layer_2.bias [128]                     (Actor) */
+  const float* wout;      /* output_layer.weight [2][128]                  (Actor) */
+  const float* bout;      /* output_layer.bias [2]                         (Actor) */
+  const void* ae_frag;    /* action_encoder as a 128 x 16 image (cols 2.. zero) (Critic) */
+  const float* b_ae;      /* action_encoder.bias [128]                     (Critic) */
+  float out_scale;        /* Actor.atan_scale = float32(2 / pi) */
+} AsvMlpWeights;
+
+/* Rows in / out of the MLP kernels. Observation rows are the packed ASVRL_OBS_DIM layout at
+ * row stride ldx floats (40 for env observations, 88 for replay rows), 16-byte aligned. */
+typedef struct AsvMlpIO {
+  const float* x;
+  int64_t ldx;
+  const float* act;       /* ENCODE: actions [n] at stride lda (G = relu(W_ae a + b_ae)) */
+  int64_t lda;
+  int32_t n;
+  float* F;               /* ENCODE out [n][256] */
+  float* G;               /* ENCODE out [n][128] (optional) */
+  void* xb;               /* ENCODE (optional) / TRAIN out: bf16 copy of obs columns 0..31 [n][32] */
+  float* a_out;           /* FWD / TRAIN out: actions, stride ld_aout */
+  int64_t ld_aout;
+  double* a_out64;        /* ACT out: [n][2] f64 */
+  float* pre;             /* TRAIN out / backward in: pre-atan outputs [n][2] */
+  void* h0;               /* TRAIN out: bf16 [n][256] encoder output (hidden_layer input) */
+  void* h1;               /* TRAIN out: bf16 [n][128] */
+  void* h2;               /* TRAIN out: bf16 [n][128] */
+  const float* dA;        /* backward in: dL/d(action) [n][2] */
+  float* dout;            /* backward out: dL/d(output_layer pre-activation) [n][2] */
+  void* dz2;              /* backward out: bf16 [n][128] hidden_layer_2 pre-activation grad */
+  void* dz1;              /* backward out: bf16 [n][128] hidden_layer pre-activation grad */
+  void* dz0;              /* backward out: bf16 [n][256] encoder pre-activation grad */
+  const int64_t* step_dev;      /* ACT: device step counter (epsilon schedule, trainer.py:257-264) */
+  double eps_steps_per_count;   /* timesteps per counter tick (= n_envs) */
+  double eps_total, eps_fraction, eps_initial, eps_final;
+  uint64_t seed;                /* ACT: Philox key of the exploration draws */
+} AsvMlpIO;
+
+/* Pack the bf16 images of `w` from the f32 parameters in `src` (one launch). */
+int asvrl_mlp_pack(const AsvMlpSrc* src, const AsvMlpWeights* w, void* stream);
+/* observation_processor (AC_IQN_model.py:284-308) -> F, and action_encoder -> G, per row. */
+int asvrl_mlp_encode(const AsvMlpWeights* w, const AsvMlpIO* io, void* stream);
+/* Actor.forward (AC_IQN_model.py:310-321). mode 1 = ACT (epsilon-greedy f64 actions,
+ * agent.py:207-225), 2 = FWD (f32 actions), 3 = TRAIN (f32 actions + saved activations). */
+int asvrl_actor_forward(const AsvMlpWeights* w, const AsvMlpIO* io, int32_t mode, void* stream);
+/* Backward of the Actor from dA to every layer's pre-activation gradient (agent.py:425). */
+int asvrl_actor_backward(const AsvMlpWeights* w, const AsvMlpIO* io, void* stream);
+/* Fold the 256 x 32 encoder-image gradient (dw, db from asvrl_linear_wgrad) back onto
+ * self_encoder / object_encoder weight and bias gradients (object rows summed over objects). */
+int asvrl_encoder_fold(const float* dw, const float* db, float* self_w, float* self_b, float* obj_w,
+                       float* obj_b, int32_t accumulate, void* stream);
+/* dw[m][k] = sum_r dz[r][m] x[r][k], db[m] = sum_r dz[r][m] for f32 inputs with K <= 4 and
+ * M | 256 (the critic action_encoder). work >= ceil(R / 256) * (M*K + M) floats. */
+int asvrl_small_wgrad(const float* dz, int64_t ldz, const float* x, int64_t ldx, int32_t R, int32_t M,
+                      int32_t K, float* dw, float* db, int32_t accumulate, float* work,
+                      int64_t work_floats, void* stream);
 
 /* ---------------------------------------------------------------- misc */
 const char* asvrl_last_error(void);

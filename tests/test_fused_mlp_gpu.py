@@ -1,0 +1,229 @@
+"""GPU: the per-row MLP kernels (csrc/asvrl_mlp.hip) and the fully fused AC-IQN update
+(fused_update.py) against plain torch fp32 restatements of the reference layers
+(AC_IQN_model.py:284-321, 389-404, 462-480; agent.py:386-432).
+
+The kernels compute with bf16 MFMA operands and f32 accumulation, so values are compared at
+bf16 tolerance: 2% of the output scale, gradients by cosine similarity > 0.99 and norm ratio
+within 5%; the packing is checked exactly."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _policy(seed=100):
+    from distributional_rl_decision_and_control_amd.policy.AC_IQN_model import AC_IQN_Policy
+    from distributional_rl_decision_and_control_amd.vec_trainer import DEFAULT_NET
+    return AC_IQN_Policy(**DEFAULT_NET, value_ranges_of_action=[[-1, 1], [-1, 1]], device="cuda", seed=seed)
+
+
+def _obs_rows(n, seed=0, ld=40):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.zeros(n, ld, device="cuda")
+    x[:, 0:7] = torch.randn(n, 7, generator=g, device="cuda") * 3
+    x[:, 7:32] = torch.randn(n, 25, generator=g, device="cuda") * 3
+    x[:, 32:37] = (torch.rand(n, 5, generator=g, device="cuda") > 0.4).float()
+    return x
+
+
+def _split(x):
+    n = x.shape[0]
+    return x[:, 0:7], x[:, 7:32].reshape(n, 5, 5), x[:, 32:37]
+
+
+def _rel(a, b):
+    return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-30)
+
+
+def _cos(x, y):
+    x, y = x.reshape(-1).double(), y.reshape(-1).double()
+    return float((x @ y) / (x.norm() * y.norm() + 1e-30))
+
+
+def test_encoder_image_is_block_structured():
+    from distributional_rl_decision_and_control_amd.fused_critic import frag_index
+    from distributional_rl_decision_and_control_amd.fused_mlp import MlpPack
+    pol = _policy()
+    c = pol.critic
+    pack = MlpPack(c, "critic")
+    torch.cuda.synchronize()
+    W = torch.zeros(256, 32, device="cuda")
+    W[0:56, 0:7] = c.self_encoder[0].weight
+    for o in range(5):
+        W[56 + 40 * o:96 + 40 * o, 7 + 5 * o:12 + 5 * o] = c.object_encoder[0].weight
+    ref = torch.index_select(W.reshape(-1), 0, frag_index(256, 32, False, "cuda")).to(torch.bfloat16)
+    assert torch.equal(pack.enc, ref)
+    b = torch.cat([c.self_encoder[0].bias] + [c.object_encoder[0].bias] * 5)
+    assert torch.equal(pack.b_enc, b)
+    Wa = torch.zeros(128, 16, device="cuda")
+    Wa[:, 0:2] = c.action_encoder[0].weight
+    ref = torch.index_select(Wa.reshape(-1), 0, frag_index(128, 16, False, "cuda")).to(torch.bfloat16)
+    assert torch.equal(pack.ae, ref)
+
+
+@pytest.mark.parametrize("n,ld", [(4096, 88), (20480, 40), (100, 40)])
+def test_encode_matches_torch(n, ld):
+    from distributional_rl_decision_and_control_amd.fused_mlp import MlpPack, mlp_encode
+    from distributional_rl_decision_and_control_amd.policy.AC_IQN_model import encode_observation
+    pol = _policy()
+    c = pol.critic
+    x = _obs_rows(n, 1, ld)
+    act = torch.rand(n, 2, device="cuda") * 2 - 1
+    F = torch.empty(n, 256, device="cuda")
+    G = torch.empty(n, 128, device="cuda")
+    xb = torch.empty(n, 32, dtype=torch.bfloat16, device="cuda")
+    mlp_encode(MlpPack(c, "critic"), x, F, G, act=act, xb=xb)
+    with torch.no_grad():
+        Fr = encode_observation(c.self_encoder, c.object_encoder, _split(x), 5, 5, 40)
+        Gr = c.action_encoder(act)
+    assert _rel(F, Fr) < 2e-2 and _rel(G, Gr) < 2e-2
+    assert torch.equal((F > 0), (Fr > 0)) or ((F > 0) != (Fr > 0)).float().mean().item() < 1e-3
+    assert torch.equal(xb, x[:, :32].to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("n", [4096, 20480, 96])
+def test_actor_forward_matches_torch(n):
+    from distributional_rl_decision_and_control_amd.fused_mlp import MlpPack, actor_forward
+    pol = _policy()
+    x = _obs_rows(n, 2)
+    a = torch.empty(n, 2, device="cuda")
+    actor_forward(MlpPack(pol.actor, "actor"), x, a)
+    with torch.no_grad():
+        ar = pol.actor(_split(x))
+    assert (a - ar).abs().max().item() < 2e-2
+
+
+def test_actor_act_epsilon_greedy():
+    from distributional_rl_decision_and_control_amd.fused_mlp import MlpPack, actor_act, actor_forward
+    pol = _policy()
+    n = 20480
+    x = _obs_rows(n, 3)
+    pack = MlpPack(pol.actor, "actor")
+    greedy = torch.empty(n, 2, device="cuda")
+    actor_forward(pack, x, greedy)
+    out = torch.empty(n, 2, dtype=torch.float64, device="cuda")
+    step = torch.zeros(1, dtype=torch.int64, device="cuda")
+    # progress 0 -> eps = initial = 0.6
+    actor_act(pack, x, out, step, 4096, 6e6, 0.25, 0.6, 0.05, seed=5)
+    same = ((out.float() - greedy).abs().max(1).values < 1e-6)
+    frac_explore = 1 - same.float().mean().item()
+    assert abs(frac_explore - 0.6) < 0.02
+    assert bool(((out >= -1) & (out <= 1)).all())
+    # past the exploration fraction: eps = final = 0.05
+    step.fill_(1_000_000)
+    actor_act(pack, x, out, step, 4096, 6e6, 0.25, 0.6, 0.05, seed=5)
+    same = ((out.float() - greedy).abs().max(1).values < 1e-6)
+    assert abs((1 - same.float().mean().item()) - 0.05) < 0.01
+
+
+def test_actor_backward_matches_autograd():
+    from distributional_rl_decision_and_control_amd import _abi
+    from distributional_rl_decision_and_control_amd.fused_critic import linear_wgrad, linear_wgrad_vec
+    from distributional_rl_decision_and_control_amd.fused_mlp import (ActorBuffers, MlpPack, actor_backward,
+                                                                       actor_train_forward, encoder_fold)
+    pol = _policy()
+    actor = pol.actor
+    B = 4096
+    x = _obs_rows(B, 4, 88)
+    dA = torch.randn(B, 2, device="cuda") * 1e-3
+    # reference
+    params = list(actor.parameters())
+    ar = actor(_split(x))
+    grads_ref = torch.autograd.grad((ar * dA).sum(), params)
+    # fused
+    for p in params:
+        p.grad = torch.zeros_like(p)
+    pack = MlpPack(actor, "actor")
+    ab = ActorBuffers(B, "cuda")
+    a = actor_train_forward(pack, x, ab)
+    assert (a - ar.detach()).abs().max().item() < 2e-2
+    ab.dA.copy_(dA)
+    actor_backward(pack, ab)
+    work = torch.empty(int(_abi.lib().asvrl_linear_wgrad_workspace(128, 256)), device="cuda")
+    linear_wgrad(ab.dz1, ab.h0, actor.hidden_layer.weight.grad, actor.hidden_layer.bias.grad, work)
+    linear_wgrad(ab.dz2, ab.h1, actor.hidden_layer_2.weight.grad, actor.hidden_layer_2.bias.grad, work)
+    ow, ob = actor.output_layer.weight.grad, actor.output_layer.bias.grad
+    linear_wgrad_vec(ab.dout[:, 0], ab.h2, ow[0], ob[0:1], work)
+    linear_wgrad_vec(ab.dout[:, 1], ab.h2, ow[1], ob[1:2], work)
+    dw, db = torch.empty(256, 32, device="cuda"), torch.empty(256, device="cuda")
+    linear_wgrad(ab.dz0, ab.xb, dw, db, work)
+    encoder_fold(dw, db, actor)
+    names = [n for n, _ in actor.named_parameters()]
+    for n, p, gr in zip(names, params, grads_ref):
+        c = _cos(p.grad, gr)
+        ratio = p.grad.norm().item() / max(gr.norm().item(), 1e-30)
+        assert c > 0.99 and abs(ratio - 1) < 0.05, (n, c, ratio)
+
+
+def test_critic_actor_grad_dA_matches_autograd():
+    from distributional_rl_decision_and_control_amd.fused_critic import CriticPack, critic_actor_grad
+    from distributional_rl_decision_and_control_amd.fused_mlp import MlpPack, mlp_encode
+    pol = _policy()
+    c = pol.critic
+    B, N = 512, 32
+    x = _obs_rows(B, 6)
+    a = (torch.rand(B, 2, device="cuda") * 2 - 1).requires_grad_(True)
+    taus = torch.rand(B, N, device="cuda")
+    q, _ = c(_split(x), a, N, taus=taus.unsqueeze(-1))
+    (da_ref,) = torch.autograd.grad(-q.mean(), a)
+    F, G = torch.empty(B, 256, device="cuda"), torch.empty(B, 128, device="cuda")
+    mlp_encode(MlpPack(c, "critic"), x, F, G, act=a.detach())
+    dA = torch.empty(B, 2, device="cuda")
+    qk = torch.empty(B * N, device="cuda")
+    critic_actor_grad(CriticPack(c), F, G, taus, N, qk, w_ae=c.action_encoder[0].weight, dA=dA)
+    assert _cos(dA, da_ref) > 0.99
+    assert abs(dA.norm().item() / da_ref.norm().item() - 1) < 0.05
+
+
+def test_fused2_update_tracks_fp32_update():
+    """Ten AC-IQN updates (B=512, N=32) on identical batches and taus: the fully fused path's
+    critic/actor losses follow the fp32 torch path (agent.py:386-432)."""
+    from distributional_rl_decision_and_control_amd.fused_update import FusedACIQNState, ac_iqn_update_fused2
+    from distributional_rl_decision_and_control_amd.learner import FlatGrads, FusedAdam, ac_iqn_update
+    from distributional_rl_decision_and_control_amd.learn_ops import split_rows
+    B, N = 512, 32
+
+    def make(fused_opt):
+        loc, tgt = _policy(), _policy()
+        if fused_opt:
+            ao, co = FusedAdam(loc.actor.parameters(), lr=1e-4), FusedAdam(loc.critic.parameters(), lr=1e-4)
+            return loc, tgt, ao, co, co.grads, ao.grads
+        cg, ag = FlatGrads(loc.critic.parameters()), FlatGrads(loc.actor.parameters())
+        ao = torch.optim.Adam(loc.actor.parameters(), lr=1e-4)
+        co = torch.optim.Adam(loc.critic.parameters(), lr=1e-4)
+        return loc, tgt, ao, co, cg, ag
+
+    A = make(False)
+    Bm = make(True)
+    st = FusedACIQNState(Bm[0], Bm[1], B, N)
+    init = {k: v.detach().clone() for k, v in list(A[0].critic.named_parameters()) +
+            [("actor." + n, p) for n, p in A[0].actor.named_parameters()]}
+    g = torch.Generator(device="cuda").manual_seed(3)
+    la, lb = [], []
+    for _ in range(10):
+        rows = torch.zeros(B, 88, device="cuda")
+        rows[:, 0:40] = _obs_rows(B, int(torch.randint(0, 1 << 30, (1,), generator=g, device="cuda").item()))
+        rows[:, 40:80] = rows[:, 0:40].roll(1, 0)
+        rows[:, 80:82] = torch.rand(B, 2, generator=g, device="cuda") * 2 - 1
+        rows[:, 82] = torch.randn(B, generator=g, device="cuda")
+        rows[:, 83] = (torch.rand(B, generator=g, device="cuda") > 0.9).float()
+        taus = torch.rand(3, B, N, generator=g, device="cuda")
+        s, a, r, ns, d = split_rows(rows)
+        out_a = ac_iqn_update(A[0], A[1], A[2], A[3], A[4], A[5], s, a, r, ns, d, num_tau=N,
+                              taus=tuple(t.unsqueeze(-1) for t in taus))
+        out_b = ac_iqn_update_fused2(st, Bm[0], Bm[2], Bm[3], Bm[4], Bm[5], rows, taus=taus)
+        la.append([out_a[0].item(), out_a[1].item(), out_a[2].item(), out_a[3].item()])
+        lb.append([out_b[0].item(), out_b[1].item(), out_b[2].item(), out_b[3].item()])
+    la, lb = np.array(la), np.array(lb)
+    np.testing.assert_allclose(lb[:, :2], la[:, :2], rtol=3e-2, atol=2e-3)
+    np.testing.assert_allclose(lb[:, 2:], la[:, 2:], rtol=5e-2)   # pre-clip gradient norms
+    # the ten Adam updates point the same way (cosine of the weight deltas; Adam's m/sqrt(v)
+    # turns bf16 noise on near-zero gradient elements into +-lr steps, so elementwise is no bar)
+    pairs = [(n, p, q) for (n, p), q in zip(A[0].critic.named_parameters(), Bm[0].critic.parameters())]
+    pairs += [("actor." + n, p, q) for (n, p), q in zip(A[0].actor.named_parameters(), Bm[0].actor.parameters())]
+    for n, p, q in pairs:
+        c = _cos(q.detach() - init[n], p.detach() - init[n])
+        assert c > 0.9, (n, c)
