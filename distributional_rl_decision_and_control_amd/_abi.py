@@ -93,6 +93,14 @@ class AsvCriticIO(C.Structure):
                 ("dzF", _VP), ("dzG", _VP), ("w_ae", _VP), ("dA", _VP)]
 
 
+MAX_SUM_SEGS = 8
+
+
+class AsvPartialSum(C.Structure):
+    _fields_ = [("partial", _VP), ("dw", _VP), ("db", _VP), ("groups", _I32), ("nw", _I32), ("nb", _I32),
+                ("accumulate", _I32)]
+
+
 class AsvMlpSrc(C.Structure):
     _fields_ = [(n, _VP) for n in ("self_w", "self_b", "obj_w", "obj_b", "w1", "w2", "ae_w")]
 
@@ -128,6 +136,12 @@ EXPORTS = [
     ("asvrl_replay_write_rows", C.c_int, [_VP, _VP, _I32, _VP, _VP]),
     ("asvrl_adam_clip", C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, _F, _F, _VP, _VP, _VP]),
     ("asvrl_linear_wgrad_workspace", _I64, [_I32, _I32]),
+    ("asvrl_linear_wgrad_groups", _I32, [_I32, _I32, _I32]),
+    ("asvrl_linear_wgrad_vec_groups", _I32, [_I32]),
+    ("asvrl_linear_wgrad_partial", C.c_int, [_VP, _I64, _VP, _I64, _I32, _I32, _I32, _VP, _I64, _VP, _VP]),
+    ("asvrl_linear_wgrad_vec_partial", C.c_int, [_VP, _I64, _VP, _I64, _I32, _I32, _VP, _I64, _VP, _VP]),
+    ("asvrl_small_wgrad_partial", C.c_int, [_VP, _I64, _VP, _I64, _I32, _I32, _I32, _VP, _I64, _VP, _VP]),
+    ("asvrl_partial_sums", C.c_int, [_VP, _I32, _VP]),
     ("asvrl_linear_wgrad", C.c_int, [_VP, _I64, _VP, _I64, _I32, _I32, _I32, _VP, _VP, _I32, _VP, _I64, _VP]),
     ("asvrl_linear_wgrad_vec", C.c_int, [_VP, _I64, _VP, _I64, _I32, _I32, _VP, _VP, _I32, _VP, _I64, _VP]),
     ("asvrl_mlp_pack", C.c_int, [C.POINTER(AsvMlpSrc), C.POINTER(AsvMlpWeights), _VP]),

@@ -488,7 +488,9 @@ __global__ __launch_bounds__(256) void enc_fold_kernel(const float* __restrict__
 }
 
 // dW[m][k] = sum_r dz[r][m] x[r][k], db[m] = sum_r dz[r][m] for a small f32 input (K <= 4): the
-// critic action_encoder (2 -> 128). Block b handles rows [256b, 256b + 256); partials [blk][M*K+M].
+// critic action_encoder (2 -> 128). Block b handles rows [kSwRows*b, +kSwRows); thread t owns
+// feature t % M and every (256/M)-th row, four rows in flight; partials [blk][M*K+M].
+constexpr int kSwRows = 32;
 __global__ __launch_bounds__(256) void small_wgrad_kernel(const float* __restrict__ dz, int64_t ldz,
                                                            const float* __restrict__ x, int64_t ldx, int R, int M,
                                                            int K, float* __restrict__ partial) {
@@ -496,7 +498,7 @@ __global__ __launch_bounds__(256) void small_wgrad_kernel(const float* __restric
   const int per = 256 / M;   // rows in flight (M divides 256)
   const int m = t % M, rq = t / M;
   float sw[4] = {0.f, 0.f, 0.f, 0.f}, sb = 0.f;
-  const int r0 = blockIdx.x * 256, r1 = min(R, r0 + 256);
+  const int r0 = blockIdx.x * kSwRows, r1 = min(R, r0 + kSwRows);
   for (int r = r0 + rq; r < r1; r += per) {
     const float d = dz[static_cast<int64_t>(r) * ldz + m];
     sb += d;
@@ -591,16 +593,27 @@ extern "C" int asvrl_encoder_fold(const float* dw, const float* db, float* self_
   return check_launch("asvrl_encoder_fold");
 }
 
+extern "C" int asvrl_small_wgrad_partial(const float* dz, int64_t ldz, const float* x, int64_t ldx, int32_t R,
+                                         int32_t M, int32_t K, float* partial, int64_t partial_floats,
+                                         int32_t* groups_out, void* stream) {
+  ASVRL_REQUIRE(dz && x && partial && groups_out, "asvrl_small_wgrad: null argument");
+  ASVRL_REQUIRE(M >= 1 && M <= 256 && 256 % M == 0 && K >= 1 && K <= 4, "asvrl_small_wgrad: M | 256, K <= 4");
+  *groups_out = 0;
+  if (R <= 0) return 0;
+  const int groups = (R + kSwRows - 1) / kSwRows;
+  ASVRL_REQUIRE(partial_floats >= static_cast<int64_t>(groups) * (M * K + M), "asvrl_small_wgrad: workspace too small");
+  hipLaunchKernelGGL(small_wgrad_kernel, dim3(groups), dim3(256), 0, as_stream(stream), dz, ldz, x, ldx, R, M, K,
+                     partial);
+  *groups_out = groups;
+  return check_launch("asvrl_small_wgrad");
+}
+
 extern "C" int asvrl_small_wgrad(const float* dz, int64_t ldz, const float* x, int64_t ldx, int32_t R, int32_t M,
                                  int32_t K, float* dw, float* db, int32_t accumulate, float* work, int64_t work_floats,
                                  void* stream) {
-  ASVRL_REQUIRE(dz && x && dw && work, "asvrl_small_wgrad: null argument");
-  ASVRL_REQUIRE(M >= 1 && M <= 256 && 256 % M == 0 && K >= 1 && K <= 4, "asvrl_small_wgrad: M | 256, K <= 4");
-  if (R <= 0) return 0;
-  const int groups = (R + 255) / 256;
-  ASVRL_REQUIRE(work_floats >= static_cast<int64_t>(groups) * (M * K + M), "asvrl_small_wgrad: workspace too small");
-  hipLaunchKernelGGL(small_wgrad_kernel, dim3(groups), dim3(256), 0, as_stream(stream), dz, ldz, x, ldx, R, M, K,
-                     work);
-  if (int rc = check_launch("asvrl_small_wgrad")) return rc;
+  ASVRL_REQUIRE(dw != nullptr, "asvrl_small_wgrad: null dw");
+  int32_t groups = 0;
+  if (int rc = asvrl_small_wgrad_partial(dz, ldz, x, ldx, R, M, K, work, work_floats, &groups, stream)) return rc;
+  if (groups == 0) return 0;
   return launch_partial_sum(work, groups, M * K, M, dw, db, accumulate, as_stream(stream));
 }

@@ -13,6 +13,8 @@
 // workgroups write f32 partials that a second launch sums in a fixed order (deterministic).
 #include "asvrl_common.h"
 
+#include <algorithm>
+
 namespace asvrl {
 namespace {
 
@@ -224,16 +226,60 @@ __global__ __launch_bounds__(kWgThreads) void partial_sum_kernel(const float* __
   *o = accumulate ? *o + s : s;
 }
 
+// Several independent partial reductions in one launch: blockIdx.y = segment.
+struct SumSegs {
+  AsvPartialSum seg[ASVRL_MAX_SUM_SEGS];
+};
+
+__global__ __launch_bounds__(kWgThreads) void partial_sums_kernel(SumSegs t) {
+  const AsvPartialSum& g = t.seg[blockIdx.y];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;
+  const int n = g.nw + g.nb;
+  if (blockIdx.x * 64 >= n) return;   // block-uniform
+  float s0 = 0.f, s1 = 0.f;
+  if (i < n) {
+    int k = wv;
+    for (; k + 4 < g.groups; k += 8) {
+      s0 += g.partial[static_cast<int64_t>(k) * n + i];
+      s1 += g.partial[static_cast<int64_t>(k + 4) * n + i];
+    }
+    if (k < g.groups) s0 += g.partial[static_cast<int64_t>(k) * n + i];
+  }
+  __shared__ float red[4][64];
+  red[wv][lane] = s0 + s1;
+  __syncthreads();
+  if (wv != 0 || i >= n) return;
+  if (i >= g.nw && g.db == nullptr) return;
+  const float s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  float* o = i < g.nw ? g.dw + i : g.db + (i - g.nw);
+  *o = g.accumulate ? *o + s : s;
+}
+
+int wgrad_groups(int R, int M, int K) {
+  const int chunks = R / kRC;
+  int cap = (1 << 22) / (M * K);
+  cap = cap < 64 ? 64 : (cap > kMaxGroups ? kMaxGroups : cap);
+  int groups = chunks < cap ? chunks : cap;
+  if (groups < 1) return 0;
+  const int per = (chunks + groups - 1) / groups;
+  return (chunks + per - 1) / per;
+}
+
+int vec_groups(int R) {
+  int groups = R < kMaxGroups ? R : kMaxGroups;
+  if (groups < 1) return 0;
+  const int per = (R + groups - 1) / groups;
+  return (R + per - 1) / per;
+}
+
 template <int M, int K>
 int launch_wgrad(const __bf16* dz, int64_t ldz, const __bf16* x, int64_t ldx, int R, float* work, hipStream_t st,
                  int& groups) {
+  // partial traffic is groups * M * K floats: capped near 16 MB for the large layers
   const int chunks = R / kRC;
-  // partial traffic is groups * M * K floats: cap it near 16 MB for the large layers
-  int cap = (1 << 22) / (M * K);
-  cap = cap < 64 ? 64 : (cap > kMaxGroups ? kMaxGroups : cap);
-  groups = chunks < cap ? chunks : cap;
+  groups = wgrad_groups(R, M, K);
   const int per = (chunks + groups - 1) / groups;
-  groups = (chunks + per - 1) / per;
   hipLaunchKernelGGL((wgrad_kernel<M, K>), dim3(groups), dim3(kWgThreads), 0, st, dz, ldz, x, ldx, chunks, per,
                      work);
   return check_launch("asvrl_linear_wgrad");
@@ -253,56 +299,92 @@ int launch_partial_sum(const float* partial, int groups, int nw, int nb, float* 
 
 using namespace asvrl;
 
+extern "C" int32_t asvrl_linear_wgrad_groups(int32_t R, int32_t M, int32_t K) { return wgrad_groups(R, M, K); }
+extern "C" int32_t asvrl_linear_wgrad_vec_groups(int32_t R) { return vec_groups(R); }
+
 extern "C" int64_t asvrl_linear_wgrad_workspace(int32_t M, int32_t K) {
   return static_cast<int64_t>(kMaxGroups) * (static_cast<int64_t>(M) * K + M);
 }
 
-extern "C" int asvrl_linear_wgrad(const void* dz, int64_t ldz, const void* x, int64_t ldx, int32_t R, int32_t M,
-                                  int32_t K, float* dw, float* db, int32_t accumulate, float* work,
-                                  int64_t work_floats, void* stream) {
-  ASVRL_REQUIRE(dz && x && dw && work, "asvrl_linear_wgrad: null argument");
+extern "C" int asvrl_linear_wgrad_partial(const void* dz, int64_t ldz, const void* x, int64_t ldx, int32_t R,
+                                          int32_t M, int32_t K, float* partial, int64_t partial_floats,
+                                          int32_t* groups_out, void* stream) {
+  ASVRL_REQUIRE(dz && x && partial && groups_out, "asvrl_linear_wgrad: null argument");
   ASVRL_REQUIRE(R >= 0 && R % kRC == 0, "asvrl_linear_wgrad: R must be a multiple of 32");
   ASVRL_REQUIRE(ldz >= M && ldx >= K && ldz % 8 == 0 && ldx % 8 == 0,
                 "asvrl_linear_wgrad: leading dimensions must cover the rows and be multiples of 8");
   ASVRL_REQUIRE((reinterpret_cast<uintptr_t>(dz) | reinterpret_cast<uintptr_t>(x)) % 16 == 0,
                 "asvrl_linear_wgrad: operands must be 16-byte aligned");
-  ASVRL_REQUIRE(work_floats >= asvrl_linear_wgrad_workspace(M, K), "asvrl_linear_wgrad: workspace too small");
+  ASVRL_REQUIRE(partial_floats >= static_cast<int64_t>(wgrad_groups(R, M, K)) * (M * K + M),
+                "asvrl_linear_wgrad: workspace too small");
+  *groups_out = 0;
   if (R == 0) return 0;
   hipStream_t st = as_stream(stream);
   const __bf16* z = static_cast<const __bf16*>(dz);
   const __bf16* xx = static_cast<const __bf16*>(x);
   int groups = 0, rc = 0;
-  if (M == 256 && K == 64) rc = launch_wgrad<256, 64>(z, ldz, xx, ldx, R, work, st, groups);
-  else if (M == 128 && K == 256) rc = launch_wgrad<128, 256>(z, ldz, xx, ldx, R, work, st, groups);
-  else if (M == 128 && K == 128) rc = launch_wgrad<128, 128>(z, ldz, xx, ldx, R, work, st, groups);
-  else if (M == 64 && K == 64) rc = launch_wgrad<64, 64>(z, ldz, xx, ldx, R, work, st, groups);
-  else if (M == 256 && K == 32) rc = launch_wgrad<256, 32>(z, ldz, xx, ldx, R, work, st, groups);
+  if (M == 256 && K == 64) rc = launch_wgrad<256, 64>(z, ldz, xx, ldx, R, partial, st, groups);
+  else if (M == 128 && K == 256) rc = launch_wgrad<128, 256>(z, ldz, xx, ldx, R, partial, st, groups);
+  else if (M == 128 && K == 128) rc = launch_wgrad<128, 128>(z, ldz, xx, ldx, R, partial, st, groups);
+  else if (M == 64 && K == 64) rc = launch_wgrad<64, 64>(z, ldz, xx, ldx, R, partial, st, groups);
+  else if (M == 256 && K == 32) rc = launch_wgrad<256, 32>(z, ldz, xx, ldx, R, partial, st, groups);
   else ASVRL_REQUIRE(false, "asvrl_linear_wgrad: unsupported (M, K)");
-  if (rc) return rc;
-  const int n = M * K + M;
-  hipLaunchKernelGGL(partial_sum_kernel, dim3((n + 63) / 64), dim3(kWgThreads), 0, st, work, groups, M * K, M, dw,
-                     db, accumulate);
-  return check_launch("asvrl_linear_wgrad(sum)");
+  *groups_out = groups;
+  return rc;
 }
 
-extern "C" int asvrl_linear_wgrad_vec(const float* dq, int64_t ldq, const void* x, int64_t ldx, int32_t R, int32_t K, float* dw,
-                                      float* db, int32_t accumulate, float* work, int64_t work_floats, void* stream) {
-  ASVRL_REQUIRE(dq && x && dw && work, "asvrl_linear_wgrad_vec: null argument");
+extern "C" int asvrl_linear_wgrad(const void* dz, int64_t ldz, const void* x, int64_t ldx, int32_t R, int32_t M,
+                                  int32_t K, float* dw, float* db, int32_t accumulate, float* work,
+                                  int64_t work_floats, void* stream) {
+  ASVRL_REQUIRE(dw != nullptr, "asvrl_linear_wgrad: null dw");
+  int32_t groups = 0;
+  if (int rc = asvrl_linear_wgrad_partial(dz, ldz, x, ldx, R, M, K, work, work_floats, &groups, stream)) return rc;
+  if (groups == 0) return 0;
+  return launch_partial_sum(work, groups, M * K, M, dw, db, accumulate, as_stream(stream));
+}
+
+extern "C" int asvrl_partial_sums(const AsvPartialSum* segs, int32_t nseg, void* stream) {
+  ASVRL_REQUIRE(segs && nseg >= 0 && nseg <= ASVRL_MAX_SUM_SEGS, "asvrl_partial_sums: bad segment table");
+  if (nseg == 0) return 0;
+  SumSegs t{};
+  int maxn = 0;
+  for (int k = 0; k < nseg; ++k) {
+    ASVRL_REQUIRE(segs[k].partial && segs[k].dw && segs[k].groups >= 0, "asvrl_partial_sums: null segment");
+    t.seg[k] = segs[k];
+    maxn = std::max(maxn, segs[k].nw + segs[k].nb);
+  }
+  hipLaunchKernelGGL(partial_sums_kernel, dim3((maxn + 63) / 64, nseg), dim3(kWgThreads), 0, as_stream(stream), t);
+  return check_launch("asvrl_partial_sums");
+}
+
+extern "C" int asvrl_linear_wgrad_vec_partial(const float* dq, int64_t ldq, const void* x, int64_t ldx, int32_t R,
+                                              int32_t K, float* partial, int64_t partial_floats, int32_t* groups_out,
+                                              void* stream) {
+  ASVRL_REQUIRE(dq && x && partial && groups_out, "asvrl_linear_wgrad_vec: null argument");
   ASVRL_REQUIRE(K == 128 || K == 256 || K == 64, "asvrl_linear_wgrad_vec: K must be 64, 128 or 256");
   ASVRL_REQUIRE(ldx >= K && ldx % 8 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0,
                 "asvrl_linear_wgrad_vec: x must be 16-byte aligned with ldx >= K, a multiple of 8");
-  ASVRL_REQUIRE(work_floats >= static_cast<int64_t>(kMaxGroups) * (K + 1), "asvrl_linear_wgrad_vec: workspace too small");
+  ASVRL_REQUIRE(partial_floats >= static_cast<int64_t>(vec_groups(R)) * (K + 1),
+                "asvrl_linear_wgrad_vec: workspace too small");
+  *groups_out = 0;
   if (R <= 0) return 0;
   hipStream_t st = as_stream(stream);
-  int groups = R < kMaxGroups ? R : kMaxGroups;
+  const int groups = vec_groups(R);
   const int per = (R + groups - 1) / groups;
-  groups = (R + per - 1) / per;
   const __bf16* xx = static_cast<const __bf16*>(x);
-  if (K == 128) hipLaunchKernelGGL(wgrad_vec_kernel<128>, dim3(groups), dim3(kWgThreads), 0, st, dq, ldq, xx, ldx, R, per, work);
-  else if (K == 256) hipLaunchKernelGGL(wgrad_vec_kernel<256>, dim3(groups), dim3(kWgThreads), 0, st, dq, ldq, xx, ldx, R, per, work);
-  else hipLaunchKernelGGL(wgrad_vec_kernel<64>, dim3(groups), dim3(kWgThreads), 0, st, dq, ldq, xx, ldx, R, per, work);
-  if (int rc = check_launch("asvrl_linear_wgrad_vec")) return rc;
-  hipLaunchKernelGGL(partial_sum_kernel, dim3((K + 1 + 63) / 64), dim3(kWgThreads), 0, st, work, groups, K, 1, dw,
-                     db, accumulate);
-  return check_launch("asvrl_linear_wgrad_vec(sum)");
+  if (K == 128) hipLaunchKernelGGL(wgrad_vec_kernel<128>, dim3(groups), dim3(kWgThreads), 0, st, dq, ldq, xx, ldx, R, per, partial);
+  else if (K == 256) hipLaunchKernelGGL(wgrad_vec_kernel<256>, dim3(groups), dim3(kWgThreads), 0, st, dq, ldq, xx, ldx, R, per, partial);
+  else hipLaunchKernelGGL(wgrad_vec_kernel<64>, dim3(groups), dim3(kWgThreads), 0, st, dq, ldq, xx, ldx, R, per, partial);
+  *groups_out = groups;
+  return check_launch("asvrl_linear_wgrad_vec");
+}
+
+extern "C" int asvrl_linear_wgrad_vec(const float* dq, int64_t ldq, const void* x, int64_t ldx, int32_t R, int32_t K,
+                                      float* dw, float* db, int32_t accumulate, float* work, int64_t work_floats,
+                                      void* stream) {
+  ASVRL_REQUIRE(dw != nullptr, "asvrl_linear_wgrad_vec: null dw");
+  int32_t groups = 0;
+  if (int rc = asvrl_linear_wgrad_vec_partial(dq, ldq, x, ldx, R, K, work, work_floats, &groups, stream)) return rc;
+  if (groups == 0) return 0;
+  return launch_partial_sum(work, groups, K, 1, dw, db, accumulate, as_stream(stream));
 }

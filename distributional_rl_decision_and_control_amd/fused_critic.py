@@ -175,6 +175,79 @@ def linear_wgrad_vec(dq, x, dw, db, work, accumulate=False, stream=None):
     _abi.check(rc, "asvrl_linear_wgrad_vec")
 
 
+class PartialArena:
+    """Weight-gradient partials of several layers, reduced together by ONE asvrl_partial_sums
+    launch (instead of one reduction launch per layer). Regions are handed out in call order
+    from one preallocated buffer, so the pointers repeat exactly under HIP-graph replay."""
+
+    def __init__(self, floats, device):
+        self.buf = torch.empty(int(floats), dtype=torch.float32, device=device)
+        self.off = 0
+        self.segs = []
+
+    def _take(self, n):
+        if self.off + n > self.buf.numel():
+            raise RuntimeError("PartialArena too small")
+        t = self.buf[self.off:self.off + n]
+        self.off += (n + 63) // 64 * 64
+        return t
+
+    def _seg(self, part, dw, db, groups, nw, nb, accumulate):
+        g = _abi.AsvPartialSum()
+        g.partial, g.dw, g.db = part.data_ptr(), dw.data_ptr(), (db.data_ptr() if db is not None else None)
+        g.groups, g.nw, g.nb, g.accumulate = groups, nw, nb, int(accumulate)
+        self.segs.append(g)
+        if len(self.segs) == _abi.MAX_SUM_SEGS:
+            self.flush()
+
+    def linear(self, dz, x, dw, db, accumulate=False, stream=None):
+        R, M = dz.shape
+        K = x.shape[1]
+        L = _abi.lib()
+        part = self._take(int(L.asvrl_linear_wgrad_groups(R, M, K)) * (M * K + M))
+        groups = C.c_int32(0)
+        _abi.check(L.asvrl_linear_wgrad_partial(_abi.ptr(dz), dz.stride(0), _abi.ptr(x), x.stride(0), R, M, K,
+                                                _abi.ptr(part), part.numel(), C.byref(groups),
+                                                _abi.stream_ptr(stream)), "asvrl_linear_wgrad_partial")
+        self._seg(part, dw, db, groups.value, M * K, M, accumulate)
+
+    def vec(self, dq, x, dw, db, accumulate=False, stream=None):
+        R, K = x.shape
+        L = _abi.lib()
+        part = self._take(int(L.asvrl_linear_wgrad_vec_groups(R)) * (K + 1))
+        groups = C.c_int32(0)
+        _abi.check(L.asvrl_linear_wgrad_vec_partial(_abi.ptr(dq), dq.stride(0), _abi.ptr(x), x.stride(0), R, K,
+                                                    _abi.ptr(part), part.numel(), C.byref(groups),
+                                                    _abi.stream_ptr(stream)), "asvrl_linear_wgrad_vec_partial")
+        self._seg(part, dw, db, groups.value, K, 1, accumulate)
+
+    def small(self, dz, x, dw, db, accumulate=False, stream=None):
+        R, M = dz.shape
+        K = x.shape[1]
+        part = self._take(((R + 31) // 32) * (M * K + M))
+        groups = C.c_int32(0)
+        _abi.check(_abi.lib().asvrl_small_wgrad_partial(dz.data_ptr(), dz.stride(0), x.data_ptr(), x.stride(0), R,
+                                                        M, K, part.data_ptr(), part.numel(), C.byref(groups),
+                                                        _abi.stream_ptr(stream)), "asvrl_small_wgrad_partial")
+        self._seg(part, dw, db, groups.value, M * K, M, accumulate)
+
+    def flush(self, stream=None):
+        if self.segs:
+            arr = (_abi.AsvPartialSum * len(self.segs))(*self.segs)
+            _abi.check(_abi.lib().asvrl_partial_sums(arr, len(self.segs), _abi.stream_ptr(stream)),
+                       "asvrl_partial_sums")
+        self.segs = []
+        self.off = 0
+
+
+def trunk_weight_grads_into(arena, critic, bufs):
+    """Queue the trunk layers' weight/bias gradients on a PartialArena (reduced at its flush)."""
+    arena.linear(bufs.dzc, bufs.cos, critic.cos_embedding.weight.grad, critic.cos_embedding.bias.grad)
+    arena.linear(bufs.dz1, bufs.h0, critic.hidden_layer.weight.grad, critic.hidden_layer.bias.grad)
+    arena.linear(bufs.dz2, bufs.h1g, critic.hidden_layer_2.weight.grad, critic.hidden_layer_2.bias.grad)
+    arena.vec(bufs.dq, bufs.h2, critic.output_layer.weight.grad, critic.output_layer.bias.grad)
+
+
 def trunk_weight_grads(critic, bufs):
     """Weight/bias gradients of the fused trunk layers from the TRAIN activations: four
     asvrl_linear_wgrad launches pairs (MFMA reduction over the B*N rows + partial sum)."""

@@ -9,10 +9,11 @@ Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | 
     local encoders(s, a) -> F, G (+ bf16 obs copy)       asvrl_mlp_encode
     trunk forward + quantile-Huber vs r + g q_next (1-d) + backward
                                                           asvrl_critic_train (targets formed in-kernel)
-    trunk weight grads                                   asvrl_linear_wgrad x3 + _vec
+    trunk weight grads                                   asvrl_linear_wgrad_partial x3 + _vec
     encoder grads (256x32 image, folded) and action-encoder grads
-                                                          asvrl_linear_wgrad + asvrl_encoder_fold
-                                                          + asvrl_small_wgrad
+                                                          asvrl_linear_wgrad_partial + _small_wgrad_partial,
+                                                          ONE asvrl_partial_sums for all six layers,
+                                                          asvrl_encoder_fold
     [RCCL all-reduce] clip + Adam                        asvrl_adam_clip
     re-pack trunk and encoders                           asvrl_critic_pack + asvrl_mlp_pack
   actor (agent.py:419-427), through the UPDATED critic
@@ -20,17 +21,17 @@ Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | 
     encoders(s, a) -> F2, G2                             asvrl_mlp_encode
     trunk forward + backward of -mean(q) to the action   asvrl_critic_actor_grad (dA in-kernel)
     actor backward                                       asvrl_actor_backward
-    actor weight grads                                   asvrl_linear_wgrad x3 + _vec x2 + fold
+    actor weight grads                                   wgrad partials x5, one asvrl_partial_sums, fold
     [RCCL all-reduce] clip + Adam, re-pack actor         asvrl_adam_clip + asvrl_mlp_pack
 
 Arithmetic: bf16 MFMA operands with f32 accumulation everywhere, f32 master weights / Adam.
 """
 import torch
 
-from .fused_critic import (CriticPack, TrainBuffers, critic_actor_grad, critic_forward, critic_train,
-                           linear_wgrad, linear_wgrad_vec, trunk_weight_grads)
+from .fused_critic import (CriticPack, PartialArena, TrainBuffers, critic_actor_grad, critic_forward, critic_train,
+                           trunk_weight_grads_into)
 from .fused_mlp import (ActorBuffers, MlpPack, actor_act, actor_backward, actor_forward, actor_train_forward,
-                        encoder_fold, mlp_encode, small_wgrad)
+                        encoder_fold, mlp_encode)
 from .learner import clip_and_step
 
 OBS = 40
@@ -72,7 +73,9 @@ class FusedACIQNState:
         self.dzG = torch.empty(B, 128, **f)
         self.enc_dw = torch.empty(256, 32, **f)
         self.enc_db = torch.empty(256, **f)
-        self.swork = torch.empty(((B + 255) // 256) * (128 * 2 + 128), **f)
+        self.enc_dw2 = torch.empty(256, 32, **f)
+        self.enc_db2 = torch.empty(256, **f)
+        self.arena = PartialArena(16 << 20, dev)
 
     def target_changed(self):
         """Re-pack the target networks after a hard/soft update (eager, outside graphs)."""
@@ -94,7 +97,7 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
         taus = torch.rand(3, B, N, device=st.device)
     s_rows, ns_rows = rows[:, 0:OBS], rows[:, OBS:2 * OBS]
     a_rows, r_col, d_col = rows[:, 80:82], rows[:, 82], rows[:, 83]
-    bufs, ab, work = st.bufs, st.abufs, st.bufs.work
+    bufs, ab, arena = st.bufs, st.abufs, st.arena
 
     # ---- critic (agent.py:395-416); every critic .grad is overwritten below (no zeroing)
     actor_forward(st.target_actor, ns_rows, st.na)
@@ -103,11 +106,12 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     mlp_encode(st.local_cenc, s_rows, st.F, st.G, act=a_rows, xb=st.xb)
     critic_loss = critic_train(st.local_trunk, st.F, st.G, taus[1], None, bufs, q_next=st.q_next.view(B, N),
                                rewards=r_col, dones=d_col, gamma=gamma, dzF=st.dzF, dzG=st.dzG, with_dFdG=False)
-    trunk_weight_grads(critic, bufs)
-    linear_wgrad(st.dzF, st.xb, st.enc_dw, st.enc_db, work)
-    encoder_fold(st.enc_dw, st.enc_db, critic)
     ae = critic.action_encoder[0]
-    small_wgrad(st.dzG, a_rows, ae.weight.grad, ae.bias.grad, st.swork)
+    trunk_weight_grads_into(arena, critic, bufs)
+    arena.linear(st.dzF, st.xb, st.enc_dw, st.enc_db)
+    arena.small(st.dzG, a_rows, ae.weight.grad, ae.bias.grad)
+    arena.flush()                                   # one reduction launch for the six layers
+    encoder_fold(st.enc_dw, st.enc_db, critic)
     if sync is not None:
         sync(critic_grads)
     cgn = clip_and_step(critic_opt, critic_grads, max_norm)
@@ -120,13 +124,14 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     critic_actor_grad(st.local_trunk, st.F2, st.G2, taus[2], N, st.q_pi, w_ae=ae.weight, dA=ab.dA)
     actor_loss = -st.q_pi.mean()
     actor_backward(st.actor, ab)
-    linear_wgrad(ab.dz1, ab.h0, actor.hidden_layer.weight.grad, actor.hidden_layer.bias.grad, work)
-    linear_wgrad(ab.dz2, ab.h1, actor.hidden_layer_2.weight.grad, actor.hidden_layer_2.bias.grad, work)
+    arena.linear(ab.dz1, ab.h0, actor.hidden_layer.weight.grad, actor.hidden_layer.bias.grad)
+    arena.linear(ab.dz2, ab.h1, actor.hidden_layer_2.weight.grad, actor.hidden_layer_2.bias.grad)
     ow, obias = actor.output_layer.weight.grad, actor.output_layer.bias.grad
-    linear_wgrad_vec(ab.dout[:, 0], ab.h2, ow[0], obias[0:1], work)
-    linear_wgrad_vec(ab.dout[:, 1], ab.h2, ow[1], obias[1:2], work)
-    linear_wgrad(ab.dz0, ab.xb, st.enc_dw, st.enc_db, work)
-    encoder_fold(st.enc_dw, st.enc_db, actor)
+    arena.vec(ab.dout[:, 0], ab.h2, ow[0], obias[0:1])
+    arena.vec(ab.dout[:, 1], ab.h2, ow[1], obias[1:2])
+    arena.linear(ab.dz0, ab.xb, st.enc_dw2, st.enc_db2)
+    arena.flush()
+    encoder_fold(st.enc_dw2, st.enc_db2, actor)
     if sync is not None:
         sync(actor_grads)
     agn = clip_and_step(actor_opt, actor_grads, max_norm)

@@ -308,10 +308,35 @@ int asvrl_linear_wgrad(const void* dz, int64_t ldz, const void* x, int64_t ldx, 
                        int32_t K, float* dw, float* db, int32_t accumulate, float* work,
                        int64_t work_floats, void* stream);
 
+/* The same without the final reduction: writes *groups_out partials of (M*K + M) floats each
+ * into `partial` (asvrl_linear_wgrad_groups(R, M, K) of them); reduce later, possibly together
+ * with other layers, with asvrl_partial_sums. */
+int32_t asvrl_linear_wgrad_groups(int32_t R, int32_t M, int32_t K);
+int asvrl_linear_wgrad_partial(const void* dz, int64_t ldz, const void* x, int64_t ldx, int32_t R, int32_t M,
+                               int32_t K, float* partial, int64_t partial_floats, int32_t* groups_out,
+                               void* stream);
+
 /* One output unit's version: dw[k] = sum_r dq[r*ldq] x[r][k], db = sum_r dq[r*ldq] with dq f32 and
  * x bf16 (R x K, ldx); K in {64, 128, 256}; work >= 256 * (K + 1) floats. */
 int asvrl_linear_wgrad_vec(const float* dq, int64_t ldq, const void* x, int64_t ldx, int32_t R, int32_t K, float* dw,
                            float* db, int32_t accumulate, float* work, int64_t work_floats, void* stream);
+
+int32_t asvrl_linear_wgrad_vec_groups(int32_t R);
+int asvrl_linear_wgrad_vec_partial(const float* dq, int64_t ldq, const void* x, int64_t ldx, int32_t R,
+                                   int32_t K, float* partial, int64_t partial_floats, int32_t* groups_out,
+                                   void* stream);
+
+/* One pending reduction: dw[i] (+)= sum_g partial[g][i] for i < nw, db likewise for the
+ * trailing nb values of each group's (nw + nb)-float partial (db optional). */
+#define ASVRL_MAX_SUM_SEGS 8
+typedef struct AsvPartialSum {
+  const float* partial;
+  float* dw;
+  float* db;
+  int32_t groups, nw, nb, accumulate;
+} AsvPartialSum;
+/* Reduce up to ASVRL_MAX_SUM_SEGS pending partial sets in one launch (fixed order per output). */
+int asvrl_partial_sums(const AsvPartialSum* segs, int32_t nseg, void* stream);
 
 /* ---------------------------------------------------------------- per-row MLPs (actor, encoders) */
 
@@ -389,10 +414,13 @@ int asvrl_actor_backward(const AsvMlpWeights* w, const AsvMlpIO* io, void* strea
 int asvrl_encoder_fold(const float* dw, const float* db, float* self_w, float* self_b, float* obj_w,
                        float* obj_b, int32_t accumulate, void* stream);
 /* dw[m][k] = sum_r dz[r][m] x[r][k], db[m] = sum_r dz[r][m] for f32 inputs with K <= 4 and
- * M | 256 (the critic action_encoder). work >= ceil(R / 256) * (M*K + M) floats. */
+ * M | 256 (the critic action_encoder). work >= ceil(R / 32) * (M*K + M) floats. */
 int asvrl_small_wgrad(const float* dz, int64_t ldz, const float* x, int64_t ldx, int32_t R, int32_t M,
                       int32_t K, float* dw, float* db, int32_t accumulate, float* work,
                       int64_t work_floats, void* stream);
+int asvrl_small_wgrad_partial(const float* dz, int64_t ldz, const float* x, int64_t ldx, int32_t R,
+                              int32_t M, int32_t K, float* partial, int64_t partial_floats,
+                              int32_t* groups_out, void* stream);
 
 /* ---------------------------------------------------------------- misc */
 const char* asvrl_last_error(void);

@@ -79,3 +79,48 @@ def test_wgrad_vec(K):
     ref = dq.double() @ x.double()
     assert (dw.double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
     assert abs(db.item() - dq.double().sum().item()) <= 1e-4 * dq.abs().sum().item() * 1e-3
+
+
+def test_partial_arena_is_bit_identical_to_per_layer_reduction():
+    """PartialArena (partials of several layers, one asvrl_partial_sums launch) gives exactly
+    the per-layer asvrl_linear_wgrad / _vec / asvrl_small_wgrad results (same partials, same
+    fixed summation order), including more segments than one launch takes."""
+    from distributional_rl_decision_and_control_amd import _abi
+    from distributional_rl_decision_and_control_amd.fused_critic import PartialArena, linear_wgrad, linear_wgrad_vec
+    from distributional_rl_decision_and_control_amd.fused_mlp import small_wgrad
+    g = torch.Generator(device="cuda").manual_seed(9)
+    R = 8192
+    arena = PartialArena(32 << 20, "cuda")
+    work = torch.empty(int(_abi.lib().asvrl_linear_wgrad_workspace(128, 256)), device="cuda")
+    cases, outs_a, outs_b = [], [], []
+    for (M, K) in SHAPES * 2 + [(256, 32)]:
+        dz = torch.randn(R, M, generator=g, device="cuda").to(torch.bfloat16)
+        x = torch.randn(R, K, generator=g, device="cuda").to(torch.bfloat16)
+        wa, ba = torch.zeros(M, K, device="cuda"), torch.zeros(M, device="cuda")
+        wb, bb = torch.zeros(M, K, device="cuda"), torch.zeros(M, device="cuda")
+        linear_wgrad(dz, x, wa, ba, work)
+        arena.linear(dz, x, wb, bb)
+        outs_a += [wa, ba]
+        outs_b += [wb, bb]
+    dq = torch.randn(R, 2, generator=g, device="cuda")
+    h = torch.randn(R, 128, generator=g, device="cuda").to(torch.bfloat16)
+    wa, ba = torch.zeros(128, device="cuda"), torch.zeros(1, device="cuda")
+    wb, bb = torch.zeros(128, device="cuda"), torch.zeros(1, device="cuda")
+    linear_wgrad_vec(dq[:, 1], h, wa, ba, work)
+    arena.vec(dq[:, 1], h, wb, bb)
+    outs_a += [wa, ba]
+    outs_b += [wb, bb]
+    dzs = torch.randn(R, 128, generator=g, device="cuda")
+    xs = torch.randn(R, 88, generator=g, device="cuda")[:, 80:82]
+    wa, ba = torch.zeros(128, 2, device="cuda"), torch.zeros(128, device="cuda")
+    wb, bb = torch.zeros(128, 2, device="cuda"), torch.zeros(128, device="cuda")
+    small_wgrad(dzs, xs, wa, ba, torch.empty((R // 32) * 384, device="cuda"))
+    arena.small(dzs, xs, wb, bb)
+    outs_a += [wa, ba]
+    outs_b += [wb, bb]
+    arena.flush()
+    torch.cuda.synchronize()
+    for a, b in zip(outs_a, outs_b):
+        assert torch.equal(a, b)
+    ref = dzs.double().t() @ xs.double()
+    assert (wa.double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
