@@ -10,7 +10,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libasvrl.so")
+LIB_PATH = os.environ.get("ASVRL_LIB", os.path.join(HERE, "lib", "libasvrl.so"))  # override: A/B variants
 ABI_VERSION = 2
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5

@@ -61,12 +61,15 @@ struct CriticArgs {
 
 // LDS-resident forward weights: fragment images of Wc, W1, W2 (128 KB) + bc, b1, b2, wo.
 constexpr int kFragWC = kC * kNcos / 8, kFragW1 = kH * kC / 8, kFragW2 = kH * kH / 8;
+// wc holds Wc's image for FWD and W2^T's for TRAIN / ACTOR (which then read Wc from global at the
+// top of the tile, before any store, and need W2^T after the activation stores have started)
 struct CriticLds {
   bf16x8 wc[kFragWC];
   bf16x8 w1[kFragW1];
   bf16x8 w2[kFragW2];
   float bc[kC], b1[kH], b2[kH], wo[kH];
 };
+static_assert(kFragWC == kFragW2, "the Wc / W2^T slot holds either image");
 
 template <int MODE, int NT>
 __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds& L, int tile, int lane) {
@@ -76,7 +79,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
   const float tau = a.taus[grow];
   const float* Fb = a.F + static_cast<size_t>(b) * kC;
   const float* Gb = a.G + static_cast<size_t>(b) * kH;
-  const bf16x8* WC = L.wc;
+  const bf16x8* WC = MODE == MODE_FWD ? L.wc : reinterpret_cast<const bf16x8*>(a.w.wc_frag);
   const bf16x8* W1 = L.w1;
   const bf16x8* W2 = L.w2;
 
@@ -87,8 +90,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int k = ks * 16 + 8 * h + j;
-      const float pis = static_cast<float>(3.141592653589793 * k);  // torch.FloatTensor([pi*i])
-      cx[ks][j] = (__bf16)cosf(tau * pis);
+      cx[ks][j] = (__bf16)cos_pi_k_tau(tau, k);
     }
     if (MODE == MODE_TRAIN)
       *reinterpret_cast<bf16x8*>(bp(a.acts.cos) + static_cast<size_t>(grow) * kNcos + ks * 16 + 8 * h) = cx[ks];
@@ -114,7 +116,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
         for (int j = 0; j < 8; ++j) {
           const int m = feat(mb, 8 * s + j, h);
           float x = acc0[q4][8 * s + j] + L.bc[m];
-          x = x > 0.f ? x : 0.f;
+          x = relu(x);
           cpk[mb * 2 + s][j] = (__bf16)x;
           hv[j] = Fb[m] * x;
           hpk[mb * 2 + s][j] = (__bf16)hv[j];
@@ -147,7 +149,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
       for (int j = 0; j < 8; ++j) {
         const int m = feat(mb, 8 * s + j, h);
         float x = acc1[mb][8 * s + j] + L.b1[m];
-        x = x > 0.f ? x : 0.f;
+        x = relu(x);
         h1pk[mb * 2 + s][j] = (__bf16)x;
         gv[j] = x * Gb[m];
         gpk[mb * 2 + s][j] = (__bf16)gv[j];
@@ -177,7 +179,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
       const int m = feat(mb, g, h);
       float x = acc2[mb][g] + L.b2[m];
       acc2[mb][g] = x;  // keep z2 for the relu mask
-      part += L.wo[m] * (x > 0.f ? x : 0.f);
+      part += L.wo[m] * relu(x);
     }
   }
   const float q = part + __shfl_xor(part, 32, 64) + a.w.bo[0];
@@ -194,9 +196,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
       nd = 1.0f - a.don[b * a.ld_rd];
     }
     float wl = 0.f, wg = 0.f;
-    for (int j = 0; j < a.Np; ++j) {
-      // rewards + gamma * q_next * (1 - dones), in torch's evaluation order
-      const float target = a.qn != nullptr ? rb + (a.gamma * qt[j]) * nd : qt[j];
+    auto term = [&](float target) {
       const float d = target - q;  // td_error (agent.py:406)
       const float ad = fabsf(d);
       const bool quad = ad <= a.kappa;
@@ -204,6 +204,20 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
       const float w = fabsf(tau - (d < 0.f ? 1.f : 0.f));
       wl += w * hub / a.kappa;
       wg += w * (quad ? d : (d > 0.f ? a.kappa : -a.kappa)) / a.kappa;
+    };
+    if (a.Np == NT) {
+      // N' = N: lane r owns target r % N of its sample (one load per lane, no load in the loop);
+      // the loop broadcasts it: readlane when one sample fills the 32-row tile, else a shuffle
+      const float qv = qt[r % NT];
+      const float own = a.qn != nullptr ? rb + (a.gamma * qv) * nd : qv;   // r + gamma * q_next * (1 - d)
+#pragma unroll 8
+      for (int j = 0; j < NT; ++j) {
+        const float target = NT == 32 ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(own), j))
+                                      : __shfl(own, (lane & ~(NT - 1)) + j, 64);
+        term(target);
+      }
+    } else {
+      for (int j = 0; j < a.Np; ++j) term(a.qn != nullptr ? rb + (a.gamma * qt[j]) * nd : qt[j]);
     }
     dq = -wg * a.gscale;
     if (h == 0) {
@@ -225,7 +239,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
       for (int j = 0; j < 8; ++j) {
         const int m = feat(mb, 8 * s + j, h);
         const float z = acc2[mb][8 * s + j];
-        hv[j] = z > 0.f ? z : 0.f;
+        hv[j] = relu(z);
         dv[j] = z > 0.f ? dq * L.wo[m] : 0.f;
         dz2pk[mb * 2 + s][j] = (__bf16)dv[j];
       }
@@ -240,8 +254,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
   }
 
   // ---------------- layer 3: dh1g = W2^T dz2; dG[b] = sum_taus dh1g * h1; dz1 = dh1g * G * 1[h1 > 0]
-  const bf16x8* W2T = reinterpret_cast<const bf16x8*>(a.w.w2t_frag);
-  asm volatile("" : "+v"(W2T));  // not loop-invariant for the compiler (see critic_kernel)
+  const bf16x8* W2T = L.wc;   // TRAIN / ACTOR stage W2^T in this slot
   f32x16 acc3[4];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) acc3[mb] = f32x16{};
@@ -250,7 +263,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
 #pragma unroll
     for (int mb = 0; mb < 4; ++mb) acc3[mb] = mfma(W2T[(mb * 8 + ks) * 64 + lane], dz2pk[ks], acc3[mb]);
   }
-  const bool writer = (r % NT) == 0;
+  const bool writer = (r % NT) == NT - 1;   // holds the segment sums (seg_sum)
   float pa0 = 0.f, pa1 = 0.f;   // ACTOR: partial dA over this lane's features
   bf16x8 dz1pk[8];
 #pragma unroll
@@ -306,28 +319,72 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
     return;
   }
 
-  // ---------------- layer 4: dh0 = W1^T dz1; dF[b] = sum_taus dh0 * c; dzc = dh0 * F * 1[c > 0]
-  const bf16x8* W1T = reinterpret_cast<const bf16x8*>(a.w.w1t_frag);
-  asm volatile("" : "+v"(W1T));
+}
+
+// ---------------- TRAIN part B, layer 4: dh0 = W1^T dz1; dF[b] = sum_taus dh0 * c; dzc = dh0 * F * 1[c > 0].
+// c = relu(Wc cos + bc) is recomputed (bit-identical to part A's) instead of being kept live across
+// the layers, which is what lets both parts run two waves per SIMD.
+struct CriticLdsB {
+  bf16x8 wc[kFragWC];
+  bf16x8 w1t[kFragW1];
+  float bc[kC];
+};
+
+template <int NT>
+__device__ __forceinline__ void critic_tile_b(const CriticArgs& a, const CriticLdsB& L, int tile, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+  const int grow = tile * 32 + r;
+  const int b = grow / NT;
+  const float tau = a.taus[grow];
+  const float* Fb = a.F + static_cast<size_t>(b) * kC;
+  bf16x8 cx[kNcos / 16];
+#pragma unroll
+  for (int ks = 0; ks < kNcos / 16; ++ks)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = ks * 16 + 8 * h + j;
+      cx[ks][j] = (__bf16)cos_pi_k_tau(tau, k);
+    }
+  // dz1 as the chained B operand: element j of k-step ks is feature 16ks + 8(j>>2) + 4h + (j&3)
+  bf16x8 dz1pk[8];
+  const __bf16* dz1row = bp(a.acts.dz1) + static_cast<size_t>(grow) * kH;
+#pragma unroll
+  for (int ks = 0; ks < kH / 16; ++ks) {
+    const bf16x4 lo = *reinterpret_cast<const bf16x4*>(dz1row + ks * 16 + 4 * h);
+    const bf16x4 hi = *reinterpret_cast<const bf16x4*>(dz1row + ks * 16 + 8 + 4 * h);
+    dz1pk[ks] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  }
+  const bool writer = (r % NT) == NT - 1;
+  const bf16x8* W1T = L.w1t;
 #pragma unroll
   for (int half = 0; half < 2; ++half) {  // 2 x 4 output blocks keeps 64 accumulator registers live
-    f32x16 acc4[4];
+    f32x16 acc0[4], acc4[4];
 #pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) acc4[q4] = f32x16{};
+    for (int q4 = 0; q4 < 4; ++q4) {
+      acc0[q4] = f32x16{};
+      acc4[q4] = f32x16{};
+    }
 #pragma unroll
-    for (int ks = 0; ks < kH / 16; ++ks) {
+    for (int ks = 0; ks < kNcos / 16; ++ks)
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) acc0[q4] = mfma(L.wc[((half * 4 + q4) * 4 + ks) * 64 + lane], cx[ks], acc0[q4]);
+#pragma unroll
+    for (int ks = 0; ks < kH / 16; ++ks)
 #pragma unroll
       for (int q4 = 0; q4 < 4; ++q4)
         acc4[q4] = mfma(W1T[((half * 4 + q4) * 8 + ks) * 64 + lane], dz1pk[ks], acc4[q4]);
-    }
 #pragma unroll
     for (int q4 = 0; q4 < 4; ++q4) {
       const int mb = half * 4 + q4;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        float dv[8], fs[8];
+        float dv[8], fs[8], cv[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) fs[j] = acc4[q4][8 * s + j] * static_cast<float>(cpk[mb * 2 + s][j]);
+        for (int j = 0; j < 8; ++j) {
+          const float x = acc0[q4][8 * s + j] + L.bc[feat(mb, 8 * s + j, h)];
+          cv[j] = static_cast<float>((__bf16)relu(x));   // part A's bf16 c
+          fs[j] = acc4[q4][8 * s + j] * cv[j];
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) fs[j] = seg_sum<NT>(fs[j]);
         float fz[8];
@@ -335,8 +392,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
         for (int j = 0; j < 8; ++j) {
           const int m = feat(mb, 8 * s + j, h);
           const float fm = Fb[m];
-          const float c = static_cast<float>(cpk[mb * 2 + s][j]);
-          dv[j] = c > 0.f ? acc4[q4][8 * s + j] * fm : 0.f;
+          dv[j] = cv[j] > 0.f ? acc4[q4][8 * s + j] * fm : 0.f;
           fz[j] = fm > 0.f ? fs[j] : 0.f;   // through the encoders' relu / mask
         }
         if (writer) {
@@ -358,17 +414,32 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
   }
 }
 
+template <int NT>
+__global__ __launch_bounds__(8 * 64) void critic_train_b_kernel(CriticArgs a) {
+  __shared__ CriticLdsB L;
+  {
+    const bf16x8* gwc = reinterpret_cast<const bf16x8*>(a.w.wc_frag);
+    const bf16x8* gw1t = reinterpret_cast<const bf16x8*>(a.w.w1t_frag);
+    for (int i = threadIdx.x; i < kFragWC; i += 8 * 64) L.wc[i] = gwc[i];
+    for (int i = threadIdx.x; i < kFragW1; i += 8 * 64) L.w1t[i] = gw1t[i];
+    for (int i = threadIdx.x; i < kC; i += 8 * 64) L.bc[i] = a.w.bc[i];
+  }
+  __syncthreads();
+  const int tile = blockIdx.x * 8 + (threadIdx.x >> 6);
+  if (tile < a.B * NT / 32) critic_tile_b<NT>(a, L, tile, threadIdx.x & 63);
+}
+
 // Persistent: one workgroup per CU stages the forward weights into LDS once, then its waves
 // walk the 32-row tiles. 8 waves (2 per SIMD) where the registers allow, 4 for TRAIN.
 template <int MODE> struct CriticWaves { static constexpr int n = 8; };
-template <> struct CriticWaves<MODE_TRAIN> { static constexpr int n = 4; };
+template <> struct CriticWaves<MODE_TRAIN> { static constexpr int n = 8; };
 
 template <int MODE, int NT>
 __global__ __launch_bounds__(CriticWaves<MODE>::n * 64) void critic_kernel(CriticArgs a) {
   constexpr int W = CriticWaves<MODE>::n;
   __shared__ CriticLds L;
   {
-    const bf16x8* gwc = reinterpret_cast<const bf16x8*>(a.w.wc_frag);
+    const bf16x8* gwc = reinterpret_cast<const bf16x8*>(MODE == MODE_FWD ? a.w.wc_frag : a.w.w2t_frag);
     const bf16x8* gw1 = reinterpret_cast<const bf16x8*>(a.w.w1_frag);
     const bf16x8* gw2 = reinterpret_cast<const bf16x8*>(a.w.w2_frag);
     for (int i = threadIdx.x; i < kFragWC; i += W * 64) L.wc[i] = gwc[i];
@@ -422,9 +493,15 @@ void launch_mode(const CriticArgs& a, hipStream_t st) {
 
 template <int NT>
 void launch_n(int mode, const CriticArgs& a, hipStream_t st) {
-  if (mode == MODE_FWD) launch_mode<MODE_FWD, NT>(a, st);
-  else if (mode == MODE_TRAIN) launch_mode<MODE_TRAIN, NT>(a, st);
-  else launch_mode<MODE_ACTOR, NT>(a, st);
+  if (mode == MODE_FWD) {
+    launch_mode<MODE_FWD, NT>(a, st);
+  } else if (mode == MODE_TRAIN) {
+    launch_mode<MODE_TRAIN, NT>(a, st);
+    const int tiles = a.B * NT / 32;
+    hipLaunchKernelGGL((critic_train_b_kernel<NT>), dim3((tiles + 7) / 8), dim3(8 * 64), 0, st, a);
+  } else {
+    launch_mode<MODE_ACTOR, NT>(a, st);
+  }
 }
 
 int launch(int mode, const CriticArgs& a, void* stream) {

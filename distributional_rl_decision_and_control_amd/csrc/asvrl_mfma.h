@@ -30,17 +30,29 @@ __device__ __forceinline__ float dpp(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
 
-// Sum over aligned groups of NT lanes (NT | 32), every lane of a group gets the sum: xor-1 and
-// xor-2 quad butterflies, row_half_mirror (8), row_mirror (16) on DPP, one bpermute for 32.
+// Sum over aligned groups of NT lanes (NT | 32), all on DPP: xor-1 and xor-2 quad butterflies,
+// row_half_mirror (8), row_mirror (16) leave every lane of a 16-lane row with the row sum; for 32,
+// row_bcast:15 (rows 1 and 3 only) adds the previous row's sum. The full sum is guaranteed in the
+// LAST lane of each group (r % NT == NT - 1); for NT <= 16 every lane of the group has it.
 template <int NT>
 __device__ __forceinline__ float seg_sum(float v) {
   if (NT >= 2) v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
   if (NT >= 4) v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
   if (NT >= 8) v += dpp<0x141>(v);  // row_half_mirror
   if (NT >= 16) v += dpp<0x140>(v); // row_mirror
-  if (NT >= 32) v += __shfl_xor(v, 16, 64);
+  if (NT >= 32)                     // row_bcast:15 into rows 1, 3 (rows 0, 2 add 0)
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xA, 0xF, false));
   return v;
 }
+
+// cos(tau * pi * k) (Critic.calc_cos, AC_IQN_model.py:423) on the hardware cosine: v_cos_f32 takes
+// revolutions, cos(2 pi x) with x = k tau / 2 (< 32 for k < 64, tau < 1: inside its +-256 domain).
+// The value is rounded to bf16 for the MFMA right after, far above v_cos_f32's error.
+__device__ __forceinline__ float cos_pi_k_tau(float tau, int k) {
+  return __builtin_amdgcn_cosf(tau * (0.5f * static_cast<float>(k)));
+}
+
+__device__ __forceinline__ float relu(float x) { return fmaxf(x, 0.f); }
 
 // bf16x4 store of 4 consecutive features
 __device__ __forceinline__ void store4(__bf16* base, const float* v) {

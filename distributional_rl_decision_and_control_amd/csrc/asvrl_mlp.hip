@@ -74,7 +74,7 @@ __device__ __forceinline__ void encode_tile(const bf16x8* ENC, const float* benc
           const float mk0 = m0 < kSelfF ? 1.f : (mk[obj_of(m0)] < 0.5f ? 0.f : 1.f);
           const float mk1 = m0 + 4 < kSelfF ? 1.f : (mk[obj_of(m0 + 4)] < 0.5f ? 0.f : 1.f);
           float x = acc[q][g] + benc[m0 + 4 * h];
-          x = x > 0.f ? x : 0.f;
+          x = relu(x);
           v[j] = x * (h ? mk1 : mk0);
         }
         emit(mb, s, v);
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(kMlpWaves * 64) void encode_kernel(MlpArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float x = acc[8 * s + j] + a.w.b_ae[feat(mb, 8 * s + j, h)];
-        v[j] = x > 0.f ? x : 0.f;
+        v[j] = relu(x);
       }
       if (valid) {
         float* o = Gr + mb * 32 + 16 * s + 4 * h;
@@ -197,7 +197,7 @@ __device__ __forceinline__ void actor_tile(const MlpArgs& a, const ActorLds& L, 
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float x = acc1[mb][8 * s + j] + L.b1[feat(mb, 8 * s + j, h)];
-        v[j] = x > 0.f ? x : 0.f;
+        v[j] = relu(x);
         h1pk[mb * 2 + s][j] = (__bf16)v[j];
       }
       if (MODE == MLP_TRAIN && valid) {
@@ -224,7 +224,7 @@ __device__ __forceinline__ void actor_tile(const MlpArgs& a, const ActorLds& L, 
       for (int j = 0; j < 8; ++j) {
         const int m = feat(mb, 8 * s + j, h);
         const float x = acc2[mb][8 * s + j] + L.b2[m];
-        v[j] = x > 0.f ? x : 0.f;
+        v[j] = relu(x);
         p0 += L.wout[m] * v[j];
         p1 += L.wout[kHid + m] * v[j];
       }
