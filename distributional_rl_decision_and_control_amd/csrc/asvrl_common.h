@@ -103,4 +103,51 @@ struct Stream {
   }
 };
 
+// f32 draws for the training path (noise_mode 2): the perception noise only has to follow the
+// reference's distributions there (N(0, sigma), vonmises(0, kappa), wamv.py:27-40), so one Philox
+// call feeds four 24-bit uniforms and the transcendentals are the single-instruction f32 ones.
+struct StreamF {
+  uint32_t k0, k1, c1, c2, c3;
+  uint32_t n;
+  U4 buf;
+  int left;
+  __device__ StreamF(uint64_t seed, uint32_t a, uint32_t b, uint32_t c)
+      : k0(static_cast<uint32_t>(seed)), k1(static_cast<uint32_t>(seed >> 32)), c1(a), c2(b), c3(c), n(0),
+        buf{0, 0, 0, 0}, left(0) {}
+  __device__ float u01() {   // (0, 1]
+    if (left == 0) {
+      buf = philox4x32_10(U4{n++, c1, c2, c3}, k0, k1);
+      left = 4;
+    }
+    const uint32_t w = left == 4 ? buf.x : left == 3 ? buf.y : left == 2 ? buf.z : buf.w;
+    --left;
+    return (static_cast<float>(w >> 8) + 1.0f) * (1.0f / 16777216.0f);
+  }
+  __device__ void normal2(float& a, float& b) {
+    const float u1 = u01(), u2 = u01();
+    const float rad = __fsqrt_rn(-2.0f * __logf(u1));
+    const float t = 6.2831853f * u2;
+    a = rad * __cosf(t);
+    b = rad * __sinf(t);
+  }
+  __device__ float vonmises(float kappa) {   // Best & Fisher, as Stream::vonmises
+    if (kappa < 1e-6f) return 3.14159265f * (2.0f * u01() - 1.0f);
+    const float r = 1.0f + __fsqrt_rn(1.0f + 4.0f * kappa * kappa);
+    const float rho = (r - __fsqrt_rn(2.0f * r)) / (2.0f * kappa);
+    const float s = (1.0f + rho * rho) / (2.0f * rho);
+    float W = 1.0f;
+    for (int it = 0; it < 256; ++it) {
+      const float U = u01();
+      const float Z = __cosf(3.14159265f * U);
+      W = (1.0f + s * Z) / (s + Z);
+      const float Y = kappa * (s - W);
+      const float V = u01();
+      if ((Y * (2.0f - Y) - V >= 0.0f) || (__logf(Y / V) + 1.0f - Y >= 0.0f)) break;
+    }
+    const float U = u01();
+    float res = acosf(fminf(fmaxf(W, -1.0f), 1.0f));
+    return U < 0.5f ? -res : res;
+  }
+};
+
 }  // namespace asvrl

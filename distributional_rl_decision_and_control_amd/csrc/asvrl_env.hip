@@ -21,6 +21,9 @@ namespace asvrl {
 namespace {
 
 constexpr int kBlock = 256;
+// env-step workgroup: one wave of whole envs when they fit (R <= 64), spreading a 4096-env batch
+// over every CU instead of packing 51 envs per 256-lane group onto a third of them
+__host__ __device__ constexpr int step_block(int R) { return R <= 64 ? 64 : 256; }
 constexpr int kMaxCores = 16;
 
 struct Regs {
@@ -161,13 +164,15 @@ __device__ __attribute__((noinline)) bool colregs(double rself, double c, double
   const double py = sa * ox + -ca * oy;
   const double qx = ca * ev0 + sa * ev1;
   const double qy = -sa * ev0 + ca * ev1;
-  const double ang = atan2(qy, qx);
   const bool x_in = (px >= -9.0) && (px <= 12.0);  // wamv.py:344-362
   const bool y_in = (py >= -17.0) && (py <= 0.0);
   const bool in_tri = (py - (-7.0)) > (-7.0 / 12.0) * (px - 12.0);
-  const bool left = x_in && y_in && !in_tri && (ang >= kPi / 4) && (ang <= 3 * kPi / 4);
-  const bool head = (px >= 0.0) && (px <= 17.0) && (py >= -0.5 * 9.0) && (py <= 0.5 * 9.0) &&
-                    (fabs(ang) > 3 * kPi / 4);  // wamv.py:364-377
+  const bool left_pos = x_in && y_in && !in_tri;
+  const bool head_pos = (px >= 0.0) && (px <= 17.0) && (py >= -0.5 * 9.0) && (py <= 0.5 * 9.0);  // :364-377
+  if (!(left_pos || head_pos)) return false;   // the heading test below cannot rescue either zone
+  const double ang = atan2(qy, qx);
+  const bool left = left_pos && (ang >= kPi / 4) && (ang <= 3 * kPi / 4);
+  const bool head = head_pos && (fabs(ang) > 3 * kPi / 4);
   if (!(left || head)) return false;
   const double ego_ang = atan2(ev1, ev0);  // compute_COLREGs_turn_angle (wamv.py:379-396)
   const double obj_ang = atan2(oy, ox);
@@ -193,14 +198,15 @@ __device__ inline void cswap(bool cond, Cand& x, Cand& y) {
   }
 }
 
-__global__ __launch_bounds__(kBlock) void env_step_kernel(AsvParams p, AsvEnvState s,
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void env_step_kernel(AsvParams p, AsvEnvState s,
                                                           const double* __restrict__ actions,
                                                           const double* __restrict__ noise,
                                                           AsvStepCtl ctl, AsvStepOut out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int R = s.max_robots;
   const int O = s.max_obs;
-  const int epb = kBlock / R;
+  const int epb = BLOCK / R;
   const int tid = threadIdx.x;
   const int le = tid / R;
   const int i = tid - le * R;
@@ -215,12 +221,12 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(AsvParams p, AsvEnvSta
   // LDS carve (16-B aligned pieces): positions/velocities of the block's robots after the
   // move, their pre-step deactivated flags, the envs' obstacles and per-env reductions.
   double* sx = reinterpret_cast<double*>(smem);
-  double* sy = sx + kBlock;
-  double* sv0 = sy + kBlock;
-  double* sv1 = sv0 + kBlock;
-  double* sob = sv1 + kBlock;  // [epb][O][3]
+  double* sy = sx + BLOCK;
+  double* sv0 = sy + BLOCK;
+  double* sv1 = sv0 + BLOCK;
+  double* sob = sv1 + BLOCK;  // [epb][O][3]
   int* salive = reinterpret_cast<int*>(sob + static_cast<size_t>(epb) * O * 3);  // [epb]
-  unsigned char* soff = reinterpret_cast<unsigned char*>(salive + epb);          // [kBlock]
+  unsigned char* soff = reinterpret_cast<unsigned char*>(salive + epb);          // [BLOCK]
 
   Regs r{};
   uint8_t fl = 0;
@@ -311,8 +317,11 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(AsvParams p, AsvEnvSta
     const uint64_t ctr = ctl.counter + (ctl.counter_dev != nullptr ? *ctl.counter_dev : 0ull);
     Stream rng(ctl.seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull, static_cast<uint32_t>(idx),
                static_cast<uint32_t>(idx >> 32) ^ 0x5EEDu, static_cast<uint32_t>(ctr));
+    StreamF rngf(ctl.seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull, static_cast<uint32_t>(idx),
+                 static_cast<uint32_t>(idx >> 32) ^ 0xF32Au, static_cast<uint32_t>(ctr));
     int nkept = 0;
     const int ncand = no + nrob;
+    const bool full_circle = 0.5 * p.angle >= kPi;
     for (int k = 0; k < ncand; ++k) {
       double ox, oy, orad, vx0, vy0;
       int slot;
@@ -338,11 +347,17 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(AsvParams p, AsvEnvSta
       if (ctl.noise_mode == 0) {
         const double* nz = nz_base + slot * 5;
         n0 = nz[0]; n1 = nz[1]; n2 = nz[2]; n3 = nz[3]; n4 = nz[4];
-      } else {
+      } else if (ctl.noise_mode == 1) {
         rng.normal2(n0, n1);
         rng.normal2(n2, n3);
         n0 *= p.pos_std; n1 *= p.pos_std; n2 *= p.vel_std; n3 *= p.vel_std;
         n4 = rng.vonmises(p.r_kappa);
+      } else {
+        float f0, f1, f2, f3;
+        rngf.normal2(f0, f1);
+        rngf.normal2(f2, f3);
+        n0 = f0 * p.pos_std; n1 = f1 * p.pos_std; n2 = f2 * p.vel_std; n3 = f3 * p.vel_std;
+        n4 = rngf.vonmises(static_cast<float>(p.r_kappa));
       }
       const double pxn = ox + n0, pyn = oy + n1;  // Perception (wamv.py:27-40)
       const double vxn = vx0 + n2, vyn = vy0 + n3;
@@ -350,8 +365,10 @@ __global__ __launch_bounds__(kBlock) void env_step_kernel(AsvParams p, AsvEnvSta
       const double qx = (cs * pxn + sn * pyn) + tx, qy = (-sn * pxn + cs * pyn) + ty;
       const double qn = sqrt(qx * qx + qy * qy);
       if (qn > p.range + rn) continue;  // check_detection (wamv.py:293-303)
-      const double ang = atan2(qy, qx);
-      if (ang < -0.5 * p.angle || ang > 0.5 * p.angle) continue;
+      if (!full_circle) {              // atan2 lies in [-pi, pi]: the test only bites when angle < 2 pi
+        const double ang = atan2(qy, qx);
+        if (ang < -0.5 * p.angle || ang > 0.5 * p.angle) continue;
+      }
       if (!coll) {  // check_collision (wamv.py:281-291), true positions
         const double d = sqrt((r.x - ox) * (r.x - ox) + (r.y - oy) * (r.y - oy)) - orad - p.r;
         if (d <= 0.0) coll = true;
@@ -694,8 +711,9 @@ __global__ __launch_bounds__(kBlock) void current_kernel(const double* __restric
 }  // namespace
 
 size_t env_step_smem(int R, int O) {
-  const int epb = kBlock / R;
-  return sizeof(double) * (4 * kBlock + static_cast<size_t>(epb) * O * 3) + sizeof(int) * epb + kBlock;
+  const int blk = step_block(R);
+  const int epb = blk / R;
+  return sizeof(double) * (4 * blk + static_cast<size_t>(epb) * O * 3) + sizeof(int) * epb + blk;
 }
 
 }  // namespace asvrl
@@ -717,12 +735,17 @@ extern "C" int asvrl_env_step(const AsvParams* params, const AsvEnvState* state,
   ASVRL_REQUIRE(state->rs && state->rflags && state->n_robots && state->n_obs && state->n_cores && state->ep_ts,
                 "asvrl_env_step: null state array");
   if (state->n_envs == 0) return 0;
-  const int epb = kBlock / state->max_robots;
+  const int blk = step_block(state->max_robots);
+  const int epb = blk / state->max_robots;
   const int grid = (state->n_envs + epb - 1) / epb;
   const size_t smem = env_step_smem(state->max_robots, state->max_obs);
   ASVRL_REQUIRE(smem <= 160 * 1024, "asvrl_env_step: max_obs too large for LDS");
-  hipLaunchKernelGGL(env_step_kernel, dim3(grid), dim3(kBlock), smem, as_stream(stream), *params, *state,
-                     actions, noise, *ctl, *out);
+  if (blk == 64)
+    hipLaunchKernelGGL(env_step_kernel<64>, dim3(grid), dim3(64), smem, as_stream(stream), *params, *state, actions,
+                       noise, *ctl, *out);
+  else
+    hipLaunchKernelGGL(env_step_kernel<256>, dim3(grid), dim3(256), smem, as_stream(stream), *params, *state,
+                       actions, noise, *ctl, *out);
   return check_launch("asvrl_env_step");
 }
 

@@ -71,13 +71,15 @@ class DeviceEnvBatch:
 
     # ------------------------------------------------------------------ launches
     def step(self, actions, is_continuous=True, noise=None, do_dynamics=True, trainer_deactivate=False,
-             seed=0, counter=0, counter_dev=None, gamma=0.0, env_mask=None, obs=None, obj_cnt=None, stream=None):
-        """asvrl_env_step. actions: f64 [E*R, 2] device tensor. noise: f64 [E*R, O+R, 5] or None (Philox)."""
+             seed=0, counter=0, counter_dev=None, gamma=0.0, env_mask=None, obs=None, obj_cnt=None, stream=None,
+             fast_noise=False):
+        """asvrl_env_step. actions: f64 [E*R, 2] device tensor. noise: f64 [E*R, O+R, 5] or None (Philox;
+        fast_noise: f32 draws, noise_mode 2)."""
         ctl = _abi.AsvStepCtl()
         ctl.is_continuous = int(bool(is_continuous))
         ctl.do_dynamics = int(bool(do_dynamics))
         ctl.trainer_deactivate = int(bool(trainer_deactivate))
-        ctl.noise_mode = 0 if noise is not None else 1
+        ctl.noise_mode = 0 if noise is not None else (2 if fast_noise else 1)
         ctl.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         ctl.counter = int(counter) & 0xFFFFFFFFFFFFFFFF
         ctl.counter_dev = counter_dev.data_ptr() if counter_dev is not None else None

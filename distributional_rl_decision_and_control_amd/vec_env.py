@@ -71,7 +71,7 @@ class VecMarineNavEnv:
         b = self.batch
         b.reset(self.cfg, None, seed=self.seed, counter=0x40000000, counter_dev=self.counter)
         b.step(None, do_dynamics=False, seed=self.seed, counter=0x80000000, counter_dev=self.counter,
-               obs=self.obs_cur, obj_cnt=self.cnt_cur)
+               fast_noise=True, obs=self.obs_cur, obj_cnt=self.cnt_cur)
         return self.obs_cur
 
     def step(self, actions):
@@ -79,14 +79,14 @@ class VecMarineNavEnv:
         Writes obs_next / cnt_next, batch.reward / done / info / env_done."""
         self.batch.step(actions, is_continuous=self.is_continuous, trainer_deactivate=True, seed=self.seed,
                         counter=0, counter_dev=self.counter, gamma=self.gamma, obs=self.obs_next,
-                        obj_cnt=self.cnt_next)
+                        obj_cnt=self.cnt_next, fast_noise=True)   # f32 Philox draws (noise_mode 2)
 
     def auto_reset(self):
         """Reset the envs whose episode ended in the last step and observe them into obs_next."""
         b = self.batch
         b.reset(self.cfg, b.env_done, seed=self.seed, counter=0x40000000, counter_dev=self.counter)
         b.step(None, do_dynamics=False, seed=self.seed, counter=0x80000000, counter_dev=self.counter,
-               env_mask=b.env_done, obs=self.obs_next, obj_cnt=self.cnt_next)
+               fast_noise=True, env_mask=b.env_done, obs=self.obs_next, obj_cnt=self.cnt_next)
 
     def advance_device(self):
         self.obs[0].copy_(self.obs[1])

@@ -105,8 +105,10 @@ typedef struct AsvStepCtl {
   int32_t trainer_deactivate; /* 1: apply trainer.py:157-172 in-kernel (deactivate on flags,
                                  episode-end test, discounted return) */
   int32_t noise_mode;         /* 0: injected draws (noise != NULL, parity with the reference's
-                                 per-robot RandomState); 1: Philox-4x32-10 in registers */
-  uint64_t seed, counter;     /* Philox key / per-step counter (noise_mode 1) */
+                                 per-robot RandomState); 1: Philox-4x32-10 in registers, f64
+                                 Box-Muller / von Mises; 2: Philox, f32 draws on the hardware
+                                 transcendentals (the training path) */
+  uint64_t seed, counter;     /* Philox key / per-step counter (noise_mode 1, 2) */
   const uint64_t* counter_dev; /* optional device counter added to `counter` (keeps a captured
                                   HIP graph drawing fresh noise on every replay) */
   double gamma;               /* discount for ASVRL_F_RET (trainer.py:161); 0 disables */

@@ -295,3 +295,40 @@ def test_device_reset_invariants(R, O, Cn, W):
             assert (np.hypot(sx - cx, sy - cy) >= core_r + 10.0).all()
             assert (np.hypot(tx - cx, ty - cy) >= core_r + 10.0).all()
             assert cw in (0.0, 1.0) and G > 0
+
+
+@pytest.mark.parametrize("fast", [False, True])
+def test_philox_perception_noise_distribution(fast):
+    """Philox perception noise (noise_mode 1: f64 draws, 2: f32 draws) follows Perception's
+    distributions (wamv.py:27-40): position / velocity noise N(0, 0.05), radius
+    0.8 r + 0.2 r vm / pi with vm ~ vonmises(0, kappa=1). 65536 identical one-robot scenes
+    with one buoy 5 m ahead, observed once; moments against scipy to a few standard errors."""
+    from scipy import stats
+    from distributional_rl_decision_and_control_amd import _abi
+    from distributional_rl_decision_and_control_amd.device_env import DeviceEnvBatch
+    E = 65536
+    b = DeviceEnvBatch(E, 1, 1, 0)
+    b.rs.zero_()
+    b.rs[_abi.F_X].fill_(10.0)
+    b.rs[_abi.F_Y].fill_(10.0)
+    b.rs[_abi.F_GX].fill_(40.0)
+    b.rs[_abi.F_GY].fill_(40.0)
+    b.obstacles[:, 0, 0] = 15.0
+    b.obstacles[:, 0, 1] = 10.0
+    b.obstacles[:, 0, 2] = 1.0
+    b.n_robots.fill_(1)
+    b.n_obs.fill_(1)
+    b.step(None, do_dynamics=False, seed=123, counter=7, fast_noise=fast)
+    o = b.obs.double().cpu().numpy()
+    assert (b.obj_cnt.cpu().numpy() == 1).all()
+    px, py, vx, vy, rr = (o[:, 7 + k] for k in range(5))
+    n = len(px)
+    for v, mu in ((px, 5.0), (py, 0.0), (vx, 0.0), (vy, 0.0)):
+        assert abs(v.mean() - mu) < 4 * 0.05 / np.sqrt(n)
+        assert abs(v.std() / 0.05 - 1) < 0.02
+    vm_std = stats.vonmises(1.0).std()
+    assert abs(rr.mean() - 0.8) < 4 * 0.2 / np.pi * vm_std / np.sqrt(n)
+    assert abs(rr.std() / (0.2 / np.pi * vm_std) - 1) < 0.02
+    # the full shape of the von Mises draw: KS against scipy
+    vm = (rr - 0.8) / 0.2 * np.pi
+    assert stats.kstest(vm[:20000], stats.vonmises(1.0).cdf).pvalue > 1e-3
