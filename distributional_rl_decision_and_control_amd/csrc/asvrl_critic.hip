@@ -121,11 +121,8 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
           hv[j] = Fb[m] * x;
           hpk[mb * 2 + s][j] = (__bf16)hv[j];
         }
-        if (MODE == MODE_TRAIN) {
-          __bf16* row = bp(a.acts.h0) + static_cast<size_t>(grow) * kC + mb * 32 + 16 * s + 4 * h;
-          store4(row, hv);
-          store4(row + 8, hv + 4);
-        }
+        if (MODE == MODE_TRAIN)
+          store16(bp(a.acts.h0) + static_cast<size_t>(grow) * kC + mb * 32 + 16 * s, hv, h);
       }
     }
   }
@@ -154,11 +151,8 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
         gv[j] = x * Gb[m];
         gpk[mb * 2 + s][j] = (__bf16)gv[j];
       }
-      if (MODE == MODE_TRAIN) {
-        __bf16* row = bp(a.acts.h1g) + static_cast<size_t>(grow) * kH + mb * 32 + 16 * s + 4 * h;
-        store4(row, gv);
-        store4(row + 8, gv + 4);
-      }
+      if (MODE == MODE_TRAIN)
+        store16(bp(a.acts.h1g) + static_cast<size_t>(grow) * kH + mb * 32 + 16 * s, gv, h);
     }
   }
 
@@ -244,11 +238,9 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
         dz2pk[mb * 2 + s][j] = (__bf16)dv[j];
       }
       if (MODE == MODE_TRAIN) {
-        const size_t o = static_cast<size_t>(grow) * kH + mb * 32 + 16 * s + 4 * h;
-        store4(bp(a.acts.h2) + o, hv);
-        store4(bp(a.acts.h2) + o + 8, hv + 4);
-        store4(bp(a.acts.dz2) + o, dv);
-        store4(bp(a.acts.dz2) + o + 8, dv + 4);
+        const size_t o = static_cast<size_t>(grow) * kH + mb * 32 + 16 * s;
+        store16(bp(a.acts.h2) + o, hv, h);
+        store16(bp(a.acts.dz2) + o, dv, h);
       }
     }
   }
@@ -300,11 +292,8 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
           *reinterpret_cast<float4*>(a.dzG + ob + 8) = make_float4(gz[4], gz[5], gz[6], gz[7]);
         }
       }
-      if (MODE == MODE_TRAIN) {
-        __bf16* row = bp(a.acts.dz1) + static_cast<size_t>(grow) * kH + mb * 32 + 16 * s + 4 * h;
-        store4(row, dv);
-        store4(row + 8, dv + 4);
-      }
+      if (MODE == MODE_TRAIN)
+        store16(bp(a.acts.dz1) + static_cast<size_t>(grow) * kH + mb * 32 + 16 * s, dv, h);
     }
   }
   if (MODE == MODE_ACTOR) {
@@ -406,9 +395,7 @@ __device__ __forceinline__ void critic_tile_b(const CriticArgs& a, const CriticL
             store4(bp(a.dzF) + ob + 8, fz + 4);
           }
         }
-        __bf16* row = bp(a.acts.dzc) + static_cast<size_t>(grow) * kC + mb * 32 + 16 * s + 4 * h;
-        store4(row, dv);
-        store4(row + 8, dv + 4);
+        store16(bp(a.acts.dzc) + static_cast<size_t>(grow) * kC + mb * 32 + 16 * s, dv, h);
       }
     }
   }

@@ -64,6 +64,28 @@ __device__ __forceinline__ void store4(__bf16* base, const float* v) {
   *reinterpret_cast<bf16x4*>(base) = x;
 }
 
+// Store the 16 features of one k-step group (features 16s .. 16s+15 of a 32-feature block) of this
+// lane's row: lane half h holds v = {4h .. 4h+3, 8+4h .. 8+4h+3}; one exchange with the partner
+// lane (l ^ 32) gives half 0 features 0..7 and half 1 features 8..15, so each lane writes one
+// 16-byte piece and every row gets a full 32-byte sector per instruction. `grp` points at
+// feature 16s of the row. All 64 lanes must call it (cross-lane exchange).
+__device__ __forceinline__ void store16(__bf16* grp, const float* v, int h) {
+  bf16x4 lo, hi;
+  lo[0] = (__bf16)v[0]; lo[1] = (__bf16)v[1]; lo[2] = (__bf16)v[2]; lo[3] = (__bf16)v[3];
+  hi[0] = (__bf16)v[4]; hi[1] = (__bf16)v[5]; hi[2] = (__bf16)v[6]; hi[3] = (__bf16)v[7];
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 send = __builtin_bit_cast(u32x2, h ? lo : hi);
+  u32x2 recv;
+  recv[0] = __shfl_xor(send[0], 32, 64);
+  recv[1] = __shfl_xor(send[1], 32, 64);
+  if (h) lo = __builtin_bit_cast(bf16x4, recv);
+  else hi = __builtin_bit_cast(bf16x4, recv);
+  bf16x8 out;
+  out[0] = lo[0]; out[1] = lo[1]; out[2] = lo[2]; out[3] = lo[3];
+  out[4] = hi[0]; out[5] = hi[1]; out[6] = hi[2]; out[7] = hi[3];
+  if (grp != nullptr) *reinterpret_cast<bf16x8*>(grp + 8 * h) = out;
+}
+
 // 4 consecutive bf16 -> f32
 __device__ __forceinline__ void load4(const __bf16* base, float* v) {
   const bf16x4 x = *reinterpret_cast<const bf16x4*>(base);

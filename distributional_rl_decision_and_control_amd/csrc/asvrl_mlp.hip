@@ -174,11 +174,8 @@ __device__ __forceinline__ void actor_tile(const MlpArgs& a, const ActorLds& L, 
   encode_tile(L.enc, L.benc, bx, mk, lane, [&](int mb, int s, const float* v) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) fpk[mb * 2 + s][j] = (__bf16)v[j];
-    if (MODE == MLP_TRAIN && valid) {
-      __bf16* o = bp(io.h0) + static_cast<int64_t>(row) * kEnc + mb * 32 + 16 * s + 4 * h;
-      store4(o, v);
-      store4(o + 8, v + 4);
-    }
+    if (MODE == MLP_TRAIN)
+      store16(valid ? bp(io.h0) + static_cast<int64_t>(row) * kEnc + mb * 32 + 16 * s : nullptr, v, h);
   });
   // hidden_layer 256 -> 128, relu
   f32x16 acc1[4];
@@ -200,11 +197,8 @@ __device__ __forceinline__ void actor_tile(const MlpArgs& a, const ActorLds& L, 
         v[j] = relu(x);
         h1pk[mb * 2 + s][j] = (__bf16)v[j];
       }
-      if (MODE == MLP_TRAIN && valid) {
-        __bf16* o = bp(io.h1) + static_cast<int64_t>(row) * kHid + mb * 32 + 16 * s + 4 * h;
-        store4(o, v);
-        store4(o + 8, v + 4);
-      }
+      if (MODE == MLP_TRAIN)
+      store16(valid ? bp(io.h1) + static_cast<int64_t>(row) * kHid + mb * 32 + 16 * s : nullptr, v, h);
     }
   // hidden_layer_2 128 -> 128, relu; output_layer 128 -> 2
   f32x16 acc2[4];
@@ -228,11 +222,8 @@ __device__ __forceinline__ void actor_tile(const MlpArgs& a, const ActorLds& L, 
         p0 += L.wout[m] * v[j];
         p1 += L.wout[kHid + m] * v[j];
       }
-      if (MODE == MLP_TRAIN && valid) {
-        __bf16* o = bp(io.h2) + static_cast<int64_t>(row) * kHid + mb * 32 + 16 * s + 4 * h;
-        store4(o, v);
-        store4(o + 8, v + 4);
-      }
+      if (MODE == MLP_TRAIN)
+      store16(valid ? bp(io.h2) + static_cast<int64_t>(row) * kHid + mb * 32 + 16 * s : nullptr, v, h);
     }
   const float z0 = p0 + __shfl_xor(p0, 32, 64) + L.bout[0];
   const float z1 = p1 + __shfl_xor(p1, 32, 64) + L.bout[1];
@@ -344,10 +335,7 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_kernel(MlpArgs a) {
         dv[j] = hv[j] > 0.f ? L.wout[m] * d0 + L.wout[kHid + m] * d1 : 0.f;
         dz2pk[mb * 2 + s][j] = (__bf16)dv[j];
       }
-      if (valid) {
-        store4(bp(io.dz2) + row * kHid + mb * 32 + 16 * s + 4 * h, dv);
-        store4(bp(io.dz2) + row * kHid + mb * 32 + 16 * s + 4 * h + 8, dv + 4);
-      }
+      store16(valid ? bp(io.dz2) + row * kHid + mb * 32 + 16 * s : nullptr, dv, h);
     }
   // dh1 = W2^T dz2 -> dz1
   f32x16 acc3[4];
@@ -371,10 +359,7 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_kernel(MlpArgs a) {
         dv[j] = hv[j] > 0.f ? acc3[mb][8 * s + j] : 0.f;
         dz1pk[mb * 2 + s][j] = (__bf16)dv[j];
       }
-      if (valid) {
-        store4(bp(io.dz1) + row * kHid + mb * 32 + 16 * s + 4 * h, dv);
-        store4(bp(io.dz1) + row * kHid + mb * 32 + 16 * s + 4 * h + 8, dv + 4);
-      }
+      store16(valid ? bp(io.dz1) + row * kHid + mb * 32 + 16 * s : nullptr, dv, h);
     }
   // dh0 = W1^T dz1 -> dz0 (two halves of 4 blocks)
 #pragma unroll
@@ -397,10 +382,7 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_kernel(MlpArgs a) {
         load4(bp(io.h0) + off + 8, hv + 4);
 #pragma unroll
         for (int j = 0; j < 8; ++j) dv[j] = hv[j] > 0.f ? acc4[q][8 * s + j] : 0.f;
-        if (valid) {
-          store4(bp(io.dz0) + row * kEnc + mb * 32 + 16 * s + 4 * h, dv);
-          store4(bp(io.dz0) + row * kEnc + mb * 32 + 16 * s + 4 * h + 8, dv + 4);
-        }
+        store16(valid ? bp(io.dz0) + row * kEnc + mb * 32 + 16 * s : nullptr, dv, h);
       }
     }
   }

@@ -8,7 +8,7 @@ OUT="$ROOT/gpurun_out/pmc"
 mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
-ARGS="${BENCH_ARGS:---steps 4 --warmup 2 --no-cpu-baseline}"
+ARGS="${BENCH_ARGS:---steps 4 --warmup 2 --no-cpu-baseline --iqn-steps 0}"
 run() {
   local name="$1"; shift
   timeout -k 10 400 rocprofv3 --pmc "$@" --kernel-trace -d "$OUT/$name" -o run --output-format csv -- \

@@ -24,6 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--match", default="")
+    ap.add_argument("--json", default=None, help="also write {kernel: {counter: mean}} here")
     a = ap.parse_args()
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for p in ("sq", "fetch", "write"):
@@ -34,13 +35,19 @@ def main():
                 continue
             cn = r.get("Counter_Name", r.get("Counter-Name"))
             agg[name][cn].append(float(r.get("Counter_Value", r.get("Counter-Value"))))
+    summary = {}
     for name, cs in sorted(agg.items()):
         out = {k: sum(v) / len(v) for k, v in cs.items()}
         if "FETCH_SIZE" in out:
             out["FETCH_SIZE_x2"] = 2 * out["FETCH_SIZE"]
+        summary[re.sub(r"^(void )?asvrl::anon::", "", name)] = out
         print(name[:90])
         for k in sorted(out):
             print(f"    {k:28s} {out[k]:16.1f}  (n={len(cs[k]) if k in cs else len(cs['FETCH_SIZE'])})")
+    if a.json:
+        import json
+        json.dump({"source": "rocprofv3 --pmc, tools/pmc_run.sh (bench.py workload); sizes in KB per dispatch",
+                   **summary}, open(a.json, "w"), indent=1)
 
 
 if __name__ == "__main__":
