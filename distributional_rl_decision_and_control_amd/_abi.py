@@ -90,7 +90,8 @@ class AsvCriticIO(C.Structure):
     _fields_ = [("F", _VP), ("G", _VP), ("taus", _VP), ("B", _I32), ("N", _I32), ("Np", _I32), ("kappa", C.c_float),
                 ("q_targets", _VP), ("q_next", _VP), ("rewards", _VP), ("dones", _VP), ("ld_rd", _I64),
                 ("gamma", C.c_float), ("dq", C.c_float), ("q", _VP), ("row_loss", _VP), ("dF", _VP), ("dG", _VP),
-                ("dzF", _VP), ("dzG", _VP), ("w_ae", _VP), ("dA", _VP)]
+                ("dzF", _VP), ("dzG", _VP), ("w_ae", _VP), ("dA", _VP), ("tile_loss", _VP),
+                ("loss_scale", C.c_float)]
 
 
 MAX_SUM_SEGS = 8
@@ -132,7 +133,7 @@ EXPORTS = [
                                      _VP]),
     ("asvrl_critic_actor_grad", C.c_int, [C.POINTER(AsvCriticWeights), C.POINTER(AsvCriticIO), _VP]),
     ("asvrl_replay_push", C.c_int, [_VP, _VP, _VP, _VP, _I32, _VP, _VP, _I32, _VP, _I64, _VP, _VP, _VP]),
-    ("asvrl_replay_sample", C.c_int, [_VP, _I64, _VP, _VP, _I32, _U64, _U64, _VP, _VP, _VP, _VP]),
+    ("asvrl_replay_sample", C.c_int, [_VP, _I64, _VP, _VP, _I32, _U64, _U64, _VP, _I64, _VP, _VP, _VP]),
     ("asvrl_replay_write_rows", C.c_int, [_VP, _VP, _I32, _VP, _VP]),
     ("asvrl_adam_clip", C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, _F, _F, _VP, _VP, _VP]),
     ("asvrl_linear_wgrad_workspace", _I64, [_I32, _I32]),

@@ -57,7 +57,16 @@ struct CriticArgs {
   float* dzG;       // (B, 128): dG * 1[G > 0]
   const float* wae; // (128, 2) action_encoder.weight (ACTOR dA)
   float* dA;        // (B, 2)
+  float* tile_loss;  // [tiles] TRAIN: sum(row_loss) * loss_scale; ACTOR: sum(q) * loss_scale, per 32-row tile
+  float loss_scale;
 };
+
+// per-tile sum of one value per row (lane half 0 holds the rows), one store per tile
+__device__ __forceinline__ void tile_sum_store(float v, int lane, float scale, float* dst) {
+  v = (lane >> 5) == 0 ? v : 0.f;
+  v = seg_sum<32>(v);                       // lane 31: sum of lanes 0..31
+  if (lane == 31) *dst = v * scale;
+}
 
 // LDS-resident forward weights: fragment images of Wc, W1, W2 (128 KB) + bc, b1, b2, wo.
 constexpr int kFragWC = kC * kNcos / 8, kFragW1 = kH * kC / 8, kFragW2 = kH * kH / 8;
@@ -214,12 +223,14 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
       for (int j = 0; j < a.Np; ++j) term(a.qn != nullptr ? rb + (a.gamma * qt[j]) * nd : qt[j]);
     }
     dq = -wg * a.gscale;
+    if (a.tile_loss != nullptr) tile_sum_store(wl, lane, a.loss_scale, a.tile_loss + tile);
     if (h == 0) {
       a.row_loss[grow] = wl;
       a.acts.dq[grow] = dq;
     }
   } else {
     dq = a.dq_const;
+    if (a.tile_loss != nullptr) tile_sum_store(q, lane, a.loss_scale, a.tile_loss + tile);
   }
 
   // ---------------- dz2 = dq * wo * 1[z2 > 0]
@@ -558,6 +569,7 @@ CriticArgs make_args(const AsvCriticWeights* w, const AsvCriticIO* io) {
   a.qt = io->q_targets; a.qn = io->q_next; a.rew = io->rewards; a.don = io->dones; a.ld_rd = io->ld_rd;
   a.gamma = io->gamma; a.dq_const = io->dq; a.q = io->q; a.row_loss = io->row_loss; a.dF = io->dF; a.dG = io->dG;
   a.dzF = io->dzF; a.dzG = io->dzG; a.wae = io->w_ae; a.dA = io->dA;
+  a.tile_loss = io->tile_loss; a.loss_scale = io->loss_scale;
   return a;
 }
 

@@ -202,7 +202,8 @@ __global__ __launch_bounds__(4 * kWave) void replay_sample_kernel(const float* _
                                                                   const int64_t* __restrict__ indices, int B,
                                                                   uint64_t seed, uint64_t counter,
                                                                   const uint64_t* __restrict__ counter_dev,
-                                                                  float* __restrict__ out, int64_t* out_slots) {
+                                                                  int64_t guard, float* __restrict__ out,
+                                                                  int64_t* out_slots) {
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
@@ -217,7 +218,11 @@ __global__ __launch_bounds__(4 * kWave) void replay_sample_kernel(const float* _
                                   static_cast<uint32_t>(ctr)},
                                static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
     const uint64_t bits = (static_cast<uint64_t>(r.x) << 32) | r.y;
-    k = size > 0 ? static_cast<int64_t>(bits % static_cast<uint64_t>(size)) : 0;
+    // guard: skip the oldest entries a concurrent push of <= guard rows may overwrite
+    int64_t lo = size + guard - cap;
+    lo = lo > 0 ? lo : 0;
+    if (lo >= size) lo = 0;
+    k = size > 0 ? lo + static_cast<int64_t>(bits % static_cast<uint64_t>(size - lo)) : 0;
   }
   const int64_t slot = ((head - size + k) % cap + cap) % cap;  // deque index 0 = oldest
   if (lane == 0 && out_slots != nullptr) out_slots[b] = slot;
@@ -301,12 +306,13 @@ extern "C" int asvrl_replay_push(const float* obs_prev, const float* obs_next, c
 
 extern "C" int asvrl_replay_sample(const float* ring, int64_t capacity, const int64_t* ring_state,
                                    const int64_t* indices, int32_t B, uint64_t seed, uint64_t counter,
-                                   const uint64_t* counter_dev, float* out, int64_t* out_slots, void* stream) {
+                                   const uint64_t* counter_dev, int64_t guard, float* out, int64_t* out_slots,
+                                   void* stream) {
   ASVRL_REQUIRE(ring && ring_state && out, "asvrl_replay_sample: null argument");
   ASVRL_REQUIRE(capacity > 0, "asvrl_replay_sample: bad capacity");
   if (B <= 0) return 0;
   hipLaunchKernelGGL(replay_sample_kernel, dim3((B + 3) / 4), dim3(4 * kWave), 0, as_stream(stream), ring,
-                     capacity, ring_state, indices, B, seed, counter, counter_dev, out, out_slots);
+                     capacity, ring_state, indices, B, seed, counter, counter_dev, guard, out, out_slots);
   return check_launch("asvrl_replay_sample");
 }
 

@@ -57,30 +57,32 @@ __device__ __forceinline__ void load_rows(u32x4 (&r)[N], const __bf16* __restric
   for (int i = 0; i < N; ++i) r[i] = *reinterpret_cast<const u32x4*>(base + (row + i * STEP) * ld + c8 * 8);
 }
 
-template <int M, int K>
+template <int M, int K, int W = 4>
 struct Shape {
-  static constexpr int NMB = M / 32, NKB = K / 32, NB = NMB * NKB, NBW = NB / 4;
+  static constexpr int T = W * 64;                          // threads per workgroup
+  static constexpr int NMB = M / 32, NKB = K / 32, NB = NMB * NKB, NBW = NB / W;
   static constexpr bool kWide = NBW >= NKB;                // wave covers whole m-blocks
   static constexpr int NMW = kWide ? NBW / NKB : 1;        // m-blocks per wave
   static constexpr int NKW = kWide ? NKB : NBW;            // k-blocks per wave
   static constexpr int SZ = lds_stride(M), SX = lds_stride(K);
   static constexpr int NCZ = kRC * M / 8, NCX = kRC * K / 8;           // 16-B chunks per staged chunk
-  static constexpr int CZ = NCZ >= kWgThreads ? NCZ / kWgThreads : 1;    // per thread (dZ)
-  static constexpr int CX = NCX >= kWgThreads ? NCX / kWgThreads : 1;    // (X); < 256 chunks: some threads idle
-  static_assert(M % 32 == 0 && K % 32 == 0 && NB % 4 == 0, "block grid must split over 4 waves");
+  static constexpr int CZ = NCZ >= T ? NCZ / T : 1;    // per thread (dZ)
+  static constexpr int CX = NCX >= T ? NCX / T : 1;    // (X); fewer chunks than threads: some idle
+  static_assert(M % 32 == 0 && K % 32 == 0 && NB % W == 0 && NBW >= 1, "block grid must split over the waves");
   static_assert(kWide ? (NBW % NKB == 0) : (NKB % NBW == 0), "wave blocks must tile rows or columns");
-  static_assert(NCZ % kWgThreads == 0 || kWgThreads % NCZ == 0, "dZ chunks must tile the block");
-  static_assert(NCX % kWgThreads == 0 || kWgThreads % NCX == 0, "X chunks must tile the block");
+  static_assert(NCZ % T == 0 || T % NCZ == 0, "dZ chunks must tile the block");
+  static_assert(NCX % T == 0 || T % NCX == 0, "X chunks must tile the block");
 };
 
-template <int M, int K>
-__global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const __bf16* __restrict__ dz, int64_t ldz,
-                                                            const __bf16* __restrict__ x, int64_t ldx, int chunks,
-                                                            int chunks_per_group, float* __restrict__ partial) {
-  using S = Shape<M, K>;
+template <int M, int K, int W>
+__global__ __launch_bounds__(W * 64) void wgrad_kernel(const __bf16* __restrict__ dz, int64_t ldz,
+                                                        const __bf16* __restrict__ x, int64_t ldx, int chunks,
+                                                        int chunks_per_group, float* __restrict__ partial) {
+  using S = Shape<M, K, W>;
+  constexpr int kT = S::T;
   __shared__ __attribute__((aligned(16))) char lz[kRC * S::SZ];
   __shared__ __attribute__((aligned(16))) char lx[kRC * S::SX];
-  __shared__ float lbias[kWgThreads][8];
+  __shared__ float lbias[kT][8];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int c_beg = blockIdx.x * chunks_per_group;
   const int c_end = min(chunks, c_beg + chunks_per_group);
@@ -88,7 +90,7 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const __bf16* __restr
   // thread t always stages column chunk t % (M/8) (resp. K/8), rows t / (M/8) + i * (256*8/M)
   const int zc8 = t % (M / 8), zr = t / (M / 8);
   const int xc8 = t % (K / 8), xr = t / (K / 8);
-  constexpr int ZRS = kWgThreads * 8 / M, XRS = kWgThreads * 8 / K;   // row step between a thread's chunks
+  constexpr int ZRS = kT * 8 / M, XRS = kT * 8 / K;   // row step between a thread's chunks
   const bool zact = t < S::NCZ, xact = t < S::NCX;                     // staging threads
   u32x4 rz[S::CZ], rx[S::CX];
   float bacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -154,7 +156,7 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_kernel(const __bf16* __restr
   __syncthreads();
   if (t < M / 8) {
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int u = t; u < kWgThreads; u += M / 8)
+    for (int u = t; u < kT; u += M / 8)
 #pragma unroll
       for (int j = 0; j < 8; ++j) s[j] += lbias[u][j];
 #pragma unroll
@@ -234,6 +236,22 @@ struct SumSegs {
 __global__ __launch_bounds__(kWgThreads) void partial_sums_kernel(SumSegs t) {
   const AsvPartialSum& g = t.seg[blockIdx.y];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (g.nw + g.nb == 1) {   // scalar over many groups: the whole block, fixed order
+    if (blockIdx.x != 0) return;
+    float acc = 0.f;
+    for (int k = threadIdx.x; k < g.groups; k += kWgThreads) acc += g.partial[k];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, kWave);
+    __shared__ float wsum[kWgThreads / kWave];
+    if (lane == 0) wsum[wv] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float s = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+      float* o = g.nw == 1 ? g.dw : g.db;
+      *o = g.accumulate ? *o + s : s;
+    }
+    return;
+  }
   const int i = blockIdx.x * 64 + lane;
   const int n = g.nw + g.nb;
   if (blockIdx.x * 64 >= n) return;   // block-uniform
@@ -273,14 +291,14 @@ int vec_groups(int R) {
   return (R + per - 1) / per;
 }
 
-template <int M, int K>
+template <int M, int K, int W = (M * K >= 8192 ? 8 : 4)>
 int launch_wgrad(const __bf16* dz, int64_t ldz, const __bf16* x, int64_t ldx, int R, float* work, hipStream_t st,
                  int& groups) {
   // partial traffic is groups * M * K floats: capped near 16 MB for the large layers
   const int chunks = R / kRC;
   groups = wgrad_groups(R, M, K);
   const int per = (chunks + groups - 1) / groups;
-  hipLaunchKernelGGL((wgrad_kernel<M, K>), dim3(groups), dim3(kWgThreads), 0, st, dz, ldz, x, ldx, chunks, per,
+  hipLaunchKernelGGL((wgrad_kernel<M, K, W>), dim3(groups), dim3(W * 64), 0, st, dz, ldz, x, ldx, chunks, per,
                      work);
   return check_launch("asvrl_linear_wgrad");
 }

@@ -88,6 +88,7 @@ def _io(F, G, taus, N, **kw):
     io.B, io.N = F.shape[0], N
     io.Np, io.kappa, io.gamma, io.dq, io.ld_rd = kw.pop("Np", 0), kw.pop("kappa", 1.0), kw.pop("gamma", 0.0), \
         kw.pop("dq", 0.0), kw.pop("ld_rd", 1)
+    io.loss_scale = kw.pop("loss_scale", 0.0)
     for k, v in kw.items():
         setattr(io, k, v.data_ptr() if v is not None else None)
     return io
@@ -130,12 +131,15 @@ class TrainBuffers:
 
 
 def critic_train(pack, F, G, taus, q_targets, bufs, kappa=1.0, stream=None, q_next=None, rewards=None, dones=None,
-                 gamma=0.99, dzF=None, dzG=None, with_dFdG=True):
+                 gamma=0.99, dzF=None, dzG=None, with_dFdG=True, tile_loss=None):
     """TRAIN launch. Targets: q_targets (B, Np), or q_next (B, Np) with rewards/dones column
-    views (stride ld) combined in the kernel. Returns the loss as a 0-d device tensor."""
+    views (stride ld) combined in the kernel. With `tile_loss` ([B*N/32] f32) the kernel writes
+    per-tile loss partials (sum them, e.g. in a PartialArena) and None is returned; otherwise
+    the loss row_loss.sum() / (B*Np) as a 0-d device tensor."""
     B, N = F.shape[0], bufs.N
     Np = (q_targets if q_targets is not None else q_next).shape[1]
-    kw = dict(q=bufs.q, row_loss=bufs.row_loss, dzF=dzF, dzG=dzG)
+    kw = dict(q=bufs.q, row_loss=bufs.row_loss, dzF=dzF, dzG=dzG, tile_loss=tile_loss,
+              loss_scale=1.0 / float(B * Np))
     if with_dFdG:
         kw.update(dF=bufs.dF, dG=bufs.dG)
     if q_targets is not None:
@@ -145,13 +149,17 @@ def critic_train(pack, F, G, taus, q_targets, bufs, kappa=1.0, stream=None, q_ne
     io = _io(F, G, taus, N, Np=Np, kappa=float(kappa), **kw)
     _abi.check(_abi.lib().asvrl_critic_train(C.byref(pack.struct), C.byref(io), C.byref(bufs.struct),
                                              _abi.stream_ptr(stream)), "asvrl_critic_train")
+    if tile_loss is not None:
+        return None
     return bufs.row_loss.sum() / float(B * Np)
 
 
-def critic_actor_grad(pack, F, G, taus, N, q, dG=None, stream=None, w_ae=None, dA=None):
-    """ACTOR launch: dq = -1/(B*N) on every row; writes dG and/or dA (with w_ae)."""
+def critic_actor_grad(pack, F, G, taus, N, q, dG=None, stream=None, w_ae=None, dA=None, tile_loss=None):
+    """ACTOR launch: dq = -1/(B*N) on every row; writes dG and/or dA (with w_ae); with
+    `tile_loss` ([B*N/32]) per-tile partials of the actor loss -mean(q)."""
     B = F.shape[0]
-    io = _io(F, G, taus, N, dq=-1.0 / float(B * N), q=q, dG=dG, w_ae=w_ae, dA=dA)
+    io = _io(F, G, taus, N, dq=-1.0 / float(B * N), q=q, dG=dG, w_ae=w_ae, dA=dA, tile_loss=tile_loss,
+             loss_scale=-1.0 / float(B * N))
     _abi.check(_abi.lib().asvrl_critic_actor_grad(C.byref(pack.struct), C.byref(io), _abi.stream_ptr(stream)),
                "asvrl_critic_actor_grad")
 
@@ -220,6 +228,10 @@ class PartialArena:
                                                     _abi.ptr(part), part.numel(), C.byref(groups),
                                                     _abi.stream_ptr(stream)), "asvrl_linear_wgrad_vec_partial")
         self._seg(part, dw, db, groups.value, K, 1, accumulate)
+
+    def scalar(self, partials, out, accumulate=False):
+        """out (1 f32) (+)= sum(partials): a scalar segment (e.g. per-tile loss partials)."""
+        self._seg(partials, out, None, partials.numel(), 1, 0, accumulate)
 
     def small(self, dz, x, dw, db, accumulate=False, stream=None):
         R, M = dz.shape

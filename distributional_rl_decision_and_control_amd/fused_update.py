@@ -76,6 +76,8 @@ class FusedACIQNState:
         self.enc_dw2 = torch.empty(256, 32, **f)
         self.enc_db2 = torch.empty(256, **f)
         self.arena = PartialArena(16 << 20, dev)
+        self.losses = torch.zeros(2, **f)   # critic, actor loss (summed from per-tile partials)
+        self.tile_loss = torch.zeros(2, B * N // 32, **f)
 
     def target_changed(self):
         """Re-pack the target networks after a hard/soft update (eager, outside graphs)."""
@@ -88,8 +90,9 @@ class FusedACIQNState:
 
 
 def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, actor_grads, rows, gamma=0.99,
-                         taus=None, sync=None, max_norm=0.5):
+                         taus=None, sync=None, max_norm=0.5, actor_wait=None):
     """One AC-IQN update from replay rows [B][88]. taus: (3, B, N) or None (drawn here).
+    actor_wait: event to wait for before the actor's weights change (a concurrent act kernel).
     Returns (critic_loss, actor_loss, critic_grad_norm, actor_grad_norm) as device scalars."""
     B, N = st.B, st.N
     critic, actor = policy_local.critic, policy_local.actor
@@ -104,13 +107,14 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     mlp_encode(st.target_cenc, ns_rows, st.Ft, st.Gt, act=st.na)
     critic_forward(st.target_trunk, st.Ft, st.Gt, taus[0], N, q=st.q_next)
     mlp_encode(st.local_cenc, s_rows, st.F, st.G, act=a_rows, xb=st.xb)
-    critic_loss = critic_train(st.local_trunk, st.F, st.G, taus[1], None, bufs, q_next=st.q_next.view(B, N),
-                               rewards=r_col, dones=d_col, gamma=gamma, dzF=st.dzF, dzG=st.dzG, with_dFdG=False)
+    critic_train(st.local_trunk, st.F, st.G, taus[1], None, bufs, q_next=st.q_next.view(B, N), rewards=r_col,
+                 dones=d_col, gamma=gamma, dzF=st.dzF, dzG=st.dzG, with_dFdG=False, tile_loss=st.tile_loss[0])
     ae = critic.action_encoder[0]
     trunk_weight_grads_into(arena, critic, bufs)
     arena.linear(st.dzF, st.xb, st.enc_dw, st.enc_db)
     arena.small(st.dzG, a_rows, ae.weight.grad, ae.bias.grad)
-    arena.flush()                                   # one reduction launch for the six layers
+    arena.scalar(st.tile_loss[0], st.losses[0:1])   # the critic loss
+    arena.flush()                                   # one reduction launch for the six layers + loss
     encoder_fold(st.enc_dw, st.enc_db, critic)
     if sync is not None:
         sync(critic_grads)
@@ -121,8 +125,8 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     # ---- actor through the updated critic (agent.py:419-427)
     actor_train_forward(st.actor, s_rows, ab)
     mlp_encode(st.local_cenc, s_rows, st.F2, st.G2, act=ab.a_out)
-    critic_actor_grad(st.local_trunk, st.F2, st.G2, taus[2], N, st.q_pi, w_ae=ae.weight, dA=ab.dA)
-    actor_loss = -st.q_pi.mean()
+    critic_actor_grad(st.local_trunk, st.F2, st.G2, taus[2], N, st.q_pi, w_ae=ae.weight, dA=ab.dA,
+                      tile_loss=st.tile_loss[1])
     actor_backward(st.actor, ab)
     arena.linear(ab.dz1, ab.h0, actor.hidden_layer.weight.grad, actor.hidden_layer.bias.grad)
     arena.linear(ab.dz2, ab.h1, actor.hidden_layer_2.weight.grad, actor.hidden_layer_2.bias.grad)
@@ -130,10 +134,13 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     arena.vec(ab.dout[:, 0], ab.h2, ow[0], obias[0:1])
     arena.vec(ab.dout[:, 1], ab.h2, ow[1], obias[1:2])
     arena.linear(ab.dz0, ab.xb, st.enc_dw2, st.enc_db2)
+    arena.scalar(st.tile_loss[1], st.losses[1:2])   # the actor loss
     arena.flush()
     encoder_fold(st.enc_dw2, st.enc_db2, actor)
     if sync is not None:
         sync(actor_grads)
+    if actor_wait is not None:
+        torch.cuda.current_stream().wait_event(actor_wait)
     agn = clip_and_step(actor_opt, actor_grads, max_norm)
     st.actor.refresh()
-    return critic_loss.detach(), actor_loss.detach(), cgn, agn
+    return st.losses[0], st.losses[1], cgn, agn

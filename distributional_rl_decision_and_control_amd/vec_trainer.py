@@ -39,7 +39,7 @@ class VecTrainer:
                  learning_starts=None, target_update_interval=2500, total_timesteps=6_000_000,
                  exploration_fraction=0.25, initial_eps=0.6, final_eps=0.05, amp_dtype=torch.bfloat16, seed=0,
                  device="cuda", sync=None, graphs=False, schedule=None, net_seed=100, fused=True,
-                 fused_adam=True):
+                 fused_adam=True, overlap=True):
         self.device = torch.device(device)
         self.agent_type = agent_type
         self.continuous = agent_type == "AC-IQN"
@@ -106,6 +106,13 @@ class VecTrainer:
         self.graphs = graphs
         self._graph = None
         self._graph_learn = None
+        # rollout / learn on two streams (fused AC-IQN path): the learner samples against a
+        # snapshot of the ring state taken before this iteration's push, skipping the oldest
+        # E*R entries the push may overwrite, and waits for the act kernel before the actor
+        # weights change
+        self.overlap = bool(overlap)
+        self.ring_snap = torch.zeros(2, dtype=torch.int64, device=self.device)
+        self._streams = None
         self._gen = torch.Generator(device=self.device)
         self._gen.manual_seed(seed + 12345)
         self.env.reset()
@@ -154,11 +161,13 @@ class VecTrainer:
                          if self.action_dim == 1 else self.actions, env.batch.reward, env.batch.done)
         env.auto_reset()
 
-    def learn(self):
-        rows = self.replay.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter, out=self.batch_rows)
+    def learn(self, state=None, guard=0, actor_wait=None):
+        rows = self.replay.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter, out=self.batch_rows,
+                                  state=state, guard=guard)
         if self.agent_type == "AC-IQN" and self.fused2 is not None:
             out = ac_iqn_update_fused2(self.fused2, self.local, self.actor_opt, self.critic_opt, self.critic_grads,
-                                       self.actor_grads, rows, gamma=self.gamma, sync=self.sync)
+                                       self.actor_grads, rows, gamma=self.gamma, sync=self.sync,
+                                       actor_wait=actor_wait)
             self.learn_counter += 1
             return out
         s, a, r, ns, d = split_rows(rows)
@@ -193,9 +202,34 @@ class VecTrainer:
 
     # ------------------------------------------------------------------ iteration
     def _iteration_body(self, do_learn):
-        self.rollout()
-        out = self.learn() if do_learn else None
-        self.env.advance_device()
+        if not (do_learn and self.overlap and getattr(self, "fused2", None) is not None):
+            self.rollout()
+            out = self.learn() if do_learn else None
+            self.env.advance_device()
+            return out
+        main = torch.cuda.current_stream(self.device)
+        if self._streams is None:
+            self._streams = (torch.cuda.Stream(device=self.device), torch.cuda.Stream(device=self.device),
+                             torch.cuda.Event(), torch.cuda.Event())
+        s_roll, s_learn, ev_snap, ev_act = self._streams
+        s_roll.wait_stream(main)
+        s_learn.wait_stream(main)
+        with torch.cuda.stream(s_roll):
+            self.ring_snap.copy_(self.replay.state)
+            ev_snap.record(s_roll)
+            self.act()
+            ev_act.record(s_roll)
+            env = self.env
+            env.step(self.actions)
+            self.replay.push(env.obs_cur, env.obs_next, env.cnt_next, self.actions, env.batch.reward,
+                             env.batch.done)
+            env.auto_reset()
+            env.advance_device()
+        with torch.cuda.stream(s_learn):
+            s_learn.wait_event(ev_snap)
+            out = self.learn(state=self.ring_snap, guard=self.E * self.R, actor_wait=ev_act)
+        main.wait_stream(s_roll)
+        main.wait_stream(s_learn)
         return out
 
     def iteration(self, timing=None):

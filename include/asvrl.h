@@ -245,6 +245,11 @@ typedef struct AsvCriticIO {
   float* dzG;              /* TRAIN optional: [B][128] dG * 1[G > 0] (action-encoder pre-activation grad) */
   const float* w_ae;       /* ACTOR with dA: action_encoder.weight [128][2] */
   float* dA;               /* ACTOR optional: dL/d(action) [B][2] = W_ae^T (dG * 1[G > 0]) */
+  float* tile_loss;        /* optional [B*N/32]: per 32-row tile, TRAIN writes sum(row_loss) * loss_scale
+                              (the critic loss with loss_scale = 1/(B*Np)), ACTOR sum(q) * loss_scale
+                              (the actor loss with -1/(B*N)); sum them with asvrl_partial_sums
+                              (a segment with nw = 1, groups = tiles) */
+  float loss_scale;
 } AsvCriticIO;
 
 /* Critic.forward (AC_IQN_model.py:462-480): q [B*N]. */
@@ -273,11 +278,14 @@ int asvrl_replay_push(const float* obs_prev, const float* obs_next, const int8_t
 
 /* ReplayBuffer.sample (replay_buffer.py:26-45): gather B rows. With `indices` (host-chosen,
  * deque order: 0 = oldest) the rows are exactly those; with indices == NULL, B positions are
- * drawn uniformly (with replacement) by Philox(seed, counter + *counter_dev).
+ * drawn uniformly (with replacement) by Philox(seed, counter + *counter_dev), skipping the
+ * oldest entries that a push of up to `guard` rows running concurrently could overwrite
+ * (guard = 0: none). ring_state may be a snapshot {head, size} taken before that push.
  * out [B][ASVRL_TR_DIM]; out_slots optional [B]. */
 int asvrl_replay_sample(const float* ring, int64_t capacity, const int64_t* ring_state,
                         const int64_t* indices, int32_t B, uint64_t seed, uint64_t counter,
-                        const uint64_t* counter_dev, float* out, int64_t* out_slots, void* stream);
+                        const uint64_t* counter_dev, int64_t guard, float* out, int64_t* out_slots,
+                        void* stream);
 
 /* Host-side index copy helper for a ring with known (host) head/size: write rows given by
  * slot into the ring (used by the compat ReplayBuffer.add, one transition per call). */
@@ -329,7 +337,8 @@ int asvrl_linear_wgrad_vec_partial(const float* dq, int64_t ldq, const void* x, 
                                    void* stream);
 
 /* One pending reduction: dw[i] (+)= sum_g partial[g][i] for i < nw, db likewise for the
- * trailing nb values of each group's (nw + nb)-float partial (db optional). */
+ * trailing nb values of each group's (nw + nb)-float partial (db optional). A segment with
+ * nw + nb == 1 (a scalar over many groups) is reduced by a whole workgroup. */
 #define ASVRL_MAX_SUM_SEGS 8
 typedef struct AsvPartialSum {
   const float* partial;

@@ -106,3 +106,51 @@ def test_replay_push_and_sample():
     np.testing.assert_array_equal(s1, s2)
     hs = {r.tobytes() for r in host_rows}
     assert all(r.tobytes() in hs for r in s1)
+
+
+def test_replay_sample_guard_skips_entries_a_concurrent_push_overwrites():
+    """With the ring full, sample(guard=G) never returns the G oldest entries (those a push of
+    <= G rows overwrites), and stays uniform over the rest."""
+    from distributional_rl_decision_and_control_amd import learn_ops
+    from distributional_rl_decision_and_control_amd._abi import OBS_DIM
+    cap, n = 4096, 1024
+    ring = learn_ops.DeviceReplay(cap, device="cuda")
+    for it in range(5):   # 5120 pushes into 4096 slots: full, head wrapped
+        ids = torch.arange(it * n, (it + 1) * n, device="cuda", dtype=torch.float64)
+        z = torch.zeros(n, OBS_DIM, device="cuda")
+        ring.push(z, z, torch.zeros(n, dtype=torch.int8, device="cuda"), torch.zeros(n, 2, device="cuda",
+                  dtype=torch.float64), ids, torch.zeros(n, dtype=torch.uint8, device="cuda"))
+    assert ring.size() == cap
+    oldest = 5 * n - cap            # id of deque position 0
+    snap = ring.state.clone()
+    G = 1500
+    out = ring.sample(20000, seed=3, state=snap, guard=G)
+    got = out[:, 82].double().cpu().numpy()
+    assert got.min() >= oldest + G and got.max() <= 5 * n - 1
+    hist = np.bincount(((got - oldest - G) * 8 // (cap - G)).astype(int), minlength=8)
+    assert hist.min() > 0.8 * hist.mean()   # roughly uniform over the allowed window
+    out0 = ring.sample(20000, seed=3)
+    assert out0[:, 82].min().item() < oldest + G   # guard 0 reaches the oldest entries
+
+
+def test_vec_trainer_overlapped_streams_in_graph():
+    """VecTrainer with rollout and learn on two streams, captured in a HIP graph: finite losses,
+    weights move, replay fills, and the same run without overlap gives losses of the same scale."""
+    from distributional_rl_decision_and_control_amd.vec_trainer import VecTrainer
+    runs = {}
+    for overlap in (True, False):
+        tr = VecTrainer(n_envs=256, batch_size=512, num_tau=32, graphs=True, learning_starts=512, seed=3,
+                        overlap=overlap)
+        w0 = tr.local.actor.hidden_layer.weight.detach().clone()
+        losses = []
+        for _ in range(40):
+            out = tr.iteration()
+            if out is not None:
+                losses.append([float(x) for x in out[:2]])
+        torch.cuda.synchronize()
+        assert np.isfinite(np.array(losses)).all() and len(losses) > 20
+        assert not torch.equal(w0, tr.local.actor.hidden_layer.weight)
+        assert tr.replay.size() > 512
+        runs[overlap] = np.array(losses)
+    a, b = runs[True][-10:, 0].mean(), runs[False][-10:, 0].mean()
+    assert 0.2 < a / b < 5.0

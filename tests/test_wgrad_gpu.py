@@ -124,3 +124,23 @@ def test_partial_arena_is_bit_identical_to_per_layer_reduction():
         assert torch.equal(a, b)
     ref = dzs.double().t() @ xs.double()
     assert (wa.double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+
+
+def test_partial_arena_scalar_segment():
+    """A scalar segment (many groups, one output: the per-tile loss partials) is reduced by a
+    whole workgroup in a fixed order: equal to an f64 sum within f32 rounding, deterministic."""
+    from distributional_rl_decision_and_control_amd.fused_critic import PartialArena
+    arena = PartialArena(1 << 20, "cuda")
+    g = torch.Generator(device="cuda").manual_seed(4)
+    parts = torch.randn(4096, generator=g, device="cuda")
+    out1, out2 = torch.zeros(1, device="cuda"), torch.full((1,), 5.0, device="cuda")
+    arena.scalar(parts, out1)
+    arena.scalar(parts, out2, accumulate=True)
+    arena.flush()
+    again = torch.zeros(1, device="cuda")
+    arena.scalar(parts, again)
+    arena.flush()
+    ref = parts.double().sum().item()
+    assert abs(out1.item() - ref) <= 1e-5 * parts.abs().sum().item()
+    assert abs(out2.item() - (ref + 5.0)) <= 1e-5 * parts.abs().sum().item() + 1e-6
+    assert out1.item() == again.item()
