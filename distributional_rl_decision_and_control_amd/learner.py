@@ -51,6 +51,11 @@ class GradSync:
             return
         if self.avg_supported:
             dist.all_reduce(fg.flat, op=dist.ReduceOp.AVG, group=self.group)
+        elif fg.flat.is_cuda:
+            # gloo (CPU-side tests of the multi-rank GPU path): stage through host memory
+            host = fg.flat.cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=self.group)
+            fg.flat.copy_(host.div_(self.world))
         else:
             dist.all_reduce(fg.flat, op=dist.ReduceOp.SUM, group=self.group)
             fg.flat.div_(self.world)
