@@ -11,7 +11,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ASVRL_LIB", os.path.join(HERE, "lib", "libasvrl.so"))  # override: A/B variants
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
 OBS_DIM = 40   # self 7 | objects 25 | mask 5 | pad 3
@@ -94,6 +94,22 @@ class AsvCriticIO(C.Structure):
                 ("loss_scale", C.c_float)]
 
 
+IQN_MAX_ACTIONS = 32
+
+
+class AsvIqnHead(C.Structure):
+    _fields_ = [("wo_frag", _VP), ("wo", _VP), ("bo", _VP), ("n_actions", _I32)]
+
+
+class AsvIqnIO(C.Structure):
+    _fields_ = [("F", _VP), ("taus", _VP), ("B", _I32), ("N", _I32), ("Np", _I32), ("kappa", C.c_float),
+                ("q_next", _VP), ("actions", _VP), ("rewards", _VP), ("dones", _VP), ("ld_rd", _I64),
+                ("gamma", C.c_float), ("q", _VP), ("row_loss", _VP), ("dzF", _VP), ("dz_out", _VP),
+                ("tile_loss", _VP), ("loss_scale", C.c_float), ("act_out", _VP), ("ld_act", _I64),
+                ("step_dev", _VP), ("eps_steps_per_count", _D), ("eps_total", _D), ("eps_fraction", _D),
+                ("eps_initial", _D), ("eps_final", _D), ("seed", _U64)]
+
+
 MAX_SUM_SEGS = 8
 
 
@@ -132,6 +148,11 @@ EXPORTS = [
     ("asvrl_critic_train", C.c_int, [C.POINTER(AsvCriticWeights), C.POINTER(AsvCriticIO), C.POINTER(AsvCriticActs),
                                      _VP]),
     ("asvrl_critic_actor_grad", C.c_int, [C.POINTER(AsvCriticWeights), C.POINTER(AsvCriticIO), _VP]),
+    ("asvrl_iqn_pack", C.c_int, [_VP, _VP, _VP, _VP, C.POINTER(AsvCriticWeights), C.POINTER(AsvIqnHead), _VP]),
+    ("asvrl_iqn_forward_max", C.c_int, [C.POINTER(AsvCriticWeights), C.POINTER(AsvIqnHead), C.POINTER(AsvIqnIO), _VP]),
+    ("asvrl_iqn_train", C.c_int, [C.POINTER(AsvCriticWeights), C.POINTER(AsvIqnHead), C.POINTER(AsvIqnIO),
+                                  C.POINTER(AsvCriticActs), _VP]),
+    ("asvrl_iqn_act", C.c_int, [C.POINTER(AsvCriticWeights), C.POINTER(AsvIqnHead), C.POINTER(AsvIqnIO), _VP]),
     ("asvrl_replay_push", C.c_int, [_VP, _VP, _VP, _VP, _I32, _VP, _VP, _I32, _VP, _I64, _VP, _VP, _VP]),
     ("asvrl_replay_sample", C.c_int, [_VP, _I64, _VP, _VP, _I32, _U64, _U64, _VP, _I64, _VP, _VP, _VP]),
     ("asvrl_replay_write_rows", C.c_int, [_VP, _VP, _I32, _VP, _VP]),

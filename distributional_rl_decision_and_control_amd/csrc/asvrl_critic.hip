@@ -22,6 +22,15 @@
 //          and bf16 row-major activations for the weight gradients (dW = dZ^T X, a split-K
 //          GEMM on the host side)
 //   ACTOR  forward + backward of -mean(q) to the action features only (agent.py:420-425)
+//
+// The same trunk is IQN_Policy's (IQN_model.py:74-108) without the action encoder (h1g = h1)
+// and with an output layer 128 -> A (A <= 32 actions), run as one more MFMA block (the head
+// image is padded to 32 rows):
+//   IQN_MAX    target pass of train_IQN: q = max_a Q(row, a)                (agent.py:451-452)
+//   IQN_TRAIN  forward, gather at the taken action, quantile-Huber loss, backward
+//              (agent.py:455-468); the output layer's gradient leaves as a one-hot bf16
+//              [R][32] matrix so its weight gradient is one more 32 x 128 MFMA reduction
+//   IQN_ACT    act_iqn (agent.py:227-256): mean over K = 32 taus per state, argmax, epsilon-greedy
 #include "asvrl_common.h"
 #include "asvrl_mfma.h"
 
@@ -29,7 +38,15 @@ namespace asvrl {
 namespace {
 
 constexpr int kC = 256, kH = 128, kNcos = 64;
-enum { MODE_FWD = 0, MODE_TRAIN = 1, MODE_ACTOR = 2 };
+enum { MODE_FWD = 0, MODE_TRAIN = 1, MODE_ACTOR = 2, MODE_IQN_MAX = 3, MODE_IQN_TRAIN = 4, MODE_IQN_ACT = 5 };
+constexpr int kMaxA = ASVRL_IQN_MAX_ACTIONS;
+template <int MODE> constexpr bool kIqn = MODE >= MODE_IQN_MAX;
+template <int MODE> constexpr bool kTrainMode = MODE == MODE_TRAIN || MODE == MODE_IQN_TRAIN;
+// the Wc image sits in LDS for the forward-only modes; the backward modes keep W2^T there
+template <int MODE> constexpr bool kFwdOnly = MODE == MODE_FWD || MODE == MODE_IQN_MAX || MODE == MODE_IQN_ACT;
+#ifndef ASVRL_TRAIN_B_BPP32
+#define ASVRL_TRAIN_B_BPP32 2
+#endif
 #ifndef ASVRL_CRITIC_PERSISTENT
 #define ASVRL_CRITIC_PERSISTENT 0
 #endif
@@ -59,6 +76,15 @@ struct CriticArgs {
   float* dA;        // (B, 2)
   float* tile_loss;  // [tiles] TRAIN: sum(row_loss) * loss_scale; ACTOR: sum(q) * loss_scale, per 32-row tile
   float loss_scale;
+  // IQN
+  AsvIqnHead hd;
+  const float* act;  // IQN_TRAIN: action index of sample b at act[b * ld_rd]
+  void* dz_out;      // IQN_TRAIN: bf16 [R][32]
+  double* act_out;   // IQN_ACT
+  int64_t ld_act;
+  const int64_t* step_dev;
+  double eps_spc, eps_total, eps_fraction, eps_initial, eps_final;
+  uint64_t seed;
 };
 
 // per-tile sum of one value per row (lane half 0 holds the rows), one store per tile
@@ -80,15 +106,89 @@ struct CriticLds {
 };
 static_assert(kFragWC == kFragW2, "the Wc / W2^T slot holds either image");
 
-template <int MODE, int NT>
-__device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds& L, int tile, int lane) {
+// IQN head in LDS: the padded 32 x 128 output image, output_layer.weight in f32 for the
+// backward (dh2 = W_out[a] dq) and the bias
+struct CriticLdsIqn : CriticLds {
+  bf16x8 wo_img[kH / 16 * 64];
+  float wof[kMaxA * kH];
+  float bo_a[kMaxA];
+};
+template <int MODE> struct LdsOf { using T = CriticLds; };
+template <> struct LdsOf<MODE_IQN_MAX> { using T = CriticLdsIqn; };
+template <> struct LdsOf<MODE_IQN_TRAIN> { using T = CriticLdsIqn; };
+template <> struct LdsOf<MODE_IQN_ACT> { using T = CriticLdsIqn; };
+static_assert(sizeof(CriticLdsIqn) <= 160 * 1024, "IQN LDS image exceeds the CU's 160 KB");
+
+// output-layer weight feeding dh2[m]: the critic's single output row, or IQN's row of the taken action
+__device__ __forceinline__ float out_w(const CriticLds& L, int, int m) { return L.wo[m]; }
+__device__ __forceinline__ float out_w(const CriticLdsIqn& L, int ai, int m) { return L.wof[ai * kH + m]; }
+
+__device__ __forceinline__ uint64_t act_step(const CriticArgs& a) {
+  return a.step_dev != nullptr ? static_cast<uint64_t>(*a.step_dev) : 0ull;
+}
+
+// act_iqn's quantile fractions when the caller passes none: uniform [0, 1) per row (calc_cos's
+// torch.rand, IQN_model.py:63), Philox on (row, step)
+__device__ __forceinline__ float act_tau(const CriticArgs& a, int grow) {
+  const uint64_t step = act_step(a);
+  const U4 u = philox4x32_10(U4{static_cast<uint32_t>(grow), static_cast<uint32_t>(step),
+                                static_cast<uint32_t>(step >> 32), 0x1A7u},
+                             static_cast<uint32_t>(a.seed), static_cast<uint32_t>(a.seed >> 32));
+  return static_cast<float>(u.x >> 8) * (1.0f / 16777216.0f);
+}
+
+// act_iqn's selection (agent.py:240-250) for the state of this tile (its 32 rows = the K = 32
+// quantile samples): argmax_a of sum_n Q (= K * mean, same argmax; np.argmax's first maximum),
+// then greedy iff random() > eps, else a uniform action.
+__device__ __forceinline__ void iqn_act_select(const CriticArgs& a, const CriticLdsIqn& L, const f32x16& ao,
+                                               int tile, int lane) {
+  const int h = lane >> 5, A = a.hd.n_actions;
+  float best = -__builtin_inff();
+  int bi = kMaxA;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const int m = feat(0, g, h);
+    float v = m < A ? ao[g] + L.bo_a[m] : 0.f;
+    v = seg_sum<32>(v);   // lanes 31 / 63: the sum over the state's 32 taus
+    if (m < A && v > best) {
+      best = v;
+      bi = m;
+    }
+  }
+  const float ob = __shfl_xor(best, 32, 64);
+  const int oi = __shfl_xor(bi, 32, 64);
+  if (ob > best || (ob == best && oi < bi)) bi = oi;
+  if (lane != 31) return;
+  // epsilon: linear schedule of the device step counter (trainer.py:257-264)
+  const uint64_t step = act_step(a);
+  const double progress = static_cast<double>(step) * a.eps_spc / a.eps_total;
+  const double eps = progress < a.eps_fraction
+                         ? a.eps_initial + (progress / a.eps_fraction) * (a.eps_final - a.eps_initial)
+                         : a.eps_final;
+  const U4 u = philox4x32_10(U4{static_cast<uint32_t>(tile), static_cast<uint32_t>(step),
+                                static_cast<uint32_t>(step >> 32), 0x1A8u},
+                             static_cast<uint32_t>(a.seed), static_cast<uint32_t>(a.seed >> 32));
+  const double c = (static_cast<double>(u.x >> 8) + 1.0) * (1.0 / 16777216.0);   // random() in (0, 1]
+  int act = bi;
+  if (!(c > eps)) {   // random.choice(np.arange(action_size))
+    act = static_cast<int>((static_cast<uint64_t>(u.y >> 8) * static_cast<uint64_t>(A)) >> 24);
+  }
+  a.act_out[static_cast<int64_t>(tile) * a.ld_act] = static_cast<double>(act);
+}
+
+template <int MODE, int NT, class LT>
+__device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, int tile, int lane) {
+  constexpr bool IQN = kIqn<MODE>;
+  constexpr bool TRAINM = kTrainMode<MODE>;
   const int r = lane & 31, h = lane >> 5;
   const int grow = tile * 32 + r;
   const int b = grow / NT;
-  const float tau = a.taus[grow];
+  float tau;
+  if (MODE == MODE_IQN_ACT && a.taus == nullptr) tau = act_tau(a, grow);
+  else tau = a.taus[grow];
   const float* Fb = a.F + static_cast<size_t>(b) * kC;
-  const float* Gb = a.G + static_cast<size_t>(b) * kH;
-  const bf16x8* WC = MODE == MODE_FWD ? L.wc : reinterpret_cast<const bf16x8*>(a.w.wc_frag);
+  const float* Gb = IQN ? nullptr : a.G + static_cast<size_t>(b) * kH;
+  const bf16x8* WC = kFwdOnly<MODE> ? L.wc : reinterpret_cast<const bf16x8*>(a.w.wc_frag);
   const bf16x8* W1 = L.w1;
   const bf16x8* W2 = L.w2;
 
@@ -101,7 +201,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
       const int k = ks * 16 + 8 * h + j;
       cx[ks][j] = (__bf16)cos_pi_k_tau(tau, k);
     }
-    if (MODE == MODE_TRAIN)
+    if (TRAINM)
       *reinterpret_cast<bf16x8*>(bp(a.acts.cos) + static_cast<size_t>(grow) * kNcos + ks * 16 + 8 * h) = cx[ks];
   }
   bf16x8 cpk[16], hpk[16];
@@ -130,7 +230,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
           hv[j] = Fb[m] * x;
           hpk[mb * 2 + s][j] = (__bf16)hv[j];
         }
-        if (MODE == MODE_TRAIN)
+        if (TRAINM)
           store16(bp(a.acts.h0) + static_cast<size_t>(grow) * kC + mb * 32 + 16 * s, hv, h);
       }
     }
@@ -157,10 +257,10 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
         float x = acc1[mb][8 * s + j] + L.b1[m];
         x = relu(x);
         h1pk[mb * 2 + s][j] = (__bf16)x;
-        gv[j] = x * Gb[m];
+        gv[j] = IQN ? x : x * Gb[m];   // IQN: no action features
         gpk[mb * 2 + s][j] = (__bf16)gv[j];
       }
-      if (MODE == MODE_TRAIN)
+      if (TRAINM)
         store16(bp(a.acts.h1g) + static_cast<size_t>(grow) * kH + mb * 32 + 16 * s, gv, h);
     }
   }
@@ -174,24 +274,66 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
 #pragma unroll
     for (int mb = 0; mb < 4; ++mb) acc2[mb] = mfma(W2[(mb * 8 + ks) * 64 + lane], gpk[ks], acc2[mb]);
   }
-  float part = 0.f;
+  float q;
+  int ai = 0;   // IQN_TRAIN: the sample's action
+  if constexpr (IQN) {
+    // output layer 128 -> A as one 32-row MFMA block fed from h2 in registers
+    bf16x8 h2pk[8];
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb) {
+    for (int mb = 0; mb < 4; ++mb) {
 #pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const int m = feat(mb, g, h);
-      float x = acc2[mb][g] + L.b2[m];
-      acc2[mb][g] = x;  // keep z2 for the relu mask
-      part += L.wo[m] * relu(x);
+      for (int g = 0; g < 16; ++g) {
+        const float x = acc2[mb][g] + L.b2[feat(mb, g, h)];
+        acc2[mb][g] = x;  // keep z2 for the relu mask
+        h2pk[mb * 2 + (g >> 3)][g & 7] = (__bf16)relu(x);
+      }
     }
+    f32x16 ao = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < kH / 16; ++ks) ao = mfma(L.wo_img[ks * 64 + lane], h2pk[ks], ao);
+    const int A = a.hd.n_actions;   // register g of half h holds action feat(0, g, h)
+    if constexpr (MODE == MODE_IQN_ACT) {
+      iqn_act_select(a, L, ao, tile, lane);
+      return;
+    }
+    if constexpr (MODE == MODE_IQN_MAX) {
+      float mx = -__builtin_inff();
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int m = feat(0, g, h);
+        if (m < A) mx = fmaxf(mx, ao[g] + L.bo_a[m]);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if (h == 0) a.q[grow] = mx;
+      return;
+    }
+    ai = static_cast<int>(a.act[static_cast<int64_t>(b) * a.ld_rd]);
+    ai = ai < 0 ? 0 : (ai >= A ? A - 1 : ai);
+    float qs = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g)
+      if (feat(0, g, h) == ai) qs = ao[g] + L.bo_a[ai];
+    q = qs + __shfl_xor(qs, 32, 64);   // Q_expected.gather(2, actions) (agent.py:456)
+  } else {
+    float part = 0.f;
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int m = feat(mb, g, h);
+        float x = acc2[mb][g] + L.b2[m];
+        acc2[mb][g] = x;  // keep z2 for the relu mask
+        part += L.wo[m] * relu(x);
+      }
+    }
+    q = part + __shfl_xor(part, 32, 64) + a.w.bo[0];
   }
-  const float q = part + __shfl_xor(part, 32, 64) + a.w.bo[0];
   if (a.q != nullptr && h == 0) a.q[grow] = q;
   if (MODE == MODE_FWD) return;
 
   // ---------------- dL/dq
   float dq;
-  if (MODE == MODE_TRAIN) {
+  if (TRAINM) {
     const float* qt = a.qn != nullptr ? a.qn + static_cast<size_t>(b) * a.Np : a.qt + static_cast<size_t>(b) * a.Np;
     float rb = 0.f, nd = 0.f;
     if (a.qn != nullptr) {
@@ -225,8 +367,19 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
     dq = -wg * a.gscale;
     if (a.tile_loss != nullptr) tile_sum_store(wl, lane, a.loss_scale, a.tile_loss + tile);
     if (h == 0) {
-      a.row_loss[grow] = wl;
-      a.acts.dq[grow] = dq;
+      if (a.row_loss != nullptr) a.row_loss[grow] = wl;
+      if (a.acts.dq != nullptr) a.acts.dq[grow] = dq;
+    }
+    if constexpr (MODE == MODE_IQN_TRAIN) {   // dL/d(output pre-activation): dq at the taken action
+      bf16x8 o0, o1;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        o0[i] = (__bf16)(16 * h + i == ai ? dq : 0.f);
+        o1[i] = (__bf16)(16 * h + 8 + i == ai ? dq : 0.f);
+      }
+      __bf16* od = bp(a.dz_out) + static_cast<size_t>(grow) * kMaxA + 16 * h;
+      *reinterpret_cast<bf16x8*>(od) = o0;
+      *reinterpret_cast<bf16x8*>(od + 8) = o1;
     }
   } else {
     dq = a.dq_const;
@@ -245,10 +398,10 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
         const int m = feat(mb, 8 * s + j, h);
         const float z = acc2[mb][8 * s + j];
         hv[j] = relu(z);
-        dv[j] = z > 0.f ? dq * L.wo[m] : 0.f;
+        dv[j] = z > 0.f ? dq * out_w(L, ai, m) : 0.f;
         dz2pk[mb * 2 + s][j] = (__bf16)dv[j];
       }
-      if (MODE == MODE_TRAIN) {
+      if (TRAINM) {
         const size_t o = static_cast<size_t>(grow) * kH + mb * 32 + 16 * s;
         store16(bp(a.acts.h2) + o, hv, h);
         store16(bp(a.acts.dz2) + o, dv, h);
@@ -274,6 +427,12 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       float dv[8], gs[8];
+      if constexpr (IQN) {   // dz1 = dh1 * 1[h1 > 0]; no action features
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dv[j] = static_cast<float>(h1pk[mb * 2 + s][j]) > 0.f ? acc3[mb][8 * s + j] : 0.f;
+        store16(bp(a.acts.dz1) + static_cast<size_t>(grow) * kH + mb * 32 + 16 * s, dv, h);
+        continue;
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) gs[j] = acc3[mb][8 * s + j] * static_cast<float>(h1pk[mb * 2 + s][j]);
 #pragma unroll
@@ -303,7 +462,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const CriticLds
           *reinterpret_cast<float4*>(a.dzG + ob + 8) = make_float4(gz[4], gz[5], gz[6], gz[7]);
         }
       }
-      if (MODE == MODE_TRAIN)
+      if (TRAINM)
         store16(bp(a.acts.dz1) + static_cast<size_t>(grow) * kH + mb * 32 + 16 * s, dv, h);
     }
   }
@@ -356,26 +515,28 @@ __device__ __forceinline__ void critic_tile_b(const CriticArgs& a, const CriticL
   }
   const bool writer = (r % NT) == NT - 1;
   const bf16x8* W1T = L.w1t;
+  // NT = 32 (row_bcast segment sums) spills at 4 blocks per pass; 2 keeps it in registers
+  constexpr int BPP = ASVRL_TRAIN_B_BPP32 != 0 && NT == 32 ? ASVRL_TRAIN_B_BPP32 : 4;
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {  // 2 x 4 output blocks keeps 64 accumulator registers live
-    f32x16 acc0[4], acc4[4];
+  for (int half = 0; half < 8 / BPP; ++half) {  // BPP output blocks per pass: 2 * BPP accumulators live
+    f32x16 acc0[BPP], acc4[BPP];
 #pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) {
+    for (int q4 = 0; q4 < BPP; ++q4) {
       acc0[q4] = f32x16{};
       acc4[q4] = f32x16{};
     }
 #pragma unroll
     for (int ks = 0; ks < kNcos / 16; ++ks)
 #pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4) acc0[q4] = mfma(L.wc[((half * 4 + q4) * 4 + ks) * 64 + lane], cx[ks], acc0[q4]);
+      for (int q4 = 0; q4 < BPP; ++q4) acc0[q4] = mfma(L.wc[((half * BPP + q4) * 4 + ks) * 64 + lane], cx[ks], acc0[q4]);
 #pragma unroll
     for (int ks = 0; ks < kH / 16; ++ks)
 #pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4)
-        acc4[q4] = mfma(W1T[((half * 4 + q4) * 8 + ks) * 64 + lane], dz1pk[ks], acc4[q4]);
+      for (int q4 = 0; q4 < BPP; ++q4)
+        acc4[q4] = mfma(W1T[((half * BPP + q4) * 8 + ks) * 64 + lane], dz1pk[ks], acc4[q4]);
 #pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) {
-      const int mb = half * 4 + q4;
+    for (int q4 = 0; q4 < BPP; ++q4) {
+      const int mb = half * BPP + q4;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         float dv[8], fs[8], cv[8];
@@ -435,9 +596,9 @@ template <> struct CriticWaves<MODE_TRAIN> { static constexpr int n = 8; };
 template <int MODE, int NT>
 __global__ __launch_bounds__(CriticWaves<MODE>::n * 64) void critic_kernel(CriticArgs a) {
   constexpr int W = CriticWaves<MODE>::n;
-  __shared__ CriticLds L;
+  __shared__ typename LdsOf<MODE>::T L;
   {
-    const bf16x8* gwc = reinterpret_cast<const bf16x8*>(MODE == MODE_FWD ? a.w.wc_frag : a.w.w2t_frag);
+    const bf16x8* gwc = reinterpret_cast<const bf16x8*>(kFwdOnly<MODE> ? a.w.wc_frag : a.w.w2t_frag);
     const bf16x8* gw1 = reinterpret_cast<const bf16x8*>(a.w.w1_frag);
     const bf16x8* gw2 = reinterpret_cast<const bf16x8*>(a.w.w2_frag);
     for (int i = threadIdx.x; i < kFragWC; i += W * 64) L.wc[i] = gwc[i];
@@ -447,7 +608,15 @@ __global__ __launch_bounds__(CriticWaves<MODE>::n * 64) void critic_kernel(Criti
     for (int i = threadIdx.x; i < kH; i += W * 64) {
       L.b1[i] = a.w.b1[i];
       L.b2[i] = a.w.b2[i];
-      L.wo[i] = a.w.wo[i];
+      if (!kIqn<MODE>) L.wo[i] = a.w.wo[i];
+    }
+    if constexpr (kIqn<MODE>) {
+      const bf16x8* gwo = reinterpret_cast<const bf16x8*>(a.hd.wo_frag);
+      for (int i = threadIdx.x; i < kH / 16 * 64; i += W * 64) L.wo_img[i] = gwo[i];
+      const int A = a.hd.n_actions;
+      if (MODE == MODE_IQN_TRAIN)
+        for (int i = threadIdx.x; i < A * kH; i += W * 64) L.wof[i] = a.hd.wo[i];
+      for (int i = threadIdx.x; i < kMaxA; i += W * 64) L.bo_a[i] = i < A ? a.hd.bo[i] : 0.f;
     }
   }
   __syncthreads();
@@ -491,14 +660,21 @@ void launch_mode(const CriticArgs& a, hipStream_t st) {
 
 template <int NT>
 void launch_n(int mode, const CriticArgs& a, hipStream_t st) {
+  const int tiles = a.B * NT / 32;
   if (mode == MODE_FWD) {
     launch_mode<MODE_FWD, NT>(a, st);
   } else if (mode == MODE_TRAIN) {
     launch_mode<MODE_TRAIN, NT>(a, st);
-    const int tiles = a.B * NT / 32;
     hipLaunchKernelGGL((critic_train_b_kernel<NT>), dim3((tiles + 7) / 8), dim3(8 * 64), 0, st, a);
-  } else {
+  } else if (mode == MODE_ACTOR) {
     launch_mode<MODE_ACTOR, NT>(a, st);
+  } else if (mode == MODE_IQN_MAX) {
+    launch_mode<MODE_IQN_MAX, NT>(a, st);
+  } else if (mode == MODE_IQN_TRAIN) {   // part B (layer 4 + dF) is the critic's
+    launch_mode<MODE_IQN_TRAIN, NT>(a, st);
+    hipLaunchKernelGGL((critic_train_b_kernel<NT>), dim3((tiles + 7) / 8), dim3(8 * 64), 0, st, a);
+  } else if constexpr (NT == 32) {
+    launch_mode<MODE_IQN_ACT, 32>(a, st);
   }
 }
 
@@ -519,11 +695,20 @@ constexpr int kPackWc = 256 * 64, kPackW1 = 128 * 256, kPackW2 = 128 * 128;
 constexpr int kPackTotal = kPackWc + 2 * kPackW1 + 2 * kPackW2;
 
 
+constexpr int kPackHead = kMaxA * kH;
+
 __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ wc, const float* __restrict__ w1,
-                                                   const float* __restrict__ w2, AsvCriticWeights w) {
+                                                   const float* __restrict__ w2, AsvCriticWeights w,
+                                                   const float* __restrict__ wout, int n_actions, void* wo_frag) {
   int o = blockIdx.x * 256 + threadIdx.x;
-  if (o >= kPackTotal) return;
   int row, col;
+  if (o >= kPackTotal) {                                // IQN output_layer.weight (A x 128), zero rows to 32
+    o -= kPackTotal;
+    if (wo_frag == nullptr || o >= kPackHead) return;
+    frag_rc(o, kH, true, row, col);
+    static_cast<__bf16*>(wo_frag)[o] = (__bf16)(row < n_actions ? wout[row * kH + col] : 0.f);
+    return;
+  }
   if (o < kPackWc) {                                    // cos_embedding.weight (256 x 64)
     frag_rc(o, 64, false, row, col);
     const_cast<__bf16*>(static_cast<const __bf16*>(w.wc_frag))[o] = (__bf16)wc[row * 64 + col];
@@ -614,6 +799,81 @@ extern "C" int asvrl_critic_pack(const float* wc, const float* w1, const float* 
   ASVRL_REQUIRE(wc && w1 && w2 && w, "asvrl_critic_pack: null argument");
   ASVRL_REQUIRE(w->wc_frag && w->w1_frag && w->w2_frag && w->w2t_frag && w->w1t_frag,
                 "asvrl_critic_pack: null fragment buffer");
-  hipLaunchKernelGGL(pack_kernel, dim3((kPackTotal + 255) / 256), dim3(256), 0, as_stream(stream), wc, w1, w2, *w);
+  hipLaunchKernelGGL(pack_kernel, dim3((kPackTotal + 255) / 256), dim3(256), 0, as_stream(stream), wc, w1, w2, *w,
+                     static_cast<const float*>(nullptr), 0, static_cast<void*>(nullptr));
   return check_launch("asvrl_critic_pack");
+}
+
+// ------------------------------------------------------------------ IQN
+
+extern "C" int asvrl_iqn_pack(const float* wc, const float* w1, const float* w2, const float* wout,
+                              const AsvCriticWeights* w, const AsvIqnHead* head, void* stream) {
+  ASVRL_REQUIRE(wc && w1 && w2 && wout && w && head && head->wo_frag, "asvrl_iqn_pack: null argument");
+  ASVRL_REQUIRE(w->wc_frag && w->w1_frag && w->w2_frag && w->w2t_frag && w->w1t_frag,
+                "asvrl_iqn_pack: null fragment buffer");
+  ASVRL_REQUIRE(head->n_actions >= 1 && head->n_actions <= kMaxA, "asvrl_iqn_pack: 1 <= n_actions <= 32");
+  const int total = kPackTotal + kPackHead;
+  hipLaunchKernelGGL(pack_kernel, dim3((total + 255) / 256), dim3(256), 0, as_stream(stream), wc, w1, w2, *w, wout,
+                     head->n_actions, const_cast<void*>(head->wo_frag));
+  return check_launch("asvrl_iqn_pack");
+}
+
+namespace {
+
+int iqn_validate(const AsvCriticWeights* w, const AsvIqnHead* hd, const AsvIqnIO* io) {
+  ASVRL_REQUIRE(w && hd && io && io->F, "asvrl_iqn: null argument");
+  ASVRL_REQUIRE(w->wc_frag && w->w1_frag && w->w2_frag && w->bc && w->b1 && w->b2, "asvrl_iqn: null weight");
+  ASVRL_REQUIRE(hd->wo_frag && hd->bo && hd->n_actions >= 1 && hd->n_actions <= kMaxA, "asvrl_iqn: bad head");
+  ASVRL_REQUIRE(io->N == 8 || io->N == 16 || io->N == 32, "asvrl_iqn: N must be 8, 16 or 32");
+  ASVRL_REQUIRE(io->B >= 0 && (static_cast<int64_t>(io->B) * io->N) % 32 == 0, "asvrl_iqn: B*N must be a multiple of 32");
+  return 0;
+}
+
+CriticArgs iqn_args(const AsvCriticWeights* w, const AsvIqnHead* hd, const AsvIqnIO* io) {
+  CriticArgs a{};
+  a.w = *w;
+  a.hd = *hd;
+  a.F = io->F; a.taus = io->taus; a.B = io->B; a.N = io->N; a.Np = io->Np; a.kappa = io->kappa;
+  a.qn = io->q_next; a.act = io->actions; a.rew = io->rewards; a.don = io->dones; a.ld_rd = io->ld_rd;
+  a.gamma = io->gamma; a.q = io->q; a.row_loss = io->row_loss; a.dzF = io->dzF; a.dz_out = io->dz_out;
+  a.tile_loss = io->tile_loss; a.loss_scale = io->loss_scale;
+  a.act_out = io->act_out; a.ld_act = io->ld_act; a.step_dev = io->step_dev;
+  a.eps_spc = io->eps_steps_per_count; a.eps_total = io->eps_total; a.eps_fraction = io->eps_fraction;
+  a.eps_initial = io->eps_initial; a.eps_final = io->eps_final; a.seed = io->seed;
+  return a;
+}
+
+}  // namespace
+
+extern "C" int asvrl_iqn_forward_max(const AsvCriticWeights* w, const AsvIqnHead* head, const AsvIqnIO* io,
+                                     void* stream) {
+  if (int rc = iqn_validate(w, head, io)) return rc;
+  ASVRL_REQUIRE(io->taus && io->q, "asvrl_iqn_forward_max: needs taus and q");
+  if (io->B == 0) return 0;
+  return launch(MODE_IQN_MAX, iqn_args(w, head, io), stream);
+}
+
+extern "C" int asvrl_iqn_train(const AsvCriticWeights* w, const AsvIqnHead* head, const AsvIqnIO* io,
+                               const AsvCriticActs* acts, void* stream) {
+  if (int rc = iqn_validate(w, head, io)) return rc;
+  ASVRL_REQUIRE(io->taus && head->wo && w->w2t_frag && w->w1t_frag && acts, "asvrl_iqn_train: null argument");
+  ASVRL_REQUIRE(io->q_next && io->actions && io->rewards && io->dones && io->dz_out,
+                "asvrl_iqn_train: needs q_next, actions, rewards, dones and dz_out");
+  ASVRL_REQUIRE(acts->cos && acts->h0 && acts->dzc && acts->h1g && acts->dz1 && acts->h2 && acts->dz2,
+                "asvrl_iqn_train: null activation buffer");
+  ASVRL_REQUIRE(io->Np >= 1 && io->kappa > 0.f, "asvrl_iqn_train: bad Np/kappa");
+  if (io->B == 0) return 0;
+  CriticArgs a = iqn_args(w, head, io);
+  a.gscale = 1.f / (static_cast<float>(io->B) * static_cast<float>(io->Np));
+  a.acts = *acts;
+  return launch(MODE_IQN_TRAIN, a, stream);
+}
+
+extern "C" int asvrl_iqn_act(const AsvCriticWeights* w, const AsvIqnHead* head, const AsvIqnIO* io, void* stream) {
+  if (int rc = iqn_validate(w, head, io)) return rc;
+  ASVRL_REQUIRE(io->N == 32, "asvrl_iqn_act: K = 32 quantile samples per state");
+  ASVRL_REQUIRE(io->act_out && io->ld_act >= 1 && io->eps_total > 0.0 && io->eps_fraction > 0.0,
+                "asvrl_iqn_act: needs act_out, ld_act and the epsilon schedule");
+  if (io->B == 0) return 0;
+  return launch(MODE_IQN_ACT, iqn_args(w, head, io), stream);
 }

@@ -346,6 +346,7 @@ extern "C" int asvrl_linear_wgrad_partial(const void* dz, int64_t ldz, const voi
   else if (M == 128 && K == 128) rc = launch_wgrad<128, 128>(z, ldz, xx, ldx, R, partial, st, groups);
   else if (M == 64 && K == 64) rc = launch_wgrad<64, 64>(z, ldz, xx, ldx, R, partial, st, groups);
   else if (M == 256 && K == 32) rc = launch_wgrad<256, 32>(z, ldz, xx, ldx, R, partial, st, groups);
+  else if (M == 32 && K == 128) rc = launch_wgrad<32, 128>(z, ldz, xx, ldx, R, partial, st, groups);
   else ASVRL_REQUIRE(false, "asvrl_linear_wgrad: unsupported (M, K)");
   *groups_out = groups;
   return rc;

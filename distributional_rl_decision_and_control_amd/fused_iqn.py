@@ -1,0 +1,188 @@
+"""The IQN update (Agent.train_IQN, agent.py:434-476) and act_iqn (agent.py:227-256) on the
+gfx950 kernels of csrc/asvrl_critic.hip, csrc/asvrl_mlp.hip and csrc/asvrl_wgrad.hip.
+
+IQN_Policy (IQN_model.py:74-108) is the AC-IQN critic trunk without the action encoder and
+with a 128 -> 25 output layer, so it runs on the critic kernels' IQN modes. Per step, on a
+replay batch `rows` ([B][88]: obs | next obs | action | reward | done):
+
+    target encoders(ns) -> Ft                             asvrl_mlp_encode
+    target trunk, max over actions per tau -> q_next      asvrl_iqn_forward_max    (agent.py:451-452)
+    local encoders(s) -> F (+ bf16 obs copy)              asvrl_mlp_encode
+    forward, gather at a, quantile-Huber vs r + g q_next (1-d), backward
+                                                          asvrl_iqn_train (2 launches, agent.py:455-468)
+    weight grads of the 4 trunk layers + encoders         asvrl_linear_wgrad_partial x5,
+                                                          ONE asvrl_partial_sums (+ the loss), fold
+    [RCCL all-reduce] clip + Adam                         asvrl_adam_clip          (agent.py:471-472)
+    re-pack trunk, head and encoders                      asvrl_iqn_pack + asvrl_mlp_pack
+
+act_iqn for every robot row: encoders, then one kernel (K = 32 quantile samples per state,
+mean over them, argmax, epsilon-greedy on the device step counter).
+
+Arithmetic: bf16 MFMA operands with f32 accumulation, f32 master weights / Adam.
+"""
+import ctypes as C
+
+import torch
+
+from . import _abi
+from .fused_critic import CriticPack, PartialArena, TrainBuffers
+from .fused_mlp import MlpPack, encoder_fold, mlp_encode
+from .learner import clip_and_step
+
+OBS = 40
+K_ACT = 32
+
+
+def supported(net, B, N):
+    return (net.concat_feature_dimension == 256 and net.hidden_dimension == 128 and net.n == 64
+            and 1 <= net.action_size <= _abi.IQN_MAX_ACTIONS and N in (8, 16, 32) and (B * N) % 32 == 0
+            and net.self_dimension == 7 and net.object_dimension == 5 and net.max_object_num == 5
+            and net.self_feature_dimension == 56 and net.object_feature_dimension == 40)
+
+
+class IqnPack(CriticPack):
+    """bf16 images of one IQN_Policy: the trunk (CriticPack's five), the padded output head and
+    the observation encoders; refresh() is two launches."""
+
+    def __init__(self, net):
+        dev = net.cos_embedding.weight.device
+        self.head_img = torch.zeros(_abi.IQN_MAX_ACTIONS * 128, dtype=torch.bfloat16, device=dev)
+        hd = _abi.AsvIqnHead()
+        hd.wo_frag, hd.wo, hd.bo = (self.head_img.data_ptr(), net.output_layer.weight.data_ptr(),
+                                    net.output_layer.bias.data_ptr())
+        hd.n_actions = net.action_size
+        self.head = hd
+        self.enc = MlpPack(net, "encoders")
+        super().__init__(net)
+
+    def refresh(self, stream=None):
+        n = self.critic
+        rc = _abi.lib().asvrl_iqn_pack(_abi.ptr(n.cos_embedding.weight), _abi.ptr(n.hidden_layer.weight),
+                                       _abi.ptr(n.hidden_layer_2.weight), _abi.ptr(n.output_layer.weight),
+                                       C.byref(self.struct), C.byref(self.head), _abi.stream_ptr(stream))
+        _abi.check(rc, "asvrl_iqn_pack")
+        self.enc.refresh(stream)
+
+
+def _io(F, N, **kw):
+    io = _abi.AsvIqnIO()
+    io.F, io.B, io.N = F.data_ptr(), F.shape[0], N
+    for k in ("Np", "kappa", "gamma", "ld_rd", "loss_scale", "ld_act", "eps_steps_per_count", "eps_total",
+              "eps_fraction", "eps_initial", "eps_final", "seed"):
+        if k in kw:
+            setattr(io, k, kw.pop(k))
+    for k, v in kw.items():
+        setattr(io, k, v.data_ptr() if v is not None else None)
+    return io
+
+
+def iqn_forward_max(pack, F, taus, N, q, stream=None):
+    """q[b*N + n] = max_a Q(s_b, tau_bn, a) (the target of train_IQN)."""
+    io = _io(F, N, taus=taus, q=q)
+    _abi.check(_abi.lib().asvrl_iqn_forward_max(C.byref(pack.struct), C.byref(pack.head), C.byref(io),
+                                                _abi.stream_ptr(stream)), "asvrl_iqn_forward_max")
+    return q
+
+
+def iqn_train(pack, F, taus, bufs, dz_out, q_next, actions, rewards, dones, gamma, dzF, tile_loss=None, kappa=1.0,
+              q=None, stream=None):
+    """Forward + loss + backward of the local net. actions / rewards / dones are column views of
+    the replay rows (one stride). Writes bufs' activations, dz_out, dzF and, with tile_loss,
+    the per-tile loss partials (loss = their sum)."""
+    B, N = F.shape[0], bufs.N
+    Np = q_next.shape[1]
+    assert actions.stride(0) == rewards.stride(0) == dones.stride(0)
+    io = _io(F, N, taus=taus, Np=Np, kappa=float(kappa), q_next=q_next, actions=actions, rewards=rewards,
+             dones=dones, ld_rd=rewards.stride(0), gamma=float(gamma), q=q, row_loss=bufs.row_loss, dzF=dzF,
+             dz_out=dz_out, tile_loss=tile_loss, loss_scale=1.0 / float(B * Np))
+    _abi.check(_abi.lib().asvrl_iqn_train(C.byref(pack.struct), C.byref(pack.head), C.byref(io),
+                                          C.byref(bufs.struct), _abi.stream_ptr(stream)), "asvrl_iqn_train")
+
+
+def iqn_act(pack, F, actions64, step_dev, steps_per_count, total, fraction, initial, final, seed, taus=None,
+            stream=None):
+    """act_iqn for every row of F into actions64[:, 0] (f64 action index)."""
+    io = _io(F, K_ACT, taus=taus, act_out=actions64, ld_act=actions64.stride(0), step_dev=step_dev,
+             eps_steps_per_count=float(steps_per_count), eps_total=float(total), eps_fraction=float(fraction),
+             eps_initial=float(initial), eps_final=float(final), seed=int(seed) & 0xFFFFFFFFFFFFFFFF)
+    _abi.check(_abi.lib().asvrl_iqn_act(C.byref(pack.struct), C.byref(pack.head), C.byref(io),
+                                        _abi.stream_ptr(stream)), "asvrl_iqn_act")
+
+
+class FusedIQNState:
+    """Packs and buffers of the fused IQN update (allocated once, pointer-stable for graphs)."""
+
+    def __init__(self, net_local, net_target, B, N):
+        dev = net_local.cos_embedding.weight.device
+        self.B, self.N, self.device = B, N, dev
+        self.A = net_local.action_size
+        self.local = IqnPack(net_local)
+        self.target = IqnPack(net_target)
+        self.bufs = TrainBuffers(B, N, dev)
+        f = dict(dtype=torch.float32, device=dev)
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        self.F, self.Ft = torch.empty(B, 256, **f), torch.empty(B, 256, **f)
+        self.xb = torch.empty(B, 32, **bf)
+        self.q_next = torch.empty(B * N, **f)
+        self.dzF = torch.empty(B, 256, **bf)
+        self.dz_out = torch.empty(B * N, _abi.IQN_MAX_ACTIONS, **bf)
+        self.enc_dw, self.enc_db = torch.empty(256, 32, **f), torch.empty(256, **f)
+        self.out_dw = torch.empty(_abi.IQN_MAX_ACTIONS, 128, **f)
+        self.out_db = torch.empty(_abi.IQN_MAX_ACTIONS, **f)
+        self.arena = PartialArena(16 << 20, dev)
+        self.loss = torch.zeros(1, **f)
+        self.tile_loss = torch.zeros(B * N // 32, **f)
+        self.F_act = None
+
+    def target_changed(self):
+        """Re-pack the target network after a hard/soft update (eager, outside graphs)."""
+        self.target.refresh()
+
+    def act(self, obs_rows, actions64, step_dev, steps_per_count, total, fraction, initial, final, seed):
+        n = obs_rows.shape[0]
+        if self.F_act is None or self.F_act.shape[0] != n:
+            self.F_act = torch.empty(n, 256, dtype=torch.float32, device=self.device)
+        mlp_encode(self.local.enc, obs_rows, self.F_act)
+        iqn_act(self.local, self.F_act, actions64, step_dev, steps_per_count, total, fraction, initial, final, seed)
+
+
+def iqn_grads(st, net, rows, taus, gamma=0.99):
+    """Loss (st.loss) and every parameter .grad of train_IQN's backward (agent.py:449-468) for
+    replay rows [B][88] and taus (2, B, N) = (target, local)."""
+    B, N = st.B, st.N
+    s_rows, ns_rows = rows[:, 0:OBS], rows[:, OBS:2 * OBS]
+    a_col, r_col, d_col = rows[:, 80], rows[:, 82], rows[:, 83]
+    bufs, arena = st.bufs, st.arena
+    # every .grad is overwritten below (no zeroing)
+    mlp_encode(st.target.enc, ns_rows, st.Ft)
+    iqn_forward_max(st.target, st.Ft, taus[0], N, st.q_next)
+    mlp_encode(st.local.enc, s_rows, st.F, xb=st.xb)
+    iqn_train(st.local, st.F, taus[1], bufs, st.dz_out, st.q_next.view(B, N), a_col, r_col, d_col, gamma, st.dzF,
+              tile_loss=st.tile_loss)
+    arena.linear(bufs.dzc, bufs.cos, net.cos_embedding.weight.grad, net.cos_embedding.bias.grad)
+    arena.linear(bufs.dz1, bufs.h0, net.hidden_layer.weight.grad, net.hidden_layer.bias.grad)
+    arena.linear(bufs.dz2, bufs.h1g, net.hidden_layer_2.weight.grad, net.hidden_layer_2.bias.grad)
+    arena.linear(st.dz_out, bufs.h2, st.out_dw, st.out_db)
+    arena.linear(st.dzF, st.xb, st.enc_dw, st.enc_db)
+    arena.scalar(st.tile_loss, st.loss)
+    arena.flush()
+    encoder_fold(st.enc_dw, st.enc_db, net)
+    A = st.A
+    net.output_layer.weight.grad.copy_(st.out_dw[:A])
+    net.output_layer.bias.grad.copy_(st.out_db[:A])
+
+
+def iqn_update_fused(st, net, opt, grads, rows, gamma=0.99, taus=None, sync=None, max_norm=0.5, act_wait=None):
+    """One IQN update from replay rows [B][88]; taus: (2, B, N) (target, local) or None (drawn).
+    act_wait: event to wait for before the weights change (a concurrent act kernel).
+    Returns (loss, grad_norm) as device scalars."""
+    if taus is None:
+        taus = torch.rand(2, st.B, st.N, device=st.device)
+    iqn_grads(st, net, rows, taus, gamma)
+    if sync is not None:
+        sync(grads)
+    if act_wait is not None:
+        torch.cuda.current_stream().wait_event(act_wait)
+    gn = clip_and_step(opt, grads, max_norm)
+    st.local.refresh()
+    return st.loss[0], gn

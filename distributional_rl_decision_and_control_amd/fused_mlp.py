@@ -24,10 +24,11 @@ def _p(t):
 
 
 class MlpPack:
-    """Packed images of an Actor (kind='actor') or of a Critic's encoders (kind='critic')."""
+    """Packed images of an Actor (kind='actor'), of a Critic's encoders + action encoder
+    (kind='critic') or of the observation encoders alone (kind='encoders', IQN_Policy)."""
 
     def __init__(self, net, kind):
-        assert kind in ("actor", "critic")
+        assert kind in ("actor", "critic", "encoders")
         self.net, self.kind = net, kind
         dev = net.self_encoder[0].weight.device
         bf = dict(dtype=torch.bfloat16, device=dev)
@@ -45,7 +46,7 @@ class MlpPack:
             w.b1, w.b2 = net.hidden_layer.bias.data_ptr(), net.hidden_layer_2.bias.data_ptr()
             w.wout, w.bout = net.output_layer.weight.data_ptr(), net.output_layer.bias.data_ptr()
             w.out_scale = float(net.atan_scale.float().item())
-        else:
+        elif kind == "critic":
             self.ae = torch.zeros(HID * 16, **bf)
             w.ae_frag = self.ae.data_ptr()
             w.b_ae = net.action_encoder[0].bias.data_ptr()
@@ -59,7 +60,7 @@ class MlpPack:
         s.obj_w, s.obj_b = n.object_encoder[0].weight.data_ptr(), n.object_encoder[0].bias.data_ptr()
         if self.kind == "actor":
             s.w1, s.w2 = n.hidden_layer.weight.data_ptr(), n.hidden_layer_2.weight.data_ptr()
-        else:
+        elif self.kind == "critic":
             s.ae_w = n.action_encoder[0].weight.data_ptr()
         return s
 

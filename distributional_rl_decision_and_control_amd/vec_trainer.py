@@ -22,6 +22,8 @@ import torch
 
 from .fused_critic import FusedACIQN, ac_iqn_update_fused, fused_supported
 from .fused_update import FusedACIQNState, ac_iqn_update_fused2
+from .fused_iqn import FusedIQNState, iqn_update_fused
+from .fused_iqn import supported as fused_iqn_supported
 from .fused_update import supported as fused2_supported
 from .learn_ops import DeviceReplay, split_rows
 from .learner import FlatGrads, FusedAdam, GradSync, ac_iqn_update, iqn_update
@@ -55,6 +57,7 @@ class VecTrainer:
         self.exploration_fraction, self.initial_eps, self.final_eps = exploration_fraction, initial_eps, final_eps
         self.learning_starts = learning_starts if learning_starts is not None else batch_size
         capturable = bool(graphs)
+        self.fused = self.fused2 = self.fused_iqn = None
         if agent_type == "AC-IQN":
             self.local = AC_IQN_Policy(**DEFAULT_NET, value_ranges_of_action=[[-1.0, 1.0], [-1.0, 1.0]],
                                        device=self.device, seed=net_seed)
@@ -73,7 +76,6 @@ class VecTrainer:
                 self.actor_opt = torch.optim.Adam(self.local.actor.parameters(), lr=lr, capturable=capturable)
                 self.critic_opt = torch.optim.Adam(self.local.critic.parameters(), lr=lr, capturable=capturable)
             self.action_dim = 2
-            self.fused = self.fused2 = None
             # fused=True: the whole update on hand-written kernels (fused_update.py, needs the fused
             # optimiser); "v1": only the critic trunk fused; False: torch
             if fused is True and fused_adam and amp_dtype is not None and fused2_supported(self.local, batch_size,
@@ -93,6 +95,10 @@ class VecTrainer:
                 self.grads = FlatGrads(self.local.parameters())
                 self.opt = torch.optim.Adam(self.local.parameters(), lr=lr, capturable=capturable)
             self.action_dim = 1
+            # fused=True: the whole IQN update and act_iqn on hand-written kernels (fused_iqn.py)
+            if fused is True and fused_adam and amp_dtype is not None and fused_iqn_supported(self.local, batch_size,
+                                                                                            num_tau):
+                self.fused_iqn = FusedIQNState(self.local, self.target, batch_size, num_tau)
         else:
             raise NotImplementedError(f"VecTrainer agent_type {agent_type!r} (AC-IQN and IQN are batched)")
         NT = self.E * self.R
@@ -106,7 +112,7 @@ class VecTrainer:
         self.graphs = graphs
         self._graph = None
         self._graph_learn = None
-        # rollout / learn on two streams (fused AC-IQN path): the learner samples against a
+        # rollout / learn on two streams (fused learners): the learner samples against a
         # snapshot of the ring state taken before this iteration's push, skipping the oldest
         # E*R entries the push may overwrite, and waits for the act kernel before the actor
         # weights change
@@ -128,7 +134,12 @@ class VecTrainer:
 
     @torch.no_grad()
     def act(self):
-        if getattr(self, "fused2", None) is not None:
+        if self.fused_iqn is not None:
+            # encoders + one kernel: K = 32 quantiles per robot, mean, argmax, epsilon-greedy
+            self.fused_iqn.act(self.env.obs_cur, self.actions, self.env.counter, self.E, self.total_timesteps,
+                               self.exploration_fraction, self.initial_eps, self.final_eps, self.seed + 4242)
+            return
+        if self.fused2 is not None:
             # one kernel: actor on every robot row + epsilon-greedy on the device step counter
             self.fused2.act(self.env.obs_cur, self.actions, self.env.counter, self.E, self.total_timesteps,
                             self.exploration_fraction, self.initial_eps, self.final_eps, self.seed + 4242)
@@ -153,13 +164,19 @@ class VecTrainer:
             rnd = torch.randint(0, 25, (NT,), device=self.device)
             self.actions[:, 0].copy_(torch.where(explore.squeeze(1), rnd, greedy))
 
-    def rollout(self):
-        self.act()
+    def _fused_learner(self):
+        return self.fused2 is not None or self.fused_iqn is not None
+
+    def _push(self):
         env = self.env
-        env.step(self.actions)
         self.replay.push(env.obs_cur, env.obs_next, env.cnt_next, self.actions[:, :self.action_dim].contiguous()
                          if self.action_dim == 1 else self.actions, env.batch.reward, env.batch.done)
-        env.auto_reset()
+
+    def rollout(self):
+        self.act()
+        self.env.step(self.actions)
+        self._push()
+        self.env.auto_reset()
 
     def learn(self, state=None, guard=0, actor_wait=None):
         rows = self.replay.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter, out=self.batch_rows,
@@ -168,6 +185,11 @@ class VecTrainer:
             out = ac_iqn_update_fused2(self.fused2, self.local, self.actor_opt, self.critic_opt, self.critic_grads,
                                        self.actor_grads, rows, gamma=self.gamma, sync=self.sync,
                                        actor_wait=actor_wait)
+            self.learn_counter += 1
+            return out
+        if self.fused_iqn is not None:
+            out = iqn_update_fused(self.fused_iqn, self.local, self.opt, self.grads, rows, gamma=self.gamma,
+                                   sync=self.sync, act_wait=actor_wait)
             self.learn_counter += 1
             return out
         s, a, r, ns, d = split_rows(rows)
@@ -199,10 +221,12 @@ class VecTrainer:
                 self.fused.target_pack.refresh()  # eager, outside any captured graph
             if self.agent_type == "AC-IQN" and self.fused2 is not None:
                 self.fused2.target_changed()
+            if self.fused_iqn is not None:
+                self.fused_iqn.target_changed()
 
     # ------------------------------------------------------------------ iteration
     def _iteration_body(self, do_learn):
-        if not (do_learn and self.overlap and getattr(self, "fused2", None) is not None):
+        if not (do_learn and self.overlap and self._fused_learner()):
             self.rollout()
             out = self.learn() if do_learn else None
             self.env.advance_device()
@@ -221,8 +245,7 @@ class VecTrainer:
             ev_act.record(s_roll)
             env = self.env
             env.step(self.actions)
-            self.replay.push(env.obs_cur, env.obs_next, env.cnt_next, self.actions, env.batch.reward,
-                             env.batch.done)
+            self._push()
             env.auto_reset()
             env.advance_device()
         with torch.cuda.stream(s_learn):

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 2
+#define ASVRL_ABI_VERSION 3
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -264,6 +264,61 @@ int asvrl_critic_train(const AsvCriticWeights* w, const AsvCriticIO* io, const A
 /* Actor update's critic pass (agent.py:419-425): forward, then the backward of
  * sum_rows dq * q to G (dG) and through the action encoder to the action (dA). */
 int asvrl_critic_actor_grad(const AsvCriticWeights* w, const AsvCriticIO* io, void* stream);
+
+/* ---------------------------------------------------------------- IQN (IQN_model.py, agent.py:227-256, 434-476) */
+
+/* IQN_Policy has the critic's trunk without the action encoder (h1 feeds hidden_layer_2
+ * directly, IQN_model.py:106-108) and an output_layer 128 -> A (A <= 32 actions). Its trunk
+ * uses AsvCriticWeights (wo / bo unused); the head is described here. */
+#define ASVRL_IQN_MAX_ACTIONS 32
+typedef struct AsvIqnHead {
+  const void* wo_frag;  /* output_layer.weight padded to 32 x 128, chained fragment order: 8 fragments */
+  const float* wo;      /* output_layer.weight [A][128] f32 (the TRAIN backward) */
+  const float* bo;      /* output_layer.bias [A] */
+  int32_t n_actions;    /* A */
+} AsvIqnHead;
+
+/* Pack the trunk images (as asvrl_critic_pack) and the head image in one launch. */
+int asvrl_iqn_pack(const float* wc, const float* w1, const float* w2, const float* wout,
+                   const AsvCriticWeights* w, const AsvIqnHead* head, void* stream);
+
+/* Inputs / outputs of one IQN launch. Rows are (sample b, tau n), R = B*N. */
+typedef struct AsvIqnIO {
+  const float* F;          /* [B][256] observation features (asvrl_mlp_encode) */
+  const float* taus;       /* [B*N]; ACT: may be NULL = drawn in the kernel (Philox, uniform [0,1)) */
+  int32_t B, N, Np;        /* N in {8,16,32} (ACT: N = K = 32); Np = target quantiles per sample (TRAIN) */
+  float kappa;             /* Huber threshold (1.0, agent.py:458) */
+  const float* q_next;     /* TRAIN: [B][Np] max over actions of the target quantiles (asvrl_iqn_forward_max) */
+  const float* actions;    /* TRAIN: action index of sample b at actions[b*ld_rd] (f32, replay row column) */
+  const float* rewards;    /* TRAIN: rewards[b*ld_rd] */
+  const float* dones;      /* TRAIN: dones[b*ld_rd] */
+  int64_t ld_rd;
+  float gamma;
+  float* q;                /* FORWARD_MAX: [R] max_a Q(row, a); TRAIN optional: [R] Q(row, a_b) */
+  float* row_loss;         /* TRAIN optional: [R] sum over target quantiles of the quantile-Huber term */
+  void* dzF;               /* TRAIN: bf16 [B][256] dL/dF * 1[F > 0] (encoder pre-activation grad) */
+  void* dz_out;            /* TRAIN: bf16 [R][32] dL/d(output pre-activation): dq at the taken action, else 0 */
+  float* tile_loss;        /* TRAIN optional: [R/32] per-tile sum(row_loss) * loss_scale */
+  float loss_scale;
+  /* ACT (act_iqn, agent.py:227-256): action = argmax_a mean_n Q(b, n, a), epsilon-greedy */
+  double* act_out;         /* [B] action index as f64 at act_out[b*ld_act] */
+  int64_t ld_act;
+  const int64_t* step_dev; /* device step counter for the epsilon schedule and the RNG counter */
+  double eps_steps_per_count, eps_total, eps_fraction, eps_initial, eps_final;
+  uint64_t seed;
+} AsvIqnIO;
+
+/* Target pass of train_IQN (agent.py:451-452): q[row] = max_a Q(row, a). */
+int asvrl_iqn_forward_max(const AsvCriticWeights* w, const AsvIqnHead* head, const AsvIqnIO* io, void* stream);
+
+/* Local pass of train_IQN (agent.py:455-468): forward, gather at the taken action, the
+ * quantile-Huber loss against r + gamma * q_next * (1 - d), and the whole trunk backward
+ * (two launches). acts: h1g holds h1; dq is optional. */
+int asvrl_iqn_train(const AsvCriticWeights* w, const AsvIqnHead* head, const AsvIqnIO* io,
+                    const AsvCriticActs* acts, void* stream);
+
+/* act_iqn (agent.py:227-256) for every row of F with K = 32 quantile samples per state. */
+int asvrl_iqn_act(const AsvCriticWeights* w, const AsvIqnHead* head, const AsvIqnIO* io, void* stream);
 
 /* ---------------------------------------------------------------- replay (replay_buffer.py) */
 
