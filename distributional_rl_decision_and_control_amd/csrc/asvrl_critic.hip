@@ -47,9 +47,14 @@ template <int MODE> constexpr bool kFwdOnly = MODE == MODE_FWD || MODE == MODE_I
 #ifndef ASVRL_TRAIN_B_BPP32
 #define ASVRL_TRAIN_B_BPP32 2
 #endif
+// Persistent launches (one workgroup per CU stages the weights into LDS once, its waves walk
+// the tiles) per mode: bit MODE of the mask, bit 6 = TRAIN part B. Non-persistent launches
+// (one tile per wave) share the CUs better with a concurrent stream.
 #ifndef ASVRL_CRITIC_PERSISTENT
 #define ASVRL_CRITIC_PERSISTENT 0
 #endif
+template <int MODE> constexpr bool kPersistent = (ASVRL_CRITIC_PERSISTENT >> MODE) & 1;
+constexpr bool kPersistentB = (ASVRL_CRITIC_PERSISTENT >> 6) & 1;
 
 struct CriticArgs {
   AsvCriticWeights w;
@@ -313,7 +318,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
 #pragma unroll
     for (int g = 0; g < 16; ++g)
       if (feat(0, g, h) == ai) qs = ao[g] + L.bo_a[ai];
-    q = qs + __shfl_xor(qs, 32, 64);   // Q_expected.gather(2, actions) (agent.py:456)
+    q = half_sum(qs);   // Q_expected.gather(2, actions) (agent.py:456): one half holds it, the other 0
   } else {
     float part = 0.f;
 #pragma unroll
@@ -326,7 +331,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
         part += L.wo[m] * relu(x);
       }
     }
-    q = part + __shfl_xor(part, 32, 64) + a.w.bo[0];
+    q = half_sum(part) + a.w.bo[0];
   }
   if (a.q != nullptr && h == 0) a.q[grow] = q;
   if (MODE == MODE_FWD) return;
@@ -340,30 +345,42 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
       rb = a.rew[b * a.ld_rd];
       nd = 1.0f - a.don[b * a.ld_rd];
     }
+    // quantile-Huber terms over the target quantiles (agent.py:406-412), each lane half taking
+    // half of them; |tau - 1[d < 0]| is tau or 1 - tau (exact), and the division by kappa
+    // happens once per row
+    const float kap = a.kappa, hk = 0.5f * a.kappa, omt = 1.f - tau;
     float wl = 0.f, wg = 0.f;
     auto term = [&](float target) {
       const float d = target - q;  // td_error (agent.py:406)
       const float ad = fabsf(d);
-      const bool quad = ad <= a.kappa;
-      const float hub = quad ? 0.5f * (d * d) : a.kappa * (ad - 0.5f * a.kappa);
-      const float w = fabsf(tau - (d < 0.f ? 1.f : 0.f));
-      wl += w * hub / a.kappa;
-      wg += w * (quad ? d : (d > 0.f ? a.kappa : -a.kappa)) / a.kappa;
+      const bool quad = ad <= kap;
+      const float hub = quad ? 0.5f * (d * d) : kap * (ad - hk);
+      const float w = d < 0.f ? omt : tau;
+      wl += w * hub;
+      wg += w * (quad ? d : copysignf(kap, d));
     };
     if (a.Np == NT) {
       // N' = N: lane r owns target r % N of its sample (one load per lane, no load in the loop);
       // the loop broadcasts it: readlane when one sample fills the 32-row tile, else a shuffle
       const float qv = qt[r % NT];
       const float own = a.qn != nullptr ? rb + (a.gamma * qv) * nd : qv;   // r + gamma * q_next * (1 - d)
-#pragma unroll 8
-      for (int j = 0; j < NT; ++j) {
-        const float target = NT == 32 ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(own), j))
-                                      : __shfl(own, (lane & ~(NT - 1)) + j, 64);
+#pragma unroll 4
+      for (int j = 0; j < NT / 2; ++j) {
+        float target;
+        if (NT == 32) {
+          const float t0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(own), j));
+          const float t1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(own), j + NT / 2));
+          target = h ? t1 : t0;
+        } else {
+          target = __shfl(own, (lane & ~(NT - 1)) + j + h * (NT / 2), 64);
+        }
         term(target);
       }
     } else {
-      for (int j = 0; j < a.Np; ++j) term(a.qn != nullptr ? rb + (a.gamma * qt[j]) * nd : qt[j]);
+      for (int j = h; j < a.Np; j += 2) term(a.qn != nullptr ? rb + (a.gamma * qt[j]) * nd : qt[j]);
     }
+    wl = half_sum(wl) / kap;
+    wg = half_sum(wg) / kap;
     dq = -wg * a.gscale;
     if (a.tile_loss != nullptr) tile_sum_store(wl, lane, a.loss_scale, a.tile_loss + tile);
     if (h == 0) {
@@ -468,8 +485,8 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
   }
   if (MODE == MODE_ACTOR) {
     if (a.dA != nullptr) {
-      pa0 += __shfl_xor(pa0, 32, 64);
-      pa1 += __shfl_xor(pa1, 32, 64);
+      pa0 = half_sum(pa0);
+      pa1 = half_sum(pa1);
       if (writer && h == 0) {
         a.dA[2 * b] = pa0;
         a.dA[2 * b + 1] = pa1;
@@ -584,8 +601,17 @@ __global__ __launch_bounds__(8 * 64) void critic_train_b_kernel(CriticArgs a) {
     for (int i = threadIdx.x; i < kC; i += 8 * 64) L.bc[i] = a.w.bc[i];
   }
   __syncthreads();
-  const int tile = blockIdx.x * 8 + (threadIdx.x >> 6);
-  if (tile < a.B * NT / 32) critic_tile_b<NT>(a, L, tile, threadIdx.x & 63);
+  if constexpr (kPersistentB) {
+#pragma unroll 1
+    for (int tile = blockIdx.x * 8 + (threadIdx.x >> 6); tile < a.B * NT / 32; tile += gridDim.x * 8) {
+      int ln = threadIdx.x & 63;   // opaque per iteration (see critic_kernel)
+      asm volatile("" : "+v"(ln));
+      critic_tile_b<NT>(a, L, tile, ln);
+    }
+  } else {
+    const int tile = blockIdx.x * 8 + (threadIdx.x >> 6);
+    if (tile < a.B * NT / 32) critic_tile_b<NT>(a, L, tile, threadIdx.x & 63);
+  }
 }
 
 // Persistent: one workgroup per CU stages the forward weights into LDS once, then its waves
@@ -622,18 +648,20 @@ __global__ __launch_bounds__(CriticWaves<MODE>::n * 64) void critic_kernel(Criti
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int tiles = a.B * NT / 32;
-#if ASVRL_CRITIC_PERSISTENT
+  if constexpr (kPersistent<MODE>) {
+#pragma unroll 1
   for (int tile = blockIdx.x * W + (threadIdx.x >> 6); tile < tiles; tile += gridDim.x * W) {
-    // opaque per-iteration copy of the LDS base: keeps the (loop-invariant) weight-fragment
-    // reads inside the loop instead of hoisting thousands of them into registers
-    const CriticLds* Lp = &L;
-    asm volatile("" : "+v"(Lp));
-    critic_tile<MODE, NT>(a, *Lp, tile, lane);
+    // opaque per-iteration copy of the lane index: every weight-fragment address depends on it,
+    // which keeps those (loop-invariant) LDS reads inside the loop instead of hoisting them
+    // into registers, while L keeps its LDS address space (ds_read, not flat loads)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    critic_tile<MODE, NT>(a, L, tile, ln);
   }
-#else
-  const int tile = blockIdx.x * W + (threadIdx.x >> 6);
-  if (tile < tiles) critic_tile<MODE, NT>(a, L, tile, lane);
-#endif
+  } else {
+    const int tile = blockIdx.x * W + (threadIdx.x >> 6);
+    if (tile < tiles) critic_tile<MODE, NT>(a, L, tile, lane);
+  }
 }
 
 int num_cus() {
@@ -647,14 +675,18 @@ int num_cus() {
   return n;
 }
 
+int train_b_grid(int tiles) {
+  int grid = (tiles + 7) / 8;
+  if (kPersistentB && grid > num_cus()) grid = num_cus();
+  return grid;
+}
+
 template <int MODE, int NT>
 void launch_mode(const CriticArgs& a, hipStream_t st) {
   constexpr int W = CriticWaves<MODE>::n;
   const int tiles = a.B * NT / 32;
   int grid = (tiles + W - 1) / W;
-#if ASVRL_CRITIC_PERSISTENT
-  if (grid > num_cus()) grid = num_cus();
-#endif
+  if (kPersistent<MODE> && grid > num_cus()) grid = num_cus();
   hipLaunchKernelGGL((critic_kernel<MODE, NT>), dim3(grid), dim3(W * 64), 0, st, a);
 }
 
@@ -665,14 +697,14 @@ void launch_n(int mode, const CriticArgs& a, hipStream_t st) {
     launch_mode<MODE_FWD, NT>(a, st);
   } else if (mode == MODE_TRAIN) {
     launch_mode<MODE_TRAIN, NT>(a, st);
-    hipLaunchKernelGGL((critic_train_b_kernel<NT>), dim3((tiles + 7) / 8), dim3(8 * 64), 0, st, a);
+    hipLaunchKernelGGL((critic_train_b_kernel<NT>), dim3(train_b_grid(tiles)), dim3(8 * 64), 0, st, a);
   } else if (mode == MODE_ACTOR) {
     launch_mode<MODE_ACTOR, NT>(a, st);
   } else if (mode == MODE_IQN_MAX) {
     launch_mode<MODE_IQN_MAX, NT>(a, st);
   } else if (mode == MODE_IQN_TRAIN) {   // part B (layer 4 + dF) is the critic's
     launch_mode<MODE_IQN_TRAIN, NT>(a, st);
-    hipLaunchKernelGGL((critic_train_b_kernel<NT>), dim3((tiles + 7) / 8), dim3(8 * 64), 0, st, a);
+    hipLaunchKernelGGL((critic_train_b_kernel<NT>), dim3(train_b_grid(tiles)), dim3(8 * 64), 0, st, a);
   } else if constexpr (NT == 32) {
     launch_mode<MODE_IQN_ACT, 32>(a, st);
   }

@@ -45,6 +45,14 @@ __device__ __forceinline__ float seg_sum(float v) {
   return v;
 }
 
+// x(lane) + x(lane ^ 32) in every lane, in the same order in both halves: one v_permlane32_swap of
+// x with itself leaves (lower half's x, upper half's x) in the two results of every lane
+__device__ __forceinline__ float half_sum(float x) {
+  const unsigned u = __float_as_uint(x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // cos(tau * pi * k) (Critic.calc_cos, AC_IQN_model.py:423) on the hardware cosine: v_cos_f32 takes
 // revolutions, cos(2 pi x) with x = k tau / 2 (< 32 for k < 64, tau < 1: inside its +-256 domain).
 // The value is rounded to bf16 for the MFMA right after, far above v_cos_f32's error.
@@ -65,25 +73,22 @@ __device__ __forceinline__ void store4(__bf16* base, const float* v) {
 }
 
 // Store the 16 features of one k-step group (features 16s .. 16s+15 of a 32-feature block) of this
-// lane's row: lane half h holds v = {4h .. 4h+3, 8+4h .. 8+4h+3}; one exchange with the partner
-// lane (l ^ 32) gives half 0 features 0..7 and half 1 features 8..15, so each lane writes one
-// 16-byte piece and every row gets a full 32-byte sector per instruction. `grp` points at
-// feature 16s of the row. All 64 lanes must call it (cross-lane exchange).
+// lane's row: lane half h holds v = {4h .. 4h+3, 8+4h .. 8+4h+3}. v_permlane32_swap (one per
+// dword, VALU, no LDS round trip) trades the upper half's features 4..7 against the lower half's
+// 8..11, so half 0 then holds features 0..7 and half 1 features 8..15, and each lane writes one
+// 16-byte piece: every row gets a full 32-byte sector per instruction. `grp` points at feature
+// 16s of the row (nullptr: exchange only). All 64 lanes must call it.
 __device__ __forceinline__ void store16(__bf16* grp, const float* v, int h) {
   bf16x4 lo, hi;
   lo[0] = (__bf16)v[0]; lo[1] = (__bf16)v[1]; lo[2] = (__bf16)v[2]; lo[3] = (__bf16)v[3];
   hi[0] = (__bf16)v[4]; hi[1] = (__bf16)v[5]; hi[2] = (__bf16)v[6]; hi[3] = (__bf16)v[7];
   typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-  const u32x2 send = __builtin_bit_cast(u32x2, h ? lo : hi);
-  u32x2 recv;
-  recv[0] = __shfl_xor(send[0], 32, 64);
-  recv[1] = __shfl_xor(send[1], 32, 64);
-  if (h) lo = __builtin_bit_cast(bf16x4, recv);
-  else hi = __builtin_bit_cast(bf16x4, recv);
-  bf16x8 out;
-  out[0] = lo[0]; out[1] = lo[1]; out[2] = lo[2]; out[3] = lo[3];
-  out[4] = hi[0]; out[5] = hi[1]; out[6] = hi[2]; out[7] = hi[3];
-  if (grp != nullptr) *reinterpret_cast<bf16x8*>(grp + 8 * h) = out;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x2 l = __builtin_bit_cast(u32x2, lo), u = __builtin_bit_cast(u32x2, hi);
+  const auto r0 = __builtin_amdgcn_permlane32_swap(l[0], u[0], false, false);
+  const auto r1 = __builtin_amdgcn_permlane32_swap(l[1], u[1], false, false);
+  const u32x4 out = {r0[0], r1[0], r0[1], r1[1]};
+  if (grp != nullptr) *reinterpret_cast<u32x4*>(grp + 8 * h) = out;
 }
 
 // 4 consecutive bf16 -> f32

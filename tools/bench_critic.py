@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--B", type=int, default=4096)
     ap.add_argument("--N", type=int, default=32)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--act-rows", type=int, default=4096 * 5)
     a = ap.parse_args()
     from distributional_rl_decision_and_control_amd.fused_critic import (CriticPack, TrainBuffers, critic_actor_grad,
                                                                           critic_forward, critic_train)
@@ -42,6 +43,25 @@ def main():
         "train": lambda: critic_train(pack, F, G, taus, qt, bufs, dzF=dzF, dzG=dzG, with_dFdG=False),
         "actor": lambda: critic_actor_grad(pack, F, G, taus, N, q, w_ae=c.action_encoder[0].weight, dA=dA),
     }
+    # IQN modes at the same shape; act_iqn over the rollout's robot rows (4096 envs x 5)
+    from distributional_rl_decision_and_control_amd.fused_iqn import IqnPack, iqn_act, iqn_forward_max, iqn_train
+    from distributional_rl_decision_and_control_amd.policy.IQN_model import IQN_Policy
+    inet = IQN_Policy(7, 5, 5, 56, 40, 256, 128, 25, "cuda", 101).cuda()
+    ipack = IqnPack(inet)
+    rows = torch.zeros(B, 88, device="cuda")
+    rows[:, 80] = torch.randint(0, 25, (B,), device="cuda").float()
+    rows[:, 82] = torch.randn(B, device="cuda")
+    dz_out = torch.empty(B * N, 32, dtype=torch.bfloat16, device="cuda")
+    n_act = a.act_rows
+    F_act = torch.rand(n_act, 256, device="cuda")
+    act64 = torch.zeros(n_act, 2, dtype=torch.float64, device="cuda")
+    step = torch.zeros(1, dtype=torch.int64, device="cuda")
+    runs.update({
+        "iqn_max": lambda: iqn_forward_max(ipack, F, taus, N, q),
+        "iqn_train": lambda: iqn_train(ipack, F, taus, bufs, dz_out, qt, rows[:, 80], rows[:, 82], rows[:, 83], 0.99,
+                                       dzF),
+        "iqn_act": lambda: iqn_act(ipack, F_act, act64, step, 1.0, 1e6, 0.25, 0.1, 0.1, 7),
+    })
     out = {}
     for k, fn in runs.items():
         for _ in range(3):
