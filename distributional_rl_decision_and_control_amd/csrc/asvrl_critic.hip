@@ -48,13 +48,17 @@ template <int MODE> constexpr bool kFwdOnly = MODE == MODE_FWD || MODE == MODE_I
 #define ASVRL_TRAIN_B_BPP32 2
 #endif
 // Persistent launches (one workgroup per CU stages the weights into LDS once, its waves walk
-// the tiles) per mode: bit MODE of the mask, bit 6 = TRAIN part B. Non-persistent launches
+// the tiles) per mode: bit MODE of the mask (not TRAIN / ACTOR). Non-persistent launches
 // (one tile per wave) share the CUs better with a concurrent stream.
 #ifndef ASVRL_CRITIC_PERSISTENT
 #define ASVRL_CRITIC_PERSISTENT 0
 #endif
 template <int MODE> constexpr bool kPersistent = (ASVRL_CRITIC_PERSISTENT >> MODE) & 1;
-constexpr bool kPersistentB = (ASVRL_CRITIC_PERSISTENT >> 6) & 1;
+// TRAIN and ACTOR read G per feature after activation stores have been issued; vmcnt counts
+// stores too, so a global load there would first drain them. Each wave stages its samples' G
+// rows in LDS instead (needs one tile per wave: never persistent).
+template <int MODE> constexpr bool kStageG = MODE == MODE_TRAIN || MODE == MODE_ACTOR;
+static_assert(!kPersistent<MODE_TRAIN> && !kPersistent<MODE_ACTOR>, "TRAIN / ACTOR stage G per tile");
 
 struct CriticArgs {
   AsvCriticWeights w;
@@ -182,7 +186,8 @@ __device__ __forceinline__ void iqn_act_select(const CriticArgs& a, const Critic
 }
 
 template <int MODE, int NT, class LT>
-__device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, int tile, int lane) {
+__device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, int tile, int lane,
+                                            const float* Gl = nullptr) {
   constexpr bool IQN = kIqn<MODE>;
   constexpr bool TRAINM = kTrainMode<MODE>;
   const int r = lane & 31, h = lane >> 5;
@@ -192,7 +197,10 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
   if (MODE == MODE_IQN_ACT && a.taus == nullptr) tau = act_tau(a, grow);
   else tau = a.taus[grow];
   const float* Fb = a.F + static_cast<size_t>(b) * kC;
-  const float* Gb = IQN ? nullptr : a.G + static_cast<size_t>(b) * kH;
+  const float* Gb;   // G[b]: the wave's LDS copy (kStageG) or global
+  if constexpr (IQN) Gb = nullptr;
+  else if constexpr (kStageG<MODE>) Gb = Gl + (b - tile * 32 / NT) * kH;
+  else Gb = a.G + static_cast<size_t>(b) * kH;
   const bf16x8* WC = kFwdOnly<MODE> ? L.wc : reinterpret_cast<const bf16x8*>(a.w.wc_frag);
   const bf16x8* W1 = L.w1;
   const bf16x8* W2 = L.w2;
@@ -436,65 +444,60 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
 #pragma unroll
     for (int mb = 0; mb < 4; ++mb) acc3[mb] = mfma(W2T[(mb * 8 + ks) * 64 + lane], dz2pk[ks], acc3[mb]);
   }
-  const bool writer = (r % NT) == NT - 1;   // holds the segment sums (seg_sum)
-  float pa0 = 0.f, pa1 = 0.f;   // ACTOR: partial dA over this lane's features
-  bf16x8 dz1pk[8];
+  // dz1 = dh1g * G * 1[h1 > 0]; gsa collects dh1g * h1 for dG = its sum over the sample's taus.
+  // G is re-read here through an opaque offset: reusing layer 1's reads would keep 64 values live
+  int g0 = 0;
+  asm volatile("" : "+v"(g0));
+  const float* G3 = Gb + g0;
+  float gsa[64];   // value (mb * 2 + s) * 8 + j
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      float dv[8], gs[8];
-      if constexpr (IQN) {   // dz1 = dh1 * 1[h1 > 0]; no action features
-#pragma unroll
-        for (int j = 0; j < 8; ++j) dv[j] = static_cast<float>(h1pk[mb * 2 + s][j]) > 0.f ? acc3[mb][8 * s + j] : 0.f;
-        store16(bp(a.acts.dz1) + static_cast<size_t>(grow) * kH + mb * 32 + 16 * s, dv, h);
-        continue;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) gs[j] = acc3[mb][8 * s + j] * static_cast<float>(h1pk[mb * 2 + s][j]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) gs[j] = seg_sum<NT>(gs[j]);
-      float gz[8];
+      float dv[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int m = feat(mb, 8 * s + j, h);
-        const float gm = Gb[m];
         const float h1 = static_cast<float>(h1pk[mb * 2 + s][j]);
-        dv[j] = h1 > 0.f ? acc3[mb][8 * s + j] * gm : 0.f;
-        dz1pk[mb * 2 + s][j] = (__bf16)dv[j];
-        gz[j] = gm > 0.f ? gs[j] : 0.f;   // through the action encoder's relu
-        if (MODE == MODE_ACTOR && a.dA != nullptr) {
-          pa0 += gz[j] * a.wae[2 * m];
-          pa1 += gz[j] * a.wae[2 * m + 1];
-        }
-      }
-      if (writer) {
-        const size_t ob = static_cast<size_t>(b) * kH + mb * 32 + 16 * s + 4 * h;
-        if (a.dG != nullptr) {
-          *reinterpret_cast<float4*>(a.dG + ob) = make_float4(gs[0], gs[1], gs[2], gs[3]);
-          *reinterpret_cast<float4*>(a.dG + ob + 8) = make_float4(gs[4], gs[5], gs[6], gs[7]);
-        }
-        if (a.dzG != nullptr) {
-          *reinterpret_cast<float4*>(a.dzG + ob) = make_float4(gz[0], gz[1], gz[2], gz[3]);
-          *reinterpret_cast<float4*>(a.dzG + ob + 8) = make_float4(gz[4], gz[5], gz[6], gz[7]);
+        if constexpr (IQN) {   // no action features
+          dv[j] = h1 > 0.f ? acc3[mb][8 * s + j] : 0.f;
+        } else {
+          dv[j] = h1 > 0.f ? acc3[mb][8 * s + j] * G3[feat(mb, 8 * s + j, h)] : 0.f;
+          gsa[(mb * 2 + s) * 8 + j] = acc3[mb][8 * s + j] * h1;
         }
       }
       if (TRAINM)
         store16(bp(a.acts.dz1) + static_cast<size_t>(grow) * kH + mb * 32 + 16 * s, dv, h);
     }
   }
-  if (MODE == MODE_ACTOR) {
-    if (a.dA != nullptr) {
-      pa0 = half_sum(pa0);
-      pa1 = half_sum(pa1);
-      if (writer && h == 0) {
+  if constexpr (!IQN) {
+    // dG[b] over the sample's NT rows: transpose-reduce, lane r then holds features of values
+    // (r % NT) * PER + i
+    xreduce<64, NT>(gsa, lane);
+    constexpr int PER = 64 / NT;
+    float pa0 = 0.f, pa1 = 0.f;   // ACTOR: partial dA over this lane's features
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int v = (r % NT) * PER + i, g = v >> 3;
+      const int m = feat(g >> 1, 8 * (g & 1) + (v & 7), h);
+      const float gm = G3[m];
+      const float gz = gm > 0.f ? gsa[i] : 0.f;   // through the action encoder's relu
+      const size_t o = static_cast<size_t>(b) * kH + m;
+      if (a.dG != nullptr) a.dG[o] = gsa[i];
+      if (a.dzG != nullptr) a.dzG[o] = gz;
+      if (MODE == MODE_ACTOR && a.dA != nullptr) {
+        pa0 += gz * a.wae[2 * m];
+        pa1 += gz * a.wae[2 * m + 1];
+      }
+    }
+    if (MODE == MODE_ACTOR && a.dA != nullptr) {
+      pa0 = half_sum(seg_sum<NT>(pa0));   // lane r % NT == NT - 1 of each half holds the group sum
+      pa1 = half_sum(seg_sum<NT>(pa1));
+      if ((r % NT) == NT - 1 && h == 0) {
         a.dA[2 * b] = pa0;
         a.dA[2 * b + 1] = pa1;
       }
     }
-    return;
   }
-
 }
 
 // ---------------- TRAIN part B, layer 4: dh0 = W1^T dz1; dF[b] = sum_taus dh0 * c; dzc = dh0 * F * 1[c > 0].
@@ -507,12 +510,13 @@ struct CriticLdsB {
 };
 
 template <int NT>
-__device__ __forceinline__ void critic_tile_b(const CriticArgs& a, const CriticLdsB& L, int tile, int lane) {
+__device__ __forceinline__ void critic_tile_b(const CriticArgs& a, const CriticLdsB& L, int tile, int lane,
+                                              const float* Fl) {
   const int r = lane & 31, h = lane >> 5;
   const int grow = tile * 32 + r;
   const int b = grow / NT;
   const float tau = a.taus[grow];
-  const float* Fb = a.F + static_cast<size_t>(b) * kC;
+  const float* Fb = Fl + (b - tile * 32 / NT) * kC;   // the wave's LDS copy of F[b]
   bf16x8 cx[kNcos / 16];
 #pragma unroll
   for (int ks = 0; ks < kNcos / 16; ++ks)
@@ -530,7 +534,6 @@ __device__ __forceinline__ void critic_tile_b(const CriticArgs& a, const CriticL
     const bf16x4 hi = *reinterpret_cast<const bf16x4*>(dz1row + ks * 16 + 8 + 4 * h);
     dz1pk[ks] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   }
-  const bool writer = (r % NT) == NT - 1;
   const bf16x8* W1T = L.w1t;
   // NT = 32 (row_bcast segment sums) spills at 4 blocks per pass; 2 keeps it in registers
   constexpr int BPP = ASVRL_TRAIN_B_BPP32 != 0 && NT == 32 ? ASVRL_TRAIN_B_BPP32 : 4;
@@ -551,41 +554,34 @@ __device__ __forceinline__ void critic_tile_b(const CriticArgs& a, const CriticL
 #pragma unroll
       for (int q4 = 0; q4 < BPP; ++q4)
         acc4[q4] = mfma(W1T[((half * BPP + q4) * 8 + ks) * 64 + lane], dz1pk[ks], acc4[q4]);
+    float fsa[16 * BPP];   // dh0 * c of this pass, value (q4 * 2 + s) * 8 + j
 #pragma unroll
     for (int q4 = 0; q4 < BPP; ++q4) {
       const int mb = half * BPP + q4;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        float dv[8], fs[8], cv[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float x = acc0[q4][8 * s + j] + L.bc[feat(mb, 8 * s + j, h)];
-          cv[j] = static_cast<float>((__bf16)relu(x));   // part A's bf16 c
-          fs[j] = acc4[q4][8 * s + j] * cv[j];
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) fs[j] = seg_sum<NT>(fs[j]);
-        float fz[8];
+        float dv[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int m = feat(mb, 8 * s + j, h);
-          const float fm = Fb[m];
-          dv[j] = cv[j] > 0.f ? acc4[q4][8 * s + j] * fm : 0.f;
-          fz[j] = fm > 0.f ? fs[j] : 0.f;   // through the encoders' relu / mask
-        }
-        if (writer) {
-          const size_t ob = static_cast<size_t>(b) * kC + mb * 32 + 16 * s + 4 * h;
-          if (a.dF != nullptr) {
-            *reinterpret_cast<float4*>(a.dF + ob) = make_float4(fs[0], fs[1], fs[2], fs[3]);
-            *reinterpret_cast<float4*>(a.dF + ob + 8) = make_float4(fs[4], fs[5], fs[6], fs[7]);
-          }
-          if (a.dzF != nullptr) {
-            store4(bp(a.dzF) + ob, fz);
-            store4(bp(a.dzF) + ob + 8, fz + 4);
-          }
+          const float x = acc0[q4][8 * s + j] + L.bc[m];
+          const float cv = static_cast<float>((__bf16)relu(x));   // part A's bf16 c
+          fsa[(q4 * 2 + s) * 8 + j] = acc4[q4][8 * s + j] * cv;
+          dv[j] = cv > 0.f ? acc4[q4][8 * s + j] * Fb[m] : 0.f;
         }
         store16(bp(a.acts.dzc) + static_cast<size_t>(grow) * kC + mb * 32 + 16 * s, dv, h);
       }
+    }
+    // dF[b] over the sample's NT rows: transpose-reduce, lane r then holds values (r % NT) * PER + i
+    xreduce<16 * BPP, NT>(fsa, lane);
+    constexpr int PER = 16 * BPP / NT;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int v = (r % NT) * PER + i, g = v >> 3;
+      const int m = feat(half * BPP + (g >> 1), 8 * (g & 1) + (v & 7), h);
+      const size_t o = static_cast<size_t>(b) * kC + m;
+      if (a.dF != nullptr) a.dF[o] = fsa[i];
+      if (a.dzF != nullptr) bp(a.dzF)[o] = (__bf16)(Fb[m] > 0.f ? fsa[i] : 0.f);   // through the encoders' relu / mask
     }
   }
 }
@@ -600,18 +596,17 @@ __global__ __launch_bounds__(8 * 64) void critic_train_b_kernel(CriticArgs a) {
     for (int i = threadIdx.x; i < kFragW1; i += 8 * 64) L.w1t[i] = gw1t[i];
     for (int i = threadIdx.x; i < kC; i += 8 * 64) L.bc[i] = a.w.bc[i];
   }
-  __syncthreads();
-  if constexpr (kPersistentB) {
-#pragma unroll 1
-    for (int tile = blockIdx.x * 8 + (threadIdx.x >> 6); tile < a.B * NT / 32; tile += gridDim.x * 8) {
-      int ln = threadIdx.x & 63;   // opaque per iteration (see critic_kernel)
-      asm volatile("" : "+v"(ln));
-      critic_tile_b<NT>(a, L, tile, ln);
-    }
-  } else {
-    const int tile = blockIdx.x * 8 + (threadIdx.x >> 6);
-    if (tile < a.B * NT / 32) critic_tile_b<NT>(a, L, tile, threadIdx.x & 63);
+  // this wave's samples' F rows (read per feature after the dzc stores: LDS, not vmcnt-ordered loads)
+  __shared__ __attribute__((aligned(16))) float Fs[8 * (32 / NT) * kC];
+  const int tile = blockIdx.x * 8 + (threadIdx.x >> 6);
+  float* Fw = Fs + (threadIdx.x >> 6) * (32 / NT) * kC;
+  if (tile < a.B * NT / 32) {
+    const float4* src = reinterpret_cast<const float4*>(a.F + static_cast<size_t>(tile) * (32 / NT) * kC);
+#pragma unroll
+    for (int i = threadIdx.x & 63; i < (32 / NT) * kC / 4; i += 64) reinterpret_cast<float4*>(Fw)[i] = src[i];
   }
+  __syncthreads();
+  if (tile < a.B * NT / 32) critic_tile_b<NT>(a, L, tile, threadIdx.x & 63, Fw);
 }
 
 // Persistent: one workgroup per CU stages the forward weights into LDS once, then its waves
@@ -623,6 +618,16 @@ template <int MODE, int NT>
 __global__ __launch_bounds__(CriticWaves<MODE>::n * 64) void critic_kernel(CriticArgs a) {
   constexpr int W = CriticWaves<MODE>::n;
   __shared__ typename LdsOf<MODE>::T L;
+  __shared__ __attribute__((aligned(16))) float Gs[kStageG<MODE> ? W * (32 / NT) * kH : 1];
+  if constexpr (kStageG<MODE>) {   // this wave's samples' G rows (32 / NT rows of 128)
+    const int tile = blockIdx.x * W + (threadIdx.x >> 6), l = threadIdx.x & 63;
+    if (tile < a.B * NT / 32) {
+      const float4* src = reinterpret_cast<const float4*>(a.G + static_cast<size_t>(tile) * (32 / NT) * kH);
+      float4* dst = reinterpret_cast<float4*>(Gs + (threadIdx.x >> 6) * (32 / NT) * kH);
+#pragma unroll
+      for (int i = l; i < (32 / NT) * kH / 4; i += 64) dst[i] = src[i];
+    }
+  }
   {
     const bf16x8* gwc = reinterpret_cast<const bf16x8*>(kFwdOnly<MODE> ? a.w.wc_frag : a.w.w2t_frag);
     const bf16x8* gw1 = reinterpret_cast<const bf16x8*>(a.w.w1_frag);
@@ -660,7 +665,7 @@ __global__ __launch_bounds__(CriticWaves<MODE>::n * 64) void critic_kernel(Criti
   }
   } else {
     const int tile = blockIdx.x * W + (threadIdx.x >> 6);
-    if (tile < tiles) critic_tile<MODE, NT>(a, L, tile, lane);
+    if (tile < tiles) critic_tile<MODE, NT>(a, L, tile, lane, Gs + (threadIdx.x >> 6) * (32 / NT) * kH);
   }
 }
 
@@ -675,11 +680,7 @@ int num_cus() {
   return n;
 }
 
-int train_b_grid(int tiles) {
-  int grid = (tiles + 7) / 8;
-  if (kPersistentB && grid > num_cus()) grid = num_cus();
-  return grid;
-}
+int train_b_grid(int tiles) { return (tiles + 7) / 8; }
 
 template <int MODE, int NT>
 void launch_mode(const CriticArgs& a, hipStream_t st) {

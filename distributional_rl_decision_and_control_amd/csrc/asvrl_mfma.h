@@ -25,9 +25,10 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
 // feature index held by accumulator register g of 32-feature block mb in lane half h
 __device__ __forceinline__ int feat(int mb, int g, int h) { return mb * 32 + (g & 3) + 8 * (g >> 2) + 4 * h; }
 
+// full-mask DPP read (bound_ctrl set: lets the compiler fuse it into the consuming v_add_f32_dpp)
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 
 // Sum over aligned groups of NT lanes (NT | 32), all on DPP: xor-1 and xor-2 quad butterflies,
@@ -43,6 +44,46 @@ __device__ __forceinline__ float seg_sum(float v) {
   if (NT >= 32)                     // row_bcast:15 into rows 1, 3 (rows 0, 2 add 0)
     v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xA, 0xF, false));
   return v;
+}
+
+// One halving step of xreduce over lane bit K, partner lane by DPP control CTRL (a mirror or
+// quad permutation that flips bit K and only bits below it): the lane with bit K clear keeps the
+// lower half of x[0 .. n) plus its partner's, the other the upper half.
+template <int CTRL, int K, int N>
+__device__ __forceinline__ void xreduce_step(float* x, int lane) {
+  const bool up = (lane >> K) & 1;
+#pragma unroll
+  for (int i = 0; i < N / 2; ++i) {
+    const float lo = x[i] + dpp<CTRL>(x[i]);
+    const float hi = x[i + N / 2] + dpp<CTRL>(x[i + N / 2]);
+    x[i] = up ? hi : lo;
+  }
+}
+
+// Transpose-reduce: sums each of the V values x[] over the aligned NT-lane groups of each lane
+// half (NT | 32, NT <= V) by recursive halving, about V instructions in all instead of
+// V * log2(NT). Afterwards x[0 .. V/NT) of lane r (= lane & 31) holds the group sums of the
+// original values (r % NT) * (V/NT) + i. The 16-lane step is one v_permlane16_swap per pair: it
+// leaves the two partial sums in its two results in every lane, so no select is needed.
+template <int V, int NT>
+__device__ __forceinline__ void xreduce(float (&x)[V], int lane) {
+  static_assert(NT >= 2 && NT <= 32 && (NT & (NT - 1)) == 0 && V % NT == 0, "xreduce: NT | 32, NT <= V");
+  if constexpr (NT >= 32) {   // bit 4: rows 0 <-> 1 of 16 lanes (and 2 <-> 3)
+#pragma unroll
+    for (int i = 0; i < V / 2; ++i) {
+      const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x[i]), __float_as_uint(x[i + V / 2]), false,
+                                                      false);
+      x[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+  }
+  constexpr int N3 = NT >= 32 ? V / 2 : V;
+  if constexpr (NT >= 16) xreduce_step<0x140, 3, N3>(x, lane);                   // row_mirror
+  constexpr int N2 = NT >= 16 ? N3 / 2 : N3;
+  if constexpr (NT >= 8) xreduce_step<0x141, 2, N2>(x, lane);                    // row_half_mirror
+  constexpr int N1 = NT >= 8 ? N2 / 2 : N2;
+  if constexpr (NT >= 4) xreduce_step<0x4E, 1, N1>(x, lane);                     // quad_perm [2,3,0,1]
+  constexpr int N0 = NT >= 4 ? N1 / 2 : N1;
+  xreduce_step<0xB1, 0, N0>(x, lane);                                            // quad_perm [1,0,3,2]
 }
 
 // x(lane) + x(lane ^ 32) in every lane, in the same order in both halves: one v_permlane32_swap of
