@@ -26,6 +26,7 @@ import torch
 
 from . import _abi
 from .fused_critic import CriticPack, PartialArena, TrainBuffers
+from .fused_update import SideStreams
 from .fused_mlp import MlpPack, encoder_fold, mlp_encode
 from .learner import clip_and_step
 
@@ -133,6 +134,7 @@ class FusedIQNState:
         self.loss = torch.zeros(1, **f)
         self.tile_loss = torch.zeros(B * N // 32, **f)
         self.F_act = None
+        self.side = SideStreams(dev, 2)
 
     def target_changed(self):
         """Re-pack the target network after a hard/soft update (eager, outside graphs)."""
@@ -152,18 +154,23 @@ def iqn_grads(st, net, rows, taus, gamma=0.99):
     B, N = st.B, st.N
     s_rows, ns_rows = rows[:, 0:OBS], rows[:, OBS:2 * OBS]
     a_col, r_col, d_col = rows[:, 80], rows[:, 82], rows[:, 83]
-    bufs, arena = st.bufs, st.arena
-    # every .grad is overwritten below (no zeroing)
+    bufs, arena, side = st.bufs, st.arena, st.side
+    # every .grad is overwritten below (no zeroing); independent launches on side streams
+    with side.on(0):
+        mlp_encode(st.local.enc, s_rows, st.F, xb=st.xb)
     mlp_encode(st.target.enc, ns_rows, st.Ft)
     iqn_forward_max(st.target, st.Ft, taus[0], N, st.q_next)
-    mlp_encode(st.local.enc, s_rows, st.F, xb=st.xb)
+    side.join(0)
     iqn_train(st.local, st.F, taus[1], bufs, st.dz_out, st.q_next.view(B, N), a_col, r_col, d_col, gamma, st.dzF,
               tile_loss=st.tile_loss)
-    arena.linear(bufs.dzc, bufs.cos, net.cos_embedding.weight.grad, net.cos_embedding.bias.grad)
+    with side.on(0):
+        arena.linear(bufs.dzc, bufs.cos, net.cos_embedding.weight.grad, net.cos_embedding.bias.grad)
+        arena.linear(st.dzF, st.xb, st.enc_dw, st.enc_db)
     arena.linear(bufs.dz1, bufs.h0, net.hidden_layer.weight.grad, net.hidden_layer.bias.grad)
-    arena.linear(bufs.dz2, bufs.h1g, net.hidden_layer_2.weight.grad, net.hidden_layer_2.bias.grad)
-    arena.linear(st.dz_out, bufs.h2, st.out_dw, st.out_db)
-    arena.linear(st.dzF, st.xb, st.enc_dw, st.enc_db)
+    with side.on(1):
+        arena.linear(bufs.dz2, bufs.h1g, net.hidden_layer_2.weight.grad, net.hidden_layer_2.bias.grad)
+        arena.linear(st.dz_out, bufs.h2, st.out_dw, st.out_db)
+    side.join()
     arena.scalar(st.tile_loss, st.loss)
     arena.flush()
     encoder_fold(st.enc_dw, st.enc_db, net)

@@ -24,8 +24,15 @@ Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | 
     actor weight grads                                   wgrad partials x5, one asvrl_partial_sums, fold
     [RCCL all-reduce] clip + Adam, re-pack actor         asvrl_adam_clip + asvrl_mlp_pack
 
+Independent launches run on side streams forked from the caller's stream and joined back
+before their results are needed (SideStreams; capturable in a HIP graph): the local encoders and
+the actor's training forward beside the target chain, and the weight-gradient reductions of
+each optimizer step on three streams. Most of these kernels fill only part of the GPU alone.
+
 Arithmetic: bf16 MFMA operands with f32 accumulation everywhere, f32 master weights / Adam.
 """
+import contextlib
+
 import torch
 
 from .fused_critic import (CriticPack, PartialArena, TrainBuffers, critic_actor_grad, critic_forward, critic_train,
@@ -35,6 +42,27 @@ from .fused_mlp import (ActorBuffers, MlpPack, actor_act, actor_backward, actor_
 from .learner import clip_and_step
 
 OBS = 40
+
+
+class SideStreams:
+    """Fork/join of independent launches onto `n` side streams of one device."""
+
+    def __init__(self, device, n=2):
+        self.streams = [torch.cuda.Stream(device=device) for _ in range(n)]
+
+    @contextlib.contextmanager
+    def on(self, i):
+        """Run the block on side stream i, after everything queued so far on the current stream."""
+        cur = torch.cuda.current_stream()
+        s = self.streams[i]
+        s.wait_stream(cur)
+        with torch.cuda.stream(s):
+            yield
+
+    def join(self, *idx):
+        cur = torch.cuda.current_stream()
+        for i in (idx or range(len(self.streams))):
+            cur.wait_stream(self.streams[i])
 
 
 def supported(policy, B, N):
@@ -78,6 +106,7 @@ class FusedACIQNState:
         self.arena = PartialArena(16 << 20, dev)
         self.losses = torch.zeros(2, **f)   # critic, actor loss (summed from per-tile partials)
         self.tile_loss = torch.zeros(2, B * N // 32, **f)
+        self.side = SideStreams(dev, 2)
 
     def target_changed(self):
         """Re-pack the target networks after a hard/soft update (eager, outside graphs)."""
@@ -102,17 +131,29 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     a_rows, r_col, d_col = rows[:, 80:82], rows[:, 82], rows[:, 83]
     bufs, ab, arena = st.bufs, st.abufs, st.arena
 
+    side = st.side
     # ---- critic (agent.py:395-416); every critic .grad is overwritten below (no zeroing)
+    with side.on(0):   # local encoders: independent of the target chain
+        mlp_encode(st.local_cenc, s_rows, st.F, st.G, act=a_rows, xb=st.xb)
+    with side.on(1):   # the actor's training forward reads only s and the (not yet updated) actor
+        actor_train_forward(st.actor, s_rows, ab)
     actor_forward(st.target_actor, ns_rows, st.na)
     mlp_encode(st.target_cenc, ns_rows, st.Ft, st.Gt, act=st.na)
     critic_forward(st.target_trunk, st.Ft, st.Gt, taus[0], N, q=st.q_next)
-    mlp_encode(st.local_cenc, s_rows, st.F, st.G, act=a_rows, xb=st.xb)
+    side.join(0)
     critic_train(st.local_trunk, st.F, st.G, taus[1], None, bufs, q_next=st.q_next.view(B, N), rewards=r_col,
                  dones=d_col, gamma=gamma, dzF=st.dzF, dzG=st.dzG, with_dFdG=False, tile_loss=st.tile_loss[0])
     ae = critic.action_encoder[0]
-    trunk_weight_grads_into(arena, critic, bufs)
-    arena.linear(st.dzF, st.xb, st.enc_dw, st.enc_db)
-    arena.small(st.dzG, a_rows, ae.weight.grad, ae.bias.grad)
+    # the six weight-gradient reductions on three streams, one partial-sum launch after the join
+    with side.on(0):
+        arena.linear(bufs.dzc, bufs.cos, critic.cos_embedding.weight.grad, critic.cos_embedding.bias.grad)
+        arena.vec(bufs.dq, bufs.h2, critic.output_layer.weight.grad, critic.output_layer.bias.grad)
+    arena.linear(bufs.dz1, bufs.h0, critic.hidden_layer.weight.grad, critic.hidden_layer.bias.grad)
+    with side.on(1):
+        arena.linear(bufs.dz2, bufs.h1g, critic.hidden_layer_2.weight.grad, critic.hidden_layer_2.bias.grad)
+        arena.linear(st.dzF, st.xb, st.enc_dw, st.enc_db)
+        arena.small(st.dzG, a_rows, ae.weight.grad, ae.bias.grad)
+    side.join()
     arena.scalar(st.tile_loss[0], st.losses[0:1])   # the critic loss
     arena.flush()                                   # one reduction launch for the six layers + loss
     encoder_fold(st.enc_dw, st.enc_db, critic)
@@ -122,18 +163,20 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     st.local_trunk.refresh()
     st.local_cenc.refresh()
 
-    # ---- actor through the updated critic (agent.py:419-427)
-    actor_train_forward(st.actor, s_rows, ab)
+    # ---- actor through the updated critic (agent.py:419-427); its forward ran on side stream 1
     mlp_encode(st.local_cenc, s_rows, st.F2, st.G2, act=ab.a_out)
     critic_actor_grad(st.local_trunk, st.F2, st.G2, taus[2], N, st.q_pi, w_ae=ae.weight, dA=ab.dA,
                       tile_loss=st.tile_loss[1])
     actor_backward(st.actor, ab)
-    arena.linear(ab.dz1, ab.h0, actor.hidden_layer.weight.grad, actor.hidden_layer.bias.grad)
-    arena.linear(ab.dz2, ab.h1, actor.hidden_layer_2.weight.grad, actor.hidden_layer_2.bias.grad)
     ow, obias = actor.output_layer.weight.grad, actor.output_layer.bias.grad
-    arena.vec(ab.dout[:, 0], ab.h2, ow[0], obias[0:1])
-    arena.vec(ab.dout[:, 1], ab.h2, ow[1], obias[1:2])
-    arena.linear(ab.dz0, ab.xb, st.enc_dw2, st.enc_db2)
+    with side.on(0):
+        arena.linear(ab.dz2, ab.h1, actor.hidden_layer_2.weight.grad, actor.hidden_layer_2.bias.grad)
+        arena.vec(ab.dout[:, 0], ab.h2, ow[0], obias[0:1])
+    arena.linear(ab.dz1, ab.h0, actor.hidden_layer.weight.grad, actor.hidden_layer.bias.grad)
+    with side.on(1):
+        arena.vec(ab.dout[:, 1], ab.h2, ow[1], obias[1:2])
+        arena.linear(ab.dz0, ab.xb, st.enc_dw2, st.enc_db2)
+    side.join()
     arena.scalar(st.tile_loss[1], st.losses[1:2])   # the actor loss
     arena.flush()
     encoder_fold(st.enc_dw2, st.enc_db2, actor)

@@ -231,13 +231,14 @@ class VecTrainer:
             out = self.learn() if do_learn else None
             self.env.advance_device()
             return out
+        # the learner runs on the current stream and the rollout on a side stream: HIP graph
+        # capture (ROCm 7) segfaults at capture end on a stream forked from an already forked
+        # stream, and the learner forks side streams of its own (fused_update.SideStreams)
         main = torch.cuda.current_stream(self.device)
         if self._streams is None:
-            self._streams = (torch.cuda.Stream(device=self.device), torch.cuda.Stream(device=self.device),
-                             torch.cuda.Event(), torch.cuda.Event())
-        s_roll, s_learn, ev_snap, ev_act = self._streams
+            self._streams = (torch.cuda.Stream(device=self.device), torch.cuda.Event(), torch.cuda.Event())
+        s_roll, ev_snap, ev_act = self._streams
         s_roll.wait_stream(main)
-        s_learn.wait_stream(main)
         with torch.cuda.stream(s_roll):
             self.ring_snap.copy_(self.replay.state)
             ev_snap.record(s_roll)
@@ -248,11 +249,9 @@ class VecTrainer:
             self._push()
             env.auto_reset()
             env.advance_device()
-        with torch.cuda.stream(s_learn):
-            s_learn.wait_event(ev_snap)
-            out = self.learn(state=self.ring_snap, guard=self.E * self.R, actor_wait=ev_act)
+        main.wait_event(ev_snap)
+        out = self.learn(state=self.ring_snap, guard=self.E * self.R, actor_wait=ev_act)
         main.wait_stream(s_roll)
-        main.wait_stream(s_learn)
         return out
 
     def iteration(self, timing=None):

@@ -28,7 +28,7 @@ def main():
     fam = collections.defaultdict(lambda: [0, 0.0])
     busy = 0.0
     for r in rows[i0:i1]:
-        name = re.sub(r"\(.*", "", r[0])
+        name = re.sub(r"\(.*", "", r[0].replace("(anonymous namespace)::", "").replace("void ", ""))
         d = (r[2] - r[1]) / 1e3
         busy += d
         key = name[:70]
