@@ -113,9 +113,12 @@ class AsvIqnIO(C.Structure):
 MAX_SUM_SEGS = 8
 
 
+SUM_PLAIN, SUM_FOLD_ENCODERS = 0, 1
+
+
 class AsvPartialSum(C.Structure):
     _fields_ = [("partial", _VP), ("dw", _VP), ("db", _VP), ("groups", _I32), ("nw", _I32), ("nb", _I32),
-                ("accumulate", _I32)]
+                ("accumulate", _I32), ("stride", _I32), ("boff", _I32), ("mode", _I32), ("norm", _I32)]
 
 
 class AsvMlpSrc(C.Structure):
@@ -164,6 +167,9 @@ EXPORTS = [
     ("asvrl_linear_wgrad_vec_partial", C.c_int, [_VP, _I64, _VP, _I64, _I32, _I32, _VP, _I64, _VP, _VP]),
     ("asvrl_small_wgrad_partial", C.c_int, [_VP, _I64, _VP, _I64, _I32, _I32, _I32, _VP, _I64, _VP, _VP]),
     ("asvrl_partial_sums", C.c_int, [_VP, _I32, _VP]),
+    ("asvrl_partial_sums_norm", C.c_int, [_VP, _I32, _VP, _VP, _VP]),
+    ("asvrl_partial_sums_norm_parts", _I32, [_VP, _I32]),
+    ("asvrl_adam_step", C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, _F, _F, _VP, _VP, _I32, _VP]),
     ("asvrl_linear_wgrad", C.c_int, [_VP, _I64, _VP, _I64, _I32, _I32, _I32, _VP, _VP, _I32, _VP, _I64, _VP]),
     ("asvrl_linear_wgrad_vec", C.c_int, [_VP, _I64, _VP, _I64, _I32, _I32, _VP, _VP, _I32, _VP, _I64, _VP]),
     ("asvrl_mlp_pack", C.c_int, [C.POINTER(AsvMlpSrc), C.POINTER(AsvMlpWeights), _VP]),

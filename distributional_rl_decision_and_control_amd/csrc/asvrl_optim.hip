@@ -38,17 +38,23 @@ __global__ __launch_bounds__(kOptThreads) void sumsq_kernel(const float* __restr
 
 __global__ __launch_bounds__(kOptThreads) void adam_kernel(float* __restrict__ p, float* __restrict__ g,
                                                             float* __restrict__ m, float* __restrict__ v, int64_t n,
-                                                            const double* __restrict__ partial,
+                                                            const double* __restrict__ partial, int nparts,
                                                             const float* __restrict__ step, float lr, float beta1,
                                                             float beta2, float eps, float max_norm,
                                                             float* __restrict__ norm_out) {
   __shared__ float s_coef;
-  if (threadIdx.x < kWave) {
-    double x = threadIdx.x < kNormBlocks ? partial[threadIdx.x] : 0.0;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, kWave);  // same value in every lane/block
-    const float norm = static_cast<float>(sqrt(x));
+  __shared__ double s_red[kOptThreads];
+  {   // thread t folds partials t, t + 256, ... in order, then a fixed tree: the same in every block
+    double x = 0.0;
+    for (int k = threadIdx.x; k < nparts; k += kOptThreads) x += partial[k];
+    s_red[threadIdx.x] = x;
+    __syncthreads();
+    for (int w = kOptThreads / 2; w > 0; w >>= 1) {
+      if (threadIdx.x < w) s_red[threadIdx.x] += s_red[threadIdx.x + w];
+      __syncthreads();
+    }
     if (threadIdx.x == 0) {
+      const float norm = static_cast<float>(sqrt(s_red[0]));
       float coef = 1.f;
       if (max_norm > 0.f) {
         coef = max_norm / (norm + 1e-6f);   // clip_grad_norm_: clip_coef, clamped to 1
@@ -95,6 +101,21 @@ extern "C" int asvrl_adam_clip(float* params, float* grads, float* exp_avg, floa
   int64_t nb = (n + 4LL * kOptThreads - 1) / (4LL * kOptThreads);
   nb = nb < 1 ? 1 : (nb > 1024 ? 1024 : nb);
   hipLaunchKernelGGL(adam_kernel, dim3(static_cast<unsigned>(nb)), dim3(kOptThreads), 0, as_stream(stream), params,
-                     grads, exp_avg, exp_avg_sq, n, work, step, lr, beta1, beta2, eps, max_norm, norm_out);
+                     grads, exp_avg, exp_avg_sq, n, work, kNormBlocks, step, lr, beta1, beta2, eps, max_norm, norm_out);
   return check_launch("asvrl_adam_clip(step)");
+}
+
+extern "C" int asvrl_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+                               const float* step, float lr, float beta1, float beta2, float eps, float max_norm,
+                               float* norm_out, const double* norm_parts, int32_t nparts, void* stream) {
+  ASVRL_REQUIRE(params && grads && exp_avg && exp_avg_sq && step && norm_parts && nparts >= 1,
+                "asvrl_adam_step: null argument");
+  ASVRL_REQUIRE(n >= 0, "asvrl_adam_step: negative size");
+  if (n == 0) return 0;
+  int64_t nb = (n + 4LL * kOptThreads - 1) / (4LL * kOptThreads);
+  nb = nb < 1 ? 1 : (nb > 1024 ? 1024 : nb);
+  hipLaunchKernelGGL(adam_kernel, dim3(static_cast<unsigned>(nb)), dim3(kOptThreads), 0, as_stream(stream), params,
+                     grads, exp_avg, exp_avg_sq, n, norm_parts, nparts, step, lr, beta1, beta2, eps, max_norm,
+                     norm_out);
+  return check_launch("asvrl_adam_step");
 }

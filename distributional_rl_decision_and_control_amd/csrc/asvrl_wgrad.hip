@@ -200,30 +200,54 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_vec_kernel(const float* __re
   }
 }
 
-// out[i] (+)= sum_g partial[g][i], i < nw + nb (the trailing nb go to db). A block covers 64
-// outputs; its 4 waves take groups g = 4u + wave with two independent accumulators each, and
-// the 4 wave sums are folded in a fixed order (deterministic).
-__global__ __launch_bounds__(kWgThreads) void partial_sum_kernel(const float* __restrict__ partial, int groups,
-                                                                  int nw, int nb, float* __restrict__ dw,
-                                                                  float* __restrict__ db, int accumulate) {
+// Partial reductions: a block covers 64 outputs; its kSumWaves waves take groups
+// k = kSumWaves u + wave with two independent accumulators each, and the wave sums are folded by
+// a fixed tree (deterministic, and the same order in every reduction launch).
+#ifndef ASVRL_SUM_WAVES
+#define ASVRL_SUM_WAVES 8
+#endif
+constexpr int kSumWaves = ASVRL_SUM_WAVES, kSumThreads = kSumWaves * 64;
+static_assert(kSumWaves >= 2 && kSumWaves <= 16 && (kSumWaves & (kSumWaves - 1)) == 0, "power-of-two waves");
+
+// pairwise tree over the wave sums: (((r0 + r1) + (r2 + r3)) + ...)
+template <int W>
+__device__ __forceinline__ float tree_at(float (*red)[64], int lane, int base) {
+  if constexpr (W == 1) return red[base][lane];
+  else return tree_at<W / 2>(red, lane, base) + tree_at<W / 2>(red, lane, base + W / 2);
+}
+__device__ __forceinline__ float sum_tree(float (*red)[64], int lane) { return tree_at<kSumWaves>(red, lane, 0); }
+
+// Fixed-order sum over the groups of partial[k * stride + idx] for this thread's lane. Every
+// thread of the block must call it (it synchronises) and receives the same sum for its lane.
+__device__ __forceinline__ float group_sum(const float* __restrict__ p, int groups, int stride, int idx, bool valid,
+                                           int wv, int lane, float (*red)[64]) {
+  float s0 = 0.f, s1 = 0.f;
+  if (valid) {
+    int k = wv;
+    for (; k + kSumWaves < groups; k += 2 * kSumWaves) {
+      s0 += p[static_cast<int64_t>(k) * stride + idx];
+      s1 += p[static_cast<int64_t>(k + kSumWaves) * stride + idx];
+    }
+    if (k < groups) s0 += p[static_cast<int64_t>(k) * stride + idx];
+  }
+  red[wv][lane] = s0 + s1;
+  __syncthreads();
+  const float s = sum_tree(red, lane);
+  __syncthreads();
+  return s;
+}
+
+// out[i] (+)= sum_g partial[g][i], i < nw + nb (the trailing nb go to db).
+__global__ __launch_bounds__(kSumThreads) void partial_sum_kernel(const float* __restrict__ partial, int groups,
+                                                                   int nw, int nb, float* __restrict__ dw,
+                                                                   float* __restrict__ db, int accumulate) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + lane;
   const int n = nw + nb;
-  float s0 = 0.f, s1 = 0.f;
-  if (i < n) {
-    int g = wv;
-    for (; g + 4 < groups; g += 8) {
-      s0 += partial[static_cast<int64_t>(g) * n + i];
-      s1 += partial[static_cast<int64_t>(g + 4) * n + i];
-    }
-    if (g < groups) s0 += partial[static_cast<int64_t>(g) * n + i];
-  }
-  __shared__ float red[4][64];
-  red[wv][lane] = s0 + s1;
-  __syncthreads();
+  __shared__ float red[kSumWaves][64];
+  const float s = group_sum(partial, groups, n, i, i < n, wv, lane, red);
   if (wv != 0 || i >= n) return;
   if (i >= nw && db == nullptr) return;
-  const float s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
   float* o = i < nw ? dw + i : db + (i - nw);
   *o = accumulate ? *o + s : s;
 }
@@ -231,47 +255,157 @@ __global__ __launch_bounds__(kWgThreads) void partial_sum_kernel(const float* __
 // Several independent partial reductions in one launch: blockIdx.y = segment.
 struct SumSegs {
   AsvPartialSum seg[ASVRL_MAX_SUM_SEGS];
+  int slot0[ASVRL_MAX_SUM_SEGS];   // first norm slot of each segment's working blocks
 };
 
-__global__ __launch_bounds__(kWgThreads) void partial_sums_kernel(SumSegs t) {
+// group_sum for the five object copies of a fold output at once: one pass over the groups, each
+// copy accumulated in group_sum's order (bit-identical to five group_sum calls), one tree
+__device__ __forceinline__ void group_sum5(const float* __restrict__ p, int groups, int stride, const int* idx,
+                                           const bool* valid, int wv, int lane, float (*red5)[kSumWaves][64],
+                                           float* out) {
+  float s0[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, s1[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  int k = wv;
+  for (; k + kSumWaves < groups; k += 2 * kSumWaves) {
+#pragma unroll
+    for (int o = 0; o < 5; ++o)
+      if (valid[o]) {
+        s0[o] += p[static_cast<int64_t>(k) * stride + idx[o]];
+        s1[o] += p[static_cast<int64_t>(k + kSumWaves) * stride + idx[o]];
+      }
+  }
+  if (k < groups) {
+#pragma unroll
+    for (int o = 0; o < 5; ++o)
+      if (valid[o]) s0[o] += p[static_cast<int64_t>(k) * stride + idx[o]];
+  }
+#pragma unroll
+  for (int o = 0; o < 5; ++o) red5[o][wv][lane] = s0[o] + s1[o];
+  __syncthreads();
+#pragma unroll
+  for (int o = 0; o < 5; ++o) out[o] = sum_tree(red5[o], lane);
+}
+
+// ASVRL_SUM_FOLD_ENCODERS: output t of [self_w 56x7 | self_b 56 | obj_w 40x5 | obj_b 40] and the
+// image entry of its o-th copy (self entries: o = 0 only), as asvrl_encoder_fold reads them
+constexpr int kFoldSelfF = 56, kFoldSelfIn = 7, kFoldObjF = 40, kFoldObjIn = 5, kFoldObjN = 5, kFoldK = 32;
+constexpr int kFoldOut = kFoldSelfF * kFoldSelfIn + kFoldSelfF + kFoldObjF * kFoldObjIn + kFoldObjF;
+__device__ __forceinline__ bool fold_index(int t, int o, int boff, int& idx) {
+  if (t < kFoldSelfF * kFoldSelfIn) {
+    idx = (t / kFoldSelfIn) * kFoldK + t % kFoldSelfIn;
+    return o == 0;
+  }
+  t -= kFoldSelfF * kFoldSelfIn;
+  if (t < kFoldSelfF) {
+    idx = boff + t;
+    return o == 0;
+  }
+  t -= kFoldSelfF;
+  if (t < kFoldObjF * kFoldObjIn) {
+    const int j = t / kFoldObjIn, c = t % kFoldObjIn;
+    idx = (kFoldSelfF + kFoldObjF * o + j) * kFoldK + kFoldSelfIn + kFoldObjIn * o + c;
+    return true;
+  }
+  t -= kFoldObjF * kFoldObjIn;
+  idx = boff + kFoldSelfF + kFoldObjF * o + t;
+  return t < kFoldObjF;
+}
+
+// Grid (blocks, segments); block x of a segment owns outputs [64x, 64x + 64) (a scalar segment:
+// block 0 alone, all threads). With sq_blocks, every working block also writes the sum of the
+// squares of the outputs it wrote (segments with norm = 1) to its slot, for asvrl_adam_step.
+__global__ __launch_bounds__(kSumThreads) void partial_sums_kernel(SumSegs t, double* sq_blocks, float* step) {
   const AsvPartialSum& g = t.seg[blockIdx.y];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __shared__ float red[kSumWaves][64];
+  double sq = 0.0;
   if (g.nw + g.nb == 1) {   // scalar over many groups: the whole block, fixed order
-    if (blockIdx.x != 0) return;
-    float acc = 0.f;
-    for (int k = threadIdx.x; k < g.groups; k += kWgThreads) acc += g.partial[k];
+    if (blockIdx.x == 0) {
+      float acc = 0.f;
+      for (int k = threadIdx.x; k < g.groups; k += kSumThreads) acc += g.partial[k];
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, kWave);
-    __shared__ float wsum[kWgThreads / kWave];
-    if (lane == 0) wsum[wv] = acc;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const float s = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
-      float* o = g.nw == 1 ? g.dw : g.db;
-      *o = g.accumulate ? *o + s : s;
+      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, kWave);
+      if (lane == 0) red[wv][0] = acc;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const float s = sum_tree(red, 0);
+        float* o = g.nw == 1 ? g.dw : g.db;
+        *o = g.accumulate ? *o + s : s;
+        if (g.norm) sq += static_cast<double>(*o) * *o;
+      }
     }
-    return;
-  }
-  const int i = blockIdx.x * 64 + lane;
-  const int n = g.nw + g.nb;
-  if (blockIdx.x * 64 >= n) return;   // block-uniform
-  float s0 = 0.f, s1 = 0.f;
-  if (i < n) {
-    int k = wv;
-    for (; k + 4 < g.groups; k += 8) {
-      s0 += g.partial[static_cast<int64_t>(k) * n + i];
-      s1 += g.partial[static_cast<int64_t>(k + 4) * n + i];
+  } else if (blockIdx.x * 64 < g.nw + g.nb) {   // block-uniform
+    const int i = blockIdx.x * 64 + lane;
+    const int n = g.nw + g.nb;
+    const int stride = g.stride != 0 ? g.stride : n;
+    const int boff = g.boff != 0 ? g.boff : g.nw;
+    float s;
+    if (g.mode == ASVRL_SUM_FOLD_ENCODERS) {
+      __shared__ float red5[kFoldObjN][kSumWaves][64];
+      int idx[kFoldObjN];
+      bool v[kFoldObjN];
+      float so[kFoldObjN];
+#pragma unroll
+      for (int o = 0; o < kFoldObjN; ++o) {
+        idx[o] = 0;
+        v[o] = i < n && fold_index(i, o, boff, idx[o]);
+      }
+      group_sum5(g.partial, g.groups, stride, idx, v, wv, lane, red5, so);
+      s = 0.f;   // the copies in object order (asvrl_encoder_fold)
+#pragma unroll
+      for (int o = 0; o < kFoldObjN; ++o)
+        if (v[o]) s += so[o];
+    } else {
+      const int idx = i < g.nw ? i : boff + (i - g.nw);
+      s = group_sum(g.partial, g.groups, stride, idx, i < n, wv, lane, red);
     }
-    if (k < g.groups) s0 += g.partial[static_cast<int64_t>(k) * n + i];
+    if (wv == 0 && i < n && !(i >= g.nw && g.db == nullptr)) {
+      float* o = i < g.nw ? g.dw + i : g.db + (i - g.nw);
+      const float out = g.accumulate ? *o + s : s;
+      *o = out;
+      if (g.norm) sq = static_cast<double>(out) * out;
+    }
   }
-  __shared__ float red[4][64];
-  red[wv][lane] = s0 + s1;
-  __syncthreads();
-  if (wv != 0 || i >= n) return;
-  if (i >= g.nw && g.db == nullptr) return;
-  const float s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
-  float* o = i < g.nw ? g.dw + i : g.db + (i - g.nw);
-  *o = g.accumulate ? *o + s : s;
+  if (sq_blocks == nullptr) return;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) step[0] += 1.f;   // read by the next launch
+  // ---- squared norm: this working block's sum (wave 0 holds the outputs) into its own slot
+  const int nb = (g.nw + g.nb == 1) ? 1 : (g.nw + g.nb + 63) / 64;
+  if (static_cast<int>(blockIdx.x) >= nb || wv != 0) return;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) sq += __shfl_xor(sq, off, kWave);
+  if (lane == 0) sq_blocks[t.slot0[blockIdx.y] + blockIdx.x] = sq;
+}
+
+int sum_grid_x(const AsvPartialSum* segs, int nseg) {
+  int maxn = 0;
+  for (int k = 0; k < nseg; ++k) maxn = std::max(maxn, segs[k].nw + segs[k].nb);
+  return (maxn + 63) / 64;
+}
+
+// norm slots: one per working block of each segment, segments in order
+int norm_slots(const AsvPartialSum* segs, int nseg, int* slot0) {
+  int n = 0;
+  for (int k = 0; k < nseg; ++k) {
+    if (slot0 != nullptr) slot0[k] = n;
+    const int w = segs[k].nw + segs[k].nb;
+    n += w == 1 ? 1 : (w + 63) / 64;
+  }
+  return n;
+}
+
+int launch_partial_sums(const AsvPartialSum* segs, int nseg, double* sq_blocks, float* step, hipStream_t st) {
+  SumSegs t{};
+  for (int k = 0; k < nseg; ++k) {
+    const AsvPartialSum& g = segs[k];
+    ASVRL_REQUIRE(g.partial && g.dw && g.groups >= 0, "asvrl_partial_sums: null segment");
+    ASVRL_REQUIRE(g.mode == ASVRL_SUM_PLAIN || g.mode == ASVRL_SUM_FOLD_ENCODERS, "asvrl_partial_sums: bad mode");
+    ASVRL_REQUIRE(g.mode != ASVRL_SUM_FOLD_ENCODERS || (g.nw == kFoldOut && g.nb == 0),
+                  "asvrl_partial_sums: the encoder fold writes 688 outputs (nw = 688, nb = 0)");
+    t.seg[k] = g;
+  }
+  norm_slots(segs, nseg, t.slot0);
+  hipLaunchKernelGGL(partial_sums_kernel, dim3(sum_grid_x(segs, nseg), nseg), dim3(kSumThreads), 0, st, t, sq_blocks,
+                     step);
+  return check_launch("asvrl_partial_sums");
 }
 
 int wgrad_groups(int R, int M, int K) {
@@ -308,7 +442,7 @@ int launch_wgrad(const __bf16* dz, int64_t ldz, const __bf16* x, int64_t ldx, in
 int launch_partial_sum(const float* partial, int groups, int nw, int nb, float* dw, float* db, int accumulate,
                        hipStream_t st) {
   const int n = nw + nb;
-  hipLaunchKernelGGL(partial_sum_kernel, dim3((n + 63) / 64), dim3(kWgThreads), 0, st, partial, groups, nw, nb, dw,
+  hipLaunchKernelGGL(partial_sum_kernel, dim3((n + 63) / 64), dim3(kSumThreads), 0, st, partial, groups, nw, nb, dw,
                      db, accumulate);
   return check_launch("partial_sum");
 }
@@ -365,15 +499,19 @@ extern "C" int asvrl_linear_wgrad(const void* dz, int64_t ldz, const void* x, in
 extern "C" int asvrl_partial_sums(const AsvPartialSum* segs, int32_t nseg, void* stream) {
   ASVRL_REQUIRE(segs && nseg >= 0 && nseg <= ASVRL_MAX_SUM_SEGS, "asvrl_partial_sums: bad segment table");
   if (nseg == 0) return 0;
-  SumSegs t{};
-  int maxn = 0;
-  for (int k = 0; k < nseg; ++k) {
-    ASVRL_REQUIRE(segs[k].partial && segs[k].dw && segs[k].groups >= 0, "asvrl_partial_sums: null segment");
-    t.seg[k] = segs[k];
-    maxn = std::max(maxn, segs[k].nw + segs[k].nb);
-  }
-  hipLaunchKernelGGL(partial_sums_kernel, dim3((maxn + 63) / 64, nseg), dim3(kWgThreads), 0, as_stream(stream), t);
-  return check_launch("asvrl_partial_sums");
+  return launch_partial_sums(segs, nseg, nullptr, nullptr, as_stream(stream));
+}
+
+extern "C" int32_t asvrl_partial_sums_norm_parts(const AsvPartialSum* segs, int32_t nseg) {
+  if (segs == nullptr || nseg <= 0 || nseg > ASVRL_MAX_SUM_SEGS) return 0;
+  return norm_slots(segs, nseg, nullptr);
+}
+
+extern "C" int asvrl_partial_sums_norm(const AsvPartialSum* segs, int32_t nseg, double* norm_parts, float* step,
+                                       void* stream) {
+  ASVRL_REQUIRE(segs && nseg >= 1 && nseg <= ASVRL_MAX_SUM_SEGS, "asvrl_partial_sums_norm: bad segment table");
+  ASVRL_REQUIRE(norm_parts && step, "asvrl_partial_sums_norm: null argument");
+  return launch_partial_sums(segs, nseg, norm_parts, step, as_stream(stream));
 }
 
 extern "C" int asvrl_linear_wgrad_vec_partial(const float* dq, int64_t ldq, const void* x, int64_t ldx, int32_t R,

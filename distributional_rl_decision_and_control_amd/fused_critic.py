@@ -192,6 +192,9 @@ class PartialArena:
         self.buf = torch.empty(int(floats), dtype=torch.float32, device=device)
         self.off = 0
         self.segs = []
+        # flush(norm=...): per-workgroup squared-norm partials
+        self.norm_parts = torch.zeros(_abi.MAX_SUM_SEGS * 1024, dtype=torch.float64, device=device)
+        self.nparts = 0
 
     def _take(self, n):
         if self.off + n > self.buf.numel():
@@ -200,15 +203,16 @@ class PartialArena:
         self.off += (n + 63) // 64 * 64
         return t
 
-    def _seg(self, part, dw, db, groups, nw, nb, accumulate):
+    def _seg(self, part, dw, db, groups, nw, nb, accumulate, stride=0, boff=0, mode=_abi.SUM_PLAIN, norm=True):
         g = _abi.AsvPartialSum()
         g.partial, g.dw, g.db = part.data_ptr(), dw.data_ptr(), (db.data_ptr() if db is not None else None)
         g.groups, g.nw, g.nb, g.accumulate = groups, nw, nb, int(accumulate)
+        g.stride, g.boff, g.mode, g.norm = stride, boff, mode, int(norm)
         self.segs.append(g)
         if len(self.segs) == _abi.MAX_SUM_SEGS:
             self.flush()
 
-    def linear(self, dz, x, dw, db, accumulate=False, stream=None):
+    def _linear_partial(self, dz, x, stream):
         R, M = dz.shape
         K = x.shape[1]
         L = _abi.lib()
@@ -217,7 +221,28 @@ class PartialArena:
         _abi.check(L.asvrl_linear_wgrad_partial(_abi.ptr(dz), dz.stride(0), _abi.ptr(x), x.stride(0), R, M, K,
                                                 _abi.ptr(part), part.numel(), C.byref(groups),
                                                 _abi.stream_ptr(stream)), "asvrl_linear_wgrad_partial")
-        self._seg(part, dw, db, groups.value, M * K, M, accumulate)
+        return part, groups.value, M, K
+
+    def linear(self, dz, x, dw, db, accumulate=False, stream=None):
+        """dw (<= M rows of K) <- dz^T x, db <- dz.sum(0); a dw / db with fewer rows than dz's M
+        columns takes the leading rows (a padded 32-row output layer)."""
+        part, groups, M, K = self._linear_partial(dz, x, stream)
+        assert dw.numel() % K == 0 and dw.numel() <= M * K and (db is None or db.numel() <= M)
+        self._seg(part, dw, db, groups, dw.numel(), db.numel() if db is not None else M, accumulate,
+                  stride=M * K + M, boff=M * K)
+
+    def fold(self, dz, x, net, stream=None):
+        """The observation encoders' gradients of `net` from the 256 x 32 encoder-image rows
+        (dz [R][256], x [R][32] bf16), folded in the reduction itself (ASVRL_SUM_FOLD_ENCODERS)."""
+        se, oe = net.self_encoder[0], net.object_encoder[0]
+        gs = [se.weight.grad, se.bias.grad, oe.weight.grad, oe.bias.grad]
+        contiguous = all(gs[k].data_ptr() + 4 * gs[k].numel() == gs[k + 1].data_ptr() for k in range(3))
+        if not contiguous:   # separate gradient tensors: plain sum into scratch + asvrl_encoder_fold
+            raise RuntimeError("PartialArena.fold needs the encoder gradients contiguous (FusedAdam / FlatGrads)")
+        part, groups, M, K = self._linear_partial(dz, x, stream)
+        assert (M, K) == (256, 32)
+        self._seg(part, gs[0], None, groups, 688, 0, False, stride=M * K + M, boff=M * K,
+                  mode=_abi.SUM_FOLD_ENCODERS)
 
     def vec(self, dq, x, dw, db, accumulate=False, stream=None):
         R, K = x.shape
@@ -231,7 +256,7 @@ class PartialArena:
 
     def scalar(self, partials, out, accumulate=False):
         """out (1 f32) (+)= sum(partials): a scalar segment (e.g. per-tile loss partials)."""
-        self._seg(partials, out, None, partials.numel(), 1, 0, accumulate)
+        self._seg(partials, out, None, partials.numel(), 1, 0, accumulate, norm=False)
 
     def small(self, dz, x, dw, db, accumulate=False, stream=None):
         R, M = dz.shape
@@ -243,11 +268,23 @@ class PartialArena:
                                                         _abi.stream_ptr(stream)), "asvrl_small_wgrad_partial")
         self._seg(part, dw, db, groups.value, M * K, M, accumulate)
 
-    def flush(self, stream=None):
+    def flush(self, stream=None, norm=None):
+        """One reduction launch for the queued segments. norm: a FusedAdam whose gradients are
+        exactly these segments' outputs; the launch then also leaves the squared-norm partials in
+        self.norm_parts[:self.nparts] and advances its step, for norm.step_prenormed(...)."""
         if self.segs:
             arr = (_abi.AsvPartialSum * len(self.segs))(*self.segs)
-            _abi.check(_abi.lib().asvrl_partial_sums(arr, len(self.segs), _abi.stream_ptr(stream)),
-                       "asvrl_partial_sums")
+            L = _abi.lib()
+            if norm is not None:
+                self.nparts = int(L.asvrl_partial_sums_norm_parts(arr, len(self.segs)))
+                assert 1 <= self.nparts <= self.norm_parts.numel()
+                _abi.check(L.asvrl_partial_sums_norm(arr, len(self.segs), _abi.ptr(self.norm_parts),
+                                                     _abi.ptr(norm.step_t), _abi.stream_ptr(stream)),
+                           "asvrl_partial_sums_norm")
+            else:
+                _abi.check(L.asvrl_partial_sums(arr, len(self.segs), _abi.stream_ptr(stream)), "asvrl_partial_sums")
+        elif norm is not None:
+            raise RuntimeError("PartialArena.flush(norm=...) with nothing queued")
         self.segs = []
         self.off = 0
 

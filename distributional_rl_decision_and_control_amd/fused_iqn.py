@@ -10,9 +10,13 @@ replay batch `rows` ([B][88]: obs | next obs | action | reward | done):
     local encoders(s) -> F (+ bf16 obs copy)              asvrl_mlp_encode
     forward, gather at a, quantile-Huber vs r + g q_next (1-d), backward
                                                           asvrl_iqn_train (2 launches, agent.py:455-468)
-    weight grads of the 4 trunk layers + encoders         asvrl_linear_wgrad_partial x5,
-                                                          ONE asvrl_partial_sums (+ the loss), fold
-    [RCCL all-reduce] clip + Adam                         asvrl_adam_clip          (agent.py:471-472)
+    weight grads of the 4 trunk layers + encoders         asvrl_linear_wgrad_partial x5 (3 streams),
+                                                          ONE asvrl_partial_sums_norm: every .grad
+                                                          (encoders folded, the 32-row output
+                                                          reduction into the 25-row layer), the
+                                                          loss and the gradient norm
+    clip + Adam                                           asvrl_adam_step          (agent.py:471-472)
+      (with DP: asvrl_partial_sums, RCCL all-reduce, asvrl_adam_clip)
     re-pack trunk, head and encoders                      asvrl_iqn_pack + asvrl_mlp_pack
 
 act_iqn for every robot row: encoders, then one kernel (K = 32 quantile samples per state,
@@ -26,9 +30,8 @@ import torch
 
 from . import _abi
 from .fused_critic import CriticPack, PartialArena, TrainBuffers
-from .fused_update import SideStreams
-from .fused_mlp import MlpPack, encoder_fold, mlp_encode
-from .learner import clip_and_step
+from .fused_update import SideStreams, _reduce_and_step
+from .fused_mlp import MlpPack, mlp_encode
 
 OBS = 40
 K_ACT = 32
@@ -127,9 +130,6 @@ class FusedIQNState:
         self.q_next = torch.empty(B * N, **f)
         self.dzF = torch.empty(B, 256, **bf)
         self.dz_out = torch.empty(B * N, _abi.IQN_MAX_ACTIONS, **bf)
-        self.enc_dw, self.enc_db = torch.empty(256, 32, **f), torch.empty(256, **f)
-        self.out_dw = torch.empty(_abi.IQN_MAX_ACTIONS, 128, **f)
-        self.out_db = torch.empty(_abi.IQN_MAX_ACTIONS, **f)
         self.arena = PartialArena(16 << 20, dev)
         self.loss = torch.zeros(1, **f)
         self.tile_loss = torch.zeros(B * N // 32, **f)
@@ -148,9 +148,10 @@ class FusedIQNState:
         iqn_act(self.local, self.F_act, actions64, step_dev, steps_per_count, total, fraction, initial, final, seed)
 
 
-def iqn_grads(st, net, rows, taus, gamma=0.99):
-    """Loss (st.loss) and every parameter .grad of train_IQN's backward (agent.py:449-468) for
-    replay rows [B][88] and taus (2, B, N) = (target, local)."""
+def iqn_grads(st, net, rows, taus, gamma=0.99, flush=True):
+    """train_IQN's backward (agent.py:449-468) for replay rows [B][88] and taus (2, B, N) =
+    (target, local): every parameter .grad and st.loss. flush=False leaves the weight-gradient
+    partials queued on st.arena (the update reduces them together with the gradient norm)."""
     B, N = st.B, st.N
     s_rows, ns_rows = rows[:, 0:OBS], rows[:, OBS:2 * OBS]
     a_col, r_col, d_col = rows[:, 80], rows[:, 82], rows[:, 83]
@@ -165,18 +166,16 @@ def iqn_grads(st, net, rows, taus, gamma=0.99):
               tile_loss=st.tile_loss)
     with side.on(0):
         arena.linear(bufs.dzc, bufs.cos, net.cos_embedding.weight.grad, net.cos_embedding.bias.grad)
-        arena.linear(st.dzF, st.xb, st.enc_dw, st.enc_db)
+        arena.fold(st.dzF, st.xb, net)   # encoder image -> self/object encoder grads
     arena.linear(bufs.dz1, bufs.h0, net.hidden_layer.weight.grad, net.hidden_layer.bias.grad)
     with side.on(1):
         arena.linear(bufs.dz2, bufs.h1g, net.hidden_layer_2.weight.grad, net.hidden_layer_2.bias.grad)
-        arena.linear(st.dz_out, bufs.h2, st.out_dw, st.out_db)
+        # the padded 32-row output reduction fills the A-row output layer directly
+        arena.linear(st.dz_out, bufs.h2, net.output_layer.weight.grad, net.output_layer.bias.grad)
     side.join()
     arena.scalar(st.tile_loss, st.loss)
-    arena.flush()
-    encoder_fold(st.enc_dw, st.enc_db, net)
-    A = st.A
-    net.output_layer.weight.grad.copy_(st.out_dw[:A])
-    net.output_layer.bias.grad.copy_(st.out_db[:A])
+    if flush:
+        arena.flush()
 
 
 def iqn_update_fused(st, net, opt, grads, rows, gamma=0.99, taus=None, sync=None, max_norm=0.5, act_wait=None):
@@ -185,11 +184,7 @@ def iqn_update_fused(st, net, opt, grads, rows, gamma=0.99, taus=None, sync=None
     Returns (loss, grad_norm) as device scalars."""
     if taus is None:
         taus = torch.rand(2, st.B, st.N, device=st.device)
-    iqn_grads(st, net, rows, taus, gamma)
-    if sync is not None:
-        sync(grads)
-    if act_wait is not None:
-        torch.cuda.current_stream().wait_event(act_wait)
-    gn = clip_and_step(opt, grads, max_norm)
+    iqn_grads(st, net, rows, taus, gamma, flush=False)
+    gn = _reduce_and_step(st.arena, opt, grads, sync, max_norm, wait=act_wait)
     st.local.refresh()
     return st.loss[0], gn

@@ -1,5 +1,5 @@
 """The whole AC-IQN update (Agent.train_AC_IQN, agent.py:386-432) on hand-written gfx950
-kernels: about 40 launches per step, no torch autograd, no host synchronisation.
+kernels: about 35 launches per step, no torch autograd, no host synchronisation.
 
 Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | done):
   critic (agent.py:395-416)
@@ -10,19 +10,20 @@ Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | 
     trunk forward + quantile-Huber vs r + g q_next (1-d) + backward
                                                           asvrl_critic_train (targets formed in-kernel)
     trunk weight grads                                   asvrl_linear_wgrad_partial x3 + _vec
-    encoder grads (256x32 image, folded) and action-encoder grads
-                                                          asvrl_linear_wgrad_partial + _small_wgrad_partial,
-                                                          ONE asvrl_partial_sums for all six layers,
-                                                          asvrl_encoder_fold
-    [RCCL all-reduce] clip + Adam                        asvrl_adam_clip
+    encoder grads (256x32 image) and action-encoder grads
+                                                          asvrl_linear_wgrad_partial + _small_wgrad_partial
+    every .grad (encoders folded in the reduction), the loss and the global gradient norm
+                                                          ONE asvrl_partial_sums_norm
+    clip + Adam                                          asvrl_adam_step
+      (with DP: asvrl_partial_sums, RCCL all-reduce, asvrl_adam_clip)
     re-pack trunk and encoders                           asvrl_critic_pack + asvrl_mlp_pack
   actor (agent.py:419-427), through the UPDATED critic
     actor(s) saving activations -> a                     asvrl_actor_forward(TRAIN)
     encoders(s, a) -> F2, G2                             asvrl_mlp_encode
     trunk forward + backward of -mean(q) to the action   asvrl_critic_actor_grad (dA in-kernel)
     actor backward                                       asvrl_actor_backward
-    actor weight grads                                   wgrad partials x5, one asvrl_partial_sums, fold
-    [RCCL all-reduce] clip + Adam, re-pack actor         asvrl_adam_clip + asvrl_mlp_pack
+    actor weight grads                                   wgrad partials x5, one asvrl_partial_sums_norm
+    clip + Adam, re-pack actor                           asvrl_adam_step + asvrl_mlp_pack
 
 Independent launches run on side streams forked from the caller's stream and joined back
 before their results are needed (SideStreams; capturable in a HIP graph): the local encoders and
@@ -37,9 +38,8 @@ import torch
 
 from .fused_critic import (CriticPack, PartialArena, TrainBuffers, critic_actor_grad, critic_forward, critic_train,
                            trunk_weight_grads_into)
-from .fused_mlp import (ActorBuffers, MlpPack, actor_act, actor_backward, actor_forward, actor_train_forward,
-                        encoder_fold, mlp_encode)
-from .learner import clip_and_step
+from .fused_mlp import ActorBuffers, MlpPack, actor_act, actor_backward, actor_forward, actor_train_forward, mlp_encode
+from .learner import FusedAdam, clip_and_step
 
 OBS = 40
 
@@ -99,10 +99,6 @@ class FusedACIQNState:
         self.q_pi = torch.empty(B * N, **f)
         self.dzF = torch.empty(B, 256, **bf)
         self.dzG = torch.empty(B, 128, **f)
-        self.enc_dw = torch.empty(256, 32, **f)
-        self.enc_db = torch.empty(256, **f)
-        self.enc_dw2 = torch.empty(256, 32, **f)
-        self.enc_db2 = torch.empty(256, **f)
         self.arena = PartialArena(16 << 20, dev)
         self.losses = torch.zeros(2, **f)   # critic, actor loss (summed from per-tile partials)
         self.tile_loss = torch.zeros(2, B * N // 32, **f)
@@ -116,6 +112,24 @@ class FusedACIQNState:
 
     def act(self, obs_rows, actions64, step_dev, steps_per_count, total, fraction, initial, final, seed):
         actor_act(self.actor, obs_rows, actions64, step_dev, steps_per_count, total, fraction, initial, final, seed)
+
+
+def _reduce_and_step(arena, opt, grads, sync, max_norm, wait=None):
+    """Reduce the queued weight-gradient partials, then clip + Adam. Single process with the
+    fused optimiser: the reduction launch also forms the gradient norm (two launches in all);
+    otherwise reduce, all-reduce (sync), then asvrl_adam_clip. `wait`: an event to wait for
+    before the parameters change."""
+    if sync is None and isinstance(opt, FusedAdam):
+        arena.flush(norm=opt)
+        if wait is not None:
+            torch.cuda.current_stream().wait_event(wait)
+        return opt.step_prenormed(arena.norm_parts, arena.nparts)
+    arena.flush()
+    if sync is not None:
+        sync(grads)
+    if wait is not None:
+        torch.cuda.current_stream().wait_event(wait)
+    return clip_and_step(opt, grads, max_norm)
 
 
 def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, actor_grads, rows, gamma=0.99,
@@ -151,15 +165,11 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     arena.linear(bufs.dz1, bufs.h0, critic.hidden_layer.weight.grad, critic.hidden_layer.bias.grad)
     with side.on(1):
         arena.linear(bufs.dz2, bufs.h1g, critic.hidden_layer_2.weight.grad, critic.hidden_layer_2.bias.grad)
-        arena.linear(st.dzF, st.xb, st.enc_dw, st.enc_db)
+        arena.fold(st.dzF, st.xb, critic)             # encoder image -> self/object encoder grads
         arena.small(st.dzG, a_rows, ae.weight.grad, ae.bias.grad)
     side.join()
     arena.scalar(st.tile_loss[0], st.losses[0:1])   # the critic loss
-    arena.flush()                                   # one reduction launch for the six layers + loss
-    encoder_fold(st.enc_dw, st.enc_db, critic)
-    if sync is not None:
-        sync(critic_grads)
-    cgn = clip_and_step(critic_opt, critic_grads, max_norm)
+    cgn = _reduce_and_step(arena, critic_opt, critic_grads, sync, max_norm)
     st.local_trunk.refresh()
     st.local_cenc.refresh()
 
@@ -175,15 +185,9 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     arena.linear(ab.dz1, ab.h0, actor.hidden_layer.weight.grad, actor.hidden_layer.bias.grad)
     with side.on(1):
         arena.vec(ab.dout[:, 1], ab.h2, ow[1], obias[1:2])
-        arena.linear(ab.dz0, ab.xb, st.enc_dw2, st.enc_db2)
+        arena.fold(ab.dz0, ab.xb, actor)
     side.join()
     arena.scalar(st.tile_loss[1], st.losses[1:2])   # the actor loss
-    arena.flush()
-    encoder_fold(st.enc_dw2, st.enc_db2, actor)
-    if sync is not None:
-        sync(actor_grads)
-    if actor_wait is not None:
-        torch.cuda.current_stream().wait_event(actor_wait)
-    agn = clip_and_step(actor_opt, actor_grads, max_norm)
+    agn = _reduce_and_step(arena, actor_opt, actor_grads, sync, max_norm, wait=actor_wait)
     st.actor.refresh()
     return st.losses[0], st.losses[1], cgn, agn

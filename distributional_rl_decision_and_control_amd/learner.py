@@ -107,6 +107,16 @@ class FusedAdam:
         _abi.check(rc, "asvrl_adam_clip")
         return self.norm[0]
 
+    def step_prenormed(self, norm_parts, nparts):
+        """Clip + Adam with the squared norm as nparts f64 partials and step_t already advanced
+        (PartialArena.flush(norm=self)): one launch. Returns the pre-clip norm."""
+        rc = _abi.lib().asvrl_adam_step(
+            _abi.ptr(self.flat), _abi.ptr(self.grads.flat), _abi.ptr(self.exp_avg), _abi.ptr(self.exp_avg_sq),
+            self.n, _abi.ptr(self.step_t), self.lr, self.betas[0], self.betas[1], self.eps, self.max_norm,
+            _abi.ptr(self.norm), _abi.ptr(norm_parts), int(nparts), _abi.stream_ptr(None))
+        _abi.check(rc, "asvrl_adam_step")
+        return self.norm[0]
+
 
 def clip_and_step(opt, grads, max_norm):
     """Global-norm clip then optimizer step; returns the pre-clip norm (device scalar)."""

@@ -360,6 +360,13 @@ int asvrl_adam_clip(float* params, float* grads, float* exp_avg, float* exp_avg_
                     float* step, float lr, float beta1, float beta2, float eps, float max_norm,
                     float* norm_out, double* work, void* stream);
 
+/* The second half of asvrl_adam_clip alone: clip + Adam with the squared norm given as nparts
+ * f64 partial sums (asvrl_partial_sums_norm; every workgroup folds them in the same fixed order)
+ * and *step already incremented. One launch. */
+int asvrl_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+                    const float* step, float lr, float beta1, float beta2, float eps, float max_norm,
+                    float* norm_out, const double* norm_parts, int32_t nparts, void* stream);
+
 /* ---------------------------------------------------------------- Linear weight gradients */
 
 /* grad_weight / grad_bias of an nn.Linear from bf16 activations over R rows (the backward's
@@ -395,14 +402,34 @@ int asvrl_linear_wgrad_vec_partial(const float* dq, int64_t ldq, const void* x, 
  * trailing nb values of each group's (nw + nb)-float partial (db optional). A segment with
  * nw + nb == 1 (a scalar over many groups) is reduced by a whole workgroup. */
 #define ASVRL_MAX_SUM_SEGS 8
+#define ASVRL_SUM_PLAIN 0
+/* The 256 x 32 encoder-image partials (asvrl_mlp_pack's block-structured image) folded straight
+ * into the contiguous gradients [self_w 56x7 | self_b 56 | obj_w 40x5 | obj_b 40] at dw (688
+ * floats, nw = 688, nb = 0): the object encoder's five copies are summed, in object order, after
+ * each copy's own fixed-order group sum (bit-identical to asvrl_encoder_fold after a plain sum). */
+#define ASVRL_SUM_FOLD_ENCODERS 1
 typedef struct AsvPartialSum {
   const float* partial;
   float* dw;
   float* db;
   int32_t groups, nw, nb, accumulate;
+  int32_t stride;   /* floats per group in partial; 0 = nw + nb */
+  int32_t boff;     /* offset of the bias partials within a group; 0 = nw. With stride / boff a
+                       32-row MFMA reduction can fill a layer of fewer rows (IQN's 25 actions) */
+  int32_t mode;     /* ASVRL_SUM_PLAIN or ASVRL_SUM_FOLD_ENCODERS */
+  int32_t norm;     /* 1: the outputs count towards the gradient norm (asvrl_partial_sums_norm) */
 } AsvPartialSum;
 /* Reduce up to ASVRL_MAX_SUM_SEGS pending partial sets in one launch (fixed order per output). */
 int asvrl_partial_sums(const AsvPartialSum* segs, int32_t nseg, void* stream);
+
+/* asvrl_partial_sums that also prepares the global gradient norm of the segments with norm = 1
+ * for an asvrl_adam_step right after (replaces asvrl_adam_clip's norm pass when every gradient is
+ * produced by this launch and no all-reduce follows): each working workgroup writes the f64 sum of
+ * the squares of the outputs it wrote to its own slot of norm_parts (asvrl_partial_sums_norm_parts
+ * slots), and *step is incremented. */
+int asvrl_partial_sums_norm(const AsvPartialSum* segs, int32_t nseg, double* norm_parts, float* step,
+                            void* stream);
+int32_t asvrl_partial_sums_norm_parts(const AsvPartialSum* segs, int32_t nseg);
 
 /* ---------------------------------------------------------------- per-row MLPs (actor, encoders) */
 
