@@ -272,10 +272,12 @@ class MarineNavEnv3:
         self._batch.params = self._params()
         return self._batch
 
-    def _device_step(self, actions, is_continuous_action, do_dynamics):
+    def _pack(self, actions, is_continuous_action, R, O, Cm):
+        """Host SoA image of this env for one env-step launch, padded to (R robots, O obstacles,
+        Cm cores): robot fields, flags, obstacles, cores, actions and the perception noise drawn
+        from each active robot's RandomState in the reference's order (wamv.py:465-510): obstacles,
+        then the other active robots, five draws per candidate."""
         n = len(self.robots)
-        b = self._ensure_batch(n, len(self.obstacles), len(self.cores))
-        R, O, Cm = b.max_robots, b.max_obs, b.max_cores
         if len(self.cores) > Cm:
             raise NotImplementedError("more than 16 vortex cores")
         rs = np.zeros((_abi.NUM_FIELDS, R))
@@ -289,10 +291,10 @@ class MarineNavEnv3:
             rs[_abi.F_PHI, i] = rob.phi
             fl[i] = ((_abi.FLAG_DEACTIVATED if rob.deactivated else 0) | (_abi.FLAG_COLLISION if rob.collision else 0)
                      | (_abi.FLAG_REACH_GOAL if rob.reach_goal else 0))
-        obst = np.zeros((O, 3))
+        obst = np.zeros((max(O, 1), 3))
         for k, o in enumerate(self.obstacles):
             obst[k] = (o.x, o.y, o.r)
-        cores = np.zeros((Cm, 4))
+        cores = np.zeros((max(Cm, 1), 4))
         for k, c in enumerate(self.cores):
             cores[k] = (c.x, c.y, float(c.clockwise), c.Gamma)
         acts = np.zeros((R, 2))
@@ -304,8 +306,6 @@ class MarineNavEnv3:
                     acts[i] = (float(a[0]), float(a[1]))
                 else:
                     acts[i, 0] = int(a)
-        # perception noise: each active robot's RandomState, obstacles then active others
-        # (wamv.py:465-510), five draws per candidate
         noise = np.zeros((R, O + R, 5))
         for i, rob in enumerate(self.robots):
             if rob.deactivated:
@@ -316,20 +316,11 @@ class MarineNavEnv3:
                 if other is rob or other.deactivated:
                     continue
                 noise[i, O + j] = rob.perception.draw_candidate_noise()
-        dev = b.device
-        b.rs.copy_(torch.from_numpy(rs))
-        b.rflags.copy_(torch.from_numpy(fl))
-        b.n_robots.fill_(n)
-        b.n_obs.fill_(len(self.obstacles))
-        b.n_cores.fill_(len(self.cores))
-        b.ep_ts.fill_(int(self.episode_timesteps))
-        b.obstacles[0].copy_(torch.from_numpy(obst))
-        b.cores[0].copy_(torch.from_numpy(cores))
-        a_d = torch.from_numpy(acts).to(dev)
-        n_d = torch.from_numpy(noise).to(dev)
-        b.step(a_d, is_continuous=is_continuous_action, noise=n_d, do_dynamics=do_dynamics)
-        out = dict(rs=b.rs.cpu().numpy(), fl=b.rflags.cpu().numpy(), obs64=b.obs64.cpu().numpy(),
-                   cnt=b.obj_cnt.cpu().numpy(), reward=b.reward.cpu().numpy(), info=b.info.cpu().numpy())
+        return dict(rs=rs, fl=fl, obst=obst, cores=cores, acts=acts, noise=noise, n=n, n_obs=len(self.obstacles),
+                    n_cores=len(self.cores), ep_ts=int(self.episode_timesteps))
+
+    def _apply(self, out, do_dynamics):
+        """Write one launch's results (this env's slice) back into the Robot objects."""
         rs, fl = out["rs"], out["fl"]
         for i, rob in enumerate(self.robots):
             if do_dynamics and not rob.deactivated:
@@ -342,7 +333,11 @@ class MarineNavEnv3:
             if not rob.deactivated:
                 rob.apply_COLREGs = bool(fl[i] & _abi.FLAG_COLREGS)
                 rob.phi = float(rs[_abi.F_PHI, i])
-        return out
+
+    def _device_step(self, actions, is_continuous_action, do_dynamics):
+        n = len(self.robots)
+        b = self._ensure_batch(n, len(self.obstacles), len(self.cores))
+        return run_env_step(b, [self], [actions], is_continuous_action, do_dynamics)[0]
 
     def _observations(self, out):
         observations, collisions, reach_goals = [], [], []
@@ -366,11 +361,16 @@ class MarineNavEnv3:
         return self._observations(out)
 
     def step(self, actions, is_continuous_action=True):
-        rewards = [0] * len(self.robots)
         assert len(actions) == len(self.robots), "Number of actions not equal number of robots!"
         assert self.check_all_reach_goal() is not True, "All robots reach goals, not actions are available!"
         active = [not rob.deactivated for rob in self.robots]
         out = self._device_step(actions, is_continuous_action, do_dynamics=True)
+        return self._finish_step(actions, active, out)
+
+    def _finish_step(self, actions, active, out):
+        """env.step's bookkeeping after the launch (env.py:262-333): histories, observations,
+        rewards, dones, infos, counters."""
+        rewards = [0] * len(self.robots)
         if self.is_eval_env:  # env.py:262-269
             for i, rob in enumerate(self.robots):
                 if active[i]:
@@ -500,3 +500,48 @@ class MarineNavEnv3:
     def save_episode(self, filename):
         with open(filename, "w") as f:
             json.dump(self.episode_data(), f)
+
+
+def run_env_step(batch, envs, actions_list, is_continuous_action, do_dynamics):
+    """One asvrl_env_step launch over several MarineNavEnv3 instances with identical parameter
+    sets: env e occupies slots [e*R, (e+1)*R) of `batch` (a DeviceEnvBatch with n_envs >= len(envs)
+    and room for every env's robots, obstacles and cores). Each env's noise comes from its own
+    robots' RandomStates, so the results equal stepping the envs one at a time. Returns the
+    per-env output slices (host arrays) after writing them back into the robots."""
+    E, R, O, Cm = len(envs), batch.max_robots, batch.max_obs, batch.max_cores
+    packs = [env._pack(a, is_continuous_action, R, O, Cm) for env, a in zip(envs, actions_list)]
+    dev = batch.device
+    NT = batch.n_envs * R
+    rs = np.zeros((_abi.NUM_FIELDS, NT))
+    fl = np.zeros(NT, np.uint8)
+    acts = np.zeros((NT, 2))
+    noise = np.zeros((NT, O + R, 5))
+    cnt = np.zeros((4, batch.n_envs), np.int32)
+    obst = np.zeros((batch.n_envs, max(O, 1), 3))
+    cores = np.zeros((batch.n_envs, max(Cm, 1), 4))
+    for e, pk in enumerate(packs):
+        sl = slice(e * R, (e + 1) * R)
+        rs[:, sl], fl[sl], acts[sl], noise[sl] = pk["rs"], pk["fl"], pk["acts"], pk["noise"]
+        cnt[:, e] = (pk["n"], pk["n_obs"], pk["n_cores"], pk["ep_ts"])
+        obst[e], cores[e] = pk["obst"], pk["cores"]
+    batch.rs.copy_(torch.from_numpy(rs))
+    batch.rflags.copy_(torch.from_numpy(fl))
+    counts = torch.from_numpy(cnt).to(dev)
+    batch.n_robots.copy_(counts[0])
+    batch.n_obs.copy_(counts[1])
+    batch.n_cores.copy_(counts[2])
+    batch.ep_ts.copy_(counts[3])
+    batch.obstacles.copy_(torch.from_numpy(obst))
+    batch.cores.copy_(torch.from_numpy(cores))
+    batch.step(torch.from_numpy(acts).to(dev), is_continuous=is_continuous_action, noise=torch.from_numpy(noise).to(dev),
+               do_dynamics=do_dynamics)
+    full = dict(rs=batch.rs.cpu().numpy(), fl=batch.rflags.cpu().numpy(), obs64=batch.obs64.cpu().numpy(),
+                cnt=batch.obj_cnt.cpu().numpy(), reward=batch.reward.cpu().numpy(), info=batch.info.cpu().numpy())
+    outs = []
+    for e, env in enumerate(envs):
+        sl = slice(e * R, (e + 1) * R)
+        out = dict(rs=full["rs"][:, sl], fl=full["fl"][sl], obs64=full["obs64"][sl], cnt=full["cnt"][sl],
+                   reward=full["reward"][sl], info=full["info"][sl])
+        env._apply(out, do_dynamics)
+        outs.append(out)
+    return outs

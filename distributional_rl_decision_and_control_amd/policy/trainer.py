@@ -15,8 +15,11 @@ import numpy as np
 class Trainer:
     def __init__(self, train_env, eval_env, eval_schedule, rl_agent, UPDATE_EVERY=4, learning_starts=2000,
                  target_update_interval=10000, exploration_fraction=0.25, initial_eps=0.6, final_eps=0.05,
-                 imitation=False, il_agent=None):
+                 imitation=False, il_agent=None, batched_eval=True):
         self.train_env = train_env
+        # evaluation(): all eval configs in one device env batch (policy/batched_eval.py);
+        # False runs them one by one as trainer.py:266-392 does
+        self.batched_eval = batched_eval
         self.eval_env = eval_env
         self.rl_agent = rl_agent
         self.eval_config = []
@@ -210,19 +213,28 @@ class Trainer:
         return (copy.deepcopy(histories), np.mean(rewards), bool(env.check_all_reach_goal()), np.mean(times),
                 np.mean(energies), [[] for _ in range(n)])
 
-    def evaluation(self):
-        obs_d, act_d, traj_d, rew_d, succ_d, time_d, en_d, rel_d = [], [], [], [], [], [], [], []
-        for idx, config in enumerate(self.eval_config):
-            print(f"Evaluating episode {idx}")
-            (obs, acts, trajs), r, s, t, e, rel = self._run_eval_episode(config)
-            obs_d.append(obs)
-            act_d.append(acts)
-            traj_d.append(trajs)
-            rew_d.append(r)
-            succ_d.append(s)
-            time_d.append(t)
-            en_d.append(e)
-            rel_d.append(rel)
+    def evaluation(self, batched=None):
+        batched = self.batched_eval if batched is None else batched
+        if batched:
+            from .batched_eval import evaluate_configs
+            print(f"Evaluating episodes 0-{len(self.eval_config) - 1} (one batch)")
+            res = evaluate_configs(self.rl_agent, self.eval_config, template_env=self.eval_env)
+            obs_d, act_d, traj_d = res["observations"], res["actions"], res["trajectories"]
+            rew_d, succ_d, time_d, en_d, rel_d = (res["rewards"], res["successes"], res["times"], res["energies"],
+                                                  res["relations"])
+        else:
+            obs_d, act_d, traj_d, rew_d, succ_d, time_d, en_d, rel_d = [], [], [], [], [], [], [], []
+            for idx, config in enumerate(self.eval_config):
+                print(f"Evaluating episode {idx}")
+                (obs, acts, trajs), r, s, t, e, rel = self._run_eval_episode(config)
+                obs_d.append(obs)
+                act_d.append(acts)
+                traj_d.append(trajs)
+                rew_d.append(r)
+                succ_d.append(s)
+                time_d.append(t)
+                en_d.append(e)
+                rel_d.append(rel)
         avg_r = np.mean(rew_d)
         success_rate = np.sum(succ_d) / len(succ_d)
         idx = np.where(np.array(succ_d) == 1)[0]
