@@ -11,7 +11,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ASVRL_LIB", os.path.join(HERE, "lib", "libasvrl.so"))  # override: A/B variants
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
 OBS_DIM = 40   # self 7 | objects 25 | mask 5 | pad 3
@@ -77,7 +77,7 @@ class AsvResetCfg(C.Structure):
 
 class AsvCriticWeights(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ("wc_frag", "w1_frag", "w2_frag", "w2t_frag", "w1t_frag", "bc", "b1", "b2",
-                                          "wo", "bo")]
+                                          "wo", "bo", "self_w", "self_b", "obj_w", "obj_b", "ae_w", "ae_b")]
 
 
 class AsvCriticActs(C.Structure):
@@ -87,7 +87,8 @@ class AsvCriticActs(C.Structure):
 # (name, restype, argtypes) of every exported entry point, mirroring include/asvrl.h
 _VP, _I32, _I64, _U64, _F, _D = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_float, C.c_double
 class AsvCriticIO(C.Structure):
-    _fields_ = [("F", _VP), ("G", _VP), ("taus", _VP), ("B", _I32), ("N", _I32), ("Np", _I32), ("kappa", C.c_float),
+    _fields_ = [("F", _VP), ("G", _VP), ("obs", _VP), ("ld_obs", _I64), ("act", _VP), ("ld_act", _I64), ("xb", _VP),
+                ("taus", _VP), ("B", _I32), ("N", _I32), ("Np", _I32), ("kappa", C.c_float),
                 ("q_targets", _VP), ("q_next", _VP), ("rewards", _VP), ("dones", _VP), ("ld_rd", _I64),
                 ("gamma", C.c_float), ("dq", C.c_float), ("q", _VP), ("row_loss", _VP), ("dF", _VP), ("dG", _VP),
                 ("dzF", _VP), ("dzG", _VP), ("w_ae", _VP), ("dA", _VP), ("tile_loss", _VP),
@@ -102,8 +103,9 @@ class AsvIqnHead(C.Structure):
 
 
 class AsvIqnIO(C.Structure):
-    _fields_ = [("F", _VP), ("taus", _VP), ("B", _I32), ("N", _I32), ("Np", _I32), ("kappa", C.c_float),
-                ("q_next", _VP), ("actions", _VP), ("rewards", _VP), ("dones", _VP), ("ld_rd", _I64),
+    _fields_ = [("F", _VP), ("obs", _VP), ("ld_obs", _I64), ("xb", _VP), ("taus", _VP), ("B", _I32), ("N", _I32),
+                ("Np", _I32), ("kappa", C.c_float), ("q_next", _VP), ("actions", _VP), ("rewards", _VP),
+                ("dones", _VP), ("ld_rd", _I64),
                 ("gamma", C.c_float), ("q", _VP), ("row_loss", _VP), ("dzF", _VP), ("dz_out", _VP),
                 ("tile_loss", _VP), ("loss_scale", C.c_float), ("act_out", _VP), ("ld_act", _I64),
                 ("step_dev", _VP), ("eps_steps_per_count", _D), ("eps_total", _D), ("eps_fraction", _D),

@@ -47,23 +47,24 @@ template <int MODE> constexpr bool kFwdOnly = MODE == MODE_FWD || MODE == MODE_I
 #ifndef ASVRL_TRAIN_B_BPP32
 #define ASVRL_TRAIN_B_BPP32 2
 #endif
-// Persistent launches (one workgroup per CU stages the weights into LDS once, its waves walk
-// the tiles) per mode: bit MODE of the mask (not TRAIN / ACTOR). Non-persistent launches
-// (one tile per wave) share the CUs better with a concurrent stream.
-#ifndef ASVRL_CRITIC_PERSISTENT
-#define ASVRL_CRITIC_PERSISTENT 0
-#endif
-template <int MODE> constexpr bool kPersistent = (ASVRL_CRITIC_PERSISTENT >> MODE) & 1;
-// TRAIN and ACTOR read G per feature after activation stores have been issued; vmcnt counts
-// stores too, so a global load there would first drain them. Each wave stages its samples' G
-// rows in LDS instead (needs one tile per wave: never persistent).
-template <int MODE> constexpr bool kStageG = MODE == MODE_TRAIN || MODE == MODE_ACTOR;
-static_assert(!kPersistent<MODE_TRAIN> && !kPersistent<MODE_ACTOR>, "TRAIN / ACTOR stage G per tile");
+// Every wave stages its samples' feature rows in LDS in the prologue (F as bf16 for every mode,
+// G in f32 for the AC-IQN critic modes), computing them from the observation rows / actions when
+// given (the encoders fused into the trunk) or copying F / G. The per-feature reads that follow
+// the activation stores then come from LDS: vmcnt counts stores too, so a global load there
+// would first wait for every store in flight. One tile per wave (non-persistent launches also
+// share the CUs better with a concurrent stream).
+template <int MODE> constexpr bool kStageG = !kIqn<MODE>;
+constexpr int kSelfF = 56, kSelfIn = 7, kObjF = 40, kObjIn = 5, kObjN = 5, kObsMask = 32;
 
 struct CriticArgs {
   AsvCriticWeights w;
   const float* F;
   const float* G;
+  const float* obs;  // packed observation rows (encoders in-kernel) or NULL (F given)
+  int64_t ld_obs;
+  const float* ain;  // actions for G = action_encoder(a) or NULL (G given)
+  int64_t ld_ain;
+  void* xb;          // TRAIN: bf16 copy of obs columns 0..31 per sample
   const float* taus;
   const float* qt;  // (B, Np) target quantiles (TRAIN)
   int B, N, Np;
@@ -119,7 +120,7 @@ static_assert(kFragWC == kFragW2, "the Wc / W2^T slot holds either image");
 // backward (dh2 = W_out[a] dq) and the bias
 struct CriticLdsIqn : CriticLds {
   bf16x8 wo_img[kH / 16 * 64];
-  float wof[kMaxA * kH];
+  __bf16 wof[kMaxA * kH];   // output_layer.weight (the backward's dh2 = W_out[a] dq feeds a bf16 dz2)
   float bo_a[kMaxA];
 };
 template <int MODE> struct LdsOf { using T = CriticLds; };
@@ -128,9 +129,66 @@ template <> struct LdsOf<MODE_IQN_TRAIN> { using T = CriticLdsIqn; };
 template <> struct LdsOf<MODE_IQN_ACT> { using T = CriticLdsIqn; };
 static_assert(sizeof(CriticLdsIqn) <= 160 * 1024, "IQN LDS image exceeds the CU's 160 KB");
 
+// The wave's feature rows in LDS for its 32 / NT samples: F (bf16 [S][256]) = observation_processor
+// of the observation row (AC_IQN_model.py:284-308, IQN_model.py:80-96: self_encoder 7 -> 56 and
+// object_encoder 5 -> 40 per object, ReLU, objects with mask < 0.5 zeroed), f32 dot products with
+// 4 features per lane, or a copy of a.F; G (f32 [S][128]) = relu(action_encoder(a))
+// (AC_IQN_model.py:468-470) or a copy of a.G. TRAIN also writes the bf16 obs copy for the encoder
+// weight gradient. Global loads only: this runs before any store of the tile.
+template <int NT, bool WITH_G, bool WITH_XB>
+__device__ __forceinline__ void stage_features(const CriticArgs& a, int tile, int lane, __bf16* Fw, float* Gw) {
+  constexpr int S = 32 / NT;
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    const int b = tile * S + k;
+    if (a.obs != nullptr) {
+      const float* x = a.obs + static_cast<int64_t>(b) * a.ld_obs;
+#pragma unroll
+      for (int t = 0; t < kC / 64; ++t) {
+        const int m = lane + 64 * t;
+        float v;
+        if (m < kSelfF) {
+          const float* w = a.w.self_w + m * kSelfIn;
+          float d = 0.f;
+#pragma unroll
+          for (int i = 0; i < kSelfIn; ++i) d += w[i] * x[i];
+          v = relu(d + a.w.self_b[m]);
+        } else {
+          const int o = (m - kSelfF) / kObjF, j = (m - kSelfF) % kObjF;
+          const float* w = a.w.obj_w + j * kObjIn;
+          const float* xo = x + kSelfIn + kObjIn * o;
+          float d = 0.f;
+#pragma unroll
+          for (int i = 0; i < kObjIn; ++i) d += w[i] * xo[i];
+          v = x[kObsMask + o] < 0.5f ? 0.f : relu(d + a.w.obj_b[j]);   // masked_fill(mask < 0.5, 0)
+        }
+        Fw[k * kC + m] = (__bf16)v;
+      }
+      if (WITH_XB && a.xb != nullptr && lane < 32) bp(a.xb)[static_cast<int64_t>(b) * 32 + lane] = (__bf16)x[lane];
+    } else {
+      const float* f = a.F + static_cast<int64_t>(b) * kC;
+#pragma unroll
+      for (int t = 0; t < kC / 64; ++t) Fw[k * kC + lane + 64 * t] = (__bf16)f[lane + 64 * t];
+    }
+    if constexpr (WITH_G) {
+      if (a.ain != nullptr) {
+        const float a0 = a.ain[static_cast<int64_t>(b) * a.ld_ain], a1 = a.ain[static_cast<int64_t>(b) * a.ld_ain + 1];
+#pragma unroll
+        for (int t = 0; t < kH / 64; ++t) {
+          const int m = lane + 64 * t;
+          Gw[k * kH + m] = relu((a.w.ae_w[2 * m] * a0 + a.w.ae_w[2 * m + 1] * a1) + a.w.ae_b[m]);
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < kH / 64; ++t) Gw[k * kH + lane + 64 * t] = a.G[static_cast<int64_t>(b) * kH + lane + 64 * t];
+      }
+    }
+  }
+}
+
 // output-layer weight feeding dh2[m]: the critic's single output row, or IQN's row of the taken action
 __device__ __forceinline__ float out_w(const CriticLds& L, int, int m) { return L.wo[m]; }
-__device__ __forceinline__ float out_w(const CriticLdsIqn& L, int ai, int m) { return L.wof[ai * kH + m]; }
+__device__ __forceinline__ float out_w(const CriticLdsIqn& L, int ai, int m) { return static_cast<float>(L.wof[ai * kH + m]); }
 
 __device__ __forceinline__ uint64_t act_step(const CriticArgs& a) {
   return a.step_dev != nullptr ? static_cast<uint64_t>(*a.step_dev) : 0ull;
@@ -186,8 +244,8 @@ __device__ __forceinline__ void iqn_act_select(const CriticArgs& a, const Critic
 }
 
 template <int MODE, int NT, class LT>
-__device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, int tile, int lane,
-                                            const float* Gl = nullptr) {
+__device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, int tile, int lane, const __bf16* Fl,
+                                            const float* Gl) {
   constexpr bool IQN = kIqn<MODE>;
   constexpr bool TRAINM = kTrainMode<MODE>;
   const int r = lane & 31, h = lane >> 5;
@@ -196,11 +254,8 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
   float tau;
   if (MODE == MODE_IQN_ACT && a.taus == nullptr) tau = act_tau(a, grow);
   else tau = a.taus[grow];
-  const float* Fb = a.F + static_cast<size_t>(b) * kC;
-  const float* Gb;   // G[b]: the wave's LDS copy (kStageG) or global
-  if constexpr (IQN) Gb = nullptr;
-  else if constexpr (kStageG<MODE>) Gb = Gl + (b - tile * 32 / NT) * kH;
-  else Gb = a.G + static_cast<size_t>(b) * kH;
+  const __bf16* Fb = Fl + (b - tile * 32 / NT) * kC;                   // F[b], the wave's LDS row
+  const float* Gb = IQN ? nullptr : Gl + (b - tile * 32 / NT) * kH;     // G[b]
   const bf16x8* WC = kFwdOnly<MODE> ? L.wc : reinterpret_cast<const bf16x8*>(a.w.wc_frag);
   const bf16x8* W1 = L.w1;
   const bf16x8* W2 = L.w2;
@@ -240,7 +295,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
           float x = acc0[q4][8 * s + j] + L.bc[m];
           x = relu(x);
           cpk[mb * 2 + s][j] = (__bf16)x;
-          hv[j] = Fb[m] * x;
+          hv[j] = static_cast<float>(Fb[m]) * x;
           hpk[mb * 2 + s][j] = (__bf16)hv[j];
         }
         if (TRAINM)
@@ -511,12 +566,12 @@ struct CriticLdsB {
 
 template <int NT>
 __device__ __forceinline__ void critic_tile_b(const CriticArgs& a, const CriticLdsB& L, int tile, int lane,
-                                              const float* Fl) {
+                                              const __bf16* Fl) {
   const int r = lane & 31, h = lane >> 5;
   const int grow = tile * 32 + r;
   const int b = grow / NT;
   const float tau = a.taus[grow];
-  const float* Fb = Fl + (b - tile * 32 / NT) * kC;   // the wave's LDS copy of F[b]
+  const __bf16* Fb = Fl + (b - tile * 32 / NT) * kC;   // the wave's LDS row of F[b]
   bf16x8 cx[kNcos / 16];
 #pragma unroll
   for (int ks = 0; ks < kNcos / 16; ++ks)
@@ -567,7 +622,7 @@ __device__ __forceinline__ void critic_tile_b(const CriticArgs& a, const CriticL
           const float x = acc0[q4][8 * s + j] + L.bc[m];
           const float cv = static_cast<float>((__bf16)relu(x));   // part A's bf16 c
           fsa[(q4 * 2 + s) * 8 + j] = acc4[q4][8 * s + j] * cv;
-          dv[j] = cv > 0.f ? acc4[q4][8 * s + j] * Fb[m] : 0.f;
+          dv[j] = cv > 0.f ? acc4[q4][8 * s + j] * static_cast<float>(Fb[m]) : 0.f;
         }
         store16(bp(a.acts.dzc) + static_cast<size_t>(grow) * kC + mb * 32 + 16 * s, dv, h);
       }
@@ -581,7 +636,7 @@ __device__ __forceinline__ void critic_tile_b(const CriticArgs& a, const CriticL
       const int m = feat(half * BPP + (g >> 1), 8 * (g & 1) + (v & 7), h);
       const size_t o = static_cast<size_t>(b) * kC + m;
       if (a.dF != nullptr) a.dF[o] = fsa[i];
-      if (a.dzF != nullptr) bp(a.dzF)[o] = (__bf16)(Fb[m] > 0.f ? fsa[i] : 0.f);   // through the encoders' relu / mask
+      if (a.dzF != nullptr) bp(a.dzF)[o] = (__bf16)(static_cast<float>(Fb[m]) > 0.f ? fsa[i] : 0.f);   // encoders' relu / mask
     }
   }
 }
@@ -597,37 +652,29 @@ __global__ __launch_bounds__(8 * 64) void critic_train_b_kernel(CriticArgs a) {
     for (int i = threadIdx.x; i < kC; i += 8 * 64) L.bc[i] = a.w.bc[i];
   }
   // this wave's samples' F rows (read per feature after the dzc stores: LDS, not vmcnt-ordered loads)
-  __shared__ __attribute__((aligned(16))) float Fs[8 * (32 / NT) * kC];
+  __shared__ __attribute__((aligned(16))) __bf16 Fs[8 * (32 / NT) * kC];
   const int tile = blockIdx.x * 8 + (threadIdx.x >> 6);
-  float* Fw = Fs + (threadIdx.x >> 6) * (32 / NT) * kC;
-  if (tile < a.B * NT / 32) {
-    const float4* src = reinterpret_cast<const float4*>(a.F + static_cast<size_t>(tile) * (32 / NT) * kC);
-#pragma unroll
-    for (int i = threadIdx.x & 63; i < (32 / NT) * kC / 4; i += 64) reinterpret_cast<float4*>(Fw)[i] = src[i];
-  }
+  __bf16* Fw = Fs + (threadIdx.x >> 6) * (32 / NT) * kC;
+  if (tile < a.B * NT / 32) stage_features<NT, false, false>(a, tile, threadIdx.x & 63, Fw, nullptr);
   __syncthreads();
   if (tile < a.B * NT / 32) critic_tile_b<NT>(a, L, tile, threadIdx.x & 63, Fw);
 }
 
-// Persistent: one workgroup per CU stages the forward weights into LDS once, then its waves
-// walk the 32-row tiles. 8 waves (2 per SIMD) where the registers allow, 4 for TRAIN.
-template <int MODE> struct CriticWaves { static constexpr int n = 8; };
-template <> struct CriticWaves<MODE_TRAIN> { static constexpr int n = 8; };
+// One 32-row tile per wave; 8 waves per workgroup (2 per SIMD), 4 when a tile holds several
+// samples (N < 32) so the per-wave feature rows still fit next to the weights in LDS.
+template <int NT> struct CriticWaves { static constexpr int n = NT == 32 ? 8 : 4; };
 
 template <int MODE, int NT>
-__global__ __launch_bounds__(CriticWaves<MODE>::n * 64) void critic_kernel(CriticArgs a) {
-  constexpr int W = CriticWaves<MODE>::n;
+__global__ __launch_bounds__(CriticWaves<NT>::n * 64) void critic_kernel(CriticArgs a) {
+  constexpr int W = CriticWaves<NT>::n, S = 32 / NT;
   __shared__ typename LdsOf<MODE>::T L;
-  __shared__ __attribute__((aligned(16))) float Gs[kStageG<MODE> ? W * (32 / NT) * kH : 1];
-  if constexpr (kStageG<MODE>) {   // this wave's samples' G rows (32 / NT rows of 128)
-    const int tile = blockIdx.x * W + (threadIdx.x >> 6), l = threadIdx.x & 63;
-    if (tile < a.B * NT / 32) {
-      const float4* src = reinterpret_cast<const float4*>(a.G + static_cast<size_t>(tile) * (32 / NT) * kH);
-      float4* dst = reinterpret_cast<float4*>(Gs + (threadIdx.x >> 6) * (32 / NT) * kH);
-#pragma unroll
-      for (int i = l; i < (32 / NT) * kH / 4; i += 64) dst[i] = src[i];
-    }
-  }
+  __shared__ __attribute__((aligned(16))) __bf16 Fs[W * S * kC];
+  __shared__ __attribute__((aligned(16))) float Gs[kStageG<MODE> ? W * S * kH : 1];
+  const int tile = blockIdx.x * W + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int tiles = a.B * NT / 32;
+  __bf16* Fw = Fs + (threadIdx.x >> 6) * S * kC;
+  float* Gw = Gs + (kStageG<MODE> ? (threadIdx.x >> 6) * S * kH : 0);
+  if (tile < tiles) stage_features<NT, kStageG<MODE>, kTrainMode<MODE>>(a, tile, lane, Fw, Gw);
   {
     const bf16x8* gwc = reinterpret_cast<const bf16x8*>(kFwdOnly<MODE> ? a.w.wc_frag : a.w.w2t_frag);
     const bf16x8* gw1 = reinterpret_cast<const bf16x8*>(a.w.w1_frag);
@@ -646,49 +693,21 @@ __global__ __launch_bounds__(CriticWaves<MODE>::n * 64) void critic_kernel(Criti
       for (int i = threadIdx.x; i < kH / 16 * 64; i += W * 64) L.wo_img[i] = gwo[i];
       const int A = a.hd.n_actions;
       if (MODE == MODE_IQN_TRAIN)
-        for (int i = threadIdx.x; i < A * kH; i += W * 64) L.wof[i] = a.hd.wo[i];
+        for (int i = threadIdx.x; i < A * kH; i += W * 64) L.wof[i] = (__bf16)a.hd.wo[i];
       for (int i = threadIdx.x; i < kMaxA; i += W * 64) L.bo_a[i] = i < A ? a.hd.bo[i] : 0.f;
     }
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int tiles = a.B * NT / 32;
-  if constexpr (kPersistent<MODE>) {
-#pragma unroll 1
-  for (int tile = blockIdx.x * W + (threadIdx.x >> 6); tile < tiles; tile += gridDim.x * W) {
-    // opaque per-iteration copy of the lane index: every weight-fragment address depends on it,
-    // which keeps those (loop-invariant) LDS reads inside the loop instead of hoisting them
-    // into registers, while L keeps its LDS address space (ds_read, not flat loads)
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    critic_tile<MODE, NT>(a, L, tile, ln);
-  }
-  } else {
-    const int tile = blockIdx.x * W + (threadIdx.x >> 6);
-    if (tile < tiles) critic_tile<MODE, NT>(a, L, tile, lane, Gs + (threadIdx.x >> 6) * (32 / NT) * kH);
-  }
-}
-
-int num_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-  }
-  return n;
+  if (tile < tiles) critic_tile<MODE, NT>(a, L, tile, lane, Fw, Gw);
 }
 
 int train_b_grid(int tiles) { return (tiles + 7) / 8; }
 
 template <int MODE, int NT>
 void launch_mode(const CriticArgs& a, hipStream_t st) {
-  constexpr int W = CriticWaves<MODE>::n;
+  constexpr int W = CriticWaves<NT>::n;
   const int tiles = a.B * NT / 32;
-  int grid = (tiles + W - 1) / W;
-  if (kPersistent<MODE> && grid > num_cus()) grid = num_cus();
-  hipLaunchKernelGGL((critic_kernel<MODE, NT>), dim3(grid), dim3(W * 64), 0, st, a);
+  hipLaunchKernelGGL((critic_kernel<MODE, NT>), dim3((tiles + W - 1) / W), dim3(W * 64), 0, st, a);
 }
 
 template <int NT>
@@ -771,7 +790,11 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ wc,
 }
 
 int validate(const AsvCriticWeights* w, const AsvCriticIO* io) {
-  ASVRL_REQUIRE(w && io && io->F && io->G && io->taus, "asvrl_critic: null argument");
+  ASVRL_REQUIRE(w && io && io->taus, "asvrl_critic: null argument");
+  ASVRL_REQUIRE(io->F || (io->obs && w->self_w && w->self_b && w->obj_w && w->obj_b),
+                "asvrl_critic: needs F, or obs with the encoder weights");
+  ASVRL_REQUIRE(io->G || (io->act && w->ae_w && w->ae_b), "asvrl_critic: needs G, or act with the action encoder");
+  ASVRL_REQUIRE(!io->obs || io->ld_obs >= 37, "asvrl_critic: ld_obs must cover the packed observation row");
   ASVRL_REQUIRE(w->wc_frag && w->w1_frag && w->w2_frag && w->bc && w->b1 && w->b2 && w->wo && w->bo,
                 "asvrl_critic: null weight");
   ASVRL_REQUIRE(io->N == 8 || io->N == 16 || io->N == 32, "asvrl_critic: N must be 8, 16 or 32");
@@ -784,6 +807,7 @@ CriticArgs make_args(const AsvCriticWeights* w, const AsvCriticIO* io) {
   CriticArgs a{};
   a.w = *w;
   a.F = io->F; a.G = io->G; a.taus = io->taus; a.B = io->B; a.N = io->N; a.Np = io->Np; a.kappa = io->kappa;
+  a.obs = io->obs; a.ld_obs = io->ld_obs; a.ain = io->act; a.ld_ain = io->ld_act; a.xb = io->xb;
   a.qt = io->q_targets; a.qn = io->q_next; a.rew = io->rewards; a.don = io->dones; a.ld_rd = io->ld_rd;
   a.gamma = io->gamma; a.dq_const = io->dq; a.q = io->q; a.row_loss = io->row_loss; a.dF = io->dF; a.dG = io->dG;
   a.dzF = io->dzF; a.dzG = io->dzG; a.wae = io->w_ae; a.dA = io->dA;
@@ -854,7 +878,10 @@ extern "C" int asvrl_iqn_pack(const float* wc, const float* w1, const float* w2,
 namespace {
 
 int iqn_validate(const AsvCriticWeights* w, const AsvIqnHead* hd, const AsvIqnIO* io) {
-  ASVRL_REQUIRE(w && hd && io && io->F, "asvrl_iqn: null argument");
+  ASVRL_REQUIRE(w && hd && io, "asvrl_iqn: null argument");
+  ASVRL_REQUIRE(io->F || (io->obs && w->self_w && w->self_b && w->obj_w && w->obj_b),
+                "asvrl_iqn: needs F, or obs with the encoder weights");
+  ASVRL_REQUIRE(!io->obs || io->ld_obs >= 37, "asvrl_iqn: ld_obs must cover the packed observation row");
   ASVRL_REQUIRE(w->wc_frag && w->w1_frag && w->w2_frag && w->bc && w->b1 && w->b2, "asvrl_iqn: null weight");
   ASVRL_REQUIRE(hd->wo_frag && hd->bo && hd->n_actions >= 1 && hd->n_actions <= kMaxA, "asvrl_iqn: bad head");
   ASVRL_REQUIRE(io->N == 8 || io->N == 16 || io->N == 32, "asvrl_iqn: N must be 8, 16 or 32");
@@ -867,6 +894,7 @@ CriticArgs iqn_args(const AsvCriticWeights* w, const AsvIqnHead* hd, const AsvIq
   a.w = *w;
   a.hd = *hd;
   a.F = io->F; a.taus = io->taus; a.B = io->B; a.N = io->N; a.Np = io->Np; a.kappa = io->kappa;
+  a.obs = io->obs; a.ld_obs = io->ld_obs; a.xb = io->xb;
   a.qn = io->q_next; a.act = io->actions; a.rew = io->rewards; a.don = io->dones; a.ld_rd = io->ld_rd;
   a.gamma = io->gamma; a.q = io->q; a.row_loss = io->row_loss; a.dzF = io->dzF; a.dz_out = io->dz_out;
   a.tile_loss = io->tile_loss; a.loss_scale = io->loss_scale;

@@ -19,6 +19,10 @@ from . import _abi
 from .learner import clip_and_step
 from .policy.AC_IQN_model import encode_observation
 
+
+def _p(t):
+    return t.data_ptr() if t is not None else None
+
 _IDX = {}
 
 
@@ -58,6 +62,11 @@ class CriticPack:
         s.bc, s.b1 = critic.cos_embedding.bias.data_ptr(), critic.hidden_layer.bias.data_ptr()
         s.b2, s.wo = critic.hidden_layer_2.bias.data_ptr(), critic.output_layer.weight.data_ptr()
         s.bo = critic.output_layer.bias.data_ptr()
+        # f32 encoders, read by the kernels when given observation rows (encoders fused in the trunk)
+        s.self_w, s.self_b = critic.self_encoder[0].weight.data_ptr(), critic.self_encoder[0].bias.data_ptr()
+        s.obj_w, s.obj_b = critic.object_encoder[0].weight.data_ptr(), critic.object_encoder[0].bias.data_ptr()
+        if hasattr(critic, "action_encoder"):
+            s.ae_w, s.ae_b = critic.action_encoder[0].weight.data_ptr(), critic.action_encoder[0].bias.data_ptr()
         self.struct = s
         self.refresh()
 
@@ -81,11 +90,20 @@ class CriticPack:
         return out
 
 
-def _io(F, G, taus, N, **kw):
-    """AsvCriticIO for one launch; tensors become device pointers, None -> NULL."""
+def _io(F, G, taus, N, obs=None, act=None, xb=None, **kw):
+    """AsvCriticIO for one launch; tensors become device pointers, None -> NULL. With `obs`
+    (packed observation rows, any row stride) F may be None, with `act` ([B][2] view) G may be
+    None: the kernels then run the encoders themselves."""
     io = _abi.AsvCriticIO()
-    io.F, io.G, io.taus = F.data_ptr(), G.data_ptr(), taus.data_ptr()
-    io.B, io.N = F.shape[0], N
+    io.F, io.G, io.taus = _p(F), _p(G), taus.data_ptr()
+    io.B, io.N = (F if F is not None else obs).shape[0], N
+    if obs is not None:
+        assert obs.dtype == torch.float32 and obs.stride(-1) == 1
+        io.obs, io.ld_obs = obs.data_ptr(), obs.stride(0)
+    if act is not None:
+        assert act.dtype == torch.float32 and act.stride(-1) == 1
+        io.act, io.ld_act = act.data_ptr(), act.stride(0)
+    io.xb = _p(xb)
     io.Np, io.kappa, io.gamma, io.dq, io.ld_rd = kw.pop("Np", 0), kw.pop("kappa", 1.0), kw.pop("gamma", 0.0), \
         kw.pop("dq", 0.0), kw.pop("ld_rd", 1)
     io.loss_scale = kw.pop("loss_scale", 0.0)
@@ -94,10 +112,10 @@ def _io(F, G, taus, N, **kw):
     return io
 
 
-def critic_forward(pack, F, G, taus, N, q=None, stream=None):
-    B = F.shape[0]
-    q = q if q is not None else torch.empty(B * N, dtype=torch.float32, device=F.device)
-    io = _io(F, G, taus, N, q=q)
+def critic_forward(pack, F, G, taus, N, q=None, stream=None, obs=None, act=None):
+    B = (F if F is not None else obs).shape[0]
+    q = q if q is not None else torch.empty(B * N, dtype=torch.float32, device=taus.device)
+    io = _io(F, G, taus, N, obs=obs, act=act, q=q)
     _abi.check(_abi.lib().asvrl_critic_forward(C.byref(pack.struct), C.byref(io), _abi.stream_ptr(stream)),
                "asvrl_critic_forward")
     return q.view(B, N)
@@ -131,12 +149,12 @@ class TrainBuffers:
 
 
 def critic_train(pack, F, G, taus, q_targets, bufs, kappa=1.0, stream=None, q_next=None, rewards=None, dones=None,
-                 gamma=0.99, dzF=None, dzG=None, with_dFdG=True, tile_loss=None):
+                 gamma=0.99, dzF=None, dzG=None, with_dFdG=True, tile_loss=None, obs=None, act=None, xb=None):
     """TRAIN launch. Targets: q_targets (B, Np), or q_next (B, Np) with rewards/dones column
     views (stride ld) combined in the kernel. With `tile_loss` ([B*N/32] f32) the kernel writes
     per-tile loss partials (sum them, e.g. in a PartialArena) and None is returned; otherwise
     the loss row_loss.sum() / (B*Np) as a 0-d device tensor."""
-    B, N = F.shape[0], bufs.N
+    B, N = (F if F is not None else obs).shape[0], bufs.N
     Np = (q_targets if q_targets is not None else q_next).shape[1]
     kw = dict(q=bufs.q, row_loss=bufs.row_loss, dzF=dzF, dzG=dzG, tile_loss=tile_loss,
               loss_scale=1.0 / float(B * Np))
@@ -146,7 +164,7 @@ def critic_train(pack, F, G, taus, q_targets, bufs, kappa=1.0, stream=None, q_ne
         kw["q_targets"] = q_targets
     else:
         kw.update(q_next=q_next, rewards=rewards, dones=dones, ld_rd=rewards.stride(0), gamma=float(gamma))
-    io = _io(F, G, taus, N, Np=Np, kappa=float(kappa), **kw)
+    io = _io(F, G, taus, N, obs=obs, act=act, xb=xb, Np=Np, kappa=float(kappa), **kw)
     _abi.check(_abi.lib().asvrl_critic_train(C.byref(pack.struct), C.byref(io), C.byref(bufs.struct),
                                              _abi.stream_ptr(stream)), "asvrl_critic_train")
     if tile_loss is not None:
@@ -154,12 +172,13 @@ def critic_train(pack, F, G, taus, q_targets, bufs, kappa=1.0, stream=None, q_ne
     return bufs.row_loss.sum() / float(B * Np)
 
 
-def critic_actor_grad(pack, F, G, taus, N, q, dG=None, stream=None, w_ae=None, dA=None, tile_loss=None):
+def critic_actor_grad(pack, F, G, taus, N, q, dG=None, stream=None, w_ae=None, dA=None, tile_loss=None, obs=None,
+                      act=None):
     """ACTOR launch: dq = -1/(B*N) on every row; writes dG and/or dA (with w_ae); with
     `tile_loss` ([B*N/32]) per-tile partials of the actor loss -mean(q)."""
-    B = F.shape[0]
-    io = _io(F, G, taus, N, dq=-1.0 / float(B * N), q=q, dG=dG, w_ae=w_ae, dA=dA, tile_loss=tile_loss,
-             loss_scale=-1.0 / float(B * N))
+    B = (F if F is not None else obs).shape[0]
+    io = _io(F, G, taus, N, obs=obs, act=act, dq=-1.0 / float(B * N), q=q, dG=dG, w_ae=w_ae, dA=dA,
+             tile_loss=tile_loss, loss_scale=-1.0 / float(B * N))
     _abi.check(_abi.lib().asvrl_critic_actor_grad(C.byref(pack.struct), C.byref(io), _abi.stream_ptr(stream)),
                "asvrl_critic_actor_grad")
 

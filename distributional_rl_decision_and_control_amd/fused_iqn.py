@@ -5,10 +5,9 @@ IQN_Policy (IQN_model.py:74-108) is the AC-IQN critic trunk without the action e
 with a 128 -> 25 output layer, so it runs on the critic kernels' IQN modes. Per step, on a
 replay batch `rows` ([B][88]: obs | next obs | action | reward | done):
 
-    target encoders(ns) -> Ft                             asvrl_mlp_encode
-    target trunk, max over actions per tau -> q_next      asvrl_iqn_forward_max    (agent.py:451-452)
-    local encoders(s) -> F (+ bf16 obs copy)              asvrl_mlp_encode
-    forward, gather at a, quantile-Huber vs r + g q_next (1-d), backward
+    target encoders(ns) + trunk, max over actions per tau -> q_next
+                                                          asvrl_iqn_forward_max    (agent.py:451-452)
+    local encoders(s) + forward, gather at a, quantile-Huber vs r + g q_next (1-d), backward
                                                           asvrl_iqn_train (2 launches, agent.py:455-468)
     weight grads of the 4 trunk layers + encoders         asvrl_linear_wgrad_partial x5 (3 streams),
                                                           ONE asvrl_partial_sums_norm: every .grad
@@ -17,10 +16,11 @@ replay batch `rows` ([B][88]: obs | next obs | action | reward | done):
                                                           loss and the gradient norm
     clip + Adam                                           asvrl_adam_step          (agent.py:471-472)
       (with DP: asvrl_partial_sums, RCCL all-reduce, asvrl_adam_clip)
-    re-pack trunk, head and encoders                      asvrl_iqn_pack + asvrl_mlp_pack
+    re-pack trunk and head                                asvrl_iqn_pack
 
-act_iqn for every robot row: encoders, then one kernel (K = 32 quantile samples per state,
-mean over them, argmax, epsilon-greedy on the device step counter).
+The encoders run inside the trunk kernels' prologue (f32, from the parameters). act_iqn for
+every robot row is one kernel (encoders, K = 32 quantile samples per state, mean over them,
+argmax, epsilon-greedy on the device step counter).
 
 Arithmetic: bf16 MFMA operands with f32 accumulation, f32 master weights / Adam.
 """
@@ -31,7 +31,6 @@ import torch
 from . import _abi
 from .fused_critic import CriticPack, PartialArena, TrainBuffers
 from .fused_update import SideStreams, _reduce_and_step
-from .fused_mlp import MlpPack, mlp_encode
 
 OBS = 40
 K_ACT = 32
@@ -45,8 +44,8 @@ def supported(net, B, N):
 
 
 class IqnPack(CriticPack):
-    """bf16 images of one IQN_Policy: the trunk (CriticPack's five), the padded output head and
-    the observation encoders; refresh() is two launches."""
+    """bf16 images of one IQN_Policy: the trunk (CriticPack's five) and the padded output head,
+    one refresh launch; the observation encoders are read in f32 by the kernels themselves."""
 
     def __init__(self, net):
         dev = net.cos_embedding.weight.device
@@ -56,7 +55,6 @@ class IqnPack(CriticPack):
                                     net.output_layer.bias.data_ptr())
         hd.n_actions = net.action_size
         self.head = hd
-        self.enc = MlpPack(net, "encoders")
         super().__init__(net)
 
     def refresh(self, stream=None):
@@ -65,12 +63,18 @@ class IqnPack(CriticPack):
                                        _abi.ptr(n.hidden_layer_2.weight), _abi.ptr(n.output_layer.weight),
                                        C.byref(self.struct), C.byref(self.head), _abi.stream_ptr(stream))
         _abi.check(rc, "asvrl_iqn_pack")
-        self.enc.refresh(stream)
 
 
-def _io(F, N, **kw):
+def _io(F, N, obs=None, xb=None, **kw):
+    """AsvIqnIO for one launch: features F [B][256], or packed observation rows `obs` (any row
+    stride; the kernels run the encoders)."""
     io = _abi.AsvIqnIO()
-    io.F, io.B, io.N = F.data_ptr(), F.shape[0], N
+    io.F = F.data_ptr() if F is not None else None
+    io.B, io.N = (F if F is not None else obs).shape[0], N
+    if obs is not None:
+        assert obs.dtype == torch.float32 and obs.stride(-1) == 1
+        io.obs, io.ld_obs = obs.data_ptr(), obs.stride(0)
+    io.xb = xb.data_ptr() if xb is not None else None
     for k in ("Np", "kappa", "gamma", "ld_rd", "loss_scale", "ld_act", "eps_steps_per_count", "eps_total",
               "eps_fraction", "eps_initial", "eps_final", "seed"):
         if k in kw:
@@ -80,23 +84,23 @@ def _io(F, N, **kw):
     return io
 
 
-def iqn_forward_max(pack, F, taus, N, q, stream=None):
+def iqn_forward_max(pack, F, taus, N, q, stream=None, obs=None):
     """q[b*N + n] = max_a Q(s_b, tau_bn, a) (the target of train_IQN)."""
-    io = _io(F, N, taus=taus, q=q)
+    io = _io(F, N, obs=obs, taus=taus, q=q)
     _abi.check(_abi.lib().asvrl_iqn_forward_max(C.byref(pack.struct), C.byref(pack.head), C.byref(io),
                                                 _abi.stream_ptr(stream)), "asvrl_iqn_forward_max")
     return q
 
 
 def iqn_train(pack, F, taus, bufs, dz_out, q_next, actions, rewards, dones, gamma, dzF, tile_loss=None, kappa=1.0,
-              q=None, stream=None):
+              q=None, stream=None, obs=None, xb=None):
     """Forward + loss + backward of the local net. actions / rewards / dones are column views of
     the replay rows (one stride). Writes bufs' activations, dz_out, dzF and, with tile_loss,
     the per-tile loss partials (loss = their sum)."""
-    B, N = F.shape[0], bufs.N
+    B, N = (F if F is not None else obs).shape[0], bufs.N
     Np = q_next.shape[1]
     assert actions.stride(0) == rewards.stride(0) == dones.stride(0)
-    io = _io(F, N, taus=taus, Np=Np, kappa=float(kappa), q_next=q_next, actions=actions, rewards=rewards,
+    io = _io(F, N, obs=obs, xb=xb, taus=taus, Np=Np, kappa=float(kappa), q_next=q_next, actions=actions, rewards=rewards,
              dones=dones, ld_rd=rewards.stride(0), gamma=float(gamma), q=q, row_loss=bufs.row_loss, dzF=dzF,
              dz_out=dz_out, tile_loss=tile_loss, loss_scale=1.0 / float(B * Np))
     _abi.check(_abi.lib().asvrl_iqn_train(C.byref(pack.struct), C.byref(pack.head), C.byref(io),
@@ -104,9 +108,9 @@ def iqn_train(pack, F, taus, bufs, dz_out, q_next, actions, rewards, dones, gamm
 
 
 def iqn_act(pack, F, actions64, step_dev, steps_per_count, total, fraction, initial, final, seed, taus=None,
-            stream=None):
-    """act_iqn for every row of F into actions64[:, 0] (f64 action index)."""
-    io = _io(F, K_ACT, taus=taus, act_out=actions64, ld_act=actions64.stride(0), step_dev=step_dev,
+            stream=None, obs=None):
+    """act_iqn for every row of F (or of the observation rows `obs`) into actions64[:, 0] (f64 action index)."""
+    io = _io(F, K_ACT, obs=obs, taus=taus, act_out=actions64, ld_act=actions64.stride(0), step_dev=step_dev,
              eps_steps_per_count=float(steps_per_count), eps_total=float(total), eps_fraction=float(fraction),
              eps_initial=float(initial), eps_final=float(final), seed=int(seed) & 0xFFFFFFFFFFFFFFFF)
     _abi.check(_abi.lib().asvrl_iqn_act(C.byref(pack.struct), C.byref(pack.head), C.byref(io),
@@ -125,7 +129,6 @@ class FusedIQNState:
         self.bufs = TrainBuffers(B, N, dev)
         f = dict(dtype=torch.float32, device=dev)
         bf = dict(dtype=torch.bfloat16, device=dev)
-        self.F, self.Ft = torch.empty(B, 256, **f), torch.empty(B, 256, **f)
         self.xb = torch.empty(B, 32, **bf)
         self.q_next = torch.empty(B * N, **f)
         self.dzF = torch.empty(B, 256, **bf)
@@ -133,7 +136,6 @@ class FusedIQNState:
         self.arena = PartialArena(16 << 20, dev)
         self.loss = torch.zeros(1, **f)
         self.tile_loss = torch.zeros(B * N // 32, **f)
-        self.F_act = None
         self.side = SideStreams(dev, 2)
 
     def target_changed(self):
@@ -141,11 +143,8 @@ class FusedIQNState:
         self.target.refresh()
 
     def act(self, obs_rows, actions64, step_dev, steps_per_count, total, fraction, initial, final, seed):
-        n = obs_rows.shape[0]
-        if self.F_act is None or self.F_act.shape[0] != n:
-            self.F_act = torch.empty(n, 256, dtype=torch.float32, device=self.device)
-        mlp_encode(self.local.enc, obs_rows, self.F_act)
-        iqn_act(self.local, self.F_act, actions64, step_dev, steps_per_count, total, fraction, initial, final, seed)
+        iqn_act(self.local, None, actions64, step_dev, steps_per_count, total, fraction, initial, final, seed,
+                obs=obs_rows)
 
 
 def iqn_grads(st, net, rows, taus, gamma=0.99, flush=True):
@@ -156,14 +155,10 @@ def iqn_grads(st, net, rows, taus, gamma=0.99, flush=True):
     s_rows, ns_rows = rows[:, 0:OBS], rows[:, OBS:2 * OBS]
     a_col, r_col, d_col = rows[:, 80], rows[:, 82], rows[:, 83]
     bufs, arena, side = st.bufs, st.arena, st.side
-    # every .grad is overwritten below (no zeroing); independent launches on side streams
-    with side.on(0):
-        mlp_encode(st.local.enc, s_rows, st.F, xb=st.xb)
-    mlp_encode(st.target.enc, ns_rows, st.Ft)
-    iqn_forward_max(st.target, st.Ft, taus[0], N, st.q_next)
-    side.join(0)
-    iqn_train(st.local, st.F, taus[1], bufs, st.dz_out, st.q_next.view(B, N), a_col, r_col, d_col, gamma, st.dzF,
-              tile_loss=st.tile_loss)
+    # every .grad is overwritten below (no zeroing); the trunk kernels run the encoders on the rows
+    iqn_forward_max(st.target, None, taus[0], N, st.q_next, obs=ns_rows)
+    iqn_train(st.local, None, taus[1], bufs, st.dz_out, st.q_next.view(B, N), a_col, r_col, d_col, gamma, st.dzF,
+              tile_loss=st.tile_loss, obs=s_rows, xb=st.xb)
     with side.on(0):
         arena.linear(bufs.dzc, bufs.cos, net.cos_embedding.weight.grad, net.cos_embedding.bias.grad)
         arena.fold(st.dzF, st.xb, net)   # encoder image -> self/object encoder grads

@@ -1,13 +1,11 @@
 """The whole AC-IQN update (Agent.train_AC_IQN, agent.py:386-432) on hand-written gfx950
-kernels: about 35 launches per step, no torch autograd, no host synchronisation.
+kernels: about 30 launches per step, no torch autograd, no host synchronisation.
 
 Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | done):
   critic (agent.py:395-416)
     target actor(ns) -> na                               asvrl_actor_forward(FWD)
-    target encoders(ns, na) -> Ft, Gt                    asvrl_mlp_encode
-    target trunk -> q_next                               asvrl_critic_forward
-    local encoders(s, a) -> F, G (+ bf16 obs copy)       asvrl_mlp_encode
-    trunk forward + quantile-Huber vs r + g q_next (1-d) + backward
+    target encoders(ns, na) + trunk -> q_next            asvrl_critic_forward (encoders in the prologue)
+    local encoders(s, a) + trunk forward + quantile-Huber vs r + g q_next (1-d) + backward
                                                           asvrl_critic_train (targets formed in-kernel)
     trunk weight grads                                   asvrl_linear_wgrad_partial x3 + _vec
     encoder grads (256x32 image) and action-encoder grads
@@ -16,11 +14,11 @@ Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | 
                                                           ONE asvrl_partial_sums_norm
     clip + Adam                                          asvrl_adam_step
       (with DP: asvrl_partial_sums, RCCL all-reduce, asvrl_adam_clip)
-    re-pack trunk and encoders                           asvrl_critic_pack + asvrl_mlp_pack
+    re-pack trunk                                        asvrl_critic_pack
   actor (agent.py:419-427), through the UPDATED critic
     actor(s) saving activations -> a                     asvrl_actor_forward(TRAIN)
-    encoders(s, a) -> F2, G2                             asvrl_mlp_encode
-    trunk forward + backward of -mean(q) to the action   asvrl_critic_actor_grad (dA in-kernel)
+    encoders(s, a) + trunk forward + backward of -mean(q) to the action
+                                                          asvrl_critic_actor_grad (dA in-kernel)
     actor backward                                       asvrl_actor_backward
     actor weight grads                                   wgrad partials x5, one asvrl_partial_sums_norm
     clip + Adam, re-pack actor                           asvrl_adam_step + asvrl_mlp_pack
@@ -38,7 +36,7 @@ import torch
 
 from .fused_critic import (CriticPack, PartialArena, TrainBuffers, critic_actor_grad, critic_forward, critic_train,
                            trunk_weight_grads_into)
-from .fused_mlp import ActorBuffers, MlpPack, actor_act, actor_backward, actor_forward, actor_train_forward, mlp_encode
+from .fused_mlp import ActorBuffers, MlpPack, actor_act, actor_backward, actor_forward, actor_train_forward
 from .learner import FusedAdam, clip_and_step
 
 OBS = 40
@@ -80,10 +78,9 @@ class FusedACIQNState:
     def __init__(self, policy_local, policy_target, B, N):
         dev = policy_local.critic.cos_embedding.weight.device
         self.B, self.N, self.device = B, N, dev
+        # the critic's encoders run inside the trunk kernels (f32, straight from the parameters)
         self.local_trunk = CriticPack(policy_local.critic)
         self.target_trunk = CriticPack(policy_target.critic)
-        self.local_cenc = MlpPack(policy_local.critic, "critic")
-        self.target_cenc = MlpPack(policy_target.critic, "critic")
         self.actor = MlpPack(policy_local.actor, "actor")
         self.target_actor = MlpPack(policy_target.actor, "actor")
         self.bufs = TrainBuffers(B, N, dev)
@@ -91,9 +88,6 @@ class FusedACIQNState:
         f = dict(dtype=torch.float32, device=dev)
         bf = dict(dtype=torch.bfloat16, device=dev)
         self.na = torch.empty(B, 2, **f)
-        self.Ft, self.Gt = torch.empty(B, 256, **f), torch.empty(B, 128, **f)
-        self.F, self.G = torch.empty(B, 256, **f), torch.empty(B, 128, **f)
-        self.F2, self.G2 = torch.empty(B, 256, **f), torch.empty(B, 128, **f)
         self.xb = torch.empty(B, 32, **bf)
         self.q_next = torch.empty(B * N, **f)
         self.q_pi = torch.empty(B * N, **f)
@@ -107,7 +101,6 @@ class FusedACIQNState:
     def target_changed(self):
         """Re-pack the target networks after a hard/soft update (eager, outside graphs)."""
         self.target_trunk.refresh()
-        self.target_cenc.refresh()
         self.target_actor.refresh()
 
     def act(self, obs_rows, actions64, step_dev, steps_per_count, total, fraction, initial, final, seed):
@@ -146,17 +139,15 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     bufs, ab, arena = st.bufs, st.abufs, st.arena
 
     side = st.side
-    # ---- critic (agent.py:395-416); every critic .grad is overwritten below (no zeroing)
-    with side.on(0):   # local encoders: independent of the target chain
-        mlp_encode(st.local_cenc, s_rows, st.F, st.G, act=a_rows, xb=st.xb)
+    # ---- critic (agent.py:395-416); every critic .grad is overwritten below (no zeroing). The
+    # trunk kernels run the critic's observation / action encoders on the replay rows themselves.
     with side.on(1):   # the actor's training forward reads only s and the (not yet updated) actor
         actor_train_forward(st.actor, s_rows, ab)
     actor_forward(st.target_actor, ns_rows, st.na)
-    mlp_encode(st.target_cenc, ns_rows, st.Ft, st.Gt, act=st.na)
-    critic_forward(st.target_trunk, st.Ft, st.Gt, taus[0], N, q=st.q_next)
-    side.join(0)
-    critic_train(st.local_trunk, st.F, st.G, taus[1], None, bufs, q_next=st.q_next.view(B, N), rewards=r_col,
-                 dones=d_col, gamma=gamma, dzF=st.dzF, dzG=st.dzG, with_dFdG=False, tile_loss=st.tile_loss[0])
+    critic_forward(st.target_trunk, None, None, taus[0], N, q=st.q_next, obs=ns_rows, act=st.na)
+    critic_train(st.local_trunk, None, None, taus[1], None, bufs, q_next=st.q_next.view(B, N), rewards=r_col,
+                 dones=d_col, gamma=gamma, dzF=st.dzF, dzG=st.dzG, with_dFdG=False, tile_loss=st.tile_loss[0],
+                 obs=s_rows, act=a_rows, xb=st.xb)
     ae = critic.action_encoder[0]
     # the six weight-gradient reductions on three streams, one partial-sum launch after the join
     with side.on(0):
@@ -171,12 +162,10 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     arena.scalar(st.tile_loss[0], st.losses[0:1])   # the critic loss
     cgn = _reduce_and_step(arena, critic_opt, critic_grads, sync, max_norm)
     st.local_trunk.refresh()
-    st.local_cenc.refresh()
 
     # ---- actor through the updated critic (agent.py:419-427); its forward ran on side stream 1
-    mlp_encode(st.local_cenc, s_rows, st.F2, st.G2, act=ab.a_out)
-    critic_actor_grad(st.local_trunk, st.F2, st.G2, taus[2], N, st.q_pi, w_ae=ae.weight, dA=ab.dA,
-                      tile_loss=st.tile_loss[1])
+    critic_actor_grad(st.local_trunk, None, None, taus[2], N, st.q_pi, w_ae=ae.weight, dA=ab.dA,
+                      tile_loss=st.tile_loss[1], obs=s_rows, act=ab.a_out)
     actor_backward(st.actor, ab)
     ow, obias = actor.output_layer.weight.grad, actor.output_layer.bias.grad
     with side.on(0):

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 3
+#define ASVRL_ABI_VERSION 4
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -202,6 +202,16 @@ typedef struct AsvCriticWeights {
   const float* b2;       /* hidden_layer_2.bias [128] */
   const float* wo;       /* output_layer.weight [128] */
   const float* bo;       /* output_layer.bias [1] */
+  /* f32 encoder parameters, read when an IO struct passes observation rows (obs != NULL): the
+   * trunk kernels then compute F = observation_processor(obs) (AC_IQN_model.py:284-308,
+   * IQN_model.py:80-96) and G = action_encoder(act) (AC_IQN_model.py:468-470) per sample in their
+   * prologue instead of reading F / G. NULL when unused. */
+  const float* self_w;   /* self_encoder.0.weight (56 x 7), .bias [56] */
+  const float* self_b;
+  const float* obj_w;    /* object_encoder.0.weight (40 x 5), .bias [40] */
+  const float* obj_b;
+  const float* ae_w;     /* action_encoder.0.weight (128 x 2), .bias [128] (AC-IQN critic only) */
+  const float* ae_b;
 } AsvCriticWeights;
 
 /* bf16 row-major activations the TRAIN mode writes for the weight gradients
@@ -225,8 +235,13 @@ int asvrl_critic_pack(const float* wc, const float* w1, const float* w2, const A
 /* Inputs / outputs of one critic launch. F (B x 256) = observation_processor features,
  * G (B x 128) = action_encoder features, taus (B x N); N in {8, 16, 32}. */
 typedef struct AsvCriticIO {
-  const float* F;
-  const float* G;
+  const float* F;          /* [B][256], or NULL with obs set */
+  const float* G;          /* [B][128], or NULL with act set */
+  const float* obs;        /* optional packed observation rows (ASVRL_OBS_DIM layout) at obs[b*ld_obs] */
+  int64_t ld_obs;
+  const float* act;        /* optional actions (2 f32) at act[b*ld_act] */
+  int64_t ld_act;
+  void* xb;                /* TRAIN optional: bf16 [B][32] copy of obs columns 0..31 (encoder wgrad operand) */
   const float* taus;
   int32_t B, N, Np;
   float kappa;
@@ -284,7 +299,10 @@ int asvrl_iqn_pack(const float* wc, const float* w1, const float* w2, const floa
 
 /* Inputs / outputs of one IQN launch. Rows are (sample b, tau n), R = B*N. */
 typedef struct AsvIqnIO {
-  const float* F;          /* [B][256] observation features (asvrl_mlp_encode) */
+  const float* F;          /* [B][256] observation features, or NULL with obs set */
+  const float* obs;        /* optional packed observation rows at obs[b*ld_obs] (encoders in-kernel) */
+  int64_t ld_obs;
+  void* xb;                /* TRAIN optional: bf16 [B][32] copy of obs columns 0..31 */
   const float* taus;       /* [B*N]; ACT: may be NULL = drawn in the kernel (Philox, uniform [0,1)) */
   int32_t B, N, Np;        /* N in {8,16,32} (ACT: N = K = 32); Np = target quantiles per sample (TRAIN) */
   float kappa;             /* Huber threshold (1.0, agent.py:458) */

@@ -64,6 +64,27 @@ def test_fused_forward(B, N):
     assert err < 2e-2, err
 
 
+@pytest.mark.parametrize("B,N", [(64, 8), (256, 16), (1024, 32)])
+def test_encoders_in_kernel_match_torch(B, N):
+    """Observation rows + actions instead of F / G: the trunk kernels run the critic's encoders
+    (observation_processor, action_encoder) in f32 in their prologue; q matches torch fp32 and
+    the F / G path."""
+    from distributional_rl_decision_and_control_amd.fused_critic import CriticPack, critic_forward
+    critic, s, a, taus = _setup(B, N, seed=3)
+    rows = torch.zeros(B, 88, device="cuda")
+    rows[:, 0:7], rows[:, 7:32], rows[:, 32:37] = s[0], s[1].reshape(B, 25), s[2]
+    rows[:, 80:82] = a
+    pack = CriticPack(critic)
+    with torch.no_grad():
+        q_ref, _ = critic(s, a, N, taus=taus.unsqueeze(-1))
+        F, G = _features(critic, s, a)
+        q_fg = critic_forward(pack, F.contiguous(), G.contiguous(), taus.contiguous(), N)
+        q_obs = critic_forward(pack, None, None, taus.contiguous(), N, obs=rows[:, 0:40], act=rows[:, 80:82])
+    scale = q_ref.abs().max().item()
+    assert (q_obs - q_ref).abs().max().item() / scale < 2e-2
+    assert (q_obs - q_fg).abs().max().item() / scale < 1e-2
+
+
 @pytest.mark.parametrize("B,N,Np", [(64, 8, 8), (512, 32, 32)])
 def test_fused_train_gradients(B, N, Np):
     from distributional_rl_decision_and_control_amd.fused_critic import (CriticPack, TrainBuffers, critic_train,
