@@ -11,11 +11,12 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ASVRL_LIB", os.path.join(HERE, "lib", "libasvrl.so"))  # override: A/B variants
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
 OBS_DIM = 40   # self 7 | objects 25 | mask 5 | pad 3
 TR_DIM = 88    # obs 40 | next obs 40 | action 2 | reward | done | pad 4
+PER_DIM = 48   # obs 40 | action | reward | nonterminal | timestep (i32) | pad 4
 
 # robot state fields (enum AsvRobotField)
 F_X, F_Y, F_THETA, F_VR0, F_VR1, F_VR2, F_V0, F_V1, F_V2, F_TL, F_TR, F_LP, F_RP, F_GX, F_GY, F_PHI, F_RET = range(17)
@@ -140,6 +141,13 @@ class AsvMlpIO(C.Structure):
                 ("eps_initial", _D), ("eps_final", _D), ("seed", _U64)]
 
 
+class AsvPer(C.Structure):
+    _fields_ = [("rows", _VP), ("tree", _VP), ("state", _VP), ("t", _VP), ("maxp", _VP), ("dirty", _VP),
+                ("capacity", _I64), ("tree_leaves", _I64), ("stride", _I32), ("n_step", _I32), ("discount", _D),
+                ("priority_weight", C.c_float), ("priority_exponent", C.c_float), ("deferred", _I32),
+                ("_pad0", _I32)]
+
+
 EXPORTS = [
     ("asvrl_env_step", C.c_int, [C.POINTER(AsvParams), C.POINTER(AsvEnvState), _VP, _VP, C.POINTER(AsvStepCtl),
                                  C.POINTER(AsvStepOut), _VP]),
@@ -161,6 +169,9 @@ EXPORTS = [
     ("asvrl_replay_push", C.c_int, [_VP, _VP, _VP, _VP, _I32, _VP, _VP, _I32, _VP, _I64, _VP, _VP, _VP]),
     ("asvrl_replay_sample", C.c_int, [_VP, _I64, _VP, _VP, _I32, _U64, _U64, _VP, _I64, _VP, _VP, _VP]),
     ("asvrl_replay_write_rows", C.c_int, [_VP, _VP, _I32, _VP, _VP]),
+    ("asvrl_per_push", C.c_int, [C.POINTER(AsvPer), _VP, _VP, _VP, _I32, _VP, _VP, _I32, _VP]),
+    ("asvrl_per_sample", C.c_int, [C.POINTER(AsvPer), _I32, _VP, _U64, _U64, _VP, _VP, _VP, _VP]),
+    ("asvrl_per_update", C.c_int, [C.POINTER(AsvPer), _VP, _VP, _I32, _I32, _VP]),
     ("asvrl_adam_clip", C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, _F, _F, _VP, _VP, _VP]),
     ("asvrl_linear_wgrad_workspace", _I64, [_I32, _I32]),
     ("asvrl_linear_wgrad_groups", _I32, [_I32, _I32, _I32]),

@@ -79,21 +79,31 @@ __global__ __launch_bounds__(1024) void mean_kernel(const float* __restrict__ x,
 }
 
 // ------------------------------------------------------------------ C51 projection
-// One wave per row, lane j = atom j. The reference accumulates with two sequential CPU
-// index_add_ passes (lower masses, then upper masses, each in atom order); lane k rebuilds
-// m[k] in exactly that order from shuffles, so the f32 result is bit-identical.
-__global__ __launch_bounds__(4 * kWave) void c51_kernel(const float* __restrict__ pns_a,
-                                                        const float* __restrict__ ret,
-                                                        const float* __restrict__ nonterm,
-                                                        const float* __restrict__ support, int B, int atoms,
-                                                        float vmin, float vmax, float dz, float gamma_n,
-                                                        float* __restrict__ m) {
+// One wave per row, lane j = atom j. The reference accumulates with two sequential CPU index_add_
+// passes (lower masses, then upper masses, each in atom order), so m[k] = ((0 + the lower masses with
+// l_j = k, in j order) + the upper masses with u_j = k, in j order). b_j is non-decreasing in j
+// (Tz = R + nonterminal * gamma^n * z_j with nonterminal * gamma^n >= 0, clamp and the affine map are
+// monotone under rounding), and so are l_j and u_j after the two integer fixes, so the j with a
+// given l (or u) form one contiguous run. Each lane records in LDS where the run of its target
+// starts; lane k then adds exactly its own runs in order: bit-identical to the reference, with
+// ~2 LDS reads per lane instead of 2 * atoms shuffles.
+constexpr int kC51Waves = 4;
+
+__global__ __launch_bounds__(kC51Waves * kWave) void c51_kernel(const float* __restrict__ pns_a,
+                                                                const float* __restrict__ ret,
+                                                                const float* __restrict__ nonterm,
+                                                                const float* __restrict__ support, int B,
+                                                                int atoms, float vmin, float vmax, float dz,
+                                                                float gamma_n, float* __restrict__ m) {
+  __shared__ float s_lo[kC51Waves][kWave], s_up[kC51Waves][kWave];
+  __shared__ int s_l[kC51Waves][kWave + 1], s_u[kC51Waves][kWave + 1];
+  __shared__ int s_lstart[kC51Waves][kWave], s_ustart[kC51Waves][kWave];
   const int lane = threadIdx.x & (kWave - 1);
-  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= B) return;
-  const bool on = lane < atoms;
-  float lower = 0.f, upper = 0.f;
+  const int w = threadIdx.x >> 6;
+  const int b = blockIdx.x * kC51Waves + w;
+  const bool on = b < B && lane < atoms;
   int l = -1, u = -1;
+  float lower = 0.f, upper = 0.f;
   if (on) {
     const float ntg = nonterm[b] * gamma_n;
     float tz = ret[b] + ntg * support[lane];      // Tz = R + nonterminal * gamma^n * z
@@ -107,18 +117,24 @@ __global__ __launch_bounds__(4 * kWave) void c51_kernel(const float* __restrict_
     lower = p * (static_cast<float>(u) - bb);
     upper = p * (bb - static_cast<float>(l));
   }
+  s_l[w][lane] = l;
+  s_u[w][lane] = u;
+  s_lo[w][lane] = lower;
+  s_up[w][lane] = upper;
+  s_lstart[w][lane] = -1;
+  s_ustart[w][lane] = -1;
+  if (lane == 0) { s_l[w][kWave] = -1; s_u[w][kWave] = -1; }
+  __syncthreads();
+  if (on) {
+    if (lane == 0 || s_l[w][lane - 1] != l) s_lstart[w][l] = lane;
+    if (lane == 0 || s_u[w][lane - 1] != u) s_ustart[w][u] = lane;
+  }
+  __syncthreads();
+  if (!on) return;
   float acc = 0.f;
-  for (int j = 0; j < atoms; ++j) {
-    const int lj = __shfl(l, j, kWave);
-    const float vj = __shfl(lower, j, kWave);
-    if (lj == lane) acc += vj;
-  }
-  for (int j = 0; j < atoms; ++j) {
-    const int uj = __shfl(u, j, kWave);
-    const float vj = __shfl(upper, j, kWave);
-    if (uj == lane) acc += vj;
-  }
-  if (on) m[static_cast<size_t>(b) * atoms + lane] = acc;
+  for (int j = s_lstart[w][lane]; j >= 0 && j < atoms && s_l[w][j] == lane; ++j) acc += s_lo[w][j];
+  for (int j = s_ustart[w][lane]; j >= 0 && j < atoms && s_u[w][j] == lane; ++j) acc += s_up[w][j];
+  m[static_cast<size_t>(b) * atoms + lane] = acc;
 }
 
 // ------------------------------------------------------------------ replay ring
@@ -280,7 +296,8 @@ extern "C" int asvrl_c51_project(const float* pns_a, const float* returns, const
   ASVRL_REQUIRE(pns_a && returns && nonterminal && support && m, "asvrl_c51_project: null argument");
   ASVRL_REQUIRE(atoms >= 2 && atoms <= kWave, "asvrl_c51_project: atoms must be in [2, 64]");
   if (B <= 0) return 0;
-  hipLaunchKernelGGL(c51_kernel, dim3((B + 3) / 4), dim3(4 * kWave), 0, as_stream(stream), pns_a, returns,
+  hipLaunchKernelGGL(c51_kernel, dim3((B + kC51Waves - 1) / kC51Waves), dim3(kC51Waves * kWave), 0,
+                     as_stream(stream), pns_a, returns,
                      nonterminal, support, B, atoms, vmin, vmax, delta_z, gamma_n, m);
   return check_launch("asvrl_c51_project");
 }

@@ -133,3 +133,87 @@ def split_rows(rows):
     ns = (rows[:, OBS_DIM:OBS_DIM + 7], rows[:, OBS_DIM + 7:OBS_DIM + 32].reshape(B, 5, 5),
           rows[:, OBS_DIM + 32:OBS_DIM + 37])
     return s, rows[:, 80:82], rows[:, 82:83], ns, rows[:, 83:84]
+
+
+# ---------------------------------------------------------------------- prioritised replay
+class DevicePER:
+    """Rainbow's prioritised n-step replay (ReplayMemory + SegmentTree,
+    replay_memory_rainbow.py:14-196) resident in HBM (asvrl_per_*).
+
+    `stride` slots per time step: stride = 1 is the reference's single append sequence (its
+    n-step window spans whatever was appended next); stride = E*R gives every robot of the
+    batch its own stream, so each window is one robot's trajectory. Capacity is rounded down to
+    a multiple of stride; the sum tree has next_pow2(capacity) leaves (<= 2^22). deferred=True
+    (the batched trainer): a slot's priority enters the tree only once the push n steps later
+    completes its window, so sampling never meets the reference's rejection case.
+
+    sample() returns (rows [B, 88], tree_idx [B]): obs 0:40 | n-th next obs 40:80 | action 80 |
+    R^n 82 | nonterminal 83 | importance weight 84 (normalised by the batch max here) | p 85."""
+
+    def __init__(self, capacity, stride=1, n_step=3, discount=0.99, priority_weight=0.4, priority_exponent=0.5,
+                 deferred=False, device="cuda"):
+        _abi.lib()
+        self.device = torch.device(device)
+        self.stride = int(stride)
+        self.capacity = (int(capacity) // self.stride) * self.stride
+        P = 1 << (self.capacity - 1).bit_length()
+        if self.capacity < 2 or P > (1 << 22):
+            raise ValueError(f"DevicePER capacity {capacity} (stride {stride}) outside [2, 2^22]")
+        self.tree_leaves = P
+        self.n_step, self.discount = int(n_step), float(discount)
+        self.priority_weight, self.priority_exponent = float(priority_weight), float(priority_exponent)
+        dev = self.device
+        self.rows = torch.zeros((self.capacity, _abi.PER_DIM), dtype=torch.float32, device=dev)
+        self.tree = torch.zeros(2 * P - 1, dtype=torch.float32, device=dev)
+        self.state = torch.zeros(4, dtype=torch.int64, device=dev)
+        self.t = torch.zeros(self.stride, dtype=torch.int32, device=dev)
+        self.maxp = torch.ones(1, dtype=torch.float32, device=dev)
+        self.dirty = torch.zeros(max(1, P // 2048), dtype=torch.uint8, device=dev)
+        s = _abi.AsvPer()
+        s.rows, s.tree, s.state, s.t = self.rows.data_ptr(), self.tree.data_ptr(), self.state.data_ptr(), \
+            self.t.data_ptr()
+        s.maxp, s.dirty = self.maxp.data_ptr(), self.dirty.data_ptr()
+        s.capacity, s.tree_leaves, s.stride, s.n_step = self.capacity, P, self.stride, self.n_step
+        s.discount, s.priority_weight, s.priority_exponent = self.discount, self.priority_weight, \
+            self.priority_exponent
+        s.deferred = 1 if deferred else 0
+        self.deferred = bool(deferred)
+        self._s = s
+        self.pushed = 0   # host count of pushed slots (num_elements without a device sync)
+
+    def push(self, obs, obj_cnt, actions, reward, done, stream=None):
+        """append() for n = m * stride rows (time-major); rows with obj_cnt < 0 become blank slots."""
+        n = obs.shape[0]
+        adim = actions.shape[1] if actions.dim() == 2 else 1
+        rc = _abi.lib().asvrl_per_push(C.byref(self._s), _abi.ptr(obs), _abi.ptr(obj_cnt), _abi.ptr(actions), adim,
+                                       _abi.ptr(reward), _abi.ptr(done), n, _abi.stream_ptr(stream))
+        _abi.check(rc, "asvrl_per_push")
+        self.pushed += n
+
+    def num_elements(self):
+        """SegmentTree.num_elements (:62-66) from the host count (index + 1 until full)."""
+        return self.capacity if self.pushed >= self.capacity else self.pushed + 1
+
+    def sample(self, B, uniforms=None, seed=0, counter=0, counter_dev=None, out=None, out_idx=None, stream=None,
+               normalise=True):
+        out = out if out is not None else torch.empty((B, TR_DIM), dtype=torch.float32, device=self.device)
+        idx = out_idx if out_idx is not None else torch.empty(B, dtype=torch.int64, device=self.device)
+        if uniforms is not None:
+            uniforms = uniforms.to(device=self.device, dtype=torch.float64).contiguous()
+        rc = _abi.lib().asvrl_per_sample(C.byref(self._s), int(B), _abi.ptr(uniforms),
+                                         int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter) & 0xFFFFFFFFFFFFFFFF,
+                                         _abi.ptr(counter_dev), _abi.ptr(out), _abi.ptr(idx), _abi.stream_ptr(stream))
+        _abi.check(rc, "asvrl_per_sample")
+        if normalise:
+            w = out[:, 84]
+            w.div_(w.max())   # weights / weights.max() (:191)
+        return out, idx
+
+    def update_priorities(self, tree_idx, values, raw=False, stream=None):
+        v = values.detach().float().reshape(-1).contiguous()
+        rc = _abi.lib().asvrl_per_update(C.byref(self._s), _abi.ptr(tree_idx), _abi.ptr(v), v.shape[0],
+                                         1 if raw else 0, _abi.stream_ptr(stream))
+        _abi.check(rc, "asvrl_per_update")
+
+    def anomalies(self):
+        return int(self.state[3].item())

@@ -25,10 +25,11 @@ from .fused_update import FusedACIQNState, ac_iqn_update_fused2
 from .fused_iqn import FusedIQNState, iqn_update_fused
 from .fused_iqn import supported as fused_iqn_supported
 from .fused_update import supported as fused2_supported
-from .learn_ops import DeviceReplay, split_rows
-from .learner import FlatGrads, FusedAdam, GradSync, ac_iqn_update, iqn_update
+from .learn_ops import DevicePER, DeviceReplay, split_rows
+from .learner import FlatGrads, FusedAdam, GradSync, ac_iqn_update, iqn_update, rainbow_update
 from .policy.AC_IQN_model import AC_IQN_Policy
 from .policy.IQN_model import IQN_Policy
+from .policy.Rainbow_model import Rainbow_Policy
 from .vec_env import VecMarineNavEnv, split_obs
 
 DEFAULT_NET = dict(self_dimension=7, object_dimension=5, max_object_num=5, self_feature_dimension=56,
@@ -99,10 +100,38 @@ class VecTrainer:
             if fused is True and fused_adam and amp_dtype is not None and fused_iqn_supported(self.local, batch_size,
                                                                                             num_tau):
                 self.fused_iqn = FusedIQNState(self.local, self.target, batch_size, num_tau)
+        elif agent_type == "Rainbow":
+            # Rainbow_Policy (dueling NoisyNet C51, 51 atoms on [-1, 1]) with the prioritised n-step
+            # replay in HBM, one stream per robot (agent.py:597-641, replay_memory_rainbow.py)
+            self.local = Rainbow_Policy(**DEFAULT_NET, action_size=25, atoms=51, device=self.device,
+                                        seed=net_seed).to(self.device)
+            self.target = Rainbow_Policy(**DEFAULT_NET, action_size=25, atoms=51, device=self.device,
+                                         seed=net_seed).to(self.device)
+            for p in self.target.parameters():
+                p.requires_grad_(False)
+            if fused_adam:
+                self.opt = FusedAdam(self.local.parameters(), lr=lr)
+                self.grads = self.opt.grads
+            else:
+                self.grads = FlatGrads(self.local.parameters())
+                self.opt = torch.optim.Adam(self.local.parameters(), lr=lr, capturable=capturable)
+            self.action_dim = 1
+            self.n_step = 3
+            self.support = torch.linspace(-1.0, 1.0, 51, device=self.device)
         else:
-            raise NotImplementedError(f"VecTrainer agent_type {agent_type!r} (AC-IQN and IQN are batched)")
+            raise NotImplementedError(f"VecTrainer agent_type {agent_type!r} (AC-IQN, IQN and Rainbow are batched)")
         NT = self.E * self.R
-        self.replay = DeviceReplay(max(buffer_size, 2 * NT), device=self.device)
+        self.per = None
+        if agent_type == "Rainbow":
+            slots = max(min(buffer_size, 1 << 22) // NT, self.n_step + 3)
+            self.per = DevicePER(slots * NT, stride=NT, n_step=self.n_step, discount=gamma, deferred=True,
+                                 device=self.device)
+            self.replay = None
+            self.per_idx = torch.zeros(self.B, dtype=torch.int64, device=self.device)
+            # the tree holds complete windows once n + 1 pushes are in
+            self.learning_starts = max(self.learning_starts, (self.n_step + 1) * NT + self.B)
+        else:
+            self.replay = DeviceReplay(max(buffer_size, 2 * NT), device=self.device)
         self.actions = torch.zeros((NT, 2), dtype=torch.float64, device=self.device)
         self.learn_counter = torch.zeros(1, dtype=torch.int64, device=self.device)
         self.batch_rows = torch.zeros((self.B, 88), dtype=torch.float32, device=self.device)
@@ -148,6 +177,15 @@ class VecTrainer:
         NT = obs[0].shape[0]
         eps = self.epsilon()
         explore = torch.rand((NT, 1), device=self.device) < eps
+        if self.agent_type == "Rainbow":
+            # act_rainbow (agent.py:308-324) on every robot row, training-mode noisy weights
+            amp = torch.autocast("cuda", dtype=self.amp_dtype) if self.amp_dtype is not None else _null()
+            with amp:
+                p = self.local(obs)
+            greedy = (p.float() * self.support).sum(2).argmax(1)
+            rnd = torch.randint(0, 25, (NT,), device=self.device)
+            self.actions[:, 0].copy_(torch.where(explore.squeeze(1), rnd, greedy))
+            return
         if self.agent_type == "AC-IQN":
             # fp32 actor when the critic is fused (see ac_iqn_update_fused)
             use_amp = self.amp_dtype is not None and self.fused is None
@@ -169,6 +207,9 @@ class VecTrainer:
 
     def _push(self):
         env = self.env
+        if self.per is not None:   # ReplayMemory.append of every robot that acted (trainer.py:163-164)
+            self.per.push(env.obs_cur, env.cnt_next, self.actions[:, :1], env.batch.reward, env.batch.done)
+            return
         self.replay.push(env.obs_cur, env.obs_next, env.cnt_next, self.actions[:, :self.action_dim].contiguous()
                          if self.action_dim == 1 else self.actions, env.batch.reward, env.batch.done)
 
@@ -179,6 +220,18 @@ class VecTrainer:
         self.env.auto_reset()
 
     def learn(self, state=None, guard=0, actor_wait=None):
+        if self.per is not None:
+            rows, idx = self.per.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter,
+                                        out=self.batch_rows, out_idx=self.per_idx)
+            s, a, R, ns, nt = split_rows(rows)
+            amp = torch.autocast("cuda", dtype=self.amp_dtype) if self.amp_dtype is not None else _null()
+            with amp:
+                loss, gn = rainbow_update(self.local, self.target, self.opt, self.grads, self.support, s,
+                                          a[:, 0].to(torch.int64), R, ns, nt, rows[:, 84], gamma=self.gamma,
+                                          n=self.n_step, sync=self.sync)
+            self.per.update_priorities(idx, loss)   # update_priorities(idxs, loss) (agent.py:639)
+            self.learn_counter += 1
+            return loss.mean(), gn
         rows = self.replay.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter, out=self.batch_rows,
                                   state=state, guard=guard)
         if self.agent_type == "AC-IQN" and self.fused2 is not None:
@@ -278,7 +331,7 @@ class VecTrainer:
         # has been observed >= learning_starts (it only grows until full)
         if getattr(self, "_replay_ready", False):
             return self.learning_starts
-        n = self.replay.size()
+        n = self.per.pushed if self.per is not None else self.replay.size()
         if n >= self.learning_starts:
             self._replay_ready = True
         return n

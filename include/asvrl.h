@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 4
+#define ASVRL_ABI_VERSION 5
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -33,6 +33,7 @@ extern "C" {
 #define ASVRL_OBS_DIM 40   /* packed f32 obs row: self 7 | objects 5x5 | mask 5 | pad 3
                               (= replay_buffer.py:51-69 state_batch, padded to 16 B) */
 #define ASVRL_TR_DIM 88    /* replay row: obs 40 | next obs 40 | action 2 | reward | done | pad 4 */
+#define ASVRL_PER_DIM 48   /* prioritised replay slot: obs 40 | action | reward | nonterminal | timestep (i32) | pad 4 */
 
 /* Robot state fields, field-major SoA: rs[f * (n_envs * max_robots) + e * max_robots + i] */
 enum AsvRobotField {
@@ -364,6 +365,55 @@ int asvrl_replay_sample(const float* ring, int64_t capacity, const int64_t* ring
  * slot into the ring (used by the compat ReplayBuffer.add, one transition per call). */
 int asvrl_replay_write_rows(const float* rows, const int64_t* slots, int32_t n, float* ring,
                             void* stream);
+
+/* ---------------------------------------------------------------- prioritised n-step replay
+ * Rainbow's ReplayMemory + SegmentTree (policy/replay_memory_rainbow.py:14-196) in HBM. All members
+ * are device pointers the caller allocates (zero-initialised, maxp[0] = 1.0f); the struct itself is
+ * read on the host at each call. */
+typedef struct AsvPer {
+  float* rows;          /* [capacity][ASVRL_PER_DIM] */
+  float* tree;          /* [2 * tree_leaves - 1] sum tree, leaves at tree_leaves - 1 (:17) */
+  int64_t* state;       /* [4] {index, full, reserved, anomaly count (rejections left after 64 redraws,
+                           unsorted priority updates)} */
+  int32_t* t;           /* [stride] per-stream timestep counter (ReplayMemory.t, :107,139) */
+  float* maxp;          /* [1] SegmentTree.max (:22) */
+  uint8_t* dirty;       /* [max(1, tree_leaves / 2048)] dirty 2048-leaf blocks (cleared by the rebuild) */
+  int64_t capacity;     /* slots, a multiple of stride */
+  int64_t tree_leaves;  /* next power of two >= capacity, <= 2^22 */
+  int32_t stride;       /* slots per time step: 1 = the reference's single sequence; E*R = one stream per robot */
+  int32_t n_step;       /* n (3, :105) */
+  double discount;      /* 0.99 (:104) */
+  float priority_weight;    /* beta 0.4 (:106) */
+  float priority_exponent;  /* omega 0.5 (:107) */
+  int32_t deferred;     /* 0: the reference's tree (every append at max priority, rejection sampling);
+                           1: a slot's priority enters the tree when its n-step window is complete */
+  int32_t _pad0;
+} AsvPer;
+
+/* ReplayMemory.append (:132-139) for n = m * stride rows (m time steps, rows time-major): robot
+ * k % stride appends obs[k] (packed ASVRL_OBS_DIM row), action actions[k*action_dim], reward[k],
+ * terminal done[k] at max priority when obj_cnt[k] >= 0, else a blank slot of priority 0 (deferred: the
+ * priority is kept in the slot and set on the leaf n steps later, when the window is complete); then
+ * the dirty subtrees are rebuilt and the ring advances by n. Three launches. */
+int asvrl_per_push(const AsvPer* per, const float* obs, const int8_t* obj_cnt, const double* actions,
+                   int32_t action_dim, const double* reward, const uint8_t* done, int32_t n, void* stream);
+
+/* ReplayMemory.sample (:157-192): B stratified draws (segment b: uniform in [b*seg, (b+1)*seg) with
+ * seg = total / B in f32, the value in f64), SegmentTree.find, the validity rule of :163 (window
+ * behind the write head, not the head slot, prob != 0), the n-step window with blanking at later
+ * episode starts. uniforms (device f64 [B], optional): the reference's U(0,1) draws, one attempt;
+ * otherwise Philox(seed, counter + *counter_dev) with up to 64 per-segment redraws.
+ * out [B][ASVRL_TR_DIM]: obs 40 | n-th next obs 40 | action, 0 | R^n | nonterminal |
+ * w = (cap * p)^-beta (before the batch-max normalisation) | p = prob / total | data index | 0.
+ * out_tree_idx [B] int64: tree indices for asvrl_per_update. One launch. */
+int asvrl_per_sample(const AsvPer* per, int32_t B, const double* uniforms, uint64_t seed, uint64_t counter,
+                     const uint64_t* counter_dev, float* out, int64_t* out_tree_idx, void* stream);
+
+/* ReplayMemory.update_priorities (:194-196): leaf tree_idx[i] = values[i] ** priority_exponent
+ * (raw != 0: values already exponentiated), duplicates resolved last-wins (tree_idx as sampled, in
+ * non-decreasing order), SegmentTree.max updated, dirty subtrees rebuilt. Three launches. */
+int asvrl_per_update(const AsvPer* per, const int64_t* tree_idx, const float* values, int32_t B, int32_t raw,
+                     void* stream);
 
 /* ---------------------------------------------------------------- optimiser (agent.py) */
 
