@@ -88,6 +88,25 @@ __global__ __launch_bounds__(1024) void mean_kernel(const float* __restrict__ x,
 // starts; lane k then adds exactly its own runs in order: bit-identical to the reference, with
 // ~2 LDS reads per lane instead of 2 * atoms shuffles.
 constexpr int kC51Waves = 4;
+#ifndef ASVRL_C51_ROWS
+#define ASVRL_C51_ROWS 1
+#endif
+constexpr int kC51Rows = ASVRL_C51_ROWS;   // rows per wave: their loads are all issued before the first projection
+
+// acc + v[j0] + v[j0+1] + ... + v[j1-1], added in order; the LDS reads go out 8 at a time so a long
+// run (a terminal row sends every atom to one target) costs one LDS round trip per 8 adds
+__device__ __forceinline__ float run_sum(const float* v, int j0, int j1, float acc) {
+  int j = j0;
+  for (; j + 8 <= j1; j += 8) {
+    float x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = v[j + k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc += x[k];
+  }
+  for (; j < j1; ++j) acc += v[j];
+  return acc;
+}
 
 __global__ __launch_bounds__(kC51Waves * kWave) void c51_kernel(const float* __restrict__ pns_a,
                                                                 const float* __restrict__ ret,
@@ -96,45 +115,67 @@ __global__ __launch_bounds__(kC51Waves * kWave) void c51_kernel(const float* __r
                                                                 int atoms, float vmin, float vmax, float dz,
                                                                 float gamma_n, float* __restrict__ m) {
   __shared__ float s_lo[kC51Waves][kWave], s_up[kC51Waves][kWave];
-  __shared__ int s_l[kC51Waves][kWave + 1], s_u[kC51Waves][kWave + 1];
+  __shared__ int s_l[kC51Waves][kWave], s_u[kC51Waves][kWave];
   __shared__ int s_lstart[kC51Waves][kWave], s_ustart[kC51Waves][kWave];
+  __shared__ int s_lend[kC51Waves][kWave], s_uend[kC51Waves][kWave];
   const int lane = threadIdx.x & (kWave - 1);
   const int w = threadIdx.x >> 6;
-  const int b = blockIdx.x * kC51Waves + w;
-  const bool on = b < B && lane < atoms;
-  int l = -1, u = -1;
-  float lower = 0.f, upper = 0.f;
-  if (on) {
-    const float ntg = nonterm[b] * gamma_n;
-    float tz = ret[b] + ntg * support[lane];      // Tz = R + nonterminal * gamma^n * z
-    tz = fminf(fmaxf(tz, vmin), vmax);            // clamp(Vmin, Vmax)
-    const float bb = (tz - vmin) / dz;            // b = (Tz - Vmin) / delta_z
-    l = static_cast<int>(floorf(bb));
-    u = static_cast<int>(ceilf(bb));
-    if (u > 0 && l == u) l -= 1;                  // agent.py:623
-    if (l < atoms - 1 && l == u) u += 1;          // agent.py:624
-    const float p = pns_a[static_cast<size_t>(b) * atoms + lane];
-    lower = p * (static_cast<float>(u) - bb);
-    upper = p * (bb - static_cast<float>(l));
+  const int row0 = (blockIdx.x * kC51Waves + w) * kC51Rows;
+  const bool lane_on = lane < atoms;
+  const float z = lane_on ? support[lane] : 0.f;
+  float pv[kC51Rows], rv[kC51Rows], nv[kC51Rows];
+#pragma unroll
+  for (int r = 0; r < kC51Rows; ++r) {
+    const int b = row0 + r;
+    const bool on = b < B && lane_on;
+    pv[r] = on ? pns_a[static_cast<size_t>(b) * atoms + lane] : 0.f;
+    rv[r] = b < B ? ret[b] : 0.f;
+    nv[r] = b < B ? nonterm[b] : 0.f;
   }
-  s_l[w][lane] = l;
-  s_u[w][lane] = u;
-  s_lo[w][lane] = lower;
-  s_up[w][lane] = upper;
-  s_lstart[w][lane] = -1;
-  s_ustart[w][lane] = -1;
-  if (lane == 0) { s_l[w][kWave] = -1; s_u[w][kWave] = -1; }
-  __syncthreads();
-  if (on) {
-    if (lane == 0 || s_l[w][lane - 1] != l) s_lstart[w][l] = lane;
-    if (lane == 0 || s_u[w][lane - 1] != u) s_ustart[w][u] = lane;
+#pragma unroll
+  for (int r = 0; r < kC51Rows; ++r) {
+    const int b = row0 + r;
+    const bool on = b < B && lane_on;
+    int l = -1, u = -1;
+    float lower = 0.f, upper = 0.f;
+    if (on) {
+      const float ntg = nv[r] * gamma_n;
+      float tz = rv[r] + ntg * z;                   // Tz = R + nonterminal * gamma^n * z
+      tz = fminf(fmaxf(tz, vmin), vmax);            // clamp(Vmin, Vmax)
+      const float bb = (tz - vmin) / dz;            // b = (Tz - Vmin) / delta_z
+      l = static_cast<int>(floorf(bb));
+      u = static_cast<int>(ceilf(bb));
+      if (u > 0 && l == u) l -= 1;                  // agent.py:623
+      if (l < atoms - 1 && l == u) u += 1;          // agent.py:624
+      lower = pv[r] * (static_cast<float>(u) - bb);
+      upper = pv[r] * (bb - static_cast<float>(l));
+    }
+    s_l[w][lane] = l;
+    s_u[w][lane] = u;
+    s_lo[w][lane] = lower;
+    s_up[w][lane] = upper;
+    s_lstart[w][lane] = 0;
+    s_lend[w][lane] = 0;
+    s_ustart[w][lane] = 0;
+    s_uend[w][lane] = 0;
+    __syncthreads();
+    if (on) {   // run [start, end) of each target; the bounds make the sums branch-free on LDS data
+      if (lane == 0 || s_l[w][lane - 1] != l) s_lstart[w][l] = lane;
+      if (lane == atoms - 1 || s_l[w][lane + 1] != l) s_lend[w][l] = lane + 1;
+      if (lane == 0 || s_u[w][lane - 1] != u) s_ustart[w][u] = lane;
+      if (lane == atoms - 1 || s_u[w][lane + 1] != u) s_uend[w][u] = lane + 1;
+    }
+    __syncthreads();
+    if (on) {
+      float acc = 0.f;
+      const int l0 = s_lstart[w][lane], l1 = s_lend[w][lane];
+      const int u0 = s_ustart[w][lane], u1 = s_uend[w][lane];
+      acc = run_sum(&s_lo[w][0], l0, l1, acc);
+      acc = run_sum(&s_up[w][0], u0, u1, acc);
+      m[static_cast<size_t>(b) * atoms + lane] = acc;
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  if (!on) return;
-  float acc = 0.f;
-  for (int j = s_lstart[w][lane]; j >= 0 && j < atoms && s_l[w][j] == lane; ++j) acc += s_lo[w][j];
-  for (int j = s_ustart[w][lane]; j >= 0 && j < atoms && s_u[w][j] == lane; ++j) acc += s_up[w][j];
-  m[static_cast<size_t>(b) * atoms + lane] = acc;
 }
 
 // ------------------------------------------------------------------ replay ring
@@ -296,7 +337,8 @@ extern "C" int asvrl_c51_project(const float* pns_a, const float* returns, const
   ASVRL_REQUIRE(pns_a && returns && nonterminal && support && m, "asvrl_c51_project: null argument");
   ASVRL_REQUIRE(atoms >= 2 && atoms <= kWave, "asvrl_c51_project: atoms must be in [2, 64]");
   if (B <= 0) return 0;
-  hipLaunchKernelGGL(c51_kernel, dim3((B + kC51Waves - 1) / kC51Waves), dim3(kC51Waves * kWave), 0,
+  const int rows_per_block = kC51Waves * kC51Rows;
+  hipLaunchKernelGGL(c51_kernel, dim3((B + rows_per_block - 1) / rows_per_block), dim3(kC51Waves * kWave), 0,
                      as_stream(stream), pns_a, returns,
                      nonterminal, support, B, atoms, vmin, vmax, delta_z, gamma_n, m);
   return check_launch("asvrl_c51_project");

@@ -26,7 +26,7 @@ from .fused_iqn import FusedIQNState, iqn_update_fused
 from .fused_iqn import supported as fused_iqn_supported
 from .fused_update import supported as fused2_supported
 from .learn_ops import DevicePER, DeviceReplay, split_rows
-from .learner import FlatGrads, FusedAdam, GradSync, ac_iqn_update, iqn_update, rainbow_update
+from .learner import FlatGrads, FusedAdam, GradSync, ac_iqn_update, iqn_update, rainbow_update_rows
 from .policy.AC_IQN_model import AC_IQN_Policy
 from .policy.IQN_model import IQN_Policy
 from .policy.Rainbow_model import Rainbow_Policy
@@ -223,12 +223,10 @@ class VecTrainer:
         if self.per is not None:
             rows, idx = self.per.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter,
                                         out=self.batch_rows, out_idx=self.per_idx)
-            s, a, R, ns, nt = split_rows(rows)
             amp = torch.autocast("cuda", dtype=self.amp_dtype) if self.amp_dtype is not None else _null()
             with amp:
-                loss, gn = rainbow_update(self.local, self.target, self.opt, self.grads, self.support, s,
-                                          a[:, 0].to(torch.int64), R, ns, nt, rows[:, 84], gamma=self.gamma,
-                                          n=self.n_step, sync=self.sync)
+                loss, gn = rainbow_update_rows(self.local, self.target, self.opt, self.grads, self.support, rows,
+                                               gamma=self.gamma, n=self.n_step, sync=self.sync)
             self.per.update_priorities(idx, loss)   # update_priorities(idxs, loss) (agent.py:639)
             self.learn_counter += 1
             return loss.mean(), gn
