@@ -42,13 +42,15 @@ class GradSync:
     """All-reduce(average) of a FlatGrads buffer over the default process group (RCCL on
     MI355X: backend "nccl"; gloo on CPU tests)."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, force=False):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.avg_supported = dist.is_initialized() and dist.get_backend(group) == "nccl"
+        # force: issue the collective even over one rank (tests of the captured DP path on one GPU)
+        self.force = bool(force) and dist.is_initialized()
 
     def __call__(self, fg: FlatGrads):
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             return
         if self.avg_supported:
             dist.all_reduce(fg.flat, op=dist.ReduceOp.AVG, group=self.group)

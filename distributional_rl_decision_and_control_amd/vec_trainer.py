@@ -16,6 +16,7 @@ Cadence in the batched setting: one learn step of batch B per iteration (after
 timesteps; target updates count learn steps (2500 = 10000 timesteps / UPDATE_EVERY 4).
 With `graphs=True` steps 1-5 are captured once into a HIP graph and replayed.
 """
+import os
 import time
 
 import torch
@@ -26,7 +27,7 @@ from .fused_iqn import FusedIQNState, iqn_update_fused
 from .fused_iqn import supported as fused_iqn_supported
 from .fused_update import supported as fused2_supported
 from .learn_ops import DevicePER, DeviceReplay, split_rows
-from .learner import FlatGrads, FusedAdam, GradSync, ac_iqn_update, iqn_update, rainbow_update_rows
+from .learner import FlatGrads, FusedAdam, GradSync, ac_iqn_update, iqn_update, rainbow_update, rainbow_update_rows
 from .policy.AC_IQN_model import AC_IQN_Policy
 from .policy.IQN_model import IQN_Policy
 from .policy.Rainbow_model import Rainbow_Policy
@@ -118,6 +119,8 @@ class VecTrainer:
             self.action_dim = 1
             self.n_step = 3
             self.support = torch.linspace(-1.0, 1.0, 51, device=self.device)
+            # one online forward over s and s_{t+n} (learner.rainbow_update_rows) or two (rainbow_update)
+            self.rainbow_packed = os.environ.get("ASVRL_RAINBOW_PACKED", "0") == "1"
         else:
             raise NotImplementedError(f"VecTrainer agent_type {agent_type!r} (AC-IQN, IQN and Rainbow are batched)")
         NT = self.E * self.R
@@ -225,8 +228,14 @@ class VecTrainer:
                                         out=self.batch_rows, out_idx=self.per_idx)
             amp = torch.autocast("cuda", dtype=self.amp_dtype) if self.amp_dtype is not None else _null()
             with amp:
-                loss, gn = rainbow_update_rows(self.local, self.target, self.opt, self.grads, self.support, rows,
-                                               gamma=self.gamma, n=self.n_step, sync=self.sync)
+                if self.rainbow_packed:
+                    loss, gn = rainbow_update_rows(self.local, self.target, self.opt, self.grads, self.support,
+                                                   rows, gamma=self.gamma, n=self.n_step, sync=self.sync)
+                else:
+                    s, a, R, ns, nt = split_rows(rows)
+                    loss, gn = rainbow_update(self.local, self.target, self.opt, self.grads, self.support, s,
+                                              a[:, 0].to(torch.int64), R, ns, nt, rows[:, 84], gamma=self.gamma,
+                                              n=self.n_step, sync=self.sync)
             self.per.update_priorities(idx, loss)   # update_priorities(idxs, loss) (agent.py:639)
             self.learn_counter += 1
             return loss.mean(), gn
@@ -308,9 +317,14 @@ class VecTrainer:
     def iteration(self, timing=None):
         """One fused rollout+learn iteration. Returns losses (device tensors) or None."""
         do_learn = self.replay_size_host() >= self.learning_starts
-        if self.graphs and do_learn:
-            if self._graph is None:
+        if self.graphs and do_learn and self._graph is None:
+            try:
                 self._capture()
+            except RuntimeError as e:   # a capture the runtime refuses: keep going eagerly, loudly
+                import sys
+                print(f"VecTrainer: HIP graph capture failed ({e}); continuing without graphs", file=sys.stderr)
+                self.graphs, self._graph = False, None
+        if self.graphs and do_learn:
             self._graph.replay()
             out = self._graph_out
         else:
