@@ -11,7 +11,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ASVRL_LIB", os.path.join(HERE, "lib", "libasvrl.so"))  # override: A/B variants
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
 OBS_DIM = 40   # self 7 | objects 25 | mask 5 | pad 3
@@ -148,6 +148,27 @@ class AsvPer(C.Structure):
                 ("_pad0", _I32)]
 
 
+MAX_NOISY_SEGS = 16
+
+
+class AsvNoisySeg(C.Structure):
+    _fields_ = [(n, _VP) for n in ("mu", "sigma", "eps", "out", "dout", "dmu", "dsigma")]
+
+
+class AsvNoisySegs(C.Structure):
+    _fields_ = [("n", _I32), ("_pad0", _I32), ("off", _I64 * (MAX_NOISY_SEGS + 1)),
+                ("seg", AsvNoisySeg * MAX_NOISY_SEGS)]
+
+
+class AsvRainbowHeadIO(C.Structure):
+    _fields_ = [("v", _VP), ("ldv", _I64), ("a", _VP), ("lda", _I64), ("N", _I32), ("atoms", _I32),
+                ("actions_n", _I32), ("_pad0", _I32), ("support", _VP), ("act_out", _VP), ("ld_act", _I64),
+                ("act_idx", _VP), ("step_dev", _VP), ("eps_steps_per_count", _D), ("eps_total", _D),
+                ("eps_fraction", _D), ("eps_initial", _D), ("eps_final", _D), ("seed", _U64), ("p_out", _VP),
+                ("actions", _VP), ("weights", _VP), ("ld_rd", _I64), ("m", _VP), ("loss", _VP), ("dv", _VP),
+                ("da", _VP), ("grad_scale", C.c_float), ("_pad1", _I32)]
+
+
 EXPORTS = [
     ("asvrl_env_step", C.c_int, [C.POINTER(AsvParams), C.POINTER(AsvEnvState), _VP, _VP, C.POINTER(AsvStepCtl),
                                  C.POINTER(AsvStepOut), _VP]),
@@ -172,6 +193,11 @@ EXPORTS = [
     ("asvrl_per_push", C.c_int, [C.POINTER(AsvPer), _VP, _VP, _VP, _I32, _VP, _VP, _I32, _VP]),
     ("asvrl_per_sample", C.c_int, [C.POINTER(AsvPer), _I32, _VP, _U64, _U64, _VP, _VP, _VP, _VP]),
     ("asvrl_per_update", C.c_int, [C.POINTER(AsvPer), _VP, _VP, _I32, _I32, _VP]),
+    ("asvrl_noisy_compose", C.c_int, [C.POINTER(AsvNoisySegs), _I32, _VP]),
+    ("asvrl_noisy_reset", C.c_int, [C.POINTER(AsvNoisySegs), _VP, _VP, _U64, _VP, _VP]),
+    ("asvrl_rainbow_act", C.c_int, [C.POINTER(AsvRainbowHeadIO), _VP]),
+    ("asvrl_rainbow_pick", C.c_int, [C.POINTER(AsvRainbowHeadIO), _VP]),
+    ("asvrl_rainbow_loss", C.c_int, [C.POINTER(AsvRainbowHeadIO), _VP]),
     ("asvrl_adam_clip", C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, _F, _F, _VP, _VP, _VP]),
     ("asvrl_linear_wgrad_workspace", _I64, [_I32, _I32]),
     ("asvrl_linear_wgrad_groups", _I32, [_I32, _I32, _I32]),

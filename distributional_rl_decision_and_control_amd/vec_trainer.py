@@ -25,6 +25,7 @@ from .fused_critic import FusedACIQN, ac_iqn_update_fused, fused_supported
 from .fused_update import FusedACIQNState, ac_iqn_update_fused2
 from .fused_iqn import FusedIQNState, iqn_update_fused
 from .fused_iqn import supported as fused_iqn_supported
+from .fused_rainbow import FusedRainbow
 from .fused_update import supported as fused2_supported
 from .learn_ops import DevicePER, DeviceReplay, split_rows
 from .learner import FlatGrads, FusedAdam, GradSync, ac_iqn_update, iqn_update, rainbow_update, rainbow_update_rows
@@ -59,7 +60,7 @@ class VecTrainer:
         self.exploration_fraction, self.initial_eps, self.final_eps = exploration_fraction, initial_eps, final_eps
         self.learning_starts = learning_starts if learning_starts is not None else batch_size
         capturable = bool(graphs)
-        self.fused = self.fused2 = self.fused_iqn = None
+        self.fused = self.fused2 = self.fused_iqn = self.fused_rb = None
         if agent_type == "AC-IQN":
             self.local = AC_IQN_Policy(**DEFAULT_NET, value_ranges_of_action=[[-1.0, 1.0], [-1.0, 1.0]],
                                        device=self.device, seed=net_seed)
@@ -121,6 +122,10 @@ class VecTrainer:
             self.support = torch.linspace(-1.0, 1.0, 51, device=self.device)
             # one online forward over s and s_{t+n} (learner.rainbow_update_rows) or two (rainbow_update)
             self.rainbow_packed = os.environ.get("ASVRL_RAINBOW_PACKED", "0") == "1"
+            # fused=True: noisy weights, dueling head, loss gradient and act on hand-written kernels
+            # (fused_rainbow.py; fp32 GEMMs); otherwise the torch update with the C51 kernel
+            if fused is True and fused_adam:
+                self.fused_rb = FusedRainbow(self.local, self.target, batch_size, self.support)
         else:
             raise NotImplementedError(f"VecTrainer agent_type {agent_type!r} (AC-IQN, IQN and Rainbow are batched)")
         NT = self.E * self.R
@@ -166,6 +171,11 @@ class VecTrainer:
 
     @torch.no_grad()
     def act(self):
+        if self.fused_rb is not None:
+            # composed noisy weights, logits, one head kernel: expected Q, argmax, epsilon-greedy
+            self.fused_rb.act(self.env.obs_cur, self.actions, self.env.counter, self.E, self.total_timesteps,
+                              self.exploration_fraction, self.initial_eps, self.final_eps, self.seed + 4242)
+            return
         if self.fused_iqn is not None:
             # encoders + one kernel: K = 32 quantiles per robot, mean, argmax, epsilon-greedy
             self.fused_iqn.act(self.env.obs_cur, self.actions, self.env.counter, self.E, self.total_timesteps,
@@ -226,6 +236,13 @@ class VecTrainer:
         if self.per is not None:
             rows, idx = self.per.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter,
                                         out=self.batch_rows, out_idx=self.per_idx)
+            if self.fused_rb is not None:   # act() composed the online weights this iteration
+                loss, gn = self.fused_rb.update(self.opt, self.grads, rows, gamma=self.gamma, n=self.n_step,
+                                                sync=self.sync, seed=self.seed + 999, counter_dev=self.learn_counter,
+                                                compose=False)
+                self.per.update_priorities(idx, loss)
+                self.learn_counter += 1
+                return loss.mean(), gn
             amp = torch.autocast("cuda", dtype=self.amp_dtype) if self.amp_dtype is not None else _null()
             with amp:
                 if self.rainbow_packed:
@@ -283,6 +300,8 @@ class VecTrainer:
                 self.fused2.target_changed()
             if self.fused_iqn is not None:
                 self.fused_iqn.target_changed()
+            if self.fused_rb is not None:
+                self.fused_rb.target_changed()
 
     # ------------------------------------------------------------------ iteration
     def _iteration_body(self, do_learn):

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 5
+#define ASVRL_ABI_VERSION 6
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -414,6 +414,75 @@ int asvrl_per_sample(const AsvPer* per, int32_t B, const double* uniforms, uint6
  * non-decreasing order), SegmentTree.max updated, dirty subtrees rebuilt. Three launches. */
 int asvrl_per_update(const AsvPer* per, const int64_t* tree_idx, const float* values, int32_t B, int32_t raw,
                      void* stream);
+
+/* ---------------------------------------------------------------- Rainbow (Rainbow_model.py, agent.py)
+ * NoisyLinear weights and the dueling C51 head. A network's noisy tensors are described by up to 16
+ * segments (weight, bias of each layer); off[k] is the flat offset of segment k (off[n] = total). */
+#define ASVRL_MAX_NOISY_SEGS 16
+typedef struct AsvNoisySeg {
+  const float* mu;      /* weight_mu / bias_mu */
+  const float* sigma;   /* weight_sigma / bias_sigma */
+  float* eps;           /* weight_epsilon / bias_epsilon (written by asvrl_noisy_reset) */
+  float* out;           /* composed mu + sigma * eps */
+  const float* dout;    /* backward: gradient of out */
+  float* dmu;           /* backward: written with dout */
+  float* dsigma;        /* backward: written with dout * eps */
+} AsvNoisySeg;
+
+typedef struct AsvNoisySegs {
+  int32_t n;
+  int32_t _pad0;
+  int64_t off[ASVRL_MAX_NOISY_SEGS + 1];
+  AsvNoisySeg seg[ASVRL_MAX_NOISY_SEGS];
+} AsvNoisySegs;
+
+/* NoisyLinear.forward in training mode (Rainbow_model.py:47-51) for every segment: out = mu + sigma * eps;
+ * backward != 0: dmu = dout, dsigma = dout * eps (assigned, the parameters' only use). One launch. */
+int asvrl_noisy_compose(const AsvNoisySegs* segs, int32_t backward, void* stream);
+
+/* reset_noise() of every layer (Rainbow_model.py:35-45,141-145) with (weight, bias) segment pairs:
+ * f(x) = sign(x) sqrt|x| of N(0, 1) Philox draws (seed, *counter_dev), eps_w = f(eps_out) f(eps_in)^T,
+ * eps_b = f(eps_out), and out = mu + sigma * eps in the same launch. in/out_features: device int32
+ * [n/2] (in <= 256, out <= 2048). One workgroup per layer. */
+int asvrl_noisy_reset(const AsvNoisySegs* segs, const int32_t* in_features, const int32_t* out_features,
+                      uint64_t seed, const int64_t* counter_dev, void* stream);
+
+typedef struct AsvRainbowHeadIO {
+  const float* v;           /* [N][ldv] value logits (51) */
+  int64_t ldv;
+  const float* a;           /* [N][lda] advantage logits (25 x 51, action-major) */
+  int64_t lda;
+  int32_t N, atoms, actions_n, _pad0;   /* atoms 51, actions_n 25 */
+  const float* support;     /* [51] */
+  /* act: argmax_a sum softmax(q[a]) z (agent.py:320), epsilon-greedy when step_dev != NULL */
+  double* act_out;          /* optional [N] action as f64 at act_out[row * ld_act] */
+  int64_t ld_act;
+  int64_t* act_idx;         /* optional [N] greedy action (act) / a* input (pick) */
+  const int64_t* step_dev;
+  double eps_steps_per_count, eps_total, eps_fraction, eps_initial, eps_final;
+  uint64_t seed;
+  float* p_out;             /* pick: [N][51] softmax(q[a*]) */
+  /* loss */
+  const float* actions;     /* [N] at actions[row * ld_rd] (replay row column) */
+  const float* weights;     /* [N] importance weights at weights[row * ld_rd] */
+  int64_t ld_rd;
+  const float* m;           /* [N][51] projected target distribution */
+  float* loss;              /* [N] per-sample loss */
+  float* dv;                /* [N][51] d(grad_scale * sum_b w_b loss_b) / dv */
+  float* da;                /* [N][1275] ... / da */
+  float grad_scale;         /* 1 / B for the mean */
+  int32_t _pad1;
+} AsvRainbowHeadIO;
+
+/* Dueling head q = v + a - mean_a(a) (Rainbow_model.py:128-134) per row: softmax over atoms per action,
+ * expected value, argmax (first maximum); epsilon-greedy exploration (agent.py:318-322) with the linear
+ * schedule of the device step counter when step_dev != NULL. One wave per two rows. */
+int asvrl_rainbow_act(const AsvRainbowHeadIO* io, void* stream);
+/* p(s', a*) = softmax(q[a*]) (agent.py:611-612), a* = act_idx[row]. One wave per row. */
+int asvrl_rainbow_pick(const AsvRainbowHeadIO* io, void* stream);
+/* loss_b = -sum m log softmax(q[a_b]) (agent.py:633) and the gradients of grad_scale * sum_b w_b loss_b
+ * with respect to v and a. One wave per row. */
+int asvrl_rainbow_loss(const AsvRainbowHeadIO* io, void* stream);
 
 /* ---------------------------------------------------------------- optimiser (agent.py) */
 
