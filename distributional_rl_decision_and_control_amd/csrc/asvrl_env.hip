@@ -198,15 +198,22 @@ __device__ inline void cswap(bool cond, Cand& x, Cand& y) {
   }
 }
 
-template <int BLOCK>
+// PAIRS: perception spread over (robot, candidate) pairs -- one lane per pair computes the noisy
+// observation, detection, collision and sort key of one candidate into LDS, then each robot lane
+// merges its candidates in the reference's order (stable top-5 insertion, collision as an OR), so the
+// kept objects and masks are the serial sweep's exactly; the Philox draws (noise modes 1, 2) are keyed
+// by (robot, candidate slot) instead of one stream per robot. `epb_arg` envs per workgroup (PAIRS).
+template <int BLOCK, bool PAIRS>
 __global__ __launch_bounds__(BLOCK) void env_step_kernel(AsvParams p, AsvEnvState s,
                                                           const double* __restrict__ actions,
                                                           const double* __restrict__ noise,
-                                                          AsvStepCtl ctl, AsvStepOut out) {
+                                                          AsvStepCtl ctl, AsvStepOut out, int epb_arg) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int R = s.max_robots;
   const int O = s.max_obs;
-  const int epb = BLOCK / R;
+  const int epb = PAIRS ? epb_arg : BLOCK / R;
+  const int S = O + R;               // candidate slots per robot (obstacles, then robots)
+  const int npairs = PAIRS ? epb * R * S : 0;
   const int tid = threadIdx.x;
   const int le = tid / R;
   const int i = tid - le * R;
@@ -224,9 +231,19 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(AsvParams p, AsvEnvStat
   double* sy = sx + BLOCK;
   double* sv0 = sy + BLOCK;
   double* sv1 = sv0 + BLOCK;
-  double* sob = sv1 + BLOCK;  // [epb][O][3]
+  double* scs = sv1 + BLOCK;                 // PAIRS: robot frame cos, sin, translation
+  double* ssn = scs + (PAIRS ? BLOCK : 0);
+  double* stx = ssn + (PAIRS ? BLOCK : 0);
+  double* sty = stx + (PAIRS ? BLOCK : 0);
+  double* pk = sty + (PAIRS ? BLOCK : 0);    // PAIRS: [npairs] sort key, [npairs][5] candidate row
+  double* pc = pk + npairs;
+  double* sob = pc + 5 * static_cast<size_t>(npairs);  // [epb][O][3]
   int* salive = reinterpret_cast<int*>(sob + static_cast<size_t>(epb) * O * 3);  // [epb]
-  unsigned char* soff = reinterpret_cast<unsigned char*>(salive + epb);          // [BLOCK]
+  int* sno = salive + epb;                   // PAIRS: [epb] obstacles, robots of each env
+  int* snr = sno + (PAIRS ? epb : 0);
+  unsigned char* soff = reinterpret_cast<unsigned char*>(snr + (PAIRS ? epb : 0));  // [BLOCK]
+  unsigned char* sact = soff + BLOCK;        // PAIRS: [BLOCK] robot active; [npairs] detected | 2 * collision
+  unsigned char* pfl = sact + (PAIRS ? BLOCK : 0);
 
   Regs r{};
   uint8_t fl = 0;
@@ -288,8 +305,114 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(AsvParams p, AsvEnvStat
       }
     }
     if (i == 0) salive[le] = 0;
+    if (PAIRS && i == 0) {
+      sno[le] = s.n_obs[e];
+      snr[le] = nrob;
+    }
+  }
+  if constexpr (PAIRS) {
+    sact[tid] = active ? 1 : 0;
+    if (active) {
+      double sn_, cs_;
+      sincos(r.th, &sn_, &cs_);
+      scs[tid] = cs_;
+      ssn[tid] = sn_;
+      stx[tid] = -(cs_ * r.x + sn_ * r.y);
+      sty[tid] = -(-sn_ * r.x + cs_ * r.y);
+    }
   }
   __syncthreads();
+
+  if constexpr (PAIRS) {
+    // ---------------- phase 2a: one (robot, candidate) pair per lane (wamv.py:478-511)
+    const uint64_t ctr = ctl.counter + (ctl.counter_dev != nullptr ? *ctl.counter_dev : 0ull);
+    const bool full_circle = 0.5 * p.angle >= kPi;
+    for (int q = tid; q < npairs; q += BLOCK) {
+      const int qe = q / (R * S);
+      const int rem = q - qe * R * S;
+      const int qi = rem / S;
+      const int c = rem - qi * S;
+      const int qt = qe * R + qi;
+      unsigned char flag = 0;
+      double key = INFINITY, ca = 0, cb = 0, cc = 0, cd = 0, ce = 0;
+      bool valid = false;
+      double ox = 0, oy = 0, orad = 0, vx0 = 0, vy0 = 0;
+      if (sact[qt]) {
+        if (c < O) {
+          valid = c < sno[qe];
+          if (valid) {
+            const double* ob = sob + (static_cast<size_t>(qe) * O + c) * 3;
+            ox = ob[0];
+            oy = ob[1];
+            orad = ob[2];
+          }
+        } else {
+          const int j = c - O;
+          valid = j < snr[qe] && j != qi && !soff[qe * R + j];   // self / deactivated (wamv.py:487-491)
+          if (valid) {
+            ox = sx[qe * R + j];
+            oy = sy[qe * R + j];
+            orad = p.r;
+            vx0 = sv0[qe * R + j];
+            vy0 = sv1[qe * R + j];
+          }
+        }
+      }
+      if (valid) {
+        const size_t qidx = static_cast<size_t>(blockIdx.x * epb + qe) * R + qi;
+        double n0, n1, n2, n3, n4;
+        if (ctl.noise_mode == 0) {
+          const double* nz = noise + (qidx * static_cast<size_t>(O + R) + c) * 5;
+          n0 = nz[0]; n1 = nz[1]; n2 = nz[2]; n3 = nz[3]; n4 = nz[4];
+        } else if (ctl.noise_mode == 1) {
+          Stream rng(ctl.seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull, static_cast<uint32_t>(qidx),
+                     (static_cast<uint32_t>(qidx >> 32) ^ 0x5EEDu) + (static_cast<uint32_t>(c) << 20),
+                     static_cast<uint32_t>(ctr));
+          rng.normal2(n0, n1);
+          rng.normal2(n2, n3);
+          n0 *= p.pos_std; n1 *= p.pos_std; n2 *= p.vel_std; n3 *= p.vel_std;
+          n4 = rng.vonmises(p.r_kappa);
+        } else {
+          StreamF rngf(ctl.seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull, static_cast<uint32_t>(qidx),
+                       (static_cast<uint32_t>(qidx >> 32) ^ 0xF32Au) + (static_cast<uint32_t>(c) << 20),
+                       static_cast<uint32_t>(ctr));
+          float f0, f1, f2, f3;
+          rngf.normal2(f0, f1);
+          rngf.normal2(f2, f3);
+          n0 = f0 * p.pos_std; n1 = f1 * p.pos_std; n2 = f2 * p.vel_std; n3 = f3 * p.vel_std;
+          n4 = rngf.vonmises(static_cast<float>(p.r_kappa));
+        }
+        const double cs = scs[qt], sn = ssn[qt], tx = stx[qt], ty = sty[qt];
+        const double pxn = ox + n0, pyn = oy + n1;  // Perception (wamv.py:27-40)
+        const double vxn = vx0 + n2, vyn = vy0 + n3;
+        const double rn = p.r_mean_ratio * orad + (1 - p.r_mean_ratio) * n4 / kPi * orad;
+        const double qx = (cs * pxn + sn * pyn) + tx, qy = (-sn * pxn + cs * pyn) + ty;
+        const double qn = sqrt(qx * qx + qy * qy);
+        bool det = qn <= p.range + rn;  // check_detection (wamv.py:293-303)
+        if (det && !full_circle) {
+          const double ang = atan2(qy, qx);
+          det = !(ang < -0.5 * p.angle || ang > 0.5 * p.angle);
+        }
+        if (det) {
+          flag = 1;
+          const double rx = sx[qt], ry = sy[qt];   // check_collision (wamv.py:281-291), true positions
+          const double d = sqrt((rx - ox) * (rx - ox) + (ry - oy) * (ry - oy)) - orad - p.r;
+          if (d <= 0.0) flag |= 2;
+          key = qn - rn - p.r;
+          ca = qx;
+          cb = qy;
+          cc = cs * vxn + sn * vyn;
+          cd = -sn * vxn + cs * vyn;
+          ce = rn;
+        }
+      }
+      pk[q] = key;
+      double* row = pc + 5 * static_cast<size_t>(q);
+      row[0] = ca; row[1] = cb; row[2] = cc; row[3] = cd; row[4] = ce;
+      pfl[q] = flag;
+    }
+    __syncthreads();
+  }
 
   // ---------------- phase 2: perception_output (wamv.py:436-529)
   bool coll = (fl & ASVRL_FLAG_COLLISION) != 0;
@@ -300,9 +423,17 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(AsvParams p, AsvEnvStat
   Cand t0{INFINITY, 0, 0, 0, 0, 0}, t1 = t0, t2 = t0, t3 = t0, t4 = t0;
   double so0 = 0, so1 = 0, so2 = 0, so3 = 0, so4 = 0;
   if (active) {
-    double sn, cs;
-    sincos(r.th, &sn, &cs);
-    const double tx = -(cs * r.x + sn * r.y), ty = -(-sn * r.x + cs * r.y);
+    double sn, cs, tx, ty;
+    if constexpr (PAIRS) {
+      cs = scs[tid];
+      sn = ssn[tid];
+      tx = stx[tid];
+      ty = sty[tid];
+    } else {
+      sincos(r.th, &sn, &cs);
+      tx = -(cs * r.x + sn * r.y);
+      ty = -(-sn * r.x + cs * r.y);
+    }
     so0 = (cs * gx + sn * gy) + tx;
     so1 = (-sn * gx + cs * gy) + ty;
     so2 = cs * r.v0 + sn * r.v1;
@@ -310,6 +441,24 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(AsvParams p, AsvEnvStat
     so4 = r.v2;
     if (sqrt((gx - r.x) * (gx - r.x) + (gy - r.y) * (gy - r.y)) <= p.goal_dis) reach = true;
 
+    int nkept = 0;
+    if constexpr (PAIRS) {
+      // ---------------- phase 2b: the robot's candidates in the reference's order
+      const int q0 = tid * S;
+      for (int c = 0; c < S; ++c) {
+        const unsigned char f = pfl[q0 + c];
+        if (!(f & 1)) continue;
+        if (f & 2) coll = true;
+        const double* row = pc + 5 * static_cast<size_t>(q0 + c);
+        Cand cd{pk[q0 + c], row[0], row[1], row[2], row[3], row[4]};
+        cswap(cd.key < t0.key, cd, t0);
+        cswap(cd.key < t1.key, cd, t1);
+        cswap(cd.key < t2.key, cd, t2);
+        cswap(cd.key < t3.key, cd, t3);
+        cswap(cd.key < t4.key, cd, t4);
+        ++nkept;
+      }
+    } else {
     const int no = s.n_obs[e];
     const int base = le * R;
     const double* nz_base =
@@ -319,7 +468,6 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(AsvParams p, AsvEnvStat
                static_cast<uint32_t>(idx >> 32) ^ 0x5EEDu, static_cast<uint32_t>(ctr));
     StreamF rngf(ctl.seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull, static_cast<uint32_t>(idx),
                  static_cast<uint32_t>(idx >> 32) ^ 0xF32Au, static_cast<uint32_t>(ctr));
-    int nkept = 0;
     const int ncand = no + nrob;
     const bool full_circle = 0.5 * p.angle >= kPi;
     for (int k = 0; k < ncand; ++k) {
@@ -381,6 +529,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(AsvParams p, AsvEnvStat
       cswap(cd.key < t3.key, cd, t3);
       cswap(cd.key < t4.key, cd, t4);
       ++nkept;
+    }
     }
     cnt = nkept < p.max_obj_num ? nkept : p.max_obj_num;
     // COLREGs over the kept objects in order, stop at the first hit (wamv.py:517-521)
@@ -716,6 +865,28 @@ size_t env_step_smem(int R, int O) {
   return sizeof(double) * (4 * blk + static_cast<size_t>(epb) * O * 3) + sizeof(int) * epb + blk;
 }
 
+// the pair-parallel launch: workgroup size from the pair count, envs per workgroup so that the
+// pairs fill it (at least one env); ASVRL_ENV_EPB overrides the envs per workgroup (tuning)
+struct PairLaunch {
+  int blk, epb;
+  size_t smem;
+};
+PairLaunch pair_launch(int R, int O) {
+  const int np1 = R * (O + R);
+  PairLaunch L;
+  L.blk = np1 > 128 || R > 64 ? 256 : (np1 > 64 ? 128 : 64);
+  L.epb = L.blk / np1 > 1 ? L.blk / np1 : 1;
+  static const int epb_env = [] {
+    const char* v = getenv("ASVRL_ENV_EPB");
+    return v != nullptr ? atoi(v) : 0;
+  }();
+  if (epb_env > 0) L.epb = epb_env * R <= L.blk ? epb_env : L.blk / R;
+  const size_t np = static_cast<size_t>(L.epb) * np1;
+  L.smem = sizeof(double) * (8 * static_cast<size_t>(L.blk) + 6 * np + static_cast<size_t>(L.epb) * O * 3) +
+           sizeof(int) * 3 * L.epb + 2 * L.blk + np;
+  return L;
+}
+
 }  // namespace asvrl
 
 using namespace asvrl;
@@ -735,17 +906,35 @@ extern "C" int asvrl_env_step(const AsvParams* params, const AsvEnvState* state,
   ASVRL_REQUIRE(state->rs && state->rflags && state->n_robots && state->n_obs && state->n_cores && state->ep_ts,
                 "asvrl_env_step: null state array");
   if (state->n_envs == 0) return 0;
+  static const bool pairs_env = [] {
+    const char* v = getenv("ASVRL_ENV_PAIRS");   // 0: the per-robot sweep (A/B)
+    return v == nullptr || v[0] != '0';
+  }();
+  const PairLaunch pl = pair_launch(state->max_robots, state->max_obs);
+  if (pairs_env && pl.smem <= 64 * 1024) {
+    const int grid = (state->n_envs + pl.epb - 1) / pl.epb;
+    if (pl.blk == 64)
+      hipLaunchKernelGGL((env_step_kernel<64, true>), dim3(grid), dim3(64), pl.smem, as_stream(stream), *params,
+                         *state, actions, noise, *ctl, *out, pl.epb);
+    else if (pl.blk == 128)
+      hipLaunchKernelGGL((env_step_kernel<128, true>), dim3(grid), dim3(128), pl.smem, as_stream(stream), *params,
+                         *state, actions, noise, *ctl, *out, pl.epb);
+    else
+      hipLaunchKernelGGL((env_step_kernel<256, true>), dim3(grid), dim3(256), pl.smem, as_stream(stream), *params,
+                         *state, actions, noise, *ctl, *out, pl.epb);
+    return check_launch("asvrl_env_step");
+  }
   const int blk = step_block(state->max_robots);
   const int epb = blk / state->max_robots;
   const int grid = (state->n_envs + epb - 1) / epb;
   const size_t smem = env_step_smem(state->max_robots, state->max_obs);
   ASVRL_REQUIRE(smem <= 160 * 1024, "asvrl_env_step: max_obs too large for LDS");
   if (blk == 64)
-    hipLaunchKernelGGL(env_step_kernel<64>, dim3(grid), dim3(64), smem, as_stream(stream), *params, *state, actions,
-                       noise, *ctl, *out);
+    hipLaunchKernelGGL((env_step_kernel<64, false>), dim3(grid), dim3(64), smem, as_stream(stream), *params, *state,
+                       actions, noise, *ctl, *out, epb);
   else
-    hipLaunchKernelGGL(env_step_kernel<256>, dim3(grid), dim3(256), smem, as_stream(stream), *params, *state,
-                       actions, noise, *ctl, *out);
+    hipLaunchKernelGGL((env_step_kernel<256, false>), dim3(grid), dim3(256), smem, as_stream(stream), *params,
+                       *state, actions, noise, *ctl, *out, epb);
   return check_launch("asvrl_env_step");
 }
 

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--robots", type=int, default=5)
     ap.add_argument("--obstacles", type=int, default=4)
+    ap.add_argument("--width", type=float, default=55.0, help="map width = height (config 5: 110)")
     ap.add_argument("--noise", default="f32,f64", help="Philox draw precision(s): f32 (noise_mode 2), f64 (1)")
     ap.add_argument("--obs-only", action="store_true", help="time the observation pass alone (do_dynamics=0)")
     a = ap.parse_args()
@@ -31,7 +32,7 @@ def main():
     for E, mode in [(int(x), m) for x in a.envs.split(",") for m in a.noise.split(",")]:
         fast = mode == "f32"
         b = DeviceEnvBatch(E, R, O, 0)
-        b.reset(reset_cfg(R, O, 0, 40.0), seed=1)
+        b.reset(reset_cfg(R, O, 0, 40.0, a.width, a.width), seed=1)
         b.step(None, do_dynamics=False, seed=1, counter=0, fast_noise=fast)
         g = torch.Generator(device="cuda").manual_seed(0)
         acts = [(torch.rand((E * R, 2), generator=g, device="cuda", dtype=torch.float64) * 2 - 1) for _ in range(4)]
@@ -49,7 +50,8 @@ def main():
         torch.cuda.synchronize()
         us = 1e3 * e0.elapsed_time(e1) / a.iters
         gbs = bpe * E / (us * 1e-6) / 1e9
-        print(json.dumps({"envs": E, "noise": mode, "obs_only": a.obs_only, "robots": R, "obstacles": O, "us_per_step": us, "env_steps_per_s": E / (us * 1e-6),
+        print(json.dumps({"envs": E, "noise": mode, "obs_only": a.obs_only, "robots": R, "obstacles": O, "width": a.width,
+                          "pairs": os.environ.get("ASVRL_ENV_PAIRS", "1") != "0", "us_per_step": us, "env_steps_per_s": E / (us * 1e-6),
                           "alg_bytes_per_env_step": bpe, "achieved_GBps": gbs, "hbm_frac": gbs / 8000.0}))
         del b
 
