@@ -533,11 +533,13 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(AsvParams p, AsvEnvStat
     }
     cnt = nkept < p.max_obj_num ? nkept : p.max_obj_num;
     // COLREGs over the kept objects in order, stop at the first hit (wamv.py:517-521)
+#ifndef ASVRL_NO_COLREGS
     if (cnt > 0) apply = colregs(p.r, cs, sn, r.v0, r.v1, t0.a, t0.b, t0.c, t0.d, t0.e, phi);
     if (!apply && cnt > 1) apply = colregs(p.r, cs, sn, r.v0, r.v1, t1.a, t1.b, t1.c, t1.d, t1.e, phi);
     if (!apply && cnt > 2) apply = colregs(p.r, cs, sn, r.v0, r.v1, t2.a, t2.b, t2.c, t2.d, t2.e, phi);
     if (!apply && cnt > 3) apply = colregs(p.r, cs, sn, r.v0, r.v1, t3.a, t3.b, t3.c, t3.d, t3.e, phi);
     if (!apply && cnt > 4) apply = colregs(p.r, cs, sn, r.v0, r.v1, t4.a, t4.b, t4.c, t4.d, t4.e, phi);
+#endif
   }
 
   // ---------------- reward / done / info (env.py:290-331)
@@ -874,13 +876,25 @@ struct PairLaunch {
 PairLaunch pair_launch(int R, int O) {
   const int np1 = R * (O + R);
   PairLaunch L;
-  L.blk = np1 > 128 || R > 64 ? 256 : (np1 > 64 ? 128 : 64);
-  L.epb = L.blk / np1 > 1 ? L.blk / np1 : 1;
+  // the robots of the workgroup's envs fill its first wave (dynamics, merge, COLREGs run per robot:
+  // every wave issues them whatever its active lanes, so robots are packed densely); the pairs then
+  // spread over all four waves
+  static const int blk_env = [] {
+    const char* v = getenv("ASVRL_ENV_BLK");
+    return v != nullptr ? atoi(v) : 0;
+  }();
   static const int epb_env = [] {
     const char* v = getenv("ASVRL_ENV_EPB");
     return v != nullptr ? atoi(v) : 0;
   }();
-  if (epb_env > 0) L.epb = epb_env * R <= L.blk ? epb_env : L.blk / R;
+  L.blk = (blk_env == 64 || blk_env == 128 || blk_env == 256) ? blk_env : 256;
+  if (R > L.blk) L.blk = 256;
+  // about 40 robots per workgroup: measured best at 4096 envs (R = 5: 8 envs, 34 us vs 58 us for the
+  // per-robot sweep; R = 17: 3 envs, 133 us vs 203 us); more envs per group trade latency for
+  // throughput at very large batches (tools/env_ab3.sh)
+  L.epb = R <= 64 ? ((40 + R - 1) / R < 64 / R ? (40 + R - 1) / R : 64 / R) : 1;
+  if (epb_env > 0) L.epb = epb_env;
+  if (L.epb * R > L.blk) L.epb = L.blk / R;
   const size_t np = static_cast<size_t>(L.epb) * np1;
   L.smem = sizeof(double) * (8 * static_cast<size_t>(L.blk) + 6 * np + static_cast<size_t>(L.epb) * O * 3) +
            sizeof(int) * 3 * L.epb + 2 * L.blk + np;
@@ -911,7 +925,7 @@ extern "C" int asvrl_env_step(const AsvParams* params, const AsvEnvState* state,
     return v == nullptr || v[0] != '0';
   }();
   const PairLaunch pl = pair_launch(state->max_robots, state->max_obs);
-  if (pairs_env && pl.smem <= 64 * 1024) {
+  if (pairs_env && pl.smem <= 150 * 1024) {
     const int grid = (state->n_envs + pl.epb - 1) / pl.epb;
     if (pl.blk == 64)
       hipLaunchKernelGGL((env_step_kernel<64, true>), dim3(grid), dim3(64), pl.smem, as_stream(stream), *params,
