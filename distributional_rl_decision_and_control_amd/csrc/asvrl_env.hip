@@ -3,14 +3,16 @@
 // Replaces MarineNavEnv3.step / reset (rfarl/rfarl/envs/marinenav/env.py:72-164,240-333)
 // and the per-robot Robot methods they call (rfarl/rfarl/envs/marinenav/vehicles/wamv.py).
 //
-// Layout: robot state is field-major SoA in HBM (rs[field][e * R + i]); a workgroup of 256
-// lanes owns floor(256 / R) whole envs, lane = (env_in_block, robot). Phase 1 runs the N
-// Fossen substeps of each robot entirely in registers (f64, one sincos per substep). The
-// post-move positions/velocities of the block's robots and the env's buoys are then staged
-// in LDS, and phase 2 does each robot's perception sweep over obstacles + other vehicles
-// from LDS, keeping the 5 nearest candidates in registers (stable insertion network), then
-// COLREGs, reward, done/info and -- in the fused training loop -- trainer.py's deactivation
-// and the episode-end test, reduced per env through LDS.
+// Layout: robot state is field-major SoA in HBM (rs[field][e * R + i]). A 256-lane workgroup
+// owns about 40 robots' worth of whole envs, lane = (env_in_block, robot) in its first wave.
+// Phase 1 runs the N Fossen substeps of each robot entirely in registers (f64, one sincos per
+// substep). The post-move positions/velocities of the block's robots, their frames and the envs'
+// buoys are then staged in LDS; phase 2a gives every (robot, candidate) pair of the block one lane
+// across all four waves (noisy observation, detection, collision, sort key into LDS), and phase 2b
+// merges each robot's candidates in the reference's order (stable top-5 insertion), then COLREGs,
+// reward, done/info and -- in the fused training loop -- trainer.py's deactivation and the
+// episode-end test, reduced per env through LDS. (ASVRL_ENV_PAIRS=0: the per-robot sweep, phase 2
+// as one serial loop per lane, 64-lane groups.)
 //
 // Arithmetic follows the reference's operation order (np.matrix products as explicit row
 // sums, no FMA contraction: built with -ffp-contract=off) so f64 state agrees with the

@@ -51,40 +51,55 @@ __device__ __forceinline__ float scale_noise(float x) {   // x.sign() * x.abs().
   return x > 0.f ? r : (x < 0.f ? -r : 0.f);
 }
 
-// One workgroup per layer (segment pairs: weight 2j, bias 2j + 1): eps_in / eps_out drawn into LDS,
-// then eps_w, eps_b and the composed W, b written.
-__global__ __launch_bounds__(256) void noisy_reset_kernel(AsvNoisySegs s, const int32_t* __restrict__ in_f,
-                                                          const int32_t* __restrict__ out_f, uint64_t seed,
+// reset_noise chunks: each workgroup owns kResetRows output units of one layer (segment pairs: weight 2j,
+// bias 2j + 1). The Philox draws are counter-based per (layer, draw index), so every workgroup of a layer
+// regenerates the same eps_in and its own eps_out rows; draw j < in is eps_in[j], j >= in is eps_out[j - in].
+constexpr int kResetRows = 16;
+constexpr int kMaxNoisyLayers = ASVRL_MAX_NOISY_SEGS / 2;
+struct NoisyDims {
+  int n_layers;
+  int in_f[kMaxNoisyLayers], out_f[kMaxNoisyLayers], chunk0[kMaxNoisyLayers + 1];
+};
+
+__device__ __forceinline__ float noise_draw(int layer, int j, uint64_t seed, uint64_t ctr) {
+  const int t = j >> 1;
+  const U4 r = philox4x32_10(U4{static_cast<uint32_t>(t), static_cast<uint32_t>(layer), static_cast<uint32_t>(ctr),
+                                static_cast<uint32_t>(ctr >> 32) ^ 0x4E015u},
+                             static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
+  const float u1 = (static_cast<float>(r.x >> 8) + 1.0f) * (1.0f / 16777216.0f);
+  const float u2 = static_cast<float>(r.y >> 8) * (1.0f / 16777216.0f);
+  const float rad = __fsqrt_rn(-2.0f * __logf(u1));
+  float sn, cs;
+  __sincosf(6.2831853f * u2, &sn, &cs);
+  return scale_noise(rad * ((j & 1) ? sn : cs));   // N(0, 1) -> sign(x) sqrt|x|
+}
+
+__global__ __launch_bounds__(256) void noisy_reset_kernel(AsvNoisySegs s, NoisyDims dims, uint64_t seed,
                                                           const int64_t* __restrict__ counter_dev) {
-  __shared__ float e_in[256], e_out[2048];
-  const int layer = blockIdx.x;
-  const int nin = in_f[layer], nout = out_f[layer];
+  __shared__ float e_in[256], e_out[kResetRows];
+  const int chunk = blockIdx.x;
+  int layer = 0;
+  while (layer + 1 < dims.n_layers && chunk >= dims.chunk0[layer + 1]) ++layer;
+  const int nin = dims.in_f[layer], nout = dims.out_f[layer];
+  const int o0 = (chunk - dims.chunk0[layer]) * kResetRows;
+  const int no = nout - o0 < kResetRows ? nout - o0 : kResetRows;
   const uint64_t ctr = counter_dev != nullptr ? static_cast<uint64_t>(*counter_dev) : 0ull;
-  for (int t = threadIdx.x; 2 * t < nin + nout; t += blockDim.x) {
-    const U4 r = philox4x32_10(U4{static_cast<uint32_t>(t), static_cast<uint32_t>(layer), static_cast<uint32_t>(ctr),
-                                  static_cast<uint32_t>(ctr >> 32) ^ 0x4E015u},
-                               static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
-    const float u1 = (static_cast<float>(r.x >> 8) + 1.0f) * (1.0f / 16777216.0f);
-    const float u2 = static_cast<float>(r.y >> 8) * (1.0f / 16777216.0f);
-    const float rad = __fsqrt_rn(-2.0f * __logf(u1));
-    float sn, cs;
-    __sincosf(6.2831853f * u2, &sn, &cs);
-    const int j0 = 2 * t, j1 = 2 * t + 1;
-    const float z0 = scale_noise(rad * cs), z1 = scale_noise(rad * sn);
-    if (j0 < nin) e_in[j0] = z0; else if (j0 < nin + nout) e_out[j0 - nin] = z0;
-    if (j1 < nin) e_in[j1] = z1; else if (j1 < nin + nout) e_out[j1 - nin] = z1;
-  }
+  for (int j = threadIdx.x; j < nin; j += blockDim.x) e_in[j] = noise_draw(layer, j, seed, ctr);
+  if (threadIdx.x < no) e_out[threadIdx.x] = noise_draw(layer, nin + o0 + threadIdx.x, seed, ctr);
   __syncthreads();
   const AsvNoisySeg& w = s.seg[2 * layer];
   const AsvNoisySeg& b = s.seg[2 * layer + 1];
-  const int64_t nw = static_cast<int64_t>(nin) * nout;
-  for (int64_t i = threadIdx.x; i < nw; i += blockDim.x) {
-    const float e = e_out[i / nin] * e_in[i % nin];   // epsilon_out.ger(epsilon_in) (:44)
-    w.eps[i] = e;
-    w.out[i] = w.mu[i] + w.sigma[i] * e;
+  const int n = no * nin;
+  const int64_t base = static_cast<int64_t>(o0) * nin;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int o = i / nin, k = i - o * nin;
+    const float e = e_out[o] * e_in[k];   // epsilon_out.ger(epsilon_in) (:44)
+    w.eps[base + i] = e;
+    w.out[base + i] = w.mu[base + i] + w.sigma[base + i] * e;
   }
-  for (int o = threadIdx.x; o < nout; o += blockDim.x) {
-    const float e = e_out[o];
+  if (threadIdx.x < no) {
+    const int o = o0 + threadIdx.x;
+    const float e = e_out[threadIdx.x];
     b.eps[o] = e;
     b.out[o] = b.mu[o] + b.sigma[o] * e;
   }
@@ -273,8 +288,20 @@ extern "C" int asvrl_noisy_reset(const AsvNoisySegs* segs, const int32_t* in_fea
                                  uint64_t seed, const int64_t* counter_dev, void* stream) {
   if (int rc = check_segs(segs, "asvrl_noisy_reset")) return rc;
   ASVRL_REQUIRE(segs->n % 2 == 0 && in_features && out_features, "asvrl_noisy_reset: (weight, bias) segment pairs");
-  hipLaunchKernelGGL(noisy_reset_kernel, dim3(segs->n / 2), dim3(256), 0, as_stream(stream), *segs, in_features,
-                     out_features, seed, counter_dev);
+  NoisyDims d{};
+  d.n_layers = segs->n / 2;
+  d.chunk0[0] = 0;
+  for (int l = 0; l < d.n_layers; ++l) {
+    d.in_f[l] = in_features[l];
+    d.out_f[l] = out_features[l];
+    ASVRL_REQUIRE(d.in_f[l] >= 1 && d.in_f[l] <= 256 && d.out_f[l] >= 1, "asvrl_noisy_reset: in_features in [1, 256]");
+    ASVRL_REQUIRE(segs->off[2 * l + 1] - segs->off[2 * l] == static_cast<int64_t>(d.in_f[l]) * d.out_f[l] &&
+                      segs->off[2 * l + 2] - segs->off[2 * l + 1] == d.out_f[l],
+                  "asvrl_noisy_reset: segment sizes do not match in/out features");
+    d.chunk0[l + 1] = d.chunk0[l] + (d.out_f[l] + kResetRows - 1) / kResetRows;
+  }
+  hipLaunchKernelGGL(noisy_reset_kernel, dim3(d.chunk0[d.n_layers]), dim3(256), 0, as_stream(stream), *segs, d, seed,
+                     counter_dev);
   return check_launch("asvrl_noisy_reset");
 }
 

@@ -64,8 +64,8 @@ class NoisyPack:
         s.off[k] = off
         self.segs = s
         self.layers = layers
-        self.in_f = torch.tensor([L.in_features for L in layers], dtype=torch.int32, device=dev)
-        self.out_f = torch.tensor([L.out_features for L in layers], dtype=torch.int32, device=dev)
+        self.in_f = (C.c_int32 * len(layers))(*[L.in_features for L in layers])     # host arrays
+        self.out_f = (C.c_int32 * len(layers))(*[L.out_features for L in layers])
 
     def weights(self, detach_grad=False):
         """{layer: (W, b)}; detach_grad: fresh leaf tensors (same storage) that collect dW, db."""
@@ -78,7 +78,7 @@ class NoisyPack:
 
     def reset(self, seed, counter_dev, stream=None):
         """reset_noise() on every noisy layer + compose, one launch."""
-        _abi.check(_abi.lib().asvrl_noisy_reset(C.byref(self.segs), _abi.ptr(self.in_f), _abi.ptr(self.out_f),
+        _abi.check(_abi.lib().asvrl_noisy_reset(C.byref(self.segs), self.in_f, self.out_f,
                                                 int(seed) & 0xFFFFFFFFFFFFFFFF, _abi.ptr(counter_dev),
                                                 _abi.stream_ptr(stream)), "asvrl_noisy_reset")
 

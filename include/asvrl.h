@@ -442,8 +442,8 @@ int asvrl_noisy_compose(const AsvNoisySegs* segs, int32_t backward, void* stream
 
 /* reset_noise() of every layer (Rainbow_model.py:35-45,141-145) with (weight, bias) segment pairs:
  * f(x) = sign(x) sqrt|x| of N(0, 1) Philox draws (seed, *counter_dev), eps_w = f(eps_out) f(eps_in)^T,
- * eps_b = f(eps_out), and out = mu + sigma * eps in the same launch. in/out_features: device int32
- * [n/2] (in <= 256, out <= 2048). One workgroup per layer. */
+ * eps_b = f(eps_out), and out = mu + sigma * eps in the same launch. in/out_features: HOST int32
+ * [n/2] (in <= 256). One workgroup per 16 output units. */
 int asvrl_noisy_reset(const AsvNoisySegs* segs, const int32_t* in_features, const int32_t* out_features,
                       uint64_t seed, const int64_t* counter_dev, void* stream);
 
