@@ -11,7 +11,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ASVRL_LIB", os.path.join(HERE, "lib", "libasvrl.so"))  # override: A/B variants
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
 OBS_DIM = 40   # self 7 | objects 25 | mask 5 | pad 3
@@ -188,7 +188,8 @@ EXPORTS = [
                                   C.POINTER(AsvCriticActs), _VP]),
     ("asvrl_iqn_act", C.c_int, [C.POINTER(AsvCriticWeights), C.POINTER(AsvIqnHead), C.POINTER(AsvIqnIO), _VP]),
     ("asvrl_replay_push", C.c_int, [_VP, _VP, _VP, _VP, _I32, _VP, _VP, _I32, _VP, _I64, _VP, _VP, _VP]),
-    ("asvrl_replay_sample", C.c_int, [_VP, _I64, _VP, _VP, _I32, _U64, _U64, _VP, _I64, _VP, _VP, _VP]),
+    ("asvrl_replay_sample", C.c_int, [_VP, _I64, _VP, _VP, _I32, _U64, _U64, _VP, _I64, _VP, _VP, _VP, _I32, _I32,
+                                      _VP]),
     ("asvrl_replay_write_rows", C.c_int, [_VP, _VP, _I32, _VP, _VP]),
     ("asvrl_per_push", C.c_int, [C.POINTER(AsvPer), _VP, _VP, _VP, _I32, _VP, _VP, _I32, _VP]),
     ("asvrl_per_sample", C.c_int, [C.POINTER(AsvPer), _I32, _VP, _U64, _U64, _VP, _VP, _VP, _VP]),

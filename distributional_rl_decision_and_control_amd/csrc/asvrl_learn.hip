@@ -260,7 +260,8 @@ __global__ __launch_bounds__(4 * kWave) void replay_sample_kernel(const float* _
                                                                   uint64_t seed, uint64_t counter,
                                                                   const uint64_t* __restrict__ counter_dev,
                                                                   int64_t guard, float* __restrict__ out,
-                                                                  int64_t* out_slots) {
+                                                                  int64_t* out_slots, float* __restrict__ taus,
+                                                                  int tau_sets, int tau_n) {
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
@@ -283,6 +284,26 @@ __global__ __launch_bounds__(4 * kWave) void replay_sample_kernel(const float* _
   }
   const int64_t slot = ((head - size + k) % cap + cap) % cap;  // deque index 0 = oldest
   if (lane == 0 && out_slots != nullptr) out_slots[b] = slot;
+  if (taus != nullptr) {
+    // the update's quantile fractions tau ~ U[0, 1) (AC_IQN_model.py:419, torch.rand), tau_sets sets of
+    // [B][tau_n] drawn here so the learner needs no RNG launch: Philox(seed, step) per (row, set, 4 taus)
+    const uint64_t ctr = counter + (counter_dev != nullptr ? *counter_dev : 0ull);
+    const int per_row = tau_sets * tau_n;
+    for (int k0 = 4 * lane; k0 < per_row; k0 += 4 * kWave) {
+      const U4 r = philox4x32_10(U4{static_cast<uint32_t>(b), static_cast<uint32_t>(k0) ^ 0x7A0000u,
+                                    static_cast<uint32_t>(ctr >> 32), static_cast<uint32_t>(ctr)},
+                                 static_cast<uint32_t>(seed) ^ 0x51EDu, static_cast<uint32_t>(seed >> 32));
+      const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = k0 + j;
+        if (k < per_row) {
+          const int set = k / tau_n, t = k - set * tau_n;
+          taus[(static_cast<size_t>(set) * B + b) * tau_n + t] = static_cast<float>(w[j] >> 8) * (1.0f / 16777216.0f);
+        }
+      }
+    }
+  }
   if (lane < ASVRL_TR_DIM / 4) {
     const float4* src = reinterpret_cast<const float4*>(ring + slot * ASVRL_TR_DIM);
     reinterpret_cast<float4*>(out + static_cast<size_t>(b) * ASVRL_TR_DIM)[lane] = src[lane];
@@ -366,12 +387,14 @@ extern "C" int asvrl_replay_push(const float* obs_prev, const float* obs_next, c
 extern "C" int asvrl_replay_sample(const float* ring, int64_t capacity, const int64_t* ring_state,
                                    const int64_t* indices, int32_t B, uint64_t seed, uint64_t counter,
                                    const uint64_t* counter_dev, int64_t guard, float* out, int64_t* out_slots,
-                                   void* stream) {
+                                   float* taus, int32_t tau_sets, int32_t tau_n, void* stream) {
   ASVRL_REQUIRE(ring && ring_state && out, "asvrl_replay_sample: null argument");
   ASVRL_REQUIRE(capacity > 0, "asvrl_replay_sample: bad capacity");
+  ASVRL_REQUIRE(taus == nullptr || (tau_sets >= 1 && tau_n >= 1), "asvrl_replay_sample: bad tau shape");
   if (B <= 0) return 0;
   hipLaunchKernelGGL(replay_sample_kernel, dim3((B + 3) / 4), dim3(4 * kWave), 0, as_stream(stream), ring,
-                     capacity, ring_state, indices, B, seed, counter, counter_dev, guard, out, out_slots);
+                     capacity, ring_state, indices, B, seed, counter, counter_dev, guard, out, out_slots, taus,
+                     tau_sets, tau_n);
   return check_launch("asvrl_replay_sample");
 }
 

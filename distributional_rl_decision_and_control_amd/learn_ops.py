@@ -106,21 +106,25 @@ class DeviceReplay:
         B = indices.shape[0]
         out = out if out is not None else torch.empty((B, TR_DIM), dtype=torch.float32, device=self.device)
         rc = _abi.lib().asvrl_replay_sample(_abi.ptr(self.ring), self.capacity, _abi.ptr(self.state),
-                                            _abi.ptr(indices), B, 0, 0, None, 0, _abi.ptr(out), None,
+                                            _abi.ptr(indices), B, 0, 0, None, 0, _abi.ptr(out), None, None, 0, 0,
                                             _abi.stream_ptr(stream))
         _abi.check(rc, "asvrl_replay_sample")
         return out
 
-    def sample(self, B, seed=0, counter=0, counter_dev=None, out=None, stream=None, state=None, guard=0):
+    def sample(self, B, seed=0, counter=0, counter_dev=None, out=None, stream=None, state=None, guard=0, taus=None):
         """B rows drawn uniformly with replacement on the device (Philox). `state`: a {head, size}
         snapshot to sample against (default: the live ring state); `guard`: skip the oldest
-        entries a concurrent push of up to `guard` rows may overwrite."""
+        entries a concurrent push of up to `guard` rows may overwrite. taus: optional (sets, B, N)
+        f32 buffer filled with U[0, 1) quantile fractions by the same launch."""
         out = out if out is not None else torch.empty((B, TR_DIM), dtype=torch.float32, device=self.device)
         st = state if state is not None else self.state
+        ts, tn = (taus.shape[0], taus.shape[2]) if taus is not None else (0, 0)
+        if taus is not None:
+            assert taus.is_contiguous() and taus.shape[1] == B and taus.dtype == torch.float32
         rc = _abi.lib().asvrl_replay_sample(_abi.ptr(self.ring), self.capacity, _abi.ptr(st), None, B,
                                             int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter) & 0xFFFFFFFFFFFFFFFF,
-                                            _abi.ptr(counter_dev), int(guard), _abi.ptr(out), None,
-                                            _abi.stream_ptr(stream))
+                                            _abi.ptr(counter_dev), int(guard), _abi.ptr(out), None, _abi.ptr(taus),
+                                            ts, tn, _abi.stream_ptr(stream))
         _abi.check(rc, "asvrl_replay_sample")
         return out
 

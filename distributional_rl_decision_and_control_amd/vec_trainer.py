@@ -143,6 +143,8 @@ class VecTrainer:
         self.actions = torch.zeros((NT, 2), dtype=torch.float64, device=self.device)
         self.learn_counter = torch.zeros(1, dtype=torch.int64, device=self.device)
         self.batch_rows = torch.zeros((self.B, 88), dtype=torch.float32, device=self.device)
+        # the fused updates' quantile fractions (AC-IQN: target, local, actor step; IQN: the first two)
+        self.taus = torch.zeros((3, self.B, self.num_tau), dtype=torch.float32, device=self.device)
         self.learn_steps = 0
         self.iterations = 0
         self.last_losses = None
@@ -256,17 +258,18 @@ class VecTrainer:
             self.per.update_priorities(idx, loss)   # update_priorities(idxs, loss) (agent.py:639)
             self.learn_counter += 1
             return loss.mean(), gn
+        taus = self.taus if self._fused_learner() else None   # drawn by the sampling launch
         rows = self.replay.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter, out=self.batch_rows,
-                                  state=state, guard=guard)
+                                  state=state, guard=guard, taus=taus)
         if self.agent_type == "AC-IQN" and self.fused2 is not None:
             out = ac_iqn_update_fused2(self.fused2, self.local, self.actor_opt, self.critic_opt, self.critic_grads,
                                        self.actor_grads, rows, gamma=self.gamma, sync=self.sync,
-                                       actor_wait=actor_wait)
+                                       actor_wait=actor_wait, taus=taus)
             self.learn_counter += 1
             return out
         if self.fused_iqn is not None:
             out = iqn_update_fused(self.fused_iqn, self.local, self.opt, self.grads, rows, gamma=self.gamma,
-                                   sync=self.sync, act_wait=actor_wait)
+                                   sync=self.sync, act_wait=actor_wait, taus=taus[:2])
             self.learn_counter += 1
             return out
         s, a, r, ns, d = split_rows(rows)

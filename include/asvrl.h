@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 6
+#define ASVRL_ABI_VERSION 7
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -355,11 +355,13 @@ int asvrl_replay_push(const float* obs_prev, const float* obs_next, const int8_t
  * drawn uniformly (with replacement) by Philox(seed, counter + *counter_dev), skipping the
  * oldest entries that a push of up to `guard` rows running concurrently could overwrite
  * (guard = 0: none). ring_state may be a snapshot {head, size} taken before that push.
- * out [B][ASVRL_TR_DIM]; out_slots optional [B]. */
+ * out [B][ASVRL_TR_DIM]; out_slots optional [B]. taus (optional): tau_sets x [B][tau_n] quantile
+ * fractions U[0, 1) for the update (the torch.rand of AC_IQN_model.py:419 / IQN_model.py:62), drawn
+ * from Philox(seed, counter + *counter_dev) in the same launch. */
 int asvrl_replay_sample(const float* ring, int64_t capacity, const int64_t* ring_state,
                         const int64_t* indices, int32_t B, uint64_t seed, uint64_t counter,
                         const uint64_t* counter_dev, int64_t guard, float* out, int64_t* out_slots,
-                        void* stream);
+                        float* taus, int32_t tau_sets, int32_t tau_n, void* stream);
 
 /* Host-side index copy helper for a ring with known (host) head/size: write rows given by
  * slot into the ring (used by the compat ReplayBuffer.add, one transition per call). */

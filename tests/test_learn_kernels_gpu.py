@@ -154,3 +154,24 @@ def test_vec_trainer_overlapped_streams_in_graph():
         runs[overlap] = np.array(losses)
     a, b = runs[True][-10:, 0].mean(), runs[False][-10:, 0].mean()
     assert 0.2 < a / b < 5.0
+
+
+def test_replay_sample_draws_taus():
+    """The sampling launch also draws the update's quantile fractions (torch.rand of
+    AC_IQN_model.py:419): U[0, 1) moments, independent sets, fresh values per learn step."""
+    from distributional_rl_decision_and_control_amd import learn_ops
+    ring = learn_ops.DeviceReplay(1000, device="cuda")
+    ring.state[0], ring.state[1] = 0, 1000
+    B, N = 4096, 32
+    taus = torch.empty(3, B, N, device="cuda")
+    ctr = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ring.sample(B, seed=9, counter_dev=ctr, taus=taus)
+    t1 = taus.clone()
+    ctr += 1
+    ring.sample(B, seed=9, counter_dev=ctr, taus=taus)
+    x = t1.double().cpu().numpy()
+    assert x.min() >= 0.0 and x.max() < 1.0
+    assert abs(x.mean() - 0.5) < 4 * (1 / np.sqrt(12)) / np.sqrt(x.size)
+    assert abs(x.var() - 1 / 12) < 0.002
+    assert abs(np.corrcoef(x[0].ravel(), x[1].ravel())[0, 1]) < 0.01
+    assert not torch.equal(t1, taus)
