@@ -11,7 +11,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ASVRL_LIB", os.path.join(HERE, "lib", "libasvrl.so"))  # override: A/B variants
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
 OBS_DIM = 40   # self 7 | objects 25 | mask 5 | pad 3
@@ -82,7 +82,7 @@ class AsvCriticWeights(C.Structure):
 
 
 class AsvCriticActs(C.Structure):
-    _fields_ = [(n, C.c_void_p) for n in ("cos", "h0", "dzc", "h1g", "dz1", "h2", "dz2", "dq")]
+    _fields_ = [(n, C.c_void_p) for n in ("cos", "h0", "dzc", "h1g", "dz1", "h2", "dz2", "dq", "wout_part")]
 
 
 # (name, restype, argtypes) of every exported entry point, mirroring include/asvrl.h
@@ -201,6 +201,7 @@ EXPORTS = [
     ("asvrl_rainbow_loss", C.c_int, [C.POINTER(AsvRainbowHeadIO), _VP]),
     ("asvrl_adam_clip", C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, _F, _F, _VP, _VP, _VP]),
     ("asvrl_linear_wgrad_workspace", _I64, [_I32, _I32]),
+    ("asvrl_critic_wout_groups", _I32, [_I32, _I32]),
     ("asvrl_linear_wgrad_groups", _I32, [_I32, _I32, _I32]),
     ("asvrl_linear_wgrad_vec_groups", _I32, [_I32]),
     ("asvrl_linear_wgrad_partial", C.c_int, [_VP, _I64, _VP, _I64, _I32, _I32, _I32, _VP, _I64, _VP, _VP]),

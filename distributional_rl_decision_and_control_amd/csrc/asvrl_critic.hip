@@ -245,7 +245,7 @@ __device__ __forceinline__ void iqn_act_select(const CriticArgs& a, const Critic
 
 template <int MODE, int NT, class LT>
 __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, int tile, int lane, const __bf16* Fl,
-                                            const float* Gl) {
+                                            const float* Gl, float* wsum = nullptr) {
   constexpr bool IQN = kIqn<MODE>;
   constexpr bool TRAINM = kTrainMode<MODE>;
   const int r = lane & 31, h = lane >> 5;
@@ -467,7 +467,13 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
   }
 
   // ---------------- dz2 = dq * wo * 1[z2 > 0]
+  // AC-IQN TRAIN with wout_part: output_layer's weight gradient sum_rows dq * h2 is reduced over the
+  // tile's 32 rows right here (transpose-reduce per two 32-feature blocks) and then over the
+  // workgroup's tiles in LDS, so h2 never goes to HBM
+  const bool wout = MODE == MODE_TRAIN && wsum != nullptr;   // this wave's row of the workgroup's LDS sums
+  float* wp = wsum;
   bf16x8 dz2pk[8];
+  float wsa[32];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) {
 #pragma unroll
@@ -480,13 +486,23 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
         hv[j] = relu(z);
         dv[j] = z > 0.f ? dq * out_w(L, ai, m) : 0.f;
         dz2pk[mb * 2 + s][j] = (__bf16)dv[j];
+        wsa[((mb & 1) * 2 + s) * 8 + j] = dq * hv[j];
       }
       if (TRAINM) {
         const size_t o = static_cast<size_t>(grow) * kH + mb * 32 + 16 * s;
-        store16(bp(a.acts.h2) + o, hv, h);
+        if (!wout) store16(bp(a.acts.h2) + o, hv, h);
         store16(bp(a.acts.dz2) + o, dv, h);
       }
     }
+    if (MODE == MODE_TRAIN && (mb & 1) && wout) {   // wave-uniform
+      xreduce<32, 32>(wsa, lane);   // lane r: the tile sum of value r of this block pair
+      const int mbb = (mb & ~1) + (r >> 4);
+      wp[feat(mbb, 8 * ((r >> 3) & 1) + (r & 7), h)] = wsa[0];
+    }
+  }
+  if (MODE == MODE_TRAIN && wout) {
+    const float db = seg_sum<32>(h == 0 ? dq : 0.f);   // lane 31: the tile's sum of dq
+    if (lane == 31) wp[kH] = db;
   }
 
   // ---------------- layer 3: dh1g = W2^T dz2; dG[b] = sum_taus dh1g * h1; dz1 = dh1g * G * 1[h1 > 0]
@@ -670,6 +686,7 @@ __global__ __launch_bounds__(CriticWaves<NT>::n * 64) void critic_kernel(CriticA
   __shared__ typename LdsOf<MODE>::T L;
   __shared__ __attribute__((aligned(16))) __bf16 Fs[W * S * kC];
   __shared__ __attribute__((aligned(16))) float Gs[kStageG<MODE> ? W * S * kH : 1];
+  __shared__ float Ws[MODE == MODE_TRAIN ? W * (kH + 1) : 1];   // per-wave output-layer gradient sums
   const int tile = blockIdx.x * W + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int tiles = a.B * NT / 32;
   __bf16* Fw = Fs + (threadIdx.x >> 6) * S * kC;
@@ -698,10 +715,32 @@ __global__ __launch_bounds__(CriticWaves<NT>::n * 64) void critic_kernel(CriticA
     }
   }
   __syncthreads();
-  if (tile < tiles) critic_tile<MODE, NT>(a, L, tile, lane, Fw, Gw);
+  const bool wout = MODE == MODE_TRAIN && a.acts.wout_part != nullptr;
+  float* wsum = wout ? Ws + (threadIdx.x >> 6) * (kH + 1) : nullptr;
+  if (tile < tiles) {
+    critic_tile<MODE, NT>(a, L, tile, lane, Fw, Gw, wsum);
+  } else if (wout) {
+    for (int i = lane; i < kH + 1; i += 64) wsum[i] = 0.f;
+  }
+  if (MODE == MODE_TRAIN && wout) {
+    // the workgroup's W tile sums in wave order: one [129] partial per workgroup
+    __syncthreads();
+    for (int i = threadIdx.x; i < kH + 1; i += W * 64) {
+      float acc = 0.f;
+#pragma unroll
+      for (int w = 0; w < W; ++w) acc += Ws[w * (kH + 1) + i];
+      a.acts.wout_part[static_cast<size_t>(blockIdx.x) * (kH + 1) + i] = acc;
+    }
+  }
 }
 
 int train_b_grid(int tiles) { return (tiles + 7) / 8; }
+
+int wout_groups(int B, int N) {   // workgroups of the TRAIN launch = groups of wout_part
+  const int tiles = B * N / 32;
+  const int W = N == 32 ? CriticWaves<32>::n : (N == 16 ? CriticWaves<16>::n : CriticWaves<8>::n);
+  return (tiles + W - 1) / W;
+}
 
 template <int MODE, int NT>
 void launch_mode(const CriticArgs& a, hipStream_t st) {
@@ -833,8 +872,9 @@ extern "C" int asvrl_critic_train(const AsvCriticWeights* w, const AsvCriticIO* 
   ASVRL_REQUIRE(io->row_loss && acts && w->w2t_frag && w->w1t_frag, "asvrl_critic_train: null argument");
   ASVRL_REQUIRE(io->q_targets || (io->q_next && io->rewards && io->dones),
                 "asvrl_critic_train: needs q_targets or q_next + rewards + dones");
-  ASVRL_REQUIRE(acts->cos && acts->h0 && acts->dzc && acts->h1g && acts->dz1 && acts->h2 && acts->dz2 && acts->dq,
-                "asvrl_critic_train: null activation buffer");
+  ASVRL_REQUIRE(acts->cos && acts->h0 && acts->dzc && acts->h1g && acts->dz1 && acts->dz2 &&
+                    ((acts->h2 && acts->dq) || acts->wout_part),
+                "asvrl_critic_train: null activation buffer (h2 and dq, or wout_part)");
   ASVRL_REQUIRE(io->Np >= 1 && io->kappa > 0.f, "asvrl_critic_train: bad Np/kappa");
   if (io->B == 0) return 0;
   CriticArgs a = make_args(w, io);
@@ -938,3 +978,5 @@ extern "C" int asvrl_iqn_act(const AsvCriticWeights* w, const AsvIqnHead* head, 
   if (io->B == 0) return 0;
   return launch(MODE_IQN_ACT, iqn_args(w, head, io), stream);
 }
+
+extern "C" int32_t asvrl_critic_wout_groups(int32_t B, int32_t N) { return wout_groups(B, N); }

@@ -148,12 +148,20 @@ class TrainBuffers:
         self.struct = a
 
 
+def wout_groups(B, N):
+    """Partials critic_train(wout_part=...) writes (one per TRAIN workgroup)."""
+    return int(_abi.lib().asvrl_critic_wout_groups(B, N))
+
+
 def critic_train(pack, F, G, taus, q_targets, bufs, kappa=1.0, stream=None, q_next=None, rewards=None, dones=None,
-                 gamma=0.99, dzF=None, dzG=None, with_dFdG=True, tile_loss=None, obs=None, act=None, xb=None):
+                 gamma=0.99, dzF=None, dzG=None, with_dFdG=True, tile_loss=None, obs=None, act=None, xb=None,
+                 wout_part=None):
     """TRAIN launch. Targets: q_targets (B, Np), or q_next (B, Np) with rewards/dones column
     views (stride ld) combined in the kernel. With `tile_loss` ([B*N/32] f32) the kernel writes
     per-tile loss partials (sum them, e.g. in a PartialArena) and None is returned; otherwise
-    the loss row_loss.sum() / (B*Np) as a 0-d device tensor."""
+    the loss row_loss.sum() / (B*Np) as a 0-d device tensor. With `wout_part` ([wout_groups(B, N)]
+    [129] f32) the output layer's weight / bias gradient leaves as per-workgroup partials
+    (PartialArena.tiles) and neither h2 nor dq is written."""
     B, N = (F if F is not None else obs).shape[0], bufs.N
     Np = (q_targets if q_targets is not None else q_next).shape[1]
     kw = dict(q=bufs.q, row_loss=bufs.row_loss, dzF=dzF, dzG=dzG, tile_loss=tile_loss,
@@ -165,7 +173,13 @@ def critic_train(pack, F, G, taus, q_targets, bufs, kappa=1.0, stream=None, q_ne
     else:
         kw.update(q_next=q_next, rewards=rewards, dones=dones, ld_rd=rewards.stride(0), gamma=float(gamma))
     io = _io(F, G, taus, N, obs=obs, act=act, xb=xb, Np=Np, kappa=float(kappa), **kw)
-    _abi.check(_abi.lib().asvrl_critic_train(C.byref(pack.struct), C.byref(io), C.byref(bufs.struct),
+    acts = bufs.struct
+    if wout_part is not None:
+        assert wout_part.numel() >= wout_groups(B, N) * 129
+        acts = _abi.AsvCriticActs()
+        C.memmove(C.byref(acts), C.byref(bufs.struct), C.sizeof(acts))
+        acts.h2, acts.dq, acts.wout_part = None, None, wout_part.data_ptr()
+    _abi.check(_abi.lib().asvrl_critic_train(C.byref(pack.struct), C.byref(io), C.byref(acts),
                                              _abi.stream_ptr(stream)), "asvrl_critic_train")
     if tile_loss is not None:
         return None
@@ -272,6 +286,15 @@ class PartialArena:
                                                     _abi.ptr(part), part.numel(), C.byref(groups),
                                                     _abi.stream_ptr(stream)), "asvrl_linear_wgrad_vec_partial")
         self._seg(part, dw, db, groups.value, K, 1, accumulate)
+
+    def take_tiles(self, tiles, nw):
+        """A region for [tiles][nw + 1] per-tile partials written by a kernel (critic_train's
+        wout_part); queue its reduction with tiles() after the launch."""
+        return self._take(tiles * (nw + 1))
+
+    def tiles(self, part, tiles, dw, db, accumulate=False):
+        """dw (nw) (+)= sum over tiles of part[t][0:nw], db (+)= sum of part[t][nw]."""
+        self._seg(part, dw, db, tiles, dw.numel(), 1, accumulate)
 
     def scalar(self, partials, out, accumulate=False):
         """out (1 f32) (+)= sum(partials): a scalar segment (e.g. per-tile loss partials)."""

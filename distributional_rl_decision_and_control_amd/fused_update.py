@@ -7,7 +7,8 @@ Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | 
     target encoders(ns, na) + trunk -> q_next            asvrl_critic_forward (encoders in the prologue)
     local encoders(s, a) + trunk forward + quantile-Huber vs r + g q_next (1-d) + backward
                                                           asvrl_critic_train (targets formed in-kernel)
-    trunk weight grads                                   asvrl_linear_wgrad_partial x3 + _vec
+    trunk weight grads                                   asvrl_linear_wgrad_partial x3 (the output layer's
+                                                          as per-tile partials from the TRAIN kernel)
     encoder grads (256x32 image) and action-encoder grads
                                                           asvrl_linear_wgrad_partial + _small_wgrad_partial
     every .grad (encoders folded in the reduction), the loss and the global gradient norm
@@ -35,7 +36,7 @@ import contextlib
 import torch
 
 from .fused_critic import (CriticPack, PartialArena, TrainBuffers, critic_actor_grad, critic_forward, critic_train,
-                           trunk_weight_grads_into)
+                           trunk_weight_grads_into, wout_groups)
 from .fused_mlp import ActorBuffers, MlpPack, actor_act, actor_backward, actor_forward, actor_train_forward
 from .learner import FusedAdam, clip_and_step
 
@@ -145,14 +146,16 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
         actor_train_forward(st.actor, s_rows, ab)
     actor_forward(st.target_actor, ns_rows, st.na)
     critic_forward(st.target_trunk, None, None, taus[0], N, q=st.q_next, obs=ns_rows, act=st.na)
+    tiles = wout_groups(B, N)
+    wout_part = arena.take_tiles(tiles, 128)   # output_layer's gradient, reduced per workgroup in the kernel
     critic_train(st.local_trunk, None, None, taus[1], None, bufs, q_next=st.q_next.view(B, N), rewards=r_col,
                  dones=d_col, gamma=gamma, dzF=st.dzF, dzG=st.dzG, with_dFdG=False, tile_loss=st.tile_loss[0],
-                 obs=s_rows, act=a_rows, xb=st.xb)
+                 obs=s_rows, act=a_rows, xb=st.xb, wout_part=wout_part)
     ae = critic.action_encoder[0]
-    # the six weight-gradient reductions on three streams, one partial-sum launch after the join
+    arena.tiles(wout_part, tiles, critic.output_layer.weight.grad, critic.output_layer.bias.grad)
+    # the five weight-gradient reductions on three streams, one partial-sum launch after the join
     with side.on(0):
         arena.linear(bufs.dzc, bufs.cos, critic.cos_embedding.weight.grad, critic.cos_embedding.bias.grad)
-        arena.vec(bufs.dq, bufs.h2, critic.output_layer.weight.grad, critic.output_layer.bias.grad)
     arena.linear(bufs.dz1, bufs.h0, critic.hidden_layer.weight.grad, critic.hidden_layer.bias.grad)
     with side.on(1):
         arena.linear(bufs.dz2, bufs.h1g, critic.hidden_layer_2.weight.grad, critic.hidden_layer_2.bias.grad)

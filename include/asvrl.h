@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 7
+#define ASVRL_ABI_VERSION 8
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -226,7 +226,13 @@ typedef struct AsvCriticActs {
   void* h2;    /* [R][128]  relu(hidden_layer_2)     -> d output_layer.weight with dq */
   void* dz2;   /* [R][128]  dL/d(hidden_layer_2 pre-activation) */
   float* dq;   /* [R]       dL/dq */
+  float* wout_part; /* optional, AC-IQN TRAIN: [asvrl_critic_wout_groups(B, N)][129] per-workgroup
+                       partials of output_layer's dW (128) | db, reduced in the kernel from f32 h2 and
+                       dq (h2 and dq may then be NULL; reduce them with asvrl_partial_sums, nw 128, nb 1) */
 } AsvCriticActs;
+
+/* Number of [129] output-layer gradient partials asvrl_critic_train writes to acts->wout_part. */
+int32_t asvrl_critic_wout_groups(int32_t B, int32_t N);
 
 /* Fill the five bf16 fragment images of w (wc_frag .. w1t_frag) from the row-major f32
  * weights cos_embedding.weight (256 x 64), hidden_layer.weight (128 x 256) and
