@@ -89,15 +89,17 @@ class FusedACIQNState:
         f = dict(dtype=torch.float32, device=dev)
         bf = dict(dtype=torch.bfloat16, device=dev)
         self.na = torch.empty(B, 2, **f)
+        self.na_p = torch.empty(B, 2, **f)       # the pipelined target chain's actions
         self.xb = torch.empty(B, 32, **bf)
         self.q_next = torch.empty(B * N, **f)
+        self.q_next_buf = [self.q_next, torch.empty(B * N, **f)]   # pipelined: per batch parity
         self.q_pi = torch.empty(B * N, **f)
         self.dzF = torch.empty(B, 256, **bf)
         self.dzG = torch.empty(B, 128, **f)
         self.arena = PartialArena(16 << 20, dev)
         self.losses = torch.zeros(2, **f)   # critic, actor loss (summed from per-tile partials)
         self.tile_loss = torch.zeros(2, B * N // 32, **f)
-        self.side = SideStreams(dev, 2)
+        self.side = SideStreams(dev, 3)   # 0, 1: gradient reductions / actor forward; 2: next batch
 
     def target_changed(self):
         """Re-pack the target networks after a hard/soft update (eager, outside graphs)."""
@@ -126,10 +128,21 @@ def _reduce_and_step(arena, opt, grads, sync, max_norm, wait=None):
     return clip_and_step(opt, grads, max_norm)
 
 
+def target_q(st, rows, tau0, q_out, na):
+    """Q_targets_next of agent.py:397-400 for the rows' next states: target actor, then the target
+    critic with the target encoders inside the trunk kernel (q_out [B*N])."""
+    ns_rows = rows[:, OBS:2 * OBS]
+    actor_forward(st.target_actor, ns_rows, na)
+    critic_forward(st.target_trunk, None, None, tau0, st.N, q=q_out, obs=ns_rows, act=na)
+
+
 def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, actor_grads, rows, gamma=0.99,
-                         taus=None, sync=None, max_norm=0.5, actor_wait=None):
+                         taus=None, sync=None, max_norm=0.5, actor_wait=None, q_next=None, produce=None):
     """One AC-IQN update from replay rows [B][88]. taus: (3, B, N) or None (drawn here).
     actor_wait: event to wait for before the actor's weights change (a concurrent act kernel).
+    q_next: the rows' target quantiles already computed (the pipelined loop); produce: a callable
+    that samples the NEXT batch and computes its q_next, run on a side stream beside the actor
+    step (after the critic step, so the target chain overlaps the actor's kernels).
     Returns (critic_loss, actor_loss, critic_grad_norm, actor_grad_norm) as device scalars."""
     B, N = st.B, st.N
     critic, actor = policy_local.critic, policy_local.actor
@@ -144,11 +157,12 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     # trunk kernels run the critic's observation / action encoders on the replay rows themselves.
     with side.on(1):   # the actor's training forward reads only s and the (not yet updated) actor
         actor_train_forward(st.actor, s_rows, ab)
-    actor_forward(st.target_actor, ns_rows, st.na)
-    critic_forward(st.target_trunk, None, None, taus[0], N, q=st.q_next, obs=ns_rows, act=st.na)
+    if q_next is None:
+        q_next = st.q_next
+        target_q(st, rows, taus[0], q_next, st.na)
     tiles = wout_groups(B, N)
     wout_part = arena.take_tiles(tiles, 128)   # output_layer's gradient, reduced per workgroup in the kernel
-    critic_train(st.local_trunk, None, None, taus[1], None, bufs, q_next=st.q_next.view(B, N), rewards=r_col,
+    critic_train(st.local_trunk, None, None, taus[1], None, bufs, q_next=q_next.view(B, N), rewards=r_col,
                  dones=d_col, gamma=gamma, dzF=st.dzF, dzG=st.dzG, with_dFdG=False, tile_loss=st.tile_loss[0],
                  obs=s_rows, act=a_rows, xb=st.xb, wout_part=wout_part)
     ae = critic.action_encoder[0]
@@ -165,6 +179,9 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     arena.scalar(st.tile_loss[0], st.losses[0:1])   # the critic loss
     cgn = _reduce_and_step(arena, critic_opt, critic_grads, sync, max_norm)
     st.local_trunk.refresh()
+    if produce is not None:   # next batch + its target quantiles beside the actor step
+        with side.on(2):
+            produce()
 
     # ---- actor through the updated critic (agent.py:419-427); its forward ran on side stream 1
     critic_actor_grad(st.local_trunk, None, None, taus[2], N, st.q_pi, w_ae=ae.weight, dA=ab.dA,
@@ -182,4 +199,6 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     arena.scalar(st.tile_loss[1], st.losses[1:2])   # the actor loss
     agn = _reduce_and_step(arena, actor_opt, actor_grads, sync, max_norm, wait=actor_wait)
     st.actor.refresh()
+    if produce is not None:
+        side.join(2)
     return st.losses[0], st.losses[1], cgn, agn

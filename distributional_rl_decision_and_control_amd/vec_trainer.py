@@ -44,7 +44,7 @@ class VecTrainer:
                  learning_starts=None, target_update_interval=2500, total_timesteps=6_000_000,
                  exploration_fraction=0.25, initial_eps=0.6, final_eps=0.05, amp_dtype=torch.bfloat16, seed=0,
                  device="cuda", sync=None, graphs=False, schedule=None, net_seed=100, fused=True,
-                 fused_adam=True, overlap=True, unroll=1):
+                 fused_adam=True, overlap=True, unroll=1, pipeline=False):
         self.device = torch.device(device)
         self.agent_type = agent_type
         self.continuous = agent_type == "AC-IQN"
@@ -145,6 +145,17 @@ class VecTrainer:
         self.batch_rows = torch.zeros((self.B, 88), dtype=torch.float32, device=self.device)
         # the fused updates' quantile fractions (AC-IQN: target, local, actor step; IQN: the first two)
         self.taus = torch.zeros((3, self.B, self.num_tau), dtype=torch.float32, device=self.device)
+        # pipelined AC-IQN learner (opt-in): the next batch and its target quantiles are produced
+        # beside the current actor step (fused_update.target_q), so the critic step starts at once.
+        # Two buffer sets alternate by parity; a captured graph then holds two iterations (one per
+        # parity). Measured: no gain at the bench shape (0.5595 vs 0.559 ms) -- the GPU is saturated,
+        # the overlap only moves the contention (the rollout then lands on the TRAIN kernel).
+        self.pipeline = bool(pipeline) and self.fused2 is not None
+        if self.pipeline:
+            self.rows_buf = [self.batch_rows, torch.zeros_like(self.batch_rows)]
+            self.taus_buf = [self.taus, torch.zeros_like(self.taus)]
+            self._parity = 0
+            self._primed = False
         self.learn_steps = 0
         self.iterations = 0
         self.last_losses = None
@@ -153,7 +164,7 @@ class VecTrainer:
         # iterations per captured graph: one replay enqueues `unroll` whole iterations (the host
         # calls iteration() once per iteration; every unroll-th call replays). Measured: 2 gives no
         # gain over 1 (0.564 vs 0.559 ms/step), the in-graph joins keep the same gaps
-        self.unroll = max(1, int(unroll))
+        self.unroll = max(1, int(unroll), 2 if self.pipeline and graphs else 1)
         self._phase = 0
         self._graph_learn = None
         # rollout / learn on two streams (fused learners): the learner samples against a
@@ -239,7 +250,31 @@ class VecTrainer:
         self._push()
         self.env.auto_reset()
 
+    def _produce(self, nxt, state, guard, counter):
+        st = self.fused2
+        rows = self.replay.sample(self.B, seed=self.seed + 777, counter=counter, counter_dev=self.learn_counter,
+                                  out=self.rows_buf[nxt], state=state, guard=guard, taus=self.taus_buf[nxt])
+        from .fused_update import target_q
+        target_q(st, rows, self.taus_buf[nxt][0], st.q_next_buf[nxt], st.na_p)
+
+    def _learn_pipelined(self, state, guard, actor_wait):
+        cur = self._parity
+        nxt = 1 - cur
+        if not self._primed:   # the first batch of the run (eager, before any capture)
+            self._produce(cur, state, guard, 0)
+            self._primed = True
+        st = self.fused2
+        out = ac_iqn_update_fused2(st, self.local, self.actor_opt, self.critic_opt, self.critic_grads,
+                                   self.actor_grads, self.rows_buf[cur], gamma=self.gamma, sync=self.sync,
+                                   actor_wait=actor_wait, taus=self.taus_buf[cur], q_next=st.q_next_buf[cur],
+                                   produce=lambda: self._produce(nxt, state, guard, 1))
+        self._parity = nxt
+        self.learn_counter += 1
+        return out
+
     def learn(self, state=None, guard=0, actor_wait=None):
+        if self.pipeline:
+            return self._learn_pipelined(state, guard, actor_wait)
         if self.per is not None:
             rows, idx = self.per.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter,
                                         out=self.batch_rows, out_idx=self.per_idx)
@@ -386,6 +421,12 @@ class VecTrainer:
                 self._iteration_body(True)
                 self.env.advance_host()
         torch.cuda.current_stream(self.device).wait_stream(s)
+        if self.pipeline:   # the graph's first body consumes parity 0
+            while self._parity != 0:
+                with torch.cuda.stream(s):
+                    self._iteration_body(True)
+                    self.env.advance_host()
+                torch.cuda.current_stream(self.device).wait_stream(s)
         g = torch.cuda.CUDAGraph()
         # thread_local: the RCCL process group's watchdog thread queries its work events while this
         # thread captures; under the default global mode that query invalidates the capture and the
