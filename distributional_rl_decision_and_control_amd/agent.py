@@ -8,23 +8,27 @@ save_latest_model / load_model surfaces and return types. Differences:
   * train_* run the fused gfx950 quantile-Huber / C51 kernels (learner.py);
   * load_model rebuilds the optimizers for the loaded networks (the reference keeps
     optimizing the replaced ones, agent.py:684-698 vs :75-76,98);
-  * DQN / DDPG / SAC (non-distributional baselines) are out of scope and raise.
+  * DQN runs as the reference's plain torch update (BASELINE config 1 is the DQN plumbing run of
+    train_RL_agents.py); DDPG / SAC (non-distributional baselines) are out of scope and raise.
 """
 import copy
 import random
 
 import numpy as np
 import torch
+import torch.nn.functional as F
 
 from . import _abi
 from .learner import FlatGrads, ac_iqn_update, iqn_update, rainbow_update
 from .policy.AC_IQN_model import AC_IQN_Policy
+from .policy.DQN_model import DQN_Policy
 from .policy.IQN_model import IQN_Policy
 from .policy.Rainbow_model import Rainbow_Policy
 from .policy.replay_memory_rainbow import ReplayMemory
 from .utils.replay_buffer import ReplayBuffer
 
 DISTRIBUTIONAL = ("AC-IQN", "IQN", "Rainbow")
+SUPPORTED = DISTRIBUTIONAL + ("DQN",)
 
 
 def resolve_device(device):
@@ -58,8 +62,8 @@ class Agent:
         self.tau_override = None  # optional list of pre-drawn taus for the next train() (tests)
         self._net_args = (self_dimension, object_dimension, max_object_num, self_feature_dimension,
                           object_feature_dimension, concat_feature_dimension, hidden_dimension)
-        if agent_type not in DISTRIBUTIONAL:
-            if agent_type in ("DQN", "DDPG", "SAC"):
+        if agent_type not in SUPPORTED:
+            if agent_type in ("DDPG", "SAC"):
                 raise NotImplementedError(f"{agent_type} is a non-distributional baseline, outside this "
                                           "framework's hot path (SURVEY.md section 2, row 14)")
             raise RuntimeError("Agent type not implemented!")
@@ -86,6 +90,8 @@ class Agent:
             return AC_IQN_Policy(*a, value_ranges_of_action, self.device, seed)
         if self.agent_type == "IQN":
             return IQN_Policy(*a, action_size, self.device, seed).to(self.device)
+        if self.agent_type == "DQN":
+            return DQN_Policy(*a, action_size, self.device, seed).to(self.device)
         return Rainbow_Policy(*a, action_size, 51, self.device, seed).to(self.device)
 
     def _make_optimizers(self):
@@ -144,10 +150,20 @@ class Agent:
             return (p * self.support).sum(2).argmax(1).item()
         return random.choice(np.arange(self.action_size))
 
-    def act_dqn(self, *a, **k):
-        raise NotImplementedError("DQN is outside this framework's hot path")
+    def act_dqn(self, state, eps=0.0, use_eval=True):  # agent.py:271-287
+        s = self._batch1(state)
+        self.policy_local.eval() if use_eval else self.policy_local.train()
+        with torch.no_grad():
+            action_values = self.policy_local(s)
+        self.policy_local.train()
+        if random.random() > eps:
+            return np.argmax(action_values.cpu().data.numpy())
+        return random.choice(np.arange(self.action_size))
 
-    act_ddpg = act_sac = act_dqn
+    def act_ddpg(self, *a, **k):
+        raise NotImplementedError("DDPG is outside this framework's hot path")
+
+    act_sac = act_ddpg
 
     # ------------------------------------------------------------------ learning (agent.py:370-641)
     def train(self):
@@ -157,6 +173,8 @@ class Agent:
             return self.train_IQN()
         if self.agent_type == "Rainbow":
             return self.train_Rainbow()
+        if self.agent_type == "DQN":
+            return self.train_DQN()
         raise RuntimeError("Agent type not implemented!")
 
     def _taus(self, k):
@@ -188,6 +206,21 @@ class Agent:
         self.memory.update_priorities(idxs, loss)
         return loss
 
+    def train_DQN(self):
+        """agent.py:518-545: max-over-actions target, smooth L1, clip 0.5, Adam (plain torch)."""
+        s, a, r, ns, d = self.memory.sample()
+        actions = a[:, :1].to(torch.int64)
+        self.optimizer.zero_grad()
+        with torch.no_grad():
+            q_next = self.policy_target(ns).max(dim=1, keepdim=True)[0]
+            q_targets = r + (1 - d) * self.GAMMA * q_next
+        q_expected = self.policy_local(s).gather(1, actions)
+        loss = F.smooth_l1_loss(q_expected, q_targets)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(self.policy_local.parameters(), 0.5)
+        self.optimizer.step()
+        return loss.detach().cpu().numpy()
+
     def soft_update(self):
         """theta_t <- TAU theta + (1 - TAU) theta_t (agent.py:643-679)."""
         if self.agent_type == "AC-IQN":
@@ -204,7 +237,8 @@ class Agent:
 
     def load_model(self, path, device="cpu"):
         dev = resolve_device(device)
-        cls = {"AC-IQN": AC_IQN_Policy, "IQN": IQN_Policy, "Rainbow": Rainbow_Policy}[self.agent_type]
+        cls = {"AC-IQN": AC_IQN_Policy, "IQN": IQN_Policy, "Rainbow": Rainbow_Policy,
+               "DQN": DQN_Policy}[self.agent_type]
         self.policy_local = cls.load(path, dev)
         if self.training:
             self._make_optimizers()

@@ -60,6 +60,12 @@ def batched_greedy_actions(agent, states):
         p = net(s)
         net.train()
         greedy = [int(v) for v in (p * agent.support).sum(2).argmax(1).cpu().numpy()]
+    elif kind == "DQN":
+        net = agent.policy_local
+        net.eval()
+        q = net(s)
+        net.train()
+        greedy = [int(v) for v in q.argmax(dim=1).cpu().numpy()]
     else:
         raise RuntimeError("Agent type not implemented!")
     out = []

@@ -77,6 +77,8 @@ class Trainer:
                 return agent.act_iqn(state, eps, use_eval=False)[0]
             if kind == "Rainbow":
                 return agent.act_rainbow(state, eps, use_eval=False)
+            if kind == "DQN":
+                return agent.act_dqn(state, eps, use_eval=False)
         else:
             if kind == "AC-IQN":
                 return agent.act_ac_iqn(state)
@@ -84,6 +86,8 @@ class Trainer:
                 return agent.act_iqn(state)[0]
             if kind == "Rainbow":
                 return agent.act_rainbow(state)
+            if kind == "DQN":
+                return agent.act_dqn(state)
         raise RuntimeError("Agent type not implemented!")
 
     def _gather_actions(self, env, states, eps, training):

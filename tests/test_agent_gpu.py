@@ -135,3 +135,20 @@ def test_train_rainbow_matches_reference():
     np.testing.assert_allclose(loss, z["b64/loss"], rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(pr[0], z["b64/loss"], rtol=1e-5, atol=1e-6)
     _cmp_sd(ag.policy_local, z, "after/")
+
+
+def test_train_dqn_matches_reference():
+    """train_DQN (agent.py:518-545), the BASELINE config 1 agent: two steps on the captured batches."""
+    from distributional_rl_decision_and_control_amd.agent import Agent
+    z = np.load(eo.GOLDEN + "/learn_dqn.npz")
+    ag = Agent(seed=100, agent_type="DQN")
+    for k, v in ag.policy_local.state_dict().items():
+        np.testing.assert_array_equal(v.cpu().numpy(), z["init/" + k])
+    for step in range(2):
+        b = _batch(z, f"step{step}/", ag.device, long_actions=True)
+        ag.memory.sample = (lambda b=b: b)
+        loss = ag.train()
+        np.testing.assert_allclose(loss, z[f"step{step}/loss"], rtol=1e-5)
+    _cmp_sd(ag.policy_local, z, "after1/")
+    st = (z["act/state_self"].tolist(), z["act/state_obj"].tolist())
+    assert ag.act_dqn(st, eps=0.0) == int(z["act/action"])

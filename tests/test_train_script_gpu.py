@@ -25,6 +25,7 @@ CFG = {
     ("AC-IQN", ["actor_network_params.pth", "actor_constructor_params.json", "critic_network_params.pth",
                 "critic_constructor_params.json"]),
     ("IQN", ["network_params.pth", "constructor_params.json"]),
+    ("DQN", ["network_params.pth", "constructor_params.json"]),   # BASELINE config 1
 ])
 def test_train_rl_agents_cli(tmp_path, agent_type, files):
     from distributional_rl_decision_and_control_amd.scripts import train_RL_agents as cli
@@ -43,4 +44,4 @@ def test_train_rl_agents_cli(tmp_path, agent_type, files):
     from distributional_rl_decision_and_control_amd.agent import Agent
     ag = Agent(agent_type=agent_type)
     ag.load_model(d)
-    assert next(iter(ag.policy_local.parameters() if agent_type == "IQN" else ag.policy_local.actor.parameters())).is_cuda
+    assert next(iter(ag.policy_local.parameters() if agent_type != "AC-IQN" else ag.policy_local.actor.parameters())).is_cuda

@@ -778,9 +778,38 @@ def capture_rainbow():
     print("rainbow keys:", len(out))
 
 
+def capture_dqn():
+    """F8: Agent.train_DQN (agent.py:518-545) x 2 steps and act_dqn's Q values (agent.py:271-287)."""
+    out = {}
+    trans = collect_transitions(300, seed=6, discrete=True)
+    rs = np.random.RandomState(61)
+    agent = ref_agent_mod.Agent(device="cpu", seed=100, agent_type="DQN")
+    out.update(sd_arrays("init/", agent.policy_local))
+    for step in range(2):
+        idx = rs.choice(len(trans), 64, replace=False)
+        batch = make_batch(agent, trans, idx)
+        out.update(batch_arrays(f"step{step}/", *batch, 64))
+        agent.memory.sample = (lambda b=batch: b)
+        with ClipRecorder() as cr:
+            loss = agent.train_DQN()
+        out[f"step{step}/loss"] = np.float64(loss)
+        out[f"step{step}/grad_norms"] = np.array(cr.norms)
+    out.update(sd_arrays("after1/", agent.policy_local))
+    st = trans[7][0]
+    a = agent.act_dqn(st, eps=0.0)
+    with torch.no_grad():
+        q = agent.policy_local(agent.state_to_tensor(agent.memory.state_batch([st]))).numpy()
+    out["act/state_self"] = np.array(st[0], dtype=np.float64)
+    out["act/state_obj"] = np.array(st[1], dtype=np.float64).reshape(-1, 5)
+    out["act/action"] = np.int64(a)
+    out["act/q"] = np.asarray(q)
+    np.savez_compressed(os.path.join(OUT, "learn_dqn.npz"), **out)
+    print("dqn keys:", len(out))
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
-    what = sys.argv[1:] or ["dynamics", "traces", "reset", "ac_iqn", "iqn", "rainbow"]
+    what = sys.argv[1:] or ["dynamics", "traces", "reset", "ac_iqn", "iqn", "rainbow", "dqn"]
     torch.set_num_threads(1)
     for w in what:
         globals()["capture_" + w]()
