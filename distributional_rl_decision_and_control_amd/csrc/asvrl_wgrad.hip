@@ -201,8 +201,8 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_vec_kernel(const float* __re
 }
 
 // Partial reductions: a block covers 64 outputs; its kSumWaves waves take groups
-// k = kSumWaves u + wave with two independent accumulators each, and the wave sums are folded by
-// a fixed tree (deterministic, and the same order in every reduction launch).
+// k = kSumWaves u + wave with kSumAcc independent accumulators each, and the wave sums are folded
+// by a fixed tree (deterministic, and the same order in every reduction launch).
 #ifndef ASVRL_SUM_WAVES
 #define ASVRL_SUM_WAVES 8
 #endif
@@ -217,20 +217,39 @@ __device__ __forceinline__ float tree_at(float (*red)[64], int lane, int base) {
 }
 __device__ __forceinline__ float sum_tree(float (*red)[64], int lane) { return tree_at<kSumWaves>(red, lane, 0); }
 
+// A wave's share of the groups, k = wv + kSumWaves u, into kSumAcc accumulators (u mod kSumAcc:
+// kSumAcc independent loads in flight per lane) folded by a fixed pairwise tree.
+#ifndef ASVRL_SUM_ACC
+#define ASVRL_SUM_ACC 8
+#endif
+constexpr int kSumAcc = ASVRL_SUM_ACC;
+static_assert(kSumAcc >= 1 && (kSumAcc & (kSumAcc - 1)) == 0, "power-of-two accumulators");
+template <int W>
+__device__ __forceinline__ float acc_tree(const float* a, int base) {
+  if constexpr (W == 1) return a[base];
+  else return acc_tree<W / 2>(a, base) + acc_tree<W / 2>(a, base + W / 2);
+}
+__device__ __forceinline__ float wave_groups_sum(const float* __restrict__ p, int groups, int stride, int idx,
+                                                 int wv) {
+  float acc[kSumAcc];
+#pragma unroll
+  for (int a = 0; a < kSumAcc; ++a) acc[a] = 0.f;
+  int k = wv;
+  for (; k + (kSumAcc - 1) * kSumWaves < groups; k += kSumAcc * kSumWaves) {
+#pragma unroll
+    for (int a = 0; a < kSumAcc; ++a) acc[a] += p[static_cast<int64_t>(k + a * kSumWaves) * stride + idx];
+  }
+#pragma unroll
+  for (int a = 0; a < kSumAcc; ++a)
+    if (k + a * kSumWaves < groups) acc[a] += p[static_cast<int64_t>(k + a * kSumWaves) * stride + idx];
+  return acc_tree<kSumAcc>(acc, 0);
+}
+
 // Fixed-order sum over the groups of partial[k * stride + idx] for this thread's lane. Every
 // thread of the block must call it (it synchronises) and receives the same sum for its lane.
 __device__ __forceinline__ float group_sum(const float* __restrict__ p, int groups, int stride, int idx, bool valid,
                                            int wv, int lane, float (*red)[64]) {
-  float s0 = 0.f, s1 = 0.f;
-  if (valid) {
-    int k = wv;
-    for (; k + kSumWaves < groups; k += 2 * kSumWaves) {
-      s0 += p[static_cast<int64_t>(k) * stride + idx];
-      s1 += p[static_cast<int64_t>(k + kSumWaves) * stride + idx];
-    }
-    if (k < groups) s0 += p[static_cast<int64_t>(k) * stride + idx];
-  }
-  red[wv][lane] = s0 + s1;
+  red[wv][lane] = valid ? wave_groups_sum(p, groups, stride, idx, wv) : 0.f;
   __syncthreads();
   const float s = sum_tree(red, lane);
   __syncthreads();
@@ -263,23 +282,8 @@ struct SumSegs {
 __device__ __forceinline__ void group_sum5(const float* __restrict__ p, int groups, int stride, const int* idx,
                                            const bool* valid, int wv, int lane, float (*red5)[kSumWaves][64],
                                            float* out) {
-  float s0[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, s1[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-  int k = wv;
-  for (; k + kSumWaves < groups; k += 2 * kSumWaves) {
 #pragma unroll
-    for (int o = 0; o < 5; ++o)
-      if (valid[o]) {
-        s0[o] += p[static_cast<int64_t>(k) * stride + idx[o]];
-        s1[o] += p[static_cast<int64_t>(k + kSumWaves) * stride + idx[o]];
-      }
-  }
-  if (k < groups) {
-#pragma unroll
-    for (int o = 0; o < 5; ++o)
-      if (valid[o]) s0[o] += p[static_cast<int64_t>(k) * stride + idx[o]];
-  }
-#pragma unroll
-  for (int o = 0; o < 5; ++o) red5[o][wv][lane] = s0[o] + s1[o];
+  for (int o = 0; o < 5; ++o) red5[o][wv][lane] = valid[o] ? wave_groups_sum(p, groups, stride, idx[o], wv) : 0.f;
   __syncthreads();
 #pragma unroll
   for (int o = 0; o < 5; ++o) out[o] = sum_tree(red5[o], lane);
@@ -310,65 +314,101 @@ __device__ __forceinline__ bool fold_index(int t, int o, int boff, int& idx) {
   return t < kFoldObjF;
 }
 
-// Grid (blocks, segments); block x of a segment owns outputs [64x, 64x + 64) (a scalar segment:
-// block 0 alone, all threads). With sq_blocks, every working block also writes the sum of the
-// squares of the outputs it wrote (segments with norm = 1) to its slot, for asvrl_adam_step.
+// Outputs per lane of partial_sums_kernel: a block owns kSumSpan consecutive outputs, lane l the
+// outputs base + 64 j + l. Every output is summed in group_sum's order. More than 1 measured slower
+// (fewer waves in flight: 22.8 us at 1, 38.7 at 2, 51.4 at 4 for the critic's reduction).
+#ifndef ASVRL_SUM_OPL
+#define ASVRL_SUM_OPL 1
+#endif
+constexpr int kSumOpl = ASVRL_SUM_OPL, kSumSpan = 64 * kSumOpl;
+
+__device__ __forceinline__ void group_sum_n(const float* __restrict__ p, int groups, int stride, const int* idx,
+                                            const bool* valid, int wv, int lane, float (*red)[kSumWaves][64],
+                                            float* out) {
+#pragma unroll
+  for (int j = 0; j < kSumOpl; ++j) red[j][wv][lane] = valid[j] ? wave_groups_sum(p, groups, stride, idx[j], wv) : 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kSumOpl; ++j) out[j] = sum_tree(red[j], lane);
+}
+
+// Grid (blocks, segments); block x of a segment owns outputs [kSumSpan x, kSumSpan (x + 1)) (a
+// scalar segment: block 0 alone, all threads). With sq_blocks, every working block also writes the
+// sum of the squares of the outputs it wrote (segments with norm = 1) to its slot, for
+// asvrl_adam_step.
 __global__ __launch_bounds__(kSumThreads) void partial_sums_kernel(SumSegs t, double* sq_blocks, float* step) {
   const AsvPartialSum& g = t.seg[blockIdx.y];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  __shared__ float red[kSumWaves][64];
+  __shared__ float red[kSumOpl][kSumWaves][64];
   double sq = 0.0;
-  if (g.nw + g.nb == 1) {   // scalar over many groups: the whole block, fixed order
+  const int n = g.nw + g.nb;
+  if (n == 1) {   // scalar over many groups: the whole block, fixed order
     if (blockIdx.x == 0) {
       float acc = 0.f;
       for (int k = threadIdx.x; k < g.groups; k += kSumThreads) acc += g.partial[k];
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, kWave);
-      if (lane == 0) red[wv][0] = acc;
+      if (lane == 0) red[0][wv][0] = acc;
       __syncthreads();
       if (threadIdx.x == 0) {
-        const float s = sum_tree(red, 0);
+        const float s = sum_tree(red[0], 0);
         float* o = g.nw == 1 ? g.dw : g.db;
         *o = g.accumulate ? *o + s : s;
         if (g.norm) sq += static_cast<double>(*o) * *o;
       }
     }
-  } else if (blockIdx.x * 64 < g.nw + g.nb) {   // block-uniform
-    const int i = blockIdx.x * 64 + lane;
-    const int n = g.nw + g.nb;
+  } else if (static_cast<int>(blockIdx.x) * kSumSpan < n) {   // block-uniform
+    const int base = blockIdx.x * kSumSpan + lane;
     const int stride = g.stride != 0 ? g.stride : n;
     const int boff = g.boff != 0 ? g.boff : g.nw;
-    float s;
+    float s[kSumOpl];
     if (g.mode == ASVRL_SUM_FOLD_ENCODERS) {
       __shared__ float red5[kFoldObjN][kSumWaves][64];
-      int idx[kFoldObjN];
-      bool v[kFoldObjN];
-      float so[kFoldObjN];
+      for (int j = 0; j < kSumOpl; ++j) {
+        const int i = base + 64 * j;
+        int idx[kFoldObjN];
+        bool v[kFoldObjN];
+        float so[kFoldObjN];
 #pragma unroll
-      for (int o = 0; o < kFoldObjN; ++o) {
-        idx[o] = 0;
-        v[o] = i < n && fold_index(i, o, boff, idx[o]);
+        for (int o = 0; o < kFoldObjN; ++o) {
+          idx[o] = 0;
+          v[o] = i < n && fold_index(i, o, boff, idx[o]);
+        }
+        group_sum5(g.partial, g.groups, stride, idx, v, wv, lane, red5, so);
+        __syncthreads();   // red5 is rewritten by the next chunk
+        s[j] = 0.f;   // the copies in object order (asvrl_encoder_fold)
+#pragma unroll
+        for (int o = 0; o < kFoldObjN; ++o)
+          if (v[o]) s[j] += so[o];
       }
-      group_sum5(g.partial, g.groups, stride, idx, v, wv, lane, red5, so);
-      s = 0.f;   // the copies in object order (asvrl_encoder_fold)
-#pragma unroll
-      for (int o = 0; o < kFoldObjN; ++o)
-        if (v[o]) s += so[o];
     } else {
-      const int idx = i < g.nw ? i : boff + (i - g.nw);
-      s = group_sum(g.partial, g.groups, stride, idx, i < n, wv, lane, red);
+      int idx[kSumOpl];
+      bool v[kSumOpl];
+#pragma unroll
+      for (int j = 0; j < kSumOpl; ++j) {
+        const int i = base + 64 * j;
+        v[j] = i < n;
+        idx[j] = i < g.nw ? i : boff + (i - g.nw);
+      }
+      group_sum_n(g.partial, g.groups, stride, idx, v, wv, lane, red, s);
     }
-    if (wv == 0 && i < n && !(i >= g.nw && g.db == nullptr)) {
-      float* o = i < g.nw ? g.dw + i : g.db + (i - g.nw);
-      const float out = g.accumulate ? *o + s : s;
-      *o = out;
-      if (g.norm) sq = static_cast<double>(out) * out;
+    if (wv == 0) {
+#pragma unroll
+      for (int j = 0; j < kSumOpl; ++j) {
+        const int i = base + 64 * j;
+        if (i < n && !(i >= g.nw && g.db == nullptr)) {
+          float* o = i < g.nw ? g.dw + i : g.db + (i - g.nw);
+          const float out = g.accumulate ? *o + s[j] : s[j];
+          *o = out;
+          if (g.norm) sq += static_cast<double>(out) * out;
+        }
+      }
     }
   }
   if (sq_blocks == nullptr) return;
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) step[0] += 1.f;   // read by the next launch
   // ---- squared norm: this working block's sum (wave 0 holds the outputs) into its own slot
-  const int nb = (g.nw + g.nb == 1) ? 1 : (g.nw + g.nb + 63) / 64;
+  const int nb = n == 1 ? 1 : (n + kSumSpan - 1) / kSumSpan;
   if (static_cast<int>(blockIdx.x) >= nb || wv != 0) return;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) sq += __shfl_xor(sq, off, kWave);
@@ -378,7 +418,7 @@ __global__ __launch_bounds__(kSumThreads) void partial_sums_kernel(SumSegs t, do
 int sum_grid_x(const AsvPartialSum* segs, int nseg) {
   int maxn = 0;
   for (int k = 0; k < nseg; ++k) maxn = std::max(maxn, segs[k].nw + segs[k].nb);
-  return (maxn + 63) / 64;
+  return (maxn + kSumSpan - 1) / kSumSpan;
 }
 
 // norm slots: one per working block of each segment, segments in order
@@ -387,7 +427,7 @@ int norm_slots(const AsvPartialSum* segs, int nseg, int* slot0) {
   for (int k = 0; k < nseg; ++k) {
     if (slot0 != nullptr) slot0[k] = n;
     const int w = segs[k].nw + segs[k].nb;
-    n += w == 1 ? 1 : (w + 63) / 64;
+    n += w == 1 ? 1 : (w + kSumSpan - 1) / kSumSpan;
   }
   return n;
 }
@@ -408,10 +448,19 @@ int launch_partial_sums(const AsvPartialSum* segs, int nseg, double* sq_blocks, 
   return check_launch("asvrl_partial_sums");
 }
 
+// At least kMinChunks chunks per group: a small batch (the actor's B rows) would otherwise give a
+// group per chunk and partials several times the size of the activations they reduce.
+#ifndef ASVRL_WGRAD_MIN_CHUNKS
+#define ASVRL_WGRAD_MIN_CHUNKS 4
+#endif
+constexpr int kMinChunks = ASVRL_WGRAD_MIN_CHUNKS;
+
 int wgrad_groups(int R, int M, int K) {
   const int chunks = R / kRC;
   int cap = (1 << 22) / (M * K);
   cap = cap < 64 ? 64 : (cap > kMaxGroups ? kMaxGroups : cap);
+  const int by_rows = (chunks + kMinChunks - 1) / kMinChunks;
+  if (by_rows < cap) cap = by_rows;
   int groups = chunks < cap ? chunks : cap;
   if (groups < 1) return 0;
   const int per = (chunks + groups - 1) / groups;
