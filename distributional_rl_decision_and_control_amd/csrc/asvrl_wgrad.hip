@@ -27,6 +27,11 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kWgThreads = 256;
 constexpr int kRC = 32;           // rows per staged chunk (2 MFMA k-steps)
 constexpr int kMaxGroups = 256;
+#ifndef ASVRL_WGRAD_PF
+#define ASVRL_WGRAD_PF 4
+#endif
+constexpr int kPF = ASVRL_WGRAD_PF;   // staged chunks in flight per thread
+static_assert(kPF >= 1 && kPF <= 4, "1..4 chunks in flight");
 
 __host__ __device__ constexpr int lds_stride(int cols) {  // bytes, == 64 (mod 256)
   return ((2 * cols - 64 + 255) / 256) * 256 + 64;
@@ -92,7 +97,9 @@ __global__ __launch_bounds__(W * 64) void wgrad_kernel(const __bf16* __restrict_
   const int xc8 = t % (K / 8), xr = t / (K / 8);
   constexpr int ZRS = kT * 8 / M, XRS = kT * 8 / K;   // row step between a thread's chunks
   const bool zact = t < S::NCZ, xact = t < S::NCX;                     // staging threads
-  u32x4 rz[S::CZ], rx[S::CX];
+  // PF chunks in flight per thread (registers), chunk c + PF loaded while chunk c is consumed;
+  // the chunk order and the MFMA order are those of PF = 1 (bit-identical results)
+  u32x4 rz[kPF][S::CZ], rx[kPF][S::CX];
   float bacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   f32x16 acc[S::NMW * S::NKW];
 #pragma unroll
@@ -101,41 +108,50 @@ __global__ __launch_bounds__(W * 64) void wgrad_kernel(const __bf16* __restrict_
   const int kb0 = S::kWide ? 0 : (w * S::NBW) % S::NKB;
 
   if (c_beg < c_end) {
-    if (zact) load_rows<S::CZ, ZRS>(rz, dz, ldz, static_cast<int64_t>(c_beg) * kRC + zr, zc8);
-    if (xact) load_rows<S::CX, XRS>(rx, x, ldx, static_cast<int64_t>(c_beg) * kRC + xr, xc8);
+#pragma unroll
+    for (int b = 0; b < kPF; ++b) {   // chunk indices past the group's end reload its last chunk
+      const int64_t cb = min(c_beg + b, c_end - 1);
+      if (zact) load_rows<S::CZ, ZRS>(rz[b], dz, ldz, cb * kRC + zr, zc8);
+      if (xact) load_rows<S::CX, XRS>(rx[b], x, ldx, cb * kRC + xr, xc8);
+    }
   }
-  for (int c = c_beg; c < c_end; ++c) {
-    if (zact) {
+  for (int c0 = c_beg; c0 < c_end; c0 += kPF) {
 #pragma unroll
-      for (int i = 0; i < S::CZ; ++i) {
-        *reinterpret_cast<u32x4*>(lz + (zr + i * ZRS) * S::SZ + zc8 * 16) = rz[i];
-        const bf16x8 v = __builtin_bit_cast(bf16x8, rz[i]);
+    for (int b = 0; b < kPF; ++b) {
+      const int c = c0 + b;
+      if (c >= c_end) break;
+      if (zact) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) bacc[j] += static_cast<float>(v[j]);
+        for (int i = 0; i < S::CZ; ++i) {
+          *reinterpret_cast<u32x4*>(lz + (zr + i * ZRS) * S::SZ + zc8 * 16) = rz[b][i];
+          const bf16x8 v = __builtin_bit_cast(bf16x8, rz[b][i]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) bacc[j] += static_cast<float>(v[j]);
+        }
       }
+      if (xact) {
+#pragma unroll
+        for (int i = 0; i < S::CX; ++i) *reinterpret_cast<u32x4*>(lx + (xr + i * XRS) * S::SX + xc8 * 16) = rx[b][i];
+      }
+      __syncthreads();
+      if (c + kPF < c_end) {   // prefetch under the MFMAs
+        if (zact) load_rows<S::CZ, ZRS>(rz[b], dz, ldz, static_cast<int64_t>(c + kPF) * kRC + zr, zc8);
+        if (xact) load_rows<S::CX, XRS>(rx[b], x, ldx, static_cast<int64_t>(c + kPF) * kRC + xr, xc8);
+      }
+#pragma unroll
+      for (int ks = 0; ks < kRC / 16; ++ks) {
+        bf16x8 fa[S::NMW], fb[S::NKW];
+#pragma unroll
+        for (int i = 0; i < S::NMW; ++i) fa[i] = frag_tr(lz, S::SZ, ks * 16, (mb0 + i) * 32, lane);
+#pragma unroll
+        for (int j = 0; j < S::NKW; ++j) fb[j] = frag_tr(lx, S::SX, ks * 16, (kb0 + j) * 32, lane);
+#pragma unroll
+        for (int i = 0; i < S::NMW; ++i)
+#pragma unroll
+          for (int j = 0; j < S::NKW; ++j) acc[i * S::NKW + j] = mfma(fa[i], fb[j], acc[i * S::NKW + j]);
+      }
+      __syncthreads();
     }
-    if (xact) {
-#pragma unroll
-      for (int i = 0; i < S::CX; ++i) *reinterpret_cast<u32x4*>(lx + (xr + i * XRS) * S::SX + xc8 * 16) = rx[i];
-    }
-    __syncthreads();
-    if (c + 1 < c_end) {   // prefetch under the MFMAs
-      if (zact) load_rows<S::CZ, ZRS>(rz, dz, ldz, static_cast<int64_t>(c + 1) * kRC + zr, zc8);
-      if (xact) load_rows<S::CX, XRS>(rx, x, ldx, static_cast<int64_t>(c + 1) * kRC + xr, xc8);
-    }
-#pragma unroll
-    for (int ks = 0; ks < kRC / 16; ++ks) {
-      bf16x8 fa[S::NMW], fb[S::NKW];
-#pragma unroll
-      for (int i = 0; i < S::NMW; ++i) fa[i] = frag_tr(lz, S::SZ, ks * 16, (mb0 + i) * 32, lane);
-#pragma unroll
-      for (int j = 0; j < S::NKW; ++j) fb[j] = frag_tr(lx, S::SX, ks * 16, (kb0 + j) * 32, lane);
-#pragma unroll
-      for (int i = 0; i < S::NMW; ++i)
-#pragma unroll
-        for (int j = 0; j < S::NKW; ++j) acc[i * S::NKW + j] = mfma(fa[i], fb[j], acc[i * S::NKW + j]);
-    }
-    __syncthreads();
   }
 
   // partial dW block (mb, kb): lane l holds column l&31, rows (reg&3) + 8(reg>>2) + 4h
@@ -455,9 +471,13 @@ int launch_partial_sums(const AsvPartialSum* segs, int nseg, double* sq_blocks, 
 #endif
 constexpr int kMinChunks = ASVRL_WGRAD_MIN_CHUNKS;
 
+// partial traffic is about groups * M * K floats: 2^ASVRL_WGRAD_CAP_LOG2 floats per layer at most
+#ifndef ASVRL_WGRAD_CAP_LOG2
+#define ASVRL_WGRAD_CAP_LOG2 23
+#endif
 int wgrad_groups(int R, int M, int K) {
   const int chunks = R / kRC;
-  int cap = (1 << 22) / (M * K);
+  int cap = (1 << ASVRL_WGRAD_CAP_LOG2) / (M * K);
   cap = cap < 64 ? 64 : (cap > kMaxGroups ? kMaxGroups : cap);
   const int by_rows = (chunks + kMinChunks - 1) / kMinChunks;
   if (by_rows < cap) cap = by_rows;
@@ -477,7 +497,7 @@ int vec_groups(int R) {
 template <int M, int K, int W = (M * K >= 8192 ? 8 : 4)>
 int launch_wgrad(const __bf16* dz, int64_t ldz, const __bf16* x, int64_t ldx, int R, float* work, hipStream_t st,
                  int& groups) {
-  // partial traffic is groups * M * K floats: capped near 16 MB for the large layers
+  // partial traffic is groups * M * K floats: capped near 32 MB for the large layers
   const int chunks = R / kRC;
   groups = wgrad_groups(R, M, K);
   const int per = (chunks + groups - 1) / groups;

@@ -133,7 +133,7 @@ class FusedIQNState:
         self.q_next = torch.empty(B * N, **f)
         self.dzF = torch.empty(B, 256, **bf)
         self.dz_out = torch.empty(B * N, _abi.IQN_MAX_ACTIONS, **bf)
-        self.arena = PartialArena(16 << 20, dev)
+        self.arena = PartialArena(32 << 20, dev)
         self.loss = torch.zeros(1, **f)
         self.tile_loss = torch.zeros(B * N // 32, **f)
         self.side = SideStreams(dev, 2)

@@ -96,7 +96,7 @@ class FusedACIQNState:
         self.q_pi = torch.empty(B * N, **f)
         self.dzF = torch.empty(B, 256, **bf)
         self.dzG = torch.empty(B, 128, **f)
-        self.arena = PartialArena(16 << 20, dev)
+        self.arena = PartialArena(32 << 20, dev)
         self.losses = torch.zeros(2, **f)   # critic, actor loss (summed from per-tile partials)
         self.tile_loss = torch.zeros(2, B * N // 32, **f)
         self.side = SideStreams(dev, 3)   # 0, 1: gradient reductions / actor forward; 2: next batch
