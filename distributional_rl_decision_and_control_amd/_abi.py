@@ -11,7 +11,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ASVRL_LIB", os.path.join(HERE, "lib", "libasvrl.so"))  # override: A/B variants
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
 OBS_DIM = 40   # self 7 | objects 25 | mask 5 | pad 3
@@ -119,6 +119,15 @@ MAX_SUM_SEGS = 8
 SUM_PLAIN, SUM_FOLD_ENCODERS = 0, 1
 
 
+MAX_WGRAD_SEGS = 8
+WGRAD_MFMA, WGRAD_VEC, WGRAD_SMALL = 0, 1, 2
+
+
+class AsvWgradSeg(C.Structure):
+    _fields_ = [("dz", _VP), ("ldz", _I64), ("x", _VP), ("ldx", _I64), ("R", _I32), ("M", _I32), ("K", _I32),
+                ("kind", _I32), ("partial", _VP), ("partial_floats", _I64)]
+
+
 class AsvPartialSum(C.Structure):
     _fields_ = [("partial", _VP), ("dw", _VP), ("db", _VP), ("groups", _I32), ("nw", _I32), ("nb", _I32),
                 ("accumulate", _I32), ("stride", _I32), ("boff", _I32), ("mode", _I32), ("norm", _I32)]
@@ -205,6 +214,7 @@ EXPORTS = [
     ("asvrl_linear_wgrad_groups", _I32, [_I32, _I32, _I32]),
     ("asvrl_linear_wgrad_vec_groups", _I32, [_I32]),
     ("asvrl_linear_wgrad_partial", C.c_int, [_VP, _I64, _VP, _I64, _I32, _I32, _I32, _VP, _I64, _VP, _VP]),
+    ("asvrl_linear_wgrad_multi", C.c_int, [_VP, _I32, _VP, _VP]),
     ("asvrl_linear_wgrad_vec_partial", C.c_int, [_VP, _I64, _VP, _I64, _I32, _I32, _VP, _I64, _VP, _VP]),
     ("asvrl_small_wgrad_partial", C.c_int, [_VP, _I64, _VP, _I64, _I32, _I32, _I32, _VP, _I64, _VP, _VP]),
     ("asvrl_partial_sums", C.c_int, [_VP, _I32, _VP]),

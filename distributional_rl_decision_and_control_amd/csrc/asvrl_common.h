@@ -150,4 +150,41 @@ struct StreamF {
   }
 };
 
+// Small-layer weight gradient (f32 dZ, K <= 4 inputs; the action encoder): partial `blk` of 32
+// rows, dw[m][k] and db[m] into partial[blk][M*K + M]. Threads 0..255 work, every thread of the
+// workgroup must call it (it synchronises); red: 256 x 5 floats of LDS.
+constexpr int kSwRows = 32;
+__device__ __forceinline__ void small_wgrad_body(const float* __restrict__ dz, int64_t ldz, const float* __restrict__ x,
+                                                 int64_t ldx, int R, int M, int K, float* __restrict__ partial,
+                                                 int blk, float (*red)[5]) {
+  const int t = threadIdx.x;
+  const bool act = t < 256;
+  const int per = 256 / M;   // rows in flight (M divides 256)
+  const int m = t % M, rq = t / M;
+  float sw[4] = {0.f, 0.f, 0.f, 0.f}, sb = 0.f;
+  const int r0 = blk * kSwRows, r1 = min(R, r0 + kSwRows);
+  if (act) {
+    for (int r = r0 + rq; r < r1; r += per) {
+      const float d = dz[static_cast<int64_t>(r) * ldz + m];
+      sb += d;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k < K) sw[k] += d * x[static_cast<int64_t>(r) * ldx + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red[t][k] = sw[k];
+    red[t][4] = sb;
+  }
+  __syncthreads();
+  if (t < M) {
+    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int u = t; u < 256; u += M)
+#pragma unroll
+      for (int k = 0; k < 5; ++k) acc[k] += red[u][k];
+    float* p = partial + static_cast<int64_t>(blk) * (M * K + M);
+    for (int k = 0; k < K; ++k) p[t * K + k] = acc[k];
+    p[M * K + t] = acc[4];
+  }
+}
+
 }  // namespace asvrl

@@ -472,36 +472,11 @@ __global__ __launch_bounds__(256) void enc_fold_kernel(const float* __restrict__
 // dW[m][k] = sum_r dz[r][m] x[r][k], db[m] = sum_r dz[r][m] for a small f32 input (K <= 4): the
 // critic action_encoder (2 -> 128). Block b handles rows [kSwRows*b, +kSwRows); thread t owns
 // feature t % M and every (256/M)-th row, four rows in flight; partials [blk][M*K+M].
-constexpr int kSwRows = 32;
 __global__ __launch_bounds__(256) void small_wgrad_kernel(const float* __restrict__ dz, int64_t ldz,
                                                            const float* __restrict__ x, int64_t ldx, int R, int M,
                                                            int K, float* __restrict__ partial) {
-  const int t = threadIdx.x;
-  const int per = 256 / M;   // rows in flight (M divides 256)
-  const int m = t % M, rq = t / M;
-  float sw[4] = {0.f, 0.f, 0.f, 0.f}, sb = 0.f;
-  const int r0 = blockIdx.x * kSwRows, r1 = min(R, r0 + kSwRows);
-  for (int r = r0 + rq; r < r1; r += per) {
-    const float d = dz[static_cast<int64_t>(r) * ldz + m];
-    sb += d;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (k < K) sw[k] += d * x[static_cast<int64_t>(r) * ldx + k];
-  }
   __shared__ float red[256][5];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) red[t][k] = sw[k];
-  red[t][4] = sb;
-  __syncthreads();
-  if (t < M) {
-    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int u = t; u < 256; u += M)
-#pragma unroll
-      for (int k = 0; k < 5; ++k) acc[k] += red[u][k];
-    float* p = partial + static_cast<int64_t>(blockIdx.x) * (M * K + M);
-    for (int k = 0; k < K; ++k) p[t * K + k] = acc[k];
-    p[M * K + t] = acc[4];
-  }
+  small_wgrad_body(dz, ldz, x, ldx, R, M, K, partial, blockIdx.x, red);
 }
 
 }  // namespace

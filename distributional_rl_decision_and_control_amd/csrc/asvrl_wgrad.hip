@@ -28,7 +28,7 @@ constexpr int kWgThreads = 256;
 constexpr int kRC = 32;           // rows per staged chunk (2 MFMA k-steps)
 constexpr int kMaxGroups = 256;
 #ifndef ASVRL_WGRAD_PF
-#define ASVRL_WGRAD_PF 4
+#define ASVRL_WGRAD_PF 1
 #endif
 constexpr int kPF = ASVRL_WGRAD_PF;   // staged chunks in flight per thread
 static_assert(kPF >= 1 && kPF <= 4, "1..4 chunks in flight");
@@ -79,17 +79,16 @@ struct Shape {
   static_assert(NCX % T == 0 || T % NCX == 0, "X chunks must tile the block");
 };
 
+// One workgroup's share (`group`) of dW / db: chunks [group * per, (group + 1) * per) into its
+// (M*K + M)-float partial. lz / lx / lbias: the workgroup's LDS (kRC*SZ, kRC*SX bytes, T x 8 floats).
 template <int M, int K, int W>
-__global__ __launch_bounds__(W * 64) void wgrad_kernel(const __bf16* __restrict__ dz, int64_t ldz,
-                                                        const __bf16* __restrict__ x, int64_t ldx, int chunks,
-                                                        int chunks_per_group, float* __restrict__ partial) {
+__device__ __forceinline__ void wgrad_body(const __bf16* __restrict__ dz, int64_t ldz, const __bf16* __restrict__ x,
+                                           int64_t ldx, int chunks, int chunks_per_group, float* __restrict__ partial,
+                                           int group, char* lz, char* lx, float (*lbias)[8]) {
   using S = Shape<M, K, W>;
   constexpr int kT = S::T;
-  __shared__ __attribute__((aligned(16))) char lz[kRC * S::SZ];
-  __shared__ __attribute__((aligned(16))) char lx[kRC * S::SX];
-  __shared__ float lbias[kT][8];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int c_beg = blockIdx.x * chunks_per_group;
+  const int c_beg = group * chunks_per_group;
   const int c_end = min(chunks, c_beg + chunks_per_group);
 
   // thread t always stages column chunk t % (M/8) (resp. K/8), rows t / (M/8) + i * (256*8/M)
@@ -155,7 +154,7 @@ __global__ __launch_bounds__(W * 64) void wgrad_kernel(const __bf16* __restrict_
   }
 
   // partial dW block (mb, kb): lane l holds column l&31, rows (reg&3) + 8(reg>>2) + 4h
-  float* pw = partial + static_cast<int64_t>(blockIdx.x) * (M * K + M);
+  float* pw = partial + static_cast<int64_t>(group) * (M * K + M);
   const int h = lane >> 5, col = lane & 31;
 #pragma unroll
   for (int i = 0; i < S::NMW; ++i)
@@ -180,15 +179,27 @@ __global__ __launch_bounds__(W * 64) void wgrad_kernel(const __bf16* __restrict_
   }
 }
 
+template <int M, int K, int W>
+__global__ __launch_bounds__(W * 64) void wgrad_kernel(const __bf16* __restrict__ dz, int64_t ldz,
+                                                        const __bf16* __restrict__ x, int64_t ldx, int chunks,
+                                                        int chunks_per_group, float* __restrict__ partial) {
+  using S = Shape<M, K, W>;
+  __shared__ __attribute__((aligned(16))) char lz[kRC * S::SZ];
+  __shared__ __attribute__((aligned(16))) char lx[kRC * S::SX];
+  __shared__ float lbias[S::T][8];
+  wgrad_body<M, K, W>(dz, ldz, x, ldx, chunks, chunks_per_group, partial, blockIdx.x, lz, lx, lbias);
+}
+
 // dw[k] = sum_r dq[r] * X[r][k], db = sum_r dq[r] for an output layer with one unit.
 // Thread t reads 16 bytes (8 columns) of row t / (K/8) + i * RP: RP rows in flight per block.
+// Threads 0..255 work; every thread of the workgroup must call it. sa: 256 x 9 floats of LDS.
 template <int K>
-__global__ __launch_bounds__(kWgThreads) void wgrad_vec_kernel(const float* __restrict__ dq, int64_t ldq,
-                                                                const __bf16* __restrict__ x, int64_t ldx, int R,
-                                                                int rows_per_group, float* __restrict__ partial) {
+__device__ __forceinline__ void wgrad_vec_body(const float* __restrict__ dq, int64_t ldq, const __bf16* __restrict__ x,
+                                               int64_t ldx, int R, int rows_per_group, float* __restrict__ partial,
+                                               int group, float (*sa)[9]) {
   constexpr int C8 = K / 8, RP = kWgThreads / C8;
   const int t = threadIdx.x, c8 = t % C8, rr = t / C8;
-  const int r_beg = blockIdx.x * rows_per_group, r_end = min(R, r_beg + rows_per_group);
+  const int r_beg = group * rows_per_group, r_end = t < kWgThreads ? min(R, r_beg + rows_per_group) : 0;
   float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float b = 0.f;
   for (int r = r_beg + rr; r < r_end; r += RP) {
@@ -198,12 +209,13 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_vec_kernel(const float* __re
     for (int j = 0; j < 8; ++j) a[j] += d * static_cast<float>(v[j]);
     b += d;
   }
-  __shared__ float sa[kWgThreads][9];
+  if (t < kWgThreads) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) sa[t][j] = a[j];
-  sa[t][8] = b;
+    for (int j = 0; j < 8; ++j) sa[t][j] = a[j];
+    sa[t][8] = b;
+  }
   __syncthreads();
-  float* pw = partial + static_cast<int64_t>(blockIdx.x) * (K + 1);
+  float* pw = partial + static_cast<int64_t>(group) * (K + 1);
   if (t < K) {   // column t = 8 * (t / 8) + t % 8 lives in threads with c8 == t / 8
     float s = 0.f;
     for (int u = t / 8; u < kWgThreads; u += C8) s += sa[u][t % 8];
@@ -213,6 +225,71 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_vec_kernel(const float* __re
     float s = 0.f;
     for (int u = 0; u < kWgThreads; u += C8) s += sa[u][8];   // c8 == 0 threads saw every row once
     pw[K] = s;
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(kWgThreads) void wgrad_vec_kernel(const float* __restrict__ dq, int64_t ldq,
+                                                                const __bf16* __restrict__ x, int64_t ldx, int R,
+                                                                int rows_per_group, float* __restrict__ partial) {
+  __shared__ float sa[kWgThreads][9];
+  wgrad_vec_body<K>(dq, ldq, x, ldx, R, rows_per_group, partial, blockIdx.x, sa);
+}
+
+// Several layers in one launch (asvrl_linear_wgrad_multi): workgroup b belongs to the segment whose
+// group range holds it and runs exactly the workgroup `b - first group` of that layer's own launch.
+// Every shape here has 8 waves; the LDS is one buffer sized for the largest.
+constexpr int kMultiW = 8;
+enum WgShape { WG_256x64 = 0, WG_128x256, WG_128x128, WG_256x32, WG_VEC128, WG_SMALL };
+struct WgSeg {
+  const void* dz;    // bf16 (MFMA shapes), f32 (WG_VEC128: dq with stride ldz; WG_SMALL)
+  const void* x;     // bf16, f32 (WG_SMALL)
+  int64_t ldz, ldx;
+  float* partial;
+  int chunks, per, shape, first;   // chunks / per: 32-row chunks (MFMA), rows (VEC), R (SMALL)
+  int M, K;                        // WG_SMALL only
+};
+struct WgMulti {
+  WgSeg s[ASVRL_MAX_WGRAD_SEGS];
+  int n;
+};
+template <int M, int K>
+constexpr int stage_bytes() { return kRC * (Shape<M, K, kMultiW>::SZ + Shape<M, K, kMultiW>::SX); }
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+constexpr int kMultiStage = cmax(cmax(stage_bytes<256, 64>(), stage_bytes<128, 256>()),
+                                 cmax(stage_bytes<128, 128>(), stage_bytes<256, 32>()));
+
+template <int M, int K>
+__device__ __forceinline__ void multi_run(const WgSeg& g, int group, char* lds, float (*lbias)[8]) {
+  using S = Shape<M, K, kMultiW>;
+  wgrad_body<M, K, kMultiW>(static_cast<const __bf16*>(g.dz), g.ldz, static_cast<const __bf16*>(g.x), g.ldx,
+                            g.chunks, g.per, g.partial, group, lds, lds + kRC * S::SZ, lbias);
+}
+
+#ifndef ASVRL_WGRAD_MULTI_WAVES
+#define ASVRL_WGRAD_MULTI_WAVES 1
+#endif
+__global__ __launch_bounds__(kMultiW * 64, ASVRL_WGRAD_MULTI_WAVES) void wgrad_multi_kernel(WgMulti t) {
+  __shared__ __attribute__((aligned(16))) char lds[kMultiStage];
+  __shared__ float lbias[kMultiW * 64][8];
+  const int b = blockIdx.x;
+  int k = 0;
+  while (k + 1 < t.n && b >= t.s[k + 1].first) ++k;
+  const WgSeg& g = t.s[k];
+  const int group = b - g.first;
+  switch (g.shape) {
+    case WG_256x64: multi_run<256, 64>(g, group, lds, lbias); break;
+    case WG_128x256: multi_run<128, 256>(g, group, lds, lbias); break;
+    case WG_128x128: multi_run<128, 128>(g, group, lds, lbias); break;
+    case WG_256x32: multi_run<256, 32>(g, group, lds, lbias); break;
+    case WG_VEC128:
+      wgrad_vec_body<128>(static_cast<const float*>(g.dz), g.ldz, static_cast<const __bf16*>(g.x), g.ldx, g.chunks,
+                          g.per, g.partial, group, reinterpret_cast<float(*)[9]>(&lbias[0][0]));
+      break;
+    default:
+      small_wgrad_body(static_cast<const float*>(g.dz), g.ldz, static_cast<const float*>(g.x), g.ldx, g.chunks, g.M,
+                       g.K, g.partial, group, reinterpret_cast<float(*)[5]>(&lbias[0][0]));
+      break;
   }
 }
 
@@ -553,6 +630,68 @@ extern "C" int asvrl_linear_wgrad_partial(const void* dz, int64_t ldz, const voi
   else ASVRL_REQUIRE(false, "asvrl_linear_wgrad: unsupported (M, K)");
   *groups_out = groups;
   return rc;
+}
+
+extern "C" int asvrl_linear_wgrad_multi(const AsvWgradSeg* segs, int32_t nseg, int32_t* groups_out, void* stream) {
+  ASVRL_REQUIRE(segs && groups_out && nseg >= 0 && nseg <= ASVRL_MAX_WGRAD_SEGS,
+                "asvrl_linear_wgrad_multi: bad segment table");
+  WgMulti t{};
+  int total = 0;
+  for (int k = 0; k < nseg; ++k) {
+    const AsvWgradSeg& a = segs[k];
+    ASVRL_REQUIRE(a.dz && a.x && a.partial, "asvrl_linear_wgrad_multi: null argument");
+    WgSeg& g = t.s[t.n];
+    g.dz = a.dz; g.x = a.x; g.ldz = a.ldz; g.ldx = a.ldx; g.partial = a.partial; g.first = total;
+    int groups = 0;
+    if (a.kind != ASVRL_WGRAD_MFMA) {
+      ASVRL_REQUIRE(a.R >= 0, "asvrl_linear_wgrad_multi: negative R");
+      if (a.kind == ASVRL_WGRAD_VEC) {   // asvrl_linear_wgrad_vec_partial: dq f32 (stride ldz), x bf16, K = 128
+        ASVRL_REQUIRE(a.M == 1 && a.K == 128 && a.ldx >= 128 && a.ldx % 8 == 0 &&
+                          reinterpret_cast<uintptr_t>(a.x) % 16 == 0,
+                      "asvrl_linear_wgrad_multi: vec segments need M = 1, K = 128, 16-byte aligned x");
+        groups = a.R > 0 ? vec_groups(a.R) : 0;
+        g.shape = WG_VEC128; g.chunks = a.R; g.per = groups ? (a.R + groups - 1) / groups : 1;
+        ASVRL_REQUIRE(a.partial_floats >= static_cast<int64_t>(groups) * (a.K + 1),
+                      "asvrl_linear_wgrad_multi: workspace too small");
+      } else {   // asvrl_small_wgrad_partial: f32 dz (R x M) and x (R x K)
+        ASVRL_REQUIRE(a.kind == ASVRL_WGRAD_SMALL, "asvrl_linear_wgrad_multi: bad kind");
+        ASVRL_REQUIRE(a.M >= 1 && a.M <= 256 && 256 % a.M == 0 && a.K >= 1 && a.K <= 4,
+                      "asvrl_linear_wgrad_multi: small segments need M | 256, K <= 4");
+        groups = (a.R + kSwRows - 1) / kSwRows;
+        g.shape = WG_SMALL; g.chunks = a.R; g.per = kSwRows; g.M = a.M; g.K = a.K;
+        ASVRL_REQUIRE(a.partial_floats >= static_cast<int64_t>(groups) * (a.M * a.K + a.M),
+                      "asvrl_linear_wgrad_multi: workspace too small");
+      }
+      groups_out[k] = groups;
+      if (groups == 0) continue;
+      ++t.n;
+      total += groups;
+      continue;
+    }
+    ASVRL_REQUIRE(a.R >= 0 && a.R % kRC == 0, "asvrl_linear_wgrad_multi: R must be a multiple of 32");
+    ASVRL_REQUIRE(a.ldz >= a.M && a.ldx >= a.K && a.ldz % 8 == 0 && a.ldx % 8 == 0,
+                  "asvrl_linear_wgrad_multi: leading dimensions must cover the rows and be multiples of 8");
+    ASVRL_REQUIRE((reinterpret_cast<uintptr_t>(a.dz) | reinterpret_cast<uintptr_t>(a.x)) % 16 == 0,
+                  "asvrl_linear_wgrad_multi: operands must be 16-byte aligned");
+    int shape;
+    if (a.M == 256 && a.K == 64) shape = WG_256x64;
+    else if (a.M == 128 && a.K == 256) shape = WG_128x256;
+    else if (a.M == 128 && a.K == 128) shape = WG_128x128;
+    else if (a.M == 256 && a.K == 32) shape = WG_256x32;
+    else ASVRL_REQUIRE(false, "asvrl_linear_wgrad_multi: (M, K) must be (256,64), (128,256), (128,128) or (256,32)");
+    groups = a.R == 0 ? 0 : wgrad_groups(a.R, a.M, a.K);
+    ASVRL_REQUIRE(a.partial_floats >= static_cast<int64_t>(groups) * (a.M * a.K + a.M),
+                  "asvrl_linear_wgrad_multi: workspace too small");
+    const int chunks = a.R / kRC;
+    g.chunks = chunks; g.per = groups ? (chunks + groups - 1) / groups : 1; g.shape = shape;
+    groups_out[k] = groups;
+    if (groups == 0) continue;   // empty layers take no workgroups (and no table slot)
+    ++t.n;
+    total += groups;
+  }
+  if (total == 0) return 0;
+  hipLaunchKernelGGL(wgrad_multi_kernel, dim3(total), dim3(kMultiW * 64), 0, as_stream(stream), t);
+  return check_launch("asvrl_linear_wgrad_multi");
 }
 
 extern "C" int asvrl_linear_wgrad(const void* dz, int64_t ldz, const void* x, int64_t ldx, int32_t R, int32_t M,

@@ -11,6 +11,7 @@ cos embedding, both hidden layers, the output layer, the quantile-Huber loss and
 backward -- in two kernel launches per critic pass, the state/action encoders and the actor
 on torch, and the trunk's weight gradients as split-K bf16 GEMMs over the saved activations.
 """
+import contextlib
 import ctypes as C
 
 import torch
@@ -225,6 +226,7 @@ class PartialArena:
         self.buf = torch.empty(int(floats), dtype=torch.float32, device=device)
         self.off = 0
         self.segs = []
+        self.pending = None   # inside batch(): MFMA weight-gradient layers waiting for one launch
         # flush(norm=...): per-workgroup squared-norm partials
         self.norm_parts = torch.zeros(_abi.MAX_SUM_SEGS * 1024, dtype=torch.float64, device=device)
         self.nparts = 0
@@ -243,13 +245,42 @@ class PartialArena:
         g.stride, g.boff, g.mode, g.norm = stride, boff, mode, int(norm)
         self.segs.append(g)
         if len(self.segs) == _abi.MAX_SUM_SEGS:
+            if self.pending is not None:   # the reduction would run before the batched launch
+                raise RuntimeError("PartialArena: too many segments inside batch()")
             self.flush()
+
+    @contextlib.contextmanager
+    def batch(self, stream=None):
+        """linear() / fold() calls inside the block queue their layers; on exit ONE
+        asvrl_linear_wgrad_multi launch writes all their partials (bit-identical to one launch
+        per layer), instead of several launches on side streams joined back."""
+        assert self.pending is None, "PartialArena.batch does not nest"
+        self.pending = []
+        try:
+            yield self
+        finally:
+            segs, self.pending = self.pending, None
+            for i in range(0, len(segs), _abi.MAX_WGRAD_SEGS):
+                chunk = segs[i:i + _abi.MAX_WGRAD_SEGS]
+                arr = (_abi.AsvWgradSeg * len(chunk))(*chunk)
+                groups = (C.c_int32 * len(chunk))()
+                _abi.check(_abi.lib().asvrl_linear_wgrad_multi(arr, len(chunk), groups, _abi.stream_ptr(stream)),
+                           "asvrl_linear_wgrad_multi")
 
     def _linear_partial(self, dz, x, stream):
         R, M = dz.shape
         K = x.shape[1]
         L = _abi.lib()
-        part = self._take(int(L.asvrl_linear_wgrad_groups(R, M, K)) * (M * K + M))
+        ngroups = int(L.asvrl_linear_wgrad_groups(R, M, K))
+        part = self._take(ngroups * (M * K + M))
+        if self.pending is not None:
+            assert dz.dtype == x.dtype == torch.bfloat16 and dz.stride(1) == 1 and x.stride(1) == 1
+            g = _abi.AsvWgradSeg()
+            g.dz, g.ldz, g.x, g.ldx = dz.data_ptr(), dz.stride(0), x.data_ptr(), x.stride(0)
+            g.R, g.M, g.K, g.partial, g.partial_floats = R, M, K, part.data_ptr(), part.numel()
+            g.kind = _abi.WGRAD_MFMA
+            self.pending.append(g)
+            return part, ngroups, M, K
         groups = C.c_int32(0)
         _abi.check(L.asvrl_linear_wgrad_partial(_abi.ptr(dz), dz.stride(0), _abi.ptr(x), x.stride(0), R, M, K,
                                                 _abi.ptr(part), part.numel(), C.byref(groups),
@@ -277,10 +308,22 @@ class PartialArena:
         self._seg(part, gs[0], None, groups, 688, 0, False, stride=M * K + M, boff=M * K,
                   mode=_abi.SUM_FOLD_ENCODERS)
 
+    def _queue(self, kind, dz, ldz, x, ldx, R, M, K, part):
+        g = _abi.AsvWgradSeg()
+        g.dz, g.ldz, g.x, g.ldx = dz.data_ptr(), ldz, x.data_ptr(), ldx
+        g.R, g.M, g.K, g.kind, g.partial, g.partial_floats = R, M, K, kind, part.data_ptr(), part.numel()
+        self.pending.append(g)
+
     def vec(self, dq, x, dw, db, accumulate=False, stream=None):
         R, K = x.shape
         L = _abi.lib()
-        part = self._take(int(L.asvrl_linear_wgrad_vec_groups(R)) * (K + 1))
+        ngroups = int(L.asvrl_linear_wgrad_vec_groups(R))
+        part = self._take(ngroups * (K + 1))
+        if self.pending is not None and K == 128:
+            assert dq.dtype == torch.float32 and x.dtype == torch.bfloat16 and x.stride(1) == 1
+            self._queue(_abi.WGRAD_VEC, dq, dq.stride(0), x, x.stride(0), R, 1, K, part)
+            self._seg(part, dw, db, ngroups, K, 1, accumulate)
+            return
         groups = C.c_int32(0)
         _abi.check(L.asvrl_linear_wgrad_vec_partial(_abi.ptr(dq), dq.stride(0), _abi.ptr(x), x.stride(0), R, K,
                                                     _abi.ptr(part), part.numel(), C.byref(groups),
@@ -304,6 +347,11 @@ class PartialArena:
         R, M = dz.shape
         K = x.shape[1]
         part = self._take(((R + 31) // 32) * (M * K + M))
+        if self.pending is not None:
+            assert dz.dtype == x.dtype == torch.float32 and dz.stride(1) == 1 and x.stride(1) == 1
+            self._queue(_abi.WGRAD_SMALL, dz, dz.stride(0), x, x.stride(0), R, M, K, part)
+            self._seg(part, dw, db, (R + 31) // 32, M * K, M, accumulate)
+            return
         groups = C.c_int32(0)
         _abi.check(_abi.lib().asvrl_small_wgrad_partial(dz.data_ptr(), dz.stride(0), x.data_ptr(), x.stride(0), R,
                                                         M, K, part.data_ptr(), part.numel(), C.byref(groups),

@@ -7,10 +7,8 @@ Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | 
     target encoders(ns, na) + trunk -> q_next            asvrl_critic_forward (encoders in the prologue)
     local encoders(s, a) + trunk forward + quantile-Huber vs r + g q_next (1-d) + backward
                                                           asvrl_critic_train (targets formed in-kernel)
-    trunk weight grads                                   asvrl_linear_wgrad_partial x3 (the output layer's
-                                                          as per-tile partials from the TRAIN kernel)
-    encoder grads (256x32 image) and action-encoder grads
-                                                          asvrl_linear_wgrad_partial + _small_wgrad_partial
+    trunk, encoder-image and action-encoder weight grads ONE asvrl_linear_wgrad_multi (the output
+                                                          layer's as per-tile partials from the TRAIN kernel)
     every .grad (encoders folded in the reduction), the loss and the global gradient norm
                                                           ONE asvrl_partial_sums_norm
     clip + Adam                                          asvrl_adam_step
@@ -21,13 +19,13 @@ Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | 
     encoders(s, a) + trunk forward + backward of -mean(q) to the action
                                                           asvrl_critic_actor_grad (dA in-kernel)
     actor backward                                       asvrl_actor_backward
-    actor weight grads                                   wgrad partials x5, one asvrl_partial_sums_norm
+    actor weight grads                                   ONE asvrl_linear_wgrad_multi, one asvrl_partial_sums_norm
     clip + Adam, re-pack actor                           asvrl_adam_step + asvrl_mlp_pack
 
 Independent launches run on side streams forked from the caller's stream and joined back
 before their results are needed (SideStreams; capturable in a HIP graph): the local encoders and
-the actor's training forward beside the target chain, and the weight-gradient reductions of
-each optimizer step on three streams. Most of these kernels fill only part of the GPU alone.
+the actor's training forward beside the target chain. The weight-gradient reductions of each
+optimizer step are one multi-layer launch (a cross-stream join in a replayed graph costs ≈10 µs).
 
 Arithmetic: bf16 MFMA operands with f32 accumulation everywhere, f32 master weights / Adam.
 """
@@ -167,15 +165,13 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
                  obs=s_rows, act=a_rows, xb=st.xb, wout_part=wout_part)
     ae = critic.action_encoder[0]
     arena.tiles(wout_part, tiles, critic.output_layer.weight.grad, critic.output_layer.bias.grad)
-    # the five weight-gradient reductions on three streams, one partial-sum launch after the join
-    with side.on(0):
+    # the five weight-gradient reductions in ONE launch, then one partial-sum launch
+    with arena.batch():
         arena.linear(bufs.dzc, bufs.cos, critic.cos_embedding.weight.grad, critic.cos_embedding.bias.grad)
-    arena.linear(bufs.dz1, bufs.h0, critic.hidden_layer.weight.grad, critic.hidden_layer.bias.grad)
-    with side.on(1):
+        arena.linear(bufs.dz1, bufs.h0, critic.hidden_layer.weight.grad, critic.hidden_layer.bias.grad)
         arena.linear(bufs.dz2, bufs.h1g, critic.hidden_layer_2.weight.grad, critic.hidden_layer_2.bias.grad)
         arena.fold(st.dzF, st.xb, critic)             # encoder image -> self/object encoder grads
         arena.small(st.dzG, a_rows, ae.weight.grad, ae.bias.grad)
-    side.join()
     arena.scalar(st.tile_loss[0], st.losses[0:1])   # the critic loss
     cgn = _reduce_and_step(arena, critic_opt, critic_grads, sync, max_norm)
     st.local_trunk.refresh()
@@ -184,18 +180,17 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
             produce()
 
     # ---- actor through the updated critic (agent.py:419-427); its forward ran on side stream 1
+    side.join(1)
     critic_actor_grad(st.local_trunk, None, None, taus[2], N, st.q_pi, w_ae=ae.weight, dA=ab.dA,
                       tile_loss=st.tile_loss[1], obs=s_rows, act=ab.a_out)
     actor_backward(st.actor, ab)
     ow, obias = actor.output_layer.weight.grad, actor.output_layer.bias.grad
-    with side.on(0):
+    with arena.batch():
         arena.linear(ab.dz2, ab.h1, actor.hidden_layer_2.weight.grad, actor.hidden_layer_2.bias.grad)
         arena.vec(ab.dout[:, 0], ab.h2, ow[0], obias[0:1])
-    arena.linear(ab.dz1, ab.h0, actor.hidden_layer.weight.grad, actor.hidden_layer.bias.grad)
-    with side.on(1):
+        arena.linear(ab.dz1, ab.h0, actor.hidden_layer.weight.grad, actor.hidden_layer.bias.grad)
         arena.vec(ab.dout[:, 1], ab.h2, ow[1], obias[1:2])
         arena.fold(ab.dz0, ab.xb, actor)
-    side.join()
     arena.scalar(st.tile_loss[1], st.losses[1:2])   # the actor loss
     agn = _reduce_and_step(arena, actor_opt, actor_grads, sync, max_norm, wait=actor_wait)
     st.actor.refresh()

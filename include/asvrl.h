@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 8
+#define ASVRL_ABI_VERSION 9
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -532,6 +532,28 @@ int32_t asvrl_linear_wgrad_groups(int32_t R, int32_t M, int32_t K);
 int asvrl_linear_wgrad_partial(const void* dz, int64_t ldz, const void* x, int64_t ldx, int32_t R, int32_t M,
                                int32_t K, float* partial, int64_t partial_floats, int32_t* groups_out,
                                void* stream);
+
+/* Several layers' partials in ONE launch (ABI v9; replaces one partial launch per layer on side
+ * streams joined back). Segment k writes groups_out[k] partials, bit-identical to its own launch
+ * (same groups, same summation order):
+ *   kind ASVRL_WGRAD_MFMA : asvrl_linear_wgrad_partial (bf16 dz, x); (M, K) in {(256, 64), (128, 256),
+ *                           (128, 128), (256, 32)};
+ *   kind ASVRL_WGRAD_VEC  : asvrl_linear_wgrad_vec_partial (dz = dq f32 with stride ldz, M = 1, K = 128);
+ *   kind ASVRL_WGRAD_SMALL: asvrl_small_wgrad_partial (f32 dz, x; M | 256, K <= 4). */
+#define ASVRL_MAX_WGRAD_SEGS 8
+#define ASVRL_WGRAD_MFMA 0
+#define ASVRL_WGRAD_VEC 1
+#define ASVRL_WGRAD_SMALL 2
+typedef struct AsvWgradSeg {
+  const void* dz;
+  int64_t ldz;
+  const void* x;
+  int64_t ldx;
+  int32_t R, M, K, kind;
+  float* partial;
+  int64_t partial_floats;
+} AsvWgradSeg;
+int asvrl_linear_wgrad_multi(const AsvWgradSeg* segs, int32_t nseg, int32_t* groups_out, void* stream);
 
 /* One output unit's version: dw[k] = sum_r dq[r*ldq] x[r][k], db = sum_r dq[r*ldq] with dq f32 and
  * x bf16 (R x K, ldx); K in {64, 128, 256}; work >= 256 * (K + 1) floats. */

@@ -232,3 +232,87 @@ def test_flush_with_norm_matches_separate_norm_pass():
     assert abs(n0.item() - n1.item()) <= 1e-6 * n1.item()
     assert n1.item() > 0.05   # the clip is active
     assert (opts[0].flat - opts[1].flat).abs().max().item() <= 1e-6
+
+
+def _partials_single(kind, dz, x, M, K):
+    """The partial buffer of one layer's own launch (asvrl_linear_wgrad_partial / _vec_ / small)."""
+    import ctypes as C
+    from distributional_rl_decision_and_control_amd import _abi
+    L, R = _abi.lib(), x.shape[0]
+    g = C.c_int32(0)
+    if kind == _abi.WGRAD_MFMA:
+        part = torch.full((int(L.asvrl_linear_wgrad_groups(R, M, K)) * (M * K + M),), float("nan"), device="cuda")
+        rc = L.asvrl_linear_wgrad_partial(dz.data_ptr(), dz.stride(0), x.data_ptr(), x.stride(0), R, M, K,
+                                          part.data_ptr(), part.numel(), C.byref(g), None)
+    elif kind == _abi.WGRAD_VEC:
+        part = torch.full((int(L.asvrl_linear_wgrad_vec_groups(R)) * (K + 1),), float("nan"), device="cuda")
+        rc = L.asvrl_linear_wgrad_vec_partial(dz.data_ptr(), dz.stride(0), x.data_ptr(), x.stride(0), R, K,
+                                              part.data_ptr(), part.numel(), C.byref(g), None)
+    else:
+        part = torch.full((((R + 31) // 32) * (M * K + M),), float("nan"), device="cuda")
+        rc = L.asvrl_small_wgrad_partial(dz.data_ptr(), dz.stride(0), x.data_ptr(), x.stride(0), R, M, K,
+                                         part.data_ptr(), part.numel(), C.byref(g), None)
+    _abi.check(rc, "single partial")
+    return part, g.value
+
+
+@pytest.mark.parametrize("R", [4096 + 96, 131072])
+def test_wgrad_multi_is_bit_identical_to_one_launch_per_layer(R):
+    """asvrl_linear_wgrad_multi (every kind and shape in one launch, as the fused updates use it)
+    writes exactly the partials of the per-layer launches, NaN-initialised buffers included."""
+    import ctypes as C
+    from distributional_rl_decision_and_control_amd import _abi
+    g = torch.Generator(device="cuda").manual_seed(7)
+    bf = lambda *s: torch.randn(*s, generator=g, device="cuda").to(torch.bfloat16)
+    wide = bf(R, 384)   # strided operands: column slices of a wider buffer
+    dq = torch.randn(R, 2, generator=g, device="cuda")
+    cases = [(_abi.WGRAD_MFMA, wide[:, 0:256], bf(R, 64), 256, 64),
+             (_abi.WGRAD_MFMA, bf(R, 128), wide[:, 128:384], 128, 256),
+             (_abi.WGRAD_MFMA, wide[:, 0:128], bf(R, 128), 128, 128),
+             (_abi.WGRAD_MFMA, bf(R, 256), bf(R, 32), 256, 32),
+             (_abi.WGRAD_VEC, dq[:, 1], bf(R, 128), 1, 128),
+             (_abi.WGRAD_SMALL, torch.randn(R, 128, generator=g, device="cuda"),
+              torch.randn(R, 2, generator=g, device="cuda"), 128, 2)]
+    segs, outs, refs = [], [], []
+    for kind, dz, x, M, K in cases:
+        ref, ng = _partials_single(kind, dz, x, M, K)
+        out = torch.full_like(ref, float("nan"))
+        s = _abi.AsvWgradSeg()
+        s.dz, s.ldz, s.x, s.ldx = dz.data_ptr(), dz.stride(0), x.data_ptr(), x.stride(0)
+        s.R, s.M, s.K, s.kind, s.partial, s.partial_floats = R, M, K, kind, out.data_ptr(), out.numel()
+        segs.append(s)
+        outs.append(out)
+        refs.append((ref, ng))
+    groups = (C.c_int32 * len(segs))()
+    _abi.check(_abi.lib().asvrl_linear_wgrad_multi((_abi.AsvWgradSeg * len(segs))(*segs), len(segs), groups, None),
+               "asvrl_linear_wgrad_multi")
+    torch.cuda.synchronize()
+    for k, (out, (ref, ng)) in enumerate(zip(outs, refs)):
+        assert groups[k] == ng
+        assert torch.equal(out, ref), f"segment {k}"
+
+
+def test_arena_batch_matches_separate_launches():
+    """PartialArena.batch(): the same gradients, bit for bit, as one launch per layer."""
+    from distributional_rl_decision_and_control_amd.fused_critic import PartialArena
+    R = 8192
+    g = torch.Generator(device="cuda").manual_seed(3)
+    dz1, x1 = (torch.randn(R, n, generator=g, device="cuda").to(torch.bfloat16) for n in (128, 256))
+    dz2, x2 = (torch.randn(R, n, generator=g, device="cuda").to(torch.bfloat16) for n in (256, 64))
+    dq, h = torch.randn(R, 2, generator=g, device="cuda"), torch.randn(R, 128, generator=g, device="cuda").to(torch.bfloat16)
+    res = []
+    for batched in (False, True):
+        arena = PartialArena(1 << 24, "cuda")
+        w1, b1 = torch.zeros(128, 256, device="cuda"), torch.zeros(128, device="cuda")
+        w2, b2 = torch.zeros(256, 64, device="cuda"), torch.zeros(256, device="cuda")
+        w3, b3 = torch.zeros(128, device="cuda"), torch.zeros(1, device="cuda")
+        ctx = arena.batch() if batched else __import__("contextlib").nullcontext()
+        with ctx:
+            arena.linear(dz1, x1, w1, b1)
+            arena.vec(dq[:, 0], h, w3, b3)
+            arena.linear(dz2, x2, w2, b2)
+        arena.flush()
+        torch.cuda.synchronize()
+        res.append([w1, b1, w2, b2, w3, b3])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
