@@ -155,15 +155,12 @@ __global__ __launch_bounds__(kMlpWaves * 64) void encode_kernel(MlpArgs a) {
 
 // ------------------------------------------------------------------ Actor forward (ACT/FWD/TRAIN)
 template <int MODE>
-__device__ __forceinline__ void actor_tile(const MlpArgs& a, const ActorLds& L, int tile, int lane) {
+__device__ __forceinline__ void actor_tile(const MlpArgs& a, const ActorLds& L, int tile, int lane,
+                                           const bf16x8 (&bx)[2], const float (&mk)[kObjN]) {
   const AsvMlpIO& io = a.io;
   const int h = lane >> 5, r = lane & 31;
   const int row = tile * 32 + r;
   const bool valid = row < io.n;
-  const int rr = valid ? row : io.n - 1;
-  bf16x8 bx[2];
-  float mk[kObjN];
-  load_obs(io.x, io.ldx, rr, h, bx, mk);
   if (MODE == MLP_TRAIN && valid) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -264,6 +261,15 @@ __device__ __forceinline__ void actor_tile(const MlpArgs& a, const ActorLds& L, 
 template <int MODE>
 __global__ __launch_bounds__(kMlpWaves * 64) void actor_kernel(MlpArgs a) {
   __shared__ ActorLds L;
+  // the tile's observation rows are loaded first, in flight under the weight staging
+  const int tile = blockIdx.x * kMlpWaves + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const bool active = tile * 32 < a.io.n;
+  bf16x8 bx[2];
+  float mk[kObjN];
+  if (active) {
+    const int row = tile * 32 + (lane & 31);
+    load_obs(a.io.x, a.io.ldx, row < a.io.n ? row : a.io.n - 1, lane >> 5, bx, mk);
+  }
   {
     const bf16x8* ge = reinterpret_cast<const bf16x8*>(a.w.enc_frag);
     const bf16x8* g1 = reinterpret_cast<const bf16x8*>(a.w.w1_frag);
@@ -281,8 +287,7 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_kernel(MlpArgs a) {
     if (threadIdx.x < kNa) L.bout[threadIdx.x] = a.w.bout[threadIdx.x];
   }
   __syncthreads();
-  const int tile = blockIdx.x * kMlpWaves + (threadIdx.x >> 6);
-  if (tile * 32 < a.io.n) actor_tile<MODE>(a, L, tile, threadIdx.x & 63);
+  if (active) actor_tile<MODE>(a, L, tile, lane, bx, mk);
 }
 
 // ------------------------------------------------------------------ Actor backward
@@ -297,6 +302,40 @@ struct ActorBwdLds {
 
 __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_kernel(MlpArgs a) {
   __shared__ ActorBwdLds L;
+  const AsvMlpIO& io = a.io;
+  const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
+  const int tile = blockIdx.x * kMlpWaves + (threadIdx.x >> 6);
+  const bool active = tile * 32 < io.n;
+  const int row = tile * 32 + r;
+  const bool valid = row < io.n;
+  const int64_t rr = valid ? row : io.n - 1;
+  // one wave per SIMD (97 KB of LDS per workgroup): registers are free, so the tile's pre-activations,
+  // dL/da and h2 / h1 / h0 rows are all loaded up front, in flight under the weight staging
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  bf16x4 ph2[16], ph1[16], ph0[32];
+  float z0 = 0.f, z1 = 0.f, da0 = 0.f, da1 = 0.f;
+  if (active) {
+    z0 = io.pre[rr * 2]; z1 = io.pre[rr * 2 + 1];
+    da0 = io.dA[rr * 2]; da1 = io.dA[rr * 2 + 1];
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int64_t off = rr * kHid + mb * 32 + 16 * s + 4 * h + 8 * q;
+          ph2[(mb * 2 + s) * 2 + q] = *reinterpret_cast<const bf16x4*>(bp(io.h2) + off);
+          ph1[(mb * 2 + s) * 2 + q] = *reinterpret_cast<const bf16x4*>(bp(io.h1) + off);
+        }
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          ph0[(mb * 2 + s) * 2 + q] =
+              *reinterpret_cast<const bf16x4*>(bp(io.h0) + rr * kEnc + mb * 32 + 16 * s + 4 * h + 8 * q);
+  }
   {
     const bf16x8* g2 = reinterpret_cast<const bf16x8*>(a.w.w2t_frag);
     const bf16x8* g1 = reinterpret_cast<const bf16x8*>(a.w.w1t_frag);
@@ -305,16 +344,15 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_kernel(MlpArgs a) {
     for (int i = threadIdx.x; i < kNa * kHid; i += kMlpWaves * 64) L.wout[i] = a.w.wout[i];
   }
   __syncthreads();
-  const AsvMlpIO& io = a.io;
-  const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
-  const int tile = blockIdx.x * kMlpWaves + (threadIdx.x >> 6);
-  if (tile * 32 >= io.n) return;
-  const int row = tile * 32 + r;
-  const bool valid = row < io.n;
-  const int64_t rr = valid ? row : io.n - 1;
-  const float z0 = io.pre[rr * 2], z1 = io.pre[rr * 2 + 1];
-  const float d0 = io.dA[rr * 2] * a.w.out_scale / (1.f + z0 * z0);
-  const float d1 = io.dA[rr * 2 + 1] * a.w.out_scale / (1.f + z1 * z1);
+  if (!active) return;
+  auto unpack = [](const bf16x4* p, float* v) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[4 * q + j] = static_cast<float>(p[q][j]);
+  };
+  const float d0 = da0 * a.w.out_scale / (1.f + z0 * z0);
+  const float d1 = da1 * a.w.out_scale / (1.f + z1 * z1);
   if (valid && h == 0) {
     io.dout[row * 2] = d0;
     io.dout[row * 2 + 1] = d1;
@@ -325,10 +363,8 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_kernel(MlpArgs a) {
   for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int64_t off = rr * kHid + mb * 32 + 16 * s + 4 * h;
       float hv[8], dv[8];
-      load4(bp(io.h2) + off, hv);
-      load4(bp(io.h2) + off + 8, hv + 4);
+      unpack(&ph2[(mb * 2 + s) * 2], hv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int m = feat(mb, 8 * s + j, h);
@@ -350,10 +386,8 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_kernel(MlpArgs a) {
   for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int64_t off = rr * kHid + mb * 32 + 16 * s + 4 * h;
       float hv[8], dv[8];
-      load4(bp(io.h1) + off, hv);
-      load4(bp(io.h1) + off + 8, hv + 4);
+      unpack(&ph1[(mb * 2 + s) * 2], hv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         dv[j] = hv[j] > 0.f ? acc3[mb][8 * s + j] : 0.f;
@@ -376,10 +410,8 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_kernel(MlpArgs a) {
       const int mb = half * 4 + q;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const int64_t off = rr * kEnc + mb * 32 + 16 * s + 4 * h;
         float hv[8], dv[8];
-        load4(bp(io.h0) + off, hv);
-        load4(bp(io.h0) + off + 8, hv + 4);
+        unpack(&ph0[(mb * 2 + s) * 2], hv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) dv[j] = hv[j] > 0.f ? acc4[q][8 * s + j] : 0.f;
         store16(valid ? bp(io.dz0) + row * kEnc + mb * 32 + 16 * s : nullptr, dv, h);

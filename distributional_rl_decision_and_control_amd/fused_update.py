@@ -30,6 +30,7 @@ optimizer step are one multi-layer launch (a cross-stream join in a replayed gra
 Arithmetic: bf16 MFMA operands with f32 accumulation everywhere, f32 master weights / Adam.
 """
 import contextlib
+import os
 
 import torch
 
@@ -39,6 +40,9 @@ from .fused_mlp import ActorBuffers, MlpPack, actor_act, actor_backward, actor_f
 from .learner import FusedAdam, clip_and_step
 
 OBS = 40
+# the actor's training forward on a side stream beside the target chain (1) or on the caller's stream
+# (0): a join costs about as much as the forward in a replayed graph
+ACTOR_FWD_SIDE = os.environ.get("ASVRL_ACTOR_FWD_SIDE", "1") == "1"
 
 
 class SideStreams:
@@ -153,7 +157,10 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     side = st.side
     # ---- critic (agent.py:395-416); every critic .grad is overwritten below (no zeroing). The
     # trunk kernels run the critic's observation / action encoders on the replay rows themselves.
-    with side.on(1):   # the actor's training forward reads only s and the (not yet updated) actor
+    if ACTOR_FWD_SIDE:   # the actor's training forward reads only s and the (not yet updated) actor
+        with side.on(1):
+            actor_train_forward(st.actor, s_rows, ab)
+    else:
         actor_train_forward(st.actor, s_rows, ab)
     if q_next is None:
         q_next = st.q_next
@@ -180,7 +187,8 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
             produce()
 
     # ---- actor through the updated critic (agent.py:419-427); its forward ran on side stream 1
-    side.join(1)
+    if ACTOR_FWD_SIDE:
+        side.join(1)
     critic_actor_grad(st.local_trunk, None, None, taus[2], N, st.q_pi, w_ae=ae.weight, dA=ab.dA,
                       tile_loss=st.tile_loss[1], obs=s_rows, act=ab.a_out)
     actor_backward(st.actor, ab)
