@@ -41,8 +41,8 @@ from .learner import FusedAdam, clip_and_step
 
 OBS = 40
 # the actor's training forward on a side stream beside the target chain (1) or on the caller's stream
-# (0): a join costs about as much as the forward in a replayed graph
-ACTOR_FWD_SIDE = os.environ.get("ASVRL_ACTOR_FWD_SIDE", "1") == "1"
+# (0, default): the fork + join cost more than the 13 us forward in a replayed graph (-1 % per step)
+ACTOR_FWD_SIDE = os.environ.get("ASVRL_ACTOR_FWD_SIDE", "0") == "1"
 
 
 class SideStreams:
