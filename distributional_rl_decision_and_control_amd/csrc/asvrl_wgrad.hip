@@ -95,7 +95,10 @@ __device__ __forceinline__ void wgrad_body(const __bf16* __restrict__ dz, int64_
   const int zc8 = t % (M / 8), zr = t / (M / 8);
   const int xc8 = t % (K / 8), xr = t / (K / 8);
   constexpr int ZRS = kT * 8 / M, XRS = kT * 8 / K;   // row step between a thread's chunks
-  const bool zact = t < S::NCZ, xact = t < S::NCX;                     // staging threads
+  // threads past the shape's W waves (a 4-wave shape inside the 8-wave multi-layer launch) only
+  // take part in the barriers
+  const bool in_wg = t < kT;
+  const bool zact = in_wg && t < S::NCZ, xact = in_wg && t < S::NCX;   // staging threads
   // PF chunks in flight per thread (registers), chunk c + PF loaded while chunk c is consumed;
   // the chunk order and the MFMA order are those of PF = 1 (bit-identical results)
   u32x4 rz[kPF][S::CZ], rx[kPF][S::CX];
@@ -139,6 +142,7 @@ __device__ __forceinline__ void wgrad_body(const __bf16* __restrict__ dz, int64_
       }
 #pragma unroll
       for (int ks = 0; ks < kRC / 16; ++ks) {
+        if (!in_wg) break;
         bf16x8 fa[S::NMW], fb[S::NKW];
 #pragma unroll
         for (int i = 0; i < S::NMW; ++i) fa[i] = frag_tr(lz, S::SZ, ks * 16, (mb0 + i) * 32, lane);
@@ -156,15 +160,17 @@ __device__ __forceinline__ void wgrad_body(const __bf16* __restrict__ dz, int64_
   // partial dW block (mb, kb): lane l holds column l&31, rows (reg&3) + 8(reg>>2) + 4h
   float* pw = partial + static_cast<int64_t>(group) * (M * K + M);
   const int h = lane >> 5, col = lane & 31;
+  if (in_wg) {
 #pragma unroll
-  for (int i = 0; i < S::NMW; ++i)
+    for (int i = 0; i < S::NMW; ++i)
 #pragma unroll
-    for (int j = 0; j < S::NKW; ++j)
+      for (int j = 0; j < S::NKW; ++j)
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int m = (mb0 + i) * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        pw[m * K + (kb0 + j) * 32 + col] = acc[i * S::NKW + j][reg];
-      }
+        for (int reg = 0; reg < 16; ++reg) {
+          const int m = (mb0 + i) * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+          pw[m * K + (kb0 + j) * 32 + col] = acc[i * S::NKW + j][reg];
+        }
+  }
   // partial db: threads sharing a column chunk fold their sums
 #pragma unroll
   for (int j = 0; j < 8; ++j) lbias[t][j] = bacc[j];
@@ -240,7 +246,7 @@ __global__ __launch_bounds__(kWgThreads) void wgrad_vec_kernel(const float* __re
 // group range holds it and runs exactly the workgroup `b - first group` of that layer's own launch.
 // Every shape here has 8 waves; the LDS is one buffer sized for the largest.
 constexpr int kMultiW = 8;
-enum WgShape { WG_256x64 = 0, WG_128x256, WG_128x128, WG_256x32, WG_VEC128, WG_SMALL };
+enum WgShape { WG_256x64 = 0, WG_128x256, WG_128x128, WG_256x32, WG_32x128, WG_VEC128, WG_SMALL };
 struct WgSeg {
   const void* dz;    // bf16 (MFMA shapes), f32 (WG_VEC128: dq with stride ldz; WG_SMALL)
   const void* x;     // bf16, f32 (WG_SMALL)
@@ -253,16 +259,17 @@ struct WgMulti {
   WgSeg s[ASVRL_MAX_WGRAD_SEGS];
   int n;
 };
-template <int M, int K>
-constexpr int stage_bytes() { return kRC * (Shape<M, K, kMultiW>::SZ + Shape<M, K, kMultiW>::SX); }
+template <int M, int K, int W = kMultiW>
+constexpr int stage_bytes() { return kRC * (Shape<M, K, W>::SZ + Shape<M, K, W>::SX); }
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
-constexpr int kMultiStage = cmax(cmax(stage_bytes<256, 64>(), stage_bytes<128, 256>()),
-                                 cmax(stage_bytes<128, 128>(), stage_bytes<256, 32>()));
+constexpr int kMultiStage = cmax(cmax(cmax(stage_bytes<256, 64>(), stage_bytes<128, 256>()),
+                                      cmax(stage_bytes<128, 128>(), stage_bytes<256, 32>())),
+                                 stage_bytes<32, 128, 4>());
 
-template <int M, int K>
+template <int M, int K, int W = kMultiW>
 __device__ __forceinline__ void multi_run(const WgSeg& g, int group, char* lds, float (*lbias)[8]) {
-  using S = Shape<M, K, kMultiW>;
-  wgrad_body<M, K, kMultiW>(static_cast<const __bf16*>(g.dz), g.ldz, static_cast<const __bf16*>(g.x), g.ldx,
+  using S = Shape<M, K, W>;
+  wgrad_body<M, K, W>(static_cast<const __bf16*>(g.dz), g.ldz, static_cast<const __bf16*>(g.x), g.ldx,
                             g.chunks, g.per, g.partial, group, lds, lds + kRC * S::SZ, lbias);
 }
 
@@ -282,6 +289,7 @@ __global__ __launch_bounds__(kMultiW * 64, ASVRL_WGRAD_MULTI_WAVES) void wgrad_m
     case WG_128x256: multi_run<128, 256>(g, group, lds, lbias); break;
     case WG_128x128: multi_run<128, 128>(g, group, lds, lbias); break;
     case WG_256x32: multi_run<256, 32>(g, group, lds, lbias); break;
+    case WG_32x128: multi_run<32, 128, 4>(g, group, lds, lbias); break;   // 4 of the 8 waves
     case WG_VEC128:
       wgrad_vec_body<128>(static_cast<const float*>(g.dz), g.ldz, static_cast<const __bf16*>(g.x), g.ldx, g.chunks,
                           g.per, g.partial, group, reinterpret_cast<float(*)[9]>(&lbias[0][0]));
@@ -678,7 +686,9 @@ extern "C" int asvrl_linear_wgrad_multi(const AsvWgradSeg* segs, int32_t nseg, i
     else if (a.M == 128 && a.K == 256) shape = WG_128x256;
     else if (a.M == 128 && a.K == 128) shape = WG_128x128;
     else if (a.M == 256 && a.K == 32) shape = WG_256x32;
-    else ASVRL_REQUIRE(false, "asvrl_linear_wgrad_multi: (M, K) must be (256,64), (128,256), (128,128) or (256,32)");
+    else if (a.M == 32 && a.K == 128) shape = WG_32x128;
+    else ASVRL_REQUIRE(false,
+                       "asvrl_linear_wgrad_multi: (M, K) must be (256,64), (128,256), (128,128), (256,32) or (32,128)");
     groups = a.R == 0 ? 0 : wgrad_groups(a.R, a.M, a.K);
     ASVRL_REQUIRE(a.partial_floats >= static_cast<int64_t>(groups) * (a.M * a.K + a.M),
                   "asvrl_linear_wgrad_multi: workspace too small");

@@ -159,15 +159,13 @@ def iqn_grads(st, net, rows, taus, gamma=0.99, flush=True):
     iqn_forward_max(st.target, None, taus[0], N, st.q_next, obs=ns_rows)
     iqn_train(st.local, None, taus[1], bufs, st.dz_out, st.q_next.view(B, N), a_col, r_col, d_col, gamma, st.dzF,
               tile_loss=st.tile_loss, obs=s_rows, xb=st.xb)
-    with side.on(1):
-        # the padded 32-row output reduction (its own launch) fills the A-row output layer directly
+    with arena.batch():   # the five layers in one launch
+        # the padded 32-row output reduction fills the A-row output layer directly
         arena.linear(st.dz_out, bufs.h2, net.output_layer.weight.grad, net.output_layer.bias.grad)
-    with arena.batch():   # the other four layers in one launch
         arena.linear(bufs.dzc, bufs.cos, net.cos_embedding.weight.grad, net.cos_embedding.bias.grad)
         arena.fold(st.dzF, st.xb, net)   # encoder image -> self/object encoder grads
         arena.linear(bufs.dz1, bufs.h0, net.hidden_layer.weight.grad, net.hidden_layer.bias.grad)
         arena.linear(bufs.dz2, bufs.h1g, net.hidden_layer_2.weight.grad, net.hidden_layer_2.bias.grad)
-    side.join(1)
     arena.scalar(st.tile_loss, st.loss)
     if flush:
         arena.flush()

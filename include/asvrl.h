@@ -537,7 +537,7 @@ int asvrl_linear_wgrad_partial(const void* dz, int64_t ldz, const void* x, int64
  * streams joined back). Segment k writes groups_out[k] partials, bit-identical to its own launch
  * (same groups, same summation order):
  *   kind ASVRL_WGRAD_MFMA : asvrl_linear_wgrad_partial (bf16 dz, x); (M, K) in {(256, 64), (128, 256),
- *                           (128, 128), (256, 32)};
+ *                           (128, 128), (256, 32), (32, 128)};
  *   kind ASVRL_WGRAD_VEC  : asvrl_linear_wgrad_vec_partial (dz = dq f32 with stride ldz, M = 1, K = 128);
  *   kind ASVRL_WGRAD_SMALL: asvrl_small_wgrad_partial (f32 dz, x; M | 256, K <= 4). */
 #define ASVRL_MAX_WGRAD_SEGS 8

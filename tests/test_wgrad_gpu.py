@@ -270,6 +270,7 @@ def test_wgrad_multi_is_bit_identical_to_one_launch_per_layer(R):
              (_abi.WGRAD_MFMA, bf(R, 128), wide[:, 128:384], 128, 256),
              (_abi.WGRAD_MFMA, wide[:, 0:128], bf(R, 128), 128, 128),
              (_abi.WGRAD_MFMA, bf(R, 256), bf(R, 32), 256, 32),
+             (_abi.WGRAD_MFMA, bf(R, 32), wide[:, 256:384], 32, 128),   # IQN's padded head (4 of 8 waves)
              (_abi.WGRAD_VEC, dq[:, 1], bf(R, 128), 1, 128),
              (_abi.WGRAD_SMALL, torch.randn(R, 128, generator=g, device="cuda"),
               torch.randn(R, 2, generator=g, device="cuda"), 128, 2)]
