@@ -11,7 +11,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ASVRL_LIB", os.path.join(HERE, "lib", "libasvrl.so"))  # override: A/B variants
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
 OBS_DIM = 40   # self 7 | objects 25 | mask 5 | pad 3
@@ -120,6 +120,13 @@ SUM_PLAIN, SUM_FOLD_ENCODERS = 0, 1
 
 
 MAX_WGRAD_SEGS = 8
+MAX_PACK_SEGS = 8
+
+
+class AsvPackSeg(C.Structure):
+    _fields_ = [("flat_off", _I64), ("image", _VP), ("rows", _I32), ("cols", _I32), ("K", _I32), ("chained", _I32),
+                ("transposed", _I32), ("f32", _I32), ("row0", _I32), ("col0", _I32), ("nrep", _I32),
+                ("rep_row", _I32), ("rep_col", _I32), ("reserved", _I32)]
 WGRAD_MFMA, WGRAD_VEC, WGRAD_SMALL = 0, 1, 2
 
 
@@ -221,6 +228,8 @@ EXPORTS = [
     ("asvrl_partial_sums_norm", C.c_int, [_VP, _I32, _VP, _VP, _VP]),
     ("asvrl_partial_sums_norm_parts", _I32, [_VP, _I32]),
     ("asvrl_adam_step", C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, _F, _F, _VP, _VP, _I32, _VP]),
+    ("asvrl_adam_step_pack", C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, _F, _F, _VP, _VP, _I32, _VP, _I32,
+                                       _VP, _VP]),
     ("asvrl_linear_wgrad", C.c_int, [_VP, _I64, _VP, _I64, _I32, _I32, _I32, _VP, _VP, _I32, _VP, _I64, _VP]),
     ("asvrl_linear_wgrad_vec", C.c_int, [_VP, _I64, _VP, _I64, _I32, _I32, _VP, _VP, _I32, _VP, _I64, _VP]),
     ("asvrl_mlp_pack", C.c_int, [C.POINTER(AsvMlpSrc), C.POINTER(AsvMlpWeights), _VP]),

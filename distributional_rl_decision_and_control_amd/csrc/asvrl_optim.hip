@@ -14,6 +14,38 @@ namespace {
 constexpr int kNormBlocks = 64;
 constexpr int kOptThreads = 256;
 
+struct PackTable {
+  AsvPackSeg s[ASVRL_MAX_PACK_SEGS];
+  int n;
+};
+
+// Position of W[row][col] in an (M x K) A-operand fragment image: the inverse of frag_rc
+// (asvrl_mfma.h): o = ((mb*KS + ks)*64 + lane)*8 + j with lane = 32h + (row & 31).
+__device__ __forceinline__ int64_t frag_pos(int row, int col, int K, bool chained) {
+  const int mb = row >> 5, ks = col >> 4, c = col & 15;
+  const int h = chained ? ((c >> 2) & 1) : (c >> 3);
+  const int j = chained ? (((c >> 3) << 2) | (c & 3)) : (c & 7);
+  const int lane = 32 * h + (row & 31);
+  return (static_cast<int64_t>(mb) * (K >> 4) + ks) * 512 + lane * 8 + j;
+}
+
+// The updated parameter i into every image position a pack table gives it (asvrl_critic_pack /
+// asvrl_mlp_pack / asvrl_iqn_pack write the same values from the same f32 weights).
+__device__ __forceinline__ void pack_param(const PackTable& t, int64_t i, float p) {
+  for (int k = 0; k < t.n; ++k) {
+    const AsvPackSeg& g = t.s[k];
+    const int64_t u = i - g.flat_off;
+    if (u < 0 || u >= static_cast<int64_t>(g.rows) * g.cols) continue;
+    const int r = static_cast<int>(u / g.cols), c = static_cast<int>(u % g.cols);
+    for (int q = 0; q < g.nrep; ++q) {
+      int R = g.row0 + r + q * g.rep_row, Cc = g.col0 + c + q * g.rep_col;
+      if (g.transposed) { const int x = R; R = Cc; Cc = x; }
+      if (g.f32) static_cast<float*>(g.image)[R] = p;
+      else static_cast<__bf16*>(g.image)[frag_pos(R, Cc, g.K, g.chained != 0)] = static_cast<__bf16>(p);
+    }
+  }
+}
+
 __global__ __launch_bounds__(kOptThreads) void sumsq_kernel(const float* __restrict__ g, int64_t n,
                                                              double* __restrict__ partial, float* step) {
   double acc = 0.0;
@@ -41,7 +73,8 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(float* __restrict__ p
                                                             const double* __restrict__ partial, int nparts,
                                                             const float* __restrict__ step, float lr, float beta1,
                                                             float beta2, float eps, float max_norm,
-                                                            float* __restrict__ norm_out) {
+                                                            float* __restrict__ norm_out, PackTable pk,
+                                                            int64_t* __restrict__ counter) {
   __shared__ float s_coef;
   __shared__ double s_red[kOptThreads];
   {   // thread t folds partials t, t + 256, ... in order, then a fixed tree: the same in every block
@@ -80,8 +113,11 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(float* __restrict__ p
     m[i] = mi;
     v[i] = vi;
     const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    p[i] = p[i] - step_size * (mi / denom);            // param.addcdiv_(exp_avg, denom, -step_size)
+    const float pn = p[i] - step_size * (mi / denom);  // param.addcdiv_(exp_avg, denom, -step_size)
+    p[i] = pn;
+    if (pk.n > 0) pack_param(pk, i, pn);
   }
+  if (counter != nullptr && blockIdx.x == 0 && threadIdx.x == 0) counter[0] += 1;
 }
 
 }  // namespace
@@ -101,7 +137,8 @@ extern "C" int asvrl_adam_clip(float* params, float* grads, float* exp_avg, floa
   int64_t nb = (n + 4LL * kOptThreads - 1) / (4LL * kOptThreads);
   nb = nb < 1 ? 1 : (nb > 1024 ? 1024 : nb);
   hipLaunchKernelGGL(adam_kernel, dim3(static_cast<unsigned>(nb)), dim3(kOptThreads), 0, as_stream(stream), params,
-                     grads, exp_avg, exp_avg_sq, n, work, kNormBlocks, step, lr, beta1, beta2, eps, max_norm, norm_out);
+                     grads, exp_avg, exp_avg_sq, n, work, kNormBlocks, step, lr, beta1, beta2, eps, max_norm, norm_out,
+                     PackTable{}, static_cast<int64_t*>(nullptr));
   return check_launch("asvrl_adam_clip(step)");
 }
 
@@ -116,6 +153,33 @@ extern "C" int asvrl_adam_step(float* params, float* grads, float* exp_avg, floa
   nb = nb < 1 ? 1 : (nb > 1024 ? 1024 : nb);
   hipLaunchKernelGGL(adam_kernel, dim3(static_cast<unsigned>(nb)), dim3(kOptThreads), 0, as_stream(stream), params,
                      grads, exp_avg, exp_avg_sq, n, norm_parts, nparts, step, lr, beta1, beta2, eps, max_norm,
-                     norm_out);
+                     norm_out, PackTable{}, static_cast<int64_t*>(nullptr));
   return check_launch("asvrl_adam_step");
+}
+
+extern "C" int asvrl_adam_step_pack(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+                                    const float* step, float lr, float beta1, float beta2, float eps, float max_norm,
+                                    float* norm_out, const double* norm_parts, int32_t nparts, const AsvPackSeg* segs,
+                                    int32_t nseg, int64_t* counter, void* stream) {
+  ASVRL_REQUIRE(params && grads && exp_avg && exp_avg_sq && step && norm_parts && nparts >= 1,
+                "asvrl_adam_step_pack: null argument");
+  ASVRL_REQUIRE(n >= 0 && nseg >= 0 && nseg <= ASVRL_MAX_PACK_SEGS && (nseg == 0 || segs != nullptr),
+                "asvrl_adam_step_pack: bad size or pack table");
+  PackTable t{};
+  for (int k = 0; k < nseg; ++k) {
+    const AsvPackSeg& g = segs[k];
+    ASVRL_REQUIRE(g.image && g.rows >= 1 && g.cols >= 1 && g.nrep >= 1 && g.flat_off >= 0 &&
+                      g.flat_off + static_cast<int64_t>(g.rows) * g.cols <= n,
+                  "asvrl_adam_step_pack: segment outside the parameters");
+    ASVRL_REQUIRE(g.f32 || (g.K % 16 == 0 && g.K >= 16), "asvrl_adam_step_pack: image K must be a multiple of 16");
+    t.s[k] = g;
+  }
+  t.n = nseg;
+  if (n == 0) return 0;
+  int64_t nb = (n + 4LL * kOptThreads - 1) / (4LL * kOptThreads);
+  nb = nb < 1 ? 1 : (nb > 1024 ? 1024 : nb);
+  hipLaunchKernelGGL(adam_kernel, dim3(static_cast<unsigned>(nb)), dim3(kOptThreads), 0, as_stream(stream), params,
+                     grads, exp_avg, exp_avg_sq, n, norm_parts, nparts, step, lr, beta1, beta2, eps, max_norm,
+                     norm_out, t, counter);
+  return check_launch("asvrl_adam_step_pack");
 }

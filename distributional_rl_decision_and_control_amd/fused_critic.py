@@ -71,6 +71,16 @@ class CriticPack:
         self.struct = s
         self.refresh()
 
+    def adam_segments(self, opt):
+        """The five trunk images as AsvPackSeg of FusedAdam `opt` (asvrl_adam_step_pack)."""
+        c = self.critic
+        W1, W2 = c.hidden_layer.weight, c.hidden_layer_2.weight
+        return [opt.pack_seg(c.cos_embedding.weight, self.wc, K=64),
+                opt.pack_seg(W1, self.w1, K=256, chained=True), opt.pack_seg(W1, self.w1t, K=128, chained=True,
+                                                                            transposed=True),
+                opt.pack_seg(W2, self.w2, K=128, chained=True), opt.pack_seg(W2, self.w2t, K=128, chained=True,
+                                                                            transposed=True)]
+
     def refresh(self, stream=None):
         """Re-pack from the critic's current f32 weights: one asvrl_critic_pack launch."""
         c = self.critic

@@ -57,6 +57,11 @@ class IqnPack(CriticPack):
         self.head = hd
         super().__init__(net)
 
+    def adam_segments(self, opt):
+        """The trunk images and the head's leading rows (the padding rows stay zero)."""
+        return super().adam_segments(opt) + [opt.pack_seg(self.critic.output_layer.weight, self.head_img, K=128,
+                                                          chained=True)]
+
     def refresh(self, stream=None):
         n = self.critic
         rc = _abi.lib().asvrl_iqn_pack(_abi.ptr(n.cos_embedding.weight), _abi.ptr(n.hidden_layer.weight),
@@ -171,13 +176,13 @@ def iqn_grads(st, net, rows, taus, gamma=0.99, flush=True):
         arena.flush()
 
 
-def iqn_update_fused(st, net, opt, grads, rows, gamma=0.99, taus=None, sync=None, max_norm=0.5, act_wait=None):
+def iqn_update_fused(st, net, opt, grads, rows, gamma=0.99, taus=None, sync=None, max_norm=0.5, act_wait=None,
+                     counter=None):
     """One IQN update from replay rows [B][88]; taus: (2, B, N) (target, local) or None (drawn).
     act_wait: event to wait for before the weights change (a concurrent act kernel).
     Returns (loss, grad_norm) as device scalars."""
     if taus is None:
         taus = torch.rand(2, st.B, st.N, device=st.device)
     iqn_grads(st, net, rows, taus, gamma, flush=False)
-    gn = _reduce_and_step(st.arena, opt, grads, sync, max_norm, wait=act_wait)
-    st.local.refresh()
+    gn = _reduce_and_step(st.arena, opt, grads, sync, max_norm, wait=act_wait, pack=st.local, counter=counter)
     return st.loss[0], gn

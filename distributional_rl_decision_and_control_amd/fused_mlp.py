@@ -16,6 +16,7 @@ import torch
 from . import _abi
 
 ENC, OBSK, HID = 256, 32, 128
+MAX_OBJ = 5   # object-encoder copies in the encoder image (max_object_num)
 MODE_ACT, MODE_FWD, MODE_TRAIN = 1, 2, 3
 
 
@@ -63,6 +64,25 @@ class MlpPack:
         elif self.kind == "critic":
             s.ae_w = n.action_encoder[0].weight.data_ptr()
         return s
+
+    def adam_segments(self, opt):
+        """The actor's images as AsvPackSeg of FusedAdam `opt` (asvrl_adam_step_pack): the block-structured
+        encoder image (self encoder once, the object encoder at its five diagonal blocks), the f32 encoder
+        bias copy and the four hidden-layer images."""
+        assert self.kind == "actor"
+        n = self.net
+        se, oe = n.self_encoder[0], n.object_encoder[0]
+        nso, nsi = se.weight.shape
+        noo, noi = oe.weight.shape
+        W1, W2 = n.hidden_layer.weight, n.hidden_layer_2.weight
+        return [opt.pack_seg(se.weight, self.enc, K=OBSK),
+                opt.pack_seg(oe.weight, self.enc, K=OBSK, row0=nso, col0=nsi, nrep=MAX_OBJ, rep_row=noo, rep_col=noi),
+                opt.pack_seg(se.bias, self.b_enc, f32=True),
+                opt.pack_seg(oe.bias, self.b_enc, f32=True, row0=nso, nrep=MAX_OBJ, rep_row=noo),
+                opt.pack_seg(W1, self.w1, K=ENC, chained=True), opt.pack_seg(W1, self.w1t, K=HID, chained=True,
+                                                                            transposed=True),
+                opt.pack_seg(W2, self.w2, K=HID, chained=True), opt.pack_seg(W2, self.w2t, K=HID, chained=True,
+                                                                            transposed=True)]
 
     def refresh(self, stream=None):
         src = self.src()

@@ -112,16 +112,29 @@ class FusedACIQNState:
         actor_act(self.actor, obs_rows, actions64, step_dev, steps_per_count, total, fraction, initial, final, seed)
 
 
-def _reduce_and_step(arena, opt, grads, sync, max_norm, wait=None):
+def _reduce_and_step(arena, opt, grads, sync, max_norm, wait=None, pack=None, counter=None):
     """Reduce the queued weight-gradient partials, then clip + Adam. Single process with the
-    fused optimiser: the reduction launch also forms the gradient norm (two launches in all);
-    otherwise reduce, all-reduce (sync), then asvrl_adam_clip. `wait`: an event to wait for
-    before the parameters change."""
+    fused optimiser: the reduction launch also forms the gradient norm and the Adam launch writes the
+    weight images of `pack` (a CriticPack / MlpPack / IqnPack) and increments `counter` (two launches
+    in all); otherwise reduce, all-reduce (sync), asvrl_adam_clip, then pack.refresh() and
+    counter += 1. `wait`: an event to wait for before the parameters change."""
     if sync is None and isinstance(opt, FusedAdam):
         arena.flush(norm=opt)
         if wait is not None:
             torch.cuda.current_stream().wait_event(wait)
-        return opt.step_prenormed(arena.norm_parts, arena.nparts)
+        if pack is not None and not hasattr(pack, "_adam_segs"):
+            pack._adam_segs = pack.adam_segments(opt)
+        return opt.step_prenormed(arena.norm_parts, arena.nparts, pack=pack._adam_segs if pack is not None else None,
+                                  counter=counter)
+    gn = _step_unfused(arena, opt, grads, sync, max_norm, wait)
+    if pack is not None:
+        pack.refresh()
+    if counter is not None:
+        counter += 1
+    return gn
+
+
+def _step_unfused(arena, opt, grads, sync, max_norm, wait):
     arena.flush()
     if sync is not None:
         sync(grads)
@@ -139,10 +152,12 @@ def target_q(st, rows, tau0, q_out, na):
 
 
 def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, actor_grads, rows, gamma=0.99,
-                         taus=None, sync=None, max_norm=0.5, actor_wait=None, q_next=None, produce=None):
+                         taus=None, sync=None, max_norm=0.5, actor_wait=None, q_next=None, produce=None,
+                         counter=None):
     """One AC-IQN update from replay rows [B][88]. taus: (3, B, N) or None (drawn here).
     actor_wait: event to wait for before the actor's weights change (a concurrent act kernel).
-    q_next: the rows' target quantiles already computed (the pipelined loop); produce: a callable
+    counter: an int64 device scalar incremented after the step (the learn counter; in-kernel when
+    the optimiser step is fused). q_next: the rows' target quantiles already computed (the pipelined loop); produce: a callable
     that samples the NEXT batch and computes its q_next, run on a side stream beside the actor
     step (after the critic step, so the target chain overlaps the actor's kernels).
     Returns (critic_loss, actor_loss, critic_grad_norm, actor_grad_norm) as device scalars."""
@@ -180,8 +195,7 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
         arena.fold(st.dzF, st.xb, critic)             # encoder image -> self/object encoder grads
         arena.small(st.dzG, a_rows, ae.weight.grad, ae.bias.grad)
     arena.scalar(st.tile_loss[0], st.losses[0:1])   # the critic loss
-    cgn = _reduce_and_step(arena, critic_opt, critic_grads, sync, max_norm)
-    st.local_trunk.refresh()
+    cgn = _reduce_and_step(arena, critic_opt, critic_grads, sync, max_norm, pack=st.local_trunk)
     if produce is not None:   # next batch + its target quantiles beside the actor step
         with side.on(2):
             produce()
@@ -200,8 +214,8 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
         arena.vec(ab.dout[:, 1], ab.h2, ow[1], obias[1:2])
         arena.fold(ab.dz0, ab.xb, actor)
     arena.scalar(st.tile_loss[1], st.losses[1:2])   # the actor loss
-    agn = _reduce_and_step(arena, actor_opt, actor_grads, sync, max_norm, wait=actor_wait)
-    st.actor.refresh()
+    agn = _reduce_and_step(arena, actor_opt, actor_grads, sync, max_norm, wait=actor_wait, pack=st.actor,
+                           counter=counter)
     if produce is not None:
         side.join(2)
     return st.losses[0], st.losses[1], cgn, agn

@@ -110,9 +110,34 @@ class FusedAdam:
         _abi.check(rc, "asvrl_adam_clip")
         return self.norm[0]
 
-    def step_prenormed(self, norm_parts, nparts):
+    def pack_seg(self, w, image, K=0, chained=False, transposed=False, f32=False, row0=0, col0=0, nrep=1, rep_row=0,
+                 rep_col=0):
+        """An AsvPackSeg sending parameter w (one of this optimiser's, re-pointed into its flat buffer)
+        into a weight image at every step (asvrl_adam_step_pack)."""
+        off = (w.data_ptr() - self.flat.data_ptr()) // 4
+        assert 0 <= off and off + w.numel() <= self.n and w.is_contiguous()
+        g = _abi.AsvPackSeg()
+        g.flat_off, g.image = off, image.data_ptr()
+        g.rows, g.cols = (w.shape[0], w.shape[1]) if w.dim() == 2 else (w.shape[0], 1)
+        g.K, g.chained, g.transposed, g.f32 = K, int(chained), int(transposed), int(f32)
+        g.row0, g.col0, g.nrep, g.rep_row, g.rep_col = row0, col0, nrep, rep_row, rep_col
+        return g
+
+    def step_prenormed(self, norm_parts, nparts, pack=None, counter=None):
         """Clip + Adam with the squared norm as nparts f64 partials and step_t already advanced
-        (PartialArena.flush(norm=self)): one launch. Returns the pre-clip norm."""
+        (PartialArena.flush(norm=self)): one launch. pack: AsvPackSeg list -- the same launch writes
+        the updated weights into those images (no re-pack launch); counter: an int64 device scalar
+        the launch increments. Returns the pre-clip norm."""
+        if pack or counter is not None:
+            pack = list(pack or [])
+            arr = (_abi.AsvPackSeg * max(1, len(pack)))(*pack)
+            rc = _abi.lib().asvrl_adam_step_pack(
+                _abi.ptr(self.flat), _abi.ptr(self.grads.flat), _abi.ptr(self.exp_avg), _abi.ptr(self.exp_avg_sq),
+                self.n, _abi.ptr(self.step_t), self.lr, self.betas[0], self.betas[1], self.eps, self.max_norm,
+                _abi.ptr(self.norm), _abi.ptr(norm_parts), int(nparts), arr, len(pack),
+                _abi.ptr(counter) if counter is not None else None, _abi.stream_ptr(None))
+            _abi.check(rc, "asvrl_adam_step_pack")
+            return self.norm[0]
         rc = _abi.lib().asvrl_adam_step(
             _abi.ptr(self.flat), _abi.ptr(self.grads.flat), _abi.ptr(self.exp_avg), _abi.ptr(self.exp_avg_sq),
             self.n, _abi.ptr(self.step_t), self.lr, self.betas[0], self.betas[1], self.eps, self.max_norm,

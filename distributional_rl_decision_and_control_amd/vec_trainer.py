@@ -302,16 +302,12 @@ class VecTrainer:
         rows = self.replay.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter, out=self.batch_rows,
                                   state=state, guard=guard, taus=taus)
         if self.agent_type == "AC-IQN" and self.fused2 is not None:
-            out = ac_iqn_update_fused2(self.fused2, self.local, self.actor_opt, self.critic_opt, self.critic_grads,
-                                       self.actor_grads, rows, gamma=self.gamma, sync=self.sync,
-                                       actor_wait=actor_wait, taus=taus)
-            self.learn_counter += 1
-            return out
+            return ac_iqn_update_fused2(self.fused2, self.local, self.actor_opt, self.critic_opt, self.critic_grads,
+                                        self.actor_grads, rows, gamma=self.gamma, sync=self.sync,
+                                        actor_wait=actor_wait, taus=taus, counter=self.learn_counter)
         if self.fused_iqn is not None:
-            out = iqn_update_fused(self.fused_iqn, self.local, self.opt, self.grads, rows, gamma=self.gamma,
-                                   sync=self.sync, act_wait=actor_wait, taus=taus[:2])
-            self.learn_counter += 1
-            return out
+            return iqn_update_fused(self.fused_iqn, self.local, self.opt, self.grads, rows, gamma=self.gamma,
+                                    sync=self.sync, act_wait=actor_wait, taus=taus[:2], counter=self.learn_counter)
         s, a, r, ns, d = split_rows(rows)
         if self.agent_type == "AC-IQN" and self.fused is not None:
             out = ac_iqn_update_fused(self.fused, self.local, self.target, self.actor_opt, self.critic_opt,

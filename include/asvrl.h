@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 9
+#define ASVRL_ABI_VERSION 10
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -511,6 +511,25 @@ int asvrl_adam_clip(float* params, float* grads, float* exp_avg, float* exp_avg_
 int asvrl_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
                     const float* step, float lr, float beta1, float beta2, float eps, float max_norm,
                     float* norm_out, const double* norm_parts, int32_t nparts, void* stream);
+
+/* asvrl_adam_step that also writes every updated parameter into the bf16 MFMA weight images (ABI v10;
+ * replaces the asvrl_critic_pack / asvrl_mlp_pack / asvrl_iqn_pack launch after the step, same values).
+ * Segment: the rows x cols row-major weight at params[flat_off...]; element (r, c) goes to image position
+ * (row0 + r + q*rep_row, col0 + c + q*rep_col) for q < nrep, swapped if transposed; f32 = 1 writes
+ * image[row] as f32 (a bias copy, cols = 1), otherwise the bf16 fragment image of K columns (chained = 1:
+ * an accumulator-fed layer's order). counter (optional): incremented once by the launch. */
+#define ASVRL_MAX_PACK_SEGS 8
+typedef struct AsvPackSeg {
+  int64_t flat_off;
+  void* image;
+  int32_t rows, cols, K, chained;
+  int32_t transposed, f32, row0, col0;
+  int32_t nrep, rep_row, rep_col, reserved;
+} AsvPackSeg;
+int asvrl_adam_step_pack(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+                         const float* step, float lr, float beta1, float beta2, float eps, float max_norm,
+                         float* norm_out, const double* norm_parts, int32_t nparts, const AsvPackSeg* segs,
+                         int32_t nseg, int64_t* counter, void* stream);
 
 /* ---------------------------------------------------------------- Linear weight gradients */
 

@@ -227,3 +227,56 @@ def test_fused2_update_tracks_fp32_update():
     for n, p, q in pairs:
         c = _cos(q.detach() - init[n], p.detach() - init[n])
         assert c > 0.9, (n, c)
+
+
+def test_adam_step_pack_writes_the_repacked_images():
+    """asvrl_adam_step_pack (ABI v10): the weight images written by the Adam launch itself equal a
+    separate re-pack of the updated weights bit for bit (actor: encoder image + f32 bias copy + four
+    hidden images; critic trunk; IQN trunk + head), the parameters equal the plain asvrl_adam_step,
+    and the counter advances once."""
+    from distributional_rl_decision_and_control_amd.fused_critic import CriticPack
+    from distributional_rl_decision_and_control_amd.fused_mlp import MlpPack
+    from distributional_rl_decision_and_control_amd.learner import FusedAdam
+    pol, ref = _policy(), _policy()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    for net, rnet, mk in ((pol.actor, ref.actor, lambda n: MlpPack(n, "actor")), (pol.critic, ref.critic, CriticPack)):
+        opt, ropt = FusedAdam(net.parameters(), lr=1e-2), FusedAdam(rnet.parameters(), lr=1e-2)
+        pk = mk(net)
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        for _ in range(3):
+            gr = torch.randn(opt.n, generator=g, device="cuda")
+            opt.grads.flat.copy_(gr)
+            ropt.grads.flat.copy_(gr)
+            parts = (gr.double() ** 2).sum().reshape(1)
+            for o in (opt, ropt):
+                o.step_t += 1
+            opt.step_prenormed(parts, 1, pack=pk.adam_segments(opt), counter=cnt)
+            ropt.step_prenormed(parts, 1)
+            torch.cuda.synchronize()
+            assert torch.equal(opt.flat, ropt.flat)
+            imgs = [t.clone() for t in vars(pk).values() if isinstance(t, torch.Tensor)]
+            pk.refresh()
+            torch.cuda.synchronize()
+            after = [t for t in vars(pk).values() if isinstance(t, torch.Tensor)]
+            assert len(imgs) >= 5 and all(torch.equal(a, b) for a, b in zip(imgs, after))
+        assert int(cnt.item()) == 3
+
+
+def test_adam_step_pack_iqn_head():
+    from distributional_rl_decision_and_control_amd.fused_iqn import IqnPack
+    from distributional_rl_decision_and_control_amd.learner import FusedAdam
+    from distributional_rl_decision_and_control_amd.policy.IQN_model import IQN_Policy
+    from distributional_rl_decision_and_control_amd.vec_trainer import DEFAULT_NET
+    net = IQN_Policy(**DEFAULT_NET, action_size=25, device="cuda", seed=3).cuda()
+    opt = FusedAdam(net.parameters(), lr=1e-2)
+    pk = IqnPack(net)
+    gr = torch.randn(opt.n, device="cuda")
+    opt.grads.flat.copy_(gr)
+    opt.step_t += 1
+    opt.step_prenormed((gr.double() ** 2).sum().reshape(1), 1, pack=pk.adam_segments(opt))
+    torch.cuda.synchronize()
+    imgs = [t.clone() for t in (pk.wc, pk.w1, pk.w2, pk.w2t, pk.w1t, pk.head_img)]
+    pk.refresh()
+    torch.cuda.synchronize()
+    for a, b in zip(imgs, (pk.wc, pk.w1, pk.w2, pk.w2t, pk.w1t, pk.head_img)):
+        assert torch.equal(a, b)
