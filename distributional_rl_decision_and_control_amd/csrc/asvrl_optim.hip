@@ -34,9 +34,10 @@ __device__ __forceinline__ int64_t frag_pos(int row, int col, int K, bool chaine
 __device__ __forceinline__ void pack_param(const PackTable& t, int64_t i, float p) {
   for (int k = 0; k < t.n; ++k) {
     const AsvPackSeg& g = t.s[k];
-    const int64_t u = i - g.flat_off;
-    if (u < 0 || u >= static_cast<int64_t>(g.rows) * g.cols) continue;
-    const int r = static_cast<int>(u / g.cols), c = static_cast<int>(u % g.cols);
+    const int64_t u64 = i - g.flat_off;
+    if (u64 < 0 || u64 >= static_cast<int64_t>(g.rows) * g.cols) continue;
+    const unsigned u = static_cast<unsigned>(u64), cols = static_cast<unsigned>(g.cols);   // 32-bit division
+    const int r = static_cast<int>(u / cols), c = static_cast<int>(u - static_cast<unsigned>(r) * cols);
     for (int q = 0; q < g.nrep; ++q) {
       int R = g.row0 + r + q * g.rep_row, Cc = g.col0 + c + q * g.rep_col;
       if (g.transposed) { const int x = R; R = Cc; Cc = x; }
