@@ -13,6 +13,10 @@ namespace {
 
 constexpr int kNormBlocks = 64;
 constexpr int kOptThreads = 256;
+#ifndef ASVRL_ADAM_PER_THREAD
+#define ASVRL_ADAM_PER_THREAD 1
+#endif
+constexpr int64_t kAdamPer = ASVRL_ADAM_PER_THREAD;   // parameters per thread (grid size), at most 1024 blocks
 
 struct PackTable {
   AsvPackSeg s[ASVRL_MAX_PACK_SEGS];
@@ -135,7 +139,7 @@ extern "C" int asvrl_adam_clip(float* params, float* grads, float* exp_avg, floa
   hipLaunchKernelGGL(sumsq_kernel, dim3(kNormBlocks), dim3(kOptThreads), 0, as_stream(stream), grads, n, work,
                      step);
   if (int rc = check_launch("asvrl_adam_clip(norm)")) return rc;
-  int64_t nb = (n + 4LL * kOptThreads - 1) / (4LL * kOptThreads);
+  int64_t nb = (n + kAdamPer * kOptThreads - 1) / (kAdamPer * kOptThreads);
   nb = nb < 1 ? 1 : (nb > 1024 ? 1024 : nb);
   hipLaunchKernelGGL(adam_kernel, dim3(static_cast<unsigned>(nb)), dim3(kOptThreads), 0, as_stream(stream), params,
                      grads, exp_avg, exp_avg_sq, n, work, kNormBlocks, step, lr, beta1, beta2, eps, max_norm, norm_out,
@@ -150,7 +154,7 @@ extern "C" int asvrl_adam_step(float* params, float* grads, float* exp_avg, floa
                 "asvrl_adam_step: null argument");
   ASVRL_REQUIRE(n >= 0, "asvrl_adam_step: negative size");
   if (n == 0) return 0;
-  int64_t nb = (n + 4LL * kOptThreads - 1) / (4LL * kOptThreads);
+  int64_t nb = (n + kAdamPer * kOptThreads - 1) / (kAdamPer * kOptThreads);
   nb = nb < 1 ? 1 : (nb > 1024 ? 1024 : nb);
   hipLaunchKernelGGL(adam_kernel, dim3(static_cast<unsigned>(nb)), dim3(kOptThreads), 0, as_stream(stream), params,
                      grads, exp_avg, exp_avg_sq, n, norm_parts, nparts, step, lr, beta1, beta2, eps, max_norm,
@@ -177,7 +181,7 @@ extern "C" int asvrl_adam_step_pack(float* params, float* grads, float* exp_avg,
   }
   t.n = nseg;
   if (n == 0) return 0;
-  int64_t nb = (n + 4LL * kOptThreads - 1) / (4LL * kOptThreads);
+  int64_t nb = (n + kAdamPer * kOptThreads - 1) / (kAdamPer * kOptThreads);
   nb = nb < 1 ? 1 : (nb > 1024 ? 1024 : nb);
   hipLaunchKernelGGL(adam_kernel, dim3(static_cast<unsigned>(nb)), dim3(kOptThreads), 0, as_stream(stream), params,
                      grads, exp_avg, exp_avg_sq, n, norm_parts, nparts, step, lr, beta1, beta2, eps, max_norm,
