@@ -20,13 +20,14 @@ The online net's noise is never resampled during training, as in the reference (
 only called on the target, agent.py:610). The target noise comes from Philox instead of torch.randn.
 """
 import ctypes as C
+import os
 
 import torch
 import torch.nn.functional as F
 
 from . import _abi
 from .learn_ops import c51_project
-from .policy.AC_IQN_model import encode_observation
+from .splitk_linear import SPLITK_MIN_ROWS, _SplitKLinear
 
 NOISY = ("hidden_layer_v", "hidden_layer_v_2", "output_layer_v", "hidden_layer_a", "hidden_layer_a_2",
          "output_layer_a")
@@ -100,17 +101,39 @@ class NoisyPack:
         _abi.check(_abi.lib().asvrl_noisy_compose(C.byref(s), 1, _abi.stream_ptr(stream)), "asvrl_noisy_compose(bwd)")
 
 
+_SPLITK = os.environ.get("ASVRL_RAINBOW_SPLITK", "1") != "0"
+
+
+def _lin(x, w, b):
+    """F.linear; with grad on a batch of >= SPLITK_MIN_ROWS rows the weight gradient is a split-K
+    batched GEMM (a single hipBLASLt call at K = 8192 leaves most CUs idle: 50 us per layer)."""
+    if _SPLITK and torch.is_grad_enabled() and x.shape[0] >= SPLITK_MIN_ROWS and (w.requires_grad or x.requires_grad):
+        return _SplitKLinear.apply(x, w, b)
+    return F.linear(x, w, b)
+
+
 def logits(net, x, W):
     """Rainbow_Policy.forward up to the dueling combine (Rainbow_model.py:97-127): value (N, 51) and
-    advantage (N, 25*51) logits with the composed noisy weights W."""
-    f = encode_observation(net.self_encoder, net.object_encoder, x, net.max_object_num, net.object_dimension,
-                           net.object_feature_dimension)
-    fv = F.relu(F.linear(f, *W["hidden_layer_v"]))
-    fv = F.relu(F.linear(fv, *W["hidden_layer_v_2"]))
-    v = F.linear(fv, *W["output_layer_v"])
-    fa = F.relu(F.linear(f, *W["hidden_layer_a"]))
-    fa = F.relu(F.linear(fa, *W["hidden_layer_a_2"]))
-    a = F.linear(fa, *W["output_layer_a"])
+    advantage (N, 25*51) logits with the composed noisy weights W. The encoders are
+    encode_observation (AC_IQN_model.py:284-308) written out so their layers take _lin too."""
+    x_1, x_2, x_2_mask = x
+    B = x_1.shape[0]
+    se, oe = net.self_encoder[0], net.object_encoder[0]
+    f1 = F.relu(_lin(x_1, se.weight, se.bias))
+    if x_2 is None:
+        f2 = torch.zeros((B, net.max_object_num * net.object_feature_dimension), device=x_1.device, dtype=f1.dtype)
+    else:
+        f2 = F.relu(_lin(x_2.reshape(B * net.max_object_num, net.object_dimension), oe.weight, oe.bias))
+        f2 = f2.view(B, net.max_object_num, net.object_feature_dimension)
+        f2 = f2.masked_fill(x_2_mask.unsqueeze(-1) < 0.5, 0.0)
+        f2 = f2.reshape(B, net.max_object_num * net.object_feature_dimension)
+    f = torch.cat((f1, f2), 1)
+    fv = F.relu(_lin(f, *W["hidden_layer_v"]))
+    fv = F.relu(_lin(fv, *W["hidden_layer_v_2"]))
+    v = _lin(fv, *W["output_layer_v"])
+    fa = F.relu(_lin(f, *W["hidden_layer_a"]))
+    fa = F.relu(_lin(fa, *W["hidden_layer_a_2"]))
+    a = _lin(fa, *W["output_layer_a"])
     return v, a
 
 

@@ -96,11 +96,11 @@ def test_act_greedy_matches_torch():
     assert h.min() > 0.5 * N / 25
 
 
-def test_fused_update_matches_rainbow_update():
+@pytest.mark.parametrize("B", [1024, 8192])  # 8192: split-K weight gradients (SPLITK_MIN_ROWS)
+def test_fused_update_matches_rainbow_update(B):
     from distributional_rl_decision_and_control_amd.fused_rainbow import FusedRainbow
     from distributional_rl_decision_and_control_amd.learn_ops import split_rows
     from distributional_rl_decision_and_control_amd.learner import FlatGrads, rainbow_update
-    B = 1024
     rows = _rows(B)
     sup = torch.linspace(-1.0, 1.0, 51, device="cuda")
     local, target = _nets()
