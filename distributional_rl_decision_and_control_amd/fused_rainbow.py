@@ -112,6 +112,18 @@ def _lin(x, w, b):
     return F.linear(x, w, b)
 
 
+_RELU_EPILOGUE = os.environ.get("ASVRL_RAINBOW_EPI", "1") != "0"
+
+
+def _lin_relu(x, w, b):
+    """relu(x W^T + b). Without grad on the device it is one hipBLASLt GEMM with the bias + ReLU
+    epilogue (torch._addmm_activation) instead of a GEMM and a clamp launch (4-5 us each, 18 per
+    Rainbow iteration in the act and target forwards)."""
+    if _RELU_EPILOGUE and not torch.is_grad_enabled() and x.is_cuda and x.dim() == 2:
+        return torch._addmm_activation(b, x, w.t())
+    return F.relu(_lin(x, w, b))
+
+
 def logits(net, x, W):
     """Rainbow_Policy.forward up to the dueling combine (Rainbow_model.py:97-127): value (N, 51) and
     advantage (N, 25*51) logits with the composed noisy weights W. The encoders are
@@ -119,20 +131,20 @@ def logits(net, x, W):
     x_1, x_2, x_2_mask = x
     B = x_1.shape[0]
     se, oe = net.self_encoder[0], net.object_encoder[0]
-    f1 = F.relu(_lin(x_1, se.weight, se.bias))
+    f1 = _lin_relu(x_1, se.weight, se.bias)
     if x_2 is None:
         f2 = torch.zeros((B, net.max_object_num * net.object_feature_dimension), device=x_1.device, dtype=f1.dtype)
     else:
-        f2 = F.relu(_lin(x_2.reshape(B * net.max_object_num, net.object_dimension), oe.weight, oe.bias))
+        f2 = _lin_relu(x_2.reshape(B * net.max_object_num, net.object_dimension), oe.weight, oe.bias)
         f2 = f2.view(B, net.max_object_num, net.object_feature_dimension)
         f2 = f2.masked_fill(x_2_mask.unsqueeze(-1) < 0.5, 0.0)
         f2 = f2.reshape(B, net.max_object_num * net.object_feature_dimension)
     f = torch.cat((f1, f2), 1)
-    fv = F.relu(_lin(f, *W["hidden_layer_v"]))
-    fv = F.relu(_lin(fv, *W["hidden_layer_v_2"]))
+    fv = _lin_relu(f, *W["hidden_layer_v"])
+    fv = _lin_relu(fv, *W["hidden_layer_v_2"])
     v = _lin(fv, *W["output_layer_v"])
-    fa = F.relu(_lin(f, *W["hidden_layer_a"]))
-    fa = F.relu(_lin(fa, *W["hidden_layer_a_2"]))
+    fa = _lin_relu(f, *W["hidden_layer_a"])
+    fa = _lin_relu(fa, *W["hidden_layer_a_2"])
     a = _lin(fa, *W["output_layer_a"])
     return v, a
 
