@@ -27,7 +27,7 @@ import torch.nn.functional as F
 
 from . import _abi
 from .learn_ops import c51_project
-from .splitk_linear import SPLITK_MIN_ROWS, _SplitKLinear
+from .splitk_linear import SPLITK_MIN_ROWS, _SplitKLinear, _SplitKLinearReLU
 
 NOISY = ("hidden_layer_v", "hidden_layer_v_2", "output_layer_v", "hidden_layer_a", "hidden_layer_a_2",
          "output_layer_a")
@@ -119,8 +119,11 @@ def _lin_relu(x, w, b):
     """relu(x W^T + b). Without grad on the device it is one hipBLASLt GEMM with the bias + ReLU
     epilogue (torch._addmm_activation) instead of a GEMM and a clamp launch (4-5 us each, 18 per
     Rainbow iteration in the act and target forwards)."""
-    if _RELU_EPILOGUE and not torch.is_grad_enabled() and x.is_cuda and x.dim() == 2:
-        return torch._addmm_activation(b, x, w.t())
+    if _RELU_EPILOGUE and x.is_cuda and x.dim() == 2:
+        if not torch.is_grad_enabled():
+            return torch._addmm_activation(b, x, w.t())
+        if _SPLITK and x.shape[0] >= SPLITK_MIN_ROWS:
+            return _SplitKLinearReLU.apply(x, w, b)
     return F.relu(_lin(x, w, b))
 
 

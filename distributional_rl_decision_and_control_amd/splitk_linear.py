@@ -23,6 +23,25 @@ def _groups(rows):
     return g
 
 
+def _splitk_grads(ctx, x, weight, gy):
+    gx = gw = gb = None
+    if ctx.needs_input_grad[0]:
+        gx = gy.matmul(weight.to(gy.dtype))
+    rows = x.shape[0]
+    if ctx.needs_input_grad[1]:
+        g = _groups(rows)
+        xs = x.reshape(g, rows // g, x.shape[1])
+        ys = gy.reshape(g, rows // g, gy.shape[1])
+        gw = torch.bmm(ys.transpose(1, 2), xs.to(ys.dtype)).sum(0, dtype=torch.float32).to(weight.dtype)
+    if ctx.has_bias and ctx.needs_input_grad[2]:
+        if _BIAS_TWO_STAGE:
+            g = _groups(rows)
+            gb = gy.reshape(g, rows // g, gy.shape[1]).sum(1, dtype=torch.float32).sum(0).to(gy.dtype)
+        else:
+            gb = gy.sum(0, dtype=torch.float32).to(gy.dtype)
+    return gx, gw, gb
+
+
 class _SplitKLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
@@ -33,22 +52,24 @@ class _SplitKLinear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x, weight = ctx.saved_tensors
-        gx = gw = gb = None
-        if ctx.needs_input_grad[0]:
-            gx = gy.matmul(weight.to(gy.dtype))
-        rows = x.shape[0]
-        if ctx.needs_input_grad[1]:
-            g = _groups(rows)
-            xs = x.reshape(g, rows // g, x.shape[1])
-            ys = gy.reshape(g, rows // g, gy.shape[1])
-            gw = torch.bmm(ys.transpose(1, 2), xs.to(ys.dtype)).sum(0, dtype=torch.float32).to(weight.dtype)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            if _BIAS_TWO_STAGE:
-                g = _groups(rows)
-                gb = gy.reshape(g, rows // g, gy.shape[1]).sum(1, dtype=torch.float32).sum(0).to(gy.dtype)
-            else:
-                gb = gy.sum(0, dtype=torch.float32).to(gy.dtype)
-        return gx, gw, gb
+        return _splitk_grads(ctx, x, weight, gy)
+
+
+class _SplitKLinearReLU(torch.autograd.Function):
+    """relu(F.linear(x, weight, bias)) with the bias + ReLU in the GEMM epilogue
+    (torch._addmm_activation has no autograd formula of its own); fp32/bf16 2-D x, bias required."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        y = torch._addmm_activation(bias, x, weight.t())
+        ctx.save_for_backward(x, weight, y)
+        ctx.has_bias = True
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight, y = ctx.saved_tensors
+        return _splitk_grads(ctx, x, weight, torch.ops.aten.threshold_backward(gy, y, 0))
 
 
 ENABLED = os.environ.get("ASVRL_SPLITK", "1") != "0"
