@@ -102,13 +102,15 @@ class NoisyPack:
 
 
 _SPLITK = os.environ.get("ASVRL_RAINBOW_SPLITK", "1") != "0"
+# rows per split-K group: 1024 gave the shortest Rainbow step of 256/512/1024/2048 (rocprof A/B)
+_GROUP_ROWS = int(os.environ.get("ASVRL_RAINBOW_GROUP_ROWS", "1024"))
 
 
 def _lin(x, w, b):
     """F.linear; with grad on a batch of >= SPLITK_MIN_ROWS rows the weight gradient is a split-K
     batched GEMM (a single hipBLASLt call at K = 8192 leaves most CUs idle: 50 us per layer)."""
     if _SPLITK and torch.is_grad_enabled() and x.shape[0] >= SPLITK_MIN_ROWS and (w.requires_grad or x.requires_grad):
-        return _SplitKLinear.apply(x, w, b)
+        return _SplitKLinear.apply(x, w, b, _GROUP_ROWS)
     return F.linear(x, w, b)
 
 
@@ -123,7 +125,7 @@ def _lin_relu(x, w, b):
         if not torch.is_grad_enabled():
             return torch._addmm_activation(b, x, w.t())
         if _SPLITK and x.shape[0] >= SPLITK_MIN_ROWS:
-            return _SplitKLinearReLU.apply(x, w, b)
+            return _SplitKLinearReLU.apply(x, w, b, _GROUP_ROWS)
     return F.relu(_lin(x, w, b))
 
 
