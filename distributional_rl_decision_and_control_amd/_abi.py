@@ -11,7 +11,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ASVRL_LIB", os.path.join(HERE, "lib", "libasvrl.so"))  # override: A/B variants
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
 OBS_DIM = 40   # self 7 | objects 25 | mask 5 | pad 3
@@ -74,6 +74,13 @@ class AsvResetCfg(C.Structure):
                 ("min_start_goal_dis", C.c_double), ("width", C.c_double), ("height", C.c_double),
                 ("clear_r", C.c_double), ("obs_r_lo", C.c_double), ("obs_r_hi", C.c_double), ("v_lo", C.c_double),
                 ("v_hi", C.c_double), ("v_rel_max", C.c_double), ("p_rel", C.c_double)]
+
+
+class AsvEnvLaunch(C.Structure):
+    _fields_ = [("layout", C.c_int32), ("block", C.c_int32), ("envs_per_block", C.c_int32), ("_pad0", C.c_int32)]
+
+
+ENV_LAYOUT_AUTO, ENV_LAYOUT_PAIRS, ENV_LAYOUT_SWEEP = 0, 1, 2
 
 
 class AsvCriticWeights(C.Structure):
@@ -188,6 +195,8 @@ class AsvRainbowHeadIO(C.Structure):
 EXPORTS = [
     ("asvrl_env_step", C.c_int, [C.POINTER(AsvParams), C.POINTER(AsvEnvState), _VP, _VP, C.POINTER(AsvStepCtl),
                                  C.POINTER(AsvStepOut), _VP]),
+    ("asvrl_env_step_ex", C.c_int, [C.POINTER(AsvParams), C.POINTER(AsvEnvState), _VP, _VP, C.POINTER(AsvStepCtl),
+                                    C.POINTER(AsvStepOut), C.POINTER(AsvEnvLaunch), _VP]),
     ("asvrl_env_reset", C.c_int, [C.POINTER(AsvParams), C.POINTER(AsvEnvState), C.POINTER(AsvResetCfg), _VP, _U64,
                                   _U64, _VP, _VP]),
     ("asvrl_current_field", C.c_int, [_VP, _I32, _D, _VP, _I32, _VP, _VP]),

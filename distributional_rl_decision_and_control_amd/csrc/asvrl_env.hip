@@ -11,7 +11,7 @@
 // across all four waves (noisy observation, detection, collision, sort key into LDS), and phase 2b
 // merges each robot's candidates in the reference's order (stable top-5 insertion), then COLREGs,
 // reward, done/info and -- in the fused training loop -- trainer.py's deactivation and the
-// episode-end test, reduced per env through LDS. (ASVRL_ENV_PAIRS=0: the per-robot sweep, phase 2
+// episode-end test, reduced per env through LDS. (AsvEnvLaunch layout 2: the per-robot sweep, phase 2
 // as one serial loop per lane, 64-lane groups.)
 //
 // Arithmetic follows the reference's operation order (np.matrix products as explicit row
@@ -204,7 +204,8 @@ __device__ inline void cswap(bool cond, Cand& x, Cand& y) {
 // observation, detection, collision and sort key of one candidate into LDS, then each robot lane
 // merges its candidates in the reference's order (stable top-5 insertion, collision as an OR), so the
 // kept objects and masks are the serial sweep's exactly; the Philox draws (noise modes 1, 2) are keyed
-// by (robot, candidate slot) instead of one stream per robot. `epb_arg` envs per workgroup (PAIRS).
+// by (robot, candidate slot) in both layouts, so results do not depend on the launch shape.
+// `epb_arg` envs per workgroup (PAIRS).
 template <int BLOCK, bool PAIRS>
 __global__ __launch_bounds__(BLOCK) void env_step_kernel(AsvParams p, AsvEnvState s,
                                                           const double* __restrict__ actions,
@@ -466,10 +467,6 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(AsvParams p, AsvEnvStat
     const double* nz_base =
         noise != nullptr ? noise + idx * static_cast<size_t>(O + R) * 5 : nullptr;
     const uint64_t ctr = ctl.counter + (ctl.counter_dev != nullptr ? *ctl.counter_dev : 0ull);
-    Stream rng(ctl.seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull, static_cast<uint32_t>(idx),
-               static_cast<uint32_t>(idx >> 32) ^ 0x5EEDu, static_cast<uint32_t>(ctr));
-    StreamF rngf(ctl.seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull, static_cast<uint32_t>(idx),
-                 static_cast<uint32_t>(idx >> 32) ^ 0xF32Au, static_cast<uint32_t>(ctr));
     const int ncand = no + nrob;
     const bool full_circle = 0.5 * p.angle >= kPi;
     for (int k = 0; k < ncand; ++k) {
@@ -498,11 +495,18 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(AsvParams p, AsvEnvStat
         const double* nz = nz_base + slot * 5;
         n0 = nz[0]; n1 = nz[1]; n2 = nz[2]; n3 = nz[3]; n4 = nz[4];
       } else if (ctl.noise_mode == 1) {
+        // the pair layout's substream of (robot, candidate slot): both layouts draw the same noise
+        Stream rng(ctl.seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull, static_cast<uint32_t>(idx),
+                   (static_cast<uint32_t>(idx >> 32) ^ 0x5EEDu) + (static_cast<uint32_t>(slot) << 20),
+                   static_cast<uint32_t>(ctr));
         rng.normal2(n0, n1);
         rng.normal2(n2, n3);
         n0 *= p.pos_std; n1 *= p.pos_std; n2 *= p.vel_std; n3 *= p.vel_std;
         n4 = rng.vonmises(p.r_kappa);
       } else {
+        StreamF rngf(ctl.seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull, static_cast<uint32_t>(idx),
+                     (static_cast<uint32_t>(idx >> 32) ^ 0xF32Au) + (static_cast<uint32_t>(slot) << 20),
+                     static_cast<uint32_t>(ctr));
         float f0, f1, f2, f3;
         rngf.normal2(f0, f1);
         rngf.normal2(f2, f3);
@@ -870,32 +874,24 @@ size_t env_step_smem(int R, int O) {
 }
 
 // the pair-parallel launch: workgroup size from the pair count, envs per workgroup so that the
-// pairs fill it (at least one env); ASVRL_ENV_EPB overrides the envs per workgroup (tuning)
+// pairs fill it (at least one env); AsvEnvLaunch may set the block and the envs per workgroup
 struct PairLaunch {
   int blk, epb;
   size_t smem;
 };
-PairLaunch pair_launch(int R, int O) {
+PairLaunch pair_launch(int R, int O, int blk_req, int epb_req) {
   const int np1 = R * (O + R);
   PairLaunch L;
   // the robots of the workgroup's envs fill its first wave (dynamics, merge, COLREGs run per robot:
   // every wave issues them whatever its active lanes, so robots are packed densely); the pairs then
   // spread over all four waves
-  static const int blk_env = [] {
-    const char* v = getenv("ASVRL_ENV_BLK");
-    return v != nullptr ? atoi(v) : 0;
-  }();
-  static const int epb_env = [] {
-    const char* v = getenv("ASVRL_ENV_EPB");
-    return v != nullptr ? atoi(v) : 0;
-  }();
-  L.blk = (blk_env == 64 || blk_env == 128 || blk_env == 256) ? blk_env : 256;
+  L.blk = (blk_req == 64 || blk_req == 128 || blk_req == 256) ? blk_req : 256;
   if (R > L.blk) L.blk = 256;
   // about 40 robots per workgroup: measured best at 4096 envs (R = 5: 8 envs, 34 us vs 58 us for the
   // per-robot sweep; R = 17: 3 envs, 133 us vs 203 us); more envs per group trade latency for
   // throughput at very large batches (tools/env_ab3.sh)
   L.epb = R <= 64 ? ((40 + R - 1) / R < 64 / R ? (40 + R - 1) / R : 64 / R) : 1;
-  if (epb_env > 0) L.epb = epb_env;
+  if (epb_req > 0) L.epb = epb_req;
   if (L.epb * R > L.blk) L.epb = L.blk / R;
   const size_t np = static_cast<size_t>(L.epb) * np1;
   L.smem = sizeof(double) * (8 * static_cast<size_t>(L.blk) + 6 * np + static_cast<size_t>(L.epb) * O * 3) +
@@ -907,9 +903,9 @@ PairLaunch pair_launch(int R, int O) {
 
 using namespace asvrl;
 
-extern "C" int asvrl_env_step(const AsvParams* params, const AsvEnvState* state, const double* actions,
-                              const double* noise, const AsvStepCtl* ctl, const AsvStepOut* out,
-                              void* stream) {
+extern "C" int asvrl_env_step_ex(const AsvParams* params, const AsvEnvState* state, const double* actions,
+                                 const double* noise, const AsvStepCtl* ctl, const AsvStepOut* out,
+                                 const AsvEnvLaunch* launch, void* stream) {
   ASVRL_REQUIRE(params && state && ctl && out, "asvrl_env_step: null argument");
   ASVRL_REQUIRE(state->max_robots >= 1 && state->max_robots <= kBlock, "asvrl_env_step: max_robots must be in [1, 256]");
   ASVRL_REQUIRE(state->max_obs >= 0 && state->max_cores >= 0 && state->max_cores <= kMaxCores,
@@ -922,12 +918,15 @@ extern "C" int asvrl_env_step(const AsvParams* params, const AsvEnvState* state,
   ASVRL_REQUIRE(state->rs && state->rflags && state->n_robots && state->n_obs && state->n_cores && state->ep_ts,
                 "asvrl_env_step: null state array");
   if (state->n_envs == 0) return 0;
-  static const bool pairs_env = [] {
-    const char* v = getenv("ASVRL_ENV_PAIRS");   // 0: the per-robot sweep (A/B)
-    return v == nullptr || v[0] != '0';
-  }();
-  const PairLaunch pl = pair_launch(state->max_robots, state->max_obs);
-  if (pairs_env && pl.smem <= 150 * 1024) {
+  const AsvEnvLaunch lz{};
+  const AsvEnvLaunch& lc = launch != nullptr ? *launch : lz;
+  ASVRL_REQUIRE(lc.layout >= 0 && lc.layout <= 2, "asvrl_env_step: layout must be 0 (auto), 1 (pairs) or 2 (sweep)");
+  ASVRL_REQUIRE(lc.block == 0 || lc.block == 64 || lc.block == 128 || lc.block == 256,
+                "asvrl_env_step: block must be 0, 64, 128 or 256");
+  ASVRL_REQUIRE(lc.envs_per_block >= 0, "asvrl_env_step: negative envs_per_block");
+  const PairLaunch pl = pair_launch(state->max_robots, state->max_obs, lc.block, lc.envs_per_block);
+  ASVRL_REQUIRE(lc.layout != 1 || pl.smem <= 150 * 1024, "asvrl_env_step: the pair layout's LDS does not fit");
+  if (lc.layout != 2 && pl.smem <= 150 * 1024) {
     const int grid = (state->n_envs + pl.epb - 1) / pl.epb;
     if (pl.blk == 64)
       hipLaunchKernelGGL((env_step_kernel<64, true>), dim3(grid), dim3(64), pl.smem, as_stream(stream), *params,
@@ -952,6 +951,11 @@ extern "C" int asvrl_env_step(const AsvParams* params, const AsvEnvState* state,
     hipLaunchKernelGGL((env_step_kernel<256, false>), dim3(grid), dim3(256), smem, as_stream(stream), *params,
                        *state, actions, noise, *ctl, *out, epb);
   return check_launch("asvrl_env_step");
+}
+
+extern "C" int asvrl_env_step(const AsvParams* params, const AsvEnvState* state, const double* actions,
+                              const double* noise, const AsvStepCtl* ctl, const AsvStepOut* out, void* stream) {
+  return asvrl_env_step_ex(params, state, actions, noise, ctl, out, nullptr, stream);
 }
 
 extern "C" int asvrl_env_reset(const AsvParams* params, const AsvEnvState* state, const AsvResetCfg* cfg,

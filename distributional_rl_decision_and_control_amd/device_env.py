@@ -72,9 +72,10 @@ class DeviceEnvBatch:
     # ------------------------------------------------------------------ launches
     def step(self, actions, is_continuous=True, noise=None, do_dynamics=True, trainer_deactivate=False,
              seed=0, counter=0, counter_dev=None, gamma=0.0, env_mask=None, obs=None, obj_cnt=None, stream=None,
-             fast_noise=False):
+             fast_noise=False, launch=None):
         """asvrl_env_step. actions: f64 [E*R, 2] device tensor. noise: f64 [E*R, O+R, 5] or None (Philox;
-        fast_noise: f32 draws, noise_mode 2)."""
+        fast_noise: f32 draws, noise_mode 2). launch: (layout, block, envs_per_block) of the kernel
+        (asvrl_env_step_ex; _abi.ENV_LAYOUT_*), None = automatic."""
         ctl = _abi.AsvStepCtl()
         ctl.is_continuous = int(bool(is_continuous))
         ctl.do_dynamics = int(bool(do_dynamics))
@@ -93,8 +94,13 @@ class DeviceEnvBatch:
             assert noise.numel() >= self.n_envs * self.max_robots * (self.max_obs + self.max_robots) * 5
         st = self.state_struct()
         out = self.out_struct(obs, obj_cnt, with_env_done=trainer_deactivate)
-        rc = _abi.lib().asvrl_env_step(C.byref(self.params), C.byref(st), _abi.ptr(actions), _abi.ptr(noise),
-                                       C.byref(ctl), C.byref(out), _abi.stream_ptr(stream))
+        if launch is None:
+            rc = _abi.lib().asvrl_env_step(C.byref(self.params), C.byref(st), _abi.ptr(actions), _abi.ptr(noise),
+                                           C.byref(ctl), C.byref(out), _abi.stream_ptr(stream))
+        else:
+            ln = _abi.AsvEnvLaunch(*(int(v) for v in launch))
+            rc = _abi.lib().asvrl_env_step_ex(C.byref(self.params), C.byref(st), _abi.ptr(actions), _abi.ptr(noise),
+                                              C.byref(ctl), C.byref(out), C.byref(ln), _abi.stream_ptr(stream))
         _abi.check(rc, "asvrl_env_step")
 
     def reset(self, cfg, env_mask=None, seed=0, counter=0, counter_dev=None, stream=None):

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 10
+#define ASVRL_ABI_VERSION 11
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -151,6 +151,25 @@ typedef struct AsvResetCfg {
 int asvrl_env_step(const AsvParams* params, const AsvEnvState* state, const double* actions,
                    const double* noise, const AsvStepCtl* ctl, const AsvStepOut* out,
                    void* stream);
+
+/* Launch shape of the env-step kernel (asvrl_env_step_ex). Zero members mean "choose":
+ *   layout 0: automatic (pair-parallel perception when its LDS fits, else the per-robot sweep),
+ *          1: pair-parallel (one lane per (robot, candidate) pair; fails if the LDS does not fit),
+ *          2: per-robot sweep (one lane per robot, candidates in a serial loop);
+ *   block  threads per workgroup of the pair layout (64, 128 or 256);
+ *   envs_per_block  envs per workgroup of the pair layout (0: about 40 robots per group). */
+typedef struct AsvEnvLaunch {
+  int32_t layout;
+  int32_t block;
+  int32_t envs_per_block;
+  int32_t _pad0;
+} AsvEnvLaunch;
+
+/* asvrl_env_step with an explicit kernel shape (tests of every shipped layout, A/B tools);
+ * launch == NULL is asvrl_env_step. Results do not depend on the shape. */
+int asvrl_env_step_ex(const AsvParams* params, const AsvEnvState* state, const double* actions,
+                      const double* noise, const AsvStepCtl* ctl, const AsvStepOut* out,
+                      const AsvEnvLaunch* launch, void* stream);
 
 /* MarineNavEnv3.reset (env.py:72-164) for envs with env_mask != 0, sampled on the device
  * with Philox (same rejection rules and iteration caps; not the reference's RandomState

@@ -218,3 +218,27 @@ def trace_step_inputs(tr, t):
                 obstacles=tr["obstacles"], n_obs=int(tr["n_obs"]), O=O, cores=tr["cores"],
                 n_cores=int(tr["n_cores"]), actions=tr["actions"][t][:n], noise=noise_full,
                 ep_ts=int(tr["ep_ts"][t]), R=R)
+
+
+def trainer_bookkeeping(rewards, deact_before, collision, reach, ep_ts, gamma=0.99, episode_limit=1000):
+    """Trainer.learn's per-step bookkeeping (rfarl/rfarl/policy/trainer.py:157-172) over a trace:
+    ep_rewards[i] += gamma ** ep_length * r_i for every robot not deactivated before the step,
+    then deactivation on collision or goal, then end_episode = ep_length >= 1000 or all
+    deactivated. rewards [T][n], deact_before [T][n], collision / reach [T][n] (flags after the
+    step), ep_ts [T] (the env's episode_timesteps before the step = the trainer's ep_length).
+    Returns (ep_return [T][n], deact_after [T][n], end_episode [T])."""
+    T, n = np.asarray(rewards).shape
+    ret = np.zeros(n)
+    rets, deacts, ends = np.zeros((T, n)), np.zeros((T, n), np.uint8), np.zeros(T, np.uint8)
+    for t in range(T):
+        deact = np.asarray(deact_before[t][:n]).astype(bool).copy()
+        ep_length = int(ep_ts[t])
+        for i in range(n):
+            if deact[i]:
+                continue
+            ret[i] += gamma ** ep_length * float(rewards[t][i])
+            if collision[t][i] or reach[t][i]:
+                deact[i] = True
+        rets[t], deacts[t] = ret, deact
+        ends[t] = (ep_length >= episode_limit) or bool(deact.all())
+    return rets, deacts, ends

@@ -35,7 +35,7 @@ def _batch_from_traces(traces, continuous):
     return rows
 
 
-def _run_rows(rows, continuous):
+def _run_rows(rows, continuous, launch=None):
     from distributional_rl_decision_and_control_amd.device_env import DeviceEnvBatch
     from distributional_rl_decision_and_control_amd import _abi
 
@@ -88,7 +88,7 @@ def _run_rows(rows, continuous):
     b.cores.copy_(torch.from_numpy(cores))
     a_d = torch.from_numpy(acts).to(dev)
     n_d = torch.from_numpy(noise).to(dev)
-    b.step(a_d, is_continuous=continuous, noise=n_d)
+    b.step(a_d, is_continuous=continuous, noise=n_d, launch=launch)
     torch.cuda.synchronize()
     return b, R
 
@@ -145,12 +145,19 @@ def _check_rows(rows, b, R):
     return worst
 
 
+# every shipped kernel layout (asvrl_env_step_ex): the automatic choice (pair-parallel at these
+# sizes), the per-robot sweep (the automatic fallback when the pair layout's LDS does not fit,
+# e.g. R ~ 64) and a non-default pair shape (128 threads, 2 envs per workgroup)
+LAYOUTS = {"auto": None, "sweep": (2, 0, 0), "pairs_b128_e2": (1, 128, 2)}
+
+
+@pytest.mark.parametrize("layout", list(LAYOUTS))
 @pytest.mark.parametrize("continuous", [True, False])
-def test_env_step_matches_reference_traces(continuous):
+def test_env_step_matches_reference_traces(continuous, layout):
     traces = eo.load_traces()
     rows = _batch_from_traces(traces, continuous)
     assert len(rows) > 0
-    b, R = _run_rows(rows, continuous)
+    b, R = _run_rows(rows, continuous, LAYOUTS[layout])
     worst = _check_rows(rows, b, R)
     print("worst relative errors:", worst)
 
@@ -332,3 +339,58 @@ def test_philox_perception_noise_distribution(fast):
     # the full shape of the von Mises draw: KS against scipy
     vm = (rr - 0.8) / 0.2 * np.pi
     assert stats.kstest(vm[:20000], stats.vonmises(1.0).cdf).pvalue > 1e-3
+
+
+def test_config5_full_size():
+    """BASELINE config 5 at full size: 4096 envs x 17 vehicles (ego + 16), 4 buoys, 110 m map
+    (the reference's 55 m map cannot place 17 robots, env.py:33-40,106-120).
+    Device reset, 50 Philox (f32 noise, the training path) steps with the trainer bookkeeping, on
+    both kernel layouts (pair-parallel and the per-robot sweep must agree bit for bit: same Philox
+    substreams, same operation order), then the fused rollout + AC-IQN learn loop (B = 4096,
+    N = 32) for a few iterations: every env gets all 17 robots, invariants hold, losses finite."""
+    from distributional_rl_decision_and_control_amd import _abi
+    from distributional_rl_decision_and_control_amd.device_env import DeviceEnvBatch, reset_cfg
+    from distributional_rl_decision_and_control_amd.vec_trainer import VecTrainer
+    E, R, O, W = 4096, 17, 4, 110.0
+
+    def run(launch):
+        b = DeviceEnvBatch(E, R, O, 0)
+        b.reset(reset_cfg(R, O, 0, 40.0, width=W, height=W), seed=5)
+        b.step(None, do_dynamics=False, seed=5, counter=0, fast_noise=True, launch=launch)
+        g = torch.Generator(device="cuda").manual_seed(4)
+        outs = []
+        for t in range(50):
+            a = (torch.rand((E * R, 2), generator=g, device="cuda", dtype=torch.float64) * 2 - 1).contiguous()
+            prev_fl, prev_rs = b.rflags.clone(), b.rs.clone()
+            b.step(a, seed=5, counter=t + 1, trainer_deactivate=True, gamma=0.99, fast_noise=True, launch=launch)
+            th = b.rs[_abi.F_THETA]
+            assert bool(((th >= 0) & (th < 2 * np.pi)).all())
+            was_off = (prev_fl & _abi.FLAG_DEACTIVATED) > 0
+            assert torch.equal(b.rs[:13][:, was_off], prev_rs[:13][:, was_off])
+            cnt = b.obj_cnt.view(E, R)
+            assert int(cnt.max().item()) <= 5
+            outs.append(torch.cat([b.reward, b.rs[_abi.F_RET], b.obs.reshape(-1).double(),
+                                   b.rflags.double(), b.env_done.double()]))
+        return b, torch.stack(outs)
+
+    b, o_pairs = run(None)
+    assert (b.n_robots.cpu().numpy() == R).all(), "every env must place all 17 robots on the 110 m map"
+    assert (b.n_obs.cpu().numpy() == O).all()
+    _, o_sweep = run((_abi.ENV_LAYOUT_SWEEP, 0, 0))
+    assert torch.equal(o_pairs, o_sweep), "pair-parallel and per-robot-sweep layouts differ"
+    # perception keeps up to 5 of the 20 candidates; every count 0..5 occurs at this size
+    cnt = b.obj_cnt.cpu().numpy()
+    assert all((cnt == k).any() for k in range(6)), np.bincount(cnt[cnt >= 0], minlength=6)
+
+    tr = VecTrainer(n_envs=E, agent_type="AC-IQN", num_robots=R, num_obs=O, width=W, batch_size=4096, num_tau=32,
+                    seed=5, buffer_size=E * R * 8)
+    while tr.replay_size_host() < tr.learning_starts:
+        tr.iteration()
+    p0 = torch.cat([p.detach().reshape(-1) for p in tr.local.critic.parameters()]).clone()
+    for _ in range(3):
+        out = tr.iteration()
+    torch.cuda.synchronize()
+    losses = [float(x.item()) for x in out[:2]]
+    assert np.all(np.isfinite(losses)), losses
+    p1 = torch.cat([p.detach().reshape(-1) for p in tr.local.critic.parameters()])
+    assert bool(torch.isfinite(p1).all()) and not torch.equal(p0, p1)

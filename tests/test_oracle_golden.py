@@ -64,6 +64,21 @@ def test_oracle_env_step_traces(name):
         assert out["ep_ts"] == tr["ep_ts"][t] + 1
 
 
+@pytest.mark.parametrize("name", list(eo.load_traces().keys()))
+def test_oracle_trainer_bookkeeping(name):
+    """Discounted returns, deactivation and episode end (trainer.py:157-172) as the reference
+    trainer computed them during the capture: returns bit-exact, masks exact."""
+    tr = eo.load_traces()[name]
+    n = int(tr["n_robots"])
+    ret, deact, end = eo.trainer_bookkeeping(tr["reward"][:, :n], tr["deact_before"][:, :n], tr["collision"][:, :n],
+                                             tr["reach"][:, :n], tr["ep_ts"])
+    np.testing.assert_array_equal(ret, tr["ep_return"][:, :n])
+    np.testing.assert_array_equal(deact, tr["deact_after"][:, :n])
+    np.testing.assert_array_equal(end, tr["end_episode"])
+    # the next step's deactivation mask is this step's trainer output
+    np.testing.assert_array_equal(tr["deact_after"][:-1, :n], tr["deact_before"][1:, :n])
+
+
 def test_traces_cover_every_branch():
     """The fixture set exercises collisions, goals, timeouts, COLREGs, cores, discrete."""
     tr = eo.load_traces()
@@ -72,6 +87,9 @@ def test_traces_cover_every_branch():
         assert (allinfo == code).any(), code
     assert sum(int(t["apply_colregs"].sum()) for t in tr.values()) > 20
     assert any(int(t["n_cores"]) > 0 for t in tr.values())
+    # episode ends by all-deactivated (goal and crowd traces) and by the 1000-step limit
+    assert sum(int(t["end_episode"].sum()) for t in tr.values()) >= 3
+    assert int(tr["timeout_r5o4_s7"]["end_episode"].sum()) >= 1
 
 
 @pytest.mark.parametrize("tag", ["b64", "b1024"])

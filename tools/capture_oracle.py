@@ -155,7 +155,13 @@ def run_trace(env, n_steps, action_fn, continuous, R, O, ep_ts_override=None,
     n = len(env.robots)
     rec = {k: [] for k in ["state_before", "state_after", "deact_before", "actions", "noise",
                            "self_obs", "obj_obs", "obj_cnt", "obs_valid", "collision", "reach",
-                           "apply_colregs", "phi", "reward", "done", "info", "ep_ts"]}
+                           "apply_colregs", "phi", "reward", "done", "info", "ep_ts",
+                           "ep_return", "deact_after", "end_episode"]}
+    # Trainer.learn's per-episode bookkeeping (trainer.py:96-98,157-172), GAMMA = Agent.GAMMA
+    # default (agent.py:23). ep_length is the env's episode_timesteps before the step (equal to the
+    # trainer's counter from a reset; the timeout trace starts it at ep_ts_override)
+    GAMMA = 0.99
+    ep_rewards = np.zeros(R)
     static = dict(
         obstacles=np.array([[o.x, o.y, o.r] for o in env.obstacles] + [[0, 0, 0]] * (O - len(env.obstacles)), dtype=np.float64).reshape(O, 3),
         n_obs=len(env.obstacles),
@@ -219,10 +225,21 @@ def run_trace(env, n_steps, action_fn, continuous, R, O, ep_ts_override=None,
                      ("collision", coll), ("reach", reach), ("apply_colregs", app), ("phi", phi),
                      ("reward", rw), ("done", dn), ("info", inf), ("ep_ts", ep_ts)]:
             rec[k].append(v)
-        # trainer-side deactivation (trainer.py:168-170)
+        # trainer.py:157-172: discounted return of every robot active this step, then the
+        # deactivation on collision / goal, then the episode-end test
+        ep_length = ep_ts
         for i, r in enumerate(env.robots):
-            if not r.deactivated and (r.collision or r.reach_goal):
+            if r.deactivated:
+                continue
+            ep_rewards[i] += GAMMA ** ep_length * rew[i]
+            if r.collision or r.reach_goal:
                 r.deactivated = True
+        end_episode = (ep_length >= 1000) or env.check_all_deactivated()
+        da = np.zeros(R, np.uint8)
+        da[:n] = [bool(r.deactivated) for r in env.robots]
+        rec["ep_return"].append(ep_rewards.copy())
+        rec["deact_after"].append(da)
+        rec["end_episode"].append(np.uint8(end_episode))
     out = {k: np.array(v) for k, v in rec.items()}
     out.update({k: np.array(v) for k, v in static.items()})
     return out
