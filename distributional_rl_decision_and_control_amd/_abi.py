@@ -11,6 +11,9 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ASVRL_LIB", os.path.join(HERE, "lib", "libasvrl.so"))  # override: A/B variants
+# the same sources built with f32 learner operands (the parity build; asvrl_operand_bytes() == 4)
+LIB_PATH_F32 = os.path.join(HERE, "lib", "libasvrl_f32.so")
+OPERANDS = {"bf16": (LIB_PATH, 2), "f32": (LIB_PATH_F32, 4)}
 ABI_VERSION = 11
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
@@ -249,40 +252,54 @@ EXPORTS = [
     ("asvrl_small_wgrad", C.c_int, [_VP, _I64, _VP, _I64, _I32, _I32, _I32, _VP, _VP, _I32, _VP, _I64, _VP]),
     ("asvrl_last_error", C.c_char_p, []),
     ("asvrl_abi_version", C.c_int, []),
+    ("asvrl_operand_bytes", C.c_int32, []),
     ("asvrl_struct_sizes", None, [C.c_void_p]),
 ]
 
-_lib = None
+_libs = {}
 
 
 class AsvrlError(RuntimeError):
     pass
 
 
-def lib():
-    """Load libasvrl.so (built by __graft_entry__.build / `python -m ...build`). Raises if absent."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise AsvrlError(f"libasvrl.so not found at {LIB_PATH}: build it with "
+def lib(operands="bf16"):
+    """Load libasvrl.so (operands="bf16", the product) or libasvrl_f32.so (operands="f32", the
+    f32-operand parity build of the same sources), built by __graft_entry__.build /
+    `python -m ...build`. Raises if absent: there is no CPU fallback."""
+    L = _libs.get(operands)
+    if L is not None:
+        return L
+    if operands not in OPERANDS:
+        raise ValueError(f"operands must be one of {sorted(OPERANDS)}")
+    path, nbytes = OPERANDS[operands]
+    if not os.path.exists(path):
+        raise AsvrlError(f"{os.path.basename(path)} not found at {path}: build it with "
                          "`python -m distributional_rl_decision_and_control_amd.build` (hipcc, gfx950). "
                          "There is no CPU fallback.")
-    L = C.CDLL(LIB_PATH)
+    L = C.CDLL(path)
     for name, res, args in EXPORTS:
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
     v = L.asvrl_abi_version()
     if v != ABI_VERSION:
-        raise AsvrlError(f"libasvrl.so ABI {v} != expected {ABI_VERSION}; rebuild")
-    _lib = L
+        raise AsvrlError(f"{os.path.basename(path)} ABI {v} != expected {ABI_VERSION}; rebuild")
+    if L.asvrl_operand_bytes() != nbytes:
+        raise AsvrlError(f"{path}: operand element of {L.asvrl_operand_bytes()} bytes, expected {nbytes}")
+    _libs[operands] = L
     return L
 
 
-def check(rc, what=""):
+def operand_dtype(operands="bf16"):
+    """torch dtype of the weight images / saved activations of a learner-kernel build."""
+    import torch
+    return {"bf16": torch.bfloat16, "f32": torch.float32}[operands]
+
+
+def check(rc, what="", L=None):
     if rc != 0:
-        msg = lib().asvrl_last_error().decode(errors="replace")
+        msg = (L if L is not None else lib()).asvrl_last_error().decode(errors="replace")
         raise AsvrlError(f"{what} failed ({rc}): {msg}")
 
 

@@ -5,7 +5,12 @@ training, memory, policy_local/policy_target), act_* / train / soft_update /
 save_latest_model / load_model surfaces and return types. Differences:
   * tensors live on the GPU: `device="cpu"` (the reference default) selects the current
     HIP device -- the kernels have no CPU implementation and no CPU fallback;
-  * train_* run the fused gfx950 quantile-Huber / C51 kernels (learner.py);
+  * train_AC_IQN / train_IQN run the hand-written learner of the batched trainer
+    (fused_update.ac_iqn_update_fused2, fused_iqn.iqn_update_fused) built with f32 operands
+    (libasvrl_f32.so: the reference's fp32 arithmetic, pinned to its train_* outputs at 1e-5 by
+    tests/test_learner_golden_gpu.py and test_agent_gpu.py); set_learner("fused-bf16") selects the
+    bf16-operand training build, set_learner("torch") the torch-autograd restatement with the HIP
+    quantile-Huber kernel (learner.py). train_Rainbow runs learner.rainbow_update (C51 kernel);
   * load_model rebuilds the optimizers for the loaded networks (the reference keeps
     optimizing the replaced ones, agent.py:684-698 vs :75-76,98);
   * DQN runs as the reference's plain torch update (BASELINE config 1 is the DQN plumbing run of
@@ -19,7 +24,9 @@ import torch
 import torch.nn.functional as F
 
 from . import _abi
-from .learner import FlatGrads, ac_iqn_update, iqn_update, rainbow_update
+from . import fused_iqn, fused_update
+from .learn_ops import rows_from_batch
+from .learner import FlatGrads, FusedAdam, ac_iqn_update, iqn_update, rainbow_update
 from .policy.AC_IQN_model import AC_IQN_Policy
 from .policy.DQN_model import DQN_Policy
 from .policy.IQN_model import IQN_Policy
@@ -29,6 +36,10 @@ from .utils.replay_buffer import ReplayBuffer
 
 DISTRIBUTIONAL = ("AC-IQN", "IQN", "Rainbow")
 SUPPORTED = DISTRIBUTIONAL + ("DQN",)
+# learners of train_AC_IQN / train_IQN: the hand-written kernels with f32 operands (default, the
+# reference's arithmetic), the same kernels with bf16 operands (the batched trainer's build), or
+# the torch-autograd restatement
+LEARNERS = {"fused-f32": "f32", "fused-bf16": "bf16", "torch": None}
 
 
 def resolve_device(device):
@@ -60,6 +71,8 @@ class Agent:
         self.agent_type = agent_type
         self.num_tau = 8  # training quantiles N = N' (AC_IQN_model.py:462, IQN_model.py:74)
         self.tau_override = None  # optional list of pre-drawn taus for the next train() (tests)
+        self.learner = "fused-f32"
+        self._fused = None   # (B, N) -> FusedACIQNState / FusedIQNState, built on the first train()
         self._net_args = (self_dimension, object_dimension, max_object_num, self_feature_dimension,
                           object_feature_dimension, concat_feature_dimension, hidden_dimension)
         if agent_type not in SUPPORTED:
@@ -95,14 +108,48 @@ class Agent:
         return Rainbow_Policy(*a, action_size, 51, self.device, seed).to(self.device)
 
     def _make_optimizers(self):
+        """optim.Adam(lr) + clip 0.5 (agent.py:75-76,98): FusedAdam (asvrl_adam_*) of the learner's
+        operand build for AC-IQN / IQN, torch Adam for Rainbow / DQN."""
+        self._fused = None
+        ops = LEARNERS[self.learner] or "bf16"
         if self.agent_type == "AC-IQN":
-            self.critic_grads = FlatGrads(self.policy_local.critic.parameters())
-            self.actor_grads = FlatGrads(self.policy_local.actor.parameters())
-            self.actor_optimizer = torch.optim.Adam(self.policy_local.actor.parameters(), lr=self.LR)
-            self.critic_optimizer = torch.optim.Adam(self.policy_local.critic.parameters(), lr=self.LR)
+            self.actor_optimizer = FusedAdam(self.policy_local.actor.parameters(), lr=self.LR, operands=ops)
+            self.critic_optimizer = FusedAdam(self.policy_local.critic.parameters(), lr=self.LR, operands=ops)
+            self.actor_grads, self.critic_grads = self.actor_optimizer.grads, self.critic_optimizer.grads
+        elif self.agent_type == "IQN":
+            self.optimizer = FusedAdam(self.policy_local.parameters(), lr=self.LR, operands=ops)
+            self.grads = self.optimizer.grads
         else:
             self.grads = FlatGrads(self.policy_local.parameters())
             self.optimizer = torch.optim.Adam(self.policy_local.parameters(), lr=self.LR)
+
+    def set_learner(self, learner):
+        """Select train_AC_IQN / train_IQN's learner (LEARNERS); rebuilds the optimisers (fresh Adam
+        state, as load_model does)."""
+        if learner not in LEARNERS:
+            raise ValueError(f"learner must be one of {sorted(LEARNERS)}")
+        self.learner = learner
+        if self.training:
+            self._make_optimizers()
+
+    def _fused_state(self, B):
+        """The fused update's packs and buffers for batch B and N = self.num_tau, or None when the
+        torch learner is selected or the network shape is not the kernels' (supported())."""
+        ops = LEARNERS[self.learner]
+        if ops is None:
+            return None
+        key = (B, self.num_tau)
+        if self._fused is None or self._fused[0] != key:
+            if self.agent_type == "AC-IQN":
+                ok = fused_update.supported(self.policy_local, B, self.num_tau)
+                st = fused_update.FusedACIQNState(self.policy_local, self.policy_target, B, self.num_tau,
+                                                  operands=ops) if ok else None
+            else:
+                ok = fused_iqn.supported(self.policy_local, B, self.num_tau)
+                st = fused_iqn.FusedIQNState(self.policy_local, self.policy_target, B, self.num_tau,
+                                             operands=ops) if ok else None
+            self._fused = (key, st)
+        return self._fused[1]
 
     # ------------------------------------------------------------------ acting (agent.py:207-324)
     def state_to_tensor(self, states):
@@ -183,8 +230,21 @@ class Agent:
             return (None,) * k
         return tuple(torch.as_tensor(x, device=self.device, dtype=torch.float32) for x in t)
 
+    def _fused_taus(self, k, B):
+        t = self._taus(k)
+        if t[0] is None:
+            return None
+        return torch.stack([x.reshape(B, self.num_tau) for x in t]).contiguous()
+
     def train_AC_IQN(self):
         s, a, r, ns, d = self.memory.sample()
+        st = self._fused_state(s[0].shape[0])
+        if st is not None:   # the hand-written learner (agent.py:386-432)
+            B = s[0].shape[0]
+            cl, al, _, _ = fused_update.ac_iqn_update_fused2(
+                st, self.policy_local, self.actor_optimizer, self.critic_optimizer, self.critic_grads,
+                self.actor_grads, rows_from_batch(s, a, r, ns, d), gamma=self.GAMMA, taus=self._fused_taus(3, B))
+            return cl.cpu().numpy(), al.cpu().numpy()
         cl, al, _, _ = ac_iqn_update(self.policy_local, self.policy_target, self.actor_optimizer,
                                      self.critic_optimizer, self.critic_grads, self.actor_grads, s, a, r, ns, d,
                                      gamma=self.GAMMA, num_tau=self.num_tau, taus=self._taus(3))
@@ -192,6 +252,13 @@ class Agent:
 
     def train_IQN(self):
         s, a, r, ns, d = self.memory.sample()
+        st = self._fused_state(s[0].shape[0])
+        if st is not None:   # the hand-written learner (agent.py:434-476)
+            B = s[0].shape[0]
+            loss, _ = fused_iqn.iqn_update_fused(st, self.policy_local, self.optimizer, self.grads,
+                                                 rows_from_batch(s, a[:, :1], r, ns, d), gamma=self.GAMMA,
+                                                 taus=self._fused_taus(2, B))
+            return loss.cpu().numpy()
         loss, _ = iqn_update(self.policy_local, self.policy_target, self.optimizer, self.grads, s,
                              a[:, 0].to(torch.int64), r, ns, d, gamma=self.GAMMA, num_tau=self.num_tau,
                              taus=self._taus(2))
@@ -231,6 +298,8 @@ class Agent:
         with torch.no_grad():
             for t, l in pairs:
                 t.data.copy_(self.TAU * l.data + (1.0 - self.TAU) * t.data)
+        if self._fused is not None and self._fused[1] is not None:
+            self._fused[1].target_changed()   # re-pack the target networks' weight images
 
     def save_latest_model(self, directory):
         self.policy_local.save(directory)

@@ -1,6 +1,12 @@
-"""Build libasvrl.so for gfx950 in-tree (hipcc cross-compiles; no GPU needed).
+"""Build the gfx950 libraries in-tree (hipcc cross-compiles; no GPU needed).
 
     python -m distributional_rl_decision_and_control_amd.build [--force]
+
+lib/libasvrl.so      the product: learner kernels with bf16 MFMA operands, f32 accumulation
+lib/libasvrl_f32.so  the same sources with ASVRL_OPERAND_F32=1: every learner operand, weight image
+                     and saved activation f32 (v_mfma_f32_32x32x2_f32), the parity build that pins
+                     the hand-written learner to the reference's fp32 arithmetic
+Both are compiled concurrently.
 """
 import os
 import subprocess
@@ -14,6 +20,8 @@ SOURCES = [os.path.join(HERE, "csrc", f) for f in ("asvrl_env.hip", "asvrl_learn
 HEADERS = [os.path.join(HERE, "csrc", "asvrl_common.h"), os.path.join(HERE, "csrc", "asvrl_mfma.h"),
            os.path.join(ROOT, "include", "asvrl.h")]
 OUT = os.path.join(HERE, "lib", "libasvrl.so")
+OUT_F32 = os.path.join(HERE, "lib", "libasvrl_f32.so")
+VARIANTS = {OUT: [], OUT_F32: ["-DASVRL_OPERAND_F32=1"]}
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("ASVRL_OFFLOAD_ARCH", "gfx950")
 
@@ -23,23 +31,28 @@ FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17", "-ff
          "-munsafe-fp-atomics", "-I", os.path.join(ROOT, "include")]
 
 
-def stale():
-    if not os.path.exists(OUT):
+def stale(out):
+    if not os.path.exists(out):
         return True
-    t = os.path.getmtime(OUT)
+    t = os.path.getmtime(out)
     return any(os.path.getmtime(f) > t for f in SOURCES + HEADERS)
 
 
 def build_lib(force=False, verbose=False):
-    if not force and not stale():
-        return OUT
+    """Build every stale variant (concurrently); returns the product library's path."""
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    tmp = OUT + ".tmp"
-    cmd = [HIPCC] + FLAGS + ["-o", tmp] + SOURCES
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
-    os.replace(tmp, OUT)
+    procs = []
+    for out, extra in VARIANTS.items():
+        if not force and not stale(out):
+            continue
+        cmd = [HIPCC] + FLAGS + extra + ["-o", out + ".tmp"] + SOURCES
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((out, subprocess.Popen(cmd)))
+    for out, p in procs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, f"hipcc -> {out}")
+        os.replace(out + ".tmp", out)
     return OUT
 
 

@@ -109,9 +109,9 @@ constexpr int kFragWC = kC * kNcos / 8, kFragW1 = kH * kC / 8, kFragW2 = kH * kH
 // wc holds Wc's image for FWD and W2^T's for TRAIN / ACTOR (which then read Wc from global at the
 // top of the tile, before any store, and need W2^T after the activation stores have started)
 struct CriticLds {
-  bf16x8 wc[kFragWC];
-  bf16x8 w1[kFragW1];
-  bf16x8 w2[kFragW2];
+  frag8 wc[lds_frags(kFragWC)];
+  frag8 w1[lds_frags(kFragW1)];
+  frag8 w2[lds_frags(kFragW2)];
   float bc[kC], b1[kH], b2[kH], wo[kH];
 };
 static_assert(kFragWC == kFragW2, "the Wc / W2^T slot holds either image");
@@ -119,8 +119,8 @@ static_assert(kFragWC == kFragW2, "the Wc / W2^T slot holds either image");
 // IQN head in LDS: the padded 32 x 128 output image, output_layer.weight in f32 for the
 // backward (dh2 = W_out[a] dq) and the bias
 struct CriticLdsIqn : CriticLds {
-  bf16x8 wo_img[kH / 16 * 64];
-  __bf16 wof[kMaxA * kH];   // output_layer.weight (the backward's dh2 = W_out[a] dq feeds a bf16 dz2)
+  frag8 wo_img[kH / 16 * 64];
+  elem_t wof[kMaxA * kH];   // output_layer.weight (the backward's dh2 = W_out[a] dq feeds a bf16 dz2)
   float bo_a[kMaxA];
 };
 template <int MODE> struct LdsOf { using T = CriticLds; };
@@ -136,7 +136,7 @@ static_assert(sizeof(CriticLdsIqn) <= 160 * 1024, "IQN LDS image exceeds the CU'
 // (AC_IQN_model.py:468-470) or a copy of a.G. TRAIN also writes the bf16 obs copy for the encoder
 // weight gradient. Global loads only: this runs before any store of the tile.
 template <int NT, bool WITH_G, bool WITH_XB>
-__device__ __forceinline__ void stage_features(const CriticArgs& a, int tile, int lane, __bf16* Fw, float* Gw) {
+__device__ __forceinline__ void stage_features(const CriticArgs& a, int tile, int lane, elem_t* Fw, float* Gw) {
   constexpr int S = 32 / NT;
 #pragma unroll
   for (int k = 0; k < S; ++k) {
@@ -162,13 +162,13 @@ __device__ __forceinline__ void stage_features(const CriticArgs& a, int tile, in
           for (int i = 0; i < kObjIn; ++i) d += w[i] * xo[i];
           v = x[kObsMask + o] < 0.5f ? 0.f : relu(d + a.w.obj_b[j]);   // masked_fill(mask < 0.5, 0)
         }
-        Fw[k * kC + m] = (__bf16)v;
+        Fw[k * kC + m] = (elem_t)v;
       }
-      if (WITH_XB && a.xb != nullptr && lane < 32) bp(a.xb)[static_cast<int64_t>(b) * 32 + lane] = (__bf16)x[lane];
+      if (WITH_XB && a.xb != nullptr && lane < 32) bp(a.xb)[static_cast<int64_t>(b) * 32 + lane] = (elem_t)x[lane];
     } else {
       const float* f = a.F + static_cast<int64_t>(b) * kC;
 #pragma unroll
-      for (int t = 0; t < kC / 64; ++t) Fw[k * kC + lane + 64 * t] = (__bf16)f[lane + 64 * t];
+      for (int t = 0; t < kC / 64; ++t) Fw[k * kC + lane + 64 * t] = (elem_t)f[lane + 64 * t];
     }
     if constexpr (WITH_G) {
       if (a.ain != nullptr) {
@@ -244,7 +244,7 @@ __device__ __forceinline__ void iqn_act_select(const CriticArgs& a, const Critic
 }
 
 template <int MODE, int NT, class LT>
-__device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, int tile, int lane, const __bf16* Fl,
+__device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, int tile, int lane, const elem_t* Fl,
                                             const float* Gl, float* wsum = nullptr) {
   constexpr bool IQN = kIqn<MODE>;
   constexpr bool TRAINM = kTrainMode<MODE>;
@@ -254,25 +254,25 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
   float tau;
   if (MODE == MODE_IQN_ACT && a.taus == nullptr) tau = act_tau(a, grow);
   else tau = a.taus[grow];
-  const __bf16* Fb = Fl + (b - tile * 32 / NT) * kC;                   // F[b], the wave's LDS row
+  const elem_t* Fb = Fl + (b - tile * 32 / NT) * kC;                   // F[b], the wave's LDS row
   const float* Gb = IQN ? nullptr : Gl + (b - tile * 32 / NT) * kH;     // G[b]
-  const bf16x8* WC = kFwdOnly<MODE> ? L.wc : reinterpret_cast<const bf16x8*>(a.w.wc_frag);
-  const bf16x8* W1 = L.w1;
-  const bf16x8* W2 = L.w2;
+  const frag8* WC = kFwdOnly<MODE> ? wimg(L.wc, a.w.wc_frag) : reinterpret_cast<const frag8*>(a.w.wc_frag);
+  const frag8* W1 = wimg(L.w1, a.w.w1_frag);
+  const frag8* W2 = wimg(L.w2, a.w.w2_frag);
 
   // ---------------- layer 0: c = relu(Wc cos + bc), h0 = F[b] * c   (two halves of 4 blocks)
-  bf16x8 cx[kNcos / 16];
+  frag8 cx[kNcos / 16];
 #pragma unroll
   for (int ks = 0; ks < kNcos / 16; ++ks) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int k = ks * 16 + 8 * h + j;
-      cx[ks][j] = (__bf16)cos_pi_k_tau(tau, k);
+      cx[ks][j] = (elem_t)cos_pi_k_tau(tau, k);
     }
     if (TRAINM)
-      *reinterpret_cast<bf16x8*>(bp(a.acts.cos) + static_cast<size_t>(grow) * kNcos + ks * 16 + 8 * h) = cx[ks];
+      *reinterpret_cast<frag8*>(bp(a.acts.cos) + static_cast<size_t>(grow) * kNcos + ks * 16 + 8 * h) = cx[ks];
   }
-  bf16x8 cpk[16], hpk[16];
+  frag8 cpk[16], hpk[16];
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     f32x16 acc0[4];
@@ -294,9 +294,9 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
           const int m = feat(mb, 8 * s + j, h);
           float x = acc0[q4][8 * s + j] + L.bc[m];
           x = relu(x);
-          cpk[mb * 2 + s][j] = (__bf16)x;
+          cpk[mb * 2 + s][j] = (elem_t)x;
           hv[j] = static_cast<float>(Fb[m]) * x;
-          hpk[mb * 2 + s][j] = (__bf16)hv[j];
+          hpk[mb * 2 + s][j] = (elem_t)hv[j];
         }
         if (TRAINM)
           store16(bp(a.acts.h0) + static_cast<size_t>(grow) * kC + mb * 32 + 16 * s, hv, h);
@@ -313,7 +313,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
 #pragma unroll
     for (int mb = 0; mb < 4; ++mb) acc1[mb] = mfma(W1[(mb * 16 + ks) * 64 + lane], hpk[ks], acc1[mb]);
   }
-  bf16x8 h1pk[8], gpk[8];
+  frag8 h1pk[8], gpk[8];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) {
 #pragma unroll
@@ -324,9 +324,9 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
         const int m = feat(mb, 8 * s + j, h);
         float x = acc1[mb][8 * s + j] + L.b1[m];
         x = relu(x);
-        h1pk[mb * 2 + s][j] = (__bf16)x;
+        h1pk[mb * 2 + s][j] = (elem_t)x;
         gv[j] = IQN ? x : x * Gb[m];   // IQN: no action features
-        gpk[mb * 2 + s][j] = (__bf16)gv[j];
+        gpk[mb * 2 + s][j] = (elem_t)gv[j];
       }
       if (TRAINM)
         store16(bp(a.acts.h1g) + static_cast<size_t>(grow) * kH + mb * 32 + 16 * s, gv, h);
@@ -346,14 +346,14 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
   int ai = 0;   // IQN_TRAIN: the sample's action
   if constexpr (IQN) {
     // output layer 128 -> A as one 32-row MFMA block fed from h2 in registers
-    bf16x8 h2pk[8];
+    frag8 h2pk[8];
 #pragma unroll
     for (int mb = 0; mb < 4; ++mb) {
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const float x = acc2[mb][g] + L.b2[feat(mb, g, h)];
         acc2[mb][g] = x;  // keep z2 for the relu mask
-        h2pk[mb * 2 + (g >> 3)][g & 7] = (__bf16)relu(x);
+        h2pk[mb * 2 + (g >> 3)][g & 7] = (elem_t)relu(x);
       }
     }
     f32x16 ao = f32x16{};
@@ -451,15 +451,15 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
       if (a.acts.dq != nullptr) a.acts.dq[grow] = dq;
     }
     if constexpr (MODE == MODE_IQN_TRAIN) {   // dL/d(output pre-activation): dq at the taken action
-      bf16x8 o0, o1;
+      frag8 o0, o1;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        o0[i] = (__bf16)(16 * h + i == ai ? dq : 0.f);
-        o1[i] = (__bf16)(16 * h + 8 + i == ai ? dq : 0.f);
+        o0[i] = (elem_t)(16 * h + i == ai ? dq : 0.f);
+        o1[i] = (elem_t)(16 * h + 8 + i == ai ? dq : 0.f);
       }
-      __bf16* od = bp(a.dz_out) + static_cast<size_t>(grow) * kMaxA + 16 * h;
-      *reinterpret_cast<bf16x8*>(od) = o0;
-      *reinterpret_cast<bf16x8*>(od + 8) = o1;
+      elem_t* od = bp(a.dz_out) + static_cast<size_t>(grow) * kMaxA + 16 * h;
+      *reinterpret_cast<frag8*>(od) = o0;
+      *reinterpret_cast<frag8*>(od + 8) = o1;
     }
   } else {
     dq = a.dq_const;
@@ -472,7 +472,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
   // workgroup's tiles in LDS, so h2 never goes to HBM
   const bool wout = MODE == MODE_TRAIN && wsum != nullptr;   // this wave's row of the workgroup's LDS sums
   float* wp = wsum;
-  bf16x8 dz2pk[8];
+  frag8 dz2pk[8];
   float wsa[32];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) {
@@ -485,7 +485,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
         const float z = acc2[mb][8 * s + j];
         hv[j] = relu(z);
         dv[j] = z > 0.f ? dq * out_w(L, ai, m) : 0.f;
-        dz2pk[mb * 2 + s][j] = (__bf16)dv[j];
+        dz2pk[mb * 2 + s][j] = (elem_t)dv[j];
         wsa[((mb & 1) * 2 + s) * 8 + j] = dq * hv[j];
       }
       if (TRAINM) {
@@ -506,7 +506,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
   }
 
   // ---------------- layer 3: dh1g = W2^T dz2; dG[b] = sum_taus dh1g * h1; dz1 = dh1g * G * 1[h1 > 0]
-  const bf16x8* W2T = L.wc;   // TRAIN / ACTOR stage W2^T in this slot
+  const frag8* W2T = wimg(L.wc, a.w.w2t_frag);   // TRAIN / ACTOR stage W2^T in this slot
   f32x16 acc3[4];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) acc3[mb] = f32x16{};
@@ -575,37 +575,38 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
 // c = relu(Wc cos + bc) is recomputed (bit-identical to part A's) instead of being kept live across
 // the layers, which is what lets both parts run two waves per SIMD.
 struct CriticLdsB {
-  bf16x8 wc[kFragWC];
-  bf16x8 w1t[kFragW1];
+  frag8 wc[lds_frags(kFragWC)];
+  frag8 w1t[lds_frags(kFragW1)];
   float bc[kC];
 };
 
 template <int NT>
 __device__ __forceinline__ void critic_tile_b(const CriticArgs& a, const CriticLdsB& L, int tile, int lane,
-                                              const __bf16* Fl) {
+                                              const elem_t* Fl) {
   const int r = lane & 31, h = lane >> 5;
   const int grow = tile * 32 + r;
   const int b = grow / NT;
   const float tau = a.taus[grow];
-  const __bf16* Fb = Fl + (b - tile * 32 / NT) * kC;   // the wave's LDS row of F[b]
-  bf16x8 cx[kNcos / 16];
+  const elem_t* Fb = Fl + (b - tile * 32 / NT) * kC;   // the wave's LDS row of F[b]
+  frag8 cx[kNcos / 16];
 #pragma unroll
   for (int ks = 0; ks < kNcos / 16; ++ks)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int k = ks * 16 + 8 * h + j;
-      cx[ks][j] = (__bf16)cos_pi_k_tau(tau, k);
+      cx[ks][j] = (elem_t)cos_pi_k_tau(tau, k);
     }
   // dz1 as the chained B operand: element j of k-step ks is feature 16ks + 8(j>>2) + 4h + (j&3)
-  bf16x8 dz1pk[8];
-  const __bf16* dz1row = bp(a.acts.dz1) + static_cast<size_t>(grow) * kH;
+  frag8 dz1pk[8];
+  const elem_t* dz1row = bp(a.acts.dz1) + static_cast<size_t>(grow) * kH;
 #pragma unroll
   for (int ks = 0; ks < kH / 16; ++ks) {
-    const bf16x4 lo = *reinterpret_cast<const bf16x4*>(dz1row + ks * 16 + 4 * h);
-    const bf16x4 hi = *reinterpret_cast<const bf16x4*>(dz1row + ks * 16 + 8 + 4 * h);
-    dz1pk[ks] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    const elem4 lo = *reinterpret_cast<const elem4*>(dz1row + ks * 16 + 4 * h);
+    const elem4 hi = *reinterpret_cast<const elem4*>(dz1row + ks * 16 + 8 + 4 * h);
+    dz1pk[ks] = frag8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   }
-  const bf16x8* W1T = L.w1t;
+  const frag8* W1T = wimg(L.w1t, a.w.w1t_frag);
+  const frag8* WCB = wimg(L.wc, a.w.wc_frag);
   // NT = 32 (row_bcast segment sums) spills at 4 blocks per pass; 2 keeps it in registers
   constexpr int BPP = ASVRL_TRAIN_B_BPP32 != 0 && NT == 32 ? ASVRL_TRAIN_B_BPP32 : 4;
 #pragma unroll
@@ -619,7 +620,7 @@ __device__ __forceinline__ void critic_tile_b(const CriticArgs& a, const CriticL
 #pragma unroll
     for (int ks = 0; ks < kNcos / 16; ++ks)
 #pragma unroll
-      for (int q4 = 0; q4 < BPP; ++q4) acc0[q4] = mfma(L.wc[((half * BPP + q4) * 4 + ks) * 64 + lane], cx[ks], acc0[q4]);
+      for (int q4 = 0; q4 < BPP; ++q4) acc0[q4] = mfma(WCB[((half * BPP + q4) * 4 + ks) * 64 + lane], cx[ks], acc0[q4]);
 #pragma unroll
     for (int ks = 0; ks < kH / 16; ++ks)
 #pragma unroll
@@ -636,7 +637,7 @@ __device__ __forceinline__ void critic_tile_b(const CriticArgs& a, const CriticL
         for (int j = 0; j < 8; ++j) {
           const int m = feat(mb, 8 * s + j, h);
           const float x = acc0[q4][8 * s + j] + L.bc[m];
-          const float cv = static_cast<float>((__bf16)relu(x));   // part A's bf16 c
+          const float cv = static_cast<float>((elem_t)relu(x));   // part A's bf16 c
           fsa[(q4 * 2 + s) * 8 + j] = acc4[q4][8 * s + j] * cv;
           dv[j] = cv > 0.f ? acc4[q4][8 * s + j] * static_cast<float>(Fb[m]) : 0.f;
         }
@@ -652,7 +653,7 @@ __device__ __forceinline__ void critic_tile_b(const CriticArgs& a, const CriticL
       const int m = feat(half * BPP + (g >> 1), 8 * (g & 1) + (v & 7), h);
       const size_t o = static_cast<size_t>(b) * kC + m;
       if (a.dF != nullptr) a.dF[o] = fsa[i];
-      if (a.dzF != nullptr) bp(a.dzF)[o] = (__bf16)(static_cast<float>(Fb[m]) > 0.f ? fsa[i] : 0.f);   // encoders' relu / mask
+      if (a.dzF != nullptr) bp(a.dzF)[o] = (elem_t)(static_cast<float>(Fb[m]) > 0.f ? fsa[i] : 0.f);   // encoders' relu / mask
     }
   }
 }
@@ -661,16 +662,18 @@ template <int NT>
 __global__ __launch_bounds__(8 * 64) void critic_train_b_kernel(CriticArgs a) {
   __shared__ CriticLdsB L;
   {
-    const bf16x8* gwc = reinterpret_cast<const bf16x8*>(a.w.wc_frag);
-    const bf16x8* gw1t = reinterpret_cast<const bf16x8*>(a.w.w1t_frag);
-    for (int i = threadIdx.x; i < kFragWC; i += 8 * 64) L.wc[i] = gwc[i];
-    for (int i = threadIdx.x; i < kFragW1; i += 8 * 64) L.w1t[i] = gw1t[i];
+    const frag8* gwc = reinterpret_cast<const frag8*>(a.w.wc_frag);
+    const frag8* gw1t = reinterpret_cast<const frag8*>(a.w.w1t_frag);
+    if constexpr (kWeightsInLds) {
+      for (int i = threadIdx.x; i < kFragWC; i += 8 * 64) L.wc[i] = gwc[i];
+      for (int i = threadIdx.x; i < kFragW1; i += 8 * 64) L.w1t[i] = gw1t[i];
+    }
     for (int i = threadIdx.x; i < kC; i += 8 * 64) L.bc[i] = a.w.bc[i];
   }
   // this wave's samples' F rows (read per feature after the dzc stores: LDS, not vmcnt-ordered loads)
-  __shared__ __attribute__((aligned(16))) __bf16 Fs[8 * (32 / NT) * kC];
+  __shared__ __attribute__((aligned(16))) elem_t Fs[8 * (32 / NT) * kC];
   const int tile = blockIdx.x * 8 + (threadIdx.x >> 6);
-  __bf16* Fw = Fs + (threadIdx.x >> 6) * (32 / NT) * kC;
+  elem_t* Fw = Fs + (threadIdx.x >> 6) * (32 / NT) * kC;
   if (tile < a.B * NT / 32) stage_features<NT, false, false>(a, tile, threadIdx.x & 63, Fw, nullptr);
   __syncthreads();
   if (tile < a.B * NT / 32) critic_tile_b<NT>(a, L, tile, threadIdx.x & 63, Fw);
@@ -684,21 +687,23 @@ template <int MODE, int NT>
 __global__ __launch_bounds__(CriticWaves<NT>::n * 64) void critic_kernel(CriticArgs a) {
   constexpr int W = CriticWaves<NT>::n, S = 32 / NT;
   __shared__ typename LdsOf<MODE>::T L;
-  __shared__ __attribute__((aligned(16))) __bf16 Fs[W * S * kC];
+  __shared__ __attribute__((aligned(16))) elem_t Fs[W * S * kC];
   __shared__ __attribute__((aligned(16))) float Gs[kStageG<MODE> ? W * S * kH : 1];
   __shared__ float Ws[MODE == MODE_TRAIN ? W * (kH + 1) : 1];   // per-wave output-layer gradient sums
   const int tile = blockIdx.x * W + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int tiles = a.B * NT / 32;
-  __bf16* Fw = Fs + (threadIdx.x >> 6) * S * kC;
+  elem_t* Fw = Fs + (threadIdx.x >> 6) * S * kC;
   float* Gw = Gs + (kStageG<MODE> ? (threadIdx.x >> 6) * S * kH : 0);
   if (tile < tiles) stage_features<NT, kStageG<MODE>, kTrainMode<MODE>>(a, tile, lane, Fw, Gw);
   {
-    const bf16x8* gwc = reinterpret_cast<const bf16x8*>(kFwdOnly<MODE> ? a.w.wc_frag : a.w.w2t_frag);
-    const bf16x8* gw1 = reinterpret_cast<const bf16x8*>(a.w.w1_frag);
-    const bf16x8* gw2 = reinterpret_cast<const bf16x8*>(a.w.w2_frag);
-    for (int i = threadIdx.x; i < kFragWC; i += W * 64) L.wc[i] = gwc[i];
-    for (int i = threadIdx.x; i < kFragW1; i += W * 64) L.w1[i] = gw1[i];
-    for (int i = threadIdx.x; i < kFragW2; i += W * 64) L.w2[i] = gw2[i];
+    const frag8* gwc = reinterpret_cast<const frag8*>(kFwdOnly<MODE> ? a.w.wc_frag : a.w.w2t_frag);
+    const frag8* gw1 = reinterpret_cast<const frag8*>(a.w.w1_frag);
+    const frag8* gw2 = reinterpret_cast<const frag8*>(a.w.w2_frag);
+    if constexpr (kWeightsInLds) {
+      for (int i = threadIdx.x; i < kFragWC; i += W * 64) L.wc[i] = gwc[i];
+      for (int i = threadIdx.x; i < kFragW1; i += W * 64) L.w1[i] = gw1[i];
+      for (int i = threadIdx.x; i < kFragW2; i += W * 64) L.w2[i] = gw2[i];
+    }
     for (int i = threadIdx.x; i < kC; i += W * 64) L.bc[i] = a.w.bc[i];
     for (int i = threadIdx.x; i < kH; i += W * 64) {
       L.b1[i] = a.w.b1[i];
@@ -706,11 +711,11 @@ __global__ __launch_bounds__(CriticWaves<NT>::n * 64) void critic_kernel(CriticA
       if (!kIqn<MODE>) L.wo[i] = a.w.wo[i];
     }
     if constexpr (kIqn<MODE>) {
-      const bf16x8* gwo = reinterpret_cast<const bf16x8*>(a.hd.wo_frag);
+      const frag8* gwo = reinterpret_cast<const frag8*>(a.hd.wo_frag);
       for (int i = threadIdx.x; i < kH / 16 * 64; i += W * 64) L.wo_img[i] = gwo[i];
       const int A = a.hd.n_actions;
       if (MODE == MODE_IQN_TRAIN)
-        for (int i = threadIdx.x; i < A * kH; i += W * 64) L.wof[i] = (__bf16)a.hd.wo[i];
+        for (int i = threadIdx.x; i < A * kH; i += W * 64) L.wof[i] = (elem_t)a.hd.wo[i];
       for (int i = threadIdx.x; i < kMaxA; i += W * 64) L.bo_a[i] = i < A ? a.hd.bo[i] : 0.f;
     }
   }
@@ -797,35 +802,35 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ wc,
     o -= kPackTotal;
     if (wo_frag == nullptr || o >= kPackHead) return;
     frag_rc(o, kH, true, row, col);
-    static_cast<__bf16*>(wo_frag)[o] = (__bf16)(row < n_actions ? wout[row * kH + col] : 0.f);
+    static_cast<elem_t*>(wo_frag)[o] = (elem_t)(row < n_actions ? wout[row * kH + col] : 0.f);
     return;
   }
   if (o < kPackWc) {                                    // cos_embedding.weight (256 x 64)
     frag_rc(o, 64, false, row, col);
-    const_cast<__bf16*>(static_cast<const __bf16*>(w.wc_frag))[o] = (__bf16)wc[row * 64 + col];
+    const_cast<elem_t*>(static_cast<const elem_t*>(w.wc_frag))[o] = (elem_t)wc[row * 64 + col];
     return;
   }
   o -= kPackWc;
   if (o < kPackW1) {                                    // hidden_layer.weight (128 x 256)
     frag_rc(o, 256, true, row, col);
-    const_cast<__bf16*>(static_cast<const __bf16*>(w.w1_frag))[o] = (__bf16)w1[row * 256 + col];
+    const_cast<elem_t*>(static_cast<const elem_t*>(w.w1_frag))[o] = (elem_t)w1[row * 256 + col];
     return;
   }
   o -= kPackW1;
   if (o < kPackW2) {                                    // hidden_layer_2.weight (128 x 128)
     frag_rc(o, 128, true, row, col);
-    const_cast<__bf16*>(static_cast<const __bf16*>(w.w2_frag))[o] = (__bf16)w2[row * 128 + col];
+    const_cast<elem_t*>(static_cast<const elem_t*>(w.w2_frag))[o] = (elem_t)w2[row * 128 + col];
     return;
   }
   o -= kPackW2;
   if (o < kPackW2) {                                    // its transpose
     frag_rc(o, 128, true, row, col);
-    const_cast<__bf16*>(static_cast<const __bf16*>(w.w2t_frag))[o] = (__bf16)w2[col * 128 + row];
+    const_cast<elem_t*>(static_cast<const elem_t*>(w.w2t_frag))[o] = (elem_t)w2[col * 128 + row];
     return;
   }
   o -= kPackW2;                                         // hidden_layer.weight^T (256 x 128)
   frag_rc(o, 128, true, row, col);
-  const_cast<__bf16*>(static_cast<const __bf16*>(w.w1t_frag))[o] = (__bf16)w1[col * 256 + row];
+  const_cast<elem_t*>(static_cast<const elem_t*>(w.w1t_frag))[o] = (elem_t)w1[col * 256 + row];
 }
 
 int validate(const AsvCriticWeights* w, const AsvCriticIO* io) {

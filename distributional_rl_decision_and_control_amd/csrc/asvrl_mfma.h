@@ -6,21 +6,60 @@
 // (g & 3) + 8 (g >> 2) + 4 h of the block. Registers 8s..8s+7, converted to bf16, are directly
 // the B operand of a following layer's k-step s ("chained" k order 16s + 8(j>>2) + 4h + (j&3));
 // the A operand (weights) is pre-packed into per-lane fragments in that same k order.
+//
+// Operand type. The library is built twice from the same sources: libasvrl.so with bf16 operands
+// (the training path) and libasvrl_f32.so with ASVRL_OPERAND_F32=1, where every operand, weight
+// image and saved activation is f32 and each 32x32x16 bf16 MFMA becomes eight
+// v_mfma_f32_32x32x2_f32 over the same fragments (instruction j takes element j of both operands,
+// k = lane half: the k order is permuted identically on both sides, so the product is the same sum).
+// The f32 build is the parity build of the hand-written learner (reference fp32 arithmetic).
+// Its weight images are twice as large, so they are read from global memory (L2) instead of LDS.
 #pragma once
 
 #include <hip/hip_runtime.h>
+
+#ifndef ASVRL_OPERAND_F32
+#define ASVRL_OPERAND_F32 0
+#endif
 
 namespace asvrl {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ __bf16* bp(void* p) { return reinterpret_cast<__bf16*>(p); }
-
-__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+#if ASVRL_OPERAND_F32
+typedef float elem_t;   // MFMA operand / saved-activation / weight-image element
+typedef f32x8 frag8;    // one lane's 8 operand elements of a 32x32x16 k-step
+typedef f32x4 elem4;
+constexpr bool kWeightsInLds = false;
+__device__ __forceinline__ f32x16 mfma(frag8 a, frag8 b, f32x16 c) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[j], c, 0, 0, 0);
+  return c;
+}
+#else
+typedef __bf16 elem_t;
+typedef bf16x8 frag8;
+typedef bf16x4 elem4;
+constexpr bool kWeightsInLds = true;
+__device__ __forceinline__ f32x16 mfma(frag8 a, frag8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+#endif
+constexpr int kElemBytes = static_cast<int>(sizeof(elem_t));
+
+__device__ __forceinline__ elem_t* bp(void* p) { return reinterpret_cast<elem_t*>(p); }
+__device__ __forceinline__ const elem_t* bp(const void* p) { return reinterpret_cast<const elem_t*>(p); }
+
+// the weight image a kernel reads: its LDS copy (bf16 build) or the global image (f32 build)
+__device__ __forceinline__ const frag8* wimg(const frag8* lds, const void* glob) {
+  return kWeightsInLds ? lds : reinterpret_cast<const frag8*>(glob);
+}
+// LDS slots of a weight image: full size in the bf16 build, one fragment (unused) in the f32 build
+constexpr int lds_frags(int n) { return kWeightsInLds ? n : 1; }
 
 // feature index held by accumulator register g of 32-feature block mb in lane half h
 __device__ __forceinline__ int feat(int mb, int g, int h) { return mb * 32 + (g & 3) + 8 * (g >> 2) + 4 * h; }
@@ -96,21 +135,28 @@ __device__ __forceinline__ float half_sum(float x) {
 
 // cos(tau * pi * k) (Critic.calc_cos, AC_IQN_model.py:423) on the hardware cosine: v_cos_f32 takes
 // revolutions, cos(2 pi x) with x = k tau / 2 (< 32 for k < 64, tau < 1: inside its +-256 domain).
-// The value is rounded to bf16 for the MFMA right after, far above v_cos_f32's error.
+// The value is rounded to bf16 for the MFMA right after, far above v_cos_f32's error. The f32 build
+// computes the reference's expression itself: cos(tau * pis[k]) with pis[k] = f32(np.pi * k)
+// (AC_IQN_model.py:389,423; IQN_model.py) and an f32 product.
 __device__ __forceinline__ float cos_pi_k_tau(float tau, int k) {
+#if ASVRL_OPERAND_F32
+  const float pis = static_cast<float>(3.141592653589793 * static_cast<double>(k));
+  return cosf(tau * pis);
+#else
   return __builtin_amdgcn_cosf(tau * (0.5f * static_cast<float>(k)));
+#endif
 }
 
 __device__ __forceinline__ float relu(float x) { return fmaxf(x, 0.f); }
 
-// bf16x4 store of 4 consecutive features
-__device__ __forceinline__ void store4(__bf16* base, const float* v) {
-  bf16x4 x;
-  x[0] = (__bf16)v[0];
-  x[1] = (__bf16)v[1];
-  x[2] = (__bf16)v[2];
-  x[3] = (__bf16)v[3];
-  *reinterpret_cast<bf16x4*>(base) = x;
+// store of 4 consecutive features
+__device__ __forceinline__ void store4(elem_t* base, const float* v) {
+  elem4 x;
+  x[0] = (elem_t)v[0];
+  x[1] = (elem_t)v[1];
+  x[2] = (elem_t)v[2];
+  x[3] = (elem_t)v[3];
+  *reinterpret_cast<elem4*>(base) = x;
 }
 
 // Store the 16 features of one k-step group (features 16s .. 16s+15 of a 32-feature block) of this
@@ -119,7 +165,14 @@ __device__ __forceinline__ void store4(__bf16* base, const float* v) {
 // 8..11, so half 0 then holds features 0..7 and half 1 features 8..15, and each lane writes one
 // 16-byte piece: every row gets a full 32-byte sector per instruction. `grp` points at feature
 // 16s of the row (nullptr: exchange only). All 64 lanes must call it.
-__device__ __forceinline__ void store16(__bf16* grp, const float* v, int h) {
+__device__ __forceinline__ void store16(elem_t* grp, const float* v, int h) {
+#if ASVRL_OPERAND_F32
+  // f32: each lane writes its two 4-feature pieces (16 B each) directly
+  if (grp != nullptr) {
+    *reinterpret_cast<f32x4*>(grp + 4 * h) = f32x4{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<f32x4*>(grp + 8 + 4 * h) = f32x4{v[4], v[5], v[6], v[7]};
+  }
+#else
   bf16x4 lo, hi;
   lo[0] = (__bf16)v[0]; lo[1] = (__bf16)v[1]; lo[2] = (__bf16)v[2]; lo[3] = (__bf16)v[3];
   hi[0] = (__bf16)v[4]; hi[1] = (__bf16)v[5]; hi[2] = (__bf16)v[6]; hi[3] = (__bf16)v[7];
@@ -130,11 +183,12 @@ __device__ __forceinline__ void store16(__bf16* grp, const float* v, int h) {
   const auto r1 = __builtin_amdgcn_permlane32_swap(l[1], u[1], false, false);
   const u32x4 out = {r0[0], r1[0], r0[1], r1[1]};
   if (grp != nullptr) *reinterpret_cast<u32x4*>(grp + 8 * h) = out;
+#endif
 }
 
-// 4 consecutive bf16 -> f32
-__device__ __forceinline__ void load4(const __bf16* base, float* v) {
-  const bf16x4 x = *reinterpret_cast<const bf16x4*>(base);
+// 4 consecutive elements -> f32
+__device__ __forceinline__ void load4(const elem_t* base, float* v) {
+  const elem4 x = *reinterpret_cast<const elem4*>(base);
   v[0] = static_cast<float>(x[0]);
   v[1] = static_cast<float>(x[1]);
   v[2] = static_cast<float>(x[2]);

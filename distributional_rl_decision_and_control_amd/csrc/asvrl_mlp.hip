@@ -37,9 +37,9 @@ struct MlpArgs {
 };
 
 struct ActorLds {
-  bf16x8 enc[kFragEnc];
-  bf16x8 w1[kFragH1];
-  bf16x8 w2[kFragH2];
+  frag8 enc[lds_frags(kFragEnc)];
+  frag8 w1[lds_frags(kFragH1)];
+  frag8 w2[lds_frags(kFragH2)];
   float benc[kEnc], b1[kHid], b2[kHid], wout[kNa * kHid], bout[kNa];
 };
 
@@ -49,7 +49,7 @@ __host__ __device__ constexpr int obj_of(int m) { return (m - kSelfF) / kObjF; }
 // Encoder output of one 32-row tile: B operand from obs columns 0..31, 8 blocks in 2 halves;
 // epilogue bias + relu + mask. Hands each finished (block, s) group of 8 features to `emit`.
 template <typename Emit>
-__device__ __forceinline__ void encode_tile(const bf16x8* ENC, const float* benc, const bf16x8 (&bx)[2],
+__device__ __forceinline__ void encode_tile(const frag8* ENC, const float* benc, const frag8 (&bx)[2],
                                             const float (&mk)[kObjN], int lane, Emit emit) {
   const int h = lane >> 5;
 #pragma unroll
@@ -84,15 +84,15 @@ __device__ __forceinline__ void encode_tile(const bf16x8* ENC, const float* benc
 }
 
 // bf16 B operand of the encoder (obs columns 0..31) + the object mask, for row `row`
-__device__ __forceinline__ void load_obs(const float* __restrict__ x, int64_t ldx, int row, int h, bf16x8 (&bx)[2],
+__device__ __forceinline__ void load_obs(const float* __restrict__ x, int64_t ldx, int row, int h, frag8 (&bx)[2],
                                          float (&mk)[kObjN]) {
   const float* xr = x + static_cast<int64_t>(row) * ldx;
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
     const float4 u = *reinterpret_cast<const float4*>(xr + ks * 16 + 8 * h);
     const float4 v = *reinterpret_cast<const float4*>(xr + ks * 16 + 8 * h + 4);
-    bx[ks][0] = (__bf16)u.x; bx[ks][1] = (__bf16)u.y; bx[ks][2] = (__bf16)u.z; bx[ks][3] = (__bf16)u.w;
-    bx[ks][4] = (__bf16)v.x; bx[ks][5] = (__bf16)v.y; bx[ks][6] = (__bf16)v.z; bx[ks][7] = (__bf16)v.w;
+    bx[ks][0] = (elem_t)u.x; bx[ks][1] = (elem_t)u.y; bx[ks][2] = (elem_t)u.z; bx[ks][3] = (elem_t)u.w;
+    bx[ks][4] = (elem_t)v.x; bx[ks][5] = (elem_t)v.y; bx[ks][6] = (elem_t)v.z; bx[ks][7] = (elem_t)v.w;
   }
 #pragma unroll
   for (int o = 0; o < kObjN; ++o) mk[o] = xr[32 + o];
@@ -107,15 +107,15 @@ __global__ __launch_bounds__(kMlpWaves * 64) void encode_kernel(MlpArgs a) {
   const int row = tile * 32 + r;
   const bool valid = row < io.n;
   const int rr = valid ? row : io.n - 1;
-  bf16x8 bx[2];
+  frag8 bx[2];
   float mk[kObjN];
   load_obs(io.x, io.ldx, rr, h, bx, mk);
   if (io.xb != nullptr && valid) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
-      *reinterpret_cast<bf16x8*>(bp(io.xb) + static_cast<int64_t>(row) * kObsK + ks * 16 + 8 * h) = bx[ks];
+      *reinterpret_cast<frag8*>(bp(io.xb) + static_cast<int64_t>(row) * kObsK + ks * 16 + 8 * h) = bx[ks];
   }
-  const bf16x8* ENC = reinterpret_cast<const bf16x8*>(a.w.enc_frag);
+  const frag8* ENC = reinterpret_cast<const frag8*>(a.w.enc_frag);
   float* Fr = io.F + static_cast<int64_t>(rr) * kEnc;
   encode_tile(ENC, a.w.b_enc, bx, mk, lane, [&](int mb, int s, const float* v) {
     if (!valid) return;
@@ -125,13 +125,13 @@ __global__ __launch_bounds__(kMlpWaves * 64) void encode_kernel(MlpArgs a) {
   });
   if (io.G == nullptr) return;
   // action encoder: B operand = (a0, a1, 0, ...) in lane half 0
-  bf16x8 ba{};
+  frag8 ba{};
   if (h == 0) {
     const float* ar = io.act + static_cast<int64_t>(rr) * io.lda;
-    ba[0] = (__bf16)ar[0];
-    ba[1] = (__bf16)ar[1];
+    ba[0] = (elem_t)ar[0];
+    ba[1] = (elem_t)ar[1];
   }
-  const bf16x8* AE = reinterpret_cast<const bf16x8*>(a.w.ae_frag);
+  const frag8* AE = reinterpret_cast<const frag8*>(a.w.ae_frag);
   float* Gr = io.G + static_cast<int64_t>(rr) * kHid;
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) {
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(kMlpWaves * 64) void encode_kernel(MlpArgs a) {
 // ------------------------------------------------------------------ Actor forward (ACT/FWD/TRAIN)
 template <int MODE>
 __device__ __forceinline__ void actor_tile(const MlpArgs& a, const ActorLds& L, int tile, int lane,
-                                           const bf16x8 (&bx)[2], const float (&mk)[kObjN]) {
+                                           const frag8 (&bx)[2], const float (&mk)[kObjN]) {
   const AsvMlpIO& io = a.io;
   const int h = lane >> 5, r = lane & 31;
   const int row = tile * 32 + r;
@@ -164,25 +164,27 @@ __device__ __forceinline__ void actor_tile(const MlpArgs& a, const ActorLds& L, 
   if (MODE == MLP_TRAIN && valid) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
-      *reinterpret_cast<bf16x8*>(bp(io.xb) + static_cast<int64_t>(row) * kObsK + ks * 16 + 8 * h) = bx[ks];
+      *reinterpret_cast<frag8*>(bp(io.xb) + static_cast<int64_t>(row) * kObsK + ks * 16 + 8 * h) = bx[ks];
   }
   // encoders -> h0 (chained B operand of hidden_layer)
-  bf16x8 fpk[16];
-  encode_tile(L.enc, L.benc, bx, mk, lane, [&](int mb, int s, const float* v) {
+  frag8 fpk[16];
+  encode_tile(wimg(L.enc, a.w.enc_frag), L.benc, bx, mk, lane, [&](int mb, int s, const float* v) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) fpk[mb * 2 + s][j] = (__bf16)v[j];
+    for (int j = 0; j < 8; ++j) fpk[mb * 2 + s][j] = (elem_t)v[j];
     if (MODE == MLP_TRAIN)
       store16(valid ? bp(io.h0) + static_cast<int64_t>(row) * kEnc + mb * 32 + 16 * s : nullptr, v, h);
   });
   // hidden_layer 256 -> 128, relu
+  const frag8* W1 = wimg(L.w1, a.w.w1_frag);
+  const frag8* W2 = wimg(L.w2, a.w.w2_frag);
   f32x16 acc1[4];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) acc1[mb] = f32x16{};
 #pragma unroll
   for (int ks = 0; ks < kEnc / 16; ++ks)
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) acc1[mb] = mfma(L.w1[(mb * 16 + ks) * 64 + lane], fpk[ks], acc1[mb]);
-  bf16x8 h1pk[8];
+    for (int mb = 0; mb < 4; ++mb) acc1[mb] = mfma(W1[(mb * 16 + ks) * 64 + lane], fpk[ks], acc1[mb]);
+  frag8 h1pk[8];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
@@ -192,7 +194,7 @@ __device__ __forceinline__ void actor_tile(const MlpArgs& a, const ActorLds& L, 
       for (int j = 0; j < 8; ++j) {
         const float x = acc1[mb][8 * s + j] + L.b1[feat(mb, 8 * s + j, h)];
         v[j] = relu(x);
-        h1pk[mb * 2 + s][j] = (__bf16)v[j];
+        h1pk[mb * 2 + s][j] = (elem_t)v[j];
       }
       if (MODE == MLP_TRAIN)
       store16(valid ? bp(io.h1) + static_cast<int64_t>(row) * kHid + mb * 32 + 16 * s : nullptr, v, h);
@@ -204,7 +206,7 @@ __device__ __forceinline__ void actor_tile(const MlpArgs& a, const ActorLds& L, 
 #pragma unroll
   for (int ks = 0; ks < kHid / 16; ++ks)
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) acc2[mb] = mfma(L.w2[(mb * 8 + ks) * 64 + lane], h1pk[ks], acc2[mb]);
+    for (int mb = 0; mb < 4; ++mb) acc2[mb] = mfma(W2[(mb * 8 + ks) * 64 + lane], h1pk[ks], acc2[mb]);
   float p0 = 0.f, p1 = 0.f;
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb)
@@ -264,19 +266,21 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_kernel(MlpArgs a) {
   // the tile's observation rows are loaded first, in flight under the weight staging
   const int tile = blockIdx.x * kMlpWaves + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   const bool active = tile * 32 < a.io.n;
-  bf16x8 bx[2];
+  frag8 bx[2];
   float mk[kObjN];
   if (active) {
     const int row = tile * 32 + (lane & 31);
     load_obs(a.io.x, a.io.ldx, row < a.io.n ? row : a.io.n - 1, lane >> 5, bx, mk);
   }
   {
-    const bf16x8* ge = reinterpret_cast<const bf16x8*>(a.w.enc_frag);
-    const bf16x8* g1 = reinterpret_cast<const bf16x8*>(a.w.w1_frag);
-    const bf16x8* g2 = reinterpret_cast<const bf16x8*>(a.w.w2_frag);
-    for (int i = threadIdx.x; i < kFragEnc; i += kMlpWaves * 64) L.enc[i] = ge[i];
-    for (int i = threadIdx.x; i < kFragH1; i += kMlpWaves * 64) L.w1[i] = g1[i];
-    for (int i = threadIdx.x; i < kFragH2; i += kMlpWaves * 64) L.w2[i] = g2[i];
+    const frag8* ge = reinterpret_cast<const frag8*>(a.w.enc_frag);
+    const frag8* g1 = reinterpret_cast<const frag8*>(a.w.w1_frag);
+    const frag8* g2 = reinterpret_cast<const frag8*>(a.w.w2_frag);
+    if constexpr (kWeightsInLds) {
+      for (int i = threadIdx.x; i < kFragEnc; i += kMlpWaves * 64) L.enc[i] = ge[i];
+      for (int i = threadIdx.x; i < kFragH1; i += kMlpWaves * 64) L.w1[i] = g1[i];
+      for (int i = threadIdx.x; i < kFragH2; i += kMlpWaves * 64) L.w2[i] = g2[i];
+    }
     for (int i = threadIdx.x; i < kEnc; i += kMlpWaves * 64) L.benc[i] = a.w.b_enc[i];
     for (int i = threadIdx.x; i < kHid; i += kMlpWaves * 64) {
       L.b1[i] = a.w.b1[i];
@@ -295,8 +299,8 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_kernel(MlpArgs a) {
 // dz1 = (W2^T dz2) 1[h1 > 0], dz0 = (W1^T dz1) 1[h0 > 0] (relu and masked_fill both zero where
 // h0 == 0). Writes dOut f32 and dz2, dz1, dz0 bf16 for the weight gradients.
 struct ActorBwdLds {
-  bf16x8 w2t[kFragH2];
-  bf16x8 w1t[kFragH1];
+  frag8 w2t[lds_frags(kFragH2)];
+  frag8 w1t[lds_frags(kFragH1)];
   float wout[kNa * kHid];
 };
 
@@ -311,8 +315,7 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_kernel(MlpArgs a) {
   const int64_t rr = valid ? row : io.n - 1;
   // one wave per SIMD (97 KB of LDS per workgroup): registers are free, so the tile's pre-activations,
   // dL/da and h2 / h1 / h0 rows are all loaded up front, in flight under the weight staging
-  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-  bf16x4 ph2[16], ph1[16], ph0[32];
+  elem4 ph2[16], ph1[16], ph0[32];
   float z0 = 0.f, z1 = 0.f, da0 = 0.f, da1 = 0.f;
   if (active) {
     z0 = io.pre[rr * 2]; z1 = io.pre[rr * 2 + 1];
@@ -324,8 +327,8 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_kernel(MlpArgs a) {
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           const int64_t off = rr * kHid + mb * 32 + 16 * s + 4 * h + 8 * q;
-          ph2[(mb * 2 + s) * 2 + q] = *reinterpret_cast<const bf16x4*>(bp(io.h2) + off);
-          ph1[(mb * 2 + s) * 2 + q] = *reinterpret_cast<const bf16x4*>(bp(io.h1) + off);
+          ph2[(mb * 2 + s) * 2 + q] = *reinterpret_cast<const elem4*>(bp(io.h2) + off);
+          ph1[(mb * 2 + s) * 2 + q] = *reinterpret_cast<const elem4*>(bp(io.h1) + off);
         }
 #pragma unroll
     for (int mb = 0; mb < 8; ++mb)
@@ -334,23 +337,27 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_kernel(MlpArgs a) {
 #pragma unroll
         for (int q = 0; q < 2; ++q)
           ph0[(mb * 2 + s) * 2 + q] =
-              *reinterpret_cast<const bf16x4*>(bp(io.h0) + rr * kEnc + mb * 32 + 16 * s + 4 * h + 8 * q);
+              *reinterpret_cast<const elem4*>(bp(io.h0) + rr * kEnc + mb * 32 + 16 * s + 4 * h + 8 * q);
   }
   {
-    const bf16x8* g2 = reinterpret_cast<const bf16x8*>(a.w.w2t_frag);
-    const bf16x8* g1 = reinterpret_cast<const bf16x8*>(a.w.w1t_frag);
-    for (int i = threadIdx.x; i < kFragH2; i += kMlpWaves * 64) L.w2t[i] = g2[i];
-    for (int i = threadIdx.x; i < kFragH1; i += kMlpWaves * 64) L.w1t[i] = g1[i];
+    const frag8* g2 = reinterpret_cast<const frag8*>(a.w.w2t_frag);
+    const frag8* g1 = reinterpret_cast<const frag8*>(a.w.w1t_frag);
+    if constexpr (kWeightsInLds) {
+      for (int i = threadIdx.x; i < kFragH2; i += kMlpWaves * 64) L.w2t[i] = g2[i];
+      for (int i = threadIdx.x; i < kFragH1; i += kMlpWaves * 64) L.w1t[i] = g1[i];
+    }
     for (int i = threadIdx.x; i < kNa * kHid; i += kMlpWaves * 64) L.wout[i] = a.w.wout[i];
   }
   __syncthreads();
   if (!active) return;
-  auto unpack = [](const bf16x4* p, float* v) {
+  auto unpack = [](const elem4* p, float* v) {
 #pragma unroll
     for (int q = 0; q < 2; ++q)
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[4 * q + j] = static_cast<float>(p[q][j]);
   };
+  const frag8* W2T = wimg(L.w2t, a.w.w2t_frag);
+  const frag8* W1T = wimg(L.w1t, a.w.w1t_frag);
   const float d0 = da0 * a.w.out_scale / (1.f + z0 * z0);
   const float d1 = da1 * a.w.out_scale / (1.f + z1 * z1);
   if (valid && h == 0) {
@@ -358,7 +365,7 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_kernel(MlpArgs a) {
     io.dout[row * 2 + 1] = d1;
   }
   // dz2 (chained B operand of W2^T)
-  bf16x8 dz2pk[8];
+  frag8 dz2pk[8];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
@@ -369,7 +376,7 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_kernel(MlpArgs a) {
       for (int j = 0; j < 8; ++j) {
         const int m = feat(mb, 8 * s + j, h);
         dv[j] = hv[j] > 0.f ? L.wout[m] * d0 + L.wout[kHid + m] * d1 : 0.f;
-        dz2pk[mb * 2 + s][j] = (__bf16)dv[j];
+        dz2pk[mb * 2 + s][j] = (elem_t)dv[j];
       }
       store16(valid ? bp(io.dz2) + row * kHid + mb * 32 + 16 * s : nullptr, dv, h);
     }
@@ -380,8 +387,8 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_kernel(MlpArgs a) {
 #pragma unroll
   for (int ks = 0; ks < kHid / 16; ++ks)
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) acc3[mb] = mfma(L.w2t[(mb * 8 + ks) * 64 + lane], dz2pk[ks], acc3[mb]);
-  bf16x8 dz1pk[8];
+    for (int mb = 0; mb < 4; ++mb) acc3[mb] = mfma(W2T[(mb * 8 + ks) * 64 + lane], dz2pk[ks], acc3[mb]);
+  frag8 dz1pk[8];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
@@ -391,7 +398,7 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_kernel(MlpArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         dv[j] = hv[j] > 0.f ? acc3[mb][8 * s + j] : 0.f;
-        dz1pk[mb * 2 + s][j] = (__bf16)dv[j];
+        dz1pk[mb * 2 + s][j] = (elem_t)dv[j];
       }
       store16(valid ? bp(io.dz1) + row * kHid + mb * 32 + 16 * s : nullptr, dv, h);
     }
@@ -404,7 +411,7 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_kernel(MlpArgs a) {
 #pragma unroll
     for (int ks = 0; ks < kHid / 16; ++ks)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc4[q] = mfma(L.w1t[((half * 4 + q) * 8 + ks) * 64 + lane], dz1pk[ks], acc4[q]);
+      for (int q = 0; q < 4; ++q) acc4[q] = mfma(W1T[((half * 4 + q) * 8 + ks) * 64 + lane], dz1pk[ks], acc4[q]);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int mb = half * 4 + q;
@@ -436,7 +443,7 @@ __global__ __launch_bounds__(256) void mlp_pack_kernel(AsvMlpSrc src, AsvMlpWeig
   int row, col;
   if (o < kPackEnc) {
     frag_rc(o, kObsK, false, row, col);
-    const_cast<__bf16*>(static_cast<const __bf16*>(w.enc_frag))[o] = (__bf16)enc_weight(src, row, col);
+    const_cast<elem_t*>(static_cast<const elem_t*>(w.enc_frag))[o] = (elem_t)enc_weight(src, row, col);
     if (o < kEnc)
       const_cast<float*>(w.b_enc)[o] = o < kSelfF ? src.self_b[o] : src.obj_b[(o - kSelfF) % kObjF];
     return;
@@ -445,33 +452,33 @@ __global__ __launch_bounds__(256) void mlp_pack_kernel(AsvMlpSrc src, AsvMlpWeig
   if (o < kPackAe) {
     if (w.ae_frag == nullptr) return;
     frag_rc(o, 16, false, row, col);
-    const_cast<__bf16*>(static_cast<const __bf16*>(w.ae_frag))[o] =
-        (__bf16)(col < kNa ? src.ae_w[row * kNa + col] : 0.f);
+    const_cast<elem_t*>(static_cast<const elem_t*>(w.ae_frag))[o] =
+        (elem_t)(col < kNa ? src.ae_w[row * kNa + col] : 0.f);
     return;
   }
   o -= kPackAe;
   if (src.w1 == nullptr) return;
   if (o < kPackW1) {
     frag_rc(o, kEnc, true, row, col);
-    const_cast<__bf16*>(static_cast<const __bf16*>(w.w1_frag))[o] = (__bf16)src.w1[row * kEnc + col];
+    const_cast<elem_t*>(static_cast<const elem_t*>(w.w1_frag))[o] = (elem_t)src.w1[row * kEnc + col];
     return;
   }
   o -= kPackW1;
   if (o < kPackW2) {
     frag_rc(o, kHid, true, row, col);
-    const_cast<__bf16*>(static_cast<const __bf16*>(w.w2_frag))[o] = (__bf16)src.w2[row * kHid + col];
+    const_cast<elem_t*>(static_cast<const elem_t*>(w.w2_frag))[o] = (elem_t)src.w2[row * kHid + col];
     return;
   }
   o -= kPackW2;
   if (o < kPackW2) {
     frag_rc(o, kHid, true, row, col);
-    const_cast<__bf16*>(static_cast<const __bf16*>(w.w2t_frag))[o] = (__bf16)src.w2[col * kHid + row];
+    const_cast<elem_t*>(static_cast<const elem_t*>(w.w2t_frag))[o] = (elem_t)src.w2[col * kHid + row];
     return;
   }
   o -= kPackW2;
   if (o < kPackW1) {  // W1^T (256 x 128)
     frag_rc(o, kHid, true, row, col);
-    const_cast<__bf16*>(static_cast<const __bf16*>(w.w1t_frag))[o] = (__bf16)src.w1[col * kEnc + row];
+    const_cast<elem_t*>(static_cast<const elem_t*>(w.w1t_frag))[o] = (elem_t)src.w1[col * kEnc + row];
   }
 }
 

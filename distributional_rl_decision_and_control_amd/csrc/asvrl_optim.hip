@@ -7,6 +7,7 @@
 //      see the identical norm), scales g by min(1, max_norm / (norm + 1e-6)) in place, as
 //      clip_grad_norm_ does, then applies Adam with the bias corrections of the new step.
 #include "asvrl_common.h"
+#include "asvrl_mfma.h"
 
 namespace asvrl {
 namespace {
@@ -46,7 +47,7 @@ __device__ __forceinline__ void pack_param(const PackTable& t, int64_t i, float 
       int R = g.row0 + r + q * g.rep_row, Cc = g.col0 + c + q * g.rep_col;
       if (g.transposed) { const int x = R; R = Cc; Cc = x; }
       if (g.f32) static_cast<float*>(g.image)[R] = p;
-      else static_cast<__bf16*>(g.image)[frag_pos(R, Cc, g.K, g.chained != 0)] = static_cast<__bf16>(p);
+      else static_cast<elem_t*>(g.image)[frag_pos(R, Cc, g.K, g.chained != 0)] = static_cast<elem_t>(p);
     }
   }
 }
@@ -188,3 +189,6 @@ extern "C" int asvrl_adam_step_pack(float* params, float* grads, float* exp_avg,
                      norm_out, t, counter);
   return check_launch("asvrl_adam_step_pack");
 }
+
+// 2: bf16 MFMA operands, weight images and saved activations (libasvrl.so); 4: f32 (libasvrl_f32.so)
+extern "C" int32_t asvrl_operand_bytes(void) { return kElemBytes; }

@@ -11,15 +11,16 @@
 // 64 mod 256 bytes, which makes the 32-lane halves of every transposed read conflict-free.
 // Each wave owns a fixed set of 32x32 output blocks for the whole R range of its workgroup;
 // workgroups write f32 partials that a second launch sums in a fixed order (deterministic).
+// The f32 build (ASVRL_OPERAND_F32, asvrl_mfma.h) stages f32 rows (4 per 16-byte chunk) and reads
+// its operand fragments with plain LDS loads into the eight v_mfma_f32_32x32x2_f32 of mfma().
 #include "asvrl_common.h"
+#include "asvrl_mfma.h"
 
 #include <algorithm>
 
 namespace asvrl {
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -32,18 +33,23 @@ constexpr int kMaxGroups = 256;
 #endif
 constexpr int kPF = ASVRL_WGRAD_PF;   // staged chunks in flight per thread
 static_assert(kPF >= 1 && kPF <= 4, "1..4 chunks in flight");
+constexpr int kE16 = 16 / kElemBytes;   // elements per 16-byte staging chunk
+typedef elem_t elem16B __attribute__((ext_vector_type(kE16)));
 
 __host__ __device__ constexpr int lds_stride(int cols) {  // bytes, == 64 (mod 256)
-  return ((2 * cols - 64 + 255) / 256) * 256 + 64;
-}
-
-__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  return ((kElemBytes * cols - 64 + 255) / 256) * 256 + 64;
 }
 
 // Operand fragment of rows [r0, r0 + 16) x columns [c0, c0 + 32) of a row-major LDS image:
 // lane l gets column c0 + (l & 31), rows r0 + 8(l >> 5) + j, j = 0..7.
-__device__ __forceinline__ bf16x8 frag_tr(const char* img, int stride, int r0, int c0, int lane) {
+__device__ __forceinline__ frag8 frag_tr(const char* img, int stride, int r0, int c0, int lane) {
+#if ASVRL_OPERAND_F32
+  const int col = c0 + (lane & 31), rb = r0 + 8 * (lane >> 5);
+  frag8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const float*>(img + (rb + j) * stride + col * 4);
+  return v;
+#else
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
   const int col = c0 + 16 * (g & 1) + 4 * p;
   const int row = r0 + 8 * (g >> 1) + q;
@@ -52,14 +58,15 @@ __device__ __forceinline__ bf16x8 frag_tr(const char* img, int stride, int r0, i
   const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
   const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * stride));
   const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
+  return __builtin_bit_cast(frag8, v);
+#endif
 }
 
 template <int N, int STEP>
-__device__ __forceinline__ void load_rows(u32x4 (&r)[N], const __bf16* __restrict__ base, int64_t ld, int64_t row,
+__device__ __forceinline__ void load_rows(u32x4 (&r)[N], const elem_t* __restrict__ base, int64_t ld, int64_t row,
                                           int c8) {
 #pragma unroll
-  for (int i = 0; i < N; ++i) r[i] = *reinterpret_cast<const u32x4*>(base + (row + i * STEP) * ld + c8 * 8);
+  for (int i = 0; i < N; ++i) r[i] = *reinterpret_cast<const u32x4*>(base + (row + i * STEP) * ld + c8 * kE16);
 }
 
 template <int M, int K, int W = 4>
@@ -70,7 +77,7 @@ struct Shape {
   static constexpr int NMW = kWide ? NBW / NKB : 1;        // m-blocks per wave
   static constexpr int NKW = kWide ? NKB : NBW;            // k-blocks per wave
   static constexpr int SZ = lds_stride(M), SX = lds_stride(K);
-  static constexpr int NCZ = kRC * M / 8, NCX = kRC * K / 8;           // 16-B chunks per staged chunk
+  static constexpr int NCZ = kRC * M / kE16, NCX = kRC * K / kE16;     // 16-B chunks per staged chunk
   static constexpr int CZ = NCZ >= T ? NCZ / T : 1;    // per thread (dZ)
   static constexpr int CX = NCX >= T ? NCX / T : 1;    // (X); fewer chunks than threads: some idle
   static_assert(M % 32 == 0 && K % 32 == 0 && NB % W == 0 && NBW >= 1, "block grid must split over the waves");
@@ -82,7 +89,7 @@ struct Shape {
 // One workgroup's share (`group`) of dW / db: chunks [group * per, (group + 1) * per) into its
 // (M*K + M)-float partial. lz / lx / lbias: the workgroup's LDS (kRC*SZ, kRC*SX bytes, T x 8 floats).
 template <int M, int K, int W>
-__device__ __forceinline__ void wgrad_body(const __bf16* __restrict__ dz, int64_t ldz, const __bf16* __restrict__ x,
+__device__ __forceinline__ void wgrad_body(const elem_t* __restrict__ dz, int64_t ldz, const elem_t* __restrict__ x,
                                            int64_t ldx, int chunks, int chunks_per_group, float* __restrict__ partial,
                                            int group, char* lz, char* lx, float (*lbias)[8]) {
   using S = Shape<M, K, W>;
@@ -91,10 +98,10 @@ __device__ __forceinline__ void wgrad_body(const __bf16* __restrict__ dz, int64_
   const int c_beg = group * chunks_per_group;
   const int c_end = min(chunks, c_beg + chunks_per_group);
 
-  // thread t always stages column chunk t % (M/8) (resp. K/8), rows t / (M/8) + i * (256*8/M)
-  const int zc8 = t % (M / 8), zr = t / (M / 8);
-  const int xc8 = t % (K / 8), xr = t / (K / 8);
-  constexpr int ZRS = kT * 8 / M, XRS = kT * 8 / K;   // row step between a thread's chunks
+  // thread t always stages column chunk t % (M/kE16) (resp. K/kE16), rows t / (M/kE16) + i * (T*kE16/M)
+  const int zc8 = t % (M / kE16), zr = t / (M / kE16);
+  const int xc8 = t % (K / kE16), xr = t / (K / kE16);
+  constexpr int ZRS = kT * kE16 / M, XRS = kT * kE16 / K;   // row step between a thread's chunks
   // threads past the shape's W waves (a 4-wave shape inside the 8-wave multi-layer launch) only
   // take part in the barriers
   const bool in_wg = t < kT;
@@ -126,9 +133,9 @@ __device__ __forceinline__ void wgrad_body(const __bf16* __restrict__ dz, int64_
 #pragma unroll
         for (int i = 0; i < S::CZ; ++i) {
           *reinterpret_cast<u32x4*>(lz + (zr + i * ZRS) * S::SZ + zc8 * 16) = rz[b][i];
-          const bf16x8 v = __builtin_bit_cast(bf16x8, rz[b][i]);
+          const elem16B v = __builtin_bit_cast(elem16B, rz[b][i]);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) bacc[j] += static_cast<float>(v[j]);
+          for (int j = 0; j < kE16; ++j) bacc[j] += static_cast<float>(v[j]);
         }
       }
       if (xact) {
@@ -143,7 +150,7 @@ __device__ __forceinline__ void wgrad_body(const __bf16* __restrict__ dz, int64_
 #pragma unroll
       for (int ks = 0; ks < kRC / 16; ++ks) {
         if (!in_wg) break;
-        bf16x8 fa[S::NMW], fb[S::NKW];
+        frag8 fa[S::NMW], fb[S::NKW];
 #pragma unroll
         for (int i = 0; i < S::NMW; ++i) fa[i] = frag_tr(lz, S::SZ, ks * 16, (mb0 + i) * 32, lane);
 #pragma unroll
@@ -175,19 +182,21 @@ __device__ __forceinline__ void wgrad_body(const __bf16* __restrict__ dz, int64_
 #pragma unroll
   for (int j = 0; j < 8; ++j) lbias[t][j] = bacc[j];
   __syncthreads();
-  if (t < M / 8) {
-    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int u = t; u < kT; u += M / 8)
+  if (t < M / kE16) {
+    float s[kE16];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s[j] += lbias[u][j];
+    for (int j = 0; j < kE16; ++j) s[j] = 0.f;
+    for (int u = t; u < kT; u += M / kE16)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) pw[M * K + t * 8 + j] = s[j];
+      for (int j = 0; j < kE16; ++j) s[j] += lbias[u][j];
+#pragma unroll
+    for (int j = 0; j < kE16; ++j) pw[M * K + t * kE16 + j] = s[j];
   }
 }
 
 template <int M, int K, int W>
-__global__ __launch_bounds__(W * 64) void wgrad_kernel(const __bf16* __restrict__ dz, int64_t ldz,
-                                                        const __bf16* __restrict__ x, int64_t ldx, int chunks,
+__global__ __launch_bounds__(W * 64) void wgrad_kernel(const elem_t* __restrict__ dz, int64_t ldz,
+                                                        const elem_t* __restrict__ x, int64_t ldx, int chunks,
                                                         int chunks_per_group, float* __restrict__ partial) {
   using S = Shape<M, K, W>;
   __shared__ __attribute__((aligned(16))) char lz[kRC * S::SZ];
@@ -200,7 +209,7 @@ __global__ __launch_bounds__(W * 64) void wgrad_kernel(const __bf16* __restrict_
 // Thread t reads 16 bytes (8 columns) of row t / (K/8) + i * RP: RP rows in flight per block.
 // Threads 0..255 work; every thread of the workgroup must call it. sa: 256 x 9 floats of LDS.
 template <int K>
-__device__ __forceinline__ void wgrad_vec_body(const float* __restrict__ dq, int64_t ldq, const __bf16* __restrict__ x,
+__device__ __forceinline__ void wgrad_vec_body(const float* __restrict__ dq, int64_t ldq, const elem_t* __restrict__ x,
                                                int64_t ldx, int R, int rows_per_group, float* __restrict__ partial,
                                                int group, float (*sa)[9]) {
   constexpr int C8 = K / 8, RP = kWgThreads / C8;
@@ -210,7 +219,7 @@ __device__ __forceinline__ void wgrad_vec_body(const float* __restrict__ dq, int
   float b = 0.f;
   for (int r = r_beg + rr; r < r_end; r += RP) {
     const float d = dq[static_cast<int64_t>(r) * ldq];
-    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + static_cast<int64_t>(r) * ldx + c8 * 8);
+    const frag8 v = *reinterpret_cast<const frag8*>(x + static_cast<int64_t>(r) * ldx + c8 * 8);
 #pragma unroll
     for (int j = 0; j < 8; ++j) a[j] += d * static_cast<float>(v[j]);
     b += d;
@@ -236,7 +245,7 @@ __device__ __forceinline__ void wgrad_vec_body(const float* __restrict__ dq, int
 
 template <int K>
 __global__ __launch_bounds__(kWgThreads) void wgrad_vec_kernel(const float* __restrict__ dq, int64_t ldq,
-                                                                const __bf16* __restrict__ x, int64_t ldx, int R,
+                                                                const elem_t* __restrict__ x, int64_t ldx, int R,
                                                                 int rows_per_group, float* __restrict__ partial) {
   __shared__ float sa[kWgThreads][9];
   wgrad_vec_body<K>(dq, ldq, x, ldx, R, rows_per_group, partial, blockIdx.x, sa);
@@ -269,7 +278,7 @@ constexpr int kMultiStage = cmax(cmax(cmax(stage_bytes<256, 64>(), stage_bytes<1
 template <int M, int K, int W = kMultiW>
 __device__ __forceinline__ void multi_run(const WgSeg& g, int group, char* lds, float (*lbias)[8]) {
   using S = Shape<M, K, W>;
-  wgrad_body<M, K, W>(static_cast<const __bf16*>(g.dz), g.ldz, static_cast<const __bf16*>(g.x), g.ldx,
+  wgrad_body<M, K, W>(static_cast<const elem_t*>(g.dz), g.ldz, static_cast<const elem_t*>(g.x), g.ldx,
                             g.chunks, g.per, g.partial, group, lds, lds + kRC * S::SZ, lbias);
 }
 
@@ -291,7 +300,7 @@ __global__ __launch_bounds__(kMultiW * 64, ASVRL_WGRAD_MULTI_WAVES) void wgrad_m
     case WG_256x32: multi_run<256, 32>(g, group, lds, lbias); break;
     case WG_32x128: multi_run<32, 128, 4>(g, group, lds, lbias); break;   // 4 of the 8 waves
     case WG_VEC128:
-      wgrad_vec_body<128>(static_cast<const float*>(g.dz), g.ldz, static_cast<const __bf16*>(g.x), g.ldx, g.chunks,
+      wgrad_vec_body<128>(static_cast<const float*>(g.dz), g.ldz, static_cast<const elem_t*>(g.x), g.ldx, g.chunks,
                           g.per, g.partial, group, reinterpret_cast<float(*)[9]>(&lbias[0][0]));
       break;
     default:
@@ -580,7 +589,7 @@ int vec_groups(int R) {
 }
 
 template <int M, int K, int W = (M * K >= 8192 ? 8 : 4)>
-int launch_wgrad(const __bf16* dz, int64_t ldz, const __bf16* x, int64_t ldx, int R, float* work, hipStream_t st,
+int launch_wgrad(const elem_t* dz, int64_t ldz, const elem_t* x, int64_t ldx, int R, float* work, hipStream_t st,
                  int& groups) {
   // partial traffic is groups * M * K floats: capped near 32 MB for the large layers
   const int chunks = R / kRC;
@@ -626,8 +635,8 @@ extern "C" int asvrl_linear_wgrad_partial(const void* dz, int64_t ldz, const voi
   *groups_out = 0;
   if (R == 0) return 0;
   hipStream_t st = as_stream(stream);
-  const __bf16* z = static_cast<const __bf16*>(dz);
-  const __bf16* xx = static_cast<const __bf16*>(x);
+  const elem_t* z = static_cast<const elem_t*>(dz);
+  const elem_t* xx = static_cast<const elem_t*>(x);
   int groups = 0, rc = 0;
   if (M == 256 && K == 64) rc = launch_wgrad<256, 64>(z, ldz, xx, ldx, R, partial, st, groups);
   else if (M == 128 && K == 256) rc = launch_wgrad<128, 256>(z, ldz, xx, ldx, R, partial, st, groups);
@@ -746,7 +755,7 @@ extern "C" int asvrl_linear_wgrad_vec_partial(const float* dq, int64_t ldq, cons
   hipStream_t st = as_stream(stream);
   const int groups = vec_groups(R);
   const int per = (R + groups - 1) / groups;
-  const __bf16* xx = static_cast<const __bf16*>(x);
+  const elem_t* xx = static_cast<const elem_t*>(x);
   if (K == 128) hipLaunchKernelGGL(wgrad_vec_kernel<128>, dim3(groups), dim3(kWgThreads), 0, st, dq, ldq, xx, ldx, R, per, partial);
   else if (K == 256) hipLaunchKernelGGL(wgrad_vec_kernel<256>, dim3(groups), dim3(kWgThreads), 0, st, dq, ldq, xx, ldx, R, per, partial);
   else hipLaunchKernelGGL(wgrad_vec_kernel<64>, dim3(groups), dim3(kWgThreads), 0, st, dq, ldq, xx, ldx, R, per, partial);

@@ -43,12 +43,16 @@ def frag_index(M, K, chained, device):
 
 
 class CriticPack:
-    """bf16 fragment images of one Critic's trunk weights + pointers (AsvCriticWeights)."""
+    """bf16 fragment images of one Critic's trunk weights + pointers (AsvCriticWeights).
+    operands="f32": f32 images for libasvrl_f32.so (the parity build); every launch on this pack
+    goes to the library of its operand type (self.L)."""
 
-    def __init__(self, critic):
+    def __init__(self, critic, operands="bf16"):
         dev = critic.cos_embedding.weight.device
         self.critic = critic
-        bf = dict(dtype=torch.bfloat16, device=dev)
+        self.operands = operands
+        self.L = _abi.lib(operands)
+        bf = dict(dtype=_abi.operand_dtype(operands), device=dev)
         self.wc = torch.empty(256 * 64, **bf)
         self.w1 = torch.empty(128 * 256, **bf)
         self.w2 = torch.empty(128 * 128, **bf)
@@ -84,10 +88,10 @@ class CriticPack:
     def refresh(self, stream=None):
         """Re-pack from the critic's current f32 weights: one asvrl_critic_pack launch."""
         c = self.critic
-        rc = _abi.lib().asvrl_critic_pack(_abi.ptr(c.cos_embedding.weight), _abi.ptr(c.hidden_layer.weight),
-                                          _abi.ptr(c.hidden_layer_2.weight), C.byref(self.struct),
-                                          _abi.stream_ptr(stream))
-        _abi.check(rc, "asvrl_critic_pack")
+        rc = self.L.asvrl_critic_pack(_abi.ptr(c.cos_embedding.weight), _abi.ptr(c.hidden_layer.weight),
+                                      _abi.ptr(c.hidden_layer_2.weight), C.byref(self.struct),
+                                      _abi.stream_ptr(stream))
+        _abi.check(rc, "asvrl_critic_pack", self.L)
 
     @torch.no_grad()
     def reference_images(self):
@@ -97,7 +101,7 @@ class CriticPack:
         out = {}
         for name, W in (("wc", c.cos_embedding.weight), ("w1", W1), ("w2", W2), ("w2t", W2.t().contiguous()),
                         ("w1t", W1.t().contiguous())):
-            out[name] = torch.index_select(W.reshape(-1), 0, self.idx[name]).to(torch.bfloat16)
+            out[name] = torch.index_select(W.reshape(-1), 0, self.idx[name]).to(_abi.operand_dtype(self.operands))
         return out
 
 
@@ -127,15 +131,17 @@ def critic_forward(pack, F, G, taus, N, q=None, stream=None, obs=None, act=None)
     B = (F if F is not None else obs).shape[0]
     q = q if q is not None else torch.empty(B * N, dtype=torch.float32, device=taus.device)
     io = _io(F, G, taus, N, obs=obs, act=act, q=q)
-    _abi.check(_abi.lib().asvrl_critic_forward(C.byref(pack.struct), C.byref(io), _abi.stream_ptr(stream)),
-               "asvrl_critic_forward")
+    _abi.check(pack.L.asvrl_critic_forward(C.byref(pack.struct), C.byref(io), _abi.stream_ptr(stream)),
+               "asvrl_critic_forward", pack.L)
     return q.view(B, N)
 
 
 class TrainBuffers:
-    def __init__(self, B, N, device):
+    """Saved activations of one TRAIN pass (operand dtype of the build, see CriticPack)."""
+
+    def __init__(self, B, N, device, operands="bf16"):
         R = B * N
-        bf = dict(dtype=torch.bfloat16, device=device)
+        bf = dict(dtype=_abi.operand_dtype(operands), device=device)
         self.B, self.N = B, N
         self.cos = torch.empty(R, 64, **bf)
         self.h0 = torch.empty(R, 256, **bf)
@@ -150,7 +156,7 @@ class TrainBuffers:
         self.q = torch.empty(R, **f)
         self.dF = torch.empty(B, 256, **f)
         self.dG = torch.empty(B, 128, **f)
-        self.work_floats = max(int(_abi.lib().asvrl_linear_wgrad_workspace(M, K))
+        self.work_floats = max(int(_abi.lib(operands).asvrl_linear_wgrad_workspace(M, K))
                                for M, K in ((256, 64), (128, 256), (128, 128)))
         self.work = torch.empty(self.work_floats, **f)
         a = _abi.AsvCriticActs()
@@ -190,8 +196,8 @@ def critic_train(pack, F, G, taus, q_targets, bufs, kappa=1.0, stream=None, q_ne
         acts = _abi.AsvCriticActs()
         C.memmove(C.byref(acts), C.byref(bufs.struct), C.sizeof(acts))
         acts.h2, acts.dq, acts.wout_part = None, None, wout_part.data_ptr()
-    _abi.check(_abi.lib().asvrl_critic_train(C.byref(pack.struct), C.byref(io), C.byref(acts),
-                                             _abi.stream_ptr(stream)), "asvrl_critic_train")
+    _abi.check(pack.L.asvrl_critic_train(C.byref(pack.struct), C.byref(io), C.byref(acts),
+                                         _abi.stream_ptr(stream)), "asvrl_critic_train", pack.L)
     if tile_loss is not None:
         return None
     return bufs.row_loss.sum() / float(B * Np)
@@ -204,8 +210,8 @@ def critic_actor_grad(pack, F, G, taus, N, q, dG=None, stream=None, w_ae=None, d
     B = (F if F is not None else obs).shape[0]
     io = _io(F, G, taus, N, obs=obs, act=act, dq=-1.0 / float(B * N), q=q, dG=dG, w_ae=w_ae, dA=dA,
              tile_loss=tile_loss, loss_scale=-1.0 / float(B * N))
-    _abi.check(_abi.lib().asvrl_critic_actor_grad(C.byref(pack.struct), C.byref(io), _abi.stream_ptr(stream)),
-               "asvrl_critic_actor_grad")
+    _abi.check(pack.L.asvrl_critic_actor_grad(C.byref(pack.struct), C.byref(io), _abi.stream_ptr(stream)),
+               "asvrl_critic_actor_grad", pack.L)
 
 
 def linear_wgrad(dz, x, dw, db, work, accumulate=False, stream=None):
@@ -230,9 +236,12 @@ def linear_wgrad_vec(dq, x, dw, db, work, accumulate=False, stream=None):
 class PartialArena:
     """Weight-gradient partials of several layers, reduced together by ONE asvrl_partial_sums
     launch (instead of one reduction launch per layer). Regions are handed out in call order
-    from one preallocated buffer, so the pointers repeat exactly under HIP-graph replay."""
+    from one preallocated buffer, so the pointers repeat exactly under HIP-graph replay.
+    operands: the learner build whose activations it reduces (bf16 / f32, see CriticPack)."""
 
-    def __init__(self, floats, device):
+    def __init__(self, floats, device, operands="bf16"):
+        self.L = _abi.lib(operands)
+        self.dtype = _abi.operand_dtype(operands)
         self.buf = torch.empty(int(floats), dtype=torch.float32, device=device)
         self.off = 0
         self.segs = []
@@ -274,17 +283,17 @@ class PartialArena:
                 chunk = segs[i:i + _abi.MAX_WGRAD_SEGS]
                 arr = (_abi.AsvWgradSeg * len(chunk))(*chunk)
                 groups = (C.c_int32 * len(chunk))()
-                _abi.check(_abi.lib().asvrl_linear_wgrad_multi(arr, len(chunk), groups, _abi.stream_ptr(stream)),
-                           "asvrl_linear_wgrad_multi")
+                _abi.check(self.L.asvrl_linear_wgrad_multi(arr, len(chunk), groups, _abi.stream_ptr(stream)),
+                           "asvrl_linear_wgrad_multi", self.L)
 
     def _linear_partial(self, dz, x, stream):
         R, M = dz.shape
         K = x.shape[1]
-        L = _abi.lib()
+        L = self.L
         ngroups = int(L.asvrl_linear_wgrad_groups(R, M, K))
         part = self._take(ngroups * (M * K + M))
         if self.pending is not None:
-            assert dz.dtype == x.dtype == torch.bfloat16 and dz.stride(1) == 1 and x.stride(1) == 1
+            assert dz.dtype == x.dtype == self.dtype and dz.stride(1) == 1 and x.stride(1) == 1
             g = _abi.AsvWgradSeg()
             g.dz, g.ldz, g.x, g.ldx = dz.data_ptr(), dz.stride(0), x.data_ptr(), x.stride(0)
             g.R, g.M, g.K, g.partial, g.partial_floats = R, M, K, part.data_ptr(), part.numel()
@@ -294,7 +303,7 @@ class PartialArena:
         groups = C.c_int32(0)
         _abi.check(L.asvrl_linear_wgrad_partial(_abi.ptr(dz), dz.stride(0), _abi.ptr(x), x.stride(0), R, M, K,
                                                 _abi.ptr(part), part.numel(), C.byref(groups),
-                                                _abi.stream_ptr(stream)), "asvrl_linear_wgrad_partial")
+                                                _abi.stream_ptr(stream)), "asvrl_linear_wgrad_partial", L)
         return part, groups.value, M, K
 
     def linear(self, dz, x, dw, db, accumulate=False, stream=None):
@@ -326,18 +335,18 @@ class PartialArena:
 
     def vec(self, dq, x, dw, db, accumulate=False, stream=None):
         R, K = x.shape
-        L = _abi.lib()
+        L = self.L
         ngroups = int(L.asvrl_linear_wgrad_vec_groups(R))
         part = self._take(ngroups * (K + 1))
         if self.pending is not None and K == 128:
-            assert dq.dtype == torch.float32 and x.dtype == torch.bfloat16 and x.stride(1) == 1
+            assert dq.dtype == torch.float32 and x.dtype == self.dtype and x.stride(1) == 1
             self._queue(_abi.WGRAD_VEC, dq, dq.stride(0), x, x.stride(0), R, 1, K, part)
             self._seg(part, dw, db, ngroups, K, 1, accumulate)
             return
         groups = C.c_int32(0)
         _abi.check(L.asvrl_linear_wgrad_vec_partial(_abi.ptr(dq), dq.stride(0), _abi.ptr(x), x.stride(0), R, K,
                                                     _abi.ptr(part), part.numel(), C.byref(groups),
-                                                    _abi.stream_ptr(stream)), "asvrl_linear_wgrad_vec_partial")
+                                                    _abi.stream_ptr(stream)), "asvrl_linear_wgrad_vec_partial", L)
         self._seg(part, dw, db, groups.value, K, 1, accumulate)
 
     def take_tiles(self, tiles, nw):
@@ -363,9 +372,9 @@ class PartialArena:
             self._seg(part, dw, db, (R + 31) // 32, M * K, M, accumulate)
             return
         groups = C.c_int32(0)
-        _abi.check(_abi.lib().asvrl_small_wgrad_partial(dz.data_ptr(), dz.stride(0), x.data_ptr(), x.stride(0), R,
-                                                        M, K, part.data_ptr(), part.numel(), C.byref(groups),
-                                                        _abi.stream_ptr(stream)), "asvrl_small_wgrad_partial")
+        _abi.check(self.L.asvrl_small_wgrad_partial(dz.data_ptr(), dz.stride(0), x.data_ptr(), x.stride(0), R,
+                                                    M, K, part.data_ptr(), part.numel(), C.byref(groups),
+                                                    _abi.stream_ptr(stream)), "asvrl_small_wgrad_partial", self.L)
         self._seg(part, dw, db, groups.value, M * K, M, accumulate)
 
     def flush(self, stream=None, norm=None):
@@ -374,15 +383,16 @@ class PartialArena:
         self.norm_parts[:self.nparts] and advances its step, for norm.step_prenormed(...)."""
         if self.segs:
             arr = (_abi.AsvPartialSum * len(self.segs))(*self.segs)
-            L = _abi.lib()
+            L = self.L
             if norm is not None:
                 self.nparts = int(L.asvrl_partial_sums_norm_parts(arr, len(self.segs)))
                 assert 1 <= self.nparts <= self.norm_parts.numel()
                 _abi.check(L.asvrl_partial_sums_norm(arr, len(self.segs), _abi.ptr(self.norm_parts),
                                                      _abi.ptr(norm.step_t), _abi.stream_ptr(stream)),
-                           "asvrl_partial_sums_norm")
+                           "asvrl_partial_sums_norm", L)
             else:
-                _abi.check(L.asvrl_partial_sums(arr, len(self.segs), _abi.stream_ptr(stream)), "asvrl_partial_sums")
+                _abi.check(L.asvrl_partial_sums(arr, len(self.segs), _abi.stream_ptr(stream)), "asvrl_partial_sums",
+                           L)
         elif norm is not None:
             raise RuntimeError("PartialArena.flush(norm=...) with nothing queued")
         self.segs = []

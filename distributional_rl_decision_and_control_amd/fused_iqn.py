@@ -45,17 +45,18 @@ def supported(net, B, N):
 
 class IqnPack(CriticPack):
     """bf16 images of one IQN_Policy: the trunk (CriticPack's five) and the padded output head,
-    one refresh launch; the observation encoders are read in f32 by the kernels themselves."""
+    one refresh launch; the observation encoders are read in f32 by the kernels themselves.
+    operands="f32": the f32 images of libasvrl_f32.so (the parity build)."""
 
-    def __init__(self, net):
+    def __init__(self, net, operands="bf16"):
         dev = net.cos_embedding.weight.device
-        self.head_img = torch.zeros(_abi.IQN_MAX_ACTIONS * 128, dtype=torch.bfloat16, device=dev)
+        self.head_img = torch.zeros(_abi.IQN_MAX_ACTIONS * 128, dtype=_abi.operand_dtype(operands), device=dev)
         hd = _abi.AsvIqnHead()
         hd.wo_frag, hd.wo, hd.bo = (self.head_img.data_ptr(), net.output_layer.weight.data_ptr(),
                                     net.output_layer.bias.data_ptr())
         hd.n_actions = net.action_size
         self.head = hd
-        super().__init__(net)
+        super().__init__(net, operands)
 
     def adam_segments(self, opt):
         """The trunk images and the head's leading rows (the padding rows stay zero)."""
@@ -64,10 +65,10 @@ class IqnPack(CriticPack):
 
     def refresh(self, stream=None):
         n = self.critic
-        rc = _abi.lib().asvrl_iqn_pack(_abi.ptr(n.cos_embedding.weight), _abi.ptr(n.hidden_layer.weight),
-                                       _abi.ptr(n.hidden_layer_2.weight), _abi.ptr(n.output_layer.weight),
-                                       C.byref(self.struct), C.byref(self.head), _abi.stream_ptr(stream))
-        _abi.check(rc, "asvrl_iqn_pack")
+        rc = self.L.asvrl_iqn_pack(_abi.ptr(n.cos_embedding.weight), _abi.ptr(n.hidden_layer.weight),
+                                   _abi.ptr(n.hidden_layer_2.weight), _abi.ptr(n.output_layer.weight),
+                                   C.byref(self.struct), C.byref(self.head), _abi.stream_ptr(stream))
+        _abi.check(rc, "asvrl_iqn_pack", self.L)
 
 
 def _io(F, N, obs=None, xb=None, **kw):
@@ -92,8 +93,8 @@ def _io(F, N, obs=None, xb=None, **kw):
 def iqn_forward_max(pack, F, taus, N, q, stream=None, obs=None):
     """q[b*N + n] = max_a Q(s_b, tau_bn, a) (the target of train_IQN)."""
     io = _io(F, N, obs=obs, taus=taus, q=q)
-    _abi.check(_abi.lib().asvrl_iqn_forward_max(C.byref(pack.struct), C.byref(pack.head), C.byref(io),
-                                                _abi.stream_ptr(stream)), "asvrl_iqn_forward_max")
+    _abi.check(pack.L.asvrl_iqn_forward_max(C.byref(pack.struct), C.byref(pack.head), C.byref(io),
+                                            _abi.stream_ptr(stream)), "asvrl_iqn_forward_max", pack.L)
     return q
 
 
@@ -108,8 +109,8 @@ def iqn_train(pack, F, taus, bufs, dz_out, q_next, actions, rewards, dones, gamm
     io = _io(F, N, obs=obs, xb=xb, taus=taus, Np=Np, kappa=float(kappa), q_next=q_next, actions=actions, rewards=rewards,
              dones=dones, ld_rd=rewards.stride(0), gamma=float(gamma), q=q, row_loss=bufs.row_loss, dzF=dzF,
              dz_out=dz_out, tile_loss=tile_loss, loss_scale=1.0 / float(B * Np))
-    _abi.check(_abi.lib().asvrl_iqn_train(C.byref(pack.struct), C.byref(pack.head), C.byref(io),
-                                          C.byref(bufs.struct), _abi.stream_ptr(stream)), "asvrl_iqn_train")
+    _abi.check(pack.L.asvrl_iqn_train(C.byref(pack.struct), C.byref(pack.head), C.byref(io),
+                                      C.byref(bufs.struct), _abi.stream_ptr(stream)), "asvrl_iqn_train", pack.L)
 
 
 def iqn_act(pack, F, actions64, step_dev, steps_per_count, total, fraction, initial, final, seed, taus=None,
@@ -118,27 +119,29 @@ def iqn_act(pack, F, actions64, step_dev, steps_per_count, total, fraction, init
     io = _io(F, K_ACT, obs=obs, taus=taus, act_out=actions64, ld_act=actions64.stride(0), step_dev=step_dev,
              eps_steps_per_count=float(steps_per_count), eps_total=float(total), eps_fraction=float(fraction),
              eps_initial=float(initial), eps_final=float(final), seed=int(seed) & 0xFFFFFFFFFFFFFFFF)
-    _abi.check(_abi.lib().asvrl_iqn_act(C.byref(pack.struct), C.byref(pack.head), C.byref(io),
-                                        _abi.stream_ptr(stream)), "asvrl_iqn_act")
+    _abi.check(pack.L.asvrl_iqn_act(C.byref(pack.struct), C.byref(pack.head), C.byref(io),
+                                    _abi.stream_ptr(stream)), "asvrl_iqn_act", pack.L)
 
 
 class FusedIQNState:
-    """Packs and buffers of the fused IQN update (allocated once, pointer-stable for graphs)."""
+    """Packs and buffers of the fused IQN update (allocated once, pointer-stable for graphs).
+    operands="f32": every kernel from libasvrl_f32.so (the parity build; the optimiser must be a
+    FusedAdam of the same operands)."""
 
-    def __init__(self, net_local, net_target, B, N):
+    def __init__(self, net_local, net_target, B, N, operands="bf16"):
         dev = net_local.cos_embedding.weight.device
         self.B, self.N, self.device = B, N, dev
         self.A = net_local.action_size
-        self.local = IqnPack(net_local)
-        self.target = IqnPack(net_target)
-        self.bufs = TrainBuffers(B, N, dev)
+        self.local = IqnPack(net_local, operands)
+        self.target = IqnPack(net_target, operands)
+        self.bufs = TrainBuffers(B, N, dev, operands)
         f = dict(dtype=torch.float32, device=dev)
-        bf = dict(dtype=torch.bfloat16, device=dev)
+        bf = dict(dtype=_abi.operand_dtype(operands), device=dev)
         self.xb = torch.empty(B, 32, **bf)
         self.q_next = torch.empty(B * N, **f)
         self.dzF = torch.empty(B, 256, **bf)
         self.dz_out = torch.empty(B * N, _abi.IQN_MAX_ACTIONS, **bf)
-        self.arena = PartialArena(32 << 20, dev)
+        self.arena = PartialArena(32 << 20, dev, operands)
         self.loss = torch.zeros(1, **f)
         self.tile_loss = torch.zeros(B * N // 32, **f)
         self.side = SideStreams(dev, 2)

@@ -26,13 +26,16 @@ def _p(t):
 
 class MlpPack:
     """Packed images of an Actor (kind='actor'), of a Critic's encoders + action encoder
-    (kind='critic') or of the observation encoders alone (kind='encoders', IQN_Policy)."""
+    (kind='critic') or of the observation encoders alone (kind='encoders', IQN_Policy).
+    operands="f32": f32 images for libasvrl_f32.so (the parity build); launches go to self.L."""
 
-    def __init__(self, net, kind):
+    def __init__(self, net, kind, operands="bf16"):
         assert kind in ("actor", "critic", "encoders")
         self.net, self.kind = net, kind
+        self.operands = operands
+        self.L = _abi.lib(operands)
         dev = net.self_encoder[0].weight.device
-        bf = dict(dtype=torch.bfloat16, device=dev)
+        bf = dict(dtype=_abi.operand_dtype(operands), device=dev)
         self.enc = torch.zeros(ENC * OBSK, **bf)
         self.b_enc = torch.zeros(ENC, dtype=torch.float32, device=dev)
         w = _abi.AsvMlpWeights()
@@ -86,8 +89,8 @@ class MlpPack:
 
     def refresh(self, stream=None):
         src = self.src()
-        _abi.check(_abi.lib().asvrl_mlp_pack(C.byref(src), C.byref(self.w), _abi.stream_ptr(stream)),
-                   "asvrl_mlp_pack")
+        _abi.check(self.L.asvrl_mlp_pack(C.byref(src), C.byref(self.w), _abi.stream_ptr(stream)),
+                   "asvrl_mlp_pack", self.L)
 
 
 def _rows(x):
@@ -104,8 +107,8 @@ def mlp_encode(pack, x, F, G=None, act=None, xb=None, stream=None):
     io.F, io.G, io.xb = _p(F), _p(G), _p(xb)
     if act is not None:
         io.act, io.lda = act.data_ptr(), act.stride(0)
-    _abi.check(_abi.lib().asvrl_mlp_encode(C.byref(pack.w), C.byref(io), _abi.stream_ptr(stream)),
-               "asvrl_mlp_encode")
+    _abi.check(pack.L.asvrl_mlp_encode(C.byref(pack.w), C.byref(io), _abi.stream_ptr(stream)),
+               "asvrl_mlp_encode", pack.L)
 
 
 def actor_forward(pack, x, a_out, stream=None):
@@ -114,8 +117,8 @@ def actor_forward(pack, x, a_out, stream=None):
     io = _abi.AsvMlpIO()
     io.x, io.ldx, io.n = x.data_ptr(), ldx, x.shape[0]
     io.a_out, io.ld_aout = a_out.data_ptr(), a_out.stride(0)
-    _abi.check(_abi.lib().asvrl_actor_forward(C.byref(pack.w), C.byref(io), MODE_FWD, _abi.stream_ptr(stream)),
-               "asvrl_actor_forward")
+    _abi.check(pack.L.asvrl_actor_forward(C.byref(pack.w), C.byref(io), MODE_FWD, _abi.stream_ptr(stream)),
+               "asvrl_actor_forward", pack.L)
 
 
 def actor_act(pack, x, actions64, step_dev, steps_per_count, total, fraction, initial, final, seed, stream=None):
@@ -127,15 +130,16 @@ def actor_act(pack, x, actions64, step_dev, steps_per_count, total, fraction, in
     io.step_dev = step_dev.data_ptr()
     io.eps_steps_per_count, io.eps_total, io.eps_fraction = float(steps_per_count), float(total), float(fraction)
     io.eps_initial, io.eps_final, io.seed = float(initial), float(final), int(seed) & 0xFFFFFFFFFFFFFFFF
-    _abi.check(_abi.lib().asvrl_actor_forward(C.byref(pack.w), C.byref(io), MODE_ACT, _abi.stream_ptr(stream)),
-               "asvrl_actor_forward(act)")
+    _abi.check(pack.L.asvrl_actor_forward(C.byref(pack.w), C.byref(io), MODE_ACT, _abi.stream_ptr(stream)),
+               "asvrl_actor_forward(act)", pack.L)
 
 
 class ActorBuffers:
-    """Saved activations and backward outputs of one Actor training pass over B rows."""
+    """Saved activations and backward outputs of one Actor training pass over B rows (operand dtype
+    of the build, see MlpPack)."""
 
-    def __init__(self, B, device):
-        bf = dict(dtype=torch.bfloat16, device=device)
+    def __init__(self, B, device, operands="bf16"):
+        bf = dict(dtype=_abi.operand_dtype(operands), device=device)
         f = dict(dtype=torch.float32, device=device)
         self.B = B
         self.xb = torch.empty(B, OBSK, **bf)
@@ -166,16 +170,16 @@ class ActorBuffers:
 
 def actor_train_forward(pack, x, bufs, stream=None):
     io = bufs.io(x)
-    _abi.check(_abi.lib().asvrl_actor_forward(C.byref(pack.w), C.byref(io), MODE_TRAIN, _abi.stream_ptr(stream)),
-               "asvrl_actor_forward(train)")
+    _abi.check(pack.L.asvrl_actor_forward(C.byref(pack.w), C.byref(io), MODE_TRAIN, _abi.stream_ptr(stream)),
+               "asvrl_actor_forward(train)", pack.L)
     return bufs.a_out
 
 
 def actor_backward(pack, bufs, stream=None):
     """bufs.dA -> dout, dz2, dz1, dz0 (pre-activation gradients of every Actor layer)."""
     io = bufs.io()
-    _abi.check(_abi.lib().asvrl_actor_backward(C.byref(pack.w), C.byref(io), _abi.stream_ptr(stream)),
-               "asvrl_actor_backward")
+    _abi.check(pack.L.asvrl_actor_backward(C.byref(pack.w), C.byref(io), _abi.stream_ptr(stream)),
+               "asvrl_actor_backward", pack.L)
 
 
 def encoder_fold(dw, db, net, accumulate=False, stream=None):

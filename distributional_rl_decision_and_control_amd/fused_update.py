@@ -34,6 +34,7 @@ import os
 
 import torch
 
+from . import _abi
 from .fused_critic import (CriticPack, PartialArena, TrainBuffers, critic_actor_grad, critic_forward, critic_train,
                            trunk_weight_grads_into, wout_groups)
 from .fused_mlp import ActorBuffers, MlpPack, actor_act, actor_backward, actor_forward, actor_train_forward
@@ -76,20 +77,23 @@ def supported(policy, B, N):
 
 
 class FusedACIQNState:
-    """Packs and buffers of the fused update (allocated once, pointer-stable for graph replay)."""
+    """Packs and buffers of the fused update (allocated once, pointer-stable for graph replay).
+    operands="f32": every kernel from libasvrl_f32.so, the f32-operand parity build of the same
+    sources (the optimisers must be FusedAdam of the same operands)."""
 
-    def __init__(self, policy_local, policy_target, B, N):
+    def __init__(self, policy_local, policy_target, B, N, operands="bf16"):
         dev = policy_local.critic.cos_embedding.weight.device
         self.B, self.N, self.device = B, N, dev
+        self.operands = operands
         # the critic's encoders run inside the trunk kernels (f32, straight from the parameters)
-        self.local_trunk = CriticPack(policy_local.critic)
-        self.target_trunk = CriticPack(policy_target.critic)
-        self.actor = MlpPack(policy_local.actor, "actor")
-        self.target_actor = MlpPack(policy_target.actor, "actor")
-        self.bufs = TrainBuffers(B, N, dev)
-        self.abufs = ActorBuffers(B, dev)
+        self.local_trunk = CriticPack(policy_local.critic, operands)
+        self.target_trunk = CriticPack(policy_target.critic, operands)
+        self.actor = MlpPack(policy_local.actor, "actor", operands)
+        self.target_actor = MlpPack(policy_target.actor, "actor", operands)
+        self.bufs = TrainBuffers(B, N, dev, operands)
+        self.abufs = ActorBuffers(B, dev, operands)
         f = dict(dtype=torch.float32, device=dev)
-        bf = dict(dtype=torch.bfloat16, device=dev)
+        bf = dict(dtype=_abi.operand_dtype(operands), device=dev)
         self.na = torch.empty(B, 2, **f)
         self.na_p = torch.empty(B, 2, **f)       # the pipelined target chain's actions
         self.xb = torch.empty(B, 32, **bf)
@@ -98,7 +102,7 @@ class FusedACIQNState:
         self.q_pi = torch.empty(B * N, **f)
         self.dzF = torch.empty(B, 256, **bf)
         self.dzG = torch.empty(B, 128, **f)
-        self.arena = PartialArena(32 << 20, dev)
+        self.arena = PartialArena(32 << 20, dev, operands)
         self.losses = torch.zeros(2, **f)   # critic, actor loss (summed from per-tile partials)
         self.tile_loss = torch.zeros(2, B * N // 32, **f)
         self.side = SideStreams(dev, 3)   # 0, 1: gradient reductions / actor forward; 2: next batch
@@ -118,6 +122,7 @@ def _reduce_and_step(arena, opt, grads, sync, max_norm, wait=None, pack=None, co
     weight images of `pack` (a CriticPack / MlpPack / IqnPack) and increments `counter` (two launches
     in all); otherwise reduce, all-reduce (sync), asvrl_adam_clip, then pack.refresh() and
     counter += 1. `wait`: an event to wait for before the parameters change."""
+    assert pack is None or not isinstance(opt, FusedAdam) or opt.L is pack.L, "optimiser and pack of different builds"
     if sync is None and isinstance(opt, FusedAdam):
         arena.flush(norm=opt)
         if wait is not None:

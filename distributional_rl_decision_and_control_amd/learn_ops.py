@@ -139,6 +139,24 @@ def split_rows(rows):
     return s, rows[:, 80:82], rows[:, 82:83], ns, rows[:, 83:84]
 
 
+def rows_from_batch(states, actions, rewards, next_states, dones):
+    """The inverse of split_rows: (B, 88) f32 replay rows from Agent.train_*'s batch tensors (objects /
+    mask may be None: state_batch's all-empty case, numerically all-masked, AC_IQN_model.py:293-294);
+    actions (B, 1) or (B, 2)."""
+    B = states[0].shape[0]
+    rows = torch.zeros(B, 88, dtype=torch.float32, device=states[0].device)
+    for c, st in ((0, states), (OBS_DIM, next_states)):
+        rows[:, c:c + 7] = st[0]
+        if st[1] is not None:
+            rows[:, c + 7:c + 32] = st[1].reshape(B, 25)
+            rows[:, c + 32:c + 37] = st[2]
+    a = actions.reshape(B, -1)
+    rows[:, 80:80 + a.shape[1]] = a
+    rows[:, 82] = rewards.reshape(B)
+    rows[:, 83] = dones.reshape(B)
+    return rows
+
+
 # ---------------------------------------------------------------------- prioritised replay
 class DevicePER:
     """Rainbow's prioritised n-step replay (ReplayMemory + SegmentTree,

@@ -77,7 +77,9 @@ class FusedAdam:
     same order; `grads` is that FlatGrads, to be all-reduced by GradSync before step().
     Construct it before anything caches parameter pointers (CriticPack)."""
 
-    def __init__(self, params, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, max_norm=0.5):
+    def __init__(self, params, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, max_norm=0.5, operands="bf16"):
+        # operands: the learner build whose weight images asvrl_adam_step_pack writes (bf16 / f32)
+        self.L = _abi.lib(operands)
         self.params = [p for p in params if p.requires_grad]
         dev = self.params[0].device
         n = sum(p.numel() for p in self.params)
@@ -103,11 +105,11 @@ class FusedAdam:
 
     def step(self):
         """Clip + Adam; returns the pre-clip global norm as a 0-d device tensor."""
-        rc = _abi.lib().asvrl_adam_clip(
+        rc = self.L.asvrl_adam_clip(
             _abi.ptr(self.flat), _abi.ptr(self.grads.flat), _abi.ptr(self.exp_avg), _abi.ptr(self.exp_avg_sq),
             self.n, _abi.ptr(self.step_t), self.lr, self.betas[0], self.betas[1], self.eps, self.max_norm,
             _abi.ptr(self.norm), _abi.ptr(self.work), _abi.stream_ptr(None))
-        _abi.check(rc, "asvrl_adam_clip")
+        _abi.check(rc, "asvrl_adam_clip", self.L)
         return self.norm[0]
 
     def pack_seg(self, w, image, K=0, chained=False, transposed=False, f32=False, row0=0, col0=0, nrep=1, rep_row=0,
@@ -131,18 +133,18 @@ class FusedAdam:
         if pack or counter is not None:
             pack = list(pack or [])
             arr = (_abi.AsvPackSeg * max(1, len(pack)))(*pack)
-            rc = _abi.lib().asvrl_adam_step_pack(
+            rc = self.L.asvrl_adam_step_pack(
                 _abi.ptr(self.flat), _abi.ptr(self.grads.flat), _abi.ptr(self.exp_avg), _abi.ptr(self.exp_avg_sq),
                 self.n, _abi.ptr(self.step_t), self.lr, self.betas[0], self.betas[1], self.eps, self.max_norm,
                 _abi.ptr(self.norm), _abi.ptr(norm_parts), int(nparts), arr, len(pack),
                 _abi.ptr(counter) if counter is not None else None, _abi.stream_ptr(None))
-            _abi.check(rc, "asvrl_adam_step_pack")
+            _abi.check(rc, "asvrl_adam_step_pack", self.L)
             return self.norm[0]
-        rc = _abi.lib().asvrl_adam_step(
+        rc = self.L.asvrl_adam_step(
             _abi.ptr(self.flat), _abi.ptr(self.grads.flat), _abi.ptr(self.exp_avg), _abi.ptr(self.exp_avg_sq),
             self.n, _abi.ptr(self.step_t), self.lr, self.betas[0], self.betas[1], self.eps, self.max_norm,
             _abi.ptr(self.norm), _abi.ptr(norm_parts), int(nparts), _abi.stream_ptr(None))
-        _abi.check(rc, "asvrl_adam_step")
+        _abi.check(rc, "asvrl_adam_step", self.L)
         return self.norm[0]
 
 

@@ -14,6 +14,10 @@
  *    stream-ordered; no entry point synchronises the device.
  *  - Return value: 0 on success, nonzero on a bad argument or launch failure, with a
  *    thread-local message from asvrl_last_error(). No C++ exception crosses the ABI.
+ *  - Two builds export this same header: libasvrl.so, whose learner kernels take bf16 MFMA
+ *    operands (weight images, saved activations) with f32 accumulation, and libasvrl_f32.so,
+ *    the same sources with every such operand f32 (the parity build). "bf16" in the comments
+ *    below means the operand element type: f32 in libasvrl_f32.so (asvrl_operand_bytes()).
  */
 #ifndef ASVRL_H
 #define ASVRL_H
@@ -723,6 +727,11 @@ int asvrl_small_wgrad_partial(const float* dz, int64_t ldz, const float* x, int6
 /* ---------------------------------------------------------------- misc */
 const char* asvrl_last_error(void);
 int asvrl_abi_version(void);
+/* Bytes per learner-kernel operand element: 2 in libasvrl.so (bf16 MFMA operands, weight images
+ * and saved activations, f32 accumulation), 4 in libasvrl_f32.so -- the same sources built with
+ * ASVRL_OPERAND_F32=1, every operand f32 (v_mfma_f32_32x32x2_f32), the parity build of the
+ * hand-written learner. Every other entry point is identical in both libraries. */
+int32_t asvrl_operand_bytes(void);
 /* sizeof(AsvParams, AsvEnvState, AsvStepCtl, AsvStepOut, AsvResetCfg) as compiled, for
  * binding checks (host pointer to 5 int64). */
 void asvrl_struct_sizes(int64_t* out5);

@@ -1,7 +1,9 @@
 """GPU parity of the drop-in Agent's distributional updates against the reference's own
 train_AC_IQN / train_IQN / train_Rainbow outputs (tests/golden/learn_*.npz): same seeded
 initial weights, the captured batch and tau draws injected, losses within 1e-5 relative
-(fp32, GPU GEMM order vs CPU), weights after 1 and 3 Adam steps within 1e-4."""
+(fp32, GPU GEMM order vs CPU), weights after 1 and 3 Adam steps within 1e-4. AC-IQN and IQN
+run both learners Agent.train can use: the hand-written kernels' f32 build (the default) and the
+torch-autograd restatement."""
 import numpy as np
 import pytest
 import torch
@@ -35,10 +37,12 @@ def test_agent_init_matches_reference():
         np.testing.assert_array_equal(v.cpu().numpy(), z["init/critic/" + k])
 
 
-def test_train_ac_iqn_matches_reference():
+@pytest.mark.parametrize("learner", ["fused-f32", "torch"])
+def test_train_ac_iqn_matches_reference(learner):
     from distributional_rl_decision_and_control_amd.agent import Agent
     z = np.load(eo.GOLDEN + "/learn_ac_iqn.npz")
     ag = Agent(seed=100, agent_type="AC-IQN")
+    ag.set_learner(learner)
     dev = ag.device
     for step in range(3):
         b = _batch(z, f"step{step}/", dev)
@@ -52,10 +56,12 @@ def test_train_ac_iqn_matches_reference():
             _cmp_sd(ag.policy_local.critic, z, f"after{step}/critic/")
 
 
-def test_train_ac_iqn_32_quantiles_matches_reference():
+@pytest.mark.parametrize("learner", ["fused-f32", "torch"])
+def test_train_ac_iqn_32_quantiles_matches_reference(learner):
     from distributional_rl_decision_and_control_amd.agent import Agent
     z = np.load(eo.GOLDEN + "/learn_ac_iqn.npz")
     ag = Agent(seed=100, agent_type="AC-IQN")
+    ag.set_learner(learner)
     ag.num_tau = 32
     b = _batch(z, "n32/", ag.device)
     ag.memory.sample = (lambda: b)
@@ -79,10 +85,12 @@ def test_actor_forward_without_objects():
     np.testing.assert_allclose(out, z["fwd/noobj_actions"], rtol=1e-5, atol=1e-6)
 
 
-def test_train_iqn_matches_reference():
+@pytest.mark.parametrize("learner", ["fused-f32", "torch"])
+def test_train_iqn_matches_reference(learner):
     from distributional_rl_decision_and_control_amd.agent import Agent
     z = np.load(eo.GOLDEN + "/learn_iqn.npz")
     ag = Agent(seed=100, agent_type="IQN")
+    ag.set_learner(learner)
     for step in range(3):
         b = _batch(z, f"step{step}/", ag.device, long_actions=True)
         ag.memory.sample = (lambda b=b: b)
