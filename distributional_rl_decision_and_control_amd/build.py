@@ -6,7 +6,7 @@ lib/libasvrl.so      the product: learner kernels with bf16 MFMA operands, f32 a
 lib/libasvrl_f32.so  the same sources with ASVRL_OPERAND_F32=1: every learner operand, weight image
                      and saved activation f32 (v_mfma_f32_32x32x2_f32), the parity build that pins
                      the hand-written learner to the reference's fp32 arithmetic
-Both are compiled concurrently.
+Sources compile to objects in parallel (lib/obj/), then each variant links once.
 """
 import os
 import subprocess
@@ -27,7 +27,7 @@ ARCH = os.environ.get("ASVRL_OFFLOAD_ARCH", "gfx950")
 
 # -ffp-contract=off: the env kernel reproduces the reference's f64 operation order; FMA
 # contraction would change rounding (the masks are compared bit-exactly).
-FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=off",
+FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-ffp-contract=off",
          "-munsafe-fp-atomics", "-I", os.path.join(ROOT, "include")]
 
 
@@ -38,20 +38,45 @@ def stale(out):
     return any(os.path.getmtime(f) > t for f in SOURCES + HEADERS)
 
 
-def build_lib(force=False, verbose=False):
-    """Build every stale variant (concurrently); returns the product library's path."""
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    procs = []
+def _obj(out, src):
+    return os.path.join(os.path.dirname(out), "obj", os.path.basename(out) + "." + os.path.basename(src) + ".o")
+
+
+def build_lib(force=False, verbose=False, jobs=None):
+    """Build every stale variant: each source compiled to an object in parallel (objects newer than
+    their source and the headers are kept), then one link per variant. Returns the product path."""
+    os.makedirs(os.path.join(os.path.dirname(OUT), "obj"), exist_ok=True)
+    jobs = jobs or max(1, min(16, os.cpu_count() or 1))
+    hdr_t = max(os.path.getmtime(h) for h in HEADERS)
+    todo, links = [], []
     for out, extra in VARIANTS.items():
         if not force and not stale(out):
             continue
-        cmd = [HIPCC] + FLAGS + extra + ["-o", out + ".tmp"] + SOURCES
+        objs = []
+        for src in SOURCES:
+            o = _obj(out, src)
+            objs.append(o)
+            if force or not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(src), hdr_t):
+                todo.append(([HIPCC] + FLAGS[:3] + ["-c"] + FLAGS[3:] + extra + ["-o", o + ".tmp", src], o))
+        links.append((out, objs))
+    running = []
+    while todo or running:
+        while todo and len(running) < jobs:
+            cmd, o = todo.pop(0)
+            if verbose:
+                print(" ".join(cmd))
+            running.append((subprocess.Popen(cmd), o))
+        p, o = running.pop(0)
+        if p.wait() != 0:
+            for q, _ in running:
+                q.wait()
+            raise subprocess.CalledProcessError(p.returncode, f"hipcc -> {o}")
+        os.replace(o + ".tmp", o)
+    for out, objs in links:
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"] + objs
         if verbose:
             print(" ".join(cmd))
-        procs.append((out, subprocess.Popen(cmd)))
-    for out, p in procs:
-        if p.wait() != 0:
-            raise subprocess.CalledProcessError(p.returncode, f"hipcc -> {out}")
+        subprocess.run(cmd, check=True)
         os.replace(out + ".tmp", out)
     return OUT
 

@@ -879,18 +879,22 @@ struct PairLaunch {
   int blk, epb;
   size_t smem;
 };
-PairLaunch pair_launch(int R, int O, int blk_req, int epb_req) {
+PairLaunch pair_launch(int R, int O, int n_envs, int blk_req, int epb_req) {
   const int np1 = R * (O + R);
   PairLaunch L;
   // the robots of the workgroup's envs fill its first wave (dynamics, merge, COLREGs run per robot:
   // every wave issues them whatever its active lanes, so robots are packed densely); the pairs then
   // spread over all four waves
-  L.blk = (blk_req == 64 || blk_req == 128 || blk_req == 256) ? blk_req : 256;
+  // Batch-size rule (tools/env_sweep.sh, profiles/r02_env_launch_sweep.txt): up to 8192 envs, about 40
+  // robots in a 256-lane workgroup (R = 5: 8 envs, 34 us at 4096 envs vs 44 us for 128 lanes x 12
+  // envs and 47 us for the per-robot sweep; R = 17: 3 envs, 133 us vs 241 us); from 16384 envs with
+  // R <= 8, 128-lane workgroups of about 60 robots (R = 5: 12 envs) -- more resident workgroups per
+  // CU: 319 M env-steps/s at 2^18 envs vs 154 M with the small-batch shape
+  const bool large = n_envs >= 16384 && R <= 8;
+  L.blk = (blk_req == 64 || blk_req == 128 || blk_req == 256) ? blk_req : (large ? 128 : 256);
   if (R > L.blk) L.blk = 256;
-  // about 40 robots per workgroup: measured best at 4096 envs (R = 5: 8 envs, 34 us vs 58 us for the
-  // per-robot sweep; R = 17: 3 envs, 133 us vs 203 us); more envs per group trade latency for
-  // throughput at very large batches (tools/env_ab3.sh)
   L.epb = R <= 64 ? ((40 + R - 1) / R < 64 / R ? (40 + R - 1) / R : 64 / R) : 1;
+  if (large) L.epb = 60 / R;
   if (epb_req > 0) L.epb = epb_req;
   if (L.epb * R > L.blk) L.epb = L.blk / R;
   const size_t np = static_cast<size_t>(L.epb) * np1;
@@ -924,7 +928,7 @@ extern "C" int asvrl_env_step_ex(const AsvParams* params, const AsvEnvState* sta
   ASVRL_REQUIRE(lc.block == 0 || lc.block == 64 || lc.block == 128 || lc.block == 256,
                 "asvrl_env_step: block must be 0, 64, 128 or 256");
   ASVRL_REQUIRE(lc.envs_per_block >= 0, "asvrl_env_step: negative envs_per_block");
-  const PairLaunch pl = pair_launch(state->max_robots, state->max_obs, lc.block, lc.envs_per_block);
+  const PairLaunch pl = pair_launch(state->max_robots, state->max_obs, state->n_envs, lc.block, lc.envs_per_block);
   ASVRL_REQUIRE(lc.layout != 1 || pl.smem <= 150 * 1024, "asvrl_env_step: the pair layout's LDS does not fit");
   if (lc.layout != 2 && pl.smem <= 150 * 1024) {
     const int grid = (state->n_envs + pl.epb - 1) / pl.epb;

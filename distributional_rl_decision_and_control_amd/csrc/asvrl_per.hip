@@ -228,7 +228,10 @@ __global__ __launch_bounds__(256) void per_sample_kernel(AsvPer per, int B, cons
   }
   const float p = prob / total;                                            // probs / p_total
   const int64_t cap = full ? C : index;
-  const float w = powf(static_cast<float>(cap) * p, -per.priority_weight);  // (capacity * probs) ** -beta
+  // (capacity * probs) ** -beta; a draw that never validated (64 rejected redraws, counted above) gets
+  // weight 0 -- it may sit on a zero-priority leaf, where the power is inf and w / w.max() would turn
+  // the whole batch NaN -- so it takes no part in the loss
+  const float w = ok ? powf(static_cast<float>(cap) * p, -per.priority_weight) : 0.f;
   o[2 * ASVRL_OBS_DIM / 4] = make_float4(r0[kMeta], 0.f, R, nonterm);
   o[2 * ASVRL_OBS_DIM / 4 + 1] = make_float4(w, p, static_cast<float>(di), 0.f);
 }

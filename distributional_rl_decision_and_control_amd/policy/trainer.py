@@ -5,6 +5,13 @@ Agent: same constructor, learn() cadence (learning_starts, UPDATE_EVERY, target 
 evaluation + checkpoint at learning_starts and every eval_freq), epsilon schedule, episode
 bookkeeping and printouts, evaluation metrics and the evaluations.npz / eval_configs.json
 artefacts. For throughput use vec_trainer.VecTrainer (the same loop batched over envs).
+
+Route from the unchanged reference CLI to the batched loop: the reference's run_trial passes
+params["training_schedule"] straight into MarineNavEnv3 (train_RL_agents.py:85), and the reference
+reads only its own keys from it (env.py:75-94). An optional "vectorized" dict in that schedule
+(ignored by the reference) makes learn() drive VecTrainer instead: {"n_envs": E, "batch_size": B,
+"num_tau": N, ...} are VecTrainer's keyword arguments. Evaluation, evaluations.npz and the model
+files keep the reference's cadence and format; the trained networks are copied into rl_agent first.
 """
 import json
 import os
@@ -103,6 +110,9 @@ class Trainer:
 
     # ------------------------------------------------------------------ training loop (trainer.py:85-255)
     def learn(self, total_timesteps, eval_freq, eval_log_path, verbose=True):
+        sched = getattr(self.train_env, "schedule", None)
+        if isinstance(sched, dict) and sched.get("vectorized") is not None:
+            return self.learn_vectorized(sched["vectorized"], total_timesteps, eval_freq, eval_log_path, verbose)
         agent = self.rl_agent
         env = self.train_env
         states, _, _ = env.reset()
@@ -129,6 +139,62 @@ class Trainer:
                 states = next_states
                 ep["length"] += 1
             self.current_timestep += 1
+
+    def learn_vectorized(self, vec, total_timesteps, eval_freq, eval_log_path, verbose=True):
+        """learn() on the batched GPU loop (vec_trainer.VecTrainer): one iteration advances every env of
+        the batch by one step (E env-steps) and runs one learn step of batch B. Evaluation and the
+        checkpoint happen at the first learning iteration and whenever the env-step count crosses a
+        multiple of eval_freq (trainer.py:200-206), with rl_agent holding the trained networks."""
+        import torch
+
+        from ..vec_trainer import VecTrainer
+        agent = self.rl_agent
+        if agent.agent_type not in ("AC-IQN", "IQN", "Rainbow"):
+            raise ValueError(f"vectorized training covers AC-IQN, IQN and Rainbow, not {agent.agent_type}")
+        sched = {k: v for k, v in self.train_env.schedule.items() if k != "vectorized"}
+        kw = dict(vec)
+        kw.setdefault("graphs", True)
+        for key, sk in (("num_robots", "num_robots"), ("num_obs", "num_obstacles"), ("num_cores", "num_cores")):
+            if sk in sched:
+                kw.setdefault(key, max(sched[sk]))
+        tr = VecTrainer(agent_type=agent.agent_type, seed=getattr(self.train_env, "seed", 0), device=agent.device,
+                        total_timesteps=total_timesteps, schedule=sched, gamma=agent.GAMMA, lr=agent.LR,
+                        exploration_fraction=self.exploration_fraction, initial_eps=self.initial_eps,
+                        final_eps=self.final_eps, **kw)
+        self.vec_trainer = tr
+        next_eval = None
+        while self.current_timestep < total_timesteps:   # iteration k covers env-steps [kE, (k + 1)E)
+            tr.env.apply_schedule(tr.env.total_timesteps)
+            learning = tr.replay_size_host() >= tr.learning_starts
+            tr.iteration()
+            self.current_timestep += tr.E
+            if learning and (next_eval is None or self.current_timestep >= next_eval):
+                next_eval = (self.current_timestep // eval_freq + 1) * eval_freq
+                self._sync_agent(tr)
+                self.evaluation()
+                self.save_evaluation(eval_log_path)
+                if agent.training:
+                    agent.save_latest_model(eval_log_path)
+                if verbose:
+                    st = tr.env.episode_stats()
+                    print(f"timesteps {self.current_timestep}/{total_timesteps}: {st}")
+        torch.cuda.synchronize(tr.device)
+        self._sync_agent(tr)
+        return tr
+
+    def _sync_agent(self, tr):
+        """rl_agent's local / target networks <- the batched trainer's (same architectures)."""
+        import torch
+        pairs = [(self.rl_agent.policy_local, tr.local), (self.rl_agent.policy_target, tr.target)]
+        with torch.no_grad():
+            for dst, src in pairs:
+                if hasattr(src, "actor"):   # AC_IQN_Policy holds two modules
+                    dst.actor.load_state_dict(src.actor.state_dict())
+                    dst.critic.load_state_dict(src.critic.state_dict())
+                else:
+                    dst.load_state_dict(src.state_dict())
+        if hasattr(self.rl_agent, "_fused"):
+            self.rl_agent._fused = None   # the drop-in learner re-packs its weight images on its next train()
 
     @staticmethod
     def _new_episode(n, num=0):

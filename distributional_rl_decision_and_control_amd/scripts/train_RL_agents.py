@@ -4,8 +4,11 @@ the GPU-backed env/agent/trainer.
     python -m distributional_rl_decision_and_control_amd.scripts.train_RL_agents -C config/ac_iqn.json [-P n] [-D dev]
 
 Same flags, the same config JSON schema (list-valued keys expand to a cartesian product of
-trials), the same per-trial directory layout and artefacts. Optional extra keys, ignored by
-the reference: "vectorized": {"n_envs": E, ...} runs the batched VecTrainer instead.
+trials), the same per-trial directory layout and artefacts, and run_trial is the reference's
+(train_RL_agents.py:74-109). The batched GPU loop is reached through an optional key the reference
+ignores: "training_schedule": {..., "vectorized": {"n_envs": E, "batch_size": B, ...}} -- the
+schedule goes into MarineNavEnv3 unchanged and the drop-in Trainer.learn drives VecTrainer when the
+key is present (policy/trainer.py). A top-level "vectorized" entry is moved into the schedule.
 Trials run in spawned worker processes (HIP-safe) and worker errors are re-raised.
 """
 import argparse
@@ -52,8 +55,6 @@ def run_trial(device, params):
     os.makedirs(exp_dir)
     with open(os.path.join(exp_dir, "trial_config.json"), "w+") as f:
         json.dump(params, f)
-    if "vectorized" in params:
-        return run_vectorized(device, params, exp_dir)
     train_env = MarineNavEnv3(seed=params["seed"], schedule=params["training_schedule"])
     eval_env = MarineNavEnv3(seed=253, is_eval_env=True)
     rl_agent = Agent(device=device, seed=params["seed"] + 100, agent_type=params["agent_type"])
@@ -65,22 +66,6 @@ def run_trial(device, params):
     trainer.learn(total_timesteps=params["total_timesteps"], eval_freq=params["eval_freq"], eval_log_path=exp_dir)
 
 
-def run_vectorized(device, params, exp_dir):
-    import torch
-    from distributional_rl_decision_and_control_amd.vec_trainer import VecTrainer
-    v = dict(params["vectorized"])
-    dev = torch.device("cuda") if device in (None, "cpu") else torch.device(device)
-    tr = VecTrainer(agent_type=params["agent_type"], seed=params["seed"], device=dev,
-                    total_timesteps=params["total_timesteps"], schedule=params.get("training_schedule"), **v)
-    iters = max(1, params["total_timesteps"] // tr.E)
-    for k in range(iters):
-        tr.env.apply_schedule(tr.env.total_timesteps)
-        tr.iteration()
-        if (k + 1) % max(1, iters // 10) == 0:
-            print(f"iteration {k + 1}/{iters}: {tr.env.episode_stats()}")
-    tr.local.save(exp_dir) if hasattr(tr.local, "save") else None
-
-
 def main(argv=None):
     args = parser.parse_args(argv)
     params = json.load(args.config_file)
@@ -88,14 +73,14 @@ def main(argv=None):
     training_schedule = params.pop("training_schedule")
     eval_schedule = params.pop("eval_schedule")
     vectorized = params.pop("vectorized", None)
+    if vectorized is not None:
+        training_schedule = dict(training_schedule, vectorized=vectorized)
     trials = trial_params(params)
     timestamp = datetime.now().strftime("%Y-%m-%d-%H-%M-%S")
     for p in trials:
         p["training_time"] = timestamp
         p["training_schedule"] = training_schedule
         p["eval_schedule"] = eval_schedule
-        if vectorized is not None:
-            p["vectorized"] = vectorized
     if args.num_procs == 1:
         for p in trials:
             run_trial(args.device, p)

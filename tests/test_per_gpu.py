@@ -236,3 +236,24 @@ def test_rainbow_update_rows_matches_train_rainbow():
     torch.testing.assert_close(outs[1][0], outs[0][0], rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(outs[1][1], outs[0][1], rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(outs[1][2], outs[0][2], rtol=1e-5, atol=1e-7)
+
+
+def test_per_unvalidated_draw_gets_zero_weight():
+    """A draw that never validates (here: the injected uniform of the last segment lands on a
+    transition whose n-step window reaches the write head, replay_memory_rainbow.py:163) is counted
+    as an anomaly and gets importance weight 0, so it cannot turn w / w.max() into NaN."""
+    from distributional_rl_decision_and_control_amd.learn_ops import DevicePER
+    rng = np.random.RandomState(5)
+    per = DevicePER(256, stride=1, device="cuda")
+    n = 100
+    obs = rng.randn(n, 40).astype(np.float32)
+    _push(per, obs, np.ones(n, bool), rng.randint(0, 25, n), rng.randn(n), np.zeros(n, np.uint8))
+    B = 32
+    u = np.full(B, 0.5)
+    u[B - 1] = 0.999
+    rows, idx = per.sample(B, uniforms=torch.from_numpy(u))
+    rows = rows.cpu().numpy()
+    torch.cuda.synchronize()
+    assert per.anomalies() == 1
+    w = rows[:, 84]
+    assert np.all(np.isfinite(w)) and w[B - 1] == 0.0 and np.all(w[:B - 1] > 0) and np.isclose(w.max(), 1.0)

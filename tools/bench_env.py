@@ -25,11 +25,14 @@ def main():
     ap.add_argument("--width", type=float, default=55.0, help="map width = height (config 5: 110)")
     ap.add_argument("--noise", default="f32,f64", help="Philox draw precision(s): f32 (noise_mode 2), f64 (1)")
     ap.add_argument("--obs-only", action="store_true", help="time the observation pass alone (do_dynamics=0)")
+    ap.add_argument("--launch", default="auto",
+                    help="';'-separated launch shapes layout,block,envs_per_block (asvrl_env_step_ex), or auto")
     a = ap.parse_args()
     from distributional_rl_decision_and_control_amd.device_env import DeviceEnvBatch, reset_cfg
     R, O = a.robots, a.obstacles
     bpe = R * 360 + 24 * O + 8
-    for E, mode in [(int(x), m) for x in a.envs.split(",") for m in a.noise.split(",")]:
+    shapes = [None if x == "auto" else tuple(int(v) for v in x.split(",")) for x in a.launch.split(";")]
+    for E, mode, ln in [(int(x), m, s) for x in a.envs.split(",") for m in a.noise.split(",") for s in shapes]:
         fast = mode == "f32"
         b = DeviceEnvBatch(E, R, O, 0)
         b.reset(reset_cfg(R, O, 0, 40.0, a.width, a.width), seed=1)
@@ -43,15 +46,15 @@ def main():
         e0.record()
         for t in range(a.iters):
             if a.obs_only:
-                b.step(None, do_dynamics=False, seed=1, counter=t + 10, fast_noise=fast)
+                b.step(None, do_dynamics=False, seed=1, counter=t + 10, fast_noise=fast, launch=ln)
             else:
-                b.step(acts[t % 4], seed=1, counter=t + 10, trainer_deactivate=False, fast_noise=fast)
+                b.step(acts[t % 4], seed=1, counter=t + 10, trainer_deactivate=False, fast_noise=fast, launch=ln)
         e1.record()
         torch.cuda.synchronize()
         us = 1e3 * e0.elapsed_time(e1) / a.iters
         gbs = bpe * E / (us * 1e-6) / 1e9
         print(json.dumps({"envs": E, "noise": mode, "obs_only": a.obs_only, "robots": R, "obstacles": O, "width": a.width,
-                          "pairs": os.environ.get("ASVRL_ENV_PAIRS", "1") != "0", "us_per_step": us, "env_steps_per_s": E / (us * 1e-6),
+                          "launch": list(ln) if ln else "auto", "us_per_step": us, "env_steps_per_s": E / (us * 1e-6),
                           "alg_bytes_per_env_step": bpe, "achieved_GBps": gbs, "hbm_frac": gbs / 8000.0}))
         del b
 
