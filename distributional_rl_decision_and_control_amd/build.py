@@ -14,7 +14,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SOURCES = [os.path.join(HERE, "csrc", f) for f in ("asvrl_env.hip", "asvrl_learn.hip", "asvrl_critic.hip",
+SOURCES = [os.path.join(HERE, "csrc", f) for f in ("asvrl_env.hip", "asvrl_learn.hip", "asvrl_critic.hip", "asvrl_critic_fused.hip",
                                                              "asvrl_optim.hip", "asvrl_wgrad.hip", "asvrl_mlp.hip",
                                                              "asvrl_per.hip", "asvrl_rainbow.hip")]
 HEADERS = [os.path.join(HERE, "csrc", "asvrl_common.h"), os.path.join(HERE, "csrc", "asvrl_mfma.h"),
@@ -22,6 +22,9 @@ HEADERS = [os.path.join(HERE, "csrc", "asvrl_common.h"), os.path.join(HERE, "csr
 OUT = os.path.join(HERE, "lib", "libasvrl.so")
 OUT_F32 = os.path.join(HERE, "lib", "libasvrl_f32.so")
 VARIANTS = {OUT: [], OUT_F32: ["-DASVRL_OPERAND_F32=1"]}
+# per-source flags: the fused critic keeps its persistent weight-gradient accumulators in AGPRs (inline
+# asm) and every other MFMA in the VGPR form
+SOURCE_FLAGS = {"asvrl_critic_fused.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("ASVRL_OFFLOAD_ARCH", "gfx950")
 
@@ -57,7 +60,8 @@ def build_lib(force=False, verbose=False, jobs=None):
             o = _obj(out, src)
             objs.append(o)
             if force or not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(src), hdr_t):
-                todo.append(([HIPCC] + FLAGS[:3] + ["-c"] + FLAGS[3:] + extra + ["-o", o + ".tmp", src], o))
+                todo.append(([HIPCC] + FLAGS[:3] + ["-c"] + FLAGS[3:] + extra +
+                             SOURCE_FLAGS.get(os.path.basename(src), []) + ["-o", o + ".tmp", src], o))
         links.append((out, objs))
     running = []
     while todo or running:

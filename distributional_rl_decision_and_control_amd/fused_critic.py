@@ -203,6 +203,40 @@ def critic_train(pack, F, G, taus, q_targets, bufs, kappa=1.0, stream=None, q_ne
     return bufs.row_loss.sum() / float(B * Np)
 
 
+def fused_groups(pack, B, N):
+    """Workgroups (= partial groups) of critic_train_fused; 0 when the shape is unsupported."""
+    return int(pack.L.asvrl_critic_fused_groups(B, N))
+
+
+def fused_train_supported(pack, B, N):
+    """asvrl_critic_train_fused's shape rule: N in (8, 16, 32), B*N a multiple of its round size."""
+    rows = 32 if pack.operands == "f32" else 64
+    return N in (8, 16, 32) and B > 0 and (B * N) % rows == 0
+
+
+def critic_train_fused(pack, critic, taus, N, q_next, rewards, dones, gamma, obs, act, arena, dzF=None, dzG=None,
+                       xb=None, tile_loss=None, kappa=1.0, q=None, row_loss=None, stream=None):
+    """asvrl_critic_train_fused: the critic step's forward, quantile-Huber loss against
+    r + gamma q_next (1 - d), backward AND the trunk's weight gradients in one launch. The per-workgroup
+    partials land in `arena` (PartialArena) as segments of critic's cos_embedding / hidden_layer /
+    hidden_layer_2 / output_layer .grad (reduced by the arena's next flush)."""
+    B = obs.shape[0]
+    groups = fused_groups(pack, B, N)
+    assert groups > 0 and fused_train_supported(pack, B, N), (B, N)
+    shapes = ((critic.cos_embedding, 256, 64), (critic.hidden_layer, 128, 256), (critic.hidden_layer_2, 128, 128),
+              (critic.output_layer, 1, 128))
+    regions = [arena._take(groups * (M * K + M)) for _, M, K in shapes]
+    parts = _abi.AsvCriticParts()
+    parts.cos_emb, parts.hidden, parts.hidden2, parts.out = (t.data_ptr() for t in regions)
+    io = _io(None, None, taus, N, obs=obs, act=act, xb=xb, Np=N, kappa=float(kappa), q_next=q_next,
+             rewards=rewards, dones=dones, ld_rd=rewards.stride(0), gamma=float(gamma), q=q, row_loss=row_loss,
+             dzF=dzF, dzG=dzG, tile_loss=tile_loss, loss_scale=1.0 / float(B * N))
+    _abi.check(pack.L.asvrl_critic_train_fused(C.byref(pack.struct), C.byref(io), C.byref(parts),
+                                               _abi.stream_ptr(stream)), "asvrl_critic_train_fused", pack.L)
+    for (layer, M, K), part in zip(shapes, regions):
+        arena.groups(part, groups, M, K, layer.weight.grad, layer.bias.grad)
+
+
 def critic_actor_grad(pack, F, G, taus, N, q, dG=None, stream=None, w_ae=None, dA=None, tile_loss=None, obs=None,
                       act=None):
     """ACTOR launch: dq = -1/(B*N) on every row; writes dG and/or dA (with w_ae); with
@@ -357,6 +391,12 @@ class PartialArena:
     def tiles(self, part, tiles, dw, db, accumulate=False):
         """dw (nw) (+)= sum over tiles of part[t][0:nw], db (+)= sum of part[t][nw]."""
         self._seg(part, dw, db, tiles, dw.numel(), 1, accumulate)
+
+    def groups(self, part, groups, M, K, dw, db, accumulate=False):
+        """dw (M x K) (+)= sum over groups of part[g][0:M*K], db (M) (+)= of part[g][M*K:]: per-workgroup
+        partials a kernel wrote in the [groups][M*K + M] layout (critic_train_fused)."""
+        assert dw.numel() == M * K and db.numel() == M
+        self._seg(part, dw, db, groups, M * K, M, accumulate, stride=M * K + M, boff=M * K)
 
     def scalar(self, partials, out, accumulate=False):
         """out (1 f32) (+)= sum(partials): a scalar segment (e.g. per-tile loss partials)."""

@@ -36,7 +36,7 @@ import torch
 
 from . import _abi
 from .fused_critic import (CriticPack, PartialArena, TrainBuffers, critic_actor_grad, critic_forward, critic_train,
-                           trunk_weight_grads_into, wout_groups)
+                           critic_train_fused, fused_train_supported, trunk_weight_grads_into, wout_groups)
 from .fused_mlp import ActorBuffers, MlpPack, actor_act, actor_backward, actor_forward, actor_train_forward
 from .learner import FusedAdam, clip_and_step
 
@@ -44,6 +44,10 @@ OBS = 40
 # the actor's training forward on a side stream beside the target chain (1) or on the caller's stream
 # (0, default): the fork + join cost more than the 13 us forward in a replayed graph (-1 % per step)
 ACTOR_FWD_SIDE = os.environ.get("ASVRL_ACTOR_FWD_SIDE", "0") == "1"
+# the critic step's forward / loss / backward and trunk weight gradients in ONE launch
+# (asvrl_critic_train_fused; 1, default) or the two TRAIN kernels + the batched weight-gradient launch
+# over saved activations (0; also the path for shapes the fused launch does not take)
+FUSED_TRAIN = os.environ.get("ASVRL_FUSED_TRAIN", "1") == "1"
 
 
 class SideStreams:
@@ -185,20 +189,28 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     if q_next is None:
         q_next = st.q_next
         target_q(st, rows, taus[0], q_next, st.na)
-    tiles = wout_groups(B, N)
-    wout_part = arena.take_tiles(tiles, 128)   # output_layer's gradient, reduced per workgroup in the kernel
-    critic_train(st.local_trunk, None, None, taus[1], None, bufs, q_next=q_next.view(B, N), rewards=r_col,
-                 dones=d_col, gamma=gamma, dzF=st.dzF, dzG=st.dzG, with_dFdG=False, tile_loss=st.tile_loss[0],
-                 obs=s_rows, act=a_rows, xb=st.xb, wout_part=wout_part)
     ae = critic.action_encoder[0]
-    arena.tiles(wout_part, tiles, critic.output_layer.weight.grad, critic.output_layer.bias.grad)
-    # the five weight-gradient reductions in ONE launch, then one partial-sum launch
-    with arena.batch():
-        arena.linear(bufs.dzc, bufs.cos, critic.cos_embedding.weight.grad, critic.cos_embedding.bias.grad)
-        arena.linear(bufs.dz1, bufs.h0, critic.hidden_layer.weight.grad, critic.hidden_layer.bias.grad)
-        arena.linear(bufs.dz2, bufs.h1g, critic.hidden_layer_2.weight.grad, critic.hidden_layer_2.bias.grad)
-        arena.fold(st.dzF, st.xb, critic)             # encoder image -> self/object encoder grads
-        arena.small(st.dzG, a_rows, ae.weight.grad, ae.bias.grad)
+    if FUSED_TRAIN and fused_train_supported(st.local_trunk, B, N):
+        # forward, loss, backward and the four trunk layers' weight-gradient partials in one launch
+        critic_train_fused(st.local_trunk, critic, taus[1], N, q_next.view(B, N), r_col, d_col, gamma, s_rows,
+                           a_rows, arena, dzF=st.dzF, dzG=st.dzG, xb=st.xb, tile_loss=st.tile_loss[0])
+        with arena.batch():   # the encoders' gradients from the per-sample dzF / dzG
+            arena.fold(st.dzF, st.xb, critic)
+            arena.small(st.dzG, a_rows, ae.weight.grad, ae.bias.grad)
+    else:
+        tiles = wout_groups(B, N)
+        wout_part = arena.take_tiles(tiles, 128)   # output_layer's gradient, reduced per workgroup in the kernel
+        critic_train(st.local_trunk, None, None, taus[1], None, bufs, q_next=q_next.view(B, N), rewards=r_col,
+                     dones=d_col, gamma=gamma, dzF=st.dzF, dzG=st.dzG, with_dFdG=False, tile_loss=st.tile_loss[0],
+                     obs=s_rows, act=a_rows, xb=st.xb, wout_part=wout_part)
+        arena.tiles(wout_part, tiles, critic.output_layer.weight.grad, critic.output_layer.bias.grad)
+        # the five weight-gradient reductions in ONE launch, then one partial-sum launch
+        with arena.batch():
+            arena.linear(bufs.dzc, bufs.cos, critic.cos_embedding.weight.grad, critic.cos_embedding.bias.grad)
+            arena.linear(bufs.dz1, bufs.h0, critic.hidden_layer.weight.grad, critic.hidden_layer.bias.grad)
+            arena.linear(bufs.dz2, bufs.h1g, critic.hidden_layer_2.weight.grad, critic.hidden_layer_2.bias.grad)
+            arena.fold(st.dzF, st.xb, critic)             # encoder image -> self/object encoder grads
+            arena.small(st.dzG, a_rows, ae.weight.grad, ae.bias.grad)
     arena.scalar(st.tile_loss[0], st.losses[0:1])   # the critic loss
     cgn = _reduce_and_step(arena, critic_opt, critic_grads, sync, max_norm, pack=st.local_trunk)
     if produce is not None:   # next batch + its target quantiles beside the actor step

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 11
+#define ASVRL_ABI_VERSION 12
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -305,6 +305,29 @@ int asvrl_critic_forward(const AsvCriticWeights* w, const AsvCriticIO* io, void*
  * gradients. */
 int asvrl_critic_train(const AsvCriticWeights* w, const AsvCriticIO* io, const AsvCriticActs* acts,
                        void* stream);
+
+/* Per-workgroup weight-gradient partials of asvrl_critic_train_fused, [groups][M*K + M] per layer
+ * (dW row-major in the layer's own feature order, then db); groups = asvrl_critic_fused_groups.
+ * Sum them over the groups with asvrl_partial_sums (nw = M*K, nb = M, stride = M*K + M). */
+typedef struct AsvCriticParts {
+  float* cos_emb;   /* cos_embedding   (256 x 64): [groups][16384 + 256] */
+  float* hidden;    /* hidden_layer    (128 x 256): [groups][32768 + 128] */
+  float* hidden2;   /* hidden_layer_2  (128 x 128): [groups][16384 + 128] */
+  float* out;       /* output_layer    (1 x 128):  [groups][128 + 1] */
+} AsvCriticParts;
+
+/* Workgroups (= partial groups) of asvrl_critic_train_fused for B samples x N quantiles: one per
+ * CU at most, each taking rounds of 64 rows (32 in the f32 build). */
+int32_t asvrl_critic_fused_groups(int32_t B, int32_t N);
+
+/* The critic update of train_AC_IQN (agent.py:395-414) WITH its trunk weight gradients, in one
+ * persistent launch: encoders from io->obs / io->act, forward, quantile-Huber loss against
+ * r + gamma q_next (1 - d) (io->q_next [B][N], rewards / dones at stride ld_rd), backward, and
+ * per-workgroup dW / db partials of the four trunk layers (parts); per-sample dzF / dzG and xb for
+ * the encoder gradients, per-tile loss partials (tile_loss) as asvrl_critic_train. N' must equal N;
+ * B*N a multiple of the round size. No activation goes to HBM. */
+int asvrl_critic_train_fused(const AsvCriticWeights* w, const AsvCriticIO* io, const AsvCriticParts* parts,
+                             void* stream);
 
 /* Actor update's critic pass (agent.py:419-425): forward, then the backward of
  * sum_rows dq * q to G (dG) and through the action encoder to the action (dA). */

@@ -15,6 +15,7 @@ run() {
     python3 "$ROOT/bench.py" $ARGS > "$OUT/$name.log" 2>&1
 }
 run sq SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAVES
+[ -n "$PMC_EXTRA" ] && run sq2 SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM
 run fetch FETCH_SIZE
 run write WRITE_SIZE
 echo "pmc passes done"
