@@ -23,8 +23,9 @@ OUT = os.path.join(HERE, "lib", "libasvrl.so")
 OUT_F32 = os.path.join(HERE, "lib", "libasvrl_f32.so")
 VARIANTS = {OUT: [], OUT_F32: ["-DASVRL_OPERAND_F32=1"]}
 # per-source flags: the fused critic keeps its persistent weight-gradient accumulators in AGPRs (inline
-# asm) and every other MFMA in the VGPR form
-SOURCE_FLAGS = {"asvrl_critic_fused.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+# asm) and every other MFMA in the VGPR form; no NaN operands on the path (ReLU as one v_max_f32, no
+# canonicalising max)
+SOURCE_FLAGS = {"asvrl_critic_fused.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-honor-nans"]}
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("ASVRL_OFFLOAD_ARCH", "gfx950")
 

@@ -95,6 +95,87 @@ __device__ __forceinline__ frag8 tr_frag(const elem_t* img, int r0, int c0, int 
 #endif
 }
 
+// Per-lane byte bases of the swizzled images, computed once per phase so that every access is one XOR
+// plus an immediate offset (the swizzle arithmetic per access was most of the kernel's VALU).
+// Row access (row 32 j + r, positions 16 ks + 8 h .. + 7): (chunk ^ x(row)) with chunk = 2 ks + h
+// equals 2 (ks ^ (x >> 1)) + (h ^ (x & 1)) below 16 chunks, and x(32 j + r) = x(r).
+template <int P>
+__device__ __forceinline__ int swz(int r) {
+  if constexpr (P == 64) return (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
+  else return ((r & 3) << 2) | ((r >> 2) & 3);
+}
+
+template <int P>
+struct RowA {
+  int base;
+  __device__ __forceinline__ RowA(int r, int h) {
+#if ASVRL_OPERAND_F32
+    base = (r * P + 8 * h) * 4;
+#else
+    const int x = swz<P>(r);
+    base = r * P * 2 + 32 * (x >> 1) + 16 * (h ^ (x & 1));
+#endif
+  }
+  __device__ __forceinline__ int at(int j, int ks) const {
+#if ASVRL_OPERAND_F32
+    return base + (j * 32 * P + 16 * ks) * 4;
+#else
+    return (base ^ (32 * (ks & 7))) + 256 * (ks >> 3) + j * 32 * P * 2;
+#endif
+  }
+};
+
+template <int P>
+__device__ __forceinline__ frag8 rowf(const elem_t* img, const RowA<P>& A, int j, int ks) {
+  return *reinterpret_cast<const frag8*>(reinterpret_cast<const char*>(img) + A.at(j, ks));
+}
+
+template <int P>
+__device__ __forceinline__ void rows(elem_t* img, const RowA<P>& A, int j, int ks, const frag8& v) {
+  *reinterpret_cast<frag8*>(reinterpret_cast<char*>(img) + A.at(j, ks)) = v;
+}
+
+// Transposed access (rows 16 kk .. + 15 x columns 32 n .. + 31, see tr_frag): the lane's two 4-row
+// reads start at rows ro and ro + 4 (ro = 8 (g >> 1) + q) and column chunk 4 n + cp; below 16 chunks
+// (4 n + cp) ^ x = 4 (n ^ (x >> 2)) + (cp ^ (x & 3)).
+template <int P>
+struct TrA {
+  int lo, hi;
+  __device__ __forceinline__ TrA(int lane) {
+#if ASVRL_OPERAND_F32
+    lo = (8 * (lane >> 5) * P + (lane & 31)) * 4;
+    hi = 0;
+#else
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int cp = 2 * (g & 1) + (p >> 1), ro = 8 * (g >> 1) + q;
+    const int x0 = swz<P>(ro), x1 = swz<P>(ro + 4);
+    lo = ro * P * 2 + 64 * (x0 >> 2) + 16 * (cp ^ (x0 & 3)) + 8 * (p & 1);
+    hi = (ro + 4) * P * 2 + 64 * (x1 >> 2) + 16 * (cp ^ (x1 & 3)) + 8 * (p & 1);
+#endif
+  }
+};
+
+template <int P>
+__device__ __forceinline__ frag8 trf(const elem_t* img, const TrA<P>& A, int kk, int n) {
+  const char* b = reinterpret_cast<const char*>(img);
+#if ASVRL_OPERAND_F32
+  b += A.lo + (16 * kk * P + 32 * n) * 4;
+  frag8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const float*>(b + j * P * 4);
+  return v;
+#else
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const int off = 256 * (n >> 2) + kk * 16 * P * 2;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + ((A.lo ^ (64 * (n & 3))) + off)));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + ((A.hi ^ (64 * (n & 3))) + off)));
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(frag8, v);
+#endif
+}
+
 // keep a fragment materialised in its packed operand form (4 VGPRs for bf16) while it lives across
 // phases, instead of the compiler's choice of carrying the f32 values and rounding at the use
 __device__ __forceinline__ void pin(frag8& v) {
@@ -105,14 +186,34 @@ __device__ __forceinline__ void pin(frag8& v) {
 }
 
 __device__ __forceinline__ float sum8(const frag8& v) {
+#if ASVRL_OPERAND_F32
   float s = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) s += static_cast<float>(v[j]);
   return s;
+#else
+  // four v_dot2_f32_bf16 against ones (exact products, f32 accumulation)
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  const bf16x2 one = {(__bf16)1.0f, (__bf16)1.0f};
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) s = __builtin_amdgcn_fdot2_f32_bf16(bf16x2{v[j], v[j + 1]}, one, s, false);
+  return s;
+#endif
 }
 
 // accumulator block initialised with a bias in position order: register 8s + i of lane half h is
 // position base + 16 s + 8 h + i
+// 8 consecutive f32 (positions p0 .. p0 + 7) from LDS as two 16-byte reads
+__device__ __forceinline__ void lds8(const float* src, float (&v)[8]) {
+  const f32x4 lo = *reinterpret_cast<const f32x4*>(src), hi = *reinterpret_cast<const f32x4*>(src + 4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[i] = lo[i];
+    v[4 + i] = hi[i];
+  }
+}
+
 __device__ __forceinline__ f32x16 bias_init(const float* bpos, int base, int h) {
   f32x16 acc;
 #pragma unroll
@@ -169,6 +270,23 @@ __device__ __forceinline__ f32x16 acc_init(const float* bpos, int base, int h) {
   return f32x16{};
 }
 
+// Phase timing (tools/fused_stamps.py; a variant build with -DASVRL_FUSED_STAMPS, never the shipped
+// library): lane 0 of every wave records s_memtime before and after each of the round's barriers.
+#ifdef ASVRL_FUSED_STAMPS
+constexpr int kStampRounds = 8, kStamps = 16;
+__device__ uint64_t g_stamps[1024 * kNW * kStampRounds * kStamps];
+#define ASVRL_STAMP(k)                                                                                   \
+  do {                                                                                                   \
+    if ((threadIdx.x & 63) == 0 && it_ < kStampRounds && blockIdx.x < 1024)                              \
+      g_stamps[((blockIdx.x * kNW + (threadIdx.x >> 6)) * kStampRounds + it_) * kStamps + (k)] =         \
+          __builtin_amdgcn_s_memtime();                                                                  \
+  } while (0)
+#else
+#define ASVRL_STAMP(k) \
+  do {                 \
+  } while (0)
+#endif
+
 struct FusedArgs {
   AsvCriticWeights w;
   const float* obs;
@@ -191,67 +309,125 @@ struct FusedArgs {
   AsvCriticParts parts;
 };
 
-template <int NB, int S>
+constexpr int kObsIn = 37;   // self 7 | objects 25 | mask 5 of the packed observation row
+constexpr int kEncFloats = 56 * 7 + 56 + 40 * 5 + 40 + 128 * 2 + 128;
+
+// One round's inputs in LDS (floats): obs rows [S][37] | actions [S][2] | taus [G] | q_next [S][NT] |
+// rewards [S] | dones [S]
+template <int NT, int S, int G>
+struct InLayout {
+  static constexpr int kObs = 0, kAct = S * kObsIn, kTau = kAct + 2 * S, kQn = kTau + G, kRew = kQn + S * NT,
+                       kDon = kRew + S, kSize = kDon + S;
+  static constexpr int kPer = (kSize + kNW * 64 - 1) / (kNW * 64);   // elements per thread
+};
+
+template <int NT, int NB, int S>
 struct FusedLds {
-  elem_t cos[32 * NB * kNcos];   // natural order (the cos layer is input-fed)
-  elem_t x[32 * NB * kC];        // F * c; after dW1: four waves' dzc images [G][64]
-  elem_t a[32 * NB * kH];        // h1g, then dz1
-  elem_t b[32 * NB * kH];        // dz2
-  elem_t F[S * kC];              // position order
-  float G[S * kH];               // position order
+  elem_t cos[32 * NB * kNcos];        // natural order (the cos layer is input-fed)
+  elem_t x[32 * NB * kC];             // F * c
+  elem_t a[32 * NB * kH];             // h1g
+  elem_t b[32 * NB * kH];             // h2, then dz2 in place
+  elem_t dz1[32 * NB * kH];
+  elem_t dzc[kNW][32 * NB * kNcos];   // each wave's own dzc image (the A operand of its dWc rows)
+  float F[S * kC];                    // position order; operand-rounded values held in f32
+  float G[S * kH];                    // position order
   float qpart[kNW][32 * NB];
   float dq[32 * NB];
-  float bias[kC + 3 * kH];       // bc | b1 | b2 | wo, position order
+  float bias[kC + 3 * kH + 4];        // bc | b1 | b2 | wo, position order | bo
+  float enc[kEncFloats];              // encoder parameters (stage_fg)
+  float in[2][InLayout<NT, S, 32 * NB>::kSize];   // the round's inputs, double-buffered (prefetched a round ahead)
   float red[kNW];
 };
 
 constexpr int kSelfF = 56, kSelfIn = 7, kObjF = 40, kObjIn = 5, kObsMask = 32;
 
+// element e of round t's input block (InLayout), read from the kernel's global inputs
+template <int NT, int S, int G>
+__device__ __forceinline__ float fetch_in(const FusedArgs& a, int t, int e) {
+  // one load from a selected address (a branch per source would serialise the loads)
+  using IL = InLayout<NT, S, G>;
+  const int64_t b0 = static_cast<int64_t>(t) * S;
+  const float* p;
+  if (e < IL::kAct) p = a.obs + (b0 + e / kObsIn) * a.ld_obs + e % kObsIn;
+  else if (e < IL::kTau) p = a.ain + (b0 + (e - IL::kAct) / 2) * a.ld_ain + (e - IL::kAct) % 2;
+  else if (e < IL::kQn) p = a.taus + static_cast<int64_t>(t) * G + (e - IL::kTau);
+  else if (e < IL::kRew) p = a.qn + b0 * NT + (e - IL::kQn);
+  else if (e < IL::kDon) p = a.rew + (b0 + e - IL::kRew) * a.ld_rd;
+  else p = a.don + (b0 + e - IL::kDon) * a.ld_rd;
+  return *p;
+}
+
 // F (observation_processor, AC_IQN_model.py:284-308) and G (relu(action_encoder(a)),
 // AC_IQN_model.py:468-470) of the round's S samples into LDS, position order; xb for the encoder
-// weight gradient. f32 dot products in the same order as asvrl_critic.hip's stage_features.
-template <int S>
-__device__ __forceinline__ void stage_fg(const FusedArgs& a, int b0, elem_t* Fs, float* Gs) {
-  for (int idx = threadIdx.x; idx < S * kC; idx += kNW * 64) {
-    const int k = idx / kC, m = idx % kC;
-    const float* x = a.obs + static_cast<int64_t>(b0 + k) * a.ld_obs;
-    float v;
+// weight gradient. f32 dot products in the same order as asvrl_critic.hip's stage_features, from the
+// round's staged inputs and the staged encoder parameters.
+template <int NT, int S, int G>
+__device__ __forceinline__ void stage_fg(const FusedArgs& a, int b0, int tid, const float* in, const float* enc,
+                                         float* Fs, float* Gs) {
+  using IL = InLayout<NT, S, G>;
+  constexpr int T = kNW * 64;
+  const float* self_w = enc;
+  const float* self_b = self_w + 56 * 7;
+  const float* obj_w = self_b + 56;
+  const float* obj_b = obj_w + 40 * 5;
+  const float* ae_w = obj_b + 40;
+  const float* ae_b = ae_w + 128 * 2;
+  // thread tid: feature m = tid (S * 256 / T samples each); compile-time trip counts, the feature's
+  // weights loaded once for all its samples
+  static_assert(kC == T, "one cos-layer feature per thread");
+  {
+    const int m = tid;
     if (m < kSelfF) {
-      const float* w = a.w.self_w + m * kSelfIn;
-      float d = 0.f;
+      float w[kSelfIn];
 #pragma unroll
-      for (int i = 0; i < kSelfIn; ++i) d += w[i] * x[i];
-      v = relu(d + a.w.self_b[m]);
+      for (int i = 0; i < kSelfIn; ++i) w[i] = self_w[m * kSelfIn + i];
+      const float bb = self_b[m];
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        const float* x = in + IL::kObs + k * kObsIn;
+        float d = 0.f;
+#pragma unroll
+        for (int i = 0; i < kSelfIn; ++i) d += w[i] * x[i];
+        Fs[k * kC + swap23(m)] = static_cast<float>((elem_t)relu(d + bb));
+      }
     } else {
       const int o = (m - kSelfF) / kObjF, j = (m - kSelfF) % kObjF;
-      const float* w = a.w.obj_w + j * kObjIn;
-      const float* xo = x + kSelfIn + kObjIn * o;
-      float d = 0.f;
+      float w[kObjIn];
 #pragma unroll
-      for (int i = 0; i < kObjIn; ++i) d += w[i] * xo[i];
-      v = x[kObsMask + o] < 0.5f ? 0.f : relu(d + a.w.obj_b[j]);   // masked_fill(mask < 0.5, 0)
+      for (int i = 0; i < kObjIn; ++i) w[i] = obj_w[j * kObjIn + i];
+      const float bb = obj_b[j];
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        const float* x = in + IL::kObs + k * kObsIn;
+        const float* xo = x + kSelfIn + kObjIn * o;
+        float d = 0.f;
+#pragma unroll
+        for (int i = 0; i < kObjIn; ++i) d += w[i] * xo[i];
+        const float v = x[kObsMask + o] < 0.5f ? 0.f : relu(d + bb);   // masked_fill(mask < 0.5, 0)
+        Fs[k * kC + swap23(m)] = static_cast<float>((elem_t)v);        // the operand type's F
+      }
     }
-    Fs[k * kC + swap23(m)] = (elem_t)v;
   }
-  for (int idx = threadIdx.x; idx < S * kH; idx += kNW * 64) {
-    const int k = idx / kH, m = idx % kH;
-    const float a0 = a.ain[static_cast<int64_t>(b0 + k) * a.ld_ain], a1 = a.ain[static_cast<int64_t>(b0 + k) * a.ld_ain + 1];
-    Gs[k * kH + swap23(m)] = relu((a.w.ae_w[2 * m] * a0 + a.w.ae_w[2 * m + 1] * a1) + a.w.ae_b[m]);
+  if (tid < kH) {
+    const int m = tid;
+    const float w0 = ae_w[2 * m], w1 = ae_w[2 * m + 1], bb = ae_b[m];
+#pragma unroll
+    for (int k = 0; k < S; ++k)
+      Gs[k * kH + swap23(m)] = relu((w0 * in[IL::kAct + 2 * k] + w1 * in[IL::kAct + 2 * k + 1]) + bb);
   }
-  if (a.xb != nullptr)
-    for (int idx = threadIdx.x; idx < S * 32; idx += kNW * 64) {
-      const int k = idx / 32, c = idx % 32;
-      bp(a.xb)[static_cast<int64_t>(b0 + k) * 32 + c] = (elem_t)a.obs[static_cast<int64_t>(b0 + k) * a.ld_obs + c];
-    }
+  if (a.xb != nullptr && tid < S * 32) {
+    const int k = tid / 32, c = tid % 32;
+    bp(a.xb)[static_cast<int64_t>(b0 + k) * 32 + c] = (elem_t)in[IL::kObs + k * kObsIn + c];
+  }
 }
 
 // quantile-Huber terms of one row against its sample's N' = NT targets r + gamma q_next (1 - d)
 // (agent.py:399-412); lane half h takes half of them. Returns dq; *wl = the row's loss sum.
 template <int NT>
-__device__ __forceinline__ float row_loss_dq(const FusedArgs& a, int b, float tau, float q, int lane, float* wl_out) {
+__device__ __forceinline__ float row_loss_dq(const FusedArgs& a, const float* qt, float rb, float done, float tau,
+                                             float q, int lane, float* wl_out) {
   const int r = lane & 31, h = lane >> 5;
-  const float* qt = a.qn + static_cast<size_t>(b) * NT;
-  const float rb = a.rew[b * a.ld_rd], nd = 1.0f - a.don[b * a.ld_rd];
+  const float nd = 1.0f - done;
   const float kap = a.kappa, hk = 0.5f * a.kappa, omt = 1.f - tau;
   float wl = 0.f, wg = 0.f;
   auto term = [&](float target) {
@@ -311,7 +487,7 @@ template <int NT>
 __global__ __launch_bounds__(kNW * 64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void critic_fused_kernel(FusedArgs a) {
   constexpr int NB = FusedNB<NT>::v, G = 32 * NB, S = G / NT;
-  __shared__ __attribute__((aligned(16))) FusedLds<NB, S> L;
+  __shared__ __attribute__((aligned(16))) FusedLds<NT, NB, S> L;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
   const frag8* WC = reinterpret_cast<const frag8*>(a.w.wc_frag);
   const frag8* W1 = reinterpret_cast<const frag8*>(a.w.w1_frag);
@@ -328,6 +504,26 @@ void critic_fused_kernel(FusedArgs a) {
     b2p[swap23(i)] = a.w.b2[i];
     wop[swap23(i)] = a.w.wo[i];
   }
+  if (threadIdx.x == 0) L.bias[kC + 3 * kH] = a.w.bo[0];
+
+  using IL = InLayout<NT, S, G>;
+  {
+    const float* srcs[6] = {a.w.self_w, a.w.self_b, a.w.obj_w, a.w.obj_b, a.w.ae_w, a.w.ae_b};
+    const int lens[6] = {56 * 7, 56, 40 * 5, 40, 128 * 2, 128};
+    int off = 0;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      for (int i = threadIdx.x; i < lens[q]; i += kNW * 64) L.enc[off + i] = srcs[q][i];
+      off += lens[q];
+    }
+    if (blockIdx.x < a.rounds)
+#pragma unroll
+      for (int u = 0; u < IL::kPer; ++u) {
+        const int e = threadIdx.x + u * kNW * 64;
+        if (e < IL::kSize) L.in[0][e] = fetch_in<NT, S, G>(a, blockIdx.x, e);
+      }
+  }
+  __syncthreads();
 
   // persistent per-wave weight-gradient accumulators (rows = this wave's features, positions)
   f32x16 dW2[4], dW1[8], dWc[4];
@@ -339,201 +535,274 @@ void critic_fused_kernel(FusedArgs a) {
   float dwo[16];
 #pragma unroll
   for (int g = 0; g < 16; ++g) dwo[g] = 0.f;
-  for (int t = blockIdx.x; t < a.rounds; t += gridDim.x) {
+  int buf = 0, it_ = 0;
+  (void)it_;
+  for (int t = blockIdx.x; t < a.rounds; t += gridDim.x, buf ^= 1, ++it_) {
+    // the next round's inputs, into registers now and into LDS at the end of this round
+    float pre[IL::kPer];
+    int tid_p = threadIdx.x;
+    asm volatile("" : "+v"(tid_p));
+#pragma unroll
+    for (int u = 0; u < IL::kPer; ++u) {
+      const int e = tid_p + u * kNW * 64;
+      pre[u] = (t + static_cast<int>(gridDim.x) < a.rounds && e < IL::kSize)
+                   ? fetch_in<NT, S, G>(a, t + gridDim.x, e) : 0.f;
+    }
+    const float* in = L.in[buf];
     // the lane indices re-derived through an opaque copy every round: otherwise every LDS / weight
     // address of the round body is loop-invariant, gets hoisted out of the loop and spills
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
-    const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5, r = lane & 31;
-    elem_t* const dzc_w = L.x + w * G * kNcos;   // this wave's dzc image [G][64] (after dW1)
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int row0 = t * G, b0 = row0 / NT;
-    // ---------------- stage: F, G, xb; cos(tau pi k) for the round's rows (natural order)
-    stage_fg<S>(a, b0, L.F, L.G);
-    for (int c = threadIdx.x; c < G * (kNcos / 8); c += kNW * 64) {
-      const int row = c / (kNcos / 8), ch = c % (kNcos / 8);
-      const float tau = a.taus[row0 + row];
-      frag8 v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (elem_t)cos_pi_k_tau(tau, 8 * ch + j);
-      row_store<kNcos>(L.cos, row, 8 * ch, v);
-    }
-    __syncthreads();
-
-    // ---------------- L0: c = relu(Wc cos + bc), x = F * c      (this wave: blocks 2w, 2w+1)
-    {
-    ASVRL_FRESH_LANE();
-#pragma unroll
-    for (int mq = 0; mq < 2; ++mq) {
-      const int mb = 2 * w + mq;
-      frag8 wa[4];
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) wa[ks] = WC[(mb * 4 + ks) * 64 + lane];
-#pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        f32x16 acc = acc_init(bcp, mb * 32, h);
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) acc = mfma(wa[ks], row_frag<kNcos>(L.cos, 32 * j + r, 16 * ks + 8 * h), acc);
-        if constexpr (!kBiasFirst) acc += bias_init(bcp, mb * 32, h);
-        const int bl = (32 * j + r) / NT;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const int p0 = mb * 32 + 16 * s + 8 * h;
-          const frag8 fv = *reinterpret_cast<const frag8*>(L.F + bl * kC + p0);
-          frag8 xo;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) xo[i] = (elem_t)(static_cast<float>(fv[i]) * relu(acc[8 * s + i]));
-          row_store<kC>(L.x, 32 * j + r, p0, xo);
-        }
-      }
-    }
-    }
-    __syncthreads();
-
-    // ---------------- L1: h1 = relu(W1 x + b1) (own block w), h1g = h1 * G
-    frag8 h1k[NB][2];
+    elem_t* const dzc_w = L.dzc[w];
+    // ---------------- stage: F, G, xb; cos(tau pi k) for the round's rows (natural order); the
+    // cos layer's weight fragments are fetched meanwhile
+    frag8 wc0[4], wc1[4];
     {
       ASVRL_FRESH_LANE();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        wc0[ks] = WC[((2 * w) * 4 + ks) * 64 + lane];
+        wc1[ks] = WC[((2 * w + 1) * 4 + ks) * 64 + lane];
+      }
+    }
+    {
+      int tid_s = threadIdx.x;
+      asm volatile("" : "+v"(tid_s));
+      stage_fg<NT, S, G>(a, b0, tid_s, in, L.enc, L.F, L.G);
+      static_assert((G * (kNcos / 8)) % (kNW * 64) == 0, "whole cos chunks per thread");
+#pragma unroll
+      for (int u = 0; u < G * (kNcos / 8) / (kNW * 64); ++u) {
+        const int c = tid_s + u * kNW * 64;
+        const int row = c / (kNcos / 8), ch = c % (kNcos / 8);
+        const float tau = in[IL::kTau + row];
+        frag8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (elem_t)cos_pi_k_tau(tau, 8 * ch + j);
+        row_store<kNcos>(L.cos, row, 8 * ch, v);
+      }
+    }
+    ASVRL_STAMP(0);
+    __syncthreads();
+    ASVRL_STAMP(1);
+
+    // ---------------- L0: c = relu(Wc cos + bc), x = F * c      (this wave: blocks 2w, 2w+1); W1 fetched
+    frag8 w1f[16];
+    {
+      ASVRL_FRESH_LANE();
+      const RowA<kNcos> RA_cos(r, h);
+      const RowA<kC> RA_x(r, h);
+#pragma unroll
+      for (int mq = 0; mq < 2; ++mq) {
+        const int mb = 2 * w + mq;
+        float fv[NB][2][8];
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+#pragma unroll
+          for (int s = 0; s < 2; ++s) lds8(L.F + ((32 * j + r) / NT) * kC + mb * 32 + 16 * s + 8 * h, fv[j][s]);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          f32x16 acc = acc_init(bcp, mb * 32, h);
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) acc = mfma(mq ? wc1[ks] : wc0[ks], rowf(L.cos, RA_cos, j, ks), acc);
+          if constexpr (!kBiasFirst) acc += bias_init(bcp, mb * 32, h);
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            frag8 xo;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) xo[i] = (elem_t)(fv[j][s][i] * relu(acc[8 * s + i]));
+            rows(L.x, RA_x, j, 2 * mb + s, xo);
+          }
+        }
+      }
+#pragma unroll
+      for (int ks = 0; ks < kC / 16; ++ks) w1f[ks] = W1[(w * 16 + ks) * 64 + lane];
+    }
+    ASVRL_STAMP(2);
+    __syncthreads();
+    ASVRL_STAMP(3);
+
+    // ---------------- L1: h1 = relu(W1 x + b1) (own block w), h1g = h1 * G; W2 fetched
+    frag8 h1k[NB][2];
+    frag8 w2f[8];
+    {
+      ASVRL_FRESH_LANE();
+      const RowA<kC> RA_x(r, h);
+      const RowA<kH> RA_a(r, h);
+      float gv[NB][2][8];
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) lds8(L.G + ((32 * j + r) / NT) * kH + w * 32 + 16 * s + 8 * h, gv[j][s]);
       f32x16 acc[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[j] = acc_init(b1p, w * 32, h);
 #pragma unroll
-      for (int ks = 0; ks < kC / 16; ++ks) {
-        const frag8 wa = W1[(w * 16 + ks) * 64 + lane];
+      for (int ks = 0; ks < kC / 16; ++ks)
 #pragma unroll
-        for (int j = 0; j < NB; ++j) acc[j] = mfma(wa, row_frag<kC>(L.x, 32 * j + r, 16 * ks + 8 * h), acc[j]);
-      }
+        for (int j = 0; j < NB; ++j) acc[j] = mfma(w1f[ks], rowf(L.x, RA_x, j, ks), acc[j]);
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) w2f[ks] = W2[(w * 8 + ks) * 64 + lane];
       if constexpr (!kBiasFirst)
 #pragma unroll
         for (int j = 0; j < NB; ++j) acc[j] += bias_init(b1p, w * 32, h);
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
-        const int bl = (32 * j + r) / NT;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          const int p0 = w * 32 + 16 * s + 8 * h;
-          const f32x4 g0 = *reinterpret_cast<const f32x4*>(L.G + bl * kH + p0);
-          const f32x4 g1 = *reinterpret_cast<const f32x4*>(L.G + bl * kH + p0 + 4);
           frag8 go;
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             const float hv = relu(acc[j][8 * s + i]);
             h1k[j][s][i] = (elem_t)hv;
-            go[i] = (elem_t)(hv * (i < 4 ? g0[i] : g1[i - 4]));
+            go[i] = (elem_t)(hv * gv[j][s][i]);
           }
-          row_store<kH>(L.a, 32 * j + r, p0, go);
+          rows(L.a, RA_a, j, 2 * w + s, go);
           pin(h1k[j][s]);
         }
       }
     }
+    ASVRL_STAMP(4);
     __syncthreads();
+    ASVRL_STAMP(5);
 
     // ---------------- L2: z2 = W2 h1g + b2 (own block w); partial q over its 32 features; h2 = relu(z2)
-    // parked in the dz2 image (operand type) until dq is known
+    // parked in the dz2 image (operand type) until dq is known; W2^T fetched
+    frag8 w2tf[8];
     {
       ASVRL_FRESH_LANE();
+      const RowA<kH> RA_a(r, h);
+      const RowA<kH> RA_b(r, h);
       f32x16 z2[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) z2[j] = acc_init(b2p, w * 32, h);
 #pragma unroll
-      for (int ks = 0; ks < kH / 16; ++ks) {
-        const frag8 wa = W2[(w * 8 + ks) * 64 + lane];
+      for (int ks = 0; ks < kH / 16; ++ks)
 #pragma unroll
-        for (int j = 0; j < NB; ++j) z2[j] = mfma(wa, row_frag<kH>(L.a, 32 * j + r, 16 * ks + 8 * h), z2[j]);
-      }
+        for (int j = 0; j < NB; ++j) z2[j] = mfma(w2f[ks], rowf(L.a, RA_a, j, ks), z2[j]);
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) w2tf[ks] = W2T[(w * 8 + ks) * 64 + lane];
       if constexpr (!kBiasFirst)
 #pragma unroll
         for (int j = 0; j < NB; ++j) z2[j] += bias_init(b2p, w * 32, h);
+      float wov[2][8];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) lds8(wop + w * 32 + 16 * s + 8 * h, wov[s]);
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         float part = 0.f;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          const int p0 = w * 32 + 16 * s + 8 * h;
           frag8 hv;
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             const float h2 = relu(z2[j][8 * s + i]);
-            part += wop[p0 + i] * h2;
+            part += wov[s][i] * h2;
             hv[i] = (elem_t)h2;
           }
-          row_store<kH>(L.b, 32 * j + r, p0, hv);
+          rows(L.b, RA_b, j, 2 * w + s, hv);
         }
         part = half_sum(part);
         if (h == 0) L.qpart[w][32 * j + r] = part;
       }
     }
+    ASVRL_STAMP(6);
     __syncthreads();
+    ASVRL_STAMP(7);
 
     // ---------------- loss: q = sum of the four partials + bo; quantile-Huber -> dq (row block j = w)
     {
-    ASVRL_FRESH_LANE();
-    for (int j = w; j < NB; j += kNW) {
-      const int lr = 32 * j + r, grow = row0 + lr, b = grow / NT;
-      const float q = (((L.qpart[0][lr] + L.qpart[1][lr]) + L.qpart[2][lr]) + L.qpart[3][lr]) + a.w.bo[0];
-      float wl;
-      const float dq = row_loss_dq<NT>(a, b, a.taus[grow], q, lane, &wl);
-      if (a.tile_loss != nullptr) {
-        float v = h == 0 ? wl : 0.f;
-        v = seg_sum<32>(v);
-        if (lane == 31) a.tile_loss[grow / 32] = v * a.loss_scale;
-      }
-      if (h == 0) {
-        L.dq[lr] = dq;
-        if (a.row_loss != nullptr) a.row_loss[grow] = wl;
-        if (a.q != nullptr) a.q[grow] = q;
-        dbo += dq;
+      ASVRL_FRESH_LANE();
+      for (int j = w; j < NB; j += kNW) {
+        const int lr = 32 * j + r, grow = row0 + lr, b = grow / NT;
+        const float q = (((L.qpart[0][lr] + L.qpart[1][lr]) + L.qpart[2][lr]) + L.qpart[3][lr]) + L.bias[kC + 3 * kH];
+        float wl;
+        const int bl = b - b0;
+        const float dq = row_loss_dq<NT>(a, in + IL::kQn + bl * NT, in[IL::kRew + bl], in[IL::kDon + bl],
+                                         in[IL::kTau + lr], q, lane, &wl);
+        if (a.tile_loss != nullptr) {
+          float v = h == 0 ? wl : 0.f;
+          v = seg_sum<32>(v);
+          if (lane == 31) a.tile_loss[grow / 32] = v * a.loss_scale;
+        }
+        if (h == 0) {
+          L.dq[lr] = dq;
+          if (a.row_loss != nullptr) a.row_loss[grow] = wl;
+          if (a.q != nullptr) a.q[grow] = q;
+          dbo += dq;
+        }
       }
     }
-    }
+    ASVRL_STAMP(8);
     __syncthreads();
+    ASVRL_STAMP(9);
 
     // ---------------- dz2 = dq wo 1[h2 > 0] (own block, in place over h2), output layer's gradient
     // sum of dq h2
     {
-    ASVRL_FRESH_LANE();
+      ASVRL_FRESH_LANE();
+      const RowA<kH> RA_b(r, h);
+      // every LDS operand first (one wait), then the arithmetic and the in-place stores
+      float wov[2][8], dqv[NB];
+      frag8 hv[NB][2];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      const float dqv = L.dq[32 * j + r];
+      for (int s = 0; s < 2; ++s) lds8(wop + w * 32 + 16 * s + 8 * h, wov[s]);
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int p0 = w * 32 + 16 * s + 8 * h;
-        const frag8 hv = row_frag<kH>(L.b, 32 * j + r, p0);
-        frag8 dz;
+      for (int j = 0; j < NB; ++j) {
+        dqv[j] = L.dq[32 * j + r];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float h2 = static_cast<float>(hv[i]);
-          dz[i] = (elem_t)(h2 > 0.f ? dqv * wop[p0 + i] : 0.f);
-          dwo[8 * s + i] += dqv * h2;
+        for (int s = 0; s < 2; ++s) hv[j][s] = rowf(L.b, RA_b, j, 2 * w + s);
+      }
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          frag8 dz;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float h2 = static_cast<float>(hv[j][s][i]);
+            dz[i] = (elem_t)(h2 > 0.f ? dqv[j] * wov[s][i] : 0.f);
+            dwo[8 * s + i] += dqv[j] * h2;
+          }
+          rows(L.b, RA_b, j, 2 * w + s, dz);
         }
-        row_store<kH>(L.b, 32 * j + r, p0, dz);
       }
     }
-    }
+    ASVRL_STAMP(10);
     __syncthreads();
+    ASVRL_STAMP(11);
 
-    // ---------------- dW2[own][:] += dz2^T h1g;  L3: dh1g = W2^T dz2 (own block)
-    {
-    ASVRL_FRESH_LANE();
-#pragma unroll
-    for (int kk = 0; kk < G / 16; ++kk) {
-      const frag8 A = tr_frag<kH>(L.b, 16 * kk, 32 * w, lane);
-      db2 += sum8(A);
-#pragma unroll
-      for (int n = 0; n < 4; ++n) mfma_acc(dW2[n], A, tr_frag<kH>(L.a, 16 * kk, 32 * n, lane));
-    }
-    }
-    frag8 dz1k[NB][2];
+    // ---------------- dW2[own][:] += dz2^T h1g;  L3: dh1g = W2^T dz2 (own block) -> dG, dz1 (own
+    // slice into the dz1 image, which nobody reads before the next barrier)
     {
       ASVRL_FRESH_LANE();
+      const TrA<kH> TA_a(lane);
+      const TrA<kH> TA_b(lane);
+#pragma unroll
+      for (int kk = 0; kk < G / 16; ++kk) {
+        const frag8 A = trf(L.b, TA_b, kk, w);
+        db2 += sum8(A);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) mfma_acc(dW2[n], A, trf(L.a, TA_a, kk, n));
+      }
+    }
+    {
+      ASVRL_FRESH_LANE();
+      const RowA<kH> RA_b(r, h);
+      const RowA<kH> RA_d(r, h);
+      float gv[NB][2][8];
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) lds8(L.G + ((32 * j + r) / NT) * kH + w * 32 + 16 * s + 8 * h, gv[j][s]);
       f32x16 acc[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[j] = f32x16{};
 #pragma unroll
-      for (int ks = 0; ks < kH / 16; ++ks) {
-        const frag8 wa = W2T[(w * 8 + ks) * 64 + lane];
+      for (int ks = 0; ks < kH / 16; ++ks)
 #pragma unroll
-        for (int j = 0; j < NB; ++j) acc[j] = mfma(wa, row_frag<kH>(L.b, 32 * j + r, 16 * ks + 8 * h), acc[j]);
-      }
+        for (int j = 0; j < NB; ++j) acc[j] = mfma(w2tf[ks], rowf(L.b, RA_b, j, ks), acc[j]);
       // dz1 = dh1g G 1[h1 > 0]; dG = sum over the sample's taus of dh1g h1 (-> dzG = dG 1[G > 0])
 #pragma unroll
       for (int j = 0; j < NB; ++j) {   // h1 unpacked here, not earlier
@@ -543,19 +812,17 @@ void critic_fused_kernel(FusedArgs a) {
       float gsa[NB][16];
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
-        const int bl = (32 * j + r) / NT;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          const int p0 = w * 32 + 16 * s + 8 * h;
-          const f32x4 g0 = *reinterpret_cast<const f32x4*>(L.G + bl * kH + p0);
-          const f32x4 g1 = *reinterpret_cast<const f32x4*>(L.G + bl * kH + p0 + 4);
+          frag8 dz1;
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             const float h1 = static_cast<float>(h1k[j][s][i]);
             const float d = acc[j][8 * s + i];
-            dz1k[j][s][i] = (elem_t)(h1 > 0.f ? d * (i < 4 ? g0[i] : g1[i - 4]) : 0.f);
+            dz1[i] = (elem_t)(h1 > 0.f ? d * gv[j][s][i] : 0.f);
             gsa[j][8 * s + i] = d * h1;
           }
+          rows(L.dz1, RA_d, j, 2 * w + s, dz1);
         }
       }
       sample_sums<NT, NB>(gsa, w * 32, lane, [&](int bl, int p, float v) {
@@ -563,92 +830,106 @@ void critic_fused_kernel(FusedArgs a) {
         if (a.dzG != nullptr) a.dzG[static_cast<size_t>(b0 + bl) * kH + swap23(p)] = gm > 0.f ? v : 0.f;
       });
     }
-    __syncthreads();   // every wave is past dW2 (h1g dead) and L3 (dz2 dead)
+    ASVRL_STAMP(12);
+    __syncthreads();
+    ASVRL_STAMP(13);
+
+    // ---------------- dW1[own][:] += dz1^T x; L4's first weight fragments fetched meanwhile
+    frag8 wt[8], wcc[4];
     {
       ASVRL_FRESH_LANE();
+      const TrA<kH> TA_d(lane);
+      const TrA<kC> TA_x(lane);
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) wt[ks] = W1T[((2 * w) * 8 + ks) * 64 + lane];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) wcc[ks] = WC[((2 * w) * 4 + ks) * 64 + lane];
+#pragma unroll
+      for (int kk = 0; kk < G / 16; ++kk) {
+        const frag8 A = trf(L.dz1, TA_d, kk, w);
+        db1 += sum8(A);
+#pragma unroll
+        for (int n = 0; n < 8; ++n) mfma_acc(dW1[n], A, trf(L.x, TA_x, kk, n));
+      }
+    }
+
+    // ---------------- L4: dx = W1^T dz1 (own blocks 2w, 2w+1) with c = relu(Wc cos + bc) recomputed
+    // (bit-identical to L0's); dF = sum over taus of dx c (-> dzF), dzc = dx F 1[c > 0] into the
+    // wave's own dzc image. No barrier: L4 reads dz1 and cos, which nothing writes this round any more.
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq) {
+      ASVRL_FRESH_LANE();
+      const RowA<kNcos> RA_cos(r, h);
+      const RowA<kH> RA_d(r, h);
+      const RowA<kNcos> RA_dzc(r, h);
+      const int mb = 2 * w + mq;
+      float fv[NB][2][8];
 #pragma unroll
       for (int j = 0; j < NB; ++j)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) row_store<kH>(L.a, 32 * j + r, w * 32 + 16 * s + 8 * h, dz1k[j][s]);
-    }
-    __syncthreads();
-
-    // ---------------- dW1[own][:] += dz1^T x
-    {
-    ASVRL_FRESH_LANE();
-#pragma unroll
-    for (int kk = 0; kk < G / 16; ++kk) {
-      const frag8 A = tr_frag<kH>(L.a, 16 * kk, 32 * w, lane);
-      db1 += sum8(A);
-#pragma unroll
-      for (int n = 0; n < 8; ++n) mfma_acc(dW1[n], A, tr_frag<kC>(L.x, 16 * kk, 32 * n, lane));
-    }
-    }
-    __syncthreads();   // x dead: the waves' dzc images take its place
-
-    // ---------------- L4: dx = W1^T dz1 (own blocks 2w, 2w+1) with c = relu(Wc cos + bc) recomputed
-    // (bit-identical to L0's); dF = sum over taus of dx c (-> dzF), dzc = dx F 1[c > 0]
-    {
-    ASVRL_FRESH_LANE();
-#pragma unroll
-    for (int mq = 0; mq < 2; ++mq) {
-      const int mb = 2 * w + mq;
-      frag8 wt[8], wc[4];
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks) wt[ks] = W1T[(mb * 8 + ks) * 64 + lane];
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) wc[ks] = WC[(mb * 4 + ks) * 64 + lane];
+        for (int s = 0; s < 2; ++s) lds8(L.F + ((32 * j + r) / NT) * kC + mb * 32 + 16 * s + 8 * h, fv[j][s]);
       float fsa[NB][16];
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         f32x16 dx = f32x16{};
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks) dx = mfma(wt[ks], row_frag<kH>(L.a, 32 * j + r, 16 * ks + 8 * h), dx);
+        for (int ks = 0; ks < 8; ++ks) dx = mfma(wt[ks], rowf(L.dz1, RA_d, j, ks), dx);
         f32x16 cc = acc_init(bcp, mb * 32, h);
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) cc = mfma(wc[ks], row_frag<kNcos>(L.cos, 32 * j + r, 16 * ks + 8 * h), cc);
+        for (int ks = 0; ks < 4; ++ks) cc = mfma(wcc[ks], rowf(L.cos, RA_cos, j, ks), cc);
         if constexpr (!kBiasFirst) cc += bias_init(bcp, mb * 32, h);
-        const int bl = (32 * j + r) / NT;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          const int p0 = mb * 32 + 16 * s + 8 * h;
-          const frag8 fv = *reinterpret_cast<const frag8*>(L.F + bl * kC + p0);
           frag8 dz;
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
-            const float cv = static_cast<float>((elem_t)relu(cc[8 * s + i]));   // L0's bf16 c
+            const float cv = relu(cc[8 * s + i]);
             fsa[j][8 * s + i] = dx[8 * s + i] * cv;
-            dz[i] = (elem_t)(cv > 0.f ? dx[8 * s + i] * static_cast<float>(fv[i]) : 0.f);
+            dz[i] = (elem_t)(cv > 0.f ? dx[8 * s + i] * fv[j][s][i] : 0.f);
           }
-          row_store<kNcos>(dzc_w, 32 * j + r, mq * 32 + 16 * s + 8 * h, dz);
+          rows(dzc_w, RA_dzc, j, 2 * mq + s, dz);
         }
       }
+      if (mq == 0) {   // the second block's fragments
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) wt[ks] = W1T[((2 * w + 1) * 8 + ks) * 64 + lane];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) wcc[ks] = WC[((2 * w + 1) * 4 + ks) * 64 + lane];
+      }
       sample_sums<NT, NB>(fsa, mb * 32, lane, [&](int bl, int p, float v) {
-        const float fm = static_cast<float>(L.F[bl * kC + p]);
+        const float fm = L.F[bl * kC + p];
         if (a.dzF != nullptr)
           bp(a.dzF)[static_cast<size_t>(b0 + bl) * kC + swap23(p)] = (elem_t)(fm > 0.f ? v : 0.f);
       });
     }
 
-    }
     // ---------------- dWc[own 64][:] += dzc^T cos (this wave's own dzc image: in-order LDS, no barrier)
     {
-    ASVRL_FRESH_LANE();
+      ASVRL_FRESH_LANE();
+      const TrA<kNcos> TA_cos(lane);
+      const TrA<kNcos> TA_dzc(lane);
 #pragma unroll
-    for (int kk = 0; kk < G / 16; ++kk) {
-      const frag8 A0 = tr_frag<kNcos>(dzc_w, 16 * kk, 0, lane);
-      const frag8 A1 = tr_frag<kNcos>(dzc_w, 16 * kk, 32, lane);
-      dbc0 += sum8(A0);
-      dbc1 += sum8(A1);
+      for (int kk = 0; kk < G / 16; ++kk) {
+        const frag8 A0 = trf(dzc_w, TA_dzc, kk, 0);
+        const frag8 A1 = trf(dzc_w, TA_dzc, kk, 1);
+        dbc0 += sum8(A0);
+        dbc1 += sum8(A1);
 #pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        const frag8 Bf = tr_frag<kNcos>(L.cos, 16 * kk, 32 * n, lane);
-        mfma_acc(dWc[n], A0, Bf);
-        mfma_acc(dWc[2 + n], A1, Bf);
+        for (int n = 0; n < 2; ++n) {
+          const frag8 Bf = trf(L.cos, TA_cos, kk, n);
+          mfma_acc(dWc[n], A0, Bf);
+          mfma_acc(dWc[2 + n], A1, Bf);
+        }
       }
     }
+#pragma unroll
+    for (int u = 0; u < IL::kPer; ++u) {
+      const int e = tid_p + u * kNW * 64;
+      if (e < IL::kSize) L.in[buf ^ 1][e] = pre[u];
     }
-    __syncthreads();   // the next round overwrites cos, F, G, x
+    ASVRL_STAMP(14);
+    __syncthreads();   // the next round overwrites cos, F, G, x, a, b, dz1
+    ASVRL_STAMP(15);
   }
 
   // ---------------- the workgroup's partials: [M*K + M] per layer, features in natural order
@@ -721,6 +1002,12 @@ int fused_rounds(int B, int N) { return static_cast<int>(static_cast<int64_t>(B)
 }  // namespace asvrl
 
 using namespace asvrl;
+
+#ifdef ASVRL_FUSED_STAMPS
+extern "C" int asvrl_debug_fused_stamps(uint64_t* out, int64_t n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), n * sizeof(uint64_t)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 extern "C" int32_t asvrl_critic_fused_groups(int32_t B, int32_t N) {
   if (B <= 0 || (N != 8 && N != 16 && N != 32)) return 0;
