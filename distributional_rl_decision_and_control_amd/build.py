@@ -24,7 +24,8 @@ OUT_F32 = os.path.join(HERE, "lib", "libasvrl_f32.so")
 VARIANTS = {OUT: [], OUT_F32: ["-DASVRL_OPERAND_F32=1"]}
 # per-source flags: the fused critic keeps its persistent weight-gradient accumulators in AGPRs (inline
 # asm) and every other MFMA in the VGPR form; no NaN operands on the path (ReLU as one v_max_f32, no
-# canonicalising max)
+# canonicalising max). The f32 build drops the VGPR form: it has no inline-asm accumulators, and the
+# compiler's own AGPR placement spills far less there.
 SOURCE_FLAGS = {"asvrl_critic_fused.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-honor-nans"]}
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("ASVRL_OFFLOAD_ARCH", "gfx950")
@@ -61,8 +62,10 @@ def build_lib(force=False, verbose=False, jobs=None):
             o = _obj(out, src)
             objs.append(o)
             if force or not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(src), hdr_t):
-                todo.append(([HIPCC] + FLAGS[:3] + ["-c"] + FLAGS[3:] + extra +
-                             SOURCE_FLAGS.get(os.path.basename(src), []) + ["-o", o + ".tmp", src], o))
+                sf = SOURCE_FLAGS.get(os.path.basename(src), [])
+                if extra:   # the f32 build: its accumulators are plain MFMA results (no AGPR pinning)
+                    sf = [f for f in sf if f not in ("-mllvm", "-amdgpu-mfma-vgpr-form=1")]
+                todo.append(([HIPCC] + FLAGS[:3] + ["-c"] + FLAGS[3:] + extra + sf + ["-o", o + ".tmp", src], o))
         links.append((out, objs))
     running = []
     while todo or running:

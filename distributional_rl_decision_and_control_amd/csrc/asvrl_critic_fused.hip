@@ -28,13 +28,18 @@
 //
 // Per round: stage (F, G, cos) | L0 -> x | L1 -> h1g | L2 -> q partials | loss -> dq | dz2, dwo |
 // dW2 + L3 (W2^T dz2) -> dG, dz1 | dW1 | L4 (W1^T dz1, c recomputed) -> dF, dzc | dWc, ten barriers.
+//
+// IQN (template flag; train_IQN, agent.py:449-468, IQN_model.py:74-108): the same trunk without the
+// action encoder (h1g = h1, no G / dG), q = W_out[a_b] . h2 + b_out[a_b] at the sample's action, and the
+// output layer's gradient as one more MFMA per wave and round, dW_out[:, own] += D^T h2 with D the
+// one-hot dq image (rows = 32 padded actions), accumulated in VGPRs.
 #include "asvrl_common.h"
 #include "asvrl_mfma.h"
 
 namespace asvrl {
 namespace {
 
-constexpr int kC = 256, kH = 128, kNcos = 64, kNW = 4;
+constexpr int kC = 256, kH = 128, kNcos = 64, kNW = 4, kMaxA = ASVRL_IQN_MAX_ACTIONS;
 
 #if ASVRL_OPERAND_F32
 template <int NT> struct FusedNB { static constexpr int v = 1; };
@@ -307,49 +312,54 @@ struct FusedArgs {
   void* dzF;
   float* dzG;
   AsvCriticParts parts;
+  const float* iwo;   // IQN: output_layer.weight [A][128], bias [A] (f32)
+  const float* ibo;
+  int n_actions;
 };
 
 constexpr int kObsIn = 37;   // self 7 | objects 25 | mask 5 of the packed observation row
 constexpr int kEncFloats = 56 * 7 + 56 + 40 * 5 + 40 + 128 * 2 + 128;
 
-// One round's inputs in LDS (floats): obs rows [S][37] | actions [S][2] | taus [G] | q_next [S][NT] |
-// rewards [S] | dones [S]
-template <int NT, int S, int G>
+// One round's inputs in LDS (floats): obs rows [S][37] | actions [S][NA] | taus [G] | q_next [S][NT] |
+// rewards [S] | dones [S]; NA = 2 (AC-IQN's continuous action) or 1 (IQN's action index)
+template <int NT, int S, int G, int NA>
 struct InLayout {
-  static constexpr int kObs = 0, kAct = S * kObsIn, kTau = kAct + 2 * S, kQn = kTau + G, kRew = kQn + S * NT,
+  static constexpr int kObs = 0, kAct = S * kObsIn, kTau = kAct + NA * S, kQn = kTau + G, kRew = kQn + S * NT,
                        kDon = kRew + S, kSize = kDon + S;
   static constexpr int kPer = (kSize + kNW * 64 - 1) / (kNW * 64);   // elements per thread
 };
 
-template <int NT, int NB, int S>
+template <int NT, int NB, int S, bool IQN>
 struct FusedLds {
   elem_t cos[32 * NB * kNcos];        // natural order (the cos layer is input-fed)
   elem_t x[32 * NB * kC];             // F * c
   elem_t a[32 * NB * kH];             // h1g
   elem_t b[32 * NB * kH];             // h2, then dz2 in place
-  elem_t dz1[32 * NB * kH];
+  elem_t dz1[32 * NB * kH];           // IQN: first the one-hot dq image [G][64] (output layer's dZ)
   elem_t dzc[kNW][32 * NB * kNcos];   // each wave's own dzc image (the A operand of its dWc rows)
   float F[S * kC];                    // position order; operand-rounded values held in f32
-  float G[S * kH];                    // position order
+  float G[IQN ? 4 : S * kH];          // position order (AC-IQN's action features)
   float qpart[kNW][32 * NB];
   float dq[32 * NB];
   float bias[kC + 3 * kH + 4];        // bc | b1 | b2 | wo, position order | bo
+  float woA[IQN ? kMaxA * kH : 4];    // IQN: output_layer.weight, position order, zero rows to 32
+  float boA[IQN ? kMaxA : 4];
   float enc[kEncFloats];              // encoder parameters (stage_fg)
-  float in[2][InLayout<NT, S, 32 * NB>::kSize];   // the round's inputs, double-buffered (prefetched a round ahead)
+  float in[2][InLayout<NT, S, 32 * NB, IQN ? 1 : 2>::kSize];   // the round's inputs, double-buffered
   float red[kNW];
 };
 
 constexpr int kSelfF = 56, kSelfIn = 7, kObjF = 40, kObjIn = 5, kObsMask = 32;
 
 // element e of round t's input block (InLayout), read from the kernel's global inputs
-template <int NT, int S, int G>
+template <int NT, int S, int G, int NA>
 __device__ __forceinline__ float fetch_in(const FusedArgs& a, int t, int e) {
   // one load from a selected address (a branch per source would serialise the loads)
-  using IL = InLayout<NT, S, G>;
+  using IL = InLayout<NT, S, G, NA>;
   const int64_t b0 = static_cast<int64_t>(t) * S;
   const float* p;
   if (e < IL::kAct) p = a.obs + (b0 + e / kObsIn) * a.ld_obs + e % kObsIn;
-  else if (e < IL::kTau) p = a.ain + (b0 + (e - IL::kAct) / 2) * a.ld_ain + (e - IL::kAct) % 2;
+  else if (e < IL::kTau) p = a.ain + (b0 + (e - IL::kAct) / NA) * a.ld_ain + (e - IL::kAct) % NA;
   else if (e < IL::kQn) p = a.taus + static_cast<int64_t>(t) * G + (e - IL::kTau);
   else if (e < IL::kRew) p = a.qn + b0 * NT + (e - IL::kQn);
   else if (e < IL::kDon) p = a.rew + (b0 + e - IL::kRew) * a.ld_rd;
@@ -361,10 +371,10 @@ __device__ __forceinline__ float fetch_in(const FusedArgs& a, int t, int e) {
 // AC_IQN_model.py:468-470) of the round's S samples into LDS, position order; xb for the encoder
 // weight gradient. f32 dot products in the same order as asvrl_critic.hip's stage_features, from the
 // round's staged inputs and the staged encoder parameters.
-template <int NT, int S, int G>
+template <int NT, int S, int G, bool IQN>
 __device__ __forceinline__ void stage_fg(const FusedArgs& a, int b0, int tid, const float* in, const float* enc,
                                          float* Fs, float* Gs) {
-  using IL = InLayout<NT, S, G>;
+  using IL = InLayout<NT, S, G, IQN ? 1 : 2>;
   constexpr int T = kNW * 64;
   const float* self_w = enc;
   const float* self_b = self_w + 56 * 7;
@@ -408,7 +418,7 @@ __device__ __forceinline__ void stage_fg(const FusedArgs& a, int b0, int tid, co
       }
     }
   }
-  if (tid < kH) {
+  if (!IQN && tid < kH) {
     const int m = tid;
     const float w0 = ae_w[2 * m], w1 = ae_w[2 * m + 1], bb = ae_b[m];
 #pragma unroll
@@ -483,11 +493,19 @@ __device__ __forceinline__ void sample_sums(float (&X)[NB][16], int base, int la
   }
 }
 
-template <int NT>
+// IQN: the action index of the round's local row lr (clamped as asvrl_critic.hip's IQN_TRAIN)
+template <int OFF>
+__device__ __forceinline__ int row_action(const float* in, int bl, int A) {
+  const int ai = static_cast<int>(in[OFF + bl]);
+  return ai < 0 ? 0 : (ai >= A ? A - 1 : ai);
+}
+
+template <int NT, bool IQN>
 __global__ __launch_bounds__(kNW * 64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void critic_fused_kernel(FusedArgs a) {
-  constexpr int NB = FusedNB<NT>::v, G = 32 * NB, S = G / NT;
-  __shared__ __attribute__((aligned(16))) FusedLds<NT, NB, S> L;
+  constexpr int NB = FusedNB<NT>::v, G = 32 * NB, S = G / NT, NA = IQN ? 1 : 2;
+  __shared__ __attribute__((aligned(16))) FusedLds<NT, NB, S, IQN> L;
+  static_assert(sizeof(L) <= 160 * 1024, "fused critic LDS image exceeds the CU's 160 KB");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
   const frag8* WC = reinterpret_cast<const frag8*>(a.w.wc_frag);
   const frag8* W1 = reinterpret_cast<const frag8*>(a.w.w1_frag);
@@ -502,17 +520,25 @@ void critic_fused_kernel(FusedArgs a) {
   for (int i = threadIdx.x; i < kH; i += kNW * 64) {
     b1p[swap23(i)] = a.w.b1[i];
     b2p[swap23(i)] = a.w.b2[i];
-    wop[swap23(i)] = a.w.wo[i];
+    if constexpr (!IQN) wop[swap23(i)] = a.w.wo[i];
   }
-  if (threadIdx.x == 0) L.bias[kC + 3 * kH] = a.w.bo[0];
+  if constexpr (IQN) {   // the head, rows >= n_actions zero (never gathered: actions are clamped)
+    for (int i = threadIdx.x; i < kMaxA * kH; i += kNW * 64) {
+      const int row = i / kH, col = i % kH;
+      L.woA[row * kH + swap23(col)] = row < a.n_actions ? a.iwo[i] : 0.f;
+    }
+    if (threadIdx.x < kMaxA) L.boA[threadIdx.x] = threadIdx.x < a.n_actions ? a.ibo[threadIdx.x] : 0.f;
+  } else {
+    if (threadIdx.x == 0) L.bias[kC + 3 * kH] = a.w.bo[0];
+  }
 
-  using IL = InLayout<NT, S, G>;
+  using IL = InLayout<NT, S, G, NA>;
   {
     const float* srcs[6] = {a.w.self_w, a.w.self_b, a.w.obj_w, a.w.obj_b, a.w.ae_w, a.w.ae_b};
     const int lens[6] = {56 * 7, 56, 40 * 5, 40, 128 * 2, 128};
     int off = 0;
 #pragma unroll
-    for (int q = 0; q < 6; ++q) {
+    for (int q = 0; q < (IQN ? 4 : 6); ++q) {
       for (int i = threadIdx.x; i < lens[q]; i += kNW * 64) L.enc[off + i] = srcs[q][i];
       off += lens[q];
     }
@@ -520,7 +546,7 @@ void critic_fused_kernel(FusedArgs a) {
 #pragma unroll
       for (int u = 0; u < IL::kPer; ++u) {
         const int e = threadIdx.x + u * kNW * 64;
-        if (e < IL::kSize) L.in[0][e] = fetch_in<NT, S, G>(a, blockIdx.x, e);
+        if (e < IL::kSize) L.in[0][e] = fetch_in<NT, S, G, NA>(a, blockIdx.x, e);
       }
   }
   __syncthreads();
@@ -532,9 +558,12 @@ void critic_fused_kernel(FusedArgs a) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) dW1[i] = f32x16{};
   float db2 = 0.f, db1 = 0.f, dbc0 = 0.f, dbc1 = 0.f, dbo = 0.f;
-  float dwo[16];
+  // output layer: AC-IQN's single row (per-lane sums over rows), IQN's [32 actions][own 32 features]
+  // MFMA block (rows = actions)
+  float dwo[IQN ? 1 : 16];
+  f32x16 dWo = f32x16{};
 #pragma unroll
-  for (int g = 0; g < 16; ++g) dwo[g] = 0.f;
+  for (int g = 0; g < (IQN ? 1 : 16); ++g) dwo[g] = 0.f;
   int buf = 0, it_ = 0;
   (void)it_;
   for (int t = blockIdx.x; t < a.rounds; t += gridDim.x, buf ^= 1, ++it_) {
@@ -546,7 +575,7 @@ void critic_fused_kernel(FusedArgs a) {
     for (int u = 0; u < IL::kPer; ++u) {
       const int e = tid_p + u * kNW * 64;
       pre[u] = (t + static_cast<int>(gridDim.x) < a.rounds && e < IL::kSize)
-                   ? fetch_in<NT, S, G>(a, t + gridDim.x, e) : 0.f;
+                   ? fetch_in<NT, S, G, NA>(a, t + gridDim.x, e) : 0.f;
     }
     const float* in = L.in[buf];
     // the lane indices re-derived through an opaque copy every round: otherwise every LDS / weight
@@ -570,7 +599,7 @@ void critic_fused_kernel(FusedArgs a) {
     {
       int tid_s = threadIdx.x;
       asm volatile("" : "+v"(tid_s));
-      stage_fg<NT, S, G>(a, b0, tid_s, in, L.enc, L.F, L.G);
+      stage_fg<NT, S, G, IQN>(a, b0, tid_s, in, L.enc, L.F, L.G);
       static_assert((G * (kNcos / 8)) % (kNW * 64) == 0, "whole cos chunks per thread");
 #pragma unroll
       for (int u = 0; u < G * (kNcos / 8) / (kNW * 64); ++u) {
@@ -631,10 +660,11 @@ void critic_fused_kernel(FusedArgs a) {
       const RowA<kC> RA_x(r, h);
       const RowA<kH> RA_a(r, h);
       float gv[NB][2][8];
+      if constexpr (!IQN)
 #pragma unroll
-      for (int j = 0; j < NB; ++j)
+        for (int j = 0; j < NB; ++j)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) lds8(L.G + ((32 * j + r) / NT) * kH + w * 32 + 16 * s + 8 * h, gv[j][s]);
+          for (int s = 0; s < 2; ++s) lds8(L.G + ((32 * j + r) / NT) * kH + w * 32 + 16 * s + 8 * h, gv[j][s]);
       f32x16 acc[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[j] = acc_init(b1p, w * 32, h);
@@ -656,7 +686,7 @@ void critic_fused_kernel(FusedArgs a) {
           for (int i = 0; i < 8; ++i) {
             const float hv = relu(acc[j][8 * s + i]);
             h1k[j][s][i] = (elem_t)hv;
-            go[i] = (elem_t)(hv * gv[j][s][i]);
+            go[i] = IQN ? h1k[j][s][i] : (elem_t)(hv * gv[j][s][i]);
           }
           rows(L.a, RA_a, j, 2 * w + s, go);
           pin(h1k[j][s]);
@@ -686,9 +716,15 @@ void critic_fused_kernel(FusedArgs a) {
       if constexpr (!kBiasFirst)
 #pragma unroll
         for (int j = 0; j < NB; ++j) z2[j] += bias_init(b2p, w * 32, h);
-      float wov[2][8];
+      // the output row feeding q: AC-IQN's single row, IQN's row of the sample's action
+      constexpr int NWO = IQN ? NB : 1;
+      float wov[NWO][2][8];
 #pragma unroll
-      for (int s = 0; s < 2; ++s) lds8(wop + w * 32 + 16 * s + 8 * h, wov[s]);
+      for (int j = 0; j < NWO; ++j) {
+        const float* src = IQN ? L.woA + row_action<IL::kAct>(in, (32 * j + r) / NT, a.n_actions) * kH : wop;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) lds8(src + w * 32 + 16 * s + 8 * h, wov[j][s]);
+      }
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         float part = 0.f;
@@ -698,7 +734,7 @@ void critic_fused_kernel(FusedArgs a) {
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             const float h2 = relu(z2[j][8 * s + i]);
-            part += wov[s][i] * h2;
+            part += wov[IQN ? j : 0][s][i] * h2;
             hv[i] = (elem_t)h2;
           }
           rows(L.b, RA_b, j, 2 * w + s, hv);
@@ -716,9 +752,12 @@ void critic_fused_kernel(FusedArgs a) {
       ASVRL_FRESH_LANE();
       for (int j = w; j < NB; j += kNW) {
         const int lr = 32 * j + r, grow = row0 + lr, b = grow / NT;
-        const float q = (((L.qpart[0][lr] + L.qpart[1][lr]) + L.qpart[2][lr]) + L.qpart[3][lr]) + L.bias[kC + 3 * kH];
-        float wl;
         const int bl = b - b0;
+        int ai = 0;
+        if constexpr (IQN) ai = row_action<IL::kAct>(in, bl, a.n_actions);
+        const float bo = IQN ? L.boA[ai] : L.bias[kC + 3 * kH];
+        const float q = (((L.qpart[0][lr] + L.qpart[1][lr]) + L.qpart[2][lr]) + L.qpart[3][lr]) + bo;
+        float wl;
         const float dq = row_loss_dq<NT>(a, in + IL::kQn + bl * NT, in[IL::kRew + bl], in[IL::kDon + bl],
                                          in[IL::kTau + lr], q, lane, &wl);
         if (a.tile_loss != nullptr) {
@@ -730,7 +769,17 @@ void critic_fused_kernel(FusedArgs a) {
           L.dq[lr] = dq;
           if (a.row_loss != nullptr) a.row_loss[grow] = wl;
           if (a.q != nullptr) a.q[grow] = q;
-          dbo += dq;
+          if constexpr (!IQN) dbo += dq;
+        }
+        if constexpr (IQN) {   // the output layer's dZ row: dq at the taken action (agent.py:456 gather)
+          frag8 o0, o1;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            o0[i] = (elem_t)(16 * h + i == ai ? dq : 0.f);
+            o1[i] = (elem_t)(16 * h + 8 + i == ai ? dq : 0.f);
+          }
+          row_store<64>(L.dz1, lr, 16 * h, o0);
+          row_store<64>(L.dz1, lr, 16 * h + 8, o1);
         }
       }
     }
@@ -743,11 +792,28 @@ void critic_fused_kernel(FusedArgs a) {
     {
       ASVRL_FRESH_LANE();
       const RowA<kH> RA_b(r, h);
+      if constexpr (IQN) {
+        // dW_out[:, own] += D^T h2 with D the one-hot dq image (rows = actions): h2 read before the
+        // in-place dz2 stores below (same wave, in-order LDS)
+        const TrA<64> TA_o(lane);
+        const TrA<kH> TA_b(lane);
+#pragma unroll
+        for (int kk = 0; kk < G / 16; ++kk) {
+          const frag8 A = trf(L.dz1, TA_o, kk, 0);
+          dbo += sum8(A);
+          dWo = mfma(A, trf(L.b, TA_b, kk, w), dWo);
+        }
+      }
       // every LDS operand first (one wait), then the arithmetic and the in-place stores
-      float wov[2][8], dqv[NB];
+      constexpr int NWO = IQN ? NB : 1;
+      float wov[NWO][2][8], dqv[NB];
       frag8 hv[NB][2];
 #pragma unroll
-      for (int s = 0; s < 2; ++s) lds8(wop + w * 32 + 16 * s + 8 * h, wov[s]);
+      for (int j = 0; j < NWO; ++j) {
+        const float* src = IQN ? L.woA + row_action<IL::kAct>(in, (32 * j + r) / NT, a.n_actions) * kH : wop;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) lds8(src + w * 32 + 16 * s + 8 * h, wov[j][s]);
+      }
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         dqv[j] = L.dq[32 * j + r];
@@ -762,8 +828,8 @@ void critic_fused_kernel(FusedArgs a) {
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             const float h2 = static_cast<float>(hv[j][s][i]);
-            dz[i] = (elem_t)(h2 > 0.f ? dqv[j] * wov[s][i] : 0.f);
-            dwo[8 * s + i] += dqv[j] * h2;
+            dz[i] = (elem_t)(h2 > 0.f ? dqv[j] * wov[IQN ? j : 0][s][i] : 0.f);
+            if constexpr (!IQN) dwo[8 * s + i] += dqv[j] * h2;
           }
           rows(L.b, RA_b, j, 2 * w + s, dz);
         }
@@ -792,10 +858,11 @@ void critic_fused_kernel(FusedArgs a) {
       const RowA<kH> RA_b(r, h);
       const RowA<kH> RA_d(r, h);
       float gv[NB][2][8];
+      if constexpr (!IQN)
 #pragma unroll
-      for (int j = 0; j < NB; ++j)
+        for (int j = 0; j < NB; ++j)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) lds8(L.G + ((32 * j + r) / NT) * kH + w * 32 + 16 * s + 8 * h, gv[j][s]);
+          for (int s = 0; s < 2; ++s) lds8(L.G + ((32 * j + r) / NT) * kH + w * 32 + 16 * s + 8 * h, gv[j][s]);
       f32x16 acc[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[j] = f32x16{};
@@ -819,16 +886,17 @@ void critic_fused_kernel(FusedArgs a) {
           for (int i = 0; i < 8; ++i) {
             const float h1 = static_cast<float>(h1k[j][s][i]);
             const float d = acc[j][8 * s + i];
-            dz1[i] = (elem_t)(h1 > 0.f ? d * gv[j][s][i] : 0.f);
+            dz1[i] = (elem_t)(h1 > 0.f ? (IQN ? d : d * gv[j][s][i]) : 0.f);
             gsa[j][8 * s + i] = d * h1;
           }
           rows(L.dz1, RA_d, j, 2 * w + s, dz1);
         }
       }
-      sample_sums<NT, NB>(gsa, w * 32, lane, [&](int bl, int p, float v) {
-        const float gm = L.G[bl * kH + p];
-        if (a.dzG != nullptr) a.dzG[static_cast<size_t>(b0 + bl) * kH + swap23(p)] = gm > 0.f ? v : 0.f;
-      });
+      if constexpr (!IQN)
+        sample_sums<NT, NB>(gsa, w * 32, lane, [&](int bl, int p, float v) {
+          const float gm = L.G[bl * kH + p];
+          if (a.dzG != nullptr) a.dzG[static_cast<size_t>(b0 + bl) * kH + swap23(p)] = gm > 0.f ? v : 0.f;
+        });
     }
     ASVRL_STAMP(12);
     __syncthreads();
@@ -963,11 +1031,20 @@ void critic_fused_kernel(FusedArgs a) {
     pc[kC * kNcos + swap23(2 * w * 32 + r)] = dbc0;
     pc[kC * kNcos + swap23((2 * w + 1) * 32 + r)] = dbc1;
   }
+  if constexpr (IQN) {
+    // output layer [32 actions][128] + [32]: register g = action row, lane = feature position
+    float* po = a.parts.out + static_cast<size_t>(grp) * (kMaxA * kH + kMaxA);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) po[((g & 3) + 8 * (g >> 2) + 4 * h) * kH + swap23(w * 32 + r)] = dWo[g];
+    dbo = half_sum(dbo);   // lane r: the action r column's sum over the round rows (every wave alike)
+    if (w == 0 && h == 0) po[kMaxA * kH + r] = dbo;
+    return;
+  }
   // output layer: sum over the half's 32 lanes (rows) of each register (feature), then the waves' dbo
   float* po = a.parts.out + static_cast<size_t>(grp) * (kH + 1);
 #pragma unroll
   for (int g = 0; g < 16; ++g) {
-    const float v = seg_sum<32>(dwo[g]);   // lane 31 of each half
+    const float v = seg_sum<32>(dwo[IQN ? 0 : g]);   // lane 31 of each half
     if (r == 31) po[swap23(w * 32 + 16 * (g >> 3) + 8 * h + (g & 7))] = v;
   }
   dbo = seg_sum<32>(h == 0 ? dbo : 0.f);
@@ -1046,8 +1123,51 @@ extern "C" int asvrl_critic_train_fused(const AsvCriticWeights* w, const AsvCrit
   a.parts = *parts;
   const int grid = asvrl_critic_fused_groups(io->B, io->N);
   hipStream_t st = as_stream(stream);
-  if (io->N == 32) hipLaunchKernelGGL((critic_fused_kernel<32>), dim3(grid), dim3(kNW * 64), 0, st, a);
-  else if (io->N == 16) hipLaunchKernelGGL((critic_fused_kernel<16>), dim3(grid), dim3(kNW * 64), 0, st, a);
-  else hipLaunchKernelGGL((critic_fused_kernel<8>), dim3(grid), dim3(kNW * 64), 0, st, a);
+  if (io->N == 32) hipLaunchKernelGGL((critic_fused_kernel<32, false>), dim3(grid), dim3(kNW * 64), 0, st, a);
+  else if (io->N == 16) hipLaunchKernelGGL((critic_fused_kernel<16, false>), dim3(grid), dim3(kNW * 64), 0, st, a);
+  else hipLaunchKernelGGL((critic_fused_kernel<8, false>), dim3(grid), dim3(kNW * 64), 0, st, a);
   return check_launch("asvrl_critic_train_fused");
+}
+
+// train_IQN's update (agent.py:449-468) in one launch: the same kernel with IQN_Policy's trunk (no action
+// encoder, IQN_model.py:74-108) and its 128 -> A output layer gathered at the taken action; the output
+// layer's partial is [32 x 128 + 32] per workgroup (rows >= n_actions zero).
+extern "C" int asvrl_iqn_train_fused(const AsvCriticWeights* w, const AsvIqnHead* head, const AsvIqnIO* io,
+                                     const AsvCriticParts* parts, void* stream) {
+  ASVRL_REQUIRE(w && head && io && parts, "asvrl_iqn_train_fused: null argument");
+  ASVRL_REQUIRE(io->taus && io->obs && io->actions && io->q_next && io->rewards && io->dones,
+                "asvrl_iqn_train_fused: needs taus, obs, actions, q_next, rewards and dones");
+  ASVRL_REQUIRE(io->ld_obs >= 37, "asvrl_iqn_train_fused: ld_obs must cover the packed observation row");
+  ASVRL_REQUIRE(w->wc_frag && w->w1_frag && w->w2_frag && w->w2t_frag && w->w1t_frag && w->bc && w->b1 && w->b2 &&
+                    w->self_w && w->self_b && w->obj_w && w->obj_b,
+                "asvrl_iqn_train_fused: null weight");
+  ASVRL_REQUIRE(head->wo && head->bo && head->n_actions >= 1 && head->n_actions <= kMaxA,
+                "asvrl_iqn_train_fused: bad head");
+  ASVRL_REQUIRE(parts->cos_emb && parts->hidden && parts->hidden2 && parts->out,
+                "asvrl_iqn_train_fused: null partial buffer");
+  ASVRL_REQUIRE(io->N == 8 || io->N == 16 || io->N == 32, "asvrl_iqn_train_fused: N must be 8, 16 or 32");
+  ASVRL_REQUIRE(io->Np == io->N, "asvrl_iqn_train_fused: N' must equal N");
+  ASVRL_REQUIRE(io->kappa > 0.f, "asvrl_iqn_train_fused: kappa must be positive");
+  ASVRL_REQUIRE(io->B >= 0 && (static_cast<int64_t>(io->B) * io->N) % (32 * fused_nb(io->N)) == 0,
+                "asvrl_iqn_train_fused: B*N must be a multiple of the round size (64 rows; 32 in the f32 build)");
+  if (io->B == 0) return 0;
+  FusedArgs a{};
+  a.w = *w;
+  a.obs = io->obs; a.ld_obs = io->ld_obs; a.ain = io->actions; a.ld_ain = io->ld_rd; a.xb = io->xb;
+  a.taus = io->taus; a.qn = io->q_next; a.rew = io->rewards; a.don = io->dones; a.ld_rd = io->ld_rd;
+  a.gamma = io->gamma; a.kappa = io->kappa;
+  a.gscale = 1.f / (static_cast<float>(io->B) * static_cast<float>(io->Np));
+  a.loss_scale = io->loss_scale;
+  a.B = io->B;
+  a.rounds = fused_rounds(io->B, io->N);
+  a.q = io->q; a.row_loss = io->row_loss; a.tile_loss = io->tile_loss;
+  a.dzF = io->dzF; a.dzG = nullptr;
+  a.parts = *parts;
+  a.iwo = head->wo; a.ibo = head->bo; a.n_actions = head->n_actions;
+  const int grid = asvrl_critic_fused_groups(io->B, io->N);
+  hipStream_t st = as_stream(stream);
+  if (io->N == 32) hipLaunchKernelGGL((critic_fused_kernel<32, true>), dim3(grid), dim3(kNW * 64), 0, st, a);
+  else if (io->N == 16) hipLaunchKernelGGL((critic_fused_kernel<16, true>), dim3(grid), dim3(kNW * 64), 0, st, a);
+  else hipLaunchKernelGGL((critic_fused_kernel<8, true>), dim3(grid), dim3(kNW * 64), 0, st, a);
+  return check_launch("asvrl_iqn_train_fused");
 }

@@ -394,9 +394,10 @@ class PartialArena:
 
     def groups(self, part, groups, M, K, dw, db, accumulate=False):
         """dw (M x K) (+)= sum over groups of part[g][0:M*K], db (M) (+)= of part[g][M*K:]: per-workgroup
-        partials a kernel wrote in the [groups][M*K + M] layout (critic_train_fused)."""
-        assert dw.numel() == M * K and db.numel() == M
-        self._seg(part, dw, db, groups, M * K, M, accumulate, stride=M * K + M, boff=M * K)
+        partials a kernel wrote in the [groups][M*K + M] layout (critic_train_fused); a dw / db with fewer
+        rows takes the leading rows (IQN's padded 32-row output layer)."""
+        assert dw.numel() % K == 0 and dw.numel() <= M * K and db.numel() <= M
+        self._seg(part, dw, db, groups, dw.numel(), db.numel(), accumulate, stride=M * K + M, boff=M * K)
 
     def scalar(self, partials, out, accumulate=False):
         """out (1 f32) (+)= sum(partials): a scalar segment (e.g. per-tile loss partials)."""

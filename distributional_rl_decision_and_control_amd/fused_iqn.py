@@ -7,15 +7,18 @@ replay batch `rows` ([B][88]: obs | next obs | action | reward | done):
 
     target encoders(ns) + trunk, max over actions per tau -> q_next
                                                           asvrl_iqn_forward_max    (agent.py:451-452)
-    local encoders(s) + forward, gather at a, quantile-Huber vs r + g q_next (1-d), backward
-                                                          asvrl_iqn_train (2 launches, agent.py:455-468)
-    weight grads of the 4 trunk layers + encoders         asvrl_linear_wgrad_partial x5 (3 streams),
+    local encoders(s) + forward, gather at a, quantile-Huber vs r + g q_next (1-d), backward,
+    and the per-workgroup weight-gradient partials of the four layers
+                                                          asvrl_iqn_train_fused (ONE launch, agent.py:455-468)
+    encoder gradients                                     asvrl_linear_wgrad_multi (the fold image),
                                                           ONE asvrl_partial_sums_norm: every .grad
                                                           (encoders folded, the 32-row output
                                                           reduction into the 25-row layer), the
                                                           loss and the gradient norm
     clip + Adam                                           asvrl_adam_step          (agent.py:471-472)
       (with DP: asvrl_partial_sums, RCCL all-reduce, asvrl_adam_clip)
+    (ASVRL_FUSED_TRAIN=0: asvrl_iqn_train's two launches + the batched weight-gradient launch over the
+    saved activations, the round-1 path)
     re-pack trunk and head                                asvrl_iqn_pack
 
 The encoders run inside the trunk kernels' prologue (f32, from the parameters). act_iqn for
@@ -29,8 +32,8 @@ import ctypes as C
 import torch
 
 from . import _abi
-from .fused_critic import CriticPack, PartialArena, TrainBuffers
-from .fused_update import SideStreams, _reduce_and_step
+from .fused_critic import CriticPack, PartialArena, TrainBuffers, fused_groups, fused_train_supported
+from .fused_update import FUSED_TRAIN, SideStreams, _reduce_and_step
 
 OBS = 40
 K_ACT = 32
@@ -113,6 +116,30 @@ def iqn_train(pack, F, taus, bufs, dz_out, q_next, actions, rewards, dones, gamm
                                       C.byref(bufs.struct), _abi.stream_ptr(stream)), "asvrl_iqn_train", pack.L)
 
 
+def iqn_train_fused(pack, net, taus, N, q_next, actions, rewards, dones, gamma, obs, arena, dzF=None, xb=None,
+                    tile_loss=None, kappa=1.0, q=None, row_loss=None, stream=None):
+    """asvrl_iqn_train_fused: train_IQN's local pass (agent.py:455-468) -- forward, gather at the
+    taken action, quantile-Huber loss, backward -- AND the weight gradients of the trunk and the
+    output layer in one launch; the per-workgroup partials land in `arena` as segments of net's
+    cos_embedding / hidden_layer / hidden_layer_2 / output_layer .grad."""
+    B = obs.shape[0]
+    groups = fused_groups(pack, B, N)
+    assert groups > 0 and fused_train_supported(pack, B, N), (B, N)
+    assert actions.stride(0) == rewards.stride(0) == dones.stride(0)
+    shapes = ((net.cos_embedding, 256, 64), (net.hidden_layer, 128, 256), (net.hidden_layer_2, 128, 128),
+              (net.output_layer, _abi.IQN_MAX_ACTIONS, 128))
+    regions = [arena._take(groups * (M * K + M)) for _, M, K in shapes]
+    parts = _abi.AsvCriticParts()
+    parts.cos_emb, parts.hidden, parts.hidden2, parts.out = (t.data_ptr() for t in regions)
+    io = _io(None, N, obs=obs, xb=xb, taus=taus, Np=N, kappa=float(kappa), q_next=q_next, actions=actions,
+             rewards=rewards, dones=dones, ld_rd=rewards.stride(0), gamma=float(gamma), q=q, row_loss=row_loss,
+             dzF=dzF, tile_loss=tile_loss, loss_scale=1.0 / float(B * N))
+    _abi.check(pack.L.asvrl_iqn_train_fused(C.byref(pack.struct), C.byref(pack.head), C.byref(io), C.byref(parts),
+                                            _abi.stream_ptr(stream)), "asvrl_iqn_train_fused", pack.L)
+    for (layer, M, K), part in zip(shapes, regions):
+        arena.groups(part, groups, M, K, layer.weight.grad, layer.bias.grad)
+
+
 def iqn_act(pack, F, actions64, step_dev, steps_per_count, total, fraction, initial, final, seed, taus=None,
             stream=None, obs=None):
     """act_iqn for every row of F (or of the observation rows `obs`) into actions64[:, 0] (f64 action index)."""
@@ -165,6 +192,16 @@ def iqn_grads(st, net, rows, taus, gamma=0.99, flush=True):
     bufs, arena, side = st.bufs, st.arena, st.side
     # every .grad is overwritten below (no zeroing); the trunk kernels run the encoders on the rows
     iqn_forward_max(st.target, None, taus[0], N, st.q_next, obs=ns_rows)
+    if FUSED_TRAIN and fused_train_supported(st.local, B, N):
+        # forward, loss, backward and the four layers' weight-gradient partials in one launch
+        iqn_train_fused(st.local, net, taus[1], N, st.q_next.view(B, N), a_col, r_col, d_col, gamma, s_rows, arena,
+                        dzF=st.dzF, xb=st.xb, tile_loss=st.tile_loss)
+        with arena.batch():
+            arena.fold(st.dzF, st.xb, net)   # encoder image -> self/object encoder grads
+        arena.scalar(st.tile_loss, st.loss)
+        if flush:
+            arena.flush()
+        return
     iqn_train(st.local, None, taus[1], bufs, st.dz_out, st.q_next.view(B, N), a_col, r_col, d_col, gamma, st.dzF,
               tile_loss=st.tile_loss, obs=s_rows, xb=st.xb)
     with arena.batch():   # the five layers in one launch

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 12
+#define ASVRL_ABI_VERSION 13
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -387,6 +387,14 @@ int asvrl_iqn_forward_max(const AsvCriticWeights* w, const AsvIqnHead* head, con
  * (two launches). acts: h1g holds h1; dq is optional. */
 int asvrl_iqn_train(const AsvCriticWeights* w, const AsvIqnHead* head, const AsvIqnIO* io,
                     const AsvCriticActs* acts, void* stream);
+
+/* train_IQN's local pass (agent.py:455-468) WITH the trunk and output-layer weight gradients, in
+ * one persistent launch (asvrl_critic_train_fused's kernel on IQN_Policy's trunk): encoders from
+ * io->obs, forward, gather at io->actions, quantile-Huber loss, backward, per-workgroup partials
+ * (parts; parts->out is [groups][32*128 + 32], output rows >= A zero), dzF / xb / tile_loss.
+ * dz_out is not written; N' must equal N; groups = asvrl_critic_fused_groups(B, N). */
+int asvrl_iqn_train_fused(const AsvCriticWeights* w, const AsvIqnHead* head, const AsvIqnIO* io,
+                          const AsvCriticParts* parts, void* stream);
 
 /* act_iqn (agent.py:227-256) for every row of F with K = 32 quantile samples per state. */
 int asvrl_iqn_act(const AsvCriticWeights* w, const AsvIqnHead* head, const AsvIqnIO* io, void* stream);

@@ -1,0 +1,127 @@
+"""GPU: asvrl_iqn_train_fused (train_IQN's local pass, agent.py:455-468 -- forward, gather at the taken
+action, quantile-Huber, backward -- plus the weight gradients of the trunk and the 128 -> A output layer
+in one launch, asvrl_critic_fused.hip on IQN_Policy's trunk) against the two-kernel path with its batched
+weight-gradient launch over saved activations (asvrl_iqn_train + asvrl_linear_wgrad_multi), on the same
+batch, taus and weights; the f32 build also against torch autograd on the CPU in f32, the reference's
+own arithmetic (oracle/learn_ref.py; in f64 a cos-layer pre-activation within f32 rounding of 0 takes
+the other side of the ReLU for one row at B = 256, for both GPU paths alike).
+
+Bars as tests/test_critic_fused_gpu.py: f32 build every gradient within 2e-5 of the tensor's scale,
+loss 1e-6 rel.; bf16 build gradient cosine > 0.999, norm within 1 %, loss 1e-4 rel. The reference pin
+of the fused path through Agent.train is test_learner_golden_gpu.test_fused_iqn_matches_reference.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+A = 25
+
+
+def _batch(B, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    rows = torch.zeros(B, 88, device="cuda")
+    for c in (0, 40):
+        rows[:, c:c + 7] = torch.randn(B, 7, generator=g, device="cuda") * 3
+        rows[:, c + 7:c + 32] = torch.randn(B, 25, generator=g, device="cuda") * 3
+        rows[:, c + 32:c + 37] = (torch.rand(B, 5, generator=g, device="cuda") > 0.4).float()
+    rows[:, 80] = torch.randint(0, A, (B,), generator=g, device="cuda").float()
+    rows[:, 82] = torch.randn(B, generator=g, device="cuda")
+    rows[:, 83] = (torch.rand(B, generator=g, device="cuda") > 0.9).float()
+    return rows
+
+
+def _iqn_grads(ops, B, N, fused, rows, taus, seed=100):
+    """Every IQN_Policy .grad (reduced) and the loss of one train_IQN step, without the optimizer."""
+    from distributional_rl_decision_and_control_amd import fused_iqn as fi
+    from distributional_rl_decision_and_control_amd.agent import Agent
+    from distributional_rl_decision_and_control_amd.learner import FusedAdam
+    ag = Agent(seed=seed, agent_type="IQN")
+    net = ag.policy_local
+    opt = FusedAdam(net.parameters(), lr=1e-4, operands=ops)
+    st = fi.FusedIQNState(net, ag.policy_target, B, N, operands=ops)
+    opt.grads.zero_()
+    old, fi.FUSED_TRAIN = fi.FUSED_TRAIN, fused
+    try:
+        fi.iqn_grads(st, net, rows, taus, 0.99, flush=True)
+    finally:
+        fi.FUSED_TRAIN = old
+    torch.cuda.synchronize()
+    grads = {n: p.grad.detach().cpu().numpy().astype(np.float64).copy() for n, p in net.named_parameters()}
+    return grads, float(st.loss[0].item())
+
+
+def _reference_grads(rows, taus, seed=100):
+    """The same step by torch autograd in f32 on the CPU (oracle/learn_ref.py's IQN forward and
+    quantile-Huber loss, agent.py:449-468)."""
+    from distributional_rl_decision_and_control_amd.agent import Agent
+    from oracle import learn_ref as lr
+    ag = Agent(seed=seed, agent_type="IQN")
+    cw = {k: v.detach().cpu().float().requires_grad_(True) for k, v in ag.policy_local.state_dict().items()}
+    tw = {k: v.detach().cpu().float() for k, v in ag.policy_target.state_dict().items()}
+    x = rows.detach().cpu().float()
+    B = x.shape[0]
+
+    def st(c):
+        return x[:, c:c + 7], x[:, c + 7:c + 32].reshape(B, 5, 5), x[:, c + 32:c + 37]
+    t = taus.detach().cpu().float()
+    N = t.shape[2]
+    with torch.no_grad():
+        qn = lr.iqn_forward(tw, st(40), t[0].view(B, N, 1)).max(2)[0]
+    qt = x[:, 82:83] + 0.99 * qn * (1.0 - x[:, 83:84])
+    a = x[:, 80].long().view(B, 1, 1).expand(B, N, 1)
+    qe = lr.iqn_forward(cw, st(0), t[1].view(B, N, 1)).gather(2, a).squeeze(2)
+    loss = lr.quantile_huber(qt, qe, t[1].view(B, N, 1))
+    names = list(cw)
+    g = torch.autograd.grad(loss, [cw[n] for n in names])
+    return {n: gi.double().numpy() for n, gi in zip(names, g)}, float(loss.detach())
+
+
+def _cos(x, y):
+    x, y = x.reshape(-1), y.reshape(-1)
+    return float(x @ y / (np.linalg.norm(x) * np.linalg.norm(y) + 1e-300))
+
+
+@pytest.mark.parametrize("ops,B,N", [("f32", 64, 8), ("f32", 64, 16), ("f32", 64, 32), ("f32", 256, 32),
+                                     ("bf16", 64, 8), ("bf16", 128, 16), ("bf16", 4096, 32)])
+def test_iqn_fused_train_matches_two_kernel_path(ops, B, N):
+    rows = _batch(B, 11 + N)
+    taus = torch.rand(2, B, N, generator=torch.Generator(device="cuda").manual_seed(3 + B), device="cuda")
+    gf, lf = _iqn_grads(ops, B, N, True, rows, taus)
+    gu, lu = _iqn_grads(ops, B, N, False, rows, taus)
+    if ops == "f32" and B <= 256:
+        gr, lr_ = _reference_grads(rows, taus)
+        for n in gr:
+            scale = np.abs(gr[n]).max() + 1e-30
+            print(f"{n:28s} fused {np.abs(gf[n] - gr[n]).max() / scale:.2e}  "
+                  f"two-kernel {np.abs(gu[n] - gr[n]).max() / scale:.2e}")
+        for n in gr:
+            scale = np.abs(gr[n]).max() + 1e-30
+            assert np.abs(gf[n] - gr[n]).max() / scale < 2e-5, n
+        np.testing.assert_allclose(lf, lr_, rtol=1e-5)
+    if ops == "f32":
+        np.testing.assert_allclose(lf, lu, rtol=1e-6)
+        for n in gu:
+            scale = np.abs(gu[n]).max() + 1e-30
+            err = np.abs(gf[n] - gu[n]).max() / scale
+            assert err < 2e-5, (n, err)
+    else:
+        np.testing.assert_allclose(lf, lu, rtol=1e-4)
+        for n in gu:
+            if np.abs(gu[n]).max() == 0:
+                continue
+            c = _cos(gf[n], gu[n])
+            ratio = np.linalg.norm(gf[n]) / np.linalg.norm(gu[n])
+            assert c > 0.999 and abs(ratio - 1) < 1e-2, (n, c, ratio)
+
+
+def test_iqn_fused_train_deterministic():
+    B, N = 1024, 32
+    rows = _batch(B, 5)
+    taus = torch.rand(2, B, N, generator=torch.Generator(device="cuda").manual_seed(6), device="cuda")
+    g1, l1 = _iqn_grads("bf16", B, N, True, rows, taus)
+    g2, l2 = _iqn_grads("bf16", B, N, True, rows, taus)
+    assert l1 == l2
+    for n in g1:
+        np.testing.assert_array_equal(g1[n], g2[n], err_msg=n)
