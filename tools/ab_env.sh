@@ -4,7 +4,7 @@
 # each argument: a variant name (variants/libasvrl_<name>.so, "default" = in-tree) then VAR=VALUE pairs.
 set -e
 ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
-ARGS="--steps 300 --warmup 30 --no-cpu-baseline --iqn-steps ${IQN_STEPS:-0} --rainbow-steps 0"
+ARGS="--steps 300 --warmup 30 --no-cpu-baseline --iqn-steps ${IQN_STEPS:-0} --rainbow-steps 0 --config5-steps 0 --plateau-envs 0"
 SPECS=("$@")
 for rep in 1 2; do
   for spec in "${SPECS[@]}"; do

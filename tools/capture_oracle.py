@@ -19,6 +19,8 @@ Fixture families:
   learn_iqn.npz     F5  Agent.train_IQN (agent.py:434-476)
   learn_rainbow.npz F6  Agent.train_Rainbow incl. the C51 projection target m
                         (agent.py:597-641)
+  learn_dqn.npz     F8  Agent.train_DQN / act_dqn (agent.py:518-545, 271-287)
+  eval_ref.npz      F9  Trainer.evaluation (trainer.py:266-392), AC-IQN and Rainbow
 """
 import os
 import sys
@@ -822,6 +824,43 @@ def capture_dqn():
     out["act/q"] = np.asarray(q)
     np.savez_compressed(os.path.join(OUT, "learn_dqn.npz"), **out)
     print("dqn keys:", len(out))
+
+
+EVAL_SCHEDULE = {"num_episodes": [2, 2], "num_robots": [3, 5], "num_cores": [0, 2], "num_obstacles": [2, 4],
+                 "min_start_goal_dis": [30.0, 40.0]}
+
+
+def capture_eval():
+    """F9: Trainer.evaluation (trainer.py:266-392) with the seeded initial AC-IQN and Rainbow agents
+    (greedy, batch-1 CPU policy per robot) on the eval configs of EVAL_SCHEDULE: the configs, the
+    network weights and every per-config metric, per-robot trajectory and action history."""
+    import json
+    import random
+    from rfarl.policy.trainer import Trainer
+    out = {}
+    for kind in ("AC-IQN", "Rainbow"):
+        torch.manual_seed(0)
+        agent = ref_agent_mod.Agent(device="cpu", seed=100, agent_type=kind)
+        tr = Trainer(MarineNavEnv3(seed=1), MarineNavEnv3(seed=253, is_eval_env=True), EVAL_SCHEDULE, agent)
+        random.seed(77)
+        np.random.seed(77)
+        tr.evaluation()
+        p = kind + "/"
+        out[p + "configs"] = np.array(json.dumps(tr.eval_config))
+        net = agent.policy_local.actor if kind == "AC-IQN" else agent.policy_local
+        out.update(sd_arrays(p + "net/", net))
+        out[p + "rewards"] = np.array(tr.eval_rewards[0], dtype=np.float64)
+        out[p + "successes"] = np.array(tr.eval_successes[0], dtype=bool)
+        out[p + "times"] = np.array(tr.eval_times[0], dtype=np.float64)
+        out[p + "energies"] = np.array(tr.eval_energies[0], dtype=np.float64)
+        for e, ep in enumerate(tr.eval_trajectories[0]):
+            for i, traj in enumerate(ep):
+                out[f"{p}traj/{e}/{i}"] = np.array(traj, dtype=np.float64)
+                out[f"{p}act/{e}/{i}"] = np.array(tr.eval_actions[0][e][i], dtype=np.float64)
+        print(kind, "eval lengths", [[len(t) for t in ep] for ep in tr.eval_trajectories[0]],
+              "successes", tr.eval_successes[0])
+    np.savez_compressed(os.path.join(OUT, "eval_ref.npz"), **out)
+    print("eval keys:", len(out))
 
 
 if __name__ == "__main__":
