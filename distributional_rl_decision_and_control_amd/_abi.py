@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("ASVRL_LIB", os.path.join(HERE, "lib", "libasvrl.so"))
 # the same sources built with f32 learner operands (the parity build; asvrl_operand_bytes() == 4)
 LIB_PATH_F32 = os.path.join(HERE, "lib", "libasvrl_f32.so")
 OPERANDS = {"bf16": (LIB_PATH, 2), "f32": (LIB_PATH_F32, 4)}
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
 OBS_DIM = 40   # self 7 | objects 25 | mask 5 | pad 3
@@ -199,6 +199,26 @@ class AsvRainbowHeadIO(C.Structure):
                 ("da", _VP), ("grad_scale", C.c_float), ("_pad1", _I32)]
 
 
+
+class AsvRainbowSrc(C.Structure):
+    _fields_ = [(n, _VP) for n in ("self_w", "self_b", "obj_w", "obj_b", "w_v1", "b_v1", "w_a1", "b_a1", "w_v2", "b_v2",
+                                   "w_a2", "b_a2", "w_vo", "b_vo", "w_ao", "b_ao")]
+
+
+RAINBOW_IMG_FIELDS = ("enc", "v1", "a1", "v2", "a2", "vo", "mo", "ao")
+RAINBOW_BIAS_FIELDS = ("b_enc", "b_v1p", "b_a1p", "b_v2p", "b_a2p", "b_vop", "b_mop", "b_aop")
+
+
+class AsvRainbowImg(C.Structure):   # also AsvRainbowImgOut (same layout)
+    _fields_ = [(n, _VP) for n in RAINBOW_IMG_FIELDS + RAINBOW_BIAS_FIELDS]
+
+
+class AsvRainbowNetIO(C.Structure):
+    _fields_ = [("x", _VP), ("ldx", _I64), ("N", _I32), ("_pad0", _I32), ("support", _VP), ("act_out", _VP),
+                ("ld_act", _I64), ("act_idx", _VP), ("step_dev", _VP), ("eps_steps_per_count", _D), ("eps_total", _D),
+                ("eps_fraction", _D), ("eps_initial", _D), ("eps_final", _D), ("seed", _U64), ("p_out", _VP)]
+
+
 EXPORTS = [
     ("asvrl_env_step", C.c_int, [C.POINTER(AsvParams), C.POINTER(AsvEnvState), _VP, _VP, C.POINTER(AsvStepCtl),
                                  C.POINTER(AsvStepOut), _VP]),
@@ -231,6 +251,10 @@ EXPORTS = [
     ("asvrl_rainbow_act", C.c_int, [C.POINTER(AsvRainbowHeadIO), _VP]),
     ("asvrl_rainbow_pick", C.c_int, [C.POINTER(AsvRainbowHeadIO), _VP]),
     ("asvrl_rainbow_loss", C.c_int, [C.POINTER(AsvRainbowHeadIO), _VP]),
+    ("asvrl_rainbow_pack", C.c_int, [C.POINTER(AsvRainbowSrc), C.POINTER(AsvRainbowImg), _VP]),
+    ("asvrl_rainbow_net_act", C.c_int, [C.POINTER(AsvRainbowImg), C.POINTER(AsvRainbowNetIO), _VP]),
+    ("asvrl_rainbow_net_argmax", C.c_int, [C.POINTER(AsvRainbowImg), C.POINTER(AsvRainbowNetIO), _VP]),
+    ("asvrl_rainbow_net_pick", C.c_int, [C.POINTER(AsvRainbowImg), C.POINTER(AsvRainbowNetIO), _VP]),
     ("asvrl_adam_clip", C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, _F, _F, _VP, _VP, _VP]),
     ("asvrl_linear_wgrad_workspace", _I64, [_I32, _I32]),
     ("asvrl_critic_wout_groups", _I32, [_I32, _I32]),

@@ -1,20 +1,25 @@
-"""Rainbow (dueling NoisyNet C51) act and train_Rainbow with the head and the noisy weights on
-gfx950 kernels (asvrl_rainbow.hip); the layer GEMMs stay hipBLASLt GEMMs through torch.
+"""Rainbow (dueling NoisyNet C51) act and train_Rainbow on gfx950 kernels: the whole network + head
+of act and of the two s_{t+n} passes as one kernel per 32-row tile (asvrl_rainbow_net.hip), the noisy
+weights and the loss head in asvrl_rainbow.hip; the training pass's GEMMs (forward with grad and
+backward) stay hipBLASLt GEMMs through torch (fp32).
 
 Per learn step (agent.py:597-641), on PER rows [B][88] (obs | n-th next obs | action | R | nonterminal |
 weight):
-  online W = mu + sigma * eps, composed once per iteration     asvrl_noisy_compose (in act)
-  logits v, a of s (with grad) and of s_{t+n}                    torch GEMMs (fp32)
-  double-Q argmax over s_{t+n} with the online head              asvrl_rainbow_act (no exploration)
-  target reset_noise() + compose                                 asvrl_noisy_reset (one launch)
-  target logits of s_{t+n}, p(s_{t+n}, a*)                       torch GEMMs, asvrl_rainbow_pick
+  online W = mu + sigma * eps, composed + packed once per iteration
+                                                                 asvrl_noisy_compose, asvrl_rainbow_pack (in act)
+  double-Q argmax over s_{t+n} with the online net               asvrl_rainbow_net_argmax (one launch)
+  target reset_noise() + compose, packed                         asvrl_noisy_reset, asvrl_rainbow_pack
+  p(s_{t+n}, a*) of the target net                               asvrl_rainbow_net_pick (one launch)
+  logits v, a of s (with grad)                                   torch GEMMs (fp32)
   projection m                                                   asvrl_c51_project (bit-exact)
   per-sample loss and d mean(w loss) / d(v, a)                   asvrl_rainbow_loss
   backward through the GEMMs                                     torch.autograd.backward([v, a], [dv, da])
   dmu = dW, dsigma = dW * eps                                    asvrl_noisy_compose(backward)
   clip + Adam                                                    asvrl_adam_clip
-Act (agent.py:308-324) on every robot: the same composed online weights, logits, asvrl_rainbow_act
-with epsilon-greedy on the device step counter.
+Act (agent.py:308-324) on every robot: the same composed online weights, asvrl_rainbow_net_act
+(network, head, epsilon-greedy on the device step counter) in one launch.
+operands: the network kernel's MFMA operands, "bf16" (the training path) or "f32" (libasvrl_f32.so,
+the parity build).
 
 The online net's noise is never resampled during training, as in the reference (its reset_noise is
 only called on the target, agent.py:610). The target noise comes from Philox instead of torch.randn.
@@ -159,13 +164,67 @@ def _split(rows):
     return rows[:, 0:7], rows[:, 7:32].reshape(M, 5, 5), rows[:, 32:37]
 
 
+IMG_SIZES = {"enc": 256 * 32, "v1": 128 * 256, "a1": 128 * 256, "v2": 128 * 128, "a2": 128 * 128, "vo": 64 * 128,
+             "mo": 64 * 128, "ao": 25 * 64 * 128}
+BIAS_SIZES = {"b_enc": 256, "b_v1p": 128, "b_a1p": 128, "b_v2p": 128, "b_a2p": 128, "b_vop": 64, "b_mop": 64,
+              "b_aop": 25 * 64}
+
+
+class RainbowNetImage:
+    """Fragment images of one Rainbow_Policy for asvrl_rainbow_net_*: the encoders and the composed noisy
+    layers of `noisy` (a NoisyPack of the same net), packed by refresh() (asvrl_rainbow_pack)."""
+
+    def __init__(self, net, noisy, operands="bf16"):
+        self.L = _abi.lib(operands)
+        dev = noisy.flat.device
+        self.img = torch.zeros(sum(IMG_SIZES.values()), dtype=_abi.operand_dtype(operands), device=dev)
+        self.bias = torch.zeros(sum(BIAS_SIZES.values()), dtype=torch.float32, device=dev)
+        st = _abi.AsvRainbowImg()
+        off = 0
+        for n, k in IMG_SIZES.items():
+            setattr(st, n, self.img[off:off + k].data_ptr())
+            off += k
+        off = 0
+        for n, k in BIAS_SIZES.items():
+            setattr(st, n, self.bias[off:off + k].data_ptr())
+            off += k
+        self.struct = st
+        W, _ = noisy.weights()
+        se, oe = net.self_encoder[0], net.object_encoder[0]
+        src = _abi.AsvRainbowSrc()
+        src.self_w, src.self_b, src.obj_w, src.obj_b = (t.data_ptr() for t in (se.weight, se.bias, oe.weight, oe.bias))
+        for key, name in (("v1", "hidden_layer_v"), ("a1", "hidden_layer_a"), ("v2", "hidden_layer_v_2"),
+                          ("a2", "hidden_layer_a_2"), ("vo", "output_layer_v"), ("ao", "output_layer_a")):
+            setattr(src, "w_" + key, W[name][0].data_ptr())
+            setattr(src, "b_" + key, W[name][1].data_ptr())
+        self.src = src
+
+    def refresh(self, stream=None):
+        _abi.check(self.L.asvrl_rainbow_pack(C.byref(self.src), C.byref(self.struct), _abi.stream_ptr(stream)),
+                   "asvrl_rainbow_pack", self.L)
+
+    def io(self, x, support, **kw):
+        assert x.dtype == torch.float32 and x.stride(-1) == 1
+        io = _abi.AsvRainbowNetIO()
+        io.x, io.ldx, io.N = x.data_ptr(), x.stride(0), x.shape[0]
+        io.support = support.data_ptr()
+        for k, v in kw.items():
+            setattr(io, k, v)
+        return io
+
+    def run(self, fn, io, stream=None):
+        _abi.check(getattr(self.L, fn)(C.byref(self.struct), C.byref(io), _abi.stream_ptr(stream)), fn, self.L)
+
+
 class FusedRainbow:
     """Packs and buffers (pointer-stable for graph replay) of the batched Rainbow path."""
 
-    def __init__(self, local, target, B, support):
+    def __init__(self, local, target, B, support, operands="bf16"):
         self.local, self.target, self.B = local, target, B
         self.pack = NoisyPack(local)
         self.tpack = NoisyPack(target)
+        self.img = RainbowNetImage(local, self.pack, operands)
+        self.timg = RainbowNetImage(target, self.tpack, operands)
         dev = support.device
         self.support = support.float().contiguous()
         f = dict(dtype=torch.float32, device=dev)
@@ -176,9 +235,12 @@ class FusedRainbow:
         self.da = torch.zeros(B, ATOMS * ACTIONS, **f)
         self.pack.compose()
         self.tpack.compose()
+        self.img.refresh()
+        self.timg.refresh()
 
     def target_changed(self):
         self.tpack.compose()
+        self.timg.refresh()
 
     def _head(self, v, a, **kw):
         io = _abi.AsvRainbowHeadIO()
@@ -193,13 +255,12 @@ class FusedRainbow:
     def act(self, obs_rows, actions64, step_dev, steps_per_count, total, fraction, initial, final, seed):
         """act_rainbow for every row (training mode: noisy online weights), epsilon-greedy."""
         self.pack.compose()
-        W, _ = self.pack.weights()
-        v, a = logits(self.local, _split(obs_rows), W)
-        io = self._head(v, a, act_out=actions64.data_ptr(), ld_act=actions64.stride(0), step_dev=step_dev.data_ptr(),
-                        eps_steps_per_count=float(steps_per_count), eps_total=float(total),
-                        eps_fraction=float(fraction), eps_initial=float(initial), eps_final=float(final),
-                        seed=int(seed) & 0xFFFFFFFFFFFFFFFF)
-        _abi.check(_abi.lib().asvrl_rainbow_act(C.byref(io), _abi.stream_ptr()), "asvrl_rainbow_act")
+        self.img.refresh()
+        io = self.img.io(obs_rows, self.support, act_out=actions64.data_ptr(), ld_act=actions64.stride(0),
+                         step_dev=step_dev.data_ptr(), eps_steps_per_count=float(steps_per_count),
+                         eps_total=float(total), eps_fraction=float(fraction), eps_initial=float(initial),
+                         eps_final=float(final), seed=int(seed) & 0xFFFFFFFFFFFFFFFF)
+        self.img.run("asvrl_rainbow_net_act", io)
 
     def update(self, opt, grads, rows, gamma=0.99, n=3, vmin=-1.0, vmax=1.0, sync=None, max_norm=0.5, seed=0,
                counter_dev=None, compose=True):
@@ -209,19 +270,19 @@ class FusedRainbow:
         B = rows.shape[0]
         if compose:
             self.pack.compose()
+            self.img.refresh()
         W, leaves = self.pack.weights(detach_grad=True)
         grads.zero_()
+        ns_rows = rows[:, 40:80]
+        # double-Q argmax over s_{t+n} with the online net, then p(s_{t+n}, a*) of the target net with
+        # fresh target noise (agent.py:605-612)
+        self.img.run("asvrl_rainbow_net_argmax", self.img.io(ns_rows, self.support, act_idx=self.a_star.data_ptr()))
+        self.tpack.reset(seed, counter_dev)
+        self.timg.refresh()
+        self.timg.run("asvrl_rainbow_net_pick", self.timg.io(ns_rows, self.support, act_idx=self.a_star.data_ptr(),
+                                                               p_out=self.p_star.data_ptr()))
         v, a = logits(self.local, _split(rows[:, 0:40]), W)
         with torch.no_grad():
-            Wn, _ = self.pack.weights()
-            vn, an = logits(self.local, _split(rows[:, 40:80]), Wn)
-            io = self._head(vn, an, act_idx=self.a_star.data_ptr())
-            _abi.check(_abi.lib().asvrl_rainbow_act(C.byref(io), _abi.stream_ptr()), "asvrl_rainbow_act")
-            self.tpack.reset(seed, counter_dev)
-            Wt, _ = self.tpack.weights()
-            vt, at = logits(self.target, _split(rows[:, 40:80]), Wt)
-            io = self._head(vt, at, act_idx=self.a_star.data_ptr(), p_out=self.p_star.data_ptr())
-            _abi.check(_abi.lib().asvrl_rainbow_pick(C.byref(io), _abi.stream_ptr()), "asvrl_rainbow_pick")
             m = c51_project(self.p_star, rows[:, 82], rows[:, 83], self.support, vmin, vmax, gamma ** n)
             io = self._head(v.detach(), a.detach(), actions=rows.data_ptr() + 80 * 4, weights=rows.data_ptr() + 84 * 4,
                             ld_rd=rows.stride(0), m=m.data_ptr(), loss=self.loss.data_ptr(), dv=self.dv.data_ptr(),

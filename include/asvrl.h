@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 13
+#define ASVRL_ABI_VERSION 14
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -545,6 +545,51 @@ int asvrl_rainbow_pick(const AsvRainbowHeadIO* io, void* stream);
 /* loss_b = -sum m log softmax(q[a_b]) (agent.py:633) and the gradients of grad_scale * sum_b w_b loss_b
  * with respect to v and a. One wave per row. */
 int asvrl_rainbow_loss(const AsvRainbowHeadIO* io, void* stream);
+
+/* Rainbow_Policy (Rainbow_model.py:56-139) as one kernel per 32-row tile: encoders, both streams, the
+ * dueling combine and the C51 head, bf16 MFMA operands (f32 in libasvrl_f32.so). The weights are
+ * fragment images packed from the COMPOSED NoisyLinear weights (asvrl_noisy_compose / _reset, then
+ * asvrl_rainbow_pack), including the action-mean of output_layer_a (mean_k a[k] as one more layer). */
+typedef struct AsvRainbowSrc {   /* f32 row-major [out][in] */
+  const float *self_w, *self_b, *obj_w, *obj_b;            /* self_encoder.0 (56 x 7), object_encoder.0 (40 x 5) */
+  const float *w_v1, *b_v1, *w_a1, *b_a1;                  /* hidden_layer_v / _a (128 x 256), composed */
+  const float *w_v2, *b_v2, *w_a2, *b_a2;                  /* hidden_layer_v_2 / _a_2 (128 x 128) */
+  const float *w_vo, *b_vo, *w_ao, *b_ao;                  /* output_layer_v (51 x 128), output_layer_a (1275 x 128) */
+} AsvRainbowSrc;
+
+/* The packed images (operand element type; biases f32). Sizes in elements: enc 8192, v1 / a1 32768,
+ * v2 / a2 16384, vo / mo 8192, ao 204800; b_enc 256, b_v1p .. b_a2p 128, b_vop / b_mop 64, b_aop 1600. */
+typedef struct AsvRainbowImgOut {
+  void *enc, *v1, *a1, *v2, *a2, *vo, *mo, *ao;
+  float *b_enc, *b_v1p, *b_a1p, *b_v2p, *b_a2p, *b_vop, *b_mop, *b_aop;
+} AsvRainbowImgOut;
+typedef struct AsvRainbowImg {   /* the same buffers, read-only */
+  const void *enc, *v1, *a1, *v2, *a2, *vo, *mo, *ao;
+  const float *b_enc, *b_v1p, *b_a1p, *b_v2p, *b_a2p, *b_vop, *b_mop, *b_aop;
+} AsvRainbowImg;
+
+typedef struct AsvRainbowNetIO {
+  const float* x;           /* [N] packed observation rows at x[row * ldx] (16-byte aligned, ldx >= 40) */
+  int64_t ldx;
+  int32_t N, _pad0;
+  const float* support;     /* [51] */
+  double* act_out;          /* act: [N] action as f64 at act_out[row * ld_act] */
+  int64_t ld_act;
+  int64_t* act_idx;         /* argmax: [N] greedy action out; pick: a* in; act: optional greedy out */
+  const int64_t* step_dev;  /* act: epsilon schedule on the device step counter (NULL: greedy) */
+  double eps_steps_per_count, eps_total, eps_fraction, eps_initial, eps_final;
+  uint64_t seed;
+  float* p_out;             /* pick: [N][51] softmax(q[a*]) */
+} AsvRainbowNetIO;
+
+/* Pack the encoders and composed noisy layers into AsvRainbowImgOut (one launch). */
+int asvrl_rainbow_pack(const AsvRainbowSrc* src, const AsvRainbowImgOut* img, void* stream);
+/* act_rainbow (agent.py:308-324) for every row: argmax_k sum softmax(q[k]) z, epsilon-greedy. */
+int asvrl_rainbow_net_act(const AsvRainbowImg* w, const AsvRainbowNetIO* io, void* stream);
+/* The double-Q argmax of train_Rainbow (agent.py:605-609): act_idx[row] = argmax_k Q[k]. */
+int asvrl_rainbow_net_argmax(const AsvRainbowImg* w, const AsvRainbowNetIO* io, void* stream);
+/* p(s', a*) of the target net (agent.py:610-612): p_out[row] = softmax(q[act_idx[row]]). */
+int asvrl_rainbow_net_pick(const AsvRainbowImg* w, const AsvRainbowNetIO* io, void* stream);
 
 /* ---------------------------------------------------------------- optimiser (agent.py) */
 
