@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("ASVRL_LIB", os.path.join(HERE, "lib", "libasvrl.so"))
 # the same sources built with f32 learner operands (the parity build; asvrl_operand_bytes() == 4)
 LIB_PATH_F32 = os.path.join(HERE, "lib", "libasvrl_f32.so")
 OPERANDS = {"bf16": (LIB_PATH, 2), "f32": (LIB_PATH_F32, 4)}
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
 OBS_DIM = 40   # self 7 | objects 25 | mask 5 | pad 3
@@ -127,13 +127,13 @@ class AsvIqnIO(C.Structure):
                 ("eps_initial", _D), ("eps_final", _D), ("seed", _U64)]
 
 
-MAX_SUM_SEGS = 8
+MAX_SUM_SEGS = 24
 
 
 SUM_PLAIN, SUM_FOLD_ENCODERS = 0, 1
 
 
-MAX_WGRAD_SEGS = 8
+MAX_WGRAD_SEGS = 24
 MAX_PACK_SEGS = 8
 
 
@@ -207,16 +207,20 @@ class AsvRainbowSrc(C.Structure):
 
 RAINBOW_IMG_FIELDS = ("enc", "v1", "a1", "v2", "a2", "vo", "mo", "ao")
 RAINBOW_BIAS_FIELDS = ("b_enc", "b_v1p", "b_a1p", "b_v2p", "b_a2p", "b_vop", "b_mop", "b_aop")
+RAINBOW_IMGT_FIELDS = ("vot", "mot", "aot", "v2t", "a2t", "v1t", "a1t")
 
 
 class AsvRainbowImg(C.Structure):   # also AsvRainbowImgOut (same layout)
-    _fields_ = [(n, _VP) for n in RAINBOW_IMG_FIELDS + RAINBOW_BIAS_FIELDS]
+    _fields_ = [(n, _VP) for n in RAINBOW_IMG_FIELDS + RAINBOW_BIAS_FIELDS + RAINBOW_IMGT_FIELDS]
 
 
 class AsvRainbowNetIO(C.Structure):
     _fields_ = [("x", _VP), ("ldx", _I64), ("N", _I32), ("_pad0", _I32), ("support", _VP), ("act_out", _VP),
                 ("ld_act", _I64), ("act_idx", _VP), ("step_dev", _VP), ("eps_steps_per_count", _D), ("eps_total", _D),
-                ("eps_fraction", _D), ("eps_initial", _D), ("eps_final", _D), ("seed", _U64), ("p_out", _VP)]
+                ("eps_fraction", _D), ("eps_initial", _D), ("eps_final", _D), ("seed", _U64), ("p_out", _VP),
+                ("actions", _VP), ("weights", _VP), ("ld_rd", _I64), ("m", _VP), ("grad_scale", _F), ("_pad1", _I32),
+                ("loss", _VP)] + [(n, _VP) for n in ("xb", "f", "hv1", "ha1", "hv2", "ha2", "dzv", "dza", "dz2v",
+                                                     "dz2a", "dz1v", "dz1a", "dzf")]
 
 
 EXPORTS = [
@@ -255,6 +259,7 @@ EXPORTS = [
     ("asvrl_rainbow_net_act", C.c_int, [C.POINTER(AsvRainbowImg), C.POINTER(AsvRainbowNetIO), _VP]),
     ("asvrl_rainbow_net_argmax", C.c_int, [C.POINTER(AsvRainbowImg), C.POINTER(AsvRainbowNetIO), _VP]),
     ("asvrl_rainbow_net_pick", C.c_int, [C.POINTER(AsvRainbowImg), C.POINTER(AsvRainbowNetIO), _VP]),
+    ("asvrl_rainbow_net_train", C.c_int, [C.POINTER(AsvRainbowImg), C.POINTER(AsvRainbowNetIO), _VP]),
     ("asvrl_adam_clip", C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, _F, _F, _VP, _VP, _VP]),
     ("asvrl_linear_wgrad_workspace", _I64, [_I32, _I32]),
     ("asvrl_critic_wout_groups", _I32, [_I32, _I32]),

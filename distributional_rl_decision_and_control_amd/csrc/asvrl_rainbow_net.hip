@@ -45,8 +45,182 @@ struct RbLds {
 };
 static_assert(2 * 32 * kHid * sizeof(elem_t) >= 2 * 32 * kAP * sizeof(float), "v / mean logits fit over h1");
 
+// The training pass keeps every activation image until its mask has been taken (the masks then live
+// in registers): f, later dz2 | h1, later dz1 | h2 | v, mean logits, later the dq image + dq (f32).
+struct RbTrainLds {
+  elem_t x0[32 * kEnc];
+  elem_t h1[2][32 * kHid];
+  elem_t h2[2][32 * kHid];
+  float vm[2][32 * kAP];
+  float z[kAP];
+  int act[32];
+};
+static_assert(2 * 32 * kAP * sizeof(float) >= 32 * kAP * (sizeof(elem_t) + sizeof(float)), "dq images fit over vm");
+
 // object index of encoder feature m (>= 56)
 __device__ __forceinline__ int obj_of(int m) { return (m - kSelfF) / kObjF; }
+
+// natural atom index of register g of block b in lane half h
+__device__ __forceinline__ int atom_of(int b, int g, int h) { return b * 32 + (g & 3) + 8 * (g >> 2) + 4 * h; }
+
+// ---------------- forward phases (wave w of 4), shared by the inference and training kernels. SAVE:
+// also the activations to HBM (store16: all 64 lanes call it; dst nullptr for rows past N) and the
+// lane's ReLU masks (bit 8 s + i of a block = register 8 s + i positive).
+
+// encoders -> f (wave w: blocks 2w, 2w + 1) into x0
+template <bool SAVE>
+__device__ __forceinline__ void phase_encode(const AsvRainbowImg& W, const float* xr, elem_t* x0, int w, int lane,
+                                             elem_t* f_row, uint32_t& fmask) {
+  const int h = lane >> 5, r = lane & 31;
+  frag8 bx[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const f32x4 u = *reinterpret_cast<const f32x4*>(xr + ks * 16 + 8 * h);
+    const f32x4 v = *reinterpret_cast<const f32x4*>(xr + ks * 16 + 8 * h + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bx[ks][j] = (elem_t)u[j];
+      bx[ks][4 + j] = (elem_t)v[j];
+    }
+  }
+  float mk[kObjN];
+#pragma unroll
+  for (int o = 0; o < kObjN; ++o) mk[o] = xr[32 + o];
+  const frag8* ENC = reinterpret_cast<const frag8*>(W.enc);
+  const RowA<kEnc> RA(r, h);
+  fmask = 0;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int mb = 2 * w + q;
+    f32x16 acc = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) acc = mfma(ENC[(mb * 2 + ks) * 64 + lane], bx[ks], acc);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      frag8 o;
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = feat(mb, 8 * s + i, h);
+        const int ob = m < kSelfF ? -1 : obj_of(m);   // select chain: no dynamic register index
+        const float mo = ob == 0 ? mk[0] : ob == 1 ? mk[1] : ob == 2 ? mk[2] : ob == 3 ? mk[3] : mk[4];
+        const float keep = ob < 0 ? 1.f : (mo < 0.5f ? 0.f : 1.f);   // masked_fill(mask < 0.5, 0)
+        v[i] = relu(acc[8 * s + i] + W.b_enc[m]) * keep;
+        o[i] = (elem_t)v[i];
+        if (SAVE && v[i] > 0.f) fmask |= 1u << (16 * q + 8 * s + i);
+      }
+      rows(x0, RA, 0, 2 * mb + s, o);
+      if constexpr (SAVE) store16(f_row != nullptr ? f_row + mb * 32 + 16 * s : nullptr, v, h);
+    }
+  }
+}
+
+// one hidden layer pair (value, advantage streams; wave w: block w of each): out = relu(W in + b)
+template <int K, bool SAVE>
+__device__ __forceinline__ void phase_hidden(const void* wv, const void* wa, const float* bv, const float* ba,
+                                             const elem_t* inv, const elem_t* ina, elem_t* outv, elem_t* outa, int w,
+                                             int lane, elem_t* sv_row, elem_t* sa_row, uint32_t& mask) {
+  const int h = lane >> 5, r = lane & 31;
+  const frag8* V = reinterpret_cast<const frag8*>(wv);
+  const frag8* A = reinterpret_cast<const frag8*>(wa);
+  const RowA<K> RX(r, h);
+  const RowA<kHid> RH(r, h);
+  f32x16 av = acc_init(bv, w * 32, h), aa = acc_init(ba, w * 32, h);
+#pragma unroll
+  for (int ks = 0; ks < K / 16; ++ks) {
+    const frag8 b0 = rowf(inv, RX, 0, ks);
+    av = mfma(V[(w * (K / 16) + ks) * 64 + lane], b0, av);
+    const frag8 b1 = inv == ina ? b0 : rowf(ina, RX, 0, ks);
+    aa = mfma(A[(w * (K / 16) + ks) * 64 + lane], b1, aa);
+  }
+  if constexpr (!kBiasFirst) {
+    av += bias_init(bv, w * 32, h);
+    aa += bias_init(ba, w * 32, h);
+  }
+  mask = 0;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    frag8 ov, oa;
+    float fv[8], fa[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      fv[i] = relu(av[8 * s + i]);
+      fa[i] = relu(aa[8 * s + i]);
+      ov[i] = (elem_t)fv[i];
+      oa[i] = (elem_t)fa[i];
+      if (SAVE) mask |= (fv[i] > 0.f ? 1u : 0u) << (8 * s + i) | (fa[i] > 0.f ? 1u : 0u) << (16 + 8 * s + i);
+    }
+    rows(outv, RH, 0, 2 * w + s, ov);
+    rows(outa, RH, 0, 2 * w + s, oa);
+    if constexpr (SAVE) {
+      store16(sv_row != nullptr ? sv_row + w * 32 + 16 * s : nullptr, fv, h);
+      store16(sa_row != nullptr ? sa_row + w * 32 + 16 * s : nullptr, fa, h);
+    }
+  }
+}
+
+// v (waves 0, 1: atom blocks 0, 1) and the action-mean logits (waves 2, 3) -> f32 [32][64], natural order
+__device__ __forceinline__ void phase_vm(const AsvRainbowImg& W, const elem_t* hv2, const elem_t* ha2, float* vl,
+                                         float* ml, int w, int lane) {
+  const int h = lane >> 5, r = lane & 31;
+  const bool val = w < 2;
+  const int blk = w & 1;
+  const frag8* M = reinterpret_cast<const frag8*>(val ? W.vo : W.mo);
+  const float* bias = val ? W.b_vop : W.b_mop;
+  const elem_t* src = val ? hv2 : ha2;
+  const RowA<kHid> RH(r, h);
+  f32x16 acc = acc_init(bias, blk * 32, h);
+#pragma unroll
+  for (int ks = 0; ks < kHid / 16; ++ks) acc = mfma(M[(blk * 8 + ks) * 64 + lane], rowf(src, RH, 0, ks), acc);
+  if constexpr (!kBiasFirst) acc += bias_init(bias, blk * 32, h);
+  float* dst = (val ? vl : ml) + r * kAP + blk * 32;
+#pragma unroll
+  for (int g = 0; g < 16; g += 4) {   // registers g .. g + 3 hold atoms atom_of(0, g, h) .. + 3
+    const int m = atom_of(0, g, h);
+    *reinterpret_cast<f32x4*>(dst + m) = f32x4{acc[g], acc[g + 1], acc[g + 2], acc[g + 3]};
+  }
+}
+
+// base = v - mean and the support for this lane's atoms (block b, register g)
+__device__ __forceinline__ void load_base(const float* vl, const float* ml, const float* z, int r, int h,
+                                          float (&base)[2][16], float (&zz)[2][16]) {
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int g = 0; g < 16; g += 4) {
+      const int m = atom_of(b, g, h);
+      const f32x4 vv = *reinterpret_cast<const f32x4*>(vl + r * kAP + m);
+      const f32x4 mm = *reinterpret_cast<const f32x4*>(ml + r * kAP + m);
+      const f32x4 z4 = *reinterpret_cast<const f32x4*>(z + m);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        base[b][g + i] = vv[i] - mm[i];
+        zz[b][g + i] = z4[i];
+      }
+    }
+}
+
+// action k's 51 advantage logits (two 32-atom blocks) from the ha2 fragments
+__device__ __forceinline__ void action_logits(const AsvRainbowImg& W, const frag8 (&bh)[kHid / 16], int k, int lane,
+                                              f32x16 (&acc)[2]) {
+  const int h = lane >> 5;
+  const frag8* AO = reinterpret_cast<const frag8*>(W.ao);
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    acc[b] = acc_init(W.b_aop + k * kAP, b * 32, h);
+#pragma unroll
+    for (int ks = 0; ks < kHid / 16; ++ks) acc[b] = mfma(AO[((k * 2 + b) * 8 + ks) * 64 + lane], bh[ks], acc[b]);
+    if constexpr (!kBiasFirst) acc[b] += bias_init(W.b_aop + k * kAP, b * 32, h);
+  }
+}
+
+__device__ __forceinline__ float fexp(float x) {
+#if ASVRL_OPERAND_F32
+  return expf(x);
+#else
+  return __expf(x);
+#endif
+}
 
 template <int MODE>
 __global__ __launch_bounds__(kNW * 64) void rainbow_net_kernel(RbArgs a) {
@@ -58,178 +232,43 @@ __global__ __launch_bounds__(kNW * 64) void rainbow_net_kernel(RbArgs a) {
   const bool valid = row < io.N;
   const int64_t rr = valid ? row : io.N - 1;
   if (threadIdx.x < kAP) L.z[threadIdx.x] = threadIdx.x < kAtoms ? io.support[threadIdx.x] : 0.f;
-
-  // ---------------- encoders (wave w: features 64w .. 64w + 63) -> f in x0
-  {
-    const float* xr = io.x + rr * io.ldx;
-    frag8 bx[2];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const f32x4 u = *reinterpret_cast<const f32x4*>(xr + ks * 16 + 8 * h);
-      const f32x4 v = *reinterpret_cast<const f32x4*>(xr + ks * 16 + 8 * h + 4);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        bx[ks][j] = (elem_t)u[j];
-        bx[ks][4 + j] = (elem_t)v[j];
-      }
-    }
-    float mk[kObjN];
-#pragma unroll
-    for (int o = 0; o < kObjN; ++o) mk[o] = xr[32 + o];
-    const frag8* ENC = reinterpret_cast<const frag8*>(a.w.enc);
-    const RowA<kEnc> RA(r, h);
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int mb = 2 * w + q;
-      f32x16 acc = f32x16{};
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) acc = mfma(ENC[(mb * 2 + ks) * 64 + lane], bx[ks], acc);
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        frag8 o;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int m = feat(mb, 8 * s + i, h);
-          const int ob = m < kSelfF ? -1 : obj_of(m);   // select chain: no dynamic register index
-          const float mo = ob == 0 ? mk[0] : ob == 1 ? mk[1] : ob == 2 ? mk[2] : ob == 3 ? mk[3] : mk[4];
-          const float keep = ob < 0 ? 1.f : (mo < 0.5f ? 0.f : 1.f);   // masked_fill(mask < 0.5, 0)
-          o[i] = (elem_t)(relu(acc[8 * s + i] + a.w.b_enc[m]) * keep);
-        }
-        rows(L.x0, RA, 0, 2 * mb + s, o);
-      }
-    }
-  }
+  uint32_t unused = 0;
+  phase_encode<false>(a.w, io.x + rr * io.ldx, L.x0, w, lane, nullptr, unused);
   __syncthreads();
-
-  // ---------------- hv1, ha1 (wave w: block w of each)
-  {
-    const frag8* V1 = reinterpret_cast<const frag8*>(a.w.v1);
-    const frag8* A1 = reinterpret_cast<const frag8*>(a.w.a1);
-    const RowA<kEnc> RX(r, h);
-    const RowA<kHid> RH(r, h);
-    f32x16 av = acc_init(a.w.b_v1p, w * 32, h), aa = acc_init(a.w.b_a1p, w * 32, h);
-#pragma unroll
-    for (int ks = 0; ks < kEnc / 16; ++ks) {
-      const frag8 b = rowf(L.x0, RX, 0, ks);
-      av = mfma(V1[(w * 16 + ks) * 64 + lane], b, av);
-      aa = mfma(A1[(w * 16 + ks) * 64 + lane], b, aa);
-    }
-    if constexpr (!kBiasFirst) {
-      av += bias_init(a.w.b_v1p, w * 32, h);
-      aa += bias_init(a.w.b_a1p, w * 32, h);
-    }
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      frag8 ov, oa;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        ov[i] = (elem_t)relu(av[8 * s + i]);
-        oa[i] = (elem_t)relu(aa[8 * s + i]);
-      }
-      rows(L.h1[0], RH, 0, 2 * w + s, ov);
-      rows(L.h1[1], RH, 0, 2 * w + s, oa);
-    }
-  }
+  phase_hidden<kEnc, false>(a.w.v1, a.w.a1, a.w.b_v1p, a.w.b_a1p, L.x0, L.x0, L.h1[0], L.h1[1], w, lane, nullptr,
+                            nullptr, unused);
   __syncthreads();
-
-  // ---------------- hv2, ha2 into x0's space
-  elem_t* const hv2 = L.x0;
+  elem_t* const hv2 = L.x0;               // x0 is dead after the first hidden layers
   elem_t* const ha2 = L.x0 + 32 * kHid;
-  {
-    const frag8* V2 = reinterpret_cast<const frag8*>(a.w.v2);
-    const frag8* A2 = reinterpret_cast<const frag8*>(a.w.a2);
-    const RowA<kHid> RH(r, h);
-    f32x16 av = acc_init(a.w.b_v2p, w * 32, h), aa = acc_init(a.w.b_a2p, w * 32, h);
-#pragma unroll
-    for (int ks = 0; ks < kHid / 16; ++ks) {
-      av = mfma(V2[(w * 8 + ks) * 64 + lane], rowf(L.h1[0], RH, 0, ks), av);
-      aa = mfma(A2[(w * 8 + ks) * 64 + lane], rowf(L.h1[1], RH, 0, ks), aa);
-    }
-    if constexpr (!kBiasFirst) {
-      av += bias_init(a.w.b_v2p, w * 32, h);
-      aa += bias_init(a.w.b_a2p, w * 32, h);
-    }
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      frag8 ov, oa;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        ov[i] = (elem_t)relu(av[8 * s + i]);
-        oa[i] = (elem_t)relu(aa[8 * s + i]);
-      }
-      rows(hv2, RH, 0, 2 * w + s, ov);
-      rows(ha2, RH, 0, 2 * w + s, oa);
-    }
-  }
+  phase_hidden<kHid, false>(a.w.v2, a.w.a2, a.w.b_v2p, a.w.b_a2p, L.h1[0], L.h1[1], hv2, ha2, w, lane, nullptr,
+                            nullptr, unused);
   __syncthreads();
-
-  // ---------------- v (waves 0, 1: atom blocks 0, 1) and the action-mean logits (waves 2, 3), f32 in
-  // h1's space (last read by layer 2, behind the barrier), row-major [32][64] in natural atom order
-  float* const vl = reinterpret_cast<float*>(&L.h1[0][0]);
+  float* const vl = reinterpret_cast<float*>(&L.h1[0][0]);   // h1: last read by layer 2, behind the barrier
   float* const ml = vl + 32 * kAP;
-  {
-    const bool val = w < 2;
-    const int blk = w & 1;
-    const frag8* W = reinterpret_cast<const frag8*>(val ? a.w.vo : a.w.mo);
-    const float* bias = val ? a.w.b_vop : a.w.b_mop;
-    const elem_t* src = val ? hv2 : ha2;
-    const RowA<kHid> RH(r, h);
-    f32x16 acc = acc_init(bias, blk * 32, h);
-#pragma unroll
-    for (int ks = 0; ks < kHid / 16; ++ks) acc = mfma(W[(blk * 8 + ks) * 64 + lane], rowf(src, RH, 0, ks), acc);
-    if constexpr (!kBiasFirst) acc += bias_init(bias, blk * 32, h);
-    float* dst = (val ? vl : ml) + r * kAP + blk * 32;
-#pragma unroll
-    for (int g = 0; g < 16; g += 4) {   // positions 16 s + 8 h + i hold atoms feat(0, g, h) (natural order)
-      const int m = (g & 3) + 8 * (g >> 2) + 4 * h;
-      *reinterpret_cast<f32x4*>(dst + m) = f32x4{acc[g], acc[g + 1], acc[g + 2], acc[g + 3]};
-    }
-  }
+  phase_vm(a.w, hv2, ha2, vl, ml, w, lane);
   __syncthreads();
 
   // ---------------- the wave's actions: logits, softmax over atoms, expected value; argmax
   {
-    const frag8* AO = reinterpret_cast<const frag8*>(a.w.ao);
     const RowA<kHid> RH(r, h);
     frag8 bh[kHid / 16];
 #pragma unroll
     for (int ks = 0; ks < kHid / 16; ++ks) bh[ks] = rowf(ha2, RH, 0, ks);
-    // base = v - mean, and the support, for this lane's atoms: block b, register g
     float base[2][16], zz[2][16];
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int g = 0; g < 16; g += 4) {
-        const int m = b * 32 + (g & 3) + 8 * (g >> 2) + 4 * h;
-        const f32x4 vv = *reinterpret_cast<const f32x4*>(vl + r * kAP + m);
-        const f32x4 mm = *reinterpret_cast<const f32x4*>(ml + r * kAP + m);
-        const f32x4 z4 = *reinterpret_cast<const f32x4*>(L.z + m);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          base[b][g + i] = vv[i] - mm[i];
-          zz[b][g + i] = z4[i];
-        }
-      }
+    load_base(vl, ml, L.z, r, h, base, zz);
     int pick = -1;
     if constexpr (MODE == RB_PICK) pick = static_cast<int>(io.act_idx[rr]);
     float bq = -INFINITY;
     int bk = 1 << 20;
     for (int k = w; k < kActs; k += kNW) {
       f32x16 acc[2];
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        acc[b] = acc_init(a.w.b_aop + k * kAP, b * 32, h);
-#pragma unroll
-        for (int ks = 0; ks < kHid / 16; ++ks) acc[b] = mfma(AO[((k * 2 + b) * 8 + ks) * 64 + lane], bh[ks], acc[b]);
-        if constexpr (!kBiasFirst) acc[b] += bias_init(a.w.b_aop + k * kAP, b * 32, h);
-      }
+      action_logits(a.w, bh, k, lane, acc);
       float q[2][16], mx = -INFINITY;
 #pragma unroll
       for (int b = 0; b < 2; ++b)
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
-          const int m = b * 32 + (g & 3) + 8 * (g >> 2) + 4 * h;
-          q[b][g] = m < kAtoms ? acc[b][g] + base[b][g] : -INFINITY;
+          q[b][g] = atom_of(b, g, h) < kAtoms ? acc[b][g] + base[b][g] : -INFINITY;
           mx = fmaxf(mx, q[b][g]);
         }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
@@ -238,11 +277,7 @@ __global__ __launch_bounds__(kNW * 64) void rainbow_net_kernel(RbArgs a) {
       for (int b = 0; b < 2; ++b)
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
-#if ASVRL_OPERAND_F32
-          const float e = expf(q[b][g] - mx);
-#else
-          const float e = __expf(q[b][g] - mx);
-#endif
+          const float e = fexp(q[b][g] - mx);
           q[b][g] = e;
           se += e;
           sz += e * zz[b][g];
@@ -261,10 +296,8 @@ __global__ __launch_bounds__(kNW * 64) void rainbow_net_kernel(RbArgs a) {
 #pragma unroll
           for (int b = 0; b < 2; ++b)
 #pragma unroll
-            for (int g = 0; g < 16; ++g) {
-              const int m = b * 32 + (g & 3) + 8 * (g >> 2) + 4 * h;
-              if (m < kAtoms) po[m] = q[b][g] * inv;
-            }
+            for (int g = 0; g < 16; ++g)
+              if (atom_of(b, g, h) < kAtoms) po[atom_of(b, g, h)] = q[b][g] * inv;
         }
       }
     }
@@ -312,6 +345,260 @@ __global__ __launch_bounds__(kNW * 64) void rainbow_net_kernel(RbArgs a) {
   }
 }
 
+// ---------------- train_Rainbow's training pass (agent.py:613-636) on the online net, rows = s.
+// Forward as above saving the weight-gradient inputs; the wave owning action a_b computes row b's
+// loss_b = -sum m log p (p = softmax(q[a_b])) and dq = grad_scale w_b (p sum(m) - m) (the gradient of
+// grad_scale sum_b w_b loss_b with respect to q[a_b]); q = v + a - mean_k a gives dv = dq and
+// da[k] = dq (1{k = a_b} - 1/25), so
+//   dh2v = Wvo^T dq,   dh2a = Wao[a_b]^T dq - mean_k(Wao[k])^T dq
+// (the first term as 25 MFMA passes over the action-masked dq image), then relu masks, W2^T, W1^T down
+// to the encoders' pre-activations.
+template <int K>
+__device__ __forceinline__ void phase_back(const void* wvt, const void* wat, const elem_t* dinv, const elem_t* dina,
+                                           int mb, int lane, f32x16& dv, f32x16& da) {
+  const int h = lane >> 5, r = lane & 31;
+  const frag8* VT = reinterpret_cast<const frag8*>(wvt);
+  const frag8* AT = reinterpret_cast<const frag8*>(wat);
+  const RowA<K> RD(r, h);
+  dv = f32x16{};
+  da = f32x16{};
+#pragma unroll
+  for (int ks = 0; ks < K / 16; ++ks) {
+    dv = mfma(VT[(mb * (K / 16) + ks) * 64 + lane], rowf(dinv, RD, 0, ks), dv);
+    da = mfma(AT[(mb * (K / 16) + ks) * 64 + lane], rowf(dina, RD, 0, ks), da);
+  }
+}
+
+__global__ __launch_bounds__(kNW * 64) void rainbow_train_kernel(RbArgs a) {
+  __shared__ __attribute__((aligned(16))) RbTrainLds L;
+  const AsvRainbowNetIO& io = a.io;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
+  const int row0 = blockIdx.x * 32;
+  const int row = row0 + r;
+  const bool valid = row < io.N;
+  const int64_t rr = valid ? row : io.N - 1;
+  if (threadIdx.x < kAP) L.z[threadIdx.x] = threadIdx.x < kAtoms ? io.support[threadIdx.x] : 0.f;
+  if (threadIdx.x < 32) {
+    const int k = static_cast<int>(io.actions[(row0 + threadIdx.x < io.N ? row0 + threadIdx.x : io.N - 1) * io.ld_rd]);
+    L.act[threadIdx.x] = k < 0 ? 0 : (k >= kActs ? kActs - 1 : k);
+  }
+  auto orow = [&](void* base, int width) -> elem_t* {
+    return valid ? bp(base) + static_cast<int64_t>(row) * width : nullptr;
+  };
+  // ---------------- forward, saving f, hv1, ha1, hv2, ha2 (and xb) with the ReLU masks in registers
+  const float* xr = io.x + rr * io.ldx;
+  if (w == 0 && valid) {   // xb: obs columns 0 .. 31 in the operand type (the encoder fold's input)
+    elem_t* xo = bp(io.xb) + static_cast<int64_t>(row) * kObsK + 16 * h;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) xo[j] = (elem_t)xr[16 * h + j];
+  }
+  uint32_t fmask, m1, m2;
+  phase_encode<true>(a.w, xr, L.x0, w, lane, orow(io.f, kEnc), fmask);
+  __syncthreads();
+  phase_hidden<kEnc, true>(a.w.v1, a.w.a1, a.w.b_v1p, a.w.b_a1p, L.x0, L.x0, L.h1[0], L.h1[1], w, lane,
+                           orow(io.hv1, kHid), orow(io.ha1, kHid), m1);
+  __syncthreads();
+  phase_hidden<kHid, true>(a.w.v2, a.w.a2, a.w.b_v2p, a.w.b_a2p, L.h1[0], L.h1[1], L.h2[0], L.h2[1], w, lane,
+                           orow(io.hv2, kHid), orow(io.ha2, kHid), m2);
+  __syncthreads();
+  float* const vl = L.vm[0];
+  float* const ml = L.vm[1];
+  phase_vm(a.w, L.h2[0], L.h2[1], vl, ml, w, lane);
+  __syncthreads();
+
+  // ---------------- loss and dq of each row, by the wave owning its action
+  const int act_r = L.act[r];
+  {
+    const RowA<kHid> RH(r, h);
+    frag8 bh[kHid / 16];
+#pragma unroll
+    for (int ks = 0; ks < kHid / 16; ++ks) bh[ks] = rowf(L.h2[1], RH, 0, ks);
+    float base[2][16], zz[2][16];
+    load_base(vl, ml, L.z, r, h, base, zz);
+    float mv[2][16], wgt = 0.f;
+    {
+      const float* mr = io.m + rr * kAtoms;
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) mv[b][g] = atom_of(b, g, h) < kAtoms ? mr[atom_of(b, g, h)] : 0.f;
+      wgt = io.weights[rr * io.ld_rd];
+    }
+    float sm = 0.f;
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) sm += mv[b][g];
+    sm = half_sum(sm);
+    __syncthreads();   // every wave holds its base: vm becomes the dq images
+    elem_t* const dqi = reinterpret_cast<elem_t*>(L.vm[0]);   // [32][64] chained position order
+    float* const dqf = L.vm[1];                                // [32][64] natural order
+    const RowA<kAP> RQ(r, h);
+    for (int k = w; k < kActs; k += kNW) {
+      f32x16 acc[2];
+      action_logits(a.w, bh, k, lane, acc);
+      if (act_r != k) continue;   // lane-divergent from here: no cross-lane ops other than within the row pair
+      float q[2][16], mx = -INFINITY;
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          q[b][g] = atom_of(b, g, h) < kAtoms ? acc[b][g] + base[b][g] : -INFINITY;
+          mx = fmaxf(mx, q[b][g]);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      float se = 0.f;
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) se += fexp(q[b][g] - mx);
+      se = half_sum(se);
+      const float lse = mx + logf(se);
+      float l = 0.f;
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int g = 0; g < 16; ++g)
+          if (atom_of(b, g, h) < kAtoms) l -= mv[b][g] * (q[b][g] - lse);
+      l = half_sum(l);
+      if (valid && h == 0) io.loss[row] = l;
+      const float sc = valid ? wgt * io.grad_scale : 0.f;
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          frag8 o;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int g = 8 * s + i;
+            const bool on = atom_of(b, g, h) < kAtoms;
+            const float d = on ? (fexp(q[b][g] - lse) * sm - mv[b][g]) * sc : 0.f;
+            o[i] = (elem_t)d;
+            dqf[r * kAP + atom_of(b, g, h)] = d;
+          }
+          rows(dqi, RQ, 0, 2 * b + s, o);
+        }
+    }
+  }
+  __syncthreads();
+  const elem_t* const dqi = reinterpret_cast<const elem_t*>(L.vm[0]);
+  const float* const dqf = L.vm[1];
+
+  // ---------------- dZ of the output layers to HBM: dzv [N][64] = dq, dza [N][1280] = da (51 per action)
+  for (int c = threadIdx.x; c < 32 * (kAP / 8); c += kNW * 64) {
+    const int rw = c / (kAP / 8), ch = c % (kAP / 8);
+    if (row0 + rw >= io.N) continue;
+    frag8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (elem_t)dqf[rw * kAP + 8 * ch + i];
+    *reinterpret_cast<frag8*>(bp(io.dzv) + static_cast<int64_t>(row0 + rw) * kAP + 8 * ch) = o;
+  }
+  constexpr int kDa = 1280;
+  for (int c = threadIdx.x; c < 32 * (kDa / 8); c += kNW * 64) {
+    const int rw = c / (kDa / 8), ch = c % (kDa / 8);
+    if (row0 + rw >= io.N) continue;
+    const int ar = L.act[rw];
+    frag8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int col = 8 * ch + i, k = col / kAtoms, m = col - k * kAtoms;
+      const float d = col < kActs * kAtoms ? dqf[rw * kAP + m] : 0.f;
+      o[i] = (elem_t)(col < kActs * kAtoms ? (k == ar ? d - d / static_cast<float>(kActs) : -d / static_cast<float>(kActs)) : 0.f);
+    }
+    *reinterpret_cast<frag8*>(bp(io.dza) + static_cast<int64_t>(row0 + rw) * kDa + 8 * ch) = o;
+  }
+
+  // ---------------- dh2 (wave w: block w) -> dz2 into x0's space (f is only needed as the mask now)
+  elem_t* const dz2v = L.x0;
+  elem_t* const dz2a = L.x0 + 32 * kHid;
+  {
+    const RowA<kAP> RQ(r, h);
+    const RowA<kHid> RH(r, h);
+    const frag8* VOT = reinterpret_cast<const frag8*>(a.w.vot);
+    const frag8* MOT = reinterpret_cast<const frag8*>(a.w.mot);
+    const frag8* AOT = reinterpret_cast<const frag8*>(a.w.aot);
+    frag8 bq[kAP / 16];
+#pragma unroll
+    for (int ks = 0; ks < kAP / 16; ++ks) bq[ks] = rowf(dqi, RQ, 0, ks);
+    f32x16 dv = f32x16{}, da = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < kAP / 16; ++ks) {
+      dv = mfma(VOT[(w * 4 + ks) * 64 + lane], bq[ks], dv);
+      da = mfma(MOT[(w * 4 + ks) * 64 + lane], bq[ks], da);   // - mean_k Wao[k]^T dq
+    }
+    for (int k = 0; k < kActs; ++k) {
+      if (__builtin_amdgcn_readfirstlane(__ballot(act_r == k) != 0) == 0) continue;   // action absent from the tile
+      const frag8 zero{};
+#pragma unroll
+      for (int ks = 0; ks < kAP / 16; ++ks)
+        da = mfma(AOT[((k * 4 + w) * 4 + ks) * 64 + lane], act_r == k ? bq[ks] : zero, da);
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      frag8 ov, oa;
+      float fv[8], fa[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        fv[i] = (m2 >> (8 * s + i)) & 1u ? dv[8 * s + i] : 0.f;
+        fa[i] = (m2 >> (16 + 8 * s + i)) & 1u ? da[8 * s + i] : 0.f;
+        ov[i] = (elem_t)fv[i];
+        oa[i] = (elem_t)fa[i];
+      }
+      rows(dz2v, RH, 0, 2 * w + s, ov);
+      rows(dz2a, RH, 0, 2 * w + s, oa);
+      elem_t* sv = orow(io.dz2v, kHid);
+      elem_t* sa = orow(io.dz2a, kHid);
+      store16(sv != nullptr ? sv + w * 32 + 16 * s : nullptr, fv, h);
+      store16(sa != nullptr ? sa + w * 32 + 16 * s : nullptr, fa, h);
+    }
+  }
+  __syncthreads();
+
+  // ---------------- dh1 = W2^T dz2 (block w) -> dz1 into h1's space
+  elem_t* const dz1v = L.h1[0];
+  elem_t* const dz1a = L.h1[1];
+  {
+    f32x16 dv, da;
+    phase_back<kHid>(a.w.v2t, a.w.a2t, dz2v, dz2a, w, lane, dv, da);
+    const RowA<kHid> RH(r, h);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      frag8 ov, oa;
+      float fv[8], fa[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        fv[i] = (m1 >> (8 * s + i)) & 1u ? dv[8 * s + i] : 0.f;
+        fa[i] = (m1 >> (16 + 8 * s + i)) & 1u ? da[8 * s + i] : 0.f;
+        ov[i] = (elem_t)fv[i];
+        oa[i] = (elem_t)fa[i];
+      }
+      rows(dz1v, RH, 0, 2 * w + s, ov);
+      rows(dz1a, RH, 0, 2 * w + s, oa);
+      elem_t* sv = orow(io.dz1v, kHid);
+      elem_t* sa = orow(io.dz1a, kHid);
+      store16(sv != nullptr ? sv + w * 32 + 16 * s : nullptr, fv, h);
+      store16(sa != nullptr ? sa + w * 32 + 16 * s : nullptr, fa, h);
+    }
+  }
+  __syncthreads();
+
+  // ---------------- df = Wv1^T dz1v + Wa1^T dz1a (blocks 2w, 2w + 1) -> dz of the encoders
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    f32x16 dv, da;
+    phase_back<kHid>(a.w.v1t, a.w.a1t, dz1v, dz1a, 2 * w + q, lane, dv, da);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float fv[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        fv[i] = (fmask >> (16 * q + 8 * s + i)) & 1u ? dv[8 * s + i] + da[8 * s + i] : 0.f;
+      elem_t* sf = orow(io.dzf, kEnc);
+      store16(sf != nullptr ? sf + (2 * w + q) * 32 + 16 * s : nullptr, fv, h);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ packing
 // Fragment images (asvrl_mfma.h frag_rc) of the encoders (256 x 32, input-fed) and the six composed
 // NoisyLinear layers (chained): value / advantage hidden layers, the value output (51 rows, zero to 64),
@@ -322,6 +609,9 @@ constexpr int kImgEnc = kEnc * kObsK, kImgH1 = kHid * kEnc, kImgH2 = kHid * kHid
               kImgAO = kActs * kAP * kHid;
 constexpr int kPackImg = kImgEnc + 2 * kImgH1 + 2 * kImgH2 + 2 * kImgO + kImgAO;
 constexpr int kPackBias = kEnc + 4 * kHid + 2 * kAP + kActs * kAP;
+// the backward's transposed images (A = W^T, chained over the layer's outputs): vot, mot (-mean), aot,
+// v2t, a2t, v1t, a1t
+constexpr int kPackT = 2 * kImgO + kImgAO + 2 * kImgH2 + 2 * kImgH1;
 
 __device__ float enc_w(const AsvRainbowSrc& s, int m, int k) {
   if (m < kSelfF) return k < kSelfIn ? s.self_w[m * kSelfIn + k] : 0.f;
@@ -333,8 +623,47 @@ __device__ float out_row(const float* W, int rows, int row, int col) {
   return row < rows ? W[row * kHid + col] : 0.f;
 }
 
+__device__ void pack_transposed(const AsvRainbowSrc& s, const AsvRainbowImgOut& o, int e) {
+  int row, col;
+  float v;
+  elem_t* dst;
+  if (e < kImgO) {   // Wvo^T: M = 128 inputs, K = 64 atoms (51 + zeros)
+    frag_rc(e, kAP, true, row, col);
+    v = col < kAtoms ? s.w_vo[col * kHid + row] : 0.f;
+    dst = bp(o.vot) + e;
+  } else if ((e -= kImgO) < kImgO) {   // -mean_k Wao[k]^T
+    frag_rc(e, kAP, true, row, col);
+    float acc = 0.f;
+    if (col < kAtoms)
+      for (int k = 0; k < kActs; ++k) acc += s.w_ao[(k * kAtoms + col) * kHid + row];
+    v = -(acc / static_cast<float>(kActs));
+    dst = bp(o.mot) + e;
+  } else if ((e -= kImgO) < kImgAO) {   // Wao[k]^T per action
+    const int k = e / kImgO, f = e % kImgO;
+    frag_rc(f, kAP, true, row, col);
+    v = col < kAtoms ? s.w_ao[(k * kAtoms + col) * kHid + row] : 0.f;
+    dst = bp(o.aot) + e;
+  } else if ((e -= kImgAO) < 2 * kImgH2) {   // W2^T
+    const int which = e / kImgH2, f = e % kImgH2;
+    frag_rc(f, kHid, true, row, col);
+    v = (which ? s.w_a2 : s.w_v2)[col * kHid + row];
+    dst = bp(which ? o.a2t : o.v2t) + f;
+  } else {   // W1^T: M = 256 inputs, K = 128 outputs
+    e -= 2 * kImgH2;
+    const int which = e / kImgH1, f = e % kImgH1;
+    frag_rc(f, kHid, true, row, col);
+    v = (which ? s.w_a1 : s.w_v1)[col * kEnc + row];
+    dst = bp(which ? o.a1t : o.v1t) + f;
+  }
+  *dst = (elem_t)v;
+}
+
 __global__ __launch_bounds__(256) void rainbow_pack_kernel(AsvRainbowSrc s, AsvRainbowImgOut o) {
   const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= kPackImg + kPackBias) {
+    if (t < kPackImg + kPackBias + kPackT && o.vot != nullptr) pack_transposed(s, o, t - kPackImg - kPackBias);
+    return;
+  }
   if (t < kPackImg) {
     int e = t, row, col;
     elem_t* dst;
@@ -398,6 +727,12 @@ __global__ __launch_bounds__(256) void rainbow_pack_kernel(AsvRainbowSrc s, AsvR
   }
 }
 
+int launch_train(const AsvRainbowImg* w, const AsvRainbowNetIO* io, void* stream) {
+  RbArgs a{*w, *io};
+  hipLaunchKernelGGL(rainbow_train_kernel, dim3((io->N + 31) / 32), dim3(kNW * 64), 0, as_stream(stream), a);
+  return check_launch("asvrl_rainbow_net_train");
+}
+
 int launch_net(int mode, const AsvRainbowImg* w, const AsvRainbowNetIO* io, void* stream) {
   RbArgs a{*w, *io};
   const dim3 grid((io->N + 31) / 32), block(kNW * 64);
@@ -433,7 +768,10 @@ extern "C" int asvrl_rainbow_pack(const AsvRainbowSrc* src, const AsvRainbowImgO
   ASVRL_REQUIRE(img->enc && img->b_enc && img->v1 && img->a1 && img->v2 && img->a2 && img->vo && img->mo && img->ao &&
                     img->b_v1p && img->b_a1p && img->b_v2p && img->b_a2p && img->b_vop && img->b_mop && img->b_aop,
                 "asvrl_rainbow_pack: null image");
-  const int total = kPackImg + kPackBias;
+  const bool tr = img->vot != nullptr;
+  ASVRL_REQUIRE(!tr || (img->mot && img->aot && img->v2t && img->a2t && img->v1t && img->a1t),
+                "asvrl_rainbow_pack: the transposed images come all or none");
+  const int total = kPackImg + kPackBias + (tr ? kPackT : 0);
   hipLaunchKernelGGL(rainbow_pack_kernel, dim3((total + 255) / 256), dim3(256), 0, as_stream(stream), *src, *img);
   return check_launch("asvrl_rainbow_pack");
 }
@@ -459,4 +797,17 @@ extern "C" int asvrl_rainbow_net_pick(const AsvRainbowImg* w, const AsvRainbowNe
   ASVRL_REQUIRE(io->act_idx && io->p_out, "asvrl_rainbow_net_pick: needs act_idx and p_out");
   if (io->N <= 0) return 0;
   return launch_net(RB_PICK, w, io, stream);
+}
+
+extern "C" int asvrl_rainbow_net_train(const AsvRainbowImg* w, const AsvRainbowNetIO* io, void* stream) {
+  if (int rc = check_img(w, io)) return rc;
+  ASVRL_REQUIRE(w->vot && w->mot && w->aot && w->v2t && w->a2t && w->v1t && w->a1t,
+                "asvrl_rainbow_net_train: needs the transposed images (asvrl_rainbow_pack with vot ... a1t)");
+  ASVRL_REQUIRE(io->actions && io->weights && io->ld_rd >= 1 && io->m && io->loss,
+                "asvrl_rainbow_net_train: needs actions, weights, m and loss");
+  ASVRL_REQUIRE(io->xb && io->f && io->hv1 && io->ha1 && io->hv2 && io->ha2 && io->dzv && io->dza && io->dz2v &&
+                    io->dz2a && io->dz1v && io->dz1a && io->dzf,
+                "asvrl_rainbow_net_train: null activation / gradient image");
+  if (io->N <= 0) return 0;
+  return launch_train(w, io, stream);
 }

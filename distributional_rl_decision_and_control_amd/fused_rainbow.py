@@ -1,7 +1,7 @@
-"""Rainbow (dueling NoisyNet C51) act and train_Rainbow on gfx950 kernels: the whole network + head
-of act and of the two s_{t+n} passes as one kernel per 32-row tile (asvrl_rainbow_net.hip), the noisy
-weights and the loss head in asvrl_rainbow.hip; the training pass's GEMMs (forward with grad and
-backward) stay hipBLASLt GEMMs through torch (fp32).
+"""Rainbow (dueling NoisyNet C51) act and train_Rainbow on gfx950 kernels, no torch GEMM or autograd:
+the whole network + head of act, of the two s_{t+n} passes and of the training pass (forward, loss,
+backward) as one kernel per 32-row tile each (asvrl_rainbow_net.hip), the noisy weights in
+asvrl_rainbow.hip, the weight gradients in asvrl_wgrad.hip.
 
 Per learn step (agent.py:597-641), on PER rows [B][88] (obs | n-th next obs | action | R | nonterminal |
 weight):
@@ -10,10 +10,12 @@ weight):
   double-Q argmax over s_{t+n} with the online net               asvrl_rainbow_net_argmax (one launch)
   target reset_noise() + compose, packed                         asvrl_noisy_reset, asvrl_rainbow_pack
   p(s_{t+n}, a*) of the target net                               asvrl_rainbow_net_pick (one launch)
-  logits v, a of s (with grad)                                   torch GEMMs (fp32)
   projection m                                                   asvrl_c51_project (bit-exact)
-  per-sample loss and d mean(w loss) / d(v, a)                   asvrl_rainbow_loss
-  backward through the GEMMs                                     torch.autograd.backward([v, a], [dv, da])
+  forward of s saving the activations, per-sample loss, backward to the encoders' pre-activations
+                                                                 asvrl_rainbow_net_train (one launch)
+  weight gradients of the six layers + the encoder fold          ONE asvrl_linear_wgrad_multi, ONE
+                                                                 asvrl_partial_sums (into the composed-
+                                                                 weight gradient buffer)
   dmu = dW, dsigma = dW * eps                                    asvrl_noisy_compose(backward)
   clip + Adam                                                    asvrl_adam_clip
 Act (agent.py:308-324) on every robot: the same composed online weights, asvrl_rainbow_net_act
@@ -25,14 +27,12 @@ The online net's noise is never resampled during training, as in the reference (
 only called on the target, agent.py:610). The target noise comes from Philox instead of torch.randn.
 """
 import ctypes as C
-import os
 
 import torch
-import torch.nn.functional as F
 
 from . import _abi
+from .fused_critic import PartialArena
 from .learn_ops import c51_project
-from .splitk_linear import SPLITK_MIN_ROWS, _SplitKLinear, _SplitKLinearReLU
 
 NOISY = ("hidden_layer_v", "hidden_layer_v_2", "output_layer_v", "hidden_layer_a", "hidden_layer_a_2",
          "output_layer_a")
@@ -88,84 +88,40 @@ class NoisyPack:
                                                 int(seed) & 0xFFFFFFFFFFFFFFFF, _abi.ptr(counter_dev),
                                                 _abi.stream_ptr(stream)), "asvrl_noisy_reset")
 
+    def grad_buffer(self):
+        """A flat buffer shaped like the composed weights for their gradient: {layer: (dW, db)} views."""
+        if not hasattr(self, "dflat"):
+            self.dflat = torch.zeros_like(self.flat)
+            self.dviews = [self.dflat[(v.data_ptr() - self.flat.data_ptr()) // 4:][:v.numel()].view_as(v)
+                           for v in self.views]
+        return {n: (self.dviews[2 * j], self.dviews[2 * j + 1]) for j, n in enumerate(NOISY)}
+
     def backward(self, leaves, stream=None):
-        """dmu = dW, dsigma = dW * eps into the parameters' .grad buffers (assigned)."""
+        """dmu = dW, dsigma = dW * eps into the parameters' .grad buffers (assigned); dW from the leaves'
+        .grad (autograd) or, with leaves=None, from self.dviews (the gradient buffer grad_buffer() made)."""
         s = _abi.AsvNoisySegs()
         C.memmove(C.byref(s), C.byref(self.segs), C.sizeof(s))
         k = 0
         for L in self.layers:
             for mu, sig in ((L.weight_mu, L.weight_sigma), (L.bias_mu, L.bias_sigma)):
-                g = leaves[k].grad
-                if g is None:
-                    g = torch.zeros_like(leaves[k])
-                g = g.contiguous()
-                leaves[k]._keep = g   # keep alive until the launch is queued
+                if leaves is None:
+                    g = self.dviews[k]
+                else:
+                    g = leaves[k].grad
+                    if g is None:
+                        g = torch.zeros_like(leaves[k])
+                    g = g.contiguous()
+                    leaves[k]._keep = g   # keep alive until the launch is queued
                 seg = s.seg[k]
                 seg.dout, seg.dmu, seg.dsigma = g.data_ptr(), mu.grad.data_ptr(), sig.grad.data_ptr()
                 k += 1
         _abi.check(_abi.lib().asvrl_noisy_compose(C.byref(s), 1, _abi.stream_ptr(stream)), "asvrl_noisy_compose(bwd)")
 
 
-_SPLITK = os.environ.get("ASVRL_RAINBOW_SPLITK", "1") != "0"
-# rows per split-K group: 1024 gave the shortest Rainbow step of 256/512/1024/2048 (rocprof A/B)
-_GROUP_ROWS = int(os.environ.get("ASVRL_RAINBOW_GROUP_ROWS", "1024"))
-
-
-def _lin(x, w, b):
-    """F.linear; with grad on a batch of >= SPLITK_MIN_ROWS rows the weight gradient is a split-K
-    batched GEMM (a single hipBLASLt call at K = 8192 leaves most CUs idle: 50 us per layer)."""
-    if _SPLITK and torch.is_grad_enabled() and x.shape[0] >= SPLITK_MIN_ROWS and (w.requires_grad or x.requires_grad):
-        return _SplitKLinear.apply(x, w, b, _GROUP_ROWS)
-    return F.linear(x, w, b)
-
-
-_RELU_EPILOGUE = os.environ.get("ASVRL_RAINBOW_EPI", "1") != "0"
-
-
-def _lin_relu(x, w, b):
-    """relu(x W^T + b). Without grad on the device it is one hipBLASLt GEMM with the bias + ReLU
-    epilogue (torch._addmm_activation) instead of a GEMM and a clamp launch (4-5 us each, 18 per
-    Rainbow iteration in the act and target forwards)."""
-    if _RELU_EPILOGUE and x.is_cuda and x.dim() == 2:
-        if not torch.is_grad_enabled():
-            return torch._addmm_activation(b, x, w.t())
-        if _SPLITK and x.shape[0] >= SPLITK_MIN_ROWS:
-            return _SplitKLinearReLU.apply(x, w, b, _GROUP_ROWS)
-    return F.relu(_lin(x, w, b))
-
-
-def logits(net, x, W):
-    """Rainbow_Policy.forward up to the dueling combine (Rainbow_model.py:97-127): value (N, 51) and
-    advantage (N, 25*51) logits with the composed noisy weights W. The encoders are
-    encode_observation (AC_IQN_model.py:284-308) written out so their layers take _lin too."""
-    x_1, x_2, x_2_mask = x
-    B = x_1.shape[0]
-    se, oe = net.self_encoder[0], net.object_encoder[0]
-    f1 = _lin_relu(x_1, se.weight, se.bias)
-    if x_2 is None:
-        f2 = torch.zeros((B, net.max_object_num * net.object_feature_dimension), device=x_1.device, dtype=f1.dtype)
-    else:
-        f2 = _lin_relu(x_2.reshape(B * net.max_object_num, net.object_dimension), oe.weight, oe.bias)
-        f2 = f2.view(B, net.max_object_num, net.object_feature_dimension)
-        f2 = f2.masked_fill(x_2_mask.unsqueeze(-1) < 0.5, 0.0)
-        f2 = f2.reshape(B, net.max_object_num * net.object_feature_dimension)
-    f = torch.cat((f1, f2), 1)
-    fv = _lin_relu(f, *W["hidden_layer_v"])
-    fv = _lin_relu(fv, *W["hidden_layer_v_2"])
-    v = _lin(fv, *W["output_layer_v"])
-    fa = _lin_relu(f, *W["hidden_layer_a"])
-    fa = _lin_relu(fa, *W["hidden_layer_a_2"])
-    a = _lin(fa, *W["output_layer_a"])
-    return v, a
-
-
-def _split(rows):
-    M = rows.shape[0]
-    return rows[:, 0:7], rows[:, 7:32].reshape(M, 5, 5), rows[:, 32:37]
-
-
 IMG_SIZES = {"enc": 256 * 32, "v1": 128 * 256, "a1": 128 * 256, "v2": 128 * 128, "a2": 128 * 128, "vo": 64 * 128,
              "mo": 64 * 128, "ao": 25 * 64 * 128}
+IMGT_SIZES = {"vot": 128 * 64, "mot": 128 * 64, "aot": 25 * 128 * 64, "v2t": 128 * 128, "a2t": 128 * 128,
+              "v1t": 256 * 128, "a1t": 256 * 128}
 BIAS_SIZES = {"b_enc": 256, "b_v1p": 128, "b_a1p": 128, "b_v2p": 128, "b_a2p": 128, "b_vop": 64, "b_mop": 64,
               "b_aop": 25 * 64}
 
@@ -174,14 +130,15 @@ class RainbowNetImage:
     """Fragment images of one Rainbow_Policy for asvrl_rainbow_net_*: the encoders and the composed noisy
     layers of `noisy` (a NoisyPack of the same net), packed by refresh() (asvrl_rainbow_pack)."""
 
-    def __init__(self, net, noisy, operands="bf16"):
+    def __init__(self, net, noisy, operands="bf16", train=False):
         self.L = _abi.lib(operands)
         dev = noisy.flat.device
-        self.img = torch.zeros(sum(IMG_SIZES.values()), dtype=_abi.operand_dtype(operands), device=dev)
+        sizes = dict(IMG_SIZES, **(IMGT_SIZES if train else {}))
+        self.img = torch.zeros(sum(sizes.values()), dtype=_abi.operand_dtype(operands), device=dev)
         self.bias = torch.zeros(sum(BIAS_SIZES.values()), dtype=torch.float32, device=dev)
         st = _abi.AsvRainbowImg()
         off = 0
-        for n, k in IMG_SIZES.items():
+        for n, k in sizes.items():
             setattr(st, n, self.img[off:off + k].data_ptr())
             off += k
         off = 0
@@ -223,16 +180,22 @@ class FusedRainbow:
         self.local, self.target, self.B = local, target, B
         self.pack = NoisyPack(local)
         self.tpack = NoisyPack(target)
-        self.img = RainbowNetImage(local, self.pack, operands)
+        self.img = RainbowNetImage(local, self.pack, operands, train=True)
         self.timg = RainbowNetImage(target, self.tpack, operands)
         dev = support.device
         self.support = support.float().contiguous()
+        # the training pass's saved activations and pre-activation gradients (operand type)
+        od = dict(dtype=_abi.operand_dtype(operands), device=dev)
+        self.acts = {n: torch.zeros(B, k, **od) for n, k in (("xb", 32), ("f", 256), ("hv1", 128), ("ha1", 128),
+                                                              ("hv2", 128), ("ha2", 128), ("dzv", 64), ("dza", 1280),
+                                                              ("dz2v", 128), ("dz2a", 128), ("dz1v", 128),
+                                                              ("dz1a", 128), ("dzf", 256))}
+        self.arena = PartialArena(48 << 20, dev, operands)
+        self.dW = self.pack.grad_buffer()
         f = dict(dtype=torch.float32, device=dev)
         self.a_star = torch.zeros(B, dtype=torch.int64, device=dev)
         self.p_star = torch.zeros(B, ATOMS, **f)
         self.loss = torch.zeros(B, **f)
-        self.dv = torch.zeros(B, ATOMS, **f)
-        self.da = torch.zeros(B, ATOMS * ACTIONS, **f)
         self.pack.compose()
         self.tpack.compose()
         self.img.refresh()
@@ -241,15 +204,6 @@ class FusedRainbow:
     def target_changed(self):
         self.tpack.compose()
         self.timg.refresh()
-
-    def _head(self, v, a, **kw):
-        io = _abi.AsvRainbowHeadIO()
-        io.v, io.ldv, io.a, io.lda = v.data_ptr(), v.stride(0), a.data_ptr(), a.stride(0)
-        io.N, io.atoms, io.actions_n = v.shape[0], ATOMS, ACTIONS
-        io.support = self.support.data_ptr()
-        for k, val in kw.items():
-            setattr(io, k, val)
-        return io
 
     @torch.no_grad()
     def act(self, obs_rows, actions64, step_dev, steps_per_count, total, fraction, initial, final, seed):
@@ -271,8 +225,6 @@ class FusedRainbow:
         if compose:
             self.pack.compose()
             self.img.refresh()
-        W, leaves = self.pack.weights(detach_grad=True)
-        grads.zero_()
         ns_rows = rows[:, 40:80]
         # double-Q argmax over s_{t+n} with the online net, then p(s_{t+n}, a*) of the target net with
         # fresh target noise (agent.py:605-612)
@@ -281,15 +233,34 @@ class FusedRainbow:
         self.timg.refresh()
         self.timg.run("asvrl_rainbow_net_pick", self.timg.io(ns_rows, self.support, act_idx=self.a_star.data_ptr(),
                                                                p_out=self.p_star.data_ptr()))
-        v, a = logits(self.local, _split(rows[:, 0:40]), W)
         with torch.no_grad():
             m = c51_project(self.p_star, rows[:, 82], rows[:, 83], self.support, vmin, vmax, gamma ** n)
-            io = self._head(v.detach(), a.detach(), actions=rows.data_ptr() + 80 * 4, weights=rows.data_ptr() + 84 * 4,
-                            ld_rd=rows.stride(0), m=m.data_ptr(), loss=self.loss.data_ptr(), dv=self.dv.data_ptr(),
-                            da=self.da.data_ptr(), grad_scale=1.0 / B)
-            _abi.check(_abi.lib().asvrl_rainbow_loss(C.byref(io), _abi.stream_ptr()), "asvrl_rainbow_loss")
-        torch.autograd.backward([v, a], [self.dv, self.da])
-        self.pack.backward(leaves)
+        # forward of s saving the activations, loss, backward to the encoders (agent.py:613-636)
+        A = self.acts
+        io = self.img.io(rows[:, 0:40], self.support, actions=rows.data_ptr() + 80 * 4,
+                         weights=rows.data_ptr() + 84 * 4, ld_rd=rows.stride(0), m=m.data_ptr(), grad_scale=1.0 / B,
+                         loss=self.loss.data_ptr(), **{k: t.data_ptr() for k, t in A.items()})
+        self.img.run("asvrl_rainbow_net_train", io)
+        # the six layers' weight gradients (into the composed-weight gradient buffer) and the encoder
+        # fold in one launch, one reduction, then dmu = dW, dsigma = dW eps
+        arena, dW, net = self.arena, self.dW, self.local
+        with arena.batch():
+            # the output layers in the kernel's (32, 128) / (128, 128) shapes: column slices of the padded
+            # dz images into the leading rows of each slice of the gradient
+            Wv, bv = dW["output_layer_v"]
+            for i in range(2):
+                arena.linear(A["dzv"][:, 32 * i:32 * i + 32], A["hv2"], Wv[32 * i:32 * i + 32], bv[32 * i:32 * i + 32])
+            Wa, ba = dW["output_layer_a"]
+            for i in range(10):
+                arena.linear(A["dza"][:, 128 * i:128 * i + 128], A["ha2"], Wa[128 * i:128 * i + 128],
+                             ba[128 * i:128 * i + 128])
+            arena.linear(A["dz2v"], A["hv1"], *dW["hidden_layer_v_2"])
+            arena.linear(A["dz2a"], A["ha1"], *dW["hidden_layer_a_2"])
+            arena.linear(A["dz1v"], A["f"], *dW["hidden_layer_v"])
+            arena.linear(A["dz1a"], A["f"], *dW["hidden_layer_a"])
+            arena.fold(A["dzf"], A["xb"], net)
+        arena.flush()
+        self.pack.backward(None)
         if sync is not None:
             sync(grads)
         gn = clip_and_step(opt, grads, max_norm)

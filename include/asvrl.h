@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 14
+#define ASVRL_ABI_VERSION 15
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -558,14 +558,18 @@ typedef struct AsvRainbowSrc {   /* f32 row-major [out][in] */
 } AsvRainbowSrc;
 
 /* The packed images (operand element type; biases f32). Sizes in elements: enc 8192, v1 / a1 32768,
- * v2 / a2 16384, vo / mo 8192, ao 204800; b_enc 256, b_v1p .. b_a2p 128, b_vop / b_mop 64, b_aop 1600. */
+ * v2 / a2 16384, vo / mo 8192, ao 204800; b_enc 256, b_v1p .. b_a2p 128, b_vop / b_mop 64, b_aop 1600.
+ * The backward's transposed images (train only; may be NULL otherwise): vot / mot 8192 (mot holds
+ * -mean_k), aot 204800, v2t / a2t 16384, v1t / a1t 32768. */
 typedef struct AsvRainbowImgOut {
   void *enc, *v1, *a1, *v2, *a2, *vo, *mo, *ao;
   float *b_enc, *b_v1p, *b_a1p, *b_v2p, *b_a2p, *b_vop, *b_mop, *b_aop;
+  void *vot, *mot, *aot, *v2t, *a2t, *v1t, *a1t;
 } AsvRainbowImgOut;
 typedef struct AsvRainbowImg {   /* the same buffers, read-only */
   const void *enc, *v1, *a1, *v2, *a2, *vo, *mo, *ao;
   const float *b_enc, *b_v1p, *b_a1p, *b_v2p, *b_a2p, *b_vop, *b_mop, *b_aop;
+  const void *vot, *mot, *aot, *v2t, *a2t, *v1t, *a1t;
 } AsvRainbowImg;
 
 typedef struct AsvRainbowNetIO {
@@ -580,6 +584,19 @@ typedef struct AsvRainbowNetIO {
   double eps_steps_per_count, eps_total, eps_fraction, eps_initial, eps_final;
   uint64_t seed;
   float* p_out;             /* pick: [N][51] softmax(q[a*]) */
+  /* train (agent.py:613-636): loss and backward of mean_b w_b loss_b on the rows x (= s) */
+  const float* actions;     /* [N] taken action at actions[row * ld_rd] (replay row column) */
+  const float* weights;     /* [N] importance weights at weights[row * ld_rd] */
+  int64_t ld_rd;
+  const float* m;           /* [N][51] projected target distribution (asvrl_c51_project) */
+  float grad_scale;         /* 1 / B */
+  int32_t _pad1;
+  float* loss;              /* [N] -sum m log softmax(q[a_b]) */
+  /* saved activations (operand type, row-major, natural feature order): the weight-gradient inputs */
+  void *xb, *f, *hv1, *ha1, *hv2, *ha2;   /* [N][32], [N][256], [N][128] x 4 */
+  /* pre-activation gradients (operand type): dz of output_layer_v [N][64] (51 + zero pad), of
+   * output_layer_a [N][1280] (1275 + zero pad), of the hidden layers [N][128] x 4, of the encoders [N][256] */
+  void *dzv, *dza, *dz2v, *dz2a, *dz1v, *dz1a, *dzf;
 } AsvRainbowNetIO;
 
 /* Pack the encoders and composed noisy layers into AsvRainbowImgOut (one launch). */
@@ -590,6 +607,11 @@ int asvrl_rainbow_net_act(const AsvRainbowImg* w, const AsvRainbowNetIO* io, voi
 int asvrl_rainbow_net_argmax(const AsvRainbowImg* w, const AsvRainbowNetIO* io, void* stream);
 /* p(s', a*) of the target net (agent.py:610-612): p_out[row] = softmax(q[act_idx[row]]). */
 int asvrl_rainbow_net_pick(const AsvRainbowImg* w, const AsvRainbowNetIO* io, void* stream);
+/* The training pass of train_Rainbow (agent.py:613-636) on the online net: forward saving the
+ * activations, loss_b = -sum m log softmax(q[a_b]), and the backward of grad_scale * sum_b w_b loss_b
+ * down to the encoders' pre-activations (the weight gradients then come from asvrl_linear_wgrad_multi
+ * over the saved activations / dz images, the encoders' by the fold). */
+int asvrl_rainbow_net_train(const AsvRainbowImg* w, const AsvRainbowNetIO* io, void* stream);
 
 /* ---------------------------------------------------------------- optimiser (agent.py) */
 
@@ -658,7 +680,7 @@ int asvrl_linear_wgrad_partial(const void* dz, int64_t ldz, const void* x, int64
  *                           (128, 128), (256, 32), (32, 128)};
  *   kind ASVRL_WGRAD_VEC  : asvrl_linear_wgrad_vec_partial (dz = dq f32 with stride ldz, M = 1, K = 128);
  *   kind ASVRL_WGRAD_SMALL: asvrl_small_wgrad_partial (f32 dz, x; M | 256, K <= 4). */
-#define ASVRL_MAX_WGRAD_SEGS 8
+#define ASVRL_MAX_WGRAD_SEGS 24
 #define ASVRL_WGRAD_MFMA 0
 #define ASVRL_WGRAD_VEC 1
 #define ASVRL_WGRAD_SMALL 2
@@ -686,7 +708,7 @@ int asvrl_linear_wgrad_vec_partial(const float* dq, int64_t ldq, const void* x, 
 /* One pending reduction: dw[i] (+)= sum_g partial[g][i] for i < nw, db likewise for the
  * trailing nb values of each group's (nw + nb)-float partial (db optional). A segment with
  * nw + nb == 1 (a scalar over many groups) is reduced by a whole workgroup. */
-#define ASVRL_MAX_SUM_SEGS 8
+#define ASVRL_MAX_SUM_SEGS 24
 #define ASVRL_SUM_PLAIN 0
 /* The 256 x 32 encoder-image partials (asvrl_mlp_pack's block-structured image) folded straight
  * into the contiguous gradients [self_w 56x7 | self_b 56 | obj_w 40x5 | obj_b 40] at dw (688
