@@ -33,6 +33,18 @@ int launch_partial_sum(const float* partial, int groups, int nw, int nb, float* 
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// compute units of the current device (cached; 256 on MI355X when the query fails)
+inline int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
 // ------------------------------------------------------------------ Philox-4x32-10
 struct U4 {
   uint32_t x, y, z, w;

@@ -882,17 +882,6 @@ void critic_fused_kernel(FusedArgs a) {
   if (threadIdx.x == 0) po[kH] = ((L.red[0] + L.red[1]) + L.red[2]) + L.red[3];
 }
 
-int cu_count() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-  }
-  return n;
-}
-
 int fused_nb(int N) {
 #if ASVRL_OPERAND_F32
   (void)N;

@@ -1,33 +1,32 @@
 """The whole AC-IQN update (Agent.train_AC_IQN, agent.py:386-432) on hand-written gfx950
-kernels: about 30 launches per step, no torch autograd, no host synchronisation.
+kernels: about 16 launches per step, no torch autograd, no host synchronisation.
 
 Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | done):
+  actor(s) saving activations -> a (for the actor step)  asvrl_actor_forward(TRAIN)
   critic (agent.py:395-416)
     target actor(ns) -> na                               asvrl_actor_forward(FWD)
     target encoders(ns, na) + trunk -> q_next            asvrl_critic_forward (encoders in the prologue)
-    local encoders(s, a) + trunk forward + quantile-Huber vs r + g q_next (1-d) + backward
-                                                          asvrl_critic_train (targets formed in-kernel)
-    trunk, encoder-image and action-encoder weight grads ONE asvrl_linear_wgrad_multi (the output
-                                                          layer's as per-tile partials from the TRAIN kernel)
+    local encoders(s, a), trunk forward, quantile-Huber vs r + g q_next (1-d), backward AND the
+    four trunk layers' weight-gradient partials          asvrl_critic_train_fused (ONE launch)
+    encoder / action-encoder gradients from dzF / dzG    ONE asvrl_linear_wgrad_multi (fold + small)
     every .grad (encoders folded in the reduction), the loss and the global gradient norm
                                                           ONE asvrl_partial_sums_norm
-    clip + Adam                                          asvrl_adam_step
-      (with DP: asvrl_partial_sums, RCCL all-reduce, asvrl_adam_clip)
-    re-pack trunk                                        asvrl_critic_pack
+    clip + Adam + re-pack of the weight images           asvrl_adam_step_pack
+      (with DP: asvrl_partial_sums, RCCL all-reduce, asvrl_adam_clip, re-pack)
   actor (agent.py:419-427), through the UPDATED critic
-    actor(s) saving activations -> a                     asvrl_actor_forward(TRAIN)
     encoders(s, a) + trunk forward + backward of -mean(q) to the action
                                                           asvrl_critic_actor_grad (dA in-kernel)
     actor backward                                       asvrl_actor_backward
     actor weight grads                                   ONE asvrl_linear_wgrad_multi, one asvrl_partial_sums_norm
-    clip + Adam, re-pack actor                           asvrl_adam_step + asvrl_mlp_pack
+    clip + Adam + re-pack                                asvrl_adam_step_pack
+(ASVRL_FUSED_TRAIN=0, or B*N not a multiple of the fused launch's round: the critic step as the two
+TRAIN kernels asvrl_critic_train + the batched weight-gradient launch over saved activations.)
 
-Independent launches run on side streams forked from the caller's stream and joined back
-before their results are needed (SideStreams; capturable in a HIP graph): the local encoders and
-the actor's training forward beside the target chain. The weight-gradient reductions of each
-optimizer step are one multi-layer launch (a cross-stream join in a replayed graph costs ≈10 µs).
+The learner runs on the caller's stream; a replayed graph pays ~10 us per cross-stream join, so the
+side streams (SideStreams) are used only where an overlap pays.
 
-Arithmetic: bf16 MFMA operands with f32 accumulation everywhere, f32 master weights / Adam.
+Arithmetic: bf16 MFMA operands with f32 accumulation everywhere, f32 master weights / Adam
+(operands="f32": the same kernels from libasvrl_f32.so, the parity build).
 """
 import contextlib
 import os
