@@ -170,6 +170,7 @@ struct FusedLds {
   float G[IQN ? 4 : S * kH];          // position order (AC-IQN's action features)
   float qpart[kNW][32 * NB];
   float dq[32 * NB];
+  float tsum[2 * NB];                 // loss sums of the round's 16-row groups
   float bias[kC + 3 * kH + 4];        // bc | b1 | b2 | wo, position order | bo
   float woA[IQN ? kMaxA * kH : 4];    // IQN: output_layer.weight, position order, zero rows to 32
   float boA[IQN ? kMaxA : 4];
@@ -261,39 +262,32 @@ __device__ __forceinline__ void stage_fg(const FusedArgs& a, int b0, int tid, co
 }
 
 // quantile-Huber terms of one row against its sample's N' = NT targets r + gamma q_next (1 - d)
-// (agent.py:399-412); lane half h takes half of them. Returns dq; *wl = the row's loss sum.
+// (agent.py:399-412), split over four lanes: lane quarter q4 (lanes 16 q4 .. 16 q4 + 15 share the
+// row block) takes targets q4 NT/4 .. + NT/4 - 1 from the staged q_next, and the four partial sums
+// are combined by two xor shuffles (a fixed order). Returns dq; *wl = the row's loss sum.
 template <int NT>
-__device__ __forceinline__ float row_loss_dq(const FusedArgs& a, const float* qt, float rb, float done, float tau,
-                                             float q, int lane, float* wl_out) {
-  const int r = lane & 31, h = lane >> 5;
+__device__ __forceinline__ float quarter_loss_dq(const FusedArgs& a, const float* qt, float rb, float done, float tau,
+                                                 float q, int q4, float* wl_out) {
   const float nd = 1.0f - done;
   const float kap = a.kappa, hk = 0.5f * a.kappa, omt = 1.f - tau;
   float wl = 0.f, wg = 0.f;
-  auto term = [&](float target) {
-    const float d = target - q;  // td_error (agent.py:406)
+#pragma unroll
+  for (int j = 0; j < NT / 4; ++j) {
+    const float target = rb + (a.gamma * qt[q4 * (NT / 4) + j]) * nd;   // r + gamma * q_next * (1 - d)
+    const float d = target - q;   // td_error (agent.py:406)
     const float ad = fabsf(d);
     const bool quad = ad <= kap;
     const float hub = quad ? 0.5f * (d * d) : kap * (ad - hk);
     const float w = d < 0.f ? omt : tau;
     wl += w * hub;
     wg += w * (quad ? d : copysignf(kap, d));
-  };
-  const float qv = qt[r % NT];
-  const float own = rb + (a.gamma * qv) * nd;   // r + gamma * q_next * (1 - d)
-#pragma unroll 4
-  for (int j = 0; j < NT / 2; ++j) {
-    float target;
-    if (NT == 32) {
-      const float t0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(own), j));
-      const float t1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(own), j + NT / 2));
-      target = h ? t1 : t0;
-    } else {
-      target = __shfl(own, (lane & ~(NT - 1)) + j + h * (NT / 2), 64);
-    }
-    term(target);
   }
-  *wl_out = half_sum(wl) / kap;
-  return -(half_sum(wg) / kap) * a.gscale;
+  wl += __shfl_xor(wl, 16, 64);
+  wg += __shfl_xor(wg, 16, 64);
+  wl += __shfl_xor(wl, 32, 64);
+  wg += __shfl_xor(wg, 32, 64);
+  *wl_out = wl / kap;
+  return -(wg / kap) * a.gscale;
 }
 
 // Per-sample sums over the NT rows of each sample (dG, dF) of a wave's 16-feature-per-lane block
@@ -576,39 +570,36 @@ void critic_fused_kernel(FusedArgs a) {
     __syncthreads();
     ASVRL_STAMP(7);
 
-    // ---------------- loss: q = sum of the four partials + bo; quantile-Huber -> dq (row block j = w)
+    // ---------------- loss: q = sum of the four partials + bo; quantile-Huber -> dq. Every wave takes
+    // 16-row groups (rows 16 g + (lane & 15)), each row's targets split over the four lane quarters
     {
       ASVRL_FRESH_LANE();
-      for (int j = w; j < NB; j += kNW) {
-        const int lr = 32 * j + r, grow = row0 + lr, b = grow / NT;
+      const int q4 = lane >> 4;
+      for (int g = w; g < G / 16; g += kNW) {
+        const int lr = 16 * g + (lane & 15), grow = row0 + lr, b = grow / NT;
         const int bl = b - b0;
         int ai = 0;
         if constexpr (IQN) ai = row_action<IL::kAct>(in, bl, a.n_actions);
         const float bo = IQN ? L.boA[ai] : L.bias[kC + 3 * kH];
         const float q = (((L.qpart[0][lr] + L.qpart[1][lr]) + L.qpart[2][lr]) + L.qpart[3][lr]) + bo;
         float wl;
-        const float dq = row_loss_dq<NT>(a, in + IL::kQn + bl * NT, in[IL::kRew + bl], in[IL::kDon + bl],
-                                         in[IL::kTau + lr], q, lane, &wl);
+        const float dq = quarter_loss_dq<NT>(a, in + IL::kQn + bl * NT, in[IL::kRew + bl], in[IL::kDon + bl],
+                                             in[IL::kTau + lr], q, q4, &wl);
         if (a.tile_loss != nullptr) {
-          float v = h == 0 ? wl : 0.f;
-          v = seg_sum<32>(v);
-          if (lane == 31) a.tile_loss[grow / 32] = v * a.loss_scale;
+          const float v = seg_sum<16>(wl);   // every lane of the 16-lane row: the group's sum
+          if (lane == 0) L.tsum[g] = v;
         }
-        if (h == 0) {
+        if (q4 == 0) {
           L.dq[lr] = dq;
           if (a.row_loss != nullptr) a.row_loss[grow] = wl;
           if (a.q != nullptr) a.q[grow] = q;
           if constexpr (!IQN) dbo += dq;
         }
         if constexpr (IQN) {   // the output layer's dZ row: dq at the taken action (agent.py:456 gather)
-          frag8 o0, o1;
+          frag8 o;
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            o0[i] = (elem_t)(16 * h + i == ai ? dq : 0.f);
-            o1[i] = (elem_t)(16 * h + 8 + i == ai ? dq : 0.f);
-          }
-          row_store<64>(L.dz1, lr, 16 * h, o0);
-          row_store<64>(L.dz1, lr, 16 * h + 8, o1);
+          for (int i = 0; i < 8; ++i) o[i] = (elem_t)(8 * q4 + i == ai ? dq : 0.f);
+          row_store<64>(L.dz1, lr, 8 * q4, o);
         }
       }
     }
@@ -617,7 +608,9 @@ void critic_fused_kernel(FusedArgs a) {
     ASVRL_STAMP(9);
 
     // ---------------- dz2 = dq wo 1[h2 > 0] (own block, in place over h2), output layer's gradient
-    // sum of dq h2
+    // sum of dq h2; the loss partial of each 32-row tile from its two 16-row sums
+    if (a.tile_loss != nullptr && threadIdx.x < G / 32)
+      a.tile_loss[row0 / 32 + threadIdx.x] = (L.tsum[2 * threadIdx.x] + L.tsum[2 * threadIdx.x + 1]) * a.loss_scale;
     {
       ASVRL_FRESH_LANE();
       const RowA<kH> RA_b(r, h);
