@@ -682,10 +682,19 @@ __global__ __launch_bounds__(8 * 64) void critic_train_b_kernel(CriticArgs a) {
 // One 32-row tile per wave; 8 waves per workgroup (2 per SIMD), 4 when a tile holds several
 // samples (N < 32) so the per-wave feature rows still fit next to the weights in LDS.
 template <int NT> struct CriticWaves { static constexpr int n = NT == 32 ? 8 : 4; };
+// IQN_ACT (the rollout's K = 32 pass, ~20 k tiles): 16 waves share one staged weight image, 4 per SIMD
+// (the 150 KB LDS image admits one workgroup per CU, so the wave count per workgroup sets the occupancy;
+// 128 VGPRs then, 6 spilled): 137 vs 150 us per launch, IQN iteration 0.370 vs 0.390 ms. The same for
+// FWD / IQN_MAX / ACTOR measured neutral to worse (IQN iteration 0.385 ms; ACTOR spills 53).
+#ifndef ASVRL_IQN_ACT_WAVES
+#define ASVRL_IQN_ACT_WAVES 16
+#endif
+template <int MODE, int NT> struct ModeWaves { static constexpr int n = CriticWaves<NT>::n; };
+template <> struct ModeWaves<MODE_IQN_ACT, 32> { static constexpr int n = ASVRL_IQN_ACT_WAVES; };
 
 template <int MODE, int NT>
-__global__ __launch_bounds__(CriticWaves<NT>::n * 64) void critic_kernel(CriticArgs a) {
-  constexpr int W = CriticWaves<NT>::n, S = 32 / NT;
+__global__ __launch_bounds__((ModeWaves<MODE, NT>::n) * 64) void critic_kernel(CriticArgs a) {
+  constexpr int W = ModeWaves<MODE, NT>::n, S = 32 / NT;
   __shared__ typename LdsOf<MODE>::T L;
   __shared__ __attribute__((aligned(16))) elem_t Fs[W * S * kC];
   __shared__ __attribute__((aligned(16))) float Gs[kStageG<MODE> ? W * S * kH : 1];
@@ -749,7 +758,7 @@ int wout_groups(int B, int N) {   // workgroups of the TRAIN launch = groups of 
 
 template <int MODE, int NT>
 void launch_mode(const CriticArgs& a, hipStream_t st) {
-  constexpr int W = CriticWaves<NT>::n;
+  constexpr int W = ModeWaves<MODE, NT>::n;
   const int tiles = a.B * NT / 32;
   hipLaunchKernelGGL((critic_kernel<MODE, NT>), dim3((tiles + W - 1) / W), dim3(W * 64), 0, st, a);
 }
