@@ -116,49 +116,60 @@ struct Stream {
 };
 
 // f32 draws for the training path (noise_mode 2): the perception noise only has to follow the
-// reference's distributions there (N(0, sigma), vonmises(0, kappa), wamv.py:27-40), so one Philox
-// call feeds four 24-bit uniforms and the transcendentals are the single-instruction f32 ones.
+// reference's distributions there (N(0, sigma), vonmises(0, kappa), wamv.py:27-40). One Philox call
+// (counter 0) feeds the four Gaussians (two Box-Muller pairs); the von Mises radius takes one call per
+// two Best-Fisher attempts (counters 1, 2, ...), its sign a spare low bit of the accepted attempt's
+// first word (the uniforms use the top 24 bits). No draw indexes a runtime buffer position, so a
+// wave whose lanes accept at different attempts issues one Philox call per attempt pair, not per
+// draw; the transcendentals, square roots and reciprocals are the single-instruction f32 ones.
 struct StreamF {
   uint32_t k0, k1, c1, c2, c3;
-  uint32_t n;
-  U4 buf;
-  int left;
   __device__ StreamF(uint64_t seed, uint32_t a, uint32_t b, uint32_t c)
-      : k0(static_cast<uint32_t>(seed)), k1(static_cast<uint32_t>(seed >> 32)), c1(a), c2(b), c3(c), n(0),
-        buf{0, 0, 0, 0}, left(0) {}
-  __device__ float u01() {   // (0, 1]
-    if (left == 0) {
-      buf = philox4x32_10(U4{n++, c1, c2, c3}, k0, k1);
-      left = 4;
-    }
-    const uint32_t w = left == 4 ? buf.x : left == 3 ? buf.y : left == 2 ? buf.z : buf.w;
-    --left;
+      : k0(static_cast<uint32_t>(seed)), k1(static_cast<uint32_t>(seed >> 32)), c1(a), c2(b), c3(c) {}
+  static __device__ float u24(uint32_t w) {   // (0, 1]
     return (static_cast<float>(w >> 8) + 1.0f) * (1.0f / 16777216.0f);
   }
-  __device__ void normal2(float& a, float& b) {
-    const float u1 = u01(), u2 = u01();
-    const float rad = __fsqrt_rn(-2.0f * __logf(u1));
+  static __device__ void box_muller(float u1, float u2, float& a, float& b) {
+    const float rad = __builtin_amdgcn_sqrtf(-2.0f * __logf(u1));
     const float t = 6.2831853f * u2;
     a = rad * __cosf(t);
     b = rad * __sinf(t);
   }
-  __device__ float vonmises(float kappa) {   // Best & Fisher, as Stream::vonmises
-    if (kappa < 1e-6f) return 3.14159265f * (2.0f * u01() - 1.0f);
-    const float r = 1.0f + __fsqrt_rn(1.0f + 4.0f * kappa * kappa);
-    const float rho = (r - __fsqrt_rn(2.0f * r)) / (2.0f * kappa);
-    const float s = (1.0f + rho * rho) / (2.0f * rho);
-    float W = 1.0f;
-    for (int it = 0; it < 256; ++it) {
-      const float U = u01();
-      const float Z = __cosf(3.14159265f * U);
-      W = (1.0f + s * Z) / (s + Z);
-      const float Y = kappa * (s - W);
-      const float V = u01();
-      if ((Y * (2.0f - Y) - V >= 0.0f) || (__logf(Y / V) + 1.0f - Y >= 0.0f)) break;
+  __device__ void normal4(float& a, float& b, float& c, float& d) const {
+    const U4 w = philox4x32_10(U4{0u, c1, c2, c3}, k0, k1);
+    box_muller(u24(w.x), u24(w.y), a, b);
+    box_muller(u24(w.z), u24(w.w), c, d);
+  }
+  // one Best-Fisher attempt from the uniforms (U, V): W and whether it is accepted
+  static __device__ bool attempt(float U, float V, float s, float kappa, float& W) {
+    const float Z = __cosf(3.14159265f * U);
+    W = (1.0f + s * Z) * __builtin_amdgcn_rcpf(s + Z);
+    const float Y = kappa * (s - W);
+    return (Y * (2.0f - Y) - V >= 0.0f) || (__logf(Y * __builtin_amdgcn_rcpf(V)) + 1.0f - Y >= 0.0f);
+  }
+  __device__ float vonmises(float kappa) const {   // Best & Fisher, as Stream::vonmises
+    if (kappa < 1e-6f) {
+      const U4 w = philox4x32_10(U4{1u, c1, c2, c3}, k0, k1);
+      return 3.14159265f * (2.0f * u24(w.x) - 1.0f);
     }
-    const float U = u01();
-    float res = acosf(fminf(fmaxf(W, -1.0f), 1.0f));
-    return U < 0.5f ? -res : res;
+    const float r = 1.0f + __builtin_amdgcn_sqrtf(1.0f + 4.0f * kappa * kappa);
+    const float rho = (r - __builtin_amdgcn_sqrtf(2.0f * r)) * __builtin_amdgcn_rcpf(2.0f * kappa);
+    const float s = (1.0f + rho * rho) * __builtin_amdgcn_rcpf(2.0f * rho);
+    float W = 1.0f;
+    uint32_t sgn = 0;
+    for (uint32_t blk = 1; blk <= 128; ++blk) {   // acceptance > 0.85 per attempt at kappa = 1; bounded
+      const U4 w = philox4x32_10(U4{blk, c1, c2, c3}, k0, k1);
+      if (attempt(u24(w.x), u24(w.y), s, kappa, W)) {
+        sgn = w.x & 1u;
+        break;
+      }
+      if (attempt(u24(w.z), u24(w.w), s, kappa, W)) {
+        sgn = w.z & 1u;
+        break;
+      }
+    }
+    const float res = acosf(fminf(fmaxf(W, -1.0f), 1.0f));
+    return sgn ? -res : res;
   }
 };
 

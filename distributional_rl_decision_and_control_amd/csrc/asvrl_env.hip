@@ -17,6 +17,8 @@
 // Arithmetic follows the reference's operation order (np.matrix products as explicit row
 // sums, no FMA contraction: built with -ffp-contract=off) so f64 state agrees with the
 // reference to ~1e-14 and collision/goal/done masks bit-exactly.
+#include <type_traits>
+
 #include "asvrl_common.h"
 
 namespace asvrl {
@@ -151,10 +153,89 @@ __device__ inline double wrap_to_pi(double a) {  // wamv.py:425-434
   return a;
 }
 
-// check_apply_COLREGs (wamv.py:398-423) for one kept object; phi written when evaluated.
-__device__ __attribute__((noinline)) bool colregs(double rself, double c, double s, double v0, double v1,
-                               double ox, double oy, double ovx, double ovy, double orad,
-                               double& phi) {
+// reward / done / info (env.py:290-331) and the trainer's bookkeeping (trainer.py:157-172): the
+// discounted return gamma^ep_ts * r and deactivation on collision or goal
+struct StepResult {
+  double reward, ret;
+  uint8_t done, info, nfl;
+};
+
+__device__ inline StepResult step_result(const AsvParams& p, const AsvStepCtl& ctl, bool exists, bool deact,
+                                         bool active, int ep_ts, uint8_t fl, bool coll, bool reach, bool apply,
+                                         double phi, double reward, double ret) {
+  uint8_t done = 1, info = ASVRL_INFO_ABSENT;
+  if (exists) {
+    if (deact) {
+      reward = 0.0;
+      done = 1;
+      info = coll ? ASVRL_INFO_DEACT_COLLISION : (reach ? ASVRL_INFO_DEACT_GOAL : ASVRL_INFO_ABSENT);
+    } else if (ctl.do_dynamics) {
+      double pen = 0.0;
+      if (apply) pen += p.COLREGs_penalty * phi;
+      reward += pen;
+      if (ep_ts >= p.episode_limit) {
+        done = 1;
+        info = ASVRL_INFO_TOO_LONG;
+      } else if (coll) {
+        reward += p.collision_penalty;
+        done = 1;
+        info = ASVRL_INFO_COLLISION;
+      } else if (reach) {
+        reward += p.goal_reward;
+        done = 1;
+        info = ASVRL_INFO_REACH_GOAL;
+      } else {
+        done = 0;
+        info = ASVRL_INFO_NORMAL;
+      }
+    } else {
+      done = 0;
+      info = ASVRL_INFO_NORMAL;
+    }
+  }
+  uint8_t nfl = static_cast<uint8_t>((fl & ASVRL_FLAG_DEACTIVATED) | (coll ? ASVRL_FLAG_COLLISION : 0) |
+                                     (reach ? ASVRL_FLAG_REACH_GOAL : 0) | (apply ? ASVRL_FLAG_COLREGS : 0));
+  if (active && ctl.do_dynamics && ctl.trainer_deactivate) {
+    if (ctl.gamma > 0) ret += pow(ctl.gamma, static_cast<double>(ep_ts)) * reward;
+    if (coll || reach) nfl |= ASVRL_FLAG_DEACTIVATED;
+  }
+  return StepResult{reward, ret, done, info, nfl};
+}
+
+// per-env end of the step (env.py:330, trainer.py:172): episode counter, episode end when the limit is
+// hit or no robot is left active, and the finished episode's totals
+__device__ inline void env_end(const AsvParams& p, const AsvEnvState& s, const AsvStepCtl& ctl,
+                               const AsvStepOut& out, int e, int ep_ts, int nrob, int alive, size_t NT) {
+  s.ep_ts[e] = ep_ts + 1;
+  if (ctl.trainer_deactivate && out.env_done != nullptr) {
+    const bool end = (ep_ts >= p.episode_limit) || alive == 0;
+    out.env_done[e] = end ? 1 : 0;
+    if (end && out.stats != nullptr) {
+      double sr = 0, sc = 0, sg = 0, sk = 0, st = 0;
+      for (int j = 0; j < nrob; ++j) {
+        const size_t jd = static_cast<size_t>(e) * s.max_robots + j;
+        const uint8_t fj = s.rflags[jd];
+        sr += s.rs[ASVRL_F_RET * NT + jd];
+        sc += 1;
+        sg += (fj & ASVRL_FLAG_REACH_GOAL) ? 1 : 0;
+        sk += (fj & ASVRL_FLAG_COLLISION) ? 1 : 0;
+        st += (fj & ASVRL_FLAG_DEACTIVATED) ? 0 : 1;
+      }
+      atomicAdd(out.stats + 0, sr);
+      atomicAdd(out.stats + 1, sc);
+      atomicAdd(out.stats + 2, sg);
+      atomicAdd(out.stats + 3, sk);
+      atomicAdd(out.stats + 4, st);
+      atomicAdd(out.stats + 5, 1.0);
+    }
+  }
+}
+
+// check_apply_COLREGs (wamv.py:398-423) for one kept object. `ev` says whether the test got as far as
+// the turn angle (the reference assigns phi exactly then); returns phi > 0.
+__device__ __forceinline__ bool colregs_body(double rself, double c, double s, double v0, double v1, double ox,
+                                             double oy, double ovx, double ovy, double orad, double& phi, bool& ev) {
+  ev = false;
   if (sqrt(ovx * ovx + ovy * ovy) < 0.5) return false;
   const double ev0 = c * v0 + s * v1;
   const double ev1 = -s * v0 + c * v1;
@@ -185,7 +266,24 @@ __device__ __attribute__((noinline)) bool colregs(double rself, double c, double
   const double add2 = atan2(rself, tang);
   const double desired = wrap_to_pi(obj_ang + add1 + add2);
   phi = wrap_to_pi(desired - ego_ang);
+  ev = true;
   return phi > 0;
+}
+
+// called out of line: its f64 atan2 / asin / sincos inlined at a call site would set the whole kernel's
+// register budget (the pair kernel: 162 -> 133 VGPRs)
+__device__ __attribute__((noinline)) bool colregs_ev(double rself, double c, double s, double v0, double v1,
+                                                     double ox, double oy, double ovx, double ovy, double orad,
+                                                     double& phi, bool& ev) {
+  return colregs_body(rself, c, s, v0, v1, ox, oy, ovx, ovy, orad, phi, ev);
+}
+
+// the per-robot sweep's serial chain (phi written when evaluated)
+__device__ __attribute__((noinline)) bool colregs(double rself, double c, double s, double v0, double v1,
+                               double ox, double oy, double ovx, double ovy, double orad,
+                               double& phi) {
+  bool ev;
+  return colregs_body(rself, c, s, v0, v1, ox, oy, ovx, ovy, orad, phi, ev);
 }
 
 struct Cand {
@@ -200,23 +298,58 @@ __device__ inline void cswap(bool cond, Cand& x, Cand& y) {
   }
 }
 
-// PAIRS: perception spread over (robot, candidate) pairs -- one lane per pair computes the noisy
-// observation, detection, collision and sort key of one candidate into LDS, then each robot lane
-// merges its candidates in the reference's order (stable top-5 insertion, collision as an OR), so the
-// kept objects and masks are the serial sweep's exactly; the Philox draws (noise modes 1, 2) are keyed
-// by (robot, candidate slot) in both layouts, so results do not depend on the launch shape.
-// `epb_arg` envs per workgroup (PAIRS).
-template <int BLOCK, bool PAIRS>
-__global__ __launch_bounds__(BLOCK) void env_step_kernel(AsvParams p, AsvEnvState s,
+// perception noise of (robot qidx, candidate slot): injected (noise_mode 0, [robot][O + R][5]), f64
+// Philox (1) or f32 Philox (2), the substream keyed by (robot, slot) so every launch shape draws the same
+// NM: the mode fixed at compile time (the pair kernel's instances), -1: read from ctl. VM = false skips the
+// von Mises radius draw n4 (a rejection loop, the costly part; it comes after the four Gaussians in the
+// substream, so the Gaussians are the same either way)
+template <int NM, bool VM = true>
+__device__ __forceinline__ void draw_noise(const AsvParams& p, const AsvStepCtl& ctl, uint64_t ctr,
+                                          const double* __restrict__ noise, size_t qidx, int slot, int S,
+                                          double& n0, double& n1, double& n2, double& n3, double& n4) {
+  const int mode = NM >= 0 ? NM : ctl.noise_mode;
+  if (mode == 0) {
+    const double* nz = noise + (qidx * static_cast<size_t>(S) + slot) * 5;
+    n0 = nz[0]; n1 = nz[1]; n2 = nz[2]; n3 = nz[3];
+    if (VM) n4 = nz[4];
+  } else if (mode == 1) {
+    Stream rng(ctl.seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull, static_cast<uint32_t>(qidx),
+               (static_cast<uint32_t>(qidx >> 32) ^ 0x5EEDu) + (static_cast<uint32_t>(slot) << 20),
+               static_cast<uint32_t>(ctr));
+    rng.normal2(n0, n1);
+    rng.normal2(n2, n3);
+    n0 *= p.pos_std; n1 *= p.pos_std; n2 *= p.vel_std; n3 *= p.vel_std;
+    if (VM) n4 = rng.vonmises(p.r_kappa);
+  } else {
+    StreamF rngf(ctl.seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull, static_cast<uint32_t>(qidx),
+                 (static_cast<uint32_t>(qidx >> 32) ^ 0xF32Au) + (static_cast<uint32_t>(slot) << 20),
+                 static_cast<uint32_t>(ctr));
+    float f0, f1, f2, f3;
+#ifdef ASVRL_DBG_NO_NOISE
+    f0 = f1 = f2 = f3 = 0.f;
+    if (VM) { n4 = 0.0; }
+    n0 = f0; n1 = f1; n2 = f2; n3 = f3; return;
+#endif
+    rngf.normal4(f0, f1, f2, f3);
+#ifdef ASVRL_DBG_NO_VM
+    n0 = f0 * p.pos_std; n1 = f1 * p.pos_std; n2 = f2 * p.vel_std; n3 = f3 * p.vel_std; if (VM) n4 = 0.0; return;
+#endif
+    n0 = f0 * p.pos_std; n1 = f1 * p.pos_std; n2 = f2 * p.vel_std; n3 = f3 * p.vel_std;
+    if (VM) n4 = rngf.vonmises(static_cast<float>(p.r_kappa));
+  }
+}
+
+// Per-robot sweep (AsvEnvLaunch layout 2): one lane per robot, BLOCK / R whole envs per workgroup;
+// perception is one serial loop over the robot's candidates (wamv.py:478-511), top-5 kept in registers.
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void env_sweep_kernel(AsvParams p, AsvEnvState s,
                                                           const double* __restrict__ actions,
                                                           const double* __restrict__ noise,
-                                                          AsvStepCtl ctl, AsvStepOut out, int epb_arg) {
+                                                          AsvStepCtl ctl, AsvStepOut out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int R = s.max_robots;
   const int O = s.max_obs;
-  const int epb = PAIRS ? epb_arg : BLOCK / R;
-  const int S = O + R;               // candidate slots per robot (obstacles, then robots)
-  const int npairs = PAIRS ? epb * R * S : 0;
+  const int epb = BLOCK / R;
   const int tid = threadIdx.x;
   const int le = tid / R;
   const int i = tid - le * R;
@@ -228,25 +361,15 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(AsvParams p, AsvEnvStat
   const size_t NT = static_cast<size_t>(s.n_envs) * R;
   const size_t idx = static_cast<size_t>(e) * R + i;
 
-  // LDS carve (16-B aligned pieces): positions/velocities of the block's robots after the
-  // move, their pre-step deactivated flags, the envs' obstacles and per-env reductions.
+  // LDS carve: positions/velocities of the block's robots after the move, their pre-step
+  // deactivated flags, the envs' obstacles and per-env reductions.
   double* sx = reinterpret_cast<double*>(smem);
   double* sy = sx + BLOCK;
   double* sv0 = sy + BLOCK;
   double* sv1 = sv0 + BLOCK;
-  double* scs = sv1 + BLOCK;                 // PAIRS: robot frame cos, sin, translation
-  double* ssn = scs + (PAIRS ? BLOCK : 0);
-  double* stx = ssn + (PAIRS ? BLOCK : 0);
-  double* sty = stx + (PAIRS ? BLOCK : 0);
-  double* pk = sty + (PAIRS ? BLOCK : 0);    // PAIRS: [npairs] sort key, [npairs][5] candidate row
-  double* pc = pk + npairs;
-  double* sob = pc + 5 * static_cast<size_t>(npairs);  // [epb][O][3]
+  double* sob = sv1 + BLOCK;                 // [epb][O][3]
   int* salive = reinterpret_cast<int*>(sob + static_cast<size_t>(epb) * O * 3);  // [epb]
-  int* sno = salive + epb;                   // PAIRS: [epb] obstacles, robots of each env
-  int* snr = sno + (PAIRS ? epb : 0);
-  unsigned char* soff = reinterpret_cast<unsigned char*>(snr + (PAIRS ? epb : 0));  // [BLOCK]
-  unsigned char* sact = soff + BLOCK;        // PAIRS: [BLOCK] robot active; [npairs] detected | 2 * collision
-  unsigned char* pfl = sact + (PAIRS ? BLOCK : 0);
+  unsigned char* soff = reinterpret_cast<unsigned char*>(salive + epb);         // [BLOCK]
 
   Regs r{};
   uint8_t fl = 0;
@@ -308,114 +431,8 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(AsvParams p, AsvEnvStat
       }
     }
     if (i == 0) salive[le] = 0;
-    if (PAIRS && i == 0) {
-      sno[le] = s.n_obs[e];
-      snr[le] = nrob;
-    }
-  }
-  if constexpr (PAIRS) {
-    sact[tid] = active ? 1 : 0;
-    if (active) {
-      double sn_, cs_;
-      sincos(r.th, &sn_, &cs_);
-      scs[tid] = cs_;
-      ssn[tid] = sn_;
-      stx[tid] = -(cs_ * r.x + sn_ * r.y);
-      sty[tid] = -(-sn_ * r.x + cs_ * r.y);
-    }
   }
   __syncthreads();
-
-  if constexpr (PAIRS) {
-    // ---------------- phase 2a: one (robot, candidate) pair per lane (wamv.py:478-511)
-    const uint64_t ctr = ctl.counter + (ctl.counter_dev != nullptr ? *ctl.counter_dev : 0ull);
-    const bool full_circle = 0.5 * p.angle >= kPi;
-    for (int q = tid; q < npairs; q += BLOCK) {
-      const int qe = q / (R * S);
-      const int rem = q - qe * R * S;
-      const int qi = rem / S;
-      const int c = rem - qi * S;
-      const int qt = qe * R + qi;
-      unsigned char flag = 0;
-      double key = INFINITY, ca = 0, cb = 0, cc = 0, cd = 0, ce = 0;
-      bool valid = false;
-      double ox = 0, oy = 0, orad = 0, vx0 = 0, vy0 = 0;
-      if (sact[qt]) {
-        if (c < O) {
-          valid = c < sno[qe];
-          if (valid) {
-            const double* ob = sob + (static_cast<size_t>(qe) * O + c) * 3;
-            ox = ob[0];
-            oy = ob[1];
-            orad = ob[2];
-          }
-        } else {
-          const int j = c - O;
-          valid = j < snr[qe] && j != qi && !soff[qe * R + j];   // self / deactivated (wamv.py:487-491)
-          if (valid) {
-            ox = sx[qe * R + j];
-            oy = sy[qe * R + j];
-            orad = p.r;
-            vx0 = sv0[qe * R + j];
-            vy0 = sv1[qe * R + j];
-          }
-        }
-      }
-      if (valid) {
-        const size_t qidx = static_cast<size_t>(blockIdx.x * epb + qe) * R + qi;
-        double n0, n1, n2, n3, n4;
-        if (ctl.noise_mode == 0) {
-          const double* nz = noise + (qidx * static_cast<size_t>(O + R) + c) * 5;
-          n0 = nz[0]; n1 = nz[1]; n2 = nz[2]; n3 = nz[3]; n4 = nz[4];
-        } else if (ctl.noise_mode == 1) {
-          Stream rng(ctl.seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull, static_cast<uint32_t>(qidx),
-                     (static_cast<uint32_t>(qidx >> 32) ^ 0x5EEDu) + (static_cast<uint32_t>(c) << 20),
-                     static_cast<uint32_t>(ctr));
-          rng.normal2(n0, n1);
-          rng.normal2(n2, n3);
-          n0 *= p.pos_std; n1 *= p.pos_std; n2 *= p.vel_std; n3 *= p.vel_std;
-          n4 = rng.vonmises(p.r_kappa);
-        } else {
-          StreamF rngf(ctl.seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull, static_cast<uint32_t>(qidx),
-                       (static_cast<uint32_t>(qidx >> 32) ^ 0xF32Au) + (static_cast<uint32_t>(c) << 20),
-                       static_cast<uint32_t>(ctr));
-          float f0, f1, f2, f3;
-          rngf.normal2(f0, f1);
-          rngf.normal2(f2, f3);
-          n0 = f0 * p.pos_std; n1 = f1 * p.pos_std; n2 = f2 * p.vel_std; n3 = f3 * p.vel_std;
-          n4 = rngf.vonmises(static_cast<float>(p.r_kappa));
-        }
-        const double cs = scs[qt], sn = ssn[qt], tx = stx[qt], ty = sty[qt];
-        const double pxn = ox + n0, pyn = oy + n1;  // Perception (wamv.py:27-40)
-        const double vxn = vx0 + n2, vyn = vy0 + n3;
-        const double rn = p.r_mean_ratio * orad + (1 - p.r_mean_ratio) * n4 / kPi * orad;
-        const double qx = (cs * pxn + sn * pyn) + tx, qy = (-sn * pxn + cs * pyn) + ty;
-        const double qn = sqrt(qx * qx + qy * qy);
-        bool det = qn <= p.range + rn;  // check_detection (wamv.py:293-303)
-        if (det && !full_circle) {
-          const double ang = atan2(qy, qx);
-          det = !(ang < -0.5 * p.angle || ang > 0.5 * p.angle);
-        }
-        if (det) {
-          flag = 1;
-          const double rx = sx[qt], ry = sy[qt];   // check_collision (wamv.py:281-291), true positions
-          const double d = sqrt((rx - ox) * (rx - ox) + (ry - oy) * (ry - oy)) - orad - p.r;
-          if (d <= 0.0) flag |= 2;
-          key = qn - rn - p.r;
-          ca = qx;
-          cb = qy;
-          cc = cs * vxn + sn * vyn;
-          cd = -sn * vxn + cs * vyn;
-          ce = rn;
-        }
-      }
-      pk[q] = key;
-      double* row = pc + 5 * static_cast<size_t>(q);
-      row[0] = ca; row[1] = cb; row[2] = cc; row[3] = cd; row[4] = ce;
-      pfl[q] = flag;
-    }
-    __syncthreads();
-  }
 
   // ---------------- phase 2: perception_output (wamv.py:436-529)
   bool coll = (fl & ASVRL_FLAG_COLLISION) != 0;
@@ -426,17 +443,10 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(AsvParams p, AsvEnvStat
   Cand t0{INFINITY, 0, 0, 0, 0, 0}, t1 = t0, t2 = t0, t3 = t0, t4 = t0;
   double so0 = 0, so1 = 0, so2 = 0, so3 = 0, so4 = 0;
   if (active) {
-    double sn, cs, tx, ty;
-    if constexpr (PAIRS) {
-      cs = scs[tid];
-      sn = ssn[tid];
-      tx = stx[tid];
-      ty = sty[tid];
-    } else {
-      sincos(r.th, &sn, &cs);
-      tx = -(cs * r.x + sn * r.y);
-      ty = -(-sn * r.x + cs * r.y);
-    }
+    double sn, cs;
+    sincos(r.th, &sn, &cs);
+    const double tx = -(cs * r.x + sn * r.y);
+    const double ty = -(-sn * r.x + cs * r.y);
     so0 = (cs * gx + sn * gy) + tx;
     so1 = (-sn * gx + cs * gy) + ty;
     so2 = cs * r.v0 + sn * r.v1;
@@ -445,27 +455,8 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(AsvParams p, AsvEnvStat
     if (sqrt((gx - r.x) * (gx - r.x) + (gy - r.y) * (gy - r.y)) <= p.goal_dis) reach = true;
 
     int nkept = 0;
-    if constexpr (PAIRS) {
-      // ---------------- phase 2b: the robot's candidates in the reference's order
-      const int q0 = tid * S;
-      for (int c = 0; c < S; ++c) {
-        const unsigned char f = pfl[q0 + c];
-        if (!(f & 1)) continue;
-        if (f & 2) coll = true;
-        const double* row = pc + 5 * static_cast<size_t>(q0 + c);
-        Cand cd{pk[q0 + c], row[0], row[1], row[2], row[3], row[4]};
-        cswap(cd.key < t0.key, cd, t0);
-        cswap(cd.key < t1.key, cd, t1);
-        cswap(cd.key < t2.key, cd, t2);
-        cswap(cd.key < t3.key, cd, t3);
-        cswap(cd.key < t4.key, cd, t4);
-        ++nkept;
-      }
-    } else {
     const int no = s.n_obs[e];
     const int base = le * R;
-    const double* nz_base =
-        noise != nullptr ? noise + idx * static_cast<size_t>(O + R) * 5 : nullptr;
     const uint64_t ctr = ctl.counter + (ctl.counter_dev != nullptr ? *ctl.counter_dev : 0ull);
     const int ncand = no + nrob;
     const bool full_circle = 0.5 * p.angle >= kPi;
@@ -491,28 +482,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(AsvParams p, AsvEnvStat
         slot = O + j;
       }
       double n0, n1, n2, n3, n4;
-      if (ctl.noise_mode == 0) {
-        const double* nz = nz_base + slot * 5;
-        n0 = nz[0]; n1 = nz[1]; n2 = nz[2]; n3 = nz[3]; n4 = nz[4];
-      } else if (ctl.noise_mode == 1) {
-        // the pair layout's substream of (robot, candidate slot): both layouts draw the same noise
-        Stream rng(ctl.seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull, static_cast<uint32_t>(idx),
-                   (static_cast<uint32_t>(idx >> 32) ^ 0x5EEDu) + (static_cast<uint32_t>(slot) << 20),
-                   static_cast<uint32_t>(ctr));
-        rng.normal2(n0, n1);
-        rng.normal2(n2, n3);
-        n0 *= p.pos_std; n1 *= p.pos_std; n2 *= p.vel_std; n3 *= p.vel_std;
-        n4 = rng.vonmises(p.r_kappa);
-      } else {
-        StreamF rngf(ctl.seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull, static_cast<uint32_t>(idx),
-                     (static_cast<uint32_t>(idx >> 32) ^ 0xF32Au) + (static_cast<uint32_t>(slot) << 20),
-                     static_cast<uint32_t>(ctr));
-        float f0, f1, f2, f3;
-        rngf.normal2(f0, f1);
-        rngf.normal2(f2, f3);
-        n0 = f0 * p.pos_std; n1 = f1 * p.pos_std; n2 = f2 * p.vel_std; n3 = f3 * p.vel_std;
-        n4 = rngf.vonmises(static_cast<float>(p.r_kappa));
-      }
+      draw_noise<-1>(p, ctl, ctr, noise, idx, slot, O + R, n0, n1, n2, n3, n4);
       const double pxn = ox + n0, pyn = oy + n1;  // Perception (wamv.py:27-40)
       const double vxn = vx0 + n2, vyn = vy0 + n3;
       const double rn = p.r_mean_ratio * orad + (1 - p.r_mean_ratio) * n4 / kPi * orad;
@@ -536,7 +506,6 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(AsvParams p, AsvEnvStat
       cswap(cd.key < t4.key, cd, t4);
       ++nkept;
     }
-    }
     cnt = nkept < p.max_obj_num ? nkept : p.max_obj_num;
     // COLREGs over the kept objects in order, stop at the first hit (wamv.py:517-521)
 #ifndef ASVRL_NO_COLREGS
@@ -548,48 +517,9 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(AsvParams p, AsvEnvStat
 #endif
   }
 
-  // ---------------- reward / done / info (env.py:290-331)
-  uint8_t done = 1, info = ASVRL_INFO_ABSENT;
-  if (exists) {
-    if (deact) {
-      reward = 0.0;
-      done = 1;
-      info = coll ? ASVRL_INFO_DEACT_COLLISION : (reach ? ASVRL_INFO_DEACT_GOAL : ASVRL_INFO_ABSENT);
-    } else if (ctl.do_dynamics) {
-      double pen = 0.0;
-      if (apply) pen += p.COLREGs_penalty * phi;
-      reward += pen;
-      if (ep_ts >= p.episode_limit) {
-        done = 1;
-        info = ASVRL_INFO_TOO_LONG;
-      } else if (coll) {
-        reward += p.collision_penalty;
-        done = 1;
-        info = ASVRL_INFO_COLLISION;
-      } else if (reach) {
-        reward += p.goal_reward;
-        done = 1;
-        info = ASVRL_INFO_REACH_GOAL;
-      } else {
-        done = 0;
-        info = ASVRL_INFO_NORMAL;
-      }
-    } else {
-      done = 0;
-      info = ASVRL_INFO_NORMAL;
-    }
-  }
-
-  // ---------------- trainer-side bookkeeping (trainer.py:157-172), fused
-  uint8_t nfl = static_cast<uint8_t>((fl & ASVRL_FLAG_DEACTIVATED) | (coll ? ASVRL_FLAG_COLLISION : 0) |
-                                     (reach ? ASVRL_FLAG_REACH_GOAL : 0) | (apply ? ASVRL_FLAG_COLREGS : 0));
-  double ret = 0.0;
-  if (exists) ret = s.rs[ASVRL_F_RET * NT + idx];
-  if (active && ctl.do_dynamics && ctl.trainer_deactivate) {
-    if (ctl.gamma > 0) ret += pow(ctl.gamma, static_cast<double>(ep_ts)) * reward;
-    if (coll || reach) nfl |= ASVRL_FLAG_DEACTIVATED;
-  }
-  if (ctl.trainer_deactivate && ctl.do_dynamics && exists && !(nfl & ASVRL_FLAG_DEACTIVATED))
+  const StepResult res = step_result(p, ctl, exists, deact, active, ep_ts, fl, coll, reach, apply, phi, reward,
+                                     exists ? s.rs[ASVRL_F_RET * NT + idx] : 0.0);
+  if (ctl.trainer_deactivate && ctl.do_dynamics && exists && !(res.nfl & ASVRL_FLAG_DEACTIVATED))
     atomicAdd(&salive[le], 1);
 
   // ---------------- write back
@@ -607,10 +537,10 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(AsvParams p, AsvEnvStat
       rs[ASVRL_F_V2 * NT + idx] = r.v2;
       rs[ASVRL_F_TL * NT + idx] = r.tl;
       rs[ASVRL_F_TR * NT + idx] = r.tr;
-      rs[ASVRL_F_RET * NT + idx] = ret;
+      rs[ASVRL_F_RET * NT + idx] = res.ret;
     }
     rs[ASVRL_F_PHI * NT + idx] = phi;
-    s.rflags[idx] = nfl;
+    s.rflags[idx] = res.nfl;
   }
   if (env_on && i < R) {
     // packed f32 obs row (replay_buffer.py:51-69 + the .float() of agent.py:363-366)
@@ -644,36 +574,432 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(AsvParams p, AsvEnvStat
       }
     }
     out.obj_cnt[idx] = static_cast<int8_t>(exists ? cnt : -1);
-    out.reward[idx] = reward;
-    out.done[idx] = done;
-    out.info[idx] = info;
+    out.reward[idx] = res.reward;
+    out.done[idx] = res.done;
+    out.info[idx] = res.info;
   }
   __syncthreads();
-  if (env_on && i == 0 && ctl.do_dynamics) {
-    s.ep_ts[e] = ep_ts + 1;  // env.py:330
-    if (ctl.trainer_deactivate && out.env_done != nullptr) {
-      const bool end = (ep_ts >= p.episode_limit) || salive[le] == 0;  // trainer.py:172
-      out.env_done[e] = end ? 1 : 0;
-      if (end && out.stats != nullptr) {
-        double sr = 0, sc = 0, sg = 0, sk = 0, st = 0;
-        for (int j = 0; j < nrob; ++j) {
-          const size_t jd = static_cast<size_t>(e) * R + j;
-          const uint8_t fj = s.rflags[jd];
-          sr += s.rs[ASVRL_F_RET * NT + jd];
-          sc += 1;
-          sg += (fj & ASVRL_FLAG_REACH_GOAL) ? 1 : 0;
-          sk += (fj & ASVRL_FLAG_COLLISION) ? 1 : 0;
-          st += (fj & ASVRL_FLAG_DEACTIVATED) ? 0 : 1;
-        }
-        atomicAdd(out.stats + 0, sr);
-        atomicAdd(out.stats + 1, sc);
-        atomicAdd(out.stats + 2, sg);
-        atomicAdd(out.stats + 3, sk);
-        atomicAdd(out.stats + 4, st);
-        atomicAdd(out.stats + 5, 1.0);
+  if (env_on && i == 0 && ctl.do_dynamics) env_end(p, s, ctl, out, e, ep_ts, nrob, salive[le], NT);
+}
+
+// Pair-parallel env step (AsvEnvLaunch layout 1). A workgroup owns `epb` whole envs; their robots
+// occupy its first nrb = epb * R lanes. Phases, each over all lanes, separated by workgroup barriers:
+//   1  robot lanes: N Fossen substeps in registers, state written back, the observation's self part,
+//      the robot's frame, position and velocity into LDS
+//   2  one lane per (robot, candidate slot) pair: noise, detection, collision, sort key -- 13 B per
+//      pair in LDS (key, von Mises draw, flag; 17 B with f64 draws)
+//   3  robot lanes: the stable top-5 of the keys in the reference's order (slot indices only), collision
+//      as an OR
+//   4  one lane per kept object (a work list built by a scan of the counts): the object's row
+//      recomputed from the same noise draw and arithmetic as in phase 2 (bit-identical; the von Mises
+//      radius draw kept from phase 2, the Gaussians redrawn), written into the observation; its
+//      COLREGs test
+//   5  robot lanes: the first COLREGs hit in order and the phi the reference's serial chain leaves,
+//      reward / done / info, trainer bookkeeping; then the per-env episode end
+// No phase keeps another's values in registers and LDS holds ~15 KB per 12-env workgroup, so several
+// workgroups share a CU (the round-1 form kept 40-B rows per pair and the top-5 rows in registers:
+// 239 VGPRs, 35 KB, two waves per SIMD).
+#ifndef ASVRL_ENV_PAIRS_WPE
+#define ASVRL_ENV_PAIRS_WPE 4
+#endif
+template <int BLOCK, int NM>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NM == 1 ? 1 : ASVRL_ENV_PAIRS_WPE))) void env_pairs_kernel(AsvParams p, AsvEnvState s,
+                                                          const double* __restrict__ actions,
+                                                          const double* __restrict__ noise,
+                                                          AsvStepCtl ctl, AsvStepOut out, int epb) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int R = s.max_robots;
+  const int O = s.max_obs;
+  const int S = O + R;               // candidate slots per robot (obstacles, then robots)
+  const int nrb = epb * R;
+  const int npairs = nrb * S;
+  const int nslot = npairs > 5 * nrb ? npairs : 5 * nrb;
+  const int tid = threadIdx.x;
+
+  double* sx = reinterpret_cast<double*>(smem);   // [nrb] robots after the move
+  double* sy = sx + nrb;
+  double* sv0 = sy + nrb;
+  double* sv1 = sv0 + nrb;
+  double* scs = sv1 + nrb;           // robot frame: cos, sin, translation
+  double* ssn = scs + nrb;
+  double* stx = ssn + nrb;
+  double* sty = stx + nrb;
+  double* pk = sty + nrb;            // [nslot] phase 2 sort keys; phase 4 phi of (robot, k)
+  double* sob = pk + nslot;          // [epb][O][3]
+  using VmT = typename std::conditional<NM == 2, float, double>::type;   // the f32 stream's draw is a float
+  VmT* pvm = reinterpret_cast<VmT*>(sob + static_cast<size_t>(epb) * O * 3);  // [npairs] von Mises radius draws
+  int* salive = reinterpret_cast<int*>(pvm + npairs);  // [epb]
+  int* sno = salive + epb;           // [epb] obstacles, robots of each env
+  int* snr = sno + epb;
+  int* swt = snr + epb;              // [BLOCK / 64] kept objects per wave (phase 3 scan)
+  unsigned short* skept = reinterpret_cast<unsigned short*>(swt + BLOCK / kWave);  // [nrb][5] kept slots in order
+  unsigned short* sitem = skept + 5 * nrb;   // [5 * nrb] phase 4 work list: robot * 5 + k of every kept object
+  unsigned char* pfl = reinterpret_cast<unsigned char*>(sitem + 5 * nrb);  // [nslot] 1 detected | 2 collision; phase 4: 1 evaluated | 2 hit
+  unsigned char* soff = pfl + nslot;   // [nrb] not a candidate (absent / deactivated before the step)
+  unsigned char* sact = soff + nrb;    // [nrb] active
+  signed char* scnt = reinterpret_cast<signed char*>(sact + nrb);  // [nrb] kept count, -1 inactive
+
+  const bool rlane = tid < nrb;
+  const int le = tid / R;
+  const int i = tid - le * R;
+  const int e = blockIdx.x * epb + le;
+  const bool lane_env = rlane && e < s.n_envs;
+  const bool env_on = lane_env && (ctl.env_mask == nullptr || ctl.env_mask[e] != 0);
+  const int nrob = lane_env ? s.n_robots[e] : 0;
+  const bool exists = env_on && i < nrob;
+  const size_t NT = static_cast<size_t>(s.n_envs) * R;
+  const size_t idx = static_cast<size_t>(e) * R + i;
+  const uint8_t fl = exists ? s.rflags[idx] : 0;
+  const bool deact = (fl & ASVRL_FLAG_DEACTIVATED) != 0;
+  const bool active = exists && !deact;
+  const int ep_ts = env_on ? s.ep_ts[e] : 0;
+  bool coll = (fl & ASVRL_FLAG_COLLISION) != 0;
+  bool reach = (fl & ASVRL_FLAG_REACH_GOAL) != 0;
+  double reward = 0.0;
+
+  // ---------------- phase 1: dynamics (env.py:247-277), the observation's self part
+  {
+    Regs r{};
+    double gx = 0, gy = 0;
+    if (exists) {
+      const double* rs = s.rs;
+      r.x = rs[ASVRL_F_X * NT + idx];
+      r.y = rs[ASVRL_F_Y * NT + idx];
+      r.th = rs[ASVRL_F_THETA * NT + idx];
+      r.vr0 = rs[ASVRL_F_VR0 * NT + idx];
+      r.vr1 = rs[ASVRL_F_VR1 * NT + idx];
+      r.vr2 = rs[ASVRL_F_VR2 * NT + idx];
+      r.v0 = rs[ASVRL_F_V0 * NT + idx];
+      r.v1 = rs[ASVRL_F_V1 * NT + idx];
+      r.v2 = rs[ASVRL_F_V2 * NT + idx];
+      r.tl = rs[ASVRL_F_TL * NT + idx];
+      r.tr = rs[ASVRL_F_TR * NT + idx];
+      r.lp = rs[ASVRL_F_LP * NT + idx];
+      r.rp = rs[ASVRL_F_RP * NT + idx];
+      gx = rs[ASVRL_F_GX * NT + idx];
+      gy = rs[ASVRL_F_GY * NT + idx];
+    }
+    if (active && ctl.do_dynamics) {
+      const double d_before = sqrt((gx - r.x) * (gx - r.x) + (gy - r.y) * (gy - r.y));
+      const int nc = s.n_cores[e];
+      const double* cores = s.cores + static_cast<size_t>(e) * s.max_cores * 4;
+      robot_act(p, r, actions[2 * idx], actions[2 * idx + 1], ctl.is_continuous, cores,
+                nc < s.max_cores ? nc : s.max_cores);
+      const double d_after = sqrt((gx - r.x) * (gx - r.x) + (gy - r.y) * (gy - r.y));
+      reward = 0.0;
+      reward += p.timestep_penalty;
+      reward += d_before - d_after;
+    }
+    if (exists && ctl.do_dynamics) {
+      double* rs = s.rs;
+      rs[ASVRL_F_X * NT + idx] = r.x;
+      rs[ASVRL_F_Y * NT + idx] = r.y;
+      rs[ASVRL_F_THETA * NT + idx] = r.th;
+      rs[ASVRL_F_VR0 * NT + idx] = r.vr0;
+      rs[ASVRL_F_VR1 * NT + idx] = r.vr1;
+      rs[ASVRL_F_VR2 * NT + idx] = r.vr2;
+      rs[ASVRL_F_V0 * NT + idx] = r.v0;
+      rs[ASVRL_F_V1 * NT + idx] = r.v1;
+      rs[ASVRL_F_V2 * NT + idx] = r.v2;
+      rs[ASVRL_F_TL * NT + idx] = r.tl;
+      rs[ASVRL_F_TR * NT + idx] = r.tr;
+    }
+    double so0 = 0, so1 = 0, so2 = 0, so3 = 0, so4 = 0;
+    if (rlane) {
+      sx[tid] = r.x;
+      sy[tid] = r.y;
+      sv0[tid] = r.v0;
+      sv1[tid] = r.v1;
+      soff[tid] = exists ? (deact ? 1 : 0) : 1;
+      sact[tid] = active ? 1 : 0;
+    }
+    if (active) {
+      double sn, cs;
+      sincos(r.th, &sn, &cs);
+      const double tx = -(cs * r.x + sn * r.y);
+      const double ty = -(-sn * r.x + cs * r.y);
+      scs[tid] = cs;
+      ssn[tid] = sn;
+      stx[tid] = tx;
+      sty[tid] = ty;
+      so0 = (cs * gx + sn * gy) + tx;
+      so1 = (-sn * gx + cs * gy) + ty;
+      so2 = cs * r.v0 + sn * r.v1;
+      so3 = -sn * r.v0 + cs * r.v1;
+      so4 = r.v2;
+      if (sqrt((gx - r.x) * (gx - r.x) + (gy - r.y) * (gy - r.y)) <= p.goal_dis) reach = true;
+    }
+    if (env_on) {   // packed f32 obs row, self part (replay_buffer.py:51-69 + the .float() of agent.py:363-366)
+      float* of = out.obs + idx * ASVRL_OBS_DIM;
+      const bool a = active;
+      *reinterpret_cast<float4*>(of) = a ? make_float4(static_cast<float>(so0), static_cast<float>(so1),
+                                                        static_cast<float>(so2), static_cast<float>(so3))
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+      of[4] = a ? static_cast<float>(so4) : 0.f;
+      of[5] = a ? static_cast<float>(r.tl) : 0.f;
+      of[6] = a ? static_cast<float>(r.tr) : 0.f;
+      if (out.obs64 != nullptr) {
+        double* o = out.obs64 + idx * 32;
+        o[0] = a ? so0 : 0.0;
+        o[1] = a ? so1 : 0.0;
+        o[2] = a ? so2 : 0.0;
+        o[3] = a ? so3 : 0.0;
+        o[4] = a ? so4 : 0.0;
+        o[5] = a ? r.tl : 0.0;
+        o[6] = a ? r.tr : 0.0;
       }
     }
   }
+  if (env_on) {
+    const int no = s.n_obs[e];
+    for (int k = i; k < O; k += R) {
+      const double* ob = s.obstacles + (static_cast<size_t>(e) * O + k) * 3;
+      double* dst = sob + (static_cast<size_t>(le) * O + k) * 3;
+      if (k < no) {
+        dst[0] = ob[0];
+        dst[1] = ob[1];
+        dst[2] = ob[2];
+      }
+    }
+    if (i == 0) {
+      salive[le] = 0;
+      sno[le] = no;
+      snr[le] = nrob;
+    }
+  }
+  __syncthreads();
+
+  // candidate slot c of robot qi in local env qe: obstacles first, then robots (self, deactivated and
+  // absent ones are not candidates, wamv.py:487-491)
+  auto candidate = [&](int qe, int qi, int c, double& ox, double& oy, double& orad, double& vx0, double& vy0) {
+    if (c < O) {
+      if (c >= sno[qe]) return false;
+      const double* ob = sob + (static_cast<size_t>(qe) * O + c) * 3;
+      ox = ob[0];
+      oy = ob[1];
+      orad = ob[2];
+      vx0 = 0.0;
+      vy0 = 0.0;
+      return true;
+    }
+    const int j = c - O;
+    if (!(j < snr[qe] && j != qi && !soff[qe * R + j])) return false;
+    ox = sx[qe * R + j];
+    oy = sy[qe * R + j];
+    orad = p.r;
+    vx0 = sv0[qe * R + j];
+    vy0 = sv1[qe * R + j];
+    return true;
+  };
+  const uint64_t ctr = ctl.counter + (ctl.counter_dev != nullptr ? *ctl.counter_dev : 0ull);
+  const bool full_circle = 0.5 * p.angle >= kPi;
+
+  // ---------------- phase 2: one (robot, candidate) pair per lane (wamv.py:478-511)
+  for (int q = tid; q < npairs; q += BLOCK) {
+    const int qr = q / S;
+    const int c = q - qr * S;
+    const int qe = qr / R;
+    const int qi = qr - qe * R;
+    unsigned char flag = 0;
+    double key = INFINITY;
+    double ox = 0, oy = 0, orad = 0, vx0 = 0, vy0 = 0;
+    if (sact[qr] && candidate(qe, qi, c, ox, oy, orad, vx0, vy0)) {
+      const size_t qidx = static_cast<size_t>(blockIdx.x * epb + qe) * R + qi;
+      double n0, n1, n2, n3, n4;
+      draw_noise<NM>(p, ctl, ctr, noise, qidx, c, S, n0, n1, n2, n3, n4);
+      pvm[q] = static_cast<VmT>(n4);
+      const double cs = scs[qr], sn = ssn[qr], tx = stx[qr], ty = sty[qr];
+      const double pxn = ox + n0, pyn = oy + n1;  // Perception (wamv.py:27-40)
+      const double rn = p.r_mean_ratio * orad + (1 - p.r_mean_ratio) * n4 / kPi * orad;
+      const double qx = (cs * pxn + sn * pyn) + tx, qy = (-sn * pxn + cs * pyn) + ty;
+      const double qn = sqrt(qx * qx + qy * qy);
+      bool det = qn <= p.range + rn;  // check_detection (wamv.py:293-303)
+      if (det && !full_circle) {
+        const double ang = atan2(qy, qx);
+        det = !(ang < -0.5 * p.angle || ang > 0.5 * p.angle);
+      }
+      if (det) {
+        flag = 1;
+        const double rx = sx[qr], ry = sy[qr];   // check_collision (wamv.py:281-291), true positions
+        const double d = sqrt((rx - ox) * (rx - ox) + (ry - oy) * (ry - oy)) - orad - p.r;
+        if (d <= 0.0) flag |= 2;
+        key = qn - rn - p.r;
+      }
+    }
+    pk[q] = key;
+    pfl[q] = flag;
+  }
+  __syncthreads();
+
+  // ---------------- phase 3: the robot's candidates in the reference's order (wamv.py:512-516)
+  int cnt = -1;
+  if (active) {
+    double k0 = INFINITY, k1 = INFINITY, k2 = INFINITY, k3 = INFINITY, k4 = INFINITY;
+    int c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0;
+    int nkept = 0;
+    const int q0 = tid * S;
+    for (int c = 0; c < S; ++c) {
+      const unsigned char f = pfl[q0 + c];
+      if (!(f & 1)) continue;
+      if (f & 2) coll = true;
+      double kc = pk[q0 + c];
+      int cc = c;
+      // heapq.nsmallest == stable ascending order: a new candidate passes equal keys
+      auto ins = [&](double& kk, int& ck) {
+        if (kc < kk) {
+          const double tk = kk;
+          const int tc = ck;
+          kk = kc;
+          ck = cc;
+          kc = tk;
+          cc = tc;
+        }
+      };
+      ins(k0, c0);
+      ins(k1, c1);
+      ins(k2, c2);
+      ins(k3, c3);
+      ins(k4, c4);
+      ++nkept;
+    }
+    cnt = nkept < p.max_obj_num ? nkept : p.max_obj_num;
+    unsigned short* kp = skept + 5 * tid;
+    kp[0] = static_cast<unsigned short>(c0);
+    kp[1] = static_cast<unsigned short>(c1);
+    kp[2] = static_cast<unsigned short>(c2);
+    kp[3] = static_cast<unsigned short>(c3);
+    kp[4] = static_cast<unsigned short>(c4);
+  }
+  if (rlane) scnt[tid] = static_cast<signed char>(cnt);
+  // phase 4's work list: the kept objects only (about half of the 5 * nrb (robot, k) slots), placed by
+  // a workgroup scan of the counts in robot order
+  const int lane = tid & (kWave - 1);
+  int kin = cnt > 0 ? cnt : 0;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const int t = __shfl_up(kin, d);
+    if (lane >= d) kin += t;
+  }
+  if (lane == kWave - 1) swt[tid / kWave] = kin;
+  __syncthreads();
+  int nitem = 0, ibase = 0;
+#pragma unroll
+  for (int w = 0; w < BLOCK / kWave; ++w) {
+    ibase += w < tid / kWave ? swt[w] : 0;
+    nitem += swt[w];
+  }
+  if (cnt > 0) {
+    const int off = ibase + kin - cnt;
+    for (int k = 0; k < cnt; ++k) sitem[off + k] = static_cast<unsigned short>(5 * tid + k);
+  }
+  __syncthreads();
+
+  // ---------------- phase 4: one lane per kept object: its observation row and COLREGs test
+#ifdef ASVRL_DBG_NO_P4
+  if (ctl.seed != 12345) {} else
+#endif
+  for (int it = tid; it < nitem; it += BLOCK) {
+    const int kq = sitem[it];
+    const int qr = kq / 5;
+    const int k = kq - 5 * qr;
+    const int qe = qr / R;
+    const int qi = qr - qe * R;
+    const int e2 = blockIdx.x * epb + qe;
+    unsigned char cf = 0;
+    double ph = 0.0;
+    {
+      const size_t qidx = static_cast<size_t>(e2) * R + qi;
+      double ra, rb, rc, rd, re;
+      {
+        const int c = skept[kq];
+        double ox = 0, oy = 0, orad = 0, vx0 = 0, vy0 = 0;
+        candidate(qe, qi, c, ox, oy, orad, vx0, vy0);
+        double n0, n1, n2, n3, n4 = static_cast<double>(pvm[qr * S + c]);
+        draw_noise<NM, false>(p, ctl, ctr, noise, qidx, c, S, n0, n1, n2, n3, n4);
+        const double cs = scs[qr], sn = ssn[qr], tx = stx[qr], ty = sty[qr];
+        const double pxn = ox + n0, pyn = oy + n1;  // as phase 2
+        const double vxn = vx0 + n2, vyn = vy0 + n3;
+        const double rn = p.r_mean_ratio * orad + (1 - p.r_mean_ratio) * n4 / kPi * orad;
+        ra = (cs * pxn + sn * pyn) + tx;
+        rb = (-sn * pxn + cs * pyn) + ty;
+        rc = cs * vxn + sn * vyn;
+        rd = -sn * vxn + cs * vyn;
+        re = rn;
+#ifndef ASVRL_NO_COLREGS
+        bool ev;
+        const bool hit = colregs_ev(p.r, cs, sn, sv0[qr], sv1[qr], ra, rb, rc, rd, re, ph, ev);
+        cf = static_cast<unsigned char>((ev ? 1 : 0) | (hit ? 2 : 0));
+#endif
+      }
+      float* of = out.obs + qidx * ASVRL_OBS_DIM + 7 + 5 * k;
+      of[0] = static_cast<float>(ra);
+      of[1] = static_cast<float>(rb);
+      of[2] = static_cast<float>(rc);
+      of[3] = static_cast<float>(rd);
+      of[4] = static_cast<float>(re);
+      if (out.obs64 != nullptr) {
+        double* o = out.obs64 + qidx * 32 + 7 + 5 * k;
+        o[0] = ra;
+        o[1] = rb;
+        o[2] = rc;
+        o[3] = rd;
+        o[4] = re;
+      }
+    }
+    pfl[kq] = cf;
+    pk[kq] = ph;
+  }
+  __syncthreads();
+
+  // ---------------- phase 5: COLREGs in order (wamv.py:517-521), reward / done / info, bookkeeping
+  bool apply = false;
+  double phi = exists ? s.rs[ASVRL_F_PHI * NT + idx] : 0.0;
+  for (int k = 0; k < cnt; ++k) {   // the serial chain: phi of every evaluated object up to the first hit
+    const unsigned char f = pfl[5 * tid + k];
+    if (f & 1) phi = pk[5 * tid + k];
+    if (f & 2) {
+      apply = true;
+      break;
+    }
+  }
+  const StepResult res = step_result(p, ctl, exists, deact, active, ep_ts, fl, coll, reach, apply, phi, reward,
+                                     exists ? s.rs[ASVRL_F_RET * NT + idx] : 0.0);
+  if (ctl.trainer_deactivate && ctl.do_dynamics && exists && !(res.nfl & ASVRL_FLAG_DEACTIVATED))
+    atomicAdd(&salive[le], 1);
+  if (exists) {
+    if (ctl.do_dynamics) s.rs[ASVRL_F_RET * NT + idx] = res.ret;
+    s.rs[ASVRL_F_PHI * NT + idx] = phi;
+    s.rflags[idx] = res.nfl;
+  }
+  if (env_on) {
+    float4* o4 = reinterpret_cast<float4*>(out.obs + idx * ASVRL_OBS_DIM);
+    const bool a = active;
+    for (int k = cnt > 0 ? cnt : 0; k < 5; ++k) {   // the object rows phase 4 did not write
+      float* of = out.obs + idx * ASVRL_OBS_DIM + 7 + 5 * k;
+      of[0] = 0.f;
+      of[1] = 0.f;
+      of[2] = 0.f;
+      of[3] = 0.f;
+      of[4] = 0.f;
+      if (out.obs64 != nullptr) {
+        double* o = out.obs64 + idx * 32 + 7 + 5 * k;
+        o[0] = 0.0;
+        o[1] = 0.0;
+        o[2] = 0.0;
+        o[3] = 0.0;
+        o[4] = 0.0;
+      }
+    }
+    o4[8] = make_float4((a && cnt > 0) ? 1.f : 0.f, (a && cnt > 1) ? 1.f : 0.f, (a && cnt > 2) ? 1.f : 0.f,
+                        (a && cnt > 3) ? 1.f : 0.f);
+    o4[9] = make_float4((a && cnt > 4) ? 1.f : 0.f, 0.f, 0.f, 0.f);
+    out.obj_cnt[idx] = static_cast<int8_t>(exists ? cnt : -1);
+    out.reward[idx] = res.reward;
+    out.done[idx] = res.done;
+    out.info[idx] = res.info;
+  }
+  __syncthreads();
+  if (env_on && i == 0 && ctl.do_dynamics) env_end(p, s, ctl, out, e, ep_ts, nrob, salive[le], NT);
 }
 
 // ------------------------------------------------------------------ reset (env.py:72-164)
@@ -867,7 +1193,7 @@ __global__ __launch_bounds__(kBlock) void current_kernel(const double* __restric
 
 }  // namespace
 
-size_t env_step_smem(int R, int O) {
+size_t env_sweep_smem(int R, int O) {
   const int blk = step_block(R);
   const int epb = blk / R;
   return sizeof(double) * (4 * blk + static_cast<size_t>(epb) * O * 3) + sizeof(int) * epb + blk;
@@ -879,7 +1205,7 @@ struct PairLaunch {
   int blk, epb;
   size_t smem;
 };
-PairLaunch pair_launch(int R, int O, int n_envs, int blk_req, int epb_req) {
+PairLaunch pair_launch(int R, int O, int n_envs, int blk_req, int epb_req, int vm_bytes) {
   const int np1 = R * (O + R);
   PairLaunch L;
   // the robots of the workgroup's envs fill its first wave (dynamics, merge, COLREGs run per robot:
@@ -897,9 +1223,15 @@ PairLaunch pair_launch(int R, int O, int n_envs, int blk_req, int epb_req) {
   if (large) L.epb = 60 / R;
   if (epb_req > 0) L.epb = epb_req;
   if (L.epb * R > L.blk) L.epb = L.blk / R;
+  // env_pairs_kernel's carve: 8 per-robot f64 arrays, the per-pair keys (reused as phase 4's phi),
+  // obstacles, the per-pair radius draws (f32 for noise mode 2), 3 ints per env and one per wave, 5 kept
+  // slots and 5 work-list entries (u16) per robot, then bytes (pair / COLREGs flags, 2 per-robot flags,
+  // kept count)
+  const size_t nrb = static_cast<size_t>(L.epb) * R;
   const size_t np = static_cast<size_t>(L.epb) * np1;
-  L.smem = sizeof(double) * (8 * static_cast<size_t>(L.blk) + 6 * np + static_cast<size_t>(L.epb) * O * 3) +
-           sizeof(int) * 3 * L.epb + 2 * L.blk + np;
+  const size_t nslot = np > 5 * nrb ? np : 5 * nrb;
+  L.smem = sizeof(double) * (8 * nrb + nslot + static_cast<size_t>(L.epb) * O * 3) + vm_bytes * np +
+           sizeof(int) * (3 * L.epb + L.blk / 64) + sizeof(unsigned short) * 10 * nrb + nslot + 3 * nrb;
   return L;
 }
 
@@ -928,32 +1260,35 @@ extern "C" int asvrl_env_step_ex(const AsvParams* params, const AsvEnvState* sta
   ASVRL_REQUIRE(lc.block == 0 || lc.block == 64 || lc.block == 128 || lc.block == 256,
                 "asvrl_env_step: block must be 0, 64, 128 or 256");
   ASVRL_REQUIRE(lc.envs_per_block >= 0, "asvrl_env_step: negative envs_per_block");
-  const PairLaunch pl = pair_launch(state->max_robots, state->max_obs, state->n_envs, lc.block, lc.envs_per_block);
+  const int nm = ctl->noise_mode == 0 ? 0 : (ctl->noise_mode == 1 ? 1 : 2);
+  const PairLaunch pl = pair_launch(state->max_robots, state->max_obs, state->n_envs, lc.block, lc.envs_per_block,
+                                    nm == 2 ? 4 : 8);
   ASVRL_REQUIRE(lc.layout != 1 || pl.smem <= 150 * 1024, "asvrl_env_step: the pair layout's LDS does not fit");
   if (lc.layout != 2 && pl.smem <= 150 * 1024) {
     const int grid = (state->n_envs + pl.epb - 1) / pl.epb;
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(pl.blk), pl.smem, as_stream(stream), *params, *state, actions, noise,
+                         *ctl, *out, pl.epb);
+    };
     if (pl.blk == 64)
-      hipLaunchKernelGGL((env_step_kernel<64, true>), dim3(grid), dim3(64), pl.smem, as_stream(stream), *params,
-                         *state, actions, noise, *ctl, *out, pl.epb);
+      nm == 0 ? go(env_pairs_kernel<64, 0>) : nm == 1 ? go(env_pairs_kernel<64, 1>) : go(env_pairs_kernel<64, 2>);
     else if (pl.blk == 128)
-      hipLaunchKernelGGL((env_step_kernel<128, true>), dim3(grid), dim3(128), pl.smem, as_stream(stream), *params,
-                         *state, actions, noise, *ctl, *out, pl.epb);
+      nm == 0 ? go(env_pairs_kernel<128, 0>) : nm == 1 ? go(env_pairs_kernel<128, 1>) : go(env_pairs_kernel<128, 2>);
     else
-      hipLaunchKernelGGL((env_step_kernel<256, true>), dim3(grid), dim3(256), pl.smem, as_stream(stream), *params,
-                         *state, actions, noise, *ctl, *out, pl.epb);
+      nm == 0 ? go(env_pairs_kernel<256, 0>) : nm == 1 ? go(env_pairs_kernel<256, 1>) : go(env_pairs_kernel<256, 2>);
     return check_launch("asvrl_env_step");
   }
   const int blk = step_block(state->max_robots);
   const int epb = blk / state->max_robots;
   const int grid = (state->n_envs + epb - 1) / epb;
-  const size_t smem = env_step_smem(state->max_robots, state->max_obs);
+  const size_t smem = env_sweep_smem(state->max_robots, state->max_obs);
   ASVRL_REQUIRE(smem <= 160 * 1024, "asvrl_env_step: max_obs too large for LDS");
   if (blk == 64)
-    hipLaunchKernelGGL((env_step_kernel<64, false>), dim3(grid), dim3(64), smem, as_stream(stream), *params, *state,
-                       actions, noise, *ctl, *out, epb);
+    hipLaunchKernelGGL((env_sweep_kernel<64>), dim3(grid), dim3(64), smem, as_stream(stream), *params, *state,
+                       actions, noise, *ctl, *out);
   else
-    hipLaunchKernelGGL((env_step_kernel<256, false>), dim3(grid), dim3(256), smem, as_stream(stream), *params,
-                       *state, actions, noise, *ctl, *out, epb);
+    hipLaunchKernelGGL((env_sweep_kernel<256>), dim3(grid), dim3(256), smem, as_stream(stream), *params,
+                       *state, actions, noise, *ctl, *out);
   return check_launch("asvrl_env_step");
 }
 

@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--json", default=None, help="also write {kernel: {counter: mean}} here")
     a = ap.parse_args()
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
-    for p in ("sq", "sq2", "fetch", "write"):
+    for p in ("sq", "sq2", "f64", "fetch", "write"):
         for r in load(os.path.join(a.dir, p)):
             name = r.get("Kernel_Name", r.get("Kernel-Name", "")).replace("(anonymous namespace)", "anon")
             name = re.sub(r"\(.*", "", name)
