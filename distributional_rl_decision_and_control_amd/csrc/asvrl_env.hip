@@ -325,15 +325,7 @@ __device__ __forceinline__ void draw_noise(const AsvParams& p, const AsvStepCtl&
                  (static_cast<uint32_t>(qidx >> 32) ^ 0xF32Au) + (static_cast<uint32_t>(slot) << 20),
                  static_cast<uint32_t>(ctr));
     float f0, f1, f2, f3;
-#ifdef ASVRL_DBG_NO_NOISE
-    f0 = f1 = f2 = f3 = 0.f;
-    if (VM) { n4 = 0.0; }
-    n0 = f0; n1 = f1; n2 = f2; n3 = f3; return;
-#endif
     rngf.normal4(f0, f1, f2, f3);
-#ifdef ASVRL_DBG_NO_VM
-    n0 = f0 * p.pos_std; n1 = f1 * p.pos_std; n2 = f2 * p.vel_std; n3 = f3 * p.vel_std; if (VM) n4 = 0.0; return;
-#endif
     n0 = f0 * p.pos_std; n1 = f1 * p.pos_std; n2 = f2 * p.vel_std; n3 = f3 * p.vel_std;
     if (VM) n4 = rngf.vonmises(static_cast<float>(p.r_kappa));
   }
@@ -895,9 +887,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NM == 1 ?
   __syncthreads();
 
   // ---------------- phase 4: one lane per kept object: its observation row and COLREGs test
-#ifdef ASVRL_DBG_NO_P4
-  if (ctl.seed != 12345) {} else
-#endif
   for (int it = tid; it < nitem; it += BLOCK) {
     const int kq = sitem[it];
     const int qr = kq / 5;
@@ -926,9 +915,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NM == 1 ?
         rd = -sn * vxn + cs * vyn;
         re = rn;
 #ifndef ASVRL_NO_COLREGS
-        bool ev;
-        const bool hit = colregs_ev(p.r, cs, sn, sv0[qr], sv1[qr], ra, rb, rc, rd, re, ph, ev);
-        cf = static_cast<unsigned char>((ev ? 1 : 0) | (hit ? 2 : 0));
+        if (!(sqrt(rc * rc + rd * rd) < 0.5)) {   // colregs_body's first test, ahead of the call
+          bool ev;
+          const bool hit = colregs_ev(p.r, cs, sn, sv0[qr], sv1[qr], ra, rb, rc, rd, re, ph, ev);
+          cf = static_cast<unsigned char>((ev ? 1 : 0) | (hit ? 2 : 0));
+        }
 #endif
       }
       float* of = out.obs + qidx * ASVRL_OBS_DIM + 7 + 5 * k;
@@ -1208,19 +1199,21 @@ struct PairLaunch {
 PairLaunch pair_launch(int R, int O, int n_envs, int blk_req, int epb_req, int vm_bytes) {
   const int np1 = R * (O + R);
   PairLaunch L;
-  // the robots of the workgroup's envs fill its first wave (dynamics, merge, COLREGs run per robot:
-  // every wave issues them whatever its active lanes, so robots are packed densely); the pairs then
-  // spread over all four waves
-  // Batch-size rule (tools/env_sweep.sh, profiles/r02_env_launch_sweep.txt): up to 8192 envs, about 40
-  // robots in a 256-lane workgroup (R = 5: 8 envs, 34 us at 4096 envs vs 44 us for 128 lanes x 12
-  // envs and 47 us for the per-robot sweep; R = 17: 3 envs, 133 us vs 241 us); from 16384 envs with
-  // R <= 8, 128-lane workgroups of about 60 robots (R = 5: 12 envs) -- more resident workgroups per
-  // CU: 319 M env-steps/s at 2^18 envs vs 154 M with the small-batch shape
+  // Launch-shape rule (tools/env_try.sh, profiles/r02_env_pairs_v2_sweep*.jsonl; the kernel holds 4
+  // waves per SIMD by registers, so the shape sets LDS use, tail waste and per-workgroup overheads):
+  //  - up to 8 robots per env, below 16384 envs: 256-lane workgroups of about 40 robots (R = 5: 8 envs,
+  //    27 us at 4096 envs vs 31-42 us for the other shapes)
+  //  - up to 8 robots, from 16384 envs: one-wave workgroups of about 40 robots (R = 5: 8 envs; 416-422 us
+  //    at 2^18 envs vs 428-440 us for 128/256 lanes)
+  //  - more robots: 256-lane workgroups of about 120 robots (R = 17: 7 envs, 61 us at 4096 envs vs 70 us
+  //    for 3 envs and 74-124 us for the other shapes)
   const bool large = n_envs >= 16384 && R <= 8;
-  L.blk = (blk_req == 64 || blk_req == 128 || blk_req == 256) ? blk_req : (large ? 128 : 256);
+  L.blk = (blk_req == 64 || blk_req == 128 || blk_req == 256) ? blk_req : (large ? 64 : 256);
   if (R > L.blk) L.blk = 256;
-  L.epb = R <= 64 ? ((40 + R - 1) / R < 64 / R ? (40 + R - 1) / R : 64 / R) : 1;
-  if (large) L.epb = 60 / R;
+  if (R <= 8)
+    L.epb = large ? 40 / R : ((40 + R - 1) / R < 64 / R ? (40 + R - 1) / R : 64 / R);
+  else
+    L.epb = 120 / R > 1 ? 120 / R : 1;
   if (epb_req > 0) L.epb = epb_req;
   if (L.epb * R > L.blk) L.epb = L.blk / R;
   // env_pairs_kernel's carve: 8 per-robot f64 arrays, the per-pair keys (reused as phase 4's phi),
