@@ -348,6 +348,7 @@ __global__ __launch_bounds__(BLOCK) void env_sweep_kernel(AsvParams p, AsvEnvSta
   const int e = blockIdx.x * epb + le;
   const bool lane_env = (le < epb) && (e < s.n_envs);
   const bool env_on = lane_env && (ctl.env_mask == nullptr || ctl.env_mask[e] != 0);
+  if (ctl.env_mask != nullptr && !__syncthreads_or(env_on ? 1 : 0)) return;   // no env of the workgroup is on
   const int nrob = lane_env ? s.n_robots[e] : 0;
   const bool exists = env_on && i < nrob;
   const size_t NT = static_cast<size_t>(s.n_envs) * R;
@@ -637,6 +638,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NM == 1 ?
   const int e = blockIdx.x * epb + le;
   const bool lane_env = rlane && e < s.n_envs;
   const bool env_on = lane_env && (ctl.env_mask == nullptr || ctl.env_mask[e] != 0);
+  // a masked pass (the observation pass after a reset) touches few envs: workgroups with none leave
+  if (ctl.env_mask != nullptr && !__syncthreads_or(env_on ? 1 : 0)) return;
   const int nrob = lane_env ? s.n_robots[e] : 0;
   const bool exists = env_on && i < nrob;
   const size_t NT = static_cast<size_t>(s.n_envs) * R;

@@ -145,10 +145,12 @@ def _check_rows(rows, b, R):
     return worst
 
 
-# every shipped kernel layout (asvrl_env_step_ex): the automatic choice (pair-parallel at these
-# sizes), the per-robot sweep (the automatic fallback when the pair layout's LDS does not fit,
-# e.g. R ~ 64) and a non-default pair shape (128 threads, 2 envs per workgroup)
-LAYOUTS = {"auto": None, "sweep": (2, 0, 0), "pairs_b128_e2": (1, 128, 2)}
+# every shipped kernel layout (asvrl_env_step_ex): the automatic choice (pair-parallel, 256 lanes at
+# these sizes), the per-robot sweep (the automatic fallback when the pair layout's LDS does not fit,
+# e.g. R ~ 64), the large-batch shape (one wave of 8 envs, from 16384 envs), the many-robot shape
+# (256 lanes, 7 envs) and a non-default pair shape (128 threads, 2 envs per workgroup)
+LAYOUTS = {"auto": None, "sweep": (2, 0, 0), "pairs_b64_e8": (1, 64, 8), "pairs_b256_e7": (1, 256, 7),
+           "pairs_b128_e2": (1, 128, 2)}
 
 
 @pytest.mark.parametrize("layout", list(LAYOUTS))
