@@ -1,9 +1,10 @@
 #!/bin/bash
 # PMC passes of the env-step kernel alone at 2^18 envs (tools/bench_env.py, f32 noise, automatic
-# launch shape). Output gpurun_out/pmc_env/<pass>/; summarise with tools/pmc_summary.py --match env_.
+# launch shape; ENV_ARGS overrides). Output gpurun_out/$PMC_NAME (default pmc_env)/<pass>/; summarise with
+# tools/pmc_summary.py --match env_.
 set -e
 ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
-OUT="$ROOT/gpurun_out/pmc_env"
+OUT="$ROOT/gpurun_out/${PMC_NAME:-pmc_env}"
 mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
