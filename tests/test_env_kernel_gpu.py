@@ -396,3 +396,50 @@ def test_config5_full_size():
     assert np.all(np.isfinite(losses)), losses
     p1 = torch.cat([p.detach().reshape(-1) for p in tr.local.critic.parameters()])
     assert bool(torch.isfinite(p1).all()) and not torch.equal(p0, p1)
+
+
+CROSS_SHAPES = [(1, 0, 55.0, 0), (1, 3, 55.0, 0), (3, 0, 55.0, 0), (5, 4, 55.0, 2), (12, 8, 110.0, 0),
+                (30, 2, 110.0, 0)]
+
+
+@pytest.mark.parametrize("fast", [True, False])
+@pytest.mark.parametrize("R,O,W,C", CROSS_SHAPES)
+def test_pair_kernel_matches_sweep(R, O, W, C, fast):
+    """The pair kernel (automatic shape and a forced one-wave shape) against the per-robot sweep, bit
+    for bit, over (robots, buoys) shapes the traces do not reach: one robot, no buoys, vortex cores,
+    12 and 30 robots (absent robots where the sampler cannot place all). Device reset, Philox noise in
+    f32 and f64, 12 steps with the trainer bookkeeping (returns, deactivation, episode end) and one
+    masked observation pass over every third env; f32 and f64 observations, state, flags, counts."""
+    from distributional_rl_decision_and_control_amd import _abi
+    from distributional_rl_decision_and_control_amd.device_env import DeviceEnvBatch, reset_cfg
+    E = 300
+
+    def run(launch):
+        b = DeviceEnvBatch(E, R, O, C, obs64=True)
+        b.reset(reset_cfg(R, O, C, 20.0, width=W, height=W), seed=11)
+        b.step(None, do_dynamics=False, seed=11, counter=0, fast_noise=fast, launch=launch)
+        g = torch.Generator(device="cuda").manual_seed(3)
+        outs = []
+        for t in range(12):
+            a = (torch.rand((E * R, 2), generator=g, device="cuda", dtype=torch.float64) * 2 - 1).contiguous()
+            b.step(a, seed=11, counter=t + 1, trainer_deactivate=True, gamma=0.99, fast_noise=fast, launch=launch)
+            outs.append(torch.cat([b.reward, b.rs.reshape(-1), b.obs.reshape(-1).double(), b.obs64.reshape(-1),
+                                   b.rflags.double(), b.obj_cnt.double(), b.done.double(), b.info.double(),
+                                   b.env_done.double(), b.ep_ts.double()]))
+            if t == 5:
+                mask = torch.zeros(E, dtype=torch.uint8, device="cuda")
+                mask[::3] = 1
+                b.step(None, do_dynamics=False, seed=11, counter=100, fast_noise=fast, env_mask=mask, launch=launch)
+                outs.append(torch.cat([b.obs.reshape(-1).double(), b.obs64.reshape(-1), b.obj_cnt.double()]))
+        return b, outs
+
+    b, ref = run((_abi.ENV_LAYOUT_SWEEP, 0, 0))
+    cnt = b.obj_cnt.cpu().numpy()
+    assert (cnt >= -1).all() and (cnt <= 5).all()
+    for launch in (None, (_abi.ENV_LAYOUT_PAIRS, 64, max(1, 64 // R))):
+        _, got = run(launch)
+        for t, (x, y) in enumerate(zip(ref, got)):
+            # exact, NaN = NaN: phi is NaN, in both layouts and in the reference, when COLREGs evaluates an
+            # object closer than its radius + 1 (asin of a ratio > 1, wamv.py:388); it never enters a reward
+            torch.testing.assert_close(x, y, rtol=0, atol=0, equal_nan=True,
+                                       msg=f"layout {launch} differs from the sweep at output {t}")
