@@ -160,8 +160,10 @@ int asvrl_env_step(const AsvParams* params, const AsvEnvState* state, const doub
  *   layout 0: automatic (pair-parallel perception when its LDS fits, else the per-robot sweep),
  *          1: pair-parallel (one lane per (robot, candidate) pair; fails if the LDS does not fit),
  *          2: per-robot sweep (one lane per robot, candidates in a serial loop);
- *   block  threads per workgroup of the pair layout (64, 128 or 256);
- *   envs_per_block  envs per workgroup of the pair layout (0: about 40 robots per group). */
+ *   block  threads per workgroup of the pair layout (64, 128 or 256; 0: 256 lanes, or one wave from
+ *          16384 envs when an env has at most 8 robots);
+ *   envs_per_block  envs per workgroup of the pair layout (0: about 40 robots per group, about 120
+ *          when an env has more than 8 robots). */
 typedef struct AsvEnvLaunch {
   int32_t layout;
   int32_t block;
