@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("ASVRL_LIB", os.path.join(HERE, "lib", "libasvrl.so"))
 # the same sources built with f32 learner operands (the parity build; asvrl_operand_bytes() == 4)
 LIB_PATH_F32 = os.path.join(HERE, "lib", "libasvrl_f32.so")
 OPERANDS = {"bf16": (LIB_PATH, 2), "f32": (LIB_PATH_F32, 4)}
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
 OBS_DIM = 40   # self 7 | objects 25 | mask 5 | pad 3
@@ -96,7 +96,7 @@ class AsvCriticActs(C.Structure):
 
 
 class AsvCriticParts(C.Structure):
-    _fields_ = [(n, C.c_void_p) for n in ("cos_emb", "hidden", "hidden2", "out")]
+    _fields_ = [(n, C.c_void_p) for n in ("cos_emb", "hidden", "hidden2", "out", "enc", "aenc")]
 
 
 # (name, restype, argtypes) of every exported entry point, mirroring include/asvrl.h

@@ -42,6 +42,12 @@ namespace {
 
 constexpr int kC = 256, kH = 128, kNcos = 64, kNW = 4, kMaxA = ASVRL_IQN_MAX_ACTIONS;
 
+// where a round issues the global loads of the next round's inputs (A/B knob of variant builds):
+// 0 at the top of the round, 1 behind the W2 fragment fetch in L1
+#ifndef ASVRL_PRE_AT
+#define ASVRL_PRE_AT 0
+#endif
+
 #if ASVRL_OPERAND_F32
 template <int NT> struct FusedNB { static constexpr int v = 1; };
 #else
@@ -177,6 +183,11 @@ struct FusedLds {
   float enc[kEncFloats];              // encoder parameters (stage_fg)
   float in[2][InLayout<NT, S, 32 * NB, IQN ? 1 : 2>::kSize];   // the round's inputs, double-buffered
   float red[kNW];
+  // AC-IQN with parts.enc / parts.aenc: the encoders' gradient sums over the workgroup's rows, one
+  // lane-private slot per (feature, input): [input 0..6 | bias at 7][256 features], natural order;
+  // action encoder [w0 | w1 | b][lane half][128 features]
+  float encacc[IQN ? 1 : 8 * kC];
+  float aeacc[IQN ? 1 : 3 * 2 * kH];
 };
 
 constexpr int kSelfF = 56, kSelfIn = 7, kObjF = 40, kObjIn = 5, kObsMask = 32;
@@ -365,6 +376,10 @@ void critic_fused_kernel(FusedArgs a) {
       for (int i = threadIdx.x; i < lens[q]; i += kNW * 64) L.enc[off + i] = srcs[q][i];
       off += lens[q];
     }
+    if constexpr (!IQN) {
+      for (int i = threadIdx.x; i < 8 * kC; i += kNW * 64) L.encacc[i] = 0.f;
+      for (int i = threadIdx.x; i < 3 * 2 * kH; i += kNW * 64) L.aeacc[i] = 0.f;
+    }
     if (blockIdx.x < a.rounds)
 #pragma unroll
       for (int u = 0; u < IL::kPer; ++u) {
@@ -387,19 +402,25 @@ void critic_fused_kernel(FusedArgs a) {
   f32x16 dWo = f32x16{};
 #pragma unroll
   for (int g = 0; g < (IQN ? 1 : 16); ++g) dwo[g] = 0.f;
+  float encr[IQN ? 8 : 1];   // IQN with parts.enc: this lane's feature's encoder sums
+#pragma unroll
+  for (int i = 0; i < (IQN ? 8 : 1); ++i) encr[i] = 0.f;
   int buf = 0, it_ = 0;
   (void)it_;
   for (int t = blockIdx.x; t < a.rounds; t += gridDim.x, buf ^= 1, ++it_) {
-    // the next round's inputs, into registers now and into LDS at the end of this round
+    // the next round's inputs, into registers during this round and into LDS at its end
     float pre[IL::kPer];
     int tid_p = threadIdx.x;
     asm volatile("" : "+v"(tid_p));
-#pragma unroll
-    for (int u = 0; u < IL::kPer; ++u) {
-      const int e = tid_p + u * kNW * 64;
-      pre[u] = (t + static_cast<int>(gridDim.x) < a.rounds && e < IL::kSize)
-                   ? fetch_in<NT, S, G, NA>(a, t + gridDim.x, e) : 0.f;
-    }
+#define ASVRL_FETCH_PRE()                                                                   \
+  _Pragma("unroll") for (int u = 0; u < IL::kPer; ++u) {                                   \
+    const int e = tid_p + u * kNW * 64;                                                    \
+    pre[u] = (t + static_cast<int>(gridDim.x) < a.rounds && e < IL::kSize)                 \
+                 ? fetch_in<NT, S, G, NA>(a, t + gridDim.x, e) : 0.f;                      \
+  }
+#if ASVRL_PRE_AT == 0
+    ASVRL_FETCH_PRE();
+#endif
     const float* in = L.in[buf];
     // the lane indices re-derived through an opaque copy every round: otherwise every LDS / weight
     // address of the round body is loop-invariant, gets hoisted out of the loop and spills
@@ -497,6 +518,11 @@ void critic_fused_kernel(FusedArgs a) {
         for (int j = 0; j < NB; ++j) acc[j] = mfma(w1f[ks], rowf(L.x, RA_x, j, ks), acc[j]);
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) w2f[ks] = W2[(w * 8 + ks) * 64 + lane];
+#if ASVRL_PRE_AT == 1
+      // issued behind W2's fragments: the wait for those (in L2) does not include this load, whose
+      // first waiter (W2^T's fragments, in L3) comes two phases later
+      ASVRL_FETCH_PRE();
+#endif
       if constexpr (!kBiasFirst)
 #pragma unroll
         for (int j = 0; j < NB; ++j) acc[j] += bias_init(b1p, w * 32, h);
@@ -714,11 +740,32 @@ void critic_fused_kernel(FusedArgs a) {
           rows(L.dz1, RA_d, j, 2 * w + s, dz1);
         }
       }
-      if constexpr (!IQN)
+      if constexpr (!IQN) {
+        const bool enc = a.parts.aenc != nullptr;
         sample_sums<NT, NB>(gsa, w * 32, lane, [&](int bl, int p, float v) {
           const float gm = L.G[bl * kH + p];
-          if (a.dzG != nullptr) a.dzG[static_cast<size_t>(b0 + bl) * kH + swap23(p)] = gm > 0.f ? v : 0.f;
+          const float dz = gm > 0.f ? v : 0.f;
+          if (a.dzG != nullptr) a.dzG[static_cast<size_t>(b0 + bl) * kH + swap23(p)] = dz;
+          if (enc) L.G[bl * kH + p] = dz;   // G's block w is this wave's own: dzG in place
         });
+        if (enc) {
+          // action_encoder's gradient (AC_IQN_model.py:468-470): lane (half hh, position 32w + rr)
+          // sums dzG[b] * (a_b0, a_b1, 1) over its half of the round's samples, in sample order
+          const int hh = lane >> 5, rr = lane & 31, p = w * 32 + rr, m = swap23(p);
+          float s0 = 0.f, s1 = 0.f, sb = 0.f;
+#pragma unroll
+          for (int k = hh; k < S; k += 2) {
+            const float d = L.G[k * kH + p];
+            s0 += d * in[IL::kAct + 2 * k];
+            s1 += d * in[IL::kAct + 2 * k + 1];
+            sb += d;
+          }
+          float* acc = L.aeacc + hh * kH + m;
+          acc[0] += s0;
+          acc[2 * kH] += s1;
+          acc[4 * kH] += sb;
+        }
+      }
     }
     ASVRL_STAMP(12);
     __syncthreads();
@@ -788,9 +835,37 @@ void critic_fused_kernel(FusedArgs a) {
       }
       sample_sums<NT, NB>(fsa, mb * 32, lane, [&](int bl, int p, float v) {
         const float fm = L.F[bl * kC + p];
-        if (a.dzF != nullptr)
-          bp(a.dzF)[static_cast<size_t>(b0 + bl) * kC + swap23(p)] = (elem_t)(fm > 0.f ? v : 0.f);
+        const float dz = fm > 0.f ? v : 0.f;
+        if (a.dzF != nullptr) bp(a.dzF)[static_cast<size_t>(b0 + bl) * kC + swap23(p)] = (elem_t)dz;
+        if (a.parts.enc != nullptr) L.F[bl * kC + p] = dz;   // F's blocks 2w, 2w+1 are this wave's own
       });
+    }
+    {
+      if (a.parts.enc != nullptr) {
+        // the observation encoders' gradients (AC_IQN_model.py:284-308): lane l owns feature
+        // m = swap23(64 w + l) and sums dzF[b][m] * (its encoder's inputs, 1) over the round's samples
+        // in order; object features keep their object's slot (folded over the objects at the end)
+        ASVRL_FRESH_LANE();
+        const int p = 64 * w + lane, m = swap23(p);
+        const bool self = m < kSelfF;
+        const int off = self ? 0 : kSelfIn + kObjIn * ((m - kSelfF) / kObjF);
+        float acc[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+          const float d = L.F[k * kC + p];
+          const float* x = in + IL::kObs + k * kObsIn + off;
+#pragma unroll
+          for (int i = 0; i < kSelfIn; ++i) acc[i] += d * ((self || i < kObjIn) ? x[i] : 0.f);
+          acc[7] += d;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if constexpr (IQN) encr[i] += acc[i];   // IQN: no LDS to spare at N = 8, VGPRs to spare
+          else L.encacc[i * kC + m] += acc[i];
+        }
+      }
     }
 
     // ---------------- dWc[own 64][:] += dzc^T cos (this wave's own dzc image: in-order LDS, no barrier)
@@ -825,6 +900,46 @@ void critic_fused_kernel(FusedArgs a) {
   // ---------------- the workgroup's partials: [M*K + M] per layer, features in natural order
   mfma_drain();
   const int grp = blockIdx.x;
+  {
+    // encoders (the round loop ended on a barrier: every wave's sums are in LDS; IQN's are moved from
+    // registers into the x image, free now). Object features folded over the five objects in object
+    // order; the action encoder's two lane halves in order.
+    const float* ea = L.encacc;
+    if constexpr (IQN) {
+      if (a.parts.enc != nullptr) {
+        float* ex = reinterpret_cast<float*>(L.x);
+        const int m = swap23(64 * w + lane);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) ex[i * kC + m] = encr[i];
+        ea = ex;
+      }
+      __syncthreads();
+    }
+    if (a.parts.enc != nullptr) {
+      float* pe = a.parts.enc + static_cast<size_t>(grp) * 688;
+      for (int i = threadIdx.x; i < 688; i += kNW * 64) {
+        float v;
+        if (i < kSelfF * kSelfIn) v = ea[(i % kSelfIn) * kC + i / kSelfIn];
+        else if (i < kSelfF * (kSelfIn + 1)) v = ea[7 * kC + i - kSelfF * kSelfIn];
+        else {
+          const int e = i - kSelfF * (kSelfIn + 1);
+          const int j = e < kObjF * kObjIn ? e / kObjIn : e - kObjF * kObjIn;
+          const int slot = e < kObjF * kObjIn ? e % kObjIn : 7;
+          v = 0.f;
+#pragma unroll
+          for (int o = 0; o < 5; ++o) v += ea[slot * kC + kSelfF + kObjF * o + j];
+        }
+        pe[i] = v;
+      }
+    }
+    if (!IQN && a.parts.aenc != nullptr) {
+      float* pa = a.parts.aenc + static_cast<size_t>(grp) * (3 * kH);
+      for (int i = threadIdx.x; i < 3 * kH; i += kNW * 64) {
+        const int m = i < 2 * kH ? i / 2 : i - 2 * kH, c = i < 2 * kH ? i % 2 : 2;
+        pa[i] = L.aeacc[(2 * c) * kH + m] + L.aeacc[(2 * c + 1) * kH + m];
+      }
+    }
+  }
   float* p2 = a.parts.hidden2 + static_cast<size_t>(grp) * (kH * kH + kH);
   float* p1 = a.parts.hidden + static_cast<size_t>(grp) * (kH * kC + kH);
   float* pc = a.parts.cos_emb + static_cast<size_t>(grp) * (kC * kNcos + kC);
@@ -956,6 +1071,7 @@ extern "C" int asvrl_iqn_train_fused(const AsvCriticWeights* w, const AsvIqnHead
                 "asvrl_iqn_train_fused: bad head");
   ASVRL_REQUIRE(parts->cos_emb && parts->hidden && parts->hidden2 && parts->out,
                 "asvrl_iqn_train_fused: null partial buffer");
+  ASVRL_REQUIRE(parts->aenc == nullptr, "asvrl_iqn_train_fused: IQN_Policy has no action encoder (parts->aenc)");
   ASVRL_REQUIRE(io->N == 8 || io->N == 16 || io->N == 32, "asvrl_iqn_train_fused: N must be 8, 16 or 32");
   ASVRL_REQUIRE(io->Np == io->N, "asvrl_iqn_train_fused: N' must equal N");
   ASVRL_REQUIRE(io->kappa > 0.f, "asvrl_iqn_train_fused: kappa must be positive");

@@ -215,11 +215,14 @@ def fused_train_supported(pack, B, N):
 
 
 def critic_train_fused(pack, critic, taus, N, q_next, rewards, dones, gamma, obs, act, arena, dzF=None, dzG=None,
-                       xb=None, tile_loss=None, kappa=1.0, q=None, row_loss=None, stream=None):
+                       xb=None, tile_loss=None, kappa=1.0, q=None, row_loss=None, stream=None, encoders=False):
     """asvrl_critic_train_fused: the critic step's forward, quantile-Huber loss against
     r + gamma q_next (1 - d), backward AND the trunk's weight gradients in one launch. The per-workgroup
     partials land in `arena` (PartialArena) as segments of critic's cos_embedding / hidden_layer /
-    hidden_layer_2 / output_layer .grad (reduced by the arena's next flush)."""
+    hidden_layer_2 / output_layer .grad (reduced by the arena's next flush).
+    encoders=True: the launch also forms the observation / action encoders' gradients (ABI 16
+    parts.enc / parts.aenc) as segments of their .grad, which must be contiguous
+    [self_w | self_b | obj_w | obj_b] (FusedAdam); dzF / dzG / xb are then not needed."""
     B = obs.shape[0]
     groups = fused_groups(pack, B, N)
     assert groups > 0 and fused_train_supported(pack, B, N), (B, N)
@@ -228,6 +231,13 @@ def critic_train_fused(pack, critic, taus, N, q_next, rewards, dones, gamma, obs
     regions = [arena._take(groups * (M * K + M)) for _, M, K in shapes]
     parts = _abi.AsvCriticParts()
     parts.cos_emb, parts.hidden, parts.hidden2, parts.out = (t.data_ptr() for t in regions)
+    if encoders:
+        se, oe, ae = critic.self_encoder[0], critic.object_encoder[0], critic.action_encoder[0]
+        gs = [se.weight.grad, se.bias.grad, oe.weight.grad, oe.bias.grad]
+        if not all(gs[k].data_ptr() + 4 * gs[k].numel() == gs[k + 1].data_ptr() for k in range(3)):
+            raise RuntimeError("critic_train_fused(encoders=True) needs the encoder gradients contiguous (FusedAdam)")
+        enc_part, ae_part = arena._take(groups * 688), arena._take(groups * 384)
+        parts.enc, parts.aenc = enc_part.data_ptr(), ae_part.data_ptr()
     io = _io(None, None, taus, N, obs=obs, act=act, xb=xb, Np=N, kappa=float(kappa), q_next=q_next,
              rewards=rewards, dones=dones, ld_rd=rewards.stride(0), gamma=float(gamma), q=q, row_loss=row_loss,
              dzF=dzF, dzG=dzG, tile_loss=tile_loss, loss_scale=1.0 / float(B * N))
@@ -235,6 +245,9 @@ def critic_train_fused(pack, critic, taus, N, q_next, rewards, dones, gamma, obs
                                                _abi.stream_ptr(stream)), "asvrl_critic_train_fused", pack.L)
     for (layer, M, K), part in zip(shapes, regions):
         arena.groups(part, groups, M, K, layer.weight.grad, layer.bias.grad)
+    if encoders:
+        arena._seg(enc_part, gs[0], None, groups, 688, 0, False)
+        arena._seg(ae_part, ae.weight.grad, ae.bias.grad, groups, 256, 128, False)
 
 
 def critic_actor_grad(pack, F, G, taus, N, q, dG=None, stream=None, w_ae=None, dA=None, tile_loss=None, obs=None,

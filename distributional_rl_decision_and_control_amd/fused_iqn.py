@@ -33,7 +33,7 @@ import torch
 
 from . import _abi
 from .fused_critic import CriticPack, PartialArena, TrainBuffers, fused_groups, fused_train_supported
-from .fused_update import FUSED_TRAIN, SideStreams, _reduce_and_step
+from .fused_update import ENC_IN_KERNEL, FUSED_TRAIN, SideStreams, _reduce_and_step
 
 OBS = 40
 K_ACT = 32
@@ -117,11 +117,13 @@ def iqn_train(pack, F, taus, bufs, dz_out, q_next, actions, rewards, dones, gamm
 
 
 def iqn_train_fused(pack, net, taus, N, q_next, actions, rewards, dones, gamma, obs, arena, dzF=None, xb=None,
-                    tile_loss=None, kappa=1.0, q=None, row_loss=None, stream=None):
+                    tile_loss=None, kappa=1.0, q=None, row_loss=None, stream=None, encoders=False):
     """asvrl_iqn_train_fused: train_IQN's local pass (agent.py:455-468) -- forward, gather at the
     taken action, quantile-Huber loss, backward -- AND the weight gradients of the trunk and the
     output layer in one launch; the per-workgroup partials land in `arena` as segments of net's
-    cos_embedding / hidden_layer / hidden_layer_2 / output_layer .grad."""
+    cos_embedding / hidden_layer / hidden_layer_2 / output_layer .grad.
+    encoders=True: also the observation encoders' gradients (ABI 16 parts.enc; their .grad contiguous
+    [self_w | self_b | obj_w | obj_b]); dzF / xb are then not needed."""
     B = obs.shape[0]
     groups = fused_groups(pack, B, N)
     assert groups > 0 and fused_train_supported(pack, B, N), (B, N)
@@ -131,6 +133,13 @@ def iqn_train_fused(pack, net, taus, N, q_next, actions, rewards, dones, gamma, 
     regions = [arena._take(groups * (M * K + M)) for _, M, K in shapes]
     parts = _abi.AsvCriticParts()
     parts.cos_emb, parts.hidden, parts.hidden2, parts.out = (t.data_ptr() for t in regions)
+    if encoders:
+        se, oe = net.self_encoder[0], net.object_encoder[0]
+        gs = [se.weight.grad, se.bias.grad, oe.weight.grad, oe.bias.grad]
+        if not all(gs[k].data_ptr() + 4 * gs[k].numel() == gs[k + 1].data_ptr() for k in range(3)):
+            raise RuntimeError("iqn_train_fused(encoders=True) needs the encoder gradients contiguous (FusedAdam)")
+        enc_part = arena._take(groups * 688)
+        parts.enc = enc_part.data_ptr()
     io = _io(None, N, obs=obs, xb=xb, taus=taus, Np=N, kappa=float(kappa), q_next=q_next, actions=actions,
              rewards=rewards, dones=dones, ld_rd=rewards.stride(0), gamma=float(gamma), q=q, row_loss=row_loss,
              dzF=dzF, tile_loss=tile_loss, loss_scale=1.0 / float(B * N))
@@ -138,6 +147,8 @@ def iqn_train_fused(pack, net, taus, N, q_next, actions, rewards, dones, gamma, 
                                             _abi.stream_ptr(stream)), "asvrl_iqn_train_fused", pack.L)
     for (layer, M, K), part in zip(shapes, regions):
         arena.groups(part, groups, M, K, layer.weight.grad, layer.bias.grad)
+    if encoders:
+        arena._seg(enc_part, gs[0], None, groups, 688, 0, False)
 
 
 def iqn_act(pack, F, actions64, step_dev, steps_per_count, total, fraction, initial, final, seed, taus=None,
@@ -194,10 +205,14 @@ def iqn_grads(st, net, rows, taus, gamma=0.99, flush=True):
     iqn_forward_max(st.target, None, taus[0], N, st.q_next, obs=ns_rows)
     if FUSED_TRAIN and fused_train_supported(st.local, B, N):
         # forward, loss, backward and the four layers' weight-gradient partials in one launch
-        iqn_train_fused(st.local, net, taus[1], N, st.q_next.view(B, N), a_col, r_col, d_col, gamma, s_rows, arena,
-                        dzF=st.dzF, xb=st.xb, tile_loss=st.tile_loss)
-        with arena.batch():
-            arena.fold(st.dzF, st.xb, net)   # encoder image -> self/object encoder grads
+        if ENC_IN_KERNEL:   # ... and the encoders' gradient partials
+            iqn_train_fused(st.local, net, taus[1], N, st.q_next.view(B, N), a_col, r_col, d_col, gamma, s_rows,
+                            arena, tile_loss=st.tile_loss, encoders=True)
+        else:
+            iqn_train_fused(st.local, net, taus[1], N, st.q_next.view(B, N), a_col, r_col, d_col, gamma, s_rows,
+                            arena, dzF=st.dzF, xb=st.xb, tile_loss=st.tile_loss)
+            with arena.batch():
+                arena.fold(st.dzF, st.xb, net)   # encoder image -> self/object encoder grads
         arena.scalar(st.tile_loss, st.loss)
         if flush:
             arena.flush()

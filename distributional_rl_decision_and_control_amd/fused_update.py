@@ -8,7 +8,8 @@ Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | 
     target encoders(ns, na) + trunk -> q_next            asvrl_critic_forward (encoders in the prologue)
     local encoders(s, a), trunk forward, quantile-Huber vs r + g q_next (1-d), backward AND the
     four trunk layers' weight-gradient partials          asvrl_critic_train_fused (ONE launch)
-    encoder / action-encoder gradients from dzF / dzG    ONE asvrl_linear_wgrad_multi (fold + small)
+    and the observation / action encoders' gradient partials (ABI 16; ASVRL_ENC_IN_KERNEL=0: from
+    dzF / dzG by ONE asvrl_linear_wgrad_multi, fold + small)
     every .grad (encoders folded in the reduction), the loss and the global gradient norm
                                                           ONE asvrl_partial_sums_norm
     clip + Adam + re-pack of the weight images           asvrl_adam_step_pack
@@ -47,6 +48,9 @@ ACTOR_FWD_SIDE = os.environ.get("ASVRL_ACTOR_FWD_SIDE", "0") == "1"
 # (asvrl_critic_train_fused; 1, default) or the two TRAIN kernels + the batched weight-gradient launch
 # over saved activations (0; also the path for shapes the fused launch does not take)
 FUSED_TRAIN = os.environ.get("ASVRL_FUSED_TRAIN", "1") == "1"
+# the encoders' gradients formed inside the fused critic launch (1; ABI 16) or by a batched
+# weight-gradient launch over its per-sample dzF / dzG (0, default until measured on the GPU)
+ENC_IN_KERNEL = os.environ.get("ASVRL_ENC_IN_KERNEL", "0") == "1"
 
 
 class SideStreams:
@@ -190,12 +194,17 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
         target_q(st, rows, taus[0], q_next, st.na)
     ae = critic.action_encoder[0]
     if FUSED_TRAIN and fused_train_supported(st.local_trunk, B, N):
-        # forward, loss, backward and the four trunk layers' weight-gradient partials in one launch
-        critic_train_fused(st.local_trunk, critic, taus[1], N, q_next.view(B, N), r_col, d_col, gamma, s_rows,
-                           a_rows, arena, dzF=st.dzF, dzG=st.dzG, xb=st.xb, tile_loss=st.tile_loss[0])
-        with arena.batch():   # the encoders' gradients from the per-sample dzF / dzG
-            arena.fold(st.dzF, st.xb, critic)
-            arena.small(st.dzG, a_rows, ae.weight.grad, ae.bias.grad)
+        # forward, loss, backward and the weight-gradient partials of the four trunk layers and the
+        # three encoders in one launch
+        if ENC_IN_KERNEL:
+            critic_train_fused(st.local_trunk, critic, taus[1], N, q_next.view(B, N), r_col, d_col, gamma, s_rows,
+                               a_rows, arena, tile_loss=st.tile_loss[0], encoders=True)
+        else:
+            critic_train_fused(st.local_trunk, critic, taus[1], N, q_next.view(B, N), r_col, d_col, gamma, s_rows,
+                               a_rows, arena, dzF=st.dzF, dzG=st.dzG, xb=st.xb, tile_loss=st.tile_loss[0])
+            with arena.batch():   # the encoders' gradients from the per-sample dzF / dzG
+                arena.fold(st.dzF, st.xb, critic)
+                arena.small(st.dzG, a_rows, ae.weight.grad, ae.bias.grad)
     else:
         tiles = wout_groups(B, N)
         wout_part = arena.take_tiles(tiles, 128)   # output_layer's gradient, reduced per workgroup in the kernel

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 15
+#define ASVRL_ABI_VERSION 16
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -316,6 +316,15 @@ typedef struct AsvCriticParts {
   float* hidden;    /* hidden_layer    (128 x 256): [groups][32768 + 128] */
   float* hidden2;   /* hidden_layer_2  (128 x 128): [groups][16384 + 128] */
   float* out;       /* output_layer    (1 x 128):  [groups][128 + 1] */
+  /* optional (ABI 16; asvrl_critic_train_fused only, NULL = not formed, then dzF / dzG / xb as
+   * before): the encoders' gradients from the kernel's own per-sample dzF / dzG, without them
+   * leaving the chip.
+   * enc:  observation encoders, folded over the five objects (the contiguous layout of
+   *       AC_IQN_model.py's self_encoder / object_encoder parameters):
+   *       [groups][self_w 56x7 | self_b 56 | obj_w 40x5 | obj_b 40] = [groups][688]
+   * aenc: action encoder (2 -> 128): [groups][w 128x2 | b 128] = [groups][384] */
+  float* enc;
+  float* aenc;
 } AsvCriticParts;
 
 /* Workgroups (= partial groups) of asvrl_critic_train_fused for B samples x N quantiles: one per

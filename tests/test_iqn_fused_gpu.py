@@ -32,8 +32,10 @@ def _batch(B, seed):
     return rows
 
 
-def _iqn_grads(ops, B, N, fused, rows, taus, seed=100):
-    """Every IQN_Policy .grad (reduced) and the loss of one train_IQN step, without the optimizer."""
+def _iqn_grads(ops, B, N, fused, rows, taus, seed=100, enc=True):
+    """Every IQN_Policy .grad (reduced) and the loss of one train_IQN step, without the optimizer.
+    enc: the fused launch forms the encoders' gradients itself (ABI 16) instead of the batched
+    weight-gradient launch over its dzF."""
     from distributional_rl_decision_and_control_amd import fused_iqn as fi
     from distributional_rl_decision_and_control_amd.agent import Agent
     from distributional_rl_decision_and_control_amd.learner import FusedAdam
@@ -43,10 +45,11 @@ def _iqn_grads(ops, B, N, fused, rows, taus, seed=100):
     st = fi.FusedIQNState(net, ag.policy_target, B, N, operands=ops)
     opt.grads.zero_()
     old, fi.FUSED_TRAIN = fi.FUSED_TRAIN, fused
+    old_enc, fi.ENC_IN_KERNEL = fi.ENC_IN_KERNEL, enc
     try:
         fi.iqn_grads(st, net, rows, taus, 0.99, flush=True)
     finally:
-        fi.FUSED_TRAIN = old
+        fi.FUSED_TRAIN, fi.ENC_IN_KERNEL = old, old_enc
     torch.cuda.synchronize()
     grads = {n: p.grad.detach().cpu().numpy().astype(np.float64).copy() for n, p in net.named_parameters()}
     return grads, float(st.loss[0].item())
@@ -125,3 +128,28 @@ def test_iqn_fused_train_deterministic():
     assert l1 == l2
     for n in g1:
         np.testing.assert_array_equal(g1[n], g2[n], err_msg=n)
+
+
+@pytest.mark.parametrize("ops,B,N", [("f32", 64, 8), ("f32", 256, 32), ("bf16", 64, 8), ("bf16", 4096, 32)])
+def test_iqn_fused_encoder_grads_in_kernel(ops, B, N):
+    """parts.enc (ABI 16) on IQN_Policy: the observation encoders' gradients summed in the fused launch
+    (register accumulators; no LDS to spare at N = 8) against the batched launch over its dzF. Every
+    other gradient and the loss bit-identical; encoders f32 2e-5 of scale, bf16 cosine > 0.999."""
+    rows = _batch(B, 21 + N)
+    taus = torch.rand(2, B, N, generator=torch.Generator(device="cuda").manual_seed(9 + B), device="cuda")
+    ge, le = _iqn_grads(ops, B, N, True, rows, taus, enc=True)
+    gf, lf = _iqn_grads(ops, B, N, True, rows, taus, enc=False)
+    assert le == lf
+    enc_names = [n for n in gf if "encoder" in n]
+    assert len(enc_names) == 4
+    for n in gf:
+        if n not in enc_names:
+            np.testing.assert_array_equal(ge[n], gf[n], err_msg=n)
+    for n in enc_names:
+        if ops == "f32":
+            scale = np.abs(gf[n]).max() + 1e-30
+            assert np.abs(ge[n] - gf[n]).max() / scale < 2e-5, n
+        else:
+            c = _cos(ge[n], gf[n])
+            ratio = np.linalg.norm(ge[n]) / np.linalg.norm(gf[n])
+            assert c > 0.999 and abs(ratio - 1) < 1e-2, (n, c, ratio)
