@@ -3,8 +3,10 @@
 # Tests of the fused learner first, then kernel timing / stamps / bench A/B; stops at the first failure.
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
-timeout -k 10 500 python -u -m pytest tests/test_critic_fused_gpu.py tests/test_learner_golden_gpu.py tests/test_dp_fused_gpu.py -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/enc_tests.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_critic_fused_gpu.py tests/test_iqn_fused_gpu.py -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/enc_tests.log 2>&1
 rc=$?; tail -3 gpurun_out/enc_tests.log; [ $rc -eq 0 ] || exit $rc
+ASVRL_ENC_IN_KERNEL=1 timeout -k 10 400 python -u -m pytest tests/test_learner_golden_gpu.py tests/test_dp_fused_gpu.py tests/test_chain_schedule_gpu.py -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/enc_tests2.log 2>&1
+rc=$?; tail -3 gpurun_out/enc_tests2.log; [ $rc -eq 0 ] || exit $rc
 for L in default pre1 default pre1; do
   if [ $L = default ]; then unset ASVRL_LIB; else export ASVRL_LIB=variants/libasvrl_$L.so; fi
   timeout -k 10 120 python tools/fused_time.py >> gpurun_out/fused_time.jsonl 2>gpurun_out/fused_time.err || exit 1
