@@ -42,10 +42,12 @@ namespace {
 
 constexpr int kC = 256, kH = 128, kNcos = 64, kNW = 4, kMaxA = ASVRL_IQN_MAX_ACTIONS;
 
-// where a round issues the global loads of the next round's inputs (A/B knob of variant builds):
-// 0 at the top of the round, 1 behind the W2 fragment fetch in L1
+// where a round issues the global loads of the next round's inputs: 1 (default) behind the W2 fragment
+// fetch in L1, so the wait for the weight fragments fetched before it never includes these loads
+// (127-129 vs 130 us per launch, stage phase 3.7k -> 3.1k cycles: profiles/r02_enc_ab.txt); 0 at the
+// top of the round
 #ifndef ASVRL_PRE_AT
-#define ASVRL_PRE_AT 0
+#define ASVRL_PRE_AT 1
 #endif
 
 #if ASVRL_OPERAND_F32

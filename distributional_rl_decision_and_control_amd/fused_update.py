@@ -48,9 +48,9 @@ ACTOR_FWD_SIDE = os.environ.get("ASVRL_ACTOR_FWD_SIDE", "0") == "1"
 # (asvrl_critic_train_fused; 1, default) or the two TRAIN kernels + the batched weight-gradient launch
 # over saved activations (0; also the path for shapes the fused launch does not take)
 FUSED_TRAIN = os.environ.get("ASVRL_FUSED_TRAIN", "1") == "1"
-# the encoders' gradients formed inside the fused critic launch (1; ABI 16) or by a batched
-# weight-gradient launch over its per-sample dzF / dzG (0, default until measured on the GPU)
-ENC_IN_KERNEL = os.environ.get("ASVRL_ENC_IN_KERNEL", "0") == "1"
+# the encoders' gradients formed inside the fused critic launch (1, default; ABI 16: 0.333 -> 0.323 ms per
+# AC-IQN step, profiles/r02_enc_ab.txt) or by a batched launch over its per-sample dzF / dzG (0)
+ENC_IN_KERNEL = os.environ.get("ASVRL_ENC_IN_KERNEL", "1") == "1"
 
 
 class SideStreams:
