@@ -442,6 +442,8 @@ class VecTrainer:
         ev_act = [torch.cuda.Event() for _ in range(U)]
         ev_snap = [torch.cuda.Event() for _ in range(U)]
         ev_learn = [torch.cuda.Event() for _ in range(U)]
+        # the events live as long as the graph: the captured cross-stream waits may refer to them at replay
+        self._chain_events = (ev_act, ev_snap, ev_learn)
         s_roll.wait_stream(main)
         out = None
         for k in range(U):
