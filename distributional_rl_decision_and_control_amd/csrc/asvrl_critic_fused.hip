@@ -277,7 +277,7 @@ __device__ __forceinline__ void stage_fg(const FusedArgs& a, int b0, int tid, co
 // quantile-Huber terms of one row against its sample's N' = NT targets r + gamma q_next (1 - d)
 // (agent.py:399-412), split over four lanes: lane quarter q4 (lanes 16 q4 .. 16 q4 + 15 share the
 // row block) takes targets q4 NT/4 .. + NT/4 - 1 from the staged q_next, and the four partial sums
-// are combined by two xor shuffles (a fixed order). Returns dq; *wl = the row's loss sum.
+// are combined by two lane exchanges (a fixed order). Returns dq; *wl = the row's loss sum.
 template <int NT>
 __device__ __forceinline__ float quarter_loss_dq(const FusedArgs& a, const float* qt, float rb, float done, float tau,
                                                  float q, int q4, float* wl_out) {
@@ -295,10 +295,10 @@ __device__ __forceinline__ float quarter_loss_dq(const FusedArgs& a, const float
     wl += w * hub;
     wg += w * (quad ? d : copysignf(kap, d));
   }
-  wl += __shfl_xor(wl, 16, 64);
-  wg += __shfl_xor(wg, 16, 64);
-  wl += __shfl_xor(wl, 32, 64);
-  wg += __shfl_xor(wg, 32, 64);
+  // lane-quarter sums on the VALU (v_permlane16/32_swap): the same two-step order as xor shuffles
+  // (fp addition of two terms commutes), without two LDS round trips
+  wl = half_sum(row_pair_sum(wl));
+  wg = half_sum(row_pair_sum(wg));
   *wl_out = wl / kap;
   return -(wg / kap) * a.gscale;
 }

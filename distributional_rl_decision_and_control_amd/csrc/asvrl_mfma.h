@@ -133,6 +133,15 @@ __device__ __forceinline__ float half_sum(float x) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// x(lane) + x(lane ^ 16) in every lane, the even 16-lane row's value first in both rows: one
+// v_permlane16_swap of x with itself leaves (even row's x, odd row's x) in its two results (VALU; a
+// __shfl_xor is an LDS ds_bpermute round trip)
+__device__ __forceinline__ float row_pair_sum(float x) {
+  const unsigned u = __float_as_uint(x);
+  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // cos(tau * pi * k) (Critic.calc_cos, AC_IQN_model.py:423) on the hardware cosine: v_cos_f32 takes
 // revolutions, cos(2 pi x) with x = k tau / 2 (< 32 for k < 64, tau < 1: inside its +-256 domain).
 // The value is rounded to bf16 for the MFMA right after, far above v_cos_f32's error. The f32 build

@@ -148,11 +148,11 @@ class VecTrainer:
         # pipelined AC-IQN learner (opt-in): the next batch and its target quantiles are produced
         # beside the current actor step (fused_update.target_q), so the critic step starts at once.
         # Two buffer sets alternate by parity; a captured graph then holds two iterations (one per
-        # parity). On the chained schedule the batch is sampled against the snapshot behind the
-        # previous push with the learn counter learn(i+1) sees, so the results equal the unpipelined
-        # ones bit for bit (tests/test_chain_schedule_gpu.py); measured 11 % slower there (0.373 vs
-        # 0.334 ms: its target-critic pass competes with the ACTOR pass for CUs,
-        # profiles/r02_pipeline_chain_ab.txt), so it stays opt-in.
+        # parity), on the joined schedule. Measured: no gain at the bench shape (0.5595 vs 0.559 ms) --
+        # the GPU is saturated, the overlap only moves the contention. A chained form (the batch sampled
+        # against the snapshot behind the previous push) was bit-identical and 11 % slower
+        # (profiles/r02_pipeline_chain_ab.txt), and its graph segfaulted in hipGraphLaunch late in the
+        # full GPU suite (never alone): reverted.
         self.pipeline = bool(pipeline) and self.fused2 is not None
         if self.pipeline:
             self.rows_buf = [self.batch_rows, torch.zeros_like(self.batch_rows)]
@@ -263,10 +263,9 @@ class VecTrainer:
         self._push()
         self.env.auto_reset()
 
-    def _produce(self, nxt, state, guard, counter, counter_dev=None):
+    def _produce(self, nxt, state, guard, counter):
         st = self.fused2
-        rows = self.replay.sample(self.B, seed=self.seed + 777, counter=counter,
-                                  counter_dev=self.learn_counter if counter_dev is None else counter_dev,
+        rows = self.replay.sample(self.B, seed=self.seed + 777, counter=counter, counter_dev=self.learn_counter,
                                   out=self.rows_buf[nxt], state=state, guard=guard, taus=self.taus_buf[nxt])
         from .fused_update import target_q
         target_q(st, rows, self.taus_buf[nxt][0], st.q_next_buf[nxt], st.na_p)
@@ -287,7 +286,7 @@ class VecTrainer:
         return out
 
     def learn(self, state=None, guard=0, actor_wait=None):
-        if self.pipeline and not self._chained():
+        if self.pipeline:
             return self._learn_pipelined(state, guard, actor_wait)
         if self.per is not None:
             rows, idx = self.per.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter,
@@ -351,12 +350,6 @@ class VecTrainer:
                 self.fused.target_pack.refresh()  # eager, outside any captured graph
             if self.agent_type == "AC-IQN" and self.fused2 is not None:
                 self.fused2.target_changed()
-                if self.pipeline and self._graph is not None and self._chained():
-                    # the batch the next replay's first learn consumes was produced against the old
-                    # target: its target quantiles again, with the refreshed one
-                    from .fused_update import target_q
-                    st = self.fused2
-                    target_q(st, self.rows_buf[0], self.taus_buf[0][0], st.q_next_buf[0], st.na_p)
             if self.fused_iqn is not None:
                 self.fused_iqn.target_changed()
             if self.fused_rb is not None:
@@ -430,7 +423,8 @@ class VecTrainer:
         return n
 
     def _chained(self):
-        return self.chain and self.overlap and self._fused_learner() and self.unroll % 2 == 0
+        return (self.chain and self.overlap and self._fused_learner() and not self.pipeline
+                and self.unroll % 2 == 0)
 
     def _chain_body(self):
         """self.unroll iterations with per-dependency stream ordering (captured only; see __init__)."""
@@ -459,33 +453,12 @@ class VecTrainer:
                 ev_snap[k].record(s_roll)
                 env.auto_reset()
                 env.advance_device()
-            if self.pipeline:   # this batch was produced by the previous learn (or primed before capture)
-                out = self._learn_chain_pipelined(k, ev_act[k], ev_snap[k])
-            else:
-                if k > 0:
-                    main.wait_event(ev_snap[k - 1])
-                out = self.learn(state=self.ring_snap2[(k - 1) % 2], guard=self.E * self.R, actor_wait=ev_act[k])
+            if k > 0:
+                main.wait_event(ev_snap[k - 1])
+            out = self.learn(state=self.ring_snap2[(k - 1) % 2], guard=self.E * self.R, actor_wait=ev_act[k])
             ev_learn[k].record(main)
         main.wait_stream(s_roll)
         return out
-
-    def _learn_chain_pipelined(self, k, actor_wait, snap_ready):
-        """learn(k) of the chained graph on the batch produced for it, producing batch k+1 beside its actor
-        step: sampled against the snapshot behind push(k) (waited for on the side stream) with the learn
-        counter as learn(k+1) will see it (copied before learn(k) increments it), and its target quantiles
-        -- the same data the joined schedule gives learn(k+1)."""
-        cur, nxt = k % 2, 1 - k % 2
-        st = self.fused2
-        self.counter_snap.copy_(self.learn_counter)
-
-        def produce():
-            torch.cuda.current_stream(self.device).wait_event(snap_ready)
-            self._produce(nxt, self.ring_snap2[k % 2], self.E * self.R, 1, counter_dev=self.counter_snap)
-
-        return ac_iqn_update_fused2(st, self.local, self.actor_opt, self.critic_opt, self.critic_grads,
-                                    self.actor_grads, self.rows_buf[cur], gamma=self.gamma, sync=self.sync,
-                                    actor_wait=actor_wait, taus=self.taus_buf[cur], q_next=st.q_next_buf[cur],
-                                    produce=produce, counter=self.learn_counter)
 
     def _capture(self):
         # warm up the captured region on a side stream (allocator + autograd state)
@@ -496,8 +469,7 @@ class VecTrainer:
                 self._iteration_body(True)
                 self.env.advance_host()
         torch.cuda.current_stream(self.device).wait_stream(s)
-        chained = self._chained()
-        if self.pipeline and not chained:   # the graph's first body consumes parity 0
+        if self.pipeline:   # the graph's first body consumes parity 0
             while self._parity != 0:
                 with torch.cuda.stream(s):
                     self._iteration_body(True)
@@ -507,11 +479,9 @@ class VecTrainer:
         # thread_local: the RCCL process group's watchdog thread queries its work events while this
         # thread captures; under the default global mode that query invalidates the capture and the
         # watchdog aborts the process
+        chained = self._chained()
         if chained:   # the ring state after the last eager push: what the graph's first learner samples against
             self.ring_snap2[(self.unroll - 1) % 2].copy_(self.replay.state)
-            if self.pipeline:   # the graph's first learn consumes a batch produced now
-                self.counter_snap = torch.zeros_like(self.learn_counter)
-                self._produce(0, self.ring_snap2[(self.unroll - 1) % 2], self.E * self.R, 0)
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
             if chained:
                 self._graph_out = self._chain_body()

@@ -1,21 +1,18 @@
 """GPU: VecTrainer's dependency-chained graph schedule (two iterations per captured graph, the rollout
 and learner streams ordered by the exact dependencies: act after the previous learn, learn after the
-ring snapshot behind the previous push, weight updates after this iteration's act) and its pipelined
-AC-IQN learner (the next batch and its target quantiles produced beside the actor step, sampled against
-the same snapshot with the same learn counter) against the joined schedule (a full join of the two
-streams per iteration): the same operations on the same data, so weights, losses, env state and replay
-state agree bit for bit -- also across target refreshes (the pipelined batch's target quantiles are
-recomputed after one)."""
+ring snapshot behind the previous push, weight updates after this iteration's act) against the
+joined schedule (a full join of the two streams per iteration): the same operations on the same data,
+so weights, losses, env state and replay state agree bit for bit."""
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
 
 
-def _run(agent_type, iters, interval=2500, **kw):
+def _run(agent_type, chain, iters):
     from distributional_rl_decision_and_control_amd.vec_trainer import VecTrainer
     tr = VecTrainer(n_envs=256, agent_type=agent_type, batch_size=256, num_tau=32, seed=21, graphs=True,
-                    unroll=2, buffer_size=256 * 5 * 40, learning_starts=512, target_update_interval=interval, **kw)
+                    unroll=2, chain=chain, buffer_size=256 * 5 * 40, learning_starts=512)
     while tr.replay_size_host() < tr.learning_starts:
         tr.iteration()
     for _ in range(iters):
@@ -27,14 +24,10 @@ def _run(agent_type, iters, interval=2500, **kw):
     return tr, params, losses
 
 
-CASES = [("AC-IQN", dict(chain=True), 2500), ("AC-IQN", dict(chain=True, pipeline=True), 2500),
-         ("AC-IQN", dict(chain=True, pipeline=True), 4), ("IQN", dict(chain=True), 2500)]
-
-
-@pytest.mark.parametrize("agent_type,kw,interval", CASES)
-def test_chained_schedule_matches_joined(agent_type, kw, interval):
-    a, pa, la = _run(agent_type, 8, interval, **kw)
-    b, pb, lb = _run(agent_type, 8, interval, chain=False)
+@pytest.mark.parametrize("agent_type", ["AC-IQN", "IQN"])
+def test_chained_schedule_matches_joined(agent_type):
+    a, pa, la = _run(agent_type, True, 8)
+    b, pb, lb = _run(agent_type, False, 8)
     assert a._chained() and not b._chained()
     assert torch.isfinite(la).all()
     assert torch.equal(la, lb), (la, lb)
@@ -42,7 +35,3 @@ def test_chained_schedule_matches_joined(agent_type, kw, interval):
     assert torch.equal(a.env.batch.rs, b.env.batch.rs)
     assert torch.equal(a.replay.state, b.replay.state)
     assert torch.equal(a.replay.ring, b.replay.ring)
-    if interval < 2500:   # the target refreshes happened
-        ta = torch.cat([p.detach().reshape(-1) for p in a.target.critic.parameters()])
-        tb = torch.cat([p.detach().reshape(-1) for p in b.target.critic.parameters()])
-        assert torch.equal(ta, tb)
