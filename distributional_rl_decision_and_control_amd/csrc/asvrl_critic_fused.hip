@@ -49,6 +49,17 @@ constexpr int kC = 256, kH = 128, kNcos = 64, kNW = 4, kMaxA = ASVRL_IQN_MAX_ACT
 #ifndef ASVRL_PRE_AT
 #define ASVRL_PRE_AT 1
 #endif
+// stage-ahead (A/B knob): round t + grid's F, G and cos images are staged in round t's last phase into
+// a second set of images (double-buffered), so a round starts with its first layer instead of the
+// staging phase and its barrier. Where the second set fits in LDS: AC-IQN, N = 32, bf16 operands.
+#ifndef ASVRL_STAGE_AHEAD
+#define ASVRL_STAGE_AHEAD 0
+#endif
+// with stage-ahead: the cos layer's weight fragments of the wave's two blocks held in registers for the
+// kernel's life (L0 and L4 read the same 8 fragments every round) instead of fetched three times a round
+#ifndef ASVRL_WC_RESIDENT
+#define ASVRL_WC_RESIDENT 1
+#endif
 
 #if ASVRL_OPERAND_F32
 template <int NT> struct FusedNB { static constexpr int v = 1; };
@@ -166,16 +177,16 @@ struct InLayout {
   static constexpr int kPer = (kSize + kNW * 64 - 1) / (kNW * 64);   // elements per thread
 };
 
-template <int NT, int NB, int S, bool IQN>
+template <int NT, int NB, int S, bool IQN, int NSB>
 struct FusedLds {
-  elem_t cos[32 * NB * kNcos];        // natural order (the cos layer is input-fed)
+  elem_t cos[NSB][32 * NB * kNcos];   // natural order (the cos layer is input-fed); NSB = 2: stage-ahead
   elem_t x[32 * NB * kC];             // F * c
   elem_t a[32 * NB * kH];             // h1g
   elem_t b[32 * NB * kH];             // h2, then dz2 in place
   elem_t dz1[32 * NB * kH];           // IQN: first the one-hot dq image [G][64] (output layer's dZ)
   elem_t dzc[kNW][32 * NB * kNcos];   // each wave's own dzc image (the A operand of its dWc rows)
-  float F[S * kC];                    // position order; operand-rounded values held in f32
-  float G[IQN ? 4 : S * kH];          // position order (AC-IQN's action features)
+  float F[NSB][S * kC];               // position order; operand-rounded values held in f32
+  float G[NSB][IQN ? 4 : S * kH];     // position order (AC-IQN's action features)
   float qpart[kNW][32 * NB];
   float dq[32 * NB];
   float tsum[2 * NB];                 // loss sums of the round's 16-row groups
@@ -340,7 +351,9 @@ template <int NT, bool IQN>
 __global__ __launch_bounds__(kNW * 64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void critic_fused_kernel(FusedArgs a) {
   constexpr int NB = FusedNB<NT>::v, G = 32 * NB, S = G / NT, NA = IQN ? 1 : 2;
-  __shared__ __attribute__((aligned(16))) FusedLds<NT, NB, S, IQN> L;
+  constexpr bool AH = ASVRL_STAGE_AHEAD && !IQN && NT == 32 && !ASVRL_OPERAND_F32;
+  constexpr int NSB = AH ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) FusedLds<NT, NB, S, IQN, NSB> L;
   static_assert(sizeof(L) <= 160 * 1024, "fused critic LDS image exceeds the CU's 160 KB");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
   const frag8* WC = reinterpret_cast<const frag8*>(a.w.wc_frag);
@@ -391,6 +404,28 @@ void critic_fused_kernel(FusedArgs a) {
   }
   __syncthreads();
 
+  // one round's F, G, xb (stage_fg) and cos(tau pi k) rows (natural order) from its staged inputs
+  auto stage = [&](int b0s, const float* ins, elem_t* cosd, float* Fd, float* Gd) {
+    int tid_s = threadIdx.x;
+    asm volatile("" : "+v"(tid_s));
+    stage_fg<NT, S, G, IQN>(a, b0s, tid_s, ins, L.enc, Fd, Gd);
+    static_assert((G * (kNcos / 8)) % (kNW * 64) == 0, "whole cos chunks per thread");
+#pragma unroll
+    for (int u = 0; u < G * (kNcos / 8) / (kNW * 64); ++u) {
+      const int c = tid_s + u * kNW * 64;
+      const int row = c / (kNcos / 8), ch = c % (kNcos / 8);
+      const float tau = ins[IL::kTau + row];
+      frag8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (elem_t)cos_pi_k_tau(tau, 8 * ch + j);
+      row_store<kNcos>(cosd, row, 8 * ch, v);
+    }
+  };
+  if constexpr (AH) {
+    if (blockIdx.x < a.rounds) stage(blockIdx.x * G / NT, L.in[0], L.cos[0], L.F[0], L.G[0]);
+    __syncthreads();
+  }
+
   // persistent per-wave weight-gradient accumulators (rows = this wave's features, positions)
   f32x16 dW2[4], dW1[8], dWc[4];
 #pragma unroll
@@ -404,6 +439,15 @@ void critic_fused_kernel(FusedArgs a) {
   f32x16 dWo = f32x16{};
 #pragma unroll
   for (int g = 0; g < (IQN ? 1 : 16); ++g) dwo[g] = 0.f;
+  constexpr bool WCR = AH && ASVRL_WC_RESIDENT;
+  frag8 wcr0[WCR ? 4 : 1], wcr1[WCR ? 4 : 1];   // resident cos-layer fragments (blocks 2w, 2w + 1)
+  if constexpr (WCR) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      wcr0[ks] = WC[((2 * w) * 4 + ks) * 64 + lane];
+      wcr1[ks] = WC[((2 * w + 1) * 4 + ks) * 64 + lane];
+    }
+  }
   float encr[IQN ? 8 : 1];   // IQN with parts.enc: this lane's feature's encoder sums
 #pragma unroll
   for (int i = 0; i < (IQN ? 8 : 1); ++i) encr[i] = 0.f;
@@ -434,7 +478,13 @@ void critic_fused_kernel(FusedArgs a) {
     // ---------------- stage: F, G, xb; cos(tau pi k) for the round's rows (natural order); the
     // cos layer's weight fragments are fetched meanwhile
     frag8 wc0[4], wc1[4];
-    {
+    if constexpr (WCR) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        wc0[ks] = wcr0[ks];
+        wc1[ks] = wcr1[ks];
+      }
+    } else {
       ASVRL_FRESH_LANE();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
@@ -442,25 +492,19 @@ void critic_fused_kernel(FusedArgs a) {
         wc1[ks] = WC[((2 * w + 1) * 4 + ks) * 64 + lane];
       }
     }
-    {
-      int tid_s = threadIdx.x;
-      asm volatile("" : "+v"(tid_s));
-      stage_fg<NT, S, G, IQN>(a, b0, tid_s, in, L.enc, L.F, L.G);
-      static_assert((G * (kNcos / 8)) % (kNW * 64) == 0, "whole cos chunks per thread");
-#pragma unroll
-      for (int u = 0; u < G * (kNcos / 8) / (kNW * 64); ++u) {
-        const int c = tid_s + u * kNW * 64;
-        const int row = c / (kNcos / 8), ch = c % (kNcos / 8);
-        const float tau = in[IL::kTau + row];
-        frag8 v;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (elem_t)cos_pi_k_tau(tau, 8 * ch + j);
-        row_store<kNcos>(L.cos, row, 8 * ch, v);
-      }
+    const int sb = AH ? buf : 0;   // this round's F, G, cos images
+    elem_t* const cosb = L.cos[sb];
+    float* const Fb = L.F[sb];
+    float* const Gb = L.G[sb];
+    if constexpr (!AH) {
+      stage(b0, in, cosb, Fb, Gb);
+      ASVRL_STAMP(0);
+      __syncthreads();
+      ASVRL_STAMP(1);
+    } else {   // staged by the previous round (or the prologue)
+      ASVRL_STAMP(0);
+      ASVRL_STAMP(1);
     }
-    ASVRL_STAMP(0);
-    __syncthreads();
-    ASVRL_STAMP(1);
 
     // ---------------- L0: c = relu(Wc cos + bc), x = F * c      (this wave: blocks 2w, 2w+1); W1 fetched
     frag8 w1f[16];
@@ -475,12 +519,12 @@ void critic_fused_kernel(FusedArgs a) {
 #pragma unroll
         for (int j = 0; j < NB; ++j)
 #pragma unroll
-          for (int s = 0; s < 2; ++s) lds8(L.F + ((32 * j + r) / NT) * kC + mb * 32 + 16 * s + 8 * h, fv[j][s]);
+          for (int s = 0; s < 2; ++s) lds8(Fb + ((32 * j + r) / NT) * kC + mb * 32 + 16 * s + 8 * h, fv[j][s]);
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
           f32x16 acc = acc_init(bcp, mb * 32, h);
 #pragma unroll
-          for (int ks = 0; ks < 4; ++ks) acc = mfma(mq ? wc1[ks] : wc0[ks], rowf(L.cos, RA_cos, j, ks), acc);
+          for (int ks = 0; ks < 4; ++ks) acc = mfma(mq ? wc1[ks] : wc0[ks], rowf(cosb, RA_cos, j, ks), acc);
           if constexpr (!kBiasFirst) acc += bias_init(bcp, mb * 32, h);
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
@@ -510,7 +554,7 @@ void critic_fused_kernel(FusedArgs a) {
 #pragma unroll
         for (int j = 0; j < NB; ++j)
 #pragma unroll
-          for (int s = 0; s < 2; ++s) lds8(L.G + ((32 * j + r) / NT) * kH + w * 32 + 16 * s + 8 * h, gv[j][s]);
+          for (int s = 0; s < 2; ++s) lds8(Gb + ((32 * j + r) / NT) * kH + w * 32 + 16 * s + 8 * h, gv[j][s]);
       f32x16 acc[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[j] = acc_init(b1p, w * 32, h);
@@ -712,7 +756,7 @@ void critic_fused_kernel(FusedArgs a) {
 #pragma unroll
         for (int j = 0; j < NB; ++j)
 #pragma unroll
-          for (int s = 0; s < 2; ++s) lds8(L.G + ((32 * j + r) / NT) * kH + w * 32 + 16 * s + 8 * h, gv[j][s]);
+          for (int s = 0; s < 2; ++s) lds8(Gb + ((32 * j + r) / NT) * kH + w * 32 + 16 * s + 8 * h, gv[j][s]);
       f32x16 acc[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[j] = f32x16{};
@@ -745,10 +789,10 @@ void critic_fused_kernel(FusedArgs a) {
       if constexpr (!IQN) {
         const bool enc = a.parts.aenc != nullptr;
         sample_sums<NT, NB>(gsa, w * 32, lane, [&](int bl, int p, float v) {
-          const float gm = L.G[bl * kH + p];
+          const float gm = Gb[bl * kH + p];
           const float dz = gm > 0.f ? v : 0.f;
           if (a.dzG != nullptr) a.dzG[static_cast<size_t>(b0 + bl) * kH + swap23(p)] = dz;
-          if (enc) L.G[bl * kH + p] = dz;   // G's block w is this wave's own: dzG in place
+          if (enc) Gb[bl * kH + p] = dz;   // G's block w is this wave's own: dzG in place
         });
         if (enc) {
           // action_encoder's gradient (AC_IQN_model.py:468-470): lane (half hh, position 32w + rr)
@@ -757,7 +801,7 @@ void critic_fused_kernel(FusedArgs a) {
           float s0 = 0.f, s1 = 0.f, sb = 0.f;
 #pragma unroll
           for (int k = hh; k < S; k += 2) {
-            const float d = L.G[k * kH + p];
+            const float d = Gb[k * kH + p];
             s0 += d * in[IL::kAct + 2 * k];
             s1 += d * in[IL::kAct + 2 * k + 1];
             sb += d;
@@ -767,6 +811,13 @@ void critic_fused_kernel(FusedArgs a) {
           acc[2 * kH] += s1;
           acc[4 * kH] += sb;
         }
+      }
+    }
+    if constexpr (AH) {   // the next round's inputs, for its staging in this round's last phase
+#pragma unroll
+      for (int u = 0; u < IL::kPer; ++u) {
+        const int e = tid_p + u * kNW * 64;
+        if (e < IL::kSize) L.in[buf ^ 1][e] = pre[u];
       }
     }
     ASVRL_STAMP(12);
@@ -782,7 +833,7 @@ void critic_fused_kernel(FusedArgs a) {
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) wt[ks] = W1T[((2 * w) * 8 + ks) * 64 + lane];
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) wcc[ks] = WC[((2 * w) * 4 + ks) * 64 + lane];
+      for (int ks = 0; ks < 4; ++ks) wcc[ks] = WCR ? wcr0[ks] : WC[((2 * w) * 4 + ks) * 64 + lane];
 #pragma unroll
       for (int kk = 0; kk < G / 16; ++kk) {
         const frag8 A = trf(L.dz1, TA_d, kk, w);
@@ -790,6 +841,10 @@ void critic_fused_kernel(FusedArgs a) {
 #pragma unroll
         for (int n = 0; n < 8; ++n) mfma_acc(dW1[n], A, trf(L.x, TA_x, kk, n));
       }
+    }
+    if constexpr (AH) {   // round t + grid's images, behind the dW1 MFMAs
+      const int tn = t + static_cast<int>(gridDim.x);
+      if (tn < a.rounds) stage(tn * G / NT, L.in[buf ^ 1], L.cos[buf ^ 1], L.F[buf ^ 1], L.G[buf ^ 1]);
     }
 
     // ---------------- L4: dx = W1^T dz1 (own blocks 2w, 2w+1) with c = relu(Wc cos + bc) recomputed
@@ -806,7 +861,7 @@ void critic_fused_kernel(FusedArgs a) {
 #pragma unroll
       for (int j = 0; j < NB; ++j)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) lds8(L.F + ((32 * j + r) / NT) * kC + mb * 32 + 16 * s + 8 * h, fv[j][s]);
+        for (int s = 0; s < 2; ++s) lds8(Fb + ((32 * j + r) / NT) * kC + mb * 32 + 16 * s + 8 * h, fv[j][s]);
       float fsa[NB][16];
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
@@ -815,7 +870,7 @@ void critic_fused_kernel(FusedArgs a) {
         for (int ks = 0; ks < 8; ++ks) dx = mfma(wt[ks], rowf(L.dz1, RA_d, j, ks), dx);
         f32x16 cc = acc_init(bcp, mb * 32, h);
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) cc = mfma(wcc[ks], rowf(L.cos, RA_cos, j, ks), cc);
+        for (int ks = 0; ks < 4; ++ks) cc = mfma(wcc[ks], rowf(cosb, RA_cos, j, ks), cc);
         if constexpr (!kBiasFirst) cc += bias_init(bcp, mb * 32, h);
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
@@ -833,13 +888,13 @@ void critic_fused_kernel(FusedArgs a) {
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks) wt[ks] = W1T[((2 * w + 1) * 8 + ks) * 64 + lane];
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) wcc[ks] = WC[((2 * w + 1) * 4 + ks) * 64 + lane];
+        for (int ks = 0; ks < 4; ++ks) wcc[ks] = WCR ? wcr1[ks] : WC[((2 * w + 1) * 4 + ks) * 64 + lane];
       }
       sample_sums<NT, NB>(fsa, mb * 32, lane, [&](int bl, int p, float v) {
-        const float fm = L.F[bl * kC + p];
+        const float fm = Fb[bl * kC + p];
         const float dz = fm > 0.f ? v : 0.f;
         if (a.dzF != nullptr) bp(a.dzF)[static_cast<size_t>(b0 + bl) * kC + swap23(p)] = (elem_t)dz;
-        if (a.parts.enc != nullptr) L.F[bl * kC + p] = dz;   // F's blocks 2w, 2w+1 are this wave's own
+        if (a.parts.enc != nullptr) Fb[bl * kC + p] = dz;   // F's blocks 2w, 2w+1 are this wave's own
       });
     }
     {
@@ -856,7 +911,7 @@ void critic_fused_kernel(FusedArgs a) {
         for (int i = 0; i < 8; ++i) acc[i] = 0.f;
 #pragma unroll
         for (int k = 0; k < S; ++k) {
-          const float d = L.F[k * kC + p];
+          const float d = Fb[k * kC + p];
           const float* x = in + IL::kObs + k * kObsIn + off;
 #pragma unroll
           for (int i = 0; i < kSelfIn; ++i) acc[i] += d * ((self || i < kObjIn) ? x[i] : 0.f);
@@ -883,16 +938,18 @@ void critic_fused_kernel(FusedArgs a) {
         dbc1 += sum8(A1);
 #pragma unroll
         for (int n = 0; n < 2; ++n) {
-          const frag8 Bf = trf(L.cos, TA_cos, kk, n);
+          const frag8 Bf = trf(cosb, TA_cos, kk, n);
           mfma_acc(dWc[n], A0, Bf);
           mfma_acc(dWc[2 + n], A1, Bf);
         }
       }
     }
+    if constexpr (!AH) {
 #pragma unroll
-    for (int u = 0; u < IL::kPer; ++u) {
-      const int e = tid_p + u * kNW * 64;
-      if (e < IL::kSize) L.in[buf ^ 1][e] = pre[u];
+      for (int u = 0; u < IL::kPer; ++u) {
+        const int e = tid_p + u * kNW * 64;
+        if (e < IL::kSize) L.in[buf ^ 1][e] = pre[u];
+      }
     }
     ASVRL_STAMP(14);
     __syncthreads();   // the next round overwrites cos, F, G, x, a, b, dz1
