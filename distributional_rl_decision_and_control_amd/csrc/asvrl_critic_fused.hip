@@ -49,14 +49,17 @@ constexpr int kC = 256, kH = 128, kNcos = 64, kNW = 4, kMaxA = ASVRL_IQN_MAX_ACT
 #ifndef ASVRL_PRE_AT
 #define ASVRL_PRE_AT 1
 #endif
-// stage-ahead (A/B knob): round t + grid's F, G and cos images are staged in round t's last phase into
-// a second set of images (double-buffered), so a round starts with its first layer instead of the
-// staging phase and its barrier. Where the second set fits in LDS: AC-IQN, N = 32, bf16 operands.
+// stage-ahead (1, default): round t + grid's F, G and cos images are staged in round t's last phase,
+// behind the dW1 MFMAs, into a second set of images (double-buffered), so a round starts with its first
+// layer instead of the staging phase and its barrier. Where the second set fits in LDS: AC-IQN, N = 32,
+// bf16 operands (the bench shape). Measured 129-133 -> 125-127 us per launch, round 34.2k -> 33.4k
+// cycles (profiles/r02_stage_ahead_ab.txt).
 #ifndef ASVRL_STAGE_AHEAD
-#define ASVRL_STAGE_AHEAD 0
+#define ASVRL_STAGE_AHEAD 1
 #endif
 // with stage-ahead: the cos layer's weight fragments of the wave's two blocks held in registers for the
 // kernel's life (L0 and L4 read the same 8 fragments every round) instead of fetched three times a round
+// (the VGPRs stage-ahead frees): 125-127 -> 121-126 us, round 32.8k cycles (profiles/r02_wc_resident_ab.txt)
 #ifndef ASVRL_WC_RESIDENT
 #define ASVRL_WC_RESIDENT 1
 #endif
