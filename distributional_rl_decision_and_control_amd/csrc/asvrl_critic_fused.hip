@@ -57,6 +57,10 @@ constexpr int kC = 256, kH = 128, kNcos = 64, kNW = 4, kMaxA = ASVRL_IQN_MAX_ACT
 #ifndef ASVRL_STAGE_AHEAD
 #define ASVRL_STAGE_AHEAD 1
 #endif
+// stage-ahead for IQN_Policy's update at N = 32 too (its second image set fits: no action features)
+#ifndef ASVRL_STAGE_AHEAD_IQN
+#define ASVRL_STAGE_AHEAD_IQN 0
+#endif
 // with stage-ahead: the cos layer's weight fragments of the wave's two blocks held in registers for the
 // kernel's life (L0 and L4 read the same 8 fragments every round) instead of fetched three times a round
 // (the VGPRs stage-ahead frees): 125-127 -> 121-126 us, round 32.8k cycles (profiles/r02_wc_resident_ab.txt)
@@ -354,7 +358,7 @@ template <int NT, bool IQN>
 __global__ __launch_bounds__(kNW * 64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void critic_fused_kernel(FusedArgs a) {
   constexpr int NB = FusedNB<NT>::v, G = 32 * NB, S = G / NT, NA = IQN ? 1 : 2;
-  constexpr bool AH = ASVRL_STAGE_AHEAD && !IQN && NT == 32 && !ASVRL_OPERAND_F32;
+  constexpr bool AH = ASVRL_STAGE_AHEAD && (!IQN || ASVRL_STAGE_AHEAD_IQN) && NT == 32 && !ASVRL_OPERAND_F32;
   constexpr int NSB = AH ? 2 : 1;
   __shared__ __attribute__((aligned(16))) FusedLds<NT, NB, S, IQN, NSB> L;
   static_assert(sizeof(L) <= 160 * 1024, "fused critic LDS image exceeds the CU's 160 KB");
