@@ -57,9 +57,10 @@ constexpr int kC = 256, kH = 128, kNcos = 64, kNW = 4, kMaxA = ASVRL_IQN_MAX_ACT
 #ifndef ASVRL_STAGE_AHEAD
 #define ASVRL_STAGE_AHEAD 1
 #endif
-// stage-ahead for IQN_Policy's update at N = 32 too (its second image set fits: no action features)
+// stage-ahead for IQN_Policy's update at N = 32 too (its second image set fits: no action features):
+// IQN loop 2852-2863 -> 2892-2896 learn-steps/s (profiles/r02_iqn_stage_ahead_ab.txt)
 #ifndef ASVRL_STAGE_AHEAD_IQN
-#define ASVRL_STAGE_AHEAD_IQN 0
+#define ASVRL_STAGE_AHEAD_IQN 1
 #endif
 // with stage-ahead: the cos layer's weight fragments of the wave's two blocks held in registers for the
 // kernel's life (L0 and L4 read the same 8 fragments every round) instead of fetched three times a round
