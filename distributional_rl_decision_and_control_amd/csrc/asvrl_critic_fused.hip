@@ -355,6 +355,72 @@ __device__ __forceinline__ int row_action(const float* in, int bl, int A) {
   return ai < 0 ? 0 : (ai >= A ? A - 1 : ai);
 }
 
+// acc[j] += W(ks) B(j, ks) over ks < KS for the NB row blocks, B(j, ks) = rowf(img, RA, j, ks) read D
+// k-steps ahead: without the explicit read-ahead and a scheduling fence per k-step the compiler (at its
+// VGPR limit) issues each operand read right before its MFMA and waits for it (ds_read, s_waitcnt
+// lgkmcnt(0), v_mfma for every MFMA), exposing the LDS latency on every one. Same MFMA order (results
+// bit-identical); D = 0: the plain loop. D = 2 (default): round 32.8k -> 28.4k cycles, fused critic
+// 125 -> 110.5 us, AC-IQN step 0.316 -> 0.302 ms, IQN 2780 -> 2920 learn-steps/s; D = 3 spills
+// (profiles/r02_read_ahead_ab.txt).
+#ifndef ASVRL_READ_AHEAD
+#define ASVRL_READ_AHEAD 2
+#endif
+template <int KS, int NB, int P, class WF>
+__device__ __forceinline__ void mfma_rows(f32x16 (&acc)[NB], const elem_t* img, const RowA<P>& RA, WF wf) {
+  constexpr int D = ASVRL_READ_AHEAD < KS ? ASVRL_READ_AHEAD : KS;
+  if constexpr (D == 0) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int j = 0; j < NB; ++j) acc[j] = mfma(wf(ks), rowf(img, RA, j, ks), acc[j]);
+  } else {
+    frag8 bq[D][NB];
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+      for (int j = 0; j < NB; ++j) bq[d][j] = rowf(img, RA, j, d);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) acc[j] = mfma(wf(ks), bq[ks % D][j], acc[j]);
+      if (ks + D < KS)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) bq[ks % D][j] = rowf(img, RA, j, ks + D);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// The weight-gradient grid dW[n] += A(kk)^T-read x B(kk, n) over kk < KK, n < NN (mf(kk, n, A, B) does
+// the MFMA and, at n = 0, the bias sum): every B(kk, n) read D steps ahead in (kk, n) order, each A(kk)
+// a whole kk ahead, one scheduling fence per step (see mfma_rows).
+template <int KK, int NN, class AF, class BF, class MF>
+__device__ __forceinline__ void mfma_grid(AF af, BF bf, MF mf) {
+  constexpr int T = KK * NN, D0 = ASVRL_READ_AHEAD < T ? ASVRL_READ_AHEAD : T;
+  if constexpr (D0 == 0) {
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      const frag8 A = af(kk);
+#pragma unroll
+      for (int n = 0; n < NN; ++n) mf(kk, n, A, bf(kk, n));
+    }
+  } else {
+    constexpr int D = D0;
+    frag8 bq[D], aq[2];
+    aq[0] = af(0);
+#pragma unroll
+    for (int t = 0; t < D; ++t) bq[t] = bf(t / NN, t % NN);
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int kk = t / NN, n = t % NN;
+      if (n == 0 && kk + 1 < KK) aq[(kk + 1) % 2] = af(kk + 1);
+      mf(kk, n, aq[kk % 2], bq[t % D]);
+      if (t + D < T) bq[t % D] = bf((t + D) / NN, (t + D) % NN);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
 template <int NT, bool IQN>
 __global__ __launch_bounds__(kNW * 64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void critic_fused_kernel(FusedArgs a) {
@@ -520,6 +586,15 @@ void critic_fused_kernel(FusedArgs a) {
       ASVRL_FRESH_LANE();
       const RowA<kNcos> RA_cos(r, h);
       const RowA<kC> RA_x(r, h);
+      // the cos rows' operand fragments are the same for both blocks: with read-ahead, all read first
+      frag8 cb[ASVRL_READ_AHEAD ? NB : 1][4];
+      if constexpr (ASVRL_READ_AHEAD != 0) {
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) cb[j][ks] = rowf(cosb, RA_cos, j, ks);
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int mq = 0; mq < 2; ++mq) {
         const int mb = 2 * w + mq;
@@ -532,7 +607,9 @@ void critic_fused_kernel(FusedArgs a) {
         for (int j = 0; j < NB; ++j) {
           f32x16 acc = acc_init(bcp, mb * 32, h);
 #pragma unroll
-          for (int ks = 0; ks < 4; ++ks) acc = mfma(mq ? wc1[ks] : wc0[ks], rowf(cosb, RA_cos, j, ks), acc);
+          for (int ks = 0; ks < 4; ++ks)
+            acc = mfma(mq ? wc1[ks] : wc0[ks], ASVRL_READ_AHEAD ? cb[ASVRL_READ_AHEAD ? j : 0][ks]
+                                                                  : rowf(cosb, RA_cos, j, ks), acc);
           if constexpr (!kBiasFirst) acc += bias_init(bcp, mb * 32, h);
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
@@ -566,10 +643,7 @@ void critic_fused_kernel(FusedArgs a) {
       f32x16 acc[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[j] = acc_init(b1p, w * 32, h);
-#pragma unroll
-      for (int ks = 0; ks < kC / 16; ++ks)
-#pragma unroll
-        for (int j = 0; j < NB; ++j) acc[j] = mfma(w1f[ks], rowf(L.x, RA_x, j, ks), acc[j]);
+      mfma_rows<kC / 16, NB>(acc, L.x, RA_x, [&](int ks) { return w1f[ks]; });
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) w2f[ks] = W2[(w * 8 + ks) * 64 + lane];
 #if ASVRL_PRE_AT == 1
@@ -610,10 +684,7 @@ void critic_fused_kernel(FusedArgs a) {
       f32x16 z2[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) z2[j] = acc_init(b2p, w * 32, h);
-#pragma unroll
-      for (int ks = 0; ks < kH / 16; ++ks)
-#pragma unroll
-        for (int j = 0; j < NB; ++j) z2[j] = mfma(w2f[ks], rowf(L.a, RA_a, j, ks), z2[j]);
+      mfma_rows<kH / 16, NB>(z2, L.a, RA_a, [&](int ks) { return w2f[ks]; });
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) w2tf[ks] = W2T[(w * 8 + ks) * 64 + lane];
       if constexpr (!kBiasFirst)
@@ -747,13 +818,12 @@ void critic_fused_kernel(FusedArgs a) {
       ASVRL_FRESH_LANE();
       const TrA<kH> TA_a(lane);
       const TrA<kH> TA_b(lane);
-#pragma unroll
-      for (int kk = 0; kk < G / 16; ++kk) {
-        const frag8 A = trf(L.b, TA_b, kk, w);
-        db2 += sum8(A);
-#pragma unroll
-        for (int n = 0; n < 4; ++n) mfma_acc(dW2[n], A, trf(L.a, TA_a, kk, n));
-      }
+      mfma_grid<G / 16, 4>([&](int kk) { return trf(L.b, TA_b, kk, w); },
+                           [&](int kk, int n) { return trf(L.a, TA_a, kk, n); },
+                           [&](int kk, int n, const frag8& A, const frag8& B) {
+                             if (n == 0) db2 += sum8(A);
+                             mfma_acc(dW2[n], A, B);
+                           });
     }
     {
       ASVRL_FRESH_LANE();
@@ -768,10 +838,7 @@ void critic_fused_kernel(FusedArgs a) {
       f32x16 acc[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[j] = f32x16{};
-#pragma unroll
-      for (int ks = 0; ks < kH / 16; ++ks)
-#pragma unroll
-        for (int j = 0; j < NB; ++j) acc[j] = mfma(w2tf[ks], rowf(L.b, RA_b, j, ks), acc[j]);
+      mfma_rows<kH / 16, NB>(acc, L.b, RA_b, [&](int ks) { return w2tf[ks]; });
       // dz1 = dh1g G 1[h1 > 0]; dG = sum over the sample's taus of dh1g h1 (-> dzG = dG 1[G > 0])
 #pragma unroll
       for (int j = 0; j < NB; ++j) {   // h1 unpacked here, not earlier
@@ -842,13 +909,12 @@ void critic_fused_kernel(FusedArgs a) {
       for (int ks = 0; ks < 8; ++ks) wt[ks] = W1T[((2 * w) * 8 + ks) * 64 + lane];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) wcc[ks] = WCR ? wcr0[ks] : WC[((2 * w) * 4 + ks) * 64 + lane];
-#pragma unroll
-      for (int kk = 0; kk < G / 16; ++kk) {
-        const frag8 A = trf(L.dz1, TA_d, kk, w);
-        db1 += sum8(A);
-#pragma unroll
-        for (int n = 0; n < 8; ++n) mfma_acc(dW1[n], A, trf(L.x, TA_x, kk, n));
-      }
+      mfma_grid<G / 16, 8>([&](int kk) { return trf(L.dz1, TA_d, kk, w); },
+                           [&](int kk, int n) { return trf(L.x, TA_x, kk, n); },
+                           [&](int kk, int n, const frag8& A, const frag8& B) {
+                             if (n == 0) db1 += sum8(A);
+                             mfma_acc(dW1[n], A, B);
+                           });
     }
     if constexpr (AH) {   // round t + grid's images, behind the dW1 MFMAs
       const int tn = t + static_cast<int>(gridDim.x);
@@ -871,14 +937,30 @@ void critic_fused_kernel(FusedArgs a) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) lds8(Fb + ((32 * j + r) / NT) * kC + mb * 32 + 16 * s + 8 * h, fv[j][s]);
       float fsa[NB][16];
+      f32x16 dxs[ASVRL_READ_AHEAD ? NB : 1], ccs[ASVRL_READ_AHEAD ? NB : 1];
+      if constexpr (ASVRL_READ_AHEAD != 0) {
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          dxs[j] = f32x16{};
+          ccs[j] = acc_init(bcp, mb * 32, h);
+        }
+        mfma_rows<8, NB>(dxs, L.dz1, RA_d, [&](int ks) { return wt[ks]; });
+        mfma_rows<4, NB>(ccs, cosb, RA_cos, [&](int ks) { return wcc[ks]; });
+      }
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
-        f32x16 dx = f32x16{};
+        f32x16 dx, cc;
+        if constexpr (ASVRL_READ_AHEAD != 0) {
+          dx = dxs[ASVRL_READ_AHEAD ? j : 0];
+          cc = ccs[ASVRL_READ_AHEAD ? j : 0];
+        } else {
+          dx = f32x16{};
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks) dx = mfma(wt[ks], rowf(L.dz1, RA_d, j, ks), dx);
-        f32x16 cc = acc_init(bcp, mb * 32, h);
+          for (int ks = 0; ks < 8; ++ks) dx = mfma(wt[ks], rowf(L.dz1, RA_d, j, ks), dx);
+          cc = acc_init(bcp, mb * 32, h);
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) cc = mfma(wcc[ks], rowf(cosb, RA_cos, j, ks), cc);
+          for (int ks = 0; ks < 4; ++ks) cc = mfma(wcc[ks], rowf(cosb, RA_cos, j, ks), cc);
+        }
         if constexpr (!kBiasFirst) cc += bias_init(bcp, mb * 32, h);
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
