@@ -365,6 +365,10 @@ __device__ __forceinline__ int row_action(const float* in, int bl, int A) {
 #ifndef ASVRL_READ_AHEAD
 #define ASVRL_READ_AHEAD 2
 #endif
+// the cos layer's weight-gradient loop with its next k-step's operands in flight (A/B knob)
+#ifndef ASVRL_DWC_AHEAD
+#define ASVRL_DWC_AHEAD 0
+#endif
 template <int KS, int NB, int P, class WF>
 __device__ __forceinline__ void mfma_rows(f32x16 (&acc)[NB], const elem_t* img, const RowA<P>& RA, WF wf) {
   constexpr int D = ASVRL_READ_AHEAD < KS ? ASVRL_READ_AHEAD : KS;
@@ -1020,17 +1024,41 @@ void critic_fused_kernel(FusedArgs a) {
       ASVRL_FRESH_LANE();
       const TrA<kNcos> TA_cos(lane);
       const TrA<kNcos> TA_dzc(lane);
+      if constexpr (ASVRL_DWC_AHEAD != 0) {   // k-step kk + 1's four operands read during kk's MFMAs
+        frag8 q[2][4];
+        auto load = [&](int kk, frag8 (&d)[4]) {
+          d[0] = trf(dzc_w, TA_dzc, kk, 0);
+          d[1] = trf(dzc_w, TA_dzc, kk, 1);
+          d[2] = trf(cosb, TA_cos, kk, 0);
+          d[3] = trf(cosb, TA_cos, kk, 1);
+        };
+        load(0, q[0]);
 #pragma unroll
-      for (int kk = 0; kk < G / 16; ++kk) {
-        const frag8 A0 = trf(dzc_w, TA_dzc, kk, 0);
-        const frag8 A1 = trf(dzc_w, TA_dzc, kk, 1);
-        dbc0 += sum8(A0);
-        dbc1 += sum8(A1);
+        for (int kk = 0; kk < G / 16; ++kk) {
+          if (kk + 1 < G / 16) load(kk + 1, q[(kk + 1) % 2]);
+          const frag8(&o)[4] = q[kk % 2];
+          dbc0 += sum8(o[0]);
+          dbc1 += sum8(o[1]);
 #pragma unroll
-        for (int n = 0; n < 2; ++n) {
-          const frag8 Bf = trf(cosb, TA_cos, kk, n);
-          mfma_acc(dWc[n], A0, Bf);
-          mfma_acc(dWc[2 + n], A1, Bf);
+          for (int n = 0; n < 2; ++n) {
+            mfma_acc(dWc[n], o[0], o[2 + n]);
+            mfma_acc(dWc[2 + n], o[1], o[2 + n]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < G / 16; ++kk) {
+          const frag8 A0 = trf(dzc_w, TA_dzc, kk, 0);
+          const frag8 A1 = trf(dzc_w, TA_dzc, kk, 1);
+          dbc0 += sum8(A0);
+          dbc1 += sum8(A1);
+#pragma unroll
+          for (int n = 0; n < 2; ++n) {
+            const frag8 Bf = trf(cosb, TA_cos, kk, n);
+            mfma_acc(dWc[n], A0, Bf);
+            mfma_acc(dWc[2 + n], A1, Bf);
+          }
         }
       }
     }
