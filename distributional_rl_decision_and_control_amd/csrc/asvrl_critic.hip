@@ -243,6 +243,35 @@ __device__ __forceinline__ void iqn_act_select(const CriticArgs& a, const Critic
   a.act_out[static_cast<int64_t>(tile) * a.ld_act] = static_cast<double>(act);
 }
 
+// acc[mb] += W(mb, ks) B(ks) over ks < KS for MB feature blocks, the weight fragments W (staged in LDS)
+// of k-step ks + 1 read while k-step ks's MFMAs issue, one scheduling fence per k-step: otherwise each
+// MFMA waits on its own fragment read (A/B knob; same MFMA order, bit-identical).
+#ifndef ASVRL_CRIT_READ_AHEAD
+#define ASVRL_CRIT_READ_AHEAD 0
+#endif
+template <int KS, int MB, class WF, class BF>
+__device__ __forceinline__ void mfma_wrows(f32x16 (&acc)[MB], WF wf, BF bf) {
+  if constexpr (ASVRL_CRIT_READ_AHEAD == 0) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) acc[mb] = mfma(wf(mb, ks), bf(ks), acc[mb]);
+  } else {
+    frag8 aq[2][MB];
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) aq[0][mb] = wf(mb, 0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 1 < KS)
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) aq[(ks + 1) % 2][mb] = wf(mb, ks + 1);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) acc[mb] = mfma(aq[ks % 2][mb], bf(ks), acc[mb]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
 template <int MODE, int NT, class LT>
 __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, int tile, int lane, const elem_t* Fl,
                                             const float* Gl, float* wsum = nullptr) {
@@ -308,11 +337,8 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
   f32x16 acc1[4];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) acc1[mb] = f32x16{};
-#pragma unroll
-  for (int ks = 0; ks < kC / 16; ++ks) {
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb) acc1[mb] = mfma(W1[(mb * 16 + ks) * 64 + lane], hpk[ks], acc1[mb]);
-  }
+  mfma_wrows<kC / 16, 4>(acc1, [&](int mb, int ks) { return W1[(mb * 16 + ks) * 64 + lane]; },
+                         [&](int ks) { return hpk[ks]; });
   frag8 h1pk[8], gpk[8];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) {
@@ -337,11 +363,8 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
   f32x16 acc2[4];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) acc2[mb] = f32x16{};
-#pragma unroll
-  for (int ks = 0; ks < kH / 16; ++ks) {
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb) acc2[mb] = mfma(W2[(mb * 8 + ks) * 64 + lane], gpk[ks], acc2[mb]);
-  }
+  mfma_wrows<kH / 16, 4>(acc2, [&](int mb, int ks) { return W2[(mb * 8 + ks) * 64 + lane]; },
+                         [&](int ks) { return gpk[ks]; });
   float q;
   int ai = 0;   // IQN_TRAIN: the sample's action
   if constexpr (IQN) {
@@ -510,11 +533,8 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
   f32x16 acc3[4];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) acc3[mb] = f32x16{};
-#pragma unroll
-  for (int ks = 0; ks < kH / 16; ++ks) {
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb) acc3[mb] = mfma(W2T[(mb * 8 + ks) * 64 + lane], dz2pk[ks], acc3[mb]);
-  }
+  mfma_wrows<kH / 16, 4>(acc3, [&](int mb, int ks) { return W2T[(mb * 8 + ks) * 64 + lane]; },
+                         [&](int ks) { return dz2pk[ks]; });
   // dz1 = dh1g * G * 1[h1 > 0]; gsa collects dh1g * h1 for dG = its sum over the sample's taus.
   // G is re-read here through an opaque offset: reusing layer 1's reads would keep 64 values live
   int g0 = 0;
