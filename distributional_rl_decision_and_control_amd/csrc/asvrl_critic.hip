@@ -245,13 +245,14 @@ __device__ __forceinline__ void iqn_act_select(const CriticArgs& a, const Critic
 
 // acc[mb] += W(mb, ks) B(ks) over ks < KS for MB feature blocks, the weight fragments W (staged in LDS)
 // of k-step ks + 1 read while k-step ks's MFMAs issue, one scheduling fence per k-step: otherwise each
-// MFMA waits on its own fragment read (A/B knob; same MFMA order, bit-identical).
+// MFMA waits on its own fragment read (A/B knob; same MFMA order, bit-identical). Not for IQN_ACT, whose
+// 16-wave launch holds 128 VGPRs.
 #ifndef ASVRL_CRIT_READ_AHEAD
 #define ASVRL_CRIT_READ_AHEAD 0
 #endif
-template <int KS, int MB, class WF, class BF>
+template <int KS, int MB, bool RA, class WF, class BF>
 __device__ __forceinline__ void mfma_wrows(f32x16 (&acc)[MB], WF wf, BF bf) {
-  if constexpr (ASVRL_CRIT_READ_AHEAD == 0) {
+  if constexpr (ASVRL_CRIT_READ_AHEAD == 0 || !RA) {
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
@@ -337,7 +338,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
   f32x16 acc1[4];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) acc1[mb] = f32x16{};
-  mfma_wrows<kC / 16, 4>(acc1, [&](int mb, int ks) { return W1[(mb * 16 + ks) * 64 + lane]; },
+  mfma_wrows<kC / 16, 4, MODE != MODE_IQN_ACT>(acc1, [&](int mb, int ks) { return W1[(mb * 16 + ks) * 64 + lane]; },
                          [&](int ks) { return hpk[ks]; });
   frag8 h1pk[8], gpk[8];
 #pragma unroll
@@ -363,7 +364,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
   f32x16 acc2[4];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) acc2[mb] = f32x16{};
-  mfma_wrows<kH / 16, 4>(acc2, [&](int mb, int ks) { return W2[(mb * 8 + ks) * 64 + lane]; },
+  mfma_wrows<kH / 16, 4, MODE != MODE_IQN_ACT>(acc2, [&](int mb, int ks) { return W2[(mb * 8 + ks) * 64 + lane]; },
                          [&](int ks) { return gpk[ks]; });
   float q;
   int ai = 0;   // IQN_TRAIN: the sample's action
@@ -533,7 +534,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
   f32x16 acc3[4];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) acc3[mb] = f32x16{};
-  mfma_wrows<kH / 16, 4>(acc3, [&](int mb, int ks) { return W2T[(mb * 8 + ks) * 64 + lane]; },
+  mfma_wrows<kH / 16, 4, MODE != MODE_IQN_ACT>(acc3, [&](int mb, int ks) { return W2T[(mb * 8 + ks) * 64 + lane]; },
                          [&](int ks) { return dz2pk[ks]; });
   // dz1 = dh1g * G * 1[h1 > 0]; gsa collects dh1g * h1 for dG = its sum over the sample's taus.
   // G is re-read here through an opaque offset: reusing layer 1's reads would keep 64 values live

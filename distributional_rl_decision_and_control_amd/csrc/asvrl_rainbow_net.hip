@@ -115,6 +115,35 @@ __device__ __forceinline__ void phase_encode(const AsvRainbowImg& W, const float
   }
 }
 
+// MFMA chains whose A operands (weight fragment images) come from L2: t < T steps, step t's fragment(s)
+// fetched D steps ahead into a ring, one scheduling fence per step -- otherwise every MFMA waits for its
+// own global load (A/B knob ASVRL_RB_READ_AHEAD = D; same MFMA order, bit-identical).
+#ifndef ASVRL_RB_READ_AHEAD
+#define ASVRL_RB_READ_AHEAD 0
+#endif
+template <int T, int NA, class AF, class MF>
+__device__ __forceinline__ void mfma_ring(AF af, MF mf) {
+  constexpr int D = ASVRL_RB_READ_AHEAD < T ? ASVRL_RB_READ_AHEAD : T;
+  if constexpr (D == 0) {
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      frag8 A[NA];
+      af(t, A);
+      mf(t, A);
+    }
+  } else {
+    frag8 q[D][NA];
+#pragma unroll
+    for (int t = 0; t < D; ++t) af(t, q[t]);
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      mf(t, q[t % D]);
+      if (t + D < T) af(t + D, q[t % D]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
 // one hidden layer pair (value, advantage streams; wave w: block w of each): out = relu(W in + b)
 template <int K, bool SAVE>
 __device__ __forceinline__ void phase_hidden(const void* wv, const void* wa, const float* bv, const float* ba,
@@ -126,13 +155,17 @@ __device__ __forceinline__ void phase_hidden(const void* wv, const void* wa, con
   const RowA<K> RX(r, h);
   const RowA<kHid> RH(r, h);
   f32x16 av = acc_init(bv, w * 32, h), aa = acc_init(ba, w * 32, h);
-#pragma unroll
-  for (int ks = 0; ks < K / 16; ++ks) {
-    const frag8 b0 = rowf(inv, RX, 0, ks);
-    av = mfma(V[(w * (K / 16) + ks) * 64 + lane], b0, av);
-    const frag8 b1 = inv == ina ? b0 : rowf(ina, RX, 0, ks);
-    aa = mfma(A[(w * (K / 16) + ks) * 64 + lane], b1, aa);
-  }
+  mfma_ring<K / 16, 2>(
+      [&](int ks, frag8(&q)[2]) {
+        q[0] = V[(w * (K / 16) + ks) * 64 + lane];
+        q[1] = A[(w * (K / 16) + ks) * 64 + lane];
+      },
+      [&](int ks, const frag8(&q)[2]) {
+        const frag8 b0 = rowf(inv, RX, 0, ks);
+        av = mfma(q[0], b0, av);
+        const frag8 b1 = inv == ina ? b0 : rowf(ina, RX, 0, ks);
+        aa = mfma(q[1], b1, aa);
+      });
   if constexpr (!kBiasFirst) {
     av += bias_init(bv, w * 32, h);
     aa += bias_init(ba, w * 32, h);
@@ -170,8 +203,8 @@ __device__ __forceinline__ void phase_vm(const AsvRainbowImg& W, const elem_t* h
   const elem_t* src = val ? hv2 : ha2;
   const RowA<kHid> RH(r, h);
   f32x16 acc = acc_init(bias, blk * 32, h);
-#pragma unroll
-  for (int ks = 0; ks < kHid / 16; ++ks) acc = mfma(M[(blk * 8 + ks) * 64 + lane], rowf(src, RH, 0, ks), acc);
+  mfma_ring<kHid / 16, 1>([&](int ks, frag8(&q)[1]) { q[0] = M[(blk * 8 + ks) * 64 + lane]; },
+                          [&](int ks, const frag8(&q)[1]) { acc = mfma(q[0], rowf(src, RH, 0, ks), acc); });
   if constexpr (!kBiasFirst) acc += bias_init(bias, blk * 32, h);
   float* dst = (val ? vl : ml) + r * kAP + blk * 32;
 #pragma unroll
@@ -206,12 +239,13 @@ __device__ __forceinline__ void action_logits(const AsvRainbowImg& W, const frag
   const int h = lane >> 5;
   const frag8* AO = reinterpret_cast<const frag8*>(W.ao);
 #pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    acc[b] = acc_init(W.b_aop + k * kAP, b * 32, h);
+  for (int b = 0; b < 2; ++b) acc[b] = acc_init(W.b_aop + k * kAP, b * 32, h);
+  mfma_ring<2 * (kHid / 16), 1>(
+      [&](int t, frag8(&q)[1]) { q[0] = AO[((k * 2 + t / 8) * 8 + t % 8) * 64 + lane]; },
+      [&](int t, const frag8(&q)[1]) { acc[t / 8] = mfma(q[0], bh[t % 8], acc[t / 8]); });
 #pragma unroll
-    for (int ks = 0; ks < kHid / 16; ++ks) acc[b] = mfma(AO[((k * 2 + b) * 8 + ks) * 64 + lane], bh[ks], acc[b]);
+  for (int b = 0; b < 2; ++b)
     if constexpr (!kBiasFirst) acc[b] += bias_init(W.b_aop + k * kAP, b * 32, h);
-  }
 }
 
 __device__ __forceinline__ float fexp(float x) {

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Rainbow network kernels with the weight fragments fetched D steps ahead (rb4, rb8) vs default: Rainbow tests
+# on each, then the bench's Rainbow line alternating.
+set -o pipefail
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+for L in rb4 rb8; do
+  ASVRL_LIB=variants/libasvrl_$L.so timeout -k 10 300 python -u -m pytest tests/test_fused_rainbow_gpu.py -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/${L}_tests.log 2>&1
+  rc=$?; echo "$L"; tail -1 gpurun_out/${L}_tests.log; [ $rc -eq 0 ] || exit $rc
+done
+for rep in 1 2; do
+  for L in default rb4 rb8; do
+    if [ "$L" = default ]; then unset ASVRL_LIB; else export ASVRL_LIB=variants/libasvrl_$L.so; fi
+    timeout -k 10 300 python bench.py --steps 20 --warmup 4 --iqn-steps 0 --config5-steps 0 --plateau-envs 0 --no-cpu-baseline --rainbow-steps 40 > gpurun_out/rbra_$L.json 2> gpurun_out/rbra_$L.err || exit 1
+    python3 -c "import json; d=json.loads(open('gpurun_out/rbra_$L.json').read().strip().splitlines()[-1]); print('$L', round(d['rainbow']['ms_per_step'], 4), round(d['rainbow']['env_steps_per_s']))"
+  done
+done
