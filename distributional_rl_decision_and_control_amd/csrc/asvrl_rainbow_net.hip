@@ -117,9 +117,10 @@ __device__ __forceinline__ void phase_encode(const AsvRainbowImg& W, const float
 
 // MFMA chains whose A operands (weight fragment images) come from L2: t < T steps, step t's fragment(s)
 // fetched D steps ahead into a ring, one scheduling fence per step -- otherwise every MFMA waits for its
-// own global load (A/B knob ASVRL_RB_READ_AHEAD = D; same MFMA order, bit-identical).
+// own global load (ASVRL_RB_READ_AHEAD = D; same MFMA order, bit-identical). D = 4 (default): Rainbow step
+// 0.489-0.494 -> 0.411-0.413 ms at 8192 envs (profiles/r02_rb_read_ahead_ab.txt); D = 8 no better.
 #ifndef ASVRL_RB_READ_AHEAD
-#define ASVRL_RB_READ_AHEAD 0
+#define ASVRL_RB_READ_AHEAD 4
 #endif
 template <int T, int NA, class AF, class MF>
 __device__ __forceinline__ void mfma_ring(AF af, MF mf) {
@@ -396,11 +397,15 @@ __device__ __forceinline__ void phase_back(const void* wvt, const void* wat, con
   const RowA<K> RD(r, h);
   dv = f32x16{};
   da = f32x16{};
-#pragma unroll
-  for (int ks = 0; ks < K / 16; ++ks) {
-    dv = mfma(VT[(mb * (K / 16) + ks) * 64 + lane], rowf(dinv, RD, 0, ks), dv);
-    da = mfma(AT[(mb * (K / 16) + ks) * 64 + lane], rowf(dina, RD, 0, ks), da);
-  }
+  mfma_ring<K / 16, 2>(
+      [&](int ks, frag8(&q)[2]) {
+        q[0] = VT[(mb * (K / 16) + ks) * 64 + lane];
+        q[1] = AT[(mb * (K / 16) + ks) * 64 + lane];
+      },
+      [&](int ks, const frag8(&q)[2]) {
+        dv = mfma(q[0], rowf(dinv, RD, 0, ks), dv);
+        da = mfma(q[1], rowf(dina, RD, 0, ks), da);
+      });
 }
 
 __global__ __launch_bounds__(kNW * 64) void rainbow_train_kernel(RbArgs a) {
@@ -555,17 +560,20 @@ __global__ __launch_bounds__(kNW * 64) void rainbow_train_kernel(RbArgs a) {
 #pragma unroll
     for (int ks = 0; ks < kAP / 16; ++ks) bq[ks] = rowf(dqi, RQ, 0, ks);
     f32x16 dv = f32x16{}, da = f32x16{};
-#pragma unroll
-    for (int ks = 0; ks < kAP / 16; ++ks) {
-      dv = mfma(VOT[(w * 4 + ks) * 64 + lane], bq[ks], dv);
-      da = mfma(MOT[(w * 4 + ks) * 64 + lane], bq[ks], da);   // - mean_k Wao[k]^T dq
-    }
+    mfma_ring<kAP / 16, 2>(
+        [&](int ks, frag8(&q)[2]) {
+          q[0] = VOT[(w * 4 + ks) * 64 + lane];
+          q[1] = MOT[(w * 4 + ks) * 64 + lane];
+        },
+        [&](int ks, const frag8(&q)[2]) {
+          dv = mfma(q[0], bq[ks], dv);
+          da = mfma(q[1], bq[ks], da);   // - mean_k Wao[k]^T dq
+        });
     for (int k = 0; k < kActs; ++k) {
       if (__builtin_amdgcn_readfirstlane(__ballot(act_r == k) != 0) == 0) continue;   // action absent from the tile
       const frag8 zero{};
-#pragma unroll
-      for (int ks = 0; ks < kAP / 16; ++ks)
-        da = mfma(AOT[((k * 4 + w) * 4 + ks) * 64 + lane], act_r == k ? bq[ks] : zero, da);
+      mfma_ring<kAP / 16, 1>([&](int ks, frag8(&q)[1]) { q[0] = AOT[((k * 4 + w) * 4 + ks) * 64 + lane]; },
+                             [&](int ks, const frag8(&q)[1]) { da = mfma(q[0], act_r == k ? bq[ks] : zero, da); });
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
