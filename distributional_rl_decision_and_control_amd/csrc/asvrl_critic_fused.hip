@@ -1189,10 +1189,16 @@ extern "C" int asvrl_debug_fused_stamps(uint64_t* out, int64_t n) {
 }
 #endif
 
+// CUs the persistent launch leaves to a concurrent stream (A/B knob): the rollout's small kernels that
+// queue while it holds every CU otherwise wait for its end
+#ifndef ASVRL_FUSED_CU_RESERVE
+#define ASVRL_FUSED_CU_RESERVE 0
+#endif
 extern "C" int32_t asvrl_critic_fused_groups(int32_t B, int32_t N) {
   if (B <= 0 || (N != 8 && N != 16 && N != 32)) return 0;
   const int rounds = fused_rounds(B, N);
-  return rounds < cu_count() ? rounds : cu_count();
+  const int cus = cu_count() > 2 * ASVRL_FUSED_CU_RESERVE ? cu_count() - ASVRL_FUSED_CU_RESERVE : cu_count();
+  return rounds < cus ? rounds : cus;
 }
 
 extern "C" int asvrl_critic_train_fused(const AsvCriticWeights* w, const AsvCriticIO* io, const AsvCriticParts* parts,
