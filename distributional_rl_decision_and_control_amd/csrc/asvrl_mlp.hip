@@ -26,6 +26,38 @@
 namespace asvrl {
 namespace {
 
+// The split actor kernels run one wave per SIMD (4 waves per 32-row workgroup), so a weight fragment
+// fetched from L2 right before its MFMA exposes the whole L2 latency on every MFMA of a chain. With
+// ASVRL_MLP_WPRE a chain's fragments are all fetched first (A/B knob; same MFMA order, bit-identical).
+#ifndef ASVRL_MLP_WPRE
+#define ASVRL_MLP_WPRE 0
+#endif
+template <int KS, int P>
+__device__ __forceinline__ f32x16 wchain(const frag8* W, int base, int lane, const elem_t* img, const RowA<P>& RA) {
+  f32x16 acc = f32x16{};
+  if constexpr (ASVRL_MLP_WPRE != 0) {
+    frag8 q[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) q[ks] = W[(base + ks) * 64 + lane];
+    if constexpr (ASVRL_MLP_WPRE >= 2) {   // the LDS operands too
+      frag8 b[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) b[ks] = rowf(img, RA, 0, ks);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) acc = mfma(q[ks], b[ks], acc);
+    } else {
+      __builtin_amdgcn_sched_barrier(0);   // every fetch issued before the chain (not sunk to its MFMA)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) acc = mfma(q[ks], rowf(img, RA, 0, ks), acc);
+    }
+  } else {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) acc = mfma(W[(base + ks) * 64 + lane], rowf(img, RA, 0, ks), acc);
+  }
+  return acc;
+}
+
 constexpr int kEnc = 256, kObsK = 32, kHid = 128, kNa = 2;
 constexpr int kSelfF = 56, kObjF = 40, kSelfIn = 7, kObjIn = 5, kObjN = 5;
 constexpr int kFragEnc = kEnc * kObsK / 8;   // 1024 fragments
@@ -362,9 +394,7 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_split_kernel(MlpArgs a) 
     const frag8* W1 = reinterpret_cast<const frag8*>(a.w.w1_frag);
     const RowA<kEnc> RX(r, h);
     const RowA<kHid> RH(r, h);
-    f32x16 acc = f32x16{};
-#pragma unroll
-    for (int ks = 0; ks < kEnc / 16; ++ks) acc = mfma(W1[(w * 16 + ks) * 64 + lane], rowf(L.x0, RX, 0, ks), acc);
+    const f32x16 acc = wchain<kEnc / 16>(W1, w * 16, lane, L.x0, RX);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       float v[8];
@@ -384,9 +414,7 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_split_kernel(MlpArgs a) 
   {
     const frag8* W2 = reinterpret_cast<const frag8*>(a.w.w2_frag);
     const RowA<kHid> RH(r, h);
-    f32x16 acc = f32x16{};
-#pragma unroll
-    for (int ks = 0; ks < kHid / 16; ++ks) acc = mfma(W2[(w * 8 + ks) * 64 + lane], rowf(L.h1, RH, 0, ks), acc);
+    const f32x16 acc = wchain<kHid / 16>(W2, w * 8, lane, L.h1, RH);
     float p0 = 0.f, p1 = 0.f;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -476,9 +504,7 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_split_kernel(MlpArgs
     const frag8* W2T = reinterpret_cast<const frag8*>(a.w.w2t_frag);
     float hv[16];
     load_block16(bp(io.h1) + rr * kHid, w, h, hv);
-    f32x16 acc = f32x16{};
-#pragma unroll
-    for (int ks = 0; ks < kHid / 16; ++ks) acc = mfma(W2T[(w * 8 + ks) * 64 + lane], rowf(dz2i, RH, 0, ks), acc);
+    const f32x16 acc = wchain<kHid / 16>(W2T, w * 8, lane, dz2i, RH);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       float dv[8];
@@ -501,9 +527,7 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_split_kernel(MlpArgs
       const int mb = 2 * w + q;
       float hv[16];
       load_block16(bp(io.h0) + rr * kEnc, mb, h, hv);
-      f32x16 acc = f32x16{};
-#pragma unroll
-      for (int ks = 0; ks < kHid / 16; ++ks) acc = mfma(W1T[(mb * 8 + ks) * 64 + lane], rowf(dz1i, RH, 0, ks), acc);
+      const f32x16 acc = wchain<kHid / 16>(W1T, mb * 8, lane, dz1i, RH);
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         float dv[8];
