@@ -365,6 +365,11 @@ __device__ __forceinline__ int row_action(const float* in, int bl, int A) {
 #ifndef ASVRL_READ_AHEAD
 #define ASVRL_READ_AHEAD 2
 #endif
+// instruction kinds the per-step fences let through (sched_barrier mask; 0: none, 0x6: VALU and SALU, so
+// independent vector work may fill the MFMA gaps while the reads stay ahead) -- A/B knob
+#ifndef ASVRL_RA_FENCE_MASK
+#define ASVRL_RA_FENCE_MASK 0
+#endif
 // the cos layer's weight-gradient loop with its next k-step's operands in flight (A/B knob)
 #ifndef ASVRL_DWC_AHEAD
 #define ASVRL_DWC_AHEAD 0
@@ -390,7 +395,7 @@ __device__ __forceinline__ void mfma_rows(f32x16 (&acc)[NB], const elem_t* img, 
       if (ks + D < KS)
 #pragma unroll
         for (int j = 0; j < NB; ++j) bq[ks % D][j] = rowf(img, RA, j, ks + D);
-      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(ASVRL_RA_FENCE_MASK);
     }
   }
 }
@@ -420,7 +425,7 @@ __device__ __forceinline__ void mfma_grid(AF af, BF bf, MF mf) {
       if (n == 0 && kk + 1 < KK) aq[(kk + 1) % 2] = af(kk + 1);
       mf(kk, n, aq[kk % 2], bq[t % D]);
       if (t + D < T) bq[t % D] = bf((t + D) / NN, (t + D) % NN);
-      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(ASVRL_RA_FENCE_MASK);
     }
   }
 }
