@@ -34,7 +34,7 @@ import os
 
 import torch
 
-from . import _abi
+from . import _abi, streams
 from .fused_critic import (CriticPack, PartialArena, TrainBuffers, critic_actor_grad, critic_forward, critic_train,
                            critic_train_fused, fused_train_supported, trunk_weight_grads_into, wout_groups)
 from .fused_mlp import ActorBuffers, MlpPack, actor_act, actor_backward, actor_forward, actor_train_forward
@@ -54,10 +54,11 @@ ENC_IN_KERNEL = os.environ.get("ASVRL_ENC_IN_KERNEL", "1") == "1"
 
 
 class SideStreams:
-    """Fork/join of independent launches onto `n` side streams of one device."""
+    """Fork/join of independent launches onto `n` side streams of one device (dedicated streams,
+    streams.py: never an alias of the capture or rollout stream)."""
 
     def __init__(self, device, n=2):
-        self.streams = [torch.cuda.Stream(device=device) for _ in range(n)]
+        self.streams = [streams.stream(device, ("side", i)) for i in range(n)]
 
     @contextlib.contextmanager
     def on(self, i):

@@ -21,6 +21,7 @@ import time
 
 import torch
 
+from . import streams
 from .fused_critic import FusedACIQN, ac_iqn_update_fused, fused_supported
 from .fused_update import FusedACIQNState, ac_iqn_update_fused2
 from .fused_iqn import FusedIQNState, iqn_update_fused
@@ -367,7 +368,7 @@ class VecTrainer:
         # stream, and the learner forks side streams of its own (fused_update.SideStreams)
         main = torch.cuda.current_stream(self.device)
         if self._streams is None:
-            self._streams = (torch.cuda.Stream(device=self.device), torch.cuda.Event(), torch.cuda.Event())
+            self._streams = (self.roll_stream(),) + self._roll_events()
         s_roll, ev_snap, ev_act = self._streams
         # the replay state the learner samples against (after the previous iteration's push, which
         # the caller's stream joined), copied on the learner's own stream: the learner's chain then
@@ -422,6 +423,14 @@ class VecTrainer:
             self._replay_ready = True
         return n
 
+    def roll_stream(self):
+        """The rollout's stream: a dedicated one (streams.py), never an alias of the capture stream or
+        of the learner's side streams."""
+        return streams.stream(self.device, "roll")
+
+    def _roll_events(self):
+        return torch.cuda.Event(), torch.cuda.Event()
+
     def _chained(self):
         return (self.chain and self.overlap and self._fused_learner() and not self.pipeline
                 and self.unroll % 2 == 0)
@@ -430,7 +439,7 @@ class VecTrainer:
         """self.unroll iterations with per-dependency stream ordering (captured only; see __init__)."""
         main = torch.cuda.current_stream(self.device)
         if self._streams is None:
-            self._streams = (torch.cuda.Stream(device=self.device), torch.cuda.Event(), torch.cuda.Event())
+            self._streams = (self.roll_stream(),) + self._roll_events()
         s_roll = self._streams[0]
         U = self.unroll
         ev_act = [torch.cuda.Event() for _ in range(U)]
@@ -462,7 +471,7 @@ class VecTrainer:
 
     def _capture(self):
         # warm up the captured region on a side stream (allocator + autograd state)
-        s = torch.cuda.Stream(device=self.device)
+        s = streams.stream(self.device, "warmup")
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
             for _ in range(3):
@@ -482,7 +491,9 @@ class VecTrainer:
         chained = self._chained()
         if chained:   # the ring state after the last eager push: what the graph's first learner samples against
             self.ring_snap2[(self.unroll - 1) % 2].copy_(self.replay.state)
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        # captured on the dedicated capture stream: torch.cuda.graph's default is a pool stream that a
+        # long process also hands out as "another" stream (streams.py)
+        with torch.cuda.graph(g, stream=streams.capture_stream(self.device), capture_error_mode="thread_local"):
             if chained:
                 self._graph_out = self._chain_body()
             else:
