@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("ASVRL_LIB", os.path.join(HERE, "lib", "libasvrl.so"))
 # the same sources built with f32 learner operands (the parity build; asvrl_operand_bytes() == 4)
 LIB_PATH_F32 = os.path.join(HERE, "lib", "libasvrl_f32.so")
 OPERANDS = {"bf16": (LIB_PATH, 2), "f32": (LIB_PATH_F32, 4)}
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
 OBS_DIM = 40   # self 7 | objects 25 | mask 5 | pad 3
@@ -58,7 +58,8 @@ class AsvParams(C.Structure):
 class AsvEnvState(C.Structure):
     _fields_ = [("n_envs", C.c_int32), ("max_robots", C.c_int32), ("max_obs", C.c_int32), ("max_cores", C.c_int32),
                 ("rs", C.c_void_p), ("rflags", C.c_void_p), ("n_robots", C.c_void_p), ("n_obs", C.c_void_p),
-                ("n_cores", C.c_void_p), ("ep_ts", C.c_void_p), ("obstacles", C.c_void_p), ("cores", C.c_void_p)]
+                ("n_cores", C.c_void_p), ("ep_ts", C.c_void_p), ("obstacles", C.c_void_p), ("cores", C.c_void_p),
+                ("robot_params", C.c_void_p)]
 
 
 class AsvStepCtl(C.Structure):

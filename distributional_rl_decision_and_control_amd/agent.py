@@ -10,7 +10,13 @@ save_latest_model / load_model surfaces and return types. Differences:
     (libasvrl_f32.so: the reference's fp32 arithmetic, pinned to its train_* outputs at 1e-5 by
     tests/test_learner_golden_gpu.py and test_agent_gpu.py); set_learner("fused-bf16") selects the
     bf16-operand training build, set_learner("torch") the torch-autograd restatement with the HIP
-    quantile-Huber kernel (learner.py). train_Rainbow runs learner.rainbow_update (C51 kernel);
+    quantile-Huber kernel (learner.py). train_Rainbow runs the hand-written Rainbow learner
+    (fused_rainbow.FusedRainbow: network, C51 projection, loss, backward and weight-gradient kernels)
+    of the same operand build, pinned to the reference's train_Rainbow by
+    tests/test_rainbow_golden_gpu.py; set_learner("torch") (or network dims the kernels do not take)
+    runs learner.rainbow_update (torch autograd + the C51 kernel). Every learner's optimiser: FusedAdam
+    (asvrl_adam_*, pinned to torch.optim.Adam at 1e-5) for AC-IQN / IQN, torch.optim.Adam for Rainbow
+    and DQN;
   * load_model rebuilds the optimizers for the loaded networks (the reference keeps
     optimizing the replaced ones, agent.py:684-698 vs :75-76,98);
   * DQN runs as the reference's plain torch update (BASELINE config 1 is the DQN plumbing run of
@@ -24,7 +30,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _abi
-from . import fused_iqn, fused_update
+from . import fused_iqn, fused_rainbow, fused_update
 from .learn_ops import rows_from_batch
 from .learner import FlatGrads, FusedAdam, ac_iqn_update, iqn_update, rainbow_update
 from .policy.AC_IQN_model import AC_IQN_Policy
@@ -69,6 +75,7 @@ class Agent:
         self.value_ranges_of_action = copy.deepcopy(value_ranges_of_action)
         self.action_size = action_size
         self.agent_type = agent_type
+        self._rb_seed = int(seed) + 999   # the kernel path's target-noise Philox stream
         self.num_tau = 8  # training quantiles N = N' (AC_IQN_model.py:462, IQN_model.py:74)
         self.tau_override = None  # optional list of pre-drawn taus for the next train() (tests)
         self.learner = "fused-f32"
@@ -140,7 +147,11 @@ class Agent:
             return None
         key = (B, self.num_tau)
         if self._fused is None or self._fused[0] != key:
-            if self.agent_type == "AC-IQN":
+            if self.agent_type == "Rainbow":
+                ok = fused_rainbow.supported(self.policy_local, B)
+                st = fused_rainbow.FusedRainbow(self.policy_local, self.policy_target, B, self.support,
+                                                operands=ops) if ok else None
+            elif self.agent_type == "AC-IQN":
                 ok = fused_update.supported(self.policy_local, B, self.num_tau)
                 st = fused_update.FusedACIQNState(self.policy_local, self.policy_target, B, self.num_tau,
                                                   operands=ops) if ok else None
@@ -265,11 +276,23 @@ class Agent:
         return loss.cpu().numpy()
 
     def train_Rainbow(self, reset_target_noise=True):
+        """agent.py:597-641. reset_target_noise=False keeps the target's noise buffers (the parity tests
+        inject the reference's draw); otherwise reset_noise() draws them (Philox in the kernel path)."""
         idxs, s, a, R, ns, nt, w = self.memory.sample(self.BATCH_SIZE)
-        loss, _ = rainbow_update(self.policy_local, self.policy_target, self.optimizer, self.grads, self.support, s, a,
-                                 R, ns, nt, w, gamma=self.GAMMA, n=self.n, vmin=self.Vmin, vmax=self.Vmax,
-                                 reset_target_noise=reset_target_noise)
-        loss = loss.cpu().numpy()
+        st = self._fused_state(s[0].shape[0])
+        if st is not None:   # the hand-written learner
+            rows = rows_from_batch(s, a.reshape(-1, 1).float(), R, ns, nt)
+            rows[:, 84] = w.reshape(-1)
+            self._rb_step = getattr(self, "_rb_step", 0) + 1
+            ctr = torch.full((1,), self._rb_step, dtype=torch.int64, device=self.device)
+            loss, _ = st.update(self.optimizer, self.grads, rows, gamma=self.GAMMA, n=self.n, vmin=self.Vmin,
+                                vmax=self.Vmax, seed=self._rb_seed, counter_dev=ctr,
+                                reset_target=reset_target_noise)
+        else:
+            loss, _ = rainbow_update(self.policy_local, self.policy_target, self.optimizer, self.grads, self.support,
+                                     s, a, R, ns, nt, w, gamma=self.GAMMA, n=self.n, vmin=self.Vmin, vmax=self.Vmax,
+                                     reset_target_noise=reset_target_noise)
+        loss = loss.cpu().numpy().copy()
         self.memory.update_priorities(idxs, loss)
         return loss
 

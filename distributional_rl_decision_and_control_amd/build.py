@@ -8,6 +8,7 @@ lib/libasvrl_f32.so  the same sources with ASVRL_OPERAND_F32=1: every learner op
                      the hand-written learner to the reference's fp32 arithmetic
 Sources compile to objects in parallel (lib/obj/), then each variant links once.
 """
+import hashlib
 import os
 import subprocess
 import sys
@@ -37,15 +38,56 @@ FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-ffp-contract=
          "-munsafe-fp-atomics", "-I", os.path.join(ROOT, "include")]
 
 
+def _sig(cmd):
+    """Signature of one compile: the full command (compiler, arch, every flag, the source) and this file's
+    own text, so a change of HIPCC, ASVRL_OFFLOAD_ARCH, FLAGS / SOURCE_FLAGS or build.py rebuilds."""
+    h = hashlib.sha1(" ".join(c for c in cmd if not c.endswith(".tmp")).encode())
+    with open(os.path.abspath(__file__), "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()
+
+
+def _obj_fresh(o, src, hdr_t, sig):
+    if not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(src), hdr_t):
+        return False
+    try:
+        with open(o + ".sig") as f:
+            return f.read().strip() == sig
+    except OSError:
+        return False
+
+
 def stale(out):
     if not os.path.exists(out):
         return True
     t = os.path.getmtime(out)
-    return any(os.path.getmtime(f) > t for f in SOURCES + HEADERS)
+    if any(os.path.getmtime(f) > t for f in SOURCES + HEADERS):
+        return True
+    try:   # the link's signature: the objects' signatures in order
+        with open(out + ".sig") as f:
+            return f.read().strip() != _link_sig(out)
+    except OSError:
+        return True
 
 
 def _obj(out, src):
     return os.path.join(os.path.dirname(out), "obj", os.path.basename(out) + "." + os.path.basename(src) + ".o")
+
+
+def _compile_cmd(out, src, extra):
+    sf = SOURCE_FLAGS.get(os.path.basename(src), [])
+    if extra:   # the f32 build: its accumulators are plain MFMA results (no AGPR pinning)
+        sf = [f for f in sf if f not in ("-mllvm", "-amdgpu-mfma-vgpr-form=1")]
+    o = _obj(out, src)
+    return [HIPCC] + FLAGS[:3] + ["-c"] + FLAGS[3:] + extra + sf + ["-o", o + ".tmp", src]
+
+
+def _link_sig(out):
+    extra = VARIANTS[out]
+    h = hashlib.sha1()
+    for src in SOURCES:
+        h.update(_sig(_compile_cmd(out, src, extra)).encode())
+    return h.hexdigest()
 
 
 def build_lib(force=False, verbose=False, jobs=None):
@@ -62,11 +104,9 @@ def build_lib(force=False, verbose=False, jobs=None):
         for src in SOURCES:
             o = _obj(out, src)
             objs.append(o)
-            if force or not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(src), hdr_t):
-                sf = SOURCE_FLAGS.get(os.path.basename(src), [])
-                if extra:   # the f32 build: its accumulators are plain MFMA results (no AGPR pinning)
-                    sf = [f for f in sf if f not in ("-mllvm", "-amdgpu-mfma-vgpr-form=1")]
-                todo.append(([HIPCC] + FLAGS[:3] + ["-c"] + FLAGS[3:] + extra + sf + ["-o", o + ".tmp", src], o))
+            cmd = _compile_cmd(out, src, extra)
+            if force or not _obj_fresh(o, src, hdr_t, _sig(cmd)):
+                todo.append((cmd, o))
         links.append((out, objs))
     running = []
     while todo or running:
@@ -74,19 +114,23 @@ def build_lib(force=False, verbose=False, jobs=None):
             cmd, o = todo.pop(0)
             if verbose:
                 print(" ".join(cmd))
-            running.append((subprocess.Popen(cmd), o))
-        p, o = running.pop(0)
+            running.append((subprocess.Popen(cmd), o, cmd))
+        p, o, cmd = running.pop(0)
         if p.wait() != 0:
-            for q, _ in running:
+            for q, _, _ in running:
                 q.wait()
             raise subprocess.CalledProcessError(p.returncode, f"hipcc -> {o}")
         os.replace(o + ".tmp", o)
+        with open(o + ".sig", "w") as f:
+            f.write(_sig(cmd) + "\n")
     for out, objs in links:
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"] + objs
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
         os.replace(out + ".tmp", out)
+        with open(out + ".sig", "w") as f:
+            f.write(_link_sig(out) + "\n")
     return OUT
 
 

@@ -28,7 +28,8 @@ constexpr int kBlock = 256;
 // env-step workgroup: one wave of whole envs when they fit (R <= 64), spreading a 4096-env batch
 // over every CU instead of packing 51 envs per 256-lane group onto a third of them
 __host__ __device__ constexpr int step_block(int R) { return R <= 64 ? 64 : 256; }
-constexpr int kMaxCores = 16;
+constexpr int kMaxCores = 16;        // the device reset sampler's LDS table (env_reset_kernel)
+constexpr int kMaxCoresStep = 4096;  // the step and the current field read the cores from HBM
 
 struct Regs {
   double x, y, th, vr0, vr1, vr2, v0, v1, v2, tl, tr, lp, rp;
@@ -333,7 +334,9 @@ __device__ __forceinline__ void draw_noise(const AsvParams& p, const AsvStepCtl&
 
 // Per-robot sweep (AsvEnvLaunch layout 2): one lane per robot, BLOCK / R whole envs per workgroup;
 // perception is one serial loop over the robot's candidates (wamv.py:478-511), top-5 kept in registers.
-template <int BLOCK>
+// PR: every robot's own vehicle / perception parameters from s.robot_params (reset_with_eval_config,
+// env.py:553-607); the env-level members (rewards, episode limit, core radius) stay p's.
+template <int BLOCK, bool PR>
 __global__ __launch_bounds__(BLOCK) void env_sweep_kernel(AsvParams p, AsvEnvState s,
                                                           const double* __restrict__ actions,
                                                           const double* __restrict__ noise,
@@ -353,6 +356,7 @@ __global__ __launch_bounds__(BLOCK) void env_sweep_kernel(AsvParams p, AsvEnvSta
   const bool exists = env_on && i < nrob;
   const size_t NT = static_cast<size_t>(s.n_envs) * R;
   const size_t idx = static_cast<size_t>(e) * R + i;
+  const AsvParams& P = PR ? s.robot_params[exists ? idx : 0] : p;   // this robot's parameters
 
   // LDS carve: positions/velocities of the block's robots after the move, their pre-step
   // deactivated flags, the envs' obstacles and per-env reductions.
@@ -398,7 +402,7 @@ __global__ __launch_bounds__(BLOCK) void env_sweep_kernel(AsvParams p, AsvEnvSta
     const double d_before = sqrt((gx - r.x) * (gx - r.x) + (gy - r.y) * (gy - r.y));
     const int nc = s.n_cores[e];
     const double* cores = s.cores + static_cast<size_t>(e) * s.max_cores * 4;
-    robot_act(p, r, actions[2 * idx], actions[2 * idx + 1], ctl.is_continuous, cores,
+    robot_act(P, r, actions[2 * idx], actions[2 * idx + 1], ctl.is_continuous, cores,
               nc < s.max_cores ? nc : s.max_cores);
     const double d_after = sqrt((gx - r.x) * (gx - r.x) + (gy - r.y) * (gy - r.y));
     reward = 0.0;
@@ -445,14 +449,14 @@ __global__ __launch_bounds__(BLOCK) void env_sweep_kernel(AsvParams p, AsvEnvSta
     so2 = cs * r.v0 + sn * r.v1;
     so3 = -sn * r.v0 + cs * r.v1;
     so4 = r.v2;
-    if (sqrt((gx - r.x) * (gx - r.x) + (gy - r.y) * (gy - r.y)) <= p.goal_dis) reach = true;
+    if (sqrt((gx - r.x) * (gx - r.x) + (gy - r.y) * (gy - r.y)) <= P.goal_dis) reach = true;
 
     int nkept = 0;
     const int no = s.n_obs[e];
     const int base = le * R;
     const uint64_t ctr = ctl.counter + (ctl.counter_dev != nullptr ? *ctl.counter_dev : 0ull);
     const int ncand = no + nrob;
-    const bool full_circle = 0.5 * p.angle >= kPi;
+    const bool full_circle = 0.5 * P.angle >= kPi;
     for (int k = 0; k < ncand; ++k) {
       double ox, oy, orad, vx0, vy0;
       int slot;
@@ -469,28 +473,28 @@ __global__ __launch_bounds__(BLOCK) void env_sweep_kernel(AsvParams p, AsvEnvSta
         if (j == i || soff[base + j]) continue;  // self / deactivated (wamv.py:487-491)
         ox = sx[base + j];
         oy = sy[base + j];
-        orad = p.r;
+        orad = PR ? s.robot_params[static_cast<size_t>(e) * R + j].r : p.r;   // the other robot's r
         vx0 = sv0[base + j];
         vy0 = sv1[base + j];
         slot = O + j;
       }
       double n0, n1, n2, n3, n4;
-      draw_noise<-1>(p, ctl, ctr, noise, idx, slot, O + R, n0, n1, n2, n3, n4);
+      draw_noise<-1>(P, ctl, ctr, noise, idx, slot, O + R, n0, n1, n2, n3, n4);
       const double pxn = ox + n0, pyn = oy + n1;  // Perception (wamv.py:27-40)
       const double vxn = vx0 + n2, vyn = vy0 + n3;
-      const double rn = p.r_mean_ratio * orad + (1 - p.r_mean_ratio) * n4 / kPi * orad;
+      const double rn = P.r_mean_ratio * orad + (1 - P.r_mean_ratio) * n4 / kPi * orad;
       const double qx = (cs * pxn + sn * pyn) + tx, qy = (-sn * pxn + cs * pyn) + ty;
       const double qn = sqrt(qx * qx + qy * qy);
-      if (qn > p.range + rn) continue;  // check_detection (wamv.py:293-303)
+      if (qn > P.range + rn) continue;  // check_detection (wamv.py:293-303)
       if (!full_circle) {              // atan2 lies in [-pi, pi]: the test only bites when angle < 2 pi
         const double ang = atan2(qy, qx);
-        if (ang < -0.5 * p.angle || ang > 0.5 * p.angle) continue;
+        if (ang < -0.5 * P.angle || ang > 0.5 * P.angle) continue;
       }
       if (!coll) {  // check_collision (wamv.py:281-291), true positions
-        const double d = sqrt((r.x - ox) * (r.x - ox) + (r.y - oy) * (r.y - oy)) - orad - p.r;
+        const double d = sqrt((r.x - ox) * (r.x - ox) + (r.y - oy) * (r.y - oy)) - orad - P.r;
         if (d <= 0.0) coll = true;
       }
-      Cand cd{qn - rn - p.r, qx, qy, cs * vxn + sn * vyn, -sn * vxn + cs * vyn, rn};
+      Cand cd{qn - rn - P.r, qx, qy, cs * vxn + sn * vyn, -sn * vxn + cs * vyn, rn};
       // heapq.nsmallest == stable ascending order: a new candidate passes equal keys
       cswap(cd.key < t0.key, cd, t0);
       cswap(cd.key < t1.key, cd, t1);
@@ -499,14 +503,14 @@ __global__ __launch_bounds__(BLOCK) void env_sweep_kernel(AsvParams p, AsvEnvSta
       cswap(cd.key < t4.key, cd, t4);
       ++nkept;
     }
-    cnt = nkept < p.max_obj_num ? nkept : p.max_obj_num;
+    cnt = nkept < P.max_obj_num ? nkept : P.max_obj_num;
     // COLREGs over the kept objects in order, stop at the first hit (wamv.py:517-521)
 #ifndef ASVRL_NO_COLREGS
-    if (cnt > 0) apply = colregs(p.r, cs, sn, r.v0, r.v1, t0.a, t0.b, t0.c, t0.d, t0.e, phi);
-    if (!apply && cnt > 1) apply = colregs(p.r, cs, sn, r.v0, r.v1, t1.a, t1.b, t1.c, t1.d, t1.e, phi);
-    if (!apply && cnt > 2) apply = colregs(p.r, cs, sn, r.v0, r.v1, t2.a, t2.b, t2.c, t2.d, t2.e, phi);
-    if (!apply && cnt > 3) apply = colregs(p.r, cs, sn, r.v0, r.v1, t3.a, t3.b, t3.c, t3.d, t3.e, phi);
-    if (!apply && cnt > 4) apply = colregs(p.r, cs, sn, r.v0, r.v1, t4.a, t4.b, t4.c, t4.d, t4.e, phi);
+    if (cnt > 0) apply = colregs(P.r, cs, sn, r.v0, r.v1, t0.a, t0.b, t0.c, t0.d, t0.e, phi);
+    if (!apply && cnt > 1) apply = colregs(P.r, cs, sn, r.v0, r.v1, t1.a, t1.b, t1.c, t1.d, t1.e, phi);
+    if (!apply && cnt > 2) apply = colregs(P.r, cs, sn, r.v0, r.v1, t2.a, t2.b, t2.c, t2.d, t2.e, phi);
+    if (!apply && cnt > 3) apply = colregs(P.r, cs, sn, r.v0, r.v1, t3.a, t3.b, t3.c, t3.d, t3.e, phi);
+    if (!apply && cnt > 4) apply = colregs(P.r, cs, sn, r.v0, r.v1, t4.a, t4.b, t4.c, t4.d, t4.e, phi);
 #endif
   }
 
@@ -1240,7 +1244,7 @@ extern "C" int asvrl_env_step_ex(const AsvParams* params, const AsvEnvState* sta
                                  const AsvEnvLaunch* launch, void* stream) {
   ASVRL_REQUIRE(params && state && ctl && out, "asvrl_env_step: null argument");
   ASVRL_REQUIRE(state->max_robots >= 1 && state->max_robots <= kBlock, "asvrl_env_step: max_robots must be in [1, 256]");
-  ASVRL_REQUIRE(state->max_obs >= 0 && state->max_cores >= 0 && state->max_cores <= kMaxCores,
+  ASVRL_REQUIRE(state->max_obs >= 0 && state->max_cores >= 0 && state->max_cores <= kMaxCoresStep,
                 "asvrl_env_step: bad max_obs/max_cores");
   ASVRL_REQUIRE(params->max_obj_num >= 0 && params->max_obj_num <= ASVRL_MAX_OBJ, "asvrl_env_step: max_obj_num > 5");
   ASVRL_REQUIRE(params->N >= 1, "asvrl_env_step: N < 1");
@@ -1259,8 +1263,10 @@ extern "C" int asvrl_env_step_ex(const AsvParams* params, const AsvEnvState* sta
   const int nm = ctl->noise_mode == 0 ? 0 : (ctl->noise_mode == 1 ? 1 : 2);
   const PairLaunch pl = pair_launch(state->max_robots, state->max_obs, state->n_envs, lc.block, lc.envs_per_block,
                                     nm == 2 ? 4 : 8);
+  const bool per_robot = state->robot_params != nullptr;
   ASVRL_REQUIRE(lc.layout != 1 || pl.smem <= 150 * 1024, "asvrl_env_step: the pair layout's LDS does not fit");
-  if (lc.layout != 2 && pl.smem <= 150 * 1024) {
+  ASVRL_REQUIRE(lc.layout != 1 || !per_robot, "asvrl_env_step: per-robot parameters take the sweep layout (2)");
+  if (lc.layout != 2 && !per_robot && pl.smem <= 150 * 1024) {
     const int grid = (state->n_envs + pl.epb - 1) / pl.epb;
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3(grid), dim3(pl.blk), pl.smem, as_stream(stream), *params, *state, actions, noise,
@@ -1279,12 +1285,14 @@ extern "C" int asvrl_env_step_ex(const AsvParams* params, const AsvEnvState* sta
   const int grid = (state->n_envs + epb - 1) / epb;
   const size_t smem = env_sweep_smem(state->max_robots, state->max_obs);
   ASVRL_REQUIRE(smem <= 160 * 1024, "asvrl_env_step: max_obs too large for LDS");
+  auto sweep = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(blk), smem, as_stream(stream), *params, *state, actions, noise, *ctl,
+                       *out);
+  };
   if (blk == 64)
-    hipLaunchKernelGGL((env_sweep_kernel<64>), dim3(grid), dim3(64), smem, as_stream(stream), *params, *state,
-                       actions, noise, *ctl, *out);
+    per_robot ? sweep(env_sweep_kernel<64, true>) : sweep(env_sweep_kernel<64, false>);
   else
-    hipLaunchKernelGGL((env_sweep_kernel<256>), dim3(grid), dim3(256), smem, as_stream(stream), *params,
-                       *state, actions, noise, *ctl, *out);
+    per_robot ? sweep(env_sweep_kernel<256, true>) : sweep(env_sweep_kernel<256, false>);
   return check_launch("asvrl_env_step");
 }
 
@@ -1311,7 +1319,7 @@ extern "C" int asvrl_env_reset(const AsvParams* params, const AsvEnvState* state
 extern "C" int asvrl_current_field(const double* cores, int32_t n_cores, double core_r, const double* xy,
                                    int32_t n, double* out, void* stream) {
   ASVRL_REQUIRE(xy && out && (n_cores == 0 || cores), "asvrl_current_field: null argument");
-  ASVRL_REQUIRE(n_cores >= 0 && n_cores <= kMaxCores, "asvrl_current_field: n_cores > 16");
+  ASVRL_REQUIRE(n_cores >= 0 && n_cores <= kMaxCoresStep, "asvrl_current_field: n_cores > 4096");
   if (n <= 0) return 0;
   hipLaunchKernelGGL(current_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, as_stream(stream), cores,
                      n_cores, core_r, xy, n, out);

@@ -198,7 +198,9 @@ __global__ __launch_bounds__(256) void per_sample_kernel(AsvPer per, int B, cons
       ok = pymod(index - di, C) > static_cast<int64_t>(n) * S && pymod(di - index, C) >= S && prob != 0.f;
   }
   if (!ok) atomicAdd(reinterpret_cast<unsigned long long*>(per.state + 3), 1ull);   // reported, row still valid data
-  out_idx[b] = node;
+  // an unvalidated draw's leaf is marked -1: update_priorities skips it (the reference never updates a
+  // draw it did not accept; a priority written there could make an empty slot sampleable)
+  out_idx[b] = ok ? node : -1;
   // n-step window: blank from the first later transition whose timestep is 0 (:146-150)
   float rew[8];
   bool blank = false;
@@ -249,9 +251,14 @@ __global__ __launch_bounds__(256) void per_update_kernel(AsvPer per, const int64
     const float x = values[i];
     v = raw ? x : (per.priority_exponent == 0.5f ? __fsqrt_rn(x) : powf(x, per.priority_exponent));
     const int64_t ti = tree_idx[i];
-    const bool last = i == B - 1 || tree_idx[i + 1] != ti;
-    if (i < B - 1 && tree_idx[i + 1] < ti) atomicAdd(reinterpret_cast<unsigned long long*>(per.state + 3), 1ull);
-    if (last) {
+    // the next VALID draw's leaf (-1 marks an unvalidated draw, asvrl_per_sample): duplicates are
+    // adjacent among the valid ones
+    int64_t nx = -1;
+    for (int j = i + 1; j < B && nx < 0; ++j) nx = tree_idx[j];
+    const bool last = nx != ti;
+    if (ti >= 0 && nx >= 0 && nx < ti) atomicAdd(reinterpret_cast<unsigned long long*>(per.state + 3), 1ull);
+    if (ti < 0) v = 0.f;   // skipped: no write, no part in the running max
+    if (ti >= 0 && last) {
       per.tree[ti] = v;
       per.dirty[(ti - (per.tree_leaves - 1)) / kLeafBlock] = 1;
     }

@@ -42,6 +42,24 @@ class DeviceEnvBatch:
         self.info = torch.zeros(NT, dtype=torch.uint8, device=dev)
         self.env_done = torch.zeros(E, dtype=torch.uint8, device=dev)
         self.stats = torch.zeros(8, **f64)
+        # optional per-robot AsvParams table (AsvEnvState.robot_params; set_robot_params)
+        self.robot_params = None
+
+    def set_robot_params(self, table):
+        """Every robot slot's own vehicle / perception parameters: a sequence of n_envs * max_robots
+        AsvParams (reset_with_eval_config, env.py:553-607), or None for `params` everywhere. The
+        table's env-level members are ignored (the kernel takes those from `params`)."""
+        if table is None:
+            self.robot_params = None
+            return
+        NT = self.n_envs * self.max_robots
+        if len(table) != NT:
+            raise ValueError(f"robot parameter table: {len(table)} entries for {NT} robot slots")
+        arr = (_abi.AsvParams * NT)(*table)
+        host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+        if self.robot_params is None or self.robot_params.numel() != host.numel():
+            self.robot_params = torch.empty(host.numel(), dtype=torch.uint8, device=self.device)
+        self.robot_params.copy_(host)
 
     # ------------------------------------------------------------------ ABI structs
     def state_struct(self):
@@ -55,6 +73,7 @@ class DeviceEnvBatch:
         s.ep_ts = self.ep_ts.data_ptr()
         s.obstacles = self.obstacles.data_ptr()
         s.cores = self.cores.data_ptr()
+        s.robot_params = self.robot_params.data_ptr() if self.robot_params is not None else None
         return s
 
     def out_struct(self, obs=None, obj_cnt=None, with_env_done=True):

@@ -255,21 +255,22 @@ class MarineNavEnv3:
 
     # ------------------------------------------------------------------ device step
     def _params(self):
-        sig = self.robots[0].physics_signature() if self.robots else None
-        for rob in self.robots[1:]:
-            if rob.physics_signature() != sig:
-                raise NotImplementedError("robots with different physical/perception parameters in one env: "
-                                          "the env-step kernel takes one parameter set per batch")
+        """The launch's AsvParams: the first robot's vehicle / perception values and this env's rewards
+        (robots with other values get a per-robot table, set_batch_params)."""
         return _abi.params_from(self.robots[0] if self.robots else None, self)
+
+    def env_key(self):
+        """The env-level launch parameters (rewards, episode limit, core radius): envs that share them can
+        share one launch, whatever their robots' own parameters."""
+        return (self.timestep_penalty, self.COLREGs_penalty, self.collision_penalty, self.goal_reward, self.r)
 
     def _ensure_batch(self, R, O, Cc):
         shape = (R, O, Cc)
         if self._batch is None or any(a > b for a, b in zip(shape, self._shape)):
             R2, O2, C2 = (max(a, b) for a, b in zip(shape, self._shape))
-            self._batch = DeviceEnvBatch(1, max(R2, 1), max(O2, 1), min(max(C2, 1), 16), device=self._device,
+            self._batch = DeviceEnvBatch(1, max(R2, 1), max(O2, 1), max(C2, 1), device=self._device,
                                          obs64=True)
             self._shape = (self._batch.max_robots, self._batch.max_obs, self._batch.max_cores)
-        self._batch.params = self._params()
         return self._batch
 
     def _pack(self, actions, is_continuous_action, R, O, Cm):
@@ -278,8 +279,7 @@ class MarineNavEnv3:
         from each active robot's RandomState in the reference's order (wamv.py:465-510): obstacles,
         then the other active robots, five draws per candidate."""
         n = len(self.robots)
-        if len(self.cores) > Cm:
-            raise NotImplementedError("more than 16 vortex cores")
+        assert len(self.cores) <= Cm, "the batch was sized for fewer cores"
         rs = np.zeros((_abi.NUM_FIELDS, R))
         fl = np.zeros(R, np.uint8)
         for i, rob in enumerate(self.robots):
@@ -502,12 +502,34 @@ class MarineNavEnv3:
             json.dump(self.episode_data(), f)
 
 
+def set_batch_params(batch, envs):
+    """The launch parameters of `envs` on `batch` (env e in slots [e*R, (e+1)*R)): one AsvParams when
+    every robot shares its vehicle / perception values, else a per-robot table as well
+    (reset_with_eval_config gives each robot its own dt, N, m, Izz, hydrodynamic coefficients, thrust
+    limits, radius, goal distance and perception sigma / kappa, env.py:553-607). The envs share their
+    env-level values (env_key)."""
+    assert len({env.env_key() for env in envs}) <= 1, "one launch takes one set of env-level parameters"
+    batch.params = envs[0]._params() if envs else _abi.params_from()
+    sigs = {rob.physics_signature() for env in envs for rob in env.robots}
+    if len(sigs) <= 1:
+        batch.set_robot_params(None)
+        return
+    R = batch.max_robots
+    table = [batch.params] * (batch.n_envs * R)
+    for e, env in enumerate(envs):
+        for i, rob in enumerate(env.robots):
+            table[e * R + i] = _abi.params_from(rob, env)
+    batch.set_robot_params(table)
+
+
 def run_env_step(batch, envs, actions_list, is_continuous_action, do_dynamics):
-    """One asvrl_env_step launch over several MarineNavEnv3 instances with identical parameter
-    sets: env e occupies slots [e*R, (e+1)*R) of `batch` (a DeviceEnvBatch with n_envs >= len(envs)
-    and room for every env's robots, obstacles and cores). Each env's noise comes from its own
+    """One asvrl_env_step launch over several MarineNavEnv3 instances that share their env-level
+    parameters: env e occupies slots [e*R, (e+1)*R) of `batch` (a DeviceEnvBatch with n_envs >= len(envs)
+    and room for every env's robots, obstacles and cores); robots with their own vehicle / perception
+    parameters go through the per-robot table (set_batch_params). Each env's noise comes from its own
     robots' RandomStates, so the results equal stepping the envs one at a time. Returns the
     per-env output slices (host arrays) after writing them back into the robots."""
+    set_batch_params(batch, envs)
     E, R, O, Cm = len(envs), batch.max_robots, batch.max_obs, batch.max_cores
     packs = [env._pack(a, is_continuous_action, R, O, Cm) for env, a in zip(envs, actions_list)]
     dev = batch.device

@@ -468,81 +468,3 @@ def trunk_weight_grads(critic, bufs):
     linear_wgrad(bufs.dz1, bufs.h0, critic.hidden_layer.weight.grad, critic.hidden_layer.bias.grad, bufs.work)
     linear_wgrad(bufs.dz2, bufs.h1g, critic.hidden_layer_2.weight.grad, critic.hidden_layer_2.bias.grad, bufs.work)
     linear_wgrad_vec(bufs.dq, bufs.h2, critic.output_layer.weight.grad, critic.output_layer.bias.grad, bufs.work)
-
-
-def fused_supported(critic, B, N):
-    return (critic.concat_feature_dimension == 256 and critic.hidden_dimension == 128 and critic.n == 64
-            and N in (8, 16, 32) and (B * N) % 32 == 0)
-
-
-class FusedACIQN:
-    """State for ac_iqn_update_fused: weight packs and activation buffers (allocated once)."""
-
-    def __init__(self, policy_local, policy_target, B, N):
-        self.local_pack = CriticPack(policy_local.critic)
-        self.target_pack = CriticPack(policy_target.critic)
-        self.bufs = TrainBuffers(B, N, policy_local.critic.cos_embedding.weight.device)
-        dev = self.bufs.q.device
-        self.q_next = torch.empty(B * N, dtype=torch.float32, device=dev)
-        self.q_pi = torch.empty(B * N, dtype=torch.float32, device=dev)
-        self.dG_pi = torch.empty(B, 128, dtype=torch.float32, device=dev)
-        self.B, self.N = B, N
-        self.target_dirty = False  # the pack was just built
-
-    def target_changed(self):
-        """Call after the target critic's weights change (hard/soft update): re-packed lazily."""
-        self.target_dirty = True
-
-
-def ac_iqn_update_fused(fz, policy_local, policy_target, actor_opt, critic_opt, critic_grads, actor_grads, states,
-                        actions, rewards, next_states, dones, gamma=0.99, taus=(None, None, None), sync=None,
-                        amp_dtype=torch.bfloat16, max_norm=0.5):
-    actor, critic = policy_local.actor, policy_local.critic
-    tcritic = policy_target.critic
-    B, N = fz.B, fz.N
-    dev = fz.bufs.q.device
-    # the actor and the encoders stay fp32 here: their GEMMs are small and autocast would
-    # re-cast every weight to bf16 on every call (54 cast kernels per step); only the critic
-    # trunk, which holds the FLOPs, runs bf16 (in the fused kernels)
-
-    def draw(t):
-        return torch.rand(B, N, device=dev) if t is None else t.reshape(B, N).float().contiguous()
-
-    # ---- critic (agent.py:395-416)
-    critic_grads.zero_()
-    with torch.no_grad():
-        na = policy_target.actor(next_states)
-        Ft = encode_observation(tcritic.self_encoder, tcritic.object_encoder, next_states, tcritic.max_object_num,
-                                tcritic.object_dimension, tcritic.object_feature_dimension).float().contiguous()
-        Gt = tcritic.action_encoder(na.float()).contiguous()
-        if fz.target_dirty:
-            fz.target_pack.refresh()
-            fz.target_dirty = False
-        q_next = critic_forward(fz.target_pack, Ft, Gt, draw(taus[0]), N, q=fz.q_next)
-        q_targets = (rewards + gamma * q_next * (1.0 - dones)).contiguous()
-    F = encode_observation(critic.self_encoder, critic.object_encoder, states, critic.max_object_num,
-                           critic.object_dimension, critic.object_feature_dimension)
-    G = critic.action_encoder(actions)
-    fz.local_pack.refresh()
-    critic_loss = critic_train(fz.local_pack, F.detach().float().contiguous(), G.detach().float().contiguous(),
-                               draw(taus[1]), q_targets, fz.bufs)
-    trunk_weight_grads(critic, fz.bufs)
-    torch.autograd.backward([F, G], [fz.bufs.dF, fz.bufs.dG])
-    if sync is not None:
-        sync(critic_grads)
-    cgn = clip_and_step(critic_opt, critic_grads, max_norm)
-    # ---- actor through the updated critic (agent.py:419-427)
-    fz.local_pack.refresh()
-    a_out = actor(states)
-    with torch.no_grad():
-        F2 = encode_observation(critic.self_encoder, critic.object_encoder, states, critic.max_object_num,
-                                critic.object_dimension, critic.object_feature_dimension).float().contiguous()
-    G2 = critic.action_encoder(a_out.float())
-    critic_actor_grad(fz.local_pack, F2, G2.detach().float().contiguous(), draw(taus[2]), N, fz.q_pi, fz.dG_pi)
-    actor_loss = -fz.q_pi.mean()
-    g = torch.autograd.grad(G2, actor_grads.params, grad_outputs=fz.dG_pi)
-    actor_grads.assign(g)
-    if sync is not None:
-        sync(actor_grads)
-    agn = clip_and_step(actor_opt, actor_grads, max_norm)
-    return critic_loss.detach(), actor_loss.detach(), cgn, agn

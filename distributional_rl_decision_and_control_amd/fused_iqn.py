@@ -17,7 +17,7 @@ replay batch `rows` ([B][88]: obs | next obs | action | reward | done):
                                                           loss and the gradient norm
     clip + Adam                                           asvrl_adam_step          (agent.py:471-472)
       (with DP: asvrl_partial_sums, RCCL all-reduce, asvrl_adam_clip)
-    (ASVRL_FUSED_TRAIN=0: asvrl_iqn_train's two launches + the batched weight-gradient launch over the
+    (B*N not a multiple of the 64-row round: asvrl_iqn_train's two launches + the weight-gradient launch over the
     saved activations, the round-1 path)
     re-pack trunk and head                                asvrl_iqn_pack
 
@@ -33,10 +33,16 @@ import torch
 
 from . import _abi
 from .fused_critic import CriticPack, PartialArena, TrainBuffers, fused_groups, fused_train_supported
-from .fused_update import ENC_IN_KERNEL, FUSED_TRAIN, SideStreams, _reduce_and_step
+from .fused_update import ENC_IN_KERNEL, _reduce_and_step
 
 OBS = 40
 K_ACT = 32
+
+
+# the IQN step's forward / loss / backward and weight gradients in ONE launch (asvrl_iqn_train_fused)
+# wherever it takes the shape (B*N a multiple of its 64-row round); otherwise asvrl_iqn_train's two
+# launches + the batched weight-gradient launch over saved activations (tests toggle it)
+FUSED_TRAIN = True
 
 
 def supported(net, B, N):
@@ -182,7 +188,6 @@ class FusedIQNState:
         self.arena = PartialArena(32 << 20, dev, operands)
         self.loss = torch.zeros(1, **f)
         self.tile_loss = torch.zeros(B * N // 32, **f)
-        self.side = SideStreams(dev, 2)
 
     def target_changed(self):
         """Re-pack the target network after a hard/soft update (eager, outside graphs)."""
@@ -200,7 +205,7 @@ def iqn_grads(st, net, rows, taus, gamma=0.99, flush=True):
     B, N = st.B, st.N
     s_rows, ns_rows = rows[:, 0:OBS], rows[:, OBS:2 * OBS]
     a_col, r_col, d_col = rows[:, 80], rows[:, 82], rows[:, 83]
-    bufs, arena, side = st.bufs, st.arena, st.side
+    bufs, arena = st.bufs, st.arena
     # every .grad is overwritten below (no zeroing); the trunk kernels run the encoders on the rows
     iqn_forward_max(st.target, None, taus[0], N, st.q_next, obs=ns_rows)
     if FUSED_TRAIN and fused_train_supported(st.local, B, N):

@@ -39,6 +39,15 @@ NOISY = ("hidden_layer_v", "hidden_layer_v_2", "output_layer_v", "hidden_layer_a
 ATOMS, ACTIONS = 51, 25
 
 
+def supported(net, B):
+    """The Rainbow kernels' network shape (Rainbow_Policy defaults: 256 concatenated features, 128 hidden,
+    25 actions x 51 atoms, encoders 7 -> 56 and 5 x (5 -> 40)) and a batch of whole 32-row tiles."""
+    return (net.concat_feature_dimension == 256 and net.hidden_dimension == 128 and net.action_size == ACTIONS
+            and net.atoms == ATOMS and net.self_dimension == 7 and net.object_dimension == 5
+            and net.max_object_num == 5 and net.self_feature_dimension == 56 and net.object_feature_dimension == 40
+            and B > 0 and B % 32 == 0)
+
+
 class NoisyPack:
     """Composed NoisyLinear weights of one Rainbow_Policy in one flat buffer (views W[name], b[name]).
     Build it after anything that re-points the parameters (FusedAdam)."""
@@ -217,9 +226,11 @@ class FusedRainbow:
         self.img.run("asvrl_rainbow_net_act", io)
 
     def update(self, opt, grads, rows, gamma=0.99, n=3, vmin=-1.0, vmax=1.0, sync=None, max_norm=0.5, seed=0,
-               counter_dev=None, compose=True):
+               counter_dev=None, compose=True, reset_target=True):
         """train_Rainbow on PER rows; returns (per-sample loss, pre-clip grad norm). compose=False reuses
-        the online weights composed by act() this iteration."""
+        the online weights composed by act() this iteration. reset_target=False keeps the target's noise
+        buffers as they are (composed from them) instead of reset_noise() from Philox: the parity tests
+        inject the noise the reference drew."""
         from .learner import clip_and_step
         B = rows.shape[0]
         if compose:
@@ -229,7 +240,10 @@ class FusedRainbow:
         # double-Q argmax over s_{t+n} with the online net, then p(s_{t+n}, a*) of the target net with
         # fresh target noise (agent.py:605-612)
         self.img.run("asvrl_rainbow_net_argmax", self.img.io(ns_rows, self.support, act_idx=self.a_star.data_ptr()))
-        self.tpack.reset(seed, counter_dev)
+        if reset_target:
+            self.tpack.reset(seed, counter_dev)
+        else:
+            self.tpack.compose()
         self.timg.refresh()
         self.timg.run("asvrl_rainbow_net_pick", self.timg.io(ns_rows, self.support, act_idx=self.a_star.data_ptr(),
                                                                p_out=self.p_star.data_ptr()))

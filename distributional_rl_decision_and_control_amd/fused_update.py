@@ -8,7 +8,7 @@ Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | 
     target encoders(ns, na) + trunk -> q_next            asvrl_critic_forward (encoders in the prologue)
     local encoders(s, a), trunk forward, quantile-Huber vs r + g q_next (1-d), backward AND the
     four trunk layers' weight-gradient partials          asvrl_critic_train_fused (ONE launch)
-    and the observation / action encoders' gradient partials (ABI 16; ASVRL_ENC_IN_KERNEL=0: from
+    and the observation / action encoders' gradient partials (ABI 16; ENC_IN_KERNEL = False: from
     dzF / dzG by ONE asvrl_linear_wgrad_multi, fold + small)
     every .grad (encoders folded in the reduction), the loss and the global gradient norm
                                                           ONE asvrl_partial_sums_norm
@@ -20,59 +20,27 @@ Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | 
     actor backward                                       asvrl_actor_backward
     actor weight grads                                   ONE asvrl_linear_wgrad_multi, one asvrl_partial_sums_norm
     clip + Adam + re-pack                                asvrl_adam_step_pack
-(ASVRL_FUSED_TRAIN=0, or B*N not a multiple of the fused launch's round: the critic step as the two
-TRAIN kernels asvrl_critic_train + the batched weight-gradient launch over saved activations.)
+(supported() admits only shapes the fused critic launch takes: B a multiple of 32, so B*N one of its
+64-row round.)
 
-The learner runs on the caller's stream; a replayed graph pays ~10 us per cross-stream join, so the
-side streams (SideStreams) are used only where an overlap pays.
+The learner runs on the caller's stream (a replayed graph pays ~10 us per cross-stream join; the only
+other stream is the rollout's, vec_trainer.py).
 
 Arithmetic: bf16 MFMA operands with f32 accumulation everywhere, f32 master weights / Adam
 (operands="f32": the same kernels from libasvrl_f32.so, the parity build).
 """
-import contextlib
-import os
-
 import torch
 
-from . import _abi, streams
-from .fused_critic import (CriticPack, PartialArena, TrainBuffers, critic_actor_grad, critic_forward, critic_train,
-                           critic_train_fused, fused_train_supported, trunk_weight_grads_into, wout_groups)
+from . import _abi
+from .fused_critic import CriticPack, PartialArena, critic_actor_grad, critic_forward, critic_train_fused
 from .fused_mlp import ActorBuffers, MlpPack, actor_act, actor_backward, actor_forward, actor_train_forward
 from .learner import FusedAdam, clip_and_step
 
 OBS = 40
-# the actor's training forward on a side stream beside the target chain (1) or on the caller's stream
-# (0, default): the fork + join cost more than the 13 us forward in a replayed graph (-1 % per step)
-ACTOR_FWD_SIDE = os.environ.get("ASVRL_ACTOR_FWD_SIDE", "0") == "1"
-# the critic step's forward / loss / backward and trunk weight gradients in ONE launch
-# (asvrl_critic_train_fused; 1, default) or the two TRAIN kernels + the batched weight-gradient launch
-# over saved activations (0; also the path for shapes the fused launch does not take)
-FUSED_TRAIN = os.environ.get("ASVRL_FUSED_TRAIN", "1") == "1"
-# the encoders' gradients formed inside the fused critic launch (1, default; ABI 16: 0.333 -> 0.323 ms per
-# AC-IQN step, profiles/r02_enc_ab.txt) or by a batched launch over its per-sample dzF / dzG (0)
-ENC_IN_KERNEL = os.environ.get("ASVRL_ENC_IN_KERNEL", "1") == "1"
-
-
-class SideStreams:
-    """Fork/join of independent launches onto `n` side streams of one device (dedicated streams,
-    streams.py: never an alias of the capture or rollout stream)."""
-
-    def __init__(self, device, n=2):
-        self.streams = [streams.stream(device, ("side", i)) for i in range(n)]
-
-    @contextlib.contextmanager
-    def on(self, i):
-        """Run the block on side stream i, after everything queued so far on the current stream."""
-        cur = torch.cuda.current_stream()
-        s = self.streams[i]
-        s.wait_stream(cur)
-        with torch.cuda.stream(s):
-            yield
-
-    def join(self, *idx):
-        cur = torch.cuda.current_stream()
-        for i in (idx or range(len(self.streams))):
-            cur.wait_stream(self.streams[i])
+# the encoders' gradients formed inside the fused critic launch (ABI 16: 0.333 -> 0.323 ms per AC-IQN
+# step, profiles/r02_enc_ab.txt); False keeps the earlier form (per-sample dzF / dzG + a batched launch)
+# for the kernel tests that compare the two
+ENC_IN_KERNEL = True
 
 
 def supported(policy, B, N):
@@ -98,22 +66,18 @@ class FusedACIQNState:
         self.target_trunk = CriticPack(policy_target.critic, operands)
         self.actor = MlpPack(policy_local.actor, "actor", operands)
         self.target_actor = MlpPack(policy_target.actor, "actor", operands)
-        self.bufs = TrainBuffers(B, N, dev, operands)
         self.abufs = ActorBuffers(B, dev, operands)
         f = dict(dtype=torch.float32, device=dev)
         bf = dict(dtype=_abi.operand_dtype(operands), device=dev)
         self.na = torch.empty(B, 2, **f)
-        self.na_p = torch.empty(B, 2, **f)       # the pipelined target chain's actions
         self.xb = torch.empty(B, 32, **bf)
         self.q_next = torch.empty(B * N, **f)
-        self.q_next_buf = [self.q_next, torch.empty(B * N, **f)]   # pipelined: per batch parity
         self.q_pi = torch.empty(B * N, **f)
         self.dzF = torch.empty(B, 256, **bf)
         self.dzG = torch.empty(B, 128, **f)
         self.arena = PartialArena(32 << 20, dev, operands)
         self.losses = torch.zeros(2, **f)   # critic, actor loss (summed from per-tile partials)
         self.tile_loss = torch.zeros(2, B * N // 32, **f)
-        self.side = SideStreams(dev, 3)   # 0, 1: gradient reductions / actor forward; 2: next batch
 
     def target_changed(self):
         """Re-pack the target networks after a hard/soft update (eager, outside graphs)."""
@@ -165,70 +129,41 @@ def target_q(st, rows, tau0, q_out, na):
 
 
 def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, actor_grads, rows, gamma=0.99,
-                         taus=None, sync=None, max_norm=0.5, actor_wait=None, q_next=None, produce=None,
-                         counter=None):
+                         taus=None, sync=None, max_norm=0.5, actor_wait=None, counter=None):
     """One AC-IQN update from replay rows [B][88]. taus: (3, B, N) or None (drawn here).
     actor_wait: event to wait for before the actor's weights change (a concurrent act kernel).
     counter: an int64 device scalar incremented after the step (the learn counter; in-kernel when
-    the optimiser step is fused). q_next: the rows' target quantiles already computed (the pipelined loop); produce: a callable
-    that samples the NEXT batch and computes its q_next, run on a side stream beside the actor
-    step (after the critic step, so the target chain overlaps the actor's kernels).
+    the optimiser step is fused).
     Returns (critic_loss, actor_loss, critic_grad_norm, actor_grad_norm) as device scalars."""
     B, N = st.B, st.N
     critic, actor = policy_local.critic, policy_local.actor
     if taus is None:
         taus = torch.rand(3, B, N, device=st.device)
-    s_rows, ns_rows = rows[:, 0:OBS], rows[:, OBS:2 * OBS]
+    s_rows = rows[:, 0:OBS]
     a_rows, r_col, d_col = rows[:, 80:82], rows[:, 82], rows[:, 83]
-    bufs, ab, arena = st.bufs, st.abufs, st.arena
+    ab, arena = st.abufs, st.arena
 
-    side = st.side
     # ---- critic (agent.py:395-416); every critic .grad is overwritten below (no zeroing). The
     # trunk kernels run the critic's observation / action encoders on the replay rows themselves.
-    if ACTOR_FWD_SIDE:   # the actor's training forward reads only s and the (not yet updated) actor
-        with side.on(1):
-            actor_train_forward(st.actor, s_rows, ab)
-    else:
-        actor_train_forward(st.actor, s_rows, ab)
-    if q_next is None:
-        q_next = st.q_next
-        target_q(st, rows, taus[0], q_next, st.na)
+    actor_train_forward(st.actor, s_rows, ab)   # reads only s and the (not yet updated) actor
+    q_next = st.q_next
+    target_q(st, rows, taus[0], q_next, st.na)
     ae = critic.action_encoder[0]
-    if FUSED_TRAIN and fused_train_supported(st.local_trunk, B, N):
-        # forward, loss, backward and the weight-gradient partials of the four trunk layers and the
-        # three encoders in one launch
-        if ENC_IN_KERNEL:
-            critic_train_fused(st.local_trunk, critic, taus[1], N, q_next.view(B, N), r_col, d_col, gamma, s_rows,
-                               a_rows, arena, tile_loss=st.tile_loss[0], encoders=True)
-        else:
-            critic_train_fused(st.local_trunk, critic, taus[1], N, q_next.view(B, N), r_col, d_col, gamma, s_rows,
-                               a_rows, arena, dzF=st.dzF, dzG=st.dzG, xb=st.xb, tile_loss=st.tile_loss[0])
-            with arena.batch():   # the encoders' gradients from the per-sample dzF / dzG
-                arena.fold(st.dzF, st.xb, critic)
-                arena.small(st.dzG, a_rows, ae.weight.grad, ae.bias.grad)
+    # forward, loss, backward and the weight-gradient partials of the four trunk layers and the three
+    # encoders in one launch (supported() guarantees its shape: B a multiple of 32, so B*N of 64)
+    if ENC_IN_KERNEL:
+        critic_train_fused(st.local_trunk, critic, taus[1], N, q_next.view(B, N), r_col, d_col, gamma, s_rows,
+                           a_rows, arena, tile_loss=st.tile_loss[0], encoders=True)
     else:
-        tiles = wout_groups(B, N)
-        wout_part = arena.take_tiles(tiles, 128)   # output_layer's gradient, reduced per workgroup in the kernel
-        critic_train(st.local_trunk, None, None, taus[1], None, bufs, q_next=q_next.view(B, N), rewards=r_col,
-                     dones=d_col, gamma=gamma, dzF=st.dzF, dzG=st.dzG, with_dFdG=False, tile_loss=st.tile_loss[0],
-                     obs=s_rows, act=a_rows, xb=st.xb, wout_part=wout_part)
-        arena.tiles(wout_part, tiles, critic.output_layer.weight.grad, critic.output_layer.bias.grad)
-        # the five weight-gradient reductions in ONE launch, then one partial-sum launch
-        with arena.batch():
-            arena.linear(bufs.dzc, bufs.cos, critic.cos_embedding.weight.grad, critic.cos_embedding.bias.grad)
-            arena.linear(bufs.dz1, bufs.h0, critic.hidden_layer.weight.grad, critic.hidden_layer.bias.grad)
-            arena.linear(bufs.dz2, bufs.h1g, critic.hidden_layer_2.weight.grad, critic.hidden_layer_2.bias.grad)
-            arena.fold(st.dzF, st.xb, critic)             # encoder image -> self/object encoder grads
+        critic_train_fused(st.local_trunk, critic, taus[1], N, q_next.view(B, N), r_col, d_col, gamma, s_rows,
+                           a_rows, arena, dzF=st.dzF, dzG=st.dzG, xb=st.xb, tile_loss=st.tile_loss[0])
+        with arena.batch():   # the encoders' gradients from the per-sample dzF / dzG
+            arena.fold(st.dzF, st.xb, critic)
             arena.small(st.dzG, a_rows, ae.weight.grad, ae.bias.grad)
     arena.scalar(st.tile_loss[0], st.losses[0:1])   # the critic loss
     cgn = _reduce_and_step(arena, critic_opt, critic_grads, sync, max_norm, pack=st.local_trunk)
-    if produce is not None:   # next batch + its target quantiles beside the actor step
-        with side.on(2):
-            produce()
 
-    # ---- actor through the updated critic (agent.py:419-427); its forward ran on side stream 1
-    if ACTOR_FWD_SIDE:
-        side.join(1)
+    # ---- actor through the updated critic (agent.py:419-427)
     critic_actor_grad(st.local_trunk, None, None, taus[2], N, st.q_pi, w_ae=ae.weight, dA=ab.dA,
                       tile_loss=st.tile_loss[1], obs=s_rows, act=ab.a_out)
     actor_backward(st.actor, ab)
@@ -242,6 +177,4 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     arena.scalar(st.tile_loss[1], st.losses[1:2])   # the actor loss
     agn = _reduce_and_step(arena, actor_opt, actor_grads, sync, max_norm, wait=actor_wait, pack=st.actor,
                            counter=counter)
-    if produce is not None:
-        side.join(2)
     return st.losses[0], st.losses[1], cgn, agn

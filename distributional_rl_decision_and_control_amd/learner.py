@@ -240,39 +240,6 @@ def rainbow_update(policy_local, policy_target, opt, grads, support, states, act
     return loss.detach(), gn
 
 
-def rainbow_update_rows(policy_local, policy_target, opt, grads, support, rows, gamma=0.99, n=3, vmin=-1.0,
-                        vmax=1.0, sync=None, max_norm=0.5):
-    """train_Rainbow (agent.py:597-641) on packed replay rows (DevicePER.sample: obs 0:40 | n-th next
-    obs 40:80 | action 80 | R 82 | nonterminal 83 | normalised weight 84). The online net sees s and
-    s_{t+n} in ONE forward over 2B interleaved rows (its noise is fixed between resets, so this is the
-    same function as the reference's two calls); p(s_{t+n}) for the double-Q argmax is exp of that
-    log-softmax. Returns the per-sample loss and the pre-clip gradient norm."""
-    B = rows.shape[0]
-    both = rows[:, :2 * OBS_DIM].reshape(2 * B, OBS_DIM)        # s_0, s'_0, s_1, s'_1, ...
-    log_p = policy_local(_split_obs(both), log=True)
-    actions = rows[:, 80].to(torch.int64)
-    ar = torch.arange(B, device=rows.device)
-    log_ps_a = log_p[0::2][ar, actions]
-    with torch.no_grad():
-        pns = log_p[1::2].detach().float().exp()
-        argmax_ns = (support.expand_as(pns) * pns).sum(2).argmax(1)
-        policy_target.reset_noise()
-        pns_t = policy_target(_split_obs(rows[:, OBS_DIM:2 * OBS_DIM]))
-        m = c51_project(pns_t[ar, argmax_ns], rows[:, 82], rows[:, 83], support, vmin, vmax, gamma ** n)
-    loss = -torch.sum(m * log_ps_a.float(), 1)
-    grads.zero_()
-    (rows[:, 84] * loss).mean().backward()
-    if sync is not None:
-        sync(grads)
-    gn = clip_and_step(opt, grads, max_norm)
-    return loss.detach(), gn
-
-
-def _split_obs(obs_rows):
-    M = obs_rows.shape[0]
-    return obs_rows[:, 0:7], obs_rows[:, 7:32].reshape(M, 5, 5), obs_rows[:, 32:37]
-
-
 class _null:
     def __enter__(self):
         return self

@@ -15,8 +15,6 @@ import torch
 import torch.nn as nn
 from torch.nn.functional import relu
 
-from ..splitk_linear import RowLinear
-
 
 def encoder(input_dimension, output_dimension):
     return nn.Sequential(nn.Linear(input_dimension, output_dimension), nn.ReLU())
@@ -155,11 +153,11 @@ class Critic(_Saveable, nn.Module):
         self.object_encoder = encoder(object_dimension, object_feature_dimension)
         self.register_buffer("pis", torch.FloatTensor([np.pi * i for i in range(self.n)]).view(1, 1, self.n),
                              persistent=False)
-        self.cos_embedding = RowLinear(self.n, self.concat_feature_dimension)
+        self.cos_embedding = nn.Linear(self.n, self.concat_feature_dimension)
         self.action_encoder = encoder(self.action_dimension, hidden_dimension)
-        self.hidden_layer = RowLinear(self.concat_feature_dimension, hidden_dimension)
-        self.hidden_layer_2 = RowLinear(hidden_dimension, hidden_dimension)
-        self.output_layer = RowLinear(hidden_dimension, 1)
+        self.hidden_layer = nn.Linear(self.concat_feature_dimension, hidden_dimension)
+        self.hidden_layer_2 = nn.Linear(hidden_dimension, hidden_dimension)
+        self.output_layer = nn.Linear(hidden_dimension, 1)
 
     def calc_cos(self, batch_size, num_tau=8, cvar=1.0, taus=None):
         """AC_IQN_model.py:410-426; `taus` (B, N, 1) may be supplied instead of torch.rand."""

@@ -5,7 +5,6 @@ import torch
 import torch.nn as nn
 from torch.nn.functional import relu
 
-from ..splitk_linear import RowLinear
 from .AC_IQN_model import _Saveable, encoder, encode_observation
 
 
@@ -33,10 +32,10 @@ class IQN_Policy(_Saveable, nn.Module):
         self.n = 64
         self.register_buffer("pis", torch.FloatTensor([np.pi * i for i in range(self.n)]).view(1, 1, self.n),
                              persistent=False)
-        self.cos_embedding = RowLinear(self.n, self.concat_feature_dimension)
-        self.hidden_layer = RowLinear(self.concat_feature_dimension, hidden_dimension)
-        self.hidden_layer_2 = RowLinear(hidden_dimension, hidden_dimension)
-        self.output_layer = RowLinear(hidden_dimension, action_size)
+        self.cos_embedding = nn.Linear(self.n, self.concat_feature_dimension)
+        self.hidden_layer = nn.Linear(self.concat_feature_dimension, hidden_dimension)
+        self.hidden_layer_2 = nn.Linear(hidden_dimension, hidden_dimension)
+        self.output_layer = nn.Linear(hidden_dimension, action_size)
 
     def calc_cos(self, batch_size, num_tau=8, cvar=1.0, taus=None):  # IQN_model.py:56-72
         if taus is None:

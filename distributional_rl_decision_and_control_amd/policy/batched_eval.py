@@ -31,8 +31,9 @@ from ..envs.marinenav.env import MarineNavEnv3, run_env_step
 
 
 def _params_key(env):
-    """Bytes of the AsvParams one launch would use for this env (envs sharing it can share a launch)."""
-    return bytes(env._params())
+    """The env-level launch parameters (envs sharing them share a launch; robots with their own vehicle /
+    perception parameters go through the per-robot table, envs.marinenav.env.set_batch_params)."""
+    return env.env_key()
 
 
 @torch.no_grad()
@@ -113,11 +114,7 @@ def evaluate_configs(agent, configs, device=None, template_env=None):
         R = max(len(envs[e].robots) for e in members)
         O = max(len(envs[e].obstacles) for e in members)
         Cm = max(len(envs[e].cores) for e in members)
-        if Cm > 16:
-            raise NotImplementedError("more than 16 vortex cores")
-        b = DeviceEnvBatch(len(members), max(R, 1), max(O, 1), max(min(Cm, 16), 1), device=dev, obs64=True)
-        b.params = envs[members[0]]._params()
-        batches[key] = b
+        batches[key] = DeviceEnvBatch(len(members), max(R, 1), max(O, 1), max(Cm, 1), device=dev, obs64=True)
     while running:
         # one policy call for every active robot of every running episode (trainer.py:300-322)
         rows = [(e, i) for e in running for i, rob in enumerate(envs[e].robots) if not rob.deactivated]

@@ -157,10 +157,19 @@ class Trainer:
         for key, sk in (("num_robots", "num_robots"), ("num_obs", "num_obstacles"), ("num_cores", "num_cores")):
             if sk in sched:
                 kw.setdefault(key, max(sched[sk]))
+        # the Trainer's cadence in the batched loop's units: learning starts once the replay holds
+        # learning_starts transitions (and at least one batch); the hard target update every
+        # target_update_interval env-steps = every target_update_interval / UPDATE_EVERY learn steps
+        # (trainer.py:175-192: one B=64 learn step per UPDATE_EVERY timesteps)
+        kw.setdefault("learning_starts", max(int(kw.get("batch_size", 4096)), int(self.learning_starts)))
+        kw.setdefault("target_update_interval", max(1, int(self.target_update_interval) // int(self.UPDATE_EVERY)))
         tr = VecTrainer(agent_type=agent.agent_type, seed=getattr(self.train_env, "seed", 0), device=agent.device,
                         total_timesteps=total_timesteps, schedule=sched, gamma=agent.GAMMA, lr=agent.LR,
                         exploration_fraction=self.exploration_fraction, initial_eps=self.initial_eps,
                         final_eps=self.final_eps, **kw)
+        # start from rl_agent's networks (its seeded init, or what load_model put there), not the
+        # batched trainer's own initialisation
+        tr.load_policies(agent.policy_local, agent.policy_target)
         self.vec_trainer = tr
         next_eval = None
         while self.current_timestep < total_timesteps:   # iteration k covers env-steps [kE, (k + 1)E)

@@ -16,24 +16,22 @@ Cadence in the batched setting: one learn step of batch B per iteration (after
 timesteps; target updates count learn steps (2500 = 10000 timesteps / UPDATE_EVERY 4).
 With `graphs=True` steps 1-5 are captured once into a HIP graph and replayed.
 """
-import os
 import time
 
 import torch
 
 from . import streams
-from .fused_critic import FusedACIQN, ac_iqn_update_fused, fused_supported
 from .fused_update import FusedACIQNState, ac_iqn_update_fused2
 from .fused_iqn import FusedIQNState, iqn_update_fused
 from .fused_iqn import supported as fused_iqn_supported
 from .fused_rainbow import FusedRainbow
 from .fused_update import supported as fused2_supported
-from .learn_ops import DevicePER, DeviceReplay, split_rows
-from .learner import FlatGrads, FusedAdam, GradSync, ac_iqn_update, iqn_update, rainbow_update, rainbow_update_rows
+from .learn_ops import DevicePER, DeviceReplay
+from .learner import FusedAdam
 from .policy.AC_IQN_model import AC_IQN_Policy
 from .policy.IQN_model import IQN_Policy
 from .policy.Rainbow_model import Rainbow_Policy
-from .vec_env import VecMarineNavEnv, split_obs
+from .vec_env import VecMarineNavEnv
 
 DEFAULT_NET = dict(self_dimension=7, object_dimension=5, max_object_num=5, self_feature_dimension=56,
                    object_feature_dimension=40, concat_feature_dimension=256, hidden_dimension=128)
@@ -43,9 +41,12 @@ class VecTrainer:
     def __init__(self, n_envs=4096, agent_type="AC-IQN", num_robots=5, num_obs=4, num_cores=0, min_start_goal_dis=40.0,
                  width=55.0, batch_size=4096, num_tau=32, buffer_size=4_000_000, lr=1e-4, gamma=0.99,
                  learning_starts=None, target_update_interval=2500, total_timesteps=6_000_000,
-                 exploration_fraction=0.25, initial_eps=0.6, final_eps=0.05, amp_dtype=torch.bfloat16, seed=0,
-                 device="cuda", sync=None, graphs=False, schedule=None, net_seed=100, fused=True,
-                 fused_adam=True, overlap=True, unroll=1, pipeline=False, chain=None):
+                 exploration_fraction=0.25, initial_eps=0.6, final_eps=0.05, seed=0,
+                 device="cuda", sync=None, graphs=False, schedule=None, net_seed=100, overlap=True, unroll=1,
+                 chain=None, operands="bf16"):
+        """Every learner runs on the hand-written kernels (fused_update / fused_iqn / fused_rainbow) with
+        FusedAdam; operands="f32" takes them from the f32-operand parity build (libasvrl_f32.so). Shapes
+        the kernels do not take raise ValueError."""
         self.device = torch.device(device)
         self.agent_type = agent_type
         self.continuous = agent_type == "AC-IQN"
@@ -53,15 +54,14 @@ class VecTrainer:
                                    device=self.device, is_continuous=self.continuous, gamma=gamma, schedule=schedule)
         self.E, self.R = n_envs, self.env.max_robots
         self.B, self.num_tau, self.gamma = batch_size, num_tau, gamma
-        self.amp_dtype = amp_dtype
+        self.operands = operands
         self.sync = sync
         self.seed = seed
         self.target_update_interval = target_update_interval
         self.total_timesteps = total_timesteps
         self.exploration_fraction, self.initial_eps, self.final_eps = exploration_fraction, initial_eps, final_eps
         self.learning_starts = learning_starts if learning_starts is not None else batch_size
-        capturable = bool(graphs)
-        self.fused = self.fused2 = self.fused_iqn = self.fused_rb = None
+        self.fused2 = self.fused_iqn = self.fused_rb = None
         if agent_type == "AC-IQN":
             self.local = AC_IQN_Policy(**DEFAULT_NET, value_ranges_of_action=[[-1.0, 1.0], [-1.0, 1.0]],
                                        device=self.device, seed=net_seed)
@@ -69,40 +69,26 @@ class VecTrainer:
                                         device=self.device, seed=net_seed)
             for p in list(self.target.actor.parameters()) + list(self.target.critic.parameters()):
                 p.requires_grad_(False)
-            if fused_adam:
-                # clip + Adam as two kernels over flat buffers (must precede FusedACIQN's packs)
-                self.actor_opt = FusedAdam(self.local.actor.parameters(), lr=lr)
-                self.critic_opt = FusedAdam(self.local.critic.parameters(), lr=lr)
-                self.actor_grads, self.critic_grads = self.actor_opt.grads, self.critic_opt.grads
-            else:
-                self.critic_grads = FlatGrads(self.local.critic.parameters())
-                self.actor_grads = FlatGrads(self.local.actor.parameters())
-                self.actor_opt = torch.optim.Adam(self.local.actor.parameters(), lr=lr, capturable=capturable)
-                self.critic_opt = torch.optim.Adam(self.local.critic.parameters(), lr=lr, capturable=capturable)
+            if not fused2_supported(self.local, batch_size, num_tau):
+                raise ValueError(f"AC-IQN learner kernels: B={batch_size}, N={num_tau} (B a multiple of 32, "
+                                 f"N in 8, 16, 32)")
+            # clip + Adam over flat buffers (must precede the packs, which cache parameter pointers)
+            self.actor_opt = FusedAdam(self.local.actor.parameters(), lr=lr, operands=operands)
+            self.critic_opt = FusedAdam(self.local.critic.parameters(), lr=lr, operands=operands)
+            self.actor_grads, self.critic_grads = self.actor_opt.grads, self.critic_opt.grads
             self.action_dim = 2
-            # fused=True: the whole update on hand-written kernels (fused_update.py, needs the fused
-            # optimiser); "v1": only the critic trunk fused; False: torch
-            if fused is True and fused_adam and amp_dtype is not None and fused2_supported(self.local, batch_size,
-                                                                                          num_tau):
-                self.fused2 = FusedACIQNState(self.local, self.target, batch_size, num_tau)
-            elif fused and amp_dtype is not None and fused_supported(self.local.critic, batch_size, num_tau):
-                self.fused = FusedACIQN(self.local, self.target, batch_size, num_tau)
+            self.fused2 = FusedACIQNState(self.local, self.target, batch_size, num_tau, operands)
         elif agent_type == "IQN":
             self.local = IQN_Policy(**DEFAULT_NET, action_size=25, device=self.device, seed=net_seed).to(self.device)
             self.target = IQN_Policy(**DEFAULT_NET, action_size=25, device=self.device, seed=net_seed).to(self.device)
             for p in self.target.parameters():
                 p.requires_grad_(False)
-            if fused_adam:
-                self.opt = FusedAdam(self.local.parameters(), lr=lr)
-                self.grads = self.opt.grads
-            else:
-                self.grads = FlatGrads(self.local.parameters())
-                self.opt = torch.optim.Adam(self.local.parameters(), lr=lr, capturable=capturable)
+            if not fused_iqn_supported(self.local, batch_size, num_tau):
+                raise ValueError(f"IQN learner kernels: B={batch_size}, N={num_tau}")
+            self.opt = FusedAdam(self.local.parameters(), lr=lr, operands=operands)
+            self.grads = self.opt.grads
             self.action_dim = 1
-            # fused=True: the whole IQN update and act_iqn on hand-written kernels (fused_iqn.py)
-            if fused is True and fused_adam and amp_dtype is not None and fused_iqn_supported(self.local, batch_size,
-                                                                                            num_tau):
-                self.fused_iqn = FusedIQNState(self.local, self.target, batch_size, num_tau)
+            self.fused_iqn = FusedIQNState(self.local, self.target, batch_size, num_tau, operands)
         elif agent_type == "Rainbow":
             # Rainbow_Policy (dueling NoisyNet C51, 51 atoms on [-1, 1]) with the prioritised n-step
             # replay in HBM, one stream per robot (agent.py:597-641, replay_memory_rainbow.py)
@@ -112,21 +98,13 @@ class VecTrainer:
                                          seed=net_seed).to(self.device)
             for p in self.target.parameters():
                 p.requires_grad_(False)
-            if fused_adam:
-                self.opt = FusedAdam(self.local.parameters(), lr=lr)
-                self.grads = self.opt.grads
-            else:
-                self.grads = FlatGrads(self.local.parameters())
-                self.opt = torch.optim.Adam(self.local.parameters(), lr=lr, capturable=capturable)
+            self.opt = FusedAdam(self.local.parameters(), lr=lr, operands=operands)
+            self.grads = self.opt.grads
             self.action_dim = 1
             self.n_step = 3
             self.support = torch.linspace(-1.0, 1.0, 51, device=self.device)
-            # one online forward over s and s_{t+n} (learner.rainbow_update_rows) or two (rainbow_update)
-            self.rainbow_packed = os.environ.get("ASVRL_RAINBOW_PACKED", "0") == "1"
-            # fused=True: noisy weights, dueling head, loss gradient and act on hand-written kernels
-            # (fused_rainbow.py; fp32 GEMMs); otherwise the torch update with the C51 kernel
-            if fused is True and fused_adam:
-                self.fused_rb = FusedRainbow(self.local, self.target, batch_size, self.support)
+            # noisy weights, the network, loss gradient and act on hand-written kernels (fused_rainbow.py)
+            self.fused_rb = FusedRainbow(self.local, self.target, batch_size, self.support, operands)
         else:
             raise NotImplementedError(f"VecTrainer agent_type {agent_type!r} (AC-IQN, IQN and Rainbow are batched)")
         NT = self.E * self.R
@@ -146,29 +124,15 @@ class VecTrainer:
         self.batch_rows = torch.zeros((self.B, 88), dtype=torch.float32, device=self.device)
         # the fused updates' quantile fractions (AC-IQN: target, local, actor step; IQN: the first two)
         self.taus = torch.zeros((3, self.B, self.num_tau), dtype=torch.float32, device=self.device)
-        # pipelined AC-IQN learner (opt-in): the next batch and its target quantiles are produced
-        # beside the current actor step (fused_update.target_q), so the critic step starts at once.
-        # Two buffer sets alternate by parity; a captured graph then holds two iterations (one per
-        # parity), on the joined schedule. Measured: no gain at the bench shape (0.5595 vs 0.559 ms) --
-        # the GPU is saturated, the overlap only moves the contention. A chained form (the batch sampled
-        # against the snapshot behind the previous push) was bit-identical and 11 % slower
-        # (profiles/r02_pipeline_chain_ab.txt), and its graph segfaulted in hipGraphLaunch late in the
-        # full GPU suite (never alone): reverted.
-        self.pipeline = bool(pipeline) and self.fused2 is not None
-        if self.pipeline:
-            self.rows_buf = [self.batch_rows, torch.zeros_like(self.batch_rows)]
-            self.taus_buf = [self.taus, torch.zeros_like(self.taus)]
-            self._parity = 0
-            self._primed = False
         self.learn_steps = 0
         self.iterations = 0
         self.last_losses = None
         self.graphs = graphs
         self._graph = None
         # iterations per captured graph: one replay enqueues `unroll` whole iterations (the host
-        # calls iteration() once per iteration; every unroll-th call replays). Measured: 2 gives no
-        # gain over 1 (0.564 vs 0.559 ms/step), the in-graph joins keep the same gaps
-        self.unroll = max(1, int(unroll), 2 if self.pipeline and graphs else 1)
+        # calls iteration() once per iteration; every unroll-th call replays): 10 with the chained
+        # schedule at the bench shape (profiles/r02_unroll_chain_ab.txt)
+        self.unroll = max(1, int(unroll))
         self._phase = 0
         self._graph_learn = None
         # rollout / learn on two streams (fused learners): the learner samples against a
@@ -203,52 +167,16 @@ class VecTrainer:
 
     @torch.no_grad()
     def act(self):
-        if self.fused_rb is not None:
-            # composed noisy weights, logits, one head kernel: expected Q, argmax, epsilon-greedy
-            self.fused_rb.act(self.env.obs_cur, self.actions, self.env.counter, self.E, self.total_timesteps,
-                              self.exploration_fraction, self.initial_eps, self.final_eps, self.seed + 4242)
-            return
-        if self.fused_iqn is not None:
-            # encoders + one kernel: K = 32 quantiles per robot, mean, argmax, epsilon-greedy
-            self.fused_iqn.act(self.env.obs_cur, self.actions, self.env.counter, self.E, self.total_timesteps,
-                               self.exploration_fraction, self.initial_eps, self.final_eps, self.seed + 4242)
-            return
-        if self.fused2 is not None:
-            # one kernel: actor on every robot row + epsilon-greedy on the device step counter
-            self.fused2.act(self.env.obs_cur, self.actions, self.env.counter, self.E, self.total_timesteps,
-                            self.exploration_fraction, self.initial_eps, self.final_eps, self.seed + 4242)
-            return
-        obs = split_obs(self.env.obs_cur)
-        NT = obs[0].shape[0]
-        eps = self.epsilon()
-        explore = torch.rand((NT, 1), device=self.device) < eps
-        if self.agent_type == "Rainbow":
-            # act_rainbow (agent.py:308-324) on every robot row, training-mode noisy weights
-            amp = torch.autocast("cuda", dtype=self.amp_dtype) if self.amp_dtype is not None else _null()
-            with amp:
-                p = self.local(obs)
-            greedy = (p.float() * self.support).sum(2).argmax(1)
-            rnd = torch.randint(0, 25, (NT,), device=self.device)
-            self.actions[:, 0].copy_(torch.where(explore.squeeze(1), rnd, greedy))
-            return
-        if self.agent_type == "AC-IQN":
-            # fp32 actor when the critic is fused (see ac_iqn_update_fused)
-            use_amp = self.amp_dtype is not None and self.fused is None
-            amp = torch.autocast("cuda", dtype=self.amp_dtype) if use_amp else _null()
-            with amp:
-                a = self.local.actor(obs).float()
-            rnd = torch.rand((NT, 2), device=self.device) * 2.0 - 1.0
-            self.actions.copy_(torch.where(explore, rnd, a))
-        else:
-            amp = torch.autocast("cuda", dtype=self.amp_dtype) if self.amp_dtype is not None else _null()
-            with amp:
-                q, _ = self.local(obs, self.local.K)
-            greedy = q.float().mean(dim=1).argmax(dim=1)
-            rnd = torch.randint(0, 25, (NT,), device=self.device)
-            self.actions[:, 0].copy_(torch.where(explore.squeeze(1), rnd, greedy))
-
-    def _fused_learner(self):
-        return self.fused2 is not None or self.fused_iqn is not None
+        """The local policy on every robot row with the epsilon-greedy schedule on the device step counter
+        (trainer.py:106-135, agent.py:207-250,308-324), one kernel per agent type."""
+        args = (self.env.obs_cur, self.actions, self.env.counter, self.E, self.total_timesteps,
+                self.exploration_fraction, self.initial_eps, self.final_eps, self.seed + 4242)
+        if self.fused_rb is not None:   # composed noisy weights, logits, head: expected Q, argmax, explore
+            self.fused_rb.act(*args)
+        elif self.fused_iqn is not None:   # K = 32 quantiles per robot, mean, argmax, explore
+            self.fused_iqn.act(*args)
+        else:   # actor on every robot row, explore
+            self.fused2.act(*args)
 
     def _push(self):
         env = self.env
@@ -264,79 +192,29 @@ class VecTrainer:
         self._push()
         self.env.auto_reset()
 
-    def _produce(self, nxt, state, guard, counter):
-        st = self.fused2
-        rows = self.replay.sample(self.B, seed=self.seed + 777, counter=counter, counter_dev=self.learn_counter,
-                                  out=self.rows_buf[nxt], state=state, guard=guard, taus=self.taus_buf[nxt])
-        from .fused_update import target_q
-        target_q(st, rows, self.taus_buf[nxt][0], st.q_next_buf[nxt], st.na_p)
-
-    def _learn_pipelined(self, state, guard, actor_wait):
-        cur = self._parity
-        nxt = 1 - cur
-        if not self._primed:   # the first batch of the run (eager, before any capture)
-            self._produce(cur, state, guard, 0)
-            self._primed = True
-        st = self.fused2
-        out = ac_iqn_update_fused2(st, self.local, self.actor_opt, self.critic_opt, self.critic_grads,
-                                   self.actor_grads, self.rows_buf[cur], gamma=self.gamma, sync=self.sync,
-                                   actor_wait=actor_wait, taus=self.taus_buf[cur], q_next=st.q_next_buf[cur],
-                                   produce=lambda: self._produce(nxt, state, guard, 1))
-        self._parity = nxt
-        self.learn_counter += 1
-        return out
-
     def learn(self, state=None, guard=0, actor_wait=None):
-        if self.pipeline:
-            return self._learn_pipelined(state, guard, actor_wait)
+        """One learn step of batch B: sample (uniform ring, or the prioritised tree for Rainbow) and the
+        agent's fused update. state / guard: the ring snapshot to sample against and the newest entries to
+        skip (the overlapped schedule); actor_wait: an event to wait for before the actor's weights change."""
         if self.per is not None:
             rows, idx = self.per.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter,
                                         out=self.batch_rows, out_idx=self.per_idx)
-            if self.fused_rb is not None:   # act() composed the online weights this iteration
-                loss, gn = self.fused_rb.update(self.opt, self.grads, rows, gamma=self.gamma, n=self.n_step,
-                                                sync=self.sync, seed=self.seed + 999, counter_dev=self.learn_counter,
-                                                compose=False)
-                self.per.update_priorities(idx, loss)
-                self.learn_counter += 1
-                return loss.mean(), gn
-            amp = torch.autocast("cuda", dtype=self.amp_dtype) if self.amp_dtype is not None else _null()
-            with amp:
-                if self.rainbow_packed:
-                    loss, gn = rainbow_update_rows(self.local, self.target, self.opt, self.grads, self.support,
-                                                   rows, gamma=self.gamma, n=self.n_step, sync=self.sync)
-                else:
-                    s, a, R, ns, nt = split_rows(rows)
-                    loss, gn = rainbow_update(self.local, self.target, self.opt, self.grads, self.support, s,
-                                              a[:, 0].to(torch.int64), R, ns, nt, rows[:, 84], gamma=self.gamma,
-                                              n=self.n_step, sync=self.sync)
+            # act() composed the online noisy weights this iteration
+            loss, gn = self.fused_rb.update(self.opt, self.grads, rows, gamma=self.gamma, n=self.n_step,
+                                            sync=self.sync, seed=self.seed + 999, counter_dev=self.learn_counter,
+                                            compose=False)
             self.per.update_priorities(idx, loss)   # update_priorities(idxs, loss) (agent.py:639)
             self.learn_counter += 1
             return loss.mean(), gn
-        taus = self.taus if self._fused_learner() else None   # drawn by the sampling launch
+        # the update's quantile fractions are drawn by the sampling launch
         rows = self.replay.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter, out=self.batch_rows,
-                                  state=state, guard=guard, taus=taus)
-        if self.agent_type == "AC-IQN" and self.fused2 is not None:
+                                  state=state, guard=guard, taus=self.taus)
+        if self.fused2 is not None:
             return ac_iqn_update_fused2(self.fused2, self.local, self.actor_opt, self.critic_opt, self.critic_grads,
                                         self.actor_grads, rows, gamma=self.gamma, sync=self.sync,
-                                        actor_wait=actor_wait, taus=taus, counter=self.learn_counter)
-        if self.fused_iqn is not None:
-            return iqn_update_fused(self.fused_iqn, self.local, self.opt, self.grads, rows, gamma=self.gamma,
-                                    sync=self.sync, act_wait=actor_wait, taus=taus[:2], counter=self.learn_counter)
-        s, a, r, ns, d = split_rows(rows)
-        if self.agent_type == "AC-IQN" and self.fused is not None:
-            out = ac_iqn_update_fused(self.fused, self.local, self.target, self.actor_opt, self.critic_opt,
-                                      self.critic_grads, self.actor_grads, s, a, r, ns, d, gamma=self.gamma,
-                                      sync=self.sync, amp_dtype=self.amp_dtype)
-        elif self.agent_type == "AC-IQN":
-            out = ac_iqn_update(self.local, self.target, self.actor_opt, self.critic_opt, self.critic_grads,
-                                self.actor_grads, s, a, r, ns, d, gamma=self.gamma, num_tau=self.num_tau,
-                                sync=self.sync, amp_dtype=self.amp_dtype)
-        else:
-            act = a[:, 0].to(torch.int64)
-            out = iqn_update(self.local, self.target, self.opt, self.grads, s, act, r, ns, d, gamma=self.gamma,
-                             num_tau=self.num_tau, sync=self.sync, amp_dtype=self.amp_dtype)
-        self.learn_counter += 1
-        return out
+                                        actor_wait=actor_wait, taus=self.taus, counter=self.learn_counter)
+        return iqn_update_fused(self.fused_iqn, self.local, self.opt, self.grads, rows, gamma=self.gamma,
+                                sync=self.sync, act_wait=actor_wait, taus=self.taus[:2], counter=self.learn_counter)
 
     def hard_update(self):
         """soft_update with TAU = 1.0 (agent.py:643-679): target <- local."""
@@ -347,18 +225,42 @@ class VecTrainer:
             else:
                 pairs = list(zip(self.target.parameters(), self.local.parameters()))
             torch._foreach_copy_([t for t, _ in pairs], [l for _, l in pairs])
-            if self.agent_type == "AC-IQN" and self.fused is not None:
-                self.fused.target_pack.refresh()  # eager, outside any captured graph
-            if self.agent_type == "AC-IQN" and self.fused2 is not None:
+            if self.fused2 is not None:   # eager, outside any captured graph
                 self.fused2.target_changed()
             if self.fused_iqn is not None:
                 self.fused_iqn.target_changed()
             if self.fused_rb is not None:
                 self.fused_rb.target_changed()
 
+    @torch.no_grad()
+    def load_policies(self, local, target):
+        """Start from the given networks (a drop-in Agent's policy_local / policy_target, e.g. after its
+        load_model): their weights are copied in place into this trainer's networks (whose parameters
+        are views of the optimisers' flat buffers) and every weight image is re-packed. Eager, before
+        the first captured graph."""
+        assert self._graph is None, "load_policies before the first captured iteration"
+        pairs = [(self.local, local), (self.target, target)]
+        for dst, src in pairs:
+            mods = [(dst.actor, src.actor), (dst.critic, src.critic)] if hasattr(dst, "actor") else [(dst, src)]
+            for d, s in mods:
+                sd = s.state_dict()
+                for name, t in d.state_dict(keep_vars=True).items():
+                    t.data.copy_(sd[name].to(device=t.device, dtype=t.dtype))
+        if self.fused2 is not None:
+            self.fused2.local_trunk.refresh()
+            self.fused2.actor.refresh()
+            self.fused2.target_changed()
+        if self.fused_iqn is not None:
+            self.fused_iqn.local.refresh()
+            self.fused_iqn.target_changed()
+        if self.fused_rb is not None:
+            self.fused_rb.pack.compose()
+            self.fused_rb.img.refresh()
+            self.fused_rb.target_changed()
+
     # ------------------------------------------------------------------ iteration
     def _iteration_body(self, do_learn):
-        if not (do_learn and self.overlap and self._fused_learner()):
+        if not (do_learn and self.overlap and self.per is None):
             self.rollout()
             out = self.learn() if do_learn else None
             self.env.advance_device()
@@ -432,8 +334,7 @@ class VecTrainer:
         return torch.cuda.Event(), torch.cuda.Event()
 
     def _chained(self):
-        return (self.chain and self.overlap and self._fused_learner() and not self.pipeline
-                and self.unroll % 2 == 0)
+        return self.chain and self.overlap and self.per is None and self.unroll % 2 == 0
 
     def _chain_body(self):
         """self.unroll iterations with per-dependency stream ordering (captured only; see __init__)."""
@@ -478,12 +379,6 @@ class VecTrainer:
                 self._iteration_body(True)
                 self.env.advance_host()
         torch.cuda.current_stream(self.device).wait_stream(s)
-        if self.pipeline:   # the graph's first body consumes parity 0
-            while self._parity != 0:
-                with torch.cuda.stream(s):
-                    self._iteration_body(True)
-                    self.env.advance_host()
-                torch.cuda.current_stream(self.device).wait_stream(s)
         g = torch.cuda.CUDAGraph()
         # thread_local: the RCCL process group's watchdog thread queries its work events while this
         # thread captures; under the default global mode that query invalidates the capture and the
@@ -507,11 +402,3 @@ class VecTrainer:
             self.iteration()
         torch.cuda.synchronize(self.device)
         return time.time() - t0
-
-
-class _null:
-    def __enter__(self):
-        return self
-
-    def __exit__(self, *a):
-        return False

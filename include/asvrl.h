@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 16
+#define ASVRL_ABI_VERSION 17
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -101,6 +101,11 @@ typedef struct AsvEnvState {
   int32_t* ep_ts;    /* [n_envs] episode_timesteps (env.py:64) */
   double* obstacles; /* [n_envs][max_obs][3] x, y, r (env.py:16-22) */
   double* cores;     /* [n_envs][max_cores][4] x, y, clockwise, Gamma (env.py:7-14) */
+  const AsvParams* robot_params; /* optional [n_envs * max_robots]: each robot's own vehicle and
+                                    perception parameters (reset_with_eval_config, env.py:553-607);
+                                    NULL: `params` for every robot. The env-level members (episode
+                                    limit, rewards, core radius) always come from `params`. Taken by the
+                                    per-robot sweep layout (asvrl_env_step chooses it; layout 1 fails) */
 } AsvEnvState;
 
 /* Per-call control of asvrl_env_step. */

@@ -186,8 +186,8 @@ def c51_project(pns_a, returns, nonterminal, support, vmin=-1.0, vmax=1.0, gamma
 GOLDEN = os.path.join(HERE, "..", "tests", "golden")
 
 
-def load_traces():
-    z = np.load(os.path.join(GOLDEN, "env_traces.npz"))
+def load_traces(fname="env_traces.npz"):
+    z = np.load(os.path.join(GOLDEN, fname))
     names = list(z["names"])
     out = {}
     for nm in names:

@@ -203,3 +203,46 @@ def c51_target(pns_a, returns, nonterminal, support, gamma_n, vmin=-1.0, vmax=1.
     for j in range(A):
         m[rows, u[:, j]] += hi[:, j]
     return m
+
+
+# ---------------------------------------------------------------------------------------------------
+# Synthetic Rainbow_Policy state (full dims) reproducible bit for bit from numpy alone: the capture of
+# the reference's train_Rainbow at the network size the kernels take (tools/capture_oracle.py
+# capture_rainbow_full -> tests/golden/learn_rainbow_full.npz) stores only this generator's seed, not
+# the 540k parameters. Layout follows Rainbow_model.py:17-139 (NoisyLinear: weight/bias mu, sigma and
+# the factorised epsilon = f(eps_out) f(eps_in)^T, f(x) = sign(x) sqrt|x|).
+RAINBOW_NOISY = (("hidden_layer_v", 256, 128), ("hidden_layer_v_2", 128, 128), ("output_layer_v", 128, 51),
+                 ("hidden_layer_a", 256, 128), ("hidden_layer_a_2", 128, 128), ("output_layer_a", 128, 25 * 51))
+
+
+def scaled_noise(x):
+    """NoisyLinear._scale_noise (Rainbow_model.py:35-37) on given normals, f32."""
+    x = np.asarray(x, np.float32)
+    return (np.sign(x) * np.sqrt(np.abs(x))).astype(np.float32)
+
+
+def noisy_epsilon(eps_in, eps_out):
+    """reset_noise's buffers (Rainbow_model.py:39-43): weight eps = eps_out ger eps_in (one f32 product
+    per element, as torch.ger), bias eps = eps_out."""
+    return np.outer(eps_out, eps_in).astype(np.float32), np.asarray(eps_out, np.float32).copy()
+
+
+def synthetic_rainbow_state(seed, std_init=0.05):
+    """{state_dict key: f32 array} of a default-dims Rainbow_Policy (self 7 -> 56, objects 5 x (5 -> 40),
+    dueling heads 256 -> 128 -> 128 -> 51 / 25 x 51): mu ~ U(-1/sqrt(in), 1/sqrt(in)) and the encoders
+    likewise, sigma as NoisyLinear.reset_parameters (std_init / sqrt(fan)), epsilon from N(0, 1) draws."""
+    rs = np.random.RandomState(seed)
+    sd = {}
+    for name, fin, fout in (("self_encoder.0", 7, 56), ("object_encoder.0", 5, 40)):
+        r = 1.0 / math.sqrt(fin)
+        sd[name + ".weight"] = rs.uniform(-r, r, (fout, fin)).astype(np.float32)
+        sd[name + ".bias"] = rs.uniform(-r, r, fout).astype(np.float32)
+    for name, fin, fout in RAINBOW_NOISY:
+        r = 1.0 / math.sqrt(fin)
+        sd[name + ".weight_mu"] = rs.uniform(-r, r, (fout, fin)).astype(np.float32)
+        sd[name + ".weight_sigma"] = np.full((fout, fin), std_init / math.sqrt(fin), np.float32)
+        sd[name + ".bias_mu"] = rs.uniform(-r, r, fout).astype(np.float32)
+        sd[name + ".bias_sigma"] = np.full(fout, std_init / math.sqrt(fout), np.float32)
+        we, be = noisy_epsilon(scaled_noise(rs.standard_normal(fin)), scaled_noise(rs.standard_normal(fout)))
+        sd[name + ".weight_epsilon"], sd[name + ".bias_epsilon"] = we, be
+    return sd

@@ -33,7 +33,7 @@ def test_struct_layouts():
     from distributional_rl_decision_and_control_amd import _abi
     # sizes the header implies on LP64 (checked against the compiled library's own view)
     assert C.sizeof(_abi.AsvParams) == 480
-    assert C.sizeof(_abi.AsvEnvState) == 16 + 8 * 8
+    assert C.sizeof(_abi.AsvEnvState) == 16 + 9 * 8   # ABI 17: + robot_params
     assert C.sizeof(_abi.AsvStepCtl) == 16 + 16 + 8 + 8 + 8
     assert C.sizeof(_abi.AsvStepOut) == 8 * 8
     assert C.sizeof(_abi.AsvResetCfg) == 16 + 10 * 8

@@ -49,7 +49,7 @@ def test_chained_schedule_bench_shape_after_pool_wrap():
     pool = [torch.cuda.Stream() for _ in range(40)]   # torch's pool (32 per device) wraps around
     a, pa, la = _run("AC-IQN", True, 20, n_envs=4096, batch=4096, unroll=10)
     handles = [streams.capture_stream(a.device).cuda_stream, a.roll_stream().cuda_stream,
-               streams.stream(a.device, "warmup").cuda_stream] + [s.cuda_stream for s in a.fused2.side.streams]
+               streams.stream(a.device, "warmup").cuda_stream]
     assert len(set(handles)) == len(handles), "the schedule's streams must be distinct"
     assert not set(handles) & {s.cuda_stream for s in pool}, "a schedule stream is also a torch pool stream"
     del a

@@ -36,7 +36,8 @@ def _critic_grads(ops, B, N, fused, rows, taus, seed=100, enc=False):
     enc: the encoders' gradients formed inside the fused launch (parts.enc / parts.aenc) instead of
     the batched weight-gradient launch over dzF / dzG."""
     from distributional_rl_decision_and_control_amd.agent import Agent
-    from distributional_rl_decision_and_control_amd.fused_critic import critic_train, critic_train_fused, wout_groups
+    from distributional_rl_decision_and_control_amd.fused_critic import (TrainBuffers, critic_train, critic_train_fused,
+                                                                          wout_groups)
     from distributional_rl_decision_and_control_amd.fused_update import FusedACIQNState, target_q
     from distributional_rl_decision_and_control_amd.learner import FusedAdam
     ag = Agent(seed=seed, agent_type="AC-IQN")
@@ -45,6 +46,7 @@ def _critic_grads(ops, B, N, fused, rows, taus, seed=100, enc=False):
     co = FusedAdam(loc.critic.parameters(), lr=1e-4, operands=ops)
     st = FusedACIQNState(loc, tgt, B, N, operands=ops)
     critic, arena = loc.critic, st.arena
+    bufs = None if fused else TrainBuffers(B, N, "cuda", ops)   # the two-kernel reference's activations
     s_rows, a_rows, r_col, d_col = rows[:, 0:40], rows[:, 80:82], rows[:, 82], rows[:, 83]
     co.grads.zero_()
     target_q(st, rows, taus[0], st.q_next, st.na)
@@ -58,7 +60,7 @@ def _critic_grads(ops, B, N, fused, rows, taus, seed=100, enc=False):
     else:
         tiles = wout_groups(B, N)
         wout = arena.take_tiles(tiles, 128)
-        critic_train(st.local_trunk, None, None, taus[1], None, st.bufs, q_next=st.q_next.view(B, N), rewards=r_col,
+        critic_train(st.local_trunk, None, None, taus[1], None, bufs, q_next=st.q_next.view(B, N), rewards=r_col,
                      dones=d_col, gamma=0.99, dzF=st.dzF, dzG=st.dzG, with_dFdG=False, tile_loss=st.tile_loss[0],
                      obs=s_rows, act=a_rows, xb=st.xb, wout_part=wout)
         arena.tiles(wout, tiles, critic.output_layer.weight.grad, critic.output_layer.bias.grad)
@@ -66,7 +68,7 @@ def _critic_grads(ops, B, N, fused, rows, taus, seed=100, enc=False):
         if enc:
             pass
         elif not fused:
-            b = st.bufs
+            b = bufs
             arena.linear(b.dzc, b.cos, critic.cos_embedding.weight.grad, critic.cos_embedding.bias.grad)
             arena.linear(b.dz1, b.h0, critic.hidden_layer.weight.grad, critic.hidden_layer.bias.grad)
             arena.linear(b.dz2, b.h1g, critic.hidden_layer_2.weight.grad, critic.hidden_layer_2.bias.grad)

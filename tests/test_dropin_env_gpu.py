@@ -46,12 +46,23 @@ def _state(r):
                      r.right_pos], dtype=np.float64)
 
 
-def _replay(env, tr, continuous, tol):
+def _set_state(r, s):
+    r.x, r.y, r.theta = s[0], s[1], s[2]
+    r.velocity_r, r.velocity = s[3:6].copy(), s[6:9].copy()
+    r.left_thrust, r.right_thrust, r.left_pos, r.right_pos = s[9], s[10], s[11], s[12]
+
+
+def _replay(env, tr, continuous, tol, force=False):
+    """Feed the recorded actions step by step. force: teacher-forced -- every step starts from the
+    reference's recorded state (the noise still comes from the robots' own RandomStates, in order), and
+    the state after the step is compared at `tol`."""
     n = len(env.robots)
     assert n == int(tr["n_robots"])
     for t in range(len(tr["reward"])):
         sb = tr["state_before"][t][:n]
         for i, r in enumerate(env.robots):
+            if force:
+                _set_state(r, sb[i])
             np.testing.assert_allclose(_state(r), sb[i], rtol=tol, atol=tol, err_msg=f"t={t} robot {i} pre-state")
         acts = []
         for i, r in enumerate(env.robots):
@@ -76,6 +87,10 @@ def _replay(env, tr, continuous, tol):
             assert len(o) == tr["obj_cnt"][t][i]
             if len(o):
                 np.testing.assert_allclose(np.array(o), tr["obj_obs"][t][i][:len(o)], rtol=tol, atol=tol)
+        if force:
+            sa = tr["state_after"][t][:n]
+            for i, r in enumerate(env.robots):
+                np.testing.assert_allclose(_state(r), sa[i], rtol=tol, atol=tol, err_msg=f"t={t} robot {i}")
         for i, r in enumerate(env.robots):  # trainer.py:168-170
             if not r.deactivated and (r.collision or r.reach_goal):
                 r.deactivated = True
@@ -136,3 +151,27 @@ def test_reset_observation_matches_reference():
             assert len(obs[i][1]) == k
             if k:
                 np.testing.assert_allclose(np.array(obs[i][1]), z[p + "obj_obs"][i][:k], rtol=1e-12, atol=1e-12)
+
+
+EVALCFG = ("evalcfg_r5o4_s11", "evalcfg_r8o4_s13", "cores20_r5o4_s12")
+
+
+@pytest.mark.parametrize("force,tol", [(True, 1e-12), (False, 1e-9)])
+@pytest.mark.parametrize("name", EVALCFG)
+def test_dropin_env_eval_config_trace(name, force, tol):
+    """reset_with_eval_config (env.py:503-614) + steps, against the reference's traces
+    (tests/golden/env_evalcfg.npz): robots with their own dt, N, size, goal distance, thrust limits, mass,
+    inertia, hydrodynamic coefficients and perception range / angle / max_obj_num / sigma / kappa
+    (the kernel's per-robot parameter table, AsvEnvState.robot_params), and a scene with 20 vortex
+    cores. Masks and info exact; f64 state 1e-12 teacher-forced per step, 1e-9 chained."""
+    import json
+    from distributional_rl_decision_and_control_amd.envs.marinenav.env import MarineNavEnv3
+    tr = eo.load_traces("env_evalcfg.npz")[name]
+    env = MarineNavEnv3(seed=0)
+    env.num_robots = int(tr["num_robots_attr"])   # the robots' RandomState seeds are drawn in [0, 5 num_robots)
+    env.reset_with_eval_config(json.loads(str(tr["config"])))
+    if name.startswith("evalcfg"):
+        assert len({r.physics_signature() for r in env.robots}) == len(env.robots)
+    else:
+        assert len(env.cores) == 20
+    _replay(env, tr, True, tol, force=force)

@@ -23,6 +23,7 @@ import pytest
 import torch
 
 from oracle import env_oracle as eo
+from oracle import learn_ref as lr
 
 pytestmark = pytest.mark.gpu
 
@@ -211,3 +212,52 @@ def test_fused_ac_iqn_bench_shape_bf16_tracks_f32():
     c = _cos(deltas["bf16"], deltas["f32"])
     print(f"bench shape: losses f32 {out['f32'][:2]}, bf16 {out['bf16'][:2]}; update cosine {c:.4f}")
     assert c > 0.95
+
+
+def test_rollout_act_kernel_f32_matches_reference_actor():
+    """The act kernel that produces every training action (actor_kernel<ACT>, asvrl_actor_forward MODE_ACT:
+    Actor.forward, AC_IQN_model.py:284-323, + epsilon-greedy, agent.py:207-225) in the f32-operand build at
+    epsilon = 0 against the reference's actor: the captured outputs of the seeded initial actor on
+    no-object states (fwd/noobj_*), and the CPU restatement (oracle.learn_ref.actor_forward, f64) of the
+    reference's actor with its initial and post-step-1 / post-step-3 weights on every F4 state (s and s').
+    Bar: 1e-5 on actions. The bf16 build (the training path) at its stated 2 % of scale: test_fused_mlp_gpu."""
+    from distributional_rl_decision_and_control_amd.fused_mlp import MlpPack, actor_act
+    from distributional_rl_decision_and_control_amd.policy.AC_IQN_model import AC_IQN_Policy
+    from distributional_rl_decision_and_control_amd.vec_trainer import DEFAULT_NET
+    z = np.load(eo.GOLDEN + "/learn_ac_iqn.npz")
+    pol = AC_IQN_Policy(**DEFAULT_NET, value_ranges_of_action=[[-1, 1], [-1, 1]], device="cuda", seed=100)
+
+    def act(rows):
+        pack = MlpPack(pol.actor, "actor", "f32")
+        out = torch.empty(rows.shape[0], 2, dtype=torch.float64, device="cuda")
+        step = torch.zeros(1, dtype=torch.int64, device="cuda")
+        actor_act(pack, rows, out, step, 1, 1e6, 0.25, 0.0, 0.0, seed=3)   # epsilon 0 throughout
+        torch.cuda.synchronize()
+        return out.cpu().numpy()
+
+    def load(prefix):
+        with torch.no_grad():
+            for k, v in pol.actor.state_dict().items():
+                v.copy_(torch.tensor(z[prefix + "actor/" + k]))
+
+    load("init/")
+    ns = z["fwd/noobj_self"]
+    rows = torch.zeros(ns.shape[0], 40, device="cuda")
+    rows[:, 0:7] = torch.tensor(ns)
+    np.testing.assert_allclose(act(rows), z["fwd/noobj_actions"], rtol=1e-5, atol=1e-6)
+    states = []
+    for st in ("step0/", "step1/", "step2/"):
+        for p in ("s_", "ns_"):
+            states.append((z[st + p + "self"], z[st + p + "obj"], z[st + p + "mask"]))
+    S = np.concatenate([s[0] for s in states]), np.concatenate([s[1] for s in states]), \
+        np.concatenate([s[2] for s in states])
+    n = S[0].shape[0]
+    rows = torch.zeros(n, 40, device="cuda")
+    rows[:, 0:7] = torch.tensor(S[0])
+    rows[:, 7:32] = torch.tensor(S[1]).reshape(n, 25)
+    rows[:, 32:37] = torch.tensor(S[2])
+    for prefix in ("init/", "after0/", "after2/"):
+        load(prefix)
+        w = {k: torch.tensor(z[prefix + "actor/" + k]).double() for k in pol.actor.state_dict()}
+        ref = lr.actor_forward(w, tuple(torch.tensor(x).double() for x in S)).numpy()
+        np.testing.assert_allclose(act(rows), ref, rtol=1e-5, atol=1e-6, err_msg=prefix)

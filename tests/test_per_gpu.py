@@ -199,45 +199,6 @@ def test_vec_trainer_rainbow_graph():
     assert tr.per.tree[0].item() > 0
 
 
-def test_rainbow_update_rows_matches_train_rainbow():
-    """The packed-row update (one online forward over s and s_{t+n}) equals the reference-shaped
-    rainbow_update (agent.py:597-641) in fp32: per-sample loss 1e-5, gradient norm 1e-5, weights."""
-    import copy
-    from distributional_rl_decision_and_control_amd.learner import FlatGrads, rainbow_update, rainbow_update_rows
-    from distributional_rl_decision_and_control_amd.learn_ops import split_rows
-    from distributional_rl_decision_and_control_amd.policy.Rainbow_model import Rainbow_Policy
-    from distributional_rl_decision_and_control_amd.vec_trainer import DEFAULT_NET
-    dev = "cuda"
-    B = 512
-    g = torch.Generator(device=dev).manual_seed(1)
-    rows = torch.zeros(B, 88, device=dev)
-    rows[:, 0:37] = torch.randn(B, 37, device=dev, generator=g)
-    rows[:, 40:77] = torch.randn(B, 37, device=dev, generator=g)
-    rows[:, 32:37] = (rows[:, 32:37] > 0).float()
-    rows[:, 72:77] = (rows[:, 72:77] > 0).float()
-    rows[:, 80] = torch.randint(0, 25, (B,), device=dev, generator=g).float()
-    rows[:, 82] = torch.randn(B, device=dev, generator=g)
-    rows[:, 83] = (torch.rand(B, device=dev, generator=g) > 0.2).float()
-    rows[:, 84] = torch.rand(B, device=dev, generator=g)
-    sup = torch.linspace(-1.0, 1.0, 51, device=dev)
-    outs = []
-    for fn in ("ref", "rows"):
-        local = Rainbow_Policy(**DEFAULT_NET, action_size=25, atoms=51, device=dev, seed=9).to(dev)
-        target = copy.deepcopy(local)
-        grads = FlatGrads(local.parameters())
-        opt = torch.optim.Adam(local.parameters(), lr=1e-4)
-        torch.cuda.manual_seed(77)
-        if fn == "ref":
-            s, a, R, ns, nt = split_rows(rows)
-            loss, gn = rainbow_update(local, target, opt, grads, sup, s, a[:, 0].long(), R, ns, nt, rows[:, 84])
-        else:
-            loss, gn = rainbow_update_rows(local, target, opt, grads, sup, rows)
-        outs.append((loss, gn, torch.cat([p.detach().reshape(-1) for p in local.parameters()])))
-    torch.testing.assert_close(outs[1][0], outs[0][0], rtol=1e-5, atol=1e-6)
-    torch.testing.assert_close(outs[1][1], outs[0][1], rtol=1e-5, atol=1e-7)
-    torch.testing.assert_close(outs[1][2], outs[0][2], rtol=1e-5, atol=1e-7)
-
-
 def test_per_unvalidated_draw_gets_zero_weight():
     """A draw that never validates (here: the injected uniform of the last segment lands on a
     transition whose n-step window reaches the write head, replay_memory_rainbow.py:163) is counted
@@ -257,3 +218,13 @@ def test_per_unvalidated_draw_gets_zero_weight():
     assert per.anomalies() == 1
     w = rows[:, 84]
     assert np.all(np.isfinite(w)) and w[B - 1] == 0.0 and np.all(w[:B - 1] > 0) and np.isclose(w.max(), 1.0)
+    # the unvalidated draw is marked -1 and update_priorities leaves its leaf as it was
+    ix = idx.cpu().numpy()
+    assert ix[B - 1] == -1 and np.all(ix[:B - 1] >= 0)
+    leaf = per.tree_leaves - 1 + int(rows[B - 1, 86])
+    before = per.tree.clone()
+    per.update_priorities(idx, torch.full((B,), 4.0, device="cuda"))
+    torch.cuda.synchronize()
+    assert per.tree[leaf].item() == before[leaf].item()
+    assert per.anomalies() == 1   # the -1 entry is not an ordering anomaly
+    assert np.all(per.tree[torch.from_numpy(ix[:B - 1]).cuda()].cpu().numpy() == 2.0)

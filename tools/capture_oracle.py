@@ -14,11 +14,15 @@ Fixture families:
                          env.py:257-260 loop, env.py:458-501 current field)
   env_traces.npz    F2/F3  MarineNavEnv3.step traces with every perception noise
                         draw recorded (env.py:240-333, wamv.py:436-529)
+  env_evalcfg.npz   F2c reset_with_eval_config with per-robot vehicle / perception parameters, and a
+                        20-core scene (env.py:503-614)
   env_reset.npz     F7  MarineNavEnv3.reset rejection sampler (env.py:72-164)
   learn_ac_iqn.npz  F4  Agent.train_AC_IQN (agent.py:386-432), N=8 and N=32
   learn_iqn.npz     F5  Agent.train_IQN (agent.py:434-476)
   learn_rainbow.npz F6  Agent.train_Rainbow incl. the C51 projection target m
                         (agent.py:597-641)
+  learn_rainbow_full.npz F6b  the same at the default network size (the size the kernels take),
+                        networks from a numpy-seeded generator (oracle/learn_ref.py)
   learn_dqn.npz     F8  Agent.train_DQN / act_dqn (agent.py:518-545, 271-287)
   eval_ref.npz      F9  Trainer.evaluation (trainer.py:266-392), AC-IQN and Rainbow
 """
@@ -143,10 +147,13 @@ def pack_obs(obs, R):
 # F2/F3: env.step traces
 # ----------------------------------------------------------------------------------
 def run_trace(env, n_steps, action_fn, continuous, R, O, ep_ts_override=None,
-              post_reset=None):
-    """Reset + run n_steps of env.step the way Trainer.learn drives it
+              post_reset=None, reset=None):
+    """Reset (env.reset(), or `reset(env)`) + run n_steps of env.step the way Trainer.learn drives it
     (trainer.py:110-172: None actions for deactivated robots, deactivate on flags)."""
-    env.reset()
+    if reset is None:
+        env.reset()
+    else:
+        reset(env)
     if post_reset is not None:
         post_reset(env)
     # re-observe so recorded observation matches a post_reset edit is not needed; the
@@ -169,7 +176,7 @@ def run_trace(env, n_steps, action_fn, continuous, R, O, ep_ts_override=None,
         n_obs=len(env.obstacles),
         goals=np.array([list(r.goal) for r in env.robots] + [[0, 0]] * (R - n)),
         n_robots=n,
-        cores=np.array([[c.x, c.y, float(c.clockwise), c.Gamma] for c in env.cores] + [[0, 0, 0, 0]] * (8 - len(env.cores))).reshape(8, 4),
+        cores=np.array([[c.x, c.y, float(c.clockwise), c.Gamma] for c in env.cores] + [[0, 0, 0, 0]] * max(0, 8 - len(env.cores))).reshape(max(8, len(env.cores)), 4),
         n_cores=len(env.cores),
         core_r=env.r,
         width=env.width, height=env.height,
@@ -795,6 +802,183 @@ def capture_rainbow():
             out.update(sd_arrays("after/", agent.policy_local))
     np.savez_compressed(os.path.join(OUT, "learn_rainbow.npz"), **out)
     print("rainbow keys:", len(out))
+
+
+def capture_rainbow_full():
+    """F6b: Agent.train_Rainbow (agent.py:597-641) at the default network size (the size the Rainbow
+    kernels take), compact: the networks come from oracle.learn_ref.synthetic_rainbow_state(seed) (numpy,
+    reproducible bit for bit), so the fixture holds the seed, the batch, the target noise reset_noise drew
+    inside train (its eps_in / eps_out vectors, recorded per layer), and the outputs: per-sample loss,
+    m, the online argmax over s_{t+n}, p(s_{t+n}, a*), the pre-clip gradient norm, and per parameter the
+    post-clip gradient and the parameter after the Adam step (full for tensors of <= 4096 elements, else
+    at 2048 fixed sampled positions plus f64 sum / sum of squares of the whole tensor)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from oracle import learn_ref as lr
+    out = {}
+    seed, bsz = 7, 64
+    out["seed"] = np.array([seed])
+    sd = lr.synthetic_rainbow_state(seed)
+    agent = ref_agent_mod.Agent(device="cpu", seed=100, agent_type="Rainbow", BATCH_SIZE=bsz)
+    with torch.no_grad():
+        for net in (agent.policy_local, agent.policy_target):
+            for k, v in net.state_dict().items():
+                v.copy_(torch.from_numpy(sd[k]))
+    # record the target's reset_noise draws (eps_in, eps_out per layer, in the reference's call order)
+    rec = {}
+    for name, layer in agent.policy_target.named_children():
+        if "hidden_layer" in name or "output_layer" in name:
+            orig = layer._scale_noise
+
+            def wrapped(size, orig=orig, name=name):
+                x = orig(size)
+                rec.setdefault(name, []).append(x.detach().numpy().copy())
+                return x
+            layer._scale_noise = wrapped
+    trans = collect_transitions(400, seed=9, discrete=True)
+    rs = np.random.RandomState(61)
+    idx = rs.choice(len(trans), bsz, replace=False)
+    samples = [trans[i] for i in idx]
+    s = agent.memory.state_batch([t[0] for t in samples])
+    ns = agent.memory.state_batch([t[3] for t in samples])
+    st = tuple(torch.tensor(x).float() for x in s)
+    nst = tuple(torch.tensor(x).float() for x in ns)
+    actions = torch.tensor([t[1] for t in samples], dtype=torch.int64)
+    R = torch.tensor(rs.uniform(-1.5, 1.5, size=bsz), dtype=torch.float32)
+    nonterm = torch.tensor(rs.randint(0, 2, size=(bsz, 1)), dtype=torch.float32)
+    R[0], nonterm[0] = 0.0, 0.0      # b = 25 exactly (the l == u fix)
+    R[1], nonterm[1] = -1.0, 0.0     # b = 0
+    R[2], nonterm[2] = 1.0, 0.0      # b = 50
+    R[3], nonterm[3] = 5.0, 1.0      # clamped high
+    R[4], nonterm[4] = -5.0, 1.0     # clamped low
+    weights = torch.tensor(rs.uniform(0.2, 1.0, size=bsz), dtype=torch.float32)
+    weights = weights / weights.max()
+    batch = (np.arange(bsz), st, actions, R, nst, nonterm, weights)
+    agent.memory.sample = (lambda b, batch=batch: batch)
+    prio = []
+    agent.memory.update_priorities = lambda i, p: prio.append(np.array(p))
+    with torch.no_grad():
+        pns_online = agent.policy_local(nst)
+        argmax_ns = (agent.support.expand_as(pns_online) * pns_online).sum(2).argmax(1)
+    grads = {}
+    opt_step = agent.optimizer.step
+
+    def step_rec(*a, **k):   # the clipped gradient the optimizer applies
+        for n, p in agent.policy_local.named_parameters():
+            grads[n] = p.grad.detach().numpy().astype(np.float32).copy()
+        return opt_step(*a, **k)
+    agent.optimizer.step = step_rec
+    proxy = TorchZerosProxy(torch)
+    ref_agent_mod.torch = proxy
+    try:
+        with ClipRecorder() as cr:
+            loss = agent.train_Rainbow()
+    finally:
+        ref_agent_mod.torch = torch
+    m = [z for z in proxy.captured if tuple(z.shape) == (bsz, 51)]
+    assert len(m) == 1
+    with torch.no_grad():
+        pns_a = agent.policy_target(nst)[range(bsz), argmax_ns]
+    for name, xs in rec.items():
+        assert len(xs) == 2, (name, len(xs))
+        out["target_eps_in/" + name], out["target_eps_out/" + name] = xs[0], xs[1]
+    out["s_self"], out["s_obj"], out["s_mask"] = [x.numpy() for x in st]
+    out["ns_self"], out["ns_obj"], out["ns_mask"] = [x.numpy() for x in nst]
+    out["actions"], out["returns"], out["nonterminal"] = actions.numpy(), R.numpy(), nonterm.numpy()
+    out["weights"], out["argmax_ns"], out["pns_a"] = weights.numpy(), argmax_ns.numpy(), pns_a.numpy()
+    out["m"], out["loss"], out["priorities"] = m[0].numpy(), np.array(loss), prio[0]
+    out["grad_norm"] = np.array(cr.norms)
+    pick = np.random.RandomState(5)
+    for n, p in agent.policy_local.named_parameters():
+        g, a = grads[n].reshape(-1), p.detach().numpy().reshape(-1)
+        if g.size <= 4096:
+            out["grad/" + n], out["after/" + n] = g, a.copy()
+        else:
+            ix = np.sort(pick.choice(g.size, 2048, replace=False))
+            out["idx/" + n] = ix.astype(np.int32)
+            out["grad/" + n], out["after/" + n] = g[ix], a[ix].copy()
+            out["gsum/" + n] = np.array([g.astype(np.float64).sum(), (g.astype(np.float64) ** 2).sum()])
+            out["asum/" + n] = np.array([a.astype(np.float64).sum(), (a.astype(np.float64) ** 2).sum()])
+    np.savez_compressed(os.path.join(OUT, "learn_rainbow_full.npz"), **out)
+    print("rainbow_full keys:", len(out), "loss mean", float(np.mean(loss)), "grad norm", cr.norms)
+
+
+def capture_evalcfg():
+    """F2c: MarineNavEnv3.reset_with_eval_config (env.py:503-614) with every robot's own vehicle and
+    perception parameters (dt, N, size, goal distance, thrust limits and grid, m, Izz, the hydrodynamic
+    coefficients, perception range / angle / max_obj_num / sigma / kappa), and a scene with 20 vortex
+    cores; then env.step traces as capture_traces records them (every perception draw). The eval config
+    is stored as its JSON text (env_evalcfg.npz, key <name>/config)."""
+    import contextlib
+    import io
+    import json
+
+    def cont_fn(seed):
+        rs = np.random.RandomState(177 + seed)
+        return lambda t, i: [float(rs.uniform(-1, 1)), float(rs.uniform(-1, 1))]
+
+    def base_config(seed, R, O, cores, msgd, width):
+        e = MarineNavEnv3(seed=seed)
+        e.num_robots, e.num_cores, e.num_obs, e.min_start_goal_dis = R, cores, O, msgd
+        e.width = e.height = width
+        with contextlib.redirect_stdout(io.StringIO()):
+            e.reset()
+        return json.loads(json.dumps(e.episode_data()))
+
+    def vary(cfg, seed):
+        rs = np.random.RandomState(seed)
+        rb = cfg["robots"]
+        n = cfg["env"]["num_robots"]
+        scale = lambda k, lo, hi: [float(v * rs.uniform(lo, hi)) for v in rb[k]]  # noqa: E731
+        for k in ("m", "Izz", "xDotU", "yDotV", "yDotR", "nDotR", "nDotV", "xU", "xUU", "yV", "yVV", "yR", "yRV",
+                  "yVR", "yRR", "nR", "nRR", "nV", "nVV", "nRV", "nVR"):
+            rb[k] = scale(k, 0.7, 1.3)
+        rb["dt"] = [[0.05, 0.04, 0.05, 0.06, 0.05][i % 5] for i in range(n)]
+        rb["N"] = [[10, 12, 8, 10, 10][i % 5] for i in range(n)]
+        rb["length"] = scale("length", 0.8, 1.2)
+        rb["width"] = scale("width", 0.8, 1.2)
+        rb["r"] = [float(0.5 * np.sqrt(L * L + W * W)) for L, W in zip(rb["length"], rb["width"])]
+        rb["detect_r"] = list(rb["r"])
+        rb["goal_dis"] = [[2.0, 2.5, 1.5, 3.0, 2.0][i % 5] for i in range(n)]
+        rb["min_thrust"] = [[-500.0, -400.0, -600.0, -500.0, -450.0][i % 5] for i in range(n)]
+        rb["max_thrust"] = [[1000.0, 900.0, 1100.0, 800.0, 1000.0][i % 5] for i in range(n)]
+        pe = rb["perception"]
+        pe["range"] = [[20.0, 15.0, 25.0, 18.0, 22.0][i % 5] for i in range(n)]
+        pe["angle"] = [[2 * np.pi, 1.5 * np.pi, 2 * np.pi, np.pi, 2 * np.pi][i % 5] for i in range(n)]
+        pe["max_obj_num"] = [[5, 4, 5, 3, 5][i % 5] for i in range(n)]
+        pe["pos_std"] = [[0.05, 0.1, 0.02, 0.08, 0.05][i % 5] for i in range(n)]
+        pe["vel_std"] = [[0.05, 0.03, 0.1, 0.05, 0.07][i % 5] for i in range(n)]
+        pe["r_kappa"] = [[1.0, 2.0, 0.5, 1.0, 3.0][i % 5] for i in range(n)]
+        pe["r_mean_ratio"] = [[0.8, 0.7, 0.9, 0.8, 0.75][i % 5] for i in range(n)]
+        return cfg
+
+    cases = {   # name -> (base seed, R, O, cores, msgd, width, vary robots, eval env seed, steps)
+        "evalcfg_r5o4_s11": (11, 5, 4, 0, 40.0, 55, True, 21, 100),
+        "evalcfg_r8o4_s13": (13, 8, 4, 0, 30.0, 80, True, 23, 120),
+        "cores20_r5o4_s12": (12, 5, 4, 20, 30.0, 110, False, 22, 60),
+    }
+    out = {}
+    for name, (seed, R, O, nc, msgd, width, var, eseed, steps) in cases.items():
+        cfg = base_config(seed, R, O, nc, msgd, width)
+        if var:
+            cfg = vary(cfg, 500 + seed)
+        env = MarineNavEnv3(seed=eseed)   # reset_with_eval_config re-seeds env.rd from the config
+        env.num_robots = R                # ... and draws the robots' seeds in [0, 5 * num_robots)
+        text = json.dumps(cfg)
+
+        def reset(e, text=text):
+            with contextlib.redirect_stdout(io.StringIO()):
+                e.reset_with_eval_config(json.loads(text))
+        tr = run_trace(env, steps, cont_fn(seed), True, R, O, reset=reset)
+        for k, v in tr.items():
+            out[f"{name}/{k}"] = v
+        out[f"{name}/R"], out[f"{name}/O"] = np.int32(R), np.int32(O)
+        out[f"{name}/config"] = np.array(text)
+        out[f"{name}/num_robots_attr"] = np.int32(R)
+        print(f"evalcfg {name}: steps={len(tr['reward'])} robots={tr['n_robots']} cores={len(env.cores)} "
+              f"collisions={int(tr['collision'].sum())} reach={int(tr['reach'].sum())} "
+              f"colregs={int(tr['apply_colregs'].sum())}")
+    out["names"] = np.array(list(cases.keys()))
+    np.savez_compressed(os.path.join(OUT, "env_evalcfg.npz"), **out)
 
 
 def capture_dqn():
