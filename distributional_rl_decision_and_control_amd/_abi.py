@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("ASVRL_LIB", os.path.join(HERE, "lib", "libasvrl.so"))
 # the same sources built with f32 learner operands (the parity build; asvrl_operand_bytes() == 4)
 LIB_PATH_F32 = os.path.join(HERE, "lib", "libasvrl_f32.so")
 OPERANDS = {"bf16": (LIB_PATH, 2), "f32": (LIB_PATH_F32, 4)}
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
 OBS_DIM = 40   # self 7 | objects 25 | mask 5 | pad 3
@@ -172,6 +172,12 @@ class AsvMlpIO(C.Structure):
                 ("eps_initial", _D), ("eps_final", _D), ("seed", _U64)]
 
 
+class AsvSampleArgs(C.Structure):
+    _fields_ = [("ring", _VP), ("capacity", _I64), ("ring_state", _VP), ("seed", _U64), ("counter", _U64),
+                ("counter_dev", _VP), ("guard", _I64), ("B", _I32), ("tau_sets", _I32), ("tau_n", _I32),
+                ("_pad0", _I32), ("out", _VP), ("taus", _VP)]
+
+
 class AsvPer(C.Structure):
     _fields_ = [("rows", _VP), ("tree", _VP), ("state", _VP), ("t", _VP), ("maxp", _VP), ("dirty", _VP),
                 ("capacity", _I64), ("tree_leaves", _I64), ("stride", _I32), ("n_step", _I32), ("discount", _D),
@@ -245,6 +251,8 @@ EXPORTS = [
                                   C.POINTER(AsvCriticActs), _VP]),
     ("asvrl_iqn_act", C.c_int, [C.POINTER(AsvCriticWeights), C.POINTER(AsvIqnHead), C.POINTER(AsvIqnIO), _VP]),
     ("asvrl_replay_push", C.c_int, [_VP, _VP, _VP, _VP, _I32, _VP, _VP, _I32, _VP, _I64, _VP, _VP, _VP]),
+    ("asvrl_replay_push_ex", C.c_int, [_VP, _VP, _VP, _VP, _I32, _I64, _VP, _VP, _I32, _VP, _I64, _VP, _VP, _VP,
+                                       _VP, _VP]),
     ("asvrl_replay_sample", C.c_int, [_VP, _I64, _VP, _VP, _I32, _U64, _U64, _VP, _I64, _VP, _VP, _VP, _I32, _I32,
                                       _VP]),
     ("asvrl_replay_write_rows", C.c_int, [_VP, _VP, _I32, _VP, _VP]),
@@ -287,6 +295,8 @@ EXPORTS = [
     ("asvrl_mlp_encode", C.c_int, [C.POINTER(AsvMlpWeights), C.POINTER(AsvMlpIO), _VP]),
     ("asvrl_actor_forward", C.c_int, [C.POINTER(AsvMlpWeights), C.POINTER(AsvMlpIO), _I32, _VP]),
     ("asvrl_actor_backward", C.c_int, [C.POINTER(AsvMlpWeights), C.POINTER(AsvMlpIO), _VP]),
+    ("asvrl_learn_prologue", C.c_int, [C.POINTER(AsvSampleArgs), C.POINTER(AsvMlpWeights), C.POINTER(AsvMlpIO),
+                                       C.POINTER(AsvMlpWeights), _VP, _VP]),
     ("asvrl_encoder_fold", C.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, _I32, _VP]),
     ("asvrl_small_wgrad", C.c_int, [_VP, _I64, _VP, _I64, _I32, _I32, _I32, _VP, _VP, _I32, _VP, _I64, _VP]),
     ("asvrl_last_error", C.c_char_p, []),

@@ -210,4 +210,42 @@ __device__ __forceinline__ void small_wgrad_body(const float* __restrict__ dz, i
   }
 }
 
+// ---------------------------------------------------------------- replay draw (uniform ring)
+// The deque position and ring slot of sampled row b (random.sample of replay_buffer.py:26-45, with
+// replacement, on Philox(seed, b, ctr)); guard: skip the oldest entries a concurrent push of <= guard
+// rows may overwrite. Shared by asvrl_replay_sample and the fused learn prologue (bit-identical draws).
+__device__ __forceinline__ int64_t replay_draw_slot(int64_t head, int64_t size, int64_t cap, int64_t guard, int b,
+                                                    uint64_t seed, uint64_t ctr) {
+  const U4 r = philox4x32_10(U4{static_cast<uint32_t>(b), 0x5A3Bu, static_cast<uint32_t>(ctr >> 32),
+                                static_cast<uint32_t>(ctr)},
+                             static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
+  const uint64_t bits = (static_cast<uint64_t>(r.x) << 32) | r.y;
+  int64_t lo = size + guard - cap;
+  lo = lo > 0 ? lo : 0;
+  if (lo >= size) lo = 0;
+  const int64_t k = size > 0 ? lo + static_cast<int64_t>(bits % static_cast<uint64_t>(size - lo)) : 0;
+  return ((head - size + k) % cap + cap) % cap;   // deque index 0 = oldest
+}
+
+// the update's quantile fractions tau ~ U[0, 1) (AC_IQN_model.py:419, torch.rand) of sampled row b:
+// tau_sets sets of [B][tau_n], Philox(seed, step) per (row, set, 4 taus), the wave's 64 lanes in turn
+__device__ __forceinline__ void replay_draw_taus(int b, int lane, int B, uint64_t seed, uint64_t ctr, float* taus,
+                                                 int tau_sets, int tau_n) {
+  const int per_row = tau_sets * tau_n;
+  for (int k0 = 4 * lane; k0 < per_row; k0 += 4 * kWave) {
+    const U4 r = philox4x32_10(U4{static_cast<uint32_t>(b), static_cast<uint32_t>(k0) ^ 0x7A0000u,
+                                  static_cast<uint32_t>(ctr >> 32), static_cast<uint32_t>(ctr)},
+                               static_cast<uint32_t>(seed) ^ 0x51EDu, static_cast<uint32_t>(seed >> 32));
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + j;
+      if (k < per_row) {
+        const int set = k / tau_n, t = k - set * tau_n;
+        taus[(static_cast<size_t>(set) * B + b) * tau_n + t] = static_cast<float>(w[j] >> 8) * (1.0f / 16777216.0f);
+      }
+    }
+  }
+}
+
 }  // namespace asvrl

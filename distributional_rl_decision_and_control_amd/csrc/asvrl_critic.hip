@@ -33,6 +33,7 @@
 //   IQN_ACT    act_iqn (agent.py:227-256): mean over K = 32 taus per state, argmax, epsilon-greedy
 #include "asvrl_common.h"
 #include "asvrl_mfma.h"
+#include "asvrl_lds.h"
 
 namespace asvrl {
 namespace {
@@ -168,7 +169,7 @@ __device__ __forceinline__ void stage_features(const CriticArgs& a, int tile, in
     } else {
       const float* f = a.F + static_cast<int64_t>(b) * kC;
 #pragma unroll
-      for (int t = 0; t < kC / 64; ++t) Fw[k * kC + lane + 64 * t] = (elem_t)f[lane + 64 * t];
+      for (int t = 0; t < kC / 64; ++t) Fw[k * kC + lane + 64 * t] = (elem_t)relu(f[lane + 64 * t]);   // ReLU outputs
     }
     if constexpr (WITH_G) {
       if (a.ain != nullptr) {
@@ -180,7 +181,7 @@ __device__ __forceinline__ void stage_features(const CriticArgs& a, int tile, in
         }
       } else {
 #pragma unroll
-        for (int t = 0; t < kH / 64; ++t) Gw[k * kH + lane + 64 * t] = a.G[static_cast<int64_t>(b) * kH + lane + 64 * t];
+        for (int t = 0; t < kH / 64; ++t) Gw[k * kH + lane + 64 * t] = relu(a.G[static_cast<int64_t>(b) * kH + lane + 64 * t]);
       }
     }
   }
@@ -302,12 +303,17 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
     if (TRAINM)
       *reinterpret_cast<frag8*>(bp(a.acts.cos) + static_cast<size_t>(grow) * kNcos + ks * 16 + 8 * h) = cx[ks];
   }
+  // BF: the bf16 build's bias-first accumulators (the bias is the MFMA's initial value, no epilogue add)
+  // and ReLU on the packed operands (relu_packed) in the modes that keep no f32 activation; TRAIN keeps
+  // the bias-after form its part B recomputes bit for bit. F and G are ReLU outputs (>= 0), so
+  // relu(F c) = F relu(c) and relu(round(x)) = round(relu(x)): the same operands either way.
+  constexpr bool BF = kBiasFirst && !TRAINM;
   frag8 cpk[16], hpk[16];
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     f32x16 acc0[4];
 #pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) acc0[q4] = f32x16{};
+    for (int q4 = 0; q4 < 4; ++q4) acc0[q4] = BF ? bias_nat(L.bc, half * 4 + q4, h) : f32x16{};
 #pragma unroll
     for (int ks = 0; ks < kNcos / 16; ++ks) {
 #pragma unroll
@@ -318,18 +324,30 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
       const int mb = half * 4 + q4;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        float hv[8];
+        if constexpr (BF) {
+          frag8 cp, hp;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int m = feat(mb, 8 * s + j, h);
-          float x = acc0[q4][8 * s + j] + L.bc[m];
-          x = relu(x);
-          cpk[mb * 2 + s][j] = (elem_t)x;
-          hv[j] = static_cast<float>(Fb[m]) * x;
-          hpk[mb * 2 + s][j] = (elem_t)hv[j];
+          for (int j = 0; j < 8; ++j) {
+            const float x = acc0[q4][8 * s + j];
+            cp[j] = (elem_t)x;
+            hp[j] = (elem_t)(static_cast<float>(Fb[feat(mb, 8 * s + j, h)]) * x);
+          }
+          cpk[mb * 2 + s] = relu_packed(cp);
+          hpk[mb * 2 + s] = relu_packed(hp);
+        } else {
+          float hv[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int m = feat(mb, 8 * s + j, h);
+            float x = acc0[q4][8 * s + j] + L.bc[m];
+            x = relu(x);
+            cpk[mb * 2 + s][j] = (elem_t)x;
+            hv[j] = static_cast<float>(Fb[m]) * x;
+            hpk[mb * 2 + s][j] = (elem_t)hv[j];
+          }
+          if (TRAINM)
+            store16(bp(a.acts.h0) + static_cast<size_t>(grow) * kC + mb * 32 + 16 * s, hv, h);
         }
-        if (TRAINM)
-          store16(bp(a.acts.h0) + static_cast<size_t>(grow) * kC + mb * 32 + 16 * s, hv, h);
       }
     }
   }
@@ -337,7 +355,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
   // ---------------- layer 1: h1 = relu(W1 h0 + b1), h1g = h1 * G[b]
   f32x16 acc1[4];
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb) acc1[mb] = f32x16{};
+  for (int mb = 0; mb < 4; ++mb) acc1[mb] = BF ? bias_nat(L.b1, mb, h) : f32x16{};
   mfma_wrows<kC / 16, 4, MODE != MODE_IQN_ACT>(acc1, [&](int mb, int ks) { return W1[(mb * 16 + ks) * 64 + lane]; },
                          [&](int ks) { return hpk[ks]; });
   frag8 h1pk[8], gpk[8];
@@ -345,25 +363,37 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
   for (int mb = 0; mb < 4; ++mb) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      float gv[8];
+      if constexpr (BF) {
+        frag8 hp, gp;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int m = feat(mb, 8 * s + j, h);
-        float x = acc1[mb][8 * s + j] + L.b1[m];
-        x = relu(x);
-        h1pk[mb * 2 + s][j] = (elem_t)x;
-        gv[j] = IQN ? x : x * Gb[m];   // IQN: no action features
-        gpk[mb * 2 + s][j] = (elem_t)gv[j];
+        for (int j = 0; j < 8; ++j) {
+          const float x = acc1[mb][8 * s + j];
+          hp[j] = (elem_t)x;
+          if constexpr (!IQN) gp[j] = (elem_t)(x * Gb[feat(mb, 8 * s + j, h)]);
+        }
+        h1pk[mb * 2 + s] = relu_packed(hp);
+        gpk[mb * 2 + s] = IQN ? h1pk[mb * 2 + s] : relu_packed(gp);   // IQN: no action features
+      } else {
+        float gv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int m = feat(mb, 8 * s + j, h);
+          float x = acc1[mb][8 * s + j] + L.b1[m];
+          x = relu(x);
+          h1pk[mb * 2 + s][j] = (elem_t)x;
+          gv[j] = IQN ? x : x * Gb[m];   // IQN: no action features
+          gpk[mb * 2 + s][j] = (elem_t)gv[j];
+        }
+        if (TRAINM)
+          store16(bp(a.acts.h1g) + static_cast<size_t>(grow) * kH + mb * 32 + 16 * s, gv, h);
       }
-      if (TRAINM)
-        store16(bp(a.acts.h1g) + static_cast<size_t>(grow) * kH + mb * 32 + 16 * s, gv, h);
     }
   }
 
   // ---------------- layer 2: h2 = relu(W2 h1g + b2), q = wo . h2 + bo
   f32x16 acc2[4];
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb) acc2[mb] = f32x16{};
+  for (int mb = 0; mb < 4; ++mb) acc2[mb] = BF ? bias_nat(L.b2, mb, h) : f32x16{};
   mfma_wrows<kH / 16, 4, MODE != MODE_IQN_ACT>(acc2, [&](int mb, int ks) { return W2[(mb * 8 + ks) * 64 + lane]; },
                          [&](int ks) { return gpk[ks]; });
   float q;
@@ -375,7 +405,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
     for (int mb = 0; mb < 4; ++mb) {
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
-        const float x = acc2[mb][g] + L.b2[feat(mb, g, h)];
+        const float x = BF ? acc2[mb][g] : acc2[mb][g] + L.b2[feat(mb, g, h)];
         acc2[mb][g] = x;  // keep z2 for the relu mask
         h2pk[mb * 2 + (g >> 3)][g & 7] = (elem_t)relu(x);
       }
@@ -413,7 +443,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const int m = feat(mb, g, h);
-        float x = acc2[mb][g] + L.b2[m];
+        float x = BF ? acc2[mb][g] : acc2[mb][g] + L.b2[m];
         acc2[mb][g] = x;  // keep z2 for the relu mask
         part += L.wo[m] * relu(x);
       }

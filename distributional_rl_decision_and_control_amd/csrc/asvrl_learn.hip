@@ -181,76 +181,87 @@ __global__ __launch_bounds__(kC51Waves * kWave) void c51_kernel(const float* __r
 // ------------------------------------------------------------------ replay ring
 constexpr int kPushBlock = 256;
 
-__global__ __launch_bounds__(kPushBlock) void replay_count_kernel(const int8_t* __restrict__ cnt, int n,
-                                                                  int* __restrict__ work) {
-  __shared__ int sh[kPushBlock / kWave];
-  const int k = blockIdx.x * kPushBlock + threadIdx.x;
-  const bool v = k < n && cnt[k] >= 0;
-  const unsigned long long bal = __ballot(v);
-  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = __popcll(bal);
+__device__ __forceinline__ int block_sum(int v, int* sh) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int t = 0;
-    for (int w = 0; w < kPushBlock / kWave; ++w) t += sh[w];
-    work[blockIdx.x] = t;
-  }
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  int t = 0;
+  for (int w = 0; w < kPushBlock / kWave; ++w) t += sh[w];
+  return t;
 }
 
-__global__ __launch_bounds__(kPushBlock) void replay_write_kernel(
+// rows of cnt[0, lim) that push (obj_cnt >= 0), counted by the whole block: four flags per 32-bit load
+// when cnt is 4-byte aligned
+__device__ __forceinline__ int count_pushed(const int8_t* __restrict__ cnt, int lim, int* sh) {
+  int c = 0;
+  if ((reinterpret_cast<uintptr_t>(cnt) & 3) == 0) {
+    const uint32_t* c4 = reinterpret_cast<const uint32_t*>(cnt);
+    for (int q = threadIdx.x; q < lim / 4; q += kPushBlock) c += 4 - __popc(c4[q] & 0x80808080u);
+    for (int k = (lim / 4) * 4 + threadIdx.x; k < lim; k += kPushBlock) c += cnt[k] >= 0 ? 1 : 0;
+  } else {
+    for (int k = threadIdx.x; k < lim; k += kPushBlock) c += cnt[k] >= 0 ? 1 : 0;
+  }
+  return block_sum(c, sh);
+}
+
+// ReplayBuffer.add for every robot that acted (trainer.py:163-166) in ONE launch: block b's first slot
+// follows the rows of the earlier blocks that push (counted by the block itself from the L2-resident
+// flags: the row order of the deque, deterministic); the last block to arrive (a counter it resets)
+// advances {head, size} and, when asked, copies the new state to `snap` (the ring snapshot the next learn
+// step samples against) and increments `counter_inc` (the env step counter).
+__global__ __launch_bounds__(kPushBlock) void replay_push_kernel(
     const float* __restrict__ obs_prev, const float* __restrict__ obs_next, const int8_t* __restrict__ cnt,
-    const double* __restrict__ actions, int adim, const double* __restrict__ reward,
-    const uint8_t* __restrict__ done, int n, float* __restrict__ ring, int64_t cap,
-    const int64_t* __restrict__ ring_state, int* __restrict__ work, int nblocks) {
-  __shared__ int sh[kPushBlock / kWave];
-  __shared__ int s_off, s_tot;
-  // block offset = sum of earlier blocks' counts (deterministic slot order)
-  int before = 0, total = 0;
-  for (int k = threadIdx.x; k < nblocks; k += kPushBlock) {
-    const int c = work[k];
-    total += c;
-    if (k < static_cast<int>(blockIdx.x)) before += c;
-  }
-  for (int off = 32; off > 0; off >>= 1) {
-    before += __shfl_xor(before, off, kWave);
-    total += __shfl_xor(total, off, kWave);
-  }
-  if (threadIdx.x == 0) { s_off = 0; s_tot = 0; }
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) {
-    atomicAdd(&s_off, before);
-    atomicAdd(&s_tot, total);
-  }
+    const double* __restrict__ actions, int adim, int64_t ald, const double* __restrict__ reward,
+    const uint8_t* __restrict__ done, int n, float* __restrict__ ring, int64_t cap, int64_t* ring_state,
+    int* arrive, int nblocks, int64_t* snap, int64_t* counter_inc) {
+  __shared__ int sh[kPushBlock / kWave], shw[kPushBlock / kWave];
+  __shared__ int s_last;
+  const int before = count_pushed(cnt, static_cast<int>(blockIdx.x) * kPushBlock, sh);
   const int k = blockIdx.x * kPushBlock + threadIdx.x;
   const bool v = k < n && cnt[k] >= 0;
   const unsigned long long bal = __ballot(v);
   const int lane = threadIdx.x & 63;
   const int rank_in_wave = __popcll(bal & ((1ull << lane) - 1ull));
-  if (lane == 0) sh[threadIdx.x >> 6] = __popcll(bal);
+  if (lane == 0) shw[threadIdx.x >> 6] = __popcll(bal);
   __syncthreads();
   const int64_t head_in = ring_state[0];
-  if (blockIdx.x == 0 && threadIdx.x == 0) work[nblocks] = s_tot;  // for the finalize kernel
-  if (!v) return;
-  int wave_off = 0;
-  for (int w = 0; w < (threadIdx.x >> 6); ++w) wave_off += sh[w];
-  const int64_t slot = (head_in + s_off + wave_off + rank_in_wave) % cap;
-  float4* dst = reinterpret_cast<float4*>(ring + slot * ASVRL_TR_DIM);
-  const float4* a4 = reinterpret_cast<const float4*>(obs_prev + static_cast<size_t>(k) * ASVRL_OBS_DIM);
-  const float4* b4 = reinterpret_cast<const float4*>(obs_next + static_cast<size_t>(k) * ASVRL_OBS_DIM);
+  if (v) {
+    int wave_off = 0;
+    for (int w = 0; w < (threadIdx.x >> 6); ++w) wave_off += shw[w];
+    const int64_t slot = (head_in + before + wave_off + rank_in_wave) % cap;
+    float4* dst = reinterpret_cast<float4*>(ring + slot * ASVRL_TR_DIM);
+    const float4* a4 = reinterpret_cast<const float4*>(obs_prev + static_cast<size_t>(k) * ASVRL_OBS_DIM);
+    const float4* b4 = reinterpret_cast<const float4*>(obs_next + static_cast<size_t>(k) * ASVRL_OBS_DIM);
 #pragma unroll
-  for (int q = 0; q < ASVRL_OBS_DIM / 4; ++q) dst[q] = a4[q];
+    for (int q = 0; q < ASVRL_OBS_DIM / 4; ++q) dst[q] = a4[q];
 #pragma unroll
-  for (int q = 0; q < ASVRL_OBS_DIM / 4; ++q) dst[ASVRL_OBS_DIM / 4 + q] = b4[q];
-  const float a0 = static_cast<float>(actions[static_cast<size_t>(k) * adim]);
-  const float a1 = adim > 1 ? static_cast<float>(actions[static_cast<size_t>(k) * adim + 1]) : 0.f;
-  dst[2 * ASVRL_OBS_DIM / 4] = make_float4(a0, a1, static_cast<float>(reward[k]), done[k] ? 1.f : 0.f);
-  dst[2 * ASVRL_OBS_DIM / 4 + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
-}
-
-__global__ void replay_finalize_kernel(int64_t* ring_state, const int* __restrict__ work, int nblocks, int64_t cap) {
-  const int64_t tot = work[nblocks];
-  ring_state[0] = (ring_state[0] + tot) % cap;
-  const int64_t ns = ring_state[1] + tot;
-  ring_state[1] = ns < cap ? ns : cap;
+    for (int q = 0; q < ASVRL_OBS_DIM / 4; ++q) dst[ASVRL_OBS_DIM / 4 + q] = b4[q];
+    const float a0 = static_cast<float>(actions[k * ald]);
+    const float a1 = adim > 1 ? static_cast<float>(actions[k * ald + 1]) : 0.f;
+    dst[2 * ASVRL_OBS_DIM / 4] = make_float4(a0, a1, static_cast<float>(reward[k]), done[k] ? 1.f : 0.f);
+    dst[2 * ASVRL_OBS_DIM / 4 + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();   // every lane's read of ring_state is done before the block arrives
+  if (threadIdx.x == 0) {
+    __threadfence();
+    s_last = atomicAdd(arrive, 1) == nblocks - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  const int tot = count_pushed(cnt, n, sh);
+  if (threadIdx.x == 0) {
+    const int64_t nh = (head_in + tot) % cap, ns0 = ring_state[1] + tot;
+    const int64_t ns = ns0 < cap ? ns0 : cap;
+    ring_state[0] = nh;
+    ring_state[1] = ns;
+    if (snap != nullptr) {
+      snap[0] = nh;
+      snap[1] = ns;
+    }
+    if (counter_inc != nullptr) *counter_inc += 1;
+    *arrive = 0;
+  }
 }
 
 // one wave per sampled row, 22 lanes x float4
@@ -267,43 +278,11 @@ __global__ __launch_bounds__(4 * kWave) void replay_sample_kernel(const float* _
   if (b >= B) return;
   const int64_t head = ring_state[0];
   const int64_t size = ring_state[1];
-  int64_t k;
-  if (indices != nullptr) {
-    k = indices[b];
-  } else {
-    const uint64_t ctr = counter + (counter_dev != nullptr ? *counter_dev : 0ull);
-    const U4 r = philox4x32_10(U4{static_cast<uint32_t>(b), 0x5A3Bu, static_cast<uint32_t>(ctr >> 32),
-                                  static_cast<uint32_t>(ctr)},
-                               static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
-    const uint64_t bits = (static_cast<uint64_t>(r.x) << 32) | r.y;
-    // guard: skip the oldest entries a concurrent push of <= guard rows may overwrite
-    int64_t lo = size + guard - cap;
-    lo = lo > 0 ? lo : 0;
-    if (lo >= size) lo = 0;
-    k = size > 0 ? lo + static_cast<int64_t>(bits % static_cast<uint64_t>(size - lo)) : 0;
-  }
-  const int64_t slot = ((head - size + k) % cap + cap) % cap;  // deque index 0 = oldest
+  const uint64_t ctr = counter + (counter_dev != nullptr ? *counter_dev : 0ull);
+  const int64_t slot = indices != nullptr ? ((head - size + indices[b]) % cap + cap) % cap
+                                          : replay_draw_slot(head, size, cap, guard, b, seed, ctr);
   if (lane == 0 && out_slots != nullptr) out_slots[b] = slot;
-  if (taus != nullptr) {
-    // the update's quantile fractions tau ~ U[0, 1) (AC_IQN_model.py:419, torch.rand), tau_sets sets of
-    // [B][tau_n] drawn here so the learner needs no RNG launch: Philox(seed, step) per (row, set, 4 taus)
-    const uint64_t ctr = counter + (counter_dev != nullptr ? *counter_dev : 0ull);
-    const int per_row = tau_sets * tau_n;
-    for (int k0 = 4 * lane; k0 < per_row; k0 += 4 * kWave) {
-      const U4 r = philox4x32_10(U4{static_cast<uint32_t>(b), static_cast<uint32_t>(k0) ^ 0x7A0000u,
-                                    static_cast<uint32_t>(ctr >> 32), static_cast<uint32_t>(ctr)},
-                                 static_cast<uint32_t>(seed) ^ 0x51EDu, static_cast<uint32_t>(seed >> 32));
-      const uint32_t w[4] = {r.x, r.y, r.z, r.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = k0 + j;
-        if (k < per_row) {
-          const int set = k / tau_n, t = k - set * tau_n;
-          taus[(static_cast<size_t>(set) * B + b) * tau_n + t] = static_cast<float>(w[j] >> 8) * (1.0f / 16777216.0f);
-        }
-      }
-    }
-  }
+  if (taus != nullptr) replay_draw_taus(b, lane, B, seed, ctr, taus, tau_sets, tau_n);
   if (lane < ASVRL_TR_DIM / 4) {
     const float4* src = reinterpret_cast<const float4*>(ring + slot * ASVRL_TR_DIM);
     reinterpret_cast<float4*>(out + static_cast<size_t>(b) * ASVRL_TR_DIM)[lane] = src[lane];
@@ -365,23 +344,31 @@ extern "C" int asvrl_c51_project(const float* pns_a, const float* returns, const
   return check_launch("asvrl_c51_project");
 }
 
-extern "C" int asvrl_replay_push(const float* obs_prev, const float* obs_next, const int8_t* obj_cnt_next,
-                                 const double* actions, int32_t action_dim, const double* reward,
-                                 const uint8_t* done, int32_t n, float* ring, int64_t capacity,
-                                 int64_t* ring_state, int32_t* work, void* stream) {
+extern "C" int asvrl_replay_push_ex(const float* obs_prev, const float* obs_next, const int8_t* obj_cnt_next,
+                                    const double* actions, int32_t action_dim, int64_t action_ld,
+                                    const double* reward,
+                                    const uint8_t* done, int32_t n, float* ring, int64_t capacity,
+                                    int64_t* ring_state, int32_t* work, int64_t* snap, int64_t* counter_inc,
+                                    void* stream) {
   ASVRL_REQUIRE(obs_prev && obs_next && obj_cnt_next && actions && reward && done && ring && ring_state && work,
                 "asvrl_replay_push: null argument");
   ASVRL_REQUIRE(capacity >= n && capacity > 0, "asvrl_replay_push: capacity smaller than one push");
   ASVRL_REQUIRE(action_dim == 1 || action_dim == 2, "asvrl_replay_push: action_dim must be 1 or 2");
+  ASVRL_REQUIRE(action_ld >= action_dim, "asvrl_replay_push: action row stride below action_dim");
   if (n <= 0) return 0;
   const int nb = (n + kPushBlock - 1) / kPushBlock;
-  hipLaunchKernelGGL(replay_count_kernel, dim3(nb), dim3(kPushBlock), 0, as_stream(stream), obj_cnt_next, n, work);
-  if (int rc = check_launch("asvrl_replay_push(count)")) return rc;
-  hipLaunchKernelGGL(replay_write_kernel, dim3(nb), dim3(kPushBlock), 0, as_stream(stream), obs_prev, obs_next,
-                     obj_cnt_next, actions, action_dim, reward, done, n, ring, capacity, ring_state, work, nb);
-  if (int rc = check_launch("asvrl_replay_push(write)")) return rc;
-  hipLaunchKernelGGL(replay_finalize_kernel, dim3(1), dim3(1), 0, as_stream(stream), ring_state, work, nb, capacity);
-  return check_launch("asvrl_replay_push(finalize)");
+  hipLaunchKernelGGL(replay_push_kernel, dim3(nb), dim3(kPushBlock), 0, as_stream(stream), obs_prev, obs_next,
+                     obj_cnt_next, actions, action_dim, action_ld, reward, done, n, ring, capacity, ring_state, work, nb, snap,
+                     counter_inc);
+  return check_launch("asvrl_replay_push");
+}
+
+extern "C" int asvrl_replay_push(const float* obs_prev, const float* obs_next, const int8_t* obj_cnt_next,
+                                 const double* actions, int32_t action_dim, const double* reward,
+                                 const uint8_t* done, int32_t n, float* ring, int64_t capacity,
+                                 int64_t* ring_state, int32_t* work, void* stream) {
+  return asvrl_replay_push_ex(obs_prev, obs_next, obj_cnt_next, actions, action_dim, action_dim, reward, done, n, ring, capacity,
+                              ring_state, work, nullptr, nullptr, stream);
 }
 
 extern "C" int asvrl_replay_sample(const float* ring, int64_t capacity, const int64_t* ring_state,

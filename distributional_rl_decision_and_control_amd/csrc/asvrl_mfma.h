@@ -158,6 +158,36 @@ __device__ __forceinline__ float cos_pi_k_tau(float tau, int k) {
 
 __device__ __forceinline__ float relu(float x) { return fmaxf(x, 0.f); }
 
+// ReLU of 8 operand-typed values. bf16: a signed 16-bit max against 0 per half-word (v_pk_max_i16, two
+// values per instruction): a bf16's sign is its int16 sign, so negatives and -0 become +0 and the rest
+// stay, i.e. relu(round(x)) == round(relu(x)) bit for bit.
+__device__ __forceinline__ frag8 relu_packed(frag8 v) {
+#if ASVRL_OPERAND_F32
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+  return v;
+#else
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 u = __builtin_elementwise_max(__builtin_bit_cast(s16x8, v), s16x8{});
+  return __builtin_bit_cast(frag8, u);
+#endif
+}
+
+// f32 accumulator of one 32-feature block initialised with the block's bias (natural feature order:
+// register g of lane half h holds feature feat(mb, g, h), i.e. 4 consecutive biases per 16-byte load)
+__device__ __forceinline__ f32x16 bias_nat(const float* b, int mb, int h) {
+  f32x16 acc;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 v = *reinterpret_cast<const float4*>(b + mb * 32 + 8 * q + 4 * h);
+    acc[4 * q] = v.x;
+    acc[4 * q + 1] = v.y;
+    acc[4 * q + 2] = v.z;
+    acc[4 * q + 3] = v.w;
+  }
+  return acc;
+}
+
 // store of 4 consecutive features
 __device__ __forceinline__ void store4(elem_t* base, const float* v) {
   elem4 x;

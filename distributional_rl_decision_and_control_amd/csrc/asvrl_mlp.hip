@@ -343,19 +343,21 @@ struct ActorSplitLds {
   float part[kMlpWaves][32][2];
 };
 
+// One 32-row tile of the split Actor (4 waves): rows tile * 32 + r of the outputs; the observation of
+// row r read from x + (xrow0 + r) * ldx (the global rows, or rows staged in LDS by the fused prologue).
 template <int MODE>
-__global__ __launch_bounds__(kMlpWaves * 64) void actor_split_kernel(MlpArgs a) {
-  __shared__ __attribute__((aligned(16))) ActorSplitLds L;
+__device__ __forceinline__ void actor_split_tile(const MlpArgs& a, ActorSplitLds& L, int tile, const float* x,
+                                                 int64_t ldx, int xrow0) {
   const AsvMlpIO& io = a.io;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
-  const int row = blockIdx.x * 32 + r;
+  const int row = tile * 32 + r;
   const bool valid = row < io.n;
   const int rr = valid ? row : io.n - 1;
   // ---------------- encoders (wave w: blocks 2w, 2w + 1) -> h0
   {
     frag8 bx[2];
     float mk[kObjN];
-    load_obs(io.x, io.ldx, rr, h, bx, mk);
+    load_obs(x, ldx, xrow0 + (rr - tile * 32), h, bx, mk);
     if (MODE == MLP_TRAIN && w == 0 && valid) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
@@ -449,6 +451,74 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_split_kernel(MlpArgs a) 
     io.pre[static_cast<int64_t>(row) * 2] = z0;
     io.pre[static_cast<int64_t>(row) * 2 + 1] = z1;
   }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kMlpWaves * 64) void actor_split_kernel(MlpArgs a) {
+  __shared__ __attribute__((aligned(16))) ActorSplitLds L;
+  actor_split_tile<MODE>(a, L, blockIdx.x, a.io.x, a.io.ldx, blockIdx.x * 32);
+}
+
+// ------------------------------------------------------------------ fused learn prologue (AC-IQN)
+// asvrl_replay_sample (B rows + the update's taus) + the local Actor's TRAIN forward on s
+// (agent.py:419-421) + the target Actor's FWD on s' (agent.py:397-398) in ONE launch of 2 * B / 32
+// workgroups: workgroup t < T draws samples 32 t .. 32 t + 31 (the same Philox draws as
+// replay_sample_kernel), writes their rows and taus, and runs the TRAIN tile on the observations it
+// staged in LDS; workgroup T + t draws the same samples, stages their next observations and runs the
+// target FWD tile into na. Results are bit-identical to the three launches.
+struct PrologueArgs {
+  const float* ring;
+  int64_t cap;
+  const int64_t* ring_state;
+  uint64_t seed, counter;
+  const uint64_t* counter_dev;
+  int64_t guard;
+  int B, tau_sets, tau_n;
+  float* out;
+  float* taus;
+};
+
+__global__ __launch_bounds__(kMlpWaves * 64) void learn_prologue_kernel(PrologueArgs p, MlpArgs train, MlpArgs tgt) {
+  __shared__ __attribute__((aligned(16))) ActorSplitLds L;
+  __shared__ __attribute__((aligned(16))) float xs[32 * ASVRL_OBS_DIM];   // the tile's 32 observation rows
+  const int T = p.B / 32;
+  const bool second = static_cast<int>(blockIdx.x) >= T;
+  const int tile = second ? blockIdx.x - T : blockIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t head = p.ring_state[0], size = p.ring_state[1];
+  const uint64_t ctr = p.counter + (p.counter_dev != nullptr ? *p.counter_dev : 0ull);
+  // wave w gathers samples 8w .. 8w + 7 of the tile: the whole row to `out` (first half), the observation
+  // (s, or s' for the second half) into LDS. Lanes 0..7 draw the eight slots at once; every row piece
+  // (one float4 per lane) is loaded before any store, so the eight HBM reads are in flight together.
+  const int64_t my_slot = replay_draw_slot(head, size, p.cap, p.guard, tile * 32 + 8 * w + (lane & 7), p.seed, ctr);
+  const int slot_lo = static_cast<int>(my_slot & 0xFFFFFFFFll), slot_hi = static_cast<int>(my_slot >> 32);
+  constexpr int kRowV = ASVRL_TR_DIM / 4, kObsV = ASVRL_OBS_DIM / 4;
+  const int per = second ? kObsV : kRowV;   // float4 pieces per sample
+  float4 v[3];
+  int jj[3], cc[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int e = lane + 64 * u;
+    jj[u] = e / per;
+    cc[u] = e - jj[u] * per;
+    const int js = jj[u] < 8 ? jj[u] : 0;
+    const int64_t slot = (static_cast<int64_t>(__shfl(slot_hi, js)) << 32) |
+                         static_cast<uint32_t>(__shfl(slot_lo, js));
+    if (jj[u] < 8)
+      v[u] = reinterpret_cast<const float4*>(p.ring + slot * ASVRL_TR_DIM)[(second ? kObsV : 0) + cc[u]];
+  }
+  if (!second && p.taus != nullptr)
+    for (int j = 0; j < 8; ++j) replay_draw_taus(tile * 32 + 8 * w + j, lane, p.B, p.seed, ctr, p.taus, p.tau_sets, p.tau_n);
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    if (jj[u] >= 8) continue;
+    const int lr = 8 * w + jj[u], b = tile * 32 + lr;
+    if (!second) reinterpret_cast<float4*>(p.out + static_cast<size_t>(b) * ASVRL_TR_DIM)[cc[u]] = v[u];
+    if (cc[u] < kObsV) reinterpret_cast<float4*>(xs + lr * ASVRL_OBS_DIM)[cc[u]] = v[u];
+  }
+  __syncthreads();
+  if (!second) actor_split_tile<MLP_TRAIN>(train, L, tile, xs, ASVRL_OBS_DIM, 0);
+  else actor_split_tile<MLP_FWD>(tgt, L, tile, xs, ASVRL_OBS_DIM, 0);
 }
 
 // The backward in the same split: dz2 (block w) from dA, dz1 = W2^T dz2 (block w), dz0 = W1^T dz1
@@ -682,6 +752,30 @@ extern "C" int asvrl_actor_forward(const AsvMlpWeights* w, const AsvMlpIO* io, i
     hipLaunchKernelGGL(actor_kernel<MLP_ACT>, dim3((tiles + kMlpWaves - 1) / kMlpWaves), block, 0, st, a);
   }
   return check_launch("asvrl_actor_forward");
+}
+
+extern "C" int asvrl_learn_prologue(const AsvSampleArgs* s, const AsvMlpWeights* actor, const AsvMlpIO* train_io,
+                                    const AsvMlpWeights* target_actor, float* na, void* stream) {
+  ASVRL_REQUIRE(s && actor && train_io && target_actor && na && s->ring && s->ring_state && s->out,
+                "asvrl_learn_prologue: null argument");
+  ASVRL_REQUIRE(s->capacity > 0 && s->B > 0 && s->B % 32 == 0, "asvrl_learn_prologue: B must be a positive multiple of 32");
+  ASVRL_REQUIRE(s->taus == nullptr || (s->tau_sets >= 1 && s->tau_n >= 1), "asvrl_learn_prologue: bad tau shape");
+  ASVRL_REQUIRE(train_io->n == s->B && train_io->a_out && train_io->xb && train_io->h0 && train_io->h1 && train_io->h2 &&
+                    train_io->pre, "asvrl_learn_prologue: the TRAIN outputs (n = B, a_out, xb, h0, h1, h2, pre)");
+  for (const AsvMlpWeights* w : {actor, target_actor})
+    ASVRL_REQUIRE(w->enc_frag && w->w1_frag && w->w2_frag && w->b1 && w->b2 && w->wout && w->bout,
+                  "asvrl_learn_prologue: null actor weight");
+  PrologueArgs p{s->ring, s->capacity, s->ring_state, s->seed, s->counter, s->counter_dev, s->guard,
+                 s->B, s->tau_sets, s->tau_n, s->out, s->taus};
+  MlpArgs tr{*actor, *train_io};
+  AsvMlpIO fio{};
+  fio.n = s->B;
+  fio.a_out = na;
+  fio.ld_aout = 2;
+  MlpArgs tg{*target_actor, fio};
+  hipLaunchKernelGGL(learn_prologue_kernel, dim3(2 * (s->B / 32)), dim3(kMlpWaves * 64), 0, as_stream(stream), p, tr,
+                     tg);
+  return check_launch("asvrl_learn_prologue");
 }
 
 extern "C" int asvrl_actor_backward(const AsvMlpWeights* w, const AsvMlpIO* io, void* stream) {

@@ -1,5 +1,6 @@
 """The whole AC-IQN update (Agent.train_AC_IQN, agent.py:386-432) on hand-written gfx950
-kernels: about 16 launches per step, no torch autograd, no host synchronisation.
+kernels: ten launches per step (with the vectorised loop's fused prologue), no torch autograd, no host
+synchronisation.
 
 Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | done):
   actor(s) saving activations -> a (for the actor step)  asvrl_actor_forward(TRAIN)
@@ -29,6 +30,8 @@ other stream is the rollout's, vec_trainer.py).
 Arithmetic: bf16 MFMA operands with f32 accumulation everywhere, f32 master weights / Adam
 (operands="f32": the same kernels from libasvrl_f32.so, the parity build).
 """
+import ctypes as C
+
 import torch
 
 from . import _abi
@@ -92,8 +95,9 @@ def _reduce_and_step(arena, opt, grads, sync, max_norm, wait=None, pack=None, co
     """Reduce the queued weight-gradient partials, then clip + Adam. Single process with the
     fused optimiser: the reduction launch also forms the gradient norm and the Adam launch writes the
     weight images of `pack` (a CriticPack / MlpPack / IqnPack) and increments `counter` (two launches
-    in all); otherwise reduce, all-reduce (sync), asvrl_adam_clip, then pack.refresh() and
-    counter += 1. `wait`: an event to wait for before the parameters change."""
+    in all; one persistent launch with a grid barrier between the two was measured slower, DESIGN.md 6);
+    otherwise reduce, all-reduce (sync), asvrl_adam_clip, then pack.refresh() and counter += 1.
+    `wait`: an event to wait for before the parameters change."""
     assert pack is None or not isinstance(opt, FusedAdam) or opt.L is pack.L, "optimiser and pack of different builds"
     if sync is None and isinstance(opt, FusedAdam):
         arena.flush(norm=opt)
@@ -128,12 +132,35 @@ def target_q(st, rows, tau0, q_out, na):
     critic_forward(st.target_trunk, None, None, tau0, st.N, q=q_out, obs=ns_rows, act=na)
 
 
+def learn_prologue(st, replay, taus, seed, counter_dev=None, counter=0, out=None, state=None, guard=0, stream=None):
+    """asvrl_learn_prologue: B rows drawn from the device ring (replay_buffer.py:26-45) with the update's
+    quantile fractions `taus` (3, B, N), the local actor's TRAIN forward on s (its activations in st.abufs)
+    and the target actor's forward on s' (st.na) in ONE launch, bit-identical to replay.sample +
+    actor_train_forward + actor_forward. Returns the rows [B][88]."""
+    B = st.B
+    out = out if out is not None else torch.empty((B, 88), dtype=torch.float32, device=st.device)
+    assert taus.is_contiguous() and taus.shape[1] == B and taus.dtype == torch.float32
+    sa = _abi.AsvSampleArgs()
+    sa.ring, sa.capacity = replay.ring.data_ptr(), replay.capacity
+    sa.ring_state = (state if state is not None else replay.state).data_ptr()
+    sa.seed, sa.counter = int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter) & 0xFFFFFFFFFFFFFFFF
+    sa.counter_dev = _abi.ptr(counter_dev)
+    sa.guard, sa.B, sa.tau_sets, sa.tau_n = int(guard), B, taus.shape[0], taus.shape[2]
+    sa.out, sa.taus = out.data_ptr(), taus.data_ptr()
+    io = st.abufs.io()
+    _abi.check(st.actor.L.asvrl_learn_prologue(C.byref(sa), C.byref(st.actor.w), C.byref(io),
+                                                C.byref(st.target_actor.w), st.na.data_ptr(),
+                                                _abi.stream_ptr(stream)), "asvrl_learn_prologue", st.actor.L)
+    return out
+
+
 def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, actor_grads, rows, gamma=0.99,
-                         taus=None, sync=None, max_norm=0.5, actor_wait=None, counter=None):
+                         taus=None, sync=None, max_norm=0.5, actor_wait=None, counter=None, prologue_done=False):
     """One AC-IQN update from replay rows [B][88]. taus: (3, B, N) or None (drawn here).
     actor_wait: event to wait for before the actor's weights change (a concurrent act kernel).
     counter: an int64 device scalar incremented after the step (the learn counter; in-kernel when
-    the optimiser step is fused).
+    the optimiser step is fused). prologue_done: learn_prologue already ran the actor's TRAIN forward and
+    the target actor on these rows.
     Returns (critic_loss, actor_loss, critic_grad_norm, actor_grad_norm) as device scalars."""
     B, N = st.B, st.N
     critic, actor = policy_local.critic, policy_local.actor
@@ -145,9 +172,12 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
 
     # ---- critic (agent.py:395-416); every critic .grad is overwritten below (no zeroing). The
     # trunk kernels run the critic's observation / action encoders on the replay rows themselves.
-    actor_train_forward(st.actor, s_rows, ab)   # reads only s and the (not yet updated) actor
     q_next = st.q_next
-    target_q(st, rows, taus[0], q_next, st.na)
+    if prologue_done:   # only the target critic is left of the target chain
+        critic_forward(st.target_trunk, None, None, taus[0], st.N, q=q_next, obs=rows[:, OBS:2 * OBS], act=st.na)
+    else:
+        actor_train_forward(st.actor, s_rows, ab)   # reads only s and the (not yet updated) actor
+        target_q(st, rows, taus[0], q_next, st.na)
     ae = critic.action_encoder[0]
     # forward, loss, backward and the weight-gradient partials of the four trunk layers and the three
     # encoders in one launch (supported() guarantees its shape: B a multiple of 32, so B*N of 64)

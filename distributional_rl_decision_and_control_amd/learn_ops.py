@@ -82,15 +82,25 @@ class DeviceReplay:
         self._work = None
         self._n_host = 0  # host mirror for the compat path (exact when fed by add())
 
-    def push(self, obs_prev, obs_next, obj_cnt_next, actions, reward, done, stream=None):
+    def push(self, obs_prev, obs_next, obj_cnt_next, actions, reward, done, stream=None, snap=None,
+             counter_inc=None):
+        """ReplayBuffer.add of every row whose obj_cnt_next >= 0, in row order, in one launch. actions:
+        [n, >= 1] f64 rows (the first 1 or 2 columns are stored, any row stride); snap: an int64[2] that
+        receives the new {head, size}; counter_inc: an int64 device counter incremented by the launch."""
         n = obs_prev.shape[0]
         if self._work is None or self._work.numel() < (n + 255) // 256 + 1:
             self._work = torch.zeros((n + 255) // 256 + 1, dtype=torch.int32, device=self.device)
-        adim = actions.shape[1] if actions.dim() == 2 else 1
-        rc = _abi.lib().asvrl_replay_push(_abi.ptr(obs_prev), _abi.ptr(obs_next), _abi.ptr(obj_cnt_next),
-                                          _abi.ptr(actions), adim, _abi.ptr(reward), _abi.ptr(done), n,
-                                          _abi.ptr(self.ring), self.capacity, _abi.ptr(self.state),
-                                          _abi.ptr(self._work), _abi.stream_ptr(stream))
+        if actions.dim() == 1:
+            adim, ald = 1, 1
+        else:
+            assert actions.stride(1) == 1, "action rows must be contiguous"
+            adim, ald = min(actions.shape[1], 2), actions.stride(0)
+        assert actions.dtype == torch.float64 and reward.dtype == torch.float64
+        rc = _abi.lib().asvrl_replay_push_ex(_abi.ptr(obs_prev), _abi.ptr(obs_next), _abi.ptr(obj_cnt_next),
+                                             _abi.ptr(actions), adim, ald, _abi.ptr(reward), _abi.ptr(done), n,
+                                             _abi.ptr(self.ring), self.capacity, _abi.ptr(self.state),
+                                             _abi.ptr(self._work), _abi.ptr(snap), _abi.ptr(counter_inc),
+                                             _abi.stream_ptr(stream))
         _abi.check(rc, "asvrl_replay_push")
 
     def write_rows(self, rows, slots, stream=None):

@@ -38,23 +38,27 @@ class VecMarineNavEnv:
         self.counter = torch.zeros(1, dtype=torch.int64, device=self.device)  # steps taken (device)
         self.total_timesteps = 0
 
-    # obs[0] is the state the agent acts on, obs[1] receives the next state; advance_device()
-    # copies 1 -> 0 so a captured HIP graph always sees the same buffers.
+    # obs[p] is the state the agent acts on and obs[1 - p] receives the next state. advance_device()
+    # flips the parity p (swap=True: no copy; a captured HIP graph of an EVEN number of iterations then
+    # ends on the parity it started from) or copies 1 -> 0 (swap=False: any graph sees the same buffers).
+    swap = False
+    _p = 0
+
     @property
     def obs_cur(self):
-        return self.obs[0]
+        return self.obs[self._p]
 
     @property
     def cnt_cur(self):
-        return self.cnt[0]
+        return self.cnt[self._p]
 
     @property
     def obs_next(self):
-        return self.obs[1]
+        return self.obs[1 - self._p]
 
     @property
     def cnt_next(self):
-        return self.cnt[1]
+        return self.cnt[1 - self._p]
 
     def apply_schedule(self, total_timesteps):
         """Curriculum stage for the next resets (env.py:75-94)."""
@@ -81,17 +85,24 @@ class VecMarineNavEnv:
                         counter=0, counter_dev=self.counter, gamma=self.gamma, obs=self.obs_next,
                         obj_cnt=self.cnt_next, fast_noise=True)   # f32 Philox draws (noise_mode 2)
 
-    def auto_reset(self):
-        """Reset the envs whose episode ended in the last step and observe them into obs_next."""
+    def auto_reset(self, counted=False):
+        """Reset the envs whose episode ended in the last step and observe them into obs_next.
+        counted: the step counter was already incremented for this step (by the replay push launch);
+        the draws are keyed as if it had not been."""
         b = self.batch
-        b.reset(self.cfg, b.env_done, seed=self.seed, counter=0x40000000, counter_dev=self.counter)
-        b.step(None, do_dynamics=False, seed=self.seed, counter=0x80000000, counter_dev=self.counter,
+        d = 1 if counted else 0
+        b.reset(self.cfg, b.env_done, seed=self.seed, counter=0x40000000 - d, counter_dev=self.counter)
+        b.step(None, do_dynamics=False, seed=self.seed, counter=0x80000000 - d, counter_dev=self.counter,
                fast_noise=True, env_mask=b.env_done, obs=self.obs_next, obj_cnt=self.cnt_next)
 
-    def advance_device(self):
-        self.obs[0].copy_(self.obs[1])
-        self.cnt[0].copy_(self.cnt[1])
-        self.counter += 1
+    def advance_device(self, counted=False):
+        if self.swap:
+            self._p ^= 1
+        else:
+            self.obs[0].copy_(self.obs[1])
+            self.cnt[0].copy_(self.cnt[1])
+        if not counted:
+            self.counter += 1
 
     def advance_host(self):
         self.total_timesteps += self.n_envs

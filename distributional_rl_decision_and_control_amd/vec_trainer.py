@@ -21,7 +21,7 @@ import time
 import torch
 
 from . import streams
-from .fused_update import FusedACIQNState, ac_iqn_update_fused2
+from .fused_update import FusedACIQNState, ac_iqn_update_fused2, learn_prologue
 from .fused_iqn import FusedIQNState, iqn_update_fused
 from .fused_iqn import supported as fused_iqn_supported
 from .fused_rainbow import FusedRainbow
@@ -133,6 +133,9 @@ class VecTrainer:
         # calls iteration() once per iteration; every unroll-th call replays): 10 with the chained
         # schedule at the bench shape (profiles/r02_unroll_chain_ab.txt)
         self.unroll = max(1, int(unroll))
+        # observation double buffer by parity flip (no copy) unless a graph of an odd number of iterations
+        # has to find the same buffers at every replay
+        self.env.swap = not graphs or self.unroll % 2 == 0
         self._phase = 0
         self._graph_learn = None
         # rollout / learn on two streams (fused learners): the learner samples against a
@@ -178,19 +181,25 @@ class VecTrainer:
         else:   # actor on every robot row, explore
             self.fused2.act(*args)
 
-    def _push(self):
+    def _push(self, snap=None):
+        """The replay push of every robot that acted; for the uniform ring it is one launch that also
+        increments the env step counter (and writes the new ring state to `snap` when given). Returns
+        whether the counter was incremented."""
         env = self.env
         if self.per is not None:   # ReplayMemory.append of every robot that acted (trainer.py:163-164)
             self.per.push(env.obs_cur, env.cnt_next, self.actions[:, :1], env.batch.reward, env.batch.done)
-            return
-        self.replay.push(env.obs_cur, env.obs_next, env.cnt_next, self.actions[:, :self.action_dim].contiguous()
-                         if self.action_dim == 1 else self.actions, env.batch.reward, env.batch.done)
+            return False
+        self.replay.push(env.obs_cur, env.obs_next, env.cnt_next, self.actions[:, :self.action_dim],
+                         env.batch.reward, env.batch.done, snap=snap, counter_inc=env.counter)
+        return True
 
-    def rollout(self):
+    def rollout(self, snap=None):
+        """act, env step, replay push, device reset and the step counter (trainer.py:142-172)."""
         self.act()
         self.env.step(self.actions)
-        self._push()
-        self.env.auto_reset()
+        counted = self._push(snap)
+        self.env.auto_reset(counted)
+        self.env.advance_device(counted)
 
     def learn(self, state=None, guard=0, actor_wait=None):
         """One learn step of batch B: sample (uniform ring, or the prioritised tree for Rainbow) and the
@@ -206,13 +215,18 @@ class VecTrainer:
             self.per.update_priorities(idx, loss)   # update_priorities(idxs, loss) (agent.py:639)
             self.learn_counter += 1
             return loss.mean(), gn
+        if self.fused2 is not None:
+            # one launch: the draw (rows + the update's quantile fractions), the actor's training forward
+            # and the target actor
+            rows = learn_prologue(self.fused2, self.replay, self.taus, self.seed + 777, counter_dev=self.learn_counter,
+                                  out=self.batch_rows, state=state, guard=guard)
+            return ac_iqn_update_fused2(self.fused2, self.local, self.actor_opt, self.critic_opt, self.critic_grads,
+                                        self.actor_grads, rows, gamma=self.gamma, sync=self.sync,
+                                        actor_wait=actor_wait, taus=self.taus, counter=self.learn_counter,
+                                        prologue_done=True)
         # the update's quantile fractions are drawn by the sampling launch
         rows = self.replay.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter, out=self.batch_rows,
                                   state=state, guard=guard, taus=self.taus)
-        if self.fused2 is not None:
-            return ac_iqn_update_fused2(self.fused2, self.local, self.actor_opt, self.critic_opt, self.critic_grads,
-                                        self.actor_grads, rows, gamma=self.gamma, sync=self.sync,
-                                        actor_wait=actor_wait, taus=self.taus, counter=self.learn_counter)
         return iqn_update_fused(self.fused_iqn, self.local, self.opt, self.grads, rows, gamma=self.gamma,
                                 sync=self.sync, act_wait=actor_wait, taus=self.taus[:2], counter=self.learn_counter)
 
@@ -261,10 +275,9 @@ class VecTrainer:
     # ------------------------------------------------------------------ iteration
     def _iteration_body(self, do_learn):
         if not (do_learn and self.overlap and self.per is None):
+            # the learner samples after the push: only the act -> push order of rollout() matters
             self.rollout()
-            out = self.learn() if do_learn else None
-            self.env.advance_device()
-            return out
+            return self.learn() if do_learn else None
         # the learner runs on the current stream and the rollout on a side stream: HIP graph
         # capture (ROCm 7) segfaults at capture end on a stream forked from an already forked
         # stream, and the learner forks side streams of its own (fused_update.SideStreams)
@@ -282,9 +295,9 @@ class VecTrainer:
             ev_act.record(s_roll)
             env = self.env
             env.step(self.actions)
-            self._push()
-            env.auto_reset()
-            env.advance_device()
+            counted = self._push()
+            env.auto_reset(counted)
+            env.advance_device(counted)
         out = self.learn(state=self.ring_snap, guard=self.E * self.R, actor_wait=ev_act)
         main.wait_stream(s_roll)
         return out
@@ -358,11 +371,10 @@ class VecTrainer:
                 ev_act[k].record(s_roll)
                 env = self.env
                 env.step(self.actions)
-                self._push()
-                self.ring_snap2[k % 2].copy_(self.replay.state)   # what learn(k+1) samples against
+                self._push(snap=self.ring_snap2[k % 2])   # + the ring state learn(k+1) samples against
                 ev_snap[k].record(s_roll)
-                env.auto_reset()
-                env.advance_device()
+                env.auto_reset(True)
+                env.advance_device(True)
             if k > 0:
                 main.wait_event(ev_snap[k - 1])
             out = self.learn(state=self.ring_snap2[(k - 1) % 2], guard=self.E * self.R, actor_wait=ev_act[k])

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 17
+#define ASVRL_ABI_VERSION 18
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -420,11 +420,21 @@ int asvrl_iqn_act(const AsvCriticWeights* w, const AsvIqnHead* head, const AsvIq
 /* ReplayBuffer.add (replay_buffer.py:22-24) for every robot that acted in the last step
  * (obj_cnt_next >= 0), in slot order, into a ring of `capacity` rows of ASVRL_TR_DIM f32.
  * ring_state: int64[2] = {head, size} in device memory (updated by the call, so the call
- * is capturable in a HIP graph). work: int32[ceil(n / 256) + 1] scratch. */
+ * is capturable in a HIP graph). work: int32[ceil(n / 256) + 1] scratch, ZERO before the first call
+ * (work[0] is the launch's arrival counter, which the call leaves zero again). One launch. */
 int asvrl_replay_push(const float* obs_prev, const float* obs_next, const int8_t* obj_cnt_next,
                       const double* actions, int32_t action_dim, const double* reward,
                       const uint8_t* done, int32_t n, float* ring, int64_t capacity,
                       int64_t* ring_state, int32_t* work, void* stream);
+/* asvrl_replay_push with actions rows action_ld doubles apart (the first action_dim used) that also
+ * writes the new {head, size} to `snap` (int64[2], optional: the ring snapshot a concurrent learner
+ * samples against) and increments *counter_inc (optional: the env step counter), in the same launch
+ * (ABI 18). */
+int asvrl_replay_push_ex(const float* obs_prev, const float* obs_next, const int8_t* obj_cnt_next,
+                         const double* actions, int32_t action_dim, int64_t action_ld, const double* reward,
+                         const uint8_t* done, int32_t n, float* ring, int64_t capacity,
+                         int64_t* ring_state, int32_t* work, int64_t* snap, int64_t* counter_inc,
+                         void* stream);
 
 /* ReplayBuffer.sample (replay_buffer.py:26-45): gather B rows. With `indices` (host-chosen,
  * deque order: 0 = oldest) the rows are exactly those; with indices == NULL, B positions are
@@ -823,6 +833,24 @@ int asvrl_mlp_encode(const AsvMlpWeights* w, const AsvMlpIO* io, void* stream);
 /* Actor.forward (AC_IQN_model.py:310-321). mode 1 = ACT (epsilon-greedy f64 actions,
  * agent.py:207-225), 2 = FWD (f32 actions), 3 = TRAIN (f32 actions + saved activations). */
 int asvrl_actor_forward(const AsvMlpWeights* w, const AsvMlpIO* io, int32_t mode, void* stream);
+/* The AC-IQN learn step's prologue in ONE launch (ABI 18): asvrl_replay_sample's draw of B rows and
+ * their quantile fractions (uniform ring, replay_buffer.py:26-45; taus of AC_IQN_model.py:419), the local
+ * Actor's TRAIN forward on s (agent.py:419-421; outputs in train_io, n = B) and the target Actor's FWD
+ * on s' into na [B][2] (agent.py:397-398) -- bit-identical to the three separate launches. B must be a
+ * multiple of 32. */
+typedef struct AsvSampleArgs {
+  const float* ring;            /* [capacity][ASVRL_TR_DIM] */
+  int64_t capacity;
+  const int64_t* ring_state;    /* {head, size} to sample against */
+  uint64_t seed, counter;
+  const uint64_t* counter_dev;  /* optional, added to counter */
+  int64_t guard;                /* skip the oldest rows a concurrent push of <= guard rows may overwrite */
+  int32_t B, tau_sets, tau_n, _pad0;
+  float* out;                   /* [B][ASVRL_TR_DIM] sampled rows */
+  float* taus;                  /* optional [tau_sets][B][tau_n] */
+} AsvSampleArgs;
+int asvrl_learn_prologue(const AsvSampleArgs* s, const AsvMlpWeights* actor, const AsvMlpIO* train_io,
+                         const AsvMlpWeights* target_actor, float* na, void* stream);
 /* Backward of the Actor from dA to every layer's pre-activation gradient (agent.py:425). */
 int asvrl_actor_backward(const AsvMlpWeights* w, const AsvMlpIO* io, void* stream);
 /* Fold the 256 x 32 encoder-image gradient (dw, db from asvrl_linear_wgrad) back onto

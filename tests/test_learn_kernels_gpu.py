@@ -108,6 +108,51 @@ def test_replay_push_and_sample():
     assert all(r.tobytes() in hs for r in s1)
 
 
+@pytest.mark.parametrize("n,aligned,adim", [(20480, True, 2), (5003, False, 1), (255, True, 1)])
+def test_replay_push_one_launch_snapshot_and_counter(n, aligned, adim):
+    """The one-launch push (asvrl_replay_push_ex) over many workgroups: rows land in row order (the
+    deque's), the launch's arrival counter is left zero (repeated pushes stay exact), the snapshot gets
+    the new {head, size}, the env counter is incremented once per push; an unaligned flag array and a
+    strided action view (IQN's [:, :1]) take the same path."""
+    from distributional_rl_decision_and_control_amd import learn_ops
+    from distributional_rl_decision_and_control_amd._abi import OBS_DIM
+    rs = np.random.RandomState(n)
+    cap = 3 * n + 17
+    ring = learn_ops.DeviceReplay(cap, device="cuda")
+    snap = torch.full((2,), -5, dtype=torch.int64, device="cuda")
+    ctr = torch.full((1,), 41, dtype=torch.int64, device="cuda")
+    rows = []
+    for it in range(5):
+        obs_prev = torch.from_numpy(rs.randn(n, OBS_DIM).astype(np.float32)).cuda()
+        obs_next = torch.from_numpy(rs.randn(n, OBS_DIM).astype(np.float32)).cuda()
+        c8 = rs.randint(-1, 6, size=n + 1).astype(np.int8)
+        cbuf = torch.from_numpy(c8).cuda()
+        cnt = cbuf[:n] if aligned else cbuf[1:]
+        c = c8[:n] if aligned else c8[1:]
+        act = torch.from_numpy(rs.randn(n, 2)).cuda()
+        rew = torch.from_numpy(rs.randn(n)).cuda()
+        done = torch.from_numpy(rs.randint(0, 2, size=n).astype(np.uint8)).cuda()
+        ring.push(obs_prev, obs_next, cnt, act[:, :adim], rew, done, snap=snap, counter_inc=ctr)
+        op, on, a, r, d = (t.cpu().numpy() for t in (obs_prev, obs_next, act, rew, done))
+        for k in np.nonzero(c >= 0)[0]:
+            rows.append((op[k], on[k], np.float32(a[k, 0]), np.float32(a[k, 1]) if adim == 2 else np.float32(0),
+                         np.float32(r[k]), np.float32(d[k])))
+        st = ring.state.cpu().numpy()
+        assert st[1] == min(len(rows), cap) and st[0] == len(rows) % cap
+        np.testing.assert_array_equal(snap.cpu().numpy(), st)
+        assert int(ctr.item()) == 42 + it
+    assert int(ring._work[0].item()) == 0
+    rows = rows[-cap:]
+    head = int(ring.state[0].item())
+    got = ring.ring.cpu().numpy()
+    for j in rs.choice(len(rows), 300, replace=False):
+        slot = (head - len(rows) + j) % cap
+        op, on, a0, a1, r, d = rows[j]
+        np.testing.assert_array_equal(got[slot, :40], op)
+        np.testing.assert_array_equal(got[slot, 40:80], on)
+        np.testing.assert_array_equal(got[slot, 80:84], np.array([a0, a1, r, d], np.float32))
+
+
 def test_replay_sample_guard_skips_entries_a_concurrent_push_overwrites():
     """With the ring full, sample(guard=G) never returns the G oldest entries (those a push of
     <= G rows overwrites), and stays uniform over the rest."""
@@ -175,3 +220,44 @@ def test_replay_sample_draws_taus():
     assert abs(x.var() - 1 / 12) < 0.002
     assert abs(np.corrcoef(x[0].ravel(), x[1].ravel())[0, 1]) < 0.01
     assert not torch.equal(t1, taus)
+
+
+@pytest.mark.parametrize("guard", [0, 20480])
+def test_learn_prologue_matches_separate_launches(guard):
+    """asvrl_learn_prologue (one launch: the replay draw + taus, the actor's TRAIN forward on s, the target
+    actor on s') writes exactly what asvrl_replay_sample + asvrl_actor_forward(TRAIN) +
+    asvrl_actor_forward(FWD) write: rows, taus, saved activations, actions, target actions bit-identical."""
+    from distributional_rl_decision_and_control_amd import learn_ops
+    from distributional_rl_decision_and_control_amd.fused_mlp import actor_forward, actor_train_forward
+    from distributional_rl_decision_and_control_amd.fused_update import FusedACIQNState, learn_prologue
+    from distributional_rl_decision_and_control_amd.learner import FusedAdam
+    from distributional_rl_decision_and_control_amd.policy.AC_IQN_model import AC_IQN_Policy
+    from distributional_rl_decision_and_control_amd.vec_trainer import DEFAULT_NET
+    B, N, cap = 512, 32, 50000
+    loc, tgt = [AC_IQN_Policy(**DEFAULT_NET, value_ranges_of_action=[[-1, 1], [-1, 1]], device="cuda", seed=s)
+                for s in (100, 7)]
+    FusedAdam(loc.actor.parameters()), FusedAdam(loc.critic.parameters())
+    st = FusedACIQNState(loc, tgt, B, N)
+    ring = learn_ops.DeviceReplay(cap, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(4)
+    ring.ring.copy_(torch.randn(cap, 88, generator=g, device="cuda") * 3)
+    for c in (32, 72):   # object masks in {0, 1}
+        ring.ring[:, c:c + 5] = (torch.rand(cap, 5, generator=g, device="cuda") > 0.4).float()
+    ring.state[0], ring.state[1] = 12345, 40000
+    ctr = torch.tensor([17], dtype=torch.int64, device="cuda")
+    taus_a = torch.empty(3, B, N, device="cuda")
+    rows_a = ring.sample(B, seed=99, counter_dev=ctr, guard=guard, taus=taus_a)
+    actor_train_forward(st.actor, rows_a[:, 0:40], st.abufs)
+    na_a = torch.empty(B, 2, device="cuda")
+    actor_forward(st.target_actor, rows_a[:, 40:80], na_a)
+    ab = st.abufs
+    ref = {k: getattr(ab, k).clone() for k in ("xb", "h0", "h1", "h2", "pre", "a_out")}
+    for k in ref:
+        getattr(ab, k).fill_(float("nan") if getattr(ab, k).is_floating_point() else 0)
+    taus_b = torch.empty(3, B, N, device="cuda")
+    rows_b = learn_prologue(st, ring, taus_b, 99, counter_dev=ctr, guard=guard)
+    torch.cuda.synchronize()
+    assert torch.equal(rows_a, rows_b) and torch.equal(taus_a, taus_b)
+    for k, v in ref.items():
+        assert torch.equal(v, getattr(ab, k)), k
+    assert torch.equal(na_a, st.na)
