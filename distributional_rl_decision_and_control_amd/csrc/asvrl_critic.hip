@@ -128,6 +128,12 @@ template <int MODE> struct LdsOf { using T = CriticLds; };
 template <> struct LdsOf<MODE_IQN_MAX> { using T = CriticLdsIqn; };
 template <> struct LdsOf<MODE_IQN_TRAIN> { using T = CriticLdsIqn; };
 template <> struct LdsOf<MODE_IQN_ACT> { using T = CriticLdsIqn; };
+// the staged F rows: f32 copies of the operand-rounded values (no per-use conversion) in the AC-IQN
+// modes; operand-typed in the IQN modes, whose larger LDS image leaves no room for them
+template <int MODE> struct FOf { using T = float; };
+template <> struct FOf<MODE_IQN_MAX> { using T = elem_t; };
+template <> struct FOf<MODE_IQN_TRAIN> { using T = elem_t; };
+template <> struct FOf<MODE_IQN_ACT> { using T = elem_t; };
 static_assert(sizeof(CriticLdsIqn) <= 160 * 1024, "IQN LDS image exceeds the CU's 160 KB");
 
 // The wave's feature rows in LDS for its 32 / NT samples: F (bf16 [S][256]) = observation_processor
@@ -136,8 +142,8 @@ static_assert(sizeof(CriticLdsIqn) <= 160 * 1024, "IQN LDS image exceeds the CU'
 // 4 features per lane, or a copy of a.F; G (f32 [S][128]) = relu(action_encoder(a))
 // (AC_IQN_model.py:468-470) or a copy of a.G. TRAIN also writes the bf16 obs copy for the encoder
 // weight gradient. Global loads only: this runs before any store of the tile.
-template <int NT, bool WITH_G, bool WITH_XB>
-__device__ __forceinline__ void stage_features(const CriticArgs& a, int tile, int lane, elem_t* Fw, float* Gw) {
+template <int NT, bool WITH_G, bool WITH_XB, class FT>
+__device__ __forceinline__ void stage_features(const CriticArgs& a, int tile, int lane, FT* Fw, float* Gw) {
   constexpr int S = 32 / NT;
 #pragma unroll
   for (int k = 0; k < S; ++k) {
@@ -163,13 +169,13 @@ __device__ __forceinline__ void stage_features(const CriticArgs& a, int tile, in
           for (int i = 0; i < kObjIn; ++i) d += w[i] * xo[i];
           v = x[kObsMask + o] < 0.5f ? 0.f : relu(d + a.w.obj_b[j]);   // masked_fill(mask < 0.5, 0)
         }
-        Fw[k * kC + m] = (elem_t)v;
+        Fw[k * kC + m] = static_cast<FT>((elem_t)v);   // the operand-rounded F (held in f32 or elem_t)
       }
       if (WITH_XB && a.xb != nullptr && lane < 32) bp(a.xb)[static_cast<int64_t>(b) * 32 + lane] = (elem_t)x[lane];
     } else {
       const float* f = a.F + static_cast<int64_t>(b) * kC;
 #pragma unroll
-      for (int t = 0; t < kC / 64; ++t) Fw[k * kC + lane + 64 * t] = (elem_t)relu(f[lane + 64 * t]);   // ReLU outputs
+      for (int t = 0; t < kC / 64; ++t) Fw[k * kC + lane + 64 * t] = static_cast<FT>((elem_t)relu(f[lane + 64 * t]));   // ReLU outputs
     }
     if constexpr (WITH_G) {
       if (a.ain != nullptr) {
@@ -274,8 +280,8 @@ __device__ __forceinline__ void mfma_wrows(f32x16 (&acc)[MB], WF wf, BF bf) {
   }
 }
 
-template <int MODE, int NT, class LT>
-__device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, int tile, int lane, const elem_t* Fl,
+template <int MODE, int NT, class LT, class FT>
+__device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, int tile, int lane, const FT* Fl,
                                             const float* Gl, float* wsum = nullptr) {
   constexpr bool IQN = kIqn<MODE>;
   constexpr bool TRAINM = kTrainMode<MODE>;
@@ -285,7 +291,7 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
   float tau;
   if (MODE == MODE_IQN_ACT && a.taus == nullptr) tau = act_tau(a, grow);
   else tau = a.taus[grow];
-  const elem_t* Fb = Fl + (b - tile * 32 / NT) * kC;                   // F[b], the wave's LDS row
+  const FT* Fb = Fl + (b - tile * 32 / NT) * kC;                       // F[b], the wave's LDS row
   const float* Gb = IQN ? nullptr : Gl + (b - tile * 32 / NT) * kH;     // G[b]
   const frag8* WC = kFwdOnly<MODE> ? wimg(L.wc, a.w.wc_frag) : reinterpret_cast<const frag8*>(a.w.wc_frag);
   const frag8* W1 = wimg(L.w1, a.w.w1_frag);
@@ -747,12 +753,13 @@ template <int MODE, int NT>
 __global__ __launch_bounds__((ModeWaves<MODE, NT>::n) * 64) void critic_kernel(CriticArgs a) {
   constexpr int W = ModeWaves<MODE, NT>::n, S = 32 / NT;
   __shared__ typename LdsOf<MODE>::T L;
-  __shared__ __attribute__((aligned(16))) elem_t Fs[W * S * kC];
+  using FT = typename FOf<MODE>::T;
+  __shared__ __attribute__((aligned(16))) FT Fs[W * S * kC];
   __shared__ __attribute__((aligned(16))) float Gs[kStageG<MODE> ? W * S * kH : 1];
   __shared__ float Ws[MODE == MODE_TRAIN ? W * (kH + 1) : 1];   // per-wave output-layer gradient sums
   const int tile = blockIdx.x * W + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int tiles = a.B * NT / 32;
-  elem_t* Fw = Fs + (threadIdx.x >> 6) * S * kC;
+  FT* Fw = Fs + (threadIdx.x >> 6) * S * kC;
   float* Gw = Gs + (kStageG<MODE> ? (threadIdx.x >> 6) * S * kH : 0);
   if (tile < tiles) stage_features<NT, kStageG<MODE>, kTrainMode<MODE>>(a, tile, lane, Fw, Gw);
   {

@@ -385,6 +385,7 @@ __global__ __launch_bounds__(kSumThreads) void partial_sum_kernel(const float* _
 struct SumSegs {
   AsvPartialSum seg[ASVRL_MAX_SUM_SEGS];
   int slot0[ASVRL_MAX_SUM_SEGS];   // first norm slot of each segment's working blocks
+  int nseg;
 };
 
 // group_sum for the five object copies of a fold output at once: one pass over the groups, each
@@ -442,18 +443,22 @@ __device__ __forceinline__ void group_sum_n(const float* __restrict__ p, int gro
   for (int j = 0; j < kSumOpl; ++j) out[j] = sum_tree(red[j], lane);
 }
 
-// Grid (blocks, segments); block x of a segment owns outputs [kSumSpan x, kSumSpan (x + 1)) (a
-// scalar segment: block 0 alone, all threads). With sq_blocks, every working block also writes the
-// sum of the squares of the outputs it wrote (segments with norm = 1) to its slot, for
-// asvrl_adam_step.
+// Block x of a segment owns outputs [kSumSpan x, kSumSpan (x + 1)) (a scalar segment: block 0 alone,
+// all threads). With sq_blocks, every block also writes the sum of the squares of the outputs it wrote
+// (segments with norm = 1) to its slot (= its index), for asvrl_adam_step.
 __global__ __launch_bounds__(kSumThreads) void partial_sums_kernel(SumSegs t, double* sq_blocks, float* step) {
-  const AsvPartialSum& g = t.seg[blockIdx.y];
+  // one block per WORKING block of a segment (no empty blocks to dispatch): block b is block x of the
+  // segment y whose working blocks [slot0[y], slot0[y + 1]) hold it
+  int y = 0;
+  while (y + 1 < t.nseg && static_cast<int>(blockIdx.x) >= t.slot0[y + 1]) ++y;
+  const int bx = static_cast<int>(blockIdx.x) - t.slot0[y];
+  const AsvPartialSum& g = t.seg[y];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   __shared__ float red[kSumOpl][kSumWaves][64];
   double sq = 0.0;
   const int n = g.nw + g.nb;
   if (n == 1) {   // scalar over many groups: the whole block, fixed order
-    if (blockIdx.x == 0) {
+    if (bx == 0) {
       float acc = 0.f;
       for (int k = threadIdx.x; k < g.groups; k += kSumThreads) acc += g.partial[k];
 #pragma unroll
@@ -467,8 +472,8 @@ __global__ __launch_bounds__(kSumThreads) void partial_sums_kernel(SumSegs t, do
         if (g.norm) sq += static_cast<double>(*o) * *o;
       }
     }
-  } else if (static_cast<int>(blockIdx.x) * kSumSpan < n) {   // block-uniform
-    const int base = blockIdx.x * kSumSpan + lane;
+  } else if (bx * kSumSpan < n) {   // block-uniform
+    const int base = bx * kSumSpan + lane;
     const int stride = g.stride != 0 ? g.stride : n;
     const int boff = g.boff != 0 ? g.boff : g.nw;
     float s[kSumOpl];
@@ -516,19 +521,12 @@ __global__ __launch_bounds__(kSumThreads) void partial_sums_kernel(SumSegs t, do
     }
   }
   if (sq_blocks == nullptr) return;
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) step[0] += 1.f;   // read by the next launch
+  if (blockIdx.x == 0 && threadIdx.x == 0) step[0] += 1.f;   // read by the next launch
   // ---- squared norm: this working block's sum (wave 0 holds the outputs) into its own slot
-  const int nb = n == 1 ? 1 : (n + kSumSpan - 1) / kSumSpan;
-  if (static_cast<int>(blockIdx.x) >= nb || wv != 0) return;
+  if (wv != 0) return;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) sq += __shfl_xor(sq, off, kWave);
-  if (lane == 0) sq_blocks[t.slot0[blockIdx.y] + blockIdx.x] = sq;
-}
-
-int sum_grid_x(const AsvPartialSum* segs, int nseg) {
-  int maxn = 0;
-  for (int k = 0; k < nseg; ++k) maxn = std::max(maxn, segs[k].nw + segs[k].nb);
-  return (maxn + kSumSpan - 1) / kSumSpan;
+  if (lane == 0) sq_blocks[blockIdx.x] = sq;
 }
 
 // norm slots: one per working block of each segment, segments in order
@@ -552,9 +550,9 @@ int launch_partial_sums(const AsvPartialSum* segs, int nseg, double* sq_blocks, 
                   "asvrl_partial_sums: the encoder fold writes 688 outputs (nw = 688, nb = 0)");
     t.seg[k] = g;
   }
-  norm_slots(segs, nseg, t.slot0);
-  hipLaunchKernelGGL(partial_sums_kernel, dim3(sum_grid_x(segs, nseg), nseg), dim3(kSumThreads), 0, st, t, sq_blocks,
-                     step);
+  t.nseg = nseg;
+  const int blocks = norm_slots(segs, nseg, t.slot0);
+  hipLaunchKernelGGL(partial_sums_kernel, dim3(blocks), dim3(kSumThreads), 0, st, t, sq_blocks, step);
   return check_launch("asvrl_partial_sums");
 }
 

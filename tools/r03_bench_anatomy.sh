@@ -1,0 +1,13 @@
+#!/bin/bash
+# round 3: selected GPU tests, the default bench, one graph-replayed step's kernels
+set -o pipefail
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+T=${1:-r03}
+TESTS=${TESTS:-tests/test_chain_schedule_gpu.py}
+timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread $TESTS > gpurun_out/${T}_pytest.log 2>&1 || exit 2
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err || exit 3
+cd /tmp && export TMPDIR=/tmp && rm -rf $GRAFT_REPO_ROOT/gpurun_out/${T}_prof && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/${T}_prof -o run --output-format csv rocpd -- python3 $GRAFT_REPO_ROOT/bench.py --steps 50 --warmup 10 --iqn-steps 0 --rainbow-steps 0 --config5-steps 0 --plateau-envs 0 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.json 2> $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.err || exit 4
+cd $GRAFT_REPO_ROOT && python tools/step_window.py gpurun_out/${T}_prof/run_results.db > gpurun_out/${T}_step_window.txt 2>&1
+exit 0
