@@ -722,8 +722,8 @@ __global__ __launch_bounds__(8 * 64) void critic_train_b_kernel(CriticArgs a) {
     const frag8* gwc = reinterpret_cast<const frag8*>(a.w.wc_frag);
     const frag8* gw1t = reinterpret_cast<const frag8*>(a.w.w1t_frag);
     if constexpr (kWeightsInLds) {
-      for (int i = threadIdx.x; i < kFragWC; i += 8 * 64) L.wc[i] = gwc[i];
-      for (int i = threadIdx.x; i < kFragW1; i += 8 * 64) L.w1t[i] = gw1t[i];
+      copy_frags<8 * 64, kFragWC, kElemBytes == 2 ? 16 : 8>(L.wc, gwc, threadIdx.x);
+      copy_frags<8 * 64, kFragW1, kElemBytes == 2 ? 16 : 8>(L.w1t, gw1t, threadIdx.x);
     }
     for (int i = threadIdx.x; i < kC; i += 8 * 64) L.bc[i] = a.w.bc[i];
   }
@@ -767,9 +767,10 @@ __global__ __launch_bounds__((ModeWaves<MODE, NT>::n) * 64) void critic_kernel(C
     const frag8* gw1 = reinterpret_cast<const frag8*>(a.w.w1_frag);
     const frag8* gw2 = reinterpret_cast<const frag8*>(a.w.w2_frag);
     if constexpr (kWeightsInLds) {
-      for (int i = threadIdx.x; i < kFragWC; i += W * 64) L.wc[i] = gwc[i];
-      for (int i = threadIdx.x; i < kFragW1; i += W * 64) L.w1[i] = gw1[i];
-      for (int i = threadIdx.x; i < kFragW2; i += W * 64) L.w2[i] = gw2[i];
+      constexpr int CH = kElemBytes == 2 ? 16 : 8;   // fragments in flight per thread
+      copy_frags<W * 64, kFragWC, CH>(L.wc, gwc, threadIdx.x);
+      copy_frags<W * 64, kFragW1, CH>(L.w1, gw1, threadIdx.x);
+      copy_frags<W * 64, kFragW2, CH>(L.w2, gw2, threadIdx.x);
     }
     for (int i = threadIdx.x; i < kC; i += W * 64) L.bc[i] = a.w.bc[i];
     for (int i = threadIdx.x; i < kH; i += W * 64) {

@@ -61,6 +61,28 @@ __device__ __forceinline__ const frag8* wimg(const frag8* lds, const void* glob)
 // LDS slots of a weight image: full size in the bf16 build, one fragment (unused) in the f32 build
 constexpr int lds_frags(int n) { return kWeightsInLds ? n : 1; }
 
+// Copy N fragments (global -> LDS) with the workgroup's T threads, up to CH per thread per batch: a
+// batch's loads all issue before its stores (a plain strided loop waits for each load before its store,
+// one L2 round trip per fragment and thread: ~5 us of a weight-staging workgroup's start)
+template <int T, int N, int CH = 16>
+__device__ __forceinline__ void copy_frags(frag8* dst, const frag8* __restrict__ src, int tid) {
+  constexpr int PER = (N + T - 1) / T;
+#pragma unroll
+  for (int c0 = 0; c0 < PER; c0 += CH) {
+    frag8 v[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int i = (c0 + c) * T + tid;
+      if (c0 + c < PER && i < N) v[c] = src[i];
+    }
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int i = (c0 + c) * T + tid;
+      if (c0 + c < PER && i < N) dst[i] = v[c];
+    }
+  }
+}
+
 // feature index held by accumulator register g of 32-feature block mb in lane half h
 __device__ __forceinline__ int feat(int mb, int g, int h) { return mb * 32 + (g & 3) + 8 * (g >> 2) + 4 * h; }
 

@@ -314,9 +314,10 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_kernel(MlpArgs a) {
     const frag8* g1 = reinterpret_cast<const frag8*>(a.w.w1_frag);
     const frag8* g2 = reinterpret_cast<const frag8*>(a.w.w2_frag);
     if constexpr (kWeightsInLds) {
-      for (int i = threadIdx.x; i < kFragEnc; i += kMlpWaves * 64) L.enc[i] = ge[i];
-      for (int i = threadIdx.x; i < kFragH1; i += kMlpWaves * 64) L.w1[i] = g1[i];
-      for (int i = threadIdx.x; i < kFragH2; i += kMlpWaves * 64) L.w2[i] = g2[i];
+      constexpr int CH = kElemBytes == 2 ? 16 : 8;   // fragments in flight per thread
+      copy_frags<kMlpWaves * 64, kFragEnc, CH>(L.enc, ge, threadIdx.x);
+      copy_frags<kMlpWaves * 64, kFragH1, CH>(L.w1, g1, threadIdx.x);
+      copy_frags<kMlpWaves * 64, kFragH2, CH>(L.w2, g2, threadIdx.x);
     }
     for (int i = threadIdx.x; i < kEnc; i += kMlpWaves * 64) L.benc[i] = a.w.b_enc[i];
     for (int i = threadIdx.x; i < kHid; i += kMlpWaves * 64) {

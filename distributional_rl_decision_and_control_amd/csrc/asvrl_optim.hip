@@ -83,6 +83,16 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(float* __restrict__ p
                                                             int64_t* __restrict__ counter) {
   __shared__ float s_coef;
   __shared__ double s_red[kOptThreads];
+  // this thread's first parameter, its moments and gradient loaded before the norm fold (they do not
+  // depend on it: one memory round trip fewer on the launch's critical path)
+  const int64_t i0 = static_cast<int64_t>(blockIdx.x) * kOptThreads + threadIdx.x;
+  float g0 = 0.f, m0 = 0.f, v0 = 0.f, p0 = 0.f;
+  if (i0 < n) {
+    g0 = g[i0];
+    m0 = m[i0];
+    v0 = v[i0];
+    p0 = p[i0];
+  }
   {   // thread t folds partials t, t + 256, ... in order, then a fixed tree: the same in every block
     double x = 0.0;
     for (int k = threadIdx.x; k < nparts; k += kOptThreads) x += partial[k];
@@ -110,16 +120,17 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(float* __restrict__ p
   const float bc2_sqrt = static_cast<float>(sqrt(1.0 - pow(static_cast<double>(beta2), t)));
   const float w1 = static_cast<float>(1.0 - static_cast<double>(beta1));
   const float w2 = static_cast<float>(1.0 - static_cast<double>(beta2));
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kOptThreads + threadIdx.x; i < n;
-       i += static_cast<int64_t>(gridDim.x) * kOptThreads) {
-    const float gi = g[i] * coef;
+  for (int64_t i = i0; i < n; i += static_cast<int64_t>(gridDim.x) * kOptThreads) {
+    const bool first = i == i0;
+    const float gi = (first ? g0 : g[i]) * coef;
+    const float mo = first ? m0 : m[i], vo = first ? v0 : v[i], po = first ? p0 : p[i];
     g[i] = gi;
-    const float mi = m[i] + w1 * (gi - m[i]);          // exp_avg.lerp_(grad, 1 - beta1)
-    const float vi = v[i] * beta2 + w2 * gi * gi;      // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
+    const float mi = mo + w1 * (gi - mo);          // exp_avg.lerp_(grad, 1 - beta1)
+    const float vi = vo * beta2 + w2 * gi * gi;    // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
     m[i] = mi;
     v[i] = vi;
     const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    const float pn = p[i] - step_size * (mi / denom);  // param.addcdiv_(exp_avg, denom, -step_size)
+    const float pn = po - step_size * (mi / denom);  // param.addcdiv_(exp_avg, denom, -step_size)
     p[i] = pn;
     if (pk.n > 0) pack_param(pk, i, pn);
   }
