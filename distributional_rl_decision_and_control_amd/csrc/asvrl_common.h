@@ -248,4 +248,23 @@ __device__ __forceinline__ void replay_draw_taus(int b, int lane, int B, uint64_
   }
 }
 
+// sum of p[k] over k = start, start + step, ... < n in that order, with the loads of each batch of CH
+// terms issued before any of them is added (the plain loop waits for every load in turn: one memory round
+// trip per term). The same additions in the same order: bit-identical to the plain loop.
+template <class T, int CH = 8>
+__device__ __forceinline__ T strided_sum(const T* __restrict__ p, int start, int n, int step, T acc) {
+  for (int k0 = start; k0 < n; k0 += CH * step) {
+    T v[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int k = k0 + c * step;
+      v[c] = k < n ? p[k] : T(0);
+    }
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+      if (k0 + c * step < n) acc += v[c];
+  }
+  return acc;
+}
+
 }  // namespace asvrl

@@ -466,14 +466,23 @@ void critic_fused_kernel(FusedArgs a) {
 
   using IL = InLayout<NT, S, G, NA>;
   {
-    const float* srcs[6] = {a.w.self_w, a.w.self_b, a.w.obj_w, a.w.obj_b, a.w.ae_w, a.w.ae_b};
-    const int lens[6] = {56 * 7, 56, 40 * 5, 40, 128 * 2, 128};
-    int off = 0;
+    // the encoder parameters into LDS: each thread's (at most five) loads issued before its stores
+    constexpr int kEncN = IQN ? 56 * 7 + 56 + 40 * 5 + 40 : kEncFloats, kEncPer = (kEncN + kNW * 64 - 1) / (kNW * 64);
+    float ev[kEncPer];
 #pragma unroll
-    for (int q = 0; q < (IQN ? 4 : 6); ++q) {
-      for (int i = threadIdx.x; i < lens[q]; i += kNW * 64) L.enc[off + i] = srcs[q][i];
-      off += lens[q];
+    for (int u = 0; u < kEncPer; ++u) {
+      int e = threadIdx.x + u * kNW * 64;
+      const float* src = a.w.self_w;
+      if (e >= 392) { e -= 392; src = a.w.self_b;
+        if (e >= 56) { e -= 56; src = a.w.obj_w;
+          if (e >= 200) { e -= 200; src = a.w.obj_b;
+            if (e >= 40) { e -= 40; src = a.w.ae_w;
+              if (e >= 256) { e -= 256; src = a.w.ae_b; } } } } }
+      ev[u] = threadIdx.x + u * kNW * 64 < kEncN ? src[e] : 0.f;
     }
+#pragma unroll
+    for (int u = 0; u < kEncPer; ++u)
+      if (threadIdx.x + u * kNW * 64 < kEncN) L.enc[threadIdx.x + u * kNW * 64] = ev[u];
     if constexpr (!IQN) {
       for (int i = threadIdx.x; i < 8 * kC; i += kNW * 64) L.encacc[i] = 0.f;
       for (int i = threadIdx.x; i < 3 * 2 * kH; i += kNW * 64) L.aeacc[i] = 0.f;

@@ -95,7 +95,7 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(float* __restrict__ p
   }
   {   // thread t folds partials t, t + 256, ... in order, then a fixed tree: the same in every block
     double x = 0.0;
-    for (int k = threadIdx.x; k < nparts; k += kOptThreads) x += partial[k];
+    x = strided_sum<double>(partial, threadIdx.x, nparts, kOptThreads, x);
     s_red[threadIdx.x] = x;
     __syncthreads();
     for (int w = kOptThreads / 2; w > 0; w >>= 1) {

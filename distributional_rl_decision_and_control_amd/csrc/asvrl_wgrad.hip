@@ -460,7 +460,7 @@ __global__ __launch_bounds__(kSumThreads) void partial_sums_kernel(SumSegs t, do
   if (n == 1) {   // scalar over many groups: the whole block, fixed order
     if (bx == 0) {
       float acc = 0.f;
-      for (int k = threadIdx.x; k < g.groups; k += kSumThreads) acc += g.partial[k];
+      acc = strided_sum<float>(g.partial, threadIdx.x, g.groups, kSumThreads, acc);
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, kWave);
       if (lane == 0) red[0][wv][0] = acc;
