@@ -344,11 +344,32 @@ struct ActorSplitLds {
   float part[kMlpWaves][32][2];
 };
 
+// A wave's weight fragments of the split tile (encoder blocks 2w, 2w + 1; W1 and W2 block w), fetched
+// ahead by the fused prologue so that their L2 latency overlaps its replay draw.
+struct SplitPre {
+  frag8 enc[4];
+  frag8 w1[kEnc / 16];
+  frag8 w2[kHid / 16];
+};
+
+__device__ __forceinline__ void split_prefetch(const AsvMlpWeights& wt, int w, int lane, SplitPre& q) {
+  const frag8* ENC = reinterpret_cast<const frag8*>(wt.enc_frag);
+  const frag8* W1 = reinterpret_cast<const frag8*>(wt.w1_frag);
+  const frag8* W2 = reinterpret_cast<const frag8*>(wt.w2_frag);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) q.enc[i] = ENC[((2 * w + (i >> 1)) * 2 + (i & 1)) * 64 + lane];
+#pragma unroll
+  for (int ks = 0; ks < kEnc / 16; ++ks) q.w1[ks] = W1[(w * 16 + ks) * 64 + lane];
+#pragma unroll
+  for (int ks = 0; ks < kHid / 16; ++ks) q.w2[ks] = W2[(w * 8 + ks) * 64 + lane];
+}
+
 // One 32-row tile of the split Actor (4 waves): rows tile * 32 + r of the outputs; the observation of
 // row r read from x + (xrow0 + r) * ldx (the global rows, or rows staged in LDS by the fused prologue).
-template <int MODE>
+// PRE: the wave's fragments already in registers (`pre`; the same MFMAs in the same order).
+template <int MODE, bool PRE = false>
 __device__ __forceinline__ void actor_split_tile(const MlpArgs& a, ActorSplitLds& L, int tile, const float* x,
-                                                 int64_t ldx, int xrow0) {
+                                                 int64_t ldx, int xrow0, const SplitPre& pre = SplitPre{}) {
   const AsvMlpIO& io = a.io;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
   const int row = tile * 32 + r;
@@ -371,7 +392,8 @@ __device__ __forceinline__ void actor_split_tile(const MlpArgs& a, ActorSplitLds
       const int mb = 2 * w + q;
       f32x16 acc = f32x16{};
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) acc = mfma(ENC[(mb * 2 + ks) * 64 + lane], bx[ks], acc);
+      for (int ks = 0; ks < 2; ++ks)
+        acc = mfma(PRE ? pre.enc[2 * q + ks] : ENC[(mb * 2 + ks) * 64 + lane], bx[ks], acc);
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         float v[8];
@@ -397,7 +419,13 @@ __device__ __forceinline__ void actor_split_tile(const MlpArgs& a, ActorSplitLds
     const frag8* W1 = reinterpret_cast<const frag8*>(a.w.w1_frag);
     const RowA<kEnc> RX(r, h);
     const RowA<kHid> RH(r, h);
-    const f32x16 acc = wchain<kEnc / 16>(W1, w * 16, lane, L.x0, RX);
+    f32x16 acc = f32x16{};
+    if constexpr (PRE) {
+#pragma unroll
+      for (int ks = 0; ks < kEnc / 16; ++ks) acc = mfma(pre.w1[ks], rowf(L.x0, RX, 0, ks), acc);
+    } else {
+      acc = wchain<kEnc / 16>(W1, w * 16, lane, L.x0, RX);
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       float v[8];
@@ -417,7 +445,13 @@ __device__ __forceinline__ void actor_split_tile(const MlpArgs& a, ActorSplitLds
   {
     const frag8* W2 = reinterpret_cast<const frag8*>(a.w.w2_frag);
     const RowA<kHid> RH(r, h);
-    const f32x16 acc = wchain<kHid / 16>(W2, w * 8, lane, L.h1, RH);
+    f32x16 acc = f32x16{};
+    if constexpr (PRE) {
+#pragma unroll
+      for (int ks = 0; ks < kHid / 16; ++ks) acc = mfma(pre.w2[ks], rowf(L.h1, RH, 0, ks), acc);
+    } else {
+      acc = wchain<kHid / 16>(W2, w * 8, lane, L.h1, RH);
+    }
     float p0 = 0.f, p1 = 0.f;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -457,7 +491,9 @@ __device__ __forceinline__ void actor_split_tile(const MlpArgs& a, ActorSplitLds
 template <int MODE>
 __global__ __launch_bounds__(kMlpWaves * 64) void actor_split_kernel(MlpArgs a) {
   __shared__ __attribute__((aligned(16))) ActorSplitLds L;
-  actor_split_tile<MODE>(a, L, blockIdx.x, a.io.x, a.io.ldx, blockIdx.x * 32);
+  SplitPre pre;
+  split_prefetch(a.w, threadIdx.x >> 6, threadIdx.x & 63, pre);
+  actor_split_tile<MODE, true>(a, L, blockIdx.x, a.io.x, a.io.ldx, blockIdx.x * 32, pre);
 }
 
 // ------------------------------------------------------------------ fused learn prologue (AC-IQN)
@@ -486,6 +522,9 @@ __global__ __launch_bounds__(kMlpWaves * 64) void learn_prologue_kernel(Prologue
   const bool second = static_cast<int>(blockIdx.x) >= T;
   const int tile = second ? blockIdx.x - T : blockIdx.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // the wave's weight fragments first: their L2 latency runs under the draw below
+  SplitPre pre;
+  split_prefetch(second ? tgt.w : train.w, w, lane, pre);
   const int64_t head = p.ring_state[0], size = p.ring_state[1];
   const uint64_t ctr = p.counter + (p.counter_dev != nullptr ? *p.counter_dev : 0ull);
   // wave w gathers samples 8w .. 8w + 7 of the tile: the whole row to `out` (first half), the observation
@@ -495,31 +534,50 @@ __global__ __launch_bounds__(kMlpWaves * 64) void learn_prologue_kernel(Prologue
   const int slot_lo = static_cast<int>(my_slot & 0xFFFFFFFFll), slot_hi = static_cast<int>(my_slot >> 32);
   constexpr int kRowV = ASVRL_TR_DIM / 4, kObsV = ASVRL_OBS_DIM / 4;
   const int per = second ? kObsV : kRowV;   // float4 pieces per sample
-  float4 v[3];
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  f4v v[3];
   int jj[3], cc[3];
 #pragma unroll
-  for (int u = 0; u < 3; ++u) {
-    const int e = lane + 64 * u;
+  for (int u = 0; u < 3; ++u) {   // every lane loads (pieces past the eight rows re-read row 0's): no
+    const int e = lane + 64 * u;  // predicated loads, so v stays in registers
     jj[u] = e / per;
     cc[u] = e - jj[u] * per;
     const int js = jj[u] < 8 ? jj[u] : 0;
     const int64_t slot = (static_cast<int64_t>(__shfl(slot_hi, js)) << 32) |
                          static_cast<uint32_t>(__shfl(slot_lo, js));
-    if (jj[u] < 8)
-      v[u] = reinterpret_cast<const float4*>(p.ring + slot * ASVRL_TR_DIM)[(second ? kObsV : 0) + cc[u]];
+    v[u] = reinterpret_cast<const f4v*>(p.ring + slot * ASVRL_TR_DIM)[(second ? kObsV : 0) + (jj[u] < 8 ? cc[u] : 0)];
   }
-  if (!second && p.taus != nullptr)
-    for (int j = 0; j < 8; ++j) replay_draw_taus(tile * 32 + 8 * w + j, lane, p.B, p.seed, ctr, p.taus, p.tau_sets, p.tau_n);
+  if (!second && p.taus != nullptr) {
+    // the eight samples' taus with every lane busy: item (sample j, Philox block k0 / 4) per lane, the
+    // draws of replay_draw_taus (same counters, bit-identical)
+    const int per_row = p.tau_sets * p.tau_n, nblk = (per_row + 3) / 4;
+    for (int it = lane; it < 8 * nblk; it += kWave) {
+      const int j = it / nblk, k0 = 4 * (it - j * nblk), b = tile * 32 + 8 * w + j;
+      const U4 r = philox4x32_10(U4{static_cast<uint32_t>(b), static_cast<uint32_t>(k0) ^ 0x7A0000u,
+                                    static_cast<uint32_t>(ctr >> 32), static_cast<uint32_t>(ctr)},
+                                 static_cast<uint32_t>(p.seed) ^ 0x51EDu, static_cast<uint32_t>(p.seed >> 32));
+      const uint32_t rw[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k = k0 + q;
+        if (k < per_row) {
+          const int set = k / p.tau_n, t = k - set * p.tau_n;
+          p.taus[(static_cast<size_t>(set) * p.B + b) * p.tau_n + t] = static_cast<float>(rw[q] >> 8) * (1.0f / 16777216.0f);
+        }
+      }
+    }
+  }
 #pragma unroll
   for (int u = 0; u < 3; ++u) {
-    if (jj[u] >= 8) continue;
-    const int lr = 8 * w + jj[u], b = tile * 32 + lr;
-    if (!second) reinterpret_cast<float4*>(p.out + static_cast<size_t>(b) * ASVRL_TR_DIM)[cc[u]] = v[u];
-    if (cc[u] < kObsV) reinterpret_cast<float4*>(xs + lr * ASVRL_OBS_DIM)[cc[u]] = v[u];
+    if (jj[u] < 8) {
+      const int lr = 8 * w + jj[u], b = tile * 32 + lr;
+      if (!second) reinterpret_cast<f4v*>(p.out + static_cast<size_t>(b) * ASVRL_TR_DIM)[cc[u]] = v[u];
+      if (cc[u] < kObsV) reinterpret_cast<f4v*>(xs + lr * ASVRL_OBS_DIM)[cc[u]] = v[u];
+    }
   }
   __syncthreads();
-  if (!second) actor_split_tile<MLP_TRAIN>(train, L, tile, xs, ASVRL_OBS_DIM, 0);
-  else actor_split_tile<MLP_FWD>(tgt, L, tile, xs, ASVRL_OBS_DIM, 0);
+  if (!second) actor_split_tile<MLP_TRAIN, true>(train, L, tile, xs, ASVRL_OBS_DIM, 0, pre);
+  else actor_split_tile<MLP_FWD, true>(tgt, L, tile, xs, ASVRL_OBS_DIM, 0, pre);
 }
 
 // The backward in the same split: dz2 (block w) from dA, dz1 = W2^T dz2 (block w), dz0 = W1^T dz1
@@ -543,6 +601,24 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_split_kernel(MlpArgs
   const int64_t rr = valid ? row : io.n - 1;
   elem_t* const dz2i = L.x0;
   elem_t* const dz1i = L.h1;
+  // every weight fragment and saved activation the wave reads, fetched up front (one L2 / HBM latency for
+  // the kernel instead of one per phase; the same MFMAs in the same order)
+  frag8 w2t[kHid / 16], w1t[2][kHid / 16];
+  {
+    const frag8* W2T = reinterpret_cast<const frag8*>(a.w.w2t_frag);
+    const frag8* W1T = reinterpret_cast<const frag8*>(a.w.w1t_frag);
+#pragma unroll
+    for (int ks = 0; ks < kHid / 16; ++ks) w2t[ks] = W2T[(w * 8 + ks) * 64 + lane];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int ks = 0; ks < kHid / 16; ++ks) w1t[q][ks] = W1T[((2 * w + q) * 8 + ks) * 64 + lane];
+  }
+  float hv2[16], hv1[16], hv0[2][16];
+  load_block16(bp(io.h2) + rr * kHid, w, h, hv2);
+  load_block16(bp(io.h1) + rr * kHid, w, h, hv1);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) load_block16(bp(io.h0) + rr * kEnc, 2 * w + q, h, hv0[q]);
   const float z0 = io.pre[rr * 2], z1 = io.pre[rr * 2 + 1];
   const float d0 = io.dA[rr * 2] * a.w.out_scale / (1.f + z0 * z0);
   const float d1 = io.dA[rr * 2 + 1] * a.w.out_scale / (1.f + z1 * z1);
@@ -553,8 +629,7 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_split_kernel(MlpArgs
   const RowA<kHid> RH(r, h);
   // ---------------- dz2 (block w)
   {
-    float hv[16];
-    load_block16(bp(io.h2) + rr * kHid, w, h, hv);
+    const float (&hv)[16] = hv2;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       float dv[8];
@@ -572,10 +647,10 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_split_kernel(MlpArgs
   __syncthreads();
   // ---------------- dz1 = (W2^T dz2) 1[h1 > 0] (block w)
   {
-    const frag8* W2T = reinterpret_cast<const frag8*>(a.w.w2t_frag);
-    float hv[16];
-    load_block16(bp(io.h1) + rr * kHid, w, h, hv);
-    const f32x16 acc = wchain<kHid / 16>(W2T, w * 8, lane, dz2i, RH);
+    const float (&hv)[16] = hv1;
+    f32x16 acc = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < kHid / 16; ++ks) acc = mfma(w2t[ks], rowf(dz2i, RH, 0, ks), acc);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       float dv[8];
@@ -592,13 +667,13 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_split_kernel(MlpArgs
   __syncthreads();
   // ---------------- dz0 = (W1^T dz1) 1[h0 > 0] (blocks 2w, 2w + 1)
   {
-    const frag8* W1T = reinterpret_cast<const frag8*>(a.w.w1t_frag);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int mb = 2 * w + q;
-      float hv[16];
-      load_block16(bp(io.h0) + rr * kEnc, mb, h, hv);
-      const f32x16 acc = wchain<kHid / 16>(W1T, mb * 8, lane, dz1i, RH);
+      const float (&hv)[16] = hv0[q];
+      f32x16 acc = f32x16{};
+#pragma unroll
+      for (int ks = 0; ks < kHid / 16; ++ks) acc = mfma(w1t[q][ks], rowf(dz1i, RH, 0, ks), acc);
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         float dv[8];
