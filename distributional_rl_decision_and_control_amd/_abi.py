@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("ASVRL_LIB", os.path.join(HERE, "lib", "libasvrl.so"))
 # the same sources built with f32 learner operands (the parity build; asvrl_operand_bytes() == 4)
 LIB_PATH_F32 = os.path.join(HERE, "lib", "libasvrl_f32.so")
 OPERANDS = {"bf16": (LIB_PATH, 2), "f32": (LIB_PATH_F32, 4)}
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
 OBS_DIM = 40   # self 7 | objects 25 | mask 5 | pad 3
@@ -148,6 +148,14 @@ WGRAD_MFMA, WGRAD_VEC, WGRAD_SMALL = 0, 1, 2
 class AsvWgradSeg(C.Structure):
     _fields_ = [("dz", _VP), ("ldz", _I64), ("x", _VP), ("ldx", _I64), ("R", _I32), ("M", _I32), ("K", _I32),
                 ("kind", _I32), ("partial", _VP), ("partial_floats", _I64)]
+
+
+class AsvActorGradIO(C.Structure):
+    _fields_ = [(n, _VP) for n in ("xb", "h0", "h1", "h2", "dout", "dz2", "dz1", "dz0")] + \
+               [("B", _I32), ("n_loss", _I32)] + \
+               [(n, _VP) for n in ("tile_loss", "loss_out", "w1_grad", "b1_grad", "w2_grad", "b2_grad", "wo_grad",
+                                   "bo_grad", "enc_grad", "norm_parts", "step", "work")] + \
+               [("work_floats", _I64), ("counters", _VP)]
 
 
 class AsvPartialSum(C.Structure):
@@ -286,6 +294,10 @@ EXPORTS = [
     ("asvrl_partial_sums", C.c_int, [_VP, _I32, _VP]),
     ("asvrl_partial_sums_norm", C.c_int, [_VP, _I32, _VP, _VP, _VP]),
     ("asvrl_partial_sums_norm_parts", _I32, [_VP, _I32]),
+    ("asvrl_actor_grads_workspace", _I64, [_I32]),
+    ("asvrl_actor_grads_counters", _I32, []),
+    ("asvrl_actor_grads_norm_parts", _I32, []),
+    ("asvrl_actor_grads", C.c_int, [C.POINTER(AsvActorGradIO), _VP]),
     ("asvrl_adam_step", C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, _F, _F, _VP, _VP, _I32, _VP]),
     ("asvrl_adam_step_pack", C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, _F, _F, _VP, _VP, _I32, _VP, _I32,
                                        _VP, _VP]),

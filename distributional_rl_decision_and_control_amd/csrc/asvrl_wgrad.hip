@@ -598,6 +598,325 @@ int launch_wgrad(const elem_t* dz, int64_t ldz, const elem_t* x, int64_t ldx, in
   return check_launch("asvrl_linear_wgrad");
 }
 
+// ------------------------------------------------------------------ the Actor's gradients in ONE launch
+// Every weight / bias gradient of the Actor (AC_IQN_model.py:284-321) from its backward's dZ and the
+// TRAIN pass's saved activations over the B rows (agent.py:424-426: actor_loss.backward()), the actor
+// loss, the squared-norm partials of clip_grad_norm_ and the Adam step count -- what wgrad_multi +
+// partial_sums_norm did in two launches with per-group partials of the whole layer.
+//
+// Work items (one 4-wave workgroup each): a 32 x 32 output tile of hidden_layer_2 (16 tiles), hidden_layer
+// (32) or the 256 x 32 encoder image (8), times S row splits of kAgRS rows; the output layer (S splits on
+// the VALU); the loss. A tile item stages its split's dZ and X columns in LDS (each wave kAgRW rows, all
+// loads issued at once), runs kAgRW / 16 MFMAs per wave (bias: one more MFMA against ones), folds the four
+// waves in order and stores the split's 32 x 32 + 32 slab write-through (sc1). The LAST split of a tile to
+// arrive (agent-scope counter, MI355X hand-off with sc1 stores / sc1 loads: no fence) sums the S slabs in
+// split order -- the result does not depend on who arrives last -- writes the gradient and the tile's
+// squared norm. The encoder image's eight tiles hand their merged tiles to the last of them, which folds
+// the image onto self_encoder / object_encoder (sum over the five object copies in object order).
+// Counters are left zero for the next launch (HIP-graph replay).
+#if ASVRL_OPERAND_F32
+constexpr int kAgRW = 32;    // rows per wave (f32 staging: 4x the bytes per row)
+#else
+constexpr int kAgRW = 128;
+#endif
+constexpr int kAgW = 4, kAgT = kAgW * 64, kAgRS = kAgW * kAgRW;   // waves, threads, rows per split
+constexpr int kAgSt = lds_stride(32);                              // staged row stride (bytes)
+constexpr int kAgCPR = 32 * kElemBytes / 16;                       // 16-byte chunks per staged row
+constexpr int kAgNL = kAgRW * kAgCPR / 64;                         // chunks per lane per operand
+static_assert(kAgNL >= 1 && (kAgRW * kAgCPR) % 64 == 0, "staging must tile the wave");
+constexpr int kAgSlab = 32 * 32 + 32;                              // one split's tile + bias slab
+constexpr int kAgT2 = 16, kAgT1 = 32, kAgTE = 8, kAgTiles = kAgT2 + kAgT1 + kAgTE;
+constexpr int kAgOutSlab = 2 * 128 + 2;
+constexpr int kAgEncImg = 256 * 32 + 256;
+constexpr int kAgCtrOut = kAgTiles, kAgCtrEnc = kAgTiles + 1, kAgCounters = kAgTiles + 2;
+constexpr int kAgSlotEnc = kAgT2 + kAgT1, kAgSlotOut = kAgSlotEnc + 1, kAgSlots = kAgSlotOut + 1;
+constexpr int kAgEncOut = 688;   // self_w 56x7 | self_b 56 | obj_w 40x5 | obj_b 40
+
+struct AgLds {
+  union {
+    struct {
+      char z[kAgW][kAgRW * kAgSt];
+      char x[kAgW][kAgRW * kAgSt];
+    } st;
+    float cmb[kAgW][kAgSlab];
+    float out[16][16][18];    // output layer: [row lane][column chunk][8 + 8 columns, 2 biases]
+  } u;
+  double red[kAgT];
+  int last;
+};
+
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// every wave's slab stores have left, then one lane takes a ticket; true in the workgroup of the n-th
+// arrival (the others return). The counter is reset by that workgroup.
+__device__ __forceinline__ bool ag_arrive(int* cnt, int n, AgLds& L) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int o = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    L.last = o == n - 1;
+    if (o == n - 1) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return L.last != 0;
+}
+
+// fixed-order f64 sum of one value per thread; thread 0 gets the total
+__device__ __forceinline__ double ag_block_sum(double v, AgLds& L) {
+  L.red[threadIdx.x] = v;
+  __syncthreads();
+  for (int w = kAgT / 2; w > 0; w >>= 1) {
+    if (static_cast<int>(threadIdx.x) < w) L.red[threadIdx.x] += L.red[threadIdx.x + w];
+    __syncthreads();
+  }
+  return L.red[0];
+}
+
+// One tile item: dW[32 m][32 k] (+ db[32 m] when bias) over rows [r0, r0 + kAgRS) of dz (columns
+// m0..m0+31) and x (columns k0..k0+31). Returns true in the tile's last arriving workgroup, which then
+// holds the S-split sum: thread t elements t + 256 j (m = e / 32, k = e % 32) in v[j], bias m = t in vb.
+__device__ __forceinline__ bool ag_tile(const elem_t* __restrict__ dz, int ldz, const elem_t* __restrict__ x, int ldx,
+                                        int R, int r0, bool bias, int S, int s, float* slabs, int* cnt, AgLds& L,
+                                        float (&v)[4], float& vb) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int rw0 = r0 + w * kAgRW;
+  typedef unsigned int u32v4 __attribute__((ext_vector_type(4)));
+  u32v4 vz[kAgNL], vx[kAgNL];
+#pragma unroll
+  for (int i = 0; i < kAgNL; ++i) {   // all of the wave's loads in flight at once
+    const int q = lane + 64 * i, row = q / kAgCPR, c = q % kAgCPR, gr = rw0 + row;
+    const bool ok = gr < R;
+    const int64_t g = ok ? gr : 0;
+    vz[i] = *reinterpret_cast<const u32v4*>(dz + g * ldz + c * kE16);
+    vx[i] = *reinterpret_cast<const u32v4*>(x + g * ldx + c * kE16);
+    if (!ok) vz[i] = vx[i] = u32v4{0u, 0u, 0u, 0u};
+  }
+  char* lz = L.u.st.z[w];
+  char* lx = L.u.st.x[w];
+#pragma unroll
+  for (int i = 0; i < kAgNL; ++i) {
+    const int q = lane + 64 * i, row = q / kAgCPR, c = q % kAgCPR;
+    *reinterpret_cast<u32v4*>(lz + row * kAgSt + c * 16) = vz[i];
+    *reinterpret_cast<u32v4*>(lx + row * kAgSt + c * 16) = vx[i];
+  }
+  __syncthreads();
+  frag8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = static_cast<elem_t>(1.0f);
+  f32x16 acc = f32x16{}, accb = f32x16{};
+#pragma unroll
+  for (int ks = 0; ks < kAgRW / 16; ++ks) {
+    const frag8 A = frag_tr(lz, kAgSt, ks * 16, 0, lane);
+    acc = mfma(A, frag_tr(lx, kAgSt, ks * 16, 0, lane), acc);
+    if (bias) accb = mfma(A, ones, accb);
+  }
+  __syncthreads();   // the staging images are reused as the fold area
+  const int h = lane >> 5, n = lane & 31;
+  float* cw = L.u.cmb[w];
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const int m = (g & 3) + 8 * (g >> 2) + 4 * h;
+    cw[m * 32 + n] = acc[g];
+    if (bias && n == 0) cw[1024 + m] = accb[g];
+  }
+  __syncthreads();
+  float* my = slabs + static_cast<size_t>(s) * kAgSlab;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int e = t + kAgT * j;
+    v[j] = ((L.u.cmb[0][e] + L.u.cmb[1][e]) + L.u.cmb[2][e]) + L.u.cmb[3][e];
+    if (S > 1) st_sc1(my + e, v[j]);
+  }
+  vb = 0.f;
+  if (bias && t < 32) {
+    vb = ((L.u.cmb[0][1024 + t] + L.u.cmb[1][1024 + t]) + L.u.cmb[2][1024 + t]) + L.u.cmb[3][1024 + t];
+    if (S > 1) st_sc1(my + 1024 + t, vb);
+  }
+  if (S == 1) return true;
+  if (!ag_arrive(cnt, S, L)) return false;
+  // the S slabs in split order (this workgroup's own from registers)
+  float a[4] = {0.f, 0.f, 0.f, 0.f}, ab = 0.f;
+  for (int s2 = 0; s2 < S; ++s2) {
+    const float* p = slabs + static_cast<size_t>(s2) * kAgSlab;
+    float u[4], ub = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) u[j] = s2 == s ? v[j] : ld_sc1(p + t + kAgT * j);
+    if (bias && t < 32) ub = s2 == s ? vb : ld_sc1(p + 1024 + t);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = s2 == 0 ? u[j] : a[j] + u[j];
+    ab = s2 == 0 ? ub : ab + ub;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = a[j];
+  vb = ab;
+  return true;
+}
+
+struct AgArgs {
+  AsvActorGradIO io;
+  int S;
+};
+
+__global__ __launch_bounds__(kAgT) void actor_grads_kernel(AgArgs a) {
+  __shared__ __attribute__((aligned(16))) AgLds L;
+  const AsvActorGradIO& io = a.io;
+  const int S = a.S, R = io.B, t = threadIdx.x;
+  const int b = blockIdx.x;
+  float* work = io.work;
+  float* out_slabs = work + static_cast<size_t>(kAgTiles) * S * kAgSlab;
+  float* enc_img = out_slabs + static_cast<size_t>(S) * kAgOutSlab;
+  if (b == 0 && t == 0 && io.step != nullptr) io.step[0] += 1.f;   // read by the Adam launch
+  if (b < kAgTiles * S) {
+    const int tile = b / S, s = b % S;
+    const elem_t *dz, *x;
+    int ldz, ldx, mb, kb;
+    if (tile < kAgT2) {   // hidden_layer_2: dz2 [R][128], h1 [R][128]
+      dz = bp(io.dz2); ldz = 128; x = bp(io.h1); ldx = 128; mb = tile / 4; kb = tile % 4;
+    } else if (tile < kAgT2 + kAgT1) {   // hidden_layer: dz1 [R][128], h0 [R][256]
+      const int u = tile - kAgT2;
+      dz = bp(io.dz1); ldz = 128; x = bp(io.h0); ldx = 256; mb = u / 8; kb = u % 8;
+    } else {   // encoder image: dz0 [R][256], xb [R][32]
+      dz = bp(io.dz0); ldz = 256; x = bp(io.xb); ldx = 32; mb = tile - kAgT2 - kAgT1; kb = 0;
+    }
+    const bool bias = kb == 0;
+    float v[4], vb;
+    if (!ag_tile(dz + mb * 32, ldz, x + kb * 32, ldx, R, s * kAgRS, bias, S, s,
+                 work + static_cast<size_t>(tile) * S * kAgSlab, io.counters + tile, L, v, vb))
+      return;
+    if (tile < kAgT2 + kAgT1) {
+      float* dw = tile < kAgT2 ? io.w2_grad : io.w1_grad;
+      float* db = tile < kAgT2 ? io.b2_grad : io.b1_grad;
+      double sq = 0.0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int e = t + kAgT * j, m = e >> 5, k = e & 31;
+        dw[(mb * 32 + m) * ldx + kb * 32 + k] = v[j];
+        sq += static_cast<double>(v[j]) * v[j];
+      }
+      if (bias && t < 32) {
+        db[mb * 32 + t] = vb;
+        sq += static_cast<double>(vb) * vb;
+      }
+      sq = ag_block_sum(sq, L);
+      if (t == 0 && io.norm_parts != nullptr) io.norm_parts[tile] = sq;
+      return;
+    }
+    // encoder image tile: to the shared image, then the last of the eight folds it
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = t + kAgT * j, m = e >> 5, k = e & 31;
+      st_sc1(enc_img + (mb * 32 + m) * 32 + k, v[j]);
+    }
+    if (t < 32) st_sc1(enc_img + 256 * 32 + mb * 32 + t, vb);
+    if (!ag_arrive(io.counters + kAgCtrEnc, kAgTE, L)) return;
+    double sq = 0.0;
+    for (int i = t; i < kAgEncOut; i += kAgT) {
+      float r;
+      if (i < 56 * 7) {
+        r = ld_sc1(enc_img + (i / 7) * 32 + i % 7);
+      } else if (i < 56 * 8) {
+        r = ld_sc1(enc_img + 256 * 32 + (i - 56 * 7));
+      } else if (i < 56 * 8 + 40 * 5) {
+        const int u = i - 56 * 8, j = u / 5, c = u % 5;
+        r = 0.f;
+#pragma unroll
+        for (int o = 0; o < 5; ++o) r += ld_sc1(enc_img + (56 + 40 * o + j) * 32 + 7 + 5 * o + c);
+      } else {
+        const int j = i - 56 * 8 - 40 * 5;
+        r = 0.f;
+#pragma unroll
+        for (int o = 0; o < 5; ++o) r += ld_sc1(enc_img + 256 * 32 + 56 + 40 * o + j);
+      }
+      io.enc_grad[i] = r;
+      sq += static_cast<double>(r) * r;
+    }
+    sq = ag_block_sum(sq, L);
+    if (t == 0 && io.norm_parts != nullptr) io.norm_parts[kAgSlotEnc] = sq;
+    return;
+  }
+  if (b < kAgTiles * S + S) {   // output layer: dWo[a][k] = sum_r dout[r][a] h2[r][k], dbo[a] = sum_r dout[r][a]
+    const int s = b - kAgTiles * S;
+    const int c8 = t & 15, rr = t >> 4;
+    const int r0 = s * kAgRS, r1 = min(R, r0 + kAgRS);
+    float a0[8], a1[8], b0 = 0.f, b1 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a0[j] = a1[j] = 0.f;
+    const elem_t* h2 = bp(io.h2);
+    for (int r = r0 + rr; r < r1; r += 16 * 4) {
+      float2 d[4];
+      frag8 hv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {   // four rows' loads in flight
+        const int ru = r + 16 * u < r1 ? r + 16 * u : r;
+        d[u] = *reinterpret_cast<const float2*>(io.dout + 2 * static_cast<int64_t>(ru));
+        hv[u] = *reinterpret_cast<const frag8*>(h2 + static_cast<int64_t>(ru) * 128 + c8 * 8);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (r + 16 * u >= r1) break;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float hj = static_cast<float>(hv[u][j]);
+          a0[j] += d[u].x * hj;
+          a1[j] += d[u].y * hj;
+        }
+        b0 += d[u].x;
+        b1 += d[u].y;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      L.u.out[rr][c8][j] = a0[j];
+      L.u.out[rr][c8][8 + j] = a1[j];
+    }
+    L.u.out[rr][c8][16] = b0;
+    L.u.out[rr][c8][17] = b1;
+    __syncthreads();
+    float vo[2] = {0.f, 0.f};
+    float* my = out_slabs + static_cast<size_t>(s) * kAgOutSlab;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int o = t + kAgT * q;
+      if (o >= kAgOutSlab) break;
+      int c, j;
+      if (o < 256) { c = (o & 127) >> 3; j = (o >> 7) * 8 + (o & 7); }
+      else { c = 0; j = 16 + (o - 256); }
+      float x0 = 0.f;
+      for (int u = 0; u < 16; ++u) x0 += L.u.out[u][c][j];
+      vo[q] = x0;
+      if (S > 1) st_sc1(my + o, x0);
+    }
+    if (S > 1 && !ag_arrive(io.counters + kAgCtrOut, S, L)) return;
+    double sq = 0.0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int o = t + kAgT * q;
+      if (o >= kAgOutSlab) break;
+      float x0 = 0.f;
+      for (int s2 = 0; s2 < S; ++s2) x0 += s2 == s ? vo[q] : ld_sc1(out_slabs + static_cast<size_t>(s2) * kAgOutSlab + o);
+      if (o < 256) io.wo_grad[o] = x0;   // output_layer.weight [2][128]
+      else io.bo_grad[o - 256] = x0;
+      sq += static_cast<double>(x0) * x0;
+    }
+    sq = ag_block_sum(sq, L);
+    if (t == 0 && io.norm_parts != nullptr) io.norm_parts[kAgSlotOut] = sq;
+    return;
+  }
+  // the actor loss: sum of the per-tile partials in a fixed order
+  if (io.loss_out == nullptr || io.tile_loss == nullptr) return;
+  float acc = 0.f;
+  acc = strided_sum<float>(io.tile_loss, t, io.n_loss, kAgT, acc);
+  const double tot = ag_block_sum(static_cast<double>(acc), L);
+  if (t == 0) io.loss_out[0] = static_cast<float>(tot);
+}
+
+int ag_splits(int B) { return (B + kAgRS - 1) / kAgRS; }
+
 }  // namespace
 
 int launch_partial_sum(const float* partial, int groups, int nw, int nb, float* dw, float* db, int accumulate,
@@ -769,4 +1088,30 @@ extern "C" int asvrl_linear_wgrad_vec(const float* dq, int64_t ldq, const void* 
   if (int rc = asvrl_linear_wgrad_vec_partial(dq, ldq, x, ldx, R, K, work, work_floats, &groups, stream)) return rc;
   if (groups == 0) return 0;
   return launch_partial_sum(work, groups, K, 1, dw, db, accumulate, as_stream(stream));
+}
+
+extern "C" int64_t asvrl_actor_grads_workspace(int32_t B) {
+  if (B <= 0) return 0;
+  const int64_t S = ag_splits(B);
+  return static_cast<int64_t>(kAgTiles) * S * kAgSlab + S * kAgOutSlab + kAgEncImg;
+}
+extern "C" int32_t asvrl_actor_grads_counters(void) { return kAgCounters; }
+extern "C" int32_t asvrl_actor_grads_norm_parts(void) { return kAgSlots; }
+
+extern "C" int asvrl_actor_grads(const AsvActorGradIO* io, void* stream) {
+  ASVRL_REQUIRE(io && io->xb && io->h0 && io->h1 && io->h2 && io->dout && io->dz2 && io->dz1 && io->dz0,
+                "asvrl_actor_grads: null activation");
+  ASVRL_REQUIRE(io->w1_grad && io->b1_grad && io->w2_grad && io->b2_grad && io->wo_grad && io->bo_grad && io->enc_grad,
+                "asvrl_actor_grads: null gradient");
+  ASVRL_REQUIRE(io->work && io->counters, "asvrl_actor_grads: null workspace");
+  ASVRL_REQUIRE(io->B >= 0 && io->n_loss >= 0, "asvrl_actor_grads: negative size");
+  ASVRL_REQUIRE(io->work_floats >= asvrl_actor_grads_workspace(io->B), "asvrl_actor_grads: workspace too small");
+  for (const void* p : {io->xb, io->h0, io->h1, io->h2, io->dz2, io->dz1, io->dz0})
+    ASVRL_REQUIRE(reinterpret_cast<uintptr_t>(p) % 16 == 0, "asvrl_actor_grads: activations must be 16-byte aligned");
+  ASVRL_REQUIRE(reinterpret_cast<uintptr_t>(io->dout) % 8 == 0, "asvrl_actor_grads: dout must be 8-byte aligned");
+  if (io->B == 0) return 0;
+  AgArgs a{*io, ag_splits(io->B)};
+  const int blocks = (kAgTiles + 1) * a.S + 1;
+  hipLaunchKernelGGL(actor_grads_kernel, dim3(blocks), dim3(kAgT), 0, as_stream(stream), a);
+  return check_launch("asvrl_actor_grads");
 }

@@ -182,6 +182,45 @@ def actor_backward(pack, bufs, stream=None):
                "asvrl_actor_backward", pack.L)
 
 
+class ActorGrads:
+    """Workspace of asvrl_actor_grads for one ActorBuffers (B rows): the split slabs, the arrival
+    counters (zero, and left zero by every launch) and the squared-norm partials for asvrl_adam_step."""
+
+    def __init__(self, B, device, operands="bf16"):
+        self.L = _abi.lib(operands)
+        self.work = torch.empty(int(self.L.asvrl_actor_grads_workspace(B)), dtype=torch.float32, device=device)
+        self.counters = torch.zeros(int(self.L.asvrl_actor_grads_counters()), dtype=torch.int32, device=device)
+        self.nparts = int(self.L.asvrl_actor_grads_norm_parts())
+        self.norm_parts = torch.zeros(self.nparts, dtype=torch.float64, device=device)
+
+
+def actor_grads(ws, bufs, actor, tile_loss=None, loss_out=None, step=None, norm=True, stream=None):
+    """Every .grad of `actor` (hidden_layer, hidden_layer_2, output_layer, both observation encoders, whose
+    four gradients must be contiguous: FusedAdam / FlatGrads) from bufs' backward outputs and saved
+    activations, the loss sum(tile_loss) -> loss_out, the norm partials (ws.norm_parts) and step += 1, in ONE
+    launch (asvrl_actor_grads; agent.py:424-426)."""
+    se, oe = actor.self_encoder[0], actor.object_encoder[0]
+    gs = [se.weight.grad, se.bias.grad, oe.weight.grad, oe.bias.grad]
+    if not all(gs[k].data_ptr() + 4 * gs[k].numel() == gs[k + 1].data_ptr() for k in range(3)):
+        raise RuntimeError("actor_grads needs the encoder gradients contiguous (FusedAdam / FlatGrads)")
+    io = _abi.AsvActorGradIO()
+    io.xb, io.h0, io.h1, io.h2, io.dout = (bufs.xb.data_ptr(), bufs.h0.data_ptr(), bufs.h1.data_ptr(),
+                                           bufs.h2.data_ptr(), bufs.dout.data_ptr())
+    io.dz2, io.dz1, io.dz0 = bufs.dz2.data_ptr(), bufs.dz1.data_ptr(), bufs.dz0.data_ptr()
+    io.B = bufs.B
+    if tile_loss is not None and loss_out is not None:
+        io.n_loss, io.tile_loss, io.loss_out = tile_loss.numel(), tile_loss.data_ptr(), loss_out.data_ptr()
+    h1l, h2l, ol = actor.hidden_layer, actor.hidden_layer_2, actor.output_layer
+    io.w1_grad, io.b1_grad = h1l.weight.grad.data_ptr(), h1l.bias.grad.data_ptr()
+    io.w2_grad, io.b2_grad = h2l.weight.grad.data_ptr(), h2l.bias.grad.data_ptr()
+    io.wo_grad, io.bo_grad = ol.weight.grad.data_ptr(), ol.bias.grad.data_ptr()
+    io.enc_grad = gs[0].data_ptr()
+    io.norm_parts = ws.norm_parts.data_ptr() if norm else None
+    io.step = _p(step)
+    io.work, io.work_floats, io.counters = ws.work.data_ptr(), ws.work.numel(), ws.counters.data_ptr()
+    _abi.check(ws.L.asvrl_actor_grads(C.byref(io), _abi.stream_ptr(stream)), "asvrl_actor_grads", ws.L)
+
+
 def encoder_fold(dw, db, net, accumulate=False, stream=None):
     """256 x 32 encoder-image gradient -> self_encoder / object_encoder .grad."""
     se, oe = net.self_encoder[0], net.object_encoder[0]

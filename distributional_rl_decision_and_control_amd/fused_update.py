@@ -1,5 +1,5 @@
 """The whole AC-IQN update (Agent.train_AC_IQN, agent.py:386-432) on hand-written gfx950
-kernels: ten launches per step (with the vectorised loop's fused prologue), no torch autograd, no host
+kernels: nine launches per step (with the vectorised loop's fused prologue), no torch autograd, no host
 synchronisation.
 
 Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | done):
@@ -19,7 +19,7 @@ Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | 
     encoders(s, a) + trunk forward + backward of -mean(q) to the action
                                                           asvrl_critic_actor_grad (dA in-kernel)
     actor backward                                       asvrl_actor_backward
-    actor weight grads                                   ONE asvrl_linear_wgrad_multi, one asvrl_partial_sums_norm
+    every actor .grad, the actor loss, the norm partials  ONE asvrl_actor_grads (split tiles reduced in-launch)
     clip + Adam + re-pack                                asvrl_adam_step_pack
 (supported() admits only shapes the fused critic launch takes: B a multiple of 32, so B*N one of its
 64-row round.)
@@ -36,7 +36,9 @@ import torch
 
 from . import _abi
 from .fused_critic import CriticPack, PartialArena, critic_actor_grad, critic_forward, critic_train_fused
-from .fused_mlp import ActorBuffers, MlpPack, actor_act, actor_backward, actor_forward, actor_train_forward
+from .fused_mlp import (ActorBuffers, ActorGrads, MlpPack, actor_act, actor_backward, actor_forward,
+                        actor_train_forward)
+from .fused_mlp import actor_grads as actor_grads_launch
 from .learner import FusedAdam, clip_and_step
 
 OBS = 40
@@ -70,6 +72,7 @@ class FusedACIQNState:
         self.actor = MlpPack(policy_local.actor, "actor", operands)
         self.target_actor = MlpPack(policy_target.actor, "actor", operands)
         self.abufs = ActorBuffers(B, dev, operands)
+        self.agrads = ActorGrads(B, dev, operands)
         f = dict(dtype=torch.float32, device=dev)
         bf = dict(dtype=_abi.operand_dtype(operands), device=dev)
         self.na = torch.empty(B, 2, **f)
@@ -155,12 +158,14 @@ def learn_prologue(st, replay, taus, seed, counter_dev=None, counter=0, out=None
 
 
 def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, actor_grads, rows, gamma=0.99,
-                         taus=None, sync=None, max_norm=0.5, actor_wait=None, counter=None, prologue_done=False):
+                         taus=None, sync=None, max_norm=0.5, actor_wait=None, counter=None, prologue_done=False,
+                         mid_hook=None):
     """One AC-IQN update from replay rows [B][88]. taus: (3, B, N) or None (drawn here).
     actor_wait: event to wait for before the actor's weights change (a concurrent act kernel).
     counter: an int64 device scalar incremented after the step (the learn counter; in-kernel when
     the optimiser step is fused). prologue_done: learn_prologue already ran the actor's TRAIN forward and
-    the target actor on these rows.
+    the target actor on these rows. mid_hook: called right after the fused critic launch (the chained
+    schedule's roll_gate issues the rollout there).
     Returns (critic_loss, actor_loss, critic_grad_norm, actor_grad_norm) as device scalars."""
     B, N = st.B, st.N
     critic, actor = policy_local.critic, policy_local.actor
@@ -190,6 +195,8 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
         with arena.batch():   # the encoders' gradients from the per-sample dzF / dzG
             arena.fold(st.dzF, st.xb, critic)
             arena.small(st.dzG, a_rows, ae.weight.grad, ae.bias.grad)
+    if mid_hook is not None:
+        mid_hook()
     arena.scalar(st.tile_loss[0], st.losses[0:1])   # the critic loss
     cgn = _reduce_and_step(arena, critic_opt, critic_grads, sync, max_norm, pack=st.local_trunk)
 
@@ -197,14 +204,24 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     critic_actor_grad(st.local_trunk, None, None, taus[2], N, st.q_pi, w_ae=ae.weight, dA=ab.dA,
                       tile_loss=st.tile_loss[1], obs=s_rows, act=ab.a_out)
     actor_backward(st.actor, ab)
-    ow, obias = actor.output_layer.weight.grad, actor.output_layer.bias.grad
-    with arena.batch():
-        arena.linear(ab.dz2, ab.h1, actor.hidden_layer_2.weight.grad, actor.hidden_layer_2.bias.grad)
-        arena.vec(ab.dout[:, 0], ab.h2, ow[0], obias[0:1])
-        arena.linear(ab.dz1, ab.h0, actor.hidden_layer.weight.grad, actor.hidden_layer.bias.grad)
-        arena.vec(ab.dout[:, 1], ab.h2, ow[1], obias[1:2])
-        arena.fold(ab.dz0, ab.xb, actor)
-    arena.scalar(st.tile_loss[1], st.losses[1:2])   # the actor loss
-    agn = _reduce_and_step(arena, actor_opt, actor_grads, sync, max_norm, wait=actor_wait, pack=st.actor,
-                           counter=counter)
+    # every actor .grad, the actor loss, the norm partials and the Adam step count in one launch
+    fused_opt = sync is None and isinstance(actor_opt, FusedAdam)
+    actor_grads_launch(st.agrads, ab, actor, st.tile_loss[1], st.losses[1:2],
+                       step=actor_opt.step_t if fused_opt else None, norm=fused_opt)
+    if fused_opt:
+        if actor_wait is not None:
+            torch.cuda.current_stream().wait_event(actor_wait)
+        if not hasattr(st.actor, "_adam_segs"):
+            st.actor._adam_segs = st.actor.adam_segments(actor_opt)
+        agn = actor_opt.step_prenormed(st.agrads.norm_parts, st.agrads.nparts, pack=st.actor._adam_segs,
+                                       counter=counter)
+    else:
+        if sync is not None:
+            sync(actor_grads)
+        if actor_wait is not None:
+            torch.cuda.current_stream().wait_event(actor_wait)
+        agn = clip_and_step(actor_opt, actor_grads, max_norm)
+        st.actor.refresh()
+        if counter is not None:
+            counter += 1
     return st.losses[0], st.losses[1], cgn, agn

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 18
+#define ASVRL_ABI_VERSION 19
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -720,6 +720,47 @@ typedef struct AsvWgradSeg {
   int64_t partial_floats;
 } AsvWgradSeg;
 int asvrl_linear_wgrad_multi(const AsvWgradSeg* segs, int32_t nseg, int32_t* groups_out, void* stream);
+
+/* Every gradient of the Actor (AC_IQN_model.py:284-321) after asvrl_actor_backward, in ONE launch (ABI 19;
+ * replaces asvrl_linear_wgrad_multi + asvrl_partial_sums_norm of agent.py:424-426's actor_loss.backward()):
+ * hidden_layer / hidden_layer_2 weight and bias grads, output_layer's, the two observation encoders' (folded
+ * from the 256 x 32 encoder image over the five object copies), the actor loss (sum of n_loss per-tile
+ * partials), the squared-norm partials clip_grad_norm_ folds (asvrl_adam_step's norm_parts) and the Adam
+ * step count (*step += 1). Each 32 x 32 output tile is reduced over S row splits by the split that arrives
+ * last, in split order: deterministic, no partial buffer for another launch. Activations (operand dtype,
+ * contiguous, 16-byte aligned): xb [B][32], h0 [B][256], h1, h2, dz2, dz1 [B][128], dz0 [B][256]; dout f32
+ * [B][2]. Gradients f32, row-major as the nn.Linear parameters; enc_grad = self_w 56x7 | self_b 56 |
+ * obj_w 40x5 | obj_b 40. work: asvrl_actor_grads_workspace(B) floats; counters:
+ * asvrl_actor_grads_counters() ints, zero before the first launch (each launch leaves them zero). */
+typedef struct AsvActorGradIO {
+  const void* xb;
+  const void* h0;
+  const void* h1;
+  const void* h2;
+  const float* dout;
+  const void* dz2;
+  const void* dz1;
+  const void* dz0;
+  int32_t B, n_loss;
+  const float* tile_loss;   /* optional (with loss_out) */
+  float* loss_out;
+  float* w1_grad;           /* hidden_layer [128][256], [128] */
+  float* b1_grad;
+  float* w2_grad;           /* hidden_layer_2 [128][128], [128] */
+  float* b2_grad;
+  float* wo_grad;           /* output_layer [2][128], [2] */
+  float* bo_grad;
+  float* enc_grad;          /* [688] */
+  double* norm_parts;       /* optional: asvrl_actor_grads_norm_parts() slots */
+  float* step;              /* optional */
+  float* work;
+  int64_t work_floats;
+  int32_t* counters;
+} AsvActorGradIO;
+int64_t asvrl_actor_grads_workspace(int32_t B);
+int32_t asvrl_actor_grads_counters(void);
+int32_t asvrl_actor_grads_norm_parts(void);
+int asvrl_actor_grads(const AsvActorGradIO* io, void* stream);
 
 /* One output unit's version: dw[k] = sum_r dq[r*ldq] x[r][k], db = sum_r dq[r*ldq] with dq f32 and
  * x bf16 (R x K, ldx); K in {64, 128, 256}; work >= 256 * (K + 1) floats. */
