@@ -6,8 +6,7 @@
 //   2. adam_kernel : every block folds the partials in the same fixed order (so all blocks
 //      see the identical norm), scales g by min(1, max_norm / (norm + 1e-6)) in place, as
 //      clip_grad_norm_ does, then applies Adam with the bias corrections of the new step.
-#include "asvrl_common.h"
-#include "asvrl_mfma.h"
+#include "asvrl_adam.h"
 
 namespace asvrl {
 namespace {
@@ -18,39 +17,6 @@ constexpr int kOptThreads = 256;
 #define ASVRL_ADAM_PER_THREAD 1
 #endif
 constexpr int64_t kAdamPer = ASVRL_ADAM_PER_THREAD;   // parameters per thread (grid size), at most 1024 blocks
-
-struct PackTable {
-  AsvPackSeg s[ASVRL_MAX_PACK_SEGS];
-  int n;
-};
-
-// Position of W[row][col] in an (M x K) A-operand fragment image: the inverse of frag_rc
-// (asvrl_mfma.h): o = ((mb*KS + ks)*64 + lane)*8 + j with lane = 32h + (row & 31).
-__device__ __forceinline__ int64_t frag_pos(int row, int col, int K, bool chained) {
-  const int mb = row >> 5, ks = col >> 4, c = col & 15;
-  const int h = chained ? ((c >> 2) & 1) : (c >> 3);
-  const int j = chained ? (((c >> 3) << 2) | (c & 3)) : (c & 7);
-  const int lane = 32 * h + (row & 31);
-  return (static_cast<int64_t>(mb) * (K >> 4) + ks) * 512 + lane * 8 + j;
-}
-
-// The updated parameter i into every image position a pack table gives it (asvrl_critic_pack /
-// asvrl_mlp_pack / asvrl_iqn_pack write the same values from the same f32 weights).
-__device__ __forceinline__ void pack_param(const PackTable& t, int64_t i, float p) {
-  for (int k = 0; k < t.n; ++k) {
-    const AsvPackSeg& g = t.s[k];
-    const int64_t u64 = i - g.flat_off;
-    if (u64 < 0 || u64 >= static_cast<int64_t>(g.rows) * g.cols) continue;
-    const unsigned u = static_cast<unsigned>(u64), cols = static_cast<unsigned>(g.cols);   // 32-bit division
-    const int r = static_cast<int>(u / cols), c = static_cast<int>(u - static_cast<unsigned>(r) * cols);
-    for (int q = 0; q < g.nrep; ++q) {
-      int R = g.row0 + r + q * g.rep_row, Cc = g.col0 + c + q * g.rep_col;
-      if (g.transposed) { const int x = R; R = Cc; Cc = x; }
-      if (g.f32) static_cast<float*>(g.image)[R] = p;
-      else static_cast<elem_t*>(g.image)[frag_pos(R, Cc, g.K, g.chained != 0)] = static_cast<elem_t>(p);
-    }
-  }
-}
 
 __global__ __launch_bounds__(kOptThreads) void sumsq_kernel(const float* __restrict__ g, int64_t n,
                                                              double* __restrict__ partial, float* step) {
@@ -81,7 +47,7 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(float* __restrict__ p
                                                             float beta2, float eps, float max_norm,
                                                             float* __restrict__ norm_out, PackTable pk,
                                                             int64_t* __restrict__ counter) {
-  __shared__ float s_coef;
+  __shared__ float s_norm;
   __shared__ double s_red[kOptThreads];
   // this thread's first parameter, its moments and gradient loaded before the norm fold (they do not
   // depend on it: one memory round trip fewer on the launch's critical path)
@@ -104,33 +70,19 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(float* __restrict__ p
     }
     if (threadIdx.x == 0) {
       const float norm = static_cast<float>(sqrt(s_red[0]));
-      float coef = 1.f;
-      if (max_norm > 0.f) {
-        coef = max_norm / (norm + 1e-6f);   // clip_grad_norm_: clip_coef, clamped to 1
-        coef = coef < 1.f ? coef : 1.f;
-      }
-      s_coef = coef;
+      s_norm = norm;
       if (blockIdx.x == 0 && norm_out != nullptr) norm_out[0] = norm;
     }
   }
   __syncthreads();
-  const float coef = s_coef;
-  const double t = static_cast<double>(step[0]);
-  const float step_size = static_cast<float>(static_cast<double>(lr) / (1.0 - pow(static_cast<double>(beta1), t)));
-  const float bc2_sqrt = static_cast<float>(sqrt(1.0 - pow(static_cast<double>(beta2), t)));
-  const float w1 = static_cast<float>(1.0 - static_cast<double>(beta1));
-  const float w2 = static_cast<float>(1.0 - static_cast<double>(beta2));
+  const AdamCoef ac = adam_coef(s_norm, static_cast<double>(step[0]), lr, beta1, beta2, max_norm);
   for (int64_t i = i0; i < n; i += static_cast<int64_t>(gridDim.x) * kOptThreads) {
     const bool first = i == i0;
-    const float gi = (first ? g0 : g[i]) * coef;
-    const float mo = first ? m0 : m[i], vo = first ? v0 : v[i], po = first ? p0 : p[i];
+    float mo = first ? m0 : m[i], vo = first ? v0 : v[i], gi;
+    const float pn = adam_elem(ac, beta2, eps, first ? g0 : g[i], mo, vo, first ? p0 : p[i], gi);
     g[i] = gi;
-    const float mi = mo + w1 * (gi - mo);          // exp_avg.lerp_(grad, 1 - beta1)
-    const float vi = vo * beta2 + w2 * gi * gi;    // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
-    m[i] = mi;
-    v[i] = vi;
-    const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    const float pn = po - step_size * (mi / denom);  // param.addcdiv_(exp_avg, denom, -step_size)
+    m[i] = mo;
+    v[i] = vo;
     p[i] = pn;
     if (pk.n > 0) pack_param(pk, i, pn);
   }

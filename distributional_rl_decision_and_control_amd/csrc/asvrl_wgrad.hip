@@ -13,8 +13,7 @@
 // workgroups write f32 partials that a second launch sums in a fixed order (deterministic).
 // The f32 build (ASVRL_OPERAND_F32, asvrl_mfma.h) stages f32 rows (4 per 16-byte chunk) and reads
 // its operand fragments with plain LDS loads into the eight v_mfma_f32_32x32x2_f32 of mfma().
-#include "asvrl_common.h"
-#include "asvrl_mfma.h"
+#include "asvrl_adam.h"
 
 #include <algorithm>
 
@@ -739,28 +738,130 @@ __device__ __forceinline__ bool ag_tile(const elem_t* __restrict__ dz, int ldz, 
   }
   if (S == 1) return true;
   if (!ag_arrive(cnt, S, L)) return false;
-  // the S slabs in split order (this workgroup's own from registers)
-  float a[4] = {0.f, 0.f, 0.f, 0.f}, ab = 0.f;
-  for (int s2 = 0; s2 < S; ++s2) {
-    const float* p = slabs + static_cast<size_t>(s2) * kAgSlab;
-    float u[4], ub = 0.f;
+  // the S slabs in split order (this workgroup's own read back too), eight slabs' loads in flight at a time
+  float acc4[4] = {0.f, 0.f, 0.f, 0.f}, accbs = 0.f;
+  for (int s0 = 0; s0 < S; s0 += 8) {
+    float u[8][4], ub[8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) u[j] = s2 == s ? v[j] : ld_sc1(p + t + kAgT * j);
-    if (bias && t < 32) ub = s2 == s ? vb : ld_sc1(p + 1024 + t);
+    for (int q = 0; q < 8; ++q) {
+      const float* p = slabs + static_cast<size_t>(s0 + q < S ? s0 + q : s0) * kAgSlab;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) a[j] = s2 == 0 ? u[j] : a[j] + u[j];
-    ab = s2 == 0 ? ub : ab + ub;
+      for (int j = 0; j < 4; ++j) u[q][j] = ld_sc1(p + t + kAgT * j);
+      ub[q] = bias && t < 32 ? ld_sc1(p + 1024 + t) : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      if (s0 + q >= S) break;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc4[j] = s0 + q == 0 ? u[q][j] : acc4[j] + u[q][j];
+      accbs = s0 + q == 0 ? ub[q] : accbs + ub[q];
+    }
   }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) v[j] = a[j];
-  vb = ab;
+  for (int j = 0; j < 4; ++j) v[j] = acc4[j];
+  vb = accbs;
   return true;
 }
 
 struct AgArgs {
   AsvActorGradIO io;
   int S;
+  int adam;                 // 1: the clip + Adam step of the actor's FusedAdam runs in this launch
+  AsvActorAdam ad;
+  PackTable pk;
 };
+
+// The finalizers (every tile's last split, the encoder fold, the output layer): kAgSlots of them.
+constexpr int kAgCtrArrive = kAgCounters, kAgCtrDone = kAgCounters + 1, kAgCtrLeave = kAgCounters + 2,
+              kAgCtrErr = kAgCounters + 3, kAgCountersAdam = kAgCounters + 4;
+constexpr int kAgMaxEl = 5;   // outputs per thread of a finalizer (tile: 4 + bias)
+
+// A finalizer's outputs (thread t: n of them, gradient addresses and values): the squared norm of the
+// finalizer into norm_parts[slot]; without the fused optimiser the gradients are stored. With it, every
+// finalizer waits for all kAgSlots partials (its parameters' moments loaded meanwhile), folds them exactly as
+// adam_kernel does (asvrl_optim.hip), and applies clip + Adam + re-pack to its own outputs; the last to leave
+// advances step / norm_out / counter. All finalizers are resident while they wait: the grid fits the chip
+// (two 67 KB workgroups per CU) and the other kernels of a step all finish.
+__device__ __forceinline__ void ag_finish(const AgArgs& a, float* const (&dst)[kAgMaxEl], const float (&val)[kAgMaxEl],
+                                          int n, int slot, AgLds& L) {
+  const AsvActorGradIO& io = a.io;
+  const int t = threadIdx.x;
+  double sq = 0.0;
+#pragma unroll
+  for (int e = 0; e < kAgMaxEl; ++e)
+    if (e < n) sq += static_cast<double>(val[e]) * val[e];
+  if (!a.adam) {
+#pragma unroll
+    for (int e = 0; e < kAgMaxEl; ++e)
+      if (e < n) *dst[e] = val[e];
+    sq = ag_block_sum(sq, L);
+    if (t == 0 && io.norm_parts != nullptr) io.norm_parts[slot] = sq;
+    return;
+  }
+  const AsvActorAdam& ad = a.ad;
+  int64_t fi[kAgMaxEl];
+  float mo[kAgMaxEl], vo[kAgMaxEl], po[kAgMaxEl];
+#pragma unroll
+  for (int e = 0; e < kAgMaxEl; ++e) {   // the moments and parameters, in flight under the wait
+    fi[e] = e < n ? dst[e] - ad.grads : 0;
+    mo[e] = ad.exp_avg[fi[e]];
+    vo[e] = ad.exp_avg_sq[fi[e]];
+    po[e] = ad.params[fi[e]];
+  }
+  const float step_old = ad.step[0];   // advanced by the last finalizer to leave, after every read
+  sq = ag_block_sum(sq, L);
+  int* ctr = io.counters;
+  if (t == 0) {
+    __hip_atomic_store(io.norm_parts + slot, sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int o = __hip_atomic_fetch_add(ctr + kAgCtrArrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (o == kAgSlots - 1) {
+      __hip_atomic_store(ctr + kAgCtrArrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctr + kAgCtrDone, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      int spins = 0;
+      while (__hip_atomic_load(ctr + kAgCtrDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1 << 24)) {   // never expected: flag it and go on rather than hang the device
+          __hip_atomic_store(ctr + kAgCtrErr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // adam_kernel's fold: thread t takes partial t (kAgSlots < 256), then the same pairwise tree
+  L.red[t] = t < kAgSlots ? __hip_atomic_load(io.norm_parts + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+  __syncthreads();
+  for (int w = kAgT / 2; w > 0; w >>= 1) {
+    if (t < w) L.red[t] += L.red[t + w];
+    __syncthreads();
+  }
+  const float norm = static_cast<float>(sqrt(L.red[0]));
+  const AdamCoef ac = adam_coef(norm, static_cast<double>(step_old) + 1.0, ad.lr, ad.beta1, ad.beta2, ad.max_norm);
+#pragma unroll
+  for (int e = 0; e < kAgMaxEl; ++e) {
+    if (e >= n) break;
+    float gi;
+    const float pn = adam_elem(ac, ad.beta2, ad.eps, val[e], mo[e], vo[e], po[e], gi);
+    *dst[e] = gi;
+    ad.exp_avg[fi[e]] = mo[e];
+    ad.exp_avg_sq[fi[e]] = vo[e];
+    ad.params[fi[e]] = pn;
+    if (a.pk.n > 0) pack_param(a.pk, fi[e], pn);
+  }
+  __syncthreads();
+  if (t == 0) {
+    const int o = __hip_atomic_fetch_add(ctr + kAgCtrLeave, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (o == kAgSlots - 1) {
+      __hip_atomic_store(ctr + kAgCtrLeave, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctr + kAgCtrDone, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ad.step[0] = step_old + 1.f;
+      if (ad.norm_out != nullptr) ad.norm_out[0] = norm;
+      if (ad.counter != nullptr) ad.counter[0] += 1;
+    }
+  }
+}
 
 __global__ __launch_bounds__(kAgT) void actor_grads_kernel(AgArgs a) {
   __shared__ __attribute__((aligned(16))) AgLds L;
@@ -771,6 +872,13 @@ __global__ __launch_bounds__(kAgT) void actor_grads_kernel(AgArgs a) {
   float* out_slabs = work + static_cast<size_t>(kAgTiles) * S * kAgSlab;
   float* enc_img = out_slabs + static_cast<size_t>(S) * kAgOutSlab;
   if (b == 0 && t == 0 && io.step != nullptr) io.step[0] += 1.f;   // read by the Adam launch
+  float* dst[kAgMaxEl];
+  float val[kAgMaxEl];
+#pragma unroll
+  for (int e = 0; e < kAgMaxEl; ++e) {
+    dst[e] = nullptr;
+    val[e] = 0.f;
+  }
   if (b < kAgTiles * S) {
     const int tile = b / S, s = b % S;
     const elem_t *dz, *x;
@@ -791,19 +899,16 @@ __global__ __launch_bounds__(kAgT) void actor_grads_kernel(AgArgs a) {
     if (tile < kAgT2 + kAgT1) {
       float* dw = tile < kAgT2 ? io.w2_grad : io.w1_grad;
       float* db = tile < kAgT2 ? io.b2_grad : io.b1_grad;
-      double sq = 0.0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int e = t + kAgT * j, m = e >> 5, k = e & 31;
-        dw[(mb * 32 + m) * ldx + kb * 32 + k] = v[j];
-        sq += static_cast<double>(v[j]) * v[j];
+        dst[j] = dw + (mb * 32 + m) * ldx + kb * 32 + k;
+        val[j] = v[j];
       }
-      if (bias && t < 32) {
-        db[mb * 32 + t] = vb;
-        sq += static_cast<double>(vb) * vb;
-      }
-      sq = ag_block_sum(sq, L);
-      if (t == 0 && io.norm_parts != nullptr) io.norm_parts[tile] = sq;
+      const int n = bias && t < 32 ? 5 : 4;
+      dst[4] = db + mb * 32 + (t & 31);
+      val[4] = vb;
+      ag_finish(a, dst, val, n, tile, L);
       return;
     }
     // encoder image tile: to the shared image, then the last of the eight folds it
@@ -814,29 +919,47 @@ __global__ __launch_bounds__(kAgT) void actor_grads_kernel(AgArgs a) {
     }
     if (t < 32) st_sc1(enc_img + 256 * 32 + mb * 32 + t, vb);
     if (!ag_arrive(io.counters + kAgCtrEnc, kAgTE, L)) return;
-    double sq = 0.0;
-    for (int i = t; i < kAgEncOut; i += kAgT) {
-      float r;
+    // thread t: outputs t, t + 256, t + 512 (< 688), each a sum of 1 or 5 image entries (object order);
+    // every load issued before the sums
+    constexpr int kEncPer = (kAgEncOut + kAgT - 1) / kAgT;
+    float r5[kEncPer][5];
+    int cnt5[kEncPer];
+#pragma unroll
+    for (int q = 0; q < kEncPer; ++q) {
+      const int i = t + kAgT * q;
+      int idx[5], c = 0;
       if (i < 56 * 7) {
-        r = ld_sc1(enc_img + (i / 7) * 32 + i % 7);
+        idx[0] = (i / 7) * 32 + i % 7; c = 1;
       } else if (i < 56 * 8) {
-        r = ld_sc1(enc_img + 256 * 32 + (i - 56 * 7));
+        idx[0] = 256 * 32 + (i - 56 * 7); c = 1;
       } else if (i < 56 * 8 + 40 * 5) {
-        const int u = i - 56 * 8, j = u / 5, c = u % 5;
-        r = 0.f;
+        const int u = i - 56 * 8, j = u / 5, cc = u % 5;
 #pragma unroll
-        for (int o = 0; o < 5; ++o) r += ld_sc1(enc_img + (56 + 40 * o + j) * 32 + 7 + 5 * o + c);
-      } else {
+        for (int o = 0; o < 5; ++o) idx[o] = (56 + 40 * o + j) * 32 + 7 + 5 * o + cc;
+        c = 5;
+      } else if (i < kAgEncOut) {
         const int j = i - 56 * 8 - 40 * 5;
-        r = 0.f;
 #pragma unroll
-        for (int o = 0; o < 5; ++o) r += ld_sc1(enc_img + 256 * 32 + 56 + 40 * o + j);
+        for (int o = 0; o < 5; ++o) idx[o] = 256 * 32 + 56 + 40 * o + j;
+        c = 5;
       }
-      io.enc_grad[i] = r;
-      sq += static_cast<double>(r) * r;
+      cnt5[q] = c;
+#pragma unroll
+      for (int o = 0; o < 5; ++o) r5[q][o] = o < c ? ld_sc1(enc_img + idx[o]) : 0.f;
     }
-    sq = ag_block_sum(sq, L);
-    if (t == 0 && io.norm_parts != nullptr) io.norm_parts[kAgSlotEnc] = sq;
+    int n = 0;
+#pragma unroll
+    for (int q = 0; q < kEncPer; ++q) {
+      if (cnt5[q] == 0) break;
+      float r = r5[q][0];
+#pragma unroll
+      for (int o = 1; o < 5; ++o)
+        if (o < cnt5[q]) r += r5[q][o];
+      dst[q] = io.enc_grad + t + kAgT * q;
+      val[q] = r;
+      n = q + 1;
+    }
+    ag_finish(a, dst, val, n, kAgSlotEnc, L);
     return;
   }
   if (b < kAgTiles * S + S) {   // output layer: dWo[a][k] = sum_r dout[r][a] h2[r][k], dbo[a] = sum_r dout[r][a]
@@ -847,17 +970,17 @@ __global__ __launch_bounds__(kAgT) void actor_grads_kernel(AgArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) a0[j] = a1[j] = 0.f;
     const elem_t* h2 = bp(io.h2);
-    for (int r = r0 + rr; r < r1; r += 16 * 4) {
-      float2 d[4];
-      frag8 hv[4];
+    for (int r = r0 + rr; r < r1; r += 16 * 8) {
+      float2 d[8];
+      frag8 hv[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {   // four rows' loads in flight
+      for (int u = 0; u < 8; ++u) {   // eight rows' loads in flight
         const int ru = r + 16 * u < r1 ? r + 16 * u : r;
         d[u] = *reinterpret_cast<const float2*>(io.dout + 2 * static_cast<int64_t>(ru));
         hv[u] = *reinterpret_cast<const frag8*>(h2 + static_cast<int64_t>(ru) * 128 + c8 * 8);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         if (r + 16 * u >= r1) break;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -892,19 +1015,30 @@ __global__ __launch_bounds__(kAgT) void actor_grads_kernel(AgArgs a) {
       if (S > 1) st_sc1(my + o, x0);
     }
     if (S > 1 && !ag_arrive(io.counters + kAgCtrOut, S, L)) return;
-    double sq = 0.0;
+    const int n = t + kAgT < kAgOutSlab ? 2 : 1;
+    float xo[2] = {0.f, 0.f};
+    for (int s0 = 0; s0 < S; s0 += 8) {
+      float u[8][2];
+#pragma unroll
+      for (int q2 = 0; q2 < 8; ++q2) {
+        const float* p = out_slabs + static_cast<size_t>(s0 + q2 < S ? s0 + q2 : s0) * kAgOutSlab;
+        u[q2][0] = S > 1 ? ld_sc1(p + t) : vo[0];
+        u[q2][1] = t + kAgT < kAgOutSlab ? (S > 1 ? ld_sc1(p + t + kAgT) : vo[1]) : 0.f;
+      }
+#pragma unroll
+      for (int q2 = 0; q2 < 8; ++q2) {
+        if (s0 + q2 >= S) break;
+        xo[0] = s0 + q2 == 0 ? u[q2][0] : xo[0] + u[q2][0];
+        xo[1] = s0 + q2 == 0 ? u[q2][1] : xo[1] + u[q2][1];
+      }
+    }
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int o = t + kAgT * q;
-      if (o >= kAgOutSlab) break;
-      float x0 = 0.f;
-      for (int s2 = 0; s2 < S; ++s2) x0 += s2 == s ? vo[q] : ld_sc1(out_slabs + static_cast<size_t>(s2) * kAgOutSlab + o);
-      if (o < 256) io.wo_grad[o] = x0;   // output_layer.weight [2][128]
-      else io.bo_grad[o - 256] = x0;
-      sq += static_cast<double>(x0) * x0;
+      dst[q] = o < 256 ? io.wo_grad + o : io.bo_grad + (o < kAgOutSlab ? o - 256 : 0);   // output_layer [2][128], [2]
+      val[q] = xo[q];
     }
-    sq = ag_block_sum(sq, L);
-    if (t == 0 && io.norm_parts != nullptr) io.norm_parts[kAgSlotOut] = sq;
+    ag_finish(a, dst, val, n, kAgSlotOut, L);
     return;
   }
   // the actor loss: sum of the per-tile partials in a fixed order
@@ -1095,10 +1229,11 @@ extern "C" int64_t asvrl_actor_grads_workspace(int32_t B) {
   const int64_t S = ag_splits(B);
   return static_cast<int64_t>(kAgTiles) * S * kAgSlab + S * kAgOutSlab + kAgEncImg;
 }
-extern "C" int32_t asvrl_actor_grads_counters(void) { return kAgCounters; }
+extern "C" int32_t asvrl_actor_grads_counters(void) { return kAgCountersAdam; }
 extern "C" int32_t asvrl_actor_grads_norm_parts(void) { return kAgSlots; }
 
-extern "C" int asvrl_actor_grads(const AsvActorGradIO* io, void* stream) {
+namespace {
+int check_actor_grads(const AsvActorGradIO* io) {
   ASVRL_REQUIRE(io && io->xb && io->h0 && io->h1 && io->h2 && io->dout && io->dz2 && io->dz1 && io->dz0,
                 "asvrl_actor_grads: null activation");
   ASVRL_REQUIRE(io->w1_grad && io->b1_grad && io->w2_grad && io->b2_grad && io->wo_grad && io->bo_grad && io->enc_grad,
@@ -1109,9 +1244,43 @@ extern "C" int asvrl_actor_grads(const AsvActorGradIO* io, void* stream) {
   for (const void* p : {io->xb, io->h0, io->h1, io->h2, io->dz2, io->dz1, io->dz0})
     ASVRL_REQUIRE(reinterpret_cast<uintptr_t>(p) % 16 == 0, "asvrl_actor_grads: activations must be 16-byte aligned");
   ASVRL_REQUIRE(reinterpret_cast<uintptr_t>(io->dout) % 8 == 0, "asvrl_actor_grads: dout must be 8-byte aligned");
-  if (io->B == 0) return 0;
-  AgArgs a{*io, ag_splits(io->B)};
+  return 0;
+}
+
+int launch_actor_grads(const AgArgs& a, hipStream_t st) {
   const int blocks = (kAgTiles + 1) * a.S + 1;
-  hipLaunchKernelGGL(actor_grads_kernel, dim3(blocks), dim3(kAgT), 0, as_stream(stream), a);
+  hipLaunchKernelGGL(actor_grads_kernel, dim3(blocks), dim3(kAgT), 0, st, a);
   return check_launch("asvrl_actor_grads");
+}
+}  // namespace
+
+extern "C" int asvrl_actor_grads(const AsvActorGradIO* io, void* stream) {
+  if (int rc = check_actor_grads(io)) return rc;
+  if (io->B == 0) return 0;
+  AgArgs a{};
+  a.io = *io;
+  a.S = ag_splits(io->B);
+  return launch_actor_grads(a, as_stream(stream));
+}
+
+extern "C" int asvrl_actor_grads_adam(const AsvActorGradIO* io, const AsvActorAdam* ad, void* stream) {
+  if (int rc = check_actor_grads(io)) return rc;
+  ASVRL_REQUIRE(ad && ad->params && ad->grads && ad->exp_avg && ad->exp_avg_sq && ad->step,
+                "asvrl_actor_grads_adam: null optimiser argument");
+  ASVRL_REQUIRE(io->norm_parts != nullptr && io->step == nullptr,
+                "asvrl_actor_grads_adam: needs norm_parts, and the step is the optimiser's (io->step = NULL)");
+  ASVRL_REQUIRE(ad->nseg >= 0 && ad->nseg <= ASVRL_MAX_PACK_SEGS && (ad->nseg == 0 || ad->segs != nullptr),
+                "asvrl_actor_grads_adam: bad pack table");
+  for (const float* g : {io->w1_grad, io->b1_grad, io->w2_grad, io->b2_grad, io->wo_grad, io->bo_grad, io->enc_grad})
+    ASVRL_REQUIRE(g >= ad->grads && g < ad->grads + ad->n, "asvrl_actor_grads_adam: a gradient outside the flat buffer");
+  ASVRL_REQUIRE(io->enc_grad + kAgEncOut <= ad->grads + ad->n, "asvrl_actor_grads_adam: encoder grads outside the buffer");
+  if (io->B == 0) return 0;
+  AgArgs a{};
+  a.io = *io;
+  a.S = ag_splits(io->B);
+  a.adam = 1;
+  a.ad = *ad;
+  for (int k = 0; k < ad->nseg; ++k) a.pk.s[k] = ad->segs[k];
+  a.pk.n = ad->nseg;
+  return launch_actor_grads(a, as_stream(stream));
 }
