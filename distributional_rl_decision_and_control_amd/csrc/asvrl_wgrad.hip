@@ -676,45 +676,48 @@ __device__ __forceinline__ double ag_block_sum(double v, AgLds& L) {
   return L.red[0];
 }
 
-// One tile item: dW[32 m][32 k] (+ db[32 m] when bias) over rows [r0, r0 + kAgRS) of dz (columns
-// m0..m0+31) and x (columns k0..k0+31). Returns true in the tile's last arriving workgroup, which then
-// holds the S-split sum: thread t elements t + 256 j (m = e / 32, k = e % 32) in v[j], bias m = t in vb.
+// One tile item: dW[32 m][32 k] (+ db[32 m] when bias) over rows [r0, r0 + nch * kAgRS) of dz (columns
+// m0..m0+31) and x (columns k0..k0+31), nch chunks of kAgRS rows. Returns true in the tile's last arriving
+// workgroup, which then holds the S-split sum: thread t elements t + 256 j (m = e / 32, k = e % 32) in v[j],
+// bias m = t in vb.
 __device__ __forceinline__ bool ag_tile(const elem_t* __restrict__ dz, int ldz, const elem_t* __restrict__ x, int ldx,
-                                        int R, int r0, bool bias, int S, int s, float* slabs, int* cnt, AgLds& L,
-                                        float (&v)[4], float& vb) {
+                                        int R, int r0, int nch, bool bias, int S, int s, float* slabs, int* cnt,
+                                        AgLds& L, float (&v)[4], float& vb) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int rw0 = r0 + w * kAgRW;
   typedef unsigned int u32v4 __attribute__((ext_vector_type(4)));
-  u32v4 vz[kAgNL], vx[kAgNL];
-#pragma unroll
-  for (int i = 0; i < kAgNL; ++i) {   // all of the wave's loads in flight at once
-    const int q = lane + 64 * i, row = q / kAgCPR, c = q % kAgCPR, gr = rw0 + row;
-    const bool ok = gr < R;
-    const int64_t g = ok ? gr : 0;
-    vz[i] = *reinterpret_cast<const u32v4*>(dz + g * ldz + c * kE16);
-    vx[i] = *reinterpret_cast<const u32v4*>(x + g * ldx + c * kE16);
-    if (!ok) vz[i] = vx[i] = u32v4{0u, 0u, 0u, 0u};
-  }
   char* lz = L.u.st.z[w];
   char* lx = L.u.st.x[w];
-#pragma unroll
-  for (int i = 0; i < kAgNL; ++i) {
-    const int q = lane + 64 * i, row = q / kAgCPR, c = q % kAgCPR;
-    *reinterpret_cast<u32v4*>(lz + row * kAgSt + c * 16) = vz[i];
-    *reinterpret_cast<u32v4*>(lx + row * kAgSt + c * 16) = vx[i];
-  }
-  __syncthreads();
   frag8 ones;
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = static_cast<elem_t>(1.0f);
   f32x16 acc = f32x16{}, accb = f32x16{};
+  for (int ch = 0; ch < nch; ++ch) {
+    const int rw0 = r0 + ch * kAgRS + w * kAgRW;
+    u32v4 vz[kAgNL], vx[kAgNL];
 #pragma unroll
-  for (int ks = 0; ks < kAgRW / 16; ++ks) {
-    const frag8 A = frag_tr(lz, kAgSt, ks * 16, 0, lane);
-    acc = mfma(A, frag_tr(lx, kAgSt, ks * 16, 0, lane), acc);
-    if (bias) accb = mfma(A, ones, accb);
+    for (int i = 0; i < kAgNL; ++i) {   // all of the wave's loads in flight at once
+      const int q = lane + 64 * i, row = q / kAgCPR, c = q % kAgCPR, gr = rw0 + row;
+      const bool ok = gr < R;
+      const int64_t g = ok ? gr : 0;
+      vz[i] = *reinterpret_cast<const u32v4*>(dz + g * ldz + c * kE16);
+      vx[i] = *reinterpret_cast<const u32v4*>(x + g * ldx + c * kE16);
+      if (!ok) vz[i] = vx[i] = u32v4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int i = 0; i < kAgNL; ++i) {
+      const int q = lane + 64 * i, row = q / kAgCPR, c = q % kAgCPR;
+      *reinterpret_cast<u32v4*>(lz + row * kAgSt + c * 16) = vz[i];
+      *reinterpret_cast<u32v4*>(lx + row * kAgSt + c * 16) = vx[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < kAgRW / 16; ++ks) {
+      const frag8 A = frag_tr(lz, kAgSt, ks * 16, 0, lane);
+      acc = mfma(A, frag_tr(lx, kAgSt, ks * 16, 0, lane), acc);
+      if (bias) accb = mfma(A, ones, accb);
+    }
+    __syncthreads();   // the staging images are rewritten by the next chunk / reused as the fold area
   }
-  __syncthreads();   // the staging images are reused as the fold area
   const int h = lane >> 5, n = lane & 31;
   float* cw = L.u.cmb[w];
 #pragma unroll
@@ -765,7 +768,7 @@ __device__ __forceinline__ bool ag_tile(const elem_t* __restrict__ dz, int ldz, 
 
 struct AgArgs {
   AsvActorGradIO io;
-  int S;
+  int S, nch;   // row splits, kAgRS-row chunks per split
   int adam;                 // 1: the clip + Adam step of the actor's FusedAdam runs in this launch
   AsvActorAdam ad;
   PackTable pk;
@@ -820,7 +823,10 @@ __device__ __forceinline__ void ag_finish(const AgArgs& a, float* const (&dst)[k
       __hip_atomic_store(ctr + kAgCtrDone, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       int spins = 0;
-      while (__hip_atomic_load(ctr + kAgCtrDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+      // polled by an atomic RMW, which executes at the memory side: a plain or sc1 poll can keep re-reading
+      // a copy of the line its own XCD's L2 took while the flag was still 0 (the f32 build's longer waits
+      // timed out that way)
+      while (__hip_atomic_fetch_or(ctr + kAgCtrDone, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
         __builtin_amdgcn_s_sleep(2);
         if (++spins > (1 << 24)) {   // never expected: flag it and go on rather than hang the device
           __hip_atomic_store(ctr + kAgCtrErr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -831,7 +837,13 @@ __device__ __forceinline__ void ag_finish(const AgArgs& a, float* const (&dst)[k
   }
   __syncthreads();
   // adam_kernel's fold: thread t takes partial t (kAgSlots < 256), then the same pairwise tree
-  L.red[t] = t < kAgSlots ? __hip_atomic_load(io.norm_parts + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+  if (t < kAgSlots) {   // memory-side reads (atomic RMW) like the flag's
+    const unsigned long long u = __hip_atomic_fetch_or(reinterpret_cast<unsigned long long*>(io.norm_parts) + t, 0ull,
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    L.red[t] = __builtin_bit_cast(double, u);
+  } else {
+    L.red[t] = 0.0;
+  }
   __syncthreads();
   for (int w = kAgT / 2; w > 0; w >>= 1) {
     if (t < w) L.red[t] += L.red[t + w];
@@ -893,7 +905,7 @@ __global__ __launch_bounds__(kAgT) void actor_grads_kernel(AgArgs a) {
     }
     const bool bias = kb == 0;
     float v[4], vb;
-    if (!ag_tile(dz + mb * 32, ldz, x + kb * 32, ldx, R, s * kAgRS, bias, S, s,
+    if (!ag_tile(dz + mb * 32, ldz, x + kb * 32, ldx, R, s * a.nch * kAgRS, a.nch, bias, S, s,
                  work + static_cast<size_t>(tile) * S * kAgSlab, io.counters + tile, L, v, vb))
       return;
     if (tile < kAgT2 + kAgT1) {
@@ -965,7 +977,7 @@ __global__ __launch_bounds__(kAgT) void actor_grads_kernel(AgArgs a) {
   if (b < kAgTiles * S + S) {   // output layer: dWo[a][k] = sum_r dout[r][a] h2[r][k], dbo[a] = sum_r dout[r][a]
     const int s = b - kAgTiles * S;
     const int c8 = t & 15, rr = t >> 4;
-    const int r0 = s * kAgRS, r1 = min(R, r0 + kAgRS);
+    const int r0 = s * a.nch * kAgRS, r1 = min(R, r0 + a.nch * kAgRS);
     float a0[8], a1[8], b0 = 0.f, b1 = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) a0[j] = a1[j] = 0.f;
@@ -1049,7 +1061,26 @@ __global__ __launch_bounds__(kAgT) void actor_grads_kernel(AgArgs a) {
   if (t == 0) io.loss_out[0] = static_cast<float>(tot);
 }
 
-int ag_splits(int B) { return (B + kAgRS - 1) / kAgRS; }
+// Row splits and chunks per split: one chunk of kAgRS rows per split where the whole grid (57 S + 1
+// workgroups) is resident at once, more chunks per split otherwise -- the fused optimiser's finishing
+// workgroups wait for each other, which needs every workgroup of the launch resident (a grid larger than
+// the chip hung the f32 build's launch behind its waiting workgroups)
+struct AgSplit {
+  int S, nch;
+};
+AgSplit ag_split(int B) {
+  static int cap = 0;
+  if (cap == 0) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, actor_grads_kernel, kAgT, 0) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    cap = per_cu * cu_count();
+  }
+  const int chunks = (B + kAgRS - 1) / kAgRS;
+  const int smax = (cap - 1) / (kAgTiles + 1) > 1 ? (cap - 1) / (kAgTiles + 1) : 1;
+  const int nch = (chunks + smax - 1) / smax;
+  return AgSplit{(chunks + nch - 1) / nch, nch};
+}
 
 }  // namespace
 
@@ -1226,7 +1257,7 @@ extern "C" int asvrl_linear_wgrad_vec(const float* dq, int64_t ldq, const void* 
 
 extern "C" int64_t asvrl_actor_grads_workspace(int32_t B) {
   if (B <= 0) return 0;
-  const int64_t S = ag_splits(B);
+  const int64_t S = ag_split(B).S;
   return static_cast<int64_t>(kAgTiles) * S * kAgSlab + S * kAgOutSlab + kAgEncImg;
 }
 extern "C" int32_t asvrl_actor_grads_counters(void) { return kAgCountersAdam; }
@@ -1259,7 +1290,9 @@ extern "C" int asvrl_actor_grads(const AsvActorGradIO* io, void* stream) {
   if (io->B == 0) return 0;
   AgArgs a{};
   a.io = *io;
-  a.S = ag_splits(io->B);
+  const AgSplit sp = ag_split(io->B);
+  a.S = sp.S;
+  a.nch = sp.nch;
   return launch_actor_grads(a, as_stream(stream));
 }
 
@@ -1277,7 +1310,9 @@ extern "C" int asvrl_actor_grads_adam(const AsvActorGradIO* io, const AsvActorAd
   if (io->B == 0) return 0;
   AgArgs a{};
   a.io = *io;
-  a.S = ag_splits(io->B);
+  const AgSplit sp = ag_split(io->B);
+  a.S = sp.S;
+  a.nch = sp.nch;
   a.adam = 1;
   a.ad = *ad;
   for (int k = 0; k < ad->nseg; ++k) a.pk.s[k] = ad->segs[k];

@@ -194,6 +194,12 @@ class ActorGrads:
         self.nparts = int(self.L.asvrl_actor_grads_norm_parts())
         self.norm_parts = torch.zeros(self.nparts, dtype=torch.float64, device=device)
 
+    def check(self):
+        """Raise if a launch's finishing workgroups ever stopped waiting for each other on the bounded spin
+        (the last counter word; never expected -- the launch sizes its grid to stay resident). Host sync."""
+        if int(self.counters[-1].item()) != 0:
+            raise RuntimeError("asvrl_actor_grads_adam: a finishing workgroup timed out waiting for the others")
+
 
 def actor_grads(ws, bufs, actor, tile_loss=None, loss_out=None, step=None, norm=True, adam=None, pack=None,
                 counter=None, stream=None):
