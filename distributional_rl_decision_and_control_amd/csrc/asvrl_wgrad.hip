@@ -625,11 +625,26 @@ constexpr int kAgNL = kAgRW * kAgCPR / 64;                         // chunks per
 static_assert(kAgNL >= 1 && (kAgRW * kAgCPR) % 64 == 0, "staging must tile the wave");
 constexpr int kAgSlab = 32 * 32 + 32;                              // one split's tile + bias slab
 constexpr int kAgT2 = 16, kAgT1 = 32, kAgTE = 8, kAgTiles = kAgT2 + kAgT1 + kAgTE;
-constexpr int kAgOutSlab = 2 * 128 + 2;
+constexpr int kAgOutItems = 16;   // output layer: one item per 8 of h2's 128 columns, over all rows
 constexpr int kAgEncImg = 256 * 32 + 256;
-constexpr int kAgCtrOut = kAgTiles, kAgCtrEnc = kAgTiles + 1, kAgCounters = kAgTiles + 2;
-constexpr int kAgSlotEnc = kAgT2 + kAgT1, kAgSlotOut = kAgSlotEnc + 1, kAgSlots = kAgSlotOut + 1;
+constexpr int kAgCtrEnc = kAgTiles, kAgCounters = kAgTiles + 1;
+constexpr int kAgSlotEnc = kAgT2 + kAgT1, kAgSlotOut = kAgSlotEnc + 1, kAgSlots = kAgSlotOut + kAgOutItems;
 constexpr int kAgEncOut = 688;   // self_w 56x7 | self_b 56 | obj_w 40x5 | obj_b 40
+
+// Phase timing (tools/ag_stamps.py; a variant build with -DASVRL_AG_STAMPS, never the shipped library):
+// thread 0 of every workgroup records s_memrealtime (100 MHz, one clock for every CU) at its phase points.
+#ifdef ASVRL_AG_STAMPS
+constexpr int kAgStamps = 12;
+__device__ uint64_t g_ag_stamps[4096 * kAgStamps];
+#define AG_STAMP(k)                                                                          \
+  do {                                                                                       \
+    if (threadIdx.x == 0) g_ag_stamps[blockIdx.x * kAgStamps + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define AG_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
 
 struct AgLds {
   union {
@@ -638,7 +653,7 @@ struct AgLds {
       char x[kAgW][kAgRW * kAgSt];
     } st;
     float cmb[kAgW][kAgSlab];
-    float out[16][16][18];    // output layer: [row lane][column chunk][8 + 8 columns, 2 biases]
+    float out[18][kAgT];      // output layer: [8 + 8 column sums, 2 bias sums][thread]
   } u;
   double red[kAgT];
   int last;
@@ -718,6 +733,7 @@ __device__ __forceinline__ bool ag_tile(const elem_t* __restrict__ dz, int ldz, 
     }
     __syncthreads();   // the staging images are rewritten by the next chunk / reused as the fold area
   }
+  AG_STAMP(1);
   const int h = lane >> 5, n = lane & 31;
   float* cw = L.u.cmb[w];
 #pragma unroll
@@ -740,7 +756,9 @@ __device__ __forceinline__ bool ag_tile(const elem_t* __restrict__ dz, int ldz, 
     if (S > 1) st_sc1(my + 1024 + t, vb);
   }
   if (S == 1) return true;
+  AG_STAMP(2);
   if (!ag_arrive(cnt, S, L)) return false;
+  AG_STAMP(3);
   // the S slabs in split order (this workgroup's own read back too), eight slabs' loads in flight at a time
   float acc4[4] = {0.f, 0.f, 0.f, 0.f}, accbs = 0.f;
   for (int s0 = 0; s0 < S; s0 += 8) {
@@ -763,6 +781,7 @@ __device__ __forceinline__ bool ag_tile(const elem_t* __restrict__ dz, int ldz, 
 #pragma unroll
   for (int j = 0; j < 4; ++j) v[j] = acc4[j];
   vb = accbs;
+  AG_STAMP(4);
   return true;
 }
 
@@ -814,6 +833,7 @@ __device__ __forceinline__ void ag_finish(const AgArgs& a, float* const (&dst)[k
   const float step_old = ad.step[0];   // advanced by the last finalizer to leave, after every read
   sq = ag_block_sum(sq, L);
   int* ctr = io.counters;
+  AG_STAMP(5);
   if (t == 0) {
     __hip_atomic_store(io.norm_parts + slot, sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -836,6 +856,7 @@ __device__ __forceinline__ void ag_finish(const AgArgs& a, float* const (&dst)[k
     }
   }
   __syncthreads();
+  AG_STAMP(6);
   // adam_kernel's fold: thread t takes partial t (kAgSlots < 256), then the same pairwise tree
   if (t < kAgSlots) {   // memory-side reads (atomic RMW) like the flag's
     const unsigned long long u = __hip_atomic_fetch_or(reinterpret_cast<unsigned long long*>(io.norm_parts) + t, 0ull,
@@ -850,7 +871,9 @@ __device__ __forceinline__ void ag_finish(const AgArgs& a, float* const (&dst)[k
     __syncthreads();
   }
   const float norm = static_cast<float>(sqrt(L.red[0]));
+  AG_STAMP(8);
   const AdamCoef ac = adam_coef(norm, static_cast<double>(step_old) + 1.0, ad.lr, ad.beta1, ad.beta2, ad.max_norm);
+  AG_STAMP(9);
 #pragma unroll
   for (int e = 0; e < kAgMaxEl; ++e) {
     if (e >= n) break;
@@ -862,6 +885,7 @@ __device__ __forceinline__ void ag_finish(const AgArgs& a, float* const (&dst)[k
     ad.params[fi[e]] = pn;
     if (a.pk.n > 0) pack_param(a.pk, fi[e], pn);
   }
+  AG_STAMP(10);
   __syncthreads();
   if (t == 0) {
     const int o = __hip_atomic_fetch_add(ctr + kAgCtrLeave, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -873,6 +897,7 @@ __device__ __forceinline__ void ag_finish(const AgArgs& a, float* const (&dst)[k
       if (ad.counter != nullptr) ad.counter[0] += 1;
     }
   }
+  AG_STAMP(7);
 }
 
 __global__ __launch_bounds__(kAgT) void actor_grads_kernel(AgArgs a) {
@@ -881,8 +906,12 @@ __global__ __launch_bounds__(kAgT) void actor_grads_kernel(AgArgs a) {
   const int S = a.S, R = io.B, t = threadIdx.x;
   const int b = blockIdx.x;
   float* work = io.work;
-  float* out_slabs = work + static_cast<size_t>(kAgTiles) * S * kAgSlab;
-  float* enc_img = out_slabs + static_cast<size_t>(S) * kAgOutSlab;
+  float* enc_img = work + static_cast<size_t>(kAgTiles) * S * kAgSlab;
+#ifdef ASVRL_AG_STAMPS
+  if (t == 0)
+    for (int k = 1; k < kAgStamps; ++k) g_ag_stamps[blockIdx.x * kAgStamps + k] = 0;
+#endif
+  AG_STAMP(0);
   if (b == 0 && t == 0 && io.step != nullptr) io.step[0] += 1.f;   // read by the Adam launch
   float* dst[kAgMaxEl];
   float val[kAgMaxEl];
@@ -974,83 +1003,56 @@ __global__ __launch_bounds__(kAgT) void actor_grads_kernel(AgArgs a) {
     ag_finish(a, dst, val, n, kAgSlotEnc, L);
     return;
   }
-  if (b < kAgTiles * S + S) {   // output layer: dWo[a][k] = sum_r dout[r][a] h2[r][k], dbo[a] = sum_r dout[r][a]
-    const int s = b - kAgTiles * S;
-    const int c8 = t & 15, rr = t >> 4;
-    const int r0 = s * a.nch * kAgRS, r1 = min(R, r0 + a.nch * kAgRS);
+  if (b < kAgTiles * S + kAgOutItems) {
+    // output layer, columns 8j .. 8j + 7 of h2 over every row: dWo[a][k] = sum_r dout[r][a] h2[r][k] (and
+    // item 0: dbo[a] = sum_r dout[r][a]); thread t takes rows t, t + 256, ... (eight in flight), then a fixed
+    // pairwise tree over the threads -- no split, no slab
+    const int j = b - kAgTiles * S, c0 = 8 * j;
     float a0[8], a1[8], b0 = 0.f, b1 = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) a0[j] = a1[j] = 0.f;
+    for (int q = 0; q < 8; ++q) a0[q] = a1[q] = 0.f;
     const elem_t* h2 = bp(io.h2);
-    for (int r = r0 + rr; r < r1; r += 16 * 8) {
+    for (int r = t; r < R; r += kAgT * 8) {
       float2 d[8];
       frag8 hv[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {   // eight rows' loads in flight
-        const int ru = r + 16 * u < r1 ? r + 16 * u : r;
+      for (int u = 0; u < 8; ++u) {
+        const int ru = r + kAgT * u < R ? r + kAgT * u : r;
         d[u] = *reinterpret_cast<const float2*>(io.dout + 2 * static_cast<int64_t>(ru));
-        hv[u] = *reinterpret_cast<const frag8*>(h2 + static_cast<int64_t>(ru) * 128 + c8 * 8);
+        hv[u] = *reinterpret_cast<const frag8*>(h2 + static_cast<int64_t>(ru) * 128 + c0);
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        if (r + 16 * u >= r1) break;
+        if (r + kAgT * u >= R) break;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float hj = static_cast<float>(hv[u][j]);
-          a0[j] += d[u].x * hj;
-          a1[j] += d[u].y * hj;
+        for (int q = 0; q < 8; ++q) {
+          const float hq = static_cast<float>(hv[u][q]);
+          a0[q] += d[u].x * hq;
+          a1[q] += d[u].y * hq;
         }
         b0 += d[u].x;
         b1 += d[u].y;
       }
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      L.u.out[rr][c8][j] = a0[j];
-      L.u.out[rr][c8][8 + j] = a1[j];
+    for (int q = 0; q < 8; ++q) {
+      L.u.out[q][t] = a0[q];
+      L.u.out[8 + q][t] = a1[q];
     }
-    L.u.out[rr][c8][16] = b0;
-    L.u.out[rr][c8][17] = b1;
+    L.u.out[16][t] = b0;
+    L.u.out[17][t] = b1;
+    AG_STAMP(1);
     __syncthreads();
-    float vo[2] = {0.f, 0.f};
-    float* my = out_slabs + static_cast<size_t>(s) * kAgOutSlab;
+    for (int w = kAgT / 2; w > 0; w >>= 1) {
+      if (t < w)
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int o = t + kAgT * q;
-      if (o >= kAgOutSlab) break;
-      int c, j;
-      if (o < 256) { c = (o & 127) >> 3; j = (o >> 7) * 8 + (o & 7); }
-      else { c = 0; j = 16 + (o - 256); }
-      float x0 = 0.f;
-      for (int u = 0; u < 16; ++u) x0 += L.u.out[u][c][j];
-      vo[q] = x0;
-      if (S > 1) st_sc1(my + o, x0);
+        for (int q = 0; q < 18; ++q) L.u.out[q][t] += L.u.out[q][t + w];
+      __syncthreads();
     }
-    if (S > 1 && !ag_arrive(io.counters + kAgCtrOut, S, L)) return;
-    const int n = t + kAgT < kAgOutSlab ? 2 : 1;
-    float xo[2] = {0.f, 0.f};
-    for (int s0 = 0; s0 < S; s0 += 8) {
-      float u[8][2];
-#pragma unroll
-      for (int q2 = 0; q2 < 8; ++q2) {
-        const float* p = out_slabs + static_cast<size_t>(s0 + q2 < S ? s0 + q2 : s0) * kAgOutSlab;
-        u[q2][0] = S > 1 ? ld_sc1(p + t) : vo[0];
-        u[q2][1] = t + kAgT < kAgOutSlab ? (S > 1 ? ld_sc1(p + t + kAgT) : vo[1]) : 0.f;
-      }
-#pragma unroll
-      for (int q2 = 0; q2 < 8; ++q2) {
-        if (s0 + q2 >= S) break;
-        xo[0] = s0 + q2 == 0 ? u[q2][0] : xo[0] + u[q2][0];
-        xo[1] = s0 + q2 == 0 ? u[q2][1] : xo[1] + u[q2][1];
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int o = t + kAgT * q;
-      dst[q] = o < 256 ? io.wo_grad + o : io.bo_grad + (o < kAgOutSlab ? o - 256 : 0);   // output_layer [2][128], [2]
-      val[q] = xo[q];
-    }
-    ag_finish(a, dst, val, n, kAgSlotOut, L);
+    const int n = t < 16 || (j == 0 && t < 18) ? 1 : 0;   // weight row a = t / 8, column c0 + t % 8; bias a
+    dst[0] = t < 16 ? io.wo_grad + (t >> 3) * 128 + c0 + (t & 7) : io.bo_grad + (t < 18 ? t - 16 : 0);
+    val[0] = L.u.out[t < 18 ? t : 0][0];
+    ag_finish(a, dst, val, n, kAgSlotOut + j, L);
     return;
   }
   // the actor loss: sum of the per-tile partials in a fixed order
@@ -1077,7 +1079,7 @@ AgSplit ag_split(int B) {
     cap = per_cu * cu_count();
   }
   const int chunks = (B + kAgRS - 1) / kAgRS;
-  const int smax = (cap - 1) / (kAgTiles + 1) > 1 ? (cap - 1) / (kAgTiles + 1) : 1;
+  const int smax = (cap - 1 - kAgOutItems) / kAgTiles > 1 ? (cap - 1 - kAgOutItems) / kAgTiles : 1;
   const int nch = (chunks + smax - 1) / smax;
   return AgSplit{(chunks + nch - 1) / nch, nch};
 }
@@ -1255,10 +1257,22 @@ extern "C" int asvrl_linear_wgrad_vec(const float* dq, int64_t ldq, const void* 
   return launch_partial_sum(work, groups, K, 1, dw, db, accumulate, as_stream(stream));
 }
 
+#ifdef ASVRL_AG_STAMPS
+extern "C" int asvrl_debug_ag_stamps(uint64_t* out, int64_t n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ag_stamps), n * sizeof(uint64_t)) == hipSuccess ? 0 : 1;
+}
+extern "C" int asvrl_debug_ag_split(int32_t B, int32_t* out2) {
+  const AgSplit sp = ag_split(B);
+  out2[0] = sp.S;
+  out2[1] = sp.nch;
+  return 0;
+}
+#endif
+
 extern "C" int64_t asvrl_actor_grads_workspace(int32_t B) {
   if (B <= 0) return 0;
   const int64_t S = ag_split(B).S;
-  return static_cast<int64_t>(kAgTiles) * S * kAgSlab + S * kAgOutSlab + kAgEncImg;
+  return static_cast<int64_t>(kAgTiles) * S * kAgSlab + kAgEncImg;
 }
 extern "C" int32_t asvrl_actor_grads_counters(void) { return kAgCountersAdam; }
 extern "C" int32_t asvrl_actor_grads_norm_parts(void) { return kAgSlots; }
@@ -1279,7 +1293,7 @@ int check_actor_grads(const AsvActorGradIO* io) {
 }
 
 int launch_actor_grads(const AgArgs& a, hipStream_t st) {
-  const int blocks = (kAgTiles + 1) * a.S + 1;
+  const int blocks = kAgTiles * a.S + kAgOutItems + 1;
   hipLaunchKernelGGL(actor_grads_kernel, dim3(blocks), dim3(kAgT), 0, st, a);
   return check_launch("asvrl_actor_grads");
 }
