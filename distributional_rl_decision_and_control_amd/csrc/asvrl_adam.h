@@ -45,21 +45,31 @@ struct AdamCoef {
   float coef, step_size, bc2_sqrt, w1, w2;
 };
 
-// clip coefficient from the global norm (clip_grad_norm_: max_norm / (norm + 1e-6), clamped to 1) and the
-// bias corrections of step t (already incremented)
-__device__ __forceinline__ AdamCoef adam_coef(float norm, double t, float lr, float beta1, float beta2,
-                                              float max_norm) {
+// the bias corrections of step t (already incremented); the clip coefficient comes later (adam_clip)
+__device__ __forceinline__ AdamCoef adam_step_scalars(double t, float lr, float beta1, float beta2) {
   AdamCoef a;
+  a.coef = 1.f;
+  a.step_size = static_cast<float>(static_cast<double>(lr) / (1.0 - pow(static_cast<double>(beta1), t)));
+  a.bc2_sqrt = static_cast<float>(sqrt(1.0 - pow(static_cast<double>(beta2), t)));
+  a.w1 = static_cast<float>(1.0 - static_cast<double>(beta1));
+  a.w2 = static_cast<float>(1.0 - static_cast<double>(beta2));
+  return a;
+}
+
+// clip_grad_norm_'s coefficient from the global norm: max_norm / (norm + 1e-6), clamped to 1
+__device__ __forceinline__ void adam_clip(AdamCoef& a, float norm, float max_norm) {
   float coef = 1.f;
   if (max_norm > 0.f) {
     coef = max_norm / (norm + 1e-6f);
     coef = coef < 1.f ? coef : 1.f;
   }
   a.coef = coef;
-  a.step_size = static_cast<float>(static_cast<double>(lr) / (1.0 - pow(static_cast<double>(beta1), t)));
-  a.bc2_sqrt = static_cast<float>(sqrt(1.0 - pow(static_cast<double>(beta2), t)));
-  a.w1 = static_cast<float>(1.0 - static_cast<double>(beta1));
-  a.w2 = static_cast<float>(1.0 - static_cast<double>(beta2));
+}
+
+__device__ __forceinline__ AdamCoef adam_coef(float norm, double t, float lr, float beta1, float beta2,
+                                              float max_norm) {
+  AdamCoef a = adam_step_scalars(t, lr, beta1, beta2);
+  adam_clip(a, norm, max_norm);
   return a;
 }
 

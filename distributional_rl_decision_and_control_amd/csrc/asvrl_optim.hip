@@ -59,6 +59,8 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(float* __restrict__ p
     v0 = v[i0];
     p0 = p[i0];
   }
+  // the step's bias corrections (two f64 pow) while the norm partials are folded: only the clip needs the norm
+  AdamCoef ac = adam_step_scalars(static_cast<double>(step[0]), lr, beta1, beta2);
   {   // thread t folds partials t, t + 256, ... in order, then a fixed tree: the same in every block
     double x = 0.0;
     x = strided_sum<double>(partial, threadIdx.x, nparts, kOptThreads, x);
@@ -75,7 +77,7 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(float* __restrict__ p
     }
   }
   __syncthreads();
-  const AdamCoef ac = adam_coef(s_norm, static_cast<double>(step[0]), lr, beta1, beta2, max_norm);
+  adam_clip(ac, s_norm, max_norm);
   for (int64_t i = i0; i < n; i += static_cast<int64_t>(gridDim.x) * kOptThreads) {
     const bool first = i == i0;
     float mo = first ? m0 : m[i], vo = first ? v0 : v[i], gi;

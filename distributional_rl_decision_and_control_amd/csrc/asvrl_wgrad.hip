@@ -831,6 +831,8 @@ __device__ __forceinline__ void ag_finish(const AgArgs& a, float* const (&dst)[k
     po[e] = ad.params[fi[e]];
   }
   const float step_old = ad.step[0];   // advanced by the last finalizer to leave, after every read
+  // the step's bias corrections (two f64 pow) before the wait: only the clip coefficient needs the norm
+  AdamCoef ac = adam_step_scalars(static_cast<double>(step_old) + 1.0, ad.lr, ad.beta1, ad.beta2);
   sq = ag_block_sum(sq, L);
   int* ctr = io.counters;
   AG_STAMP(5);
@@ -872,7 +874,7 @@ __device__ __forceinline__ void ag_finish(const AgArgs& a, float* const (&dst)[k
   }
   const float norm = static_cast<float>(sqrt(L.red[0]));
   AG_STAMP(8);
-  const AdamCoef ac = adam_coef(norm, static_cast<double>(step_old) + 1.0, ad.lr, ad.beta1, ad.beta2, ad.max_norm);
+  adam_clip(ac, norm, ad.max_norm);
   AG_STAMP(9);
 #pragma unroll
   for (int e = 0; e < kAgMaxEl; ++e) {

@@ -158,14 +158,12 @@ def learn_prologue(st, replay, taus, seed, counter_dev=None, counter=0, out=None
 
 
 def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, actor_grads, rows, gamma=0.99,
-                         taus=None, sync=None, max_norm=0.5, actor_wait=None, counter=None, prologue_done=False,
-                         mid_hook=None):
+                         taus=None, sync=None, max_norm=0.5, actor_wait=None, counter=None, prologue_done=False):
     """One AC-IQN update from replay rows [B][88]. taus: (3, B, N) or None (drawn here).
     actor_wait: event to wait for before the actor's weights change (a concurrent act kernel).
     counter: an int64 device scalar incremented after the step (the learn counter; in-kernel when
     the optimiser step is fused). prologue_done: learn_prologue already ran the actor's TRAIN forward and
-    the target actor on these rows. mid_hook: called right after the fused critic launch (the chained
-    schedule's roll_gate issues the rollout there).
+    the target actor on these rows.
     Returns (critic_loss, actor_loss, critic_grad_norm, actor_grad_norm) as device scalars."""
     B, N = st.B, st.N
     critic, actor = policy_local.critic, policy_local.actor
@@ -195,8 +193,6 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
         with arena.batch():   # the encoders' gradients from the per-sample dzF / dzG
             arena.fold(st.dzF, st.xb, critic)
             arena.small(st.dzG, a_rows, ae.weight.grad, ae.bias.grad)
-    if mid_hook is not None:
-        mid_hook()
     arena.scalar(st.tile_loss[0], st.losses[0:1])   # the critic loss
     cgn = _reduce_and_step(arena, critic_opt, critic_grads, sync, max_norm, pack=st.local_trunk)
 

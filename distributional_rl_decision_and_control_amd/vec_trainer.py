@@ -43,7 +43,7 @@ class VecTrainer:
                  learning_starts=None, target_update_interval=2500, total_timesteps=6_000_000,
                  exploration_fraction=0.25, initial_eps=0.6, final_eps=0.05, seed=0,
                  device="cuda", sync=None, graphs=False, schedule=None, net_seed=100, overlap=True, unroll=1,
-                 chain=None, operands="bf16", roll_gate=None):
+                 chain=None, operands="bf16"):
         """Every learner runs on the hand-written kernels (fused_update / fused_iqn / fused_rainbow) with
         FusedAdam; operands="f32" takes them from the f32-operand parity build (libasvrl_f32.so). Shapes
         the kernels do not take raise ValueError."""
@@ -154,11 +154,6 @@ class VecTrainer:
         # AC-IQN only (measured 0.346 -> 0.340 ms/step; IQN, whose act kernel fills the GPU, 0.363 ->
         # 0.366: profiles/r02_chain_schedule_ab.txt)
         self.chain = (agent_type == "AC-IQN") if chain is None else bool(chain)
-        # chained AC-IQN schedule only: roll_gate="critic" starts iteration k's rollout after learn(k)'s fused
-        # critic launch (the env step then shares the chip with the reduction / Adam / ACTOR pass instead of
-        # the target critic); None: as soon as learn(k-1) has written the actor
-        assert roll_gate in (None, "critic")
-        self.roll_gate = roll_gate
         self.ring_snap2 = torch.zeros((2, 2), dtype=torch.int64, device=self.device)
         self._gen = torch.Generator(device=self.device)
         self._gen.manual_seed(seed + 12345)
@@ -206,12 +201,10 @@ class VecTrainer:
         self.env.auto_reset(counted)
         self.env.advance_device(counted)
 
-    def learn(self, state=None, guard=0, actor_wait=None, mid_hook=None):
+    def learn(self, state=None, guard=0, actor_wait=None):
         """One learn step of batch B: sample (uniform ring, or the prioritised tree for Rainbow) and the
         agent's fused update. state / guard: the ring snapshot to sample against and the newest entries to
         skip (the overlapped schedule); actor_wait: an event to wait for before the actor's weights change."""
-        if mid_hook is not None and self.fused2 is None:   # only the fused AC-IQN update takes the hook
-            mid_hook()
         if self.per is not None:
             rows, idx = self.per.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter,
                                         out=self.batch_rows, out_idx=self.per_idx)
@@ -230,7 +223,7 @@ class VecTrainer:
             return ac_iqn_update_fused2(self.fused2, self.local, self.actor_opt, self.critic_opt, self.critic_grads,
                                         self.actor_grads, rows, gamma=self.gamma, sync=self.sync,
                                         actor_wait=actor_wait, taus=self.taus, counter=self.learn_counter,
-                                        prologue_done=True, mid_hook=mid_hook)
+                                        prologue_done=True)
         # the update's quantile fractions are drawn by the sampling launch
         rows = self.replay.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter, out=self.batch_rows,
                                   state=state, guard=guard, taus=self.taus)
@@ -366,34 +359,25 @@ class VecTrainer:
         ev_act = [torch.cuda.Event() for _ in range(U)]
         ev_snap = [torch.cuda.Event() for _ in range(U)]
         ev_learn = [torch.cuda.Event() for _ in range(U)]
-        ev_gate = [torch.cuda.Event() for _ in range(U)]
         # the events live as long as the graph: the captured cross-stream waits may refer to them at replay
-        self._chain_events = (ev_act, ev_snap, ev_learn, ev_gate)
+        self._chain_events = (ev_act, ev_snap, ev_learn)
         s_roll.wait_stream(main)
         out = None
         for k in range(U):
-            def rollout_k(k=k):
-                if self.roll_gate is not None:
-                    ev_gate[k].record(main)
-                with torch.cuda.stream(s_roll):
-                    if k > 0:
-                        s_roll.wait_event(ev_learn[k - 1])   # the weights learn(k-1) wrote
-                    if self.roll_gate is not None:
-                        s_roll.wait_event(ev_gate[k])
-                    self.act()
-                    ev_act[k].record(s_roll)
-                    env = self.env
-                    env.step(self.actions)
-                    self._push(snap=self.ring_snap2[k % 2])   # + the ring state learn(k+1) samples against
-                    ev_snap[k].record(s_roll)
-                    env.auto_reset(True)
-                    env.advance_device(True)
-            if self.roll_gate is None:
-                rollout_k()
+            with torch.cuda.stream(s_roll):
+                if k > 0:
+                    s_roll.wait_event(ev_learn[k - 1])   # the weights learn(k-1) wrote
+                self.act()
+                ev_act[k].record(s_roll)
+                env = self.env
+                env.step(self.actions)
+                self._push(snap=self.ring_snap2[k % 2])   # + the ring state learn(k+1) samples against
+                ev_snap[k].record(s_roll)
+                env.auto_reset(True)
+                env.advance_device(True)
             if k > 0:
                 main.wait_event(ev_snap[k - 1])
-            out = self.learn(state=self.ring_snap2[(k - 1) % 2], guard=self.E * self.R, actor_wait=ev_act[k],
-                             mid_hook=rollout_k if self.roll_gate is not None else None)
+            out = self.learn(state=self.ring_snap2[(k - 1) % 2], guard=self.E * self.R, actor_wait=ev_act[k])
             ev_learn[k].record(main)
         main.wait_stream(s_roll)
         return out

@@ -11,11 +11,11 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _run(agent_type, chain, iters, n_envs=256, batch=256, unroll=2, roll_gate=None):
+def _run(agent_type, chain, iters, n_envs=256, batch=256, unroll=2):
     from distributional_rl_decision_and_control_amd.vec_trainer import VecTrainer
     tr = VecTrainer(n_envs=n_envs, agent_type=agent_type, batch_size=batch, num_tau=32, seed=21, graphs=True,
                     unroll=unroll, chain=chain, buffer_size=max(n_envs * 5 * 40, 4 * n_envs * 5),
-                    learning_starts=2 * batch, roll_gate=roll_gate)
+                    learning_starts=2 * batch)
     while tr.replay_size_host() < tr.learning_starts:
         tr.iteration()
     for _ in range(iters):
@@ -41,13 +41,6 @@ def _same(a, pa, la, b, pb, lb):
 def test_chained_schedule_matches_joined(agent_type):
     a, pa, la = _run(agent_type, True, 8)
     b, pb, lb = _run(agent_type, False, 8)
-    _same(a, pa, la, b, pb, lb)
-
-
-def test_chained_schedule_roll_gate_matches_joined():
-    """The rollout issued behind the learner's fused critic (roll_gate="critic") changes only the overlap."""
-    a, pa, la = _run("AC-IQN", True, 8, roll_gate="critic")
-    b, pb, lb = _run("AC-IQN", False, 8)
     _same(a, pa, la, b, pb, lb)
 
 

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 3: the learner-chain tests, the default bench with one step's anatomy, then the roll_gate A/B
+# round 3: the learner-chain tests, the default bench with one step's anatomy, then a schedule A/B
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
@@ -8,4 +8,3 @@ timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method threa
   tests/test_learner_golden_gpu.py tests/test_dp_fused_gpu.py tests/test_chain_schedule_gpu.py tests/test_agent_gpu.py \
   > gpurun_out/${T}_pytest.log 2>&1 || exit 2
 TESTS=tests/test_optim_gpu.py bash tools/r03_bench_anatomy.sh ${T} || exit 3
-bash tools/r03_gate_ab.sh ${T}g || exit 4
