@@ -656,6 +656,7 @@ struct AgLds {
     float out[18][kAgT];      // output layer: [8 + 8 column sums, 2 bias sums][thread]
   } u;
   double red[kAgT];
+  AsvPackSeg pk[ASVRL_MAX_PACK_SEGS];   // the fused optimiser's pack table
   int last;
 };
 
@@ -794,8 +795,11 @@ struct AgArgs {
 };
 
 // The finalizers (every tile's last split, the encoder fold, the output layer): kAgSlots of them.
-constexpr int kAgCtrArrive = kAgCounters, kAgCtrDone = kAgCounters + 1, kAgCtrLeave = kAgCounters + 2,
-              kAgCtrErr = kAgCounters + 3, kAgCountersAdam = kAgCounters + 4;
+// the "all arrived" flag is kept in kAgDoneRep replicas on 128-byte lines of their own, finisher b polling
+// replica b % kAgDoneRep: one line polled by every finisher serialised the polls (exit lag up to 3 us)
+constexpr int kAgCtrArrive = kAgCounters, kAgCtrLeave = kAgCounters + 1, kAgDoneBase = 64, kAgDoneStride = 32,
+              kAgDoneRep = 16, kAgCtrErr = kAgDoneBase + kAgDoneStride * kAgDoneRep, kAgCountersAdam = kAgCtrErr + 1;
+static_assert(kAgCtrLeave < kAgDoneBase, "sync words before the replicas");
 constexpr int kAgMaxEl = 5;   // outputs per thread of a finalizer (tile: 4 + bias)
 
 // A finalizer's outputs (thread t: n of them, gradient addresses and values): the squared norm of the
@@ -830,9 +834,13 @@ __device__ __forceinline__ void ag_finish(const AgArgs& a, float* const (&dst)[k
     vo[e] = ad.exp_avg_sq[fi[e]];
     po[e] = ad.params[fi[e]];
   }
+  {   // the pack table into LDS (read per element below)
+    const int* src = reinterpret_cast<const int*>(a.pk.s);
+    int* dstl = reinterpret_cast<int*>(L.pk);
+    constexpr int kWords = static_cast<int>(sizeof(AsvPackSeg)) / 4 * ASVRL_MAX_PACK_SEGS;
+    for (int k = t; k < kWords; k += kAgT) dstl[k] = src[k];
+  }
   const float step_old = ad.step[0];   // advanced by the last finalizer to leave, after every read
-  // the step's bias corrections (two f64 pow) before the wait: only the clip coefficient needs the norm
-  AdamCoef ac = adam_step_scalars(static_cast<double>(step_old) + 1.0, ad.lr, ad.beta1, ad.beta2);
   sq = ag_block_sum(sq, L);
   int* ctr = io.counters;
   AG_STAMP(5);
@@ -840,20 +848,32 @@ __device__ __forceinline__ void ag_finish(const AgArgs& a, float* const (&dst)[k
     __hip_atomic_store(io.norm_parts + slot, sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int o = __hip_atomic_fetch_add(ctr + kAgCtrArrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    L.last = o == kAgSlots - 1;
     if (o == kAgSlots - 1) {
       __hip_atomic_store(ctr + kAgCtrArrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ctr + kAgCtrDone, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      int spins = 0;
-      // polled by an atomic RMW, which executes at the memory side: a plain or sc1 poll can keep re-reading
-      // a copy of the line its own XCD's L2 took while the flag was still 0 (the f32 build's longer waits
-      // timed out that way)
-      while (__hip_atomic_fetch_or(ctr + kAgCtrDone, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1 << 24)) {   // never expected: flag it and go on rather than hang the device
-          __hip_atomic_store(ctr + kAgCtrErr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
+      for (int k = 0; k < kAgDoneRep; ++k)
+        __hip_atomic_store(ctr + kAgDoneBase + kAgDoneStride * k, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  // while the others arrive: the step's bias corrections (two f64 pow; only the clip coefficient needs the
+  // norm) and the weight-image positions of this workgroup's parameters
+  AdamCoef ac = adam_step_scalars(static_cast<double>(step_old) + 1.0, ad.lr, ad.beta1, ad.beta2);
+  constexpr int kP = 5;
+  uint64_t pos[kAgMaxEl][kP];
+  int npos[kAgMaxEl];
+#pragma unroll
+  for (int e = 0; e < kAgMaxEl; ++e) npos[e] = e < n ? pack_positions<kP>(L.pk, a.pk.n, fi[e], pos[e]) : 0;
+  if (t == 0 && !L.last) {
+    int spins = 0;
+    // polled by an atomic RMW, which executes at the memory side: a plain or sc1 poll can keep re-reading
+    // a copy of the line its own XCD's L2 took while the flag was still 0 (the f32 build's longer waits
+    // timed out that way)
+    int* done = ctr + kAgDoneBase + kAgDoneStride * (static_cast<int>(blockIdx.x) % kAgDoneRep);
+    while (__hip_atomic_fetch_or(done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1 << 24)) {   // never expected: flag it and go on rather than hang the device
+        __hip_atomic_store(ctr + kAgCtrErr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
       }
     }
   }
@@ -885,7 +905,7 @@ __device__ __forceinline__ void ag_finish(const AgArgs& a, float* const (&dst)[k
     ad.exp_avg[fi[e]] = mo[e];
     ad.exp_avg_sq[fi[e]] = vo[e];
     ad.params[fi[e]] = pn;
-    if (a.pk.n > 0) pack_param(a.pk, fi[e], pn);
+    pack_store<kP>(pos[e], npos[e], pn);
   }
   AG_STAMP(10);
   __syncthreads();
@@ -893,7 +913,8 @@ __device__ __forceinline__ void ag_finish(const AgArgs& a, float* const (&dst)[k
     const int o = __hip_atomic_fetch_add(ctr + kAgCtrLeave, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (o == kAgSlots - 1) {
       __hip_atomic_store(ctr + kAgCtrLeave, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ctr + kAgCtrDone, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int k = 0; k < kAgDoneRep; ++k)
+        __hip_atomic_store(ctr + kAgDoneBase + kAgDoneStride * k, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       ad.step[0] = step_old + 1.f;
       if (ad.norm_out != nullptr) ad.norm_out[0] = norm;
       if (ad.counter != nullptr) ad.counter[0] += 1;
@@ -1014,17 +1035,18 @@ __global__ __launch_bounds__(kAgT) void actor_grads_kernel(AgArgs a) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) a0[q] = a1[q] = 0.f;
     const elem_t* h2 = bp(io.h2);
-    for (int r = t; r < R; r += kAgT * 8) {
-      float2 d[8];
-      frag8 hv[8];
+    constexpr int kRows = 16;   // rows in flight per thread (B = 4096: all of them, one memory round trip)
+    for (int r = t; r < R; r += kAgT * kRows) {
+      float2 d[kRows];
+      frag8 hv[kRows];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < kRows; ++u) {
         const int ru = r + kAgT * u < R ? r + kAgT * u : r;
         d[u] = *reinterpret_cast<const float2*>(io.dout + 2 * static_cast<int64_t>(ru));
         hv[u] = *reinterpret_cast<const frag8*>(h2 + static_cast<int64_t>(ru) * 128 + c0);
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < kRows; ++u) {
         if (r + kAgT * u >= R) break;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
