@@ -81,7 +81,7 @@ class AsvResetCfg(C.Structure):
 
 
 class AsvEnvLaunch(C.Structure):
-    _fields_ = [("layout", C.c_int32), ("block", C.c_int32), ("envs_per_block", C.c_int32), ("_pad0", C.c_int32)]
+    _fields_ = [("layout", C.c_int32), ("block", C.c_int32), ("envs_per_block", C.c_int32), ("max_groups", C.c_int32)]
 
 
 ENV_LAYOUT_AUTO, ENV_LAYOUT_PAIRS, ENV_LAYOUT_SWEEP = 0, 1, 2

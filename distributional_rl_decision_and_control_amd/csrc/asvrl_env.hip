@@ -599,12 +599,13 @@ __global__ __launch_bounds__(BLOCK) void env_sweep_kernel(AsvParams p, AsvEnvSta
 #ifndef ASVRL_ENV_PAIRS_WPE
 #define ASVRL_ENV_PAIRS_WPE 4
 #endif
+// one workgroup's envs [bid * epb, (bid + 1) * epb) of the step (env_pairs_kernel loops over them)
 template <int BLOCK, int NM>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NM == 1 ? 1 : ASVRL_ENV_PAIRS_WPE))) void env_pairs_kernel(AsvParams p, AsvEnvState s,
-                                                          const double* __restrict__ actions,
-                                                          const double* __restrict__ noise,
-                                                          AsvStepCtl ctl, AsvStepOut out, int epb) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+__device__ __forceinline__ void env_pairs_block(const AsvParams& p, const AsvEnvState& s,
+                                                const double* __restrict__ actions,
+                                                const double* __restrict__ noise,
+                                                const AsvStepCtl& ctl, const AsvStepOut& out, int epb, int bid,
+                                                unsigned char* smem) {
   const int R = s.max_robots;
   const int O = s.max_obs;
   const int S = O + R;               // candidate slots per robot (obstacles, then robots)
@@ -639,7 +640,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NM == 1 ?
   const bool rlane = tid < nrb;
   const int le = tid / R;
   const int i = tid - le * R;
-  const int e = blockIdx.x * epb + le;
+  const int e = bid * epb + le;
   const bool lane_env = rlane && e < s.n_envs;
   const bool env_on = lane_env && (ctl.env_mask == nullptr || ctl.env_mask[e] != 0);
   // a masked pass (the observation pass after a reset) touches few envs: workgroups with none leave
@@ -803,7 +804,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NM == 1 ?
     double key = INFINITY;
     double ox = 0, oy = 0, orad = 0, vx0 = 0, vy0 = 0;
     if (sact[qr] && candidate(qe, qi, c, ox, oy, orad, vx0, vy0)) {
-      const size_t qidx = static_cast<size_t>(blockIdx.x * epb + qe) * R + qi;
+      const size_t qidx = static_cast<size_t>(bid * epb + qe) * R + qi;
       double n0, n1, n2, n3, n4;
       draw_noise<NM>(p, ctl, ctr, noise, qidx, c, S, n0, n1, n2, n3, n4);
       pvm[q] = static_cast<VmT>(n4);
@@ -900,7 +901,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NM == 1 ?
     const int k = kq - 5 * qr;
     const int qe = qr / R;
     const int qi = qr - qe * R;
-    const int e2 = blockIdx.x * epb + qe;
+    const int e2 = bid * epb + qe;
     unsigned char cf = 0;
     double ph = 0.0;
     {
@@ -998,6 +999,18 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NM == 1 ?
   }
   __syncthreads();
   if (env_on && i == 0 && ctl.do_dynamics) env_end(p, s, ctl, out, e, ep_ts, nrob, salive[le], NT);
+}
+
+
+// The step kernel: workgroup b takes env group group0 + b (a step may be split into launches of at most
+// AsvEnvLaunch.max_groups workgroups, one after another: the rollout's share of the chip beside the learner)
+template <int BLOCK, int NM>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NM == 1 ? 1 : ASVRL_ENV_PAIRS_WPE))) void env_pairs_kernel(AsvParams p, AsvEnvState s,
+                                                          const double* __restrict__ actions,
+                                                          const double* __restrict__ noise,
+                                                          AsvStepCtl ctl, AsvStepOut out, int epb, int group0) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  env_pairs_block<BLOCK, NM>(p, s, actions, noise, ctl, out, epb, group0 + static_cast<int>(blockIdx.x), smem);
 }
 
 // ------------------------------------------------------------------ reset (env.py:72-164)
@@ -1259,7 +1272,7 @@ extern "C" int asvrl_env_step_ex(const AsvParams* params, const AsvEnvState* sta
   ASVRL_REQUIRE(lc.layout >= 0 && lc.layout <= 2, "asvrl_env_step: layout must be 0 (auto), 1 (pairs) or 2 (sweep)");
   ASVRL_REQUIRE(lc.block == 0 || lc.block == 64 || lc.block == 128 || lc.block == 256,
                 "asvrl_env_step: block must be 0, 64, 128 or 256");
-  ASVRL_REQUIRE(lc.envs_per_block >= 0, "asvrl_env_step: negative envs_per_block");
+  ASVRL_REQUIRE(lc.envs_per_block >= 0 && lc.max_groups >= 0, "asvrl_env_step: negative envs_per_block / max_groups");
   const int nm = ctl->noise_mode == 0 ? 0 : (ctl->noise_mode == 1 ? 1 : 2);
   const PairLaunch pl = pair_launch(state->max_robots, state->max_obs, state->n_envs, lc.block, lc.envs_per_block,
                                     nm == 2 ? 4 : 8);
@@ -1267,10 +1280,12 @@ extern "C" int asvrl_env_step_ex(const AsvParams* params, const AsvEnvState* sta
   ASVRL_REQUIRE(lc.layout != 1 || pl.smem <= 150 * 1024, "asvrl_env_step: the pair layout's LDS does not fit");
   ASVRL_REQUIRE(lc.layout != 1 || !per_robot, "asvrl_env_step: per-robot parameters take the sweep layout (2)");
   if (lc.layout != 2 && !per_robot && pl.smem <= 150 * 1024) {
-    const int grid = (state->n_envs + pl.epb - 1) / pl.epb;
+    const int groups = (state->n_envs + pl.epb - 1) / pl.epb;
+    const int chunk = lc.max_groups > 0 && lc.max_groups < groups ? lc.max_groups : groups;
     auto go = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(pl.blk), pl.smem, as_stream(stream), *params, *state, actions, noise,
-                         *ctl, *out, pl.epb);
+      for (int g0 = 0; g0 < groups; g0 += chunk)
+        hipLaunchKernelGGL(kern, dim3(groups - g0 < chunk ? groups - g0 : chunk), dim3(pl.blk), pl.smem,
+                           as_stream(stream), *params, *state, actions, noise, *ctl, *out, pl.epb, g0);
     };
     if (pl.blk == 64)
       nm == 0 ? go(env_pairs_kernel<64, 0>) : nm == 1 ? go(env_pairs_kernel<64, 1>) : go(env_pairs_kernel<64, 2>);

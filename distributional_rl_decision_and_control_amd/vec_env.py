@@ -20,6 +20,7 @@ class VecMarineNavEnv:
                  max_robots=None, max_obs=None, max_cores=None):
         self.n_envs = int(n_envs)
         self.schedule = schedule
+        self.max_groups = 0   # step kernel workgroups per launch (0: one launch; see _launch)
         R = max_robots or (max(schedule["num_robots"]) if schedule else num_robots)
         O = max_obs if max_obs is not None else (max(schedule["num_obstacles"]) if schedule else num_obs)
         Cc = max_cores if max_cores is not None else (max(schedule["num_cores"]) if schedule else num_cores)
@@ -83,7 +84,13 @@ class VecMarineNavEnv:
         Writes obs_next / cnt_next, batch.reward / done / info / env_done."""
         self.batch.step(actions, is_continuous=self.is_continuous, trainer_deactivate=True, seed=self.seed,
                         counter=0, counter_dev=self.counter, gamma=self.gamma, obs=self.obs_next,
-                        obj_cnt=self.cnt_next, fast_noise=True)   # f32 Philox draws (noise_mode 2)
+                        obj_cnt=self.cnt_next, fast_noise=True,   # f32 Philox draws (noise_mode 2)
+                        launch=self._launch())
+
+    def _launch(self):
+        """The step kernel's shape: automatic, or launches of at most `max_groups` workgroups one after another
+        (the rollout's share of the chip beside a concurrent learner; results do not depend on it)."""
+        return (0, 0, 0, self.max_groups) if self.max_groups > 0 else None
 
     def auto_reset(self, counted=False):
         """Reset the envs whose episode ended in the last step and observe them into obs_next.
@@ -93,7 +100,7 @@ class VecMarineNavEnv:
         d = 1 if counted else 0
         b.reset(self.cfg, b.env_done, seed=self.seed, counter=0x40000000 - d, counter_dev=self.counter)
         b.step(None, do_dynamics=False, seed=self.seed, counter=0x80000000 - d, counter_dev=self.counter,
-               fast_noise=True, env_mask=b.env_done, obs=self.obs_next, obj_cnt=self.cnt_next)
+               fast_noise=True, env_mask=b.env_done, obs=self.obs_next, obj_cnt=self.cnt_next, launch=self._launch())
 
     def advance_device(self, counted=False):
         if self.swap:

@@ -173,7 +173,8 @@ typedef struct AsvEnvLaunch {
   int32_t layout;
   int32_t block;
   int32_t envs_per_block;
-  int32_t _pad0;
+  int32_t max_groups;   /* ABI 19: pair layout as launches of at most this many workgroups, one after another
+                           (0 = one launch) -- the rollout's share of the chip beside a learner */
 } AsvEnvLaunch;
 
 /* asvrl_env_step with an explicit kernel shape (tests of every shipped layout, A/B tools);
