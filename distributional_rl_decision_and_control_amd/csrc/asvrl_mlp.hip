@@ -511,7 +511,6 @@ struct PrologueArgs {
   const uint64_t* counter_dev;
   int64_t guard;
   int B, tau_sets, tau_n;
-  int train;   // 0: the first half only draws and writes the rows (the actor's TRAIN pass runs later)
   float* out;
   float* taus;
 };
@@ -525,7 +524,7 @@ __global__ __launch_bounds__(kMlpWaves * 64) void learn_prologue_kernel(Prologue
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   // the wave's weight fragments first: their L2 latency runs under the draw below
   SplitPre pre;
-  if (second || p.train) split_prefetch(second ? tgt.w : train.w, w, lane, pre);
+  split_prefetch(second ? tgt.w : train.w, w, lane, pre);
   const int64_t head = p.ring_state[0], size = p.ring_state[1];
   const uint64_t ctr = p.counter + (p.counter_dev != nullptr ? *p.counter_dev : 0ull);
   // wave w gathers samples 8w .. 8w + 7 of the tile: the whole row to `out` (first half), the observation
@@ -577,11 +576,8 @@ __global__ __launch_bounds__(kMlpWaves * 64) void learn_prologue_kernel(Prologue
     }
   }
   __syncthreads();
-  if (!second) {
-    if (p.train) actor_split_tile<MLP_TRAIN, true>(train, L, tile, xs, ASVRL_OBS_DIM, 0, pre);
-  } else {
-    actor_split_tile<MLP_FWD, true>(tgt, L, tile, xs, ASVRL_OBS_DIM, 0, pre);
-  }
+  if (!second) actor_split_tile<MLP_TRAIN, true>(train, L, tile, xs, ASVRL_OBS_DIM, 0, pre);
+  else actor_split_tile<MLP_FWD, true>(tgt, L, tile, xs, ASVRL_OBS_DIM, 0, pre);
 }
 
 // The backward in the same split: dz2 (block w) from dA, dz1 = W2^T dz2 (block w), dz0 = W1^T dz1
@@ -836,21 +832,18 @@ extern "C" int asvrl_actor_forward(const AsvMlpWeights* w, const AsvMlpIO* io, i
 
 extern "C" int asvrl_learn_prologue(const AsvSampleArgs* s, const AsvMlpWeights* actor, const AsvMlpIO* train_io,
                                     const AsvMlpWeights* target_actor, float* na, void* stream) {
-  ASVRL_REQUIRE(s && target_actor && na && s->ring && s->ring_state && s->out, "asvrl_learn_prologue: null argument");
-  ASVRL_REQUIRE((actor == nullptr) == (train_io == nullptr),
-                "asvrl_learn_prologue: actor and train_io together (or both NULL: no TRAIN pass)");
+  ASVRL_REQUIRE(s && actor && train_io && target_actor && na && s->ring && s->ring_state && s->out,
+                "asvrl_learn_prologue: null argument");
   ASVRL_REQUIRE(s->capacity > 0 && s->B > 0 && s->B % 32 == 0, "asvrl_learn_prologue: B must be a positive multiple of 32");
   ASVRL_REQUIRE(s->taus == nullptr || (s->tau_sets >= 1 && s->tau_n >= 1), "asvrl_learn_prologue: bad tau shape");
-  ASVRL_REQUIRE(!train_io || (train_io->n == s->B && train_io->a_out && train_io->xb && train_io->h0 && train_io->h1 &&
-                                 train_io->h2 && train_io->pre),
-                "asvrl_learn_prologue: the TRAIN outputs (n = B, a_out, xb, h0, h1, h2, pre)");
+  ASVRL_REQUIRE(train_io->n == s->B && train_io->a_out && train_io->xb && train_io->h0 && train_io->h1 && train_io->h2 &&
+                    train_io->pre, "asvrl_learn_prologue: the TRAIN outputs (n = B, a_out, xb, h0, h1, h2, pre)");
   for (const AsvMlpWeights* w : {actor, target_actor})
-    ASVRL_REQUIRE(!w || (w->enc_frag && w->w1_frag && w->w2_frag && w->b1 && w->b2 && w->wout && w->bout),
+    ASVRL_REQUIRE(w->enc_frag && w->w1_frag && w->w2_frag && w->b1 && w->b2 && w->wout && w->bout,
                   "asvrl_learn_prologue: null actor weight");
   PrologueArgs p{s->ring, s->capacity, s->ring_state, s->seed, s->counter, s->counter_dev, s->guard,
-                 s->B, s->tau_sets, s->tau_n, actor != nullptr ? 1 : 0, s->out, s->taus};
-  MlpArgs tr{};
-  if (actor != nullptr) tr = MlpArgs{*actor, *train_io};
+                 s->B, s->tau_sets, s->tau_n, s->out, s->taus};
+  MlpArgs tr{*actor, *train_io};
   AsvMlpIO fio{};
   fio.n = s->B;
   fio.a_out = na;

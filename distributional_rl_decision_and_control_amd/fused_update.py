@@ -135,13 +135,11 @@ def target_q(st, rows, tau0, q_out, na):
     critic_forward(st.target_trunk, None, None, tau0, st.N, q=q_out, obs=ns_rows, act=na)
 
 
-def learn_prologue(st, replay, taus, seed, counter_dev=None, counter=0, out=None, state=None, guard=0, stream=None,
-                   train=True):
+def learn_prologue(st, replay, taus, seed, counter_dev=None, counter=0, out=None, state=None, guard=0, stream=None):
     """asvrl_learn_prologue: B rows drawn from the device ring (replay_buffer.py:26-45) with the update's
     quantile fractions `taus` (3, B, N), the local actor's TRAIN forward on s (its activations in st.abufs)
     and the target actor's forward on s' (st.na) in ONE launch, bit-identical to replay.sample +
-    actor_train_forward + actor_forward. train=False: without the TRAIN forward (it then runs in the update,
-    after the previous update of the actor: ac_iqn_ahead). Returns the rows [B][88]."""
+    actor_train_forward + actor_forward. Returns the rows [B][88]."""
     B = st.B
     out = out if out is not None else torch.empty((B, 88), dtype=torch.float32, device=st.device)
     assert taus.is_contiguous() and taus.shape[1] == B and taus.dtype == torch.float32
@@ -153,34 +151,19 @@ def learn_prologue(st, replay, taus, seed, counter_dev=None, counter=0, out=None
     sa.guard, sa.B, sa.tau_sets, sa.tau_n = int(guard), B, taus.shape[0], taus.shape[2]
     sa.out, sa.taus = out.data_ptr(), taus.data_ptr()
     io = st.abufs.io()
-    _abi.check(st.actor.L.asvrl_learn_prologue(C.byref(sa), C.byref(st.actor.w) if train else None,
-                                                C.byref(io) if train else None, C.byref(st.target_actor.w),
-                                                st.na.data_ptr(), _abi.stream_ptr(stream)),
-               "asvrl_learn_prologue", st.actor.L)
+    _abi.check(st.actor.L.asvrl_learn_prologue(C.byref(sa), C.byref(st.actor.w), C.byref(io),
+                                                C.byref(st.target_actor.w), st.na.data_ptr(),
+                                                _abi.stream_ptr(stream)), "asvrl_learn_prologue", st.actor.L)
     return out
 
 
-def ac_iqn_ahead(st, replay, rows, taus, q_next, seed, counter_dev, state=None, guard=0):
-    """The part of an AC-IQN update that reads only the replay ring and the target networks
-    (agent.py:387-400): the draw of the rows and their quantile fractions, the target actor on s' and the
-    target critic -> q_next [B*N] -- then counter_dev += 1 (the draws' counter). It does not wait for the
-    previous update, so the pipelined schedule (VecTrainer) runs it beside that update's actor half; the
-    update itself follows with ac_iqn_update_fused2(..., q_next=q_next, late_train=True)."""
-    learn_prologue(st, replay, taus, seed, counter_dev=counter_dev, out=rows, state=state, guard=guard, train=False)
-    counter_dev += 1
-    critic_forward(st.target_trunk, None, None, taus[0], st.N, q=q_next, obs=rows[:, OBS:2 * OBS], act=st.na)
-    return rows
-
-
 def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, actor_grads, rows, gamma=0.99,
-                         taus=None, sync=None, max_norm=0.5, actor_wait=None, counter=None, prologue_done=False,
-                         q_next=None, late_train=False):
+                         taus=None, sync=None, max_norm=0.5, actor_wait=None, counter=None, prologue_done=False):
     """One AC-IQN update from replay rows [B][88]. taus: (3, B, N) or None (drawn here).
     actor_wait: event to wait for before the actor's weights change (a concurrent act kernel).
     counter: an int64 device scalar incremented after the step (the learn counter; in-kernel when
     the optimiser step is fused). prologue_done: learn_prologue already ran the actor's TRAIN forward and
-    the target actor on these rows. q_next + late_train: ac_iqn_ahead already formed the targets; the
-    actor's TRAIN forward runs here, after the critic step (it only feeds the actor half).
+    the target actor on these rows.
     Returns (critic_loss, actor_loss, critic_grad_norm, actor_grad_norm) as device scalars."""
     B, N = st.B, st.N
     critic, actor = policy_local.critic, policy_local.actor
@@ -192,13 +175,10 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
 
     # ---- critic (agent.py:395-416); every critic .grad is overwritten below (no zeroing). The
     # trunk kernels run the critic's observation / action encoders on the replay rows themselves.
-    if late_train:   # targets from ac_iqn_ahead
-        assert q_next is not None
-    elif prologue_done:   # only the target critic is left of the target chain
-        q_next = st.q_next
+    q_next = st.q_next
+    if prologue_done:   # only the target critic is left of the target chain
         critic_forward(st.target_trunk, None, None, taus[0], st.N, q=q_next, obs=rows[:, OBS:2 * OBS], act=st.na)
     else:
-        q_next = st.q_next
         actor_train_forward(st.actor, s_rows, ab)   # reads only s and the (not yet updated) actor
         target_q(st, rows, taus[0], q_next, st.na)
     ae = critic.action_encoder[0]
@@ -217,8 +197,6 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     cgn = _reduce_and_step(arena, critic_opt, critic_grads, sync, max_norm, pack=st.local_trunk)
 
     # ---- actor through the updated critic (agent.py:419-427)
-    if late_train:
-        actor_train_forward(st.actor, s_rows, ab)   # the actor as the previous update left it
     critic_actor_grad(st.local_trunk, None, None, taus[2], N, st.q_pi, w_ae=ae.weight, dA=ab.dA,
                       tile_loss=st.tile_loss[1], obs=s_rows, act=ab.a_out)
     actor_backward(st.actor, ab)

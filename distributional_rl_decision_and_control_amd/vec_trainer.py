@@ -21,7 +21,7 @@ import time
 import torch
 
 from . import streams
-from .fused_update import FusedACIQNState, ac_iqn_ahead, ac_iqn_update_fused2
+from .fused_update import FusedACIQNState, ac_iqn_update_fused2, learn_prologue
 from .fused_iqn import FusedIQNState, iqn_update_fused
 from .fused_iqn import supported as fused_iqn_supported
 from .fused_rainbow import FusedRainbow
@@ -124,11 +124,6 @@ class VecTrainer:
         self.batch_rows = torch.zeros((self.B, 88), dtype=torch.float32, device=self.device)
         # the fused updates' quantile fractions (AC-IQN: target, local, actor step; IQN: the first two)
         self.taus = torch.zeros((3, self.B, self.num_tau), dtype=torch.float32, device=self.device)
-        if self.fused2 is not None:   # AC-IQN: a second set for the pipelined schedule (_chain_body)
-            self.rows2 = (self.batch_rows, torch.zeros_like(self.batch_rows))
-            self.taus2 = (self.taus, torch.zeros_like(self.taus))
-            self.q_next2 = (torch.zeros(self.B * self.num_tau, dtype=torch.float32, device=self.device),
-                            torch.zeros(self.B * self.num_tau, dtype=torch.float32, device=self.device))
         self.learn_steps = 0
         self.iterations = 0
         self.last_losses = None
@@ -221,26 +216,19 @@ class VecTrainer:
             self.learn_counter += 1
             return loss.mean(), gn
         if self.fused2 is not None:
-            self._ahead(0, state, guard)
-            return self._update(0, actor_wait)
+            # one launch: the draw (rows + the update's quantile fractions), the actor's training forward
+            # and the target actor
+            rows = learn_prologue(self.fused2, self.replay, self.taus, self.seed + 777, counter_dev=self.learn_counter,
+                                  out=self.batch_rows, state=state, guard=guard)
+            return ac_iqn_update_fused2(self.fused2, self.local, self.actor_opt, self.critic_opt, self.critic_grads,
+                                        self.actor_grads, rows, gamma=self.gamma, sync=self.sync,
+                                        actor_wait=actor_wait, taus=self.taus, counter=self.learn_counter,
+                                        prologue_done=True)
         # the update's quantile fractions are drawn by the sampling launch
         rows = self.replay.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter, out=self.batch_rows,
                                   state=state, guard=guard, taus=self.taus)
         return iqn_update_fused(self.fused_iqn, self.local, self.opt, self.grads, rows, gamma=self.gamma,
                                 sync=self.sync, act_wait=actor_wait, taus=self.taus[:2], counter=self.learn_counter)
-
-    def _ahead(self, j, state, guard):
-        """AC-IQN: the draw (rows + the update's quantile fractions), the target actor and the target critic into
-        buffer set j (fused_update.ac_iqn_ahead); the draws' counter advances."""
-        ac_iqn_ahead(self.fused2, self.replay, self.rows2[j], self.taus2[j], self.q_next2[j], self.seed + 777,
-                     self.learn_counter, state=state, guard=guard)
-
-    def _update(self, j, actor_wait):
-        """AC-IQN: the update from buffer set j (the actor's TRAIN forward after the critic step)."""
-        return ac_iqn_update_fused2(self.fused2, self.local, self.actor_opt, self.critic_opt, self.critic_grads,
-                                    self.actor_grads, self.rows2[j], gamma=self.gamma, sync=self.sync,
-                                    actor_wait=actor_wait, taus=self.taus2[j], q_next=self.q_next2[j],
-                                    late_train=True)
 
     def hard_update(self):
         """soft_update with TAU = 1.0 (agent.py:643-679): target <- local."""
@@ -363,8 +351,6 @@ class VecTrainer:
 
     def _chain_body(self):
         """self.unroll iterations with per-dependency stream ordering (captured only; see __init__)."""
-        if self.fused2 is not None:
-            return self._chain_body_pipelined()
         main = torch.cuda.current_stream(self.device)
         if self._streams is None:
             self._streams = (self.roll_stream(),) + self._roll_events()
@@ -394,60 +380,6 @@ class VecTrainer:
             out = self.learn(state=self.ring_snap2[(k - 1) % 2], guard=self.E * self.R, actor_wait=ev_act[k])
             ev_learn[k].record(main)
         main.wait_stream(s_roll)
-        return out
-
-    def _chain_body_pipelined(self):
-        """AC-IQN, self.unroll iterations on three streams ordered by their exact dependencies (captured only):
-          rollout k (rollout stream): act after update k-1 wrote the actor, env step, replay push + the ring
-            snapshot, device reset;
-          ahead k+1 (ahead stream): the draw against push k's snapshot, the target actor and target critic into
-            buffer set (k+1) % 2 (ac_iqn_ahead: nothing of update k is read, so it runs beside update k's
-            actor half);
-          update k (learner stream): after ahead k, on buffer set k % 2; the actor's weights change after act k.
-        Every operation and every draw is the one the joined schedule makes (bit-identical, tested); the
-        first ahead of a replay runs against the snapshot the previous replay's last push left."""
-        main = torch.cuda.current_stream(self.device)
-        if self._streams is None:
-            self._streams = (self.roll_stream(),) + self._roll_events()
-        s_roll = self._streams[0]
-        s_ahead = streams.stream(self.device, "ahead")
-        U = self.unroll
-        ev_act = [torch.cuda.Event() for _ in range(U)]
-        ev_snap = [torch.cuda.Event() for _ in range(U)]
-        ev_learn = [torch.cuda.Event() for _ in range(U)]
-        ev_ahead = [torch.cuda.Event() for _ in range(U)]
-        # the events live as long as the graph: the captured cross-stream waits may refer to them at replay
-        self._chain_events = (ev_act, ev_snap, ev_learn, ev_ahead)
-        s_roll.wait_stream(main)
-        s_ahead.wait_stream(main)
-        guard = self.E * self.R
-        with torch.cuda.stream(s_ahead):
-            self._ahead(0, self.ring_snap2[(U - 1) % 2], guard)
-            ev_ahead[0].record(s_ahead)
-        out = None
-        for k in range(U):
-            with torch.cuda.stream(s_roll):
-                if k > 0:
-                    s_roll.wait_event(ev_learn[k - 1])   # the weights update k-1 wrote
-                self.act()
-                ev_act[k].record(s_roll)
-                env = self.env
-                env.step(self.actions)
-                self._push(snap=self.ring_snap2[k % 2])   # + the ring state ahead k+1 samples against
-                ev_snap[k].record(s_roll)
-                env.auto_reset(True)
-                env.advance_device(True)
-            if k + 1 < U:
-                with torch.cuda.stream(s_ahead):
-                    # buffer set (k+1) % 2 was update k-1's: free once act k (after update k-1) has run
-                    s_ahead.wait_event(ev_snap[k])
-                    self._ahead((k + 1) % 2, self.ring_snap2[k % 2], guard)
-                    ev_ahead[k + 1].record(s_ahead)
-            main.wait_event(ev_ahead[k])
-            out = self._update(k % 2, ev_act[k])
-            ev_learn[k].record(main)
-        main.wait_stream(s_roll)
-        main.wait_stream(s_ahead)
         return out
 
     def _capture(self):

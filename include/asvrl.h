@@ -912,9 +912,6 @@ typedef struct AsvSampleArgs {
 } AsvSampleArgs;
 int asvrl_learn_prologue(const AsvSampleArgs* s, const AsvMlpWeights* actor, const AsvMlpIO* train_io,
                          const AsvMlpWeights* target_actor, float* na, void* stream);
-/* (ABI 19) actor = train_io = NULL: the draw and the target Actor only -- the local Actor's TRAIN pass then
- * runs later (asvrl_actor_forward, mode 3, on the drawn rows), so this launch does not wait for the previous
- * update of the local Actor (the pipelined learner). */
 /* Backward of the Actor from dA to every layer's pre-activation gradient (agent.py:425). */
 int asvrl_actor_backward(const AsvMlpWeights* w, const AsvMlpIO* io, void* stream);
 /* Fold the 256 x 32 encoder-image gradient (dw, db from asvrl_linear_wgrad) back onto
