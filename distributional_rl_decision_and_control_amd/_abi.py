@@ -158,12 +158,6 @@ class AsvActorGradIO(C.Structure):
                [("work_floats", _I64), ("counters", _VP)]
 
 
-class AsvActorAdam(C.Structure):
-    _fields_ = [(n, _VP) for n in ("params", "grads", "exp_avg", "exp_avg_sq")] + [("n", _I64), ("step", _VP)] + \
-               [(n, C.c_float) for n in ("lr", "beta1", "beta2", "eps", "max_norm")] + \
-               [("norm_out", _VP), ("segs", _VP), ("nseg", _I32), ("counter", _VP)]
-
-
 class AsvPartialSum(C.Structure):
     _fields_ = [("partial", _VP), ("dw", _VP), ("db", _VP), ("groups", _I32), ("nw", _I32), ("nb", _I32),
                 ("accumulate", _I32), ("stride", _I32), ("boff", _I32), ("mode", _I32), ("norm", _I32)]
@@ -304,7 +298,6 @@ EXPORTS = [
     ("asvrl_actor_grads_counters", _I32, []),
     ("asvrl_actor_grads_norm_parts", _I32, []),
     ("asvrl_actor_grads", C.c_int, [C.POINTER(AsvActorGradIO), _VP]),
-    ("asvrl_actor_grads_adam", C.c_int, [C.POINTER(AsvActorGradIO), C.POINTER(AsvActorAdam), _VP]),
     ("asvrl_adam_step", C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, _F, _F, _VP, _VP, _I32, _VP]),
     ("asvrl_adam_step_pack", C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, _F, _F, _VP, _VP, _I32, _VP, _I32,
                                        _VP, _VP]),

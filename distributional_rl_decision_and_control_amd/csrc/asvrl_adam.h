@@ -1,6 +1,5 @@
 // asvrl_adam.h -- the per-element clip + Adam update (clip_grad_norm_ then optim.Adam.step(), agent.py:75-76,98,
-// 415-416,426) and the weight-image re-pack, shared by asvrl_optim.hip's adam_kernel and the Actor's
-// one-launch gradient + optimiser tail (asvrl_wgrad.hip): both produce the same bits for the same inputs.
+// 415-416,426) and the weight-image re-pack of asvrl_optim.hip's adam_kernel.
 #pragma once
 #include "asvrl_common.h"
 #include "asvrl_mfma.h"
@@ -37,67 +36,6 @@ __device__ __forceinline__ void pack_param(const PackTable& t, int64_t i, float 
       if (g.f32) static_cast<float*>(g.image)[R] = p;
       else static_cast<elem_t*>(g.image)[frag_pos(R, Cc, g.K, g.chained != 0)] = static_cast<elem_t>(p);
     }
-  }
-}
-
-// pack_param over a table copied to LDS (the fused actor optimiser): the segment loop unrolled, so its reads
-// are issued together instead of one scalar-memory round trip per field per segment and element
-__device__ __forceinline__ void pack_param_lds(const AsvPackSeg* __restrict__ t, int n, int64_t i, float p) {
-#pragma unroll
-  for (int k = 0; k < ASVRL_MAX_PACK_SEGS; ++k) {
-    if (k >= n) break;
-    const AsvPackSeg g = t[k];
-    const int64_t u64 = i - g.flat_off;
-    if (u64 < 0 || u64 >= static_cast<int64_t>(g.rows) * g.cols) continue;
-    const unsigned u = static_cast<unsigned>(u64), cols = static_cast<unsigned>(g.cols);
-    const int r = static_cast<int>(u / cols), c = static_cast<int>(u - static_cast<unsigned>(r) * cols);
-    for (int q = 0; q < g.nrep; ++q) {
-      int R = g.row0 + r + q * g.rep_row, Cc = g.col0 + c + q * g.rep_col;
-      if (g.transposed) { const int x = R; R = Cc; Cc = x; }
-      if (g.f32) static_cast<float*>(g.image)[R] = p;
-      else static_cast<elem_t*>(g.image)[frag_pos(R, Cc, g.K, g.chained != 0)] = static_cast<elem_t>(p);
-    }
-  }
-}
-
-// The image positions pack_param would write for parameter i, from a table in LDS: up to P byte addresses
-// (bit 0 set: an f32 copy, else an operand-dtype image element), in pack_param's order -- computed while the
-// fused actor optimiser waits for the norm, stored after the update (pack_store).
-template <int P>
-__device__ __forceinline__ int pack_positions(const AsvPackSeg* __restrict__ t, int n, int64_t i, uint64_t (&pos)[P]) {
-  int np = 0;
-#pragma unroll
-  for (int q = 0; q < P; ++q) pos[q] = 0;
-#pragma unroll
-  for (int k = 0; k < ASVRL_MAX_PACK_SEGS; ++k) {
-    if (k >= n) break;
-    const AsvPackSeg g = t[k];
-    const int64_t u64 = i - g.flat_off;
-    if (u64 < 0 || u64 >= static_cast<int64_t>(g.rows) * g.cols) continue;
-    const unsigned u = static_cast<unsigned>(u64), cols = static_cast<unsigned>(g.cols);
-    const int r = static_cast<int>(u / cols), c = static_cast<int>(u - static_cast<unsigned>(r) * cols);
-    for (int q = 0; q < g.nrep; ++q) {
-      int R = g.row0 + r + q * g.rep_row, Cc = g.col0 + c + q * g.rep_col;
-      if (g.transposed) { const int x = R; R = Cc; Cc = x; }
-      const uint64_t addr = g.f32 ? reinterpret_cast<uint64_t>(static_cast<float*>(g.image) + R) | 1ull
-                                  : reinterpret_cast<uint64_t>(static_cast<elem_t*>(g.image) +
-                                                               frag_pos(R, Cc, g.K, g.chained != 0));
-#pragma unroll
-      for (int w = 0; w < P; ++w)   // pos[np] = addr without a dynamic register index
-        if (w == np) pos[w] = addr;
-      np = np + 1 < P ? np + 1 : P;
-    }
-  }
-  return np;
-}
-
-template <int P>
-__device__ __forceinline__ void pack_store(const uint64_t (&pos)[P], int np, float p) {
-#pragma unroll
-  for (int q = 0; q < P; ++q) {
-    if (q >= np) break;
-    if (pos[q] & 1ull) *reinterpret_cast<float*>(pos[q] & ~1ull) = p;
-    else *reinterpret_cast<elem_t*>(pos[q]) = static_cast<elem_t>(p);
   }
 }
 

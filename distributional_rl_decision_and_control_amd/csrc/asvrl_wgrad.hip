@@ -13,7 +13,8 @@
 // workgroups write f32 partials that a second launch sums in a fixed order (deterministic).
 // The f32 build (ASVRL_OPERAND_F32, asvrl_mfma.h) stages f32 rows (4 per 16-byte chunk) and reads
 // its operand fragments with plain LDS loads into the eight v_mfma_f32_32x32x2_f32 of mfma().
-#include "asvrl_adam.h"
+#include "asvrl_common.h"
+#include "asvrl_mfma.h"
 
 #include <algorithm>
 
@@ -656,7 +657,6 @@ struct AgLds {
     float out[18][kAgT];      // output layer: [8 + 8 column sums, 2 bias sums][thread]
   } u;
   double red[kAgT];
-  AsvPackSeg pk[ASVRL_MAX_PACK_SEGS];   // the fused optimiser's pack table
   int last;
 };
 
@@ -789,138 +789,27 @@ __device__ __forceinline__ bool ag_tile(const elem_t* __restrict__ dz, int ldz, 
 struct AgArgs {
   AsvActorGradIO io;
   int S, nch;   // row splits, kAgRS-row chunks per split
-  int adam;                 // 1: the clip + Adam step of the actor's FusedAdam runs in this launch
-  AsvActorAdam ad;
-  PackTable pk;
 };
 
-// The finalizers (every tile's last split, the encoder fold, the output layer): kAgSlots of them.
-// the "all arrived" flag is kept in kAgDoneRep replicas on 128-byte lines of their own, finisher b polling
-// replica b % kAgDoneRep: one line polled by every finisher serialised the polls (exit lag up to 3 us)
-constexpr int kAgCtrArrive = kAgCounters, kAgCtrLeave = kAgCounters + 1, kAgDoneBase = 64, kAgDoneStride = 32,
-              kAgDoneRep = 16, kAgCtrErr = kAgDoneBase + kAgDoneStride * kAgDoneRep, kAgCountersAdam = kAgCtrErr + 1;
-static_assert(kAgCtrLeave < kAgDoneBase, "sync words before the replicas");
-constexpr int kAgMaxEl = 5;   // outputs per thread of a finalizer (tile: 4 + bias)
+constexpr int kAgMaxEl = 5;   // outputs per thread of a finisher (tile: 4 + bias)
 
-// A finalizer's outputs (thread t: n of them, gradient addresses and values): the squared norm of the
-// finalizer into norm_parts[slot]; without the fused optimiser the gradients are stored. With it, every
-// finalizer waits for all kAgSlots partials (its parameters' moments loaded meanwhile), folds them exactly as
-// adam_kernel does (asvrl_optim.hip), and applies clip + Adam + re-pack to its own outputs; the last to leave
-// advances step / norm_out / counter. All finalizers are resident while they wait: the grid fits the chip
-// (two 67 KB workgroups per CU) and the other kernels of a step all finish.
+// A finisher's outputs (thread t: n of them, gradient addresses and values) are stored, and its squared
+// norm goes to norm_parts[slot] (folded by the optimiser launch). (An optimiser step inside this launch, its
+// finishers waiting for each other, was measured 22 us against 17 + 7 but could wait for minutes behind the
+// kernels of other streams: profiles/r03p1_fused_adam_timeout.txt.)
 __device__ __forceinline__ void ag_finish(const AgArgs& a, float* const (&dst)[kAgMaxEl], const float (&val)[kAgMaxEl],
                                           int n, int slot, AgLds& L) {
   const AsvActorGradIO& io = a.io;
-  const int t = threadIdx.x;
   double sq = 0.0;
-#pragma unroll
-  for (int e = 0; e < kAgMaxEl; ++e)
-    if (e < n) sq += static_cast<double>(val[e]) * val[e];
-  if (!a.adam) {
-#pragma unroll
-    for (int e = 0; e < kAgMaxEl; ++e)
-      if (e < n) *dst[e] = val[e];
-    sq = ag_block_sum(sq, L);
-    if (t == 0 && io.norm_parts != nullptr) io.norm_parts[slot] = sq;
-    return;
-  }
-  const AsvActorAdam& ad = a.ad;
-  int64_t fi[kAgMaxEl];
-  float mo[kAgMaxEl], vo[kAgMaxEl], po[kAgMaxEl];
-#pragma unroll
-  for (int e = 0; e < kAgMaxEl; ++e) {   // the moments and parameters, in flight under the wait
-    fi[e] = e < n ? dst[e] - ad.grads : 0;
-    mo[e] = ad.exp_avg[fi[e]];
-    vo[e] = ad.exp_avg_sq[fi[e]];
-    po[e] = ad.params[fi[e]];
-  }
-  {   // the pack table into LDS (read per element below)
-    const int* src = reinterpret_cast<const int*>(a.pk.s);
-    int* dstl = reinterpret_cast<int*>(L.pk);
-    constexpr int kWords = static_cast<int>(sizeof(AsvPackSeg)) / 4 * ASVRL_MAX_PACK_SEGS;
-    for (int k = t; k < kWords; k += kAgT) dstl[k] = src[k];
-  }
-  const float step_old = ad.step[0];   // advanced by the last finalizer to leave, after every read
-  sq = ag_block_sum(sq, L);
-  int* ctr = io.counters;
-  AG_STAMP(5);
-  if (t == 0) {
-    __hip_atomic_store(io.norm_parts + slot, sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int o = __hip_atomic_fetch_add(ctr + kAgCtrArrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    L.last = o == kAgSlots - 1;
-    if (o == kAgSlots - 1) {
-      __hip_atomic_store(ctr + kAgCtrArrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int k = 0; k < kAgDoneRep; ++k)
-        __hip_atomic_store(ctr + kAgDoneBase + kAgDoneStride * k, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  // while the others arrive: the step's bias corrections (two f64 pow; only the clip coefficient needs the
-  // norm) and the weight-image positions of this workgroup's parameters
-  AdamCoef ac = adam_step_scalars(static_cast<double>(step_old) + 1.0, ad.lr, ad.beta1, ad.beta2);
-  constexpr int kP = 5;
-  uint64_t pos[kAgMaxEl][kP];
-  int npos[kAgMaxEl];
-#pragma unroll
-  for (int e = 0; e < kAgMaxEl; ++e) npos[e] = e < n ? pack_positions<kP>(L.pk, a.pk.n, fi[e], pos[e]) : 0;
-  if (t == 0 && !L.last) {
-    int spins = 0;
-    // polled by an atomic RMW, which executes at the memory side: a plain or sc1 poll can keep re-reading
-    // a copy of the line its own XCD's L2 took while the flag was still 0 (the f32 build's longer waits
-    // timed out that way)
-    int* done = ctr + kAgDoneBase + kAgDoneStride * (static_cast<int>(blockIdx.x) % kAgDoneRep);
-    while (__hip_atomic_fetch_or(done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1 << 24)) {   // never expected: flag it and go on rather than hang the device
-        __hip_atomic_store(ctr + kAgCtrErr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-  AG_STAMP(6);
-  // adam_kernel's fold: thread t takes partial t (kAgSlots < 256), then the same pairwise tree
-  if (t < kAgSlots) {   // memory-side reads (atomic RMW) like the flag's
-    const unsigned long long u = __hip_atomic_fetch_or(reinterpret_cast<unsigned long long*>(io.norm_parts) + t, 0ull,
-                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    L.red[t] = __builtin_bit_cast(double, u);
-  } else {
-    L.red[t] = 0.0;
-  }
-  __syncthreads();
-  for (int w = kAgT / 2; w > 0; w >>= 1) {
-    if (t < w) L.red[t] += L.red[t + w];
-    __syncthreads();
-  }
-  const float norm = static_cast<float>(sqrt(L.red[0]));
-  AG_STAMP(8);
-  adam_clip(ac, norm, ad.max_norm);
-  AG_STAMP(9);
 #pragma unroll
   for (int e = 0; e < kAgMaxEl; ++e) {
     if (e >= n) break;
-    float gi;
-    const float pn = adam_elem(ac, ad.beta2, ad.eps, val[e], mo[e], vo[e], po[e], gi);
-    *dst[e] = gi;
-    ad.exp_avg[fi[e]] = mo[e];
-    ad.exp_avg_sq[fi[e]] = vo[e];
-    ad.params[fi[e]] = pn;
-    pack_store<kP>(pos[e], npos[e], pn);
+    *dst[e] = val[e];
+    sq += static_cast<double>(val[e]) * val[e];
   }
-  AG_STAMP(10);
-  __syncthreads();
-  if (t == 0) {
-    const int o = __hip_atomic_fetch_add(ctr + kAgCtrLeave, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (o == kAgSlots - 1) {
-      __hip_atomic_store(ctr + kAgCtrLeave, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int k = 0; k < kAgDoneRep; ++k)
-        __hip_atomic_store(ctr + kAgDoneBase + kAgDoneStride * k, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      ad.step[0] = step_old + 1.f;
-      if (ad.norm_out != nullptr) ad.norm_out[0] = norm;
-      if (ad.counter != nullptr) ad.counter[0] += 1;
-    }
-  }
-  AG_STAMP(7);
+  sq = ag_block_sum(sq, L);
+  if (threadIdx.x == 0 && io.norm_parts != nullptr) io.norm_parts[slot] = sq;
+  AG_STAMP(5);
 }
 
 __global__ __launch_bounds__(kAgT) void actor_grads_kernel(AgArgs a) {
@@ -1087,23 +976,14 @@ __global__ __launch_bounds__(kAgT) void actor_grads_kernel(AgArgs a) {
   if (t == 0) io.loss_out[0] = static_cast<float>(tot);
 }
 
-// Row splits and chunks per split: one chunk of kAgRS rows per split where the whole grid (57 S + 1
-// workgroups) is resident at once, more chunks per split otherwise -- the fused optimiser's finishing
-// workgroups wait for each other, which needs every workgroup of the launch resident (a grid larger than
-// the chip hung the f32 build's launch behind its waiting workgroups)
+// Row splits (one chunk of kAgRS rows each at the bench shape); more rows per split only where the grid would
+// pass 4096 workgroups (a very large B)
 struct AgSplit {
   int S, nch;
 };
 AgSplit ag_split(int B) {
-  static int cap = 0;
-  if (cap == 0) {
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, actor_grads_kernel, kAgT, 0) != hipSuccess || per_cu < 1)
-      per_cu = 1;
-    cap = per_cu * cu_count();
-  }
   const int chunks = (B + kAgRS - 1) / kAgRS;
-  const int smax = (cap - 1 - kAgOutItems) / kAgTiles > 1 ? (cap - 1 - kAgOutItems) / kAgTiles : 1;
+  const int smax = (4096 - 1 - kAgOutItems) / kAgTiles;
   const int nch = (chunks + smax - 1) / smax;
   return AgSplit{(chunks + nch - 1) / nch, nch};
 }
@@ -1298,7 +1178,7 @@ extern "C" int64_t asvrl_actor_grads_workspace(int32_t B) {
   const int64_t S = ag_split(B).S;
   return static_cast<int64_t>(kAgTiles) * S * kAgSlab + kAgEncImg;
 }
-extern "C" int32_t asvrl_actor_grads_counters(void) { return kAgCountersAdam; }
+extern "C" int32_t asvrl_actor_grads_counters(void) { return kAgCounters; }
 extern "C" int32_t asvrl_actor_grads_norm_parts(void) { return kAgSlots; }
 
 namespace {
@@ -1334,26 +1214,3 @@ extern "C" int asvrl_actor_grads(const AsvActorGradIO* io, void* stream) {
   return launch_actor_grads(a, as_stream(stream));
 }
 
-extern "C" int asvrl_actor_grads_adam(const AsvActorGradIO* io, const AsvActorAdam* ad, void* stream) {
-  if (int rc = check_actor_grads(io)) return rc;
-  ASVRL_REQUIRE(ad && ad->params && ad->grads && ad->exp_avg && ad->exp_avg_sq && ad->step,
-                "asvrl_actor_grads_adam: null optimiser argument");
-  ASVRL_REQUIRE(io->norm_parts != nullptr && io->step == nullptr,
-                "asvrl_actor_grads_adam: needs norm_parts, and the step is the optimiser's (io->step = NULL)");
-  ASVRL_REQUIRE(ad->nseg >= 0 && ad->nseg <= ASVRL_MAX_PACK_SEGS && (ad->nseg == 0 || ad->segs != nullptr),
-                "asvrl_actor_grads_adam: bad pack table");
-  for (const float* g : {io->w1_grad, io->b1_grad, io->w2_grad, io->b2_grad, io->wo_grad, io->bo_grad, io->enc_grad})
-    ASVRL_REQUIRE(g >= ad->grads && g < ad->grads + ad->n, "asvrl_actor_grads_adam: a gradient outside the flat buffer");
-  ASVRL_REQUIRE(io->enc_grad + kAgEncOut <= ad->grads + ad->n, "asvrl_actor_grads_adam: encoder grads outside the buffer");
-  if (io->B == 0) return 0;
-  AgArgs a{};
-  a.io = *io;
-  const AgSplit sp = ag_split(io->B);
-  a.S = sp.S;
-  a.nch = sp.nch;
-  a.adam = 1;
-  a.ad = *ad;
-  for (int k = 0; k < ad->nseg; ++k) a.pk.s[k] = ad->segs[k];
-  a.pk.n = ad->nseg;
-  return launch_actor_grads(a, as_stream(stream));
-}

@@ -189,26 +189,17 @@ class ActorGrads:
     def __init__(self, B, device, operands="bf16"):
         self.L = _abi.lib(operands)
         self.work = torch.empty(int(self.L.asvrl_actor_grads_workspace(B)), dtype=torch.float32, device=device)
-        # arrival counters and the fused optimiser's wait words: zero, and left zero by every launch
+        # arrival counters: zero, and left zero by every launch
         self.counters = torch.zeros(int(self.L.asvrl_actor_grads_counters()), dtype=torch.int32, device=device)
         self.nparts = int(self.L.asvrl_actor_grads_norm_parts())
         self.norm_parts = torch.zeros(self.nparts, dtype=torch.float64, device=device)
 
-    def check(self):
-        """Raise if a launch's finishing workgroups ever stopped waiting for each other on the bounded spin
-        (the last counter word; never expected -- the launch sizes its grid to stay resident). Host sync."""
-        if int(self.counters[-1].item()) != 0:
-            raise RuntimeError("asvrl_actor_grads_adam: a finishing workgroup timed out waiting for the others")
 
-
-def actor_grads(ws, bufs, actor, tile_loss=None, loss_out=None, step=None, norm=True, adam=None, pack=None,
-                counter=None, stream=None):
+def actor_grads(ws, bufs, actor, tile_loss=None, loss_out=None, step=None, norm=True, stream=None):
     """Every .grad of `actor` (hidden_layer, hidden_layer_2, output_layer, both observation encoders, whose
     four gradients must be contiguous: FusedAdam / FlatGrads) from bufs' backward outputs and saved
-    activations, the loss sum(tile_loss) -> loss_out, the norm partials (ws.norm_parts) and step += 1, in ONE
-    launch (asvrl_actor_grads; agent.py:424-426). adam: the actor's FusedAdam -- its clip + Adam step (with the
-    AsvPackSeg list `pack` and the device `counter`, as FusedAdam.step_prenormed) runs in the same launch
-    (asvrl_actor_grads_adam); returns its pre-clip norm then."""
+    activations, the loss sum(tile_loss) -> loss_out, the norm partials (ws.norm_parts, for
+    FusedAdam.step_prenormed) and step += 1, in ONE launch (asvrl_actor_grads; agent.py:424-426)."""
     se, oe = actor.self_encoder[0], actor.object_encoder[0]
     gs = [se.weight.grad, se.bias.grad, oe.weight.grad, oe.bias.grad]
     if not all(gs[k].data_ptr() + 4 * gs[k].numel() == gs[k + 1].data_ptr() for k in range(3)):
@@ -225,26 +216,10 @@ def actor_grads(ws, bufs, actor, tile_loss=None, loss_out=None, step=None, norm=
     io.w2_grad, io.b2_grad = h2l.weight.grad.data_ptr(), h2l.bias.grad.data_ptr()
     io.wo_grad, io.bo_grad = ol.weight.grad.data_ptr(), ol.bias.grad.data_ptr()
     io.enc_grad = gs[0].data_ptr()
-    io.norm_parts = ws.norm_parts.data_ptr() if (norm or adam is not None) else None
+    io.norm_parts = ws.norm_parts.data_ptr() if norm else None
+    io.step = _p(step)
     io.work, io.work_floats, io.counters = ws.work.data_ptr(), ws.work.numel(), ws.counters.data_ptr()
-    if adam is None:
-        io.step = _p(step)
-        _abi.check(ws.L.asvrl_actor_grads(C.byref(io), _abi.stream_ptr(stream)), "asvrl_actor_grads", ws.L)
-        return None
-    assert step is None and adam.L is ws.L, "the optimiser's step; the same build"
-    ad = _abi.AsvActorAdam()
-    ad.params, ad.grads = adam.flat.data_ptr(), adam.grads.flat.data_ptr()
-    ad.exp_avg, ad.exp_avg_sq, ad.n = adam.exp_avg.data_ptr(), adam.exp_avg_sq.data_ptr(), adam.n
-    ad.step = adam.step_t.data_ptr()
-    ad.lr, ad.beta1, ad.beta2, ad.eps, ad.max_norm = adam.lr, adam.betas[0], adam.betas[1], adam.eps, adam.max_norm
-    ad.norm_out = adam.norm.data_ptr()
-    segs = list(pack or [])
-    arr = (_abi.AsvPackSeg * max(1, len(segs)))(*segs)
-    ad.segs, ad.nseg = C.cast(arr, C.c_void_p), len(segs)
-    ad.counter = _p(counter)
-    _abi.check(ws.L.asvrl_actor_grads_adam(C.byref(io), C.byref(ad), _abi.stream_ptr(stream)),
-               "asvrl_actor_grads_adam", ws.L)
-    return adam.norm[0]
+    _abi.check(ws.L.asvrl_actor_grads(C.byref(io), _abi.stream_ptr(stream)), "asvrl_actor_grads", ws.L)
 
 
 def encoder_fold(dw, db, net, accumulate=False, stream=None):

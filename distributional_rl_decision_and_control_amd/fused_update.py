@@ -1,5 +1,5 @@
 """The whole AC-IQN update (Agent.train_AC_IQN, agent.py:386-432) on hand-written gfx950
-kernels: eight launches per step (with the vectorised loop's fused prologue), no torch autograd, no host
+kernels: nine launches per step (with the vectorised loop's fused prologue), no torch autograd, no host
 synchronisation.
 
 Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | done):
@@ -19,8 +19,8 @@ Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | 
     encoders(s, a) + trunk forward + backward of -mean(q) to the action
                                                           asvrl_critic_actor_grad (dA in-kernel)
     actor backward                                       asvrl_actor_backward
-    every actor .grad, the actor loss, clip + Adam +     ONE asvrl_actor_grads_adam (split tiles reduced
-    re-pack of the actor's weight images                 in-launch, the optimiser in their finishing workgroups)
+    every actor .grad, the actor loss, the norm partials  ONE asvrl_actor_grads (split tiles reduced in-launch)
+    clip + Adam + re-pack                                asvrl_adam_step_pack
 (supported() admits only shapes the fused critic launch takes: B a multiple of 32, so B*N one of its
 64-row round.)
 
@@ -202,15 +202,16 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     actor_backward(st.actor, ab)
     # every actor .grad, the actor loss, the norm partials and the Adam step count in one launch
     fused_opt = sync is None and isinstance(actor_opt, FusedAdam)
-    if fused_opt:   # ... and the clip + Adam + re-pack in the same launch (asvrl_actor_grads_adam)
+    actor_grads_launch(st.agrads, ab, actor, st.tile_loss[1], st.losses[1:2],
+                       step=actor_opt.step_t if fused_opt else None, norm=fused_opt)
+    if fused_opt:
         if actor_wait is not None:
             torch.cuda.current_stream().wait_event(actor_wait)
         if not hasattr(st.actor, "_adam_segs"):
             st.actor._adam_segs = st.actor.adam_segments(actor_opt)
-        agn = actor_grads_launch(st.agrads, ab, actor, st.tile_loss[1], st.losses[1:2], adam=actor_opt,
-                                 pack=st.actor._adam_segs, counter=counter)
+        agn = actor_opt.step_prenormed(st.agrads.norm_parts, st.agrads.nparts, pack=st.actor._adam_segs,
+                                       counter=counter)
     else:
-        actor_grads_launch(st.agrads, ab, actor, st.tile_loss[1], st.losses[1:2], norm=False)
         if sync is not None:
             sync(actor_grads)
         if actor_wait is not None:

@@ -762,25 +762,6 @@ int64_t asvrl_actor_grads_workspace(int32_t B);
 int32_t asvrl_actor_grads_counters(void);
 int32_t asvrl_actor_grads_norm_parts(void);
 int asvrl_actor_grads(const AsvActorGradIO* io, void* stream);
-/* asvrl_actor_grads with the actor's clip + Adam step (asvrl_adam_step_pack's arithmetic and fold order,
- * bit-identical to asvrl_actor_grads + asvrl_adam_step_pack) in the same launch: the workgroups that finish
- * the gradient tiles wait for every norm partial, then update their own parameters, moments and weight
- * images; grads hold the clipped gradients afterwards, *step / norm_out / counter advance as there.
- * io->norm_parts required, io->step NULL; every gradient pointer of io inside grads[0, n). */
-typedef struct AsvActorAdam {
-  float* params;
-  float* grads;
-  float* exp_avg;
-  float* exp_avg_sq;
-  int64_t n;
-  float* step;
-  float lr, beta1, beta2, eps, max_norm;
-  float* norm_out;
-  const AsvPackSeg* segs;
-  int32_t nseg;
-  int64_t* counter;
-} AsvActorAdam;
-int asvrl_actor_grads_adam(const AsvActorGradIO* io, const AsvActorAdam* adam, void* stream);
 
 /* One output unit's version: dw[k] = sum_r dq[r*ldq] x[r][k], db = sum_r dq[r*ldq] with dq f32 and
  * x bf16 (R x K, ldx); K in {64, 128, 256}; work >= 256 * (K + 1) floats. */

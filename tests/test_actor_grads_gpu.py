@@ -120,31 +120,3 @@ def test_actor_grads_argument_checks():
     assert L.asvrl_actor_grads(C.byref(io), None) != 0
     assert b"null" in L.asvrl_last_error()
 
-
-@pytest.mark.parametrize("operands", ["bf16", "f32"])
-def test_actor_grads_fused_adam_bit_identical(operands):
-    """asvrl_actor_grads_adam (the optimiser step in the gradient launch's finishing workgroups) equals
-    asvrl_actor_grads + asvrl_adam_step_pack bit for bit: parameters, moments, clipped gradients, step, norm,
-    learn counter and every re-packed weight image, over three consecutive steps."""
-    from distributional_rl_decision_and_control_amd.fused_mlp import MlpPack, actor_grads
-    runs = []
-    for fused in (False, True):
-        actor, opt, ab, ws = _setup(operands, 4096, seed=11)
-        pk = MlpPack(actor, "actor", operands)
-        segs = pk.adam_segments(opt)
-        counter = torch.zeros(1, dtype=torch.int64, device="cuda")
-        for k in range(3):
-            ab.dz1.mul_(1.5)   # a different gradient every step
-            if fused:
-                actor_grads(ws, ab, actor, adam=opt, pack=segs, counter=counter)
-            else:
-                actor_grads(ws, ab, actor, step=opt.step_t)
-                opt.step_prenormed(ws.norm_parts, ws.nparts, pack=segs, counter=counter)
-        torch.cuda.synchronize()
-        runs.append([opt.flat.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(), opt.grads.flat.clone(),
-                     opt.step_t.clone(), opt.norm.clone(), counter.clone(), pk.enc.clone(), pk.b_enc.clone(),
-                     pk.w1.clone(), pk.w1t.clone(), pk.w2.clone(), pk.w2t.clone()])
-        assert int(ws.counters.abs().sum()) == 0
-    for i, (x, y) in enumerate(zip(*runs)):
-        assert torch.equal(x, y), (i, float((x.double() - y.double()).abs().max()))
-    assert runs[1][4].item() == 3.0 and runs[1][6].item() == 3

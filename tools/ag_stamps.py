@@ -23,7 +23,7 @@ def main():
     from distributional_rl_decision_and_control_amd import _abi
     from distributional_rl_decision_and_control_amd.fused_mlp import MlpPack, actor_grads
     from tests.test_actor_grads_gpu import _setup
-    adam = len(sys.argv) > 1 and sys.argv[1] == "adam"
+    adam = False
     B = 4096
     actor, opt, ab, ws = _setup("bf16", B, seed=3)
     pk = MlpPack(actor, "actor", "bf16")
@@ -37,10 +37,7 @@ def main():
     for it in range(30):
         if it == 20:
             ev0.record()
-        if adam:
-            actor_grads(ws, ab, actor, adam=opt, pack=segs)
-        else:
-            actor_grads(ws, ab, actor, step=opt.step_t)
+        actor_grads(ws, ab, actor, step=opt.step_t)
     ev1.record()
     torch.cuda.synchronize()
     print(f"S={S} nch={nch} blocks={nblk} adam={adam}: {ev0.elapsed_time(ev1) / 10 * 1e3:.1f} us per launch "
