@@ -135,7 +135,7 @@ SUM_PLAIN, SUM_FOLD_ENCODERS = 0, 1
 
 
 MAX_WGRAD_SEGS = 24
-MAX_PACK_SEGS = 8
+MAX_PACK_SEGS = 16
 
 
 class AsvPackSeg(C.Structure):

@@ -39,6 +39,26 @@ __device__ __forceinline__ void pack_param(const PackTable& t, int64_t i, float 
   }
 }
 
+// pack_param over a table copied to LDS: the segment scan unrolled, so its reads are issued together instead
+// of a scalar-memory round trip per field, segment and element (the kernel-argument table read in a loop)
+__device__ __forceinline__ void pack_param_lds(const AsvPackSeg* __restrict__ t, int n, int64_t i, float p) {
+#pragma unroll
+  for (int k = 0; k < ASVRL_MAX_PACK_SEGS; ++k) {
+    if (k >= n) break;
+    const AsvPackSeg g = t[k];
+    const int64_t u64 = i - g.flat_off;
+    if (u64 < 0 || u64 >= static_cast<int64_t>(g.rows) * g.cols) continue;
+    const unsigned u = static_cast<unsigned>(u64), cols = static_cast<unsigned>(g.cols);
+    const int r = static_cast<int>(u / cols), c = static_cast<int>(u - static_cast<unsigned>(r) * cols);
+    for (int q = 0; q < g.nrep; ++q) {
+      int R = g.row0 + r + q * g.rep_row, Cc = g.col0 + c + q * g.rep_col;
+      if (g.transposed) { const int x = R; R = Cc; Cc = x; }
+      if (g.f32) static_cast<float*>(g.image)[R] = p;
+      else static_cast<elem_t*>(g.image)[frag_pos(R, Cc, g.K, g.chained != 0)] = static_cast<elem_t>(p);
+    }
+  }
+}
+
 // The step's scalars, computed identically wherever the update runs.
 struct AdamCoef {
   float coef, step_size, bc2_sqrt, w1, w2;

@@ -49,6 +49,7 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(float* __restrict__ p
                                                             int64_t* __restrict__ counter) {
   __shared__ float s_norm;
   __shared__ double s_red[kOptThreads];
+  __shared__ AsvPackSeg s_pk[ASVRL_MAX_PACK_SEGS];
   // this thread's first parameter, its moments and gradient loaded before the norm fold (they do not
   // depend on it: one memory round trip fewer on the launch's critical path)
   const int64_t i0 = static_cast<int64_t>(blockIdx.x) * kOptThreads + threadIdx.x;
@@ -61,6 +62,12 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(float* __restrict__ p
   }
   // the step's bias corrections (two f64 pow) while the norm partials are folded: only the clip needs the norm
   AdamCoef ac = adam_step_scalars(static_cast<double>(step[0]), lr, beta1, beta2);
+  {   // the pack table into LDS (read per element below)
+    const int* src = reinterpret_cast<const int*>(pk.s);
+    int* dst = reinterpret_cast<int*>(s_pk);
+    constexpr int kWords = static_cast<int>(sizeof(AsvPackSeg)) / 4 * ASVRL_MAX_PACK_SEGS;
+    for (int k = threadIdx.x; k < kWords; k += kOptThreads) dst[k] = src[k];
+  }
   {   // thread t folds partials t, t + 256, ... in order, then a fixed tree: the same in every block
     double x = 0.0;
     x = strided_sum<double>(partial, threadIdx.x, nparts, kOptThreads, x);
@@ -86,7 +93,7 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(float* __restrict__ p
     m[i] = mo;
     v[i] = vo;
     p[i] = pn;
-    if (pk.n > 0) pack_param(pk, i, pn);
+    pack_param_lds(s_pk, pk.n, i, pn);
   }
   if (counter != nullptr && blockIdx.x == 0 && threadIdx.x == 0) counter[0] += 1;
 }

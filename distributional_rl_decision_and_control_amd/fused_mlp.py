@@ -27,35 +27,70 @@ def _p(t):
 class MlpPack:
     """Packed images of an Actor (kind='actor'), of a Critic's encoders + action encoder
     (kind='critic') or of the observation encoders alone (kind='encoders', IQN_Policy).
-    operands="f32": f32 images for libasvrl_f32.so (the parity build); launches go to self.L."""
+    operands="f32": f32 images for libasvrl_f32.so (the parity build); launches go to self.L.
 
-    def __init__(self, net, kind, operands="bf16"):
+    double=True (an Actor in the batched loop): two image sets, with f32 copies of the biases and the output
+    layer in each. Launches read set `parity` (self.w); the optimiser step writes the other one
+    (adam_segments) and flip() makes it current -- so the rollout's act kernel, which reads the current set,
+    never races the step that rewrites the weights (no cross-stream wait before the optimiser)."""
+
+    def __init__(self, net, kind, operands="bf16", double=False):
         assert kind in ("actor", "critic", "encoders")
+        assert not double or kind == "actor"
         self.net, self.kind = net, kind
         self.operands = operands
         self.L = _abi.lib(operands)
+        self.double = double
+        self.parity = 0
+        self.sets = [self._make_set(net, kind, operands, double) for _ in range(2 if double else 1)]
+        self._segs = {}
+        self.refresh()
+
+    @staticmethod
+    def _make_set(net, kind, operands, copies):
         dev = net.self_encoder[0].weight.device
         bf = dict(dtype=_abi.operand_dtype(operands), device=dev)
-        self.enc = torch.zeros(ENC * OBSK, **bf)
-        self.b_enc = torch.zeros(ENC, dtype=torch.float32, device=dev)
+        f = dict(dtype=torch.float32, device=dev)
+        t = {"enc": torch.zeros(ENC * OBSK, **bf), "b_enc": torch.zeros(ENC, **f)}
         w = _abi.AsvMlpWeights()
-        w.enc_frag, w.b_enc = self.enc.data_ptr(), self.b_enc.data_ptr()
+        w.enc_frag, w.b_enc = t["enc"].data_ptr(), t["b_enc"].data_ptr()
         if kind == "actor":
-            self.w1 = torch.zeros(HID * ENC, **bf)
-            self.w2 = torch.zeros(HID * HID, **bf)
-            self.w2t = torch.zeros(HID * HID, **bf)
-            self.w1t = torch.zeros(ENC * HID, **bf)
-            w.w1_frag, w.w2_frag, w.w2t_frag, w.w1t_frag = (self.w1.data_ptr(), self.w2.data_ptr(),
-                                                           self.w2t.data_ptr(), self.w1t.data_ptr())
-            w.b1, w.b2 = net.hidden_layer.bias.data_ptr(), net.hidden_layer_2.bias.data_ptr()
-            w.wout, w.bout = net.output_layer.weight.data_ptr(), net.output_layer.bias.data_ptr()
+            for k, n in (("w1", HID * ENC), ("w2", HID * HID), ("w2t", HID * HID), ("w1t", ENC * HID)):
+                t[k] = torch.zeros(n, **bf)
+            w.w1_frag, w.w2_frag, w.w2t_frag, w.w1t_frag = (t["w1"].data_ptr(), t["w2"].data_ptr(),
+                                                           t["w2t"].data_ptr(), t["w1t"].data_ptr())
+            if copies:   # the f32 parameters the kernels read, copied per set
+                for k, p in (("b1", net.hidden_layer.bias), ("b2", net.hidden_layer_2.bias),
+                             ("wout", net.output_layer.weight), ("bout", net.output_layer.bias)):
+                    t[k] = torch.zeros(p.numel(), **f)
+                w.b1, w.b2, w.wout, w.bout = (t["b1"].data_ptr(), t["b2"].data_ptr(), t["wout"].data_ptr(),
+                                              t["bout"].data_ptr())
+            else:
+                w.b1, w.b2 = net.hidden_layer.bias.data_ptr(), net.hidden_layer_2.bias.data_ptr()
+                w.wout, w.bout = net.output_layer.weight.data_ptr(), net.output_layer.bias.data_ptr()
             w.out_scale = float(net.atan_scale.float().item())
         elif kind == "critic":
-            self.ae = torch.zeros(HID * 16, **bf)
-            w.ae_frag = self.ae.data_ptr()
+            t["ae"] = torch.zeros(HID * 16, **bf)
+            w.ae_frag = t["ae"].data_ptr()
             w.b_ae = net.action_encoder[0].bias.data_ptr()
-        self.w = w
-        self.refresh()
+        t["w"] = w
+        return t
+
+    @property
+    def w(self):
+        """The AsvMlpWeights of the current image set."""
+        return self.sets[self.parity]["w"]
+
+    def __getattr__(self, name):   # the current set's images: enc, b_enc, w1, w2, w2t, w1t, ae
+        sets = self.__dict__.get("sets")
+        if sets is not None and name in sets[self.__dict__["parity"]]:
+            return sets[self.__dict__["parity"]][name]
+        raise AttributeError(name)
+
+    def flip(self):
+        """The set the last optimiser step wrote becomes current (double packs; host-side, at enqueue)."""
+        if self.double:
+            self.parity ^= 1
 
     def src(self):
         n = self.net
@@ -71,26 +106,44 @@ class MlpPack:
     def adam_segments(self, opt):
         """The actor's images as AsvPackSeg of FusedAdam `opt` (asvrl_adam_step_pack): the block-structured
         encoder image (self encoder once, the object encoder at its five diagonal blocks), the f32 encoder
-        bias copy and the four hidden-layer images."""
+        bias copy and the four hidden-layer images -- of the set the step writes (double packs: the other
+        set, with the f32 copies of the biases and the output layer; call flip() after the step)."""
         assert self.kind == "actor"
-        n = self.net
+        dst = self.parity ^ 1 if self.double else 0
+        if dst in self._segs:
+            return self._segs[dst]
+        n, t = self.net, self.sets[dst]
         se, oe = n.self_encoder[0], n.object_encoder[0]
         nso, nsi = se.weight.shape
         noo, noi = oe.weight.shape
         W1, W2 = n.hidden_layer.weight, n.hidden_layer_2.weight
-        return [opt.pack_seg(se.weight, self.enc, K=OBSK),
-                opt.pack_seg(oe.weight, self.enc, K=OBSK, row0=nso, col0=nsi, nrep=MAX_OBJ, rep_row=noo, rep_col=noi),
-                opt.pack_seg(se.bias, self.b_enc, f32=True),
-                opt.pack_seg(oe.bias, self.b_enc, f32=True, row0=nso, nrep=MAX_OBJ, rep_row=noo),
-                opt.pack_seg(W1, self.w1, K=ENC, chained=True), opt.pack_seg(W1, self.w1t, K=HID, chained=True,
-                                                                            transposed=True),
-                opt.pack_seg(W2, self.w2, K=HID, chained=True), opt.pack_seg(W2, self.w2t, K=HID, chained=True,
-                                                                            transposed=True)]
+        segs = [opt.pack_seg(se.weight, t["enc"], K=OBSK),
+                opt.pack_seg(oe.weight, t["enc"], K=OBSK, row0=nso, col0=nsi, nrep=MAX_OBJ, rep_row=noo, rep_col=noi),
+                opt.pack_seg(se.bias, t["b_enc"], f32=True),
+                opt.pack_seg(oe.bias, t["b_enc"], f32=True, row0=nso, nrep=MAX_OBJ, rep_row=noo),
+                opt.pack_seg(W1, t["w1"], K=ENC, chained=True),
+                opt.pack_seg(W1, t["w1t"], K=HID, chained=True, transposed=True),
+                opt.pack_seg(W2, t["w2"], K=HID, chained=True),
+                opt.pack_seg(W2, t["w2t"], K=HID, chained=True, transposed=True)]
+        if self.double:
+            for k, p in (("b1", n.hidden_layer.bias), ("b2", n.hidden_layer_2.bias),
+                         ("wout", n.output_layer.weight), ("bout", n.output_layer.bias)):
+                segs.append(opt.pack_seg(p.reshape(-1), t[k], f32=True))
+        self._segs[dst] = segs
+        return segs
 
     def refresh(self, stream=None):
+        """Re-pack every image set from the f32 parameters (eager: initial packs, loads, the DP path)."""
         src = self.src()
-        _abi.check(self.L.asvrl_mlp_pack(C.byref(src), C.byref(self.w), _abi.stream_ptr(stream)),
-                   "asvrl_mlp_pack", self.L)
+        for t in self.sets:
+            _abi.check(self.L.asvrl_mlp_pack(C.byref(src), C.byref(t["w"]), _abi.stream_ptr(stream)),
+                       "asvrl_mlp_pack", self.L)
+            if self.double:
+                n = self.net
+                with torch.no_grad():
+                    for k, p in (("b1", n.hidden_layer.bias), ("b2", n.hidden_layer_2.bias),
+                                 ("wout", n.output_layer.weight), ("bout", n.output_layer.bias)):
+                        t[k].copy_(p.reshape(-1))
 
 
 def _rows(x):

@@ -62,14 +62,16 @@ class FusedACIQNState:
     operands="f32": every kernel from libasvrl_f32.so, the f32-operand parity build of the same
     sources (the optimisers must be FusedAdam of the same operands)."""
 
-    def __init__(self, policy_local, policy_target, B, N, operands="bf16"):
+    def __init__(self, policy_local, policy_target, B, N, operands="bf16", double_actor=False):
         dev = policy_local.critic.cos_embedding.weight.device
         self.B, self.N, self.device = B, N, dev
         self.operands = operands
         # the critic's encoders run inside the trunk kernels (f32, straight from the parameters)
         self.local_trunk = CriticPack(policy_local.critic, operands)
         self.target_trunk = CriticPack(policy_target.critic, operands)
-        self.actor = MlpPack(policy_local.actor, "actor", operands)
+        # double_actor (the batched loop): two actor image sets, the optimiser writing the one the act kernel
+        # does not read (MlpPack)
+        self.actor = MlpPack(policy_local.actor, "actor", operands, double=double_actor)
         self.target_actor = MlpPack(policy_target.actor, "actor", operands)
         self.abufs = ActorBuffers(B, dev, operands)
         self.agrads = ActorGrads(B, dev, operands)
@@ -205,12 +207,13 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     actor_grads_launch(st.agrads, ab, actor, st.tile_loss[1], st.losses[1:2],
                        step=actor_opt.step_t if fused_opt else None, norm=fused_opt)
     if fused_opt:
-        if actor_wait is not None:
+        # a concurrent act kernel reads the current actor images: with two sets the step writes the other one
+        # and no wait is needed (its cross-stream dependency costs ~7 us in a replayed graph)
+        if actor_wait is not None and not st.actor.double:
             torch.cuda.current_stream().wait_event(actor_wait)
-        if not hasattr(st.actor, "_adam_segs"):
-            st.actor._adam_segs = st.actor.adam_segments(actor_opt)
-        agn = actor_opt.step_prenormed(st.agrads.norm_parts, st.agrads.nparts, pack=st.actor._adam_segs,
+        agn = actor_opt.step_prenormed(st.agrads.norm_parts, st.agrads.nparts, pack=st.actor.adam_segments(actor_opt),
                                        counter=counter)
+        st.actor.flip()
     else:
         if sync is not None:
             sync(actor_grads)

@@ -77,7 +77,7 @@ class VecTrainer:
             self.critic_opt = FusedAdam(self.local.critic.parameters(), lr=lr, operands=operands)
             self.actor_grads, self.critic_grads = self.actor_opt.grads, self.critic_opt.grads
             self.action_dim = 2
-            self.fused2 = FusedACIQNState(self.local, self.target, batch_size, num_tau, operands)
+            self.fused2 = FusedACIQNState(self.local, self.target, batch_size, num_tau, operands, double_actor=True)
         elif agent_type == "IQN":
             self.local = IQN_Policy(**DEFAULT_NET, action_size=25, device=self.device, seed=net_seed).to(self.device)
             self.target = IQN_Policy(**DEFAULT_NET, action_size=25, device=self.device, seed=net_seed).to(self.device)

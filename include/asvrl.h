@@ -666,7 +666,7 @@ int asvrl_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_
  * (row0 + r + q*rep_row, col0 + c + q*rep_col) for q < nrep, swapped if transposed; f32 = 1 writes
  * image[row] as f32 (a bias copy, cols = 1), otherwise the bf16 fragment image of K columns (chained = 1:
  * an accumulator-fed layer's order). counter (optional): incremented once by the launch. */
-#define ASVRL_MAX_PACK_SEGS 8
+#define ASVRL_MAX_PACK_SEGS 16
 typedef struct AsvPackSeg {
   int64_t flat_off;
   void* image;
