@@ -160,8 +160,7 @@ def learn_prologue(st, replay, taus, seed, counter_dev=None, counter=0, out=None
 
 
 def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, actor_grads, rows, gamma=0.99,
-                         taus=None, sync=None, max_norm=0.5, actor_wait=None, counter=None, prologue_done=False,
-                         after_target=None):
+                         taus=None, sync=None, max_norm=0.5, actor_wait=None, counter=None, prologue_done=False):
     """One AC-IQN update from replay rows [B][88]. taus: (3, B, N) or None (drawn here).
     actor_wait: event to wait for before the actor's weights change (a concurrent act kernel).
     counter: an int64 device scalar incremented after the step (the learn counter; in-kernel when
@@ -181,8 +180,6 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     q_next = st.q_next
     if prologue_done:   # only the target critic is left of the target chain
         critic_forward(st.target_trunk, None, None, taus[0], st.N, q=q_next, obs=rows[:, OBS:2 * OBS], act=st.na)
-        if after_target is not None:   # the schedule's hook right after the target critic launch
-            after_target()
     else:
         actor_train_forward(st.actor, s_rows, ab)   # reads only s and the (not yet updated) actor
         target_q(st, rows, taus[0], q_next, st.na)

@@ -201,7 +201,7 @@ class VecTrainer:
         self.env.auto_reset(counted)
         self.env.advance_device(counted)
 
-    def learn(self, state=None, guard=0, actor_wait=None, after_target=None):
+    def learn(self, state=None, guard=0, actor_wait=None):
         """One learn step of batch B: sample (uniform ring, or the prioritised tree for Rainbow) and the
         agent's fused update. state / guard: the ring snapshot to sample against and the newest entries to
         skip (the overlapped schedule); actor_wait: an event to wait for before the actor's weights change."""
@@ -223,7 +223,7 @@ class VecTrainer:
             return ac_iqn_update_fused2(self.fused2, self.local, self.actor_opt, self.critic_opt, self.critic_grads,
                                         self.actor_grads, rows, gamma=self.gamma, sync=self.sync,
                                         actor_wait=actor_wait, taus=self.taus, counter=self.learn_counter,
-                                        prologue_done=True, after_target=after_target)
+                                        prologue_done=True)
         # the update's quantile fractions are drawn by the sampling launch
         rows = self.replay.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter, out=self.batch_rows,
                                   state=state, guard=guard, taus=self.taus)
@@ -363,32 +363,21 @@ class VecTrainer:
         self._chain_events = (ev_act, ev_snap, ev_learn)
         s_roll.wait_stream(main)
         out = None
-        gate = getattr(self, "env_after_target", False) and self.fused2 is not None   # A/B: env behind the target critic
-        ev_tc = [torch.cuda.Event() for _ in range(U)]
-        self._chain_events = self._chain_events + (ev_tc,)
         for k in range(U):
-            def env_part(k=k):
-                with torch.cuda.stream(s_roll):
-                    if gate:
-                        ev_tc[k].record(main)
-                        s_roll.wait_event(ev_tc[k])
-                    env = self.env
-                    env.step(self.actions)
-                    self._push(snap=self.ring_snap2[k % 2])   # + the ring state learn(k+1) samples against
-                    ev_snap[k].record(s_roll)
-                    env.auto_reset(True)
-                    env.advance_device(True)
             with torch.cuda.stream(s_roll):
                 if k > 0:
                     s_roll.wait_event(ev_learn[k - 1])   # the weights learn(k-1) wrote
                 self.act()
                 ev_act[k].record(s_roll)
-            if not gate:
-                env_part()
+                env = self.env
+                env.step(self.actions)
+                self._push(snap=self.ring_snap2[k % 2])   # + the ring state learn(k+1) samples against
+                ev_snap[k].record(s_roll)
+                env.auto_reset(True)
+                env.advance_device(True)
             if k > 0:
                 main.wait_event(ev_snap[k - 1])
-            out = self.learn(state=self.ring_snap2[(k - 1) % 2], guard=self.E * self.R, actor_wait=ev_act[k],
-                             after_target=env_part if gate else None)
+            out = self.learn(state=self.ring_snap2[(k - 1) % 2], guard=self.E * self.R, actor_wait=ev_act[k])
             ev_learn[k].record(main)
         main.wait_stream(s_roll)
         return out
