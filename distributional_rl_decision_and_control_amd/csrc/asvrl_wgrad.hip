@@ -385,34 +385,8 @@ __global__ __launch_bounds__(kSumThreads) void partial_sum_kernel(const float* _
 struct SumSegs {
   AsvPartialSum seg[ASVRL_MAX_SUM_SEGS];
   int slot0[ASVRL_MAX_SUM_SEGS];   // first norm slot of each segment's working blocks
-  int vec4[ASVRL_MAX_SUM_SEGS];    // 1: the segment's outputs four per lane (16-byte loads, span 256)
   int nseg;
 };
-
-// wave_groups_sum for four consecutive outputs (one 16-byte load per group): each output summed in exactly
-// wave_groups_sum's order (bit-identical), a quarter of the load instructions
-__device__ __forceinline__ float4 wave_groups_sum4(const float* __restrict__ p, int groups, int stride, int idx,
-                                                   int wv) {
-  float4 acc[kSumAcc];
-#pragma unroll
-  for (int a = 0; a < kSumAcc; ++a) acc[a] = make_float4(0.f, 0.f, 0.f, 0.f);
-  auto add = [](float4& x, const float4 y) { x.x += y.x; x.y += y.y; x.z += y.z; x.w += y.w; };
-  int k = wv;
-  for (; k + (kSumAcc - 1) * kSumWaves < groups; k += kSumAcc * kSumWaves) {
-#pragma unroll
-    for (int a = 0; a < kSumAcc; ++a)
-      add(acc[a], *reinterpret_cast<const float4*>(p + static_cast<int64_t>(k + a * kSumWaves) * stride + idx));
-  }
-#pragma unroll
-  for (int a = 0; a < kSumAcc; ++a)
-    if (k + a * kSumWaves < groups)
-      add(acc[a], *reinterpret_cast<const float4*>(p + static_cast<int64_t>(k + a * kSumWaves) * stride + idx));
-  float cx[kSumAcc], cy[kSumAcc], cz[kSumAcc], cw[kSumAcc];
-#pragma unroll
-  for (int a = 0; a < kSumAcc; ++a) { cx[a] = acc[a].x; cy[a] = acc[a].y; cz[a] = acc[a].z; cw[a] = acc[a].w; }
-  return make_float4(acc_tree<kSumAcc>(cx, 0), acc_tree<kSumAcc>(cy, 0), acc_tree<kSumAcc>(cz, 0),
-                     acc_tree<kSumAcc>(cw, 0));
-}
 
 // group_sum for the five object copies of a fold output at once: one pass over the groups, each
 // copy accumulated in group_sum's order (bit-identical to five group_sum calls), one tree
@@ -498,30 +472,6 @@ __global__ __launch_bounds__(kSumThreads) void partial_sums_kernel(SumSegs t, do
         if (g.norm) sq += static_cast<double>(*o) * *o;
       }
     }
-  } else if (t.vec4[y]) {   // four outputs per lane: [256 bx, 256 bx + 256)
-    __shared__ float red4[4][kSumWaves][64];
-    const int i0 = bx * 256 + 4 * lane;
-    const bool v = i0 < n;
-    const int boff = g.boff != 0 ? g.boff : g.nw;
-    const int stride = g.stride != 0 ? g.stride : n;
-    const float4 w4 = v ? wave_groups_sum4(g.partial, g.groups, stride, i0 < g.nw ? i0 : boff + (i0 - g.nw), wv)
-                        : make_float4(0.f, 0.f, 0.f, 0.f);
-    red4[0][wv][lane] = w4.x;
-    red4[1][wv][lane] = w4.y;
-    red4[2][wv][lane] = w4.z;
-    red4[3][wv][lane] = w4.w;
-    __syncthreads();
-    if (wv == 0 && v && !(i0 >= g.nw && g.db == nullptr)) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int i = i0 + c;
-        float* o = i < g.nw ? g.dw + i : g.db + (i - g.nw);
-        const float sc = sum_tree(red4[c], lane);
-        const float out = g.accumulate ? *o + sc : sc;
-        *o = out;
-        if (g.norm) sq += static_cast<double>(out) * out;
-      }
-    }
   } else if (bx * kSumSpan < n) {   // block-uniform
     const int base = bx * kSumSpan + lane;
     const int stride = g.stride != 0 ? g.stride : n;
@@ -579,24 +529,13 @@ __global__ __launch_bounds__(kSumThreads) void partial_sums_kernel(SumSegs t, do
   if (lane == 0) sq_blocks[blockIdx.x] = sq;
 }
 
-// a plain segment whose outputs, partial rows and bias offset are all multiples of 4 (16-byte aligned):
-// reduced four outputs per lane
-bool sum_vec4(const AsvPartialSum& g) {
-  const int n = g.nw + g.nb;
-  const int stride = g.stride != 0 ? g.stride : n;
-  const int boff = g.boff != 0 ? g.boff : g.nw;
-  return g.mode == ASVRL_SUM_PLAIN && n > 1 && n % 4 == 0 && g.nw % 4 == 0 && stride % 4 == 0 && boff % 4 == 0 &&
-         reinterpret_cast<uintptr_t>(g.partial) % 16 == 0;
-}
-
 // norm slots: one per working block of each segment, segments in order
 int norm_slots(const AsvPartialSum* segs, int nseg, int* slot0) {
   int n = 0;
   for (int k = 0; k < nseg; ++k) {
     if (slot0 != nullptr) slot0[k] = n;
     const int w = segs[k].nw + segs[k].nb;
-    const int span = sum_vec4(segs[k]) ? 256 : kSumSpan;
-    n += w == 1 ? 1 : (w + span - 1) / span;
+    n += w == 1 ? 1 : (w + kSumSpan - 1) / kSumSpan;
   }
   return n;
 }
@@ -610,7 +549,6 @@ int launch_partial_sums(const AsvPartialSum* segs, int nseg, double* sq_blocks, 
     ASVRL_REQUIRE(g.mode != ASVRL_SUM_FOLD_ENCODERS || (g.nw == kFoldOut && g.nb == 0),
                   "asvrl_partial_sums: the encoder fold writes 688 outputs (nw = 688, nb = 0)");
     t.seg[k] = g;
-    t.vec4[k] = sum_vec4(g) ? 1 : 0;
   }
   t.nseg = nseg;
   const int blocks = norm_slots(segs, nseg, t.slot0);

@@ -317,39 +317,3 @@ def test_arena_batch_matches_separate_launches():
         res.append([w1, b1, w2, b2, w3, b3])
     for a, b in zip(*res):
         assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("groups", [1, 7, 256])
-def test_partial_sums_vec4_matches_scalar_path(groups):
-    """asvrl_partial_sums reduces a segment whose sizes are multiples of 4 with 16-byte loads, four outputs per
-    lane; every output summed in the scalar path's order: bit-identical to the same data reduced through the
-    scalar path (the partials one float off 16-byte alignment)."""
-    import ctypes as C
-    from distributional_rl_decision_and_control_amd import _abi
-    M, K = 128, 256
-    g = torch.Generator(device="cuda").manual_seed(groups)
-    stride = M * K + M
-    buf = torch.randn(groups * stride + 4, generator=g, device="cuda")
-    outs = []
-    for off in (0, 1):   # aligned (vec4) / one float off (scalar)
-        part = buf[4 - off:4 - off + groups * stride] if off else buf[0:groups * stride]
-        if off:
-            part.copy_(buf[0:groups * stride].clone())
-        dw = torch.full((M * K,), float("nan"), device="cuda")
-        db = torch.full((M,), float("nan"), device="cuda")
-        seg = _abi.AsvPartialSum()
-        seg.partial, seg.dw, seg.db = part.data_ptr(), dw.data_ptr(), db.data_ptr()
-        seg.groups, seg.nw, seg.nb, seg.accumulate = groups, M * K, M, 0
-        seg.stride, seg.boff, seg.mode, seg.norm = stride, M * K, _abi.SUM_PLAIN, 1
-        arr = (_abi.AsvPartialSum * 1)(seg)
-        L = _abi.lib()
-        nparts = int(L.asvrl_partial_sums_norm_parts(arr, 1))
-        parts = torch.zeros(nparts, dtype=torch.float64, device="cuda")
-        step = torch.zeros(1, device="cuda")
-        _abi.check(L.asvrl_partial_sums_norm(arr, 1, parts.data_ptr(), step.data_ptr(), None), "partial_sums")
-        torch.cuda.synchronize()
-        ref = part.view(groups, stride).double().sum(0)
-        assert torch.allclose(torch.cat([dw, db]).double(), ref, rtol=1e-5, atol=1e-5)
-        assert abs(float(parts.sum()) - float((torch.cat([dw, db]).double() ** 2).sum())) <= 1e-9 * float(parts.sum())
-        outs.append(torch.cat([dw, db]))
-    assert torch.equal(outs[0], outs[1])
