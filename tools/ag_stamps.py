@@ -4,10 +4,10 @@ python tools/build_variant.py agstamps asvrl_wgrad.hip=-DASVRL_AG_STAMPS), at th
 For each workgroup role (tile split, tile finisher, encoder fold, output layer, loss) prints when its phase
 points were reached, in us after the first workgroup started: median and max over the workgroups.
 Stamps: 0 start, 1 operands staged + MFMAs done (output layer: its sums), 2 slab stored, 3 arrival
-returned (finisher), 4 slabs merged, 5 norm partial published, 6 every finisher arrived, 8 norm folded,
-9 Adam scalars, 10 parameters updated + re-packed, 7 end.
+returned (finisher), 4 slabs merged, 5 gradients and norm partial written. (Rows 6-10 were the in-launch
+optimiser's phases, removed: profiles/r03p1_fused_adam_timeout.txt.)
 
-    ASVRL_LIB=variants/libasvrl_agstamps.so python tools/ag_stamps.py [adam]
+    ASVRL_LIB=variants/libasvrl_agstamps.so python tools/ag_stamps.py
 """
 import ctypes as C
 import os
@@ -62,7 +62,7 @@ def main():
         if not sel.any():
             continue
         row = []
-        for k in range(11):
+        for k in range(6):
             v = us[sel, k]
             v = v[(v >= 0) & (v < 1e4)]
             row.append(f"{k}:{np.median(v):6.1f}/{v.max():6.1f}" if v.size else f"{k}:   -  ")
