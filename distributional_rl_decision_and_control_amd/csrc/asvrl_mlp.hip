@@ -338,11 +338,52 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_kernel(MlpArgs a) {
 // (asvrl_lds.h), with the weight fragments read from L2. A B-row batch then runs 4 B / 32 waves instead
 // of B / 32 (AC-IQN step 0.370 -> 0.350 ms with the backward below); the rollout's 20,480-row act keeps
 // the one-wave-per-tile form above, where its LDS-staged weights pay (0.356 ms with the split act).
+// Phase timing (tools/prologue_stamps.py; a variant build with -DASVRL_PRO_STAMPS, never the shipped
+// library): thread 0 of every workgroup records s_memrealtime (100 MHz) at its phase points, each after
+// draining its outstanding memory operations so the stamp marks when the phase's data arrived.
+#ifdef ASVRL_PRO_STAMPS
+constexpr int kProStamps = 12;
+__device__ uint64_t g_pro_stamps[2048 * kProStamps];
+#define PRO_STAMP(k)                                                                              \
+  do {                                                                                            \
+    __builtin_amdgcn_s_waitcnt(0);                                                                \
+    if (threadIdx.x == 0) g_pro_stamps[blockIdx.x * kProStamps + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+extern "C" int asvrl_debug_pro_stamps(uint64_t* out, int64_t n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pro_stamps), n * sizeof(uint64_t)) == hipSuccess ? 0 : 1;
+}
+#else
+#define PRO_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
+
+// The split tile's biases and output weights in LDS (b_enc | b1 | b2 | wout[2][128] | bout), staged at the
+// workgroup's start with the weight fragments: read after each layer's barrier from global memory, their
+// L2/MALL round trips were most of the tile's time (profiles/r03pro_prologue_stamps.txt).
+constexpr int kSbEnc = 0, kSbB1 = kEnc, kSbB2 = kSbB1 + kHid, kSbWout = kSbB2 + kHid, kSbBout = kSbWout + 2 * kHid,
+              kSplitBias = kSbBout + 2;
 struct ActorSplitLds {
   elem_t x0[32 * kEnc];      // h0; the backward: dz2 image
   elem_t h1[32 * kHid];      // h1; the backward: dz1 image
   float part[kMlpWaves][32][2];
+  float bias[kSplitBias];
 };
+static_assert(kMlpWaves * 64 == kEnc && kSplitBias <= 4 * kEnc, "split_bias_fetch: four values per thread");
+
+// thread t's share of the bias table: entries t + 256 k (issued first, stored by split_bias_store)
+__device__ __forceinline__ void split_bias_fetch(const AsvMlpWeights& wt, int t, float (&v)[4]) {
+  v[0] = wt.b_enc[t];
+  v[1] = t < kHid ? wt.b1[t] : wt.b2[t - kHid];
+  v[2] = wt.wout[t];
+  v[3] = t < 2 ? wt.bout[t] : 0.f;
+}
+
+__device__ __forceinline__ void split_bias_store(ActorSplitLds& L, int t, const float (&v)[4]) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) L.bias[t + kEnc * k] = v[k];
+  if (t < 2) L.bias[kSbBout + t] = v[3];
+}
 
 // A wave's weight fragments of the split tile (encoder blocks 2w, 2w + 1; W1 and W2 block w), fetched
 // ahead by the fused prologue so that their L2 latency overlaps its replay draw.
@@ -367,11 +408,35 @@ __device__ __forceinline__ void split_prefetch(const AsvMlpWeights& wt, int w, i
 // One 32-row tile of the split Actor (4 waves): rows tile * 32 + r of the outputs; the observation of
 // row r read from x + (xrow0 + r) * ldx (the global rows, or rows staged in LDS by the fused prologue).
 // PRE: the wave's fragments already in registers (`pre`; the same MFMAs in the same order).
+// the 16 values of a bias-table block that accumulator registers g = 4k + i of lane half h meet
+// (feature mb * 32 + 8k + 4h + i, asvrl_mfma.h feat): four 16-byte LDS reads, issued together
+__device__ __forceinline__ void bias16(const float* tab, int mb, int h, float (&b)[16]) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const f4v t = *reinterpret_cast<const f4v*>(tab + mb * 32 + 8 * k + 4 * h);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b[4 * k + i] = t[i];
+  }
+}
+
+// object ob's mask factor (ob wave-uniform; -1, the self encoder, and kObjN give 1): selects on a scalar
+// condition, no lane-divergent branches
+static_assert(kSelfF >= 32 && kObjF >= 32, "a 32-feature block spans at most two encoders");
+__device__ __forceinline__ float obj_sel(int ob, const float (&mf)[kObjN]) {
+  float f = 1.f;
+#pragma unroll
+  for (int o = 0; o < kObjN; ++o) f = ob == o ? mf[o] : f;
+  return f;
+}
+
 template <int MODE, bool PRE = false>
 __device__ __forceinline__ void actor_split_tile(const MlpArgs& a, ActorSplitLds& L, int tile, const float* x,
                                                  int64_t ldx, int xrow0, const SplitPre& pre = SplitPre{}) {
   const AsvMlpIO& io = a.io;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
+  // w wave-uniform (an SGPR): the encoder epilogue's feature / object indices below are scalar work
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), h = lane >> 5,
+            r = lane & 31;
   const int row = tile * 32 + r;
   const bool valid = row < io.n;
   const int rr = valid ? row : io.n - 1;
@@ -380,6 +445,7 @@ __device__ __forceinline__ void actor_split_tile(const MlpArgs& a, ActorSplitLds
     frag8 bx[2];
     float mk[kObjN];
     load_obs(x, ldx, xrow0 + (rr - tile * 32), h, bx, mk);
+    PRO_STAMP(10);
     if (MODE == MLP_TRAIN && w == 0 && valid) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
@@ -387,9 +453,20 @@ __device__ __forceinline__ void actor_split_tile(const MlpArgs& a, ActorSplitLds
     }
     const frag8* ENC = reinterpret_cast<const frag8*>(a.w.enc_frag);
     const RowA<kEnc> RA(r, h);
+    float mf[kObjN];   // masked_fill(mask < 0.5, 0) as a factor per object
+#pragma unroll
+    for (int o = 0; o < kObjN; ++o) mf[o] = mk[o] < 0.5f ? 0.f : 1.f;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int mb = 2 * w + q;
+      float bb[16];
+      bias16(L.bias + kSbEnc, mb, h, bb);
+      // a 32-feature block spans at most two encoders: A (from its first feature) up to feature bnd, then
+      // A + 1; the lane's feature 8k + i + 4h of the block is in A iff 8k + i < lim. One select per element.
+      const int m_lo = mb * 32;
+      const int obA = m_lo < kSelfF ? -1 : obj_of(m_lo);
+      const int lim = kSelfF + kObjF * (obA + 1) - m_lo - 4 * h;
+      const float fA = obj_sel(obA, mf), fB = obj_sel(obA + 1, mf);
       f32x16 acc = f32x16{};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
@@ -401,24 +478,26 @@ __device__ __forceinline__ void actor_split_tile(const MlpArgs& a, ActorSplitLds
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int g = 8 * s + j;
-          const int m = feat(mb, g, h);
-          const int ob = m < kSelfF ? -1 : obj_of(m);   // select chain: no dynamic register index
-          const float mo = ob == 0 ? mk[0] : ob == 1 ? mk[1] : ob == 2 ? mk[2] : ob == 3 ? mk[3] : mk[4];
-          v[j] = relu(acc[g] + a.w.b_enc[m]) * (ob < 0 ? 1.f : (mo < 0.5f ? 0.f : 1.f));
+          v[j] = relu(acc[g] + bb[g]) * ((g & 3) + 8 * (g >> 2) < lim ? fA : fB);
           o[j] = (elem_t)v[j];
         }
         rows(L.x0, RA, 0, 2 * mb + s, o);
         if constexpr (MODE == MLP_TRAIN)
           store16(valid ? bp(io.h0) + static_cast<int64_t>(row) * kEnc + mb * 32 + 16 * s : nullptr, v, h);
       }
+      if (q == 0) PRO_STAMP(11);
     }
   }
+  PRO_STAMP(5);
   __syncthreads();
+  PRO_STAMP(6);
   // ---------------- hidden_layer (wave w: block w) -> h1
   {
     const frag8* W1 = reinterpret_cast<const frag8*>(a.w.w1_frag);
     const RowA<kEnc> RX(r, h);
     const RowA<kHid> RH(r, h);
+    float bb[16];
+    bias16(L.bias + kSbB1, w, h, bb);
     f32x16 acc = f32x16{};
     if constexpr (PRE) {
 #pragma unroll
@@ -432,7 +511,7 @@ __device__ __forceinline__ void actor_split_tile(const MlpArgs& a, ActorSplitLds
       frag8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        v[j] = relu(acc[8 * s + j] + a.w.b1[feat(w, 8 * s + j, h)]);
+        v[j] = relu(acc[8 * s + j] + bb[8 * s + j]);
         o[j] = (elem_t)v[j];
       }
       rows(L.h1, RH, 0, 2 * w + s, o);
@@ -440,11 +519,16 @@ __device__ __forceinline__ void actor_split_tile(const MlpArgs& a, ActorSplitLds
         store16(valid ? bp(io.h1) + static_cast<int64_t>(row) * kHid + w * 32 + 16 * s : nullptr, v, h);
     }
   }
+  PRO_STAMP(7);
   __syncthreads();
   // ---------------- hidden_layer_2 (block w) -> h2, the output layer's partial sums over its features
   {
     const frag8* W2 = reinterpret_cast<const frag8*>(a.w.w2_frag);
     const RowA<kHid> RH(r, h);
+    float bb[16], wo0[16], wo1[16];
+    bias16(L.bias + kSbB2, w, h, bb);
+    bias16(L.bias + kSbWout, w, h, wo0);
+    bias16(L.bias + kSbWout + kHid, w, h, wo1);
     f32x16 acc = f32x16{};
     if constexpr (PRE) {
 #pragma unroll
@@ -458,10 +542,9 @@ __device__ __forceinline__ void actor_split_tile(const MlpArgs& a, ActorSplitLds
       float v[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int m = feat(w, 8 * s + j, h);
-        v[j] = relu(acc[8 * s + j] + a.w.b2[m]);
-        p0 += a.w.wout[m] * v[j];
-        p1 += a.w.wout[kHid + m] * v[j];
+        v[j] = relu(acc[8 * s + j] + bb[8 * s + j]);
+        p0 += wo0[8 * s + j] * v[j];
+        p1 += wo1[8 * s + j] * v[j];
       }
       if constexpr (MODE == MLP_TRAIN)
         store16(valid ? bp(io.h2) + static_cast<int64_t>(row) * kHid + w * 32 + 16 * s : nullptr, v, h);
@@ -473,10 +556,12 @@ __device__ __forceinline__ void actor_split_tile(const MlpArgs& a, ActorSplitLds
       L.part[w][r][1] = p1;
     }
   }
+  PRO_STAMP(8);
   __syncthreads();
+  PRO_STAMP(9);
   if (threadIdx.x >= 32 || !valid) return;
-  const float z0 = (((L.part[0][r][0] + L.part[1][r][0]) + L.part[2][r][0]) + L.part[3][r][0]) + a.w.bout[0];
-  const float z1 = (((L.part[0][r][1] + L.part[1][r][1]) + L.part[2][r][1]) + L.part[3][r][1]) + a.w.bout[1];
+  const float z0 = (((L.part[0][r][0] + L.part[1][r][0]) + L.part[2][r][0]) + L.part[3][r][0]) + L.bias[kSbBout];
+  const float z1 = (((L.part[0][r][1] + L.part[1][r][1]) + L.part[2][r][1]) + L.part[3][r][1]) + L.bias[kSbBout + 1];
   const float a0 = a.w.out_scale * atanf(z0);   // atan_scale * torch.atan(actions)
   const float a1 = a.w.out_scale * atanf(z1);
   float* o = io.a_out + static_cast<int64_t>(row) * io.ld_aout;
@@ -493,6 +578,10 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_split_kernel(MlpArgs a) 
   __shared__ __attribute__((aligned(16))) ActorSplitLds L;
   SplitPre pre;
   split_prefetch(a.w, threadIdx.x >> 6, threadIdx.x & 63, pre);
+  float bv[4];
+  split_bias_fetch(a.w, threadIdx.x, bv);
+  split_bias_store(L, threadIdx.x, bv);
+  __syncthreads();
   actor_split_tile<MODE, true>(a, L, blockIdx.x, a.io.x, a.io.ldx, blockIdx.x * 32, pre);
 }
 
@@ -516,6 +605,7 @@ struct PrologueArgs {
 };
 
 __global__ __launch_bounds__(kMlpWaves * 64) void learn_prologue_kernel(PrologueArgs p, MlpArgs train, MlpArgs tgt) {
+  PRO_STAMP(0);
   __shared__ __attribute__((aligned(16))) ActorSplitLds L;
   __shared__ __attribute__((aligned(16))) float xs[32 * ASVRL_OBS_DIM];   // the tile's 32 observation rows
   const int T = p.B / 32;
@@ -525,6 +615,8 @@ __global__ __launch_bounds__(kMlpWaves * 64) void learn_prologue_kernel(Prologue
   // the wave's weight fragments first: their L2 latency runs under the draw below
   SplitPre pre;
   split_prefetch(second ? tgt.w : train.w, w, lane, pre);
+  float bv[4];
+  split_bias_fetch(second ? tgt.w : train.w, threadIdx.x, bv);
   const int64_t head = p.ring_state[0], size = p.ring_state[1];
   const uint64_t ctr = p.counter + (p.counter_dev != nullptr ? *p.counter_dev : 0ull);
   // wave w gathers samples 8w .. 8w + 7 of the tile: the whole row to `out` (first half), the observation
@@ -532,6 +624,7 @@ __global__ __launch_bounds__(kMlpWaves * 64) void learn_prologue_kernel(Prologue
   // (one float4 per lane) is loaded before any store, so the eight HBM reads are in flight together.
   const int64_t my_slot = replay_draw_slot(head, size, p.cap, p.guard, tile * 32 + 8 * w + (lane & 7), p.seed, ctr);
   const int slot_lo = static_cast<int>(my_slot & 0xFFFFFFFFll), slot_hi = static_cast<int>(my_slot >> 32);
+  PRO_STAMP(1);
   constexpr int kRowV = ASVRL_TR_DIM / 4, kObsV = ASVRL_OBS_DIM / 4;
   const int per = second ? kObsV : kRowV;   // float4 pieces per sample
   typedef float f4v __attribute__((ext_vector_type(4)));
@@ -547,6 +640,7 @@ __global__ __launch_bounds__(kMlpWaves * 64) void learn_prologue_kernel(Prologue
                          static_cast<uint32_t>(__shfl(slot_lo, js));
     v[u] = reinterpret_cast<const f4v*>(p.ring + slot * ASVRL_TR_DIM)[(second ? kObsV : 0) + (jj[u] < 8 ? cc[u] : 0)];
   }
+  PRO_STAMP(2);
   if (!second && p.taus != nullptr) {
     // the eight samples' taus with every lane busy: item (sample j, Philox block k0 / 4) per lane, the
     // draws of replay_draw_taus (same counters, bit-identical)
@@ -575,9 +669,12 @@ __global__ __launch_bounds__(kMlpWaves * 64) void learn_prologue_kernel(Prologue
       if (cc[u] < kObsV) reinterpret_cast<f4v*>(xs + lr * ASVRL_OBS_DIM)[cc[u]] = v[u];
     }
   }
+  split_bias_store(L, threadIdx.x, bv);
   __syncthreads();
+  PRO_STAMP(3);
   if (!second) actor_split_tile<MLP_TRAIN, true>(train, L, tile, xs, ASVRL_OBS_DIM, 0, pre);
   else actor_split_tile<MLP_FWD, true>(tgt, L, tile, xs, ASVRL_OBS_DIM, 0, pre);
+  PRO_STAMP(4);
 }
 
 // The backward in the same split: dz2 (block w) from dA, dz1 = W2^T dz2 (block w), dz0 = W1^T dz1

@@ -60,6 +60,16 @@ static_assert(2 * 32 * kAP * sizeof(float) >= 32 * kAP * (sizeof(elem_t) + sizeo
 // object index of encoder feature m (>= 56)
 __device__ __forceinline__ int obj_of(int m) { return (m - kSelfF) / kObjF; }
 
+// object ob's mask factor (ob wave-uniform; -1, the self encoder, and kObjN give 1): selects on a scalar
+// condition, no lane-divergent branches
+static_assert(kSelfF >= 32 && kObjF >= 32, "a 32-feature block spans at most two encoders");
+__device__ __forceinline__ float obj_sel(int ob, const float (&mf)[kObjN]) {
+  float f = 1.f;
+#pragma unroll
+  for (int o = 0; o < kObjN; ++o) f = ob == o ? mf[o] : f;
+  return f;
+}
+
 // natural atom index of register g of block b in lane half h
 __device__ __forceinline__ int atom_of(int b, int g, int h) { return b * 32 + (g & 3) + 8 * (g >> 2) + 4 * h; }
 
@@ -83,28 +93,34 @@ __device__ __forceinline__ void phase_encode(const AsvRainbowImg& W, const float
       bx[ks][4 + j] = (elem_t)v[j];
     }
   }
-  float mk[kObjN];
+  float mf[kObjN];   // masked_fill(mask < 0.5, 0) as a factor per object
 #pragma unroll
-  for (int o = 0; o < kObjN; ++o) mk[o] = xr[32 + o];
+  for (int o = 0; o < kObjN; ++o) mf[o] = xr[32 + o] < 0.5f ? 0.f : 1.f;
   const frag8* ENC = reinterpret_cast<const frag8*>(W.enc);
   const RowA<kEnc> RA(r, h);
   fmask = 0;
+  w = __builtin_amdgcn_readfirstlane(w);   // wave-uniform: the block / object indices below are scalar work
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int mb = 2 * w + q;
     f32x16 acc = f32x16{};
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) acc = mfma(ENC[(mb * 2 + ks) * 64 + lane], bx[ks], acc);
+    // the block spans at most two encoders: A (from its first feature) up to the next boundary, then
+    // A + 1; the lane's feature 8k + i + 4h of the block is in A iff 8k + i < lim (one select per element)
+    const int m_lo = mb * 32;
+    const int obA = m_lo < kSelfF ? -1 : obj_of(m_lo);
+    const int lim = kSelfF + kObjF * (obA + 1) - m_lo - 4 * h;
+    const float fA = obj_sel(obA, mf), fB = obj_sel(obA + 1, mf);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       frag8 o;
       float v[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const int m = feat(mb, 8 * s + i, h);
-        const int ob = m < kSelfF ? -1 : obj_of(m);   // select chain: no dynamic register index
-        const float mo = ob == 0 ? mk[0] : ob == 1 ? mk[1] : ob == 2 ? mk[2] : ob == 3 ? mk[3] : mk[4];
-        const float keep = ob < 0 ? 1.f : (mo < 0.5f ? 0.f : 1.f);   // masked_fill(mask < 0.5, 0)
+        const int g = 8 * s + i;
+        const int m = feat(mb, g, h);
+        const float keep = (g & 3) + 8 * (g >> 2) < lim ? fA : fB;
         v[i] = relu(acc[8 * s + i] + W.b_enc[m]) * keep;
         o[i] = (elem_t)v[i];
         if (SAVE && v[i] > 0.f) fmask |= 1u << (16 * q + 8 * s + i);
