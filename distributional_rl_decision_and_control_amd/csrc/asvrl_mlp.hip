@@ -359,8 +359,9 @@ extern "C" int asvrl_debug_pro_stamps(uint64_t* out, int64_t n) {
 #endif
 
 // The split tile's biases and output weights in LDS (b_enc | b1 | b2 | wout[2][128] | bout), staged at the
-// workgroup's start with the weight fragments: read after each layer's barrier from global memory, their
-// L2/MALL round trips were most of the tile's time (profiles/r03pro_prologue_stamps.txt).
+// workgroup's start with the weight fragments instead of global reads after each layer's barrier (a small
+// gain; the tile's time was instruction issue at one wave per SIMD: the encoder mask's per-element select
+// chain, profiles/r03pro_prologue_stamps_{before,after}.txt).
 constexpr int kSbEnc = 0, kSbB1 = kEnc, kSbB2 = kSbB1 + kHid, kSbWout = kSbB2 + kHid, kSbBout = kSbWout + 2 * kHid,
               kSplitBias = kSbBout + 2;
 struct ActorSplitLds {
