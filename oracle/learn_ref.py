@@ -161,6 +161,91 @@ class IQNRef:
         return float(loss.detach()), gn
 
 
+# ---------------------------------------------------------------------------- bf16 training build
+def bf16_round(x):
+    """Round-to-nearest-even to bf16 and back (v_cvt_pk_bf16_f32, the training build's operand cast)."""
+    return x.to(torch.bfloat16).to(x.dtype)
+
+
+def critic_step_bf16(w, s, a, q_next, r, d, taus, gamma=0.99, kappa=1.0, rnd=bf16_round):
+    """agent.py:395-414's critic gradients (AC_IQN_model.py:284-308,410-480 forward, quantile-Huber
+    agent.py:701-707, backward) restated with the rounding points of the bf16 training build's ONE fused
+    launch, critic_fused_kernel<N, false> (asvrl_critic_fused.hip), at which every MFMA operand is bf16 and
+    every accumulation f32 -- here f64, so only the rounding points are emulated:
+
+      weights   Wc, W1, W2 as bf16 images (biases, wo, the encoders f32; bias = the accumulator's start)
+      forward   F = bf16(relu(enc(s)))  (masked objects 0), G = relu(enc_a(a)) f32, cos = bf16(cos(tau pi k)),
+                c = relu(bc + Wc cos), x = bf16(F c), h1 = relu(b1 + W1 x), h1g = bf16(h1 G),
+                h2 = relu(b2 + W2 h1g), q = wo . h2 + bo (h2 f32)
+      loss      the quantile-Huber terms against r + gamma q_next (1 - d), dq = dL/dq
+      backward  dz2 = bf16(dq wo 1[h2 > 0]); d wo = sum dq bf16(h2); dh1g = W2^T dz2;
+                dz1 = bf16(dh1g G 1[h1 > 0]); dG = sum_tau dh1g bf16(h1); dx = W1^T dz1;
+                dF = sum_tau dx c; dzc = bf16(dx F 1[c > 0]); dW = dZ^T X of the bf16 images
+      encoders  dzF = dF 1[F > 0], dzG = dG 1[G > 0] (f32) into the encoders' weight / bias sums
+
+    w: critic state_dict (f32 tensors, reference key names); s = (self (B,7), objects (B,5,5), mask (B,5));
+    a (B,2); q_next (B,N') the target quantiles the launch read; r, d (B,); taus (B,N). rnd=identity
+    reduces this to the plain f64 critic step (pinned to torch autograd on the reference's own batch by
+    tests/test_bf16_oracle_cpu.py). Returns (loss, {parameter name: gradient}) in f64."""
+    f64 = torch.float64
+    W = {k: torch.as_tensor(v).to(f64) for k, v in w.items()}
+    s_self, s_obj, s_mask = (torch.as_tensor(x).to(f64) for x in s)
+    a, q_next = torch.as_tensor(a).to(f64), torch.as_tensor(q_next).to(f64)
+    r, d, taus = (torch.as_tensor(x).to(f64) for x in (r, d, taus))
+    B, N = taus.shape
+    Np = q_next.shape[1]
+    wc, w1, w2 = (rnd(W[p + ".weight"]) for p in ("cos_embedding", "hidden_layer", "hidden_layer_2"))
+    bc, b1, b2 = (W[p + ".bias"] for p in ("cos_embedding", "hidden_layer", "hidden_layer_2"))
+    wo, bo = W["output_layer.weight"][0], W["output_layer.bias"][0]
+    # encoders (f32 dot products in the launch)
+    f_self = torch.relu(s_self @ W["self_encoder.0.weight"].T + W["self_encoder.0.bias"])
+    f_obj = torch.relu(s_obj @ W["object_encoder.0.weight"].T + W["object_encoder.0.bias"])   # (B,5,40)
+    f_obj = f_obj * (s_mask >= 0.5).to(f64).unsqueeze(-1)
+    Fb = rnd(torch.cat((f_self, f_obj.reshape(B, 200)), 1))                                    # (B,256)
+    G = torch.relu(a @ W["action_encoder.0.weight"].T + W["action_encoder.0.bias"])              # (B,128)
+    pis = torch.tensor([np.pi * i for i in range(64)], dtype=torch.float32).to(f64)   # AC_IQN_model.py:389
+    cos = rnd(torch.cos(taus.reshape(B * N, 1) * pis))                                             # (R,64)
+    Fr = Fb.repeat_interleave(N, 0)
+    Gr = G.repeat_interleave(N, 0)
+    c = torch.relu(cos @ wc.T + bc)
+    x = rnd(Fr * c)
+    h1 = torch.relu(x @ w1.T + b1)
+    h1g = rnd(h1 * Gr)
+    h2 = torch.relu(h1g @ w2.T + b2)
+    q = (h2 @ wo + bo).view(B, N)
+    # quantile-Huber (agent.py:399-412): L = mean_b mean_j sum_i |tau_i - 1[delta < 0]| H(delta) / kappa
+    qt = r.view(B, 1) + gamma * q_next * (1.0 - d.view(B, 1))
+    delta = qt.view(B, 1, Np) - q.view(B, N, 1)
+    quad = delta.abs() <= kappa
+    hub = torch.where(quad, 0.5 * delta * delta, kappa * (delta.abs() - 0.5 * kappa))
+    wgt = torch.where(delta < 0, 1.0 - taus.view(B, N, 1), taus.view(B, N, 1))
+    loss = (wgt * hub).sum() / (kappa * B * Np)
+    dH = torch.where(quad, delta, kappa * torch.sign(delta))
+    dq = (-(wgt * dH).sum(2) / (kappa * B * Np)).reshape(B * N)
+    # backward
+    h2b = rnd(h2)
+    dz2 = rnd(torch.where(h2b > 0, dq.view(-1, 1) * wo.view(1, -1), torch.zeros_like(h2)))
+    g = {"output_layer.weight": (dq @ h2b).view(1, -1), "output_layer.bias": dq.sum().view(1)}
+    g["hidden_layer_2.weight"], g["hidden_layer_2.bias"] = dz2.T @ h1g, dz2.sum(0)
+    dh1g = dz2 @ w2
+    h1b = rnd(h1)
+    dz1 = rnd(torch.where(h1b > 0, dh1g * Gr, torch.zeros_like(h1)))
+    dG = (dh1g * h1b).view(B, N, -1).sum(1)
+    g["hidden_layer.weight"], g["hidden_layer.bias"] = dz1.T @ x, dz1.sum(0)
+    dx = dz1 @ w1
+    dF = (dx * c).view(B, N, -1).sum(1)
+    dzc = rnd(torch.where(c > 0, dx * Fr, torch.zeros_like(c)))
+    g["cos_embedding.weight"], g["cos_embedding.bias"] = dzc.T @ cos, dzc.sum(0)
+    dzF = torch.where(Fb > 0, dF, torch.zeros_like(dF))
+    dzG = torch.where(G > 0, dG, torch.zeros_like(dG))
+    g["self_encoder.0.weight"], g["self_encoder.0.bias"] = dzF[:, :56].T @ s_self, dzF[:, :56].sum(0)
+    dzo = dzF[:, 56:].reshape(B, 5, 40)
+    g["object_encoder.0.weight"] = torch.einsum("bof,boi->fi", dzo, s_obj)
+    g["object_encoder.0.bias"] = dzo.sum((0, 1))
+    g["action_encoder.0.weight"], g["action_encoder.0.bias"] = dzG.T @ a, dzG.sum(0)
+    return float(loss), g
+
+
 # ---------------------------------------------------------------------------- Rainbow / C51
 def _noisy(w, p, x, training=True):
     if training:

@@ -1,0 +1,96 @@
+"""GPU: the EXACT launch the bench times -- asvrl_critic_train_fused in the bf16 training build
+(libasvrl.so), N = 32 with stage-ahead, the encoders' gradients formed in the launch (ENC_IN_KERNEL) --
+against the bf16-build restatement of the critic step (oracle/learn_ref.critic_step_bf16, pinned on CPU by
+tests/test_bf16_oracle_cpu.py), which rounds to bf16 exactly where the kernel does and accumulates in f64.
+
+Cases: the reference's own N = 32 batch (tests/golden/learn_ac_iqn.npz, B = 64, its captured taus, the
+seeded initial weights) and a B = 4096 random batch (the bench shape: 2048 rounds over 256 workgroups,
+the partials reduced by asvrl_partial_sums). The restatement reads the same target quantiles q_next the
+launch read (the target critic's kernel output), so the comparison isolates the fused launch.
+
+Bars: loss within 1e-4 rel.; every critic gradient tensor within 1e-4 of its scale
+(max |g|); the gradient norm within 1e-4 rel. Round-3's bf16 bars were 2e-2 / 5e-2 against the f32
+reference; this pins the benched arithmetic itself (its indexing, stage-ahead buffers and reductions).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import env_oracle as eo
+from oracle import learn_ref as lr
+
+pytestmark = pytest.mark.gpu
+
+BAR = 1e-4
+
+
+def _run(rows, taus, N, weights=None):
+    """The benched critic launch on rows [B][88] with taus (2, B, N); returns (grads, loss, q_next, critic sd)."""
+    from distributional_rl_decision_and_control_amd.agent import Agent
+    from distributional_rl_decision_and_control_amd.fused_critic import critic_train_fused
+    from distributional_rl_decision_and_control_amd.fused_update import FusedACIQNState, target_q
+    from distributional_rl_decision_and_control_amd.learner import FusedAdam
+    B = rows.shape[0]
+    ag = Agent(seed=100, agent_type="AC-IQN")
+    loc, tgt = ag.policy_local, ag.policy_target
+    if weights is not None:
+        with torch.no_grad():
+            for pol in (loc, tgt):
+                for net in ("actor", "critic"):
+                    for k, v in getattr(pol, net).state_dict().items():
+                        v.copy_(torch.tensor(weights[net][k]))
+    FusedAdam(loc.actor.parameters(), lr=1e-4, operands="bf16")
+    co = FusedAdam(loc.critic.parameters(), lr=1e-4, operands="bf16")
+    st = FusedACIQNState(loc, tgt, B, N, operands="bf16")
+    critic, arena = loc.critic, st.arena
+    co.grads.zero_()
+    target_q(st, rows, taus[0], st.q_next, st.na)
+    critic_train_fused(st.local_trunk, critic, taus[1], N, st.q_next.view(B, N), rows[:, 82], rows[:, 83], 0.99,
+                       rows[:, 0:40], rows[:, 80:82], arena, tile_loss=st.tile_loss[0], encoders=True)
+    arena.scalar(st.tile_loss[0], st.losses[0:1])
+    arena.flush()
+    torch.cuda.synchronize()
+    grads = {n: p.grad.detach().cpu().double() for n, p in critic.named_parameters()}
+    sd = {k: v.detach().cpu() for k, v in critic.state_dict().items()}
+    return grads, float(st.losses[0].item()), st.q_next.view(B, N).cpu().double(), sd
+
+
+def _check(rows, taus, N, weights=None):
+    g, loss, qn, sd = _run(rows, taus, N, weights)
+    x = rows.cpu().double()
+    B = x.shape[0]
+    s = (x[:, 0:7], x[:, 7:32].reshape(B, 5, 5), x[:, 32:37])
+    ref_loss, ref = lr.critic_step_bf16(sd, s, x[:, 80:82], qn, x[:, 82], x[:, 83], taus[1].cpu().double())
+    worst = 0.0
+    for n in ref:
+        scale = float(ref[n].abs().max()) + 1e-30
+        err = float((g[n] - ref[n]).abs().max()) / scale
+        worst = max(worst, err)
+        print(f"{n:28s} err/scale {err:.2e}  scale {scale:.3e}")
+    gn = float(torch.sqrt(sum((v * v).sum() for v in g.values())))
+    rn = float(torch.sqrt(sum((v * v).sum() for v in ref.values())))
+    print(f"loss kernel {loss:.7f} restatement {ref_loss:.7f}; norm {gn:.6f} vs {rn:.6f}; worst {worst:.2e}")
+    np.testing.assert_allclose(loss, ref_loss, rtol=BAR)
+    np.testing.assert_allclose(gn, rn, rtol=BAR)
+    for n in ref:
+        scale = float(ref[n].abs().max()) + 1e-30
+        assert float((g[n] - ref[n]).abs().max()) / scale < BAR, n
+
+
+def test_benched_critic_launch_on_the_reference_batch():
+    from tests.test_learner_golden_gpu import _rows
+    z = np.load(eo.GOLDEN + "/learn_ac_iqn.npz")
+    rows = _rows(z, "n32/")
+    taus = torch.from_numpy(z["n32/taus"][..., 0]).cuda().contiguous()
+    weights = {net: {k[len(f"init/{net}/"):]: z[k] for k in z.keys() if k.startswith(f"init/{net}/")}
+               for net in ("actor", "critic")}
+    _check(rows, taus[:2], 32, weights)
+
+
+def test_benched_critic_launch_at_the_bench_shape():
+    from tests.test_critic_fused_gpu import _batch
+    B, N = 4096, 32
+    rows, _ = _batch(B, 21)
+    g = torch.Generator(device="cuda").manual_seed(22)
+    taus = torch.rand(2, B, N, generator=g, device="cuda")
+    _check(rows, taus, N)
