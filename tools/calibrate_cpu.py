@@ -3,7 +3,7 @@
 oracle's C port of it, both single-threaded on the same workload, in the build container.
 
 Runs ONLY here, where the read-only reference is mounted at /root/reference (it imports the reference's
-Python code). Writes profiles/r02_cpu_calibration.json, which bench.py's cpu_baseline leg reads to
+Python code). Writes profiles/r04_cpu_calibration.json (--out), which bench.py's cpu_baseline leg reads to
 state what its C-port number means in reference-Python terms. Nothing on the GPU box reads the
 reference.
 
@@ -68,21 +68,33 @@ def port_rate(seconds):
     return n / el, n, el
 
 
+def numpy_rate(seconds):
+    """oracle/env_numpy.py (the per-robot NumPy restatement bench.py times on the GPU box), same loop."""
+    sys.path.insert(0, ROOT)
+    from oracle import env_numpy as en
+    n, el = en.rollout(seconds, seed=0)
+    return n / el, n, el
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--out", default="r04_cpu_calibration.json")
     a = ap.parse_args()
     ref, ref_n, resets, ref_s = reference_rate(a.seconds)
     port, port_n, port_s = port_rate(a.seconds)
+    npr, np_n, np_s = numpy_rate(a.seconds)
     out = {"workload": "MarineNavEnv3.step, 5 robots, 4 buoys, 55 m map, uniform actions, trainer deactivation, "
                        "reset on all-deactivated / 1000 steps",
            "reference_python_env_steps_per_s_1thread": ref, "reference_steps": ref_n, "reference_resets": resets,
            "reference_seconds": ref_s,
            "c_port_env_steps_per_s_1thread": port, "c_port_steps": port_n, "c_port_seconds": port_s,
            "c_port_over_reference": port / ref,
+           "numpy_restatement_env_steps_per_s_1thread": npr, "numpy_restatement_steps": np_n,
+           "numpy_restatement_seconds": np_s, "numpy_restatement_over_reference": npr / ref,
            "host": f"build container, {os.cpu_count()} CPUs, 1 thread each",
            "python": sys.version.split()[0], "numpy": np.__version__}
-    path = os.path.join(ROOT, "profiles", "r02_cpu_calibration.json")
+    path = os.path.join(ROOT, "profiles", a.out)
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))
