@@ -167,7 +167,7 @@ def bf16_round(x):
     return x.to(torch.bfloat16).to(x.dtype)
 
 
-def critic_step_bf16(w, s, a, q_next, r, d, taus, gamma=0.99, kappa=1.0, rnd=bf16_round):
+def critic_step_bf16(w, s, a, q_next, r, d, taus, gamma=0.99, kappa=1.0, rnd=bf16_round, dtype=torch.float64):
     """agent.py:395-414's critic gradients (AC_IQN_model.py:284-308,410-480 forward, quantile-Huber
     agent.py:701-707, backward) restated with the rounding points of the bf16 training build's ONE fused
     launch, critic_fused_kernel<N, false> (asvrl_critic_fused.hip), at which every MFMA operand is bf16 and
@@ -186,8 +186,11 @@ def critic_step_bf16(w, s, a, q_next, r, d, taus, gamma=0.99, kappa=1.0, rnd=bf1
     w: critic state_dict (f32 tensors, reference key names); s = (self (B,7), objects (B,5,5), mask (B,5));
     a (B,2); q_next (B,N') the target quantiles the launch read; r, d (B,); taus (B,N). rnd=identity
     reduces this to the plain f64 critic step (pinned to torch autograd on the reference's own batch by
-    tests/test_bf16_oracle_cpu.py). Returns (loss, {parameter name: gradient}) in f64."""
-    f64 = torch.float64
+    tests/test_bf16_oracle_cpu.py). dtype=torch.float32 evaluates the same rounding points with f32
+    arithmetic everywhere else (CPU summation orders): the spread between the two evaluations is the
+    noise floor any f32 implementation of these rounding points shows (tests/test_critic_bf16_oracle_gpu.py).
+    Returns (loss, {parameter name: gradient}) in `dtype`."""
+    f64 = dtype
     W = {k: torch.as_tensor(v).to(f64) for k, v in w.items()}
     s_self, s_obj, s_mask = (torch.as_tensor(x).to(f64) for x in s)
     a, q_next = torch.as_tensor(a).to(f64), torch.as_tensor(q_next).to(f64)
@@ -197,14 +200,32 @@ def critic_step_bf16(w, s, a, q_next, r, d, taus, gamma=0.99, kappa=1.0, rnd=bf1
     wc, w1, w2 = (rnd(W[p + ".weight"]) for p in ("cos_embedding", "hidden_layer", "hidden_layer_2"))
     bc, b1, b2 = (W[p + ".bias"] for p in ("cos_embedding", "hidden_layer", "hidden_layer_2"))
     wo, bo = W["output_layer.weight"][0], W["output_layer.bias"][0]
-    # encoders (f32 dot products in the launch)
-    f_self = torch.relu(s_self @ W["self_encoder.0.weight"].T + W["self_encoder.0.bias"])
-    f_obj = torch.relu(s_obj @ W["object_encoder.0.weight"].T + W["object_encoder.0.bias"])   # (B,5,40)
-    f_obj = f_obj * (s_mask >= 0.5).to(f64).unsqueeze(-1)
+    # encoders: the launch's own f32 arithmetic, op for op (stage_fg: d = ((0 + w0 x0) + w1 x1) + ...,
+    # relu(d + b); no FMA), so F and G are bit-identical to the kernel's before F's bf16 rounding
+    def enc32(wk, bk, x):
+        w32, b32, x32 = W[wk].float(), W[bk].float(), x.float()
+        acc = torch.zeros(x32.shape[:-1] + (w32.shape[0],), dtype=torch.float32)
+        for i in range(w32.shape[1]):
+            acc = acc + w32[:, i] * x32[..., i:i + 1]
+        return torch.relu(acc + b32).to(f64)
+    if rnd is bf16_round:
+        f_self = enc32("self_encoder.0.weight", "self_encoder.0.bias", s_self)
+        f_obj = enc32("object_encoder.0.weight", "object_encoder.0.bias", s_obj)
+        G = enc32("action_encoder.0.weight", "action_encoder.0.bias", a)                       # (B,128)
+    else:
+        f_self = torch.relu(s_self @ W["self_encoder.0.weight"].T + W["self_encoder.0.bias"])
+        f_obj = torch.relu(s_obj @ W["object_encoder.0.weight"].T + W["object_encoder.0.bias"])
+        G = torch.relu(a @ W["action_encoder.0.weight"].T + W["action_encoder.0.bias"])
+    f_obj = f_obj * (s_mask >= 0.5).to(f64).unsqueeze(-1)                                      # (B,5,40)
     Fb = rnd(torch.cat((f_self, f_obj.reshape(B, 200)), 1))                                    # (B,256)
-    G = torch.relu(a @ W["action_encoder.0.weight"].T + W["action_encoder.0.bias"])              # (B,128)
-    pis = torch.tensor([np.pi * i for i in range(64)], dtype=torch.float32).to(f64)   # AC_IQN_model.py:389
-    cos = rnd(torch.cos(taus.reshape(B * N, 1) * pis))                                             # (R,64)
+    if rnd is bf16_round:
+        # the bf16 build's cosine (asvrl_mfma.h cos_pi_k_tau): v_cos_f32 of the f32 revolution count
+        # tau * (k / 2), i.e. cos(2 pi f32(tau k / 2)), evaluated here in f64
+        rev = taus.float().reshape(B * N, 1) * (0.5 * torch.arange(64, dtype=torch.float32))
+        cos = rnd(torch.cos(2 * math.pi * rev.double()).to(f64))
+    else:
+        pis = torch.tensor([np.pi * i for i in range(64)], dtype=torch.float32).to(f64)   # AC_IQN_model.py:389
+        cos = torch.cos(taus.reshape(B * N, 1) * pis)                                           # (R,64)
     Fr = Fb.repeat_interleave(N, 0)
     Gr = G.repeat_interleave(N, 0)
     c = torch.relu(cos @ wc.T + bc)

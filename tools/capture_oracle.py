@@ -1047,6 +1047,73 @@ def capture_eval():
     print("eval keys:", len(out))
 
 
+def capture_eval60():
+    """F10: Trainer.evaluation (trainer.py:266-392) on the SHIPPED eval schedule (config/ac_iqn.json
+    eval_schedule: 60 episodes over six curriculum stages, 3-5 robots, 0-4 buoys) with two AC-IQN agents:
+    'init' = the seeded initial agent (its episodes mostly run to the 1000-step limit), 'trained' = the same
+    agent after 200 reference train_AC_IQN steps (agent.py:386-432) on a replay filled by 3000 steps of the
+    reference env under uniform actions (the trainer's add / deactivation, trainer.py:155-172). Stored: the
+    60 configs, each agent's actor weights, the per-config metrics (mean return, success, mean time, mean
+    energy) and per robot the trajectory length and final trajectory row (tests/golden/eval60_ref.npz)."""
+    import contextlib
+    import io
+    import json
+    import random
+    from rfarl.policy.trainer import Trainer
+    sched = json.load(open(os.path.join(REF, "rfarl", "config", "ac_iqn.json")))["eval_schedule"]
+    out = {}
+    for tag in ("init", "trained"):
+        torch.manual_seed(0)
+        random.seed(5)
+        np.random.seed(5)
+        agent = ref_agent_mod.Agent(device="cpu", seed=100, agent_type="AC-IQN")
+        if tag == "trained":
+            env = MarineNavEnv3(seed=3)
+            env.num_robots, env.num_cores, env.num_obs, env.min_start_goal_dis = 5, 0, 4, 40.0
+            rs = np.random.RandomState(9)
+            with contextlib.redirect_stdout(io.StringIO()):
+                states, _, _ = env.reset()
+            for t in range(3000):
+                acts = [None if r.deactivated else [float(rs.uniform(-1, 1)), float(rs.uniform(-1, 1))]
+                        for r in env.robots]
+                nxt, rew, done, _ = env.step(acts, True)
+                for i, r in enumerate(env.robots):
+                    if r.deactivated:
+                        continue
+                    agent.memory.add((states[i], acts[i], rew[i], nxt[i], done[i]))
+                    if r.collision or r.reach_goal:
+                        r.deactivated = True
+                states = nxt
+                if env.check_all_deactivated() or env.episode_timesteps >= 1000:
+                    with contextlib.redirect_stdout(io.StringIO()):
+                        states, _, _ = env.reset()
+            for _ in range(200):
+                agent.train()
+        tr = Trainer(MarineNavEnv3(seed=1), MarineNavEnv3(seed=253, is_eval_env=True), sched, agent)
+        random.seed(77)
+        np.random.seed(77)
+        with contextlib.redirect_stdout(io.StringIO()):
+            tr.evaluation()
+        p = tag + "/"
+        out[p + "configs"] = np.array(json.dumps(tr.eval_config))
+        out.update(sd_arrays(p + "net/", agent.policy_local.actor))
+        out[p + "rewards"] = np.array(tr.eval_rewards[0], dtype=np.float64)
+        out[p + "successes"] = np.array(tr.eval_successes[0], dtype=bool)
+        out[p + "times"] = np.array(tr.eval_times[0], dtype=np.float64)
+        out[p + "energies"] = np.array(tr.eval_energies[0], dtype=np.float64)
+        lens, last = [], []
+        for ep in tr.eval_trajectories[0]:
+            for traj in ep:
+                lens.append(len(traj))
+                last.append(np.array(traj[-1], dtype=np.float64))
+        out[p + "traj_len"] = np.array(lens, np.int32)
+        out[p + "traj_last"] = np.array(last)
+        out[p + "robots"] = np.array([len(ep) for ep in tr.eval_trajectories[0]], np.int32)
+        print(tag, "successes", int(np.sum(tr.eval_successes[0])), "of", len(tr.eval_successes[0]),
+              "lengths", [max(len(t) for t in ep) for ep in tr.eval_trajectories[0]])
+    np.savez_compressed(os.path.join(OUT, "eval60_ref.npz"), **out)
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     what = sys.argv[1:] or ["dynamics", "traces", "reset", "ac_iqn", "iqn", "rainbow", "dqn"]
