@@ -37,6 +37,17 @@
 #include "asvrl_mfma.h"
 #include "asvrl_lds.h"
 
+// FMA contraction of this file's f32 epilogue arithmetic (the loss terms, the output layer's and the encoders'
+// gradient sums, the Bellman target): one v_fma_f32 where the source writes a * b + c (the library is built
+// with -ffp-contract=off for the env kernel's f64 parity). stage_fg's encoder dot products stay uncontracted,
+// op for op what oracle/learn_ref.critic_step_bf16 restates.
+#ifndef ASVRL_FUSED_CONTRACT
+#define ASVRL_FUSED_CONTRACT 1
+#endif
+#if ASVRL_FUSED_CONTRACT
+#pragma clang fp contract(fast)
+#endif
+
 namespace asvrl {
 namespace {
 
@@ -236,6 +247,7 @@ __device__ __forceinline__ float fetch_in(const FusedArgs& a, int t, int e) {
 template <int NT, int S, int G, bool IQN>
 __device__ __forceinline__ void stage_fg(const FusedArgs& a, int b0, int tid, const float* in, const float* enc,
                                          float* Fs, float* Gs) {
+#pragma clang fp contract(off)
   using IL = InLayout<NT, S, G, IQN ? 1 : 2>;
   constexpr int T = kNW * 64;
   const float* self_w = enc;

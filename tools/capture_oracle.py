@@ -25,6 +25,8 @@ Fixture families:
                         networks from a numpy-seeded generator (oracle/learn_ref.py)
   learn_dqn.npz     F8  Agent.train_DQN / act_dqn (agent.py:518-545, 271-287)
   eval_ref.npz      F9  Trainer.evaluation (trainer.py:266-392), AC-IQN and Rainbow
+  eval60_ref.npz    F10 Trainer.evaluation on config/ac_iqn.json's 60-episode eval_schedule, the seeded
+                        AC-IQN agent and the same agent after 200 train_AC_IQN steps (capture_eval60)
 """
 import os
 import sys
