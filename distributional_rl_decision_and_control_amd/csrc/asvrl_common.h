@@ -140,6 +140,15 @@ struct StreamF {
     box_muller(u24(w.x), u24(w.y), a, b);
     box_muller(u24(w.z), u24(w.w), c, d);
   }
+  // normal4 and, from the same call, a fourth uniform in (0, 1): the low bytes of three of its words (the
+  // Gaussians take the top 24 bits of each), for the table-driven von Mises draw (asvrl_env.hip)
+  __device__ void normal4u(float& a, float& b, float& c, float& d, float& u) const {
+    const U4 w = philox4x32_10(U4{0u, c1, c2, c3}, k0, k1);
+    box_muller(u24(w.x), u24(w.y), a, b);
+    box_muller(u24(w.z), u24(w.w), c, d);
+    const uint32_t spare = ((w.x & 0xFFu) << 16) | ((w.y & 0xFFu) << 8) | (w.z & 0xFFu);
+    u = (static_cast<float>(spare) + 0.5f) * (1.0f / 16777216.0f);
+  }
   // one Best-Fisher attempt from the uniforms (U, V): W and whether it is accepted
   static __device__ bool attempt(float U, float V, float s, float kappa, float& W) {
     const float Z = __cosf(3.14159265f * U);

@@ -20,6 +20,7 @@
 #include <type_traits>
 
 #include "asvrl_common.h"
+#include "asvrl_vonmises_k1.h"
 
 namespace asvrl {
 namespace {
@@ -299,6 +300,16 @@ __device__ inline void cswap(bool cond, Cand& x, Cand& y) {
   }
 }
 
+// vonmises(0, 1) by its inverse CDF (asvrl_vonmises_k1.h, 1025 f32 knots) at the uniform u, linearly
+// interpolated: no rejection loop (Best-Fisher's one or two extra Philox calls per draw, and a wave runs
+// the second whenever one of its 64 lanes rejects twice)
+__device__ __forceinline__ float vonmises_k1_icdf(float u) {
+  const float x = u * static_cast<float>(kVmIcdfN);
+  const int i = min(static_cast<int>(x), kVmIcdfN - 1);
+  const float lo = kVmIcdfK1[i], hi = kVmIcdfK1[i + 1];
+  return lo + (x - static_cast<float>(i)) * (hi - lo);
+}
+
 // perception noise of (robot qidx, candidate slot): injected (noise_mode 0, [robot][O + R][5]), f64
 // Philox (1) or f32 Philox (2), the substream keyed by (robot, slot) so every launch shape draws the same
 // NM: the mode fixed at compile time (the pair kernel's instances), -1: read from ctl. VM = false skips the
@@ -325,10 +336,11 @@ __device__ __forceinline__ void draw_noise(const AsvParams& p, const AsvStepCtl&
     StreamF rngf(ctl.seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull, static_cast<uint32_t>(qidx),
                  (static_cast<uint32_t>(qidx >> 32) ^ 0xF32Au) + (static_cast<uint32_t>(slot) << 20),
                  static_cast<uint32_t>(ctr));
-    float f0, f1, f2, f3;
-    rngf.normal4(f0, f1, f2, f3);
+    float f0, f1, f2, f3, u;
+    rngf.normal4u(f0, f1, f2, f3, u);
     n0 = f0 * p.pos_std; n1 = f1 * p.pos_std; n2 = f2 * p.vel_std; n3 = f3 * p.vel_std;
-    if (VM) n4 = rngf.vonmises(static_cast<float>(p.r_kappa));
+    // the default radius noise (r_kappa = 1, wamv.py:24) from the table; other kappas by rejection
+    if (VM) n4 = p.r_kappa == 1.0 ? vonmises_k1_icdf(u) : rngf.vonmises(static_cast<float>(p.r_kappa));
   }
 }
 

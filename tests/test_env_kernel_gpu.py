@@ -341,6 +341,11 @@ def test_philox_perception_noise_distribution(fast):
     # the full shape of the von Mises draw: KS against scipy
     vm = (rr - 0.8) / 0.2 * np.pi
     assert stats.kstest(vm[:20000], stats.vonmises(1.0).cdf).pvalue > 1e-3
+    # f32 draws: the radius comes from the inverse-CDF table at a uniform built from the low bytes of the
+    # Gaussians' Philox words -- uncorrelated with each of them (and the KS above over all 65536)
+    assert stats.kstest(vm, stats.vonmises(1.0).cdf).pvalue > 1e-3
+    for v in (px, py, vx, vy):
+        assert abs(np.corrcoef(vm, v)[0, 1]) < 4 / np.sqrt(n)
 
 
 def test_config5_full_size():
