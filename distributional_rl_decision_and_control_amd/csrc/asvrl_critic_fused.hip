@@ -386,6 +386,13 @@ __device__ __forceinline__ int row_action(const float* in, int bl, int A) {
 #ifndef ASVRL_DWC_AHEAD
 #define ASVRL_DWC_AHEAD 0
 #endif
+// dW2 + L3 as one interleaved MFMA stream (A/B knob), and its read-ahead depth in steps of two MFMAs
+#ifndef ASVRL_L3_INTERLEAVE
+#define ASVRL_L3_INTERLEAVE 0
+#endif
+#ifndef ASVRL_L3_AHEAD
+#define ASVRL_L3_AHEAD 2
+#endif
 template <int KS, int NB, int P, class WF>
 __device__ __forceinline__ void mfma_rows(f32x16 (&acc)[NB], const elem_t* img, const RowA<P>& RA, WF wf) {
   constexpr int D = ASVRL_READ_AHEAD < KS ? ASVRL_READ_AHEAD : KS;
@@ -415,9 +422,12 @@ __device__ __forceinline__ void mfma_rows(f32x16 (&acc)[NB], const elem_t* img, 
 // The weight-gradient grid dW[n] += A(kk)^T-read x B(kk, n) over kk < KK, n < NN (mf(kk, n, A, B) does
 // the MFMA and, at n = 0, the bias sum): every B(kk, n) read D steps ahead in (kk, n) order, each A(kk)
 // a whole kk ahead, one scheduling fence per step (see mfma_rows).
+#ifndef ASVRL_GRID_AHEAD
+#define ASVRL_GRID_AHEAD ASVRL_READ_AHEAD
+#endif
 template <int KK, int NN, class AF, class BF, class MF>
 __device__ __forceinline__ void mfma_grid(AF af, BF bf, MF mf) {
-  constexpr int T = KK * NN, D0 = ASVRL_READ_AHEAD < T ? ASVRL_READ_AHEAD : T;
+  constexpr int T = KK * NN, D0 = ASVRL_GRID_AHEAD < T ? ASVRL_GRID_AHEAD : T;
   if constexpr (D0 == 0) {
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
@@ -844,7 +854,10 @@ void critic_fused_kernel(FusedArgs a) {
 
     // ---------------- dW2[own][:] += dz2^T h1g;  L3: dh1g = W2^T dz2 (own block) -> dG, dz1 (own
     // slice into the dz1 image, which nobody reads before the next barrier)
-    {
+    // ASVRL_L3_INTERLEAVE: the two independent MFMA streams issued alternately (each accumulator's MFMAs in
+    // the same order: bit-identical), so each one's LDS operand reads have the other's MFMA to land behind
+    constexpr bool L3I = ASVRL_L3_INTERLEAVE && NB == 2 && G / 16 == 4;
+    if constexpr (!L3I) {
       ASVRL_FRESH_LANE();
       const TrA<kH> TA_a(lane);
       const TrA<kH> TA_b(lane);
@@ -868,7 +881,34 @@ void critic_fused_kernel(FusedArgs a) {
       f32x16 acc[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[j] = f32x16{};
-      mfma_rows<kH / 16, NB>(acc, L.b, RA_b, [&](int ks) { return w2tf[ks]; });
+      if constexpr (L3I) {
+        // step t: dW2's MFMA (kk, n) = (t / 4, t % 4) and L3's (block j, k-step ks) = (t % 2, t / 2)
+        const TrA<kH> TA_a(lane);
+        const TrA<kH> TA_b(lane);
+        constexpr int T = 16, D = ASVRL_L3_AHEAD;
+        frag8 gA[2], gB[D], rB[D];
+        gA[0] = trf(L.b, TA_b, 0, w);
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          gB[d] = trf(L.a, TA_a, d / 4, d % 4);
+          rB[d] = rowf(L.b, RA_b, d % 2, d / 2);
+        }
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          const int kk = t / 4, n = t % 4;
+          if (n == 0 && kk + 1 < 4) gA[(kk + 1) % 2] = trf(L.b, TA_b, kk + 1, w);
+          if (n == 0) db2 += sum8(gA[kk % 2]);
+          mfma_acc(dW2[n], gA[kk % 2], gB[t % D]);
+          acc[t % 2] = mfma(w2tf[t / 2], rB[t % D], acc[t % 2]);
+          if (t + D < T) {
+            gB[t % D] = trf(L.a, TA_a, (t + D) / 4, (t + D) % 4);
+            rB[t % D] = rowf(L.b, RA_b, (t + D) % 2, (t + D) / 2);
+          }
+          __builtin_amdgcn_sched_barrier(ASVRL_RA_FENCE_MASK);
+        }
+      } else {
+        mfma_rows<kH / 16, NB>(acc, L.b, RA_b, [&](int ks) { return w2tf[ks]; });
+      }
       // dz1 = dh1g G 1[h1 > 0]; dG = sum over the sample's taus of dh1g h1 (-> dzG = dG 1[G > 0])
 #pragma unroll
       for (int j = 0; j < NB; ++j) {   // h1 unpacked here, not earlier
