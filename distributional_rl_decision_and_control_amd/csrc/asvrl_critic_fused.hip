@@ -386,6 +386,10 @@ __device__ __forceinline__ int row_action(const float* in, int bl, int A) {
 #ifndef ASVRL_DWC_AHEAD
 #define ASVRL_DWC_AHEAD 0
 #endif
+// dW1 + L4's first dx block as one interleaved stream (A/B knob)
+#ifndef ASVRL_L4_INTERLEAVE
+#define ASVRL_L4_INTERLEAVE 0
+#endif
 // dW2 + L3 as one interleaved MFMA stream (A/B knob), and its read-ahead depth in steps of two MFMAs
 #ifndef ASVRL_L3_INTERLEAVE
 #define ASVRL_L3_INTERLEAVE 0
@@ -970,7 +974,11 @@ void critic_fused_kernel(FusedArgs a) {
     ASVRL_STAMP(13);
 
     // ---------------- dW1[own][:] += dz1^T x; L4's first weight fragments fetched meanwhile
+    // ASVRL_L4_INTERLEAVE: L4's first block's dx = W1^T dz1 MFMAs issued between dW1's (one per two), each
+    // accumulator's MFMAs in the same order (bit-identical)
+    constexpr bool L4I = ASVRL_L4_INTERLEAVE && NB == 2 && G / 16 == 4 && ASVRL_READ_AHEAD != 0;
     frag8 wt[8], wcc[4];
+    f32x16 dx0[L4I ? NB : 1];
     {
       ASVRL_FRESH_LANE();
       const TrA<kH> TA_d(lane);
@@ -979,12 +987,39 @@ void critic_fused_kernel(FusedArgs a) {
       for (int ks = 0; ks < 8; ++ks) wt[ks] = W1T[((2 * w) * 8 + ks) * 64 + lane];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) wcc[ks] = WCR ? wcr0[ks] : WC[((2 * w) * 4 + ks) * 64 + lane];
-      mfma_grid<G / 16, 8>([&](int kk) { return trf(L.dz1, TA_d, kk, w); },
-                           [&](int kk, int n) { return trf(L.x, TA_x, kk, n); },
-                           [&](int kk, int n, const frag8& A, const frag8& B) {
-                             if (n == 0) db1 += sum8(A);
-                             mfma_acc(dW1[n], A, B);
-                           });
+      if constexpr (L4I) {
+        const RowA<kH> RA_d(r, h);
+        constexpr int T = 32, D = ASVRL_GRID_AHEAD, DR = 2;
+        frag8 gA[2], gB[D], rB[DR];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) dx0[j] = f32x16{};
+        gA[0] = trf(L.dz1, TA_d, 0, w);
+#pragma unroll
+        for (int d = 0; d < D; ++d) gB[d] = trf(L.x, TA_x, d / 8, d % 8);
+#pragma unroll
+        for (int d = 0; d < DR; ++d) rB[d] = rowf(L.dz1, RA_d, d % 2, d / 2);
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          const int kk = t / 8, n = t % 8;
+          if (n == 0 && kk + 1 < 4) gA[(kk + 1) % 2] = trf(L.dz1, TA_d, kk + 1, w);
+          if (n == 0) db1 += sum8(gA[kk % 2]);
+          mfma_acc(dW1[n], gA[kk % 2], gB[t % D]);
+          if (t + D < T) gB[t % D] = trf(L.x, TA_x, (t + D) / 8, (t + D) % 8);
+          if (t % 2 == 1) {   // dx step u = (j, ks) = (u % 2, u / 2)
+            const int u = t / 2;
+            dx0[u % 2] = mfma(wt[u / 2], rB[u % DR], dx0[u % 2]);
+            if (u + DR < 16) rB[u % DR] = rowf(L.dz1, RA_d, (u + DR) % 2, (u + DR) / 2);
+          }
+          __builtin_amdgcn_sched_barrier(ASVRL_RA_FENCE_MASK);
+        }
+      } else {
+        mfma_grid<G / 16, 8>([&](int kk) { return trf(L.dz1, TA_d, kk, w); },
+                             [&](int kk, int n) { return trf(L.x, TA_x, kk, n); },
+                             [&](int kk, int n, const frag8& A, const frag8& B) {
+                               if (n == 0) db1 += sum8(A);
+                               mfma_acc(dW1[n], A, B);
+                             });
+      }
     }
     if constexpr (AH) {   // round t + grid's images, behind the dW1 MFMAs
       const int tn = t + static_cast<int>(gridDim.x);
@@ -1014,7 +1049,12 @@ void critic_fused_kernel(FusedArgs a) {
           dxs[j] = f32x16{};
           ccs[j] = acc_init(bcp, mb * 32, h);
         }
-        mfma_rows<8, NB>(dxs, L.dz1, RA_d, [&](int ks) { return wt[ks]; });
+        if (L4I && mq == 0) {
+#pragma unroll
+          for (int j = 0; j < NB; ++j) dxs[j] = dx0[L4I ? j : 0];
+        } else {
+          mfma_rows<8, NB>(dxs, L.dz1, RA_d, [&](int ks) { return wt[ks]; });
+        }
         mfma_rows<4, NB>(ccs, cosb, RA_cos, [&](int ks) { return wcc[ks]; });
       }
 #pragma unroll
