@@ -160,12 +160,14 @@ def learn_prologue(st, replay, taus, seed, counter_dev=None, counter=0, out=None
 
 
 def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, actor_grads, rows, gamma=0.99,
-                         taus=None, sync=None, max_norm=0.5, actor_wait=None, counter=None, prologue_done=False):
+                         taus=None, sync=None, max_norm=0.5, actor_wait=None, counter=None, prologue_done=False,
+                         target_wait=None):
     """One AC-IQN update from replay rows [B][88]. taus: (3, B, N) or None (drawn here).
     actor_wait: event to wait for before the actor's weights change (a concurrent act kernel).
     counter: an int64 device scalar incremented after the step (the learn counter; in-kernel when
     the optimiser step is fused). prologue_done: learn_prologue already ran the actor's TRAIN forward and
-    the target actor on these rows.
+    the target actor on these rows. target_wait: an event the target critic waits for (a schedule knob:
+    the rollout's env step ahead of it instead of beside it; no data dependency).
     Returns (critic_loss, actor_loss, critic_grad_norm, actor_grad_norm) as device scalars."""
     B, N = st.B, st.N
     critic, actor = policy_local.critic, policy_local.actor
@@ -178,6 +180,8 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     # ---- critic (agent.py:395-416); every critic .grad is overwritten below (no zeroing). The
     # trunk kernels run the critic's observation / action encoders on the replay rows themselves.
     q_next = st.q_next
+    if target_wait is not None:
+        torch.cuda.current_stream().wait_event(target_wait)
     if prologue_done:   # only the target critic is left of the target chain
         critic_forward(st.target_trunk, None, None, taus[0], st.N, q=q_next, obs=rows[:, OBS:2 * OBS], act=st.na)
     else:

@@ -2,8 +2,8 @@
 (config/ac_iqn.json eval_schedule: 60 episodes over the six curriculum stages, 3-5 robots, 0-4 buoys, min
 start-goal distance 30-40 m) against the reference's own Trainer.evaluation (trainer.py:266-392), captured
 by tools/capture_oracle.py capture_eval60 (tests/golden/eval60_ref.npz) with two AC-IQN agents: the seeded
-initial agent ('init': 54 of its 60 episodes run to the 1000-step limit) and the same agent after 200
-reference train_AC_IQN steps ('trained': collisions after 8-413 steps and 1000-step timeouts).
+initial agent ('init': 41 of its 60 episodes run to the 1000-step limit) and the same agent after 200
+reference train_AC_IQN steps ('trained': 32 timeouts, the rest collisions after 8-413 steps).
 
 Same configs, weights and seeds. Per config: success and mean time exact; mean discounted return and mean
 energy within 1e-5 relative (the north star's return bar); per robot the trajectory length exact and the
