@@ -11,11 +11,11 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _run(agent_type, chain, iters, n_envs=256, batch=256, unroll=2):
+def _run(agent_type, chain, iters, n_envs=256, batch=256, unroll=2, target_after_env=False):
     from distributional_rl_decision_and_control_amd.vec_trainer import VecTrainer
     tr = VecTrainer(n_envs=n_envs, agent_type=agent_type, batch_size=batch, num_tau=32, seed=21, graphs=True,
                     unroll=unroll, chain=chain, buffer_size=max(n_envs * 5 * 40, 4 * n_envs * 5),
-                    learning_starts=2 * batch)
+                    learning_starts=2 * batch, target_after_env=target_after_env)
     while tr.replay_size_host() < tr.learning_starts:
         tr.iteration()
     for _ in range(iters):
@@ -41,6 +41,14 @@ def _same(a, pa, la, b, pb, lb):
 def test_chained_schedule_matches_joined(agent_type):
     a, pa, la = _run(agent_type, True, 8)
     b, pb, lb = _run(agent_type, False, 8)
+    _same(a, pa, la, b, pb, lb)
+
+
+def test_chained_schedule_target_after_env_matches_joined():
+    """The schedule knob that holds the learner's target critic behind the same iteration's env step: an
+    ordering only, so bit-identical to the joined schedule too."""
+    a, pa, la = _run("AC-IQN", True, 8, target_after_env=True)
+    b, pb, lb = _run("AC-IQN", False, 8)
     _same(a, pa, la, b, pb, lb)
 
 
