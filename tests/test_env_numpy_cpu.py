@@ -124,3 +124,13 @@ def test_numpy_env_reset_layouts(c):
 def test_numpy_env_rollout_runs():
     n, el = en.rollout(0.5, seed=3)
     assert n > 10 and el >= 0.5
+
+
+def test_reference_style_training_loop_runs():
+    """oracle/ref_loop.py (bench.py's reference-style CPU leg): act + env.step + replay + train_AC_IQN at B = 64
+    every 4 steps on one process, both modes."""
+    from oracle import ref_loop
+    r = ref_loop.train_loop(1.0, seed=2)
+    assert r["steps"] >= 8 and r["learns"] >= 1 and r["seconds"] >= 1.0
+    e = ref_loop.train_loop(0.3, seed=2, env_only=True)
+    assert e["learns"] == 0 and e["steps"] >= 8
