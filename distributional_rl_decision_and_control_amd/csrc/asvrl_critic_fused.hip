@@ -386,6 +386,12 @@ __device__ __forceinline__ int row_action(const float* in, int bl, int A) {
 #ifndef ASVRL_DWC_AHEAD
 #define ASVRL_DWC_AHEAD 0
 #endif
+// the workgroup's dW2 / dW1 partials stored during its last round, right after their last MFMAs (behind the
+// rest of that round) instead of all partials at the end: the chip-wide 69 MB store burst at the launch's
+// end shrinks to the cos layer's, encoders' and output layer's partials. Same values, same places.
+#ifndef ASVRL_EARLY_PARTIALS
+#define ASVRL_EARLY_PARTIALS 1
+#endif
 // dW1 + L4's first dx block as one interleaved stream (A/B knob)
 #ifndef ASVRL_L4_INTERLEAVE
 #define ASVRL_L4_INTERLEAVE 0
@@ -569,9 +575,43 @@ void critic_fused_kernel(FusedArgs a) {
   float encr[IQN ? 8 : 1];   // IQN with parts.enc: this lane's feature's encoder sums
 #pragma unroll
   for (int i = 0; i < (IQN ? 8 : 1); ++i) encr[i] = 0.f;
+  // the workgroup's dW2 / dW1 partials: [M*K + M] per layer, features in natural order (register g of lane
+  // half h is feature row (g & 3) + 8 (g >> 2) + 4 h of the wave's block, lane r its column)
+  const int grp = blockIdx.x;
+  auto store_dw2 = [&]() {
+    mfma_drain();
+    int tid_s = threadIdx.x;
+    asm volatile("" : "+v"(tid_s));
+    const int ls = tid_s & 63, hs = ls >> 5, rs = ls & 31;
+    float* p2 = a.parts.hidden2 + static_cast<size_t>(grp) * (kH * kH + kH);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int f2 = swap23(w * 32 + (g & 3) + 8 * (g >> 2) + 4 * hs);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) p2[f2 * kH + swap23(32 * n + rs)] = dW2[n][g];
+    }
+    const float v = half_sum(db2);
+    if (hs == 0) p2[kH * kH + swap23(w * 32 + rs)] = v;
+  };
+  auto store_dw1 = [&]() {
+    mfma_drain();
+    int tid_s = threadIdx.x;
+    asm volatile("" : "+v"(tid_s));
+    const int ls = tid_s & 63, hs = ls >> 5, rs = ls & 31;
+    float* p1 = a.parts.hidden + static_cast<size_t>(grp) * (kH * kC + kH);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int f2 = swap23(w * 32 + (g & 3) + 8 * (g >> 2) + 4 * hs);
+#pragma unroll
+      for (int n = 0; n < 8; ++n) p1[f2 * kC + swap23(32 * n + rs)] = dW1[n][g];
+    }
+    const float v = half_sum(db1);
+    if (hs == 0) p1[kH * kC + swap23(w * 32 + rs)] = v;
+  };
   int buf = 0, it_ = 0;
   (void)it_;
   for (int t = blockIdx.x; t < a.rounds; t += gridDim.x, buf ^= 1, ++it_) {
+    const bool last_round = t + static_cast<int>(gridDim.x) >= a.rounds;   // workgroup-uniform
     // the next round's inputs, into registers during this round and into LDS at its end
     float pre[IL::kPer];
     int tid_p = threadIdx.x;
@@ -969,6 +1009,7 @@ void critic_fused_kernel(FusedArgs a) {
         if (e < IL::kSize) L.in[buf ^ 1][e] = pre[u];
       }
     }
+    if (ASVRL_EARLY_PARTIALS && last_round) store_dw2();
     ASVRL_STAMP(12);
     __syncthreads();
     ASVRL_STAMP(13);
@@ -1021,6 +1062,7 @@ void critic_fused_kernel(FusedArgs a) {
                              });
       }
     }
+    if (ASVRL_EARLY_PARTIALS && last_round) store_dw1();
     if constexpr (AH) {   // round t + grid's images, behind the dW1 MFMAs
       const int tn = t + static_cast<int>(gridDim.x);
       if (tn < a.rounds) stage(tn * G / NT, L.in[buf ^ 1], L.cos[buf ^ 1], L.F[buf ^ 1], L.G[buf ^ 1]);
@@ -1182,7 +1224,6 @@ void critic_fused_kernel(FusedArgs a) {
 
   // ---------------- the workgroup's partials: [M*K + M] per layer, features in natural order
   mfma_drain();
-  const int grp = blockIdx.x;
   {
     // encoders (the round loop ended on a barrier: every wave's sums are in LDS; IQN's are moved from
     // registers into the x image, free now). Object features folded over the five objects in object
@@ -1225,15 +1266,19 @@ void critic_fused_kernel(FusedArgs a) {
   }
   float* p2 = a.parts.hidden2 + static_cast<size_t>(grp) * (kH * kH + kH);
   float* p1 = a.parts.hidden + static_cast<size_t>(grp) * (kH * kC + kH);
+  (void)p2;
+  (void)p1;
   float* pc = a.parts.cos_emb + static_cast<size_t>(grp) * (kC * kNcos + kC);
 #pragma unroll
   for (int g = 0; g < 16; ++g) {
     const int m = (g & 3) + 8 * (g >> 2) + 4 * h;   // MFMA C row of register g
     const int f2 = swap23(w * 32 + m);
+    if constexpr (!ASVRL_EARLY_PARTIALS) {
 #pragma unroll
-    for (int n = 0; n < 4; ++n) p2[f2 * kH + swap23(32 * n + r)] = dW2[n][g];
+      for (int n = 0; n < 4; ++n) p2[f2 * kH + swap23(32 * n + r)] = dW2[n][g];
 #pragma unroll
-    for (int n = 0; n < 8; ++n) p1[f2 * kC + swap23(32 * n + r)] = dW1[n][g];
+      for (int n = 0; n < 8; ++n) p1[f2 * kC + swap23(32 * n + r)] = dW1[n][g];
+    }
 #pragma unroll
     for (int mq = 0; mq < 2; ++mq) {
       const int fc = swap23((2 * w + mq) * 32 + m);
@@ -1241,13 +1286,17 @@ void critic_fused_kernel(FusedArgs a) {
       for (int n = 0; n < 2; ++n) pc[fc * kNcos + 32 * n + r] = dWc[mq * 2 + n][g];
     }
   }
-  db2 = half_sum(db2);
-  db1 = half_sum(db1);
   dbc0 = half_sum(dbc0);
   dbc1 = half_sum(dbc1);
+  if constexpr (!ASVRL_EARLY_PARTIALS) {
+    db2 = half_sum(db2);
+    db1 = half_sum(db1);
+  }
   if (h == 0) {
-    p2[kH * kH + swap23(w * 32 + r)] = db2;
-    p1[kH * kC + swap23(w * 32 + r)] = db1;
+    if constexpr (!ASVRL_EARLY_PARTIALS) {
+      p2[kH * kH + swap23(w * 32 + r)] = db2;
+      p1[kH * kC + swap23(w * 32 + r)] = db1;
+    }
     pc[kC * kNcos + swap23(2 * w * 32 + r)] = dbc0;
     pc[kC * kNcos + swap23((2 * w + 1) * 32 + r)] = dbc1;
   }
