@@ -388,9 +388,10 @@ __device__ __forceinline__ int row_action(const float* in, int bl, int A) {
 #endif
 // the workgroup's dW2 / dW1 partials stored during its last round, right after their last MFMAs (behind the
 // rest of that round) instead of all partials at the end: the chip-wide 69 MB store burst at the launch's
-// end shrinks to the cos layer's, encoders' and output layer's partials. Same values, same places.
+// end shrinks to the cos layer's, encoders' and output layer's partials. Same values, same places. Measured
+// no faster (108.8 vs 109.0 us median, profiles/r04e_fused_variants_ab.txt) with 5 more spilled registers: off.
 #ifndef ASVRL_EARLY_PARTIALS
-#define ASVRL_EARLY_PARTIALS 1
+#define ASVRL_EARLY_PARTIALS 0
 #endif
 // dW1 + L4's first dx block as one interleaved stream (A/B knob)
 #ifndef ASVRL_L4_INTERLEAVE
