@@ -8,8 +8,9 @@ reference train_AC_IQN steps ('trained': 32 timeouts, the rest collisions after 
 Same configs, weights and seeds. Per config: success and mean time exact, every robot's episode length exact;
 mean discounted return and mean energy within 1e-5 relative (the north star's return bar) on at least 54 of
 the 60 configs and within 1e-3 on all (the closed loop carries the batched GPU policy's f32 rounding forward
-over up to 1000 steps); final trajectory rows within 5e-2 absolute (printed: their drift over a 1000-step
-episode)."""
+over up to 1000 steps); final trajectory rows within 1e-3 absolute (observed 2.8e-4 after 1000 steps).
+Observed (r04g): 'init' returns within 1e-5 on 58 of 60 configs (the other two 2e-4), 'trained' on all 60
+(max 1.3e-6); energies within 6e-8 everywhere."""
 import json
 import random
 
@@ -63,7 +64,8 @@ def test_evaluation_on_the_shipped_schedule(tag):
     np.testing.assert_array_equal(np.array(lens), z[p + "traj_len"])
     # returns and energies: the north star's 1e-5 on the large majority of configs; over 1000 closed-loop steps
     # the batched f32 policy's summation order (vs the reference's batch-1 CPU GEMM) drifts a few configs
-    # further (r04f: 2 of 60 at 2e-4): bounded at 1e-3
+    # further (r04g: 'init' 58 of 60 within 1e-5, the other two at 2e-4; 'trained' all 60 within 1.3e-6; energies
+    # all within 6e-8): bounded at 1e-3
     assert (rr <= 1e-5).sum() >= 54 and rr.max() < 1e-3, rr
     assert (re <= 1e-5).sum() >= 54 and re.max() < 1e-3, re
-    assert d.max() < 5e-2
+    assert d.max() < 1e-3   # r04g: 2.8e-4
