@@ -92,10 +92,24 @@ __global__ __launch_bounds__(1024) void mean_kernel(const float* __restrict__ x,
 // projection; the LDS hand-offs are wave-local (a wave's LDS instructions execute in order, so only the
 // compiler has to be kept from reordering them -- no workgroup barrier). Round 3: one row per wave and
 // three workgroup barriers per row, 5.8 us at B = 8192 (0.074 of HBM), 26 us at B = 65536.
+//
+// Round 4: the serial part batched across rows. A run is at most two atoms long unless atoms clamp at
+// Vmin / Vmax or the row is terminal (b_{j+1} - b_j = gamma^n * nonterminal <= 1); the round-3 kernel walked
+// every long run on the whole wave, one row after another (up to 2 x 51 dependent adds per row: 23 us at
+// B = 65536, 0.147 of HBM). Now a wave stages its ROWS rows in LDS (masses and each target's run bounds
+// as four bytes), finishes every target whose runs are short with selects (one ds_read2 per pass), and
+// queues the others as (row, target) jobs that the wave's lanes then walk in parallel, one job per lane.
+// The run bounds are scattered unconditionally (lanes that bound no run write a dummy slot); the row's
+// scalars come through the scalar cache. Same additions in the same order: bit-identical.
 constexpr int kC51Waves = 4;
+#ifndef ASVRL_C51_ROWS
+#define ASVRL_C51_ROWS 4
+#endif
+#ifndef ASVRL_C51_DUMMY
+#define ASVRL_C51_DUMMY 0
+#endif
 
-// acc + v[j0] + v[j0+1] + ... + v[j1-1], added in order; the LDS reads go out 8 at a time so a long
-// run (a terminal row sends every atom to one target) costs one LDS round trip per 8 adds
+// acc + v[j0] + v[j0+1] + ... + v[j1-1], added in order; the LDS reads go out 8 at a time
 __device__ __forceinline__ float run_sum(const float* v, int j0, int j1, float acc) {
   int j = j0;
   for (; j + 8 <= j1; j += 8) {
@@ -128,62 +142,113 @@ __global__ __launch_bounds__(kC51Waves * kWave) void c51_kernel(const float* __r
                                                                 const float* __restrict__ support, int B,
                                                                 int atoms, float vmin, float vmax, float dz,
                                                                 float gamma_n, float* __restrict__ m) {
-  __shared__ float s_lo[kC51Waves][kWave], s_up[kC51Waves][kWave];
-  __shared__ int2 s_lr[kC51Waves][kWave], s_ur[kC51Waves][kWave];   // [start, end) of each target's run
+  // per wave and row: the lower / upper masses (a 65th slot for the second read of a run starting at lane
+  // 63) and per target its runs' bounds as bytes {lower start, lower end, upper start, upper end} (a 65th
+  // dummy slot for the lanes that bound no run); the long-run jobs (row << 6 | target)
+  __shared__ float s_lo[kC51Waves][ROWS][kWave + 1], s_up[kC51Waves][ROWS][kWave + 1];
+  __shared__ uint32_t s_rb[kC51Waves][ROWS][kWave + 1];
+  __shared__ uint16_t s_job[kC51Waves][ROWS * kWave];
   const int lane = threadIdx.x & (kWave - 1);
-  const int w = threadIdx.x >> 6;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int row0 = (blockIdx.x * kC51Waves + w) * ROWS;
+  const int nr = B - row0 < ROWS ? B - row0 : ROWS;   // wave-uniform
+  if (nr <= 0) return;
   const bool lane_on = lane < atoms;
   const float z = lane_on ? support[lane] : 0.f;
   float pv[ROWS], rv[ROWS], nv[ROWS];
 #pragma unroll
   for (int r = 0; r < ROWS; ++r) {
     const int b = row0 + r;
-    const bool on = b < B && lane_on;
-    pv[r] = on ? pns_a[static_cast<size_t>(b) * atoms + lane] : 0.f;
-    rv[r] = b < B ? ret[b] : 0.f;
-    nv[r] = b < B ? nonterm[b] : 0.f;
+    const bool on = r < nr && lane_on;
+    pv[r] = on ? __builtin_nontemporal_load(pns_a + static_cast<size_t>(b) * atoms + lane) : 0.f;
+    rv[r] = r < nr ? ret[b] : 0.f;
+    nv[r] = r < nr ? nonterm[b] : 0.f;
   }
+  // (1) every row's masses into LDS, bounds cleared; targets and run-boundary flags kept in registers
+  int lt[ROWS], ut[ROWS];
+  uint32_t fl[ROWS];
 #pragma unroll
   for (int r = 0; r < ROWS; ++r) {
-    const int b = row0 + r;
-    if (row0 + r >= B) break;   // wave-uniform
-    int l = -1, u = -1;
-    float lower = 0.f, upper = 0.f;
-    if (lane_on) {
-      const float ntg = nv[r] * gamma_n;
-      float tz = rv[r] + ntg * z;                   // Tz = R + nonterminal * gamma^n * z
-      tz = fminf(fmaxf(tz, vmin), vmax);            // clamp(Vmin, Vmax)
-      const float bb = (tz - vmin) / dz;            // b = (Tz - Vmin) / delta_z
-      l = static_cast<int>(floorf(bb));
-      u = static_cast<int>(ceilf(bb));
-      if (u > 0 && l == u) l -= 1;                  // agent.py:623
-      if (l < atoms - 1 && l == u) u += 1;          // agent.py:624
-      lower = pv[r] * (static_cast<float>(u) - bb);
-      upper = pv[r] * (bb - static_cast<float>(l));
-    }
+    const float ntg = nv[r] * gamma_n;
+    float tz = rv[r] + ntg * z;                   // Tz = R + nonterminal * gamma^n * z
+    tz = fminf(fmaxf(tz, vmin), vmax);            // clamp(Vmin, Vmax)
+    const float bb = (tz - vmin) / dz;            // b = (Tz - Vmin) / delta_z
+    int l = static_cast<int>(floorf(bb));
+    int u = static_cast<int>(ceilf(bb));
+    if (u > 0 && l == u) l -= 1;                  // agent.py:623
+    if (l < atoms - 1 && l == u) u += 1;          // agent.py:624
+    s_lo[w][r][lane] = pv[r] * (static_cast<float>(u) - bb);
+    s_up[w][r][lane] = pv[r] * (bb - static_cast<float>(l));
+    s_rb[w][r][lane] = 0u;
+    const bool on = lane_on && r < nr;
+    if (!on) l = u = -1;
     // off lanes carry target -1, lane 0 sees -2 before it: a valid target (>= 0) differs from both
     const int lp = from_prev_lane(l, -2), ln = from_next_lane(l, -2);
     const int up = from_prev_lane(u, -2), un = from_next_lane(u, -2);
-    s_lo[w][lane] = lower;
-    s_up[w][lane] = upper;
-    s_lr[w][lane] = make_int2(0, 0);
-    s_ur[w][lane] = make_int2(0, 0);
-    wave_lds_order();
-    if (lane_on) {
-      if (lp != l) s_lr[w][l].x = lane;
-      if (ln != l) s_lr[w][l].y = lane + 1;
-      if (up != u) s_ur[w][u].x = lane;
-      if (un != u) s_ur[w][u].y = lane + 1;
+    lt[r] = l;
+    ut[r] = u;
+    fl[r] = (on && lp != l ? 1u : 0u) | (on && ln != l ? 2u : 0u) | (on && up != u ? 4u : 0u) | (on && un != u ? 8u : 0u);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) s_lo[w][r][kWave] = s_up[w][r][kWave] = 0.f;
+  }
+  wave_lds_order();
+  // (2) run bounds: the first / last lane of each run writes its target's byte
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r) {
+    unsigned char* rb = reinterpret_cast<unsigned char*>(&s_rb[w][r][0]);
+#if ASVRL_C51_DUMMY
+    rb[4 * ((fl[r] & 1u) ? lt[r] : kWave) + 0] = static_cast<unsigned char>(lane);
+    rb[4 * ((fl[r] & 2u) ? lt[r] : kWave) + 1] = static_cast<unsigned char>(lane + 1);
+    rb[4 * ((fl[r] & 4u) ? ut[r] : kWave) + 2] = static_cast<unsigned char>(lane);
+    rb[4 * ((fl[r] & 8u) ? ut[r] : kWave) + 3] = static_cast<unsigned char>(lane + 1);
+#else
+    // masked stores: the lanes bounding no run would all hit one dummy address (a 64-way bank conflict)
+    if (fl[r] & 1u) rb[4 * lt[r] + 0] = static_cast<unsigned char>(lane);
+    if (fl[r] & 2u) rb[4 * lt[r] + 1] = static_cast<unsigned char>(lane + 1);
+    if (fl[r] & 4u) rb[4 * ut[r] + 2] = static_cast<unsigned char>(lane);
+    if (fl[r] & 8u) rb[4 * ut[r] + 3] = static_cast<unsigned char>(lane + 1);
+#endif
+  }
+  wave_lds_order();
+  // (3) lane k = target k: short runs finished with selects, long ones queued
+  int njob = 0;
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r) {
+    if (r >= nr) break;   // wave-uniform
+    const uint32_t q = s_rb[w][r][lane];
+    const int ls = q & 255u, ll = static_cast<int>((q >> 8) & 255u) - ls;
+    const int us = (q >> 16) & 255u, ul = static_cast<int>(q >> 24) - us;
+    const float a0 = s_lo[w][r][ls], a1 = s_lo[w][r][ls + 1];
+    const float c0 = s_up[w][r][us], c1 = s_up[w][r][us + 1];
+    float acc = 0.f;
+    acc = ll > 0 ? acc + a0 : acc;
+    acc = ll > 1 ? acc + a1 : acc;
+    acc = ul > 0 ? acc + c0 : acc;
+    acc = ul > 1 ? acc + c1 : acc;
+    const bool lng = ll > 2 || ul > 2;
+    if (lane_on && !lng) __builtin_nontemporal_store(acc, m + static_cast<size_t>(row0 + r) * atoms + lane);
+    const unsigned long long jm = __ballot(lng);
+    if (jm != 0ull) {
+      const int before = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(jm >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(jm), 0u));
+      if (lng) s_job[w][njob + before] = static_cast<uint16_t>((r << 6) | lane);
+      njob += __popcll(jm);
     }
-    wave_lds_order();
-    if (lane_on) {
-      const int2 lr = s_lr[w][lane], ur = s_ur[w][lane];
-      float acc = run_sum(&s_lo[w][0], lr.x, lr.y, 0.f);
-      acc = run_sum(&s_up[w][0], ur.x, ur.y, acc);
-      m[static_cast<size_t>(b) * atoms + lane] = acc;
+  }
+  if (njob == 0) return;   // wave-uniform
+  wave_lds_order();
+  // (4) the long runs, one (row, target) per lane, each summed in order
+  for (int j0 = 0; j0 < njob; j0 += kWave) {
+    if (j0 + lane < njob) {
+      const int job = s_job[w][j0 + lane];
+      const int r = job >> 6, k = job & 63;
+      const uint32_t q = s_rb[w][r][k];
+      float acc = run_sum(&s_lo[w][r][0], q & 255u, (q >> 8) & 255u, 0.f);
+      acc = run_sum(&s_up[w][r][0], (q >> 16) & 255u, q >> 24, acc);
+      __builtin_nontemporal_store(acc, m + static_cast<size_t>(row0 + r) * atoms + k);
     }
-    wave_lds_order();
   }
 }
 
@@ -353,16 +418,18 @@ extern "C" int asvrl_c51_project(const float* pns_a, const float* returns, const
   ASVRL_REQUIRE(pns_a && returns && nonterminal && support && m, "asvrl_c51_project: null argument");
   ASVRL_REQUIRE(atoms >= 2 && atoms <= kWave, "asvrl_c51_project: atoms must be in [2, 64]");
   if (B <= 0) return 0;
-  // rows per wave: one below 4096 rows (latency: every row its own wave), else four (their loads in flight
-  // together, two or more waves per SIMD from B = 8192)
-  if (B < 4096) {
-    hipLaunchKernelGGL(c51_kernel<1>, dim3((B + kC51Waves - 1) / kC51Waves), dim3(kC51Waves * kWave), 0,
+  // rows per wave: one below 4096 rows (latency: every row its own wave), two below 32768, else
+  // ASVRL_C51_ROWS (their loads in flight together, their long runs walked side by side)
+  auto go = [&](auto kern, int rows) {
+    hipLaunchKernelGGL(kern, dim3((B + kC51Waves * rows - 1) / (kC51Waves * rows)), dim3(kC51Waves * kWave), 0,
                        as_stream(stream), pns_a, returns, nonterminal, support, B, atoms, vmin, vmax, delta_z, gamma_n, m);
-  } else {
-    constexpr int R = 4;
-    hipLaunchKernelGGL(c51_kernel<R>, dim3((B + kC51Waves * R - 1) / (kC51Waves * R)), dim3(kC51Waves * kWave), 0,
-                       as_stream(stream), pns_a, returns, nonterminal, support, B, atoms, vmin, vmax, delta_z, gamma_n, m);
-  }
+  };
+  if (B < 4096)
+    go(c51_kernel<1>, 1);
+  else if (B < 32768)
+    go(c51_kernel<2>, 2);
+  else
+    go(c51_kernel<ASVRL_C51_ROWS>, ASVRL_C51_ROWS);
   return check_launch("asvrl_c51_project");
 }
 

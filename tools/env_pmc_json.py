@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
-"""profiles/r02_env_pmc.json from two tools/pmc_env.sh runs (tools/pmc_summary.py --json outputs):
+"""profiles/rNN_env_pmc.json from two tools/pmc_env.sh runs (tools/pmc_summary.py --json outputs):
 the env step at 4096 envs (bench config 2's shape, env_pairs_kernel<256, 2>) and at 2^18 envs (the
 plateau shape, env_pairs_kernel<64, 2>). Per-launch means; f64_flop = 64 lanes x (ADD + MUL + TRANS +
 2 FMA) FP64 wave instructions (an upper bound: every lane counted active).
 
-    python tools/env_pmc_json.py /tmp/e4096.json /tmp/e262k.json profiles/r02_env_pmc.json
+    python tools/env_pmc_json.py /tmp/e4096.json /tmp/e262k.json profiles/r04_env_pmc.json
 """
 import json
 import sys
