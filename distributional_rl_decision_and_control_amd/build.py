@@ -20,6 +20,7 @@ SOURCES = [os.path.join(HERE, "csrc", f) for f in ("asvrl_env.hip", "asvrl_learn
                                                              "asvrl_per.hip", "asvrl_rainbow.hip", "asvrl_rainbow_net.hip")]
 HEADERS = [os.path.join(HERE, "csrc", "asvrl_common.h"), os.path.join(HERE, "csrc", "asvrl_mfma.h"),
            os.path.join(HERE, "csrc", "asvrl_lds.h"), os.path.join(HERE, "csrc", "asvrl_vonmises_k1.h"),
+           os.path.join(HERE, "csrc", "asvrl_critic_tile.h"),
            os.path.join(ROOT, "include", "asvrl.h")]
 OUT = os.path.join(HERE, "lib", "libasvrl.so")
 OUT_F32 = os.path.join(HERE, "lib", "libasvrl_f32.so")

@@ -36,6 +36,7 @@
 #include "asvrl_common.h"
 #include "asvrl_mfma.h"
 #include "asvrl_lds.h"
+#include "asvrl_critic_tile.h"   // before the contraction pragma: the target critic's forward as asvrl_critic.hip's
 
 // FMA contraction of this file's f32 epilogue arithmetic (the loss terms, the output layer's and the encoders'
 // gradient sums, the Bellman target): one v_fma_f32 where the source writes a * b + c (the library is built
@@ -182,6 +183,7 @@ struct FusedArgs {
   const float* iwo;   // IQN: output_layer.weight [A][128], bias [A] (f32)
   const float* ibo;
   int n_actions;
+  ctile::CriticArgs tq;   // asvrl_critic_train_fused_tq: the target critic's forward (MODE_FWD), q -> qn
 };
 
 constexpr int kObsIn = 37;   // self 7 | objects 25 | mask 5 of the packed observation row
@@ -463,14 +465,145 @@ __device__ __forceinline__ void mfma_grid(AF af, BF bf, MF mf) {
   }
 }
 
-template <int NT, bool IQN>
+// The target critic's forward in the update's own launch (asvrl_critic_train_fused_tq): before its first
+// round, each workgroup computes q_next for exactly the samples its rounds update -- round t's rows are
+// tiles t NB .. t NB + NB - 1 -- with asvrl_critic.hip's FWD tile (critic_tile<MODE_FWD>: the same code and
+// arithmetic, bit-identical q_next), the target weights staged in the LDS the rounds use afterwards, then
+// stores them where the rounds' input fetch reads q_next (global, workgroup-coherent after the barrier).
+// No workgroup waits on another: the samples of different workgroups are disjoint.
+template <int NT, bool TQ> struct TqLds { float pad[4]; };
+// N = 32 (a tile = one sample): the workgroup's samples are staged 16 at a time by all its threads together
+// (F, G and the taus of the chunk's tiles), so the tiles then run without a global load
+constexpr int kTqChunk = 16;
+template <int NT> struct TqLds<NT, true> {
+  static constexpr int kF = NT == 32 ? kTqChunk * kC : kNW * (32 / NT) * kC;
+  static constexpr int kG = NT == 32 ? kTqChunk * kH : kNW * (32 / NT) * kH;
+  ctile::CriticLds W;
+  float F[kF];
+  float G[kG];
+  float T[NT == 32 ? kTqChunk * 32 : 4];
+};
+template <int NT, int NB, int S, bool IQN, int NSB, bool TQ>
+union FusedShared {
+  FusedLds<NT, NB, S, IQN, NSB> f;
+  TqLds<NT, TQ> t;
+};
+
+// F, G (asvrl_critic_tile.h stage_features' arithmetic, op for op, uncontracted) and the taus of n <= 16
+// samples b(0..n-1): thread m computes feature m of every sample from its weights loaded once
+template <class BF>
+__device__ __forceinline__ void tq_stage_chunk(const ctile::CriticArgs& t, int n, BF bidx, float* F, float* G,
+                                               float* T) {
+#pragma clang fp contract(off)
+  const int m = threadIdx.x;   // kNW * 64 == kC threads: one feature each
+  static_assert(kNW * 64 == kC, "one thread per feature");
+  const bool self = m < ctile::kSelfF;
+  const int o = self ? 0 : (m - ctile::kSelfF) / ctile::kObjF, j = self ? 0 : (m - ctile::kSelfF) % ctile::kObjF;
+  const float* wp = self ? t.w.self_w + m * ctile::kSelfIn : t.w.obj_w + j * ctile::kObjIn;
+  float w[ctile::kSelfIn];
+#pragma unroll
+  for (int i = 0; i < ctile::kSelfIn; ++i) w[i] = wp[(i < ctile::kObjIn || self) ? i : 0];
+  const float bb = self ? t.w.self_b[m] : t.w.obj_b[j];
+  const int xo = self ? 0 : ctile::kSelfIn + ctile::kObjIn * o;
+  float ae0 = 0.f, ae1 = 0.f, aeb = 0.f;
+  if (m < kH) {
+    ae0 = t.w.ae_w[2 * m];
+    ae1 = t.w.ae_w[2 * m + 1];
+    aeb = t.w.ae_b[m];
+  }
+  constexpr int kSub = 8;   // samples whose loads are in flight together (register budget)
+  for (int k0 = 0; k0 < n; k0 += kSub) {
+    float xs[kSub][ctile::kSelfIn], mk[kSub], a0[kSub], a1[kSub], tv[kSub];
+#pragma unroll
+    for (int q = 0; q < kSub; ++q) {   // every load of the batch issued before the first use
+      const int k = k0 + q;
+      const int b = k < n ? bidx(k) : bidx(k0);
+      const float* x = t.obs + static_cast<int64_t>(b) * t.ld_obs;
+#pragma unroll
+      for (int i = 0; i < ctile::kSelfIn; ++i) xs[q][i] = x[xo + ((i < ctile::kObjIn || self) ? i : 0)];
+      mk[q] = self ? 1.f : x[ctile::kObsMask + o];
+      a0[q] = t.ain[static_cast<int64_t>(b) * t.ld_ain];
+      a1[q] = t.ain[static_cast<int64_t>(b) * t.ld_ain + 1];
+      tv[q] = t.taus[static_cast<int64_t>(b) * 32 + (m & 31)];   // NT = 32: tile b's rows
+    }
+#pragma unroll
+    for (int q = 0; q < kSub; ++q) {
+      const int k = k0 + q;
+      if (k >= n) break;
+      float d = 0.f;
+#pragma unroll
+      for (int i = 0; i < ctile::kSelfIn; ++i)
+        if (i < ctile::kObjIn || self) d += w[i] * xs[q][i];
+      const float v = mk[q] < 0.5f ? 0.f : relu(d + bb);   // masked_fill(mask < 0.5, 0)
+      F[k * kC + m] = static_cast<float>((elem_t)v);
+      if (m < kH) G[k * kH + m] = relu((ae0 * a0[q] + ae1 * a1[q]) + aeb);
+      if (m < 32) T[k * 32 + m] = tv[q];
+    }
+  }
+}
+
+template <int NT, int NB>
+__device__ __forceinline__ void target_phase(const ctile::CriticArgs& t, TqLds<NT, true>& T, int rounds) {
+  constexpr int St = 32 / NT;
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if constexpr (kWeightsInLds) {
+    copy_frags<kNW * 64, ctile::kFragWC, 16>(T.W.wc, reinterpret_cast<const frag8*>(t.w.wc_frag), threadIdx.x);
+    copy_frags<kNW * 64, ctile::kFragW1, 16>(T.W.w1, reinterpret_cast<const frag8*>(t.w.w1_frag), threadIdx.x);
+    copy_frags<kNW * 64, ctile::kFragW2, 16>(T.W.w2, reinterpret_cast<const frag8*>(t.w.w2_frag), threadIdx.x);
+  }
+  for (int i = threadIdx.x; i < kC; i += kNW * 64) T.W.bc[i] = t.w.bc[i];
+  for (int i = threadIdx.x; i < kH; i += kNW * 64) {
+    T.W.b1[i] = t.w.b1[i];
+    T.W.b2[i] = t.w.b2[i];
+    T.W.wo[i] = t.w.wo[i];
+  }
+  const int mine = (rounds - static_cast<int>(blockIdx.x) + static_cast<int>(gridDim.x) - 1) / static_cast<int>(gridDim.x) * NB;
+  auto tile_of = [&](int i) { return (static_cast<int>(blockIdx.x) + (i / NB) * static_cast<int>(gridDim.x)) * NB + i % NB; };
+  if constexpr (NT == 32) {
+#pragma nounroll
+    for (int c0 = 0; c0 < mine; c0 += kTqChunk) {   // workgroup-uniform
+      const int n = mine - c0 < kTqChunk ? mine - c0 : kTqChunk;
+      tq_stage_chunk(t, n, [&](int k) { return tile_of(c0 + k); }, T.F, T.G, T.T);
+      __syncthreads();
+#pragma nounroll
+      for (int k = wv; k < n; k += kNW)
+      {
+        int kk = k;   // opaque VGPR copy: with a uniform k the tile's LDS addresses are hoisted and spill (573)
+        asm volatile("" : "+v"(kk));
+        ctile::critic_tile<ctile::MODE_FWD, NT>(t, T.W, tile_of(c0 + kk), lane, T.F + kk * kC, T.G + kk * kH, nullptr,
+                                                T.T + kk * 32);
+      }
+      __syncthreads();
+    }
+  } else {
+    __syncthreads();
+    float* Fw = T.F + wv * St * kC;
+    float* Gw = T.G + wv * St * kH;
+    for (int i = wv; i < mine; i += kNW) {
+      const int tile = tile_of(i);
+      ctile::stage_features<NT, true, false>(t, tile, lane, Fw, Gw);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // the wave's own rows: in-order LDS, compiler fence
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      ctile::critic_tile<ctile::MODE_FWD, NT>(t, T.W, tile, lane, Fw, Gw);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    __syncthreads();   // every q_next of the workgroup stored; the LDS is the update's from here
+  }
+}
+
+template <int NT, bool IQN, bool TQ = false>
 __global__ __launch_bounds__(kNW * 64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void critic_fused_kernel(FusedArgs a) {
   constexpr int NB = FusedNB<NT>::v, G = 32 * NB, S = G / NT, NA = IQN ? 1 : 2;
   constexpr bool AH = ASVRL_STAGE_AHEAD && (!IQN || ASVRL_STAGE_AHEAD_IQN) && NT == 32 && !ASVRL_OPERAND_F32;
   constexpr int NSB = AH ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) FusedLds<NT, NB, S, IQN, NSB> L;
-  static_assert(sizeof(L) <= 160 * 1024, "fused critic LDS image exceeds the CU's 160 KB");
+  __shared__ __attribute__((aligned(16))) FusedShared<NT, NB, S, IQN, NSB, TQ> U;
+  static_assert(sizeof(U) <= 160 * 1024, "fused critic LDS image exceeds the CU's 160 KB");
+  auto& L = U.f;
+  if constexpr (TQ) target_phase<NT, NB>(a.tq, U.t, a.rounds);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
   const frag8* WC = reinterpret_cast<const frag8*>(a.w.wc_frag);
   const frag8* W1 = reinterpret_cast<const frag8*>(a.w.w1_frag);
@@ -1357,8 +1490,9 @@ extern "C" int32_t asvrl_critic_fused_groups(int32_t B, int32_t N) {
   return rounds < cus ? rounds : cus;
 }
 
-extern "C" int asvrl_critic_train_fused(const AsvCriticWeights* w, const AsvCriticIO* io, const AsvCriticParts* parts,
-                                        void* stream) {
+namespace {
+int critic_train_fused_launch(const AsvCriticWeights* w, const AsvCriticIO* io, const AsvCriticParts* parts,
+                              const AsvCriticWeights* tw, const AsvCriticIO* tio, void* stream) {
   ASVRL_REQUIRE(w && io && parts, "asvrl_critic_train_fused: null argument");
   ASVRL_REQUIRE(io->taus && io->obs && io->act && io->q_next && io->rewards && io->dones,
                 "asvrl_critic_train_fused: needs taus, obs, act, q_next, rewards and dones");
@@ -1373,6 +1507,16 @@ extern "C" int asvrl_critic_train_fused(const AsvCriticWeights* w, const AsvCrit
   ASVRL_REQUIRE(io->kappa > 0.f, "asvrl_critic_train_fused: kappa must be positive");
   ASVRL_REQUIRE(io->B >= 0 && (static_cast<int64_t>(io->B) * io->N) % (32 * fused_nb(io->N)) == 0,
                 "asvrl_critic_train_fused: B*N must be a multiple of the round size (64 rows; 32 in the f32 build)");
+  const bool tq = tw != nullptr;
+  if (tq) {
+    ASVRL_REQUIRE(tio != nullptr, "asvrl_critic_train_fused_tq: null target IO");
+    ASVRL_REQUIRE(tw->wc_frag && tw->w1_frag && tw->w2_frag && tw->bc && tw->b1 && tw->b2 && tw->wo && tw->bo &&
+                      tw->self_w && tw->self_b && tw->obj_w && tw->obj_b && tw->ae_w && tw->ae_b,
+                  "asvrl_critic_train_fused_tq: null target weight");
+    ASVRL_REQUIRE(tio->taus && tio->obs && tio->act, "asvrl_critic_train_fused_tq: the target pass needs taus, obs and act");
+    ASVRL_REQUIRE(tio->ld_obs >= 37, "asvrl_critic_train_fused_tq: target ld_obs must cover the packed observation row");
+    ASVRL_REQUIRE(tio->B == io->B && tio->N == io->N, "asvrl_critic_train_fused_tq: target B / N differ from the update's");
+  }
   if (io->B == 0) return 0;
   FusedArgs a{};
   a.w = *w;
@@ -1386,12 +1530,36 @@ extern "C" int asvrl_critic_train_fused(const AsvCriticWeights* w, const AsvCrit
   a.q = io->q; a.row_loss = io->row_loss; a.tile_loss = io->tile_loss;
   a.dzF = io->dzF; a.dzG = io->dzG;
   a.parts = *parts;
+  if (tq) {
+    a.tq = ctile::make_args(tw, tio);
+    a.tq.F = nullptr;
+    a.tq.G = nullptr;
+    a.tq.q = const_cast<float*>(io->q_next);   // written here, read by the rounds
+  }
   const int grid = asvrl_critic_fused_groups(io->B, io->N);
   hipStream_t st = as_stream(stream);
+  if (tq) {
+    if (io->N == 32) hipLaunchKernelGGL((critic_fused_kernel<32, false, true>), dim3(grid), dim3(kNW * 64), 0, st, a);
+    else if (io->N == 16) hipLaunchKernelGGL((critic_fused_kernel<16, false, true>), dim3(grid), dim3(kNW * 64), 0, st, a);
+    else hipLaunchKernelGGL((critic_fused_kernel<8, false, true>), dim3(grid), dim3(kNW * 64), 0, st, a);
+    return check_launch("asvrl_critic_train_fused_tq");
+  }
   if (io->N == 32) hipLaunchKernelGGL((critic_fused_kernel<32, false>), dim3(grid), dim3(kNW * 64), 0, st, a);
   else if (io->N == 16) hipLaunchKernelGGL((critic_fused_kernel<16, false>), dim3(grid), dim3(kNW * 64), 0, st, a);
   else hipLaunchKernelGGL((critic_fused_kernel<8, false>), dim3(grid), dim3(kNW * 64), 0, st, a);
   return check_launch("asvrl_critic_train_fused");
+}
+}  // namespace
+
+extern "C" int asvrl_critic_train_fused(const AsvCriticWeights* w, const AsvCriticIO* io, const AsvCriticParts* parts,
+                                        void* stream) {
+  return critic_train_fused_launch(w, io, parts, nullptr, nullptr, stream);
+}
+
+extern "C" int asvrl_critic_train_fused_tq(const AsvCriticWeights* w, const AsvCriticIO* io, const AsvCriticParts* parts,
+                                           const AsvCriticWeights* tw, const AsvCriticIO* tio, void* stream) {
+  ASVRL_REQUIRE(tw != nullptr, "asvrl_critic_train_fused_tq: null target weights");
+  return critic_train_fused_launch(w, io, parts, tw, tio, stream);
 }
 
 // train_IQN's update (agent.py:449-468) in one launch: the same kernel with IQN_Policy's trunk (no action

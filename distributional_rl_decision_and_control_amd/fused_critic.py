@@ -215,14 +215,18 @@ def fused_train_supported(pack, B, N):
 
 
 def critic_train_fused(pack, critic, taus, N, q_next, rewards, dones, gamma, obs, act, arena, dzF=None, dzG=None,
-                       xb=None, tile_loss=None, kappa=1.0, q=None, row_loss=None, stream=None, encoders=False):
+                       xb=None, tile_loss=None, kappa=1.0, q=None, row_loss=None, stream=None, encoders=False,
+                       target=None):
     """asvrl_critic_train_fused: the critic step's forward, quantile-Huber loss against
     r + gamma q_next (1 - d), backward AND the trunk's weight gradients in one launch. The per-workgroup
     partials land in `arena` (PartialArena) as segments of critic's cos_embedding / hidden_layer /
     hidden_layer_2 / output_layer .grad (reduced by the arena's next flush).
     encoders=True: the launch also forms the observation / action encoders' gradients (ABI 16
     parts.enc / parts.aenc) as segments of their .grad, which must be contiguous
-    [self_w | self_b | obj_w | obj_b] (FusedAdam); dzF / dzG / xb are then not needed."""
+    [self_w | self_b | obj_w | obj_b] (FusedAdam); dzF / dzG / xb are then not needed.
+    target=(target_pack, taus', obs', act'): asvrl_critic_train_fused_tq (ABI 20) -- the same launch first
+    computes q_next = target_critic(obs', act', taus') for the samples each workgroup updates (the values
+    critic_forward(target_pack, ...) gives) into `q_next`, then the update reads it."""
     B = obs.shape[0]
     groups = fused_groups(pack, B, N)
     assert groups > 0 and fused_train_supported(pack, B, N), (B, N)
@@ -241,8 +245,16 @@ def critic_train_fused(pack, critic, taus, N, q_next, rewards, dones, gamma, obs
     io = _io(None, None, taus, N, obs=obs, act=act, xb=xb, Np=N, kappa=float(kappa), q_next=q_next,
              rewards=rewards, dones=dones, ld_rd=rewards.stride(0), gamma=float(gamma), q=q, row_loss=row_loss,
              dzF=dzF, dzG=dzG, tile_loss=tile_loss, loss_scale=1.0 / float(B * N))
-    _abi.check(pack.L.asvrl_critic_train_fused(C.byref(pack.struct), C.byref(io), C.byref(parts),
-                                               _abi.stream_ptr(stream)), "asvrl_critic_train_fused", pack.L)
+    if target is None:
+        _abi.check(pack.L.asvrl_critic_train_fused(C.byref(pack.struct), C.byref(io), C.byref(parts),
+                                                   _abi.stream_ptr(stream)), "asvrl_critic_train_fused", pack.L)
+    else:
+        tpack, ttaus, tobs, tact = target
+        assert q_next.is_contiguous() and q_next.dtype == torch.float32
+        tio = _io(None, None, ttaus, N, obs=tobs, act=tact)
+        _abi.check(pack.L.asvrl_critic_train_fused_tq(C.byref(pack.struct), C.byref(io), C.byref(parts),
+                                                      C.byref(tpack.struct), C.byref(tio), _abi.stream_ptr(stream)),
+                   "asvrl_critic_train_fused_tq", pack.L)
     for (layer, M, K), part in zip(shapes, regions):
         arena.groups(part, groups, M, K, layer.weight.grad, layer.bias.grad)
     if encoders:

@@ -6,7 +6,9 @@ Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | 
   actor(s) saving activations -> a (for the actor step)  asvrl_actor_forward(TRAIN)
   critic (agent.py:395-416)
     target actor(ns) -> na                               asvrl_actor_forward(FWD)
-    target encoders(ns, na) + trunk -> q_next            asvrl_critic_forward (encoders in the prologue)
+    target encoders(ns, na) + trunk -> q_next            asvrl_critic_forward (encoders in the prologue);
+                                                          (or inside the next launch: TARGET_IN_FUSED, ABI 20,
+                                                          measured slower, off)
     local encoders(s, a), trunk forward, quantile-Huber vs r + g q_next (1-d), backward AND the
     four trunk layers' weight-gradient partials          asvrl_critic_train_fused (ONE launch)
     and the observation / action encoders' gradient partials (ABI 16; ENC_IN_KERNEL = False: from
@@ -46,6 +48,12 @@ OBS = 40
 # step, profiles/r02_enc_ab.txt); False keeps the earlier form (per-sample dzF / dzG + a batched launch)
 # for the kernel tests that compare the two
 ENC_IN_KERNEL = True
+# the target critic's forward inside the fused critic launch (ABI 20, asvrl_critic_train_fused_tq: each
+# workgroup computes q_next for the samples it updates, bit-identical to the separate asvrl_critic_forward).
+# Off: the launch grows 111 -> 147-149 us (the FWD tiles at one wave per SIMD: 35 us against 26 us for the
+# separate launch alone) and the rollout's env step then waits for CUs beside it; bench step 0.2649 vs 0.2629
+# ms (profiles/r04t_target_in_fused_ab.txt, r04r_tq_step_window.txt)
+TARGET_IN_FUSED = False
 
 
 def supported(policy, B, N):
@@ -182,7 +190,12 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     q_next = st.q_next
     if target_wait is not None:
         torch.cuda.current_stream().wait_event(target_wait)
-    if prologue_done:   # only the target critic is left of the target chain
+    # the target critic's forward inside the update's launch (each workgroup for its own samples): one
+    # launch fewer on the learner chain
+    target_in = TARGET_IN_FUSED and prologue_done and ENC_IN_KERNEL
+    if target_in:
+        pass
+    elif prologue_done:   # only the target critic is left of the target chain
         critic_forward(st.target_trunk, None, None, taus[0], st.N, q=q_next, obs=rows[:, OBS:2 * OBS], act=st.na)
     else:
         actor_train_forward(st.actor, s_rows, ab)   # reads only s and the (not yet updated) actor
@@ -192,7 +205,8 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     # encoders in one launch (supported() guarantees its shape: B a multiple of 32, so B*N of 64)
     if ENC_IN_KERNEL:
         critic_train_fused(st.local_trunk, critic, taus[1], N, q_next.view(B, N), r_col, d_col, gamma, s_rows,
-                           a_rows, arena, tile_loss=st.tile_loss[0], encoders=True)
+                           a_rows, arena, tile_loss=st.tile_loss[0], encoders=True,
+                           target=(st.target_trunk, taus[0], rows[:, OBS:2 * OBS], st.na) if target_in else None)
     else:
         critic_train_fused(st.local_trunk, critic, taus[1], N, q_next.view(B, N), r_col, d_col, gamma, s_rows,
                            a_rows, arena, dzF=st.dzF, dzG=st.dzG, xb=st.xb, tile_loss=st.tile_loss[0])

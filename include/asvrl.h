@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 19
+#define ASVRL_ABI_VERSION 20
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -345,6 +345,14 @@ int32_t asvrl_critic_fused_groups(int32_t B, int32_t N);
  * B*N a multiple of the round size. No activation goes to HBM. */
 int asvrl_critic_train_fused(const AsvCriticWeights* w, const AsvCriticIO* io, const AsvCriticParts* parts,
                              void* stream);
+
+/* asvrl_critic_train_fused with the target critic's forward in the same launch (ABI 20; replaces the
+ * separate asvrl_critic_forward(target) of train_AC_IQN, agent.py:396-400): each workgroup first computes
+ * q_next = Critic_target(tio->obs, tio->act, tio->taus) (AC_IQN_model.py:462-480) for exactly the samples
+ * its rounds update -- the values asvrl_critic_forward(tw, tio) gives, bit for bit -- into io->q_next,
+ * then runs the update reading them. tw: the target critic (with its encoders); tio: B and N as io. */
+int asvrl_critic_train_fused_tq(const AsvCriticWeights* w, const AsvCriticIO* io, const AsvCriticParts* parts,
+                                const AsvCriticWeights* tw, const AsvCriticIO* tio, void* stream);
 
 /* Actor update's critic pass (agent.py:419-425): forward, then the backward of
  * sum_rows dq * q to G (dG) and through the action encoder to the action (dA). */

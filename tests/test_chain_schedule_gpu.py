@@ -67,3 +67,19 @@ def test_chained_schedule_bench_shape_after_pool_wrap():
     assert torch.isfinite(la).all()
     assert torch.equal(la, lb), (la, lb)
     assert torch.equal(pa, pb), float((pa - pb).abs().max())
+
+
+def test_target_critic_in_fused_launch_matches_separate(monkeypatch):
+    """fused_update.TARGET_IN_FUSED (ABI 20): the loop with the target critic's forward inside the fused
+    critic launch against the same loop with the separate asvrl_critic_forward launch -- the same values in
+    the same order, so the chained loop's weights, losses, env and replay state agree bit for bit."""
+    from distributional_rl_decision_and_control_amd import fused_update
+    monkeypatch.setattr(fused_update, "TARGET_IN_FUSED", True)
+    a, pa, la = _run("AC-IQN", True, 8)
+    monkeypatch.setattr(fused_update, "TARGET_IN_FUSED", False)
+    b, pb, lb = _run("AC-IQN", True, 8)
+    assert torch.isfinite(la).all()
+    assert torch.equal(la, lb), (la, lb)
+    assert torch.equal(pa, pb), float((pa - pb).abs().max())
+    assert torch.equal(a.env.batch.rs, b.env.batch.rs)
+    assert torch.equal(a.replay.ring, b.replay.ring)

@@ -31,10 +31,12 @@ def _batch(B, seed):
     return rows, torch.rand(2, B, 0 + 1, generator=g, device="cuda")
 
 
-def _critic_grads(ops, B, N, fused, rows, taus, seed=100, enc=False):
+def _critic_grads(ops, B, N, fused, rows, taus, seed=100, enc=False, tq=False, out=None):
     """The critic step's gradients (every critic .grad, reduced) and loss, without the optimizer.
     enc: the encoders' gradients formed inside the fused launch (parts.enc / parts.aenc) instead of
-    the batched weight-gradient launch over dzF / dzG."""
+    the batched weight-gradient launch over dzF / dzG. tq: the target critic's forward inside the same
+    launch (asvrl_critic_train_fused_tq) instead of asvrl_critic_forward (q_next poisoned with NaN
+    before the launch); out["q_next"] receives the q_next the update read."""
     from distributional_rl_decision_and_control_amd.agent import Agent
     from distributional_rl_decision_and_control_amd.fused_critic import (TrainBuffers, critic_train, critic_train_fused,
                                                                           wout_groups)
@@ -51,7 +53,12 @@ def _critic_grads(ops, B, N, fused, rows, taus, seed=100, enc=False):
     co.grads.zero_()
     target_q(st, rows, taus[0], st.q_next, st.na)
     ae = critic.action_encoder[0]
-    if fused and enc:
+    if tq:
+        st.q_next.fill_(float("nan"))
+        critic_train_fused(st.local_trunk, critic, taus[1], N, st.q_next.view(B, N), r_col, d_col, 0.99, s_rows,
+                           a_rows, arena, tile_loss=st.tile_loss[0], encoders=True,
+                           target=(st.target_trunk, taus[0], rows[:, 40:80], st.na))
+    elif fused and enc:
         critic_train_fused(st.local_trunk, critic, taus[1], N, st.q_next.view(B, N), r_col, d_col, 0.99, s_rows,
                            a_rows, arena, tile_loss=st.tile_loss[0], encoders=True)
     elif fused:
@@ -78,6 +85,8 @@ def _critic_grads(ops, B, N, fused, rows, taus, seed=100, enc=False):
     arena.scalar(st.tile_loss[0], st.losses[0:1])
     arena.flush()
     torch.cuda.synchronize()
+    if out is not None:
+        out["q_next"] = st.q_next.detach().cpu().numpy().copy()
     grads = {n: p.grad.detach().cpu().numpy().astype(np.float64).copy() for n, p in critic.named_parameters()}
     return grads, float(st.losses[0].item())
 
@@ -193,3 +202,24 @@ def test_fused_encoder_grads_in_kernel(ops, B, N):
     g2, _ = _critic_grads(ops, B, N, True, rows, taus, enc=True)
     for n in enc_names:
         np.testing.assert_array_equal(ge[n], g2[n], err_msg=n)
+
+
+@pytest.mark.parametrize("ops,B,N", [("f32", 64, 8), ("f32", 64, 32), ("f32", 256, 16),
+                                     ("bf16", 64, 8), ("bf16", 128, 16), ("bf16", 608, 32), ("bf16", 4096, 32)])
+def test_fused_train_with_target_critic_in_launch(ops, B, N):
+    """asvrl_critic_train_fused_tq (ABI 20): each workgroup computes q_next = target_critic(s', a', tau') for
+    the samples its rounds update (asvrl_critic.hip's FWD tile, compiled into the fused launch ahead of the
+    contraction pragma), then runs the update. Against asvrl_critic_forward followed by the plain fused launch:
+    q_next bit-identical (every sample: 608 x 32 gives 304 rounds over 256 workgroups, uneven), and so every
+    gradient and the loss bit-identical too."""
+    rows, _ = _batch(B, 21 + N)
+    g = torch.Generator(device="cuda").manual_seed(27 + B)
+    taus = torch.rand(2, B, N, generator=g, device="cuda")
+    o1, o2 = {}, {}
+    g1, l1 = _critic_grads(ops, B, N, True, rows, taus, enc=True, out=o1)
+    g2, l2 = _critic_grads(ops, B, N, True, rows, taus, enc=True, tq=True, out=o2)
+    assert np.isfinite(o2["q_next"]).all()
+    np.testing.assert_array_equal(o2["q_next"], o1["q_next"])
+    assert l1 == l2
+    for n in g1:
+        np.testing.assert_array_equal(g2[n], g1[n], err_msg=n)

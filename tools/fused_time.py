@@ -21,9 +21,12 @@ def main():
     ap.add_argument("--N", type=int, default=32)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--mode", default="fused", choices=["fused", "tq", "target"],
+                    help="fused: the update launch; tq: the update with the target critic inside "
+                         "(asvrl_critic_train_fused_tq); target: the separate target critic launch alone")
     a = ap.parse_args()
     from distributional_rl_decision_and_control_amd.agent import Agent
-    from distributional_rl_decision_and_control_amd.fused_critic import critic_train_fused
+    from distributional_rl_decision_and_control_amd.fused_critic import critic_forward, critic_train_fused
     from distributional_rl_decision_and_control_amd.fused_update import FusedACIQNState, target_q
     from distributional_rl_decision_and_control_amd.learner import FusedAdam
     from tests.test_critic_fused_gpu import _batch
@@ -40,9 +43,13 @@ def main():
     target_q(st, rows, taus[0], st.q_next, st.na)
 
     def launch():
+        if a.mode == "target":
+            critic_forward(st.target_trunk, None, None, taus[0], N, q=st.q_next, obs=rows[:, 40:80], act=st.na)
+            return
         arena.off, arena.segs = 0, []
         critic_train_fused(st.local_trunk, critic, taus[1], N, st.q_next.view(B, N), r_col, d_col, 0.99, s_rows,
-                           a_rows, arena, dzF=st.dzF, dzG=st.dzG, xb=st.xb, tile_loss=st.tile_loss[0])
+                           a_rows, arena, tile_loss=st.tile_loss[0], encoders=True,
+                           target=(st.target_trunk, taus[0], rows[:, 40:80], st.na) if a.mode == "tq" else None)
 
     for _ in range(5):
         launch()
@@ -57,7 +64,7 @@ def main():
         e1.synchronize()
         us.append(e0.elapsed_time(e1) * 1000.0 / a.iters)
     us.sort()
-    print(json.dumps({"lib": os.environ.get("ASVRL_LIB", "default"), "us_median": round(us[len(us) // 2], 2),
+    print(json.dumps({"lib": os.environ.get("ASVRL_LIB", "default"), "mode": a.mode, "us_median": round(us[len(us) // 2], 2),
                       "us_min": round(us[0], 2), "us_all": [round(u, 1) for u in us]}))
 
 
