@@ -64,6 +64,39 @@ def test_fused_forward(B, N):
     assert err < 2e-2, err
 
 
+@pytest.mark.parametrize("B", [1, 37, 4096])
+def test_forward_launch_matches_in_launch_target_pass(B):
+    """asvrl_critic_forward (critic_kernel<FWD>) against the fused launch's in-launch target pass
+    (asvrl_critic_train_fused_tq, the same FWD tile compiled into the other file, its q_next written for the
+    fused shape's rows): every row bit-identical, B = 1 and 37 (a partial launch) and 4096. (Round 4 also
+    measured a two-tiles-per-wave FWD kernel, one wave per SIMD, against this one: 36 vs 26 us, dropped,
+    profiles/r04u_fwd_two_tiles_ab.txt.)"""
+    from distributional_rl_decision_and_control_amd.agent import Agent
+    from distributional_rl_decision_and_control_amd.fused_update import FusedACIQNState, target_q
+    from distributional_rl_decision_and_control_amd.fused_critic import critic_forward
+    from tests.test_critic_fused_gpu import _batch
+    Bp = max(64, -(-B // 64) * 64)   # the fused launch's shape; the forward alone runs on the first B rows
+    rows, _ = _batch(Bp, 9)
+    taus = torch.rand(Bp, 32, generator=torch.Generator(device="cuda").manual_seed(B), device="cuda")
+    from distributional_rl_decision_and_control_amd.learner import FusedAdam
+    ag = Agent(seed=3, agent_type="AC-IQN")
+    FusedAdam(ag.policy_local.actor.parameters(), lr=1e-4)
+    FusedAdam(ag.policy_local.critic.parameters(), lr=1e-4)   # contiguous .grad (the fused launch's encoders)
+    st = FusedACIQNState(ag.policy_local, ag.policy_target, Bp, 32)
+    target_q(st, rows, taus, st.q_next, st.na)   # the target actor's a' (and q_next by the two-tile kernel)
+    q2 = critic_forward(st.target_trunk, None, None, taus[:B].contiguous(), 32, obs=rows[:B, 40:80],
+                        act=st.na[:B])
+    # the one-tile code path: the fused launch's target pass
+    from distributional_rl_decision_and_control_amd.fused_critic import critic_train_fused
+    q1 = torch.full_like(st.q_next, float("nan"))
+    critic_train_fused(st.local_trunk, ag.policy_local.critic, taus, 32, q1.view(Bp, 32), rows[:, 82], rows[:, 83],
+                       0.99, rows[:, 0:40], rows[:, 80:82], st.arena, tile_loss=st.tile_loss[0], encoders=True,
+                       target=(st.target_trunk, taus, rows[:, 40:80], st.na))
+    torch.cuda.synchronize()
+    assert torch.isfinite(q2).all()
+    assert torch.equal(q2.reshape(-1), q1.view(Bp, 32)[:B].reshape(-1))
+
+
 @pytest.mark.parametrize("B,N", [(64, 8), (256, 16), (1024, 32)])
 def test_encoders_in_kernel_match_torch(B, N):
     """Observation rows + actions instead of F / G: the trunk kernels run the critic's encoders
