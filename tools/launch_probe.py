@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--trials", type=int, default=8)
     ap.add_argument("--warm-replays", type=int, default=2)
     ap.add_argument("--sequence", action="store_true", help="print every trial in order (no idle variants)")
+    ap.add_argument("--pre", default="none", choices=["none", "upload", "burn"],
+                    help="before the trials: hipGraphUpload of the captured graph, or ~100 ms of unrelated GPU work")
     a = ap.parse_args()
     from distributional_rl_decision_and_control_amd.vec_trainer import VecTrainer
     dev = torch.device("cuda", 0)
@@ -32,6 +34,20 @@ def main():
     torch.cuda.synchronize(dev)
     g = tr._graph
     stream = torch.cuda.current_stream(dev)
+    if a.pre == "upload":
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        rc = hip.hipGraphUpload(ctypes.c_void_p(g.raw_cuda_graph_exec()), ctypes.c_void_p(stream.cuda_stream))
+        torch.cuda.synchronize(dev)
+        print("hipGraphUpload rc", rc, flush=True)
+    elif a.pre == "burn":
+        x = torch.randn(4096, 4096, device=dev)
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 0.1:
+            for _ in range(10):
+                x = torch.tanh(x @ x * 1e-3)
+            torch.cuda.synchronize(dev)
+        del x
     for idle_ms in ((0.0,) if a.sequence else (0.0, 5.0)):
         walls, hosts, evs = [], [], []
         for _ in range(a.trials):
