@@ -12,4 +12,4 @@ R=$PWD
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${T}_prof -o run --output-format csv rocpd \
   -- python3 $R/bench.py --steps 10 --warmup 10 --iqn-steps 50 --no-cpu-baseline --rainbow-steps 0 --config5-steps 0 --plateau-envs 0 --no-learn-b64 \
   > $R/gpurun_out/${T}_prof.json 2> $R/gpurun_out/${T}_prof.err) || exit 3
-python tools/step_window.py gpurun_out/${T}_prof/run_results.db --anchor "critic_fused_kernel<32, true>" --at 0.8 > gpurun_out/${T}_step_window.txt 2>&1; head -30 gpurun_out/${T}_step_window.txt
+python tools/step_window.py gpurun_out/${T}_prof/run_results.db --anchor "critic_fused_kernel<32, true" --at 0.8 > gpurun_out/${T}_step_window.txt 2>&1; head -30 gpurun_out/${T}_step_window.txt
