@@ -108,6 +108,12 @@ constexpr int kC51Waves = 4;
 #ifndef ASVRL_C51_DUMMY
 #define ASVRL_C51_DUMMY 0
 #endif
+// the workgroup's long-run jobs pooled and walked by its first waves (1), or each wave its own (0): at
+// four rows per wave 16.8 -> 15.9 us at B = 65536; at two (B = 8192) 5.5 -> 5.9 us, so there each wave its own
+// (profiles/r04aa_c51_pool_ab.txt)
+#ifndef ASVRL_C51_POOL
+#define ASVRL_C51_POOL 1
+#endif
 
 // acc + v[j0] + v[j0+1] + ... + v[j1-1], added in order; the LDS reads go out 8 at a time
 __device__ __forceinline__ float run_sum(const float* v, int j0, int j1, float acc) {
@@ -143,16 +149,18 @@ __global__ __launch_bounds__(kC51Waves * kWave) void c51_kernel(const float* __r
                                                                 int atoms, float vmin, float vmax, float dz,
                                                                 float gamma_n, float* __restrict__ m) {
   // per wave and row: the lower / upper masses (a 65th slot for the second read of a run starting at lane
-  // 63) and per target its runs' bounds as bytes {lower start, lower end, upper start, upper end} (a 65th
-  // dummy slot for the lanes that bound no run); the long-run jobs (row << 6 | target)
+  // 63) and per target its runs' bounds as bytes {lower start, lower end, upper start, upper end}; the
+  // workgroup's long-run jobs ((wave * ROWS + row) << 6 | target), walked by the first waves after a barrier
+  // (kPool: ASVRL_C51_POOL at four rows per wave; else each wave walks its own)
   __shared__ float s_lo[kC51Waves][ROWS][kWave + 1], s_up[kC51Waves][ROWS][kWave + 1];
   __shared__ uint32_t s_rb[kC51Waves][ROWS][kWave + 1];
-  __shared__ uint16_t s_job[kC51Waves][ROWS * kWave];
+  __shared__ uint16_t s_job[kC51Waves * ROWS * kWave];
+  __shared__ int s_njob;
+  constexpr bool kPool = ASVRL_C51_POOL && ROWS >= 4;
   const int lane = threadIdx.x & (kWave - 1);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int row0 = (blockIdx.x * kC51Waves + w) * ROWS;
-  const int nr = B - row0 < ROWS ? B - row0 : ROWS;   // wave-uniform
-  if (nr <= 0) return;
+  const int nr = B - row0 < ROWS ? (B - row0 > 0 ? B - row0 : 0) : ROWS;   // wave-uniform
   const bool lane_on = lane < atoms;
   const float z = lane_on ? support[lane] : 0.f;
   float pv[ROWS], rv[ROWS], nv[ROWS];
@@ -164,6 +172,7 @@ __global__ __launch_bounds__(kC51Waves * kWave) void c51_kernel(const float* __r
     rv[r] = r < nr ? ret[b] : 0.f;
     nv[r] = r < nr ? nonterm[b] : 0.f;
   }
+  if (kPool && threadIdx.x == 0) s_njob = 0;
   // (1) every row's masses into LDS, bounds cleared; targets and run-boundary flags kept in registers
   int lt[ROWS], ut[ROWS];
   uint32_t fl[ROWS];
@@ -212,6 +221,7 @@ __global__ __launch_bounds__(kC51Waves * kWave) void c51_kernel(const float* __r
 #endif
   }
   wave_lds_order();
+  if constexpr (kPool) __syncthreads();   // s_njob's initial value before any wave appends
   // (3) lane k = target k: short runs finished with selects, long ones queued
   int njob = 0;
 #pragma unroll
@@ -233,21 +243,35 @@ __global__ __launch_bounds__(kC51Waves * kWave) void c51_kernel(const float* __r
     if (jm != 0ull) {
       const int before = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(jm >> 32),
                                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(jm), 0u));
-      if (lng) s_job[w][njob + before] = static_cast<uint16_t>((r << 6) | lane);
+      int base = njob;
+      if constexpr (kPool) {
+        int b0 = 0;
+        if (lane == 0) b0 = atomicAdd(&s_njob, __popcll(jm));
+        base = __builtin_amdgcn_readfirstlane(b0);
+      }
+      if (lng) s_job[(kPool ? 0 : w * ROWS * kWave) + base + before] = static_cast<uint16_t>(((w * ROWS + r) << 6) | lane);
       njob += __popcll(jm);
     }
   }
-  if (njob == 0) return;   // wave-uniform
-  wave_lds_order();
+  if constexpr (kPool) {
+    __syncthreads();
+    njob = s_njob;
+  } else {
+    if (njob == 0) return;   // wave-uniform
+    wave_lds_order();
+  }
   // (4) the long runs, one (row, target) per lane, each summed in order
-  for (int j0 = 0; j0 < njob; j0 += kWave) {
+  const uint16_t* jobs = s_job + (kPool ? 0 : w * ROWS * kWave);
+  for (int j0 = kPool ? w * kWave : 0; j0 < njob; j0 += (kPool ? kC51Waves : 1) * kWave) {
     if (j0 + lane < njob) {
-      const int job = s_job[w][j0 + lane];
-      const int r = job >> 6, k = job & 63;
-      const uint32_t q = s_rb[w][r][k];
-      float acc = run_sum(&s_lo[w][r][0], q & 255u, (q >> 8) & 255u, 0.f);
-      acc = run_sum(&s_up[w][r][0], (q >> 16) & 255u, q >> 24, acc);
-      __builtin_nontemporal_store(acc, m + static_cast<size_t>(row0 + r) * atoms + k);
+      const int job = jobs[j0 + lane];
+      const int wr = job >> 6, k = job & 63;
+      const int jw = wr / ROWS, r = wr % ROWS;
+      const uint32_t q = s_rb[jw][r][k];
+      float acc = run_sum(&s_lo[jw][r][0], q & 255u, (q >> 8) & 255u, 0.f);
+      acc = run_sum(&s_up[jw][r][0], (q >> 16) & 255u, q >> 24, acc);
+      const int grow = (blockIdx.x * kC51Waves + jw) * ROWS + r;
+      __builtin_nontemporal_store(acc, m + static_cast<size_t>(grow) * atoms + k);
     }
   }
 }

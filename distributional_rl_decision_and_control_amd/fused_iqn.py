@@ -198,18 +198,16 @@ class FusedIQNState:
                 obs=obs_rows)
 
 
-def iqn_grads(st, net, rows, taus, gamma=0.99, flush=True, target_done=False):
+def iqn_grads(st, net, rows, taus, gamma=0.99, flush=True):
     """train_IQN's backward (agent.py:449-468) for replay rows [B][88] and taus (2, B, N) =
     (target, local): every parameter .grad and st.loss. flush=False leaves the weight-gradient
-    partials queued on st.arena (the update reduces them together with the gradient norm). target_done: the
-    caller already ran the target pass (st.q_next) on these rows."""
+    partials queued on st.arena (the update reduces them together with the gradient norm)."""
     B, N = st.B, st.N
     s_rows, ns_rows = rows[:, 0:OBS], rows[:, OBS:2 * OBS]
     a_col, r_col, d_col = rows[:, 80], rows[:, 82], rows[:, 83]
     bufs, arena = st.bufs, st.arena
     # every .grad is overwritten below (no zeroing); the trunk kernels run the encoders on the rows
-    if not target_done:
-        iqn_forward_max(st.target, None, taus[0], N, st.q_next, obs=ns_rows)
+    iqn_forward_max(st.target, None, taus[0], N, st.q_next, obs=ns_rows)
     if FUSED_TRAIN and fused_train_supported(st.local, B, N):
         # forward, loss, backward and the four layers' weight-gradient partials in one launch
         if ENC_IN_KERNEL:   # ... and the encoders' gradient partials
@@ -239,12 +237,12 @@ def iqn_grads(st, net, rows, taus, gamma=0.99, flush=True, target_done=False):
 
 
 def iqn_update_fused(st, net, opt, grads, rows, gamma=0.99, taus=None, sync=None, max_norm=0.5, act_wait=None,
-                     counter=None, target_done=False):
+                     counter=None):
     """One IQN update from replay rows [B][88]; taus: (2, B, N) (target, local) or None (drawn).
     act_wait: event to wait for before the weights change (a concurrent act kernel).
     Returns (loss, grad_norm) as device scalars."""
     if taus is None:
         taus = torch.rand(2, st.B, st.N, device=st.device)
-    iqn_grads(st, net, rows, taus, gamma, flush=False, target_done=target_done)
+    iqn_grads(st, net, rows, taus, gamma, flush=False)
     gn = _reduce_and_step(st.arena, opt, grads, sync, max_norm, wait=act_wait, pack=st.local, counter=counter)
     return st.loss[0], gn

@@ -43,7 +43,7 @@ class VecTrainer:
                  learning_starts=None, target_update_interval=2500, total_timesteps=6_000_000,
                  exploration_fraction=0.25, initial_eps=0.6, final_eps=0.05, seed=0,
                  device="cuda", sync=None, graphs=False, schedule=None, net_seed=100, overlap=True, unroll=1,
-                 chain=None, operands="bf16", target_after_env=False, iqn_head_first=0):
+                 chain=None, operands="bf16", target_after_env=False):
         """Every learner runs on the hand-written kernels (fused_update / fused_iqn / fused_rainbow) with
         FusedAdam; operands="f32" takes them from the f32-operand parity build (libasvrl_f32.so). Shapes
         the kernels do not take raise ValueError."""
@@ -52,8 +52,6 @@ class VecTrainer:
         # chained schedule knob: the AC-IQN learner's target critic waits for the same iteration's env step
         # (the two then run one after the other instead of side by side; results unchanged)
         self.target_after_env = bool(target_after_env)
-        # IQN, joined schedule: the learner's draw (1) and target pass (2) ahead of the rollout's act kernel
-        self.iqn_head_first = int(iqn_head_first)
         self.continuous = agent_type == "AC-IQN"
         self.env = VecMarineNavEnv(n_envs, num_robots, num_obs, num_cores, min_start_goal_dis, width, seed=seed,
                                    device=self.device, is_continuous=self.continuous, gamma=gamma, schedule=schedule)
@@ -206,7 +204,7 @@ class VecTrainer:
         self.env.auto_reset(counted)
         self.env.advance_device(counted)
 
-    def learn(self, state=None, guard=0, actor_wait=None, target_wait=None, pre=None):
+    def learn(self, state=None, guard=0, actor_wait=None, target_wait=None):
         """One learn step of batch B: sample (uniform ring, or the prioritised tree for Rainbow) and the
         agent's fused update. state / guard: the ring snapshot to sample against and the newest entries to
         skip (the overlapped schedule); actor_wait: an event to wait for before the actor's weights change."""
@@ -229,30 +227,11 @@ class VecTrainer:
                                         self.actor_grads, rows, gamma=self.gamma, sync=self.sync,
                                         actor_wait=actor_wait, taus=self.taus, counter=self.learn_counter,
                                         prologue_done=True, target_wait=target_wait)
-        if pre is not None:   # drawn (and the target pass run) ahead of the rollout: _learner_head
-            rows, target_done = pre
-        else:   # the update's quantile fractions are drawn by the sampling launch
-            rows, target_done = self._iqn_draw(state, guard), False
-        return iqn_update_fused(self.fused_iqn, self.local, self.opt, self.grads, rows, gamma=self.gamma,
-                                sync=self.sync, act_wait=actor_wait, taus=self.taus[:2], counter=self.learn_counter,
-                                target_done=target_done)
-
-    def _iqn_draw(self, state, guard):
-        return self.replay.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter, out=self.batch_rows,
+        # the update's quantile fractions are drawn by the sampling launch
+        rows = self.replay.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter, out=self.batch_rows,
                                   state=state, guard=guard, taus=self.taus)
-
-    def _learner_head(self, state, guard):
-        """IQN on the joined schedule with iqn_head_first: the learner's draw (1), and its target pass (2), issued
-        before the rollout forks, so the act kernel -- which fills every CU -- queues behind them instead of
-        beside them. The same launches on the same data: bit-identical."""
-        if self.fused_iqn is None or not self.iqn_head_first:
-            return None
-        rows = self._iqn_draw(state, guard)
-        if self.iqn_head_first >= 2:
-            from .fused_iqn import OBS as IQN_OBS, iqn_forward_max
-            st = self.fused_iqn
-            iqn_forward_max(st.target, None, self.taus[0], st.N, st.q_next, obs=rows[:, IQN_OBS:2 * IQN_OBS])
-        return rows, self.iqn_head_first >= 2
+        return iqn_update_fused(self.fused_iqn, self.local, self.opt, self.grads, rows, gamma=self.gamma,
+                                sync=self.sync, act_wait=actor_wait, taus=self.taus[:2], counter=self.learn_counter)
 
     def hard_update(self):
         """soft_update with TAU = 1.0 (agent.py:643-679): target <- local."""
@@ -313,7 +292,6 @@ class VecTrainer:
         # the caller's stream joined), copied on the learner's own stream: the learner's chain then
         # starts without a cross-stream wait (each costs ~10 us in a replayed graph)
         self.ring_snap.copy_(self.replay.state)
-        pre = self._learner_head(self.ring_snap, self.E * self.R)
         s_roll.wait_stream(main)
         with torch.cuda.stream(s_roll):
             self.act()
@@ -323,7 +301,7 @@ class VecTrainer:
             counted = self._push()
             env.auto_reset(counted)
             env.advance_device(counted)
-        out = self.learn(state=self.ring_snap, guard=self.E * self.R, actor_wait=ev_act, pre=pre)
+        out = self.learn(state=self.ring_snap, guard=self.E * self.R, actor_wait=ev_act)
         main.wait_stream(s_roll)
         return out
 

@@ -84,27 +84,3 @@ def test_target_critic_in_fused_launch_matches_separate(monkeypatch):
     assert torch.equal(a.env.batch.rs, b.env.batch.rs)
     assert torch.equal(a.replay.ring, b.replay.ring)
 
-
-@pytest.mark.parametrize("head", [1, 2])
-def test_iqn_learner_head_first_matches_default(head):
-    """VecTrainer.iqn_head_first: the IQN learner's draw (and its target pass) issued before the rollout forks
-    -- an ordering only, so weights, losses, env and replay state equal the default joined schedule's."""
-    from distributional_rl_decision_and_control_amd.vec_trainer import VecTrainer
-
-    def run(h):
-        tr = VecTrainer(n_envs=256, agent_type="IQN", batch_size=256, num_tau=32, seed=21, graphs=True, unroll=2,
-                        chain=False, buffer_size=256 * 5 * 40, learning_starts=512, iqn_head_first=h)
-        while tr.replay_size_host() < tr.learning_starts:
-            tr.iteration()
-        for _ in range(8):
-            out = tr.iteration()
-        torch.cuda.synchronize()
-        params = torch.cat([p.detach().reshape(-1).float() for p in tr.local.parameters()])
-        return tr, params, torch.stack([torch.as_tensor(x, device="cuda").float().reshape(()) for x in out[:2]])
-    a, pa, la = run(head)
-    b, pb, lb = run(0)
-    assert torch.isfinite(la).all()
-    assert torch.equal(la, lb), (la, lb)
-    assert torch.equal(pa, pb)
-    assert torch.equal(a.env.batch.rs, b.env.batch.rs)
-    assert torch.equal(a.replay.ring, b.replay.ring)
