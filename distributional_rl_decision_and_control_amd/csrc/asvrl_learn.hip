@@ -278,6 +278,11 @@ __global__ __launch_bounds__(kC51Waves * kWave) void c51_kernel(const float* __r
 
 // ------------------------------------------------------------------ replay ring
 constexpr int kPushBlock = 256;
+// the last block takes the push's row count from the blocks' own counts (one integer atomic each) instead of
+// recounting every flag: IQN loop 0.2947 -> 0.2930 ms, AC-IQN unchanged (profiles/r04ad_push_sumcount_ab.txt)
+#ifndef ASVRL_PUSH_SUMCOUNT
+#define ASVRL_PUSH_SUMCOUNT 1
+#endif
 
 __device__ __forceinline__ int block_sum(int v, int* sh) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
@@ -349,13 +354,23 @@ __global__ __launch_bounds__(kPushBlock) void replay_push_kernel(
   }
   __syncthreads();   // every lane's read of ring_state is done before the block arrives
   if (threadIdx.x == 0) {
+#if ASVRL_PUSH_SUMCOUNT
+    int cb = 0;
+    for (int w = 0; w < kPushBlock / kWave; ++w) cb += shw[w];
+    atomicAdd(arrive + 1, cb);   // the push's row count, block by block (integers: the order does not matter)
+#endif
     __threadfence();
     s_last = atomicAdd(arrive, 1) == nblocks - 1;
   }
   __syncthreads();
   if (!s_last) return;
+#if ASVRL_PUSH_SUMCOUNT
+  if (threadIdx.x == 0) {
+    const int tot = atomicExch(arrive + 1, 0);   // every block's count (added before its arrival), reset
+#else
   const int tot = count_pushed(cnt, n, sh);
   if (threadIdx.x == 0) {
+#endif
     const int64_t nh = (head_in + tot) % cap, ns0 = ring_state[1] + tot;
     const int64_t ns = ns0 < cap ? ns0 : cap;
     ring_state[0] = nh;

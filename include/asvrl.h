@@ -430,7 +430,8 @@ int asvrl_iqn_act(const AsvCriticWeights* w, const AsvIqnHead* head, const AsvIq
  * (obj_cnt_next >= 0), in slot order, into a ring of `capacity` rows of ASVRL_TR_DIM f32.
  * ring_state: int64[2] = {head, size} in device memory (updated by the call, so the call
  * is capturable in a HIP graph). work: int32[ceil(n / 256) + 1] scratch, ZERO before the first call
- * (work[0] is the launch's arrival counter, which the call leaves zero again). One launch. */
+ * (work[0] is the launch's arrival counter, work[1] the blocks' running row count; the call leaves both zero
+ * again). One launch. */
 int asvrl_replay_push(const float* obs_prev, const float* obs_next, const int8_t* obj_cnt_next,
                       const double* actions, int32_t action_dim, const double* reward,
                       const uint8_t* done, int32_t n, float* ring, int64_t capacity,
