@@ -16,7 +16,10 @@ constexpr int kOptThreads = 256;
 #ifndef ASVRL_ADAM_PER_THREAD
 #define ASVRL_ADAM_PER_THREAD 1
 #endif
-constexpr int64_t kAdamPer = ASVRL_ADAM_PER_THREAD;   // parameters per thread (grid size), at most 1024 blocks
+constexpr int64_t kAdamPer = ASVRL_ADAM_PER_THREAD;
+#ifndef ASVRL_ADAM_WAVE_TREE
+#define ASVRL_ADAM_WAVE_TREE 1
+#endif   // parameters per thread (grid size), at most 1024 blocks
 
 __global__ __launch_bounds__(kOptThreads) void sumsq_kernel(const float* __restrict__ g, int64_t n,
                                                              double* __restrict__ partial, float* step) {
@@ -71,6 +74,19 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(float* __restrict__ p
   {   // thread t folds partials t, t + 256, ... in order, then a fixed tree: the same in every block
     double x = 0.0;
     x = strided_sum<double>(partial, threadIdx.x, nparts, kOptThreads, x);
+#if ASVRL_ADAM_WAVE_TREE
+    // the tree inside each wave by xor shuffles (no barrier), then the four wave sums in order: one barrier
+    // instead of eight (AC-IQN step 0.2626 -> 0.2621 ms, profiles/r04af_adam_wave_tree_ab.txt)
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) x += __shfl_xor(x, off, kWave);
+    if ((threadIdx.x & (kWave - 1)) == 0) s_red[threadIdx.x / kWave] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+#pragma unroll
+      for (int w = 0; w < kOptThreads / kWave; ++w) t += s_red[w];
+      const float norm = static_cast<float>(sqrt(t));
+#else
     s_red[threadIdx.x] = x;
     __syncthreads();
     for (int w = kOptThreads / 2; w > 0; w >>= 1) {
@@ -79,6 +95,7 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(float* __restrict__ p
     }
     if (threadIdx.x == 0) {
       const float norm = static_cast<float>(sqrt(s_red[0]));
+#endif
       s_norm = norm;
       if (blockIdx.x == 0 && norm_out != nullptr) norm_out[0] = norm;
     }
