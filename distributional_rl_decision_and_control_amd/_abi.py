@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("ASVRL_LIB", os.path.join(HERE, "lib", "libasvrl.so"))
 # the same sources built with f32 learner operands (the parity build; asvrl_operand_bytes() == 4)
 LIB_PATH_F32 = os.path.join(HERE, "lib", "libasvrl_f32.so")
 OPERANDS = {"bf16": (LIB_PATH, 2), "f32": (LIB_PATH_F32, 4)}
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
 OBS_DIM = 40   # self 7 | objects 25 | mask 5 | pad 3
@@ -248,6 +248,8 @@ EXPORTS = [
     ("asvrl_current_field", C.c_int, [_VP, _I32, _D, _VP, _I32, _VP, _VP]),
     ("asvrl_quantile_huber", C.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, _F, _F, _VP, _VP, _VP, _VP]),
     ("asvrl_c51_project", C.c_int, [_VP, _VP, _VP, _VP, _I32, _I32, _F, _F, _F, _F, _VP, _VP]),
+    ("asvrl_c51_project_ex", C.c_int, [_VP, _VP, C.c_int64, _VP, C.c_int64, _VP, _I32, _I32, _F, _F, _F, _F, _VP,
+                                       _VP]),
     ("asvrl_critic_pack", C.c_int, [_VP, _VP, _VP, C.POINTER(AsvCriticWeights), _VP]),
     ("asvrl_critic_forward", C.c_int, [C.POINTER(AsvCriticWeights), C.POINTER(AsvCriticIO), _VP]),
     ("asvrl_critic_train", C.c_int, [C.POINTER(AsvCriticWeights), C.POINTER(AsvCriticIO), C.POINTER(AsvCriticActs),

@@ -143,8 +143,8 @@ __device__ __forceinline__ int from_next_lane(int v, int edge) { return __builti
 
 template <int ROWS>
 __global__ __launch_bounds__(kC51Waves * kWave) void c51_kernel(const float* __restrict__ pns_a,
-                                                                const float* __restrict__ ret,
-                                                                const float* __restrict__ nonterm,
+                                                                const float* __restrict__ ret, int64_t ld_ret,
+                                                                const float* __restrict__ nonterm, int64_t ld_nt,
                                                                 const float* __restrict__ support, int B,
                                                                 int atoms, float vmin, float vmax, float dz,
                                                                 float gamma_n, float* __restrict__ m) {
@@ -169,8 +169,8 @@ __global__ __launch_bounds__(kC51Waves * kWave) void c51_kernel(const float* __r
     const int b = row0 + r;
     const bool on = r < nr && lane_on;
     pv[r] = on ? __builtin_nontemporal_load(pns_a + static_cast<size_t>(b) * atoms + lane) : 0.f;
-    rv[r] = r < nr ? ret[b] : 0.f;
-    nv[r] = r < nr ? nonterm[b] : 0.f;
+    rv[r] = r < nr ? ret[b * ld_ret] : 0.f;
+    nv[r] = r < nr ? nonterm[b * ld_nt] : 0.f;
   }
   if (kPool && threadIdx.x == 0) s_njob = 0;
   // (1) every row's masses into LDS, bounds cleared; targets and run-boundary flags kept in registers
@@ -451,17 +451,20 @@ extern "C" int asvrl_quantile_huber(const float* qt, const float* qe, const floa
   return 0;
 }
 
-extern "C" int asvrl_c51_project(const float* pns_a, const float* returns, const float* nonterminal,
-                                 const float* support, int32_t B, int32_t atoms, float vmin, float vmax,
-                                 float delta_z, float gamma_n, float* m, void* stream) {
+extern "C" int asvrl_c51_project_ex(const float* pns_a, const float* returns, int64_t ld_ret,
+                                    const float* nonterminal, int64_t ld_nt, const float* support, int32_t B,
+                                    int32_t atoms, float vmin, float vmax, float delta_z, float gamma_n, float* m,
+                                    void* stream) {
   ASVRL_REQUIRE(pns_a && returns && nonterminal && support && m, "asvrl_c51_project: null argument");
   ASVRL_REQUIRE(atoms >= 2 && atoms <= kWave, "asvrl_c51_project: atoms must be in [2, 64]");
+  ASVRL_REQUIRE(ld_ret >= 1 && ld_nt >= 1, "asvrl_c51_project: strides must be positive");
   if (B <= 0) return 0;
   // rows per wave: one below 4096 rows (latency: every row its own wave), two below 32768, else
   // ASVRL_C51_ROWS (their loads in flight together, their long runs walked side by side)
   auto go = [&](auto kern, int rows) {
     hipLaunchKernelGGL(kern, dim3((B + kC51Waves * rows - 1) / (kC51Waves * rows)), dim3(kC51Waves * kWave), 0,
-                       as_stream(stream), pns_a, returns, nonterminal, support, B, atoms, vmin, vmax, delta_z, gamma_n, m);
+                       as_stream(stream), pns_a, returns, ld_ret, nonterminal, ld_nt, support, B, atoms, vmin, vmax,
+                       delta_z, gamma_n, m);
   };
   if (B < 4096)
     go(c51_kernel<1>, 1);
@@ -470,6 +473,13 @@ extern "C" int asvrl_c51_project(const float* pns_a, const float* returns, const
   else
     go(c51_kernel<ASVRL_C51_ROWS>, ASVRL_C51_ROWS);
   return check_launch("asvrl_c51_project");
+}
+
+extern "C" int asvrl_c51_project(const float* pns_a, const float* returns, const float* nonterminal,
+                                 const float* support, int32_t B, int32_t atoms, float vmin, float vmax,
+                                 float delta_z, float gamma_n, float* m, void* stream) {
+  return asvrl_c51_project_ex(pns_a, returns, 1, nonterminal, 1, support, B, atoms, vmin, vmax, delta_z, gamma_n, m,
+                              stream);
 }
 
 extern "C" int asvrl_replay_push_ex(const float* obs_prev, const float* obs_next, const int8_t* obj_cnt_next,

@@ -53,14 +53,22 @@ def c51_project(pns_a, returns, nonterminal, support, vmin=-1.0, vmax=1.0, gamma
     tensors; nonterminal may be (B,) or (B, 1)."""
     pns_a = pns_a.float().contiguous()
     B, atoms = pns_a.shape
-    R = returns.float().reshape(B).contiguous()
-    nt = nonterminal.float().reshape(B).contiguous()
+
+    def col(t):   # a strided f32 column (e.g. of the replay rows) is read in place, anything else copied
+        t = t.float()
+        if t.dim() == 2 and t.shape[1] == 1:
+            t = t[:, 0]
+        if t.dim() != 1 or t.shape[0] != B or t.stride(0) < 1:
+            t = t.reshape(B).contiguous()
+        return t
+    R, nt = col(returns), col(nonterminal)
     sup = support.float().contiguous()
     m = out if out is not None else torch.empty_like(pns_a)
     dz = float(torch.tensor((vmax - vmin) / (atoms - 1), dtype=torch.float32))
     g32 = float(torch.tensor(gamma_n, dtype=torch.float32))
-    rc = _abi.lib().asvrl_c51_project(_abi.ptr(pns_a), _abi.ptr(R), _abi.ptr(nt), _abi.ptr(sup), B, atoms,
-                                      float(vmin), float(vmax), dz, g32, _abi.ptr(m), _abi.stream_ptr())
+    rc = _abi.lib().asvrl_c51_project_ex(_abi.ptr(pns_a), _abi.ptr(R), R.stride(0), _abi.ptr(nt), nt.stride(0),
+                                         _abi.ptr(sup), B, atoms, float(vmin), float(vmax), dz, g32, _abi.ptr(m),
+                                         _abi.stream_ptr())
     _abi.check(rc, "asvrl_c51_project")
     return m
 

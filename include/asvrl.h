@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 20
+#define ASVRL_ABI_VERSION 21
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -216,6 +216,11 @@ int asvrl_quantile_huber(const float* qt, const float* qe, const float* tau, int
 int asvrl_c51_project(const float* pns_a, const float* returns, const float* nonterminal,
                       const float* support, int32_t B, int32_t atoms, float vmin, float vmax,
                       float delta_z, float gamma_n, float* m, void* stream);
+/* The same with returns[b * ld_ret] and nonterminal[b * ld_nt] (ABI 21): the columns of the replay rows
+ * read in place (the Rainbow update's R^n and nonterminal columns, no copies). */
+int asvrl_c51_project_ex(const float* pns_a, const float* returns, int64_t ld_ret, const float* nonterminal,
+                         int64_t ld_nt, const float* support, int32_t B, int32_t atoms, float vmin, float vmax,
+                         float delta_z, float gamma_n, float* m, void* stream);
 
 /* ---------------------------------------------------------------- fused IQN critic (MFMA) */
 

@@ -261,3 +261,19 @@ def test_learn_prologue_matches_separate_launches(guard):
     for k, v in ref.items():
         assert torch.equal(v, getattr(ab, k)), k
     assert torch.equal(na_a, st.na)
+
+
+def test_c51_strided_columns_read_in_place():
+    """asvrl_c51_project_ex (ABI 21): the returns / nonterminal columns of replay rows [B][88] read at their
+    row stride give the same target distribution, bit for bit, as contiguous copies of them."""
+    from distributional_rl_decision_and_control_amd import learn_ops
+    g = torch.Generator(device="cuda").manual_seed(3)
+    for B in (64, 8192):
+        rows = torch.rand(B, 88, generator=g, device="cuda") * 4 - 2
+        rows[:, 83] = (torch.rand(B, generator=g, device="cuda") > 0.1).float()
+        p = torch.softmax(torch.randn(B, 51, generator=g, device="cuda"), 1)
+        sup = torch.linspace(-1.0, 1.0, 51, device="cuda")
+        m_view = learn_ops.c51_project(p, rows[:, 82], rows[:, 83], sup)
+        m_copy = learn_ops.c51_project(p, rows[:, 82].contiguous(), rows[:, 83].contiguous(), sup)
+        torch.cuda.synchronize()
+        assert torch.equal(m_view, m_copy)
