@@ -268,7 +268,7 @@ def test_c51_strided_columns_read_in_place():
     row stride give the same target distribution, bit for bit, as contiguous copies of them."""
     from distributional_rl_decision_and_control_amd import learn_ops
     g = torch.Generator(device="cuda").manual_seed(3)
-    for B in (64, 8192):
+    for B in (64, 8192, 65536):   # the kernel's 1-, 2- and 4-row shapes
         rows = torch.rand(B, 88, generator=g, device="cuda") * 4 - 2
         rows[:, 83] = (torch.rand(B, generator=g, device="cuda") > 0.1).float()
         p = torch.softmax(torch.randn(B, 51, generator=g, device="cuda"), 1)
