@@ -384,28 +384,9 @@ __device__ __forceinline__ int row_action(const float* in, int bl, int A) {
 #ifndef ASVRL_RA_FENCE_MASK
 #define ASVRL_RA_FENCE_MASK 0
 #endif
-// the cos layer's weight-gradient loop with its next k-step's operands in flight (A/B knob)
-#ifndef ASVRL_DWC_AHEAD
-#define ASVRL_DWC_AHEAD 0
-#endif
-// the workgroup's dW2 / dW1 partials stored during its last round, right after their last MFMAs (behind the
-// rest of that round) instead of all partials at the end: the chip-wide 69 MB store burst at the launch's
-// end shrinks to the cos layer's, encoders' and output layer's partials. Same values, same places. Measured
-// no faster (108.8 vs 109.0 us median, profiles/r04e_fused_variants_ab.txt) with 5 more spilled registers: off.
-#ifndef ASVRL_EARLY_PARTIALS
-#define ASVRL_EARLY_PARTIALS 0
-#endif
-// dW1 + L4's first dx block as one interleaved stream (A/B knob)
-#ifndef ASVRL_L4_INTERLEAVE
-#define ASVRL_L4_INTERLEAVE 0
-#endif
-// dW2 + L3 as one interleaved MFMA stream (A/B knob), and its read-ahead depth in steps of two MFMAs
-#ifndef ASVRL_L3_INTERLEAVE
-#define ASVRL_L3_INTERLEAVE 0
-#endif
-#ifndef ASVRL_L3_AHEAD
-#define ASVRL_L3_AHEAD 2
-#endif
+// (Measured in round 4 and removed, profiles/r04e_fused_variants_ab.txt: a deeper weight-gradient read-ahead,
+// dW2 + L3 and dW1 + L4 as interleaved MFMA streams, the cos layer's gradient loop a k-step ahead, and the dW2 /
+// dW1 partials stored during the last round -- all bit-identical, none faster.)
 template <int KS, int NB, int P, class WF>
 __device__ __forceinline__ void mfma_rows(f32x16 (&acc)[NB], const elem_t* img, const RowA<P>& RA, WF wf) {
   constexpr int D = ASVRL_READ_AHEAD < KS ? ASVRL_READ_AHEAD : KS;
@@ -435,12 +416,9 @@ __device__ __forceinline__ void mfma_rows(f32x16 (&acc)[NB], const elem_t* img, 
 // The weight-gradient grid dW[n] += A(kk)^T-read x B(kk, n) over kk < KK, n < NN (mf(kk, n, A, B) does
 // the MFMA and, at n = 0, the bias sum): every B(kk, n) read D steps ahead in (kk, n) order, each A(kk)
 // a whole kk ahead, one scheduling fence per step (see mfma_rows).
-#ifndef ASVRL_GRID_AHEAD
-#define ASVRL_GRID_AHEAD ASVRL_READ_AHEAD
-#endif
 template <int KK, int NN, class AF, class BF, class MF>
 __device__ __forceinline__ void mfma_grid(AF af, BF bf, MF mf) {
-  constexpr int T = KK * NN, D0 = ASVRL_GRID_AHEAD < T ? ASVRL_GRID_AHEAD : T;
+  constexpr int T = KK * NN, D0 = ASVRL_READ_AHEAD < T ? ASVRL_READ_AHEAD : T;
   if constexpr (D0 == 0) {
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
@@ -709,43 +687,10 @@ void critic_fused_kernel(FusedArgs a) {
   float encr[IQN ? 8 : 1];   // IQN with parts.enc: this lane's feature's encoder sums
 #pragma unroll
   for (int i = 0; i < (IQN ? 8 : 1); ++i) encr[i] = 0.f;
-  // the workgroup's dW2 / dW1 partials: [M*K + M] per layer, features in natural order (register g of lane
-  // half h is feature row (g & 3) + 8 (g >> 2) + 4 h of the wave's block, lane r its column)
   const int grp = blockIdx.x;
-  auto store_dw2 = [&]() {
-    mfma_drain();
-    int tid_s = threadIdx.x;
-    asm volatile("" : "+v"(tid_s));
-    const int ls = tid_s & 63, hs = ls >> 5, rs = ls & 31;
-    float* p2 = a.parts.hidden2 + static_cast<size_t>(grp) * (kH * kH + kH);
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const int f2 = swap23(w * 32 + (g & 3) + 8 * (g >> 2) + 4 * hs);
-#pragma unroll
-      for (int n = 0; n < 4; ++n) p2[f2 * kH + swap23(32 * n + rs)] = dW2[n][g];
-    }
-    const float v = half_sum(db2);
-    if (hs == 0) p2[kH * kH + swap23(w * 32 + rs)] = v;
-  };
-  auto store_dw1 = [&]() {
-    mfma_drain();
-    int tid_s = threadIdx.x;
-    asm volatile("" : "+v"(tid_s));
-    const int ls = tid_s & 63, hs = ls >> 5, rs = ls & 31;
-    float* p1 = a.parts.hidden + static_cast<size_t>(grp) * (kH * kC + kH);
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const int f2 = swap23(w * 32 + (g & 3) + 8 * (g >> 2) + 4 * hs);
-#pragma unroll
-      for (int n = 0; n < 8; ++n) p1[f2 * kC + swap23(32 * n + rs)] = dW1[n][g];
-    }
-    const float v = half_sum(db1);
-    if (hs == 0) p1[kH * kC + swap23(w * 32 + rs)] = v;
-  };
   int buf = 0, it_ = 0;
   (void)it_;
   for (int t = blockIdx.x; t < a.rounds; t += gridDim.x, buf ^= 1, ++it_) {
-    const bool last_round = t + static_cast<int>(gridDim.x) >= a.rounds;   // workgroup-uniform
     // the next round's inputs, into registers during this round and into LDS at its end
     float pre[IL::kPer];
     int tid_p = threadIdx.x;
@@ -1032,10 +977,7 @@ void critic_fused_kernel(FusedArgs a) {
 
     // ---------------- dW2[own][:] += dz2^T h1g;  L3: dh1g = W2^T dz2 (own block) -> dG, dz1 (own
     // slice into the dz1 image, which nobody reads before the next barrier)
-    // ASVRL_L3_INTERLEAVE: the two independent MFMA streams issued alternately (each accumulator's MFMAs in
-    // the same order: bit-identical), so each one's LDS operand reads have the other's MFMA to land behind
-    constexpr bool L3I = ASVRL_L3_INTERLEAVE && NB == 2 && G / 16 == 4;
-    if constexpr (!L3I) {
+    {
       ASVRL_FRESH_LANE();
       const TrA<kH> TA_a(lane);
       const TrA<kH> TA_b(lane);
@@ -1059,34 +1001,8 @@ void critic_fused_kernel(FusedArgs a) {
       f32x16 acc[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[j] = f32x16{};
-      if constexpr (L3I) {
-        // step t: dW2's MFMA (kk, n) = (t / 4, t % 4) and L3's (block j, k-step ks) = (t % 2, t / 2)
-        const TrA<kH> TA_a(lane);
-        const TrA<kH> TA_b(lane);
-        constexpr int T = 16, D = ASVRL_L3_AHEAD;
-        frag8 gA[2], gB[D], rB[D];
-        gA[0] = trf(L.b, TA_b, 0, w);
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-          gB[d] = trf(L.a, TA_a, d / 4, d % 4);
-          rB[d] = rowf(L.b, RA_b, d % 2, d / 2);
-        }
-#pragma unroll
-        for (int t = 0; t < T; ++t) {
-          const int kk = t / 4, n = t % 4;
-          if (n == 0 && kk + 1 < 4) gA[(kk + 1) % 2] = trf(L.b, TA_b, kk + 1, w);
-          if (n == 0) db2 += sum8(gA[kk % 2]);
-          mfma_acc(dW2[n], gA[kk % 2], gB[t % D]);
-          acc[t % 2] = mfma(w2tf[t / 2], rB[t % D], acc[t % 2]);
-          if (t + D < T) {
-            gB[t % D] = trf(L.a, TA_a, (t + D) / 4, (t + D) % 4);
-            rB[t % D] = rowf(L.b, RA_b, (t + D) % 2, (t + D) / 2);
-          }
-          __builtin_amdgcn_sched_barrier(ASVRL_RA_FENCE_MASK);
-        }
-      } else {
-        mfma_rows<kH / 16, NB>(acc, L.b, RA_b, [&](int ks) { return w2tf[ks]; });
-      }
+      mfma_rows<kH / 16, NB>(acc, L.b, RA_b, [&](int ks) { return w2tf[ks]; });
+
       // dz1 = dh1g G 1[h1 > 0]; dG = sum over the sample's taus of dh1g h1 (-> dzG = dG 1[G > 0])
 #pragma unroll
       for (int j = 0; j < NB; ++j) {   // h1 unpacked here, not earlier
@@ -1143,17 +1059,12 @@ void critic_fused_kernel(FusedArgs a) {
         if (e < IL::kSize) L.in[buf ^ 1][e] = pre[u];
       }
     }
-    if (ASVRL_EARLY_PARTIALS && last_round) store_dw2();
     ASVRL_STAMP(12);
     __syncthreads();
     ASVRL_STAMP(13);
 
     // ---------------- dW1[own][:] += dz1^T x; L4's first weight fragments fetched meanwhile
-    // ASVRL_L4_INTERLEAVE: L4's first block's dx = W1^T dz1 MFMAs issued between dW1's (one per two), each
-    // accumulator's MFMAs in the same order (bit-identical)
-    constexpr bool L4I = ASVRL_L4_INTERLEAVE && NB == 2 && G / 16 == 4 && ASVRL_READ_AHEAD != 0;
     frag8 wt[8], wcc[4];
-    f32x16 dx0[L4I ? NB : 1];
     {
       ASVRL_FRESH_LANE();
       const TrA<kH> TA_d(lane);
@@ -1162,41 +1073,13 @@ void critic_fused_kernel(FusedArgs a) {
       for (int ks = 0; ks < 8; ++ks) wt[ks] = W1T[((2 * w) * 8 + ks) * 64 + lane];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) wcc[ks] = WCR ? wcr0[ks] : WC[((2 * w) * 4 + ks) * 64 + lane];
-      if constexpr (L4I) {
-        const RowA<kH> RA_d(r, h);
-        constexpr int T = 32, D = ASVRL_GRID_AHEAD, DR = 2;
-        frag8 gA[2], gB[D], rB[DR];
-#pragma unroll
-        for (int j = 0; j < NB; ++j) dx0[j] = f32x16{};
-        gA[0] = trf(L.dz1, TA_d, 0, w);
-#pragma unroll
-        for (int d = 0; d < D; ++d) gB[d] = trf(L.x, TA_x, d / 8, d % 8);
-#pragma unroll
-        for (int d = 0; d < DR; ++d) rB[d] = rowf(L.dz1, RA_d, d % 2, d / 2);
-#pragma unroll
-        for (int t = 0; t < T; ++t) {
-          const int kk = t / 8, n = t % 8;
-          if (n == 0 && kk + 1 < 4) gA[(kk + 1) % 2] = trf(L.dz1, TA_d, kk + 1, w);
-          if (n == 0) db1 += sum8(gA[kk % 2]);
-          mfma_acc(dW1[n], gA[kk % 2], gB[t % D]);
-          if (t + D < T) gB[t % D] = trf(L.x, TA_x, (t + D) / 8, (t + D) % 8);
-          if (t % 2 == 1) {   // dx step u = (j, ks) = (u % 2, u / 2)
-            const int u = t / 2;
-            dx0[u % 2] = mfma(wt[u / 2], rB[u % DR], dx0[u % 2]);
-            if (u + DR < 16) rB[u % DR] = rowf(L.dz1, RA_d, (u + DR) % 2, (u + DR) / 2);
-          }
-          __builtin_amdgcn_sched_barrier(ASVRL_RA_FENCE_MASK);
-        }
-      } else {
         mfma_grid<G / 16, 8>([&](int kk) { return trf(L.dz1, TA_d, kk, w); },
                              [&](int kk, int n) { return trf(L.x, TA_x, kk, n); },
                              [&](int kk, int n, const frag8& A, const frag8& B) {
                                if (n == 0) db1 += sum8(A);
                                mfma_acc(dW1[n], A, B);
                              });
-      }
     }
-    if (ASVRL_EARLY_PARTIALS && last_round) store_dw1();
     if constexpr (AH) {   // round t + grid's images, behind the dW1 MFMAs
       const int tn = t + static_cast<int>(gridDim.x);
       if (tn < a.rounds) stage(tn * G / NT, L.in[buf ^ 1], L.cos[buf ^ 1], L.F[buf ^ 1], L.G[buf ^ 1]);
@@ -1225,12 +1108,7 @@ void critic_fused_kernel(FusedArgs a) {
           dxs[j] = f32x16{};
           ccs[j] = acc_init(bcp, mb * 32, h);
         }
-        if (L4I && mq == 0) {
-#pragma unroll
-          for (int j = 0; j < NB; ++j) dxs[j] = dx0[L4I ? j : 0];
-        } else {
-          mfma_rows<8, NB>(dxs, L.dz1, RA_d, [&](int ks) { return wt[ks]; });
-        }
+        mfma_rows<8, NB>(dxs, L.dz1, RA_d, [&](int ks) { return wt[ks]; });
         mfma_rows<4, NB>(ccs, cosb, RA_cos, [&](int ks) { return wcc[ks]; });
       }
 #pragma unroll
@@ -1306,29 +1184,6 @@ void critic_fused_kernel(FusedArgs a) {
       ASVRL_FRESH_LANE();
       const TrA<kNcos> TA_cos(lane);
       const TrA<kNcos> TA_dzc(lane);
-      if constexpr (ASVRL_DWC_AHEAD != 0) {   // k-step kk + 1's four operands read during kk's MFMAs
-        frag8 q[2][4];
-        auto load = [&](int kk, frag8 (&d)[4]) {
-          d[0] = trf(dzc_w, TA_dzc, kk, 0);
-          d[1] = trf(dzc_w, TA_dzc, kk, 1);
-          d[2] = trf(cosb, TA_cos, kk, 0);
-          d[3] = trf(cosb, TA_cos, kk, 1);
-        };
-        load(0, q[0]);
-#pragma unroll
-        for (int kk = 0; kk < G / 16; ++kk) {
-          if (kk + 1 < G / 16) load(kk + 1, q[(kk + 1) % 2]);
-          const frag8(&o)[4] = q[kk % 2];
-          dbc0 += sum8(o[0]);
-          dbc1 += sum8(o[1]);
-#pragma unroll
-          for (int n = 0; n < 2; ++n) {
-            mfma_acc(dWc[n], o[0], o[2 + n]);
-            mfma_acc(dWc[2 + n], o[1], o[2 + n]);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      } else {
 #pragma unroll
         for (int kk = 0; kk < G / 16; ++kk) {
           const frag8 A0 = trf(dzc_w, TA_dzc, kk, 0);
@@ -1342,7 +1197,6 @@ void critic_fused_kernel(FusedArgs a) {
             mfma_acc(dWc[2 + n], A1, Bf);
           }
         }
-      }
     }
     if constexpr (!AH) {
 #pragma unroll
@@ -1400,19 +1254,15 @@ void critic_fused_kernel(FusedArgs a) {
   }
   float* p2 = a.parts.hidden2 + static_cast<size_t>(grp) * (kH * kH + kH);
   float* p1 = a.parts.hidden + static_cast<size_t>(grp) * (kH * kC + kH);
-  (void)p2;
-  (void)p1;
   float* pc = a.parts.cos_emb + static_cast<size_t>(grp) * (kC * kNcos + kC);
 #pragma unroll
   for (int g = 0; g < 16; ++g) {
     const int m = (g & 3) + 8 * (g >> 2) + 4 * h;   // MFMA C row of register g
     const int f2 = swap23(w * 32 + m);
-    if constexpr (!ASVRL_EARLY_PARTIALS) {
 #pragma unroll
-      for (int n = 0; n < 4; ++n) p2[f2 * kH + swap23(32 * n + r)] = dW2[n][g];
+    for (int n = 0; n < 4; ++n) p2[f2 * kH + swap23(32 * n + r)] = dW2[n][g];
 #pragma unroll
-      for (int n = 0; n < 8; ++n) p1[f2 * kC + swap23(32 * n + r)] = dW1[n][g];
-    }
+    for (int n = 0; n < 8; ++n) p1[f2 * kC + swap23(32 * n + r)] = dW1[n][g];
 #pragma unroll
     for (int mq = 0; mq < 2; ++mq) {
       const int fc = swap23((2 * w + mq) * 32 + m);
@@ -1422,15 +1272,11 @@ void critic_fused_kernel(FusedArgs a) {
   }
   dbc0 = half_sum(dbc0);
   dbc1 = half_sum(dbc1);
-  if constexpr (!ASVRL_EARLY_PARTIALS) {
-    db2 = half_sum(db2);
-    db1 = half_sum(db1);
-  }
+  db2 = half_sum(db2);
+  db1 = half_sum(db1);
   if (h == 0) {
-    if constexpr (!ASVRL_EARLY_PARTIALS) {
-      p2[kH * kH + swap23(w * 32 + r)] = db2;
-      p1[kH * kC + swap23(w * 32 + r)] = db1;
-    }
+    p2[kH * kH + swap23(w * 32 + r)] = db2;
+    p1[kH * kC + swap23(w * 32 + r)] = db1;
     pc[kC * kNcos + swap23(2 * w * 32 + r)] = dbc0;
     pc[kC * kNcos + swap23((2 * w + 1) * 32 + r)] = dbc1;
   }

@@ -16,10 +16,11 @@ constexpr int kOptThreads = 256;
 #ifndef ASVRL_ADAM_PER_THREAD
 #define ASVRL_ADAM_PER_THREAD 1
 #endif
-constexpr int64_t kAdamPer = ASVRL_ADAM_PER_THREAD;
+constexpr int64_t kAdamPer = ASVRL_ADAM_PER_THREAD;   // parameters per thread (grid size), at most 1024 blocks
+// the norm partials folded with wave shuffles and one barrier (1) instead of an eight-barrier LDS tree (0)
 #ifndef ASVRL_ADAM_WAVE_TREE
 #define ASVRL_ADAM_WAVE_TREE 1
-#endif   // parameters per thread (grid size), at most 1024 blocks
+#endif
 
 __global__ __launch_bounds__(kOptThreads) void sumsq_kernel(const float* __restrict__ g, int64_t n,
                                                              double* __restrict__ partial, float* step) {

@@ -157,6 +157,10 @@ class VecTrainer:
         # AC-IQN only (measured 0.346 -> 0.340 ms/step; IQN, whose act kernel fills the GPU, 0.363 ->
         # 0.366: profiles/r02_chain_schedule_ab.txt)
         self.chain = (agent_type == "AC-IQN") if chain is None else bool(chain)
+        if self.target_after_env and not (self.fused2 is not None and self.graphs and self._chained()):
+            # the knob orders two nodes of the chained AC-IQN graph; anywhere else it would be silently ignored
+            # and a bench config recording it would be mislabelled
+            raise ValueError("target_after_env applies only to the chained, graph-captured AC-IQN schedule")
         self.ring_snap2 = torch.zeros((2, 2), dtype=torch.int64, device=self.device)
         self._gen = torch.Generator(device=self.device)
         self._gen.manual_seed(seed + 12345)

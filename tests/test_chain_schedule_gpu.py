@@ -52,6 +52,15 @@ def test_chained_schedule_target_after_env_matches_joined():
     _same(a, pa, la, b, pb, lb)
 
 
+def test_target_after_env_refused_where_it_would_be_ignored():
+    """The knob orders two nodes of the chained graph: on the joined schedule or without graphs it would do
+    nothing, so the constructor refuses it instead of letting a bench config record it."""
+    from distributional_rl_decision_and_control_amd.vec_trainer import VecTrainer
+    for kw in (dict(chain=False, graphs=True, unroll=2), dict(chain=True, graphs=False, unroll=2)):
+        with pytest.raises(ValueError, match="target_after_env"):
+            VecTrainer(n_envs=64, agent_type="AC-IQN", batch_size=64, num_tau=32, seed=1, target_after_env=True, **kw)
+
+
 def test_chained_schedule_bench_shape_after_pool_wrap():
     from distributional_rl_decision_and_control_amd import streams
     pool = [torch.cuda.Stream() for _ in range(40)]   # torch's pool (32 per device) wraps around
