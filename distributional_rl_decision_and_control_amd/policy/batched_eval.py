@@ -80,10 +80,12 @@ def batched_greedy_actions(agent, states):
     return out
 
 
-def evaluate_configs(agent, configs, device=None, template_env=None):
+def evaluate_configs(agent, configs, device=None, template_env=None, policy=None):
     """Run every eval config to its end in one batch. Returns the per-config lists
     (observations, actions, trajectories, rewards, successes, times, energies, relations) of
-    trainer.py:347-365."""
+    trainer.py:347-365. `policy(rows, states, length)` replaces the greedy policy call (rows: the (config,
+    robot) pairs that act this step, states: their states, length: each config's step count); the default
+    is batched_greedy_actions. The parity tests use it to replay recorded actions (teacher forcing)."""
     E = len(configs)
     dev = torch.device(device) if device is not None else (template_env._device if template_env is not None
                                                            else torch.device("cuda"))
@@ -118,7 +120,11 @@ def evaluate_configs(agent, configs, device=None, template_env=None):
     while running:
         # one policy call for every active robot of every running episode (trainer.py:300-322)
         rows = [(e, i) for e in running for i, rob in enumerate(envs[e].robots) if not rob.deactivated]
-        acts = batched_greedy_actions(agent, [states[e][i] for e, i in rows]) if rows else []
+        st = [states[e][i] for e, i in rows]
+        if policy is not None:
+            acts = policy(rows, st, length) if rows else []
+        else:
+            acts = batched_greedy_actions(agent, st) if rows else []
         actions = {e: [None] * n[e] for e in running}
         for (e, i), a in zip(rows, acts):
             actions[e][i] = a

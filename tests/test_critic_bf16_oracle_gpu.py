@@ -8,14 +8,15 @@ seeded initial weights) and a B = 4096 random batch (the bench shape: 2048 round
 the partials reduced by asvrl_partial_sums). The restatement reads the same target quantiles q_next the
 launch read (the target critic's kernel output), so the comparison isolates the fused launch.
 
-Bars: loss and gradient norm within 1e-4 rel.; every critic gradient tensor within 1e-4 of
-its scale (max |g|) -- or, where larger, three times the spread of the same restatement evaluated in f32
-(critic_step_bf16(dtype=float32)): at B = 4096 that spread itself reaches 1.6e-4 of scale (bf16 rounding
-boundaries turn the f32-vs-f64 summation difference into whole-ulp operand changes), so it is the floor any
-f32 implementation of these rounding points meets. Measured (r04e): the reference batch within 1e-4 everywhere;
-B = 4096 worst 1.66e-4 against a spread of 1.64e-4 on the same tensor; loss 6e-8 rel. Round-3's bf16 bars were
-2e-2 / 5e-2 against the f32 reference; this pins the benched arithmetic itself (its indexing, stage-ahead
-buffers and reductions): an indexing slip that moves the loss by 1 % moves whole gradient tensors by far more.
+Bars, fixed up front: loss and gradient norm within 1e-4 rel.; every critic gradient
+tensor within 2e-4 of its scale (max |g|) element-wise and within 1e-4 relative in L2. The element bar sits above
+1e-4 because the restatement's own f32 evaluation (critic_step_bf16(dtype=float32), printed beside each tensor)
+already spreads up to 1.6e-4 of scale at B = 4096 on hidden_layer_2.weight: bf16 rounding boundaries turn an
+f32-vs-f64 summation difference into whole-ulp operand changes, so any f32 implementation of these rounding
+points meets that floor. Measured (r04e): the reference batch within 1e-4 everywhere; B = 4096 worst 1.66e-4
+(hidden_layer_2.weight; its f32 spread 1.64e-4); loss 6e-8 rel. Round-3's bf16 bars were 2e-2 / 5e-2 against the
+f32 reference; this pins the benched arithmetic itself (its indexing, stage-ahead buffers and reductions): an
+indexing slip that moves the loss by 1 % moves whole gradient tensors by far more.
 """
 import numpy as np
 import pytest
@@ -26,7 +27,8 @@ from oracle import learn_ref as lr
 
 pytestmark = pytest.mark.gpu
 
-BAR = 1e-4
+BAR = 1e-4        # loss, gradient norm, per-tensor relative L2
+BAR_ELEM = 2e-4   # per-tensor max |error| / max |g|
 
 
 def _run(rows, taus, N, weights=None):
@@ -75,7 +77,8 @@ def _check(rows, taus, N, weights=None):
         err = float((g[n] - ref[n]).abs().max()) / scale
         spread = float((g32[n].double() - ref[n]).abs().max()) / scale
         worst = max(worst, err)
-        print(f"{n:28s} err/scale {err:.2e}  (f32 restatement {spread:.2e})  scale {scale:.3e}")
+        l2 = float((g[n] - ref[n]).norm() / ref[n].norm())
+        print(f"{n:28s} err/scale {err:.2e}  L2 {l2:.2e}  (f32 restatement {spread:.2e})  scale {scale:.3e}")
     gn = float(torch.sqrt(sum((v * v).sum() for v in g.values())))
     rn = float(torch.sqrt(sum((v * v).sum() for v in ref.values())))
     print(f"loss kernel {loss:.7f} restatement {ref_loss:.7f} (f32 {l32:.7f}); norm {gn:.6f} vs {rn:.6f}; "
@@ -84,12 +87,11 @@ def _check(rows, taus, N, weights=None):
     np.testing.assert_allclose(gn, rn, rtol=BAR)
     for n in ref:
         scale = float(ref[n].abs().max()) + 1e-30
-        spread = float((g32[n].double() - ref[n]).abs().max()) / scale
         err = float((g[n] - ref[n]).abs().max()) / scale
-        assert err < max(BAR, 3 * spread), (n, err, spread)
+        assert err < BAR_ELEM, (n, err)
         # the whole tensor, not just its worst element: relative L2 error
-        assert float((g[n] - ref[n]).norm() / ref[n].norm()) < max(BAR, 3 * float((g32[n].double() - ref[n]).norm()
-                                                                                 / ref[n].norm())), n
+        l2 = float((g[n] - ref[n]).norm() / ref[n].norm())
+        assert l2 < BAR, (n, l2)
 
 
 def test_benched_critic_launch_on_the_reference_batch():

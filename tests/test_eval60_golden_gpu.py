@@ -6,9 +6,11 @@ initial agent ('init': 41 of its 60 episodes run to the 1000-step limit) and the
 reference train_AC_IQN steps ('trained': 32 timeouts, the rest collisions after 8-413 steps).
 
 Same configs, weights and seeds. Per config: success and mean time exact, every robot's episode length exact;
-mean discounted return and mean energy within 1e-5 relative (the north star's return bar) on at least 54 of
-the 60 configs and within 1e-3 on all (the closed loop carries the batched GPU policy's f32 rounding forward
-over up to 1000 steps); final trajectory rows within 1e-3 absolute (observed 2.8e-4 after 1000 steps).
+mean discounted return within 1e-5 relative (the north star's return bar) on at least 58 ('init') / all 60
+('trained') configs and within 5e-4 on all (the closed loop carries the batched GPU policy's f32 rounding forward
+over up to 1000 steps; the teacher-forced replay of the same episodes holds 1e-5 everywhere,
+tests/test_eval60_teacher_forced_gpu.py); mean energy within 1e-6 on all; final trajectory rows within 1e-3
+absolute (observed 2.8e-4 after 1000 steps).
 Observed (r04g): 'init' returns within 1e-5 on 58 of 60 configs (the other two 2e-4), 'trained' on all 60
 (max 1.3e-6); energies within 6e-8 everywhere."""
 import json
@@ -62,10 +64,12 @@ def test_evaluation_on_the_shipped_schedule(tag):
     np.testing.assert_array_equal(np.array(tr.eval_times[0]), z[p + "times"])
     np.testing.assert_array_equal(np.array([len(ep) for ep in tr.eval_trajectories[0]]), z[p + "robots"])
     np.testing.assert_array_equal(np.array(lens), z[p + "traj_len"])
-    # returns and energies: the north star's 1e-5 on the large majority of configs; over 1000 closed-loop steps
-    # the batched f32 policy's summation order (vs the reference's batch-1 CPU GEMM) drifts a few configs
-    # further (r04g: 'init' 58 of 60 within 1e-5, the other two at 2e-4; 'trained' all 60 within 1.3e-6; energies
-    # all within 6e-8): bounded at 1e-3
-    assert (rr <= 1e-5).sum() >= 54 and rr.max() < 1e-3, rr
-    assert (re <= 1e-5).sum() >= 54 and re.max() < 1e-3, re
+    # returns and energies: the north star's 1e-5 where the closed loop lets it hold. Over up to 1000 closed-loop
+    # steps the batched f32 policy's rounding (vs the reference's batch-1 CPU GEMM) moves two 'init' configs
+    # further (r04g: 58 of 60 within 1e-5, the other two at 2e-4; 'trained' all 60 within 1.3e-6; energies all
+    # within 6e-8). The same episodes replayed teacher-forced on the reference's own actions are within 1e-5 on
+    # all 60 (tests/test_eval60_teacher_forced_gpu.py), which pins the env path and attributes the two to the
+    # policy's per-step rounding. Bars: what was observed, with a small margin
+    assert (rr <= 1e-5).sum() >= (58 if tag == "init" else 60) and rr.max() < 5e-4, rr
+    assert re.max() < 1e-6, re
     assert d.max() < 1e-3   # r04g: 2.8e-4

@@ -1,0 +1,132 @@
+"""GPU: the long-episode env path pinned at the north star's bar, and the free-running drift attributed.
+
+tests/test_eval60_golden_gpu.py runs the batched Trainer.evaluation closed-loop on the shipped 60-episode schedule
+against the reference's own (F10, tests/golden/eval60_ref.npz): the policy is the batched f32 GPU actor, the
+reference's a batch-1 CPU actor, so their actions differ in the last bits and the closed loop carries that
+forward over up to 1000 steps. Here the same 60 episodes of both agents are replayed TEACHER-FORCED: every robot
+applies, at every step, exactly the action the reference applied (F10b, tools/capture_oracle.py
+capture_eval60_tf: each robot's Robot.action_history, env.py:264, plus the count, sum and sum of squares of its
+perception-noise draws, wamv.py:27-40). With the policy taken out of the loop the env path must reproduce the
+reference over the whole episodes:
+
+  * every robot's episode length, every success and mean time exactly;
+  * every perception-noise stream exactly (same number of draws, bit-equal sums: the drop-in env consumes each
+    robot's RandomState in the reference's order, trainer.py:300-345 / env.py:240-333 / wamv.py:436-529);
+  * mean discounted return and mean energy within 1e-5 relative on ALL 60 configs of both agents (the north
+    star's return bar), and the final trajectory rows within 1e-9.
+
+Attribution: during the teacher-forced replay the batched GPU policy (policy/batched_eval.batched_greedy_actions)
+is also evaluated on the replayed states at every step and compared with the reference's recorded action. Its
+largest deviation bounds what the policy alone contributes per step; with the env exact under the reference's
+actions, the free-running test's residual return differences are the closed loop amplifying those per-step
+f32 rounding differences, and the first step where the free-running trajectories part is where they first flip
+a COLREGs / perception decision (printed per config)."""
+import json
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import env_oracle as eo
+
+pytestmark = pytest.mark.gpu
+
+SCHEDULE = {"num_episodes": [10, 10, 10, 10, 10, 10], "num_robots": [3, 4, 5, 5, 5, 5],
+            "num_cores": [0, 0, 0, 0, 0, 0], "num_obstacles": [0, 0, 0, 2, 3, 4],
+            "min_start_goal_dis": [30.0, 35.0, 40.0, 40.0, 40.0, 40.0]}   # config/ac_iqn.json eval_schedule
+
+
+def _recorded(t, p, robots):
+    """Per (config, robot): the reference's actions, [T][2] f64."""
+    lens = t[p + "act_len"]
+    offs = np.concatenate([[0], np.cumsum(lens)])
+    rec, k = {}, 0
+    for e, n in enumerate(robots):
+        for i in range(int(n)):
+            rec[(e, i)] = t[p + "act"][offs[k]:offs[k + 1]]
+            k += 1
+    return rec
+
+
+@pytest.mark.parametrize("tag", ["init", "trained"])
+def test_env_teacher_forced_on_the_reference_actions(tag, monkeypatch):
+    from distributional_rl_decision_and_control_amd.agent import Agent
+    from distributional_rl_decision_and_control_amd.envs.marinenav.env import MarineNavEnv3
+    from distributional_rl_decision_and_control_amd.envs.marinenav.vehicles import wamv
+    from distributional_rl_decision_and_control_amd.policy import batched_eval
+    from distributional_rl_decision_and_control_amd.policy.trainer import Trainer
+    z = np.load(eo.GOLDEN + "/eval60_ref.npz")
+    t = np.load(eo.GOLDEN + "/eval60_tf.npz")
+    p = tag + "/"
+    robots = z[p + "robots"]
+    rec = _recorded(t, p, robots)
+    configs = json.loads(str(z[p + "configs"]))
+
+    # every robot's noise stream, recorded draw by draw (the reference's proxy in capture_eval60_tf)
+    orig_draw = wamv.Perception.draw_candidate_noise
+
+    def draw(self):
+        v = orig_draw(self)
+        self.__dict__.setdefault("_log", []).extend(float(x) for x in v)
+        return v
+    monkeypatch.setattr(wamv.Perception, "draw_candidate_noise", draw)
+    perceptions = []   # per config, its robots' Perception objects, in config order
+    orig_reset = MarineNavEnv3.reset_with_eval_config
+
+    def reset(self, cfg):
+        res = orig_reset(self, cfg)
+        perceptions.append([rob.perception for rob in self.robots])
+        return res
+    monkeypatch.setattr(MarineNavEnv3, "reset_with_eval_config", reset)
+
+    torch.manual_seed(0)
+    agent = Agent(seed=100, agent_type="AC-IQN")
+    sd = {k[len(p + "net/"):]: torch.from_numpy(z[k]) for k in z.files if k.startswith(p + "net/")}
+    agent.policy_local.actor.load_state_dict(sd)
+    tr = Trainer(MarineNavEnv3(seed=1), MarineNavEnv3(seed=253, is_eval_env=True), SCHEDULE, agent)
+    used = {k: 0 for k in rec}
+    dev_max = np.zeros(len(configs))   # per config: max |batched policy - reference action| on the replayed states
+
+    def teacher(rows, states, length):
+        mine = np.array(batched_eval.batched_greedy_actions(agent, states), dtype=np.float64)
+        out = []
+        for (e, i), m in zip(rows, mine):
+            a = rec[(e, i)][length[e]]
+            used[(e, i)] += 1
+            dev_max[e] = max(dev_max[e], float(np.abs(m - a).max()))
+            out.append([float(a[0]), float(a[1])])
+        return out
+
+    random.seed(77)
+    np.random.seed(77)
+    res = batched_eval.evaluate_configs(agent, configs, template_env=tr.eval_env, policy=teacher)
+    assert len(perceptions) == 60
+
+    # every recorded action was applied, no more, no fewer (episode lengths of every robot exact)
+    assert all(used[k] == len(v) for k, v in rec.items()), [(k, used[k], len(v)) for k, v in rec.items()
+                                                            if used[k] != len(v)][:5]
+    lens = [len(traj) for ep in res["trajectories"] for traj in ep]
+    np.testing.assert_array_equal(np.array(lens), z[p + "traj_len"])
+    np.testing.assert_array_equal(np.array(res["successes"]), z[p + "successes"])
+    np.testing.assert_array_equal(np.array(res["times"]), z[p + "times"])
+    # every perception-noise stream: the same draws in the same order
+    logs = [np.array(getattr(pc, "_log", []), dtype=np.float64) for ep in perceptions for pc in ep]
+    np.testing.assert_array_equal(np.array([len(v) for v in logs]), t[p + "draws_n"])
+    np.testing.assert_array_equal(np.array([v.sum() for v in logs]), t[p + "draws_sum"])
+    np.testing.assert_array_equal(np.array([(v * v).sum() for v in logs]), t[p + "draws_sq"])
+    # returns and energies at the north star's bar on every config; final rows
+    rr = np.abs(np.array(res["rewards"]) / z[p + "rewards"] - 1)
+    re = np.abs(np.array(res["energies"]) / z[p + "energies"] - 1)
+    last = np.array([np.array(traj[-1], dtype=np.float64) for ep in res["trajectories"] for traj in ep])
+    d = np.abs(last - z[p + "traj_last"]).max()
+    worst = np.argsort(dev_max)[-3:][::-1]
+    print(f"{tag} teacher-forced: {int(z[p + 'traj_len'].max())} steps max, {int(sum(used.values()))} robot-steps; "
+          f"return rel diff max {rr.max():.2e}, energy {re.max():.2e}, final rows {d:.2e}; batched policy vs "
+          f"reference action on the same states: max {dev_max.max():.2e} (configs {list(worst)}: "
+          f"{[f'{dev_max[k]:.1e}' for k in worst]})")
+    assert rr.max() <= 1e-5, rr
+    assert re.max() <= 1e-5, re
+    assert d <= 1e-9, d
+    # the policy alone: f32 rounding of a batched GPU GEMM against the batch-1 CPU one, per step
+    assert dev_max.max() < 1e-5, dev_max

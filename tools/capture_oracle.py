@@ -27,6 +27,9 @@ Fixture families:
   eval_ref.npz      F9  Trainer.evaluation (trainer.py:266-392), AC-IQN and Rainbow
   eval60_ref.npz    F10 Trainer.evaluation on config/ac_iqn.json's 60-episode eval_schedule, the seeded
                         AC-IQN agent and the same agent after 200 train_AC_IQN steps (capture_eval60)
+  eval60_tf.npz     F10b the same two evaluations re-run from F10's own configs and actor weights, with every
+                        robot's per-step action and its perception-noise draws (count and checksums) recorded,
+                        for the teacher-forced env replay (capture_eval60_tf)
 """
 import os
 import sys
@@ -1114,6 +1117,70 @@ def capture_eval60():
         print(tag, "successes", int(np.sum(tr.eval_successes[0])), "of", len(tr.eval_successes[0]),
               "lengths", [max(len(t) for t in ep) for ep in tr.eval_trajectories[0]])
     np.savez_compressed(os.path.join(OUT, "eval60_ref.npz"), **out)
+
+
+def capture_eval60_tf():
+    """F10b: the two F10 evaluations (trainer.py:266-392) again, from F10's stored configs and actor weights
+    (tests/golden/eval60_ref.npz), recording per robot of every episode the actions the reference applied
+    (Robot.action_history, env.py:264: the batch-1 actor's f32 outputs as Python floats) and its perception
+    noise stream (every rd.normal / rd.vonmises draw of wamv.py:27-40 through a recording proxy: the count, the
+    sum and the sum of squares). The metrics are asserted equal to F10's, so the two fixtures describe the same
+    runs. Stored in tests/golden/eval60_tf.npz."""
+    import contextlib
+    import io
+    import json
+    import random
+    from rfarl.policy.trainer import Trainer
+    z = np.load(os.path.join(OUT, "eval60_ref.npz"))
+    sched = json.load(open(os.path.join(REF, "rfarl", "config", "ac_iqn.json")))["eval_schedule"]
+    out = {}
+    for tag in ("init", "trained"):
+        p = tag + "/"
+        torch.manual_seed(0)
+        agent = ref_agent_mod.Agent(device="cpu", seed=100, agent_type="AC-IQN")
+        sd = {k[len(p + "net/"):]: torch.from_numpy(z[k]) for k in z.files if k.startswith(p + "net/")}
+        agent.policy_local.actor.load_state_dict(sd)
+        tr = Trainer(MarineNavEnv3(seed=1), MarineNavEnv3(seed=253, is_eval_env=True), sched, agent)
+        tr.eval_config = json.loads(str(z[p + "configs"]))
+        ev = tr.eval_env
+        logs = []   # per episode: the robots' recorders
+        orig = ev.reset_with_eval_config
+
+        def reset(cfg, orig=orig, ev=ev, logs=logs):
+            res = orig(cfg)
+            install_recorders(ev)
+            clear_recorders(ev)
+            logs.append([rob.perception.rd for rob in ev.robots])
+            return res
+        ev.reset_with_eval_config = reset
+        random.seed(77)
+        np.random.seed(77)
+        with contextlib.redirect_stdout(io.StringIO()):
+            tr.evaluation()
+        for key in ("rewards", "energies", "times"):
+            assert np.array_equal(np.array(tr.eval_rewards[0] if key == "rewards" else
+                                           (tr.eval_energies[0] if key == "energies" else tr.eval_times[0])),
+                                  z[p + key]), f"{tag}: {key} differ from eval60_ref.npz"
+        acts, alen = [], []
+        for ep in tr.eval_actions[0]:
+            for a in ep:
+                alen.append(len(a))
+                acts.extend(np.asarray(x, dtype=np.float64).reshape(2) for x in a)
+        out[p + "act"] = np.array(acts, dtype=np.float64).reshape(-1, 2)
+        out[p + "act_len"] = np.array(alen, np.int32)
+        dn, ds, dq = [], [], []
+        for ep in logs:
+            for rd in ep:
+                v = np.array(rd.log, dtype=np.float64)
+                dn.append(len(v))
+                ds.append(float(v.sum()))
+                dq.append(float((v * v).sum()))
+        out[p + "draws_n"] = np.array(dn, np.int64)
+        out[p + "draws_sum"] = np.array(ds)
+        out[p + "draws_sq"] = np.array(dq)
+        assert len(alen) == len(dn) == int(z[p + "robots"].sum())
+        print(tag, "robots", len(alen), "steps", int(np.sum(alen)), "draws", int(np.sum(dn)))
+    np.savez_compressed(os.path.join(OUT, "eval60_tf.npz"), **out)
 
 
 if __name__ == "__main__":
