@@ -146,7 +146,7 @@ __device__ __forceinline__ void mfma_drain() {
 // Phase timing (tools/fused_stamps.py; a variant build with -DASVRL_FUSED_STAMPS, never the shipped
 // library): lane 0 of every wave records s_memtime before and after each of the round's barriers.
 #ifdef ASVRL_FUSED_STAMPS
-constexpr int kStampRounds = 8, kStamps = 16;
+constexpr int kStampRounds = 8, kStamps = 32;   // 0..15: barriers (arrival, release); 16..: marks inside phases
 __device__ uint64_t g_stamps[1024 * kNW * kStampRounds * kStamps];
 #define ASVRL_STAMP(k)                                                                                   \
   do {                                                                                                   \
@@ -782,6 +782,7 @@ void critic_fused_kernel(FusedArgs a) {
             rows(L.x, RA_x, j, 2 * mb + s, xo);
           }
         }
+        if (mq == 0) ASVRL_STAMP(16);
       }
 #pragma unroll
       for (int ks = 0; ks < kC / 16; ++ks) w1f[ks] = W1[(w * 16 + ks) * 64 + lane];
@@ -807,6 +808,7 @@ void critic_fused_kernel(FusedArgs a) {
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[j] = acc_init(b1p, w * 32, h);
       mfma_rows<kC / 16, NB>(acc, L.x, RA_x, [&](int ks) { return w1f[ks]; });
+      ASVRL_STAMP(17);
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) w2f[ks] = W2[(w * 8 + ks) * 64 + lane];
 #if ASVRL_PRE_AT == 1
@@ -848,6 +850,7 @@ void critic_fused_kernel(FusedArgs a) {
 #pragma unroll
       for (int j = 0; j < NB; ++j) z2[j] = acc_init(b2p, w * 32, h);
       mfma_rows<kH / 16, NB>(z2, L.a, RA_a, [&](int ks) { return w2f[ks]; });
+      ASVRL_STAMP(18);
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) w2tf[ks] = W2T[(w * 8 + ks) * 64 + lane];
       if constexpr (!kBiasFirst)
@@ -916,6 +919,7 @@ void critic_fused_kernel(FusedArgs a) {
           row_store<64>(L.dz1, lr, 8 * q4, o);
         }
       }
+      ASVRL_STAMP(31);
     }
     ASVRL_STAMP(8);
     __syncthreads();
@@ -987,6 +991,7 @@ void critic_fused_kernel(FusedArgs a) {
                              if (n == 0) db2 += sum8(A);
                              mfma_acc(dW2[n], A, B);
                            });
+      ASVRL_STAMP(19);
     }
     {
       ASVRL_FRESH_LANE();
@@ -1002,7 +1007,7 @@ void critic_fused_kernel(FusedArgs a) {
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[j] = f32x16{};
       mfma_rows<kH / 16, NB>(acc, L.b, RA_b, [&](int ks) { return w2tf[ks]; });
-
+      ASVRL_STAMP(20);
       // dz1 = dh1g G 1[h1 > 0]; dG = sum over the sample's taus of dh1g h1 (-> dzG = dG 1[G > 0])
 #pragma unroll
       for (int j = 0; j < NB; ++j) {   // h1 unpacked here, not earlier
@@ -1025,6 +1030,7 @@ void critic_fused_kernel(FusedArgs a) {
           rows(L.dz1, RA_d, j, 2 * w + s, dz1);
         }
       }
+      ASVRL_STAMP(21);
       if constexpr (!IQN) {
         const bool enc = a.parts.aenc != nullptr;
         sample_sums<NT, NB>(gsa, w * 32, lane, [&](int bl, int p, float v) {
@@ -1079,11 +1085,13 @@ void critic_fused_kernel(FusedArgs a) {
                                if (n == 0) db1 += sum8(A);
                                mfma_acc(dW1[n], A, B);
                              });
+      ASVRL_STAMP(22);
     }
     if constexpr (AH) {   // round t + grid's images, behind the dW1 MFMAs
       const int tn = t + static_cast<int>(gridDim.x);
       if (tn < a.rounds) stage(tn * G / NT, L.in[buf ^ 1], L.cos[buf ^ 1], L.F[buf ^ 1], L.G[buf ^ 1]);
     }
+    ASVRL_STAMP(23);
 
     // ---------------- L4: dx = W1^T dz1 (own blocks 2w, 2w+1) with c = relu(Wc cos + bc) recomputed
     // (bit-identical to L0's); dF = sum over taus of dx c (-> dzF), dzc = dx F 1[c > 0] into the
@@ -1111,6 +1119,7 @@ void critic_fused_kernel(FusedArgs a) {
         mfma_rows<8, NB>(dxs, L.dz1, RA_d, [&](int ks) { return wt[ks]; });
         mfma_rows<4, NB>(ccs, cosb, RA_cos, [&](int ks) { return wcc[ks]; });
       }
+      ASVRL_STAMP(24 + 3 * mq);
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         f32x16 dx, cc;
@@ -1144,12 +1153,14 @@ void critic_fused_kernel(FusedArgs a) {
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) wcc[ks] = WCR ? wcr1[ks] : WC[((2 * w + 1) * 4 + ks) * 64 + lane];
       }
+      ASVRL_STAMP(25 + 3 * mq);
       sample_sums<NT, NB>(fsa, mb * 32, lane, [&](int bl, int p, float v) {
         const float fm = Fb[bl * kC + p];
         const float dz = fm > 0.f ? v : 0.f;
         if (a.dzF != nullptr) bp(a.dzF)[static_cast<size_t>(b0 + bl) * kC + swap23(p)] = (elem_t)dz;
         if (a.parts.enc != nullptr) Fb[bl * kC + p] = dz;   // F's blocks 2w, 2w+1 are this wave's own
       });
+      ASVRL_STAMP(26 + 3 * mq);
     }
     {
       if (a.parts.enc != nullptr) {
@@ -1179,6 +1190,7 @@ void critic_fused_kernel(FusedArgs a) {
       }
     }
 
+    ASVRL_STAMP(30);
     // ---------------- dWc[own 64][:] += dzc^T cos (this wave's own dzc image: in-order LDS, no barrier)
     {
       ASVRL_FRESH_LANE();

@@ -28,13 +28,14 @@ def main():
         _critic_grads("bf16", B, N, True, rows, taus)
     torch.cuda.synchronize()
     L = _abi.lib()
-    n = 1024 * 4 * 8 * 16
+    n = 1024 * 4 * 8 * 32
     buf = (C.c_uint64 * n)()
     L.asvrl_debug_fused_stamps.argtypes = [C.c_void_p, C.c_int64]
     assert L.asvrl_debug_fused_stamps(buf, n) == 0
-    st = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 4, 8, 16).astype(np.float64)
+    allst = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 4, 8, 32).astype(np.float64)
     groups = int(L.asvrl_critic_fused_groups(B, N))
-    st = st[:groups]
+    allst = allst[:groups]
+    st = allst[..., :16]
     arr, rel = st[..., 0::2], st[..., 1::2]          # arrival / release at barrier k
     prev_rel = np.concatenate([np.roll(rel[..., -1:], 1, axis=2), rel[..., :-1]], axis=-1)
     comp = arr - prev_rel
@@ -46,6 +47,17 @@ def main():
         tot += c + w
         print(f"{ph:12s} compute {c:8.0f}  wait {w:8.0f}  (max wait {wait[..., k].max():8.0f})")
     print(f"per round {tot:.0f} cycles; rounds per workgroup {8}, groups {groups}")
+    # marks inside phases (slot, the barrier release the phase starts from): cycles since that release
+    marks = [(16, 1, "L0: first cos block done"), (17, 3, "L1: MFMAs issued+landed"), (18, 5, "L2: MFMAs done"),
+             (31, 7, "loss: computed"), (19, 11, "dW2 grid done"), (20, 11, "L3 MFMAs done"),
+             (21, 11, "L3 epilogue (dz1) done"), (22, 13, "dW1 grid done"), (23, 13, "next-round stage done"),
+             (24, 13, "L4 blk0 MFMAs done"), (25, 13, "L4 blk0 epilogue done"), (26, 13, "L4 blk0 dF sums done"),
+             (27, 13, "L4 blk1 MFMAs done"), (28, 13, "L4 blk1 epilogue done"), (29, 13, "L4 blk1 dF sums done"),
+             (30, 13, "encoder sums done"), (14, 13, "dWc done (phase end)")]
+    rounds = allst[:, :, 1:]
+    for slot, start, label in marks:
+        d = rounds[..., slot] - rounds[..., start]
+        print(f"  mark {slot:2d} {label:28s} {d.mean():8.0f}")
 
 
 if __name__ == "__main__":
