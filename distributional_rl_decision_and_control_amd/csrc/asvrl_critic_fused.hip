@@ -311,14 +311,18 @@ __device__ __forceinline__ void stage_fg(const FusedArgs& a, int b0, int tid, co
 // (agent.py:399-412), split over four lanes: lane quarter q4 (lanes 16 q4 .. 16 q4 + 15 share the
 // row block) takes targets q4 NT/4 .. + NT/4 - 1 from the staged q_next, and the four partial sums
 // are combined by two lane exchanges (a fixed order). Returns dq; *wl = the row's loss sum.
-template <int NT>
+struct NoHook {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+template <int NT, class Hook = NoHook>
 __device__ __forceinline__ float quarter_loss_dq(const FusedArgs& a, const float* qt, float rb, float done, float tau,
-                                                 float q, int q4, float* wl_out) {
+                                                 float q, int q4, float* wl_out, Hook hook = Hook{}) {
   const float nd = 1.0f - done;
   const float kap = a.kappa, hk = 0.5f * a.kappa, omt = 1.f - tau;
   float wl = 0.f, wg = 0.f;
 #pragma unroll
   for (int j = 0; j < NT / 4; ++j) {
+    hook(j);   // independent matrix work issued between the targets' vector arithmetic (ASVRL_DWC_DEFER)
     const float target = rb + (a.gamma * qt[q4 * (NT / 4) + j]) * nd;   // r + gamma * q_next * (1 - d)
     const float d = target - q;   // td_error (agent.py:406)
     const float ad = fabsf(d);
@@ -387,6 +391,14 @@ __device__ __forceinline__ int row_action(const float* in, int bl, int A) {
 // (Measured in round 4 and removed, profiles/r04e_fused_variants_ab.txt: a deeper weight-gradient read-ahead,
 // dW2 + L3 and dW1 + L4 as interleaved MFMA streams, the cos layer's gradient loop a k-step ahead, and the dW2 /
 // dW1 partials stored during the last round -- all bit-identical, none faster.)
+// the cos layer's weight gradient of round t (dWc += dzc^T cos, 16 MFMAs per wave) issued in round t + 1's loss
+// phase, between the quantile-Huber terms (which have no matrix work of their own), instead of at the end of
+// round t: its operands are still intact there -- the wave's own dzc image until round t + 1's L4, round t's cos
+// image in the stage-ahead double buffer until round t + 2 is staged. Same MFMAs per accumulator in the same
+// order: bit-identical. Needs stage-ahead (AH); the last round's is issued after the loop.
+#ifndef ASVRL_DWC_DEFER
+#define ASVRL_DWC_DEFER 1
+#endif
 template <int KS, int NB, int P, class WF>
 __device__ __forceinline__ void mfma_rows(f32x16 (&acc)[NB], const elem_t* img, const RowA<P>& RA, WF wf) {
   constexpr int D = ASVRL_READ_AHEAD < KS ? ASVRL_READ_AHEAD : KS;
@@ -578,6 +590,8 @@ void critic_fused_kernel(FusedArgs a) {
   constexpr int NB = FusedNB<NT>::v, G = 32 * NB, S = G / NT, NA = IQN ? 1 : 2;
   constexpr bool AH = ASVRL_STAGE_AHEAD && (!IQN || ASVRL_STAGE_AHEAD_IQN) && NT == 32 && !ASVRL_OPERAND_F32;
   constexpr int NSB = AH ? 2 : 1;
+  constexpr bool DD = ASVRL_DWC_DEFER && AH;   // the cos layer's gradient one round late (see ASVRL_DWC_DEFER)
+  static_assert(!DD || G / 16 == kNW, "the deferred dWc rides on exactly one 16-row loss group per wave");
   __shared__ __attribute__((aligned(16))) FusedShared<NT, NB, S, IQN, NSB, TQ> U;
   static_assert(sizeof(U) <= 160 * 1024, "fused critic LDS image exceeds the CU's 160 KB");
   auto& L = U.f;
@@ -684,6 +698,31 @@ void critic_fused_kernel(FusedArgs a) {
       wcr1[ks] = WC[((2 * w + 1) * 4 + ks) * 64 + lane];
     }
   }
+  // the cos layer's weight gradient over one round's rows: dWc[own 64][:] += dzc^T cos from the wave's own dzc
+  // image and the round's cos image, in 8 steps (k-step kk = u / 2, cos column block n = u % 2): dwc_load(u)
+  // reads step u's operands, dwc_mfma(u) issues its two MFMAs (one step later, behind other work)
+  frag8 dA0, dA1, dB;
+  auto dwc_load = [&](const elem_t* cosp, int u) {
+    ASVRL_FRESH_LANE();
+    const int wv = __builtin_amdgcn_readfirstlane(tid_ >> 6);
+    const TrA<kNcos> TA_cos(lane);
+    const TrA<kNcos> TA_dzc(lane);
+    const int kk = u >> 1, n = u & 1;
+    if (n == 0) {
+      dA0 = trf(L.dzc[wv], TA_dzc, kk, 0);
+      dA1 = trf(L.dzc[wv], TA_dzc, kk, 1);
+    }
+    dB = trf(cosp, TA_cos, kk, n);
+  };
+  auto dwc_mfma = [&](int u) {
+    const int n = u & 1;
+    if (n == 0) {
+      dbc0 += sum8(dA0);
+      dbc1 += sum8(dA1);
+    }
+    mfma_acc(dWc[n], dA0, dB);
+    mfma_acc(dWc[2 + n], dA1, dB);
+  };
   float encr[IQN ? 8 : 1];   // IQN with parts.enc: this lane's feature's encoder sums
 #pragma unroll
   for (int i = 0; i < (IQN ? 8 : 1); ++i) encr[i] = 0.f;
@@ -900,8 +939,26 @@ void critic_fused_kernel(FusedArgs a) {
         const float bo = IQN ? L.boA[ai] : L.bias[kC + 3 * kH];
         const float q = (((L.qpart[0][lr] + L.qpart[1][lr]) + L.qpart[2][lr]) + L.qpart[3][lr]) + bo;
         float wl;
-        const float dq = quarter_loss_dq<NT>(a, in + IL::kQn + bl * NT, in[IL::kRew + bl], in[IL::kDon + bl],
-                                             in[IL::kTau + lr], q, q4, &wl);
+        float dq;
+        if constexpr (DD) {
+          // the previous round's cos-layer gradient (its cos image is the other buffer of the pair), two MFMAs
+          // per quantile target
+          const bool prev = t != static_cast<int>(blockIdx.x);   // workgroup-uniform
+          const elem_t* cosp = L.cos[sb ^ 1];
+          dq = quarter_loss_dq<NT>(a, in + IL::kQn + bl * NT, in[IL::kRew + bl], in[IL::kDon + bl], in[IL::kTau + lr],
+                                   q, q4, &wl, [&](int j) {
+                                     static_assert(NT / 4 == 2 * (G / 16), "one dWc step per target");
+                                     if (prev) {
+                                       if (j > 0) dwc_mfma(j - 1);
+                                       dwc_load(cosp, j);
+                                     }
+                                     __builtin_amdgcn_sched_barrier(0);
+                                   });
+          if (prev) dwc_mfma(NT / 4 - 1);
+        } else {
+          dq = quarter_loss_dq<NT>(a, in + IL::kQn + bl * NT, in[IL::kRew + bl], in[IL::kDon + bl],
+                                   in[IL::kTau + lr], q, q4, &wl);
+        }
         if (a.tile_loss != nullptr) {
           const float v = seg_sum<16>(wl);   // every lane of the 16-lane row: the group's sum
           if (lane == 0) L.tsum[g] = v;
@@ -1191,8 +1248,9 @@ void critic_fused_kernel(FusedArgs a) {
     }
 
     ASVRL_STAMP(30);
-    // ---------------- dWc[own 64][:] += dzc^T cos (this wave's own dzc image: in-order LDS, no barrier)
-    {
+    // ---------------- dWc[own 64][:] += dzc^T cos (this wave's own dzc image: in-order LDS, no barrier);
+    // with DD in the next round's loss phase instead
+    if constexpr (!DD) {
       ASVRL_FRESH_LANE();
       const TrA<kNcos> TA_cos(lane);
       const TrA<kNcos> TA_dzc(lane);
@@ -1222,6 +1280,14 @@ void critic_fused_kernel(FusedArgs a) {
     ASVRL_STAMP(15);
   }
 
+  if constexpr (DD) {   // the last round's cos-layer gradient (its images are intact: the loop ended on a barrier)
+    const elem_t* cosp = L.cos[buf ^ 1];
+#pragma unroll
+    for (int u = 0; u < 2 * (G / 16); ++u) {
+      dwc_load(cosp, u);
+      dwc_mfma(u);
+    }
+  }
   // ---------------- the workgroup's partials: [M*K + M] per layer, features in natural order
   mfma_drain();
   {
