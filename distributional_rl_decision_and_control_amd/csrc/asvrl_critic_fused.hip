@@ -702,17 +702,15 @@ void critic_fused_kernel(FusedArgs a) {
   // image and the round's cos image, in 8 steps (k-step kk = u / 2, cos column block n = u % 2): dwc_load(u)
   // reads step u's operands, dwc_mfma(u) issues its two MFMAs (one step later, behind other work)
   frag8 dA0, dA1, dB;
-  auto dwc_load = [&](const elem_t* cosp, int u) {
-    ASVRL_FRESH_LANE();
-    const int wv = __builtin_amdgcn_readfirstlane(tid_ >> 6);
-    const TrA<kNcos> TA_cos(lane);
-    const TrA<kNcos> TA_dzc(lane);
+  // (TA: the lane's transposed-read offsets, the same for both images (64 positions per row), computed once per
+  // phase by the caller; dzcp: the wave's own dzc image)
+  auto dwc_load = [&](const elem_t* cosp, const elem_t* dzcp, const TrA<kNcos>& TA, int u) {
     const int kk = u >> 1, n = u & 1;
     if (n == 0) {
-      dA0 = trf(L.dzc[wv], TA_dzc, kk, 0);
-      dA1 = trf(L.dzc[wv], TA_dzc, kk, 1);
+      dA0 = trf(dzcp, TA, kk, 0);
+      dA1 = trf(dzcp, TA, kk, 1);
     }
-    dB = trf(cosp, TA_cos, kk, n);
+    dB = trf(cosp, TA, kk, n);
   };
   auto dwc_mfma = [&](int u) {
     const int n = u & 1;
@@ -945,12 +943,13 @@ void critic_fused_kernel(FusedArgs a) {
           // per quantile target
           const bool prev = t != static_cast<int>(blockIdx.x);   // workgroup-uniform
           const elem_t* cosp = L.cos[sb ^ 1];
+          const TrA<kNcos> TA_d(lane);
           dq = quarter_loss_dq<NT>(a, in + IL::kQn + bl * NT, in[IL::kRew + bl], in[IL::kDon + bl], in[IL::kTau + lr],
                                    q, q4, &wl, [&](int j) {
                                      static_assert(NT / 4 == 2 * (G / 16), "one dWc step per target");
                                      if (prev) {
                                        if (j > 0) dwc_mfma(j - 1);
-                                       dwc_load(cosp, j);
+                                       dwc_load(cosp, dzc_w, TA_d, j);
                                      }
                                      __builtin_amdgcn_sched_barrier(0);
                                    });
@@ -1282,9 +1281,11 @@ void critic_fused_kernel(FusedArgs a) {
 
   if constexpr (DD) {   // the last round's cos-layer gradient (its images are intact: the loop ended on a barrier)
     const elem_t* cosp = L.cos[buf ^ 1];
+    const TrA<kNcos> TA_d(lane);
+    const elem_t* dzcp = L.dzc[w];
 #pragma unroll
     for (int u = 0; u < 2 * (G / 16); ++u) {
-      dwc_load(cosp, u);
+      dwc_load(cosp, dzcp, TA_d, u);
       dwc_mfma(u);
     }
   }
