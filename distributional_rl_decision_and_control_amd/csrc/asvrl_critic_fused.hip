@@ -198,6 +198,36 @@ struct InLayout {
   static constexpr int kPer = (kSize + kNW * 64 - 1) / (kNW * 64);   // elements per thread
 };
 
+// Each lane's swizzled-image bases (RowA / TrA of the 64-, 128- and 256-position images), computed once per
+// launch into LDS: a phase reads its two or three with one or two ds_read instead of ~10 (RowA) / ~25 (TrA) VALU
+// instructions each -- the round's vector issue, not its matrix work, sets its length (ASVRL_LANE_TABLE).
+#ifndef ASVRL_LANE_TABLE
+#define ASVRL_LANE_TABLE 1
+#endif
+struct LaneBases {
+  int r64, r128, r256, t64lo, t64hi, t128lo, t128hi, t256lo, t256hi, pad[3];
+};
+
+template <int P, bool LT>
+__device__ __forceinline__ RowA<P> row_base(const LaneBases* LB, int lane, int r, int h) {
+  if constexpr (LT) {
+    const LaneBases& b = LB[lane];
+    return RowA<P>(RawBase{}, P == 64 ? b.r64 : (P == 128 ? b.r128 : b.r256));
+  } else {
+    return RowA<P>(r, h);
+  }
+}
+template <int P, bool LT>
+__device__ __forceinline__ TrA<P> tr_base(const LaneBases* LB, int lane) {
+  if constexpr (LT) {
+    const LaneBases& b = LB[lane];
+    return P == 64 ? TrA<P>(RawBase{}, b.t64lo, b.t64hi)
+                   : (P == 128 ? TrA<P>(RawBase{}, b.t128lo, b.t128hi) : TrA<P>(RawBase{}, b.t256lo, b.t256hi));
+  } else {
+    return TrA<P>(lane);
+  }
+}
+
 template <int NT, int NB, int S, bool IQN, int NSB>
 struct FusedLds {
   elem_t cos[NSB][32 * NB * kNcos];   // natural order (the cos layer is input-fed); NSB = 2: stage-ahead
@@ -594,9 +624,30 @@ void critic_fused_kernel(FusedArgs a) {
   static_assert(!DD || G / 16 == kNW, "the deferred dWc rides on exactly one 16-row loss group per wave");
   __shared__ __attribute__((aligned(16))) FusedShared<NT, NB, S, IQN, NSB, TQ> U;
   static_assert(sizeof(U) <= 160 * 1024, "fused critic LDS image exceeds the CU's 160 KB");
+  constexpr bool LT = ASVRL_LANE_TABLE && sizeof(U) + 64 * sizeof(LaneBases) <= 160 * 1024;
+  __shared__ LaneBases LB[LT ? 64 : 1];
   auto& L = U.f;
   if constexpr (TQ) target_phase<NT, NB>(a.tq, U.t, a.rounds);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
+  if constexpr (LT) {   // read after the prologue's barrier
+    if (threadIdx.x < 64) {
+      LaneBases b;
+      b.r64 = RowA<kNcos>(r, h).base;
+      b.r128 = RowA<kH>(r, h).base;
+      b.r256 = RowA<kC>(r, h).base;
+      const TrA<kNcos> t64 = tr_base<kNcos, LT>(LB, lane);
+      const TrA<kH> t128 = tr_base<kH, LT>(LB, lane);
+      const TrA<kC> t256 = tr_base<kC, LT>(LB, lane);
+      b.t64lo = t64.lo;
+      b.t64hi = t64.hi;
+      b.t128lo = t128.lo;
+      b.t128hi = t128.hi;
+      b.t256lo = t256.lo;
+      b.t256hi = t256.hi;
+      b.pad[0] = b.pad[1] = b.pad[2] = 0;
+      LB[lane] = b;
+    }
+  }
   const frag8* WC = reinterpret_cast<const frag8*>(a.w.wc_frag);
   const frag8* W1 = reinterpret_cast<const frag8*>(a.w.w1_frag);
   const frag8* W2 = reinterpret_cast<const frag8*>(a.w.w2_frag);
@@ -784,8 +835,8 @@ void critic_fused_kernel(FusedArgs a) {
     frag8 w1f[16];
     {
       ASVRL_FRESH_LANE();
-      const RowA<kNcos> RA_cos(r, h);
-      const RowA<kC> RA_x(r, h);
+      const RowA<kNcos> RA_cos = row_base<kNcos, LT>(LB, lane, r, h);
+      const RowA<kC> RA_x = row_base<kC, LT>(LB, lane, r, h);
       // the cos rows' operand fragments are the same for both blocks: with read-ahead, all read first
       frag8 cb[ASVRL_READ_AHEAD ? NB : 1][4];
       if constexpr (ASVRL_READ_AHEAD != 0) {
@@ -833,8 +884,8 @@ void critic_fused_kernel(FusedArgs a) {
     frag8 w2f[8];
     {
       ASVRL_FRESH_LANE();
-      const RowA<kC> RA_x(r, h);
-      const RowA<kH> RA_a(r, h);
+      const RowA<kC> RA_x = row_base<kC, LT>(LB, lane, r, h);
+      const RowA<kH> RA_a = row_base<kH, LT>(LB, lane, r, h);
       float gv[NB][2][8];
       if constexpr (!IQN)
 #pragma unroll
@@ -881,8 +932,8 @@ void critic_fused_kernel(FusedArgs a) {
     frag8 w2tf[8];
     {
       ASVRL_FRESH_LANE();
-      const RowA<kH> RA_a(r, h);
-      const RowA<kH> RA_b(r, h);
+      const RowA<kH> RA_a = row_base<kH, LT>(LB, lane, r, h);
+      const RowA<kH> RA_b = row_base<kH, LT>(LB, lane, r, h);
       f32x16 z2[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) z2[j] = acc_init(b2p, w * 32, h);
@@ -943,7 +994,7 @@ void critic_fused_kernel(FusedArgs a) {
           // per quantile target
           const bool prev = t != static_cast<int>(blockIdx.x);   // workgroup-uniform
           const elem_t* cosp = L.cos[sb ^ 1];
-          const TrA<kNcos> TA_d(lane);
+          const TrA<kNcos> TA_d = tr_base<kNcos, LT>(LB, lane);
           dq = quarter_loss_dq<NT>(a, in + IL::kQn + bl * NT, in[IL::kRew + bl], in[IL::kDon + bl], in[IL::kTau + lr],
                                    q, q4, &wl, [&](int j) {
                                      static_assert(NT / 4 == 2 * (G / 16), "one dWc step per target");
@@ -987,12 +1038,12 @@ void critic_fused_kernel(FusedArgs a) {
       a.tile_loss[row0 / 32 + threadIdx.x] = (L.tsum[2 * threadIdx.x] + L.tsum[2 * threadIdx.x + 1]) * a.loss_scale;
     {
       ASVRL_FRESH_LANE();
-      const RowA<kH> RA_b(r, h);
+      const RowA<kH> RA_b = row_base<kH, LT>(LB, lane, r, h);
       if constexpr (IQN) {
         // dW_out[:, own] += D^T h2 with D the one-hot dq image (rows = actions): h2 read before the
         // in-place dz2 stores below (same wave, in-order LDS)
-        const TrA<64> TA_o(lane);
-        const TrA<kH> TA_b(lane);
+        const TrA<64> TA_o = tr_base<64, LT>(LB, lane);
+        const TrA<kH> TA_b = tr_base<kH, LT>(LB, lane);
 #pragma unroll
         for (int kk = 0; kk < G / 16; ++kk) {
           const frag8 A = trf(L.dz1, TA_o, kk, 0);
@@ -1039,8 +1090,8 @@ void critic_fused_kernel(FusedArgs a) {
     // slice into the dz1 image, which nobody reads before the next barrier)
     {
       ASVRL_FRESH_LANE();
-      const TrA<kH> TA_a(lane);
-      const TrA<kH> TA_b(lane);
+      const TrA<kH> TA_a = tr_base<kH, LT>(LB, lane);
+      const TrA<kH> TA_b = tr_base<kH, LT>(LB, lane);
       mfma_grid<G / 16, 4>([&](int kk) { return trf(L.b, TA_b, kk, w); },
                            [&](int kk, int n) { return trf(L.a, TA_a, kk, n); },
                            [&](int kk, int n, const frag8& A, const frag8& B) {
@@ -1051,8 +1102,8 @@ void critic_fused_kernel(FusedArgs a) {
     }
     {
       ASVRL_FRESH_LANE();
-      const RowA<kH> RA_b(r, h);
-      const RowA<kH> RA_d(r, h);
+      const RowA<kH> RA_b = row_base<kH, LT>(LB, lane, r, h);
+      const RowA<kH> RA_d = row_base<kH, LT>(LB, lane, r, h);
       float gv[NB][2][8];
       if constexpr (!IQN)
 #pragma unroll
@@ -1129,8 +1180,8 @@ void critic_fused_kernel(FusedArgs a) {
     frag8 wt[8], wcc[4];
     {
       ASVRL_FRESH_LANE();
-      const TrA<kH> TA_d(lane);
-      const TrA<kC> TA_x(lane);
+      const TrA<kH> TA_d = tr_base<kH, LT>(LB, lane);
+      const TrA<kC> TA_x = tr_base<kC, LT>(LB, lane);
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) wt[ks] = W1T[((2 * w) * 8 + ks) * 64 + lane];
 #pragma unroll
@@ -1155,9 +1206,9 @@ void critic_fused_kernel(FusedArgs a) {
 #pragma unroll
     for (int mq = 0; mq < 2; ++mq) {
       ASVRL_FRESH_LANE();
-      const RowA<kNcos> RA_cos(r, h);
-      const RowA<kH> RA_d(r, h);
-      const RowA<kNcos> RA_dzc(r, h);
+      const RowA<kNcos> RA_cos = row_base<kNcos, LT>(LB, lane, r, h);
+      const RowA<kH> RA_d = row_base<kH, LT>(LB, lane, r, h);
+      const RowA<kNcos> RA_dzc = row_base<kNcos, LT>(LB, lane, r, h);
       const int mb = 2 * w + mq;
       float fv[NB][2][8];
 #pragma unroll
@@ -1251,8 +1302,8 @@ void critic_fused_kernel(FusedArgs a) {
     // with DD in the next round's loss phase instead
     if constexpr (!DD) {
       ASVRL_FRESH_LANE();
-      const TrA<kNcos> TA_cos(lane);
-      const TrA<kNcos> TA_dzc(lane);
+      const TrA<kNcos> TA_cos = tr_base<kNcos, LT>(LB, lane);
+      const TrA<kNcos> TA_dzc = tr_base<kNcos, LT>(LB, lane);
 #pragma unroll
         for (int kk = 0; kk < G / 16; ++kk) {
           const frag8 A0 = trf(dzc_w, TA_dzc, kk, 0);
@@ -1281,7 +1332,7 @@ void critic_fused_kernel(FusedArgs a) {
 
   if constexpr (DD) {   // the last round's cos-layer gradient (its images are intact: the loop ended on a barrier)
     const elem_t* cosp = L.cos[buf ^ 1];
-    const TrA<kNcos> TA_d(lane);
+    const TrA<kNcos> TA_d = tr_base<kNcos, LT>(LB, lane);
     const elem_t* dzcp = L.dzc[w];
 #pragma unroll
     for (int u = 0; u < 2 * (G / 16); ++u) {

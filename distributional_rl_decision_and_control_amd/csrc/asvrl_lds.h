@@ -70,9 +70,13 @@ __device__ __forceinline__ int swz(int r) {
   else return ((r & 3) << 2) | ((r >> 2) & 3);
 }
 
+// a precomputed base (asvrl_critic_fused.hip keeps each lane's bases in an LDS table)
+struct RawBase {};
+
 template <int P>
 struct RowA {
   int base;
+  __device__ __forceinline__ RowA(RawBase, int b) : base(b) {}
   __device__ __forceinline__ RowA(int r, int h) {
 #if ASVRL_OPERAND_F32
     base = (r * P + 8 * h) * 4;
@@ -106,6 +110,7 @@ __device__ __forceinline__ void rows(elem_t* img, const RowA<P>& A, int j, int k
 template <int P>
 struct TrA {
   int lo, hi;
+  __device__ __forceinline__ TrA(RawBase, int l, int u) : lo(l), hi(u) {}
   __device__ __forceinline__ TrA(int lane) {
 #if ASVRL_OPERAND_F32
     lo = (8 * (lane >> 5) * P + (lane & 31)) * 4;

@@ -170,3 +170,22 @@ def test_dqn_policy_init_and_forward_vs_reference():
                  torch.tensor(mask).float())).numpy()
     np.testing.assert_allclose(q, z["act/q"], rtol=1e-5, atol=1e-6)
     assert int(q.argmax()) == int(z["act/action"])
+
+
+def test_eval60_teacher_forcing_fixture_matches_the_f10_runs():
+    """F10b (tests/golden/eval60_tf.npz, tools/capture_oracle.py capture_eval60_tf) records the same 60-episode
+    evaluations F10 holds: one action row per robot step (a trajectory holds the start plus one row per step), the
+    reference's f32 actor outputs (exactly representable in f32, within the action range), and per robot a noise
+    stream of five draws per detection candidate."""
+    z = np.load(eo.GOLDEN + "/eval60_ref.npz")
+    t = np.load(eo.GOLDEN + "/eval60_tf.npz")
+    for p in ("init/", "trained/"):
+        lens = t[p + "act_len"]
+        assert len(lens) == int(z[p + "robots"].sum())
+        np.testing.assert_array_equal(z[p + "traj_len"], lens + 1)
+        act = t[p + "act"]
+        assert act.shape == (int(lens.sum()), 2)
+        np.testing.assert_array_equal(act.astype(np.float32).astype(np.float64), act)
+        assert np.abs(act).max() <= 1.0
+        assert (t[p + "draws_n"] % 5 == 0).all() and (t[p + "draws_n"] > 0).all()
+        assert np.isfinite(t[p + "draws_sum"]).all() and (t[p + "draws_sq"] > 0).all()
