@@ -204,7 +204,7 @@ struct InLayout {
 #ifndef ASVRL_LANE_TABLE
 #define ASVRL_LANE_TABLE 1
 #endif
-struct LaneBases {
+struct alignas(16) LaneBases {
   int r64, r128, r256, t64lo, t64hi, t128lo, t128hi, t256lo, t256hi, pad[3];
 };
 
@@ -427,7 +427,13 @@ __device__ __forceinline__ int row_action(const float* in, int bl, int A) {
 // image in the stage-ahead double buffer until round t + 2 is staged. Same MFMAs per accumulator in the same
 // order: bit-identical. Needs stage-ahead (AH); the last round's is issued after the loop.
 #ifndef ASVRL_DWC_DEFER
-#define ASVRL_DWC_DEFER 1
+#define ASVRL_DWC_DEFER 0
+#endif
+// L3's epilogue (dz1 = dh1g G 1[h1 > 0] into the dz1 image, the dG products) issued between the MFMAs of the
+// dW2 grid, which now follows L3's MFMAs instead of preceding them: the epilogue's vector work issues while the
+// grid's MFMAs run. Same MFMAs per accumulator, same arithmetic: bit-identical.
+#ifndef ASVRL_L3_FILL
+#define ASVRL_L3_FILL 1
 #endif
 template <int KS, int NB, int P, class WF>
 __device__ __forceinline__ void mfma_rows(f32x16 (&acc)[NB], const elem_t* img, const RowA<P>& RA, WF wf) {
@@ -458,15 +464,19 @@ __device__ __forceinline__ void mfma_rows(f32x16 (&acc)[NB], const elem_t* img, 
 // The weight-gradient grid dW[n] += A(kk)^T-read x B(kk, n) over kk < KK, n < NN (mf(kk, n, A, B) does
 // the MFMA and, at n = 0, the bias sum): every B(kk, n) read D steps ahead in (kk, n) order, each A(kk)
 // a whole kk ahead, one scheduling fence per step (see mfma_rows).
-template <int KK, int NN, class AF, class BF, class MF>
-__device__ __forceinline__ void mfma_grid(AF af, BF bf, MF mf) {
+// fill(t): independent vector work placed right behind step t's MFMA (the MFMA runs while it issues)
+template <int KK, int NN, class AF, class BF, class MF, class FF = NoHook>
+__device__ __forceinline__ void mfma_grid(AF af, BF bf, MF mf, FF fill = FF{}) {
   constexpr int T = KK * NN, D0 = ASVRL_READ_AHEAD < T ? ASVRL_READ_AHEAD : T;
   if constexpr (D0 == 0) {
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
       const frag8 A = af(kk);
 #pragma unroll
-      for (int n = 0; n < NN; ++n) mf(kk, n, A, bf(kk, n));
+      for (int n = 0; n < NN; ++n) {
+        mf(kk, n, A, bf(kk, n));
+        fill(kk * NN + n);
+      }
     }
   } else {
     constexpr int D = D0;
@@ -480,6 +490,7 @@ __device__ __forceinline__ void mfma_grid(AF af, BF bf, MF mf) {
       if (n == 0 && kk + 1 < KK) aq[(kk + 1) % 2] = af(kk + 1);
       mf(kk, n, aq[kk % 2], bq[t % D]);
       if (t + D < T) bq[t % D] = bf((t + D) / NN, (t + D) % NN);
+      fill(t);
       __builtin_amdgcn_sched_barrier(ASVRL_RA_FENCE_MASK);
     }
   }
@@ -625,27 +636,25 @@ void critic_fused_kernel(FusedArgs a) {
   __shared__ __attribute__((aligned(16))) FusedShared<NT, NB, S, IQN, NSB, TQ> U;
   static_assert(sizeof(U) <= 160 * 1024, "fused critic LDS image exceeds the CU's 160 KB");
   constexpr bool LT = ASVRL_LANE_TABLE && sizeof(U) + 64 * sizeof(LaneBases) <= 160 * 1024;
-  __shared__ LaneBases LB[LT ? 64 : 1];
+  __shared__ LaneBases LB[LT ? 64 : 1];   // each lane's image bases (ASVRL_LANE_TABLE)
   auto& L = U.f;
   if constexpr (TQ) target_phase<NT, NB>(a.tq, U.t, a.rounds);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
   if constexpr (LT) {   // read after the prologue's barrier
     if (threadIdx.x < 64) {
-      LaneBases b;
+      LaneBases& b = LB[lane];   // the constructors themselves (not tr_base / row_base, which read this table)
       b.r64 = RowA<kNcos>(r, h).base;
       b.r128 = RowA<kH>(r, h).base;
       b.r256 = RowA<kC>(r, h).base;
-      const TrA<kNcos> t64 = tr_base<kNcos, LT>(LB, lane);
-      const TrA<kH> t128 = tr_base<kH, LT>(LB, lane);
-      const TrA<kC> t256 = tr_base<kC, LT>(LB, lane);
+      const auto t64 = TrA<kNcos>(lane);
+      const auto t128 = TrA<kH>(lane);
+      const auto t256 = TrA<kC>(lane);
       b.t64lo = t64.lo;
       b.t64hi = t64.hi;
       b.t128lo = t128.lo;
       b.t128hi = t128.hi;
       b.t256lo = t256.lo;
       b.t256hi = t256.hi;
-      b.pad[0] = b.pad[1] = b.pad[2] = 0;
-      LB[lane] = b;
     }
   }
   const frag8* WC = reinterpret_cast<const frag8*>(a.w.wc_frag);
@@ -1088,7 +1097,8 @@ void critic_fused_kernel(FusedArgs a) {
 
     // ---------------- dW2[own][:] += dz2^T h1g;  L3: dh1g = W2^T dz2 (own block) -> dG, dz1 (own
     // slice into the dz1 image, which nobody reads before the next barrier)
-    {
+    constexpr bool L3F = ASVRL_L3_FILL && 2 * NB == (G / 16) * 4 / 4;
+    if constexpr (!L3F) {
       ASVRL_FRESH_LANE();
       const TrA<kH> TA_a = tr_base<kH, LT>(LB, lane);
       const TrA<kH> TA_b = tr_base<kH, LT>(LB, lane);
@@ -1122,20 +1132,32 @@ void critic_fused_kernel(FusedArgs a) {
         pin(h1k[j][1]);
       }
       float gsa[NB][16];
+      auto epi = [&](int c) {   // block j = c / 2, registers 8 s .. 8 s + 7 with s = c % 2
+        const int j = c >> 1, s = c & 1;
+        frag8 dz1;
 #pragma unroll
-      for (int j = 0; j < NB; ++j) {
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          frag8 dz1;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const float h1 = static_cast<float>(h1k[j][s][i]);
-            const float d = acc[j][8 * s + i];
-            dz1[i] = (elem_t)(h1 > 0.f ? (IQN ? d : d * gv[j][s][i]) : 0.f);
-            gsa[j][8 * s + i] = d * h1;
-          }
-          rows(L.dz1, RA_d, j, 2 * w + s, dz1);
+        for (int i = 0; i < 8; ++i) {
+          const float h1 = static_cast<float>(h1k[j][s][i]);
+          const float d = acc[j][8 * s + i];
+          dz1[i] = (elem_t)(h1 > 0.f ? (IQN ? d : d * gv[j][s][i]) : 0.f);
+          gsa[j][8 * s + i] = d * h1;
         }
+        rows(L.dz1, RA_d, j, 2 * w + s, dz1);
+      };
+      if constexpr (L3F) {
+        const TrA<kH> TA_a = tr_base<kH, LT>(LB, lane);
+        mfma_grid<G / 16, 4>([&](int kk) { return trf(L.b, TA_a, kk, w); },
+                             [&](int kk, int n) { return trf(L.a, TA_a, kk, n); },
+                             [&](int kk, int n, const frag8& A, const frag8& B) {
+                               if (n == 0) db2 += sum8(A);
+                               mfma_acc(dW2[n], A, B);
+                             },
+                             [&](int t) {
+                               if ((t & 3) == 3) epi(t >> 2);
+                             });
+      } else {
+#pragma unroll
+        for (int c = 0; c < 2 * NB; ++c) epi(c);
       }
       ASVRL_STAMP(21);
       if constexpr (!IQN) {
