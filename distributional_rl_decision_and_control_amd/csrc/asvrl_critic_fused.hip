@@ -277,8 +277,7 @@ __device__ __forceinline__ float fetch_in(const FusedArgs& a, int t, int e) {
 // weight gradient. f32 dot products in the same order as asvrl_critic.hip's stage_features, from the
 // round's staged inputs and the staged encoder parameters.
 template <int NT, int S, int G, bool IQN>
-__device__ __forceinline__ void stage_fg(const FusedArgs& a, int b0, int tid, const float* in, const float* enc,
-                                         float* Fs, float* Gs) {
+__device__ __forceinline__ void stage_f(int tid, const float* in, const float* enc, float* Fs) {
 #pragma clang fp contract(off)
   using IL = InLayout<NT, S, G, IQN ? 1 : 2>;
   constexpr int T = kNW * 64;
@@ -286,8 +285,6 @@ __device__ __forceinline__ void stage_fg(const FusedArgs& a, int b0, int tid, co
   const float* self_b = self_w + 56 * 7;
   const float* obj_w = self_b + 56;
   const float* obj_b = obj_w + 40 * 5;
-  const float* ae_w = obj_b + 40;
-  const float* ae_b = ae_w + 128 * 2;
   // thread tid: feature m = tid (S * 256 / T samples each); compile-time trip counts, the feature's
   // weights loaded once for all its samples
   static_assert(kC == T, "one cos-layer feature per thread");
@@ -324,6 +321,15 @@ __device__ __forceinline__ void stage_fg(const FusedArgs& a, int b0, int tid, co
       }
     }
   }
+}
+
+template <int NT, int S, int G, bool IQN>
+__device__ __forceinline__ void stage_g(const FusedArgs& a, int b0, int tid, const float* in, const float* enc,
+                                        float* Gs) {
+#pragma clang fp contract(off)
+  using IL = InLayout<NT, S, G, IQN ? 1 : 2>;
+  const float* ae_w = enc + 56 * 7 + 56 + 40 * 5 + 40;
+  const float* ae_b = ae_w + 128 * 2;
   if (!IQN && tid < kH) {
     const int m = tid;
     const float w0 = ae_w[2 * m], w1 = ae_w[2 * m + 1], bb = ae_b[m];
@@ -335,6 +341,13 @@ __device__ __forceinline__ void stage_fg(const FusedArgs& a, int b0, int tid, co
     const int k = tid / 32, c = tid % 32;
     bp(a.xb)[static_cast<int64_t>(b0 + k) * 32 + c] = (elem_t)in[IL::kObs + k * kObsIn + c];
   }
+}
+
+template <int NT, int S, int G, bool IQN>
+__device__ __forceinline__ void stage_fg(const FusedArgs& a, int b0, int tid, const float* in, const float* enc,
+                                         float* Fs, float* Gs) {
+  stage_f<NT, S, G, IQN>(tid, in, enc, Fs);
+  stage_g<NT, S, G, IQN>(a, b0, tid, in, enc, Gs);
 }
 
 // quantile-Huber terms of one row against its sample's N' = NT targets r + gamma q_next (1 - d)
@@ -434,6 +447,17 @@ __device__ __forceinline__ int row_action(const float* in, int bl, int A) {
 // grid's MFMAs run. Same MFMAs per accumulator, same arithmetic: bit-identical.
 #ifndef ASVRL_L3_FILL
 #define ASVRL_L3_FILL 1
+#endif
+// stage-ahead's staging of the next round (F, G and the cos images: ~1.6 k cycles of vector work, 16 v_cos) issued
+// in pieces between the dW1 grid's 32 MFMAs instead of after them. Same arithmetic into the same buffers.
+#ifndef ASVRL_STAGE_FILL
+#define ASVRL_STAGE_FILL 1
+#endif
+// L4 as four units (cos-feature block mq, row block j), each unit's 12 MFMAs carrying the previous unit's
+// epilogue (relu(c), dF products, dzc = dx F 1[c > 0]) between them, instead of both row blocks' MFMAs and then
+// both epilogues. Same MFMAs per accumulator in the same order, same arithmetic: bit-identical.
+#ifndef ASVRL_L4_PIPE
+#define ASVRL_L4_PIPE 1
 #endif
 template <int KS, int NB, int P, class WF>
 __device__ __forceinline__ void mfma_rows(f32x16 (&acc)[NB], const elem_t* img, const RowA<P>& RA, WF wf) {
@@ -729,6 +753,26 @@ void critic_fused_kernel(FusedArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = (elem_t)cos_pi_k_tau(tau, 8 * ch + j);
       row_store<kNcos>(cosd, row, 8 * ch, v);
+    }
+  };
+  // stage() in pieces (ASVRL_STAGE_FILL): piece p < 8 CU cos values of chunk u = p / 8 (one each, the chunk's
+  // 16-byte store with its last value), then F, then G and xb
+  constexpr int kCosU = G * (kNcos / 8) / (kNW * 64);
+  constexpr int kStagePieces = 8 * kCosU + 2;
+  frag8 scv[kCosU];
+  auto stage_piece = [&](int p, int b0s, const float* ins, elem_t* cosd, float* Fd, float* Gd) {
+    int tid_s = threadIdx.x;
+    asm volatile("" : "+v"(tid_s));
+    if (p < 8 * kCosU) {
+      const int u = p >> 3, j = p & 7;
+      const int c = tid_s + u * kNW * 64;
+      const int row = c / (kNcos / 8), ch = c % (kNcos / 8);
+      scv[u][j] = (elem_t)cos_pi_k_tau(ins[IL::kTau + row], 8 * ch + j);
+      if (j == 7) row_store<kNcos>(cosd, row, 8 * ch, scv[u]);
+    } else if (p == 8 * kCosU) {
+      stage_f<NT, S, G, IQN>(tid_s, ins, L.enc, Fd);
+    } else {
+      stage_g<NT, S, G, IQN>(a, b0s, tid_s, ins, L.enc, Gd);
     }
   };
   if constexpr (AH) {
@@ -1208,25 +1252,37 @@ void critic_fused_kernel(FusedArgs a) {
       for (int ks = 0; ks < 8; ++ks) wt[ks] = W1T[((2 * w) * 8 + ks) * 64 + lane];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) wcc[ks] = WCR ? wcr0[ks] : WC[((2 * w) * 4 + ks) * 64 + lane];
-        mfma_grid<G / 16, 8>([&](int kk) { return trf(L.dz1, TA_d, kk, w); },
-                             [&](int kk, int n) { return trf(L.x, TA_x, kk, n); },
-                             [&](int kk, int n, const frag8& A, const frag8& B) {
-                               if (n == 0) db1 += sum8(A);
-                               mfma_acc(dW1[n], A, B);
-                             });
-      ASVRL_STAMP(22);
-    }
-    if constexpr (AH) {   // round t + grid's images, behind the dW1 MFMAs
+      // the next round's staging (stage-ahead), in pieces between the grid's MFMAs (SF) or after them
+      // (the bench shape: 32 steps, 18 pieces -- the 16 cos values on steps 0..15, F on step 20, G on step 26)
+      constexpr bool SF = AH && ASVRL_STAGE_FILL && (G / 16) * 8 == 32 && kStagePieces == 18;
       const int tn = t + static_cast<int>(gridDim.x);
-      if (tn < a.rounds) stage(tn * G / NT, L.in[buf ^ 1], L.cos[buf ^ 1], L.F[buf ^ 1], L.G[buf ^ 1]);
+      const bool stg = AH && tn < a.rounds;   // workgroup-uniform
+      mfma_grid<G / 16, 8>([&](int kk) { return trf(L.dz1, TA_d, kk, w); },
+                           [&](int kk, int n) { return trf(L.x, TA_x, kk, n); },
+                           [&](int kk, int n, const frag8& A, const frag8& B) {
+                             if (n == 0) db1 += sum8(A);
+                             mfma_acc(dW1[n], A, B);
+                           },
+                           [&](int st) {
+                             if constexpr (SF) {
+                               const int pc = st < 16 ? st : (st == 20 ? 16 : (st == 26 ? 17 : -1));
+                               if (pc >= 0 && stg)
+                                 stage_piece(pc, tn * G / NT, L.in[buf ^ 1], L.cos[buf ^ 1], L.F[buf ^ 1], L.G[buf ^ 1]);
+                             }
+                           });
+      ASVRL_STAMP(22);
+      if constexpr (AH && !SF) {   // round t + grid's images, behind the dW1 MFMAs
+        if (stg) stage(tn * G / NT, L.in[buf ^ 1], L.cos[buf ^ 1], L.F[buf ^ 1], L.G[buf ^ 1]);
+      }
     }
     ASVRL_STAMP(23);
 
     // ---------------- L4: dx = W1^T dz1 (own blocks 2w, 2w+1) with c = relu(Wc cos + bc) recomputed
     // (bit-identical to L0's); dF = sum over taus of dx c (-> dzF), dzc = dx F 1[c > 0] into the
     // wave's own dzc image. No barrier: L4 reads dz1 and cos, which nothing writes this round any more.
+    constexpr bool L4P = ASVRL_L4_PIPE && NB == 2 && ASVRL_READ_AHEAD != 0;
 #pragma unroll
-    for (int mq = 0; mq < 2; ++mq) {
+    for (int mq = 0; mq < (L4P ? 0 : 2); ++mq) {
       ASVRL_FRESH_LANE();
       const RowA<kNcos> RA_cos = row_base<kNcos, LT>(LB, lane, r, h);
       const RowA<kH> RA_d = row_base<kH, LT>(LB, lane, r, h);
@@ -1290,6 +1346,76 @@ void critic_fused_kernel(FusedArgs a) {
         if (a.parts.enc != nullptr) Fb[bl * kC + p] = dz;   // F's blocks 2w, 2w+1 are this wave's own
       });
       ASVRL_STAMP(26 + 3 * mq);
+    }
+    if constexpr (L4P) {
+      ASVRL_FRESH_LANE();
+      const RowA<kNcos> RA_cos = row_base<kNcos, LT>(LB, lane, r, h);
+      const RowA<kH> RA_d = row_base<kH, LT>(LB, lane, r, h);
+      const RowA<kNcos> RA_dzc = row_base<kNcos, LT>(LB, lane, r, h);
+      float fv[2][8], fsa[NB][16];   // fv: F of the row block whose epilogue is next
+      f32x16 dxa[2], cca[2];
+      // unit (mq, j): dx = W1^T dz1 (8 k-steps), then c (4 k-steps), B operands read two steps ahead; fill(t)
+      // right behind step t's MFMA
+      auto unit = [&](int mq, int j, auto fill) {
+        dxa[j] = f32x16{};
+        cca[j] = acc_init(bcp, (2 * w + mq) * 32, h);
+        auto bop = [&](int t) { return t < 8 ? rowf(L.dz1, RA_d, j, t) : rowf(cosb, RA_cos, j, t - 8); };
+        frag8 bq[2] = {bop(0), bop(1)};
+#pragma unroll
+        for (int t = 0; t < 12; ++t) {
+          if (t < 8) dxa[j] = mfma(wt[t], bq[t & 1], dxa[j]);
+          else cca[j] = mfma(wcc[t - 8], bq[t & 1], cca[j]);
+          if (t + 2 < 12) bq[t & 1] = bop(t + 2);
+          fill(t);
+          __builtin_amdgcn_sched_barrier(ASVRL_RA_FENCE_MASK);
+        }
+      };
+      // the epilogue of unit (mq, j), half s
+      auto epi = [&](int mq, int j, int s) {
+        if constexpr (!kBiasFirst) if (s == 0) cca[j] += bias_init(bcp, (2 * w + mq) * 32, h);
+        frag8 dz;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float cv = relu(cca[j][8 * s + i]);
+          fsa[j][8 * s + i] = dxa[j][8 * s + i] * cv;
+          dz[i] = (elem_t)(cv > 0.f ? dxa[j][8 * s + i] * fv[s][i] : 0.f);
+        }
+        rows(dzc_w, RA_dzc, j, 2 * mq + s, dz);
+      };
+      auto ldf = [&](int mq, int j) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) lds8(Fb + ((32 * j + r) / NT) * kC + (2 * w + mq) * 32 + 16 * s + 8 * h, fv[s]);
+      };
+      auto sums = [&](int mq) {
+        sample_sums<NT, NB>(fsa, (2 * w + mq) * 32, lane, [&](int bl, int p, float v) {
+          const float fm = Fb[bl * kC + p];
+          const float dz = fm > 0.f ? v : 0.f;
+          if (a.dzF != nullptr) bp(a.dzF)[static_cast<size_t>(b0 + bl) * kC + swap23(p)] = (elem_t)dz;
+          if (a.parts.enc != nullptr) Fb[bl * kC + p] = dz;   // F's blocks 2w, 2w+1 are this wave's own
+        });
+      };
+#pragma unroll
+      for (int mq = 0; mq < 2; ++mq) {
+        ldf(mq, 0);
+        unit(mq, 0, [](int) {});
+        ASVRL_STAMP(24 + 3 * mq);
+        unit(mq, 1, [&](int t) {
+          if (t == 1) epi(mq, 0, 0);
+          if (t == 6) epi(mq, 0, 1);
+          if (t == 7) ldf(mq, 1);
+        });
+        epi(mq, 1, 0);
+        epi(mq, 1, 1);
+        if (mq == 0) {   // the second block's fragments, behind the first block's dF sums
+#pragma unroll
+          for (int ks = 0; ks < 8; ++ks) wt[ks] = W1T[((2 * w + 1) * 8 + ks) * 64 + lane];
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) wcc[ks] = WCR ? wcr1[ks] : WC[((2 * w + 1) * 4 + ks) * 64 + lane];
+        }
+        ASVRL_STAMP(25 + 3 * mq);
+        sums(mq);
+        ASVRL_STAMP(26 + 3 * mq);
+      }
     }
     {
       if (a.parts.enc != nullptr) {

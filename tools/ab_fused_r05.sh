@@ -20,7 +20,7 @@ for L in "${LIBS[@]}"; do
     echo -n "$L vs $first: " >> $OUT; python tools/fused_dump.py --compare gpurun_out/${T}_dump_$first.npz gpurun_out/${T}_dump_$L.npz | tail -1 >> $OUT
   fi
 done
-for rep in 1 2; do for L in "${LIBS[@]}"; do
+for rep in $(seq 1 ${REPS:-2}); do for L in "${LIBS[@]}"; do
   if [ "$L" = default ]; then unset ASVRL_LIB; else export ASVRL_LIB=variants/libasvrl_$L.so; fi
   echo -n "$rep $L " >> $OUT
   timeout -k 10 120 python tools/fused_time.py 2>/dev/null >> $OUT || exit 3
