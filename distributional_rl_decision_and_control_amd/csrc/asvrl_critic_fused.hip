@@ -459,6 +459,11 @@ __device__ __forceinline__ int row_action(const float* in, int bl, int A) {
 #ifndef ASVRL_L4_PIPE
 #define ASVRL_L4_PIPE 1
 #endif
+// L1 / L2 with their row blocks one after the other, the first block's epilogue issued between the second
+// block's MFMAs (mfma_rows_fill). Same MFMAs per accumulator in the same order: bit-identical.
+#ifndef ASVRL_FWD_FILL
+#define ASVRL_FWD_FILL 1
+#endif
 template <int KS, int NB, int P, class WF>
 __device__ __forceinline__ void mfma_rows(f32x16 (&acc)[NB], const elem_t* img, const RowA<P>& RA, WF wf) {
   constexpr int D = ASVRL_READ_AHEAD < KS ? ASVRL_READ_AHEAD : KS;
@@ -482,6 +487,24 @@ __device__ __forceinline__ void mfma_rows(f32x16 (&acc)[NB], const elem_t* img, 
         for (int j = 0; j < NB; ++j) bq[ks % D][j] = rowf(img, RA, j, ks + D);
       __builtin_amdgcn_sched_barrier(ASVRL_RA_FENCE_MASK);
     }
+  }
+}
+
+// mfma_rows with the row blocks in turn (block j's KS MFMAs, then block j + 1's): B operands read D steps ahead
+// along that order, fill(j, ks) right behind block j's k-step ks (same MFMAs per accumulator, same order)
+template <int KS, int NB, int P, class WF, class FF>
+__device__ __forceinline__ void mfma_rows_fill(f32x16 (&acc)[NB], const elem_t* img, const RowA<P>& RA, WF wf, FF fill) {
+  constexpr int T = KS * NB, D = 2;
+  frag8 bq[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) bq[d] = rowf(img, RA, d / KS, d % KS);
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int j = t / KS, ks = t % KS;
+    acc[j] = mfma(wf(ks), bq[t % D], acc[j]);
+    if (t + D < T) bq[t % D] = rowf(img, RA, (t + D) / KS, (t + D) % KS);
+    fill(j, ks);
+    __builtin_amdgcn_sched_barrier(ASVRL_RA_FENCE_MASK);
   }
 }
 
@@ -899,8 +922,42 @@ void critic_fused_kernel(FusedArgs a) {
           for (int ks = 0; ks < 4; ++ks) cb[j][ks] = rowf(cosb, RA_cos, j, ks);
         __builtin_amdgcn_sched_barrier(0);
       }
+      constexpr bool FF0 = ASVRL_FWD_FILL && kBiasFirst && NB == 2 && ASVRL_READ_AHEAD != 0;
+      if constexpr (FF0) {
+        // units u = (mq, j) = (u / 2, u % 2): unit u's four MFMAs carry unit u - 1's epilogue (x = F relu(c))
+        f32x16 acc0[2];
+        float fv[2][8];   // F of the unit whose epilogue is next
+        auto ldf0 = [&](int u) {
 #pragma unroll
-      for (int mq = 0; mq < 2; ++mq) {
+          for (int s = 0; s < 2; ++s)
+            lds8(Fb + ((32 * (u & 1) + r) / NT) * kC + (2 * w + (u >> 1)) * 32 + 16 * s + 8 * h, fv[s]);
+        };
+        auto epi0 = [&](int u, int s) {
+          frag8 xo;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) xo[i] = (elem_t)(fv[s][i] * relu(acc0[u & 1][8 * s + i]));
+          rows(L.x, RA_x, u & 1, 2 * (2 * w + (u >> 1)) + s, xo);
+        };
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int mq = u >> 1, j = u & 1;
+          if (u > 0) ldf0(u - 1);
+          acc0[j] = acc_init(bcp, (2 * w + mq) * 32, h);
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) {
+            acc0[j] = mfma(mq ? wc1[ks] : wc0[ks], cb[j][ks], acc0[j]);
+            if (u > 0 && ks == 1) epi0(u - 1, 0);
+            if (u > 0 && ks == 3) epi0(u - 1, 1);
+            __builtin_amdgcn_sched_barrier(ASVRL_RA_FENCE_MASK);
+          }
+          if (u == 1) ASVRL_STAMP(16);
+        }
+        ldf0(3);
+        epi0(3, 0);
+        epi0(3, 1);
+      }
+#pragma unroll
+      for (int mq = 0; mq < (FF0 ? 0 : 2); ++mq) {
         const int mb = 2 * w + mq;
         float fv[NB][2][8];
 #pragma unroll
@@ -948,7 +1005,26 @@ void critic_fused_kernel(FusedArgs a) {
       f32x16 acc[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[j] = acc_init(b1p, w * 32, h);
-      mfma_rows<kC / 16, NB>(acc, L.x, RA_x, [&](int ks) { return w1f[ks]; });
+      auto epi1 = [&](int j, int s) {
+        frag8 go;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float hv = relu(acc[j][8 * s + i]);
+          h1k[j][s][i] = (elem_t)hv;
+          go[i] = IQN ? h1k[j][s][i] : (elem_t)(hv * gv[j][s][i]);
+        }
+        rows(L.a, RA_a, j, 2 * w + s, go);
+        pin(h1k[j][s]);
+      };
+      constexpr bool FF1 = ASVRL_FWD_FILL && kBiasFirst && NB == 2;
+      if constexpr (FF1) {
+        mfma_rows_fill<kC / 16, NB>(acc, L.x, RA_x, [&](int ks) { return w1f[ks]; }, [&](int j, int ks) {
+          if (j == 1 && ks == 2) epi1(0, 0);
+          if (j == 1 && ks == 9) epi1(0, 1);
+        });
+      } else {
+        mfma_rows<kC / 16, NB>(acc, L.x, RA_x, [&](int ks) { return w1f[ks]; });
+      }
       ASVRL_STAMP(17);
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) w2f[ks] = W2[(w * 8 + ks) * 64 + lane];
@@ -961,20 +1037,9 @@ void critic_fused_kernel(FusedArgs a) {
 #pragma unroll
         for (int j = 0; j < NB; ++j) acc[j] += bias_init(b1p, w * 32, h);
 #pragma unroll
-      for (int j = 0; j < NB; ++j) {
+      for (int j = FF1 ? 1 : 0; j < NB; ++j)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          frag8 go;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const float hv = relu(acc[j][8 * s + i]);
-            h1k[j][s][i] = (elem_t)hv;
-            go[i] = IQN ? h1k[j][s][i] : (elem_t)(hv * gv[j][s][i]);
-          }
-          rows(L.a, RA_a, j, 2 * w + s, go);
-          pin(h1k[j][s]);
-        }
-      }
+        for (int s = 0; s < 2; ++s) epi1(j, s);
     }
     ASVRL_STAMP(4);
     __syncthreads();
@@ -990,39 +1055,54 @@ void critic_fused_kernel(FusedArgs a) {
       f32x16 z2[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) z2[j] = acc_init(b2p, w * 32, h);
-      mfma_rows<kH / 16, NB>(z2, L.a, RA_a, [&](int ks) { return w2f[ks]; });
+      // the output row feeding q: AC-IQN's single row, IQN's row of the sample's action
+      constexpr int NWO = IQN ? NB : 1;
+      float wov[NWO][2][8];
+      float part[NB];
+      auto epi2 = [&](int j, int s) {
+        if (s == 0) part[j] = 0.f;
+        frag8 hv;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float h2 = relu(z2[j][8 * s + i]);
+          part[j] += wov[IQN ? j : 0][s][i] * h2;
+          hv[i] = (elem_t)h2;
+        }
+        rows(L.b, RA_b, j, 2 * w + s, hv);
+        if (s == 1) {
+          const float pj = half_sum(part[j]);
+          if (h == 0) L.qpart[w][32 * j + r] = pj;
+        }
+      };
+      auto ldwo = [&]() {
+#pragma unroll
+        for (int j = 0; j < NWO; ++j) {
+          const float* src = IQN ? L.woA + row_action<IL::kAct>(in, (32 * j + r) / NT, a.n_actions) * kH : wop;
+#pragma unroll
+          for (int s = 0; s < 2; ++s) lds8(src + w * 32 + 16 * s + 8 * h, wov[j][s]);
+        }
+      };
+      constexpr bool FF2 = ASVRL_FWD_FILL && kBiasFirst && NB == 2;
+      if constexpr (FF2) {
+        ldwo();
+        mfma_rows_fill<kH / 16, NB>(z2, L.a, RA_a, [&](int ks) { return w2f[ks]; }, [&](int j, int ks) {
+          if (j == 1 && ks == 1) epi2(0, 0);
+          if (j == 1 && ks == 4) epi2(0, 1);
+        });
+      } else {
+        mfma_rows<kH / 16, NB>(z2, L.a, RA_a, [&](int ks) { return w2f[ks]; });
+      }
       ASVRL_STAMP(18);
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) w2tf[ks] = W2T[(w * 8 + ks) * 64 + lane];
       if constexpr (!kBiasFirst)
 #pragma unroll
         for (int j = 0; j < NB; ++j) z2[j] += bias_init(b2p, w * 32, h);
-      // the output row feeding q: AC-IQN's single row, IQN's row of the sample's action
-      constexpr int NWO = IQN ? NB : 1;
-      float wov[NWO][2][8];
+      if constexpr (!FF2) ldwo();
 #pragma unroll
-      for (int j = 0; j < NWO; ++j) {
-        const float* src = IQN ? L.woA + row_action<IL::kAct>(in, (32 * j + r) / NT, a.n_actions) * kH : wop;
+      for (int j = FF2 ? 1 : 0; j < NB; ++j)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) lds8(src + w * 32 + 16 * s + 8 * h, wov[j][s]);
-      }
-#pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        float part = 0.f;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          frag8 hv;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const float h2 = relu(z2[j][8 * s + i]);
-            part += wov[IQN ? j : 0][s][i] * h2;
-            hv[i] = (elem_t)h2;
-          }
-          rows(L.b, RA_b, j, 2 * w + s, hv);
-        }
-        part = half_sum(part);
-        if (h == 0) L.qpart[w][32 * j + r] = part;
-      }
+        for (int s = 0; s < 2; ++s) epi2(j, s);
     }
     ASVRL_STAMP(6);
     __syncthreads();
