@@ -199,15 +199,13 @@ struct InLayout {
 };
 
 // Each lane's swizzled-image bases (RowA / TrA of the 64-, 128- and 256-position images), computed once per
-// launch into LDS: a phase reads its two or three with one or two ds_read instead of ~10 (RowA) / ~25 (TrA) VALU
-// instructions each -- the round's vector issue, not its matrix work, sets its length (ASVRL_LANE_TABLE).
-#ifndef ASVRL_LANE_TABLE
-#define ASVRL_LANE_TABLE 1
-#endif
+// launch into LDS: a phase reads the two or three it uses (ds_read) instead of recomputing them -- about 10
+// (RowA) / 25 (TrA) VALU instructions each, ~180 per round, where the round's vector issue, not its matrix work,
+// sets its length. Measured 111.0 -> 108.6 us median per launch, bit-identical (profiles/r05f_fused_variants_ab.txt,
+// r05g_fused_fill_variants_ab.txt). Where the table does not fit beside the images (IQN) the bases are computed.
 struct alignas(16) LaneBases {
   int r64, r128, r256, t64lo, t64hi, t128lo, t128hi, t256lo, t256hi, pad[3];
 };
-
 template <int P, bool LT>
 __device__ __forceinline__ RowA<P> row_base(const LaneBases* LB, int lane, int r, int h) {
   if constexpr (LT) {
@@ -277,7 +275,8 @@ __device__ __forceinline__ float fetch_in(const FusedArgs& a, int t, int e) {
 // weight gradient. f32 dot products in the same order as asvrl_critic.hip's stage_features, from the
 // round's staged inputs and the staged encoder parameters.
 template <int NT, int S, int G, bool IQN>
-__device__ __forceinline__ void stage_f(int tid, const float* in, const float* enc, float* Fs) {
+__device__ __forceinline__ void stage_fg(const FusedArgs& a, int b0, int tid, const float* in, const float* enc,
+                                         float* Fs, float* Gs) {
 #pragma clang fp contract(off)
   using IL = InLayout<NT, S, G, IQN ? 1 : 2>;
   constexpr int T = kNW * 64;
@@ -285,6 +284,8 @@ __device__ __forceinline__ void stage_f(int tid, const float* in, const float* e
   const float* self_b = self_w + 56 * 7;
   const float* obj_w = self_b + 56;
   const float* obj_b = obj_w + 40 * 5;
+  const float* ae_w = obj_b + 40;
+  const float* ae_b = ae_w + 128 * 2;
   // thread tid: feature m = tid (S * 256 / T samples each); compile-time trip counts, the feature's
   // weights loaded once for all its samples
   static_assert(kC == T, "one cos-layer feature per thread");
@@ -321,15 +322,6 @@ __device__ __forceinline__ void stage_f(int tid, const float* in, const float* e
       }
     }
   }
-}
-
-template <int NT, int S, int G, bool IQN>
-__device__ __forceinline__ void stage_g(const FusedArgs& a, int b0, int tid, const float* in, const float* enc,
-                                        float* Gs) {
-#pragma clang fp contract(off)
-  using IL = InLayout<NT, S, G, IQN ? 1 : 2>;
-  const float* ae_w = enc + 56 * 7 + 56 + 40 * 5 + 40;
-  const float* ae_b = ae_w + 128 * 2;
   if (!IQN && tid < kH) {
     const int m = tid;
     const float w0 = ae_w[2 * m], w1 = ae_w[2 * m + 1], bb = ae_b[m];
@@ -343,29 +335,18 @@ __device__ __forceinline__ void stage_g(const FusedArgs& a, int b0, int tid, con
   }
 }
 
-template <int NT, int S, int G, bool IQN>
-__device__ __forceinline__ void stage_fg(const FusedArgs& a, int b0, int tid, const float* in, const float* enc,
-                                         float* Fs, float* Gs) {
-  stage_f<NT, S, G, IQN>(tid, in, enc, Fs);
-  stage_g<NT, S, G, IQN>(a, b0, tid, in, enc, Gs);
-}
-
 // quantile-Huber terms of one row against its sample's N' = NT targets r + gamma q_next (1 - d)
 // (agent.py:399-412), split over four lanes: lane quarter q4 (lanes 16 q4 .. 16 q4 + 15 share the
 // row block) takes targets q4 NT/4 .. + NT/4 - 1 from the staged q_next, and the four partial sums
 // are combined by two lane exchanges (a fixed order). Returns dq; *wl = the row's loss sum.
-struct NoHook {
-  __device__ __forceinline__ void operator()(int) const {}
-};
-template <int NT, class Hook = NoHook>
+template <int NT>
 __device__ __forceinline__ float quarter_loss_dq(const FusedArgs& a, const float* qt, float rb, float done, float tau,
-                                                 float q, int q4, float* wl_out, Hook hook = Hook{}) {
+                                                 float q, int q4, float* wl_out) {
   const float nd = 1.0f - done;
   const float kap = a.kappa, hk = 0.5f * a.kappa, omt = 1.f - tau;
   float wl = 0.f, wg = 0.f;
 #pragma unroll
   for (int j = 0; j < NT / 4; ++j) {
-    hook(j);   // independent matrix work issued between the targets' vector arithmetic (ASVRL_DWC_DEFER)
     const float target = rb + (a.gamma * qt[q4 * (NT / 4) + j]) * nd;   // r + gamma * q_next * (1 - d)
     const float d = target - q;   // td_error (agent.py:406)
     const float ad = fabsf(d);
@@ -434,36 +415,6 @@ __device__ __forceinline__ int row_action(const float* in, int bl, int A) {
 // (Measured in round 4 and removed, profiles/r04e_fused_variants_ab.txt: a deeper weight-gradient read-ahead,
 // dW2 + L3 and dW1 + L4 as interleaved MFMA streams, the cos layer's gradient loop a k-step ahead, and the dW2 /
 // dW1 partials stored during the last round -- all bit-identical, none faster.)
-// the cos layer's weight gradient of round t (dWc += dzc^T cos, 16 MFMAs per wave) issued in round t + 1's loss
-// phase, between the quantile-Huber terms (which have no matrix work of their own), instead of at the end of
-// round t: its operands are still intact there -- the wave's own dzc image until round t + 1's L4, round t's cos
-// image in the stage-ahead double buffer until round t + 2 is staged. Same MFMAs per accumulator in the same
-// order: bit-identical. Needs stage-ahead (AH); the last round's is issued after the loop.
-#ifndef ASVRL_DWC_DEFER
-#define ASVRL_DWC_DEFER 0
-#endif
-// L3's epilogue (dz1 = dh1g G 1[h1 > 0] into the dz1 image, the dG products) issued between the MFMAs of the
-// dW2 grid, which now follows L3's MFMAs instead of preceding them: the epilogue's vector work issues while the
-// grid's MFMAs run. Same MFMAs per accumulator, same arithmetic: bit-identical.
-#ifndef ASVRL_L3_FILL
-#define ASVRL_L3_FILL 1
-#endif
-// stage-ahead's staging of the next round (F, G and the cos images: ~1.6 k cycles of vector work, 16 v_cos) issued
-// in pieces between the dW1 grid's 32 MFMAs instead of after them. Same arithmetic into the same buffers.
-#ifndef ASVRL_STAGE_FILL
-#define ASVRL_STAGE_FILL 1
-#endif
-// L4 as four units (cos-feature block mq, row block j), each unit's 12 MFMAs carrying the previous unit's
-// epilogue (relu(c), dF products, dzc = dx F 1[c > 0]) between them, instead of both row blocks' MFMAs and then
-// both epilogues. Same MFMAs per accumulator in the same order, same arithmetic: bit-identical.
-#ifndef ASVRL_L4_PIPE
-#define ASVRL_L4_PIPE 1
-#endif
-// L1 / L2 with their row blocks one after the other, the first block's epilogue issued between the second
-// block's MFMAs (mfma_rows_fill). Same MFMAs per accumulator in the same order: bit-identical.
-#ifndef ASVRL_FWD_FILL
-#define ASVRL_FWD_FILL 1
-#endif
 template <int KS, int NB, int P, class WF>
 __device__ __forceinline__ void mfma_rows(f32x16 (&acc)[NB], const elem_t* img, const RowA<P>& RA, WF wf) {
   constexpr int D = ASVRL_READ_AHEAD < KS ? ASVRL_READ_AHEAD : KS;
@@ -490,40 +441,18 @@ __device__ __forceinline__ void mfma_rows(f32x16 (&acc)[NB], const elem_t* img, 
   }
 }
 
-// mfma_rows with the row blocks in turn (block j's KS MFMAs, then block j + 1's): B operands read D steps ahead
-// along that order, fill(j, ks) right behind block j's k-step ks (same MFMAs per accumulator, same order)
-template <int KS, int NB, int P, class WF, class FF>
-__device__ __forceinline__ void mfma_rows_fill(f32x16 (&acc)[NB], const elem_t* img, const RowA<P>& RA, WF wf, FF fill) {
-  constexpr int T = KS * NB, D = 2;
-  frag8 bq[D];
-#pragma unroll
-  for (int d = 0; d < D; ++d) bq[d] = rowf(img, RA, d / KS, d % KS);
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-    const int j = t / KS, ks = t % KS;
-    acc[j] = mfma(wf(ks), bq[t % D], acc[j]);
-    if (t + D < T) bq[t % D] = rowf(img, RA, (t + D) / KS, (t + D) % KS);
-    fill(j, ks);
-    __builtin_amdgcn_sched_barrier(ASVRL_RA_FENCE_MASK);
-  }
-}
-
 // The weight-gradient grid dW[n] += A(kk)^T-read x B(kk, n) over kk < KK, n < NN (mf(kk, n, A, B) does
 // the MFMA and, at n = 0, the bias sum): every B(kk, n) read D steps ahead in (kk, n) order, each A(kk)
 // a whole kk ahead, one scheduling fence per step (see mfma_rows).
-// fill(t): independent vector work placed right behind step t's MFMA (the MFMA runs while it issues)
-template <int KK, int NN, class AF, class BF, class MF, class FF = NoHook>
-__device__ __forceinline__ void mfma_grid(AF af, BF bf, MF mf, FF fill = FF{}) {
+template <int KK, int NN, class AF, class BF, class MF>
+__device__ __forceinline__ void mfma_grid(AF af, BF bf, MF mf) {
   constexpr int T = KK * NN, D0 = ASVRL_READ_AHEAD < T ? ASVRL_READ_AHEAD : T;
   if constexpr (D0 == 0) {
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
       const frag8 A = af(kk);
 #pragma unroll
-      for (int n = 0; n < NN; ++n) {
-        mf(kk, n, A, bf(kk, n));
-        fill(kk * NN + n);
-      }
+      for (int n = 0; n < NN; ++n) mf(kk, n, A, bf(kk, n));
     }
   } else {
     constexpr int D = D0;
@@ -537,7 +466,6 @@ __device__ __forceinline__ void mfma_grid(AF af, BF bf, MF mf, FF fill = FF{}) {
       if (n == 0 && kk + 1 < KK) aq[(kk + 1) % 2] = af(kk + 1);
       mf(kk, n, aq[kk % 2], bq[t % D]);
       if (t + D < T) bq[t % D] = bf((t + D) / NN, (t + D) % NN);
-      fill(t);
       __builtin_amdgcn_sched_barrier(ASVRL_RA_FENCE_MASK);
     }
   }
@@ -678,18 +606,16 @@ void critic_fused_kernel(FusedArgs a) {
   constexpr int NB = FusedNB<NT>::v, G = 32 * NB, S = G / NT, NA = IQN ? 1 : 2;
   constexpr bool AH = ASVRL_STAGE_AHEAD && (!IQN || ASVRL_STAGE_AHEAD_IQN) && NT == 32 && !ASVRL_OPERAND_F32;
   constexpr int NSB = AH ? 2 : 1;
-  constexpr bool DD = ASVRL_DWC_DEFER && AH;   // the cos layer's gradient one round late (see ASVRL_DWC_DEFER)
-  static_assert(!DD || G / 16 == kNW, "the deferred dWc rides on exactly one 16-row loss group per wave");
   __shared__ __attribute__((aligned(16))) FusedShared<NT, NB, S, IQN, NSB, TQ> U;
   static_assert(sizeof(U) <= 160 * 1024, "fused critic LDS image exceeds the CU's 160 KB");
-  constexpr bool LT = ASVRL_LANE_TABLE && sizeof(U) + 64 * sizeof(LaneBases) <= 160 * 1024;
-  __shared__ LaneBases LB[LT ? 64 : 1];   // each lane's image bases (ASVRL_LANE_TABLE)
+  constexpr bool LT = sizeof(U) + 64 * sizeof(LaneBases) <= 160 * 1024;
+  __shared__ LaneBases LB[LT ? 64 : 1];   // each lane's image bases
   auto& L = U.f;
   if constexpr (TQ) target_phase<NT, NB>(a.tq, U.t, a.rounds);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
   if constexpr (LT) {   // read after the prologue's barrier
     if (threadIdx.x < 64) {
-      LaneBases& b = LB[lane];   // the constructors themselves (not tr_base / row_base, which read this table)
+      LaneBases& b = LB[lane];   // the constructors themselves (row_base / tr_base read this table)
       b.r64 = RowA<kNcos>(r, h).base;
       b.r128 = RowA<kH>(r, h).base;
       b.r256 = RowA<kC>(r, h).base;
@@ -778,26 +704,6 @@ void critic_fused_kernel(FusedArgs a) {
       row_store<kNcos>(cosd, row, 8 * ch, v);
     }
   };
-  // stage() in pieces (ASVRL_STAGE_FILL): piece p < 8 CU cos values of chunk u = p / 8 (one each, the chunk's
-  // 16-byte store with its last value), then F, then G and xb
-  constexpr int kCosU = G * (kNcos / 8) / (kNW * 64);
-  constexpr int kStagePieces = 8 * kCosU + 2;
-  frag8 scv[kCosU];
-  auto stage_piece = [&](int p, int b0s, const float* ins, elem_t* cosd, float* Fd, float* Gd) {
-    int tid_s = threadIdx.x;
-    asm volatile("" : "+v"(tid_s));
-    if (p < 8 * kCosU) {
-      const int u = p >> 3, j = p & 7;
-      const int c = tid_s + u * kNW * 64;
-      const int row = c / (kNcos / 8), ch = c % (kNcos / 8);
-      scv[u][j] = (elem_t)cos_pi_k_tau(ins[IL::kTau + row], 8 * ch + j);
-      if (j == 7) row_store<kNcos>(cosd, row, 8 * ch, scv[u]);
-    } else if (p == 8 * kCosU) {
-      stage_f<NT, S, G, IQN>(tid_s, ins, L.enc, Fd);
-    } else {
-      stage_g<NT, S, G, IQN>(a, b0s, tid_s, ins, L.enc, Gd);
-    }
-  };
   if constexpr (AH) {
     if (blockIdx.x < a.rounds) stage(blockIdx.x * G / NT, L.in[0], L.cos[0], L.F[0], L.G[0]);
     __syncthreads();
@@ -825,29 +731,6 @@ void critic_fused_kernel(FusedArgs a) {
       wcr1[ks] = WC[((2 * w + 1) * 4 + ks) * 64 + lane];
     }
   }
-  // the cos layer's weight gradient over one round's rows: dWc[own 64][:] += dzc^T cos from the wave's own dzc
-  // image and the round's cos image, in 8 steps (k-step kk = u / 2, cos column block n = u % 2): dwc_load(u)
-  // reads step u's operands, dwc_mfma(u) issues its two MFMAs (one step later, behind other work)
-  frag8 dA0, dA1, dB;
-  // (TA: the lane's transposed-read offsets, the same for both images (64 positions per row), computed once per
-  // phase by the caller; dzcp: the wave's own dzc image)
-  auto dwc_load = [&](const elem_t* cosp, const elem_t* dzcp, const TrA<kNcos>& TA, int u) {
-    const int kk = u >> 1, n = u & 1;
-    if (n == 0) {
-      dA0 = trf(dzcp, TA, kk, 0);
-      dA1 = trf(dzcp, TA, kk, 1);
-    }
-    dB = trf(cosp, TA, kk, n);
-  };
-  auto dwc_mfma = [&](int u) {
-    const int n = u & 1;
-    if (n == 0) {
-      dbc0 += sum8(dA0);
-      dbc1 += sum8(dA1);
-    }
-    mfma_acc(dWc[n], dA0, dB);
-    mfma_acc(dWc[2 + n], dA1, dB);
-  };
   float encr[IQN ? 8 : 1];   // IQN with parts.enc: this lane's feature's encoder sums
 #pragma unroll
   for (int i = 0; i < (IQN ? 8 : 1); ++i) encr[i] = 0.f;
@@ -922,42 +805,8 @@ void critic_fused_kernel(FusedArgs a) {
           for (int ks = 0; ks < 4; ++ks) cb[j][ks] = rowf(cosb, RA_cos, j, ks);
         __builtin_amdgcn_sched_barrier(0);
       }
-      constexpr bool FF0 = ASVRL_FWD_FILL && kBiasFirst && NB == 2 && ASVRL_READ_AHEAD != 0;
-      if constexpr (FF0) {
-        // units u = (mq, j) = (u / 2, u % 2): unit u's four MFMAs carry unit u - 1's epilogue (x = F relu(c))
-        f32x16 acc0[2];
-        float fv[2][8];   // F of the unit whose epilogue is next
-        auto ldf0 = [&](int u) {
 #pragma unroll
-          for (int s = 0; s < 2; ++s)
-            lds8(Fb + ((32 * (u & 1) + r) / NT) * kC + (2 * w + (u >> 1)) * 32 + 16 * s + 8 * h, fv[s]);
-        };
-        auto epi0 = [&](int u, int s) {
-          frag8 xo;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) xo[i] = (elem_t)(fv[s][i] * relu(acc0[u & 1][8 * s + i]));
-          rows(L.x, RA_x, u & 1, 2 * (2 * w + (u >> 1)) + s, xo);
-        };
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int mq = u >> 1, j = u & 1;
-          if (u > 0) ldf0(u - 1);
-          acc0[j] = acc_init(bcp, (2 * w + mq) * 32, h);
-#pragma unroll
-          for (int ks = 0; ks < 4; ++ks) {
-            acc0[j] = mfma(mq ? wc1[ks] : wc0[ks], cb[j][ks], acc0[j]);
-            if (u > 0 && ks == 1) epi0(u - 1, 0);
-            if (u > 0 && ks == 3) epi0(u - 1, 1);
-            __builtin_amdgcn_sched_barrier(ASVRL_RA_FENCE_MASK);
-          }
-          if (u == 1) ASVRL_STAMP(16);
-        }
-        ldf0(3);
-        epi0(3, 0);
-        epi0(3, 1);
-      }
-#pragma unroll
-      for (int mq = 0; mq < (FF0 ? 0 : 2); ++mq) {
+      for (int mq = 0; mq < 2; ++mq) {
         const int mb = 2 * w + mq;
         float fv[NB][2][8];
 #pragma unroll
@@ -1005,26 +854,7 @@ void critic_fused_kernel(FusedArgs a) {
       f32x16 acc[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[j] = acc_init(b1p, w * 32, h);
-      auto epi1 = [&](int j, int s) {
-        frag8 go;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float hv = relu(acc[j][8 * s + i]);
-          h1k[j][s][i] = (elem_t)hv;
-          go[i] = IQN ? h1k[j][s][i] : (elem_t)(hv * gv[j][s][i]);
-        }
-        rows(L.a, RA_a, j, 2 * w + s, go);
-        pin(h1k[j][s]);
-      };
-      constexpr bool FF1 = ASVRL_FWD_FILL && kBiasFirst && NB == 2;
-      if constexpr (FF1) {
-        mfma_rows_fill<kC / 16, NB>(acc, L.x, RA_x, [&](int ks) { return w1f[ks]; }, [&](int j, int ks) {
-          if (j == 1 && ks == 2) epi1(0, 0);
-          if (j == 1 && ks == 9) epi1(0, 1);
-        });
-      } else {
-        mfma_rows<kC / 16, NB>(acc, L.x, RA_x, [&](int ks) { return w1f[ks]; });
-      }
+      mfma_rows<kC / 16, NB>(acc, L.x, RA_x, [&](int ks) { return w1f[ks]; });
       ASVRL_STAMP(17);
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) w2f[ks] = W2[(w * 8 + ks) * 64 + lane];
@@ -1037,9 +867,20 @@ void critic_fused_kernel(FusedArgs a) {
 #pragma unroll
         for (int j = 0; j < NB; ++j) acc[j] += bias_init(b1p, w * 32, h);
 #pragma unroll
-      for (int j = FF1 ? 1 : 0; j < NB; ++j)
+      for (int j = 0; j < NB; ++j) {
 #pragma unroll
-        for (int s = 0; s < 2; ++s) epi1(j, s);
+        for (int s = 0; s < 2; ++s) {
+          frag8 go;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float hv = relu(acc[j][8 * s + i]);
+            h1k[j][s][i] = (elem_t)hv;
+            go[i] = IQN ? h1k[j][s][i] : (elem_t)(hv * gv[j][s][i]);
+          }
+          rows(L.a, RA_a, j, 2 * w + s, go);
+          pin(h1k[j][s]);
+        }
+      }
     }
     ASVRL_STAMP(4);
     __syncthreads();
@@ -1055,54 +896,39 @@ void critic_fused_kernel(FusedArgs a) {
       f32x16 z2[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) z2[j] = acc_init(b2p, w * 32, h);
-      // the output row feeding q: AC-IQN's single row, IQN's row of the sample's action
-      constexpr int NWO = IQN ? NB : 1;
-      float wov[NWO][2][8];
-      float part[NB];
-      auto epi2 = [&](int j, int s) {
-        if (s == 0) part[j] = 0.f;
-        frag8 hv;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float h2 = relu(z2[j][8 * s + i]);
-          part[j] += wov[IQN ? j : 0][s][i] * h2;
-          hv[i] = (elem_t)h2;
-        }
-        rows(L.b, RA_b, j, 2 * w + s, hv);
-        if (s == 1) {
-          const float pj = half_sum(part[j]);
-          if (h == 0) L.qpart[w][32 * j + r] = pj;
-        }
-      };
-      auto ldwo = [&]() {
-#pragma unroll
-        for (int j = 0; j < NWO; ++j) {
-          const float* src = IQN ? L.woA + row_action<IL::kAct>(in, (32 * j + r) / NT, a.n_actions) * kH : wop;
-#pragma unroll
-          for (int s = 0; s < 2; ++s) lds8(src + w * 32 + 16 * s + 8 * h, wov[j][s]);
-        }
-      };
-      constexpr bool FF2 = ASVRL_FWD_FILL && kBiasFirst && NB == 2;
-      if constexpr (FF2) {
-        ldwo();
-        mfma_rows_fill<kH / 16, NB>(z2, L.a, RA_a, [&](int ks) { return w2f[ks]; }, [&](int j, int ks) {
-          if (j == 1 && ks == 1) epi2(0, 0);
-          if (j == 1 && ks == 4) epi2(0, 1);
-        });
-      } else {
-        mfma_rows<kH / 16, NB>(z2, L.a, RA_a, [&](int ks) { return w2f[ks]; });
-      }
+      mfma_rows<kH / 16, NB>(z2, L.a, RA_a, [&](int ks) { return w2f[ks]; });
       ASVRL_STAMP(18);
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) w2tf[ks] = W2T[(w * 8 + ks) * 64 + lane];
       if constexpr (!kBiasFirst)
 #pragma unroll
         for (int j = 0; j < NB; ++j) z2[j] += bias_init(b2p, w * 32, h);
-      if constexpr (!FF2) ldwo();
+      // the output row feeding q: AC-IQN's single row, IQN's row of the sample's action
+      constexpr int NWO = IQN ? NB : 1;
+      float wov[NWO][2][8];
 #pragma unroll
-      for (int j = FF2 ? 1 : 0; j < NB; ++j)
+      for (int j = 0; j < NWO; ++j) {
+        const float* src = IQN ? L.woA + row_action<IL::kAct>(in, (32 * j + r) / NT, a.n_actions) * kH : wop;
 #pragma unroll
-        for (int s = 0; s < 2; ++s) epi2(j, s);
+        for (int s = 0; s < 2; ++s) lds8(src + w * 32 + 16 * s + 8 * h, wov[j][s]);
+      }
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        float part = 0.f;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          frag8 hv;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float h2 = relu(z2[j][8 * s + i]);
+            part += wov[IQN ? j : 0][s][i] * h2;
+            hv[i] = (elem_t)h2;
+          }
+          rows(L.b, RA_b, j, 2 * w + s, hv);
+        }
+        part = half_sum(part);
+        if (h == 0) L.qpart[w][32 * j + r] = part;
+      }
     }
     ASVRL_STAMP(6);
     __syncthreads();
@@ -1121,27 +947,8 @@ void critic_fused_kernel(FusedArgs a) {
         const float bo = IQN ? L.boA[ai] : L.bias[kC + 3 * kH];
         const float q = (((L.qpart[0][lr] + L.qpart[1][lr]) + L.qpart[2][lr]) + L.qpart[3][lr]) + bo;
         float wl;
-        float dq;
-        if constexpr (DD) {
-          // the previous round's cos-layer gradient (its cos image is the other buffer of the pair), two MFMAs
-          // per quantile target
-          const bool prev = t != static_cast<int>(blockIdx.x);   // workgroup-uniform
-          const elem_t* cosp = L.cos[sb ^ 1];
-          const TrA<kNcos> TA_d = tr_base<kNcos, LT>(LB, lane);
-          dq = quarter_loss_dq<NT>(a, in + IL::kQn + bl * NT, in[IL::kRew + bl], in[IL::kDon + bl], in[IL::kTau + lr],
-                                   q, q4, &wl, [&](int j) {
-                                     static_assert(NT / 4 == 2 * (G / 16), "one dWc step per target");
-                                     if (prev) {
-                                       if (j > 0) dwc_mfma(j - 1);
-                                       dwc_load(cosp, dzc_w, TA_d, j);
-                                     }
-                                     __builtin_amdgcn_sched_barrier(0);
-                                   });
-          if (prev) dwc_mfma(NT / 4 - 1);
-        } else {
-          dq = quarter_loss_dq<NT>(a, in + IL::kQn + bl * NT, in[IL::kRew + bl], in[IL::kDon + bl],
-                                   in[IL::kTau + lr], q, q4, &wl);
-        }
+        const float dq = quarter_loss_dq<NT>(a, in + IL::kQn + bl * NT, in[IL::kRew + bl], in[IL::kDon + bl],
+                                             in[IL::kTau + lr], q, q4, &wl);
         if (a.tile_loss != nullptr) {
           const float v = seg_sum<16>(wl);   // every lane of the 16-lane row: the group's sum
           if (lane == 0) L.tsum[g] = v;
@@ -1221,8 +1028,7 @@ void critic_fused_kernel(FusedArgs a) {
 
     // ---------------- dW2[own][:] += dz2^T h1g;  L3: dh1g = W2^T dz2 (own block) -> dG, dz1 (own
     // slice into the dz1 image, which nobody reads before the next barrier)
-    constexpr bool L3F = ASVRL_L3_FILL && 2 * NB == (G / 16) * 4 / 4;
-    if constexpr (!L3F) {
+    {
       ASVRL_FRESH_LANE();
       const TrA<kH> TA_a = tr_base<kH, LT>(LB, lane);
       const TrA<kH> TA_b = tr_base<kH, LT>(LB, lane);
@@ -1256,32 +1062,20 @@ void critic_fused_kernel(FusedArgs a) {
         pin(h1k[j][1]);
       }
       float gsa[NB][16];
-      auto epi = [&](int c) {   // block j = c / 2, registers 8 s .. 8 s + 7 with s = c % 2
-        const int j = c >> 1, s = c & 1;
-        frag8 dz1;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float h1 = static_cast<float>(h1k[j][s][i]);
-          const float d = acc[j][8 * s + i];
-          dz1[i] = (elem_t)(h1 > 0.f ? (IQN ? d : d * gv[j][s][i]) : 0.f);
-          gsa[j][8 * s + i] = d * h1;
+      for (int j = 0; j < NB; ++j) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          frag8 dz1;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float h1 = static_cast<float>(h1k[j][s][i]);
+            const float d = acc[j][8 * s + i];
+            dz1[i] = (elem_t)(h1 > 0.f ? (IQN ? d : d * gv[j][s][i]) : 0.f);
+            gsa[j][8 * s + i] = d * h1;
+          }
+          rows(L.dz1, RA_d, j, 2 * w + s, dz1);
         }
-        rows(L.dz1, RA_d, j, 2 * w + s, dz1);
-      };
-      if constexpr (L3F) {
-        const TrA<kH> TA_a = tr_base<kH, LT>(LB, lane);
-        mfma_grid<G / 16, 4>([&](int kk) { return trf(L.b, TA_a, kk, w); },
-                             [&](int kk, int n) { return trf(L.a, TA_a, kk, n); },
-                             [&](int kk, int n, const frag8& A, const frag8& B) {
-                               if (n == 0) db2 += sum8(A);
-                               mfma_acc(dW2[n], A, B);
-                             },
-                             [&](int t) {
-                               if ((t & 3) == 3) epi(t >> 2);
-                             });
-      } else {
-#pragma unroll
-        for (int c = 0; c < 2 * NB; ++c) epi(c);
       }
       ASVRL_STAMP(21);
       if constexpr (!IQN) {
@@ -1332,37 +1126,25 @@ void critic_fused_kernel(FusedArgs a) {
       for (int ks = 0; ks < 8; ++ks) wt[ks] = W1T[((2 * w) * 8 + ks) * 64 + lane];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) wcc[ks] = WCR ? wcr0[ks] : WC[((2 * w) * 4 + ks) * 64 + lane];
-      // the next round's staging (stage-ahead), in pieces between the grid's MFMAs (SF) or after them
-      // (the bench shape: 32 steps, 18 pieces -- the 16 cos values on steps 0..15, F on step 20, G on step 26)
-      constexpr bool SF = AH && ASVRL_STAGE_FILL && (G / 16) * 8 == 32 && kStagePieces == 18;
-      const int tn = t + static_cast<int>(gridDim.x);
-      const bool stg = AH && tn < a.rounds;   // workgroup-uniform
-      mfma_grid<G / 16, 8>([&](int kk) { return trf(L.dz1, TA_d, kk, w); },
-                           [&](int kk, int n) { return trf(L.x, TA_x, kk, n); },
-                           [&](int kk, int n, const frag8& A, const frag8& B) {
-                             if (n == 0) db1 += sum8(A);
-                             mfma_acc(dW1[n], A, B);
-                           },
-                           [&](int st) {
-                             if constexpr (SF) {
-                               const int pc = st < 16 ? st : (st == 20 ? 16 : (st == 26 ? 17 : -1));
-                               if (pc >= 0 && stg)
-                                 stage_piece(pc, tn * G / NT, L.in[buf ^ 1], L.cos[buf ^ 1], L.F[buf ^ 1], L.G[buf ^ 1]);
-                             }
-                           });
+        mfma_grid<G / 16, 8>([&](int kk) { return trf(L.dz1, TA_d, kk, w); },
+                             [&](int kk, int n) { return trf(L.x, TA_x, kk, n); },
+                             [&](int kk, int n, const frag8& A, const frag8& B) {
+                               if (n == 0) db1 += sum8(A);
+                               mfma_acc(dW1[n], A, B);
+                             });
       ASVRL_STAMP(22);
-      if constexpr (AH && !SF) {   // round t + grid's images, behind the dW1 MFMAs
-        if (stg) stage(tn * G / NT, L.in[buf ^ 1], L.cos[buf ^ 1], L.F[buf ^ 1], L.G[buf ^ 1]);
-      }
+    }
+    if constexpr (AH) {   // round t + grid's images, behind the dW1 MFMAs
+      const int tn = t + static_cast<int>(gridDim.x);
+      if (tn < a.rounds) stage(tn * G / NT, L.in[buf ^ 1], L.cos[buf ^ 1], L.F[buf ^ 1], L.G[buf ^ 1]);
     }
     ASVRL_STAMP(23);
 
     // ---------------- L4: dx = W1^T dz1 (own blocks 2w, 2w+1) with c = relu(Wc cos + bc) recomputed
     // (bit-identical to L0's); dF = sum over taus of dx c (-> dzF), dzc = dx F 1[c > 0] into the
     // wave's own dzc image. No barrier: L4 reads dz1 and cos, which nothing writes this round any more.
-    constexpr bool L4P = ASVRL_L4_PIPE && NB == 2 && ASVRL_READ_AHEAD != 0;
 #pragma unroll
-    for (int mq = 0; mq < (L4P ? 0 : 2); ++mq) {
+    for (int mq = 0; mq < 2; ++mq) {
       ASVRL_FRESH_LANE();
       const RowA<kNcos> RA_cos = row_base<kNcos, LT>(LB, lane, r, h);
       const RowA<kH> RA_d = row_base<kH, LT>(LB, lane, r, h);
@@ -1427,76 +1209,6 @@ void critic_fused_kernel(FusedArgs a) {
       });
       ASVRL_STAMP(26 + 3 * mq);
     }
-    if constexpr (L4P) {
-      ASVRL_FRESH_LANE();
-      const RowA<kNcos> RA_cos = row_base<kNcos, LT>(LB, lane, r, h);
-      const RowA<kH> RA_d = row_base<kH, LT>(LB, lane, r, h);
-      const RowA<kNcos> RA_dzc = row_base<kNcos, LT>(LB, lane, r, h);
-      float fv[2][8], fsa[NB][16];   // fv: F of the row block whose epilogue is next
-      f32x16 dxa[2], cca[2];
-      // unit (mq, j): dx = W1^T dz1 (8 k-steps), then c (4 k-steps), B operands read two steps ahead; fill(t)
-      // right behind step t's MFMA
-      auto unit = [&](int mq, int j, auto fill) {
-        dxa[j] = f32x16{};
-        cca[j] = acc_init(bcp, (2 * w + mq) * 32, h);
-        auto bop = [&](int t) { return t < 8 ? rowf(L.dz1, RA_d, j, t) : rowf(cosb, RA_cos, j, t - 8); };
-        frag8 bq[2] = {bop(0), bop(1)};
-#pragma unroll
-        for (int t = 0; t < 12; ++t) {
-          if (t < 8) dxa[j] = mfma(wt[t], bq[t & 1], dxa[j]);
-          else cca[j] = mfma(wcc[t - 8], bq[t & 1], cca[j]);
-          if (t + 2 < 12) bq[t & 1] = bop(t + 2);
-          fill(t);
-          __builtin_amdgcn_sched_barrier(ASVRL_RA_FENCE_MASK);
-        }
-      };
-      // the epilogue of unit (mq, j), half s
-      auto epi = [&](int mq, int j, int s) {
-        if constexpr (!kBiasFirst) if (s == 0) cca[j] += bias_init(bcp, (2 * w + mq) * 32, h);
-        frag8 dz;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float cv = relu(cca[j][8 * s + i]);
-          fsa[j][8 * s + i] = dxa[j][8 * s + i] * cv;
-          dz[i] = (elem_t)(cv > 0.f ? dxa[j][8 * s + i] * fv[s][i] : 0.f);
-        }
-        rows(dzc_w, RA_dzc, j, 2 * mq + s, dz);
-      };
-      auto ldf = [&](int mq, int j) {
-#pragma unroll
-        for (int s = 0; s < 2; ++s) lds8(Fb + ((32 * j + r) / NT) * kC + (2 * w + mq) * 32 + 16 * s + 8 * h, fv[s]);
-      };
-      auto sums = [&](int mq) {
-        sample_sums<NT, NB>(fsa, (2 * w + mq) * 32, lane, [&](int bl, int p, float v) {
-          const float fm = Fb[bl * kC + p];
-          const float dz = fm > 0.f ? v : 0.f;
-          if (a.dzF != nullptr) bp(a.dzF)[static_cast<size_t>(b0 + bl) * kC + swap23(p)] = (elem_t)dz;
-          if (a.parts.enc != nullptr) Fb[bl * kC + p] = dz;   // F's blocks 2w, 2w+1 are this wave's own
-        });
-      };
-#pragma unroll
-      for (int mq = 0; mq < 2; ++mq) {
-        ldf(mq, 0);
-        unit(mq, 0, [](int) {});
-        ASVRL_STAMP(24 + 3 * mq);
-        unit(mq, 1, [&](int t) {
-          if (t == 1) epi(mq, 0, 0);
-          if (t == 6) epi(mq, 0, 1);
-          if (t == 7) ldf(mq, 1);
-        });
-        epi(mq, 1, 0);
-        epi(mq, 1, 1);
-        if (mq == 0) {   // the second block's fragments, behind the first block's dF sums
-#pragma unroll
-          for (int ks = 0; ks < 8; ++ks) wt[ks] = W1T[((2 * w + 1) * 8 + ks) * 64 + lane];
-#pragma unroll
-          for (int ks = 0; ks < 4; ++ks) wcc[ks] = WCR ? wcr1[ks] : WC[((2 * w + 1) * 4 + ks) * 64 + lane];
-        }
-        ASVRL_STAMP(25 + 3 * mq);
-        sums(mq);
-        ASVRL_STAMP(26 + 3 * mq);
-      }
-    }
     {
       if (a.parts.enc != nullptr) {
         // the observation encoders' gradients (AC_IQN_model.py:284-308): lane l owns feature
@@ -1526,9 +1238,8 @@ void critic_fused_kernel(FusedArgs a) {
     }
 
     ASVRL_STAMP(30);
-    // ---------------- dWc[own 64][:] += dzc^T cos (this wave's own dzc image: in-order LDS, no barrier);
-    // with DD in the next round's loss phase instead
-    if constexpr (!DD) {
+    // ---------------- dWc[own 64][:] += dzc^T cos (this wave's own dzc image: in-order LDS, no barrier)
+    {
       ASVRL_FRESH_LANE();
       const TrA<kNcos> TA_cos = tr_base<kNcos, LT>(LB, lane);
       const TrA<kNcos> TA_dzc = tr_base<kNcos, LT>(LB, lane);
@@ -1558,16 +1269,6 @@ void critic_fused_kernel(FusedArgs a) {
     ASVRL_STAMP(15);
   }
 
-  if constexpr (DD) {   // the last round's cos-layer gradient (its images are intact: the loop ended on a barrier)
-    const elem_t* cosp = L.cos[buf ^ 1];
-    const TrA<kNcos> TA_d = tr_base<kNcos, LT>(LB, lane);
-    const elem_t* dzcp = L.dzc[w];
-#pragma unroll
-    for (int u = 0; u < 2 * (G / 16); ++u) {
-      dwc_load(cosp, dzcp, TA_d, u);
-      dwc_mfma(u);
-    }
-  }
   // ---------------- the workgroup's partials: [M*K + M] per layer, features in natural order
   mfma_drain();
   {
