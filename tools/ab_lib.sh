@@ -3,7 +3,7 @@
 # the ACTOR pass (tools/bench_critic.py) and the bench step, alternating: bash tools/ab_lib.sh TAG variant
 cd "${GRAFT_REPO_ROOT:-.}" && mkdir -p gpurun_out
 T=$1; V=$2
-ARGS="--steps 300 --warmup 30 --no-cpu-baseline --iqn-steps 0 --rainbow-steps 0 --config5-steps 0 --plateau-envs 0 --no-learn-b64"
+ARGS="--steps 300 --warmup 30 --no-cpu-baseline --iqn-steps 0 --rainbow-steps 0 --config5-steps 0 --plateau-envs 0 --no-learn-b64 --fp32-steps 0"
 for L in default $V; do
   if [ $L = default ]; then unset ASVRL_LIB; else export ASVRL_LIB=variants/libasvrl_$L.so; fi
   timeout -k 10 120 python tools/fused_time.py --mode target 2>&1 | grep us_median | tee -a gpurun_out/${T}_ab.txt

@@ -30,13 +30,13 @@ if [ "${4:-prof}" = prof ]; then
   (cd /tmp && export TMPDIR=/tmp && rm -rf $R/gpurun_out/${T}_prof && \
    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${T}_prof -o run --output-format csv rocpd \
      -- python3 $R/bench.py --steps 50 --warmup 10 --iqn-steps 0 --rainbow-steps 0 --config5-steps 0 --plateau-envs 0 \
-     --no-cpu-baseline --no-learn-b64 > $R/gpurun_out/${T}_prof.json 2> $R/gpurun_out/${T}_prof.err) || exit 4
+     --no-cpu-baseline --no-learn-b64 --fp32-steps 0 > $R/gpurun_out/${T}_prof.json 2> $R/gpurun_out/${T}_prof.err) || exit 4
   python tools/step_window.py gpurun_out/${T}_prof/run_results.db > gpurun_out/${T}_step_window.txt 2>&1
   head -20 gpurun_out/${T}_step_window.txt
 fi
 if [ "${5:-nopmc}" = pmc ]; then
   rm -rf gpurun_out/pmc
-  BENCH_ARGS="--steps 10 --warmup 5 --no-cpu-baseline --no-learn-b64 --iqn-steps 0 --rainbow-steps 0 --config5-steps 0" \
+  BENCH_ARGS="--steps 10 --warmup 5 --no-cpu-baseline --no-learn-b64 --fp32-steps 0 --iqn-steps 0 --rainbow-steps 0 --config5-steps 0" \
     PMC_EXTRA=1 timeout -k 10 1200 bash tools/pmc_run.sh || exit 5
   python tools/pmc_summary.py gpurun_out/pmc --json gpurun_out/${T}_pmc_summary.json > gpurun_out/${T}_pmc_summary.txt 2>&1
 fi
