@@ -43,7 +43,7 @@ class VecTrainer:
                  learning_starts=None, target_update_interval=2500, total_timesteps=6_000_000,
                  exploration_fraction=0.25, initial_eps=0.6, final_eps=0.05, seed=0,
                  device="cuda", sync=None, graphs=False, schedule=None, net_seed=100, overlap=True, unroll=1,
-                 chain=None, operands="bf16", target_after_env=False, snap_lag=1):
+                 chain=None, operands="bf16", target_after_env=False):
         """Every learner runs on the hand-written kernels (fused_update / fused_iqn / fused_rainbow) with
         FusedAdam; operands="f32" takes them from the f32-operand parity build (libasvrl_f32.so). Shapes
         the kernels do not take raise ValueError."""
@@ -52,15 +52,6 @@ class VecTrainer:
         # chained schedule knob: the AC-IQN learner's target critic waits for the same iteration's env step
         # (the two then run one after the other instead of side by side; results unchanged)
         self.target_after_env = bool(target_after_env)
-        # snap_lag: the learner of iteration i samples the ring as it stood after push(i - snap_lag). 1: the
-        # previous iteration's push (the learner's draw then waits for it: one cross-stream edge per iteration in
-        # the chained graph). 2: one push staler, which the learner is already ordered after through its own
-        # previous actor step (act(i-1) follows push(i-2) on the rollout stream and the actor optimiser of
-        # learn(i-1) waits for act(i-1)), so the chained graph needs no edge for it; 2 E R rows may then be
-        # overwritten concurrently (push(i-1), push(i)) and are skipped (the guard)
-        if snap_lag not in (1, 2):
-            raise ValueError("snap_lag must be 1 or 2")
-        self.snap_lag = int(snap_lag)
         self.continuous = agent_type == "AC-IQN"
         self.env = VecMarineNavEnv(n_envs, num_robots, num_obs, num_cores, min_start_goal_dis, width, seed=seed,
                                    device=self.device, is_continuous=self.continuous, gamma=gamma, schedule=schedule)
@@ -171,15 +162,6 @@ class VecTrainer:
             # and a bench config recording it would be mislabelled
             raise ValueError("target_after_env applies only to the chained, graph-captured AC-IQN schedule")
         self.ring_snap2 = torch.zeros((2, 2), dtype=torch.int64, device=self.device)
-        # snap_lag 2: the chained graph's five snapshot slots (iteration k writes slot k % 5 and samples slot
-        # (k - 2) % 5: three consecutive iterations' slots distinct, the period dividing the unroll); the joined
-        # schedule's two-deep history
-        self.ring_snap5 = torch.zeros((5, 2), dtype=torch.int64, device=self.device)
-        self.ring_hist = torch.zeros((2, 2), dtype=torch.int64, device=self.device)
-        self._hist_parity = 0
-        self._hist_ready = False
-        if self.snap_lag == 2 and self._chained() and self.unroll % 5 != 0:
-            raise ValueError("snap_lag 2 on the chained schedule needs the unroll to be a multiple of 5")
         self._gen = torch.Generator(device=self.device)
         self._gen.manual_seed(seed + 12345)
         self.env.reset()
@@ -313,17 +295,7 @@ class VecTrainer:
         # the replay state the learner samples against (after the previous iteration's push, which
         # the caller's stream joined), copied on the learner's own stream: the learner's chain then
         # starts without a cross-stream wait (each costs ~10 us in a replayed graph)
-        if self.snap_lag == 2:   # hist[p]: after push(i-1) (this copy); hist[1-p]: after push(i-2) (the draw's)
-            p = self._hist_parity
-            self._hist_parity ^= 1
-            if not self._hist_ready:   # the first learning iteration: no older state recorded yet
-                self.ring_hist[1 - p].copy_(self.replay.state)
-                self._hist_ready = True
-            self.ring_hist[p].copy_(self.replay.state)
-            snap = self.ring_hist[1 - p]
-        else:
-            self.ring_snap.copy_(self.replay.state)
-            snap = self.ring_snap
+        self.ring_snap.copy_(self.replay.state)
         s_roll.wait_stream(main)
         with torch.cuda.stream(s_roll):
             self.act()
@@ -333,7 +305,7 @@ class VecTrainer:
             counted = self._push()
             env.auto_reset(counted)
             env.advance_device(counted)
-        out = self.learn(state=snap, guard=self.snap_lag * self.E * self.R, actor_wait=ev_act)
+        out = self.learn(state=self.ring_snap, guard=self.E * self.R, actor_wait=ev_act)
         main.wait_stream(s_roll)
         return out
 
@@ -410,18 +382,13 @@ class VecTrainer:
                 env.step(self.actions)
                 if tae:
                     ev_env[k].record(s_roll)
-                # + the ring state learn(k + snap_lag) samples against
-                self._push(snap=self.ring_snap2[k % 2] if self.snap_lag == 1 else self.ring_snap5[k % 5])
+                self._push(snap=self.ring_snap2[k % 2])   # + the ring state learn(k+1) samples against
                 ev_snap[k].record(s_roll)
                 env.auto_reset(True)
                 env.advance_device(True)
-            if self.snap_lag == 1:
-                if k > 0:
-                    main.wait_event(ev_snap[k - 1])
-                state = self.ring_snap2[(k - 1) % 2]
-            else:   # no edge: ordered through learn(k-1)'s actor optimiser, which waits for act(k-1)
-                state = self.ring_snap5[(k - 2) % 5]
-            out = self.learn(state=state, guard=self.snap_lag * self.E * self.R, actor_wait=ev_act[k],
+            if k > 0:
+                main.wait_event(ev_snap[k - 1])
+            out = self.learn(state=self.ring_snap2[(k - 1) % 2], guard=self.E * self.R, actor_wait=ev_act[k],
                              target_wait=ev_env[k] if tae else None)
             ev_learn[k].record(main)
         main.wait_stream(s_roll)
@@ -441,13 +408,8 @@ class VecTrainer:
         # thread captures; under the default global mode that query invalidates the capture and the
         # watchdog aborts the process
         chained = self._chained()
-        if chained:   # the ring state after the last eager push: what the graph's first learner(s) sample against
+        if chained:   # the ring state after the last eager push: what the graph's first learner samples against
             self.ring_snap2[(self.unroll - 1) % 2].copy_(self.replay.state)
-            # snap_lag 2: the state after the warm-up's second-to-last push (what the joined schedule's history
-            # holds for its next draw), then after its last
-            self.ring_snap5[(self.unroll - 2) % 5].copy_(self.ring_hist[1 - self._hist_parity] if self._hist_ready
-                                                        else self.replay.state)
-            self.ring_snap5[(self.unroll - 1) % 5].copy_(self.replay.state)
         # captured on the dedicated capture stream: torch.cuda.graph's default is a pool stream that a
         # long process also hands out as "another" stream (streams.py)
         with torch.cuda.graph(g, stream=streams.capture_stream(self.device), capture_error_mode="thread_local"):

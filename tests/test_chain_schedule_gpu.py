@@ -11,11 +11,11 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _run(agent_type, chain, iters, n_envs=256, batch=256, unroll=2, target_after_env=False, snap_lag=1):
+def _run(agent_type, chain, iters, n_envs=256, batch=256, unroll=2, target_after_env=False):
     from distributional_rl_decision_and_control_amd.vec_trainer import VecTrainer
     tr = VecTrainer(n_envs=n_envs, agent_type=agent_type, batch_size=batch, num_tau=32, seed=21, graphs=True,
                     unroll=unroll, chain=chain, buffer_size=max(n_envs * 5 * 40, 4 * n_envs * 5),
-                    learning_starts=2 * batch, target_after_env=target_after_env, snap_lag=snap_lag)
+                    learning_starts=2 * batch, target_after_env=target_after_env)
     while tr.replay_size_host() < tr.learning_starts:
         tr.iteration()
     for _ in range(iters):
@@ -49,15 +49,6 @@ def test_chained_schedule_target_after_env_matches_joined():
     ordering only, so bit-identical to the joined schedule too."""
     a, pa, la = _run("AC-IQN", True, 8, target_after_env=True)
     b, pb, lb = _run("AC-IQN", False, 8)
-    _same(a, pa, la, b, pb, lb)
-
-
-def test_chained_schedule_snap_lag2_matches_joined():
-    """snap_lag = 2: each learner samples the ring as it stood one push earlier, which it is already ordered after
-    (no cross-stream edge in the chained graph); the joined schedule keeps a two-deep history of ring states.
-    Ten iterations per graph (the five snapshot slots need an unroll that is a multiple of 5): bit-identical."""
-    a, pa, la = _run("AC-IQN", True, 20, unroll=10, snap_lag=2)
-    b, pb, lb = _run("AC-IQN", False, 20, unroll=10, snap_lag=2)
     _same(a, pa, la, b, pb, lb)
 
 
