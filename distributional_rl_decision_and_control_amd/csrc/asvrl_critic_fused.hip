@@ -203,24 +203,26 @@ struct InLayout {
 // (RowA) / 25 (TrA) VALU instructions each, ~180 per round, where the round's vector issue, not its matrix work,
 // sets its length. Measured 111.0 -> 108.6 us median per launch, bit-identical (profiles/r05f_fused_variants_ab.txt,
 // r05g_fused_fill_variants_ab.txt). Where the table does not fit beside the images (IQN) the bases are computed.
-struct alignas(16) LaneBases {
-  int r64, r128, r256, t64lo, t64hi, t128lo, t128hi, t256lo, t256hi, pad[3];
-};
+#ifndef ASVRL_LANE_TABLE
+#define ASVRL_LANE_TABLE 1
+#endif
+// field-major [field][lane]: a phase's reads of one field are 64 consecutive dwords (conflict-free; a lane-major
+// table of 12-dword rows put four lanes on each bank)
+enum LaneField { kLbR64, kLbR128, kLbR256, kLbT64lo, kLbT64hi, kLbT128lo, kLbT128hi, kLbT256lo, kLbT256hi, kLbFields };
+using LaneBases = int[kLbFields][64];
 template <int P, bool LT>
-__device__ __forceinline__ RowA<P> row_base(const LaneBases* LB, int lane, int r, int h) {
+__device__ __forceinline__ RowA<P> row_base(const int (*LB)[64], int lane, int r, int h) {
   if constexpr (LT) {
-    const LaneBases& b = LB[lane];
-    return RowA<P>(RawBase{}, P == 64 ? b.r64 : (P == 128 ? b.r128 : b.r256));
+    return RowA<P>(RawBase{}, LB[P == 64 ? kLbR64 : (P == 128 ? kLbR128 : kLbR256)][lane]);
   } else {
     return RowA<P>(r, h);
   }
 }
 template <int P, bool LT>
-__device__ __forceinline__ TrA<P> tr_base(const LaneBases* LB, int lane) {
+__device__ __forceinline__ TrA<P> tr_base(const int (*LB)[64], int lane) {
   if constexpr (LT) {
-    const LaneBases& b = LB[lane];
-    return P == 64 ? TrA<P>(RawBase{}, b.t64lo, b.t64hi)
-                   : (P == 128 ? TrA<P>(RawBase{}, b.t128lo, b.t128hi) : TrA<P>(RawBase{}, b.t256lo, b.t256hi));
+    constexpr int f = P == 64 ? kLbT64lo : (P == 128 ? kLbT128lo : kLbT256lo);
+    return TrA<P>(RawBase{}, LB[f][lane], LB[f + 1][lane]);
   } else {
     return TrA<P>(lane);
   }
@@ -608,26 +610,26 @@ void critic_fused_kernel(FusedArgs a) {
   constexpr int NSB = AH ? 2 : 1;
   __shared__ __attribute__((aligned(16))) FusedShared<NT, NB, S, IQN, NSB, TQ> U;
   static_assert(sizeof(U) <= 160 * 1024, "fused critic LDS image exceeds the CU's 160 KB");
-  constexpr bool LT = sizeof(U) + 64 * sizeof(LaneBases) <= 160 * 1024;
-  __shared__ LaneBases LB[LT ? 64 : 1];   // each lane's image bases
+  constexpr bool LT = ASVRL_LANE_TABLE && sizeof(U) + sizeof(LaneBases) <= 160 * 1024;
+  __shared__ int LB[LT ? kLbFields : 1][64];   // each lane's image bases
   auto& L = U.f;
   if constexpr (TQ) target_phase<NT, NB>(a.tq, U.t, a.rounds);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
   if constexpr (LT) {   // read after the prologue's barrier
     if (threadIdx.x < 64) {
-      LaneBases& b = LB[lane];   // the constructors themselves (row_base / tr_base read this table)
-      b.r64 = RowA<kNcos>(r, h).base;
-      b.r128 = RowA<kH>(r, h).base;
-      b.r256 = RowA<kC>(r, h).base;
+      // the constructors themselves (row_base / tr_base read this table)
+      LB[kLbR64][lane] = RowA<kNcos>(r, h).base;
+      LB[kLbR128][lane] = RowA<kH>(r, h).base;
+      LB[kLbR256][lane] = RowA<kC>(r, h).base;
       const auto t64 = TrA<kNcos>(lane);
       const auto t128 = TrA<kH>(lane);
       const auto t256 = TrA<kC>(lane);
-      b.t64lo = t64.lo;
-      b.t64hi = t64.hi;
-      b.t128lo = t128.lo;
-      b.t128hi = t128.hi;
-      b.t256lo = t256.lo;
-      b.t256hi = t256.hi;
+      LB[kLbT64lo][lane] = t64.lo;
+      LB[kLbT64hi][lane] = t64.hi;
+      LB[kLbT128lo][lane] = t128.lo;
+      LB[kLbT128hi][lane] = t128.hi;
+      LB[kLbT256lo][lane] = t256.lo;
+      LB[kLbT256hi][lane] = t256.hi;
     }
   }
   const frag8* WC = reinterpret_cast<const frag8*>(a.w.wc_frag);
