@@ -237,7 +237,7 @@ struct FusedLds {
   elem_t dz1[32 * NB * kH];           // IQN: first the one-hot dq image [G][64] (output layer's dZ)
   elem_t dzc[kNW][32 * NB * kNcos];   // each wave's own dzc image (the A operand of its dWc rows)
   float F[NSB][S * kC];               // position order; operand-rounded values held in f32
-  float G[NSB][IQN ? 4 : S * kH];     // position order (AC-IQN's action features)
+  float G[NSB][IQN ? 1 : S * kH];     // position order (AC-IQN's action features)
   float qpart[kNW][32 * NB];
   float dq[32 * NB];
   float tsum[2 * NB];                 // loss sums of the round's 16-row groups
