@@ -201,8 +201,9 @@ struct InLayout {
 // Each lane's swizzled-image bases (RowA / TrA of the 64-, 128- and 256-position images), computed once per
 // launch into LDS: a phase reads the two or three it uses (ds_read) instead of recomputing them -- about 10
 // (RowA) / 25 (TrA) VALU instructions each, ~180 per round, where the round's vector issue, not its matrix work,
-// sets its length. Measured 111.0 -> 108.6 us median per launch, bit-identical (profiles/r05f_fused_variants_ab.txt,
-// r05g_fused_fill_variants_ab.txt). Where the table does not fit beside the images (IQN) the bases are computed.
+// sets its length. Measured 110.2 -> 107.3 us median per launch, bit-identical, SQ_INSTS_VALU -6.3 %
+// (profiles/r05k_lane_table_ab.txt; r05_pmc_summary.json). Where the table would not fit beside the images the
+// bases are computed.
 #ifndef ASVRL_LANE_TABLE
 #define ASVRL_LANE_TABLE 1
 #endif
