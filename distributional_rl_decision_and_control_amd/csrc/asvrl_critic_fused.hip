@@ -826,10 +826,13 @@ void critic_fused_kernel(FusedArgs a) {
           if constexpr (!kBiasFirst) acc += bias_init(bcp, mb * 32, h);
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
-            frag8 xo;
+            // F >= 0 (a ReLU output), so round(F relu(c)) = relu(round(F c)) up to the sign of a zero:
+            // the ReLU on the packed product (v_pk_max_i16, two values per instruction)
+            float cv[8], xv[8];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) xo[i] = (elem_t)(fv[j][s][i] * relu(acc[8 * s + i]));
-            rows(L.x, RA_x, j, 2 * mb + s, xo);
+            for (int i = 0; i < 8; ++i) cv[i] = acc[8 * s + i];
+            mul8(fv[j][s], cv, xv);
+            rows(L.x, RA_x, j, 2 * mb + s, relu_packed(pack8(xv)));
           }
         }
         if (mq == 0) ASVRL_STAMP(16);
@@ -873,14 +876,12 @@ void critic_fused_kernel(FusedArgs a) {
       for (int j = 0; j < NB; ++j) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          frag8 go;
+          float hv[8], gov[8];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const float hv = relu(acc[j][8 * s + i]);
-            h1k[j][s][i] = (elem_t)hv;
-            go[i] = IQN ? h1k[j][s][i] : (elem_t)(hv * gv[j][s][i]);
-          }
-          rows(L.a, RA_a, j, 2 * w + s, go);
+          for (int i = 0; i < 8; ++i) hv[i] = relu(acc[j][8 * s + i]);
+          h1k[j][s] = pack8(hv);
+          if constexpr (!IQN) mul8(hv, gv[j][s], gov);
+          rows(L.a, RA_a, j, 2 * w + s, IQN ? h1k[j][s] : pack8(gov));
           pin(h1k[j][s]);
         }
       }
@@ -920,14 +921,14 @@ void critic_fused_kernel(FusedArgs a) {
         float part = 0.f;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          frag8 hv;
+          float hv[8];
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             const float h2 = relu(z2[j][8 * s + i]);
             part += wov[IQN ? j : 0][s][i] * h2;
-            hv[i] = (elem_t)h2;
+            hv[i] = h2;
           }
-          rows(L.b, RA_b, j, 2 * w + s, hv);
+          rows(L.b, RA_b, j, 2 * w + s, pack8(hv));
         }
         part = half_sum(part);
         if (h == 0) L.qpart[w][32 * j + r] = part;
@@ -1014,14 +1015,13 @@ void critic_fused_kernel(FusedArgs a) {
       for (int j = 0; j < NB; ++j) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          frag8 dz;
+          float dz[8];
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
-            const float h2 = static_cast<float>(hv[j][s][i]);
-            dz[i] = (elem_t)(h2 > 0.f ? dqv[j] * wov[IQN ? j : 0][s][i] : 0.f);
-            if constexpr (!IQN) dwo[8 * s + i] += dqv[j] * h2;
+            dz[i] = dqv[j] * wov[IQN ? j : 0][s][i];
+            if constexpr (!IQN) dwo[8 * s + i] += dqv[j] * static_cast<float>(hv[j][s][i]);
           }
-          rows(L.b, RA_b, j, 2 * w + s, dz);
+          rows(L.b, RA_b, j, 2 * w + s, mask_pos(pack8(dz), hv[j][s]));   // dq wo 1[h2 > 0]
         }
       }
     }
@@ -1069,15 +1069,20 @@ void critic_fused_kernel(FusedArgs a) {
       for (int j = 0; j < NB; ++j) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          frag8 dz1;
+          float h1[8], d[8], dg[8], hd[8], dz1[8];
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
-            const float h1 = static_cast<float>(h1k[j][s][i]);
-            const float d = acc[j][8 * s + i];
-            dz1[i] = (elem_t)(h1 > 0.f ? (IQN ? d : d * gv[j][s][i]) : 0.f);
-            gsa[j][8 * s + i] = d * h1;
+            h1[i] = static_cast<float>(h1k[j][s][i]);
+            d[i] = acc[j][8 * s + i];
           }
-          rows(L.dz1, RA_d, j, 2 * w + s, dz1);
+          if constexpr (!IQN) mul8(d, gv[j][s], dg);
+          mul8(d, h1, hd);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            dz1[i] = IQN ? d[i] : dg[i];
+            gsa[j][8 * s + i] = hd[i];
+          }
+          rows(L.dz1, RA_d, j, 2 * w + s, mask_pos(pack8(dz1), h1k[j][s]));   // 1[h1 > 0]
         }
       }
       ASVRL_STAMP(21);
@@ -1187,14 +1192,20 @@ void critic_fused_kernel(FusedArgs a) {
         if constexpr (!kBiasFirst) cc += bias_init(bcp, mb * 32, h);
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          frag8 dz;
+          float cv[8], d[8], fs[8], df[8], dz[8];
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
-            const float cv = relu(cc[8 * s + i]);
-            fsa[j][8 * s + i] = dx[8 * s + i] * cv;
-            dz[i] = (elem_t)(cv > 0.f ? dx[8 * s + i] * fv[j][s][i] : 0.f);
+            cv[i] = relu(cc[8 * s + i]);
+            d[i] = dx[8 * s + i];
           }
-          rows(dzc_w, RA_dzc, j, 2 * mq + s, dz);
+          mul8(d, cv, fs);
+          mul8(d, fv[j][s], df);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            fsa[j][8 * s + i] = fs[i];
+            dz[i] = cv[i] > 0.f ? df[i] : 0.f;
+          }
+          rows(dzc_w, RA_dzc, j, 2 * mq + s, pack8(dz));
         }
       }
       if (mq == 0) {   // the second block's fragments

@@ -284,11 +284,9 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
   frag8 cx[kNcos / 16];
 #pragma unroll
   for (int ks = 0; ks < kNcos / 16; ++ks) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = ks * 16 + 8 * h + j;
-      cx[ks][j] = (elem_t)cos_pi_k_tau(tau, k);
-    }
+    float cv[8];
+    cos_pi_k_tau8(tau, ks * 16, h, cv);   // k = 16 ks + 8 h + j
+    cx[ks] = pack8(cv);
     if (TRAINM)
       *reinterpret_cast<frag8*>(bp(a.acts.cos) + static_cast<size_t>(grow) * kNcos + ks * 16 + 8 * h) = cx[ks];
   }
@@ -314,15 +312,15 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         if constexpr (BF) {
-          frag8 cp, hp;
+          float xs[8], fs[8], hs[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const float x = acc0[q4][8 * s + j];
-            cp[j] = (elem_t)x;
-            hp[j] = (elem_t)(static_cast<float>(Fb[feat(mb, 8 * s + j, h)]) * x);
+            xs[j] = acc0[q4][8 * s + j];
+            fs[j] = static_cast<float>(Fb[feat(mb, 8 * s + j, h)]);
           }
-          cpk[mb * 2 + s] = relu_packed(cp);
-          hpk[mb * 2 + s] = relu_packed(hp);
+          mul8(fs, xs, hs);
+          cpk[mb * 2 + s] = relu_packed(pack8(xs));
+          hpk[mb * 2 + s] = relu_packed(pack8(hs));
         } else {
           float hv[8];
 #pragma unroll
@@ -353,15 +351,15 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       if constexpr (BF) {
-        frag8 hp, gp;
+        float xs[8], gs[8], ps[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float x = acc1[mb][8 * s + j];
-          hp[j] = (elem_t)x;
-          if constexpr (!IQN) gp[j] = (elem_t)(x * Gb[feat(mb, 8 * s + j, h)]);
+          xs[j] = acc1[mb][8 * s + j];
+          if constexpr (!IQN) gs[j] = Gb[feat(mb, 8 * s + j, h)];
         }
-        h1pk[mb * 2 + s] = relu_packed(hp);
-        gpk[mb * 2 + s] = IQN ? h1pk[mb * 2 + s] : relu_packed(gp);   // IQN: no action features
+        if constexpr (!IQN) mul8(xs, gs, ps);
+        h1pk[mb * 2 + s] = relu_packed(pack8(xs));
+        gpk[mb * 2 + s] = IQN ? h1pk[mb * 2 + s] : relu_packed(pack8(ps));   // IQN: no action features
       } else {
         float gv[8];
 #pragma unroll
@@ -528,9 +526,9 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
         const float z = acc2[mb][8 * s + j];
         hv[j] = relu(z);
         dv[j] = z > 0.f ? dq * out_w(L, ai, m) : 0.f;
-        dz2pk[mb * 2 + s][j] = (elem_t)dv[j];
         wsa[((mb & 1) * 2 + s) * 8 + j] = dq * hv[j];
       }
+      dz2pk[mb * 2 + s] = pack8(dv);
       if (TRAINM) {
         const size_t o = static_cast<size_t>(grow) * kH + mb * 32 + 16 * s;
         if (!wout) store16(bp(a.acts.h2) + o, hv, h);
@@ -565,16 +563,21 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
   for (int mb = 0; mb < 4; ++mb) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      float dv[8];
+      float dv[8], d3[8], h1[8], gh[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float h1 = static_cast<float>(h1pk[mb * 2 + s][j]);
+        h1[j] = static_cast<float>(h1pk[mb * 2 + s][j]);
+        d3[j] = acc3[mb][8 * s + j];
         if constexpr (IQN) {   // no action features
-          dv[j] = h1 > 0.f ? acc3[mb][8 * s + j] : 0.f;
+          dv[j] = h1[j] > 0.f ? d3[j] : 0.f;
         } else {
-          dv[j] = h1 > 0.f ? acc3[mb][8 * s + j] * G3[feat(mb, 8 * s + j, h)] : 0.f;
-          gsa[(mb * 2 + s) * 8 + j] = acc3[mb][8 * s + j] * h1;
+          dv[j] = h1[j] > 0.f ? d3[j] * G3[feat(mb, 8 * s + j, h)] : 0.f;
         }
+      }
+      if constexpr (!IQN) {
+        mul8(d3, h1, gh);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gsa[(mb * 2 + s) * 8 + j] = gh[j];
       }
       if (TRAINM)
         store16(bp(a.acts.dz1) + static_cast<size_t>(grow) * kH + mb * 32 + 16 * s, dv, h);

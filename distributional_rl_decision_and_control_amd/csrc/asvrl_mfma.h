@@ -178,6 +178,21 @@ __device__ __forceinline__ float cos_pi_k_tau(float tau, int k) {
 #endif
 }
 
+// cos(tau pi k) for k = k0 + 8 h + j, j < 8 (k0 a compile-time multiple of 16, h = lane half): bf16 build,
+// x = tau (k / 2) = fma(tau, k0 / 2 + j / 2, tau * 4h) -- 4h is 0 or 4, so tau * 4h is exact and the fma's
+// one rounding is the product's: bit-identical to cos_pi_k_tau, one VALU instruction per argument
+// instead of three (int -> float, * 0.5, * tau)
+__device__ __forceinline__ void cos_pi_k_tau8(float tau, int k0, int h, float (&c)[8]) {
+#if ASVRL_OPERAND_F32
+#pragma unroll
+  for (int j = 0; j < 8; ++j) c[j] = cos_pi_k_tau(tau, k0 + 8 * h + j);
+#else
+  const float th = h ? 4.f * tau : 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) c[j] = __builtin_amdgcn_cosf(__builtin_fmaf(tau, 0.5f * static_cast<float>(k0 + j), th));
+#endif
+}
+
 __device__ __forceinline__ float relu(float x) { return fmaxf(x, 0.f); }
 
 // ReLU of 8 operand-typed values. bf16: a signed 16-bit max against 0 per half-word (v_pk_max_i16, two
@@ -193,6 +208,64 @@ __device__ __forceinline__ frag8 relu_packed(frag8 v) {
   const s16x8 u = __builtin_elementwise_max(__builtin_bit_cast(s16x8, v), s16x8{});
   return __builtin_bit_cast(frag8, u);
 #endif
+}
+
+// Eight f32 values to one operand fragment, converted two at a time: elements (2p, 2p + 1) by one
+// v_cvt_pk_bf16_f32 into dword p. Written per element, the compiler converted the values one by one (a
+// cvt against 0 each) or paired them off by one (1, 2), (3, 4), ... and repaired the halves with
+// v_perm / v_alignbit: 2.5-4.5 VALU instructions per value instead of 0.5. Same rounding either way.
+__device__ __forceinline__ frag8 pack8(const float (&v)[8]) {
+#if ASVRL_OPERAND_F32
+  frag8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = v[j];
+  return r;
+#else
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  u4 u;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) u[p] = __builtin_bit_cast(unsigned, __builtin_convertvector(f2{v[2 * p], v[2 * p + 1]}, b2));
+  return __builtin_bit_cast(frag8, u);
+#endif
+}
+
+// v where m > 0, else +0 (m: operand values, e.g. a ReLU image): a bf16 is > 0 iff its half-word is > 0
+// as int16, so t = min(max(m, 0) as int16, 1) as unsigned is 1 there and 0 elsewhere (-0 included), and
+// the half-words of v times t are the selection -- three packed 16-bit instructions per two values
+// (v_pk_max_i16, v_pk_min_u16, v_pk_mul_lo_u16) instead of a compare and a select each. Inline asm: in
+// C the compiler sees through the multiply by 0 / 1 and emits the compares and selects again.
+__device__ __forceinline__ frag8 mask_pos(frag8 v, frag8 m) {
+#if ASVRL_OPERAND_F32
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = m[j] > 0.f ? v[j] : 0.f;
+  return v;
+#else
+  typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  const u4 vu = __builtin_bit_cast(u4, v), mu = __builtin_bit_cast(u4, m);
+  u4 r;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    unsigned t;
+    asm("v_pk_max_i16 %0, %2, 0\n\tv_pk_min_u16 %0, %0, %3\n\tv_pk_mul_lo_u16 %0, %1, %0"
+        : "=&v"(t)
+        : "v"(vu[p]), "v"(mu[p]), "s"(0x00010001u));
+    r[p] = t;
+  }
+  return __builtin_bit_cast(frag8, r);
+#endif
+}
+
+// x[i] * y[i] for 8 values, two per v_pk_mul_f32 (the same f32 products)
+__device__ __forceinline__ void mul8(const float (&x)[8], const float (&y)[8], float (&o)[8]) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const f2 r = f2{x[2 * p], x[2 * p + 1]} * f2{y[2 * p], y[2 * p + 1]};
+    o[2 * p] = r.x;
+    o[2 * p + 1] = r.y;
+  }
 }
 
 // f32 accumulator of one 32-feature block initialised with the block's bias (natural feature order:
