@@ -340,17 +340,17 @@ __device__ __forceinline__ void stage_fg(const FusedArgs& a, int b0, int tid, co
 
 // quantile-Huber terms of one row against its sample's N' = NT targets r + gamma q_next (1 - d)
 // (agent.py:399-412), split over four lanes: lane quarter q4 (lanes 16 q4 .. 16 q4 + 15 share the
-// row block) takes targets q4 NT/4 .. + NT/4 - 1 from the staged q_next, and the four partial sums
-// are combined by two lane exchanges (a fixed order). Returns dq; *wl = the row's loss sum.
+// row block) takes targets q4 NT/4 .. + NT/4 - 1 (formed once per sample when the round is staged,
+// stage_targets), and the four partial sums are combined by two lane exchanges (a fixed order).
+// Returns dq; *wl = the row's loss sum.
 template <int NT>
-__device__ __forceinline__ float quarter_loss_dq(const FusedArgs& a, const float* qt, float rb, float done, float tau,
-                                                 float q, int q4, float* wl_out) {
-  const float nd = 1.0f - done;
+__device__ __forceinline__ float quarter_loss_dq(const FusedArgs& a, const float* qt, float tau, float q, int q4,
+                                                 float* wl_out) {
   const float kap = a.kappa, hk = 0.5f * a.kappa, omt = 1.f - tau;
   float wl = 0.f, wg = 0.f;
 #pragma unroll
   for (int j = 0; j < NT / 4; ++j) {
-    const float target = rb + (a.gamma * qt[q4 * (NT / 4) + j]) * nd;   // r + gamma * q_next * (1 - d)
+    const float target = qt[q4 * (NT / 4) + j];
     const float d = target - q;   // td_error (agent.py:406)
     const float ad = fabsf(d);
     const bool quad = ad <= kap;
@@ -691,20 +691,27 @@ void critic_fused_kernel(FusedArgs a) {
   __syncthreads();
 
   // one round's F, G, xb (stage_fg) and cos(tau pi k) rows (natural order) from its staged inputs
-  auto stage = [&](int b0s, const float* ins, elem_t* cosd, float* Fd, float* Gd) {
+  auto stage = [&](int b0s, float* ins, elem_t* cosd, float* Fd, float* Gd) {
     int tid_s = threadIdx.x;
     asm volatile("" : "+v"(tid_s));
     stage_fg<NT, S, G, IQN>(a, b0s, tid_s, ins, L.enc, Fd, Gd);
+    // the round's quantile targets r + gamma q_next (1 - d) (agent.py:399-400), once per (sample, j)
+    // in place over q_next, instead of in every row's loss terms
+    static_assert(S * NT <= kNW * 64, "one target per thread");
+    if (tid_s < S * NT) {
+      const int k = tid_s / NT;
+      float* qn = ins + IL::kQn + tid_s;
+      *qn = ins[IL::kRew + k] + (a.gamma * *qn) * (1.0f - ins[IL::kDon + k]);
+    }
     static_assert((G * (kNcos / 8)) % (kNW * 64) == 0, "whole cos chunks per thread");
 #pragma unroll
     for (int u = 0; u < G * (kNcos / 8) / (kNW * 64); ++u) {
       const int c = tid_s + u * kNW * 64;
       const int row = c / (kNcos / 8), ch = c % (kNcos / 8);
       const float tau = ins[IL::kTau + row];
-      frag8 v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (elem_t)cos_pi_k_tau(tau, 8 * ch + j);
-      row_store<kNcos>(cosd, row, 8 * ch, v);
+      float cv[8];
+      cos_pi_k_tau8r(tau, 8 * ch, cv);
+      row_store<kNcos>(cosd, row, 8 * ch, pack8(cv));
     }
   };
   if constexpr (AH) {
@@ -754,7 +761,7 @@ void critic_fused_kernel(FusedArgs a) {
 #if ASVRL_PRE_AT == 0
     ASVRL_FETCH_PRE();
 #endif
-    const float* in = L.in[buf];
+    float* const in = L.in[buf];
     // the lane indices re-derived through an opaque copy every round: otherwise every LDS / weight
     // address of the round body is loop-invariant, gets hoisted out of the loop and spills
     int tid = threadIdx.x;
@@ -951,8 +958,7 @@ void critic_fused_kernel(FusedArgs a) {
         const float bo = IQN ? L.boA[ai] : L.bias[kC + 3 * kH];
         const float q = (((L.qpart[0][lr] + L.qpart[1][lr]) + L.qpart[2][lr]) + L.qpart[3][lr]) + bo;
         float wl;
-        const float dq = quarter_loss_dq<NT>(a, in + IL::kQn + bl * NT, in[IL::kRew + bl], in[IL::kDon + bl],
-                                             in[IL::kTau + lr], q, q4, &wl);
+        const float dq = quarter_loss_dq<NT>(a, in + IL::kQn + bl * NT, in[IL::kTau + lr], q, q4, &wl);
         if (a.tile_loss != nullptr) {
           const float v = seg_sum<16>(wl);   // every lane of the 16-lane row: the group's sum
           if (lane == 0) L.tsum[g] = v;

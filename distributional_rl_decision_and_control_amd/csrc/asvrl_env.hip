@@ -1034,11 +1034,17 @@ __device__ inline bool far_enough(double ax, double ay, double bx, double by, do
 
 // One wave per env being reset. Every phase is rejection sampling with at most 500 draws in
 // the reference's order (robots env.py:106-120, cores :123-136 with check_core :378-418,
-// obstacles :151-162 with check_obstacle :420-456); here the wave evaluates 64 consecutive
-// candidates at once, accepts the lowest-numbered valid one and restarts right after it --
-// the same accepted sequence as drawing candidates one by one, because candidate c's values
-// come from its own Philox counter (c, env, phase, step) and not from a shared stream.
-// The accepted set of the phase lives in LDS.
+// obstacles :151-162 with check_obstacle :420-456). The wave draws 64 consecutive candidates at
+// once (candidate c's values come from its own Philox counter (c, env, phase, step), not from a
+// shared stream) and tests each against everything accepted so far; then, while the batch holds a
+// valid one, it accepts the lowest-numbered (ballot), broadcasts its values (v_readlane) and drops the
+// candidates before it and those conflicting with it -- the same accepted sequence as testing the
+// candidates one by one (a rejected candidate stays rejected as the accepted set grows; a later one is
+// valid iff it is valid against the old set and the new member). Each batch's draws and tests against
+// the set are made once (round 4's kernel restarted the batch after every acceptance, redrawing and
+// retesting up to 63 candidates each time). The accepted set of the phase lives in LDS for the phases
+// after it. Restated one candidate at a time by oracle/asv_oracle.c or_device_reset (bit-identical:
+// tests/test_env_kernel_gpu.py).
 constexpr int kResetWaves = 4;
 constexpr int kResetMaxR = 32;
 constexpr int kResetMaxO = 32;
@@ -1050,9 +1056,41 @@ struct CandDraw {
                                   static_cast<uint32_t>(phase), ctr}, k0, k1);
     const uint64_t hi = (j & 1) ? r.z : r.x, lo = (j & 1) ? r.w : r.y;
     const uint64_t bits = ((hi << 32) | lo) >> 11;
-    return (static_cast<double>(bits) + 1.0) * (1.0 / 9007199254740992.0);   // (0, 1]
+    return (static_cast<double>(bits) + 1.0) * (1.0 / 9007199254740992.0);
+  }
+  // both doubles of one Philox call (j = 2 p, 2 p + 1)
+  __device__ void u2(int phase, int cand, int p, double& a, double& b) const {
+    const U4 r = philox4x32_10(U4{static_cast<uint32_t>(cand) * 4u + static_cast<uint32_t>(p), e,
+                                  static_cast<uint32_t>(phase), ctr}, k0, k1);
+    a = (static_cast<double>(((static_cast<uint64_t>(r.x) << 32) | r.y) >> 11) + 1.0) * (1.0 / 9007199254740992.0);
+    b = (static_cast<double>(((static_cast<uint64_t>(r.z) << 32) | r.w) >> 11) + 1.0) * (1.0 / 9007199254740992.0);
   }
 };
+
+// lane f's value (f wave-uniform, from a ballot) in every lane
+__device__ __forceinline__ double bcast(double v, int f) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(u), f);
+  const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(u >> 32), f);
+  return __builtin_bit_cast(double, (static_cast<uint64_t>(hi) << 32) | lo);
+}
+
+// check_core (env.py:378-418) of candidate (cx, cy, cw, Gamma) against accepted core (qx, qy, qw, qG):
+// true when they conflict
+__device__ __forceinline__ bool core_conflict(const AsvResetCfg& cfg, double core_r, double qx, double qy, double qw,
+                                              double qG, double cx, double cy, double cw, double Gamma) {
+  const double dx = qx - cx, dy = qy - cy;
+  const double dis = sqrt(dx * dx + dy * dy);
+  if (qw == cw) {
+    const double bi = qG / (2 * kPi * cfg.v_rel_max);
+    const double bj = Gamma / (2 * kPi * cfg.v_rel_max);
+    return dis < bi + bj;
+  }
+  const double gl = fmax(qG, Gamma), gs = fmin(qG, Gamma);
+  const double v1 = gl / (2 * kPi * (dis - 2 * core_r));
+  const double v2 = gs / (2 * kPi * core_r);
+  return v1 > cfg.p_rel * v2;
+}
 
 __global__ __launch_bounds__(kResetWaves * kWave) void env_reset_kernel(AsvParams p, AsvEnvState s, AsvResetCfg cfg,
                                                                         const uint8_t* __restrict__ mask,
@@ -1077,42 +1115,46 @@ __global__ __launch_bounds__(kResetWaves * kWave) void env_reset_kernel(AsvParam
   // ---- robots
   const int want_r = cfg.num_robots < R ? cfg.num_robots : R;
   int nr = 0;
-  for (int base = 0; nr < want_r && base < kDraws;) {
+  for (int base = 0; nr < want_r && base < kDraws; base += kWave) {
     const int c = base + lane;
-    const double sxv = 2.0 + (cfg.width - 4.0) * (1.0 - g.u(0, c, 0));
-    const double syv = 2.0 + (cfg.height - 4.0) * (1.0 - g.u(0, c, 1));
-    const double gxv = 2.0 + (cfg.width - 4.0) * (1.0 - g.u(0, c, 2));
-    const double gyv = 2.0 + (cfg.height - 4.0) * (1.0 - g.u(0, c, 3));
+    double u0, u1, u2, u3;
+    g.u2(0, c, 0, u0, u1);
+    g.u2(0, c, 1, u2, u3);
+    const double sxv = 2.0 + (cfg.width - 4.0) * (1.0 - u0);
+    const double syv = 2.0 + (cfg.height - 4.0) * (1.0 - u1);
+    const double gxv = 2.0 + (cfg.width - 4.0) * (1.0 - u2);
+    const double gyv = 2.0 + (cfg.height - 4.0) * (1.0 - u3);
     bool ok = c < kDraws && far_enough(gxv, gyv, sxv, syv, cfg.min_start_goal_dis, false);  // env.py:361
     for (int k = 0; k < nr && ok; ++k)
       ok = far_enough(srob[wv][0][k], srob[wv][1][k], sxv, syv, cfg.clear_r, true) &&
            far_enough(srob[wv][2][k], srob[wv][3][k], gxv, gyv, cfg.clear_r, true);
-    const uint64_t bal = __ballot(ok);
-    if (bal == 0) {
-      base += kWave;
-      continue;
+    while (nr < want_r) {
+      const uint64_t bal = __ballot(ok);
+      if (bal == 0) break;
+      const int f = __builtin_amdgcn_readfirstlane(__ffsll(static_cast<unsigned long long>(bal)) - 1);
+      const double fx = bcast(sxv, f), fy = bcast(syv, f), fgx = bcast(gxv, f), fgy = bcast(gyv, f);
+      if (lane == f) {
+        srob[wv][0][nr] = sxv;
+        srob[wv][1][nr] = syv;
+        srob[wv][2][nr] = gxv;
+        srob[wv][3][nr] = gyv;
+        const size_t id = static_cast<size_t>(e) * R + nr;
+        rs[ASVRL_F_X * NT + id] = sxv;  // reset_robot / reset_state (env.py:166-176, wamv.py:177-193)
+        rs[ASVRL_F_Y * NT + id] = syv;
+        rs[ASVRL_F_GX * NT + id] = gxv;
+        rs[ASVRL_F_GY * NT + id] = gyv;
+        rs[ASVRL_F_THETA * NT + id] = kTwoPi * (1.0 - g.u(0, c, 4));
+        for (int fld = ASVRL_F_VR0; fld <= ASVRL_F_RP; ++fld) rs[fld * NT + id] = 0.0;
+        rs[ASVRL_F_PHI * NT + id] = 0.0;
+        rs[ASVRL_F_RET * NT + id] = 0.0;
+        s.rflags[id] = 0;
+      }
+      ok = ok && lane > f && far_enough(fx, fy, sxv, syv, cfg.clear_r, true) &&
+           far_enough(fgx, fgy, gxv, gyv, cfg.clear_r, true);
+      ++nr;
     }
-    const int f = __ffsll(static_cast<unsigned long long>(bal)) - 1;
-    if (lane == f) {
-      srob[wv][0][nr] = sxv;
-      srob[wv][1][nr] = syv;
-      srob[wv][2][nr] = gxv;
-      srob[wv][3][nr] = gyv;
-      const size_t id = static_cast<size_t>(e) * R + nr;
-      rs[ASVRL_F_X * NT + id] = sxv;  // reset_robot / reset_state (env.py:166-176, wamv.py:177-193)
-      rs[ASVRL_F_Y * NT + id] = syv;
-      rs[ASVRL_F_GX * NT + id] = gxv;
-      rs[ASVRL_F_GY * NT + id] = gyv;
-      rs[ASVRL_F_THETA * NT + id] = kTwoPi * (1.0 - g.u(0, c, 4));
-      for (int fld = ASVRL_F_VR0; fld <= ASVRL_F_RP; ++fld) rs[fld * NT + id] = 0.0;
-      rs[ASVRL_F_PHI * NT + id] = 0.0;
-      rs[ASVRL_F_RET * NT + id] = 0.0;
-      s.rflags[id] = 0;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // the batch's LDS rows before the next batch's reads
     __builtin_amdgcn_wave_barrier();
-    ++nr;
-    base += f + 1;
   }
   for (int k = nr + lane; k < R; k += kWave) s.rflags[static_cast<size_t>(e) * R + k] = ASVRL_FLAG_DEACTIVATED;
 
@@ -1120,80 +1162,75 @@ __global__ __launch_bounds__(kResetWaves * kWave) void env_reset_kernel(AsvParam
   double* cores = s.cores + static_cast<size_t>(e) * Cmax * 4;
   const int want_c = cfg.num_cores < Cmax ? cfg.num_cores : Cmax;
   int nc = 0;
-  for (int base = 0; nc < want_c && base < kDraws;) {
+  for (int base = 0; nc < want_c && base < kDraws; base += kWave) {
     const int c = base + lane;
-    const double cx = cfg.width * (1.0 - g.u(1, c, 0));
-    const double cy = cfg.height * (1.0 - g.u(1, c, 1));
-    const double cw = g.u(1, c, 2) <= 0.5 ? 1.0 : 0.0;
-    const double ve = cfg.v_lo + (cfg.v_hi - cfg.v_lo) * (1.0 - g.u(1, c, 3));
+    double u0, u1, u2, u3;
+    g.u2(1, c, 0, u0, u1);
+    g.u2(1, c, 1, u2, u3);
+    const double cx = cfg.width * (1.0 - u0);
+    const double cy = cfg.height * (1.0 - u1);
+    const double cw = u2 <= 0.5 ? 1.0 : 0.0;
+    const double ve = cfg.v_lo + (cfg.v_hi - cfg.v_lo) * (1.0 - u3);
     const double Gamma = 2 * kPi * p.core_r * ve;
     bool ok = c < kDraws && !(cx - p.core_r < 0.0 || cx + p.core_r > cfg.width) &&
               !(cy - p.core_r < 0.0 || cy + p.core_r > cfg.width);  // (sic) env.py:383
     for (int k = 0; k < nr && ok; ++k)
       ok = far_enough(cx, cy, srob[wv][0][k], srob[wv][1][k], p.core_r + cfg.clear_r, false) &&
            far_enough(cx, cy, srob[wv][2][k], srob[wv][3][k], p.core_r + cfg.clear_r, false);
-    for (int k = 0; k < nc && ok; ++k) {
-      const double dx = score[wv][k][0] - cx, dy = score[wv][k][1] - cy;
-      const double dis = sqrt(dx * dx + dy * dy);
-      if (score[wv][k][2] == cw) {
-        const double bi = score[wv][k][3] / (2 * kPi * cfg.v_rel_max);
-        const double bj = Gamma / (2 * kPi * cfg.v_rel_max);
-        if (dis < bi + bj) ok = false;
-      } else {
-        const double gl = fmax(score[wv][k][3], Gamma), gs = fmin(score[wv][k][3], Gamma);
-        const double v1 = gl / (2 * kPi * (dis - 2 * p.core_r));
-        const double v2 = gs / (2 * kPi * p.core_r);
-        if (v1 > cfg.p_rel * v2) ok = false;
+    for (int k = 0; k < nc && ok; ++k)
+      ok = !core_conflict(cfg, p.core_r, score[wv][k][0], score[wv][k][1], score[wv][k][2], score[wv][k][3], cx, cy,
+                          cw, Gamma);
+    while (nc < want_c) {
+      const uint64_t bal = __ballot(ok);
+      if (bal == 0) break;
+      const int f = __builtin_amdgcn_readfirstlane(__ffsll(static_cast<unsigned long long>(bal)) - 1);
+      const double fx = bcast(cx, f), fy = bcast(cy, f), fw = bcast(cw, f), fG = bcast(Gamma, f);
+      if (lane == f) {
+        score[wv][nc][0] = cores[4 * nc] = cx;
+        score[wv][nc][1] = cores[4 * nc + 1] = cy;
+        score[wv][nc][2] = cores[4 * nc + 2] = cw;
+        score[wv][nc][3] = cores[4 * nc + 3] = Gamma;
       }
-    }
-    const uint64_t bal = __ballot(ok);
-    if (bal == 0) {
-      base += kWave;
-      continue;
-    }
-    const int f = __ffsll(static_cast<unsigned long long>(bal)) - 1;
-    if (lane == f) {
-      score[wv][nc][0] = cores[4 * nc] = cx;
-      score[wv][nc][1] = cores[4 * nc + 1] = cy;
-      score[wv][nc][2] = cores[4 * nc + 2] = cw;
-      score[wv][nc][3] = cores[4 * nc + 3] = Gamma;
+      ok = ok && lane > f && !core_conflict(cfg, p.core_r, fx, fy, fw, fG, cx, cy, cw, Gamma);
+      ++nc;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
-    ++nc;
-    base += f + 1;
   }
 
   // ---- static obstacles (env.py:151-162, check_obstacle :420-456)
   double* obs = s.obstacles + static_cast<size_t>(e) * O * 3;
   const int want_o = cfg.num_obs < O ? cfg.num_obs : O;
   int no = 0;
-  for (int base = 0; no < want_o && base < kDraws;) {
+  for (int base = 0; no < want_o && base < kDraws; base += kWave) {
     const int c = base + lane;
-    const double ox = 5.0 + (cfg.width - 10.0) * (1.0 - g.u(2, c, 0));
-    const double oy = 5.0 + (cfg.height - 10.0) * (1.0 - g.u(2, c, 1));
-    const double orad = cfg.obs_r_lo + (cfg.obs_r_hi - cfg.obs_r_lo) * (1.0 - g.u(2, c, 2));
+    double u0, u1, u2, u3;
+    g.u2(2, c, 0, u0, u1);
+    g.u2(2, c, 1, u2, u3);
+    const double ox = 5.0 + (cfg.width - 10.0) * (1.0 - u0);
+    const double oy = 5.0 + (cfg.height - 10.0) * (1.0 - u1);
+    const double orad = cfg.obs_r_lo + (cfg.obs_r_hi - cfg.obs_r_lo) * (1.0 - u2);
     bool ok = c < kDraws && !(ox - orad < 0.0 || ox + orad > cfg.width) && !(oy - orad < 0.0 || oy + orad > cfg.height);
     for (int k = 0; k < nr && ok; ++k)
       ok = far_enough(ox, oy, srob[wv][0][k], srob[wv][1][k], orad + cfg.clear_r, false) &&
            far_enough(ox, oy, srob[wv][2][k], srob[wv][3][k], orad + cfg.clear_r, false);
     for (int k = 0; k < nc && ok; ++k) ok = far_enough(score[wv][k][0], score[wv][k][1], ox, oy, p.core_r + orad, true);
     for (int k = 0; k < no && ok; ++k) ok = far_enough(sobs[wv][k][0], sobs[wv][k][1], ox, oy, sobs[wv][k][2] + orad, true);
-    const uint64_t bal = __ballot(ok);
-    if (bal == 0) {
-      base += kWave;
-      continue;
-    }
-    const int f = __ffsll(static_cast<unsigned long long>(bal)) - 1;
-    if (lane == f) {
-      sobs[wv][no][0] = obs[3 * no] = ox;
-      sobs[wv][no][1] = obs[3 * no + 1] = oy;
-      sobs[wv][no][2] = obs[3 * no + 2] = orad;
+    while (no < want_o) {
+      const uint64_t bal = __ballot(ok);
+      if (bal == 0) break;
+      const int f = __builtin_amdgcn_readfirstlane(__ffsll(static_cast<unsigned long long>(bal)) - 1);
+      const double fx = bcast(ox, f), fy = bcast(oy, f), fr = bcast(orad, f);
+      if (lane == f) {
+        sobs[wv][no][0] = obs[3 * no] = ox;
+        sobs[wv][no][1] = obs[3 * no + 1] = oy;
+        sobs[wv][no][2] = obs[3 * no + 2] = orad;
+      }
+      ok = ok && lane > f && far_enough(fx, fy, ox, oy, fr + orad, true);
+      ++no;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
-    ++no;
-    base += f + 1;
   }
   if (lane == 0) {
     s.n_robots[e] = nr;

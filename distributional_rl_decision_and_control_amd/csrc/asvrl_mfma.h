@@ -193,6 +193,19 @@ __device__ __forceinline__ void cos_pi_k_tau8(float tau, int k0, int h, float (&
 #endif
 }
 
+// the same for k = k0 + j, j < 8, with k0 known only at run time: k / 2 = k0 / 2 + j / 2 exactly (one add
+// per argument instead of a conversion and a multiply), then the product with tau as in cos_pi_k_tau
+__device__ __forceinline__ void cos_pi_k_tau8r(float tau, int k0, float (&c)[8]) {
+#if ASVRL_OPERAND_F32
+#pragma unroll
+  for (int j = 0; j < 8; ++j) c[j] = cos_pi_k_tau(tau, k0 + j);
+#else
+  const float hb = 0.5f * static_cast<float>(k0);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) c[j] = __builtin_amdgcn_cosf(tau * (hb + 0.5f * static_cast<float>(j)));
+#endif
+}
+
 __device__ __forceinline__ float relu(float x) { return fmaxf(x, 0.f); }
 
 // ReLU of 8 operand-typed values. bf16: a signed 16-bit max against 0 per half-word (v_pk_max_i16, two

@@ -92,15 +92,22 @@ class VecMarineNavEnv:
         (the rollout's share of the chip beside a concurrent learner; results do not depend on it)."""
         return (0, 0, 0, self.max_groups) if self.max_groups > 0 else None
 
-    def auto_reset(self, counted=False):
+    def auto_reset(self, counted=False, events=None):
         """Reset the envs whose episode ended in the last step and observe them into obs_next.
         counted: the step counter was already incremented for this step (by the replay push launch);
-        the draws are keyed as if it had not been."""
+        the draws are keyed as if it had not been. events: three HIP events recorded on the current
+        stream before the reset, between the reset and the observation pass, and after it (bench.py)."""
         b = self.batch
         d = 1 if counted else 0
+        if events is not None:
+            events[0].record()
         b.reset(self.cfg, b.env_done, seed=self.seed, counter=0x40000000 - d, counter_dev=self.counter)
+        if events is not None:
+            events[1].record()
         b.step(None, do_dynamics=False, seed=self.seed, counter=0x80000000 - d, counter_dev=self.counter,
                fast_noise=True, env_mask=b.env_done, obs=self.obs_next, obj_cnt=self.cnt_next, launch=self._launch())
+        if events is not None:
+            events[2].record()
 
     def advance_device(self, counted=False):
         if self.swap:

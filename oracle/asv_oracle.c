@@ -516,3 +516,84 @@ int64_t or_batch_rollout(const OrParams* p, int E, int R, int O, int steps, uint
   if (checksum) *checksum = chk;
   return total;
 }
+
+/* ---------------------------------------------------------------- device reset, sequential */
+static double cand_u(uint32_t k0, uint32_t k1, uint32_t e, uint32_t ctr, int phase, int cand, int j) {
+  u32x4 r = philox((uint32_t)cand * 4u + (uint32_t)(j >> 1), e, (uint32_t)phase, ctr, k0, k1);
+  uint64_t hi = (j & 1) ? r.v[2] : r.v[0], lo = (j & 1) ? r.v[3] : r.v[1];
+  uint64_t bits = ((hi << 32) | lo) >> 11;
+  return ((double)bits + 1.0) * (1.0 / 9007199254740992.0);
+}
+
+/* np.linalg.norm(a - b) >= lim (strict = 0) or > lim (strict = 1), as the reference's tests read */
+static int far_enough(double ax, double ay, double bx, double by, double lim, int strict) {
+  double dx = ax - bx, dy = ay - by, d = sqrt(dx * dx + dy * dy);
+  return strict ? !(d <= lim) : !(d < lim);
+}
+
+void or_device_reset(const OrResetCfg* cfg, double core_r, int R, int O, int C, uint64_t seed, uint64_t counter,
+                     int e, double* rob, int* n_robots, double* cores, int* n_cores, double* obs, int* n_obs) {
+  const double kPi = 3.14159265358979323846;
+  uint64_t key = seed ^ (counter >> 32) * 0x9E3779B97F4A7C15ull;
+  uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32), ctr = (uint32_t)counter, ue = (uint32_t)e;
+  int want = cfg->num_robots < R ? cfg->num_robots : R, nr = 0;
+  for (int c = 0; c < 500 && nr < want; ++c) {   /* robots: start and goal (env.py:106-120) */
+    double sx = 2.0 + (cfg->width - 4.0) * (1.0 - cand_u(k0, k1, ue, ctr, 0, c, 0));
+    double sy = 2.0 + (cfg->height - 4.0) * (1.0 - cand_u(k0, k1, ue, ctr, 0, c, 1));
+    double gx = 2.0 + (cfg->width - 4.0) * (1.0 - cand_u(k0, k1, ue, ctr, 0, c, 2));
+    double gy = 2.0 + (cfg->height - 4.0) * (1.0 - cand_u(k0, k1, ue, ctr, 0, c, 3));
+    int ok = far_enough(gx, gy, sx, sy, cfg->min_start_goal_dis, 0);   /* env.py:361 */
+    for (int k = 0; k < nr && ok; ++k)
+      ok = far_enough(rob[5 * k], rob[5 * k + 1], sx, sy, cfg->clear_r, 1) &&
+           far_enough(rob[5 * k + 2], rob[5 * k + 3], gx, gy, cfg->clear_r, 1);
+    if (!ok) continue;
+    double* o = rob + 5 * nr++;
+    o[0] = sx; o[1] = sy; o[2] = gx; o[3] = gy;
+    o[4] = 2 * kPi * (1.0 - cand_u(k0, k1, ue, ctr, 0, c, 4));
+  }
+  *n_robots = nr;
+  int wc = cfg->num_cores < C ? cfg->num_cores : C, nc = 0;
+  for (int c = 0; c < 500 && nc < wc; ++c) {   /* vortex cores (env.py:123-136, check_core :378-418) */
+    double cx = cfg->width * (1.0 - cand_u(k0, k1, ue, ctr, 1, c, 0));
+    double cy = cfg->height * (1.0 - cand_u(k0, k1, ue, ctr, 1, c, 1));
+    double cw = cand_u(k0, k1, ue, ctr, 1, c, 2) <= 0.5 ? 1.0 : 0.0;
+    double ve = cfg->v_lo + (cfg->v_hi - cfg->v_lo) * (1.0 - cand_u(k0, k1, ue, ctr, 1, c, 3));
+    double Gamma = 2 * kPi * core_r * ve;
+    int ok = !(cx - core_r < 0.0 || cx + core_r > cfg->width) && !(cy - core_r < 0.0 || cy + core_r > cfg->width);
+    for (int k = 0; k < nr && ok; ++k)
+      ok = far_enough(cx, cy, rob[5 * k], rob[5 * k + 1], core_r + cfg->clear_r, 0) &&
+           far_enough(cx, cy, rob[5 * k + 2], rob[5 * k + 3], core_r + cfg->clear_r, 0);
+    for (int k = 0; k < nc && ok; ++k) {
+      const double* q = cores + 4 * k;
+      double dx = q[0] - cx, dy = q[1] - cy, dis = sqrt(dx * dx + dy * dy);
+      if (q[2] == cw) {
+        double bi = q[3] / (2 * kPi * cfg->v_rel_max), bj = Gamma / (2 * kPi * cfg->v_rel_max);
+        if (dis < bi + bj) ok = 0;
+      } else {
+        double gl = fmax(q[3], Gamma), gs = fmin(q[3], Gamma);
+        double v1 = gl / (2 * kPi * (dis - 2 * core_r)), v2 = gs / (2 * kPi * core_r);
+        if (v1 > cfg->p_rel * v2) ok = 0;
+      }
+    }
+    if (!ok) continue;
+    double* o = cores + 4 * nc++;
+    o[0] = cx; o[1] = cy; o[2] = cw; o[3] = Gamma;
+  }
+  *n_cores = nc;
+  int wo = cfg->num_obs < O ? cfg->num_obs : O, no = 0;
+  for (int c = 0; c < 500 && no < wo; ++c) {   /* static obstacles (env.py:151-162, check_obstacle :420-456) */
+    double ox = 5.0 + (cfg->width - 10.0) * (1.0 - cand_u(k0, k1, ue, ctr, 2, c, 0));
+    double oy = 5.0 + (cfg->height - 10.0) * (1.0 - cand_u(k0, k1, ue, ctr, 2, c, 1));
+    double orad = cfg->obs_r_lo + (cfg->obs_r_hi - cfg->obs_r_lo) * (1.0 - cand_u(k0, k1, ue, ctr, 2, c, 2));
+    int ok = !(ox - orad < 0.0 || ox + orad > cfg->width) && !(oy - orad < 0.0 || oy + orad > cfg->height);
+    for (int k = 0; k < nr && ok; ++k)
+      ok = far_enough(ox, oy, rob[5 * k], rob[5 * k + 1], orad + cfg->clear_r, 0) &&
+           far_enough(ox, oy, rob[5 * k + 2], rob[5 * k + 3], orad + cfg->clear_r, 0);
+    for (int k = 0; k < nc && ok; ++k) ok = far_enough(cores[4 * k], cores[4 * k + 1], ox, oy, core_r + orad, 1);
+    for (int k = 0; k < no && ok; ++k) ok = far_enough(obs[3 * k], obs[3 * k + 1], ox, oy, obs[3 * k + 2] + orad, 1);
+    if (!ok) continue;
+    double* o = obs + 3 * no++;
+    o[0] = ox; o[1] = oy; o[2] = orad;
+  }
+  *n_obs = no;
+}

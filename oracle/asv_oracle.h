@@ -73,6 +73,23 @@ int or_env_step(const OrParams* p, OrRobot* robots, int n_robots, int R, const d
 int64_t or_batch_rollout(const OrParams* p, int E, int R, int O, int steps, uint64_t seed,
                          int threads, double* checksum);
 
+/* The fast path's device reset (asvrl_env_reset) restated one candidate at a time: MarineNavEnv3.reset's
+ * rejection sampling (robots env.py:106-120 with check_start_and_goal :360-376, cores :123-136 with
+ * check_core :378-418, obstacles :151-162 with check_obstacle :420-456), each phase drawing candidates
+ * c = 0, 1, ... in order, accepting the ones valid against everything accepted before them, at most 500
+ * candidates per phase. Candidate c's values come from Philox-4x32-10 at counter (4c + j/2, env, phase,
+ * counter) under the key seed ^ (counter >> 32) * 0x9E3779B97F4A7C15 (the device streams; the reference
+ * draws them from np.random instead, so this pins the kernel's sequential semantics, not the
+ * reference's numbers). Outputs for env e: robots [R][5] = x, y, gx, gy, theta; n_robots; cores
+ * [n][4] = x, y, clockwise, Gamma; obstacles [n][3] = x, y, r. cfg: AsvResetCfg's fields in order. */
+typedef struct OrResetCfg {
+  int32_t num_robots, num_obs, num_cores, _pad0;
+  double min_start_goal_dis, width, height, clear_r, obs_r_lo, obs_r_hi, v_lo, v_hi, v_rel_max, p_rel;
+} OrResetCfg;
+void or_device_reset(const OrResetCfg* cfg, double core_r, int R, int O, int C, uint64_t seed, uint64_t counter,
+                     int e, double* robots, int* n_robots, double* cores, int* n_cores, double* obstacles,
+                     int* n_obs);
+
 /* C51 projection restated from agent.py:616-631 in f32 with the CPU index_add_ order. */
 void or_c51_project(const float* pns_a, const float* returns, const float* nonterminal,
                     const float* support, int B, int atoms, float vmin, float vmax,

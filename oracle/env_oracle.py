@@ -67,8 +67,24 @@ def lib():
         L.or_batch_rollout.restype = C.c_int64
         fp = C.POINTER(C.c_float)
         L.or_c51_project.argtypes = [fp, fp, fp, fp, C.c_int, C.c_int, C.c_float, C.c_float, C.c_float, fp]
+        ip = C.POINTER(C.c_int)
+        L.or_device_reset.argtypes = [C.c_void_p, C.c_double, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_uint64,
+                                      C.c_int, dp, ip, dp, ip, dp, ip]
         _lib = L
     return _lib
+
+
+def device_reset(cfg, core_r, R, O, Cmax, seed, counter, e):
+    """The device reset of env e restated one candidate at a time (or_device_reset; cfg: an AsvResetCfg,
+    whose layout OrResetCfg mirrors). Returns (robots [n][5] x, y, gx, gy, theta, cores [n][4],
+    obstacles [n][3])."""
+    rob = np.zeros((max(R, 1), 5))
+    cor = np.zeros((max(Cmax, 1), 4))
+    obs = np.zeros((max(O, 1), 3))
+    nr, nc, no = C.c_int(), C.c_int(), C.c_int()
+    lib().or_device_reset(C.addressof(cfg), float(core_r), R, O, Cmax, seed, counter, e, _dp(rob), C.byref(nr),
+                          _dp(cor), C.byref(nc), _dp(obs), C.byref(no))
+    return rob[:nr.value], cor[:nc.value], obs[:no.value]
 
 
 def _dp(a):

@@ -450,3 +450,51 @@ def test_pair_kernel_matches_sweep(R, O, W, C, fast):
             # object closer than its radius + 1 (asin of a ratio > 1, wamv.py:388); it never enters a reward
             torch.testing.assert_close(x, y, rtol=0, atol=0, equal_nan=True,
                                        msg=f"layout {launch} differs from the sweep at output {t}")
+
+
+@pytest.mark.parametrize("R,O,Cn,W,obs_r,v", [(5, 4, 0, 55.0, (1.0, 1.0), (3.0, 3.0)),
+                                              (5, 4, 3, 55.0, (0.5, 3.0), (2.0, 4.0)),
+                                              (17, 4, 0, 110.0, (1.0, 1.0), (3.0, 3.0)),
+                                              (8, 12, 4, 80.0, (0.5, 2.5), (1.0, 5.0))])
+def test_device_reset_matches_sequential_restatement(R, O, Cn, W, obs_r, v):
+    """asvrl_env_reset evaluates a wave of 64 candidates at a time and accepts in candidate order; the
+    C oracle (or_device_reset) restates the same sampler one candidate at a time, as MarineNavEnv3.reset
+    draws them (env.py:106-162). Bit-identical robots (start, goal, heading), cores and obstacles on
+    every env, for a full reset and for a masked reset at a device counter (the training loop's
+    auto-reset), where the envs outside the mask must stay untouched."""
+    from oracle import env_oracle as eo
+    from distributional_rl_decision_and_control_amd import _abi
+    from distributional_rl_decision_and_control_amd.device_env import DeviceEnvBatch, reset_cfg
+    E = 384
+    cfg = reset_cfg(R, O, Cn, 30.0, width=W, height=W, obs_r_range=obs_r, v_range=v)
+    b = DeviceEnvBatch(E, R, O, max(Cn, 1))
+    core_r = float(b.params.core_r)
+
+    def check(envs, seed, counter):
+        rs = b.rs.cpu().numpy().reshape(-1, E, R)
+        nr, nc, no = b.n_robots.cpu().numpy(), b.n_cores.cpu().numpy(), b.n_obs.cpu().numpy()
+        cores, obst, fl = b.cores.cpu().numpy(), b.obstacles.cpu().numpy(), b.rflags.cpu().numpy().reshape(E, R)
+        for e in envs:
+            rob, cor, ob = eo.device_reset(cfg, core_r, R, O, max(Cn, 1), seed, counter, int(e))
+            n = len(rob)
+            assert nr[e] == n and nc[e] == len(cor) and no[e] == len(ob), e
+            got = np.stack([rs[_abi.F_X][e, :n], rs[_abi.F_Y][e, :n], rs[_abi.F_GX][e, :n], rs[_abi.F_GY][e, :n],
+                            rs[_abi.F_THETA][e, :n]], axis=1)
+            np.testing.assert_array_equal(got, rob)
+            np.testing.assert_array_equal(cores[e, :len(cor)], cor)
+            np.testing.assert_array_equal(obst[e, :len(ob)], ob)
+            assert (fl[e, n:] == _abi.FLAG_DEACTIVATED).all() and (fl[e, :n] == 0).all()
+
+    b.reset(cfg, seed=21, counter=5)
+    torch.cuda.synchronize()
+    check(range(E), 21, 5)
+    # masked, counter partly on the device: the key and counter of the envs reset now are (5 + 7 + 2^33)
+    mask = (torch.arange(E, device="cuda") % 3 == 1).to(torch.uint8)
+    before = b.rs.clone()
+    cdev = torch.tensor([7 + (1 << 33)], dtype=torch.int64, device="cuda")
+    b.reset(cfg, mask, seed=21, counter=5, counter_dev=cdev)
+    torch.cuda.synchronize()
+    m = mask.cpu().numpy().astype(bool)
+    rs0, rs1 = before.cpu().numpy().reshape(-1, E, R), b.rs.cpu().numpy().reshape(-1, E, R)
+    np.testing.assert_array_equal(rs0[:, ~m], rs1[:, ~m])
+    check(np.nonzero(m)[0], 21, 5 + 7 + (1 << 33))
