@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("ASVRL_LIB", os.path.join(HERE, "lib", "libasvrl.so"))
 # the same sources built with f32 learner operands (the parity build; asvrl_operand_bytes() == 4)
 LIB_PATH_F32 = os.path.join(HERE, "lib", "libasvrl_f32.so")
 OPERANDS = {"bf16": (LIB_PATH, 2), "f32": (LIB_PATH_F32, 4)}
-ABI_VERSION = 21
+ABI_VERSION = 22
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
 OBS_DIM = 40   # self 7 | objects 25 | mask 5 | pad 3
@@ -245,6 +245,8 @@ EXPORTS = [
                                     C.POINTER(AsvStepOut), C.POINTER(AsvEnvLaunch), _VP]),
     ("asvrl_env_reset", C.c_int, [C.POINTER(AsvParams), C.POINTER(AsvEnvState), C.POINTER(AsvResetCfg), _VP, _U64,
                                   _U64, _VP, _VP]),
+    ("asvrl_env_reset_observe", C.c_int, [C.POINTER(AsvParams), C.POINTER(AsvEnvState), C.POINTER(AsvResetCfg), _VP,
+                                          _U64, _U64, _VP, C.POINTER(AsvStepCtl), C.POINTER(AsvStepOut), _VP]),
     ("asvrl_current_field", C.c_int, [_VP, _I32, _D, _VP, _I32, _VP, _VP]),
     ("asvrl_quantile_huber", C.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, _F, _F, _VP, _VP, _VP, _VP]),
     ("asvrl_c51_project", C.c_int, [_VP, _VP, _VP, _VP, _I32, _I32, _F, _F, _F, _F, _VP, _VP]),

@@ -1092,21 +1092,22 @@ __device__ __forceinline__ bool core_conflict(const AsvResetCfg& cfg, double cor
   return v1 > cfg.p_rel * v2;
 }
 
-__global__ __launch_bounds__(kResetWaves * kWave) void env_reset_kernel(AsvParams p, AsvEnvState s, AsvResetCfg cfg,
-                                                                        const uint8_t* __restrict__ mask,
-                                                                        uint64_t seed, uint64_t counter,
-                                                                        const uint64_t* __restrict__ counter_dev) {
-  __shared__ double srob[kResetWaves][4][kResetMaxR];      // x, y, gx, gy of accepted robots
-  __shared__ double score[kResetWaves][kMaxCores][4];      // x, y, clockwise, Gamma
-  __shared__ double sobs[kResetWaves][kResetMaxO][3];      // x, y, r
-  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
-  const int e = blockIdx.x * kResetWaves + wv;
-  if (e >= s.n_envs) return;                     // wave-uniform exits
-  if (mask != nullptr && mask[e] == 0) return;
+// The accepted sets of one env's reset, in the resetting wave's LDS
+struct ResetLds {
+  double rob[4][kResetMaxR];      // x, y, gx, gy of accepted robots
+  double core[kMaxCores][4];      // x, y, clockwise, Gamma
+  double obs[kResetMaxO][3];      // x, y, r
+};
+
+// env e's reset by one wave (lane = its lane index)
+__device__ __forceinline__ void reset_env(const AsvParams& p, const AsvEnvState& s, const AsvResetCfg& cfg, int e,
+                                          uint64_t seed, uint64_t ctr, int lane, ResetLds& W) {
+  double (*srob)[kResetMaxR] = W.rob;
+  double (*score)[4] = W.core;
+  double (*sobs)[3] = W.obs;
   const int R = s.max_robots, O = s.max_obs, Cmax = s.max_cores;
   const size_t NT = static_cast<size_t>(s.n_envs) * R;
   double* rs = s.rs;
-  const uint64_t ctr = counter + (counter_dev != nullptr ? *counter_dev : 0ull);
   const uint64_t key = seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull;
   const CandDraw g{static_cast<uint32_t>(key), static_cast<uint32_t>(key >> 32), static_cast<uint32_t>(e),
                    static_cast<uint32_t>(ctr)};
@@ -1126,18 +1127,18 @@ __global__ __launch_bounds__(kResetWaves * kWave) void env_reset_kernel(AsvParam
     const double gyv = 2.0 + (cfg.height - 4.0) * (1.0 - u3);
     bool ok = c < kDraws && far_enough(gxv, gyv, sxv, syv, cfg.min_start_goal_dis, false);  // env.py:361
     for (int k = 0; k < nr && ok; ++k)
-      ok = far_enough(srob[wv][0][k], srob[wv][1][k], sxv, syv, cfg.clear_r, true) &&
-           far_enough(srob[wv][2][k], srob[wv][3][k], gxv, gyv, cfg.clear_r, true);
+      ok = far_enough(srob[0][k], srob[1][k], sxv, syv, cfg.clear_r, true) &&
+           far_enough(srob[2][k], srob[3][k], gxv, gyv, cfg.clear_r, true);
     while (nr < want_r) {
       const uint64_t bal = __ballot(ok);
       if (bal == 0) break;
       const int f = __builtin_amdgcn_readfirstlane(__ffsll(static_cast<unsigned long long>(bal)) - 1);
       const double fx = bcast(sxv, f), fy = bcast(syv, f), fgx = bcast(gxv, f), fgy = bcast(gyv, f);
       if (lane == f) {
-        srob[wv][0][nr] = sxv;
-        srob[wv][1][nr] = syv;
-        srob[wv][2][nr] = gxv;
-        srob[wv][3][nr] = gyv;
+        srob[0][nr] = sxv;
+        srob[1][nr] = syv;
+        srob[2][nr] = gxv;
+        srob[3][nr] = gyv;
         const size_t id = static_cast<size_t>(e) * R + nr;
         rs[ASVRL_F_X * NT + id] = sxv;  // reset_robot / reset_state (env.py:166-176, wamv.py:177-193)
         rs[ASVRL_F_Y * NT + id] = syv;
@@ -1175,10 +1176,10 @@ __global__ __launch_bounds__(kResetWaves * kWave) void env_reset_kernel(AsvParam
     bool ok = c < kDraws && !(cx - p.core_r < 0.0 || cx + p.core_r > cfg.width) &&
               !(cy - p.core_r < 0.0 || cy + p.core_r > cfg.width);  // (sic) env.py:383
     for (int k = 0; k < nr && ok; ++k)
-      ok = far_enough(cx, cy, srob[wv][0][k], srob[wv][1][k], p.core_r + cfg.clear_r, false) &&
-           far_enough(cx, cy, srob[wv][2][k], srob[wv][3][k], p.core_r + cfg.clear_r, false);
+      ok = far_enough(cx, cy, srob[0][k], srob[1][k], p.core_r + cfg.clear_r, false) &&
+           far_enough(cx, cy, srob[2][k], srob[3][k], p.core_r + cfg.clear_r, false);
     for (int k = 0; k < nc && ok; ++k)
-      ok = !core_conflict(cfg, p.core_r, score[wv][k][0], score[wv][k][1], score[wv][k][2], score[wv][k][3], cx, cy,
+      ok = !core_conflict(cfg, p.core_r, score[k][0], score[k][1], score[k][2], score[k][3], cx, cy,
                           cw, Gamma);
     while (nc < want_c) {
       const uint64_t bal = __ballot(ok);
@@ -1186,10 +1187,10 @@ __global__ __launch_bounds__(kResetWaves * kWave) void env_reset_kernel(AsvParam
       const int f = __builtin_amdgcn_readfirstlane(__ffsll(static_cast<unsigned long long>(bal)) - 1);
       const double fx = bcast(cx, f), fy = bcast(cy, f), fw = bcast(cw, f), fG = bcast(Gamma, f);
       if (lane == f) {
-        score[wv][nc][0] = cores[4 * nc] = cx;
-        score[wv][nc][1] = cores[4 * nc + 1] = cy;
-        score[wv][nc][2] = cores[4 * nc + 2] = cw;
-        score[wv][nc][3] = cores[4 * nc + 3] = Gamma;
+        score[nc][0] = cores[4 * nc] = cx;
+        score[nc][1] = cores[4 * nc + 1] = cy;
+        score[nc][2] = cores[4 * nc + 2] = cw;
+        score[nc][3] = cores[4 * nc + 3] = Gamma;
       }
       ok = ok && lane > f && !core_conflict(cfg, p.core_r, fx, fy, fw, fG, cx, cy, cw, Gamma);
       ++nc;
@@ -1212,19 +1213,19 @@ __global__ __launch_bounds__(kResetWaves * kWave) void env_reset_kernel(AsvParam
     const double orad = cfg.obs_r_lo + (cfg.obs_r_hi - cfg.obs_r_lo) * (1.0 - u2);
     bool ok = c < kDraws && !(ox - orad < 0.0 || ox + orad > cfg.width) && !(oy - orad < 0.0 || oy + orad > cfg.height);
     for (int k = 0; k < nr && ok; ++k)
-      ok = far_enough(ox, oy, srob[wv][0][k], srob[wv][1][k], orad + cfg.clear_r, false) &&
-           far_enough(ox, oy, srob[wv][2][k], srob[wv][3][k], orad + cfg.clear_r, false);
-    for (int k = 0; k < nc && ok; ++k) ok = far_enough(score[wv][k][0], score[wv][k][1], ox, oy, p.core_r + orad, true);
-    for (int k = 0; k < no && ok; ++k) ok = far_enough(sobs[wv][k][0], sobs[wv][k][1], ox, oy, sobs[wv][k][2] + orad, true);
+      ok = far_enough(ox, oy, srob[0][k], srob[1][k], orad + cfg.clear_r, false) &&
+           far_enough(ox, oy, srob[2][k], srob[3][k], orad + cfg.clear_r, false);
+    for (int k = 0; k < nc && ok; ++k) ok = far_enough(score[k][0], score[k][1], ox, oy, p.core_r + orad, true);
+    for (int k = 0; k < no && ok; ++k) ok = far_enough(sobs[k][0], sobs[k][1], ox, oy, sobs[k][2] + orad, true);
     while (no < want_o) {
       const uint64_t bal = __ballot(ok);
       if (bal == 0) break;
       const int f = __builtin_amdgcn_readfirstlane(__ffsll(static_cast<unsigned long long>(bal)) - 1);
       const double fx = bcast(ox, f), fy = bcast(oy, f), fr = bcast(orad, f);
       if (lane == f) {
-        sobs[wv][no][0] = obs[3 * no] = ox;
-        sobs[wv][no][1] = obs[3 * no + 1] = oy;
-        sobs[wv][no][2] = obs[3 * no + 2] = orad;
+        sobs[no][0] = obs[3 * no] = ox;
+        sobs[no][1] = obs[3 * no + 1] = oy;
+        sobs[no][2] = obs[3 * no + 2] = orad;
       }
       ok = ok && lane > f && far_enough(fx, fy, ox, oy, fr + orad, true);
       ++no;
@@ -1238,6 +1239,37 @@ __global__ __launch_bounds__(kResetWaves * kWave) void env_reset_kernel(AsvParam
     s.n_obs[e] = no;
     s.ep_ts[e] = 0;
   }
+}
+
+__global__ __launch_bounds__(kResetWaves * kWave) void env_reset_kernel(AsvParams p, AsvEnvState s, AsvResetCfg cfg,
+                                                                        const uint8_t* __restrict__ mask,
+                                                                        uint64_t seed, uint64_t counter,
+                                                                        const uint64_t* __restrict__ counter_dev) {
+  __shared__ ResetLds W[kResetWaves];
+  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  const int e = blockIdx.x * kResetWaves + wv;
+  if (e >= s.n_envs) return;                     // wave-uniform exits
+  if (mask != nullptr && mask[e] == 0) return;
+  reset_env(p, s, cfg, e, seed, counter + (counter_dev != nullptr ? *counter_dev : 0ull), lane, W[wv]);
+}
+
+// The training loop's auto-reset in ONE launch (asvrl_env_reset_observe): workgroup e is one wave; if env e
+// ended its episode (mask), the wave resets it (reset_env) and then computes its reset observation with the
+// step kernel's own phases (env_pairs_block, one env per workgroup, do_dynamics = 0): the same values as
+// asvrl_env_reset followed by the masked asvrl_env_step pass, without the second launch over every env.
+template <int NM>
+__global__ __launch_bounds__(kWave) void env_reset_observe_kernel(AsvParams p, AsvEnvState s, AsvResetCfg cfg,
+                                                                  const uint8_t* __restrict__ mask, uint64_t seed,
+                                                                  uint64_t counter,
+                                                                  const uint64_t* __restrict__ counter_dev,
+                                                                  AsvStepCtl ctl, AsvStepOut out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];   // env_pairs_block's carve
+  __shared__ ResetLds W;
+  const int e = blockIdx.x;
+  if (mask[e] == 0) return;                      // workgroup-uniform
+  reset_env(p, s, cfg, e, seed, counter + (counter_dev != nullptr ? *counter_dev : 0ull), threadIdx.x, W);
+  __syncthreads();   // the reset's global writes (workgroup-scope release / acquire) before the observation reads
+  env_pairs_block<kWave, NM>(p, s, nullptr, nullptr, ctl, out, 1, e, smem);
 }
 
 __global__ __launch_bounds__(kBlock) void current_kernel(const double* __restrict__ cores, int nc, double core_r,
@@ -1378,6 +1410,33 @@ extern "C" int asvrl_env_reset(const AsvParams* params, const AsvEnvState* state
   hipLaunchKernelGGL(env_reset_kernel, dim3(grid), dim3(kResetWaves * kWave), 0, as_stream(stream), *params, *state,
                      *cfg, env_mask, seed, counter, counter_dev);
   return check_launch("asvrl_env_reset");
+}
+
+extern "C" int asvrl_env_reset_observe(const AsvParams* params, const AsvEnvState* state, const AsvResetCfg* cfg,
+                                       const uint8_t* env_mask, uint64_t seed, uint64_t counter,
+                                       const uint64_t* counter_dev, const AsvStepCtl* ctl, const AsvStepOut* out,
+                                       void* stream) {
+  ASVRL_REQUIRE(params && state && cfg && ctl && out && env_mask, "asvrl_env_reset_observe: null argument");
+  ASVRL_REQUIRE(state->max_cores <= kMaxCores, "asvrl_env_reset_observe: max_cores > 16");
+  ASVRL_REQUIRE(state->max_robots <= kResetMaxR && state->max_obs <= kResetMaxO,
+                "asvrl_env_reset_observe: max_robots and max_obs must be <= 32");
+  ASVRL_REQUIRE(cfg->width > 4.0 && cfg->height > 4.0, "asvrl_env_reset_observe: map too small");
+  ASVRL_REQUIRE(state->robot_params == nullptr, "asvrl_env_reset_observe: per-robot parameters take the two-launch path");
+  ASVRL_REQUIRE(!ctl->do_dynamics && ctl->env_mask == env_mask, "asvrl_env_reset_observe: ctl must be the masked "
+                "observation pass (do_dynamics = 0, env_mask = the reset mask)");
+  ASVRL_REQUIRE(ctl->noise_mode == 1 || ctl->noise_mode == 2, "asvrl_env_reset_observe: Philox noise only (mode 1 or 2)");
+  ASVRL_REQUIRE(out->obs && out->obj_cnt && out->reward && out->done && out->info,
+                "asvrl_env_reset_observe: null output");
+  if (state->n_envs == 0) return 0;
+  const PairLaunch pl = pair_launch(state->max_robots, state->max_obs, state->n_envs, kWave, 1,
+                                    ctl->noise_mode == 2 ? 4 : 8);
+  ASVRL_REQUIRE(pl.blk == kWave && pl.epb == 1 && pl.smem <= 60 * 1024, "asvrl_env_reset_observe: env too large");
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(state->n_envs), dim3(kWave), pl.smem, as_stream(stream), *params, *state, *cfg,
+                       env_mask, seed, counter, counter_dev, *ctl, *out);
+  };
+  ctl->noise_mode == 2 ? go(env_reset_observe_kernel<2>) : go(env_reset_observe_kernel<1>);
+  return check_launch("asvrl_env_reset_observe");
 }
 
 extern "C" int asvrl_current_field(const double* cores, int32_t n_cores, double core_r, const double* xy,

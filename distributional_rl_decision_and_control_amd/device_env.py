@@ -130,6 +130,30 @@ class DeviceEnvBatch:
         _abi.check(rc, "asvrl_env_reset")
 
 
+    def reset_observe(self, cfg, env_mask, seed=0, counter=0, counter_dev=None, obs_counter=0, obs=None,
+                      obj_cnt=None, fast_noise=True, stream=None):
+        """asvrl_env_reset_observe: reset the envs of env_mask (reset's sampler at (seed, counter)) and write
+        their reset observations (the masked do_dynamics = 0 step at (seed, obs_counter)) in one launch --
+        the same values as reset(...) followed by step(None, do_dynamics=False, env_mask=...)."""
+        ctl = _abi.AsvStepCtl()
+        ctl.is_continuous = 1
+        ctl.do_dynamics = 0
+        ctl.trainer_deactivate = 0
+        ctl.noise_mode = 2 if fast_noise else 1
+        ctl.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        ctl.counter = int(obs_counter) & 0xFFFFFFFFFFFFFFFF
+        ctl.counter_dev = counter_dev.data_ptr() if counter_dev is not None else None
+        ctl.gamma = 0.0
+        ctl.env_mask = env_mask.data_ptr()
+        st = self.state_struct()
+        out = self.out_struct(obs, obj_cnt, with_env_done=False)
+        rc = _abi.lib().asvrl_env_reset_observe(C.byref(self.params), C.byref(st), C.byref(cfg), _abi.ptr(env_mask),
+                                                int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter) & 0xFFFFFFFFFFFFFFFF,
+                                                _abi.ptr(counter_dev), C.byref(ctl), C.byref(out),
+                                                _abi.stream_ptr(stream))
+        _abi.check(rc, "asvrl_env_reset_observe")
+
+
 def reset_cfg(num_robots=5, num_obs=4, num_cores=0, min_start_goal_dis=40.0, width=55.0, height=55.0,
               clear_r=10.0, obs_r_range=(1.0, 1.0), v_range=(3.0, 3.0), v_rel_max=1.0, p=0.8):
     """AsvResetCfg with the reference's env.py:33-54 defaults (curriculum values override)."""

@@ -44,6 +44,9 @@ class VecMarineNavEnv:
     # ends on the parity it started from) or copies 1 -> 0 (swap=False: any graph sees the same buffers).
     swap = False
     _p = 0
+    # auto_reset in one launch (asvrl_env_reset_observe) instead of the reset sampler + a masked observation
+    # pass over every env; False: the two launches (A/B, tests/test_env_kernel_gpu.py)
+    fused_reset = True
 
     @property
     def obs_cur(self):
@@ -96,11 +99,19 @@ class VecMarineNavEnv:
         """Reset the envs whose episode ended in the last step and observe them into obs_next.
         counted: the step counter was already incremented for this step (by the replay push launch);
         the draws are keyed as if it had not been. events: three HIP events recorded on the current
-        stream before the reset, between the reset and the observation pass, and after it (bench.py)."""
+        stream before the reset, between the reset and the observation pass, and after it (bench.py; with
+        fused_reset only the first two)."""
         b = self.batch
         d = 1 if counted else 0
         if events is not None:
             events[0].record()
+        if self.fused_reset and b.robot_params is None:
+            # one launch: reset + the reset observation of the ended envs only (asvrl_env_reset_observe)
+            b.reset_observe(self.cfg, b.env_done, seed=self.seed, counter=0x40000000 - d, counter_dev=self.counter,
+                            obs_counter=0x80000000 - d, obs=self.obs_next, obj_cnt=self.cnt_next)
+            if events is not None:
+                events[1].record()   # (events[2] unused: there is no second launch)
+            return
         b.reset(self.cfg, b.env_done, seed=self.seed, counter=0x40000000 - d, counter_dev=self.counter)
         if events is not None:
             events[1].record()

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 21
+#define ASVRL_ABI_VERSION 22
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -190,6 +190,17 @@ int asvrl_env_step_ex(const AsvParams* params, const AsvEnvState* state, const d
 int asvrl_env_reset(const AsvParams* params, const AsvEnvState* state, const AsvResetCfg* cfg,
                     const uint8_t* env_mask, uint64_t seed, uint64_t counter,
                     const uint64_t* counter_dev, void* stream);
+
+/* The training loop's auto-reset in ONE launch: for every env with env_mask[e] != 0, asvrl_env_reset's
+ * sampler (one wave) followed by that env's reset observation, computed by the step kernel's phases with
+ * ctl (do_dynamics = 0, env_mask = the same mask, Philox noise: noise_mode 1 or 2) into out -- the
+ * same values as asvrl_env_reset + the masked asvrl_env_step, without the second launch over all envs.
+ * Replaces, for the batched trainer, the reset() + get_observations() pair of MarineNavEnv3.reset
+ * (env.py:72-164) that trainer.py calls at an episode end. Requires robot_params == NULL. */
+int asvrl_env_reset_observe(const AsvParams* params, const AsvEnvState* state, const AsvResetCfg* cfg,
+                            const uint8_t* env_mask, uint64_t seed, uint64_t counter,
+                            const uint64_t* counter_dev, const AsvStepCtl* ctl, const AsvStepOut* out,
+                            void* stream);
 
 /* Ocean current of env.py:458-501 at n query points xy [n][2] for one env's cores
  * [n_cores][4] -> out [n][3]. Used for the initial velocity of reset_with_eval_config
