@@ -603,6 +603,54 @@ __device__ __forceinline__ void target_phase(const ctile::CriticArgs& t, TqLds<N
   }
 }
 
+#ifdef ASVRL_INLAUNCH_REDUCE
+// VERDICT r04 item 2, measured as a variant build (never the shipped library): the three trunk layers'
+// partials reduced inside the update launch by a last arriver per 1 KB tile instead of partial_sums_kernel.
+constexpr int kRedN = (kH * kH + kH) + (kH * kC + kH) + (kC * kNcos + kC);   // 66,048 floats
+constexpr int kRedTiles = (kRedN + 255) / 256;
+__device__ float g_red_out[kRedN];
+__device__ unsigned g_red_cnt[kRedTiles];
+__device__ unsigned g_red_won[1024];
+
+__device__ __forceinline__ float red_part(const FusedArgs& a, int g, int x) {
+  constexpr int n2 = kH * kH + kH, n1 = kH * kC + kH, nc = kC * kNcos + kC;
+  if (x < n2) return a.parts.hidden2[static_cast<size_t>(g) * n2 + x];
+  if (x < n2 + n1) return a.parts.hidden[static_cast<size_t>(g) * n1 + (x - n2)];
+  return a.parts.cos_emb[static_cast<size_t>(g) * nc + (x - n2 - n1)];
+}
+
+// after every thread's partial stores: publish (release at agent scope), count each tile once (tiles in an
+// order rotated by the workgroup index, so that the arrival order differs per tile), and reduce -- in
+// workgroup order, deterministic -- every tile this workgroup completed as the last arriver
+template <int NT>
+__device__ void inlaunch_reduce(const FusedArgs& a, int grp, int* list) {
+  __threadfence();
+  __syncthreads();
+  const int G = static_cast<int>(gridDim.x);
+  if (threadIdx.x == 0) list[0] = 0;
+  __syncthreads();
+  for (int t = threadIdx.x; t < kRedTiles; t += kNW * 64) {
+    const int tile = (t + grp * kRedTiles / G) % kRedTiles;
+    const unsigned old = atomicAdd(&g_red_cnt[tile], 1u);
+    if (old == static_cast<unsigned>(G - 1)) list[1 + atomicAdd(&list[0], 1)] = tile;
+  }
+  __syncthreads();
+  __threadfence();   // acquire: the other workgroups' partials
+  const int nw = list[0];
+  for (int k = 0; k < nw; ++k) {
+    const int tile = list[1 + k];
+    const int x = tile * 256 + static_cast<int>(threadIdx.x);
+    if (x < kRedN) {
+      float acc = 0.f;
+      for (int g = 0; g < G; ++g) acc += red_part(a, g, x);
+      g_red_out[x] = acc;
+    }
+    if (threadIdx.x == 0) g_red_cnt[tile] = 0u;   // for the next launch
+  }
+  if (threadIdx.x == 0) g_red_won[grp] = static_cast<unsigned>(nw);
+}
+#endif
+
 template <int NT, bool IQN, bool TQ = false>
 __global__ __launch_bounds__(kNW * 64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void critic_fused_kernel(FusedArgs a) {
@@ -1359,6 +1407,9 @@ void critic_fused_kernel(FusedArgs a) {
     pc[kC * kNcos + swap23(2 * w * 32 + r)] = dbc0;
     pc[kC * kNcos + swap23((2 * w + 1) * 32 + r)] = dbc1;
   }
+#ifdef ASVRL_INLAUNCH_REDUCE
+  if constexpr (!IQN) inlaunch_reduce<NT>(a, grp, reinterpret_cast<int*>(L.x));
+#endif
   if constexpr (IQN) {
     // output layer [32 actions][128] + [32]: register g = action row, lane = feature position
     float* po = a.parts.out + static_cast<size_t>(grp) * (kMaxA * kH + kMaxA);
@@ -1396,6 +1447,13 @@ int fused_rounds(int B, int N) { return static_cast<int>(static_cast<int64_t>(B)
 }  // namespace asvrl
 
 using namespace asvrl;
+
+#ifdef ASVRL_INLAUNCH_REDUCE
+extern "C" int asvrl_debug_inlaunch_reduce(float* out, int64_t n_out, unsigned* won, int64_t n_won) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_red_out), n_out * sizeof(float)) != hipSuccess) return 1;
+  return hipMemcpyFromSymbol(won, HIP_SYMBOL(g_red_won), n_won * sizeof(unsigned)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 #ifdef ASVRL_FUSED_STAMPS
 extern "C" int asvrl_debug_fused_stamps(uint64_t* out, int64_t n) {
