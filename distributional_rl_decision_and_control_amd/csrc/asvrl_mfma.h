@@ -320,14 +320,11 @@ __device__ __forceinline__ void store16(elem_t* grp, const float* v, int h) {
     *reinterpret_cast<f32x4*>(grp + 8 + 4 * h) = f32x4{v[4], v[5], v[6], v[7]};
   }
 #else
-  bf16x4 lo, hi;
-  lo[0] = (__bf16)v[0]; lo[1] = (__bf16)v[1]; lo[2] = (__bf16)v[2]; lo[3] = (__bf16)v[3];
-  hi[0] = (__bf16)v[4]; hi[1] = (__bf16)v[5]; hi[2] = (__bf16)v[6]; hi[3] = (__bf16)v[7];
-  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  const u32x2 l = __builtin_bit_cast(u32x2, lo), u = __builtin_bit_cast(u32x2, hi);
-  const auto r0 = __builtin_amdgcn_permlane32_swap(l[0], u[0], false, false);
-  const auto r1 = __builtin_amdgcn_permlane32_swap(l[1], u[1], false, false);
+  const float (&v8)[8] = *reinterpret_cast<const float (*)[8]>(v);
+  const u32x4 pk = __builtin_bit_cast(u32x4, pack8(v8));   // features 0..3 in dwords 0, 1; 4..7 in 2, 3
+  const auto r0 = __builtin_amdgcn_permlane32_swap(pk[0], pk[2], false, false);
+  const auto r1 = __builtin_amdgcn_permlane32_swap(pk[1], pk[3], false, false);
   const u32x4 out = {r0[0], r1[0], r0[1], r1[1]};
   if (grp != nullptr) *reinterpret_cast<u32x4*>(grp + 8 * h) = out;
 #endif

@@ -128,8 +128,8 @@ __device__ __forceinline__ void load_obs(const float* __restrict__ x, int64_t ld
   for (int ks = 0; ks < 2; ++ks) {
     const float4 u = *reinterpret_cast<const float4*>(xr + ks * 16 + 8 * h);
     const float4 v = *reinterpret_cast<const float4*>(xr + ks * 16 + 8 * h + 4);
-    bx[ks][0] = (elem_t)u.x; bx[ks][1] = (elem_t)u.y; bx[ks][2] = (elem_t)u.z; bx[ks][3] = (elem_t)u.w;
-    bx[ks][4] = (elem_t)v.x; bx[ks][5] = (elem_t)v.y; bx[ks][6] = (elem_t)v.z; bx[ks][7] = (elem_t)v.w;
+    const float e[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+    bx[ks] = pack8(e);
   }
 #pragma unroll
   for (int o = 0; o < kObjN; ++o) mk[o] = xr[32 + o];
@@ -206,8 +206,7 @@ __device__ __forceinline__ void actor_tile(const MlpArgs& a, const ActorLds& L, 
   // encoders -> h0 (chained B operand of hidden_layer)
   frag8 fpk[16];
   encode_tile(wimg(L.enc, a.w.enc_frag), L.benc, bx, mk, lane, [&](int mb, int s, const float* v) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) fpk[mb * 2 + s][j] = (elem_t)v[j];
+    fpk[mb * 2 + s] = pack8(*reinterpret_cast<const float (*)[8]>(v));
     if (MODE == MLP_TRAIN)
       store16(valid ? bp(io.h0) + static_cast<int64_t>(row) * kEnc + mb * 32 + 16 * s : nullptr, v, h);
   });
@@ -231,8 +230,8 @@ __device__ __forceinline__ void actor_tile(const MlpArgs& a, const ActorLds& L, 
       for (int j = 0; j < 8; ++j) {
         const float x = acc1[mb][8 * s + j] + L.b1[feat(mb, 8 * s + j, h)];
         v[j] = relu(x);
-        h1pk[mb * 2 + s][j] = (elem_t)v[j];
       }
+      h1pk[mb * 2 + s] = pack8(v);
       if (MODE == MLP_TRAIN)
       store16(valid ? bp(io.h1) + static_cast<int64_t>(row) * kHid + mb * 32 + 16 * s : nullptr, v, h);
     }
@@ -475,14 +474,12 @@ __device__ __forceinline__ void actor_split_tile(const MlpArgs& a, ActorSplitLds
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         float v[8];
-        frag8 o;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int g = 8 * s + j;
           v[j] = relu(acc[g] + bb[g]) * ((g & 3) + 8 * (g >> 2) < lim ? fA : fB);
-          o[j] = (elem_t)v[j];
         }
-        rows(L.x0, RA, 0, 2 * mb + s, o);
+        rows(L.x0, RA, 0, 2 * mb + s, pack8(v));
         if constexpr (MODE == MLP_TRAIN)
           store16(valid ? bp(io.h0) + static_cast<int64_t>(row) * kEnc + mb * 32 + 16 * s : nullptr, v, h);
       }
@@ -509,13 +506,9 @@ __device__ __forceinline__ void actor_split_tile(const MlpArgs& a, ActorSplitLds
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       float v[8];
-      frag8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        v[j] = relu(acc[8 * s + j] + bb[8 * s + j]);
-        o[j] = (elem_t)v[j];
-      }
-      rows(L.h1, RH, 0, 2 * w + s, o);
+      for (int j = 0; j < 8; ++j) v[j] = relu(acc[8 * s + j] + bb[8 * s + j]);
+      rows(L.h1, RH, 0, 2 * w + s, pack8(v));
       if constexpr (MODE == MLP_TRAIN)
         store16(valid ? bp(io.h1) + static_cast<int64_t>(row) * kHid + w * 32 + 16 * s : nullptr, v, h);
     }
@@ -731,14 +724,12 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_split_kernel(MlpArgs
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       float dv[8];
-      frag8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int m = feat(w, 8 * s + j, h);
         dv[j] = hv[8 * s + j] > 0.f ? a.w.wout[m] * d0 + a.w.wout[kHid + m] * d1 : 0.f;
-        o[j] = (elem_t)dv[j];
       }
-      rows(dz2i, RH, 0, 2 * w + s, o);
+      rows(dz2i, RH, 0, 2 * w + s, pack8(dv));
       store16(valid ? bp(io.dz2) + rr * kHid + w * 32 + 16 * s : nullptr, dv, h);
     }
   }
@@ -752,13 +743,9 @@ __global__ __launch_bounds__(kMlpWaves * 64) void actor_bwd_split_kernel(MlpArgs
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       float dv[8];
-      frag8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        dv[j] = hv[8 * s + j] > 0.f ? acc[8 * s + j] : 0.f;
-        o[j] = (elem_t)dv[j];
-      }
-      rows(dz1i, RH, 0, 2 * w + s, o);
+      for (int j = 0; j < 8; ++j) dv[j] = hv[8 * s + j] > 0.f ? acc[8 * s + j] : 0.f;
+      rows(dz1i, RH, 0, 2 * w + s, pack8(dv));
       store16(valid ? bp(io.dz1) + rr * kHid + w * 32 + 16 * s : nullptr, dv, h);
     }
   }

@@ -87,11 +87,8 @@ __device__ __forceinline__ void phase_encode(const AsvRainbowImg& W, const float
   for (int ks = 0; ks < 2; ++ks) {
     const f32x4 u = *reinterpret_cast<const f32x4*>(xr + ks * 16 + 8 * h);
     const f32x4 v = *reinterpret_cast<const f32x4*>(xr + ks * 16 + 8 * h + 4);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      bx[ks][j] = (elem_t)u[j];
-      bx[ks][4 + j] = (elem_t)v[j];
-    }
+    const float e[8] = {u[0], u[1], u[2], u[3], v[0], v[1], v[2], v[3]};
+    bx[ks] = pack8(e);
   }
   float mf[kObjN];   // masked_fill(mask < 0.5, 0) as a factor per object
 #pragma unroll
@@ -114,7 +111,6 @@ __device__ __forceinline__ void phase_encode(const AsvRainbowImg& W, const float
     const float fA = obj_sel(obA, mf), fB = obj_sel(obA + 1, mf);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      frag8 o;
       float v[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -122,10 +118,9 @@ __device__ __forceinline__ void phase_encode(const AsvRainbowImg& W, const float
         const int m = feat(mb, g, h);
         const float keep = (g & 3) + 8 * (g >> 2) < lim ? fA : fB;
         v[i] = relu(acc[8 * s + i] + W.b_enc[m]) * keep;
-        o[i] = (elem_t)v[i];
         if (SAVE && v[i] > 0.f) fmask |= 1u << (16 * q + 8 * s + i);
       }
-      rows(x0, RA, 0, 2 * mb + s, o);
+      rows(x0, RA, 0, 2 * mb + s, pack8(v));
       if constexpr (SAVE) store16(f_row != nullptr ? f_row + mb * 32 + 16 * s : nullptr, v, h);
     }
   }
@@ -190,18 +185,15 @@ __device__ __forceinline__ void phase_hidden(const void* wv, const void* wa, con
   mask = 0;
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    frag8 ov, oa;
     float fv[8], fa[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       fv[i] = relu(av[8 * s + i]);
       fa[i] = relu(aa[8 * s + i]);
-      ov[i] = (elem_t)fv[i];
-      oa[i] = (elem_t)fa[i];
       if (SAVE) mask |= (fv[i] > 0.f ? 1u : 0u) << (8 * s + i) | (fa[i] > 0.f ? 1u : 0u) << (16 + 8 * s + i);
     }
-    rows(outv, RH, 0, 2 * w + s, ov);
-    rows(outa, RH, 0, 2 * w + s, oa);
+    rows(outv, RH, 0, 2 * w + s, pack8(fv));
+    rows(outa, RH, 0, 2 * w + s, pack8(fa));
     if constexpr (SAVE) {
       store16(sv_row != nullptr ? sv_row + w * 32 + 16 * s : nullptr, fv, h);
       store16(sa_row != nullptr ? sa_row + w * 32 + 16 * s : nullptr, fa, h);
@@ -522,16 +514,16 @@ __global__ __launch_bounds__(kNW * 64) void rainbow_train_kernel(RbArgs a) {
       for (int b = 0; b < 2; ++b)
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          frag8 o;
+          float o[8];
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             const int g = 8 * s + i;
             const bool on = atom_of(b, g, h) < kAtoms;
             const float d = on ? (fexp(q[b][g] - lse) * sm - mv[b][g]) * sc : 0.f;
-            o[i] = (elem_t)d;
+            o[i] = d;
             dqf[r * kAP + atom_of(b, g, h)] = d;
           }
-          rows(dqi, RQ, 0, 2 * b + s, o);
+          rows(dqi, RQ, 0, 2 * b + s, pack8(o));
         }
     }
   }
@@ -543,24 +535,24 @@ __global__ __launch_bounds__(kNW * 64) void rainbow_train_kernel(RbArgs a) {
   for (int c = threadIdx.x; c < 32 * (kAP / 8); c += kNW * 64) {
     const int rw = c / (kAP / 8), ch = c % (kAP / 8);
     if (row0 + rw >= io.N) continue;
-    frag8 o;
+    float o[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = (elem_t)dqf[rw * kAP + 8 * ch + i];
-    *reinterpret_cast<frag8*>(bp(io.dzv) + static_cast<int64_t>(row0 + rw) * kAP + 8 * ch) = o;
+    for (int i = 0; i < 8; ++i) o[i] = dqf[rw * kAP + 8 * ch + i];
+    *reinterpret_cast<frag8*>(bp(io.dzv) + static_cast<int64_t>(row0 + rw) * kAP + 8 * ch) = pack8(o);
   }
   constexpr int kDa = 1280;
   for (int c = threadIdx.x; c < 32 * (kDa / 8); c += kNW * 64) {
     const int rw = c / (kDa / 8), ch = c % (kDa / 8);
     if (row0 + rw >= io.N) continue;
     const int ar = L.act[rw];
-    frag8 o;
+    float o[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int col = 8 * ch + i, k = col / kAtoms, m = col - k * kAtoms;
       const float d = col < kActs * kAtoms ? dqf[rw * kAP + m] : 0.f;
-      o[i] = (elem_t)(col < kActs * kAtoms ? (k == ar ? d - d / static_cast<float>(kActs) : -d / static_cast<float>(kActs)) : 0.f);
+      o[i] = col < kActs * kAtoms ? (k == ar ? d - d / static_cast<float>(kActs) : -d / static_cast<float>(kActs)) : 0.f;
     }
-    *reinterpret_cast<frag8*>(bp(io.dza) + static_cast<int64_t>(row0 + rw) * kDa + 8 * ch) = o;
+    *reinterpret_cast<frag8*>(bp(io.dza) + static_cast<int64_t>(row0 + rw) * kDa + 8 * ch) = pack8(o);
   }
 
   // ---------------- dh2 (wave w: block w) -> dz2 into x0's space (f is only needed as the mask now)
@@ -593,17 +585,14 @@ __global__ __launch_bounds__(kNW * 64) void rainbow_train_kernel(RbArgs a) {
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      frag8 ov, oa;
       float fv[8], fa[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         fv[i] = (m2 >> (8 * s + i)) & 1u ? dv[8 * s + i] : 0.f;
         fa[i] = (m2 >> (16 + 8 * s + i)) & 1u ? da[8 * s + i] : 0.f;
-        ov[i] = (elem_t)fv[i];
-        oa[i] = (elem_t)fa[i];
       }
-      rows(dz2v, RH, 0, 2 * w + s, ov);
-      rows(dz2a, RH, 0, 2 * w + s, oa);
+      rows(dz2v, RH, 0, 2 * w + s, pack8(fv));
+      rows(dz2a, RH, 0, 2 * w + s, pack8(fa));
       elem_t* sv = orow(io.dz2v, kHid);
       elem_t* sa = orow(io.dz2a, kHid);
       store16(sv != nullptr ? sv + w * 32 + 16 * s : nullptr, fv, h);
@@ -621,17 +610,14 @@ __global__ __launch_bounds__(kNW * 64) void rainbow_train_kernel(RbArgs a) {
     const RowA<kHid> RH(r, h);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      frag8 ov, oa;
       float fv[8], fa[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         fv[i] = (m1 >> (8 * s + i)) & 1u ? dv[8 * s + i] : 0.f;
         fa[i] = (m1 >> (16 + 8 * s + i)) & 1u ? da[8 * s + i] : 0.f;
-        ov[i] = (elem_t)fv[i];
-        oa[i] = (elem_t)fa[i];
       }
-      rows(dz1v, RH, 0, 2 * w + s, ov);
-      rows(dz1a, RH, 0, 2 * w + s, oa);
+      rows(dz1v, RH, 0, 2 * w + s, pack8(fv));
+      rows(dz1a, RH, 0, 2 * w + s, pack8(fa));
       elem_t* sv = orow(io.dz1v, kHid);
       elem_t* sa = orow(io.dz1a, kHid);
       store16(sv != nullptr ? sv + w * 32 + 16 * s : nullptr, fv, h);
