@@ -295,20 +295,24 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
   // the bias-after form its part B recomputes bit for bit. F and G are ReLU outputs (>= 0), so
   // relu(F c) = F relu(c) and relu(round(x)) = round(relu(x)): the same operands either way.
   constexpr bool BF = kBiasFirst && !TRAINM;
+  // QB of the eight 32-feature blocks per pass: four, or two in the 16-wave IQN_ACT launch, whose 128
+  // VGPRs then hold one pass's accumulators beside the packed outputs of the passes before it (the same
+  // MFMAs per block in the same k order: bit-identical)
+  constexpr int QB = MODE == MODE_IQN_ACT ? 2 : 4;
   frag8 cpk[16], hpk[16];
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    f32x16 acc0[4];
+  for (int half = 0; half < 8 / QB; ++half) {
+    f32x16 acc0[QB];
 #pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) acc0[q4] = BF ? bias_nat(L.bc, half * 4 + q4, h) : f32x16{};
+    for (int q4 = 0; q4 < QB; ++q4) acc0[q4] = BF ? bias_nat(L.bc, half * QB + q4, h) : f32x16{};
 #pragma unroll
     for (int ks = 0; ks < kNcos / 16; ++ks) {
 #pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4) acc0[q4] = mfma(WC[((half * 4 + q4) * 4 + ks) * 64 + lane], cx[ks], acc0[q4]);
+      for (int q4 = 0; q4 < QB; ++q4) acc0[q4] = mfma(WC[((half * QB + q4) * 4 + ks) * 64 + lane], cx[ks], acc0[q4]);
     }
 #pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) {
-      const int mb = half * 4 + q4;
+    for (int q4 = 0; q4 < QB; ++q4) {
+      const int mb = half * QB + q4;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         if constexpr (BF) {
@@ -340,39 +344,45 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
   }
 
   // ---------------- layer 1: h1 = relu(W1 h0 + b1), h1g = h1 * G[b]
-  f32x16 acc1[4];
-#pragma unroll
-  for (int mb = 0; mb < 4; ++mb) acc1[mb] = BF ? bias_nat(L.b1, mb, h) : f32x16{};
-  mfma_wrows<kC / 16, 4, MODE != MODE_IQN_ACT>(acc1, [&](int mb, int ks) { return W1[(mb * 16 + ks) * 64 + lane]; },
-                         [&](int ks) { return hpk[ks]; });
+  // in passes of QB1 blocks (two in IQN_ACT, for its 128 VGPRs; same per-block k order: bit-identical)
+  constexpr int QB1 = MODE == MODE_IQN_ACT ? 2 : 4;
   frag8 h1pk[8], gpk[8];
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb) {
+  for (int pass = 0; pass < 4 / QB1; ++pass) {
+    f32x16 acc1[QB1];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      if constexpr (BF) {
-        float xs[8], gs[8], ps[8];
+    for (int q = 0; q < QB1; ++q) acc1[q] = BF ? bias_nat(L.b1, pass * QB1 + q, h) : f32x16{};
+    mfma_wrows<kC / 16, QB1, MODE != MODE_IQN_ACT>(
+        acc1, [&](int q, int ks) { return W1[((pass * QB1 + q) * 16 + ks) * 64 + lane]; }, [&](int ks) { return hpk[ks]; });
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          xs[j] = acc1[mb][8 * s + j];
-          if constexpr (!IQN) gs[j] = Gb[feat(mb, 8 * s + j, h)];
+    for (int q = 0; q < QB1; ++q) {
+      const int mb = pass * QB1 + q;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        if constexpr (BF) {
+          float xs[8], gs[8], ps[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            xs[j] = acc1[q][8 * s + j];
+            if constexpr (!IQN) gs[j] = Gb[feat(mb, 8 * s + j, h)];
+          }
+          if constexpr (!IQN) mul8(xs, gs, ps);
+          h1pk[mb * 2 + s] = relu_packed(pack8(xs));
+          gpk[mb * 2 + s] = IQN ? h1pk[mb * 2 + s] : relu_packed(pack8(ps));   // IQN: no action features
+        } else {
+          float gv[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int m = feat(mb, 8 * s + j, h);
+            float x = acc1[q][8 * s + j] + L.b1[m];
+            x = relu(x);
+            h1pk[mb * 2 + s][j] = (elem_t)x;
+            gv[j] = IQN ? x : x * Gb[m];   // IQN: no action features
+            gpk[mb * 2 + s][j] = (elem_t)gv[j];
+          }
+          if (TRAINM)
+            store16(bp(a.acts.h1g) + static_cast<size_t>(grow) * kH + mb * 32 + 16 * s, gv, h);
         }
-        if constexpr (!IQN) mul8(xs, gs, ps);
-        h1pk[mb * 2 + s] = relu_packed(pack8(xs));
-        gpk[mb * 2 + s] = IQN ? h1pk[mb * 2 + s] : relu_packed(pack8(ps));   // IQN: no action features
-      } else {
-        float gv[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int m = feat(mb, 8 * s + j, h);
-          float x = acc1[mb][8 * s + j] + L.b1[m];
-          x = relu(x);
-          h1pk[mb * 2 + s][j] = (elem_t)x;
-          gv[j] = IQN ? x : x * Gb[m];   // IQN: no action features
-          gpk[mb * 2 + s][j] = (elem_t)gv[j];
-        }
-        if (TRAINM)
-          store16(bp(a.acts.h1g) + static_cast<size_t>(grow) * kH + mb * 32 + 16 * s, gv, h);
       }
     }
   }
