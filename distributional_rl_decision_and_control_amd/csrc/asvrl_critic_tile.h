@@ -434,15 +434,24 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
       if (feat(0, g, h) == ai) qs = ao[g] + L.bo_a[ai];
     q = half_sum(qs);   // Q_expected.gather(2, actions) (agent.py:456): one half holds it, the other 0
   } else {
+    // the products two per v_pk_mul_f32, the sum in the same serial order
     float part = 0.f;
 #pragma unroll
     for (int mb = 0; mb < 4; ++mb) {
 #pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        const int m = feat(mb, g, h);
-        float x = BF ? acc2[mb][g] : acc2[mb][g] + L.b2[m];
-        acc2[mb][g] = x;  // keep z2 for the relu mask
-        part += L.wo[m] * relu(x);
+      for (int s8 = 0; s8 < 2; ++s8) {
+        float wv[8], hv[8], pr[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int g = 8 * s8 + j, m = feat(mb, g, h);
+          const float x = BF ? acc2[mb][g] : acc2[mb][g] + L.b2[m];
+          acc2[mb][g] = x;  // keep z2 for the relu mask
+          wv[j] = L.wo[m];
+          hv[j] = relu(x);
+        }
+        mul8(wv, hv, pr);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) part += pr[j];
       }
     }
     q = half_sum(part) + a.w.bo[0];
