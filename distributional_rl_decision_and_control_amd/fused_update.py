@@ -50,10 +50,11 @@ OBS = 40
 ENC_IN_KERNEL = True
 # the target critic's forward inside the fused critic launch (ABI 20, asvrl_critic_train_fused_tq: each
 # workgroup computes q_next for the samples it updates, bit-identical to the separate asvrl_critic_forward).
-# Off: the launch grows 111 -> 147-149 us (the FWD tiles at one wave per SIMD: 35 us against 26 us for the
-# separate launch alone) and the rollout's env step then waits for CUs beside it; bench step 0.2649 vs 0.2629
-# ms (profiles/r04t_target_in_fused_ab.txt, r04r_tq_step_window.txt)
-TARGET_IN_FUSED = False
+# Round 4 measured it slower (0.2649 vs 0.2629 ms, profiles/r04t_target_in_fused_ab.txt); at the round-5 head
+# (leaner epilogues, the one-launch auto-reset) the separate target launch costs 54 us beside the next env step
+# while the in-launch pass adds ~35 us to the update, and the step is faster: 0.2591 vs 0.2642 ms at the
+# driver's shape, 0.2478 vs 0.2503 at steady state (profiles/r05ac_target_in_fused_ab.txt)
+TARGET_IN_FUSED = True
 
 
 def supported(policy, B, N):
