@@ -36,6 +36,13 @@
 #include "asvrl_common.h"
 #include "asvrl_mfma.h"
 #include "asvrl_lds.h"
+// the target critic's forward inside this launch (target_phase) runs at one wave per SIMD, where nothing hides an
+// MFMA's wait for its weight fragment: read each k-step's fragments one step ahead (same MFMAs in the same order,
+// bit-identical; TQ launch 136 -> 130 us, step 0.2545 -> 0.2500 ms, profiles/r05ae_tq_read_ahead_ab.txt). The
+// separate forward launch (two waves per SIMD) keeps asvrl_critic_tile.h's default, measured neutral there.
+#ifndef ASVRL_CRIT_READ_AHEAD
+#define ASVRL_CRIT_READ_AHEAD 1
+#endif
 #include "asvrl_critic_tile.h"   // before the contraction pragma: the target critic's forward as asvrl_critic.hip's
 
 // FMA contraction of this file's f32 epilogue arithmetic (the loss terms, the output layer's and the encoders'
