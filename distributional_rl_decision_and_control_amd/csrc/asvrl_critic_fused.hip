@@ -562,7 +562,19 @@ template <int NT, int NB>
 __device__ __forceinline__ void target_phase(const ctile::CriticArgs& t, TqLds<NT, true>& T, int rounds) {
   constexpr int St = 32 / NT;
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if constexpr (kWeightsInLds) {
+  // N = 32: the Wc and W2 images' fragments (8 + 8 per thread) are loaded into registers first and stored to
+  // LDS after the first chunk of samples is staged, so their L2 round trip runs under the chunk's own loads
+  constexpr bool kEarly = kWeightsInLds && NT == 32;
+  constexpr int kPerC = ctile::kFragWC / (kNW * 64), kPer2 = ctile::kFragW2 / (kNW * 64);
+  static_assert(!kEarly || (kPerC * kNW * 64 == ctile::kFragWC && kPer2 * kNW * 64 == ctile::kFragW2), "whole images");
+  frag8 ec[kEarly ? kPerC : 1], e2[kEarly ? kPer2 : 1];
+  if constexpr (kEarly) {
+#pragma unroll
+    for (int c = 0; c < kPerC; ++c) ec[c] = reinterpret_cast<const frag8*>(t.w.wc_frag)[c * kNW * 64 + threadIdx.x];
+#pragma unroll
+    for (int c = 0; c < kPer2; ++c) e2[c] = reinterpret_cast<const frag8*>(t.w.w2_frag)[c * kNW * 64 + threadIdx.x];
+    copy_frags<kNW * 64, ctile::kFragW1, 16>(T.W.w1, reinterpret_cast<const frag8*>(t.w.w1_frag), threadIdx.x);
+  } else if constexpr (kWeightsInLds) {
     copy_frags<kNW * 64, ctile::kFragWC, 16>(T.W.wc, reinterpret_cast<const frag8*>(t.w.wc_frag), threadIdx.x);
     copy_frags<kNW * 64, ctile::kFragW1, 16>(T.W.w1, reinterpret_cast<const frag8*>(t.w.w1_frag), threadIdx.x);
     copy_frags<kNW * 64, ctile::kFragW2, 16>(T.W.w2, reinterpret_cast<const frag8*>(t.w.w2_frag), threadIdx.x);
@@ -580,6 +592,14 @@ __device__ __forceinline__ void target_phase(const ctile::CriticArgs& t, TqLds<N
     for (int c0 = 0; c0 < mine; c0 += kTqChunk) {   // workgroup-uniform
       const int n = mine - c0 < kTqChunk ? mine - c0 : kTqChunk;
       tq_stage_chunk(t, n, [&](int k) { return tile_of(c0 + k); }, T.F, T.G, T.T);
+      if constexpr (kEarly) {
+        if (c0 == 0) {
+#pragma unroll
+          for (int c = 0; c < kPerC; ++c) T.W.wc[c * kNW * 64 + threadIdx.x] = ec[c];
+#pragma unroll
+          for (int c = 0; c < kPer2; ++c) T.W.w2[c * kNW * 64 + threadIdx.x] = e2[c];
+        }
+      }
       __syncthreads();
 #pragma nounroll
       for (int k = wv; k < n; k += kNW)
