@@ -401,10 +401,16 @@ __device__ __forceinline__ void critic_tile(const CriticArgs& a, const LT& L, in
 #pragma unroll
     for (int mb = 0; mb < 4; ++mb) {
 #pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        const float x = BF ? acc2[mb][g] : acc2[mb][g] + L.b2[feat(mb, g, h)];
-        acc2[mb][g] = x;  // keep z2 for the relu mask
-        h2pk[mb * 2 + (g >> 3)][g & 7] = (elem_t)relu(x);
+      for (int s8 = 0; s8 < 2; ++s8) {
+        float xv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int g = 8 * s8 + j;
+          const float x = BF ? acc2[mb][g] : acc2[mb][g] + L.b2[feat(mb, g, h)];
+          acc2[mb][g] = x;  // keep z2 for the relu mask
+          xv[j] = x;
+        }
+        h2pk[mb * 2 + s8] = relu_packed(pack8(xv));   // relu(round(x)) = round(relu(x)), two per instruction
       }
     }
     f32x16 ao = f32x16{};
