@@ -13,11 +13,15 @@ Here every role gets its own stream, created once per (device, role) with hipStr
 the process can be handed the same stream. The streams live for the process.
 """
 import ctypes as C
+import os
 
 import torch
 
 # the probe (tools/graph_stream_probe.py) switches to torch's pool to show the aliasing
 USE_TORCH_POOL = False
+# per-role HIP stream priority ("role=high|low,...", e.g. "capture=high,roll=low"; unset: every stream at
+# the default priority), read when a role's stream is first created
+PRIORITIES = os.environ.get("ASVRL_STREAM_PRIORITY", "")
 
 _HIP = None
 _STREAMS = {}
@@ -31,7 +35,23 @@ def _hip():
         _HIP = C.CDLL("libamdhip64.so.7")
         _HIP.hipStreamCreateWithFlags.argtypes = [C.POINTER(C.c_void_p), C.c_uint]
         _HIP.hipStreamCreateWithFlags.restype = C.c_int
+        _HIP.hipStreamCreateWithPriority.argtypes = [C.POINTER(C.c_void_p), C.c_uint, C.c_int]
+        _HIP.hipStreamCreateWithPriority.restype = C.c_int
+        _HIP.hipDeviceGetStreamPriorityRange.argtypes = [C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        _HIP.hipDeviceGetStreamPriorityRange.restype = C.c_int
     return _HIP
+
+
+def _priority(role):
+    """The numeric HIP priority of `role` from PRIORITIES, or None (lower numbers run first)."""
+    for item in PRIORITIES.split(","):
+        name, _, level = item.partition("=")
+        if name.strip() == str(role) and level.strip() in ("high", "low"):
+            least, greatest = C.c_int(), C.c_int()
+            if _hip().hipDeviceGetStreamPriorityRange(C.byref(least), C.byref(greatest)) != 0:
+                raise RuntimeError("hipDeviceGetStreamPriorityRange failed")
+            return greatest.value if level.strip() == "high" else least.value
+    return None
 
 
 def stream(device, role):
@@ -45,10 +65,14 @@ def stream(device, role):
     s = _STREAMS.get(key)
     if s is None:
         h = C.c_void_p()
+        prio = _priority(role)
         with torch.cuda.device(dev):
-            rc = _hip().hipStreamCreateWithFlags(C.byref(h), _NON_BLOCKING)
+            if prio is None:
+                rc = _hip().hipStreamCreateWithFlags(C.byref(h), _NON_BLOCKING)
+            else:
+                rc = _hip().hipStreamCreateWithPriority(C.byref(h), _NON_BLOCKING, prio)
         if rc != 0:
-            raise RuntimeError(f"hipStreamCreateWithFlags failed ({rc})")
+            raise RuntimeError(f"hipStreamCreate failed ({rc})")
         s = torch.cuda.ExternalStream(h.value, device=dev)
         _STREAMS[key] = s
     return s
