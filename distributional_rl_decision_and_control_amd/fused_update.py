@@ -170,13 +170,14 @@ def learn_prologue(st, replay, taus, seed, counter_dev=None, counter=0, out=None
 
 def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, actor_grads, rows, gamma=0.99,
                          taus=None, sync=None, max_norm=0.5, actor_wait=None, counter=None, prologue_done=False,
-                         target_wait=None):
+                         target_wait=None, actor_done=None):
     """One AC-IQN update from replay rows [B][88]. taus: (3, B, N) or None (drawn here).
     actor_wait: event to wait for before the actor's weights change (a concurrent act kernel).
     counter: an int64 device scalar incremented after the step (the learn counter; in-kernel when
     the optimiser step is fused). prologue_done: learn_prologue already ran the actor's TRAIN forward and
     the target actor on these rows. target_wait: an event the target critic waits for (a schedule knob:
-    the rollout's env step ahead of it instead of beside it; no data dependency).
+    the rollout's env step ahead of it instead of beside it; no data dependency). actor_done: an event recorded
+    after the ACTOR pass (a schedule knob: what the rollout's replay push may wait for).
     Returns (critic_loss, actor_loss, critic_grad_norm, actor_grad_norm) as device scalars."""
     B, N = st.B, st.N
     critic, actor = policy_local.critic, policy_local.actor
@@ -220,6 +221,8 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     # ---- actor through the updated critic (agent.py:419-427)
     critic_actor_grad(st.local_trunk, None, None, taus[2], N, st.q_pi, w_ae=ae.weight, dA=ab.dA,
                       tile_loss=st.tile_loss[1], obs=s_rows, act=ab.a_out)
+    if actor_done is not None:   # behind the ACTOR pass (behind the actor's backward measured no better, r05aq)
+        actor_done.record(torch.cuda.current_stream())
     actor_backward(st.actor, ab)
     # every actor .grad, the actor loss, the norm partials and the Adam step count in one launch
     fused_opt = sync is None and isinstance(actor_opt, FusedAdam)

@@ -43,7 +43,7 @@ class VecTrainer:
                  learning_starts=None, target_update_interval=2500, total_timesteps=6_000_000,
                  exploration_fraction=0.25, initial_eps=0.6, final_eps=0.05, seed=0,
                  device="cuda", sync=None, graphs=False, schedule=None, net_seed=100, overlap=True, unroll=1,
-                 chain=None, operands="bf16", target_after_env=False):
+                 chain=None, operands="bf16", target_after_env=False, push_after_actor=None):
         """Every learner runs on the hand-written kernels (fused_update / fused_iqn / fused_rainbow) with
         FusedAdam; operands="f32" takes them from the f32-operand parity build (libasvrl_f32.so). Shapes
         the kernels do not take raise ValueError."""
@@ -52,6 +52,10 @@ class VecTrainer:
         # chained schedule knob: the AC-IQN learner's target critic waits for the same iteration's env step
         # (the two then run one after the other instead of side by side; results unchanged)
         self.target_after_env = bool(target_after_env)
+        # schedule knob: the rollout's replay push (and the reset behind it) waits for the learner's ACTOR pass
+        # of the same iteration instead of running beside it (None: wherever the chained AC-IQN graph runs)
+        self._paa_arg = push_after_actor
+        self.push_after_actor = bool(push_after_actor)
         self.continuous = agent_type == "AC-IQN"
         self.env = VecMarineNavEnv(n_envs, num_robots, num_obs, num_cores, min_start_goal_dis, width, seed=seed,
                                    device=self.device, is_continuous=self.continuous, gamma=gamma, schedule=schedule)
@@ -161,6 +165,11 @@ class VecTrainer:
             # the knob orders two nodes of the chained AC-IQN graph; anywhere else it would be silently ignored
             # and a bench config recording it would be mislabelled
             raise ValueError("target_after_env applies only to the chained, graph-captured AC-IQN schedule")
+        paa_ok = self.fused2 is not None and self.graphs and self._chained()
+        if self._paa_arg is None:
+            self.push_after_actor = paa_ok
+        elif self.push_after_actor and not paa_ok:
+            raise ValueError("push_after_actor applies only to the chained, graph-captured AC-IQN schedule")
         self.ring_snap2 = torch.zeros((2, 2), dtype=torch.int64, device=self.device)
         self._gen = torch.Generator(device=self.device)
         self._gen.manual_seed(seed + 12345)
@@ -208,7 +217,7 @@ class VecTrainer:
         self.env.auto_reset(counted)
         self.env.advance_device(counted)
 
-    def learn(self, state=None, guard=0, actor_wait=None, target_wait=None):
+    def learn(self, state=None, guard=0, actor_wait=None, target_wait=None, actor_done=None):
         """One learn step of batch B: sample (uniform ring, or the prioritised tree for Rainbow) and the
         agent's fused update. state / guard: the ring snapshot to sample against and the newest entries to
         skip (the overlapped schedule); actor_wait: an event to wait for before the actor's weights change."""
@@ -230,7 +239,7 @@ class VecTrainer:
             return ac_iqn_update_fused2(self.fused2, self.local, self.actor_opt, self.critic_opt, self.critic_grads,
                                         self.actor_grads, rows, gamma=self.gamma, sync=self.sync,
                                         actor_wait=actor_wait, taus=self.taus, counter=self.learn_counter,
-                                        prologue_done=True, target_wait=target_wait)
+                                        prologue_done=True, target_wait=target_wait, actor_done=actor_done)
         # the update's quantile fractions are drawn by the sampling launch
         rows = self.replay.sample(self.B, seed=self.seed + 777, counter_dev=self.learn_counter, out=self.batch_rows,
                                   state=state, guard=guard, taus=self.taus)
@@ -367,30 +376,40 @@ class VecTrainer:
         ev_snap = [torch.cuda.Event() for _ in range(U)]
         ev_learn = [torch.cuda.Event() for _ in range(U)]
         ev_env = [torch.cuda.Event() for _ in range(U)]
+        ev_actor = [torch.cuda.Event() for _ in range(U)]
         # the events live as long as the graph: the captured cross-stream waits may refer to them at replay
-        self._chain_events = (ev_act, ev_snap, ev_learn, ev_env)
+        self._chain_events = (ev_act, ev_snap, ev_learn, ev_env, ev_actor)
         tae = self.target_after_env and self.fused2 is not None
+        paa = self.push_after_actor and self.fused2 is not None
         s_roll.wait_stream(main)
         out = None
+
+        def push_reset(k):
+            self._push(snap=self.ring_snap2[k % 2])   # + the ring state learn(k+1) samples against
+            ev_snap[k].record(s_roll)
+            self.env.auto_reset(True)
+            self.env.advance_device(True)
+
         for k in range(U):
             with torch.cuda.stream(s_roll):
                 if k > 0:
                     s_roll.wait_event(ev_learn[k - 1])   # the weights learn(k-1) wrote
                 self.act()
                 ev_act[k].record(s_roll)
-                env = self.env
-                env.step(self.actions)
+                self.env.step(self.actions)
                 if tae:
                     ev_env[k].record(s_roll)
-                self._push(snap=self.ring_snap2[k % 2])   # + the ring state learn(k+1) samples against
-                ev_snap[k].record(s_roll)
-                env.auto_reset(True)
-                env.advance_device(True)
+                if not paa:
+                    push_reset(k)
             if k > 0:
                 main.wait_event(ev_snap[k - 1])
             out = self.learn(state=self.ring_snap2[(k - 1) % 2], guard=self.E * self.R, actor_wait=ev_act[k],
-                             target_wait=ev_env[k] if tae else None)
+                             target_wait=ev_env[k] if tae else None, actor_done=ev_actor[k] if paa else None)
             ev_learn[k].record(main)
+            if paa:
+                with torch.cuda.stream(s_roll):
+                    s_roll.wait_event(ev_actor[k])
+                    push_reset(k)
         main.wait_stream(s_roll)
         return out
 

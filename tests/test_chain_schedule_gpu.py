@@ -11,11 +11,12 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _run(agent_type, chain, iters, n_envs=256, batch=256, unroll=2, target_after_env=False):
+def _run(agent_type, chain, iters, n_envs=256, batch=256, unroll=2, target_after_env=False, push_after_actor=None):
     from distributional_rl_decision_and_control_amd.vec_trainer import VecTrainer
     tr = VecTrainer(n_envs=n_envs, agent_type=agent_type, batch_size=batch, num_tau=32, seed=21, graphs=True,
                     unroll=unroll, chain=chain, buffer_size=max(n_envs * 5 * 40, 4 * n_envs * 5),
-                    learning_starts=2 * batch, target_after_env=target_after_env)
+                    learning_starts=2 * batch, target_after_env=target_after_env,
+                    push_after_actor=push_after_actor)
     while tr.replay_size_host() < tr.learning_starts:
         tr.iteration()
     for _ in range(iters):
@@ -40,6 +41,7 @@ def _same(a, pa, la, b, pb, lb):
 @pytest.mark.parametrize("agent_type", ["AC-IQN", "IQN"])
 def test_chained_schedule_matches_joined(agent_type):
     a, pa, la = _run(agent_type, True, 8)
+    assert a.push_after_actor == (agent_type == "AC-IQN")
     b, pb, lb = _run(agent_type, False, 8)
     _same(a, pa, la, b, pb, lb)
 
@@ -50,6 +52,26 @@ def test_chained_schedule_target_after_env_matches_joined():
     a, pa, la = _run("AC-IQN", True, 8, target_after_env=True)
     b, pb, lb = _run("AC-IQN", False, 8)
     _same(a, pa, la, b, pb, lb)
+
+
+def test_chained_schedule_push_beside_actor_matches_joined():
+    """push_after_actor (on by default in the chained AC-IQN graph: the replay push and the reset behind it
+    wait for the learner's ACTOR pass) switched off -- the push beside the ACTOR pass, round 5's earlier
+    schedule: bit-identical to the joined schedule as well."""
+    a, pa, la = _run("AC-IQN", True, 8, push_after_actor=False)
+    assert not a.push_after_actor
+    b, pb, lb = _run("AC-IQN", False, 8)
+    assert not b.push_after_actor   # the joined schedule resolves the default to off
+    _same(a, pa, la, b, pb, lb)
+
+
+def test_push_after_actor_default_and_refusal():
+    from distributional_rl_decision_and_control_amd.vec_trainer import VecTrainer
+    tr = VecTrainer(n_envs=64, agent_type="AC-IQN", batch_size=64, num_tau=32, seed=1, chain=True, graphs=True, unroll=2)
+    assert tr.push_after_actor
+    for kw in (dict(chain=False, graphs=True, unroll=2), dict(chain=True, graphs=False, unroll=2)):
+        with pytest.raises(ValueError, match="push_after_actor"):
+            VecTrainer(n_envs=64, agent_type="AC-IQN", batch_size=64, num_tau=32, seed=1, push_after_actor=True, **kw)
 
 
 def test_target_after_env_refused_where_it_would_be_ignored():
