@@ -283,12 +283,6 @@ constexpr int kPushBlock = 256;
 #ifndef ASVRL_PUSH_SUMCOUNT
 #define ASVRL_PUSH_SUMCOUNT 1
 #endif
-// the block's rows copied cooperatively (1): thread t moves 16-byte pieces t, t + 256, ... of the block's
-// observation rows, so a wave's loads and stores cover whole row runs instead of one 16-byte piece of 64
-// rows 352 B apart (0)
-#ifndef ASVRL_PUSH_COALESCED
-#define ASVRL_PUSH_COALESCED 1
-#endif
 
 __device__ __forceinline__ int block_sum(int v, int* sh) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
@@ -333,9 +327,7 @@ __global__ __launch_bounds__(kPushBlock) void replay_push_kernel(
     int* arrive, int nblocks, int64_t* snap, int64_t* counter_inc) {
   __shared__ int sh[kPushBlock / kWave], shw[kPushBlock / kWave];
   __shared__ int s_last;
-#if ASVRL_PUSH_COALESCED
   __shared__ int64_t s_slot[kPushBlock];   // the ring slot of each of the block's rows, -1: not pushed
-#endif
   const int before = count_pushed(cnt, static_cast<int>(blockIdx.x) * kPushBlock, sh);
   const int k = blockIdx.x * kPushBlock + threadIdx.x;
   const bool v = k < n && cnt[k] >= 0;
@@ -350,27 +342,18 @@ __global__ __launch_bounds__(kPushBlock) void replay_push_kernel(
     for (int w = 0; w < (threadIdx.x >> 6); ++w) wave_off += shw[w];
     const int64_t slot = (head_in + before + wave_off + rank_in_wave) % cap;
     float4* dst = reinterpret_cast<float4*>(ring + slot * ASVRL_TR_DIM);
-#if ASVRL_PUSH_COALESCED
     s_slot[threadIdx.x] = slot;
-#else
-    const float4* a4 = reinterpret_cast<const float4*>(obs_prev + static_cast<size_t>(k) * ASVRL_OBS_DIM);
-    const float4* b4 = reinterpret_cast<const float4*>(obs_next + static_cast<size_t>(k) * ASVRL_OBS_DIM);
-#pragma unroll
-    for (int q = 0; q < ASVRL_OBS_DIM / 4; ++q) dst[q] = a4[q];
-#pragma unroll
-    for (int q = 0; q < ASVRL_OBS_DIM / 4; ++q) dst[ASVRL_OBS_DIM / 4 + q] = b4[q];
-#endif
     const float a0 = static_cast<float>(actions[k * ald]);
     const float a1 = adim > 1 ? static_cast<float>(actions[k * ald + 1]) : 0.f;
     dst[2 * ASVRL_OBS_DIM / 4] = make_float4(a0, a1, static_cast<float>(reward[k]), done[k] ? 1.f : 0.f);
     dst[2 * ASVRL_OBS_DIM / 4 + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-#if ASVRL_PUSH_COALESCED
-  else {
+  } else {
     s_slot[threadIdx.x] = -1;
   }
   __syncthreads();
-  {
+  {   // the block's observation rows copied cooperatively: thread t moves 16-byte pieces t, t + 256, ... so a
+      // wave's loads and stores cover whole row runs, not one piece of 64 rows 352 B apart (push 29.8 -> 21.6 us
+      // in the step, profiles/r05am_push_coalesced_ab.txt)
     constexpr int kQ = ASVRL_OBS_DIM / 4;   // 16-byte pieces per observation row
     const int k0 = blockIdx.x * kPushBlock;
     const int nr = n - k0 < kPushBlock ? n - k0 : kPushBlock;
@@ -388,7 +371,6 @@ __global__ __launch_bounds__(kPushBlock) void replay_push_kernel(
       }
     }
   }
-#endif
   __syncthreads();   // every lane's read of ring_state is done before the block arrives
   if (threadIdx.x == 0) {
 #if ASVRL_PUSH_SUMCOUNT
