@@ -113,14 +113,22 @@ def _reduce_and_step(arena, opt, grads, sync, max_norm, wait=None, pack=None, co
     otherwise reduce, all-reduce (sync), asvrl_adam_clip, then pack.refresh() and counter += 1.
     `wait`: an event to wait for before the parameters change."""
     assert pack is None or not isinstance(opt, FusedAdam) or opt.L is pack.L, "optimiser and pack of different builds"
-    if sync is None and isinstance(opt, FusedAdam):
-        arena.flush(norm=opt)
-        if wait is not None:
-            torch.cuda.current_stream().wait_event(wait)
+    if isinstance(opt, FusedAdam):
         if pack is not None and not hasattr(pack, "_adam_segs"):
             pack._adam_segs = pack.adam_segments(opt)
-        return opt.step_prenormed(arena.norm_parts, arena.nparts, pack=pack._adam_segs if pack is not None else None,
-                                  counter=counter)
+        segs = pack._adam_segs if pack is not None else None
+        if sync is None:
+            arena.flush(norm=opt)
+            if wait is not None:
+                torch.cuda.current_stream().wait_event(wait)
+            return opt.step_prenormed(arena.norm_parts, arena.nparts, pack=segs, counter=counter)
+        # data-parallel: reduce, all-reduce, then the norm over the averaged gradient and the same packing
+        # Adam launch (no re-pack launches, no counter op: DP step 0.316 ms with them, DESIGN.md 5)
+        arena.flush()
+        sync(grads)
+        if wait is not None:
+            torch.cuda.current_stream().wait_event(wait)
+        return opt.step_synced(pack=segs, counter=counter)
     gn = _step_unfused(arena, opt, grads, sync, max_norm, wait)
     if pack is not None:
         pack.refresh()
@@ -228,13 +236,18 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     fused_opt = sync is None and isinstance(actor_opt, FusedAdam)
     actor_grads_launch(st.agrads, ab, actor, st.tile_loss[1], st.losses[1:2],
                        step=actor_opt.step_t if fused_opt else None, norm=fused_opt)
-    if fused_opt:
+    if isinstance(actor_opt, FusedAdam):
+        if sync is not None:
+            sync(actor_grads)
         # a concurrent act kernel reads the current actor images: with two sets the step writes the other one
         # and no wait is needed (its cross-stream dependency costs ~7 us in a replayed graph)
         if actor_wait is not None and not st.actor.double:
             torch.cuda.current_stream().wait_event(actor_wait)
-        agn = actor_opt.step_prenormed(st.agrads.norm_parts, st.agrads.nparts, pack=st.actor.adam_segments(actor_opt),
-                                       counter=counter)
+        if fused_opt:
+            agn = actor_opt.step_prenormed(st.agrads.norm_parts, st.agrads.nparts,
+                                           pack=st.actor.adam_segments(actor_opt), counter=counter)
+        else:   # data-parallel: the norm over the all-reduced gradient, then the same packing step
+            agn = actor_opt.step_synced(pack=st.actor.adam_segments(actor_opt), counter=counter)
         st.actor.flip()
     else:
         if sync is not None:

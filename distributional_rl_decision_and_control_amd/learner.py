@@ -125,6 +125,26 @@ class FusedAdam:
         g.row0, g.col0, g.nrep, g.rep_row, g.rep_col = row0, col0, nrep, rep_row, rep_col
         return g
 
+    def step_synced(self, pack=None, counter=None, stream=None):
+        """Clip + Adam over gradients already reduced in place (the data-parallel path, after GradSync's
+        all-reduce): one asvrl_partial_sums_norm launch over the flat gradient as a single one-group segment
+        (it rewrites each value in place, leaves the squared-norm partials and advances step_t), then the
+        step_prenormed launch, which writes the weight images of `pack` and increments `counter` -- instead
+        of asvrl_adam_clip followed by a re-pack of every image and a counter op. Returns the pre-clip norm."""
+        if getattr(self, "_sync_seg", None) is None:
+            g = _abi.AsvPartialSum()
+            g.partial = g.dw = self.grads.flat.data_ptr()
+            g.db = None
+            g.groups, g.nw, g.nb, g.accumulate = 1, self.n, 0, 0
+            g.stride, g.boff, g.mode, g.norm = 0, 0, _abi.SUM_PLAIN, 1
+            self._sync_seg = (_abi.AsvPartialSum * 1)(g)
+            self._sync_nparts = int(self.L.asvrl_partial_sums_norm_parts(self._sync_seg, 1))
+            self._sync_parts = torch.zeros(self._sync_nparts, dtype=torch.float64, device=self.flat.device)
+        _abi.check(self.L.asvrl_partial_sums_norm(self._sync_seg, 1, _abi.ptr(self._sync_parts), _abi.ptr(self.step_t),
+                                                  _abi.stream_ptr(stream)), "asvrl_partial_sums_norm", self.L)
+        return self.step_prenormed(self._sync_parts, self._sync_nparts, pack=pack if pack is not None else [],
+                                   counter=counter)
+
     def step_prenormed(self, norm_parts, nparts, pack=None, counter=None):
         """Clip + Adam with the squared norm as nparts f64 partials and step_t already advanced
         (PartialArena.flush(norm=self)): one launch. pack: AsvPackSeg list -- the same launch writes
