@@ -1015,14 +1015,31 @@ __device__ __forceinline__ void env_pairs_block(const AsvParams& p, const AsvEnv
 
 
 // The step kernel: workgroup b takes env group group0 + b (a step may be split into launches of at most
-// AsvEnvLaunch.max_groups workgroups, one after another: the rollout's share of the chip beside the learner)
+// AsvEnvLaunch.max_groups workgroups, one after another: the rollout's share of the chip beside the learner).
+// XCD-aware (1): the dispatcher deals workgroups to the eight XCDs round-robin, so consecutive env groups --
+// whose state / observation rows share cache lines at their edges -- would sit in different L2s and each
+// write back its part of the shared lines; the bijection below gives each XCD a contiguous run of groups.
+#ifndef ASVRL_ENV_XCD_SWIZZLE
+#define ASVRL_ENV_XCD_SWIZZLE 1
+#endif
+__device__ __forceinline__ int xcd_group(int x, int n) {
+#if ASVRL_ENV_XCD_SWIZZLE
+  constexpr int kXcd = 8;
+  const int q = n / kXcd, rr = n % kXcd, xcd = x % kXcd, k = x / kXcd;
+  return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + k;
+#else
+  (void)n;
+  return x;
+#endif
+}
 template <int BLOCK, int NM>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NM == 1 ? 1 : ASVRL_ENV_PAIRS_WPE))) void env_pairs_kernel(AsvParams p, AsvEnvState s,
                                                           const double* __restrict__ actions,
                                                           const double* __restrict__ noise,
                                                           AsvStepCtl ctl, AsvStepOut out, int epb, int group0) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  env_pairs_block<BLOCK, NM>(p, s, actions, noise, ctl, out, epb, group0 + static_cast<int>(blockIdx.x), smem);
+  env_pairs_block<BLOCK, NM>(p, s, actions, noise, ctl, out, epb,
+                             group0 + xcd_group(static_cast<int>(blockIdx.x), static_cast<int>(gridDim.x)), smem);
 }
 
 // ------------------------------------------------------------------ reset (env.py:72-164)
