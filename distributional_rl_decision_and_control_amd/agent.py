@@ -24,6 +24,7 @@ save_latest_model / load_model surfaces and return types. Differences:
 """
 import copy
 import random
+import warnings
 
 import numpy as np
 import torch
@@ -159,6 +160,12 @@ class Agent:
                 ok = fused_iqn.supported(self.policy_local, B, self.num_tau)
                 st = fused_iqn.FusedIQNState(self.policy_local, self.policy_target, B, self.num_tau,
                                              operands=ops) if ok else None
+            if st is None:
+                # not silent: this batch / network shape runs on the torch-autograd learner (learner.py), not on
+                # the hand-written kernels
+                warnings.warn(f"Agent({self.agent_type}): batch {B}, num_tau {self.num_tau} or the network shape is "
+                              "not one the fused kernels take; this learn step runs the torch-autograd learner",
+                              RuntimeWarning, stacklevel=3)
             self._fused = (key, st)
         return self._fused[1]
 

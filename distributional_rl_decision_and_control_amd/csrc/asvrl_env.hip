@@ -517,13 +517,11 @@ __global__ __launch_bounds__(BLOCK) void env_sweep_kernel(AsvParams p, AsvEnvSta
     }
     cnt = nkept < P.max_obj_num ? nkept : P.max_obj_num;
     // COLREGs over the kept objects in order, stop at the first hit (wamv.py:517-521)
-#ifndef ASVRL_NO_COLREGS
     if (cnt > 0) apply = colregs(P.r, cs, sn, r.v0, r.v1, t0.a, t0.b, t0.c, t0.d, t0.e, phi);
     if (!apply && cnt > 1) apply = colregs(P.r, cs, sn, r.v0, r.v1, t1.a, t1.b, t1.c, t1.d, t1.e, phi);
     if (!apply && cnt > 2) apply = colregs(P.r, cs, sn, r.v0, r.v1, t2.a, t2.b, t2.c, t2.d, t2.e, phi);
     if (!apply && cnt > 3) apply = colregs(P.r, cs, sn, r.v0, r.v1, t3.a, t3.b, t3.c, t3.d, t3.e, phi);
     if (!apply && cnt > 4) apply = colregs(P.r, cs, sn, r.v0, r.v1, t4.a, t4.b, t4.c, t4.d, t4.e, phi);
-#endif
   }
 
   const StepResult res = step_result(p, ctl, exists, deact, active, ep_ts, fl, coll, reach, apply, phi, reward,
@@ -934,13 +932,11 @@ __device__ __forceinline__ void env_pairs_block(const AsvParams& p, const AsvEnv
         rc = cs * vxn + sn * vyn;
         rd = -sn * vxn + cs * vyn;
         re = rn;
-#ifndef ASVRL_NO_COLREGS
         if (!(sqrt(rc * rc + rd * rd) < 0.5)) {   // colregs_body's first test, ahead of the call
           bool ev;
           const bool hit = colregs_ev(p.r, cs, sn, sv0[qr], sv1[qr], ra, rb, rc, rd, re, ph, ev);
           cf = static_cast<unsigned char>((ev ? 1 : 0) | (hit ? 2 : 0));
         }
-#endif
       }
       float* of = out.obs + qidx * ASVRL_OBS_DIM + 7 + 5 * k;
       of[0] = static_cast<float>(ra);

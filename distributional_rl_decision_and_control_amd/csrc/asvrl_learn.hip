@@ -99,14 +99,11 @@ __global__ __launch_bounds__(1024) void mean_kernel(const float* __restrict__ x,
 // B = 65536, 0.147 of HBM). Now a wave stages its ROWS rows in LDS (masses and each target's run bounds
 // as four bytes), finishes every target whose runs are short with selects (one ds_read2 per pass), and
 // queues the others as (row, target) jobs that the wave's lanes then walk in parallel, one job per lane.
-// The run bounds are scattered unconditionally (lanes that bound no run write a dummy slot); the row's
+// The run bounds are scattered by masked byte stores (only the lanes that bound a run write); the row's
 // scalars come through the scalar cache. Same additions in the same order: bit-identical.
 constexpr int kC51Waves = 4;
 #ifndef ASVRL_C51_ROWS
 #define ASVRL_C51_ROWS 4
-#endif
-#ifndef ASVRL_C51_DUMMY
-#define ASVRL_C51_DUMMY 0
 #endif
 // the workgroup's long-run jobs pooled and walked by its first waves (1), or each wave its own (0): at
 // four rows per wave 16.8 -> 15.9 us at B = 65536; at two (B = 8192) 5.5 -> 5.9 us, so there each wave its own
@@ -207,18 +204,11 @@ __global__ __launch_bounds__(kC51Waves * kWave) void c51_kernel(const float* __r
 #pragma unroll
   for (int r = 0; r < ROWS; ++r) {
     unsigned char* rb = reinterpret_cast<unsigned char*>(&s_rb[w][r][0]);
-#if ASVRL_C51_DUMMY
-    rb[4 * ((fl[r] & 1u) ? lt[r] : kWave) + 0] = static_cast<unsigned char>(lane);
-    rb[4 * ((fl[r] & 2u) ? lt[r] : kWave) + 1] = static_cast<unsigned char>(lane + 1);
-    rb[4 * ((fl[r] & 4u) ? ut[r] : kWave) + 2] = static_cast<unsigned char>(lane);
-    rb[4 * ((fl[r] & 8u) ? ut[r] : kWave) + 3] = static_cast<unsigned char>(lane + 1);
-#else
     // masked stores: the lanes bounding no run would all hit one dummy address (a 64-way bank conflict)
     if (fl[r] & 1u) rb[4 * lt[r] + 0] = static_cast<unsigned char>(lane);
     if (fl[r] & 2u) rb[4 * lt[r] + 1] = static_cast<unsigned char>(lane + 1);
     if (fl[r] & 4u) rb[4 * ut[r] + 2] = static_cast<unsigned char>(lane);
     if (fl[r] & 8u) rb[4 * ut[r] + 3] = static_cast<unsigned char>(lane + 1);
-#endif
   }
   wave_lds_order();
   if constexpr (kPool) __syncthreads();   // s_njob's initial value before any wave appends
@@ -280,9 +270,6 @@ __global__ __launch_bounds__(kC51Waves * kWave) void c51_kernel(const float* __r
 constexpr int kPushBlock = 256;
 // the last block takes the push's row count from the blocks' own counts (one integer atomic each) instead of
 // recounting every flag: IQN loop 0.2947 -> 0.2930 ms, AC-IQN unchanged (profiles/r04ad_push_sumcount_ab.txt)
-#ifndef ASVRL_PUSH_SUMCOUNT
-#define ASVRL_PUSH_SUMCOUNT 1
-#endif
 
 __device__ __forceinline__ int block_sum(int v, int* sh) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
@@ -373,23 +360,16 @@ __global__ __launch_bounds__(kPushBlock) void replay_push_kernel(
   }
   __syncthreads();   // every lane's read of ring_state is done before the block arrives
   if (threadIdx.x == 0) {
-#if ASVRL_PUSH_SUMCOUNT
     int cb = 0;
     for (int w = 0; w < kPushBlock / kWave; ++w) cb += shw[w];
     atomicAdd(arrive + 1, cb);   // the push's row count, block by block (integers: the order does not matter)
-#endif
     __threadfence();
     s_last = atomicAdd(arrive, 1) == nblocks - 1;
   }
   __syncthreads();
   if (!s_last) return;
-#if ASVRL_PUSH_SUMCOUNT
   if (threadIdx.x == 0) {
     const int tot = atomicExch(arrive + 1, 0);   // every block's count (added before its arrival), reset
-#else
-  const int tot = count_pushed(cnt, n, sh);
-  if (threadIdx.x == 0) {
-#endif
     const int64_t nh = (head_in + tot) % cap, ns0 = ring_state[1] + tot;
     const int64_t ns = ns0 < cap ? ns0 : cap;
     ring_state[0] = nh;

@@ -18,9 +18,6 @@ constexpr int kOptThreads = 256;
 #endif
 constexpr int64_t kAdamPer = ASVRL_ADAM_PER_THREAD;   // parameters per thread (grid size), at most 1024 blocks
 // the norm partials folded with wave shuffles and one barrier (1) instead of an eight-barrier LDS tree (0)
-#ifndef ASVRL_ADAM_WAVE_TREE
-#define ASVRL_ADAM_WAVE_TREE 1
-#endif
 
 __global__ __launch_bounds__(kOptThreads) void sumsq_kernel(const float* __restrict__ g, int64_t n,
                                                              double* __restrict__ partial, float* step) {
@@ -75,7 +72,6 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(float* __restrict__ p
   {   // thread t folds partials t, t + 256, ... in order, then a fixed tree: the same in every block
     double x = 0.0;
     x = strided_sum<double>(partial, threadIdx.x, nparts, kOptThreads, x);
-#if ASVRL_ADAM_WAVE_TREE
     // the tree inside each wave by xor shuffles (no barrier), then the four wave sums in order: one barrier
     // instead of eight (AC-IQN step 0.2626 -> 0.2621 ms, profiles/r04af_adam_wave_tree_ab.txt)
 #pragma unroll
@@ -87,16 +83,6 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(float* __restrict__ p
 #pragma unroll
       for (int w = 0; w < kOptThreads / kWave; ++w) t += s_red[w];
       const float norm = static_cast<float>(sqrt(t));
-#else
-    s_red[threadIdx.x] = x;
-    __syncthreads();
-    for (int w = kOptThreads / 2; w > 0; w >>= 1) {
-      if (threadIdx.x < w) s_red[threadIdx.x] += s_red[threadIdx.x + w];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-      const float norm = static_cast<float>(sqrt(s_red[0]));
-#endif
       s_norm = norm;
       if (blockIdx.x == 0 && norm_out != nullptr) norm_out[0] = norm;
     }

@@ -7,8 +7,8 @@ Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | 
   critic (agent.py:395-416)
     target actor(ns) -> na                               asvrl_actor_forward(FWD)
     target encoders(ns, na) + trunk -> q_next            asvrl_critic_forward (encoders in the prologue);
-                                                          (or inside the next launch: TARGET_IN_FUSED, ABI 20,
-                                                          measured slower, off)
+                                                          (by default inside the next launch: TARGET_IN_FUSED,
+                                                          ABI 20, asvrl_critic_train_fused_tq)
     local encoders(s, a), trunk forward, quantile-Huber vs r + g q_next (1-d), backward AND the
     four trunk layers' weight-gradient partials          asvrl_critic_train_fused (ONE launch)
     and the observation / action encoders' gradient partials (ABI 16; ENC_IN_KERNEL = False: from
@@ -16,7 +16,8 @@ Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | 
     every .grad (encoders folded in the reduction), the loss and the global gradient norm
                                                           ONE asvrl_partial_sums_norm
     clip + Adam + re-pack of the weight images           asvrl_adam_step_pack
-      (with DP: asvrl_partial_sums, RCCL all-reduce, asvrl_adam_clip, re-pack)
+      (with DP: asvrl_partial_sums, RCCL all-reduce, asvrl_partial_sums_norm over the averaged gradient
+       (FusedAdam.step_synced), asvrl_adam_step_pack)
   actor (agent.py:419-427), through the UPDATED critic
     encoders(s, a) + trunk forward + backward of -mean(q) to the action
                                                           asvrl_critic_actor_grad (dA in-kernel)
@@ -110,10 +111,14 @@ def _reduce_and_step(arena, opt, grads, sync, max_norm, wait=None, pack=None, co
     fused optimiser: the reduction launch also forms the gradient norm and the Adam launch writes the
     weight images of `pack` (a CriticPack / MlpPack / IqnPack) and increments `counter` (two launches
     in all; one persistent launch with a grid barrier between the two was measured slower, DESIGN.md 6);
-    otherwise reduce, all-reduce (sync), asvrl_adam_clip, then pack.refresh() and counter += 1.
+    with FusedAdam and a data-parallel `sync`: reduce (asvrl_partial_sums), all-reduce, then FusedAdam.step_synced
+    (asvrl_partial_sums_norm over the averaged gradient + the same packing asvrl_adam_step_pack); with another
+    optimiser: reduce, all-reduce, clip_and_step, then pack.refresh() and counter += 1.
     `wait`: an event to wait for before the parameters change."""
     assert pack is None or not isinstance(opt, FusedAdam) or opt.L is pack.L, "optimiser and pack of different builds"
     if isinstance(opt, FusedAdam):
+        # the fused steps clip at the optimiser's own max_norm: refuse a different one rather than ignore it
+        assert opt.max_norm == max_norm, (opt.max_norm, max_norm)
         if pack is not None and not hasattr(pack, "_adam_segs"):
             pack._adam_segs = pack.adam_segments(opt)
         segs = pack._adam_segs if pack is not None else None
@@ -184,7 +189,8 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     counter: an int64 device scalar incremented after the step (the learn counter; in-kernel when
     the optimiser step is fused). prologue_done: learn_prologue already ran the actor's TRAIN forward and
     the target actor on these rows. target_wait: an event the target critic waits for (a schedule knob:
-    the rollout's env step ahead of it instead of beside it; no data dependency). actor_done: an event recorded
+    the rollout's env step ahead of it instead of beside it; no data dependency) -- with the target pass inside the
+    fused launch (TARGET_IN_FUSED) the whole fused critic update waits for it. actor_done: an event recorded
     after the ACTOR pass (a schedule knob: what the rollout's replay push may wait for).
     Returns (critic_loss, actor_loss, critic_grad_norm, actor_grad_norm) as device scalars."""
     B, N = st.B, st.N
@@ -237,6 +243,7 @@ def ac_iqn_update_fused2(st, policy_local, actor_opt, critic_opt, critic_grads, 
     actor_grads_launch(st.agrads, ab, actor, st.tile_loss[1], st.losses[1:2],
                        step=actor_opt.step_t if fused_opt else None, norm=fused_opt)
     if isinstance(actor_opt, FusedAdam):
+        assert actor_opt.max_norm == max_norm, (actor_opt.max_norm, max_norm)
         if sync is not None:
             sync(actor_grads)
         # a concurrent act kernel reads the current actor images: with two sets the step writes the other one

@@ -1,11 +1,16 @@
-"""Distributional Bellman updates of rfarl's Agent (agent.py:386-476, 597-641) on the GPU.
+"""Optimiser and data-parallel plumbing of the learner (agent.py:75-76, 98, 415-427), and the
+torch-autograd update functions the drop-in Agent falls back to for network shapes the kernels do not take.
 
-The quantile-Huber loss and its gradient come from the fused gfx950 kernel
-(learn_ops.quantile_huber_loss), the C51 target from the bit-exact projection kernel
-(learn_ops.c51_project); the MLP layers run on torch (hipBLASLt/MFMA), optionally under bf16
-autocast. Data-parallel training passes a GradSync, which all-reduces each network's flat
-gradient over RCCL between backward and clip -- twice per AC-IQN step (critic, then actor
-through the *updated* critic, agent.py:395-427), once for IQN / Rainbow.
+* FlatGrads / FusedAdam: every network's gradient in one flat buffer; clip + Adam (+ the re-pack of the
+  kernels' bf16 weight images) as hand-written launches (asvrl_adam_clip, asvrl_adam_step_pack).
+* GradSync: the data-parallel all-reduce of a flat gradient over RCCL between the gradient reduction and the
+  clip -- twice per AC-IQN step (critic, then actor through the *updated* critic, agent.py:395-427), once for
+  IQN / Rainbow.
+* ac_iqn_update / iqn_update / rainbow_update: the reference's updates on torch modules (autograd) with the
+  quantile-Huber loss (learn_ops.quantile_huber_loss) and the C51 projection (learn_ops.c51_project) on their
+  kernels. The training path does not use them: its updates are the fused launches of fused_update.py,
+  fused_iqn.py and fused_rainbow.py (no torch GEMM, no autograd); Agent uses these only for shapes those
+  launches do not take, and says so when it does (agent.py).
 """
 import ctypes as C
 
@@ -48,10 +53,23 @@ class GradSync:
         self.avg_supported = dist.is_initialized() and dist.get_backend(group) == "nccl"
         # force: issue the collective even over one rank (tests of the captured DP path on one GPU)
         self.force = bool(force) and dist.is_initialized()
+        # timing: None, or a list that collects (bytes, start event, end event) per collective -- HIP events on
+        # the stream the collective is issued on (RCCL runs on it), eager steps only (bench.py allreduce_timing)
+        self.timing = None
 
     def __call__(self, fg: FlatGrads):
         if self.world == 1 and not self.force:
             return
+        if self.timing is not None and fg.flat.is_cuda:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(torch.cuda.current_stream(fg.flat.device))
+            self._reduce(fg)
+            e1.record(torch.cuda.current_stream(fg.flat.device))
+            self.timing.append((fg.flat.numel() * fg.flat.element_size(), e0, e1))
+            return
+        self._reduce(fg)
+
+    def _reduce(self, fg):
         if self.avg_supported:
             dist.all_reduce(fg.flat, op=dist.ReduceOp.AVG, group=self.group)
         elif fg.flat.is_cuda:

@@ -37,10 +37,12 @@ def _params_key(env):
 
 
 @torch.no_grad()
-def batched_greedy_actions(agent, states):
+def batched_greedy_actions(agent, states, taus=None):
     """Greedy actions (eps = 0) for a list of per-robot states in one network call. Each robot
     consumes one random.random() like the batch-1 act functions; the (probability ~2^-53) draw
-    that is not > 0 explores as they do."""
+    that is not > 0 explores as they do. taus (IQN only): the K quantile fractions of every row
+    ((n, K) or (n, K, 1)) instead of fresh draws -- act_iqn's calc_cos draws (IQN_model.py:56-72),
+    injected by the parity test."""
     kind = agent.agent_type
     s = agent.state_to_tensor(agent.memory.state_batch(states))
     if kind == "AC-IQN":
@@ -52,7 +54,7 @@ def batched_greedy_actions(agent, states):
     elif kind == "IQN":
         net = agent.policy_local
         net.eval()
-        q, _ = net(s, net.K, 1.0)
+        q, _ = net(s, net.K, 1.0, taus=taus)
         net.train()
         greedy = [int(v) for v in q.mean(dim=1).argmax(dim=1).cpu().numpy()]
     elif kind == "Rainbow":

@@ -105,7 +105,9 @@ class VecMarineNavEnv:
         d = 1 if counted else 0
         if events is not None:
             events[0].record()
-        if self.fused_reset and b.robot_params is None:
+        # the one-launch form takes no workgroup cap (one wave-per-env workgroup per env): with max_groups set (the
+        # --env-groups A/B knob) the reset keeps the capped two-launch form, so the cap applies to every env pass
+        if self.fused_reset and b.robot_params is None and self.max_groups <= 0:
             # one launch: reset + the reset observation of the ended envs only (asvrl_env_reset_observe)
             b.reset_observe(self.cfg, b.env_done, seed=self.seed, counter=0x40000000 - d, counter_dev=self.counter,
                             obs_counter=0x80000000 - d, obs=self.obs_next, obj_cnt=self.cnt_next)

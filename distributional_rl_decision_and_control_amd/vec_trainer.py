@@ -50,7 +50,9 @@ class VecTrainer:
         self.device = torch.device(device)
         self.agent_type = agent_type
         # chained schedule knob: the AC-IQN learner's target critic waits for the same iteration's env step
-        # (the two then run one after the other instead of side by side; results unchanged)
+        # (the two then run one after the other instead of side by side; results unchanged). With the target pass
+        # inside the fused critic launch (fused_update.TARGET_IN_FUSED, the default) that wait gates the whole
+        # fused critic update, not only the target forward
         self.target_after_env = bool(target_after_env)
         # schedule knob: the rollout's replay push (and the reset behind it) waits for the learner's ACTOR pass
         # of the same iteration instead of running beside it (None: wherever the chained AC-IQN graph runs)

@@ -167,36 +167,14 @@ def bf16_round(x):
     return x.to(torch.bfloat16).to(x.dtype)
 
 
-def critic_step_bf16(w, s, a, q_next, r, d, taus, gamma=0.99, kappa=1.0, rnd=bf16_round, dtype=torch.float64):
-    """agent.py:395-414's critic gradients (AC_IQN_model.py:284-308,410-480 forward, quantile-Huber
-    agent.py:701-707, backward) restated with the rounding points of the bf16 training build's ONE fused
-    launch, critic_fused_kernel<N, false> (asvrl_critic_fused.hip), at which every MFMA operand is bf16 and
-    every accumulation f32 -- here f64, so only the rounding points are emulated:
-
-      weights   Wc, W1, W2 as bf16 images (biases, wo, the encoders f32; bias = the accumulator's start)
-      forward   F = bf16(relu(enc(s)))  (masked objects 0), G = relu(enc_a(a)) f32, cos = bf16(cos(tau pi k)),
-                c = relu(bc + Wc cos), x = bf16(F c), h1 = relu(b1 + W1 x), h1g = bf16(h1 G),
-                h2 = relu(b2 + W2 h1g), q = wo . h2 + bo (h2 f32)
-      loss      the quantile-Huber terms against r + gamma q_next (1 - d), dq = dL/dq
-      backward  dz2 = bf16(dq wo 1[h2 > 0]); d wo = sum dq bf16(h2); dh1g = W2^T dz2;
-                dz1 = bf16(dh1g G 1[h1 > 0]); dG = sum_tau dh1g bf16(h1); dx = W1^T dz1;
-                dF = sum_tau dx c; dzc = bf16(dx F 1[c > 0]); dW = dZ^T X of the bf16 images
-      encoders  dzF = dF 1[F > 0], dzG = dG 1[G > 0] (f32) into the encoders' weight / bias sums
-
-    w: critic state_dict (f32 tensors, reference key names); s = (self (B,7), objects (B,5,5), mask (B,5));
-    a (B,2); q_next (B,N') the target quantiles the launch read; r, d (B,); taus (B,N). rnd=identity
-    reduces this to the plain f64 critic step (pinned to torch autograd on the reference's own batch by
-    tests/test_bf16_oracle_cpu.py). dtype=torch.float32 evaluates the same rounding points with f32
-    arithmetic everywhere else (CPU summation orders): the spread between the two evaluations is the
-    noise floor any f32 implementation of these rounding points shows (tests/test_critic_bf16_oracle_gpu.py).
-    Returns (loss, {parameter name: gradient}) in `dtype`."""
+def _forward_bf16(w, s, a, taus, rnd, dtype):
+    """The forward of critic_step_bf16 (its rounding points, see there); returns the intermediates."""
     f64 = dtype
     W = {k: torch.as_tensor(v).to(f64) for k, v in w.items()}
     s_self, s_obj, s_mask = (torch.as_tensor(x).to(f64) for x in s)
-    a, q_next = torch.as_tensor(a).to(f64), torch.as_tensor(q_next).to(f64)
-    r, d, taus = (torch.as_tensor(x).to(f64) for x in (r, d, taus))
+    a = torch.as_tensor(a).to(f64)
+    taus = torch.as_tensor(taus).to(f64)
     B, N = taus.shape
-    Np = q_next.shape[1]
     wc, w1, w2 = (rnd(W[p + ".weight"]) for p in ("cos_embedding", "hidden_layer", "hidden_layer_2"))
     bc, b1, b2 = (W[p + ".bias"] for p in ("cos_embedding", "hidden_layer", "hidden_layer_2"))
     wo, bo = W["output_layer.weight"][0], W["output_layer.bias"][0]
@@ -234,6 +212,49 @@ def critic_step_bf16(w, s, a, q_next, r, d, taus, gamma=0.99, kappa=1.0, rnd=bf1
     h1g = rnd(h1 * Gr)
     h2 = torch.relu(h1g @ w2.T + b2)
     q = (h2 @ wo + bo).view(B, N)
+    return dict(W=W, s_self=s_self, s_obj=s_obj, a=a, taus=taus, B=B, N=N, wc=wc, w1=w1, w2=w2, wo=wo, bo=bo, G=G,
+                Fb=Fb, cos=cos, Fr=Fr, Gr=Gr, c=c, x=x, h1=h1, h1g=h1g, h2=h2, q=q)
+
+
+def critic_forward_bf16(w, s, a, taus, rnd=bf16_round, dtype=torch.float64):
+    """The critic's forward (AC_IQN_model.py:410-480) with the bf16 training build's rounding points (see
+    critic_step_bf16) -- those of the target critic's forward pass inside the update launch
+    (asvrl_critic_train_fused_tq: asvrl_critic_tile.h critic_tile<MODE_FWD>, which forms F, G, cos, x, h1g and q
+    exactly as the update's forward does). Returns q (B, N) in `dtype`."""
+    return _forward_bf16(w, s, a, taus, rnd, dtype)["q"]
+
+
+def critic_step_bf16(w, s, a, q_next, r, d, taus, gamma=0.99, kappa=1.0, rnd=bf16_round, dtype=torch.float64):
+    """agent.py:395-414's critic gradients (AC_IQN_model.py:284-308,410-480 forward, quantile-Huber
+    agent.py:701-707, backward) restated with the rounding points of the bf16 training build's ONE fused
+    launch, critic_fused_kernel<N, false> (asvrl_critic_fused.hip), at which every MFMA operand is bf16 and
+    every accumulation f32 -- here f64, so only the rounding points are emulated:
+
+      weights   Wc, W1, W2 as bf16 images (biases, wo, the encoders f32; bias = the accumulator's start)
+      forward   F = bf16(relu(enc(s)))  (masked objects 0), G = relu(enc_a(a)) f32, cos = bf16(cos(tau pi k)),
+                c = relu(bc + Wc cos), x = bf16(F c), h1 = relu(b1 + W1 x), h1g = bf16(h1 G),
+                h2 = relu(b2 + W2 h1g), q = wo . h2 + bo (h2 f32)
+      loss      the quantile-Huber terms against r + gamma q_next (1 - d), dq = dL/dq
+      backward  dz2 = bf16(dq wo 1[h2 > 0]); d wo = sum dq bf16(h2); dh1g = W2^T dz2;
+                dz1 = bf16(dh1g G 1[h1 > 0]); dG = sum_tau dh1g bf16(h1); dx = W1^T dz1;
+                dF = sum_tau dx c; dzc = bf16(dx F 1[c > 0]); dW = dZ^T X of the bf16 images
+      encoders  dzF = dF 1[F > 0], dzG = dG 1[G > 0] (f32) into the encoders' weight / bias sums
+
+    w: critic state_dict (f32 tensors, reference key names); s = (self (B,7), objects (B,5,5), mask (B,5));
+    a (B,2); q_next (B,N') the target quantiles the launch read; r, d (B,); taus (B,N). rnd=identity
+    reduces this to the plain f64 critic step (pinned to torch autograd on the reference's own batch by
+    tests/test_bf16_oracle_cpu.py). dtype=torch.float32 evaluates the same rounding points with f32
+    arithmetic everywhere else (CPU summation orders): the spread between the two evaluations is the
+    noise floor any f32 implementation of these rounding points shows (tests/test_critic_bf16_oracle_gpu.py).
+    Returns (loss, {parameter name: gradient}) in `dtype`."""
+    f64 = dtype
+    fw = _forward_bf16(w, s, a, taus, rnd, dtype)
+    W, s_self, s_obj, a, taus, B, N = (fw[k] for k in ("W", "s_self", "s_obj", "a", "taus", "B", "N"))
+    wc, w1, w2, wo, bo, G, Fb, cos, Fr, Gr = (fw[k] for k in ("wc", "w1", "w2", "wo", "bo", "G", "Fb", "cos", "Fr", "Gr"))
+    c, x, h1, h1g, h2, q = (fw[k] for k in ("c", "x", "h1", "h1g", "h2", "q"))
+    q_next = torch.as_tensor(q_next).to(f64)
+    r, d = (torch.as_tensor(v).to(f64) for v in (r, d))
+    Np = q_next.shape[1]
     # quantile-Huber (agent.py:399-412): L = mean_b mean_j sum_i |tau_i - 1[delta < 0]| H(delta) / kappa
     qt = r.view(B, 1) + gamma * q_next * (1.0 - d.view(B, 1))
     delta = qt.view(B, 1, Np) - q.view(B, N, 1)

@@ -1,6 +1,7 @@
 """Worker of tests/test_dp_fused_gpu.py (not a test module): the fused learner updates of one
-rank on its share of a fixed batch, with the gradient all-reduce of fused_update._step_unfused
-(asvrl_partial_sums -> GradSync -> asvrl_adam_clip -> re-pack).
+rank on its share of a fixed batch, with the gradient all-reduce of fused_update._reduce_and_step's
+data-parallel branch (asvrl_partial_sums -> GradSync -> FusedAdam.step_synced: asvrl_partial_sums_norm over the
+averaged gradient, then asvrl_adam_step_pack writing the weight images; Rainbow: asvrl_adam_clip + re-pack).
 
     python tests/dp_fused_worker.py RANK WORLD PORT OUT.npz
 

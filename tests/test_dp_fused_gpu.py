@@ -1,8 +1,9 @@
 """GPU, 2 ranks on one GPU over gloo: the data-parallel branch of the FUSED learners.
 
-fused_update._step_unfused is the multi-rank path of every hand-written update: the
-weight-gradient partials are reduced (asvrl_partial_sums), all-reduced (GradSync), then clipped +
-Adam (asvrl_adam_clip) and the weight images re-packed. AC-IQN all-reduces the critic gradient,
+fused_update._reduce_and_step's data-parallel branch is the multi-rank path of every hand-written update: the
+weight-gradient partials are reduced (asvrl_partial_sums), all-reduced (GradSync), then the norm is formed over the
+averaged gradient and clip + Adam write the weight images in one launch (FusedAdam.step_synced:
+asvrl_partial_sums_norm + asvrl_adam_step_pack; Rainbow: asvrl_adam_clip and a re-pack). AC-IQN all-reduces the critic gradient,
 steps the critic, then evaluates the actor loss through the UPDATED critic and all-reduces the
 actor gradient (agent.py:395-427: two collectives); IQN (agent.py:466-472) and Rainbow
 (agent.py:632-637) one each.

@@ -25,6 +25,7 @@ Fixture families:
                         networks from a numpy-seeded generator (oracle/learn_ref.py)
   learn_dqn.npz     F8  Agent.train_DQN / act_dqn (agent.py:518-545, 271-287)
   eval_ref.npz      F9  Trainer.evaluation (trainer.py:266-392), AC-IQN and Rainbow
+  eval_iqn_ref.npz  F9b the same for IQN with every act_iqn call's K = 32 taus recorded (capture_eval_iqn)
   eval60_ref.npz    F10 Trainer.evaluation on config/ac_iqn.json's 60-episode eval_schedule, the seeded
                         AC-IQN agent and the same agent after 200 train_AC_IQN steps (capture_eval60)
   eval60_tf.npz     F10b the same two evaluations re-run from F10's own configs and actor weights, with every
@@ -1050,6 +1051,68 @@ def capture_eval():
               "successes", tr.eval_successes[0])
     np.savez_compressed(os.path.join(OUT, "eval_ref.npz"), **out)
     print("eval keys:", len(out))
+
+
+def capture_eval_iqn():
+    """F9b: Trainer.evaluation (trainer.py:266-392) with the seeded initial IQN agent on the eval configs of
+    EVAL_SCHEDULE, recording the K = 32 quantile fractions of EVERY act_iqn call (agent.py:227-250, drawn by
+    IQN_Policy.calc_cos, IQN_model.py:56-72) keyed by (config, step, robot), with the action it chose and its
+    mean quantiles; plus the per-config metrics, trajectories and action histories. The parity test injects the
+    same taus into the batched evaluation (eval_iqn_ref.npz)."""
+    import json
+    import random
+    from rfarl.policy.trainer import Trainer
+    out = {}
+    torch.manual_seed(0)
+    agent = ref_agent_mod.Agent(device="cpu", seed=100, agent_type="IQN")
+    eval_env = MarineNavEnv3(seed=253, is_eval_env=True)
+    tr = Trainer(MarineNavEnv3(seed=1), eval_env, EVAL_SCHEDULE, agent)
+    pos = {"e": -1, "t": 0, "k": 0}
+    calls = []   # (config, step, robot, action, taus[32], mean quantiles[25])
+    orig_reset, orig_step, orig_act = eval_env.reset_with_eval_config, eval_env.step, agent.act_iqn
+
+    def reset(cfg):
+        pos["e"] += 1
+        pos["t"] = pos["k"] = 0
+        return orig_reset(cfg)
+
+    def step(action, cont):
+        r = orig_step(action, cont)
+        pos["t"] += 1
+        pos["k"] = 0
+        return r
+
+    def act(state, *a, **k):
+        active = [i for i, rob in enumerate(eval_env.robots) if not rob.deactivated]
+        robot = active[pos["k"]]
+        pos["k"] += 1
+        action, q, taus = orig_act(state, *a, **k)
+        calls.append((pos["e"], pos["t"], robot, int(action), np.asarray(taus, np.float32).reshape(-1),
+                      np.asarray(q, np.float64).mean(axis=1).reshape(-1)))
+        return action, q, taus
+    eval_env.reset_with_eval_config, eval_env.step, agent.act_iqn = reset, step, act
+    random.seed(77)
+    np.random.seed(77)
+    tr.evaluation()
+    p = "IQN/"
+    out[p + "configs"] = np.array(json.dumps(tr.eval_config))
+    out.update(sd_arrays(p + "net/", agent.policy_local))
+    out[p + "rewards"] = np.array(tr.eval_rewards[0], dtype=np.float64)
+    out[p + "successes"] = np.array(tr.eval_successes[0], dtype=bool)
+    out[p + "times"] = np.array(tr.eval_times[0], dtype=np.float64)
+    out[p + "energies"] = np.array(tr.eval_energies[0], dtype=np.float64)
+    out[p + "lengths"] = np.array([max(len(t) for t in ep) for ep in tr.eval_trajectories[0]], dtype=np.int64)
+    for e, ep in enumerate(tr.eval_trajectories[0]):
+        for i, traj in enumerate(ep):
+            out[f"{p}traj/{e}/{i}"] = np.array(traj, dtype=np.float64)
+            out[f"{p}act/{e}/{i}"] = np.array(tr.eval_actions[0][e][i], dtype=np.float64)
+    out[p + "calls/key"] = np.array([c[:3] for c in calls], dtype=np.int32)
+    out[p + "calls/action"] = np.array([c[3] for c in calls], dtype=np.int32)
+    out[p + "calls/taus"] = np.stack([c[4] for c in calls]).astype(np.float32)
+    out[p + "calls/qmean"] = np.stack([c[5] for c in calls]).astype(np.float32)
+    print("IQN eval lengths", [[len(t) for t in ep] for ep in tr.eval_trajectories[0]], "successes",
+          tr.eval_successes[0], "act calls", len(calls))
+    np.savez_compressed(os.path.join(OUT, "eval_iqn_ref.npz"), **out)
 
 
 def capture_eval60():
