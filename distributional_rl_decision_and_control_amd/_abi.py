@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("ASVRL_LIB", os.path.join(HERE, "lib", "libasvrl.so"))
 # the same sources built with f32 learner operands (the parity build; asvrl_operand_bytes() == 4)
 LIB_PATH_F32 = os.path.join(HERE, "lib", "libasvrl_f32.so")
 OPERANDS = {"bf16": (LIB_PATH, 2), "f32": (LIB_PATH_F32, 4)}
-ABI_VERSION = 22
+ABI_VERSION = 23
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
 OBS_DIM = 40   # self 7 | objects 25 | mask 5 | pad 3
@@ -285,6 +285,7 @@ EXPORTS = [
     ("asvrl_linear_wgrad_workspace", _I64, [_I32, _I32]),
     ("asvrl_critic_wout_groups", _I32, [_I32, _I32]),
     ("asvrl_critic_fused_groups", _I32, [_I32, _I32]),
+    ("asvrl_critic_fused_variant", _I32, [_I32]),
     ("asvrl_critic_train_fused", C.c_int, [C.POINTER(AsvCriticWeights), C.POINTER(AsvCriticIO),
                                            C.POINTER(AsvCriticParts), _VP]),
     ("asvrl_critic_train_fused_tq", C.c_int, [C.POINTER(AsvCriticWeights), C.POINTER(AsvCriticIO),

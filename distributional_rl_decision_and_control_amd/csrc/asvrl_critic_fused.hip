@@ -1459,6 +1459,684 @@ void critic_fused_kernel(FusedArgs a) {
   if (threadIdx.x == 0) po[kH] = ((L.red[0] + L.red[1]) + L.red[2]) + L.red[3];
 }
 
+#if !ASVRL_OPERAND_F32
+// =================================================================================================================
+// critic_fused8_kernel -- the same critic update (and, TQ, the target critic's forward) at TWO waves per SIMD:
+// 8 waves, 512 threads per workgroup, one workgroup per CU. VERDICT r05 item 1: at one wave per SIMD the round was
+// vector-issue and latency bound (MFMA busy ~20 %: a lone wave issues one VALU instruction per 4 cycles and nothing
+// covers its LDS / L2 waits); two waves per SIMD issue VALU at the SIMD's full rate (2 cycles per wave instruction)
+// and one wave's MFMAs run while its partner issues its epilogue. The register file is split in half: each wave owns
+// HALF of the persistent weight-gradient accumulators (128 AGPRs instead of 256) and has 128 VGPRs for the round.
+//
+// Wave v: w = v & 3 (the feature block the old kernel's wave w owned), j = v >> 2 (the half). Waves w and w + 4 share
+// a SIMD (the workgroup's waves go round the four SIMDs) and split the old wave w's work:
+//   L0, L4, dzc, dWc (256 cos-layer features)  by feature:  cos block cb = 2w + j, both row blocks;
+//   L1 (K = 256)                               by K:        hidden block w, k-steps 8j..8j+7, both row blocks;
+//                                                           the partner's partial sum of row block j is added
+//                                                           through LDS (the free dzc images) before the epilogue;
+//   L2, dz2, L3 (128 features)                 by rows:     hidden block w, row block j (= sample j at N = 32);
+//   dW2 / dW1 (rows = own features)            by columns:  n in {2j, 2j+1} / {4j .. 4j+3};
+//   loss                                        waves 0-3 (16-row groups, as before).
+// AGPRs per wave: dW2 2 + dW1 4 + dWc 2 blocks of 16 = 128. Per-sample sums over a row block (dG, dF) reduce 16
+// values over the 32 lanes of a half (half_rows_sum16); the output layer's gradient is reduced per round.
+// One barrier more per round than critic_fused_kernel (the L1 partial exchange).
+//
+// The target pass (TQ) runs the SAME forward phases (L0, L1, L2) on the target critic's weights, round by round over
+// the workgroup's own samples, and stores q_next for the update's rounds (global, read back by this workgroup after
+// the barrier); the target's biases and encoders occupy the LDS slots of the local ones until the update starts.
+//
+// Shapes: AC-IQN, N = N' = 32, bf16 operands, the encoders' gradients in the launch (parts.enc / parts.aenc), no
+// per-sample dzF / dzG / xb outputs; critic_fused_kernel takes every other case. Same rounding points as
+// critic_fused_kernel (checked against oracle/learn_ref.critic_step_bf16 / critic_forward_bf16); the f32
+// summation order differs (L1's two K halves, the per-round row sums), so the two kernels agree within f32
+// rounding, not bit for bit.
+constexpr int kNW8 = 8, kT8 = kNW8 * 64;
+
+// sum of each of 16 values over the 32 lanes of each lane half: afterwards x[0] of lane r (either 16-lane row of
+// the half) holds the sum of value r % 16 (transpose-reduce over lane bits 0..3, then the two rows)
+__device__ __forceinline__ void half_rows_sum16(float (&x)[16], int lane) {
+  xreduce<16, 16>(x, lane);
+  x[0] = row_pair_sum(x[0]);
+}
+
+// the same for 8 values: x[0] of lane r holds the sum of value r % 8 (lane bits 0..2, then bit 3 by a row rotation
+// of 8 -- lane ^ 8 inside its 16-lane row -- then bit 4)
+__device__ __forceinline__ void half_rows_sum8(float (&x)[8], int lane) {
+  xreduce<8, 8>(x, lane);
+  x[0] += dpp<0x128>(x[0]);   // row_ror:8
+  x[0] = row_pair_sum(x[0]);
+}
+
+// F (observation_processor) and G (relu(action_encoder(a))) of the round's 2 samples: thread t computes feature
+// t & 255 of sample t >> 8 (stage_fg's arithmetic, op for op, uncontracted)
+__device__ __forceinline__ void stage_fg8(int tid, const float* in, int kact, const float* enc, float* Fs, float* Gs) {
+#pragma clang fp contract(off)
+  const float* self_w = enc;
+  const float* self_b = self_w + 56 * 7;
+  const float* obj_w = self_b + 56;
+  const float* obj_b = obj_w + 40 * 5;
+  const float* ae_w = obj_b + 40;
+  const float* ae_b = ae_w + 128 * 2;
+  const int m = tid & 255, k = tid >> 8;
+  const float* x = in + k * kObsIn;
+  float v;
+  if (m < kSelfF) {
+    float d = 0.f;
+#pragma unroll
+    for (int i = 0; i < kSelfIn; ++i) d += self_w[m * kSelfIn + i] * x[i];
+    v = relu(d + self_b[m]);
+  } else {
+    const int o = (m - kSelfF) / kObjF, jf = (m - kSelfF) % kObjF;
+    const float* xo = x + kSelfIn + kObjIn * o;
+    float d = 0.f;
+#pragma unroll
+    for (int i = 0; i < kObjIn; ++i) d += obj_w[jf * kObjIn + i] * xo[i];
+    v = x[kObsMask + o] < 0.5f ? 0.f : relu(d + obj_b[jf]);   // masked_fill(mask < 0.5, 0)
+  }
+  Fs[k * kC + swap23(m)] = static_cast<float>((elem_t)v);
+  if (m < kH)
+    Gs[k * kH + swap23(m)] = relu((ae_w[2 * m] * in[kact + 2 * k] + ae_w[2 * m + 1] * in[kact + 2 * k + 1]) + ae_b[m]);
+}
+
+// element e (< kObs + kAct + kTau) of the TARGET pass's round t inputs: next observation rows, next actions, taus'
+template <class IL>
+__device__ __forceinline__ float fetch_tq(const ctile::CriticArgs& t, int r, int e) {
+  constexpr int S = 2, G = 64;
+  const int64_t b0 = static_cast<int64_t>(r) * S;
+  const float* p;
+  if (e < IL::kAct) p = t.obs + (b0 + e / kObsIn) * t.ld_obs + e % kObsIn;
+  else if (e < IL::kTau) p = t.ain + (b0 + (e - IL::kAct) / 2) * t.ld_ain + (e - IL::kAct) % 2;
+  else p = t.taus + static_cast<int64_t>(r) * G + (e - IL::kTau);
+  return *p;
+}
+
+template <bool TQ>
+__global__ __launch_bounds__(kT8) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void critic_fused8_kernel(FusedArgs a) {
+  constexpr int NT = 32, NB = 2, G = 64, S = 2;
+  using IL = InLayout<NT, S, G, 2>;
+  constexpr int kPer8 = (IL::kSize + kT8 - 1) / kT8;
+  __shared__ __attribute__((aligned(16))) FusedLds<NT, NB, S, false, 2> L;
+  __shared__ int LB[kLbFields][64];
+  __shared__ __attribute__((aligned(16))) float red8[2][kH];   // the output layer's gradient, one row per half
+  static_assert(sizeof(L) + sizeof(LB) + sizeof(red8) <= 160 * 1024, "fused8 LDS exceeds the CU's 160 KB");
+  // the L1 partial exchange: [w][row block][4 quarters][64 lanes] f32x4 in the dzc images (free until L4)
+  static_assert(sizeof(L.dzc) >= 4 * 2 * 16 * 64 * 4, "L1 exchange scratch");
+  float* const xch = reinterpret_cast<float*>(&L.dzc[0][0]);
+  {
+    const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
+    if (threadIdx.x < 64) {
+      LB[kLbR64][lane] = RowA<kNcos>(r, h).base;
+      LB[kLbR128][lane] = RowA<kH>(r, h).base;
+      LB[kLbR256][lane] = RowA<kC>(r, h).base;
+      const auto t64 = TrA<kNcos>(lane);
+      const auto t128 = TrA<kH>(lane);
+      const auto t256 = TrA<kC>(lane);
+      LB[kLbT64lo][lane] = t64.lo;
+      LB[kLbT64hi][lane] = t64.hi;
+      LB[kLbT128lo][lane] = t128.lo;
+      LB[kLbT128hi][lane] = t128.hi;
+      LB[kLbT256lo][lane] = t256.lo;
+      LB[kLbT256hi][lane] = t256.hi;
+    }
+  }
+  float* const bcp = L.bias;
+  float* const b1p = L.bias + kC;
+  float* const b2p = L.bias + kC + kH;
+  float* const wop = L.bias + kC + 2 * kH;
+  // biases (position order), wo, bo and the encoders of weight set `ws` into LDS
+  auto load_params = [&](const AsvCriticWeights& ws) {
+    for (int i = threadIdx.x; i < kC; i += kT8) bcp[swap23(i)] = ws.bc[i];
+    for (int i = threadIdx.x; i < kH; i += kT8) {
+      b1p[swap23(i)] = ws.b1[i];
+      b2p[swap23(i)] = ws.b2[i];
+      wop[swap23(i)] = ws.wo[i];
+    }
+    if (threadIdx.x == 0) L.bias[kC + 3 * kH] = ws.bo[0];
+    constexpr int kEncPer = (kEncFloats + kT8 - 1) / kT8;
+    float ev[kEncPer];
+#pragma unroll
+    for (int u = 0; u < kEncPer; ++u) {
+      int e = threadIdx.x + u * kT8;
+      const float* src = ws.self_w;
+      if (e >= 392) { e -= 392; src = ws.self_b;
+        if (e >= 56) { e -= 56; src = ws.obj_w;
+          if (e >= 200) { e -= 200; src = ws.obj_b;
+            if (e >= 40) { e -= 40; src = ws.ae_w;
+              if (e >= 256) { e -= 256; src = ws.ae_b; } } } } }
+      ev[u] = threadIdx.x + u * kT8 < kEncFloats ? src[e] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kEncPer; ++u)
+      if (threadIdx.x + u * kT8 < kEncFloats) L.enc[threadIdx.x + u * kT8] = ev[u];
+  };
+  // F, G and cos(tau pi k) of a round (inputs staged at `ins`) into one image set; targets r + gamma q' (1 - d) in
+  // place over q' unless `fwd_only`
+  auto stage = [&](float* ins, elem_t* cosd, float* Fd, float* Gd, bool fwd_only) {
+    int tid_s = threadIdx.x;
+    asm volatile("" : "+v"(tid_s));
+    stage_fg8(tid_s, ins, IL::kAct, L.enc, Fd, Gd);
+    if (!fwd_only && tid_s < S * NT) {
+      const int k = tid_s / NT;
+      float* qn = ins + IL::kQn + tid_s;
+      *qn = ins[IL::kRew + k] + (a.gamma * *qn) * (1.0f - ins[IL::kDon + k]);
+    }
+    static_assert(G * (kNcos / 8) == kT8, "one cos chunk per thread");
+    const int row = tid_s / (kNcos / 8), ch = tid_s % (kNcos / 8);
+    float cv[8];
+    cos_pi_k_tau8r(ins[IL::kTau + row], 8 * ch, cv);
+    row_store<kNcos>(cosd, row, 8 * ch, pack8(cv));
+  };
+
+  // ---------------- the forward phases, on weight set `ws` (local or target)
+  // L0: c = relu(Wc cos + bc), x = F c for cos block cb = 2w + j, both row blocks
+  // the Wc fragments of cos block cb (4) and, fetched here for L1a, the wave's W1 half (8)
+  auto load_wc = [&](const AsvCriticWeights& ws, frag8 (&wc)[4]) {
+    ASVRL_FRESH_LANE();
+    const int v = __builtin_amdgcn_readfirstlane(tid_ >> 6);
+    const int cb = 2 * (v & 3) + (v >> 2);
+    const frag8* WC = reinterpret_cast<const frag8*>(ws.wc_frag);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) wc[ks] = WC[(cb * 4 + ks) * 64 + lane];
+  };
+  auto phase_L0 = [&](const AsvCriticWeights& ws, const frag8 (&wc)[4], const elem_t* cosb, const float* Fb,
+                      frag8 (&w1f)[8]) {
+    ASVRL_FRESH_LANE();
+    const int v = __builtin_amdgcn_readfirstlane(tid_ >> 6);
+    const int w = v & 3, j = v >> 2, cb = 2 * w + j;
+    const RowA<kNcos> RA_cos = row_base<kNcos, true>(LB, lane, r, h);
+    const RowA<kC> RA_x = row_base<kC, true>(LB, lane, r, h);
+    frag8 cf[4];   // one row block's cos operands at a time (the next block's read behind this one's MFMAs)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) cf[ks] = rowf(cosb, RA_cos, 0, ks);
+#pragma unroll
+    for (int rb = 0; rb < NB; ++rb) {
+      f32x16 acc = acc_init(bcp, cb * 32, h);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) acc = mfma(wc[ks], cf[ks], acc);
+      __builtin_amdgcn_sched_barrier(0);
+      if (rb + 1 < NB) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) cf[ks] = rowf(cosb, RA_cos, rb + 1, ks);
+      } else {   // L1a's fragments, behind the last block's MFMAs
+        const frag8* W1 = reinterpret_cast<const frag8*>(ws.w1_frag);
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) w1f[kk] = W1[(w * 16 + 8 * j + kk) * 64 + lane];
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float fv[8], cv[8], xv[8];
+        lds8(Fb + rb * kC + cb * 32 + 16 * s + 8 * h, fv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) cv[i] = acc[8 * s + i];
+        mul8(fv, cv, xv);
+        rows(L.x, RA_x, rb, 2 * cb + s, relu_packed(pack8(xv)));   // F >= 0: relu of the packed product
+      }
+    }
+  };
+  // L1, first half: block w over k-steps 8j..8j+7 for both row blocks; the partial of row block 1 - j to the
+  // exchange slot, row block j's kept in `keep`
+  auto phase_L1a = [&](const AsvCriticWeights& ws, const frag8 (&w1f)[8], f32x16& keep, frag8 (&w2f)[8]) {
+    ASVRL_FRESH_LANE();
+    const int v = __builtin_amdgcn_readfirstlane(tid_ >> 6);
+    const int w = v & 3, j = v >> 2;
+    const RowA<kC> RA_x = row_base<kC, true>(LB, lane, r, h);
+    f32x16 acc[NB];
+    const f32x16 b0 = acc_init(b1p, w * 32, h);
+#pragma unroll
+    for (int rb = 0; rb < NB; ++rb) acc[rb] = j == 0 ? b0 : f32x16{};
+    // k-steps 8j + kk: the chained image's 16-byte chunk 2 (8j + kk) + h lies 256 j bytes further in the row
+    mfma_rows<8, NB>(acc, L.x + 128 * j, RA_x, [&](int kk) { return w1f[kk]; });
+    {   // L2's fragments, behind the MFMAs
+      const frag8* W2 = reinterpret_cast<const frag8*>(ws.w2_frag);
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) w2f[ks] = W2[(w * 8 + ks) * 64 + lane];
+    }
+    const f32x16 give = j ? acc[0] : acc[1];
+    keep = j ? acc[1] : acc[0];
+    float* dst = xch + ((w * 2 + (1 - j)) * 4) * 256 + lane * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<f32x4*>(dst + q * 256) = f32x4{give[4 * q], give[4 * q + 1], give[4 * q + 2], give[4 * q + 3]};
+  };
+  // L1, second half: + the partner's partial; h1 = relu(.), h1g = h1 G (row block j = sample j); returns h1
+  // (packed) for L3's mask
+  auto phase_L1b = [&](f32x16 keep, const float* Gb, frag8 (&h1k)[2]) {
+    ASVRL_FRESH_LANE();
+    const int v = __builtin_amdgcn_readfirstlane(tid_ >> 6);
+    const int w = v & 3, j = v >> 2;
+    const float* src = xch + ((w * 2 + j) * 4) * 256 + lane * 4;
+    float gv[2][8];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) lds8(Gb + j * kH + w * 32 + 16 * s + 8 * h, gv[s]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 o = *reinterpret_cast<const f32x4*>(src + q * 256);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) keep[4 * q + i] += o[i];
+    }
+    const RowA<kH> RA_a = row_base<kH, true>(LB, lane, r, h);
+    elem_t* const arow = L.a + j * 32 * kH;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float hv[8], gov[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) hv[i] = relu(keep[8 * s + i]);
+      h1k[s] = pack8(hv);
+      mul8(hv, gv[s], gov);
+      rows(arow, RA_a, 0, 2 * w + s, pack8(gov));
+    }
+  };
+  // L2: z2 = W2 h1g + b2 for block w, row block j; partial q over the block's features into qpart; h2 parked in b
+  auto phase_L2 = [&](const frag8 (&w2f)[8], const frag8* W2T, frag8 (&w2tf)[8]) {
+    ASVRL_FRESH_LANE();
+    const int v = __builtin_amdgcn_readfirstlane(tid_ >> 6);
+    const int w = v & 3, j = v >> 2;
+    const RowA<kH> RA_a = row_base<kH, true>(LB, lane, r, h);
+    f32x16 z2[1] = {acc_init(b2p, w * 32, h)};
+    mfma_rows<kH / 16, 1>(z2, L.a + j * 32 * kH, RA_a, [&](int ks) { return w2f[ks]; });
+    if (W2T != nullptr)   // L3's fragments (the update only)
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) w2tf[ks] = W2T[(w * 8 + ks) * 64 + lane];
+    float wov[2][8];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) lds8(wop + w * 32 + 16 * s + 8 * h, wov[s]);
+    float part = 0.f;
+    elem_t* const brow = L.b + j * 32 * kH;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float hv[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float h2 = relu(z2[0][8 * s + i]);
+        part += wov[s][i] * h2;
+        hv[i] = h2;
+      }
+      rows(brow, RA_a, 0, 2 * w + s, pack8(hv));
+    }
+    part = half_sum(part);
+    if (h == 0) L.qpart[w][32 * j + r] = part;
+  };
+
+  // ---------------- the target critic's forward (TQ): q_next of the workgroup's own samples
+  if constexpr (TQ) {
+    load_params(a.tq.w);
+    __syncthreads();
+    frag8 wct[4];
+    load_wc(a.tq.w, wct);
+    for (int t = blockIdx.x; t < a.rounds; t += gridDim.x) {
+      for (int e = threadIdx.x; e < IL::kQn; e += kT8) L.in[0][e] = fetch_tq<IL>(a.tq, t, e);
+      __syncthreads();
+      stage(L.in[0], L.cos[0], L.F[0], L.G[0], true);
+      __syncthreads();
+      frag8 w1f[8], w2f[8], unused[8];
+      phase_L0(a.tq.w, wct, L.cos[0], L.F[0], w1f);
+      f32x16 keep;
+      __syncthreads();
+      phase_L1a(a.tq.w, w1f, keep, w2f);
+      __syncthreads();
+      frag8 h1k[2];
+      phase_L1b(keep, L.G[0], h1k);
+      __syncthreads();
+      phase_L2(w2f, nullptr, unused);
+      __syncthreads();
+      if (threadIdx.x < G) {
+        const int lr = threadIdx.x;
+        a.tq.q[static_cast<int64_t>(t) * G + lr] =
+            (((L.qpart[0][lr] + L.qpart[1][lr]) + L.qpart[2][lr]) + L.qpart[3][lr]) + L.bias[kC + 3 * kH];
+      }
+    }
+    __syncthreads();   // every q_next of the workgroup stored; the LDS is the update's from here
+  }
+
+  // ---------------- the update: local parameters, the first round's inputs, its images
+  load_params(a.w);
+  for (int i = threadIdx.x; i < 8 * kC; i += kT8) L.encacc[i] = 0.f;
+  for (int i = threadIdx.x; i < 3 * 2 * kH; i += kT8) L.aeacc[i] = 0.f;
+  if (blockIdx.x < a.rounds)
+#pragma unroll
+    for (int u = 0; u < kPer8; ++u) {
+      const int e = threadIdx.x + u * kT8;
+      if (e < IL::kSize) L.in[0][e] = fetch_in<NT, S, G, 2>(a, blockIdx.x, e);
+    }
+  __syncthreads();
+  if (blockIdx.x < a.rounds) stage(L.in[0], L.cos[0], L.F[0], L.G[0], false);
+  __syncthreads();
+
+  f32x16 dW2[2], dW1[4], dWc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) dW2[i] = dWc[i] = f32x16{};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dW1[i] = f32x16{};
+  float db2 = 0.f, db1 = 0.f, dbc = 0.f, dbo = 0.f, dwo1 = 0.f;
+  frag8 wcr[4];   // cos block cb's Wc fragments (L0; reloaded in each round's dW1 phase for L4 and the next L0)
+  load_wc(a.w, wcr);
+  int buf = 0;
+  for (int t = blockIdx.x; t < a.rounds; t += gridDim.x, buf ^= 1) {
+    float pre[kPer8];
+    int tid_p = threadIdx.x;
+    asm volatile("" : "+v"(tid_p));
+    float* const in = L.in[buf];
+    const int row0 = t * G, b0 = row0 / NT;
+    (void)b0;
+    elem_t* const cosb = L.cos[buf];
+    float* const Fb = L.F[buf];
+    float* const Gb = L.G[buf];
+
+    frag8 w1f[8], w2f[8], w2tf[8];
+    phase_L0(a.w, wcr, cosb, Fb, w1f);
+    __syncthreads();
+    f32x16 keep;
+    phase_L1a(a.w, w1f, keep, w2f);
+    // the next round's inputs into registers (stored to LDS before the dW1 phase stages them)
+#pragma unroll
+    for (int u = 0; u < kPer8; ++u) {
+      const int e = tid_p + u * kT8;
+      pre[u] = (t + static_cast<int>(gridDim.x) < a.rounds && e < IL::kSize)
+                   ? fetch_in<NT, S, G, 2>(a, t + gridDim.x, e) : 0.f;
+    }
+    __syncthreads();
+    frag8 h1k[2];
+    phase_L1b(keep, Gb, h1k);
+    __syncthreads();
+    phase_L2(w2f, nullptr, w2tf);
+    __syncthreads();
+
+    // ---------------- loss (waves 0-3): q = sum of the four partials + bo; quantile-Huber -> dq
+    {
+      ASVRL_FRESH_LANE();
+      const int v = __builtin_amdgcn_readfirstlane(tid_ >> 6);
+      if (v < 4) {
+        const int q4 = lane >> 4;
+        const int g = v;
+        const int lr = 16 * g + (lane & 15), grow = row0 + lr, bl = lr / NT;
+        const float bo = L.bias[kC + 3 * kH];
+        const float q = (((L.qpart[0][lr] + L.qpart[1][lr]) + L.qpart[2][lr]) + L.qpart[3][lr]) + bo;
+        float wl;
+        const float dq = quarter_loss_dq<NT>(a, in + IL::kQn + bl * NT, in[IL::kTau + lr], q, q4, &wl);
+        if (a.tile_loss != nullptr) {
+          const float sv = seg_sum<16>(wl);
+          if (lane == 0) L.tsum[g] = sv;
+        }
+        if (q4 == 0) {
+          L.dq[lr] = dq;
+          if (a.row_loss != nullptr) a.row_loss[grow] = wl;
+          if (a.q != nullptr) a.q[grow] = q;
+          dbo += dq;
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---------------- dz2 = dq wo 1[h2 > 0] (block w, row block j, in place over h2); the output layer's gradient
+    // sum dq h2 over the row block
+    if (a.tile_loss != nullptr && threadIdx.x < G / 32)
+      a.tile_loss[row0 / 32 + threadIdx.x] = (L.tsum[2 * threadIdx.x] + L.tsum[2 * threadIdx.x + 1]) * a.loss_scale;
+    {
+      ASVRL_FRESH_LANE();
+      const int v = __builtin_amdgcn_readfirstlane(tid_ >> 6);
+      const int w = v & 3, j = v >> 2;
+      {   // L3's fragments, one phase ahead
+        const frag8* W2T = reinterpret_cast<const frag8*>(a.w.w2t_frag);
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) w2tf[ks] = W2T[(w * 8 + ks) * 64 + lane];
+      }
+      const RowA<kH> RA_b = row_base<kH, true>(LB, lane, r, h);
+      elem_t* const brow = L.b + j * 32 * kH;
+      float wov[2][8];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) lds8(wop + w * 32 + 16 * s + 8 * h, wov[s]);
+      const float dqv = L.dq[32 * j + r];
+      frag8 hv[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) hv[s] = rowf(brow, RA_b, 0, 2 * w + s);
+      float pr[16];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float dz[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          dz[i] = dqv * wov[s][i];
+          pr[8 * s + i] = dqv * static_cast<float>(hv[s][i]);
+        }
+        rows(brow, RA_b, 0, 2 * w + s, mask_pos(pack8(dz), hv[s]));   // dq wo 1[h2 > 0]
+      }
+      half_rows_sum16(pr, lane);
+      dwo1 += pr[0];
+    }
+    __syncthreads();
+
+    // ---------------- L3: dh1g = W2^T dz2 (block w, row block j) -> dz1, dG;  dW2[own][2j, 2j+1] += dz2^T h1g
+    {
+      ASVRL_FRESH_LANE();
+      const int v = __builtin_amdgcn_readfirstlane(tid_ >> 6);
+      const int w = v & 3, j = v >> 2;
+      const RowA<kH> RA = row_base<kH, true>(LB, lane, r, h);
+      float gv[2][8];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) lds8(Gb + j * kH + w * 32 + 16 * s + 8 * h, gv[s]);
+      f32x16 acc[1] = {f32x16{}};
+      mfma_rows<kH / 16, 1>(acc, L.b + j * 32 * kH, RA, [&](int ks) { return w2tf[ks]; });
+      pin(h1k[0]);
+      pin(h1k[1]);
+      float gsa[16];
+      elem_t* const drow = L.dz1 + j * 32 * kH;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float h1[8], d[8], dg[8], hd[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          h1[i] = static_cast<float>(h1k[s][i]);
+          d[i] = acc[0][8 * s + i];
+        }
+        mul8(d, gv[s], dg);
+        mul8(d, h1, hd);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) gsa[8 * s + i] = hd[i];
+        rows(drow, RA, 0, 2 * w + s, mask_pos(pack8(dg), h1k[s]));   // dz1 = dh1g G 1[h1 > 0]
+      }
+      // dG of sample j = sum over its 32 taus of dh1g h1 -> dzG = dG 1[G > 0], in place over G's block w
+      half_rows_sum16(gsa, lane);
+      if (r < 16) {
+        const int p = w * 32 + 16 * (r >> 3) + 8 * h + (r & 7);
+        const float gm = Gb[j * kH + p];
+        Gb[j * kH + p] = gm > 0.f ? gsa[0] : 0.f;
+      }
+      // action_encoder's gradient (AC_IQN_model.py:468-470): lanes of half 0 (feature 32 w + r) sum
+      // dzG[j] * (a_j0, a_j1, 1) into sample j's slot
+      if (h == 0) {
+        const int p = w * 32 + r, m = swap23(p);
+        const float d = Gb[j * kH + p];
+        float* acc2 = L.aeacc + j * kH + m;
+        acc2[0] += d * in[IL::kAct + 2 * j];
+        acc2[2 * kH] += d * in[IL::kAct + 2 * j + 1];
+        acc2[4 * kH] += d;
+      }
+      // dW2[own][2j, 2j+1] += dz2^T h1g (after L3: its fragments and h1 are dead by now)
+      const TrA<kH> TA = tr_base<kH, true>(LB, lane);
+      mfma_grid<G / 16, 2>([&](int kk) { return trf(L.b, TA, kk, w); },
+                           [&](int kk, int n) { return trf(L.a, TA, kk, 2 * j + n); },
+                           [&](int kk, int n, const frag8& A, const frag8& B) {
+                             if (n == 0 && j == 0) db2 += sum8(A);
+                             mfma_acc(dW2[n], A, B);
+                           });
+    }
+#pragma unroll
+    for (int u = 0; u < kPer8; ++u) {
+      const int e = tid_p + u * kT8;
+      if (e < IL::kSize) L.in[buf ^ 1][e] = pre[u];
+    }
+    __syncthreads();
+
+    frag8 wt[8];
+    // ---------------- dW1[own][4j .. 4j+3] += dz1^T x; the next round's images staged; L4: dx = W1^T dz1 for cos
+    // block cb, c recomputed -> dF, dzc; the encoders' sums; dWc[cb] += dzc^T cos
+    {
+      ASVRL_FRESH_LANE();
+      const int v = __builtin_amdgcn_readfirstlane(tid_ >> 6);
+      const int w = v & 3, j = v >> 2;
+      const TrA<kH> TA_d = tr_base<kH, true>(LB, lane);
+      const TrA<kC> TA_x = tr_base<kC, true>(LB, lane);
+      mfma_grid<G / 16, 4>([&](int kk) { return trf(L.dz1, TA_d, kk, w); },
+                           [&](int kk, int n) { return trf(L.x, TA_x, kk, 4 * j + n); },
+                           [&](int kk, int n, const frag8& A, const frag8& B) {
+                             if (n == 0 && j == 0) db1 += sum8(A);
+                             mfma_acc(dW1[n], A, B);
+                           });
+      // L4's W1^T fragments for cos block cb, in flight while the next round's images are staged
+      const frag8* W1T = reinterpret_cast<const frag8*>(a.w.w1t_frag);
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) wt[ks] = W1T[((2 * w + j) * 8 + ks) * 64 + lane];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      const int tn = t + static_cast<int>(gridDim.x);
+      if (tn < a.rounds) stage(L.in[buf ^ 1], L.cos[buf ^ 1], L.F[buf ^ 1], L.G[buf ^ 1], false);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      ASVRL_FRESH_LANE();
+      const int v = __builtin_amdgcn_readfirstlane(tid_ >> 6);
+      const int w = v & 3, j = v >> 2, cb = 2 * w + j;
+      {   // cos block cb's Wc fragments: first used after the 16 dx MFMAs below
+        const frag8* WC = reinterpret_cast<const frag8*>(a.w.wc_frag);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) wcr[ks] = WC[(cb * 4 + ks) * 64 + lane];
+      }
+      const RowA<kNcos> RA_cos = row_base<kNcos, true>(LB, lane, r, h);
+      const RowA<kH> RA_d = row_base<kH, true>(LB, lane, r, h);
+      elem_t* const dzc_w = L.dzc[w];
+      // dx of both row blocks first (the W1^T fragments then die), then per row block c and the epilogue
+      f32x16 dxs[NB];
+#pragma unroll
+      for (int rb = 0; rb < NB; ++rb) dxs[rb] = f32x16{};
+      mfma_rows<8, NB>(dxs, L.dz1, RA_d, [&](int ks) { return wt[ks]; });
+#pragma unroll
+      for (int rb = 0; rb < NB; ++rb) {
+        f32x16 cc[1] = {acc_init(bcp, cb * 32, h)};
+        mfma_rows<4, 1>(cc, cosb + rb * 32 * kNcos, RA_cos, [&](int ks) { return wcr[ks]; });
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          float fv[8], cv[8], d[8], fs[8], df[8], dz[8];
+          lds8(Fb + rb * kC + cb * 32 + 16 * s + 8 * h, fv);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            cv[i] = relu(cc[0][8 * s + i]);
+            d[i] = dxs[rb][8 * s + i];
+          }
+          mul8(d, cv, fs);
+          mul8(d, fv, df);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) dz[i] = cv[i] > 0.f ? df[i] : 0.f;
+          rows(dzc_w, RA_cos, rb, 2 * j + s, pack8(dz));   // dzc = dx F 1[c > 0], this wave's half of image w
+          // dF of sample rb = sum over its taus of dx c -> dzF = dF 1[F > 0], in place over F's block cb (the
+          // positions this wave's half h holds: 16 s + 8 h + i)
+          half_rows_sum8(fs, lane);
+          if (r < 8) {
+            const int p = cb * 32 + 16 * s + 8 * h + r;
+            const float fm = Fb[rb * kC + p];
+            Fb[rb * kC + p] = fm > 0.f ? fs[0] : 0.f;
+          }
+        }
+      }
+      // the observation encoders' gradients (AC_IQN_model.py:284-308): lane (h, r) takes feature
+      // m = swap23(32 cb + r) of sample h; the two samples' sums added in sample order (half_sum)
+      {
+        const int p = cb * 32 + r, m = swap23(p);
+        const bool self = m < kSelfF;
+        const int off = self ? 0 : kSelfIn + kObjIn * ((m - kSelfF) / kObjF);
+        const float d = Fb[h * kC + p];
+        const float* x = in + IL::kObs + h * kObsIn + off;
+        float e8[8];
+#pragma unroll
+        for (int i = 0; i < kSelfIn; ++i) e8[i] = half_sum(d * ((self || i < kObjIn) ? x[i] : 0.f));
+        e8[7] = half_sum(d);
+        if (h == 0)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) L.encacc[i * kC + m] += e8[i];
+      }
+      const TrA<kNcos> TA_c = tr_base<kNcos, true>(LB, lane);
+#pragma unroll
+      for (int kk = 0; kk < G / 16; ++kk) {
+        const frag8 A = trf(dzc_w, TA_c, kk, j);
+        dbc += sum8(A);
+#pragma unroll
+        for (int n = 0; n < 2; ++n) mfma_acc(dWc[n], A, trf(cosb, TA_c, kk, n));
+      }
+      // the next round's L0 fragments (the same Wc; not held through L1 .. L3)
+      const frag8* WC = reinterpret_cast<const frag8*>(a.w.wc_frag);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) wcr[ks] = WC[(cb * 4 + ks) * 64 + lane];
+    }
+    __syncthreads();   // the next round overwrites x, a, b, dz1, the exchange slots and dzc
+  }
+
+  // ---------------- the workgroup's partials
+  mfma_drain();
+  const int lane = threadIdx.x & 63, v = threadIdx.x >> 6, w = v & 3, j = v >> 2, h = lane >> 5, r = lane & 31;
+  const int grp = blockIdx.x;
+  if (a.parts.enc != nullptr) {
+    const float* ea = L.encacc;
+    float* pe = a.parts.enc + static_cast<size_t>(grp) * 688;
+    for (int i = threadIdx.x; i < 688; i += kT8) {
+      float val;
+      if (i < kSelfF * kSelfIn) val = ea[(i % kSelfIn) * kC + i / kSelfIn];
+      else if (i < kSelfF * (kSelfIn + 1)) val = ea[7 * kC + i - kSelfF * kSelfIn];
+      else {
+        const int e = i - kSelfF * (kSelfIn + 1);
+        const int jf = e < kObjF * kObjIn ? e / kObjIn : e - kObjF * kObjIn;
+        const int slot = e < kObjF * kObjIn ? e % kObjIn : 7;
+        val = 0.f;
+#pragma unroll
+        for (int o = 0; o < 5; ++o) val += ea[slot * kC + kSelfF + kObjF * o + jf];
+      }
+      pe[i] = val;
+    }
+  }
+  if (a.parts.aenc != nullptr) {
+    float* pa = a.parts.aenc + static_cast<size_t>(grp) * (3 * kH);
+    for (int i = threadIdx.x; i < 3 * kH; i += kT8) {
+      const int m = i < 2 * kH ? i / 2 : i - 2 * kH, c = i < 2 * kH ? i % 2 : 2;
+      pa[i] = L.aeacc[(2 * c) * kH + m] + L.aeacc[(2 * c + 1) * kH + m];
+    }
+  }
+  float* p2 = a.parts.hidden2 + static_cast<size_t>(grp) * (kH * kH + kH);
+  float* p1 = a.parts.hidden + static_cast<size_t>(grp) * (kH * kC + kH);
+  float* pc = a.parts.cos_emb + static_cast<size_t>(grp) * (kC * kNcos + kC);
+  const int cb = 2 * w + j;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const int m = (g & 3) + 8 * (g >> 2) + 4 * h;   // MFMA C row of register g
+    const int f2 = swap23(w * 32 + m);
+#pragma unroll
+    for (int n = 0; n < 2; ++n) p2[f2 * kH + swap23(32 * (2 * j + n) + r)] = dW2[n][g];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) p1[f2 * kC + swap23(32 * (4 * j + n) + r)] = dW1[n][g];
+    const int fc = swap23(cb * 32 + m);
+#pragma unroll
+    for (int n = 0; n < 2; ++n) pc[fc * kNcos + 32 * n + r] = dWc[n][g];
+  }
+  dbc = half_sum(dbc);
+  db2 = half_sum(db2);
+  db1 = half_sum(db1);
+  if (h == 0) {
+    if (j == 0) {
+      p2[kH * kH + swap23(w * 32 + r)] = db2;
+      p1[kH * kC + swap23(w * 32 + r)] = db1;
+    }
+    pc[kC * kNcos + swap23(cb * 32 + r)] = dbc;
+  }
+  // the output layer: each half's row sums per feature position, then the two halves in order; bo from waves 0-3
+  if (r < 16) red8[j][w * 32 + 16 * (r >> 3) + 8 * h + (r & 7)] = dwo1;
+  dbo = seg_sum<32>(h == 0 ? dbo : 0.f);
+  if (lane == 31 && v < 4) L.red[v] = dbo;
+  __syncthreads();
+  float* po = a.parts.out + static_cast<size_t>(grp) * (kH + 1);
+  if (threadIdx.x < kH) po[swap23(threadIdx.x)] = red8[0][threadIdx.x] + red8[1][threadIdx.x];
+  if (threadIdx.x == 0) po[kH] = ((L.red[0] + L.red[1]) + L.red[2]) + L.red[3];
+}
+#endif  // !ASVRL_OPERAND_F32
+
 int fused_nb(int N) {
 #if ASVRL_OPERAND_F32
   (void)N;
@@ -1501,6 +2179,10 @@ extern "C" int32_t asvrl_critic_fused_groups(int32_t B, int32_t N) {
 }
 
 namespace {
+// which kernel asvrl_critic_train_fused(_tq) launches where both take the shape: 8 (default) critic_fused8_kernel,
+// 4 critic_fused_kernel (asvrl_critic_fused_variant; the A/B and the kernel-vs-kernel tests)
+int g_fused_variant = 4;
+
 int critic_train_fused_launch(const AsvCriticWeights* w, const AsvCriticIO* io, const AsvCriticParts* parts,
                               const AsvCriticWeights* tw, const AsvCriticIO* tio, void* stream) {
   ASVRL_REQUIRE(w && io && parts, "asvrl_critic_train_fused: null argument");
@@ -1548,6 +2230,15 @@ int critic_train_fused_launch(const AsvCriticWeights* w, const AsvCriticIO* io, 
   }
   const int grid = asvrl_critic_fused_groups(io->B, io->N);
   hipStream_t st = as_stream(stream);
+#if !ASVRL_OPERAND_F32
+  // the two-waves-per-SIMD kernel wherever it takes the shape (AC-IQN N = 32, encoders in the launch)
+  if (g_fused_variant == 8 && io->N == 32 && parts->enc != nullptr && parts->aenc != nullptr && io->dzF == nullptr &&
+      io->dzG == nullptr && io->xb == nullptr) {
+    if (tq) hipLaunchKernelGGL((critic_fused8_kernel<true>), dim3(grid), dim3(kT8), 0, st, a);
+    else hipLaunchKernelGGL((critic_fused8_kernel<false>), dim3(grid), dim3(kT8), 0, st, a);
+    return check_launch(tq ? "asvrl_critic_train_fused_tq" : "asvrl_critic_train_fused");
+  }
+#endif
   if (tq) {
     if (io->N == 32) hipLaunchKernelGGL((critic_fused_kernel<32, false, true>), dim3(grid), dim3(kNW * 64), 0, st, a);
     else if (io->N == 16) hipLaunchKernelGGL((critic_fused_kernel<16, false, true>), dim3(grid), dim3(kNW * 64), 0, st, a);
@@ -1614,4 +2305,18 @@ extern "C" int asvrl_iqn_train_fused(const AsvCriticWeights* w, const AsvIqnHead
   else if (io->N == 16) hipLaunchKernelGGL((critic_fused_kernel<16, true>), dim3(grid), dim3(kNW * 64), 0, st, a);
   else hipLaunchKernelGGL((critic_fused_kernel<8, true>), dim3(grid), dim3(kNW * 64), 0, st, a);
   return check_launch("asvrl_iqn_train_fused");
+}
+
+// The AC-IQN critic update's kernel where both forms take the shape (N = 32, encoders' gradients in the launch,
+// bf16 build): 8 = critic_fused8_kernel (two waves per SIMD, the default), 4 = critic_fused_kernel (one wave per
+// SIMD). v < 0 only queries. Returns the previous setting; anything else is an error (-1).
+extern "C" int32_t asvrl_critic_fused_variant(int32_t v) {
+  const int prev = g_fused_variant;
+  if (v < 0) return prev;
+  if (v != 4 && v != 8) {
+    set_error("asvrl_critic_fused_variant: variant must be 4 or 8");
+    return -1;
+  }
+  g_fused_variant = v;
+  return prev;
 }

@@ -203,6 +203,24 @@ def critic_train(pack, F, G, taus, q_targets, bufs, kappa=1.0, stream=None, q_ne
     return bufs.row_loss.sum() / float(B * Np)
 
 
+class fused_variant:
+    """Context manager (or plain call) selecting asvrl_critic_train_fused(_tq)'s kernel where both forms take the
+    shape (ABI 23, asvrl_critic_fused_variant): 8 = two waves per SIMD (the default), 4 = the one-wave-per-SIMD
+    kernel of round 5 (the A/B and the bit-identity tests that pin that kernel). Process-wide, bf16 build."""
+
+    def __init__(self, v, operands="bf16"):
+        self.L = _abi.lib(operands)
+        self.prev = int(self.L.asvrl_critic_fused_variant(int(v)))
+        _abi.check(0 if self.prev >= 0 else -1, "asvrl_critic_fused_variant", self.L)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.L.asvrl_critic_fused_variant(self.prev)
+        return False
+
+
 def fused_groups(pack, B, N):
     """Workgroups (= partial groups) of critic_train_fused; 0 when the shape is unsupported."""
     return int(pack.L.asvrl_critic_fused_groups(B, N))

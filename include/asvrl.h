@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 22
+#define ASVRL_ABI_VERSION 23
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -365,10 +365,19 @@ int asvrl_critic_train_fused(const AsvCriticWeights* w, const AsvCriticIO* io, c
 /* asvrl_critic_train_fused with the target critic's forward in the same launch (ABI 20; replaces the
  * separate asvrl_critic_forward(target) of train_AC_IQN, agent.py:396-400): each workgroup first computes
  * q_next = Critic_target(tio->obs, tio->act, tio->taus) (AC_IQN_model.py:462-480) for exactly the samples
- * its rounds update -- the values asvrl_critic_forward(tw, tio) gives, bit for bit -- into io->q_next,
- * then runs the update reading them. tw: the target critic (with its encoders); tio: B and N as io. */
+ * its rounds update into io->q_next, then runs the update reading them. tw: the target critic (with its
+ * encoders); tio: B and N as io. With kernel variant 4 (asvrl_critic_fused_variant) the target pass is
+ * asvrl_critic_forward's own tile: q_next bit for bit what asvrl_critic_forward(tw, tio) gives; with variant 8
+ * (the default where it applies) it is the update kernel's own forward phases: the same rounding points, f32 sums
+ * in another order. */
 int asvrl_critic_train_fused_tq(const AsvCriticWeights* w, const AsvCriticIO* io, const AsvCriticParts* parts,
                                 const AsvCriticWeights* tw, const AsvCriticIO* tio, void* stream);
+
+/* ABI 23: the kernel asvrl_critic_train_fused(_tq) launch where both forms take the shape (bf16 build, N = 32,
+ * parts->enc and parts->aenc set, no dzF / dzG / xb): 8 = two waves per SIMD (512-thread workgroups; the
+ * default), 4 = one wave per SIMD (the round-5 kernel). Results agree within f32 summation order, not bit for bit.
+ * v < 0 only queries; returns the previous setting, or -1 (asvrl_last_error) for any other v. Process-wide. */
+int32_t asvrl_critic_fused_variant(int32_t v);
 
 /* Actor update's critic pass (agent.py:419-425): forward, then the backward of
  * sum_rows dq * q to G (dG) and through the action encoder to the action (dA). */

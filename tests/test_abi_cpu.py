@@ -51,3 +51,21 @@ def test_errors_are_reported_not_raised():
     rc = L.asvrl_c51_project(None, None, None, None, 4, 51, -1.0, 1.0, 0.04, 0.97, None, None)
     assert rc != 0
     assert b"null" in L.asvrl_last_error()
+
+
+def test_fused_variant_switch_host_side():
+    """asvrl_critic_fused_variant (ABI 23) is host state only: query, set, restore; anything but 4 / 8 is refused
+    with a message and leaves the setting alone."""
+    from distributional_rl_decision_and_control_amd import _abi
+    from distributional_rl_decision_and_control_amd.fused_critic import fused_variant
+    L = _abi.lib()
+    default = L.asvrl_critic_fused_variant(-1)
+    assert default in (4, 8)
+    with fused_variant(4):
+        assert L.asvrl_critic_fused_variant(-1) == 4
+    assert L.asvrl_critic_fused_variant(-1) == default
+    assert L.asvrl_critic_fused_variant(5) == -1
+    assert b"variant" in L.asvrl_last_error()
+    assert L.asvrl_critic_fused_variant(-1) == default
+    with pytest.raises(_abi.AsvrlError):
+        fused_variant(6)

@@ -1,0 +1,95 @@
+"""GPU: critic_fused8_kernel -- asvrl_critic_train_fused(_tq) at two waves per SIMD (kernel variant 8, ABI 23, the
+default at the bench shape) -- against the one-wave-per-SIMD kernel of round 5 (variant 4) on the same batches,
+and its in-launch target pass against asvrl_critic_forward.
+
+Both kernels form the same bf16 rounding points (oracle/learn_ref.critic_step_bf16 pins each: the launch the bench
+times is tests/test_critic_bf16_oracle_gpu.py's subject); they sum in f32 in different orders (variant 8 adds L1's
+two K halves and sums the per-sample and bias reductions per round), so they agree within f32 rounding carried
+through the bf16 rounding points, not bit for bit. Bars: loss within 1e-5 rel.; every gradient tensor within 4e-4 of
+its scale element-wise and 2e-4 in relative L2 (twice the oracle test's bars: each kernel is within those of the
+restatement); q_next of the in-launch target pass within 1e-4 of its scale of asvrl_critic_forward's. Cases: the
+bench shape (B = 4096: 2048 rounds over 256 workgroups) and B = 608 (304 rounds: some workgroups take one round
+more), with and without the target pass inside. Variant 8 is deterministic (bit-identical reruns).
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests.test_critic_fused_gpu import _batch, _critic_grads
+
+pytestmark = pytest.mark.gpu
+
+ELEM, L2, LOSS, QB = 4e-4, 2e-4, 1e-5, 1e-4
+
+
+def _run(variant, B, tq, seed):
+    from distributional_rl_decision_and_control_amd.fused_critic import fused_variant
+    rows, _ = _batch(B, seed)
+    taus = torch.rand(2, B, 32, generator=torch.Generator(device="cuda").manual_seed(seed + 1), device="cuda")
+    out = {}
+    with fused_variant(variant):
+        g, l = _critic_grads("bf16", B, 32, True, rows, taus, enc=True, tq=tq, out=out)
+    return g, l, out["q_next"]
+
+
+@pytest.mark.parametrize("B", [608, 1024, 1536, 4096])
+@pytest.mark.parametrize("tq", [False, True], ids=["separate_target", "tq_launch"])
+def test_two_wave_kernel_matches_one_wave_kernel(B, tq):
+    g8, l8, q8 = _run(8, B, tq, 31)
+    g4, l4, q4 = _run(4, B, tq, 31)
+    qerr = float(np.abs(q8 - q4).max() / (np.abs(q4).max() + 1e-30))
+    print(f"B={B} tq={tq}: q_next max err / scale {qerr:.2e}; loss {l8:.8f} vs {l4:.8f}")
+    assert np.isfinite(q8).all() and qerr < QB, qerr
+    np.testing.assert_allclose(l8, l4, rtol=LOSS)
+    bad = []
+    for n in g4:
+        scale = np.abs(g4[n]).max() + 1e-30
+        err = float(np.abs(g8[n] - g4[n]).max() / scale)
+        l2 = float(np.linalg.norm(g8[n] - g4[n]) / (np.linalg.norm(g4[n]) + 1e-30))
+        print(f"  {n:28s} err/scale {err:.2e}  L2 {l2:.2e}")
+        if not (err < ELEM and l2 < L2):
+            bad.append((n, err, l2))
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("tq", [False, True], ids=["separate_target", "tq_launch"])
+def test_two_wave_kernel_deterministic(tq):
+    g1, l1, q1 = _run(8, 1024, tq, 41)
+    g2, l2, q2 = _run(8, 1024, tq, 41)
+    assert l1 == l2
+    np.testing.assert_array_equal(q1, q2)
+    for n in g1:
+        np.testing.assert_array_equal(g1[n], g2[n], err_msg=n)
+
+
+@pytest.mark.parametrize("B", [64, 608, 4096])
+def test_two_wave_target_pass_matches_forward_launch(B):
+    """The in-launch target pass of variant 8 (the update's own L0 / L1 / L2 phases on the target weights) against
+    asvrl_critic_forward (critic_kernel<FWD>) on the same next states, next actions and taus."""
+    from distributional_rl_decision_and_control_amd.agent import Agent
+    from distributional_rl_decision_and_control_amd.fused_critic import critic_forward, critic_train_fused, fused_variant
+    from distributional_rl_decision_and_control_amd.fused_update import FusedACIQNState, target_q
+    from distributional_rl_decision_and_control_amd.learner import FusedAdam
+    rows, _ = _batch(B, 9)
+    taus = torch.rand(B, 32, generator=torch.Generator(device="cuda").manual_seed(B), device="cuda")
+    ag = Agent(seed=3, agent_type="AC-IQN")
+    FusedAdam(ag.policy_local.actor.parameters(), lr=1e-4)
+    FusedAdam(ag.policy_local.critic.parameters(), lr=1e-4)
+    with torch.no_grad():   # a target distinct from the local critic
+        g = torch.Generator().manual_seed(5)
+        for v in ag.policy_target.critic.parameters():
+            v.add_((0.05 * float(v.abs().mean()) * torch.randn(v.shape, generator=g)).to(v.device))
+    st = FusedACIQNState(ag.policy_local, ag.policy_target, B, 32)
+    target_q(st, rows, taus, st.q_next, st.na)
+    q2 = critic_forward(st.target_trunk, None, None, taus, 32, obs=rows[:, 40:80], act=st.na)
+    q1 = torch.full_like(st.q_next, float("nan"))
+    with fused_variant(8):
+        critic_train_fused(st.local_trunk, ag.policy_local.critic, taus, 32, q1.view(B, 32), rows[:, 82], rows[:, 83],
+                           0.99, rows[:, 0:40], rows[:, 80:82], st.arena, tile_loss=st.tile_loss[0], encoders=True,
+                           target=(st.target_trunk, taus, rows[:, 40:80], st.na))
+    torch.cuda.synchronize()
+    q1 = q1.view(B, 32)
+    assert torch.isfinite(q1).all()
+    err = float((q1 - q2).abs().max() / q2.abs().max())
+    print(f"B={B}: in-launch target pass vs asvrl_critic_forward max err / scale {err:.2e}")
+    assert err < QB, err

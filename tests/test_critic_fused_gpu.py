@@ -178,11 +178,15 @@ def test_fused_encoder_grads_in_kernel(ops, B, N):
     f64 autograd). f32: 2e-5 of scale; bf16: cosine > 0.999, norm within 1 % (the out-of-kernel path
     rounds dzF and the inputs to bf16, the in-kernel one keeps them f32). Every other gradient and the
     loss are unchanged bit for bit; the launch stays deterministic."""
+    from distributional_rl_decision_and_control_amd.fused_critic import fused_variant
     rows, _ = _batch(B, 11 + N)
     g = torch.Generator(device="cuda").manual_seed(17 + B)
     taus = torch.rand(2, B, N, generator=g, device="cuda")
-    ge, le = _critic_grads(ops, B, N, True, rows, taus, enc=True)
-    gf, lf = _critic_grads(ops, B, N, True, rows, taus)
+    # the one-wave-per-SIMD kernel for both forms (the per-sample dzF / dzG form has no two-wave variant, and the
+    # bit-identity below is between two forms of ONE kernel); variant 8: tests/test_critic_fused8_gpu.py
+    with fused_variant(4, ops):
+        ge, le = _critic_grads(ops, B, N, True, rows, taus, enc=True)
+        gf, lf = _critic_grads(ops, B, N, True, rows, taus)
     assert le == lf
     enc_names = [n for n in gf if "encoder" in n]
     assert len(enc_names) == 6
@@ -199,7 +203,8 @@ def test_fused_encoder_grads_in_kernel(ops, B, N):
             c = _cos(ge[n], gf[n])
             ratio = np.linalg.norm(ge[n]) / np.linalg.norm(gf[n])
             assert c > 0.999 and abs(ratio - 1) < 1e-2, (n, c, ratio)
-    g2, _ = _critic_grads(ops, B, N, True, rows, taus, enc=True)
+    with fused_variant(4, ops):
+        g2, _ = _critic_grads(ops, B, N, True, rows, taus, enc=True)
     for n in enc_names:
         np.testing.assert_array_equal(ge[n], g2[n], err_msg=n)
 
@@ -207,17 +212,19 @@ def test_fused_encoder_grads_in_kernel(ops, B, N):
 @pytest.mark.parametrize("ops,B,N", [("f32", 64, 8), ("f32", 64, 32), ("f32", 256, 16),
                                      ("bf16", 64, 8), ("bf16", 128, 16), ("bf16", 608, 32), ("bf16", 4096, 32)])
 def test_fused_train_with_target_critic_in_launch(ops, B, N):
-    """asvrl_critic_train_fused_tq (ABI 20): each workgroup computes q_next = target_critic(s', a', tau') for
+    """asvrl_critic_train_fused_tq (ABI 20), kernel variant 4: each workgroup computes q_next = target_critic(s', a', tau') for
     the samples its rounds update (asvrl_critic.hip's FWD tile, compiled into the fused launch ahead of the
     contraction pragma), then runs the update. Against asvrl_critic_forward followed by the plain fused launch:
     q_next bit-identical (every sample: 608 x 32 gives 304 rounds over 256 workgroups, uneven), and so every
     gradient and the loss bit-identical too."""
+    from distributional_rl_decision_and_control_amd.fused_critic import fused_variant
     rows, _ = _batch(B, 21 + N)
     g = torch.Generator(device="cuda").manual_seed(27 + B)
     taus = torch.rand(2, B, N, generator=g, device="cuda")
     o1, o2 = {}, {}
-    g1, l1 = _critic_grads(ops, B, N, True, rows, taus, enc=True, out=o1)
-    g2, l2 = _critic_grads(ops, B, N, True, rows, taus, enc=True, tq=True, out=o2)
+    with fused_variant(4, ops):   # this kernel's target pass is asvrl_critic_forward's tile (variant 8: test_critic_fused8_gpu)
+        g1, l1 = _critic_grads(ops, B, N, True, rows, taus, enc=True, out=o1)
+        g2, l2 = _critic_grads(ops, B, N, True, rows, taus, enc=True, tq=True, out=o2)
     assert np.isfinite(o2["q_next"]).all()
     np.testing.assert_array_equal(o2["q_next"], o1["q_next"])
     assert l1 == l2

@@ -67,7 +67,7 @@ def test_fused_forward(B, N):
 @pytest.mark.parametrize("B", [1, 37, 4096])
 def test_forward_launch_matches_in_launch_target_pass(B):
     """asvrl_critic_forward (critic_kernel<FWD>) against the fused launch's in-launch target pass
-    (asvrl_critic_train_fused_tq, the same FWD tile compiled into the other file, its q_next written for the
+    (asvrl_critic_train_fused_tq with kernel variant 4: the same FWD tile compiled into the other file, its q_next written for the
     fused shape's rows): every row bit-identical, B = 1 and 37 (a partial launch) and 4096. (Round 4 also
     measured a two-tiles-per-wave FWD kernel, one wave per SIMD, against this one: 36 vs 26 us, dropped,
     profiles/r04u_fwd_two_tiles_ab.txt.)"""
@@ -88,10 +88,12 @@ def test_forward_launch_matches_in_launch_target_pass(B):
                         act=st.na[:B])
     # the one-tile code path: the fused launch's target pass
     from distributional_rl_decision_and_control_amd.fused_critic import critic_train_fused
+    from distributional_rl_decision_and_control_amd.fused_critic import fused_variant
     q1 = torch.full_like(st.q_next, float("nan"))
-    critic_train_fused(st.local_trunk, ag.policy_local.critic, taus, 32, q1.view(Bp, 32), rows[:, 82], rows[:, 83],
-                       0.99, rows[:, 0:40], rows[:, 80:82], st.arena, tile_loss=st.tile_loss[0], encoders=True,
-                       target=(st.target_trunk, taus, rows[:, 40:80], st.na))
+    with fused_variant(4):   # the kernel whose target pass IS this tile (variant 8: tests/test_critic_fused8_gpu.py)
+        critic_train_fused(st.local_trunk, ag.policy_local.critic, taus, 32, q1.view(Bp, 32), rows[:, 82], rows[:, 83],
+                           0.99, rows[:, 0:40], rows[:, 80:82], st.arena, tile_loss=st.tile_loss[0], encoders=True,
+                           target=(st.target_trunk, taus, rows[:, 40:80], st.na))
     torch.cuda.synchronize()
     assert torch.isfinite(q2).all()
     assert torch.equal(q2.reshape(-1), q1.view(Bp, 32)[:B].reshape(-1))
