@@ -61,13 +61,9 @@ namespace {
 
 constexpr int kC = 256, kH = 128, kNcos = 64, kNW = 4, kMaxA = ASVRL_IQN_MAX_ACTIONS;
 
-// where a round issues the global loads of the next round's inputs: 1 (default) behind the W2 fragment
-// fetch in L1, so the wait for the weight fragments fetched before it never includes these loads
-// (127-129 vs 130 us per launch, stage phase 3.7k -> 3.1k cycles: profiles/r02_enc_ab.txt); 0 at the
-// top of the round
-#ifndef ASVRL_PRE_AT
-#define ASVRL_PRE_AT 1
-#endif
+// a round issues the global loads of the next round's inputs behind the W2 fragment fetch in L1, so the
+// wait for the weight fragments fetched before it never includes these loads (127-129 vs 130 us per launch
+// against issuing them at the top of the round, stage phase 3.7k -> 3.1k cycles: profiles/r02_enc_ab.txt)
 // stage-ahead (1, default): round t + grid's F, G and cos images are staged in round t's last phase,
 // behind the dW1 MFMAs, into a second set of images (double-buffered), so a round starts with its first
 // layer instead of the staging phase and its barrier. Where the second set fits in LDS: AC-IQN, N = 32,
@@ -417,11 +413,6 @@ __device__ __forceinline__ int row_action(const float* in, int bl, int A) {
 #ifndef ASVRL_READ_AHEAD
 #define ASVRL_READ_AHEAD 2
 #endif
-// instruction kinds the per-step fences let through (sched_barrier mask; 0: none, 0x6: VALU and SALU, so
-// independent vector work may fill the MFMA gaps while the reads stay ahead) -- A/B knob
-#ifndef ASVRL_RA_FENCE_MASK
-#define ASVRL_RA_FENCE_MASK 0
-#endif
 // (Measured in round 4 and removed, profiles/r04e_fused_variants_ab.txt: a deeper weight-gradient read-ahead,
 // dW2 + L3 and dW1 + L4 as interleaved MFMA streams, the cos layer's gradient loop a k-step ahead, and the dW2 /
 // dW1 partials stored during the last round -- all bit-identical, none faster.)
@@ -446,7 +437,7 @@ __device__ __forceinline__ void mfma_rows(f32x16 (&acc)[NB], const elem_t* img, 
       if (ks + D < KS)
 #pragma unroll
         for (int j = 0; j < NB; ++j) bq[ks % D][j] = rowf(img, RA, j, ks + D);
-      __builtin_amdgcn_sched_barrier(ASVRL_RA_FENCE_MASK);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 }
@@ -476,7 +467,7 @@ __device__ __forceinline__ void mfma_grid(AF af, BF bf, MF mf) {
       if (n == 0 && kk + 1 < KK) aq[(kk + 1) % 2] = af(kk + 1);
       mf(kk, n, aq[kk % 2], bq[t % D]);
       if (t + D < T) bq[t % D] = bf((t + D) / NN, (t + D) % NN);
-      __builtin_amdgcn_sched_barrier(ASVRL_RA_FENCE_MASK);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 }
@@ -630,53 +621,6 @@ __device__ __forceinline__ void target_phase(const ctile::CriticArgs& t, TqLds<N
   }
 }
 
-#ifdef ASVRL_INLAUNCH_REDUCE
-// VERDICT r04 item 2, measured as a variant build (never the shipped library): the three trunk layers'
-// partials reduced inside the update launch by a last arriver per 1 KB tile instead of partial_sums_kernel.
-constexpr int kRedN = (kH * kH + kH) + (kH * kC + kH) + (kC * kNcos + kC);   // 66,048 floats
-constexpr int kRedTiles = (kRedN + 255) / 256;
-__device__ float g_red_out[kRedN];
-__device__ unsigned g_red_cnt[kRedTiles];
-__device__ unsigned g_red_won[1024];
-
-__device__ __forceinline__ float red_part(const FusedArgs& a, int g, int x) {
-  constexpr int n2 = kH * kH + kH, n1 = kH * kC + kH, nc = kC * kNcos + kC;
-  if (x < n2) return a.parts.hidden2[static_cast<size_t>(g) * n2 + x];
-  if (x < n2 + n1) return a.parts.hidden[static_cast<size_t>(g) * n1 + (x - n2)];
-  return a.parts.cos_emb[static_cast<size_t>(g) * nc + (x - n2 - n1)];
-}
-
-// after every thread's partial stores: publish (release at agent scope), count each tile once (tiles in an
-// order rotated by the workgroup index, so that the arrival order differs per tile), and reduce -- in
-// workgroup order, deterministic -- every tile this workgroup completed as the last arriver
-template <int NT>
-__device__ void inlaunch_reduce(const FusedArgs& a, int grp, int* list) {
-  __threadfence();
-  __syncthreads();
-  const int G = static_cast<int>(gridDim.x);
-  if (threadIdx.x == 0) list[0] = 0;
-  __syncthreads();
-  for (int t = threadIdx.x; t < kRedTiles; t += kNW * 64) {
-    const int tile = (t + grp * kRedTiles / G) % kRedTiles;
-    const unsigned old = atomicAdd(&g_red_cnt[tile], 1u);
-    if (old == static_cast<unsigned>(G - 1)) list[1 + atomicAdd(&list[0], 1)] = tile;
-  }
-  __syncthreads();
-  __threadfence();   // acquire: the other workgroups' partials
-  const int nw = list[0];
-  for (int k = 0; k < nw; ++k) {
-    const int tile = list[1 + k];
-    const int x = tile * 256 + static_cast<int>(threadIdx.x);
-    if (x < kRedN) {
-      float acc = 0.f;
-      for (int g = 0; g < G; ++g) acc += red_part(a, g, x);
-      g_red_out[x] = acc;
-    }
-    if (threadIdx.x == 0) g_red_cnt[tile] = 0u;   // for the next launch
-  }
-  if (threadIdx.x == 0) g_red_won[grp] = static_cast<unsigned>(nw);
-}
-#endif
 
 template <int NT, bool IQN, bool TQ = false>
 __global__ __launch_bounds__(kNW * 64) __attribute__((amdgpu_waves_per_eu(1, 1)))
@@ -833,9 +777,6 @@ void critic_fused_kernel(FusedArgs a) {
     pre[u] = (t + static_cast<int>(gridDim.x) < a.rounds && e < IL::kSize)                 \
                  ? fetch_in<NT, S, G, NA>(a, t + gridDim.x, e) : 0.f;                      \
   }
-#if ASVRL_PRE_AT == 0
-    ASVRL_FETCH_PRE();
-#endif
     float* const in = L.in[buf];
     // the lane indices re-derived through an opaque copy every round: otherwise every LDS / weight
     // address of the round body is loop-invariant, gets hoisted out of the loop and spills
@@ -946,11 +887,9 @@ void critic_fused_kernel(FusedArgs a) {
       ASVRL_STAMP(17);
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) w2f[ks] = W2[(w * 8 + ks) * 64 + lane];
-#if ASVRL_PRE_AT == 1
       // issued behind W2's fragments: the wait for those (in L2) does not include this load, whose
       // first waiter (W2^T's fragments, in L3) comes two phases later
       ASVRL_FETCH_PRE();
-#endif
       if constexpr (!kBiasFirst)
 #pragma unroll
         for (int j = 0; j < NB; ++j) acc[j] += bias_init(b1p, w * 32, h);
@@ -1434,9 +1373,6 @@ void critic_fused_kernel(FusedArgs a) {
     pc[kC * kNcos + swap23(2 * w * 32 + r)] = dbc0;
     pc[kC * kNcos + swap23((2 * w + 1) * 32 + r)] = dbc1;
   }
-#ifdef ASVRL_INLAUNCH_REDUCE
-  if constexpr (!IQN) inlaunch_reduce<NT>(a, grp, reinterpret_cast<int*>(L.x));
-#endif
   if constexpr (IQN) {
     // output layer [32 actions][128] + [32]: register g = action row, lane = feature position
     float* po = a.parts.out + static_cast<size_t>(grp) * (kMaxA * kH + kMaxA);
@@ -2153,12 +2089,6 @@ int fused_rounds(int B, int N) { return static_cast<int>(static_cast<int64_t>(B)
 
 using namespace asvrl;
 
-#ifdef ASVRL_INLAUNCH_REDUCE
-extern "C" int asvrl_debug_inlaunch_reduce(float* out, int64_t n_out, unsigned* won, int64_t n_won) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_red_out), n_out * sizeof(float)) != hipSuccess) return 1;
-  return hipMemcpyFromSymbol(won, HIP_SYMBOL(g_red_won), n_won * sizeof(unsigned)) == hipSuccess ? 0 : 1;
-}
-#endif
 
 #ifdef ASVRL_FUSED_STAMPS
 extern "C" int asvrl_debug_fused_stamps(uint64_t* out, int64_t n) {
@@ -2166,15 +2096,11 @@ extern "C" int asvrl_debug_fused_stamps(uint64_t* out, int64_t n) {
 }
 #endif
 
-// CUs the persistent launch leaves to a concurrent stream (A/B knob): the rollout's small kernels that
-// queue while it holds every CU otherwise wait for its end
-#ifndef ASVRL_FUSED_CU_RESERVE
-#define ASVRL_FUSED_CU_RESERVE 0
-#endif
+// one workgroup per CU (leaving CUs to the concurrent rollout stream measured slower, profiles/r02_cu_reserve_ab.txt)
 extern "C" int32_t asvrl_critic_fused_groups(int32_t B, int32_t N) {
   if (B <= 0 || (N != 8 && N != 16 && N != 32)) return 0;
   const int rounds = fused_rounds(B, N);
-  const int cus = cu_count() > 2 * ASVRL_FUSED_CU_RESERVE ? cu_count() - ASVRL_FUSED_CU_RESERVE : cu_count();
+  const int cus = cu_count();
   return rounds < cus ? rounds : cus;
 }
 
