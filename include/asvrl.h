@@ -374,8 +374,9 @@ int asvrl_critic_train_fused_tq(const AsvCriticWeights* w, const AsvCriticIO* io
                                 const AsvCriticWeights* tw, const AsvCriticIO* tio, void* stream);
 
 /* ABI 23: the kernel asvrl_critic_train_fused(_tq) launch where both forms take the shape (bf16 build, N = 32,
- * parts->enc and parts->aenc set, no dzF / dzG / xb): 8 = two waves per SIMD (512-thread workgroups; the
- * default), 4 = one wave per SIMD (the round-5 kernel). Results agree within f32 summation order, not bit for bit.
+ * parts->enc and parts->aenc set, no dzF / dzG / xb): 8 = two waves per SIMD (512-thread workgroups), 4 = one
+ * wave per SIMD (the round-5 kernel; the default: variant 8 measured 11 % slower). Results
+ * agree within f32 summation order, not bit for bit.
  * v < 0 only queries; returns the previous setting, or -1 (asvrl_last_error) for any other v. Process-wide. */
 int32_t asvrl_critic_fused_variant(int32_t v);
 
