@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("ASVRL_LIB", os.path.join(HERE, "lib", "libasvrl.so"))
 # the same sources built with f32 learner operands (the parity build; asvrl_operand_bytes() == 4)
 LIB_PATH_F32 = os.path.join(HERE, "lib", "libasvrl_f32.so")
 OPERANDS = {"bf16": (LIB_PATH, 2), "f32": (LIB_PATH_F32, 4)}
-ABI_VERSION = 23
+ABI_VERSION = 24
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
 OBS_DIM = 40   # self 7 | objects 25 | mask 5 | pad 3
@@ -293,6 +293,9 @@ EXPORTS = [
                                               C.POINTER(AsvCriticIO), _VP]),
     ("asvrl_iqn_train_fused", C.c_int, [C.POINTER(AsvCriticWeights), C.POINTER(AsvIqnHead), C.POINTER(AsvIqnIO),
                                         C.POINTER(AsvCriticParts), _VP]),
+    ("asvrl_iqn_train_fused_tq", C.c_int, [C.POINTER(AsvCriticWeights), C.POINTER(AsvIqnHead), C.POINTER(AsvIqnIO),
+                                           C.POINTER(AsvCriticParts), C.POINTER(AsvCriticWeights),
+                                           C.POINTER(AsvIqnHead), C.POINTER(AsvIqnIO), _VP]),
     ("asvrl_linear_wgrad_groups", _I32, [_I32, _I32, _I32]),
     ("asvrl_linear_wgrad_vec_groups", _I32, [_I32]),
     ("asvrl_linear_wgrad_partial", C.c_int, [_VP, _I64, _VP, _I64, _I32, _I32, _I32, _VP, _I64, _VP, _VP]),

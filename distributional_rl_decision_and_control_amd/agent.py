@@ -158,8 +158,9 @@ class Agent:
                                                   operands=ops) if ok else None
             else:
                 ok = fused_iqn.supported(self.policy_local, B, self.num_tau)
+                # nothing runs beside the drop-in's update: the target's max inside the fused launch (bf16 build)
                 st = fused_iqn.FusedIQNState(self.policy_local, self.policy_target, B, self.num_tau,
-                                             operands=ops) if ok else None
+                                             operands=ops, target_in_fused=True) if ok else None
             if st is None:
                 # not silent: this batch / network shape runs on the torch-autograd learner (learner.py), not on
                 # the hand-written kernels

@@ -472,34 +472,38 @@ __device__ __forceinline__ void mfma_grid(AF af, BF bf, MF mf) {
   }
 }
 
-// The target critic's forward in the update's own launch (asvrl_critic_train_fused_tq): before its first
-// round, each workgroup computes q_next for exactly the samples its rounds update -- round t's rows are
-// tiles t NB .. t NB + NB - 1 -- with asvrl_critic.hip's FWD tile (critic_tile<MODE_FWD>: the same code and
-// arithmetic, bit-identical q_next), the target weights staged in the LDS the rounds use afterwards, then
-// stores them where the rounds' input fetch reads q_next (global, workgroup-coherent after the barrier).
-// No workgroup waits on another: the samples of different workgroups are disjoint.
-template <int NT, bool TQ> struct TqLds { float pad[4]; };
+// The target critic's forward in the update's own launch (asvrl_critic_train_fused_tq, and for IQN
+// asvrl_iqn_train_fused_tq): before its first round, each workgroup computes q_next for exactly the samples its
+// rounds update -- round t's rows are tiles t NB .. t NB + NB - 1 -- with asvrl_critic.hip's forward tile
+// (critic_tile<MODE_FWD>, or <MODE_IQN_MAX> for IQN's max over the actions: the same code and arithmetic,
+// bit-identical q_next), the target weights staged in the LDS the rounds use afterwards, then stores them where
+// the rounds' input fetch reads q_next (global, workgroup-coherent after the barrier). No workgroup waits on
+// another: the samples of different workgroups are disjoint.
+template <int NT, bool TQ, bool IQN> struct TqLds { float pad[4]; };
 // N = 32 (a tile = one sample): the workgroup's samples are staged 16 at a time by all its threads together
 // (F, G and the taus of the chunk's tiles), so the tiles then run without a global load
 constexpr int kTqChunk = 16;
-template <int NT> struct TqLds<NT, true> {
+template <int NT, bool IQN> struct TqLds<NT, true, IQN> {
+  using FT = typename ctile::FOf<IQN ? ctile::MODE_IQN_MAX : ctile::MODE_FWD>::T;   // the tile's F element
+  using WT = typename ctile::LdsOf<IQN ? ctile::MODE_IQN_MAX : ctile::MODE_FWD>::T;
   static constexpr int kF = NT == 32 ? kTqChunk * kC : kNW * (32 / NT) * kC;
-  static constexpr int kG = NT == 32 ? kTqChunk * kH : kNW * (32 / NT) * kH;
-  ctile::CriticLds W;
-  float F[kF];
+  static constexpr int kG = IQN ? 4 : (NT == 32 ? kTqChunk * kH : kNW * (32 / NT) * kH);   // IQN: no action features
+  WT W;
+  FT F[kF];
   float G[kG];
   float T[NT == 32 ? kTqChunk * 32 : 4];
 };
 template <int NT, int NB, int S, bool IQN, int NSB, bool TQ>
 union FusedShared {
   FusedLds<NT, NB, S, IQN, NSB> f;
-  TqLds<NT, TQ> t;
+  TqLds<NT, TQ, IQN> t;
 };
 
 // F, G (asvrl_critic_tile.h stage_features' arithmetic, op for op, uncontracted) and the taus of n <= 16
-// samples b(0..n-1): thread m computes feature m of every sample from its weights loaded once
-template <class BF>
-__device__ __forceinline__ void tq_stage_chunk(const ctile::CriticArgs& t, int n, BF bidx, float* F, float* G,
+// samples b(0..n-1): thread m computes feature m of every sample from its weights loaded once. WITH_G false
+// (IQN): no action features.
+template <bool WITH_G, class FT, class BF>
+__device__ __forceinline__ void tq_stage_chunk(const ctile::CriticArgs& t, int n, BF bidx, FT* F, float* G,
                                                float* T) {
 #pragma clang fp contract(off)
   const int m = threadIdx.x;   // kNW * 64 == kC threads: one feature each
@@ -513,7 +517,7 @@ __device__ __forceinline__ void tq_stage_chunk(const ctile::CriticArgs& t, int n
   const float bb = self ? t.w.self_b[m] : t.w.obj_b[j];
   const int xo = self ? 0 : ctile::kSelfIn + ctile::kObjIn * o;
   float ae0 = 0.f, ae1 = 0.f, aeb = 0.f;
-  if (m < kH) {
+  if (WITH_G && m < kH) {
     ae0 = t.w.ae_w[2 * m];
     ae1 = t.w.ae_w[2 * m + 1];
     aeb = t.w.ae_b[m];
@@ -529,8 +533,8 @@ __device__ __forceinline__ void tq_stage_chunk(const ctile::CriticArgs& t, int n
 #pragma unroll
       for (int i = 0; i < ctile::kSelfIn; ++i) xs[q][i] = x[xo + ((i < ctile::kObjIn || self) ? i : 0)];
       mk[q] = self ? 1.f : x[ctile::kObsMask + o];
-      a0[q] = t.ain[static_cast<int64_t>(b) * t.ld_ain];
-      a1[q] = t.ain[static_cast<int64_t>(b) * t.ld_ain + 1];
+      a0[q] = WITH_G ? t.ain[static_cast<int64_t>(b) * t.ld_ain] : 0.f;
+      a1[q] = WITH_G ? t.ain[static_cast<int64_t>(b) * t.ld_ain + 1] : 0.f;
       tv[q] = t.taus[static_cast<int64_t>(b) * 32 + (m & 31)];   // NT = 32: tile b's rows
     }
 #pragma unroll
@@ -542,15 +546,16 @@ __device__ __forceinline__ void tq_stage_chunk(const ctile::CriticArgs& t, int n
       for (int i = 0; i < ctile::kSelfIn; ++i)
         if (i < ctile::kObjIn || self) d += w[i] * xs[q][i];
       const float v = mk[q] < 0.5f ? 0.f : relu(d + bb);   // masked_fill(mask < 0.5, 0)
-      F[k * kC + m] = static_cast<float>((elem_t)v);
-      if (m < kH) G[k * kH + m] = relu((ae0 * a0[q] + ae1 * a1[q]) + aeb);
+      F[k * kC + m] = static_cast<FT>((elem_t)v);
+      if (WITH_G && m < kH) G[k * kH + m] = relu((ae0 * a0[q] + ae1 * a1[q]) + aeb);
       if (m < 32) T[k * 32 + m] = tv[q];
     }
   }
 }
 
-template <int NT, int NB>
-__device__ __forceinline__ void target_phase(const ctile::CriticArgs& t, TqLds<NT, true>& T, int rounds) {
+template <int NT, int NB, bool IQN>
+__device__ __forceinline__ void target_phase(const ctile::CriticArgs& t, TqLds<NT, true, IQN>& T, int rounds) {
+  constexpr int MODE = IQN ? ctile::MODE_IQN_MAX : ctile::MODE_FWD;
   constexpr int St = 32 / NT;
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // N = 32: the Wc and W2 images' fragments (8 + 8 per thread) are loaded into registers first and stored to
@@ -574,7 +579,12 @@ __device__ __forceinline__ void target_phase(const ctile::CriticArgs& t, TqLds<N
   for (int i = threadIdx.x; i < kH; i += kNW * 64) {
     T.W.b1[i] = t.w.b1[i];
     T.W.b2[i] = t.w.b2[i];
-    T.W.wo[i] = t.w.wo[i];
+    if constexpr (!IQN) T.W.wo[i] = t.w.wo[i];
+  }
+  if constexpr (IQN) {   // the head image and its bias (critic_kernel's staging for the IQN modes)
+    const frag8* gwo = reinterpret_cast<const frag8*>(t.hd.wo_frag);
+    for (int i = threadIdx.x; i < kH / 16 * 64; i += kNW * 64) T.W.wo_img[i] = gwo[i];
+    for (int i = threadIdx.x; i < kMaxA; i += kNW * 64) T.W.bo_a[i] = i < t.hd.n_actions ? t.hd.bo[i] : 0.f;
   }
   const int mine = (rounds - static_cast<int>(blockIdx.x) + static_cast<int>(gridDim.x) - 1) / static_cast<int>(gridDim.x) * NB;
   auto tile_of = [&](int i) { return (static_cast<int>(blockIdx.x) + (i / NB) * static_cast<int>(gridDim.x)) * NB + i % NB; };
@@ -582,7 +592,7 @@ __device__ __forceinline__ void target_phase(const ctile::CriticArgs& t, TqLds<N
 #pragma nounroll
     for (int c0 = 0; c0 < mine; c0 += kTqChunk) {   // workgroup-uniform
       const int n = mine - c0 < kTqChunk ? mine - c0 : kTqChunk;
-      tq_stage_chunk(t, n, [&](int k) { return tile_of(c0 + k); }, T.F, T.G, T.T);
+      tq_stage_chunk<!IQN>(t, n, [&](int k) { return tile_of(c0 + k); }, T.F, T.G, T.T);
       if constexpr (kEarly) {
         if (c0 == 0) {
 #pragma unroll
@@ -597,22 +607,22 @@ __device__ __forceinline__ void target_phase(const ctile::CriticArgs& t, TqLds<N
       {
         int kk = k;   // opaque VGPR copy: with a uniform k the tile's LDS addresses are hoisted and spill (573)
         asm volatile("" : "+v"(kk));
-        ctile::critic_tile<ctile::MODE_FWD, NT>(t, T.W, tile_of(c0 + kk), lane, T.F + kk * kC, T.G + kk * kH, nullptr,
-                                                T.T + kk * 32);
+        ctile::critic_tile<MODE, NT>(t, T.W, tile_of(c0 + kk), lane, T.F + kk * kC, IQN ? nullptr : T.G + kk * kH,
+                                     nullptr, T.T + kk * 32);
       }
       __syncthreads();
     }
   } else {
     __syncthreads();
-    float* Fw = T.F + wv * St * kC;
-    float* Gw = T.G + wv * St * kH;
+    auto* Fw = T.F + wv * St * kC;
+    float* Gw = IQN ? nullptr : T.G + wv * St * kH;
     for (int i = wv; i < mine; i += kNW) {
       const int tile = tile_of(i);
-      ctile::stage_features<NT, true, false>(t, tile, lane, Fw, Gw);
+      ctile::stage_features<NT, !IQN, false>(t, tile, lane, Fw, Gw);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // the wave's own rows: in-order LDS, compiler fence
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      ctile::critic_tile<ctile::MODE_FWD, NT>(t, T.W, tile, lane, Fw, Gw);
+      ctile::critic_tile<MODE, NT>(t, T.W, tile, lane, Fw, Gw);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -633,7 +643,7 @@ void critic_fused_kernel(FusedArgs a) {
   constexpr bool LT = ASVRL_LANE_TABLE && sizeof(U) + sizeof(LaneBases) <= 160 * 1024;
   __shared__ int LB[LT ? kLbFields : 1][64];   // each lane's image bases
   auto& L = U.f;
-  if constexpr (TQ) target_phase<NT, NB>(a.tq, U.t, a.rounds);
+  if constexpr (TQ) target_phase<NT, NB, IQN>(a.tq, U.t, a.rounds);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
   if constexpr (LT) {   // read after the prologue's barrier
     if (threadIdx.x < 64) {
@@ -2105,8 +2115,8 @@ extern "C" int32_t asvrl_critic_fused_groups(int32_t B, int32_t N) {
 }
 
 namespace {
-// which kernel asvrl_critic_train_fused(_tq) launches where both take the shape: 8 (default) critic_fused8_kernel,
-// 4 critic_fused_kernel (asvrl_critic_fused_variant; the A/B and the kernel-vs-kernel tests)
+// which kernel asvrl_critic_train_fused(_tq) launches where both take the shape: 4 (default) critic_fused_kernel,
+// 8 critic_fused8_kernel (asvrl_critic_fused_variant; measured 11 % slower, kept for the A/B and its tests)
 int g_fused_variant = 4;
 
 int critic_train_fused_launch(const AsvCriticWeights* w, const AsvCriticIO* io, const AsvCriticParts* parts,
@@ -2191,9 +2201,12 @@ extern "C" int asvrl_critic_train_fused_tq(const AsvCriticWeights* w, const AsvC
 
 // train_IQN's update (agent.py:449-468) in one launch: the same kernel with IQN_Policy's trunk (no action
 // encoder, IQN_model.py:74-108) and its 128 -> A output layer gathered at the taken action; the output
-// layer's partial is [32 x 128 + 32] per workgroup (rows >= n_actions zero).
-extern "C" int asvrl_iqn_train_fused(const AsvCriticWeights* w, const AsvIqnHead* head, const AsvIqnIO* io,
-                                     const AsvCriticParts* parts, void* stream) {
+// layer's partial is [32 x 128 + 32] per workgroup (rows >= n_actions zero). With tw (asvrl_iqn_train_fused_tq,
+// ABI 24) the target network's max over the actions (agent.py:451-452) is computed inside the launch first.
+namespace {
+int iqn_train_fused_launch(const AsvCriticWeights* w, const AsvIqnHead* head, const AsvIqnIO* io,
+                           const AsvCriticParts* parts, const AsvCriticWeights* tw, const AsvIqnHead* thead,
+                           const AsvIqnIO* tio, void* stream) {
   ASVRL_REQUIRE(w && head && io && parts, "asvrl_iqn_train_fused: null argument");
   ASVRL_REQUIRE(io->taus && io->obs && io->actions && io->q_next && io->rewards && io->dones,
                 "asvrl_iqn_train_fused: needs taus, obs, actions, q_next, rewards and dones");
@@ -2211,6 +2224,18 @@ extern "C" int asvrl_iqn_train_fused(const AsvCriticWeights* w, const AsvIqnHead
   ASVRL_REQUIRE(io->kappa > 0.f, "asvrl_iqn_train_fused: kappa must be positive");
   ASVRL_REQUIRE(io->B >= 0 && (static_cast<int64_t>(io->B) * io->N) % (32 * fused_nb(io->N)) == 0,
                 "asvrl_iqn_train_fused: B*N must be a multiple of the round size (64 rows; 32 in the f32 build)");
+  const bool tq = tw != nullptr;
+  if (tq) {
+    ASVRL_REQUIRE(thead && tio, "asvrl_iqn_train_fused_tq: null target head or IO");
+    ASVRL_REQUIRE(tw->wc_frag && tw->w1_frag && tw->w2_frag && tw->bc && tw->b1 && tw->b2 && tw->self_w &&
+                      tw->self_b && tw->obj_w && tw->obj_b,
+                  "asvrl_iqn_train_fused_tq: null target weight");
+    ASVRL_REQUIRE(thead->wo_frag && thead->bo && thead->n_actions == head->n_actions,
+                  "asvrl_iqn_train_fused_tq: bad target head");
+    ASVRL_REQUIRE(tio->taus && tio->obs && tio->ld_obs >= 37,
+                  "asvrl_iqn_train_fused_tq: the target pass needs taus and obs (packed observation rows)");
+    ASVRL_REQUIRE(tio->B == io->B && tio->N == io->N, "asvrl_iqn_train_fused_tq: target B / N differ from the update's");
+  }
   if (io->B == 0) return 0;
   FusedArgs a{};
   a.w = *w;
@@ -2225,16 +2250,42 @@ extern "C" int asvrl_iqn_train_fused(const AsvCriticWeights* w, const AsvIqnHead
   a.dzF = io->dzF; a.dzG = nullptr;
   a.parts = *parts;
   a.iwo = head->wo; a.ibo = head->bo; a.n_actions = head->n_actions;
+  if (tq) {   // asvrl_iqn_forward_max's arguments (asvrl_critic.hip iqn_args), q -> the update's q_next
+    a.tq.w = *tw;
+    a.tq.hd = *thead;
+    a.tq.taus = tio->taus; a.tq.B = tio->B; a.tq.N = tio->N; a.tq.Np = tio->N;
+    a.tq.obs = tio->obs; a.tq.ld_obs = tio->ld_obs;
+    a.tq.q = const_cast<float*>(io->q_next);   // written here, read by the rounds
+  }
   const int grid = asvrl_critic_fused_groups(io->B, io->N);
   hipStream_t st = as_stream(stream);
+  if (tq) {
+    if (io->N == 32) hipLaunchKernelGGL((critic_fused_kernel<32, true, true>), dim3(grid), dim3(kNW * 64), 0, st, a);
+    else if (io->N == 16) hipLaunchKernelGGL((critic_fused_kernel<16, true, true>), dim3(grid), dim3(kNW * 64), 0, st, a);
+    else hipLaunchKernelGGL((critic_fused_kernel<8, true, true>), dim3(grid), dim3(kNW * 64), 0, st, a);
+    return check_launch("asvrl_iqn_train_fused_tq");
+  }
   if (io->N == 32) hipLaunchKernelGGL((critic_fused_kernel<32, true>), dim3(grid), dim3(kNW * 64), 0, st, a);
   else if (io->N == 16) hipLaunchKernelGGL((critic_fused_kernel<16, true>), dim3(grid), dim3(kNW * 64), 0, st, a);
   else hipLaunchKernelGGL((critic_fused_kernel<8, true>), dim3(grid), dim3(kNW * 64), 0, st, a);
   return check_launch("asvrl_iqn_train_fused");
 }
+}  // namespace
+
+extern "C" int asvrl_iqn_train_fused(const AsvCriticWeights* w, const AsvIqnHead* head, const AsvIqnIO* io,
+                                     const AsvCriticParts* parts, void* stream) {
+  return iqn_train_fused_launch(w, head, io, parts, nullptr, nullptr, nullptr, stream);
+}
+
+extern "C" int asvrl_iqn_train_fused_tq(const AsvCriticWeights* w, const AsvIqnHead* head, const AsvIqnIO* io,
+                                        const AsvCriticParts* parts, const AsvCriticWeights* tw,
+                                        const AsvIqnHead* thead, const AsvIqnIO* tio, void* stream) {
+  ASVRL_REQUIRE(tw != nullptr, "asvrl_iqn_train_fused_tq: null target weights");
+  return iqn_train_fused_launch(w, head, io, parts, tw, thead, tio, stream);
+}
 
 // The AC-IQN critic update's kernel where both forms take the shape (N = 32, encoders' gradients in the launch,
-// bf16 build): 8 = critic_fused8_kernel (two waves per SIMD, the default), 4 = critic_fused_kernel (one wave per
+// bf16 build): 4 = critic_fused_kernel (one wave per SIMD, the default), 8 = critic_fused8_kernel (two waves per
 // SIMD). v < 0 only queries. Returns the previous setting; anything else is an error (-1).
 extern "C" int32_t asvrl_critic_fused_variant(int32_t v) {
   const int prev = g_fused_variant;

@@ -7,6 +7,8 @@ replay batch `rows` ([B][88]: obs | next obs | action | reward | done):
 
     target encoders(ns) + trunk, max over actions per tau -> q_next
                                                           asvrl_iqn_forward_max    (agent.py:451-452)
+                                                          (bf16 build, FusedIQNState.target_in_fused: inside
+                                                          the next launch, ABI 24 asvrl_iqn_train_fused_tq)
     local encoders(s) + forward, gather at a, quantile-Huber vs r + g q_next (1-d), backward,
     and the per-workgroup weight-gradient partials of the four layers
                                                           asvrl_iqn_train_fused (ONE launch, agent.py:455-468)
@@ -43,6 +45,12 @@ K_ACT = 32
 # wherever it takes the shape (B*N a multiple of its 64-row round); otherwise asvrl_iqn_train's two
 # launches + the batched weight-gradient launch over saved activations (tests toggle it)
 FUSED_TRAIN = True
+# the target network's max over the actions inside that launch (ABI 24, asvrl_iqn_train_fused_tq: each workgroup
+# forms q_next for the samples it updates, bit-identical to asvrl_iqn_forward_max); bf16 build. The default of
+# FusedIQNState.target_in_fused. Off for the batched loop, whose act pass runs beside the learner: there the longer
+# update launch runs beside the act pass instead of the env step, 0.2982 -> 0.3153 ms per IQN step; on for the
+# drop-in Agent (nothing beside its update): 55.5 -> 54.0 us per B = 64 step (profiles/r06j_*, r06k_*)
+TARGET_IN_FUSED = False
 
 
 def supported(net, B, N):
@@ -123,13 +131,15 @@ def iqn_train(pack, F, taus, bufs, dz_out, q_next, actions, rewards, dones, gamm
 
 
 def iqn_train_fused(pack, net, taus, N, q_next, actions, rewards, dones, gamma, obs, arena, dzF=None, xb=None,
-                    tile_loss=None, kappa=1.0, q=None, row_loss=None, stream=None, encoders=False):
+                    tile_loss=None, kappa=1.0, q=None, row_loss=None, stream=None, encoders=False, target=None):
     """asvrl_iqn_train_fused: train_IQN's local pass (agent.py:455-468) -- forward, gather at the
     taken action, quantile-Huber loss, backward -- AND the weight gradients of the trunk and the
     output layer in one launch; the per-workgroup partials land in `arena` as segments of net's
     cos_embedding / hidden_layer / hidden_layer_2 / output_layer .grad.
     encoders=True: also the observation encoders' gradients (ABI 16 parts.enc; their .grad contiguous
-    [self_w | self_b | obj_w | obj_b]); dzF / xb are then not needed."""
+    [self_w | self_b | obj_w | obj_b]); dzF / xb are then not needed.
+    target=(target_pack, target_taus, next_obs): q_next is first computed inside the launch
+    (asvrl_iqn_train_fused_tq) from the target network, as iqn_forward_max would."""
     B = obs.shape[0]
     groups = fused_groups(pack, B, N)
     assert groups > 0 and fused_train_supported(pack, B, N), (B, N)
@@ -149,8 +159,17 @@ def iqn_train_fused(pack, net, taus, N, q_next, actions, rewards, dones, gamma, 
     io = _io(None, N, obs=obs, xb=xb, taus=taus, Np=N, kappa=float(kappa), q_next=q_next, actions=actions,
              rewards=rewards, dones=dones, ld_rd=rewards.stride(0), gamma=float(gamma), q=q, row_loss=row_loss,
              dzF=dzF, tile_loss=tile_loss, loss_scale=1.0 / float(B * N))
-    _abi.check(pack.L.asvrl_iqn_train_fused(C.byref(pack.struct), C.byref(pack.head), C.byref(io), C.byref(parts),
-                                            _abi.stream_ptr(stream)), "asvrl_iqn_train_fused", pack.L)
+    if target is not None:
+        tpack, ttaus, next_obs = target
+        tio = _io(None, N, obs=next_obs, taus=ttaus)
+        _abi.check(pack.L.asvrl_iqn_train_fused_tq(C.byref(pack.struct), C.byref(pack.head), C.byref(io),
+                                                   C.byref(parts), C.byref(tpack.struct), C.byref(tpack.head),
+                                                   C.byref(tio), _abi.stream_ptr(stream)),
+                   "asvrl_iqn_train_fused_tq", pack.L)
+    else:
+        _abi.check(pack.L.asvrl_iqn_train_fused(C.byref(pack.struct), C.byref(pack.head), C.byref(io),
+                                                C.byref(parts), _abi.stream_ptr(stream)), "asvrl_iqn_train_fused",
+                   pack.L)
     for (layer, M, K), part in zip(shapes, regions):
         arena.groups(part, groups, M, K, layer.weight.grad, layer.bias.grad)
     if encoders:
@@ -172,9 +191,12 @@ class FusedIQNState:
     operands="f32": every kernel from libasvrl_f32.so (the parity build; the optimiser must be a
     FusedAdam of the same operands)."""
 
-    def __init__(self, net_local, net_target, B, N, operands="bf16"):
+    def __init__(self, net_local, net_target, B, N, operands="bf16", target_in_fused=None):
         dev = net_local.cos_embedding.weight.device
         self.B, self.N, self.device = B, N, dev
+        self.operands = operands
+        # the target's max inside the fused launch (bf16 build; module default TARGET_IN_FUSED)
+        self.target_in_fused = TARGET_IN_FUSED if target_in_fused is None else bool(target_in_fused)
         self.A = net_local.action_size
         self.local = IqnPack(net_local, operands)
         self.target = IqnPack(net_target, operands)
@@ -207,12 +229,16 @@ def iqn_grads(st, net, rows, taus, gamma=0.99, flush=True):
     a_col, r_col, d_col = rows[:, 80], rows[:, 82], rows[:, 83]
     bufs, arena = st.bufs, st.arena
     # every .grad is overwritten below (no zeroing); the trunk kernels run the encoders on the rows
-    iqn_forward_max(st.target, None, taus[0], N, st.q_next, obs=ns_rows)
-    if FUSED_TRAIN and fused_train_supported(st.local, B, N):
+    fused = FUSED_TRAIN and fused_train_supported(st.local, B, N)
+    target_in = fused and ENC_IN_KERNEL and st.target_in_fused and st.operands == "bf16"
+    if not target_in:
+        iqn_forward_max(st.target, None, taus[0], N, st.q_next, obs=ns_rows)
+    if fused:
         # forward, loss, backward and the four layers' weight-gradient partials in one launch
-        if ENC_IN_KERNEL:   # ... and the encoders' gradient partials
+        if ENC_IN_KERNEL:   # ... and the encoders' gradient partials (and, target_in, the target's max first)
             iqn_train_fused(st.local, net, taus[1], N, st.q_next.view(B, N), a_col, r_col, d_col, gamma, s_rows,
-                            arena, tile_loss=st.tile_loss, encoders=True)
+                            arena, tile_loss=st.tile_loss, encoders=True,
+                            target=(st.target, taus[0], ns_rows) if target_in else None)
         else:
             iqn_train_fused(st.local, net, taus[1], N, st.q_next.view(B, N), a_col, r_col, d_col, gamma, s_rows,
                             arena, dzF=st.dzF, xb=st.xb, tile_loss=st.tile_loss)

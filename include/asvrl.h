@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 23
+#define ASVRL_ABI_VERSION 24
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -446,6 +446,14 @@ int asvrl_iqn_train(const AsvCriticWeights* w, const AsvIqnHead* head, const Asv
  * dz_out is not written; N' must equal N; groups = asvrl_critic_fused_groups(B, N). */
 int asvrl_iqn_train_fused(const AsvCriticWeights* w, const AsvIqnHead* head, const AsvIqnIO* io,
                           const AsvCriticParts* parts, void* stream);
+/* ABI 24: the same launch with train_IQN's target (agent.py:451-452: qnetwork_target(next_states, taus').max over
+ * the actions) computed inside it first: each workgroup forms q_next for exactly the samples it updates (the
+ * IQN_MAX tile of asvrl_iqn_forward_max, bit-identical) into io->q_next, then the update reads it. tw / thead:
+ * the target network's images and head; tio: taus (the target's tau'), obs (next-observation rows), B and N as
+ * io. Replaces asvrl_iqn_forward_max + asvrl_iqn_train_fused. */
+int asvrl_iqn_train_fused_tq(const AsvCriticWeights* w, const AsvIqnHead* head, const AsvIqnIO* io,
+                             const AsvCriticParts* parts, const AsvCriticWeights* tw, const AsvIqnHead* thead,
+                             const AsvIqnIO* tio, void* stream);
 
 /* act_iqn (agent.py:227-256) for every row of F with K = 32 quantile samples per state. */
 int asvrl_iqn_act(const AsvCriticWeights* w, const AsvIqnHead* head, const AsvIqnIO* io, void* stream);

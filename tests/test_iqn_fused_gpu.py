@@ -153,3 +153,43 @@ def test_iqn_fused_encoder_grads_in_kernel(ops, B, N):
             c = _cos(ge[n], gf[n])
             ratio = np.linalg.norm(ge[n]) / np.linalg.norm(gf[n])
             assert c > 0.999 and abs(ratio - 1) < 1e-2, (n, c, ratio)
+
+
+@pytest.mark.parametrize("ops,B,N", [("bf16", 64, 8), ("bf16", 64, 16), ("bf16", 256, 32), ("bf16", 4096, 32),
+                                     ("f32", 64, 8), ("f32", 256, 32)])
+def test_iqn_target_max_in_launch_matches_separate(ops, B, N):
+    """asvrl_iqn_train_fused_tq (ABI 24): the target network's max over the actions (agent.py:451-452) computed
+    inside the fused launch, each workgroup for the samples it updates, against asvrl_iqn_forward_max + the
+    fused launch: the same tile code on the same inputs, so q_next, every gradient and the loss are bit-identical
+    (q_next poisoned with NaN before the launch that must write it)."""
+    from distributional_rl_decision_and_control_amd import fused_iqn as fi
+    from distributional_rl_decision_and_control_amd.agent import Agent
+    from distributional_rl_decision_and_control_amd.learner import FusedAdam
+    rows = _batch(B, 77)
+    taus = torch.rand(2, B, N, generator=torch.Generator(device="cuda").manual_seed(78), device="cuda")
+    out = {}
+    for tq in (False, True):
+        ag = Agent(seed=100, agent_type="IQN")
+        net = ag.policy_local
+        with torch.no_grad():   # a target network different from the local one
+            for p in ag.policy_target.parameters():
+                p.add_(0.05 * p.abs().mean() * torch.randn(p.shape, generator=torch.Generator().manual_seed(5)).to(p.device))
+        opt = FusedAdam(net.parameters(), lr=1e-4, operands=ops)
+        st = fi.FusedIQNState(net, ag.policy_target, B, N, operands=ops, target_in_fused=tq)
+        opt.grads.zero_()
+        st.q_next.fill_(float("nan"))
+        if tq and ops == "f32":   # the learner keeps the separate launch in the f32 build: call the entry itself
+            fi.iqn_train_fused(st.local, net, taus[1], N, st.q_next.view(B, N), rows[:, 80], rows[:, 82], rows[:, 83],
+                               0.99, rows[:, 0:40], st.arena, tile_loss=st.tile_loss, encoders=True,
+                               target=(st.target, taus[0], rows[:, 40:80]))
+            st.arena.scalar(st.tile_loss, st.loss)
+            st.arena.flush()
+        else:
+            fi.iqn_grads(st, net, rows, taus, 0.99, flush=True)
+        torch.cuda.synchronize()
+        out[tq] = ({n: p.grad.detach().clone() for n, p in net.named_parameters()}, st.loss.clone(), st.q_next.clone())
+    (ga, la, qa), (gb, lb, qb) = out[False], out[True]
+    assert torch.isfinite(qa).all() and torch.equal(qa, qb), float((qa - qb).abs().nan_to_num(1e30).max())
+    assert torch.equal(la, lb), (la, lb)
+    for n in ga:
+        assert torch.equal(ga[n], gb[n]), (n, float((ga[n] - gb[n]).abs().max()))
