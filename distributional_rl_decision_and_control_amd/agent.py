@@ -193,6 +193,28 @@ class Agent:
             action = [np.random.uniform(low=lo, high=hi) for lo, hi in self.value_ranges_of_action]
         return action
 
+    def act_ac_iqn_robots(self, states, eps=0.0, use_eval=True):
+        """act_ac_iqn for several robots' states in one actor call: each robot in order draws its
+        random.random() and, exploring, its np.random.uniform actions exactly as the per-robot calls would; the
+        greedy robots' actions come from ONE batched forward (equal to the batch-1 forwards up to the GEMM's
+        summation order). The drop-in Trainer's per-step acts (trainer.py:138-151 calls act per robot)."""
+        actions, greedy = [None] * len(states), []
+        for i in range(len(states)):
+            if random.random() > eps:
+                greedy.append(i)
+            else:
+                actions[i] = [np.random.uniform(low=lo, high=hi) for lo, hi in self.value_ranges_of_action]
+        if greedy:
+            s = self.state_to_tensor(self.memory.state_batch([states[i] for i in greedy]))
+            net = self.policy_local.actor
+            net.eval() if use_eval else net.train()
+            with torch.no_grad():
+                a = net(s).cpu().data.numpy()
+            net.train()
+            for k, i in enumerate(greedy):
+                actions[i] = a[k].tolist()
+        return actions
+
     def act_iqn(self, state, eps=0.0, cvar=1.0, use_eval=True, taus=None):
         s = self._batch1(state)
         self.policy_local.eval() if use_eval else self.policy_local.train()

@@ -98,6 +98,16 @@ class Trainer:
         raise RuntimeError("Agent type not implemented!")
 
     def _gather_actions(self, env, states, eps, training):
+        agent = self.rl_agent
+        if training and not self.imitation and agent.agent_type == "AC-IQN":
+            # every active robot's act in one actor call, the same random draws in the same robot order
+            # (Agent.act_ac_iqn_robots); IQN keeps per-robot calls (each draws its own quantile fractions)
+            active = [i for i, rob in enumerate(env.robots) if not rob.deactivated]
+            acts = agent.act_ac_iqn_robots([states[i] for i in active], eps, use_eval=False)
+            actions = [None] * len(env.robots)
+            for i, a in zip(active, acts):
+                actions[i] = a
+            return actions
         actions = []
         for i, rob in enumerate(env.robots):
             if rob.deactivated:

@@ -160,3 +160,29 @@ def test_train_dqn_matches_reference():
     _cmp_sd(ag.policy_local, z, "after1/")
     st = (z["act/state_self"].tolist(), z["act/state_obj"].tolist())
     assert ag.act_dqn(st, eps=0.0) == int(z["act/action"])
+
+
+@pytest.mark.parametrize("eps", [0.0, 0.5, 1.0])
+def test_act_ac_iqn_robots_matches_per_robot_acts(eps):
+    """Agent.act_ac_iqn_robots (the drop-in Trainer's per-step acts in one actor call) against one act_ac_iqn call
+    per robot from the same random states: the same draws in the same order (python random and numpy), so the
+    exploring robots' actions are identical and the greedy ones equal up to the batched GEMM's summation order;
+    both generators end in the same state."""
+    import random
+    from distributional_rl_decision_and_control_amd.agent import Agent
+    from distributional_rl_decision_and_control_amd.envs.marinenav.env import MarineNavEnv3
+    sched = {"timesteps": [0], "num_robots": [5], "num_cores": [0], "num_obstacles": [4], "min_start_goal_dis": [40.0]}
+    env = MarineNavEnv3(seed=3, schedule=sched)
+    states, _, _ = env.reset()
+    ag = Agent(seed=100, agent_type="AC-IQN")
+    random.seed(11)
+    np.random.seed(12)
+    per = [ag.act_ac_iqn(s, eps, use_eval=False) for s in states]
+    r_after, n_after = random.random(), np.random.rand()
+    random.seed(11)
+    np.random.seed(12)
+    bat = ag.act_ac_iqn_robots(states, eps, use_eval=False)
+    assert (random.random(), np.random.rand()) == (r_after, n_after)
+    assert len(bat) == len(per) == len(states)
+    for a, b in zip(per, bat):
+        np.testing.assert_allclose(np.asarray(b), np.asarray(a), rtol=1e-5, atol=1e-6)
