@@ -116,10 +116,20 @@ __global__ __launch_bounds__(kTreeThreads) void per_tree_blocks_kernel(float* __
   if (threadIdx.x == 0) dirty[b] = 0;
 }
 
-// The nb block roots up to the root, then the ring advance of a push.
+// Work a push / priority update finishes in its last (one-workgroup) launch instead of launches of their own
+// (asvrl_per_push_ex, asvrl_per_update_ex): a device step counter advanced by one, and the mean of the update's
+// values in a fixed order.
+struct TopExtra {
+  int64_t* counter;
+  const float* mean_in;
+  int mean_n;
+  float* mean_out;
+};
+
+// The nb block roots up to the root, then the ring advance of a push (and the TopExtra work).
 __global__ __launch_bounds__(kTopThreads) void per_tree_top_kernel(float* __restrict__ tree, int nb,
                                                                    int64_t* __restrict__ state, int64_t C,
-                                                                   int64_t advance) {
+                                                                   int64_t advance, TopExtra ex) {
   __shared__ float lv[2 * kTopThreads];
   for (int i = threadIdx.x; i < nb; i += kTopThreads) lv[i] = tree[nb - 1 + i];
   __syncthreads();
@@ -138,6 +148,56 @@ __global__ __launch_bounds__(kTopThreads) void per_tree_top_kernel(float* __rest
     if (nx >= C) state[1] = 1;           // full = full or index == 0 after a wrap (:147)
     state[0] = nx % C;
   }
+  if (threadIdx.x == 0 && ex.counter != nullptr) ex.counter[0] += 1;
+  if (ex.mean_out != nullptr) {   // thread t sums values t, t + 1024, ... in order, then a fixed pairwise tree
+    float v = 0.f;
+    for (int i = threadIdx.x; i < ex.mean_n; i += kTopThreads) v += ex.mean_in[i];
+    __syncthreads();
+    lv[threadIdx.x] = v;
+    __syncthreads();
+    for (int w = kTopThreads >> 1; w >= 1; w >>= 1) {
+      if (threadIdx.x < w) lv[threadIdx.x] += lv[threadIdx.x + w];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) ex.mean_out[0] = lv[0] / static_cast<float>(ex.mean_n);
+  }
+}
+
+// weights / weights.max() (replay_memory_rainbow.py:191) over the sampled rows' weight column, in place: one
+// workgroup (the max is order-independent, the quotient IEEE: the values of torch's w.div_(w.max())). It reads the
+// weights from the contiguous copy asvrl_per_sample_ex wrote beside the rows (coalesced; the rows' column is one
+// float per 352-byte row), kNormPer per thread in flight and kept in registers for the quotients.
+constexpr int kNormPer = 8;
+__global__ __launch_bounds__(kTopThreads) void per_normalise_kernel(float* __restrict__ rows,
+                                                                    const float* __restrict__ wsrc, int B) {
+  __shared__ float mx[kTopThreads];
+  float m = -__builtin_inff();
+  float v[kNormPer];
+  for (int b0 = 0; b0 < B; b0 += kTopThreads * kNormPer) {
+#pragma unroll
+    for (int j = 0; j < kNormPer; ++j) {   // every load of the chunk issued before the first use
+      const int b = b0 + j * kTopThreads + static_cast<int>(threadIdx.x);
+      v[j] = b < B ? wsrc[b] : -__builtin_inff();
+    }
+#pragma unroll
+    for (int j = 0; j < kNormPer; ++j) m = fmaxf(m, v[j]);
+  }
+  mx[threadIdx.x] = m;
+  __syncthreads();
+  for (int w = kTopThreads >> 1; w >= 1; w >>= 1) {
+    if (threadIdx.x < w) mx[threadIdx.x] = fmaxf(mx[threadIdx.x], mx[threadIdx.x + w]);
+    __syncthreads();
+  }
+  const float d = mx[0];
+  if (B <= kTopThreads * kNormPer) {   // the one chunk is still in registers
+#pragma unroll
+    for (int j = 0; j < kNormPer; ++j) {
+      const int b = j * kTopThreads + static_cast<int>(threadIdx.x);
+      if (b < B) rows[static_cast<int64_t>(b) * ASVRL_TR_DIM + 84] = v[j] / d;
+    }
+    return;
+  }
+  for (int b = threadIdx.x; b < B; b += kTopThreads) rows[static_cast<int64_t>(b) * ASVRL_TR_DIM + 84] = wsrc[b] / d;
 }
 
 // ------------------------------------------------------------------ sample (ReplayMemory.sample)
@@ -149,7 +209,8 @@ __global__ __launch_bounds__(kTopThreads) void per_tree_top_kernel(float* __rest
 __global__ __launch_bounds__(256) void per_sample_kernel(AsvPer per, int B, const double* __restrict__ uniforms,
                                                          uint64_t seed, uint64_t counter,
                                                          const uint64_t* __restrict__ counter_dev,
-                                                         float* __restrict__ out, int64_t* __restrict__ out_idx) {
+                                                         float* __restrict__ out, int64_t* __restrict__ out_idx,
+                                                         float* __restrict__ w_out) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const int64_t C = per.capacity, P = per.tree_leaves;
@@ -236,6 +297,7 @@ __global__ __launch_bounds__(256) void per_sample_kernel(AsvPer per, int B, cons
   const float w = ok ? powf(static_cast<float>(cap) * p, -per.priority_weight) : 0.f;
   o[2 * ASVRL_OBS_DIM / 4] = make_float4(r0[kMeta], 0.f, R, nonterm);
   o[2 * ASVRL_OBS_DIM / 4 + 1] = make_float4(w, p, static_cast<float>(di), 0.f);
+  if (w_out != nullptr) w_out[b] = w;   // the contiguous copy asvrl_per_normalise reads
 }
 
 // ------------------------------------------------------------------ update_priorities
@@ -270,7 +332,7 @@ __global__ __launch_bounds__(256) void per_update_kernel(AsvPer per, const int64
     atomicMax(reinterpret_cast<int*>(per.maxp), __float_as_int(m));
 }
 
-int launch_rebuild(const AsvPer& per, int64_t advance, hipStream_t st, const char* what) {
+int launch_rebuild(const AsvPer& per, int64_t advance, hipStream_t st, const char* what, const TopExtra& ex = {}) {
   const int64_t P = per.tree_leaves;
   const int Lb = static_cast<int>(P < kLeafBlock ? P : kLeafBlock);
   const int nb = static_cast<int>(P / Lb);
@@ -279,7 +341,7 @@ int launch_rebuild(const AsvPer& per, int64_t advance, hipStream_t st, const cha
     if (int rc = check_launch(what)) return rc;
   }
   hipLaunchKernelGGL(per_tree_top_kernel, dim3(1), dim3(kTopThreads), 0, st, per.tree, nb, per.state,
-                     per.capacity, advance);
+                     per.capacity, advance, ex);
   return check_launch(what);
 }
 
@@ -304,9 +366,9 @@ int check_per(const AsvPer* per, const char* what) {
 
 using namespace asvrl;
 
-extern "C" int asvrl_per_push(const AsvPer* per, const float* obs, const int8_t* obj_cnt, const double* actions,
-                              int32_t action_dim, const double* reward, const uint8_t* done, int32_t n,
-                              void* stream) {
+extern "C" int asvrl_per_push_ex(const AsvPer* per, const float* obs, const int8_t* obj_cnt, const double* actions,
+                                 int32_t action_dim, const double* reward, const uint8_t* done, int32_t n,
+                                 int64_t* step_counter, void* stream) {
   if (int rc = check_per(per, "asvrl_per_push")) return rc;
   ASVRL_REQUIRE(obs && obj_cnt && actions && reward && done, "asvrl_per_push: null argument");
   ASVRL_REQUIRE(action_dim >= 1, "asvrl_per_push: action_dim >= 1");
@@ -317,27 +379,57 @@ extern "C" int asvrl_per_push(const AsvPer* per, const float* obs, const int8_t*
   hipLaunchKernelGGL(per_push_kernel, dim3((per->stride + 255) / 256), dim3(256), 0, st, obs, obj_cnt, actions,
                      action_dim, reward, done, n, *per);
   if (int rc = check_launch("asvrl_per_push")) return rc;
-  return launch_rebuild(*per, n, st, "asvrl_per_push(tree)");
+  TopExtra ex{};
+  ex.counter = step_counter;
+  return launch_rebuild(*per, n, st, "asvrl_per_push(tree)", ex);
+}
+
+extern "C" int asvrl_per_push(const AsvPer* per, const float* obs, const int8_t* obj_cnt, const double* actions,
+                              int32_t action_dim, const double* reward, const uint8_t* done, int32_t n,
+                              void* stream) {
+  return asvrl_per_push_ex(per, obs, obj_cnt, actions, action_dim, reward, done, n, nullptr, stream);
+}
+
+extern "C" int asvrl_per_sample_ex(const AsvPer* per, int32_t B, const double* uniforms, uint64_t seed,
+                                   uint64_t counter, const uint64_t* counter_dev, float* out, int64_t* out_tree_idx,
+                                   float* weights, void* stream) {
+  if (int rc = check_per(per, "asvrl_per_sample")) return rc;
+  ASVRL_REQUIRE(out && out_tree_idx, "asvrl_per_sample: null argument");
+  ASVRL_REQUIRE(B >= 1, "asvrl_per_sample: B >= 1");
+  hipLaunchKernelGGL(per_sample_kernel, dim3((B + 255) / 256), dim3(256), 0, as_stream(stream), *per, B, uniforms,
+                     seed, counter, counter_dev, out, out_tree_idx, weights);
+  return check_launch("asvrl_per_sample");
 }
 
 extern "C" int asvrl_per_sample(const AsvPer* per, int32_t B, const double* uniforms, uint64_t seed,
                                 uint64_t counter, const uint64_t* counter_dev, float* out, int64_t* out_tree_idx,
                                 void* stream) {
-  if (int rc = check_per(per, "asvrl_per_sample")) return rc;
-  ASVRL_REQUIRE(out && out_tree_idx, "asvrl_per_sample: null argument");
-  ASVRL_REQUIRE(B >= 1, "asvrl_per_sample: B >= 1");
-  hipLaunchKernelGGL(per_sample_kernel, dim3((B + 255) / 256), dim3(256), 0, as_stream(stream), *per, B, uniforms,
-                     seed, counter, counter_dev, out, out_tree_idx);
-  return check_launch("asvrl_per_sample");
+  return asvrl_per_sample_ex(per, B, uniforms, seed, counter, counter_dev, out, out_tree_idx, nullptr, stream);
 }
 
-extern "C" int asvrl_per_update(const AsvPer* per, const int64_t* tree_idx, const float* values, int32_t B,
-                                int32_t raw, void* stream) {
+extern "C" int asvrl_per_update_ex(const AsvPer* per, const int64_t* tree_idx, const float* values, int32_t B,
+                                   int32_t raw, float* values_mean, int64_t* learn_counter, void* stream) {
   if (int rc = check_per(per, "asvrl_per_update")) return rc;
   ASVRL_REQUIRE(tree_idx && values, "asvrl_per_update: null argument");
   if (B <= 0) return 0;
   const hipStream_t st = as_stream(stream);
   hipLaunchKernelGGL(per_update_kernel, dim3((B + 255) / 256), dim3(256), 0, st, *per, tree_idx, values, B, raw);
   if (int rc = check_launch("asvrl_per_update")) return rc;
-  return launch_rebuild(*per, 0, st, "asvrl_per_update(tree)");
+  TopExtra ex{};
+  ex.counter = learn_counter;
+  ex.mean_in = values;
+  ex.mean_n = B;
+  ex.mean_out = values_mean;
+  return launch_rebuild(*per, 0, st, "asvrl_per_update(tree)", ex);
+}
+
+extern "C" int asvrl_per_update(const AsvPer* per, const int64_t* tree_idx, const float* values, int32_t B,
+                                int32_t raw, void* stream) {
+  return asvrl_per_update_ex(per, tree_idx, values, B, raw, nullptr, nullptr, stream);
+}
+
+extern "C" int asvrl_per_normalise(float* rows, const float* weights, int32_t B, void* stream) {
+  ASVRL_REQUIRE(rows != nullptr && weights != nullptr && B >= 1, "asvrl_per_normalise: null argument or B < 1");
+  hipLaunchKernelGGL(per_normalise_kernel, dim3(1), dim3(kTopThreads), 0, as_stream(stream), rows, weights, B);
+  return check_launch("asvrl_per_normalise");
 }

@@ -208,6 +208,7 @@ class DevicePER:
         self.state = torch.zeros(4, dtype=torch.int64, device=dev)
         self.t = torch.zeros(self.stride, dtype=torch.int32, device=dev)
         self.maxp = torch.ones(1, dtype=torch.float32, device=dev)
+        self._weights = {}   # B -> the draws' contiguous weights (asvrl_per_sample_ex -> asvrl_per_normalise)
         self.dirty = torch.zeros(max(1, P // 2048), dtype=torch.uint8, device=dev)
         s = _abi.AsvPer()
         s.rows, s.tree, s.state, s.t = self.rows.data_ptr(), self.tree.data_ptr(), self.state.data_ptr(), \
@@ -221,12 +222,14 @@ class DevicePER:
         self._s = s
         self.pushed = 0   # host count of pushed slots (num_elements without a device sync)
 
-    def push(self, obs, obj_cnt, actions, reward, done, stream=None):
-        """append() for n = m * stride rows (time-major); rows with obj_cnt < 0 become blank slots."""
+    def push(self, obs, obj_cnt, actions, reward, done, stream=None, step_counter=None):
+        """append() for n = m * stride rows (time-major); rows with obj_cnt < 0 become blank slots.
+        step_counter: a device int64 [1] advanced by one in the push's last launch (asvrl_per_push_ex)."""
         n = obs.shape[0]
         adim = actions.shape[1] if actions.dim() == 2 else 1
-        rc = _abi.lib().asvrl_per_push(C.byref(self._s), _abi.ptr(obs), _abi.ptr(obj_cnt), _abi.ptr(actions), adim,
-                                       _abi.ptr(reward), _abi.ptr(done), n, _abi.stream_ptr(stream))
+        rc = _abi.lib().asvrl_per_push_ex(C.byref(self._s), _abi.ptr(obs), _abi.ptr(obj_cnt), _abi.ptr(actions),
+                                          adim, _abi.ptr(reward), _abi.ptr(done), n, _abi.ptr(step_counter),
+                                          _abi.stream_ptr(stream))
         _abi.check(rc, "asvrl_per_push")
         self.pushed += n
 
@@ -237,22 +240,32 @@ class DevicePER:
     def sample(self, B, uniforms=None, seed=0, counter=0, counter_dev=None, out=None, out_idx=None, stream=None,
                normalise=True):
         out = out if out is not None else torch.empty((B, TR_DIM), dtype=torch.float32, device=self.device)
+        assert out.shape[0] >= B and out.stride(0) == TR_DIM and out.stride(1) == 1, "rows [B][TR_DIM], contiguous"
         idx = out_idx if out_idx is not None else torch.empty(B, dtype=torch.int64, device=self.device)
         if uniforms is not None:
             uniforms = uniforms.to(device=self.device, dtype=torch.float64).contiguous()
-        rc = _abi.lib().asvrl_per_sample(C.byref(self._s), int(B), _abi.ptr(uniforms),
-                                         int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter) & 0xFFFFFFFFFFFFFFFF,
-                                         _abi.ptr(counter_dev), _abi.ptr(out), _abi.ptr(idx), _abi.stream_ptr(stream))
+        w = None
+        if normalise:   # the draws' weights also contiguous, for the normalisation launch
+            w = self._weights.get(B)
+            if w is None:
+                w = self._weights[B] = torch.empty(B, dtype=torch.float32, device=self.device)
+        rc = _abi.lib().asvrl_per_sample_ex(C.byref(self._s), int(B), _abi.ptr(uniforms),
+                                            int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter) & 0xFFFFFFFFFFFFFFFF,
+                                            _abi.ptr(counter_dev), _abi.ptr(out), _abi.ptr(idx), _abi.ptr(w),
+                                            _abi.stream_ptr(stream))
         _abi.check(rc, "asvrl_per_sample")
-        if normalise:
-            w = out[:, 84]
-            w.div_(w.max())   # weights / weights.max() (:191)
+        if normalise:   # weights / weights.max() (:191), one launch
+            _abi.check(_abi.lib().asvrl_per_normalise(_abi.ptr(out), _abi.ptr(w), int(B), _abi.stream_ptr(stream)),
+                       "asvrl_per_normalise")
         return out, idx
 
-    def update_priorities(self, tree_idx, values, raw=False, stream=None):
+    def update_priorities(self, tree_idx, values, raw=False, stream=None, mean_out=None, learn_counter=None):
+        """mean_out: f32 [1] receives values' mean, learn_counter: int64 [1] advanced by one, both in the update's
+        last launch (asvrl_per_update_ex)."""
         v = values.detach().float().reshape(-1).contiguous()
-        rc = _abi.lib().asvrl_per_update(C.byref(self._s), _abi.ptr(tree_idx), _abi.ptr(v), v.shape[0],
-                                         1 if raw else 0, _abi.stream_ptr(stream))
+        rc = _abi.lib().asvrl_per_update_ex(C.byref(self._s), _abi.ptr(tree_idx), _abi.ptr(v), v.shape[0],
+                                            1 if raw else 0, _abi.ptr(mean_out), _abi.ptr(learn_counter),
+                                            _abi.stream_ptr(stream))
         _abi.check(rc, "asvrl_per_update")
 
     def anomalies(self):

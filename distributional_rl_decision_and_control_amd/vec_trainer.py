@@ -130,6 +130,7 @@ class VecTrainer:
             self.replay = DeviceReplay(max(buffer_size, 2 * NT), device=self.device)
         self.actions = torch.zeros((NT, 2), dtype=torch.float64, device=self.device)
         self.learn_counter = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.loss_mean = torch.zeros(1, dtype=torch.float32, device=self.device)   # PER: the update's mean loss
         self.batch_rows = torch.zeros((self.B, 88), dtype=torch.float32, device=self.device)
         # the fused updates' quantile fractions (AC-IQN: target, local, actor step; IQN: the first two)
         self.taus = torch.zeros((3, self.B, self.num_tau), dtype=torch.float32, device=self.device)
@@ -204,9 +205,11 @@ class VecTrainer:
         increments the env step counter (and writes the new ring state to `snap` when given). Returns
         whether the counter was incremented."""
         env = self.env
-        if self.per is not None:   # ReplayMemory.append of every robot that acted (trainer.py:163-164)
-            self.per.push(env.obs_cur, env.cnt_next, self.actions[:, :1], env.batch.reward, env.batch.done)
-            return False
+        if self.per is not None:   # ReplayMemory.append of every robot that acted (trainer.py:163-164), and the
+            # step counter advanced in the push's last launch
+            self.per.push(env.obs_cur, env.cnt_next, self.actions[:, :1], env.batch.reward, env.batch.done,
+                          step_counter=env.counter)
+            return True
         self.replay.push(env.obs_cur, env.obs_next, env.cnt_next, self.actions[:, :self.action_dim],
                          env.batch.reward, env.batch.done, snap=snap, counter_inc=env.counter)
         return True
@@ -230,9 +233,10 @@ class VecTrainer:
             loss, gn = self.fused_rb.update(self.opt, self.grads, rows, gamma=self.gamma, n=self.n_step,
                                             sync=self.sync, seed=self.seed + 999, counter_dev=self.learn_counter,
                                             compose=False)
-            self.per.update_priorities(idx, loss)   # update_priorities(idxs, loss) (agent.py:639)
-            self.learn_counter += 1
-            return loss.mean(), gn
+            # update_priorities(idxs, loss) (agent.py:639); the reported loss mean and the learn counter in its last
+            # launch
+            self.per.update_priorities(idx, loss, mean_out=self.loss_mean, learn_counter=self.learn_counter)
+            return self.loss_mean[0], gn
         if self.fused2 is not None:
             # one launch: the draw (rows + the update's quantile fractions), the actor's training forward
             # and the target actor

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 24
+#define ASVRL_ABI_VERSION 25
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -529,6 +529,11 @@ typedef struct AsvPer {
  * the dirty subtrees are rebuilt and the ring advances by n. Three launches. */
 int asvrl_per_push(const AsvPer* per, const float* obs, const int8_t* obj_cnt, const double* actions,
                    int32_t action_dim, const double* reward, const uint8_t* done, int32_t n, void* stream);
+/* ABI 25: the same, and the device env-step counter step_counter[0] (int64) advanced by one in its last launch
+ * (the batched loop's step count, trainer.py:172; NULL: not advanced) */
+int asvrl_per_push_ex(const AsvPer* per, const float* obs, const int8_t* obj_cnt, const double* actions,
+                      int32_t action_dim, const double* reward, const uint8_t* done, int32_t n, int64_t* step_counter,
+                      void* stream);
 
 /* ReplayMemory.sample (:157-192): B stratified draws (segment b: uniform in [b*seg, (b+1)*seg) with
  * seg = total / B in f32, the value in f64), SegmentTree.find, the validity rule of :163 (window
@@ -540,12 +545,22 @@ int asvrl_per_push(const AsvPer* per, const float* obs, const int8_t* obj_cnt, c
  * out_tree_idx [B] int64: tree indices for asvrl_per_update. One launch. */
 int asvrl_per_sample(const AsvPer* per, int32_t B, const double* uniforms, uint64_t seed, uint64_t counter,
                      const uint64_t* counter_dev, float* out, int64_t* out_tree_idx, void* stream);
+/* ABI 25: the same, and each draw's weight also into weights[B] (contiguous, for asvrl_per_normalise). */
+int asvrl_per_sample_ex(const AsvPer* per, int32_t B, const double* uniforms, uint64_t seed, uint64_t counter,
+                        const uint64_t* counter_dev, float* out, int64_t* out_tree_idx, float* weights, void* stream);
+/* ABI 25: weights / weights.max() (:191) into the weight column (84) of asvrl_per_sample_ex's B rows, from its
+ * contiguous weights, in one launch (the quotients of the reference's expression bit for bit). */
+int asvrl_per_normalise(float* rows, const float* weights, int32_t B, void* stream);
 
 /* ReplayMemory.update_priorities (:194-196): leaf tree_idx[i] = values[i] ** priority_exponent
  * (raw != 0: values already exponentiated), duplicates resolved last-wins (tree_idx as sampled, in
  * non-decreasing order), SegmentTree.max updated, dirty subtrees rebuilt. Three launches. */
 int asvrl_per_update(const AsvPer* per, const int64_t* tree_idx, const float* values, int32_t B, int32_t raw,
                      void* stream);
+/* ABI 25: the same, and in its last launch values_mean[0] = the mean of values (a fixed summation order; the
+ * train step's reported loss, agent.py:639) and learn_counter[0] (int64) += 1; either may be NULL. */
+int asvrl_per_update_ex(const AsvPer* per, const int64_t* tree_idx, const float* values, int32_t B, int32_t raw,
+                        float* values_mean, int64_t* learn_counter, void* stream);
 
 /* ---------------------------------------------------------------- Rainbow (Rainbow_model.py, agent.py)
  * NoisyLinear weights and the dueling C51 head. A network's noisy tensors are described by up to 16

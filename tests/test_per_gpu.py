@@ -228,3 +228,48 @@ def test_per_unvalidated_draw_gets_zero_weight():
     assert per.tree[leaf].item() == before[leaf].item()
     assert per.anomalies() == 1   # the -1 entry is not an ordering anomaly
     assert np.all(per.tree[torch.from_numpy(ix[:B - 1]).cuda()].cpu().numpy() == 2.0)
+
+
+def test_per_fused_tail_work():
+    """ABI 25: asvrl_per_sample_ex + asvrl_per_normalise (weights / weights.max() in one launch) equal torch's
+    w.div_(w.max()) bit for bit; asvrl_per_update_ex's values mean (fixed order) equals the mean within f32 rounding and it advances the
+    learn counter by one; asvrl_per_push_ex advances the step counter by one. The batched Rainbow loop then counts
+    exactly one env step per iteration and one learn step per learning iteration (eager)."""
+    from distributional_rl_decision_and_control_amd.learn_ops import DevicePER
+    from distributional_rl_decision_and_control_amd.vec_trainer import VecTrainer
+    S = 640
+    per = DevicePER(S * 20, stride=S, deferred=True, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(1)
+    ctr = torch.zeros(1, dtype=torch.int64, device="cuda")
+    for step in range(6):
+        obs = torch.rand((S, 40), device="cuda", generator=g)
+        cnt = torch.ones(S, dtype=torch.int8, device="cuda")
+        act = torch.randint(0, 25, (S, 1), device="cuda", generator=g).double()
+        rew = torch.rand(S, device="cuda", generator=g).double()
+        done = (torch.rand(S, device="cuda", generator=g) < 0.05).to(torch.uint8)
+        per.push(obs, cnt, act, rew, done, step_counter=ctr)
+    assert int(ctr.item()) == 6
+    B = 1000
+    rows, idx = per.sample(B, seed=3, counter=1, normalise=False)
+    w = rows[:, 84].clone()
+    w.div_(w.max())
+    rows2, idx2 = per.sample(B, seed=3, counter=1)   # the same draws, normalised by asvrl_per_normalise
+    torch.cuda.synchronize()
+    assert torch.equal(idx2, idx) and torch.equal(rows2[:, 84], w) and torch.equal(rows2[:, :84], rows[:, :84])
+    vals = torch.rand(B, device="cuda", generator=g) * 3
+    mean = torch.zeros(1, device="cuda")
+    lc = torch.full((1,), 41, dtype=torch.int64, device="cuda")
+    per.update_priorities(idx, vals, mean_out=mean, learn_counter=lc)
+    torch.cuda.synchronize()
+    assert int(lc.item()) == 42
+    assert abs(float(mean.item()) - float(vals.double().mean().item())) <= 1e-6 * float(vals.double().mean().item())
+    tr = VecTrainer(n_envs=64, agent_type="Rainbow", batch_size=128, buffer_size=64 * 5 * 40, graphs=False, seed=4)
+    c0, l0, k, learned = int(tr.env.counter.item()), int(tr.learn_counter.item()), 0, 0
+    while learned < 3:
+        out = tr.iteration()
+        k += 1
+        learned += out is not None
+    torch.cuda.synchronize()
+    assert int(tr.env.counter.item()) == c0 + k
+    assert int(tr.learn_counter.item()) == l0 + learned
+    assert np.isfinite(float(out[0].item()))
