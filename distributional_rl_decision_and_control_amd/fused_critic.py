@@ -205,8 +205,8 @@ def critic_train(pack, F, G, taus, q_targets, bufs, kappa=1.0, stream=None, q_ne
 
 class fused_variant:
     """Context manager (or plain call) selecting asvrl_critic_train_fused(_tq)'s kernel where both forms take the
-    shape (ABI 23, asvrl_critic_fused_variant): 8 = two waves per SIMD (the default), 4 = the one-wave-per-SIMD
-    kernel of round 5 (the A/B and the bit-identity tests that pin that kernel). Process-wide, bf16 build."""
+    shape (ABI 23, asvrl_critic_fused_variant): 4 = the one-wave-per-SIMD kernel (the default), 8 = two waves per
+    SIMD (measured 11 % slower; its tests and the A/B select it). Process-wide, bf16 build."""
 
     def __init__(self, v, operands="bf16"):
         self.L = _abi.lib(operands)

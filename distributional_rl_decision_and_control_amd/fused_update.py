@@ -1,6 +1,6 @@
 """The whole AC-IQN update (Agent.train_AC_IQN, agent.py:386-432) on hand-written gfx950
-kernels: nine launches per step (with the vectorised loop's fused prologue), no torch autograd, no host
-synchronisation.
+kernels: eight launches per step (with the vectorised loop's fused prologue and the target critic inside the
+critic launch), no torch autograd, no host synchronisation.
 
 Per step, on a replay batch `rows` ([B][88]: obs | next obs | action | reward | done):
   actor(s) saving activations -> a (for the actor step)  asvrl_actor_forward(TRAIN)
