@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("ASVRL_LIB", os.path.join(HERE, "lib", "libasvrl.so"))
 # the same sources built with f32 learner operands (the parity build; asvrl_operand_bytes() == 4)
 LIB_PATH_F32 = os.path.join(HERE, "lib", "libasvrl_f32.so")
 OPERANDS = {"bf16": (LIB_PATH, 2), "f32": (LIB_PATH_F32, 4)}
-ABI_VERSION = 25
+ABI_VERSION = 26
 
 SELF_DIM, OBJ_DIM, MAX_OBJ = 7, 5, 5
 OBS_DIM = 40   # self 7 | objects 25 | mask 5 | pad 3
@@ -276,6 +276,8 @@ EXPORTS = [
     ("asvrl_per_sample_ex", C.c_int, [C.POINTER(AsvPer), _I32, _VP, _U64, _U64, _VP, _VP, _VP, _VP, _VP]),
     ("asvrl_per_normalise", C.c_int, [_VP, _VP, _I32, _VP]),
     ("asvrl_noisy_compose", C.c_int, [C.POINTER(AsvNoisySegs), _I32, _VP]),
+    ("asvrl_noisy_backward_norm_parts", _I32, [C.POINTER(AsvNoisySegs)]),
+    ("asvrl_noisy_backward_norm", C.c_int, [C.POINTER(AsvNoisySegs), _VP, _VP]),
     ("asvrl_noisy_reset", C.c_int, [C.POINTER(AsvNoisySegs), _VP, _VP, _U64, _VP, _VP]),
     ("asvrl_rainbow_act", C.c_int, [C.POINTER(AsvRainbowHeadIO), _VP]),
     ("asvrl_rainbow_pick", C.c_int, [C.POINTER(AsvRainbowHeadIO), _VP]),

@@ -28,8 +28,11 @@ constexpr int kActs = 25;
 constexpr int kAdv = kAtoms * kActs;   // 1275
 constexpr int kHeadRows = 2;           // rows per wave
 
-__global__ __launch_bounds__(256) void noisy_compose_kernel(AsvNoisySegs s, int backward) {
+// sq_parts (backward, asvrl_noisy_backward_norm): each workgroup's sum of dmu^2 + dsigma^2 in f64, reduced in a
+// fixed order (the grid is fixed by the segment total), for the clip norm of the Adam step
+__global__ __launch_bounds__(256) void noisy_compose_kernel(AsvNoisySegs s, int backward, double* sq_parts) {
   const int64_t total = s.off[s.n];
+  double sq = 0.0;
   for (int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; g < total;
        g += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     int k = 0;
@@ -40,9 +43,21 @@ __global__ __launch_bounds__(256) void noisy_compose_kernel(AsvNoisySegs s, int 
       q.out[i] = q.mu[i] + q.sigma[i] * q.eps[i];
     } else {
       const float d = q.dout[i];
+      const float ds = d * q.eps[i];
       q.dmu[i] = d;
-      q.dsigma[i] = d * q.eps[i];
+      q.dsigma[i] = ds;
+      sq += static_cast<double>(d) * d + static_cast<double>(ds) * ds;
     }
+  }
+  if (sq_parts != nullptr) {
+    __shared__ double red[256];
+    red[threadIdx.x] = sq;
+    __syncthreads();
+    for (int w = 128; w >= 1; w >>= 1) {
+      if (static_cast<int>(threadIdx.x) < w) red[threadIdx.x] += red[threadIdx.x + w];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) sq_parts[blockIdx.x] = red[0];
   }
 }
 
@@ -269,19 +284,38 @@ int check_segs(const AsvNoisySegs* s, const char* what) {
 
 using namespace asvrl;
 
-extern "C" int asvrl_noisy_compose(const AsvNoisySegs* segs, int32_t backward, void* stream) {
+namespace {
+int noisy_grid(const AsvNoisySegs* segs) {
+  const int64_t blocks = (segs->off[segs->n] + 255) / 256;
+  return static_cast<int>(blocks < 1024 ? blocks : 1024);
+}
+
+int noisy_compose_launch(const AsvNoisySegs* segs, int32_t backward, double* sq_parts, void* stream) {
   if (int rc = check_segs(segs, "asvrl_noisy_compose")) return rc;
   for (int k = 0; k < segs->n; ++k) {
     const AsvNoisySeg& q = segs->seg[k];
     ASVRL_REQUIRE(q.eps && (backward ? (q.dout && q.dmu && q.dsigma) : (q.mu && q.sigma && q.out)),
                   "asvrl_noisy_compose: null segment member");
   }
-  const int64_t total = segs->off[segs->n];
-  if (total == 0) return 0;
-  const int64_t blocks = (total + 255) / 256;
-  hipLaunchKernelGGL(noisy_compose_kernel, dim3(static_cast<unsigned>(blocks < 1024 ? blocks : 1024)), dim3(256), 0,
-                     as_stream(stream), *segs, backward);
+  if (segs->off[segs->n] == 0) return 0;
+  hipLaunchKernelGGL(noisy_compose_kernel, dim3(static_cast<unsigned>(noisy_grid(segs))), dim3(256), 0,
+                     as_stream(stream), *segs, backward, sq_parts);
   return check_launch("asvrl_noisy_compose");
+}
+}  // namespace
+
+extern "C" int asvrl_noisy_compose(const AsvNoisySegs* segs, int32_t backward, void* stream) {
+  return noisy_compose_launch(segs, backward, nullptr, stream);
+}
+
+extern "C" int32_t asvrl_noisy_backward_norm_parts(const AsvNoisySegs* segs) {
+  if (check_segs(segs, "asvrl_noisy_backward_norm_parts") != 0) return 0;
+  return segs->off[segs->n] == 0 ? 0 : noisy_grid(segs);
+}
+
+extern "C" int asvrl_noisy_backward_norm(const AsvNoisySegs* segs, double* sq_parts, void* stream) {
+  ASVRL_REQUIRE(sq_parts != nullptr, "asvrl_noisy_backward_norm: null sq_parts");
+  return noisy_compose_launch(segs, 1, sq_parts, stream);
 }
 
 extern "C" int asvrl_noisy_reset(const AsvNoisySegs* segs, const int32_t* in_features, const int32_t* out_features,

@@ -383,13 +383,14 @@ class PartialArena:
                                                 _abi.stream_ptr(stream)), "asvrl_linear_wgrad_partial", L)
         return part, groups.value, M, K
 
-    def linear(self, dz, x, dw, db, accumulate=False, stream=None):
+    def linear(self, dz, x, dw, db, accumulate=False, stream=None, norm=True):
         """dw (<= M rows of K) <- dz^T x, db <- dz.sum(0); a dw / db with fewer rows than dz's M
-        columns takes the leading rows (a padded 32-row output layer)."""
+        columns takes the leading rows (a padded 32-row output layer). norm=False: outputs that are not
+        parameter gradients themselves (left out of flush(norm=...)'s squared norm)."""
         part, groups, M, K = self._linear_partial(dz, x, stream)
         assert dw.numel() % K == 0 and dw.numel() <= M * K and (db is None or db.numel() <= M)
         self._seg(part, dw, db, groups, dw.numel(), db.numel() if db is not None else M, accumulate,
-                  stride=M * K + M, boff=M * K)
+                  stride=M * K + M, boff=M * K, norm=norm)
 
     def fold(self, dz, x, net, stream=None):
         """The observation encoders' gradients of `net` from the 256 x 32 encoder-image rows

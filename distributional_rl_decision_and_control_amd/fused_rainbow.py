@@ -105,9 +105,11 @@ class NoisyPack:
                            for v in self.views]
         return {n: (self.dviews[2 * j], self.dviews[2 * j + 1]) for j, n in enumerate(NOISY)}
 
-    def backward(self, leaves, stream=None):
+    def backward(self, leaves, stream=None, sq_parts=None):
         """dmu = dW, dsigma = dW * eps into the parameters' .grad buffers (assigned); dW from the leaves'
-        .grad (autograd) or, with leaves=None, from self.dviews (the gradient buffer grad_buffer() made)."""
+        .grad (autograd) or, with leaves=None, from self.dviews (the gradient buffer grad_buffer() made).
+        sq_parts (f64 device view): the written gradients' squared-norm partials go there (ABI 26); returns
+        their count (0 without sq_parts)."""
         s = _abi.AsvNoisySegs()
         C.memmove(C.byref(s), C.byref(self.segs), C.sizeof(s))
         k = 0
@@ -124,7 +126,14 @@ class NoisyPack:
                 seg = s.seg[k]
                 seg.dout, seg.dmu, seg.dsigma = g.data_ptr(), mu.grad.data_ptr(), sig.grad.data_ptr()
                 k += 1
+        if sq_parts is not None:
+            n = int(_abi.lib().asvrl_noisy_backward_norm_parts(C.byref(s)))
+            assert 0 < n <= sq_parts.numel()
+            _abi.check(_abi.lib().asvrl_noisy_backward_norm(C.byref(s), _abi.ptr(sq_parts), _abi.stream_ptr(stream)),
+                       "asvrl_noisy_backward_norm")
+            return n
         _abi.check(_abi.lib().asvrl_noisy_compose(C.byref(s), 1, _abi.stream_ptr(stream)), "asvrl_noisy_compose(bwd)")
+        return 0
 
 
 IMG_SIZES = {"enc": 256 * 32, "v1": 128 * 256, "a1": 128 * 256, "v2": 128 * 128, "a2": 128 * 128, "vo": 64 * 128,
@@ -231,7 +240,7 @@ class FusedRainbow:
         the online weights composed by act() this iteration. reset_target=False keeps the target's noise
         buffers as they are (composed from them) instead of reset_noise() from Philox: the parity tests
         inject the noise the reference drew."""
-        from .learner import clip_and_step
+        from .learner import FusedAdam, clip_and_step
         B = rows.shape[0]
         if compose:
             self.pack.compose()
@@ -258,24 +267,47 @@ class FusedRainbow:
         # the six layers' weight gradients (into the composed-weight gradient buffer) and the encoder
         # fold in one launch, one reduction, then dmu = dW, dsigma = dW eps
         arena, dW, net = self.arena, self.dW, self.local
+        # single process with the fused optimiser: the clip norm from the reduction (the encoders' gradients) and
+        # the noisy backward (every mu / sigma gradient) instead of a norm launch over the flat gradient (ABI 26)
+        prenorm = sync is None and isinstance(opt, FusedAdam) and self._prenorm_covers(opt)
         with arena.batch():
             # the output layers in the kernel's (32, 128) / (128, 128) shapes: column slices of the padded
-            # dz images into the leading rows of each slice of the gradient
+            # dz images into the leading rows of each slice of the gradient (composed-weight gradients: not in
+            # the norm, their mu / sigma gradients are)
             Wv, bv = dW["output_layer_v"]
             for i in range(2):
-                arena.linear(A["dzv"][:, 32 * i:32 * i + 32], A["hv2"], Wv[32 * i:32 * i + 32], bv[32 * i:32 * i + 32])
+                arena.linear(A["dzv"][:, 32 * i:32 * i + 32], A["hv2"], Wv[32 * i:32 * i + 32], bv[32 * i:32 * i + 32],
+                             norm=False)
             Wa, ba = dW["output_layer_a"]
             for i in range(10):
                 arena.linear(A["dza"][:, 128 * i:128 * i + 128], A["ha2"], Wa[128 * i:128 * i + 128],
-                             ba[128 * i:128 * i + 128])
-            arena.linear(A["dz2v"], A["hv1"], *dW["hidden_layer_v_2"])
-            arena.linear(A["dz2a"], A["ha1"], *dW["hidden_layer_a_2"])
-            arena.linear(A["dz1v"], A["f"], *dW["hidden_layer_v"])
-            arena.linear(A["dz1a"], A["f"], *dW["hidden_layer_a"])
+                             ba[128 * i:128 * i + 128], norm=False)
+            arena.linear(A["dz2v"], A["hv1"], *dW["hidden_layer_v_2"], norm=False)
+            arena.linear(A["dz2a"], A["ha1"], *dW["hidden_layer_a_2"], norm=False)
+            arena.linear(A["dz1v"], A["f"], *dW["hidden_layer_v"], norm=False)
+            arena.linear(A["dz1a"], A["f"], *dW["hidden_layer_a"], norm=False)
             arena.fold(A["dzf"], A["xb"], net)
+        if prenorm:
+            assert opt.max_norm == max_norm, (opt.max_norm, max_norm)
+            arena.flush(norm=opt)
+            n1 = arena.nparts
+            n2 = self.pack.backward(None, sq_parts=arena.norm_parts[n1:])
+            return self.loss, opt.step_prenormed(arena.norm_parts, n1 + n2)
         arena.flush()
         self.pack.backward(None)
         if sync is not None:
             sync(grads)
         gn = clip_and_step(opt, grads, max_norm)
         return self.loss, gn
+
+    def _prenorm_covers(self, opt):
+        """True when the optimiser's parameters are exactly the encoders (the reduction's norm segments) and the
+        noisy layers' mu / sigma (the noisy backward's), so the two partial sets make its whole clip norm."""
+        ok = getattr(self, "_prenorm_ok", None)
+        if ok is None:
+            net = self.local
+            enc = sum(p.numel() for m in (net.self_encoder, net.object_encoder) for p in m.parameters())
+            noisy = sum(p.numel() for L in self.pack.layers for p in (L.weight_mu, L.weight_sigma, L.bias_mu,
+                                                                     L.bias_sigma))
+            ok = self._prenorm_ok = enc + noisy == opt.n
+        return ok

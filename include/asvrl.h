@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ASVRL_ABI_VERSION 25
+#define ASVRL_ABI_VERSION 26
 
 #define ASVRL_SELF_DIM 7   /* wamv.py:443-453 self observation */
 #define ASVRL_OBJ_DIM 5    /* wamv.py:481,508 [px, py, vx, vy, r] */
@@ -586,6 +586,11 @@ typedef struct AsvNoisySegs {
 /* NoisyLinear.forward in training mode (Rainbow_model.py:47-51) for every segment: out = mu + sigma * eps;
  * backward != 0: dmu = dout, dsigma = dout * eps (assigned, the parameters' only use). One launch. */
 int asvrl_noisy_compose(const AsvNoisySegs* segs, int32_t backward, void* stream);
+/* ABI 26: the backward of asvrl_noisy_compose that also leaves the squared norm of the gradients it writes
+ * (dmu^2 + dsigma^2) as asvrl_noisy_backward_norm_parts(segs) f64 per-workgroup partials in sq_parts (a fixed
+ * order): with the reduction's own partials (asvrl_partial_sums_norm) the clip norm of asvrl_adam_step. */
+int32_t asvrl_noisy_backward_norm_parts(const AsvNoisySegs* segs);
+int asvrl_noisy_backward_norm(const AsvNoisySegs* segs, double* sq_parts, void* stream);
 
 /* reset_noise() of every layer (Rainbow_model.py:35-45,141-145) with (weight, bias) segment pairs:
  * f(x) = sign(x) sqrt|x| of N(0, 1) Philox draws (seed, *counter_dev), eps_w = f(eps_out) f(eps_in)^T,
