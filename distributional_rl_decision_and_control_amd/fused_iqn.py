@@ -49,7 +49,7 @@ FUSED_TRAIN = True
 # forms q_next for the samples it updates, bit-identical to asvrl_iqn_forward_max); bf16 build. The default of
 # FusedIQNState.target_in_fused. Off for the batched loop, whose act pass runs beside the learner: there the longer
 # update launch runs beside the act pass instead of the env step, 0.2982 -> 0.3153 ms per IQN step; on for the
-# drop-in Agent (nothing beside its update): 55.5 -> 54.0 us per B = 64 step (profiles/r06j_*, r06k_*)
+# drop-in Agent (nothing beside its update; bf16 learner): 55.5 -> 54.0 us per B = 64 step (profiles/r06j_*, r06k_*)
 TARGET_IN_FUSED = False
 
 
