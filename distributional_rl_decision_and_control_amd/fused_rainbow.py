@@ -303,11 +303,11 @@ class FusedRainbow:
     def _prenorm_covers(self, opt):
         """True when the optimiser's parameters are exactly the encoders (the reduction's norm segments) and the
         noisy layers' mu / sigma (the noisy backward's), so the two partial sets make its whole clip norm."""
-        ok = getattr(self, "_prenorm_ok", None)
-        if ok is None:
+        cached = getattr(self, "_prenorm_ok", None)
+        if cached is None or cached[0] is not opt:
             net = self.local
             enc = sum(p.numel() for m in (net.self_encoder, net.object_encoder) for p in m.parameters())
             noisy = sum(p.numel() for L in self.pack.layers for p in (L.weight_mu, L.weight_sigma, L.bias_mu,
                                                                      L.bias_sigma))
-            ok = self._prenorm_ok = enc + noisy == opt.n
-        return ok
+            cached = self._prenorm_ok = (opt, enc + noisy == opt.n)
+        return cached[1]
