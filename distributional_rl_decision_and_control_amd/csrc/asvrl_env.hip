@@ -36,6 +36,36 @@ struct Regs {
   double x, y, th, vr0, vr1, vr2, v0, v1, v2, tl, tr, lp, rp;
 };
 
+// The pair kernels' arguments, read through the kernarg segment pointer (KArg) rather than as by-value
+// parameters: a by-value struct parameter is loaded whole at kernel entry and held to its last use, which
+// spilled 122 SGPRs to VGPR lanes (a v_readlane at every later use). A field loaded after kfresh() is not
+// merged with the same field's earlier load, so each phase below re-reads what it uses from the kernarg
+// segment (scalar loads) and holds it for that phase only.
+struct PairsArgs {
+  AsvParams p;
+  AsvEnvState s;
+  AsvStepCtl ctl;
+  AsvStepOut out;
+  const double* actions;
+  const double* noise;
+  int epb, group0;
+};
+template <class T>
+using KArg = const __attribute__((address_space(4))) T*;
+template <class T>
+__device__ __forceinline__ KArg<T> kfresh(KArg<T> q) {
+  asm volatile("" : "+s"(q));
+  return q;
+}
+template <class T>
+__device__ __forceinline__ const T& kref(KArg<T> q) {
+  return *(const T*)q;
+}
+template <class T>
+__device__ __forceinline__ KArg<T> kargs() {
+  return (KArg<T>)__builtin_amdgcn_kernarg_segment_ptr();
+}
+
 __device__ inline double clampd(double v, double lo, double hi) {  // np.clip
   return v < lo ? lo : (v > hi ? hi : v);
 }
@@ -77,12 +107,27 @@ __device__ inline void current_at(const double* __restrict__ cores, int nc, doub
 
 // One robot's action: N substeps of Robot.update_state (wamv.py:204-231) + compute_motion
 // (wamv.py:233-279) with the current sampled at the pre-move position (env.py:257-260).
-__device__ inline void robot_act(const AsvParams& p, Regs& r, double a0, double a1, int continuous,
-                                 const double* cores, int nc) {
+// The parameters as a plain reference (the sweep kernel) or re-read from the kernarg segment at every substep
+// (the pair kernel: the substep loop then holds no parameter in SGPRs across iterations)
+struct ParamsRef {
+  const AsvParams* q;
+  __device__ void fresh() {}
+  __device__ const AsvParams& get() const { return *q; }
+};
+struct ParamsKArg {
+  KArg<AsvParams> q;
+  __device__ void fresh() { q = kfresh(q); }
+  __device__ const AsvParams& get() const { return kref(q); }
+};
+template <class PR>
+__device__ inline void robot_act(PR P, Regs& r, double a0, double a1, int continuous, const double* cores, int nc) {
   // propulsion (wamv.py:251-264) depends only on the thrusts, which change on substep 0
   double fx = 0, fy = 0, mn = 0;
   const double clp = cos(r.lp), slp = sin(r.lp), crp = cos(r.rp), srp = sin(r.rp);
-  for (int idx = 0; idx < p.N; ++idx) {
+  const int n_sub = P.get().N;
+  for (int idx = 0; idx < n_sub; ++idx) {
+    P.fresh();
+    const AsvParams& p = P.get();
     double cx = 0.0, cy = 0.0;
     if (nc > 0) current_at(cores, nc, p.core_r, r.x, r.y, cx, cy);
     r.v0 = r.vr0 + cx;  // update_velocity (wamv.py:201-202)
@@ -414,7 +459,7 @@ __global__ __launch_bounds__(BLOCK) void env_sweep_kernel(AsvParams p, AsvEnvSta
     const double d_before = sqrt((gx - r.x) * (gx - r.x) + (gy - r.y) * (gy - r.y));
     const int nc = s.n_cores[e];
     const double* cores = s.cores + static_cast<size_t>(e) * s.max_cores * 4;
-    robot_act(P, r, actions[2 * idx], actions[2 * idx + 1], ctl.is_continuous, cores,
+    robot_act(ParamsRef{&P}, r, actions[2 * idx], actions[2 * idx + 1], ctl.is_continuous, cores,
               nc < s.max_cores ? nc : s.max_cores);
     const double d_after = sqrt((gx - r.x) * (gx - r.x) + (gy - r.y) * (gy - r.y));
     reward = 0.0;
@@ -610,14 +655,10 @@ __global__ __launch_bounds__(BLOCK) void env_sweep_kernel(AsvParams p, AsvEnvSta
 #define ASVRL_ENV_PAIRS_WPE 4
 #endif
 // one workgroup's envs [bid * epb, (bid + 1) * epb) of the step (env_pairs_kernel loops over them)
-template <int BLOCK, int NM>
-__device__ __forceinline__ void env_pairs_block(const AsvParams& p, const AsvEnvState& s,
-                                                const double* __restrict__ actions,
-                                                const double* __restrict__ noise,
-                                                const AsvStepCtl& ctl, const AsvStepOut& out, int epb, int bid,
-                                                unsigned char* smem) {
-  const int R = s.max_robots;
-  const int O = s.max_obs;
+template <int BLOCK, int NM, bool DYN = true>   // DYN false: an observation pass only (do_dynamics = 0)
+__device__ __forceinline__ void env_pairs_block(KArg<PairsArgs> A, int epb, int bid, unsigned char* smem) {
+  const int R = A->s.max_robots;
+  const int O = A->s.max_obs;
   const int S = O + R;               // candidate slots per robot (obstacles, then robots)
   const int nrb = epb * R;
   const int npairs = nrb * S;
@@ -651,18 +692,18 @@ __device__ __forceinline__ void env_pairs_block(const AsvParams& p, const AsvEnv
   const int le = tid / R;
   const int i = tid - le * R;
   const int e = bid * epb + le;
-  const bool lane_env = rlane && e < s.n_envs;
-  const bool env_on = lane_env && (ctl.env_mask == nullptr || ctl.env_mask[e] != 0);
+  const bool lane_env = rlane && e < A->s.n_envs;
+  const bool env_on = lane_env && (A->ctl.env_mask == nullptr || A->ctl.env_mask[e] != 0);
   // a masked pass (the observation pass after a reset) touches few envs: workgroups with none leave
-  if (ctl.env_mask != nullptr && !__syncthreads_or(env_on ? 1 : 0)) return;
-  const int nrob = lane_env ? s.n_robots[e] : 0;
+  if (A->ctl.env_mask != nullptr && !__syncthreads_or(env_on ? 1 : 0)) return;
+  const int nrob = lane_env ? A->s.n_robots[e] : 0;
   const bool exists = env_on && i < nrob;
-  const size_t NT = static_cast<size_t>(s.n_envs) * R;
+  const size_t NT = static_cast<size_t>(A->s.n_envs) * R;
   const size_t idx = static_cast<size_t>(e) * R + i;
-  const uint8_t fl = exists ? s.rflags[idx] : 0;
+  const uint8_t fl = exists ? A->s.rflags[idx] : 0;
   const bool deact = (fl & ASVRL_FLAG_DEACTIVATED) != 0;
   const bool active = exists && !deact;
-  const int ep_ts = env_on ? s.ep_ts[e] : 0;
+  const int ep_ts = env_on ? A->s.ep_ts[e] : 0;
   bool coll = (fl & ASVRL_FLAG_COLLISION) != 0;
   bool reach = (fl & ASVRL_FLAG_REACH_GOAL) != 0;
   double reward = 0.0;
@@ -672,7 +713,7 @@ __device__ __forceinline__ void env_pairs_block(const AsvParams& p, const AsvEnv
     Regs r{};
     double gx = 0, gy = 0;
     if (exists) {
-      const double* rs = s.rs;
+      const double* rs = A->s.rs;
       r.x = rs[ASVRL_F_X * NT + idx];
       r.y = rs[ASVRL_F_Y * NT + idx];
       r.th = rs[ASVRL_F_THETA * NT + idx];
@@ -689,19 +730,19 @@ __device__ __forceinline__ void env_pairs_block(const AsvParams& p, const AsvEnv
       gx = rs[ASVRL_F_GX * NT + idx];
       gy = rs[ASVRL_F_GY * NT + idx];
     }
-    if (active && ctl.do_dynamics) {
+    if (active && (DYN && A->ctl.do_dynamics)) {
       const double d_before = sqrt((gx - r.x) * (gx - r.x) + (gy - r.y) * (gy - r.y));
-      const int nc = s.n_cores[e];
-      const double* cores = s.cores + static_cast<size_t>(e) * s.max_cores * 4;
-      robot_act(p, r, actions[2 * idx], actions[2 * idx + 1], ctl.is_continuous, cores,
-                nc < s.max_cores ? nc : s.max_cores);
+      const int nc = A->s.n_cores[e];
+      const double* cores = A->s.cores + static_cast<size_t>(e) * A->s.max_cores * 4;
+      robot_act(ParamsKArg{&A->p}, r, A->actions[2 * idx], A->actions[2 * idx + 1], A->ctl.is_continuous, cores,
+                nc < A->s.max_cores ? nc : A->s.max_cores);
       const double d_after = sqrt((gx - r.x) * (gx - r.x) + (gy - r.y) * (gy - r.y));
       reward = 0.0;
-      reward += p.timestep_penalty;
+      reward += A->p.timestep_penalty;
       reward += d_before - d_after;
     }
-    if (exists && ctl.do_dynamics) {
-      double* rs = s.rs;
+    if (exists && (DYN && A->ctl.do_dynamics)) {
+      double* rs = A->s.rs;
       rs[ASVRL_F_X * NT + idx] = r.x;
       rs[ASVRL_F_Y * NT + idx] = r.y;
       rs[ASVRL_F_THETA * NT + idx] = r.th;
@@ -737,10 +778,10 @@ __device__ __forceinline__ void env_pairs_block(const AsvParams& p, const AsvEnv
       so2 = cs * r.v0 + sn * r.v1;
       so3 = -sn * r.v0 + cs * r.v1;
       so4 = r.v2;
-      if (sqrt((gx - r.x) * (gx - r.x) + (gy - r.y) * (gy - r.y)) <= p.goal_dis) reach = true;
+      if (sqrt((gx - r.x) * (gx - r.x) + (gy - r.y) * (gy - r.y)) <= A->p.goal_dis) reach = true;
     }
     if (env_on) {   // packed f32 obs row, self part (replay_buffer.py:51-69 + the .float() of agent.py:363-366)
-      float* of = out.obs + idx * ASVRL_OBS_DIM;
+      float* of = A->out.obs + idx * ASVRL_OBS_DIM;
       const bool a = active;
       *reinterpret_cast<float4*>(of) = a ? make_float4(static_cast<float>(so0), static_cast<float>(so1),
                                                         static_cast<float>(so2), static_cast<float>(so3))
@@ -748,8 +789,8 @@ __device__ __forceinline__ void env_pairs_block(const AsvParams& p, const AsvEnv
       of[4] = a ? static_cast<float>(so4) : 0.f;
       of[5] = a ? static_cast<float>(r.tl) : 0.f;
       of[6] = a ? static_cast<float>(r.tr) : 0.f;
-      if (out.obs64 != nullptr) {
-        double* o = out.obs64 + idx * 32;
+      if (A->out.obs64 != nullptr) {
+        double* o = A->out.obs64 + idx * 32;
         o[0] = a ? so0 : 0.0;
         o[1] = a ? so1 : 0.0;
         o[2] = a ? so2 : 0.0;
@@ -761,9 +802,9 @@ __device__ __forceinline__ void env_pairs_block(const AsvParams& p, const AsvEnv
     }
   }
   if (env_on) {
-    const int no = s.n_obs[e];
+    const int no = A->s.n_obs[e];
     for (int k = i; k < O; k += R) {
-      const double* ob = s.obstacles + (static_cast<size_t>(e) * O + k) * 3;
+      const double* ob = A->s.obstacles + (static_cast<size_t>(e) * O + k) * 3;
       double* dst = sob + (static_cast<size_t>(le) * O + k) * 3;
       if (k < no) {
         dst[0] = ob[0];
@@ -778,6 +819,7 @@ __device__ __forceinline__ void env_pairs_block(const AsvParams& p, const AsvEnv
     }
   }
   __syncthreads();
+  A = kfresh(A);
 
   // candidate slot c of robot qi in local env qe: obstacles first, then robots (self, deactivated and
   // absent ones are not candidates, wamv.py:487-491)
@@ -796,16 +838,18 @@ __device__ __forceinline__ void env_pairs_block(const AsvParams& p, const AsvEnv
     if (!(j < snr[qe] && j != qi && !soff[qe * R + j])) return false;
     ox = sx[qe * R + j];
     oy = sy[qe * R + j];
-    orad = p.r;
+    orad = A->p.r;
     vx0 = sv0[qe * R + j];
     vy0 = sv1[qe * R + j];
     return true;
   };
-  const uint64_t ctr = ctl.counter + (ctl.counter_dev != nullptr ? *ctl.counter_dev : 0ull);
-  const bool full_circle = 0.5 * p.angle >= kPi;
+  const uint64_t ctr = A->ctl.counter + (A->ctl.counter_dev != nullptr ? *A->ctl.counter_dev : 0ull);
+  const bool full_circle = 0.5 * A->p.angle >= kPi;
 
   // ---------------- phase 2: one (robot, candidate) pair per lane (wamv.py:478-511)
+  const KArg<PairsArgs> A_loop = A;
   for (int q = tid; q < npairs; q += BLOCK) {
+    const KArg<PairsArgs> A = kfresh(A_loop);   // this iteration's parameters, not held across iterations
     const int qr = q / S;
     const int c = q - qr * S;
     const int qe = qr / R;
@@ -816,30 +860,31 @@ __device__ __forceinline__ void env_pairs_block(const AsvParams& p, const AsvEnv
     if (sact[qr] && candidate(qe, qi, c, ox, oy, orad, vx0, vy0)) {
       const size_t qidx = static_cast<size_t>(bid * epb + qe) * R + qi;
       double n0, n1, n2, n3, n4;
-      draw_noise<NM>(p, ctl, ctr, noise, qidx, c, S, n0, n1, n2, n3, n4);
+      draw_noise<NM>(kref(A).p, kref(A).ctl, ctr, A->noise, qidx, c, S, n0, n1, n2, n3, n4);
       pvm[q] = static_cast<VmT>(n4);
       const double cs = scs[qr], sn = ssn[qr], tx = stx[qr], ty = sty[qr];
       const double pxn = ox + n0, pyn = oy + n1;  // Perception (wamv.py:27-40)
-      const double rn = p.r_mean_ratio * orad + (1 - p.r_mean_ratio) * n4 / kPi * orad;
+      const double rn = A->p.r_mean_ratio * orad + (1 - A->p.r_mean_ratio) * n4 / kPi * orad;
       const double qx = (cs * pxn + sn * pyn) + tx, qy = (-sn * pxn + cs * pyn) + ty;
       const double qn = sqrt(qx * qx + qy * qy);
-      bool det = qn <= p.range + rn;  // check_detection (wamv.py:293-303)
+      bool det = qn <= A->p.range + rn;  // check_detection (wamv.py:293-303)
       if (det && !full_circle) {
         const double ang = atan2(qy, qx);
-        det = !(ang < -0.5 * p.angle || ang > 0.5 * p.angle);
+        det = !(ang < -0.5 * A->p.angle || ang > 0.5 * A->p.angle);
       }
       if (det) {
         flag = 1;
         const double rx = sx[qr], ry = sy[qr];   // check_collision (wamv.py:281-291), true positions
-        const double d = sqrt((rx - ox) * (rx - ox) + (ry - oy) * (ry - oy)) - orad - p.r;
+        const double d = sqrt((rx - ox) * (rx - ox) + (ry - oy) * (ry - oy)) - orad - A->p.r;
         if (d <= 0.0) flag |= 2;
-        key = qn - rn - p.r;
+        key = qn - rn - A->p.r;
       }
     }
     pk[q] = key;
     pfl[q] = flag;
   }
   __syncthreads();
+  A = kfresh(A);
 
   // ---------------- phase 3: the robot's candidates in the reference's order (wamv.py:512-516)
   int cnt = -1;
@@ -872,7 +917,7 @@ __device__ __forceinline__ void env_pairs_block(const AsvParams& p, const AsvEnv
       ins(k4, c4);
       ++nkept;
     }
-    cnt = nkept < p.max_obj_num ? nkept : p.max_obj_num;
+    cnt = nkept < A->p.max_obj_num ? nkept : A->p.max_obj_num;
     unsigned short* kp = skept + 5 * tid;
     kp[0] = static_cast<unsigned short>(c0);
     kp[1] = static_cast<unsigned short>(c1);
@@ -892,6 +937,7 @@ __device__ __forceinline__ void env_pairs_block(const AsvParams& p, const AsvEnv
   }
   if (lane == kWave - 1) swt[tid / kWave] = kin;
   __syncthreads();
+  A = kfresh(A);
   int nitem = 0, ibase = 0;
 #pragma unroll
   for (int w = 0; w < BLOCK / kWave; ++w) {
@@ -903,9 +949,12 @@ __device__ __forceinline__ void env_pairs_block(const AsvParams& p, const AsvEnv
     for (int k = 0; k < cnt; ++k) sitem[off + k] = static_cast<unsigned short>(5 * tid + k);
   }
   __syncthreads();
+  A = kfresh(A);
 
   // ---------------- phase 4: one lane per kept object: its observation row and COLREGs test
+  const KArg<PairsArgs> A_loop4 = A;
   for (int it = tid; it < nitem; it += BLOCK) {
+    const KArg<PairsArgs> A = kfresh(A_loop4);   // this iteration's parameters, not held across iterations
     const int kq = sitem[it];
     const int qr = kq / 5;
     const int k = kq - 5 * qr;
@@ -922,11 +971,11 @@ __device__ __forceinline__ void env_pairs_block(const AsvParams& p, const AsvEnv
         double ox = 0, oy = 0, orad = 0, vx0 = 0, vy0 = 0;
         candidate(qe, qi, c, ox, oy, orad, vx0, vy0);
         double n0, n1, n2, n3, n4 = static_cast<double>(pvm[qr * S + c]);
-        draw_noise<NM, false>(p, ctl, ctr, noise, qidx, c, S, n0, n1, n2, n3, n4);
+        draw_noise<NM, false>(kref(A).p, kref(A).ctl, ctr, A->noise, qidx, c, S, n0, n1, n2, n3, n4);
         const double cs = scs[qr], sn = ssn[qr], tx = stx[qr], ty = sty[qr];
         const double pxn = ox + n0, pyn = oy + n1;  // as phase 2
         const double vxn = vx0 + n2, vyn = vy0 + n3;
-        const double rn = p.r_mean_ratio * orad + (1 - p.r_mean_ratio) * n4 / kPi * orad;
+        const double rn = A->p.r_mean_ratio * orad + (1 - A->p.r_mean_ratio) * n4 / kPi * orad;
         ra = (cs * pxn + sn * pyn) + tx;
         rb = (-sn * pxn + cs * pyn) + ty;
         rc = cs * vxn + sn * vyn;
@@ -934,18 +983,18 @@ __device__ __forceinline__ void env_pairs_block(const AsvParams& p, const AsvEnv
         re = rn;
         if (!(sqrt(rc * rc + rd * rd) < 0.5)) {   // colregs_body's first test, ahead of the call
           bool ev;
-          const bool hit = colregs_ev(p.r, cs, sn, sv0[qr], sv1[qr], ra, rb, rc, rd, re, ph, ev);
+          const bool hit = colregs_ev(A->p.r, cs, sn, sv0[qr], sv1[qr], ra, rb, rc, rd, re, ph, ev);
           cf = static_cast<unsigned char>((ev ? 1 : 0) | (hit ? 2 : 0));
         }
       }
-      float* of = out.obs + qidx * ASVRL_OBS_DIM + 7 + 5 * k;
+      float* of = A->out.obs + qidx * ASVRL_OBS_DIM + 7 + 5 * k;
       of[0] = static_cast<float>(ra);
       of[1] = static_cast<float>(rb);
       of[2] = static_cast<float>(rc);
       of[3] = static_cast<float>(rd);
       of[4] = static_cast<float>(re);
-      if (out.obs64 != nullptr) {
-        double* o = out.obs64 + qidx * 32 + 7 + 5 * k;
+      if (A->out.obs64 != nullptr) {
+        double* o = A->out.obs64 + qidx * 32 + 7 + 5 * k;
         o[0] = ra;
         o[1] = rb;
         o[2] = rc;
@@ -957,10 +1006,11 @@ __device__ __forceinline__ void env_pairs_block(const AsvParams& p, const AsvEnv
     pk[kq] = ph;
   }
   __syncthreads();
+  A = kfresh(A);
 
   // ---------------- phase 5: COLREGs in order (wamv.py:517-521), reward / done / info, bookkeeping
   bool apply = false;
-  double phi = exists ? s.rs[ASVRL_F_PHI * NT + idx] : 0.0;
+  double phi = exists ? A->s.rs[ASVRL_F_PHI * NT + idx] : 0.0;
   for (int k = 0; k < cnt; ++k) {   // the serial chain: phi of every evaluated object up to the first hit
     const unsigned char f = pfl[5 * tid + k];
     if (f & 1) phi = pk[5 * tid + k];
@@ -969,27 +1019,27 @@ __device__ __forceinline__ void env_pairs_block(const AsvParams& p, const AsvEnv
       break;
     }
   }
-  const StepResult res = step_result(p, ctl, exists, deact, active, ep_ts, fl, coll, reach, apply, phi, reward,
-                                     exists ? s.rs[ASVRL_F_RET * NT + idx] : 0.0);
-  if (ctl.trainer_deactivate && ctl.do_dynamics && exists && !(res.nfl & ASVRL_FLAG_DEACTIVATED))
+  const StepResult res = step_result(kref(A).p, kref(A).ctl, exists, deact, active, ep_ts, fl, coll, reach, apply, phi, reward,
+                                     exists ? A->s.rs[ASVRL_F_RET * NT + idx] : 0.0);
+  if (A->ctl.trainer_deactivate && (DYN && A->ctl.do_dynamics) && exists && !(res.nfl & ASVRL_FLAG_DEACTIVATED))
     atomicAdd(&salive[le], 1);
   if (exists) {
-    if (ctl.do_dynamics) s.rs[ASVRL_F_RET * NT + idx] = res.ret;
-    s.rs[ASVRL_F_PHI * NT + idx] = phi;
-    s.rflags[idx] = res.nfl;
+    if ((DYN && A->ctl.do_dynamics)) A->s.rs[ASVRL_F_RET * NT + idx] = res.ret;
+    A->s.rs[ASVRL_F_PHI * NT + idx] = phi;
+    A->s.rflags[idx] = res.nfl;
   }
   if (env_on) {
-    float4* o4 = reinterpret_cast<float4*>(out.obs + idx * ASVRL_OBS_DIM);
+    float4* o4 = reinterpret_cast<float4*>(A->out.obs + idx * ASVRL_OBS_DIM);
     const bool a = active;
     for (int k = cnt > 0 ? cnt : 0; k < 5; ++k) {   // the object rows phase 4 did not write
-      float* of = out.obs + idx * ASVRL_OBS_DIM + 7 + 5 * k;
+      float* of = A->out.obs + idx * ASVRL_OBS_DIM + 7 + 5 * k;
       of[0] = 0.f;
       of[1] = 0.f;
       of[2] = 0.f;
       of[3] = 0.f;
       of[4] = 0.f;
-      if (out.obs64 != nullptr) {
-        double* o = out.obs64 + idx * 32 + 7 + 5 * k;
+      if (A->out.obs64 != nullptr) {
+        double* o = A->out.obs64 + idx * 32 + 7 + 5 * k;
         o[0] = 0.0;
         o[1] = 0.0;
         o[2] = 0.0;
@@ -1000,13 +1050,14 @@ __device__ __forceinline__ void env_pairs_block(const AsvParams& p, const AsvEnv
     o4[8] = make_float4((a && cnt > 0) ? 1.f : 0.f, (a && cnt > 1) ? 1.f : 0.f, (a && cnt > 2) ? 1.f : 0.f,
                         (a && cnt > 3) ? 1.f : 0.f);
     o4[9] = make_float4((a && cnt > 4) ? 1.f : 0.f, 0.f, 0.f, 0.f);
-    out.obj_cnt[idx] = static_cast<int8_t>(exists ? cnt : -1);
-    out.reward[idx] = res.reward;
-    out.done[idx] = res.done;
-    out.info[idx] = res.info;
+    A->out.obj_cnt[idx] = static_cast<int8_t>(exists ? cnt : -1);
+    A->out.reward[idx] = res.reward;
+    A->out.done[idx] = res.done;
+    A->out.info[idx] = res.info;
   }
   __syncthreads();
-  if (env_on && i == 0 && ctl.do_dynamics) env_end(p, s, ctl, out, e, ep_ts, nrob, salive[le], NT);
+  A = kfresh(A);
+  if (env_on && i == 0 && (DYN && A->ctl.do_dynamics)) env_end(kref(A).p, kref(A).s, kref(A).ctl, kref(A).out, e, ep_ts, nrob, salive[le], NT);
 }
 
 
@@ -1029,13 +1080,11 @@ __device__ __forceinline__ int xcd_group(int x, int n) {
 #endif
 }
 template <int BLOCK, int NM>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NM == 1 ? 1 : ASVRL_ENV_PAIRS_WPE))) void env_pairs_kernel(AsvParams p, AsvEnvState s,
-                                                          const double* __restrict__ actions,
-                                                          const double* __restrict__ noise,
-                                                          AsvStepCtl ctl, AsvStepOut out, int epb, int group0) {
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NM == 1 ? 1 : ASVRL_ENV_PAIRS_WPE))) void env_pairs_kernel(PairsArgs) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  env_pairs_block<BLOCK, NM>(p, s, actions, noise, ctl, out, epb,
-                             group0 + xcd_group(static_cast<int>(blockIdx.x), static_cast<int>(gridDim.x)), smem);
+  const KArg<PairsArgs> A = kargs<PairsArgs>();
+  env_pairs_block<BLOCK, NM>(A, A->epb,
+                             A->group0 + xcd_group(static_cast<int>(blockIdx.x), static_cast<int>(gridDim.x)), smem);
 }
 
 // ------------------------------------------------------------------ reset (env.py:72-164)
@@ -1270,19 +1319,25 @@ __global__ __launch_bounds__(kResetWaves * kWave) void env_reset_kernel(AsvParam
 // ended its episode (mask), the wave resets it (reset_env) and then computes its reset observation with the
 // step kernel's own phases (env_pairs_block, one env per workgroup, do_dynamics = 0): the same values as
 // asvrl_env_reset followed by the masked asvrl_env_step pass, without the second launch over every env.
+struct ResetObsArgs {
+  PairsArgs k;   // actions / noise null, epb 1
+  AsvResetCfg cfg;
+  const uint8_t* mask;
+  uint64_t seed, counter;
+  const uint64_t* counter_dev;
+};
 template <int NM>
-__global__ __launch_bounds__(kWave) void env_reset_observe_kernel(AsvParams p, AsvEnvState s, AsvResetCfg cfg,
-                                                                  const uint8_t* __restrict__ mask, uint64_t seed,
-                                                                  uint64_t counter,
-                                                                  const uint64_t* __restrict__ counter_dev,
-                                                                  AsvStepCtl ctl, AsvStepOut out) {
+__global__ __launch_bounds__(kWave) void env_reset_observe_kernel(ResetObsArgs) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];   // env_pairs_block's carve
   __shared__ ResetLds W;
+  const KArg<ResetObsArgs> RA = kargs<ResetObsArgs>();
+  const ResetObsArgs& a = kref(RA);
   const int e = blockIdx.x;
-  if (mask[e] == 0) return;                      // workgroup-uniform
-  reset_env(p, s, cfg, e, seed, counter + (counter_dev != nullptr ? *counter_dev : 0ull), threadIdx.x, W);
+  if (a.mask[e] == 0) return;                      // workgroup-uniform
+  reset_env(a.k.p, a.k.s, a.cfg, e, a.seed, a.counter + (a.counter_dev != nullptr ? *a.counter_dev : 0ull),
+            threadIdx.x, W);
   __syncthreads();   // the reset's global writes (workgroup-scope release / acquire) before the observation reads
-  env_pairs_block<kWave, NM>(p, s, nullptr, nullptr, ctl, out, 1, e, smem);
+  env_pairs_block<kWave, NM, false>(kfresh<PairsArgs>(&RA->k), 1, e, smem);
 }
 
 __global__ __launch_bounds__(kBlock) void current_kernel(const double* __restrict__ cores, int nc, double core_r,
@@ -1377,9 +1432,12 @@ extern "C" int asvrl_env_step_ex(const AsvParams* params, const AsvEnvState* sta
     const int groups = (state->n_envs + pl.epb - 1) / pl.epb;
     const int chunk = lc.max_groups > 0 && lc.max_groups < groups ? lc.max_groups : groups;
     auto go = [&](auto kern) {
-      for (int g0 = 0; g0 < groups; g0 += chunk)
+      PairsArgs a{*params, *state, *ctl, *out, actions, noise, pl.epb, 0};
+      for (int g0 = 0; g0 < groups; g0 += chunk) {
+        a.group0 = g0;
         hipLaunchKernelGGL(kern, dim3(groups - g0 < chunk ? groups - g0 : chunk), dim3(pl.blk), pl.smem,
-                           as_stream(stream), *params, *state, actions, noise, *ctl, *out, pl.epb, g0);
+                           as_stream(stream), a);
+      }
     };
     if (pl.blk == 64)
       nm == 0 ? go(env_pairs_kernel<64, 0>) : nm == 1 ? go(env_pairs_kernel<64, 1>) : go(env_pairs_kernel<64, 2>);
@@ -1445,8 +1503,9 @@ extern "C" int asvrl_env_reset_observe(const AsvParams* params, const AsvEnvStat
                                     ctl->noise_mode == 2 ? 4 : 8);
   ASVRL_REQUIRE(pl.blk == kWave && pl.epb == 1 && pl.smem <= 60 * 1024, "asvrl_env_reset_observe: env too large");
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(state->n_envs), dim3(kWave), pl.smem, as_stream(stream), *params, *state, *cfg,
-                       env_mask, seed, counter, counter_dev, *ctl, *out);
+    const ResetObsArgs a{PairsArgs{*params, *state, *ctl, *out, nullptr, nullptr, 1, 0}, *cfg, env_mask, seed, counter,
+                         counter_dev};
+    hipLaunchKernelGGL(kern, dim3(state->n_envs), dim3(kWave), pl.smem, as_stream(stream), a);
   };
   ctl->noise_mode == 2 ? go(env_reset_observe_kernel<2>) : go(env_reset_observe_kernel<1>);
   return check_launch("asvrl_env_reset_observe");
