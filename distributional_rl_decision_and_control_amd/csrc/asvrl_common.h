@@ -276,4 +276,25 @@ __device__ __forceinline__ T strided_sum(const T* __restrict__ p, int start, int
   return acc;
 }
 
+// A kernel's single struct argument read through the kernarg segment pointer (kargs<T>(): the struct must be the
+// kernel's first argument) instead of as a by-value parameter, whose fields the compiler loads at kernel entry and
+// holds to their last use (spilling SGPRs into VGPR lanes when they outnumber the SGPRs). kfresh() hides the
+// pointer's identity, so loads after it are not merged with those before it: a phase or loop iteration that
+// re-reads its fields through kfresh(q) holds them for that phase or iteration only (scalar loads, kernarg cache).
+template <class T>
+using KArg = const __attribute__((address_space(4))) T*;
+template <class T>
+__device__ __forceinline__ KArg<T> kfresh(KArg<T> q) {
+  asm volatile("" : "+s"(q));
+  return q;
+}
+template <class T>
+__device__ __forceinline__ const T& kref(KArg<T> q) {
+  return *(const T*)q;
+}
+template <class T>
+__device__ __forceinline__ KArg<T> kargs() {
+  return (KArg<T>)__builtin_amdgcn_kernarg_segment_ptr();
+}
+
 }  // namespace asvrl

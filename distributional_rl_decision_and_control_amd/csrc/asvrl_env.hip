@@ -50,21 +50,6 @@ struct PairsArgs {
   const double* noise;
   int epb, group0;
 };
-template <class T>
-using KArg = const __attribute__((address_space(4))) T*;
-template <class T>
-__device__ __forceinline__ KArg<T> kfresh(KArg<T> q) {
-  asm volatile("" : "+s"(q));
-  return q;
-}
-template <class T>
-__device__ __forceinline__ const T& kref(KArg<T> q) {
-  return *(const T*)q;
-}
-template <class T>
-__device__ __forceinline__ KArg<T> kargs() {
-  return (KArg<T>)__builtin_amdgcn_kernarg_segment_ptr();
-}
 
 __device__ inline double clampd(double v, double lo, double hi) {  // np.clip
   return v < lo ? lo : (v > hi ? hi : v);
