@@ -410,8 +410,8 @@ CROSS_SHAPES = [(1, 0, 55.0, 0), (1, 3, 55.0, 0), (3, 0, 55.0, 0), (5, 4, 55.0, 
 @pytest.mark.parametrize("fast", [True, False])
 @pytest.mark.parametrize("R,O,W,C", CROSS_SHAPES)
 def test_pair_kernel_matches_sweep(R, O, W, C, fast):
-    """The pair kernel (automatic shape, a forced one-wave shape, the step split into launches of at most 7
-    workgroups) against the per-robot sweep, bit
+    """The pair kernel (automatic shape, a forced one-wave shape, a 128-lane shape, the step split into launches
+    of at most 7 workgroups) against the per-robot sweep, bit
     for bit, over (robots, buoys) shapes the traces do not reach: one robot, no buoys, vortex cores,
     12 and 30 robots (absent robots where the sampler cannot place all). Device reset, Philox noise in
     f32 and f64, 12 steps with the trainer bookkeeping (returns, deactivation, episode end) and one
@@ -442,8 +442,11 @@ def test_pair_kernel_matches_sweep(R, O, W, C, fast):
     b, ref = run((_abi.ENV_LAYOUT_SWEEP, 0, 0))
     cnt = b.obj_cnt.cpu().numpy()
     assert (cnt >= -1).all() and (cnt <= 5).all()
-    # None: automatic; a forced one-wave shape; the automatic shape as launches of at most 7 workgroups
-    for launch in (None, (_abi.ENV_LAYOUT_PAIRS, 64, max(1, 64 // R)), (0, 0, 0, 7)):
+    # None: automatic; a forced one-wave shape; a 128-lane shape of about 100 robots (which the automatic rule
+    # never picks: within 1 % of it at 2^18 envs, profiles/r06af_env_shape_interleaved.txt); the automatic shape as
+    # launches of at most 7 workgroups
+    for launch in (None, (_abi.ENV_LAYOUT_PAIRS, 64, max(1, 64 // R)), (_abi.ENV_LAYOUT_PAIRS, 128, max(1, 100 // R)),
+                   (0, 0, 0, 7)):
         _, got = run(launch)
         for t, (x, y) in enumerate(zip(ref, got)):
             # exact, NaN = NaN: phi is NaN, in both layouts and in the reference, when COLREGs evaluates an
