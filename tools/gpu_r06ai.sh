@@ -1,4 +1,5 @@
 # round 6: the next learn step's draw + target actor on the rollout stream behind the push, its actor TRAIN
+# (the --draw-ahead flag and asvrl_learn_prologue_target were removed after this A/B: DESIGN.md section 6)
 # forward behind the act (VecTrainer.draw_ahead, ABI 27) -- parity tests, then A/B against the one-launch
 # prologue at the head of each learn step, alternating, at the driver's shape and at steady state
 set -o pipefail; mkdir -p gpurun_out; export PYTHONUNBUFFERED=1; T=${T:-r06ai}

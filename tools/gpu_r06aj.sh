@@ -1,4 +1,5 @@
 # round 6: the draw-ahead schedule's chain tests (bit-identity against the joined schedule) and its step window
+# (the --draw-ahead flag and asvrl_learn_prologue_target were removed after this A/B: DESIGN.md section 6)
 set -o pipefail; mkdir -p gpurun_out; export PYTHONUNBUFFERED=1; T=${T:-r06aj}
 R=$PWD
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \

@@ -1,5 +1,6 @@
 # round 6: the partial-sums 16-byte path (a workgroup per 256 outputs of a plain segment, bit-identical to the
 # scalar path) -- its tests and the reductions' consumers, then A/B against the scalar path (variant scalarsum)
+# (the 16-byte path and its scalarsum variant were removed after this A/B: DESIGN.md section 6)
 set -o pipefail; mkdir -p gpurun_out; export PYTHONUNBUFFERED=1; T=${T:-r06ak}
 timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
   tests/test_wgrad_gpu.py tests/test_critic_fused_gpu.py tests/test_critic_bf16_oracle_gpu.py \
