@@ -1,7 +1,7 @@
 # round 6: the next learn step's draw + target actor on the rollout stream behind the push, its actor TRAIN
-# (the --draw-ahead flag and asvrl_learn_prologue_target were removed after this A/B: DESIGN.md section 6)
 # forward behind the act (VecTrainer.draw_ahead, ABI 27) -- parity tests, then A/B against the one-launch
 # prologue at the head of each learn step, alternating, at the driver's shape and at steady state
+# (the --draw-ahead flag and asvrl_learn_prologue_target were removed after this A/B: DESIGN.md section 6)
 set -o pipefail; mkdir -p gpurun_out; export PYTHONUNBUFFERED=1; T=${T:-r06ai}
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
   tests/test_learn_kernels_gpu.py -k "prologue" tests/test_chain_schedule_gpu.py > gpurun_out/${T}_tests.log 2>&1 || { tail -30 gpurun_out/${T}_tests.log; exit 1; }
